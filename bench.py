@@ -1,0 +1,185 @@
+#!/usr/bin/env python3
+"""fem355 benchmark: BASELINE.json metric "CG iterations/sec + DOFs/sec (assembly+solve), 10M P1-tet Poisson".
+
+Workload: Kuhn-cube mesh n=119 -> 10,110,954 P1 tets, 1,728,000 nodes/DOFs, scalar Poisson
+(kappa=1), z=0 face Dirichlet, unit nodal source; fp64 values, int32 indices, SELL-64 global matrix.
+  * a "step" = one Jacobi-PCG iteration (SpMV + 2 dots + vector updates) on that system, tol=0 (no early exit);
+    `value` = steps/s of the whole job (for N>1: the same global system element-partitioned over the ranks,
+    strong scaling), measured between barrier+synchronize brackets, max over ranks.
+  * DOFs/s = n_DOF / (assembly incl. pattern build + PCG solve to rtol 1e-8 on sqrt(r.z)), reported beside.
+  * roofline: the SpMV+p.Ap kernel, algorithmic bytes 12 nnz + 4 (n+1) + 16 n per launch (§8(d)) over its
+    average device time, sampled live with hip events on the solver stream inside the timed region.
+  * cpu_baseline: the oracle (torch-CPU restatement of the reference's EBE PCG, oracle/ref_cpu.py) timed on the
+    host cores on a bounded sample (assembly + a few iterations of the same 10M system), rank 0 at N=1 only.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import fem355  # noqa: E402
+from fem355 import _capi as C, mesh, system  # noqa: E402
+
+METRIC = "CG iterations/sec + DOFs/sec (assembly+solve), 10M P1-tet Poisson, 1/2/4/8 MI355X"
+HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--n", type=int, default=119, help="Kuhn cube size (119 -> 10.1M tets)")
+    ap.add_argument("--kind", default="poisson", choices=["poisson", "elastic"])
+    ap.add_argument("--sample-every", type=int, default=10, help="event-sample every k-th step")
+    ap.add_argument("--rtol", type=float, default=1e-8)
+    ap.add_argument("--cpu-iters", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", type=int, default=0, help="capture k iterations per hipGraph (0 = plain launches)")
+    return ap.parse_args()
+
+
+def sync():
+    torch.cuda.synchronize()
+
+
+def traffic_from_profiles(workload_key):
+    """HBM bytes per SpMV launch from the committed PMC summary (tools/pmc_traffic.py), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+        return d.get(workload_key, {}).get("bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(n, kind, iters):
+    """Oracle (reference op sequence on torch-CPU) on the same mesh: assembly + `iters` EBE-PCG iterations."""
+    from oracle import ref_cpu as R
+    coords, tets = mesh.kuhn_cube(n)
+    threads = torch.get_num_threads()
+    t0 = time.perf_counter()
+    K = R.tet4_poisson_K(coords, tets) if kind == "poisson" else R.tet4_K(coords, tets, 113.8e9, 0.342)
+    t_asm = time.perf_counter() - t0
+    N = coords.shape[0]
+    dpn = 1 if kind == "poisson" else 3
+    f, fixed = mesh.cube_poisson_case(coords) if kind == "poisson" else mesh.cube_elasticity_case(coords)
+    Minv = R.diag_preconditioner(K, tets, N, dpn=dpn)
+    Minv[fixed] = 0.0
+    t0 = time.perf_counter()
+    R.pcg(K, tets, f.view(N, dpn), Minv, tol=0.0, max_iter=iters)
+    t_it = time.perf_counter() - t0
+    return {"value": iters / t_it, "unit": "CG iterations/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/ref_cpu.py torch-CPU EBE Jacobi-PCG on the same {tets.shape[0]:,}-tet {kind} system: "
+                      f"{iters} iterations after element assembly ({t_asm:.2f} s) + setup; fp64",
+            "assembly_s": t_asm}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        from fem355 import dist
+        return dist.bench_main(a, METRIC)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    C.lib()
+
+    # ---- warm the kernels (module load, first-launch costs) on a small mesh
+    c0, t0_ = mesh.kuhn_cube(8, device=dev)
+    system.assemble_tet4_system(c0, t0_, a.kind, 1.0, 0.3).matvec(torch.ones(c0.shape[0] * (1 if a.kind == "poisson" else 3), dtype=torch.float64, device=dev))
+    sync()
+
+    coords, tets = mesh.kuhn_cube(a.n, device=dev)
+    M, N = tets.shape[0], coords.shape[0]
+    if a.kind == "poisson":
+        f, fixed = mesh.cube_poisson_case(coords)
+        E, nu = 1.0, 0.0
+    else:
+        f, fixed = mesh.cube_elasticity_case(coords)
+        E, nu = 113.8e9, 0.342
+    sync()
+
+    # ---- assembly (pattern + values + Jacobi) and solve to tolerance: DOFs/s
+    t0 = time.perf_counter()
+    A = system.assemble_tet4_system(coords, tets, a.kind, E, nu)
+    mask = torch.zeros((N, A.bs), dtype=torch.uint8, device=dev)
+    mask[fixed] = 1
+    w = A.jacobi(mask.view(-1))
+    sync()
+    t_asm = time.perf_counter() - t0
+    A.check_singular()
+    b = f.reshape(-1).to(torch.float64).contiguous()
+    tol = a.rtol * float(torch.sqrt(torch.dot(b, w * b)))
+    sync()
+    t0 = time.perf_counter()
+    res = A.pcg(b, None, w=w, mode=C.MODE_PCG, tol=tol, max_iter=20000, chunk=64)
+    sync()
+    t_solve = time.perf_counter() - t0
+
+    # ---- fixed-iteration timing (the metric)
+    run = system.PcgRunner(A, b, w, tol=0.0)
+    run.start()
+    if a.graph:
+        run.use_graph(a.graph)
+    run.iterate(a.warmup)
+    sync()
+    t0 = time.perf_counter()
+    ms, cnt = run.profile(a.steps, every=a.sample_every)
+    sync()
+    dt = time.perf_counter() - t0
+    it, stt, _ = run.poll()
+    assert it == a.warmup + a.steps, (it, stt)
+    run.close()
+
+    spmv_ms = ms[0] / max(cnt[0], 1)
+    alg = A.algorithmic_bytes_spmv()
+    achieved = alg / (spmv_ms * 1e-3) / 1e9
+    workload_key = f"kuhn{a.n}_{a.kind}"
+    out = {
+        "metric": METRIC,
+        "value": a.steps / dt,
+        "unit": "CG iterations/s",
+        "n_gpus": 1,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": dt / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": f"{M:,}-tet P1 {a.kind} Kuhn cube n={a.n}, Jacobi-PCG fixed iterations",
+                   "tets": M, "nodes": N, "dofs": A.n, "nnz_blocks": A.g.nnz, "format": "SELL-64 fp64 values, int32 cols",
+                   "parallelism": "single GPU"},
+        "dofs_per_s": A.n / (t_asm + t_solve),
+        "assembly_ms": t_asm * 1e3,
+        "solve_ms": t_solve * 1e3,
+        "solve_iters": res.iterations,
+        "solve_status": res.status,
+        "kernel_ms": {"spmv_dot": spmv_ms, "update": ms[1] / max(cnt[1], 1), "pupdate": ms[2] / max(cnt[2], 1),
+                      "sampled_launches": cnt[0]},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic_from_profiles(workload_key),
+                     "kernel": "k_pcg_spmv_dot", "algorithmic_bytes": alg},
+        "cpu_baseline": None,
+    }
+    if not a.no_cpu_baseline and rank == 0:
+        out["cpu_baseline"] = cpu_baseline(a.n, a.kind, a.cpu_iters)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,122 @@
+"""ctypes binding of the fem355 C-ABI (`include/fem355.h`, built into `lib/libfem355.so`).
+
+There is no CPU fallback: every compute entry point of the package goes through this library on a HIP device,
+and `lib()` raises if the library or the device is missing. `torch` is imported first on purpose: it loads the
+HIP runtime (libamdhip64.so.7) that the library then binds to by SONAME, so torch tensors' device pointers and
+streams are valid in both.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("FEM355_LIB", os.path.join(PKG_DIR, "lib", "libfem355.so"))
+
+FEM_OK, FEM_EBADTYPE, FEM_ESINGULAR, FEM_EHIP, FEM_ERCCL, FEM_EARG = range(6)
+PCG_RUNNING, PCG_CONVERGED, PCG_MAXITER, PCG_BREAKDOWN, PCG_ALPHA_NAN, PCG_BETA_NAN = range(6)
+MODE_CG_STABLE, MODE_PCG = 0, 1
+KIND_ELASTIC, KIND_POISSON, KIND_MASS = 0, 1, 2
+ISO_SUM, ISO_STACK, ISO_VOLUME = 0, 1, 2
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_int64
+_D = ctypes.c_double
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "fem_last_error": (ctypes.c_char_p, []),
+    "fem_version": (_I, []),
+    "fem_tet4_ke": (_I, [_P, _P, _L, _D, _D, _I, _P, _P, _P]),
+    "fem_tet4_geom": (_I, [_P, _P, _L, _P, _P, _P, _P, _P]),
+    "fem_iso_ke": (_I, [_P, _P, _L, _I, _D, _D, _P, _P, _I, _I, _P, _P]),
+    "fem_iso_geom": (_I, [_P, _P, _L, _I, _P, _P, _P, _P, _P]),
+    "fem_pcg_scalars": (_I, [_P, ctypes.POINTER(_D)]),
+    "fem_scan_work_len": (_L, [_L]),
+    "fem_incidence": (_I, [_P, _L, _I, _L, _P, _P, _P, _P]),
+    "fem_graph_count": (_I, [_P, _I, _P, _P, _L, _P, _P, _P]),
+    "fem_graph_fill": (_I, [_P, _I, _P, _P, _L, _P, _P, _P, _P]),
+    "fem_scan_i32": (_I, [_P, _L, _P, _P, _P]),
+    "fem_scan_i64": (_I, [_P, _L, _P, _P, _P]),
+    "fem_sell_widths": (_I, [_P, _L, _P, _P]),
+    "fem_sell_fill": (_I, [_P, _P, _L, _P, _P, _P, _P]),
+    "fem_assemble_from_ke": (_I, [_P, _P, _I, _I, _P, _P, _L, _P, _P, _P, _P, _P, _P]),
+    "fem_assemble_tet4": (_I, [_P, _P, _D, _D, _I, _P, _P, _L, _P, _P, _P, _P, _P, _P, _P]),
+    "fem_sell_to_csr_vals": (_I, [_P, _I, _P, _L, _P, _P, _P, _P]),
+    "fem_jacobi": (_I, [_P, _I, _P, _P, _P, _P, _L, _P, _P, _P]),
+    "fem_ebe_apply": (_I, [_P, _P, _I, _I, _P, _P, _L, _P, _P, _P]),
+    "fem_ebe_diag": (_I, [_P, _P, _I, _I, _P, _P, _L, _I, _P, _P]),
+    "fem_invert_diag": (_I, [_P, _L, _P, _P]),
+    "fem_spmv": (_I, [_L, _I, _P, _P, _P, _P, _P, _P]),
+    "fem_pcg_create": (_I, [_L, _I, _P, _P, _P, _P, _P, _P, _I, _D, _D, _P, _L, _P, ctypes.POINTER(_P)]),
+    "fem_pcg_start": (_I, [_P]),
+    "fem_pcg_iterate": (_I, [_P, _I]),
+    "fem_pcg_poll": (_I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_D)]),
+    "fem_pcg_solve": (_I, [_P, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_D)]),
+    "fem_pcg_use_graph": (_I, [_P, _I]),
+    "fem_pcg_profile": (_I, [_P, _I, _I, ctypes.POINTER(_D), ctypes.POINTER(_I)]),
+    "fem_pcg_destroy": (None, [_P]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class FemError(RuntimeError):
+    pass
+
+
+def load_library(path: str = LIB_PATH):
+    """Load the shared library and bind every symbol of SIGNATURES (no device needed)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(path):
+                raise FemError(f"fem355: HIP library not built: {path} (run `python -c 'import __graft_entry__ as g; g.build()'`)")
+            lib = ctypes.CDLL(path)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def lib():
+    """The library, on a HIP device. Raises when there is no GPU: the package has no CPU path."""
+    if not torch.cuda.is_available():
+        raise FemError("fem355 requires a HIP (MI355X) device; none is visible. There is no CPU fallback.")
+    return load_library()
+
+
+def check(rc: int, what: str = ""):
+    if rc == FEM_OK:
+        return
+    msg = (_lib.fem_last_error() or b"").decode(errors="replace") if _lib else ""
+    if rc == FEM_EBADTYPE:
+        raise ValueError(f"{what}: {msg}")
+    if rc == FEM_ESINGULAR:
+        raise ValueError("Singular matrix encountered while computing B matrix.")
+    raise FemError(f"fem355 {what} failed (code {rc}): {msg}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream(dev=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def compute_device(device=None) -> torch.device:
+    """The HIP device the work runs on: `device` itself when it is a cuda device, else the current one."""
+    if device is not None:
+        d = torch.device(device)
+        if d.type == "cuda":
+            return d if d.index is not None else torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cuda", torch.cuda.current_device())

@@ -1,0 +1,642 @@
+// Element stiffness quadrature (L1) and deterministic global assembly (row-gather) on gfx950.
+//
+// P1 tets use the closed form of the reference's B^T D B V (`solver/element.py:835-903`): with the
+// gradients g_a of the 4 barycentric shape functions and Lame constants
+//   lambda = E nu / ((1+nu)(1-2nu)),  mu = E / (2(1+nu))   (the D of `solver/element.py:282-306`),
+// block (a,b) of K_e is V (lambda g_a g_b^T + mu g_b g_a^T + mu (g_a.g_b) I). Isoparametric solids use
+// the same block formula per quadrature point with signed detJ (Q2), which is exactly B^T D B for the
+// isotropic D; only the rounding order differs from the reference's dense einsums.
+#include "common.hpp"
+
+namespace fem {
+
+struct Lame {
+    double lam, mu;
+};
+
+__host__ __device__ inline Lame lame(double E, double nu) {
+    // same coefficient the reference forms: coef = E/((1+nu)(1-2nu)); D33 = coef*(1-2nu)/2
+    double c = E / ((1.0 + nu) * (1.0 - 2.0 * nu));
+    return Lame{c * nu, c * ((1.0 - 2.0 * nu) / 2.0)};
+}
+
+// gradients of the P1 shape functions (rows of inv([1 x y z]) 1..3) and signed det of the edge matrix
+__device__ __forceinline__ double tet4_grads(const double* __restrict__ X, const int64_t* __restrict__ c,
+                                             double g[4][3]) {
+    double p[4][3];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+        const int64_t n = c[a];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) p[a][k] = X[3 * n + k];
+    }
+    double e1[3], e2[3], e3[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        e1[k] = p[1][k] - p[0][k];
+        e2[k] = p[2][k] - p[0][k];
+        e3[k] = p[3][k] - p[0][k];
+    }
+    double c23[3] = {e2[1] * e3[2] - e2[2] * e3[1], e2[2] * e3[0] - e2[0] * e3[2], e2[0] * e3[1] - e2[1] * e3[0]};
+    double c31[3] = {e3[1] * e1[2] - e3[2] * e1[1], e3[2] * e1[0] - e3[0] * e1[2], e3[0] * e1[1] - e3[1] * e1[0]};
+    double c12[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+    double det = e1[0] * c23[0] + e1[1] * c23[1] + e1[2] * c23[2];
+    double inv = 1.0 / det;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        g[1][k] = c23[k] * inv;
+        g[2][k] = c31[k] * inv;
+        g[3][k] = c12[k] * inv;
+        g[0][k] = -(g[1][k] + g[2][k] + g[3][k]);
+    }
+    return det;
+}
+
+// ---------------------------------------------------------------- c3d4 element matrices
+// 64 elements per 256-thread block: 64 lanes form gradients into LDS, then all 256 threads write the
+// block's contiguous output (64 * d * d values) coalesced.
+template <int KIND>
+__global__ void __launch_bounds__(256) k_tet4_ke(const double* __restrict__ X, const int64_t* __restrict__ conn,
+                                                 int64_t M, double E, double nu, double* __restrict__ Ke,
+                                                 int64_t* __restrict__ bad) {
+    constexpr int D = (KIND == FEM_KIND_POISSON) ? 4 : 12;
+    __shared__ double g_s[64][4][3];
+    __shared__ double v_s[64];
+    const int64_t e0 = (int64_t)blockIdx.x * 64;
+    if (threadIdx.x < 64) {
+        int64_t e = e0 + threadIdx.x;
+        if (e < M) {
+            double g[4][3];
+            double det = tet4_grads(X, conn + 4 * e, g);
+            if (fabs(det) < 1e-12) atomicMin((unsigned long long*)bad, (unsigned long long)e);
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int k = 0; k < 3; ++k) g_s[threadIdx.x][a][k] = g[a][k];
+            v_s[threadIdx.x] = fabs(det) / 6.0;
+        }
+    }
+    __syncthreads();
+    const Lame L = lame(E, nu);
+    const int64_t nval = min((int64_t)64, M - e0) * D * D;
+    double* out = Ke + e0 * D * D;
+    for (int64_t t = threadIdx.x; t < nval; t += 256) {
+        const int le = (int)(t / (D * D));
+        const int ij = (int)(t - (int64_t)le * D * D);
+        const int i = ij / D, j = ij - (ij / D) * D;
+        const double V = v_s[le];
+        double val;
+        if (KIND == FEM_KIND_ELASTIC) {
+            const int a = i / 3, ci = i - 3 * (i / 3), b = j / 3, cj = j - 3 * (j / 3);
+            const double* ga = g_s[le][a];
+            const double* gb = g_s[le][b];
+            double s = L.lam * ga[ci] * gb[cj] + L.mu * ga[cj] * gb[ci];
+            if (ci == cj) s += L.mu * (ga[0] * gb[0] + ga[1] * gb[1] + ga[2] * gb[2]);
+            val = s * V;
+        } else if (KIND == FEM_KIND_POISSON) {
+            const double* ga = g_s[le][i];
+            const double* gb = g_s[le][j];
+            val = E * (ga[0] * gb[0] + ga[1] * gb[1] + ga[2] * gb[2]) * V;
+        } else {  // consistent P1 mass, rho V (1 + delta_ab) / 20 per component (E carries rho)
+            const int a = i / 3, ci = i - 3 * (i / 3), b = j / 3, cj = j - 3 * (j / 3);
+            val = (ci == cj) ? E * V * ((a == b) ? 2.0 : 1.0) / 20.0 : 0.0;
+        }
+        out[t] = val;
+    }
+}
+
+// volumes / gradients / B of c3d4 (`compute_tetrahedral_volumes` `solver/element.py:514-541`,
+// `compute_c3d4_B_matrix` `:835-881`); any output pointer may be null.
+__global__ void __launch_bounds__(256) k_tet4_geom(const double* __restrict__ X, const int64_t* __restrict__ conn,
+                                                   int64_t M, double* __restrict__ vol, double* __restrict__ grads,
+                                                   double* __restrict__ B, int64_t* __restrict__ bad) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < M; e += (int64_t)gridDim.x * blockDim.x) {
+        double g[4][3];
+        const double det = tet4_grads(X, conn + 4 * e, g);
+        if (bad && fabs(det) < 1e-12) atomicMin((unsigned long long*)bad, (unsigned long long)e);
+        if (vol) vol[e] = fabs(det) / 6.0;
+        if (grads)
+            for (int a = 0; a < 4; ++a)
+                for (int k = 0; k < 3; ++k) grads[e * 12 + a * 3 + k] = g[a][k];
+        if (B) {
+            double* b = B + e * 72;
+            for (int t = 0; t < 72; ++t) b[t] = 0.0;
+            for (int a = 0; a < 4; ++a) {
+                const double gx = g[a][0], gy = g[a][1], gz = g[a][2];
+                b[0 * 12 + 3 * a] = gx;
+                b[1 * 12 + 3 * a + 1] = gy;
+                b[2 * 12 + 3 * a + 2] = gz;
+                b[3 * 12 + 3 * a] = gy;
+                b[3 * 12 + 3 * a + 1] = gx;
+                b[4 * 12 + 3 * a + 1] = gz;
+                b[4 * 12 + 3 * a + 2] = gy;
+                b[5 * 12 + 3 * a] = gz;
+                b[5 * 12 + 3 * a + 2] = gx;
+            }
+        }
+    }
+}
+
+// Jacobian / global gradients / B of an isoparametric element at ONE point (dN [npe,3] natural derivatives):
+// compute_c3d8_Jacobian `solver/element.py:1601-1632`, _shape_gradients `:1634-1664`, _B_matrix `:1666-1694`
+// (and the c3d6 `:2482-2568` / c3d10 `:1026-1125` equivalents). Thread per element; outputs may be null.
+__global__ void __launch_bounds__(256) k_iso_geom(const double* __restrict__ X, const int64_t* __restrict__ conn,
+                                                  int64_t M, int npe, const double* __restrict__ dN,
+                                                  double* __restrict__ Jout, double* __restrict__ Gout,
+                                                  double* __restrict__ Bout) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < M; e += (int64_t)gridDim.x * blockDim.x) {
+        double J[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (int j = 0; j < npe; ++j) {
+            const int64_t n = conn[e * npe + j];
+            const double x0 = X[3 * n], x1 = X[3 * n + 1], x2 = X[3 * n + 2];
+            for (int i = 0; i < 3; ++i) {
+                const double d = dN[j * 3 + i];
+                J[3 * i] += d * x0;
+                J[3 * i + 1] += d * x1;
+                J[3 * i + 2] += d * x2;
+            }
+        }
+        if (Jout)
+            for (int t = 0; t < 9; ++t) Jout[e * 9 + t] = J[t];
+        if (!Gout && !Bout) continue;
+        const double c00 = J[4] * J[8] - J[5] * J[7], c01 = J[5] * J[6] - J[3] * J[8], c02 = J[3] * J[7] - J[4] * J[6];
+        const double id = 1.0 / (J[0] * c00 + J[1] * c01 + J[2] * c02);
+        const double Ji[9] = {c00 * id, (J[2] * J[7] - J[1] * J[8]) * id, (J[1] * J[5] - J[2] * J[4]) * id,
+                              c01 * id, (J[0] * J[8] - J[2] * J[6]) * id, (J[2] * J[3] - J[0] * J[5]) * id,
+                              c02 * id, (J[1] * J[6] - J[0] * J[7]) * id, (J[0] * J[4] - J[1] * J[3]) * id};
+        const int d3 = 3 * npe;
+        if (Bout)
+            for (int t = 0; t < 6 * d3; ++t) Bout[e * 6 * d3 + t] = 0.0;
+        for (int n = 0; n < npe; ++n) {
+            double g[3];
+            for (int i = 0; i < 3; ++i)
+                g[i] = Ji[3 * i] * dN[n * 3] + Ji[3 * i + 1] * dN[n * 3 + 1] + Ji[3 * i + 2] * dN[n * 3 + 2];
+            if (Gout)
+                for (int i = 0; i < 3; ++i) Gout[(e * npe + n) * 3 + i] = g[i];
+            if (Bout) {
+                double* b = Bout + e * 6 * d3;
+                b[0 * d3 + 3 * n] = g[0];
+                b[1 * d3 + 3 * n + 1] = g[1];
+                b[2 * d3 + 3 * n + 2] = g[2];
+                b[3 * d3 + 3 * n] = g[1];
+                b[3 * d3 + 3 * n + 1] = g[0];
+                b[4 * d3 + 3 * n + 1] = g[2];
+                b[4 * d3 + 3 * n + 2] = g[1];
+                b[5 * d3 + 3 * n] = g[2];
+                b[5 * d3 + 3 * n + 2] = g[0];
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- isoparametric solids (wave per element)
+constexpr int ISO_MAX_IP = 32;
+
+template <int NPE>
+__global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, const int64_t* __restrict__ conn,
+                                                int64_t M, double E, double nu, const double* __restrict__ dN,
+                                                const double* __restrict__ w, int n_ip, int mode,
+                                                double* __restrict__ Ke) {
+    constexpr int D = 3 * NPE;
+    constexpr int NB = NPE * NPE;
+    __shared__ double dn_s[ISO_MAX_IP * NPE * 3];
+    __shared__ double x_s[4][NPE][3];
+    __shared__ double g_s[4][NPE][3];
+    __shared__ double J_s[4][9];
+    for (int t = threadIdx.x; t < n_ip * NPE * 3; t += 256) dn_s[t] = dN[t];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t e = (int64_t)blockIdx.x * 4 + wid;
+    const bool active = e < M;
+    if (active && lane < NPE * 3) {
+        int a = lane / 3, k = lane - 3 * (lane / 3);
+        x_s[wid][a][k] = X[3 * conn[e * NPE + a] + k];
+    }
+    __syncthreads();
+    const Lame L = lame(E, nu);
+    double acc[2][9];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[q][t] = 0.0;
+
+    double vol = 0.0;
+    if (mode == FEM_ISO_VOLUME) {  // wedge volume: 3 sub-tets (`solver/element.py:2198-2232`)
+        const int T[3][4] = {{0, 1, 2, 3}, {1, 2, 4, 3}, {2, 4, 5, 3}};
+        for (int s = 0; s < 3; ++s) {
+            double u[3], v[3], d[3];
+            for (int k = 0; k < 3; ++k) {
+                u[k] = x_s[wid][T[s][1]][k] - x_s[wid][T[s][0]][k];
+                v[k] = x_s[wid][T[s][2]][k] - x_s[wid][T[s][0]][k];
+                d[k] = x_s[wid][T[s][3]][k] - x_s[wid][T[s][0]][k];
+            }
+            double cx = u[1] * v[2] - u[2] * v[1], cy = u[2] * v[0] - u[0] * v[2], cz = u[0] * v[1] - u[1] * v[0];
+            vol += fabs(cx * d[0] + cy * d[1] + cz * d[2]) / 6.0;
+        }
+    }
+
+    for (int q = 0; q < n_ip; ++q) {
+        const double* dq = dn_s + q * NPE * 3;
+        // J[i][k] = sum_j dN[j][i] x[j][k]  (`einsum("ji,mjk->mik")`)
+        if (lane < 9) {
+            int i = lane / 3, k = lane - 3 * (lane / 3);
+            double s = 0.0;
+#pragma unroll
+            for (int j = 0; j < NPE; ++j) s += dq[j * 3 + i] * x_s[wid][j][k];
+            J_s[wid][lane] = s;
+        }
+        __syncthreads();
+        const double* J = J_s[wid];
+        double c00 = J[4] * J[8] - J[5] * J[7], c01 = J[5] * J[6] - J[3] * J[8], c02 = J[3] * J[7] - J[4] * J[6];
+        double det = J[0] * c00 + J[1] * c01 + J[2] * c02;
+        double id = 1.0 / det;
+        double Ji[9] = {c00 * id, (J[2] * J[7] - J[1] * J[8]) * id, (J[1] * J[5] - J[2] * J[4]) * id,
+                        c01 * id, (J[0] * J[8] - J[2] * J[6]) * id, (J[2] * J[3] - J[0] * J[5]) * id,
+                        c02 * id, (J[1] * J[6] - J[0] * J[7]) * id, (J[0] * J[4] - J[1] * J[3]) * id};
+        // global gradients g_n = Jinv dN_n (`einsum("mij,nj->mni")`)
+        if (lane < NPE * 3) {
+            int n = lane / 3, i = lane - 3 * (lane / 3);
+            g_s[wid][n][i] = Ji[3 * i] * dq[n * 3] + Ji[3 * i + 1] * dq[n * 3 + 1] + Ji[3 * i + 2] * dq[n * 3 + 2];
+        }
+        __syncthreads();
+        const double coef = (mode == FEM_ISO_SUM) ? det * w[q] : (mode == FEM_ISO_STACK ? det : vol);
+#pragma unroll
+        for (int slot = 0; slot < 2; ++slot) {
+            const int blk = lane + 64 * slot;
+            if (blk < NB) {
+                const int a = blk / NPE, b = blk - NPE * (blk / NPE);
+                const double* ga = g_s[wid][a];
+                const double* gb = g_s[wid][b];
+                const double dot = ga[0] * gb[0] + ga[1] * gb[1] + ga[2] * gb[2];
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        double s = L.lam * ga[i] * gb[k] + L.mu * ga[k] * gb[i];
+                        if (i == k) s += L.mu * dot;
+                        if (mode == FEM_ISO_STACK) acc[slot][3 * i + k] = s * coef;
+                        else acc[slot][3 * i + k] += s * coef;
+                    }
+            }
+        }
+        if (mode == FEM_ISO_STACK && active) {
+            double* out = Ke + ((int64_t)q * M + e) * D * D;
+#pragma unroll
+            for (int slot = 0; slot < 2; ++slot) {
+                const int blk = lane + 64 * slot;
+                if (blk < NB) {
+                    const int a = blk / NPE, b = blk - NPE * (blk / NPE);
+#pragma unroll
+                    for (int i = 0; i < 3; ++i)
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) out[(3 * a + i) * D + 3 * b + k] = acc[slot][3 * i + k];
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (mode != FEM_ISO_STACK && active) {
+        double* out = Ke + e * D * D;
+#pragma unroll
+        for (int slot = 0; slot < 2; ++slot) {
+            const int blk = lane + 64 * slot;
+            if (blk < NB) {
+                const int a = blk / NPE, b = blk - NPE * (blk / NPE);
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) out[(3 * a + i) * D + 3 * b + k] = acc[slot][3 * i + k];
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- SELL value addressing
+// entry index E = slice_ptr[s] + 64 k + lane  ->  value index of block entry rc (row-major in the block)
+__device__ __forceinline__ int64_t sell_val(int64_t E, int bs2, int rc) {
+    const int64_t lane = E & 63;
+    return (E - lane) * bs2 + (int64_t)rc * 64 + lane;
+}
+
+__device__ __forceinline__ int find_col(const int32_t* __restrict__ colidx, int lo, int hi, int j) {
+    // binary search of column j in the sorted row [lo, hi)
+    while (lo < hi) {
+        int mid = (lo + hi) >> 1;
+        if (colidx[mid] < j) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// ---------------------------------------------------------------- row-gather assembly from element matrices
+template <int BS>
+__global__ void __launch_bounds__(256) k_assemble_from_ke(const double* __restrict__ Ke, const int64_t* __restrict__ conn,
+                                                          int npe, const int32_t* __restrict__ inc_ptr,
+                                                          const int32_t* __restrict__ inc, int64_t N,
+                                                          const int32_t* __restrict__ rowptr,
+                                                          const int32_t* __restrict__ colidx,
+                                                          const int64_t* __restrict__ csr2sell,
+                                                          double* __restrict__ vals) {
+    const int d = npe * BS;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
+        const int lo = rowptr[i], hi = rowptr[i + 1];
+        for (int t = inc_ptr[i]; t < inc_ptr[i + 1]; ++t) {
+            const int ea = inc[t];
+            const int64_t e = ea / npe;
+            const int a = ea - (int)e * npe;
+            const double* Krow = Ke + e * d * d + (int64_t)(a * BS) * d;
+            for (int b = 0; b < npe; ++b) {
+                const int j = (int)conn[e * npe + b];
+                const int p = find_col(colidx, lo, hi, j);
+                const int64_t E = csr2sell[p];
+#pragma unroll
+                for (int r = 0; r < BS; ++r)
+#pragma unroll
+                    for (int c = 0; c < BS; ++c) vals[sell_val(E, BS * BS, r * BS + c)] += Krow[r * d + b * BS + c];
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- fused c3d4 assembly (K_e never stored)
+template <int BS>
+__global__ void __launch_bounds__(256) k_assemble_tet4(const double* __restrict__ X, const int64_t* __restrict__ conn,
+                                                       double E, double nu, const int32_t* __restrict__ inc_ptr,
+                                                       const int32_t* __restrict__ inc, int64_t N,
+                                                       const int32_t* __restrict__ rowptr,
+                                                       const int32_t* __restrict__ colidx,
+                                                       const int64_t* __restrict__ csr2sell, double* __restrict__ vals,
+                                                       int64_t* __restrict__ bad) {
+    const Lame L = lame(E, nu);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
+        const int lo = rowptr[i], hi = rowptr[i + 1];
+        for (int t = inc_ptr[i]; t < inc_ptr[i + 1]; ++t) {
+            const int ea = inc[t];
+            const int64_t e = ea >> 2;
+            const int a = ea & 3;
+            const int64_t* c = conn + 4 * e;
+            double g[4][3];
+            const double det = tet4_grads(X, c, g);
+            if (fabs(det) < 1e-12) atomicMin((unsigned long long*)bad, (unsigned long long)e);
+            const double V = fabs(det) / 6.0;
+            for (int b = 0; b < 4; ++b) {
+                const int j = (int)c[b];
+                const int p = find_col(colidx, lo, hi, j);
+                const int64_t Ei = csr2sell[p];
+                const double dot = g[a][0] * g[b][0] + g[a][1] * g[b][1] + g[a][2] * g[b][2];
+                if (BS == 1) {
+                    vals[Ei] += E * dot * V;
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 3; ++r)
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) {
+                            double s = L.lam * g[a][r] * g[b][k] + L.mu * g[a][k] * g[b][r];
+                            if (r == k) s += L.mu * dot;
+                            vals[sell_val(Ei, 9, r * 3 + k)] += s * V;
+                        }
+                }
+            }
+        }
+    }
+}
+
+template <int BS>
+__global__ void k_sell_to_csr(const double* __restrict__ vals, const int32_t* __restrict__ rowptr, int64_t nrows,
+                              const int64_t* __restrict__ csr2sell, double* __restrict__ out) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x)
+        for (int p = rowptr[r]; p < rowptr[r + 1]; ++p) {
+            const int64_t E = csr2sell[p];
+#pragma unroll
+            for (int rc = 0; rc < BS * BS; ++rc) out[(int64_t)p * BS * BS + rc] = vals[sell_val(E, BS * BS, rc)];
+        }
+}
+
+__global__ void k_jacobi(const double* __restrict__ vals, int bs, const int32_t* __restrict__ diagpos,
+                         const int64_t* __restrict__ csr2sell, int64_t nrows, const uint8_t* __restrict__ mask,
+                         double* __restrict__ w) {
+    const int64_t n = nrows * bs;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t node = i / bs;
+        const int r = (int)(i - node * bs);
+        const double dg = vals[sell_val(csr2sell[diagpos[node]], bs * bs, r * bs + r)];
+        double v = 1.0 / dg;
+        if (v == INFINITY) v = 0.0;  // `solver/solver.py:831` (only +inf)
+        if (mask && mask[i]) v = 0.0;
+        w[i] = v;
+    }
+}
+
+// ---------------------------------------------------------------- element-by-element operator
+template <int DPN>
+__global__ void __launch_bounds__(256) k_ebe_apply(const double* __restrict__ Ke, const int64_t* __restrict__ conn,
+                                                   int npe, const int32_t* __restrict__ inc_ptr,
+                                                   const int32_t* __restrict__ inc, int64_t N,
+                                                   const double* __restrict__ u, double* __restrict__ y) {
+    const int d = npe * DPN;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
+        double acc[DPN];
+#pragma unroll
+        for (int r = 0; r < DPN; ++r) acc[r] = 0.0;
+        for (int t = inc_ptr[i]; t < inc_ptr[i + 1]; ++t) {
+            const int ea = inc[t];
+            const int64_t e = ea / npe;
+            const int a = ea - (int)e * npe;
+            const double* Krow = Ke + e * d * d + (int64_t)(a * DPN) * d;
+            double f[DPN];
+#pragma unroll
+            for (int r = 0; r < DPN; ++r) f[r] = 0.0;
+            for (int b = 0; b < npe; ++b) {
+                const int64_t j = conn[e * npe + b];
+#pragma unroll
+                for (int c = 0; c < DPN; ++c) {
+                    const double uj = u[j * DPN + c];
+#pragma unroll
+                    for (int r = 0; r < DPN; ++r) f[r] += Krow[r * d + b * DPN + c] * uj;
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < DPN; ++r) acc[r] += f[r];
+        }
+#pragma unroll
+        for (int r = 0; r < DPN; ++r) y[i * DPN + r] = acc[r];
+    }
+}
+
+template <int DPN>
+__global__ void k_ebe_diag(const double* __restrict__ Ke, int npe, const int32_t* __restrict__ inc_ptr,
+                           const int32_t* __restrict__ inc, int64_t N, int colzero, double* __restrict__ diag) {
+    const int d = npe * DPN;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
+        double acc[DPN];
+#pragma unroll
+        for (int r = 0; r < DPN; ++r) acc[r] = 0.0;
+        for (int t = inc_ptr[i]; t < inc_ptr[i + 1]; ++t) {
+            const int ea = inc[t];
+            const int64_t e = ea / npe;
+            const int a = ea - (int)e * npe;
+#pragma unroll
+            for (int r = 0; r < DPN; ++r) {
+                const int row = a * DPN + r;
+                acc[r] += Ke[e * d * d + (int64_t)row * d + (colzero ? 0 : row)];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < DPN; ++r) diag[i * DPN + r] = acc[r];
+    }
+}
+
+__global__ void k_invert(const double* __restrict__ in, int64_t n, double* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        double v = 1.0 / in[i];
+        out[i] = (v == INFINITY) ? 0.0 : v;
+    }
+}
+
+}  // namespace fem
+
+using namespace fem;
+
+extern "C" {
+
+int fem_tet4_ke(const double* coords, const int64_t* conn, int64_t M, double E, double nu, int kind, double* Ke,
+                int64_t* bad_idx, fem_stream_t stream) {
+    if (M <= 0) return FEM_OK;
+    dim3 g((unsigned)cdiv(M, 64));
+    if (kind == FEM_KIND_ELASTIC)
+        hipLaunchKernelGGL(k_tet4_ke<FEM_KIND_ELASTIC>, g, dim3(256), 0, S(stream), coords, conn, M, E, nu, Ke, bad_idx);
+    else if (kind == FEM_KIND_POISSON)
+        hipLaunchKernelGGL(k_tet4_ke<FEM_KIND_POISSON>, g, dim3(256), 0, S(stream), coords, conn, M, E, nu, Ke, bad_idx);
+    else if (kind == FEM_KIND_MASS)
+        hipLaunchKernelGGL(k_tet4_ke<FEM_KIND_MASS>, g, dim3(256), 0, S(stream), coords, conn, M, E, nu, Ke, bad_idx);
+    else {
+        set_error("fem_tet4_ke: unknown kind %d", kind);
+        return FEM_EARG;
+    }
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_tet4_geom(const double* coords, const int64_t* conn, int64_t M, double* vol, double* grads, double* B,
+                  int64_t* bad_idx, fem_stream_t stream) {
+    if (M <= 0) return FEM_OK;
+    hipLaunchKernelGGL(k_tet4_geom, dim3(stream_grid(M, 256)), dim3(256), 0, S(stream), coords, conn, M, vol, grads, B,
+                       bad_idx);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_iso_geom(const double* coords, const int64_t* conn, int64_t M, int npe, const double* dN, double* J,
+                 double* grads, double* B, fem_stream_t stream) {
+    if (M <= 0) return FEM_OK;
+    if (npe != 6 && npe != 8 && npe != 10) {
+        set_error("fem_iso_geom: unsupported nodes per element %d", npe);
+        return FEM_EBADTYPE;
+    }
+    hipLaunchKernelGGL(k_iso_geom, dim3(stream_grid(M, 256)), dim3(256), 0, S(stream), coords, conn, M, npe, dN, J,
+                       grads, B);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_iso_ke(const double* coords, const int64_t* conn, int64_t M, int npe, double E, double nu, const double* dN,
+               const double* w, int n_ip, int mode, double* Ke, fem_stream_t stream) {
+    if (M <= 0) return FEM_OK;
+    if (n_ip < 1 || n_ip > ISO_MAX_IP) {
+        set_error("fem_iso_ke: n_ip = %d out of range [1, %d]", n_ip, ISO_MAX_IP);
+        return FEM_EARG;
+    }
+    dim3 g((unsigned)cdiv(M, 4));
+    switch (npe) {
+        case 6: hipLaunchKernelGGL(k_iso_ke<6>, g, dim3(256), 0, S(stream), coords, conn, M, E, nu, dN, w, n_ip, mode, Ke); break;
+        case 8: hipLaunchKernelGGL(k_iso_ke<8>, g, dim3(256), 0, S(stream), coords, conn, M, E, nu, dN, w, n_ip, mode, Ke); break;
+        case 10: hipLaunchKernelGGL(k_iso_ke<10>, g, dim3(256), 0, S(stream), coords, conn, M, E, nu, dN, w, n_ip, mode, Ke); break;
+        default: set_error("fem_iso_ke: unsupported nodes per element %d", npe); return FEM_EBADTYPE;
+    }
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_assemble_from_ke(const double* Ke, const int64_t* conn, int npe, int bs, const int32_t* inc_ptr,
+                         const int32_t* inc, int64_t N, const int32_t* rowptr, const int32_t* colidx,
+                         const int64_t* csr2sell, const int64_t* slice_ptr, double* vals, fem_stream_t stream) {
+    (void)slice_ptr;
+    dim3 g(stream_grid(N, 256));
+    if (bs == 1)
+        hipLaunchKernelGGL(k_assemble_from_ke<1>, g, dim3(256), 0, S(stream), Ke, conn, npe, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals);
+    else if (bs == 3)
+        hipLaunchKernelGGL(k_assemble_from_ke<3>, g, dim3(256), 0, S(stream), Ke, conn, npe, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals);
+    else {
+        set_error("fem_assemble_from_ke: block size %d unsupported", bs);
+        return FEM_EARG;
+    }
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_assemble_tet4(const double* coords, const int64_t* conn, double E, double nu, int bs, const int32_t* inc_ptr,
+                      const int32_t* inc, int64_t N, const int32_t* rowptr, const int32_t* colidx,
+                      const int64_t* csr2sell, const int64_t* slice_ptr, double* vals, int64_t* bad_idx,
+                      fem_stream_t stream) {
+    (void)slice_ptr;
+    dim3 g(stream_grid(N, 256));
+    if (bs == 1)
+        hipLaunchKernelGGL(k_assemble_tet4<1>, g, dim3(256), 0, S(stream), coords, conn, E, nu, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals, bad_idx);
+    else if (bs == 3)
+        hipLaunchKernelGGL(k_assemble_tet4<3>, g, dim3(256), 0, S(stream), coords, conn, E, nu, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals, bad_idx);
+    else {
+        set_error("fem_assemble_tet4: block size %d unsupported", bs);
+        return FEM_EARG;
+    }
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_sell_to_csr_vals(const double* vals, int bs, const int32_t* rowptr, int64_t nrows, const int64_t* csr2sell,
+                         const int64_t* slice_ptr, double* csr_vals, fem_stream_t stream) {
+    (void)slice_ptr;
+    dim3 g(stream_grid(nrows, 256));
+    if (bs == 1) hipLaunchKernelGGL(k_sell_to_csr<1>, g, dim3(256), 0, S(stream), vals, rowptr, nrows, csr2sell, csr_vals);
+    else if (bs == 3) hipLaunchKernelGGL(k_sell_to_csr<3>, g, dim3(256), 0, S(stream), vals, rowptr, nrows, csr2sell, csr_vals);
+    else { set_error("fem_sell_to_csr_vals: block size %d unsupported", bs); return FEM_EARG; }
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_jacobi(const double* vals, int bs, const int32_t* rowptr, const int32_t* diagpos, const int64_t* csr2sell,
+               const int64_t* slice_ptr, int64_t nrows, const uint8_t* mask, double* w, fem_stream_t stream) {
+    (void)rowptr;
+    (void)slice_ptr;
+    hipLaunchKernelGGL(k_jacobi, dim3(stream_grid(nrows * bs, 256)), dim3(256), 0, S(stream), vals, bs, diagpos,
+                       csr2sell, nrows, mask, w);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_ebe_apply(const double* Ke, const int64_t* conn, int npe, int dpn, const int32_t* inc_ptr, const int32_t* inc,
+                  int64_t N, const double* u, double* y, fem_stream_t stream) {
+    dim3 g(stream_grid(N, 256));
+    if (dpn == 1) hipLaunchKernelGGL(k_ebe_apply<1>, g, dim3(256), 0, S(stream), Ke, conn, npe, inc_ptr, inc, N, u, y);
+    else if (dpn == 3) hipLaunchKernelGGL(k_ebe_apply<3>, g, dim3(256), 0, S(stream), Ke, conn, npe, inc_ptr, inc, N, u, y);
+    else { set_error("fem_ebe_apply: dofs per node %d unsupported", dpn); return FEM_EARG; }
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_ebe_diag(const double* Ke, const int64_t* conn, int npe, int dpn, const int32_t* inc_ptr, const int32_t* inc,
+                 int64_t N, int colzero, double* diag, fem_stream_t stream) {
+    (void)conn;
+    dim3 g(stream_grid(N, 256));
+    if (dpn == 1) hipLaunchKernelGGL(k_ebe_diag<1>, g, dim3(256), 0, S(stream), Ke, npe, inc_ptr, inc, N, colzero, diag);
+    else if (dpn == 3) hipLaunchKernelGGL(k_ebe_diag<3>, g, dim3(256), 0, S(stream), Ke, npe, inc_ptr, inc, N, colzero, diag);
+    else { set_error("fem_ebe_diag: dofs per node %d unsupported", dpn); return FEM_EARG; }
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_invert_diag(const double* in, int64_t n, double* out, fem_stream_t stream) {
+    hipLaunchKernelGGL(k_invert, dim3(stream_grid(n, 256)), dim3(256), 0, S(stream), in, n, out);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+}  // extern "C"

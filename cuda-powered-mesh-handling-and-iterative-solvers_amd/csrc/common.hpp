@@ -1,0 +1,101 @@
+// Shared helpers for the fem355 HIP kernels (gfx950 / CDNA4: wave64, 256 CUs in 8 XCDs).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/fem355.h"
+
+namespace fem {
+
+constexpr int WAVE = 64;
+constexpr int NXCD = 8;
+
+// ---------------------------------------------------------------- error plumbing (host)
+void set_error(const char* fmt, ...);
+
+#define FEM_HIP(call)                                                                  \
+    do {                                                                               \
+        hipError_t _e = (call);                                                        \
+        if (_e != hipSuccess) {                                                        \
+            ::fem::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #call, hipGetErrorString(_e)); \
+            return FEM_EHIP;                                                           \
+        }                                                                              \
+    } while (0)
+
+#define FEM_LAUNCHED()                                                                 \
+    do {                                                                               \
+        hipError_t _e = hipGetLastError();                                             \
+        if (_e != hipSuccess) {                                                        \
+            ::fem::set_error("%s:%d launch -> %s", __FILE__, __LINE__, hipGetErrorString(_e)); \
+            return FEM_EHIP;                                                           \
+        }                                                                              \
+    } while (0)
+
+inline hipStream_t S(fem_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// grid for a grid-stride streaming kernel: enough blocks to fill 256 CUs a few times, multiple of 8 XCDs
+inline int stream_grid(int64_t work_items, int block) {
+    int64_t g = cdiv(work_items, block);
+    if (g > 2048) g = 2048;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+// ---------------------------------------------------------------- device reductions
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Sum over a 256-thread block; fixed tree -> deterministic. Result valid in every thread.
+__device__ __forceinline__ double block_sum256(double v, double* lds4) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) lds4[w] = v;
+    __syncthreads();
+    double t = (lds4[0] + lds4[1]) + (lds4[2] + lds4[3]);
+    return t;
+}
+
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Last-block-done ticket (agent-scope release/acquire, MI355X_MICROARCH.md §visibility): every block
+// publishes `partial` into partials[blockIdx.x]; returns true in the block whose arrival was last, after an
+// acquire, so it may read every partial. The counter is re-armed by the last block.
+__device__ __forceinline__ bool publish_partial(double partial, double* partials, unsigned* counter,
+                                                int* lds_flag) {
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(&partials[blockIdx.x], partial, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int last = (t == gridDim.x - 1);
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        *lds_flag = last;
+    }
+    __syncthreads();
+    return *lds_flag != 0;
+}
+
+// Deterministic sum of n partials by one 256-thread block (fixed order), valid in every thread.
+__device__ __forceinline__ double sum_partials(const double* partials, int n, double* lds4) {
+    double v = 0.0;
+    for (int i = threadIdx.x; i < n; i += 256)
+        v += __hip_atomic_load(&partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return block_sum256(v, lds4);
+}
+
+}  // namespace fem

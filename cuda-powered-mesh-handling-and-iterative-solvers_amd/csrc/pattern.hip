@@ -1,0 +1,223 @@
+// Mesh graph construction on the device: node->element incidence, node-graph CSR pattern, SELL-64 layout.
+//
+// The reference never assembles a CSR on its hot path (it is element-by-element, `solver/element.py:429-464`);
+// its only global matrix is the COO of `subdivision.ipynb:118-139`, coalesced by torch. The pattern built here
+// is exactly coalesce(COO) at node granularity (bit-exact against oracle.ref_cpu.node_pattern): every row
+// lists the unique nodes sharing an element with it, ascending.
+#include "common.hpp"
+
+namespace fem {
+
+// ---------------------------------------------------------------- incidence
+__global__ void k_inc_count(const int64_t* __restrict__ conn, int64_t total, int32_t* __restrict__ cnt) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x)
+        atomicAdd(&cnt[conn[i]], 1);
+}
+
+__global__ void k_inc_fill(const int64_t* __restrict__ conn, int64_t total, const int32_t* __restrict__ ptr,
+                           int32_t* __restrict__ cursor, int32_t* __restrict__ inc) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t node = conn[i];
+        int pos = atomicAdd(&cursor[node], 1);
+        inc[ptr[node] + pos] = (int32_t)i;
+    }
+}
+
+// Each node's segment is short (~24 for Kuhn tets): insertion sort makes the incidence deterministic.
+__global__ void k_inc_sort(const int32_t* __restrict__ ptr, int64_t N, int32_t* __restrict__ inc) {
+    for (int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; n < N; n += (int64_t)gridDim.x * blockDim.x) {
+        int b = ptr[n], e = ptr[n + 1];
+        for (int i = b + 1; i < e; ++i) {
+            int v = inc[i];
+            int j = i - 1;
+            while (j >= b && inc[j] > v) {
+                inc[j + 1] = inc[j];
+                --j;
+            }
+            inc[j + 1] = v;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- node graph (wave per node)
+constexpr int G_WAVES = 4;      // waves per block
+constexpr int G_CAP = 1536;     // candidate capacity per node (deg * npe)
+constexpr int G_UCAP = 512;     // unique-neighbour capacity per node
+
+template <bool FILL>
+__global__ void __launch_bounds__(256) k_graph(const int64_t* __restrict__ conn, int npe,
+                                               const int32_t* __restrict__ inc_ptr, const int32_t* __restrict__ inc,
+                                               int64_t N, int32_t* __restrict__ row_len,
+                                               const int32_t* __restrict__ rowptr, int32_t* __restrict__ colidx,
+                                               int32_t* __restrict__ diagpos, int32_t* __restrict__ overflow) {
+    __shared__ int cand[G_WAVES][G_CAP];
+    __shared__ int uniq[G_WAVES][G_UCAP];
+    const int wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+
+    for (int64_t base = (int64_t)blockIdx.x * G_WAVES; base < N; base += (int64_t)gridDim.x * G_WAVES) {
+        const int64_t node = base + wid;
+        const bool active = node < N;
+        int C = 0, start = 0;
+        if (active) {
+            start = inc_ptr[node];
+            C = (inc_ptr[node + 1] - start) * npe;
+        }
+        const bool ok = active && C <= G_CAP;
+        if (active && !ok) atomicMax(overflow, C);
+        // phase A: gather candidate neighbour nodes of all incident elements into LDS
+        if (ok) {
+            for (int t = lane; t < C; t += 64) {
+                int k = t / npe, b = t - k * npe;
+                int e = inc[start + k] / npe;
+                cand[wid][t] = (int)conn[(int64_t)e * npe + b];
+            }
+        }
+        __syncthreads();
+        // phase B: first occurrences -> compact unique list
+        int U = 0;
+        if (ok) {
+            for (int cb = 0; cb < C; cb += 64) {
+                int t = cb + lane;
+                bool first = false;
+                int v = 0;
+                if (t < C) {
+                    v = cand[wid][t];
+                    first = true;
+                    for (int u = 0; u < t; ++u)
+                        if (cand[wid][u] == v) { first = false; break; }
+                }
+                unsigned long long m = __ballot(first);
+                if (FILL && first) {
+                    int pos = U + __popcll(m & lt_mask);
+                    if (pos < G_UCAP) uniq[wid][pos] = v;
+                }
+                U += __popcll(m);
+            }
+            if (!FILL && lane == 0) row_len[node] = (U <= G_UCAP) ? U : 0;
+            if (U > G_UCAP && lane == 0) atomicMax(overflow, U);
+        } else if (active && !FILL && lane == 0) {
+            row_len[node] = 0;
+        }
+        __syncthreads();
+        // phase C (fill): rank-sort the unique list and write the row
+        if (FILL && ok && U <= G_UCAP) {
+            const int32_t rp = rowptr[node];
+            for (int j = lane; j < U; j += 64) {
+                int v = uniq[wid][j];
+                int rank = 0;
+                for (int u = 0; u < U; ++u) rank += (uniq[wid][u] < v);
+                colidx[rp + rank] = v;
+                if (v == (int)node) diagpos[node] = rp + rank;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------- SELL-64
+__global__ void k_sell_widths(const int32_t* __restrict__ rowptr, int64_t nrows, int64_t nslices,
+                              int64_t* __restrict__ width) {
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nslices; s += (int64_t)gridDim.x * blockDim.x) {
+        int w = 0;
+        int64_t r0 = s * 64, r1 = min(r0 + 64, nrows);
+        for (int64_t r = r0; r < r1; ++r) w = max(w, rowptr[r + 1] - rowptr[r]);
+        width[s] = (int64_t)w * 64;
+    }
+}
+
+__global__ void k_sell_fill(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ colidx, int64_t nrows,
+                            int64_t nslices, const int64_t* __restrict__ slice_ptr, int32_t* __restrict__ cols,
+                            int64_t* __restrict__ csr2sell) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nslices * 64; r += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = r >> 6;
+        const int lane = (int)(r & 63);
+        const int64_t e0 = slice_ptr[s] + lane;
+        const int w = (int)((slice_ptr[s + 1] - slice_ptr[s]) >> 6);
+        int len = 0, rp = 0;
+        if (r < nrows) {
+            rp = rowptr[r];
+            len = rowptr[r + 1] - rp;
+        }
+        const int pad = (r < nrows) ? (int)r : 0;
+        for (int k = 0; k < w; ++k) {
+            int64_t e = e0 + (int64_t)k * 64;
+            if (k < len) {
+                cols[e] = colidx[rp + k];
+                csr2sell[rp + k] = e;
+            } else {
+                cols[e] = pad;
+            }
+        }
+    }
+}
+
+}  // namespace fem
+
+using namespace fem;
+
+extern "C" {
+
+int fem_incidence(const int64_t* conn, int64_t M, int npe, int64_t N, int32_t* inc_ptr, int32_t* inc,
+                  int32_t* work, fem_stream_t stream) {
+    hipStream_t st = S(stream);
+    const int64_t total = M * npe;
+    if (total >= (int64_t)1 << 31) {
+        set_error("fem_incidence: M*npe = %lld exceeds int32 range", (long long)total);
+        return FEM_EARG;
+    }
+    int32_t* cnt = work;
+    int32_t* scan_work = work + N;
+    FEM_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t) * N, st));
+    hipLaunchKernelGGL(k_inc_count, dim3(stream_grid(total, 256)), dim3(256), 0, st, conn, total, cnt);
+    FEM_LAUNCHED();
+    int rc = fem_scan_i32(cnt, N, inc_ptr, scan_work, stream);
+    if (rc) return rc;
+    FEM_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t) * N, st));
+    hipLaunchKernelGGL(k_inc_fill, dim3(stream_grid(total, 256)), dim3(256), 0, st, conn, total, inc_ptr, cnt, inc);
+    FEM_LAUNCHED();
+    hipLaunchKernelGGL(k_inc_sort, dim3(stream_grid(N, 256)), dim3(256), 0, st, inc_ptr, N, inc);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+static int graph_grid(int64_t N) {
+    int64_t g = cdiv(N, G_WAVES);
+    if (g > 4096) g = 4096;
+    return (int)(g < 1 ? 1 : g);
+}
+
+int fem_graph_count(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
+                    int32_t* row_len, int32_t* overflow, fem_stream_t stream) {
+    hipLaunchKernelGGL(k_graph<false>, dim3(graph_grid(N)), dim3(256), 0, S(stream), conn, npe, inc_ptr, inc, N,
+                       row_len, (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, overflow);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_graph_fill(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
+                   const int32_t* rowptr, int32_t* colidx, int32_t* diagpos, fem_stream_t stream) {
+    hipLaunchKernelGGL(k_graph<true>, dim3(graph_grid(N)), dim3(256), 0, S(stream), conn, npe, inc_ptr, inc, N,
+                       (int32_t*)nullptr, rowptr, colidx, diagpos, (int32_t*)nullptr);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_sell_widths(const int32_t* rowptr, int64_t nrows, int64_t* width, fem_stream_t stream) {
+    int64_t ns = cdiv(nrows, 64);
+    hipLaunchKernelGGL(k_sell_widths, dim3(stream_grid(ns, 256)), dim3(256), 0, S(stream), rowptr, nrows, ns, width);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_sell_fill(const int32_t* rowptr, const int32_t* colidx, int64_t nrows, const int64_t* slice_ptr,
+                  int32_t* cols, int64_t* csr2sell, fem_stream_t stream) {
+    int64_t ns = cdiv(nrows, 64);
+    hipLaunchKernelGGL(k_sell_fill, dim3(stream_grid(ns * 64, 256)), dim3(256), 0, S(stream), rowptr, colidx, nrows,
+                       ns, slice_ptr, cols, csr2sell);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,589 @@
+// SELL-64 SpMV and the device-resident (P)CG iteration (L2 + L3 of the hot path).
+//
+// Replaces the reference's per-iteration op chain (`solver/solver.py:182-224` / `:798-810`): EBE matvec via
+// gather + bmm + index_add (`solver/element.py:429-464`), torch.sum dots and axpys, with three kernels per
+// iteration and no host synchronisation:
+//   K1 spmv_dot : q = A p (SELL-64, one wave per 64-row slice, XCD-contiguous slice ranges), p.q partials,
+//                 the last block forms pq, the breakdown guards and alpha
+//   K2 update   : r <- r - alpha q (masked in CG mode), z = w r, r.z partials; last block: stop test, beta
+//   K3 pupdate  : x <- x + alpha p ; p <- z + beta p  (x update deferred here so p is read once)
+// Scalars and the stop flag live in device memory; kernels after a stop are no-ops, so the host enqueues
+// chunks of iterations and polls once per chunk.
+#include <vector>
+
+#include "common.hpp"
+
+namespace fem {
+
+// ---------------------------------------------------------------- SELL SpMV core
+// One wave = one slice of 64 block rows; lane = row. Row entries are strided by 64, so every load of the
+// wave (cols, each of the bs*bs value planes) is one contiguous 256/512-byte segment; on meshes numbered
+// along lines the x gathers of neighbouring lanes are contiguous too.
+template <int BS>
+__device__ __forceinline__ void sell_row(int64_t s, int lane, const int64_t* __restrict__ slice_ptr,
+                                         const int32_t* __restrict__ cols, const double* __restrict__ vals,
+                                         const double* __restrict__ x, double out[BS]) {
+    const int64_t p0 = slice_ptr[s];
+    const int w = (int)((slice_ptr[s + 1] - p0) >> 6);
+    const int32_t* c = cols + p0 + lane;
+#pragma unroll
+    for (int r = 0; r < BS; ++r) out[r] = 0.0;
+    if (BS == 1) {
+        const double* v = vals + p0 + lane;
+        int k = 0;
+        for (; k + 4 <= w; k += 4) {
+            int c0 = c[64 * k], c1 = c[64 * (k + 1)], c2 = c[64 * (k + 2)], c3 = c[64 * (k + 3)];
+            double v0 = v[64 * k], v1 = v[64 * (k + 1)], v2 = v[64 * (k + 2)], v3 = v[64 * (k + 3)];
+            double x0 = x[c0], x1 = x[c1], x2 = x[c2], x3 = x[c3];
+            out[0] += v0 * x0;
+            out[0] += v1 * x1;
+            out[0] += v2 * x2;
+            out[0] += v3 * x3;
+        }
+        for (; k < w; ++k) out[0] += v[64 * k] * x[c[64 * k]];
+    } else {
+        const double* v = vals + p0 * (BS * BS) + lane;
+        for (int k = 0; k < w; ++k) {
+            const int64_t cc = (int64_t)c[64 * k] * BS;
+            double xv[BS];
+#pragma unroll
+            for (int j = 0; j < BS; ++j) xv[j] = x[cc + j];
+            const double* vk = v + (int64_t)64 * BS * BS * k;
+#pragma unroll
+            for (int r = 0; r < BS; ++r)
+#pragma unroll
+                for (int j = 0; j < BS; ++j) out[r] += vk[64 * (r * BS + j)] * xv[j];
+        }
+    }
+}
+
+// XCD-aware slice walk: XCD x (= blockIdx % 8 under the observed round-robin placement; speed only) owns the
+// contiguous slice range [x*spx, (x+1)*spx), walked 4 slices (one per wave) per block step.
+struct SliceWalk {
+    int64_t s, end, step;
+};
+
+__device__ __forceinline__ SliceWalk slice_walk(int64_t nslices) {
+    const int xcd = blockIdx.x % NXCD;
+    const int64_t lb = blockIdx.x / NXCD, nlb = gridDim.x / NXCD;
+    const int64_t spx = (nslices + NXCD - 1) / NXCD;
+    const int64_t start = (int64_t)xcd * spx;
+    const int64_t end = min(start + spx, nslices);
+    return SliceWalk{start + lb * 4 + (threadIdx.x >> 6), end, nlb * 4};
+}
+
+template <int BS>
+__global__ void __launch_bounds__(256) k_spmv(int64_t nslices, int64_t nrows, const int64_t* __restrict__ slice_ptr,
+                                              const int32_t* __restrict__ cols, const double* __restrict__ vals,
+                                              const double* __restrict__ x, double* __restrict__ y) {
+    const int lane = threadIdx.x & 63;
+    SliceWalk wk = slice_walk(nslices);
+    for (int64_t s = wk.s; s < wk.end; s += wk.step) {
+        double o[BS];
+        sell_row<BS>(s, lane, slice_ptr, cols, vals, x, o);
+        const int64_t row = s * 64 + lane;
+        if (row < nrows) {
+#pragma unroll
+            for (int r = 0; r < BS; ++r) y[row * BS + r] = o[r];
+        }
+    }
+}
+
+// ---------------------------------------------------------------- PCG device state
+struct PcgState {
+    double rz;        // r.z of the current iterate (rs_old)
+    double pq;        // p.Ap of this iteration
+    double alpha, beta;
+    double rz_new;
+    double tol, eps;
+    int iter;         // completed iterations
+    int status;       // FEM_PCG_*
+    int halt;         // 1: solve ended, K1/K2 are no-ops
+    int xupd;         // 1: K2 ran this iteration -> K3 applies x += alpha p
+    int stop_iter;    // reported iteration of a guard stop (i+1 in the reference prints)
+    int max_iter;
+    int mode;
+    int pad_;
+    unsigned counter[4];
+};
+
+constexpr int PCG_BLOCK = 256;
+constexpr int MAX_PARTIALS = 4096;
+
+template <int BS>
+__global__ void __launch_bounds__(PCG_BLOCK) k_pcg_spmv_dot(int64_t nslices, int64_t nrows,
+                                                            const int64_t* __restrict__ slice_ptr,
+                                                            const int32_t* __restrict__ cols,
+                                                            const double* __restrict__ vals,
+                                                            const double* __restrict__ p, double* __restrict__ q,
+                                                            PcgState* __restrict__ st, double* __restrict__ partials) {
+    __shared__ double lds4[4];
+    __shared__ int last;
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->xupd = 0;
+    if (st->halt || st->iter >= st->max_iter) return;
+    const int lane = threadIdx.x & 63;
+    double dot = 0.0;
+    SliceWalk wk = slice_walk(nslices);
+    for (int64_t s = wk.s; s < wk.end; s += wk.step) {
+        double o[BS];
+        sell_row<BS>(s, lane, slice_ptr, cols, vals, p, o);
+        const int64_t row = s * 64 + lane;
+        if (row < nrows) {
+#pragma unroll
+            for (int r = 0; r < BS; ++r) {
+                q[row * BS + r] = o[r];
+                dot += p[row * BS + r] * o[r];
+            }
+        }
+    }
+    dot = block_sum256(dot, lds4);
+    if (publish_partial(dot, partials, &st->counter[0], &last)) {
+        const double pq = sum_partials(partials, gridDim.x, lds4);
+        if (threadIdx.x == 0) {
+            st->pq = pq;
+            if (st->mode == FEM_MODE_CG_STABLE) {
+                if (fabs(pq) < st->eps || pq < 0.0) {                 // `solver/solver.py:187`
+                    st->status = FEM_PCG_BREAKDOWN;
+                    st->halt = 1;
+                    st->stop_iter = st->iter + 1;
+                } else {
+                    const double a = st->rz / (pq + st->eps);          // `:194`
+                    st->alpha = a;
+                    if (isnan(a) || isinf(a)) {                        // `:196`
+                        st->status = FEM_PCG_ALPHA_NAN;
+                        st->halt = 1;
+                        st->stop_iter = st->iter + 1;
+                    }
+                }
+            } else {
+                st->alpha = st->rz / pq;                              // `:800` (no guards)
+            }
+        }
+    }
+}
+
+// K2: r <- r - alpha q (CG: masked), z = w r, partial r.z (CG: r.r since w is the 0/1 free mask)
+__global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update(int64_t n, double* __restrict__ r,
+                                                          const double* __restrict__ q, const double* __restrict__ w,
+                                                          PcgState* __restrict__ st, double* __restrict__ partials,
+                                                          double* __restrict__ hist, int64_t hist_len) {
+    __shared__ double lds4[4];
+    __shared__ int last;
+    if (st->halt || st->iter >= st->max_iter) return;
+    const double alpha = st->alpha;
+    const bool cg = st->mode == FEM_MODE_CG_STABLE;
+    double acc = 0.0;
+    const int64_t n2 = n >> 1;
+    const double2* q2 = reinterpret_cast<const double2*>(q);
+    const double2* w2 = reinterpret_cast<const double2*>(w);
+    double2* r2 = reinterpret_cast<double2*>(r);
+    for (int64_t i = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; i < n2; i += (int64_t)gridDim.x * PCG_BLOCK) {
+        double2 rv = r2[i], qv = q2[i], wv = w2[i];
+        rv.x = rv.x - alpha * qv.x;
+        rv.y = rv.y - alpha * qv.y;
+        if (cg) {
+            if (wv.x == 0.0) rv.x = 0.0;
+            if (wv.y == 0.0) rv.y = 0.0;
+        }
+        r2[i] = rv;
+        acc += rv.x * (wv.x * rv.x);
+        acc += rv.y * (wv.y * rv.y);
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+        int64_t i = n - 1;
+        double rv = r[i] - alpha * q[i];
+        if (cg && w[i] == 0.0) rv = 0.0;
+        r[i] = rv;
+        acc += rv * (w[i] * rv);
+    }
+    acc = block_sum256(acc, lds4);
+    if (publish_partial(acc, partials, &st->counter[1], &last)) {
+        const double rz_new = sum_partials(partials, gridDim.x, lds4);
+        if (threadIdx.x == 0) {
+            const int it = st->iter;
+            st->rz_new = rz_new;
+            st->xupd = 1;
+            st->iter = it + 1;
+            const double nrm = sqrt(rz_new);
+            if (hist && it < hist_len) hist[it] = nrm;
+            if (nrm < st->tol) {                                      // `:210` / `:805`
+                st->status = FEM_PCG_CONVERGED;
+                st->halt = 1;
+                st->stop_iter = it + 1;
+            } else {
+                const double b = cg ? rz_new / (st->rz + st->eps) : rz_new / st->rz;   // `:213` / `:808`
+                st->beta = b;
+                if (cg && (isnan(b) || isinf(b))) {                   // `:214`
+                    st->status = FEM_PCG_BETA_NAN;
+                    st->halt = 1;
+                    st->stop_iter = it + 1;
+                }
+                st->rz = rz_new;
+            }
+        }
+    }
+}
+
+// K3: x <- x + alpha p ; p <- w r + beta p (unless stopped in K2)
+__global__ void __launch_bounds__(PCG_BLOCK) k_pcg_pupdate(int64_t n, double* __restrict__ x, double* __restrict__ p,
+                                                           const double* __restrict__ r, const double* __restrict__ w,
+                                                           const PcgState* __restrict__ st) {
+    if (!st->xupd) return;
+    const double alpha = st->alpha, beta = st->beta;
+    const bool upd_p = !st->halt;
+    const int64_t n2 = n >> 1;
+    double2* x2 = reinterpret_cast<double2*>(x);
+    double2* p2 = reinterpret_cast<double2*>(p);
+    const double2* r2 = reinterpret_cast<const double2*>(r);
+    const double2* w2 = reinterpret_cast<const double2*>(w);
+    for (int64_t i = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; i < n2; i += (int64_t)gridDim.x * PCG_BLOCK) {
+        double2 pv = p2[i], xv = x2[i];
+        xv.x += alpha * pv.x;
+        xv.y += alpha * pv.y;
+        x2[i] = xv;
+        if (upd_p) {
+            double2 rv = r2[i], wv = w2[i];
+            pv.x = wv.x * rv.x + beta * pv.x;
+            pv.y = wv.y * rv.y + beta * pv.y;
+            p2[i] = pv;
+        }
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+        int64_t i = n - 1;
+        x[i] += alpha * p[i];
+        if (upd_p) p[i] = w[i] * r[i] + beta * p[i];
+    }
+}
+
+// start: (CG) x[fixed] = 0; r = b - q (q = A x computed before), (CG) r[fixed] = 0; p = z = w r; rz = r.z
+__global__ void __launch_bounds__(PCG_BLOCK) k_pcg_init(int64_t n, const double* __restrict__ b, double* __restrict__ r,
+                                                        const double* __restrict__ q, const double* __restrict__ w,
+                                                        double* __restrict__ p, PcgState* __restrict__ st,
+                                                        double* __restrict__ partials) {
+    __shared__ double lds4[4];
+    __shared__ int last;
+    const bool cg = st->mode == FEM_MODE_CG_STABLE;
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * PCG_BLOCK) {
+        double rv = b[i] - q[i];
+        if (cg && w[i] == 0.0) rv = 0.0;
+        r[i] = rv;
+        const double z = w[i] * rv;
+        p[i] = z;
+        acc += rv * z;
+    }
+    acc = block_sum256(acc, lds4);
+    if (publish_partial(acc, partials, &st->counter[2], &last)) {
+        const double rz = sum_partials(partials, gridDim.x, lds4);
+        if (threadIdx.x == 0) st->rz = rz;
+    }
+}
+
+__global__ void k_zero_fixed(int64_t n, double* __restrict__ x, const double* __restrict__ w) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        if (w[i] == 0.0) x[i] = 0.0;
+}
+
+}  // namespace fem
+
+using namespace fem;
+
+// ---------------------------------------------------------------- host-side context
+struct fem_pcg {
+    int64_t nrows, nslices, n;
+    int bs;
+    const int64_t* slice_ptr;
+    const int32_t* cols;
+    const double* vals;
+    const double* b;
+    double* x;
+    const double* w;
+    double* hist;
+    int64_t hist_len;
+    int mode;
+    double tol, eps;
+    hipStream_t stream;
+    // owned device memory
+    double* r;
+    double* p;
+    double* q;
+    double* partials;
+    PcgState* st;
+    PcgState* st_host;  // pinned
+    int grid_spmv, grid_vec;
+    hipGraphExec_t graph;
+    int graph_k;
+    int max_iter;       // device-side iteration cap armed by fem_pcg_start
+};
+
+static int launch_spmv_dot(fem_pcg* s) {
+    if (s->bs == 1)
+        hipLaunchKernelGGL(k_pcg_spmv_dot<1>, dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream, s->nslices, s->nrows,
+                           s->slice_ptr, s->cols, s->vals, s->p, s->q, s->st, s->partials);
+    else
+        hipLaunchKernelGGL(k_pcg_spmv_dot<3>, dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream, s->nslices, s->nrows,
+                           s->slice_ptr, s->cols, s->vals, s->p, s->q, s->st, s->partials);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+static int launch_update(fem_pcg* s) {
+    hipLaunchKernelGGL(k_pcg_update, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->r, s->q, s->w, s->st,
+                       s->partials + MAX_PARTIALS, s->hist, s->hist_len);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+static int launch_pupdate(fem_pcg* s) {
+    hipLaunchKernelGGL(k_pcg_pupdate, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->x, s->p, s->r, s->w,
+                       s->st);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+static int launch_iterations(fem_pcg* s, int k) {
+    for (int i = 0; i < k; ++i) {
+        int rc;
+        if ((rc = launch_spmv_dot(s))) return rc;
+        if ((rc = launch_update(s))) return rc;
+        if ((rc = launch_pupdate(s))) return rc;
+    }
+    return FEM_OK;
+}
+
+static int grid_multiple_of_xcd(int64_t blocks, int cap) {
+    int64_t g = blocks;
+    if (g > cap) g = cap;
+    g = ((g + NXCD - 1) / NXCD) * NXCD;
+    return (int)(g < NXCD ? NXCD : g);
+}
+
+extern "C" {
+
+int fem_spmv(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_t* cols, const double* vals, const double* x,
+             double* y, fem_stream_t stream) {
+    const int64_t ns = cdiv(nrows, 64);
+    if (ns == 0) return FEM_OK;
+    const int grid = grid_multiple_of_xcd(cdiv(ns, 4), 2048);
+    if (bs == 1)
+        hipLaunchKernelGGL(k_spmv<1>, dim3(grid), dim3(256), 0, S(stream), ns, nrows, slice_ptr, cols, vals, x, y);
+    else if (bs == 3)
+        hipLaunchKernelGGL(k_spmv<3>, dim3(grid), dim3(256), 0, S(stream), ns, nrows, slice_ptr, cols, vals, x, y);
+    else {
+        set_error("fem_spmv: block size %d unsupported", bs);
+        return FEM_EARG;
+    }
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_pcg_create(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_t* cols, const double* vals,
+                   const double* b, double* x, const double* w, int mode, double tol, double eps, double* hist,
+                   int64_t hist_len, fem_stream_t stream, fem_pcg** out) {
+    if (bs != 1 && bs != 3) {
+        set_error("fem_pcg_create: block size %d unsupported", bs);
+        return FEM_EARG;
+    }
+    if (mode != FEM_MODE_CG_STABLE && mode != FEM_MODE_PCG) {
+        set_error("fem_pcg_create: unknown mode %d", mode);
+        return FEM_EARG;
+    }
+    if (((uintptr_t)b | (uintptr_t)x | (uintptr_t)w) & 15) {
+        set_error("fem_pcg_create: vectors must be 16-byte aligned");
+        return FEM_EARG;
+    }
+    fem_pcg* s = new fem_pcg();
+    s->nrows = nrows;
+    s->bs = bs;
+    s->nslices = cdiv(nrows, 64);
+    s->n = nrows * bs;
+    s->slice_ptr = slice_ptr;
+    s->cols = cols;
+    s->vals = vals;
+    s->b = b;
+    s->x = x;
+    s->w = w;
+    s->hist = hist;
+    s->hist_len = hist ? hist_len : 0;
+    s->mode = mode;
+    s->tol = tol;
+    s->eps = eps;
+    s->stream = S(stream);
+    s->graph = nullptr;
+    s->graph_k = 0;
+    s->max_iter = 0x7fffffff;
+    s->grid_spmv = grid_multiple_of_xcd(cdiv(s->nslices, 4), 2048);
+    s->grid_vec = grid_multiple_of_xcd(cdiv(s->n / 2 + 1, PCG_BLOCK), 1024);
+    size_t vec = sizeof(double) * (size_t)(s->n + 2);
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = hipMalloc(&s->r, vec);
+    if (e == hipSuccess) e = hipMalloc(&s->p, vec);
+    if (e == hipSuccess) e = hipMalloc(&s->q, vec);
+    if (e == hipSuccess) e = hipMalloc(&s->partials, sizeof(double) * 3 * MAX_PARTIALS);
+    if (e == hipSuccess) e = hipMalloc(&s->st, sizeof(PcgState));
+    if (e == hipSuccess) e = hipHostMalloc(&s->st_host, sizeof(PcgState), hipHostMallocDefault);
+    if (e != hipSuccess) {
+        set_error("fem_pcg_create: allocation failed: %s", hipGetErrorString(e));
+        fem_pcg_destroy(s);
+        return FEM_EHIP;
+    }
+    *out = s;
+    return FEM_OK;
+}
+
+int fem_pcg_start(fem_pcg* s) {
+    PcgState h{};
+    h.tol = s->tol;
+    h.eps = s->eps;
+    h.mode = s->mode;
+    h.max_iter = s->max_iter;
+    *s->st_host = h;
+    FEM_HIP(hipMemcpyAsync(s->st, s->st_host, sizeof(PcgState), hipMemcpyHostToDevice, s->stream));
+    if (s->mode == FEM_MODE_CG_STABLE) {
+        hipLaunchKernelGGL(k_zero_fixed, dim3(stream_grid(s->n, 256)), dim3(256), 0, s->stream, s->n, s->x, s->w);
+        FEM_LAUNCHED();
+    }
+    int rc = fem_spmv(s->nrows, s->bs, s->slice_ptr, s->cols, s->vals, s->x, s->q, s->stream);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_pcg_init, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->b, s->r, s->q, s->w, s->p,
+                       s->st, s->partials + 2 * MAX_PARTIALS);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_pcg_iterate(fem_pcg* s, int k) {
+    if (k <= 0) return FEM_OK;
+    if (s->graph && s->graph_k > 0 && k % s->graph_k == 0) {
+        for (int i = 0; i < k / s->graph_k; ++i) FEM_HIP(hipGraphLaunch(s->graph, s->stream));
+        return FEM_OK;
+    }
+    return launch_iterations(s, k);
+}
+
+int fem_pcg_use_graph(fem_pcg* s, int k) {
+    if (s->graph) {
+        (void)hipGraphExecDestroy(s->graph);
+        s->graph = nullptr;
+        s->graph_k = 0;
+    }
+    if (k <= 0) return FEM_OK;
+    hipGraph_t g;
+    FEM_HIP(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
+    int rc = launch_iterations(s, k);
+    hipError_t e = hipStreamEndCapture(s->stream, &g);
+    if (rc) return rc;
+    if (e != hipSuccess) {
+        set_error("fem_pcg_use_graph: capture failed: %s", hipGetErrorString(e));
+        return FEM_EHIP;
+    }
+    e = hipGraphInstantiate(&s->graph, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (e != hipSuccess) {
+        set_error("fem_pcg_use_graph: instantiate failed: %s", hipGetErrorString(e));
+        s->graph = nullptr;
+        return FEM_EHIP;
+    }
+    s->graph_k = k;
+    return FEM_OK;
+}
+
+int fem_pcg_poll(fem_pcg* s, int* iters, int* status, double* rz) {
+    FEM_HIP(hipMemcpyAsync(s->st_host, s->st, sizeof(PcgState), hipMemcpyDeviceToHost, s->stream));
+    FEM_HIP(hipStreamSynchronize(s->stream));
+    const PcgState& h = *s->st_host;
+    int stt = h.status;
+    if (stt == FEM_PCG_RUNNING && h.iter >= h.max_iter) stt = FEM_PCG_MAXITER;
+    if (iters) *iters = (stt == FEM_PCG_BREAKDOWN || stt == FEM_PCG_ALPHA_NAN) ? h.stop_iter : h.iter;
+    if (status) *status = stt;
+    if (rz) *rz = (h.iter > 0) ? h.rz_new : h.rz;
+    return FEM_OK;
+}
+
+int fem_pcg_scalars(fem_pcg* s, double* out6) {
+    FEM_HIP(hipMemcpyAsync(s->st_host, s->st, sizeof(PcgState), hipMemcpyDeviceToHost, s->stream));
+    FEM_HIP(hipStreamSynchronize(s->stream));
+    const PcgState& h = *s->st_host;
+    out6[0] = h.rz;
+    out6[1] = h.pq;
+    out6[2] = h.alpha;
+    out6[3] = h.beta;
+    out6[4] = h.rz_new;
+    out6[5] = (double)h.iter;
+    return FEM_OK;
+}
+
+int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, double* rz) {
+    s->max_iter = max_iter;
+    int rc = fem_pcg_start(s);
+    s->max_iter = 0x7fffffff;
+    if (rc) return rc;
+    if (chunk <= 0) chunk = 32;
+    int done = 0;
+    int it = 0, stt = FEM_PCG_RUNNING;
+    while (done < max_iter) {
+        int k = chunk < max_iter - done ? chunk : max_iter - done;
+        if ((rc = fem_pcg_iterate(s, k))) return rc;
+        done += k;
+        if ((rc = fem_pcg_poll(s, &it, &stt, rz))) return rc;
+        if (stt != FEM_PCG_RUNNING) break;
+        if (chunk < 256) chunk *= 2;   // poll less often once the solve is clearly long
+    }
+    if ((rc = fem_pcg_poll(s, &it, &stt, rz))) return rc;
+    if (iters) *iters = it;
+    if (status) *status = stt;
+    return FEM_OK;
+}
+
+int fem_pcg_profile(fem_pcg* s, int k, int every, double* ms, int* n) {
+    // k iterations enqueued on the solver stream; iterations i % every == 0 are bracketed by hip events
+    // around each of the three kernels (on the stream the kernels run on), the others launch bare.
+    if (every < 1) every = 1;
+    double acc[3] = {0, 0, 0};
+    int rc = FEM_OK;
+    const int ns = (k + every - 1) / every;
+    std::vector<hipEvent_t> evs((size_t)ns * 4);
+    for (auto& e : evs) FEM_HIP(hipEventCreate(&e));
+    int si = 0;
+    for (int i = 0; i < k && !rc; ++i) {
+        if (i % every) {
+            rc = launch_iterations(s, 1);
+            continue;
+        }
+        (void)hipEventRecord(evs[4 * si + 0], s->stream);
+        rc = launch_spmv_dot(s);
+        (void)hipEventRecord(evs[4 * si + 1], s->stream);
+        if (!rc) rc = launch_update(s);
+        (void)hipEventRecord(evs[4 * si + 2], s->stream);
+        if (!rc) rc = launch_pupdate(s);
+        (void)hipEventRecord(evs[4 * si + 3], s->stream);
+        ++si;
+    }
+    FEM_HIP(hipStreamSynchronize(s->stream));
+    for (int i = 0; i < si; ++i) {
+        float t;
+        for (int j = 0; j < 3; ++j) {
+            (void)hipEventElapsedTime(&t, evs[4 * i + j], evs[4 * i + j + 1]);
+            acc[j] += t;
+        }
+    }
+    for (auto& e : evs) (void)hipEventDestroy(e);
+    for (int j = 0; j < 3; ++j) {
+        if (ms) ms[j] = acc[j];
+        if (n) n[j] = si;
+    }
+    return rc;
+}
+
+void fem_pcg_destroy(fem_pcg* s) {
+    if (!s) return;
+    if (s->graph) (void)hipGraphExecDestroy(s->graph);
+    if (s->r) (void)hipFree(s->r);
+    if (s->p) (void)hipFree(s->p);
+    if (s->q) (void)hipFree(s->q);
+    if (s->partials) (void)hipFree(s->partials);
+    if (s->st) (void)hipFree(s->st);
+    if (s->st_host) (void)hipHostFree(s->st_host);
+    delete s;
+}
+
+}  // extern "C"

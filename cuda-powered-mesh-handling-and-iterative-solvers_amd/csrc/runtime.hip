@@ -1,0 +1,129 @@
+// Error plumbing, version, and device-wide exclusive scans (pattern build / SELL slice offsets).
+#include <stdarg.h>
+
+#include "common.hpp"
+
+namespace fem {
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+// ---------------------------------------------------------------- 3-phase exclusive scan
+// phase 1: per-tile sums; phase 2: one block scans the tile sums; phase 3: tile-local scan + offset.
+constexpr int SCAN_BLOCK = 256;
+constexpr int SCAN_ITEMS = 8;
+constexpr int SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
+
+template <typename T>
+__device__ __forceinline__ T block_exclusive_scan(T v, T* lds, T* total) {
+    // Hillis-Steele over 256 threads in LDS (setup-path kernel; simplicity over speed)
+    const int t = threadIdx.x;
+    lds[t] = v;
+    __syncthreads();
+    for (int o = 1; o < SCAN_BLOCK; o <<= 1) {
+        T add = (t >= o) ? lds[t - o] : T(0);
+        __syncthreads();
+        lds[t] += add;
+        __syncthreads();
+    }
+    T incl = lds[t];
+    *total = lds[SCAN_BLOCK - 1];
+    __syncthreads();
+    return incl - v;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(SCAN_BLOCK) k_tile_sums(const T* __restrict__ in, int64_t n, T* __restrict__ sums) {
+    __shared__ T lds[SCAN_BLOCK];
+    int64_t base = (int64_t)blockIdx.x * SCAN_TILE;
+    T s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        int64_t i = base + (int64_t)k * SCAN_BLOCK + threadIdx.x;
+        if (i < n) s += in[i];
+    }
+    T tot;
+    block_exclusive_scan<T>(s, lds, &tot);
+    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(SCAN_BLOCK) k_scan_sums(T* __restrict__ sums, int64_t ntiles) {
+    __shared__ T lds[SCAN_BLOCK];
+    T carry = 0;
+    for (int64_t base = 0; base < ntiles; base += SCAN_BLOCK) {
+        int64_t i = base + threadIdx.x;
+        T v = (i < ntiles) ? sums[i] : T(0);
+        T tot;
+        T ex = block_exclusive_scan<T>(v, lds, &tot);
+        if (i < ntiles) sums[i] = ex + carry;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) sums[ntiles] = carry;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(SCAN_BLOCK) k_tile_scan(const T* __restrict__ in, int64_t n, const T* __restrict__ sums,
+                                                          T* __restrict__ out, int64_t ntiles) {
+    __shared__ T lds[SCAN_BLOCK];
+    int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ITEMS;
+    T v[SCAN_ITEMS];
+    T s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        int64_t i = base + k;
+        v[k] = (i < n) ? in[i] : T(0);
+        s += v[k];
+    }
+    T tot;
+    T ex = block_exclusive_scan<T>(s, lds, &tot) + sums[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; ++k) {
+        int64_t i = base + k;
+        if (i < n) out[i] = ex;
+        ex += v[k];
+    }
+    if (blockIdx.x == ntiles - 1 && threadIdx.x == 0) out[n] = sums[ntiles];
+}
+
+template <typename T>
+int scan_impl(const T* in, int64_t n, T* out, T* work, hipStream_t st) {
+    if (n <= 0) {
+        FEM_HIP(hipMemsetAsync(out, 0, sizeof(T), st));
+        return FEM_OK;
+    }
+    int64_t ntiles = cdiv(n, SCAN_TILE);
+    hipLaunchKernelGGL(k_tile_sums<T>, dim3((unsigned)ntiles), dim3(SCAN_BLOCK), 0, st, in, n, work);
+    FEM_LAUNCHED();
+    hipLaunchKernelGGL(k_scan_sums<T>, dim3(1), dim3(SCAN_BLOCK), 0, st, work, ntiles);
+    FEM_LAUNCHED();
+    hipLaunchKernelGGL(k_tile_scan<T>, dim3((unsigned)ntiles), dim3(SCAN_BLOCK), 0, st, in, n, work, out, ntiles);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+}  // namespace fem
+
+using namespace fem;
+
+extern "C" {
+
+const char* fem_last_error(void) { return g_err; }
+int fem_version(void) { return 100; }
+
+int64_t fem_scan_work_len(int64_t n) { return cdiv(n > 0 ? n : 1, SCAN_TILE) + 1; }
+
+int fem_scan_i32(const int32_t* in, int64_t n, int32_t* out, int32_t* work, fem_stream_t stream) {
+    return scan_impl<int32_t>(in, n, out, work, S(stream));
+}
+
+int fem_scan_i64(const int64_t* in, int64_t n, int64_t* out, int64_t* work, fem_stream_t stream) {
+    return scan_impl<int64_t>(in, n, out, work, S(stream));
+}
+
+}  // extern "C"

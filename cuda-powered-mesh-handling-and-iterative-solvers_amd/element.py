@@ -1,0 +1,429 @@
+"""Reference-compatible element API (`solver/element.py` of sml2004/CUDA-powered-mesh-handling-and-Iterative-
+solvers @ 2025-04-18), executed by the fem355 HIP kernels.
+
+Same function names, arguments, defaults (device="cuda:0") and return shapes as the reference, so its
+notebook call sites work unchanged. Differences, all deliberate:
+  * arithmetic is always fp64 on the MI355X; `dtype` only selects the dtype of the returned tensor;
+  * a `device="cpu"` request is computed on the current HIP device and the result is returned on the CPU
+    (there is no CPU code path in this package: see `_capi.lib()`);
+  * integration-point tables are evaluated on the host exactly as the reference evaluates them (including its
+    quirks: c3d10 weights summing to 0.45, the float32-rounded line points of c3d6), then handed to the kernels.
+Out of scope: shells, stress recovery, topology, visualisation, c3d20/c3d15.
+"""
+from __future__ import annotations
+
+import math
+import warnings
+from collections import OrderedDict
+
+import torch
+
+try:  # package import (fem355.element) or the reference's flat import (`from element import *`)
+    from . import _capi as C
+    from . import system as _sys
+except ImportError:  # pragma: no cover - exercised by the notebook-style loader test
+    import _capi as C  # type: ignore
+    import system as _sys  # type: ignore
+
+F64 = torch.float64
+LONG = torch.long
+
+__all__ = [
+    "human_readable_number", "vtk_loader_to_torch", "compute_elasticity_matrix", "integral_points",
+    "compute_Jacobian", "compute_shape_gradients", "compute_B_matrix", "compute_K_matrix", "compute_nodal_forces",
+    "compute_tetrahedral_volumes", "compute_c3d4_B_matrix", "compute_c3d4_K_matrix", "compute_L_matrix",
+    "compute_c3d4_M_matrix", "compute_c3d4_poisson_K_matrix",
+    "c3d8_integration_points", "compute_c3d8_Jacobian", "compute_c3d8_shape_gradients", "compute_c3d8_B_matrix",
+    "compute_c3d8_K_matrix",
+    "c3d6_integration_points", "compute_c3d6_Jacobian", "compute_c3d6_shape_gradients", "compute_c3d6_B_matrix",
+    "compute_c3d6_K_matrix", "compute_wedge_volumes",
+    "c3d10_integration_points", "compute_c3d10_Jacobian", "compute_c3d10_shape_gradients", "compute_c3d10_B_matrix",
+    "compute_c3d10_K_matrix",
+]
+
+
+# ============================================================================ utilities
+def human_readable_number(num):
+    """`solver/element.py:23-37` (used by the CG progress print)."""
+    for lim, suf in ((1e18, "Quint"), (1e15, "Quad"), (1e12, "T"), (1e9, "B"), (1e6, "M"), (1e3, "K")):
+        if abs(num) >= lim:
+            return f"{num / lim:.1f}{suf}"
+    return f"{num:.1f}"
+
+
+def vtk_loader_to_torch(file_path, element_type="c3d4", device="cuda:0", dtype=torch.float32):
+    """`solver/element.py:39-90` reads VTK through pyvista, which this image does not ship; the VTK reader is
+    a ranked next step, not part of this round's hot path."""
+    raise NotImplementedError("vtk_loader_to_torch: pyvista-free VTK reader not implemented yet (SURVEY §8(f)-4)")
+
+
+def _dev(device):
+    return C.compute_device(device)
+
+
+def _prep(coords, elements, device):
+    dev = _dev(device)
+    coords = coords.to(device=dev, dtype=F64).contiguous()
+    elements = elements.to(device=dev, dtype=LONG).contiguous()
+    return dev, coords, elements
+
+
+def _out(t, device, dtype):
+    return t.to(device=torch.device(device), dtype=dtype)
+
+
+def compute_elasticity_matrix(E, nu, device="cuda:0", dtype=torch.float32):
+    """Isotropic 6x6 D, Voigt (xx,yy,zz,xy,yz,xz), engineering shear. `solver/element.py:282-306`."""
+    coef = E / ((1 + nu) * (1 - 2 * nu))
+    g = (1 - 2 * nu) / 2
+    rows = [[1 - nu, nu, nu, 0, 0, 0], [nu, 1 - nu, nu, 0, 0, 0], [nu, nu, 1 - nu, 0, 0, 0],
+            [0, 0, 0, g, 0, 0], [0, 0, 0, 0, g, 0], [0, 0, 0, 0, 0, g]]
+    return coef * torch.tensor(rows, device=device, dtype=dtype)
+
+
+# ============================================================================ c3d4
+def _bad_scalar(dev, M):
+    return torch.full((1,), M, dtype=torch.int64, device=dev)
+
+
+def _raise_if_singular(bad, M):
+    if int(bad.item()) < M:
+        raise ValueError("Singular matrix encountered while computing B matrix.")
+
+
+def _tet4_geom(coords, elements, device, want_vol=False, want_B=False, check=True):
+    lib = C.lib()
+    dev, coords, elements = _prep(coords, elements, device)
+    M = elements.shape[0]
+    vol = torch.empty(M, dtype=F64, device=dev) if want_vol else None
+    B = torch.empty((M, 6, 12), dtype=F64, device=dev) if want_B else None
+    bad = _bad_scalar(dev, M) if check else None
+    C.check(lib.fem_tet4_geom(C.ptr(coords), C.ptr(elements), M, C.ptr(vol), None, C.ptr(B), C.ptr(bad),
+                              C.stream(dev)), "fem_tet4_geom")
+    if check:
+        _raise_if_singular(bad, M)
+    return vol, B
+
+
+def compute_tetrahedral_volumes(coords, elements, device="cuda:0", dtype=torch.float32):
+    """|det[p1-p0, p2-p0, p3-p0]|/6 -> [M]. `solver/element.py:514-541`."""
+    vol, _ = _tet4_geom(coords, elements, device, want_vol=True, check=False)
+    return _out(vol, device, dtype)
+
+
+def compute_c3d4_B_matrix(coords, elements, device="cuda:0", dtype=torch.float32):
+    """Strain-displacement matrix [M,6,12]; ValueError on |det| < 1e-12. `solver/element.py:835-881`."""
+    _, B = _tet4_geom(coords, elements, device, want_B=True)
+    return _out(B, device, dtype)
+
+
+def _tet4_ke(coords, elements, a, b, kind, device, dtype):
+    lib = C.lib()
+    dev, coords, elements = _prep(coords, elements, device)
+    M = elements.shape[0]
+    d = 4 if kind == C.KIND_POISSON else 12
+    K = torch.empty((M, d, d), dtype=F64, device=dev)
+    bad = _bad_scalar(dev, M)
+    C.check(lib.fem_tet4_ke(C.ptr(coords), C.ptr(elements), M, float(a), float(b), kind, C.ptr(K), C.ptr(bad),
+                            C.stream(dev)), "fem_tet4_ke")
+    if kind != C.KIND_MASS:
+        _raise_if_singular(bad, M)
+    return _out(K, device, dtype)
+
+
+def compute_c3d4_K_matrix(coords, elements, E, nu, device="cuda:0", dtype=torch.float32):
+    """K_e = B^T D B V -> [M,12,12]. `solver/element.py:883-903`."""
+    return _tet4_ke(coords, elements, E, nu, C.KIND_ELASTIC, device, dtype)
+
+
+def compute_L_matrix(coords, elements, E, nu, device="cuda:0", dtype=torch.float32):
+    """Name used by `solver_example.ipynb:96` for the c3d4 stiffness (stale API of the reference)."""
+    return compute_c3d4_K_matrix(coords, elements, E, nu, device=device, dtype=dtype)
+
+
+def compute_c3d4_M_matrix(coords, elements, rho, device="cuda:0", dtype=torch.float32):
+    """Consistent P1 mass [M,12,12] = rho V (1 + delta_ab)/20 per component. Called at
+    `solver_example.ipynb:221` but defined nowhere in the reference: parity unpinned."""
+    return _tet4_ke(coords, elements, rho, 0.0, C.KIND_MASS, device, dtype)
+
+
+def compute_c3d4_poisson_K_matrix(coords, elements, kappa=1.0, device="cuda:0", dtype=torch.float32):
+    """Scalar P1 Laplacian kappa V G G^T -> [M,4,4] (no reference function: derived from the reference's
+    c3d4 gradients and volumes). Used with dofs-per-node 1 everywhere below."""
+    return _tet4_ke(coords, elements, kappa, 0.0, C.KIND_POISSON, device, dtype)
+
+
+# ============================================================================ isoparametric solids
+def c3d8_integration_points(device="cuda:0", dtype=torch.float32):
+    """2x2x2 Gauss, w=1, xi-major order. `solver/element.py:1583-1599`."""
+    a = 1.0 / torch.sqrt(torch.tensor(3.0, dtype=dtype, device=device))
+    s = [(-1, -1, -1), (-1, -1, 1), (-1, 1, -1), (-1, 1, 1), (1, -1, -1), (1, -1, 1), (1, 1, -1), (1, 1, 1)]
+    pts = torch.stack([torch.stack([u * a, v * a, w * a]) for (u, v, w) in s])
+    return pts, torch.ones(8, dtype=dtype, device=device)
+
+
+def c3d6_integration_points(device="cuda:0", dtype=torch.float32):
+    """3 triangle points x 2 line points, triangle weight 1/3 (weights sum to 2, quirk Q3); the line points come
+    from a float32 sqrt(3) exactly as in `solver/element.py:2448-2480`."""
+    tri = [(1 / 6, 1 / 6), (2 / 3, 1 / 6), (1 / 6, 2 / 3)]
+    t = float(1.0 / torch.sqrt(torch.tensor(3.0)))
+    pts = [[r, s, z] for (r, s) in tri for z in (-t, t)]
+    return (torch.tensor(pts, dtype=dtype, device=device),
+            torch.tensor([1 / 3] * 6, dtype=dtype, device=device))
+
+
+def c3d10_integration_points(device="cuda:0", dtype=torch.float32):
+    """The reference's 11-point tet rule (weights sum to 0.45, quirk Q2). `solver/element.py:995-1024`."""
+    pts = [[0.25, 0.25, 0.25], [0.1, 0.1, 0.1], [0.1, 0.1, 0.7], [0.1, 0.7, 0.1], [0.7, 0.1, 0.1],
+           [0.1, 0.4, 0.4], [0.4, 0.1, 0.4], [0.4, 0.4, 0.1], [0.3, 0.3, 0.3], [0.2, 0.2, 0.6], [0.2, 0.6, 0.2]]
+    w = [0.1, 0.05, 0.05, 0.05, 0.05, 0.03, 0.03, 0.03, 0.02, 0.02, 0.02]
+    return torch.tensor(pts, dtype=dtype).to(device), torch.tensor(w, dtype=dtype).to(device)
+
+
+def _dn_c3d8(xi, eta, zeta):
+    # natural derivatives, `solver/element.py:1617-1626`
+    out = []
+    for (a, b, c) in ((-1, -1, -1), (1, -1, -1), (1, 1, -1), (-1, 1, -1), (-1, -1, 1), (1, -1, 1), (1, 1, 1), (-1, 1, 1)):
+        out.append([0.125 * a * (1 + b * eta) * (1 + c * zeta), 0.125 * b * (1 + a * xi) * (1 + c * zeta),
+                    0.125 * c * (1 + a * xi) * (1 + b * eta)])
+    return out
+
+
+def _dn_c3d6(r, s, t):
+    # `solver/element.py:2498-2505`
+    return [[-0.5 * (1 - t), -0.5 * (1 - t), -0.5 * (1 - r - s)], [0.5 * (1 - t), 0.0, -0.5 * r],
+            [0.0, 0.5 * (1 - t), -0.5 * s], [-0.5 * (1 + t), -0.5 * (1 + t), 0.5 * (1 - r - s)],
+            [0.5 * (1 + t), 0.0, 0.5 * r], [0.0, 0.5 * (1 + t), 0.5 * s]]
+
+
+def _dn_c3d10(xi, eta, zeta):
+    # `solver/element.py:1043-1054`
+    L = 1 - xi - eta - zeta
+    return [[4 * xi - 1, 0, 0], [0, 4 * eta - 1, 0], [0, 0, 4 * zeta - 1], [-4 * L + 1, -4 * L + 1, -4 * L + 1],
+            [4 * eta, 4 * xi, 0], [0, 4 * zeta, 4 * eta], [4 * zeta, 0, 4 * xi],
+            [4 * (1 - 2 * xi - eta - zeta), -4 * xi, -4 * xi], [-4 * eta, 4 * (1 - xi - 2 * eta - zeta), -4 * eta],
+            [-4 * zeta, -4 * zeta, 4 * (1 - xi - eta - 2 * zeta)]]
+
+
+_ISO = {"c3d8": (8, _dn_c3d8, c3d8_integration_points), "c3d6": (6, _dn_c3d6, c3d6_integration_points),
+        "c3d10": (10, _dn_c3d10, c3d10_integration_points)}
+
+
+def _points_weights(etype, integral_point):
+    """(points [n,3] fp64 host, weights [n]) — default rule, or the caller's [n,4] (xi, eta, zeta, w) table."""
+    if integral_point is None:
+        p, w = _ISO[etype][2](device="cpu", dtype=F64)
+    else:
+        ip = integral_point.detach().to("cpu", F64)
+        p, w = ip[:, :3], ip[:, -1]
+    return p, w
+
+
+def _dn_table(etype, points, dev):
+    fn = _ISO[etype][1]
+    rows = [fn(*[float(v) for v in points[q]]) for q in range(points.shape[0])]
+    return torch.tensor(rows, dtype=F64).to(dev).contiguous()   # [n_ip, npe, 3]
+
+
+def _iso_ke(coords, elements, etype, E, nu, points, weights, mode, device, dtype):
+    lib = C.lib()
+    dev, coords, elements = _prep(coords, elements, device)
+    npe = _ISO[etype][0]
+    if elements.shape[1] != npe:
+        raise ValueError(f"{etype} expects {npe} nodes per element, got {elements.shape[1]}")
+    M = elements.shape[0]
+    dN = _dn_table(etype, points, dev)
+    w = weights.to(dev, F64).contiguous()
+    n_ip = dN.shape[0]
+    d = 3 * npe
+    shape = (n_ip, M, d, d) if mode == C.ISO_STACK else (M, d, d)
+    K = torch.empty(shape, dtype=F64, device=dev)
+    C.check(lib.fem_iso_ke(C.ptr(coords), C.ptr(elements), M, npe, float(E), float(nu), C.ptr(dN), C.ptr(w), n_ip,
+                           mode, C.ptr(K), C.stream(dev)), "fem_iso_ke")
+    return _out(K, device, dtype)
+
+
+def _iso_geom(coords, elements, etype, integral_point, what, device, dtype):
+    lib = C.lib()
+    dev, coords, elements = _prep(coords, elements, device)
+    npe = _ISO[etype][0]
+    M = elements.shape[0]
+    ip = torch.as_tensor(integral_point).detach().to("cpu", F64).reshape(-1)[:3]
+    dN = _dn_table(etype, ip.view(1, 3), dev)[0].contiguous()
+    J = torch.empty((M, 3, 3), dtype=F64, device=dev) if what == "J" else None
+    G = torch.empty((M, npe, 3), dtype=F64, device=dev) if what == "G" else None
+    B = torch.empty((M, 6, 3 * npe), dtype=F64, device=dev) if what == "B" else None
+    C.check(lib.fem_iso_geom(C.ptr(coords), C.ptr(elements), M, npe, C.ptr(dN), C.ptr(J), C.ptr(G), C.ptr(B),
+                             C.stream(dev)), "fem_iso_geom")
+    return _out({"J": J, "G": G, "B": B}[what], device, dtype)
+
+
+def compute_c3d8_Jacobian(coords, elements, integral_point, device="cuda:0", dtype=torch.float32):
+    """`solver/element.py:1601-1632` -> [M,3,3]."""
+    return _iso_geom(coords, elements, "c3d8", integral_point, "J", device, dtype)
+
+
+def compute_c3d8_shape_gradients(coords, elements, integral_point, device="cuda:0", dtype=torch.float32):
+    """`solver/element.py:1634-1664` -> [M,8,3]."""
+    return _iso_geom(coords, elements, "c3d8", integral_point, "G", device, dtype)
+
+
+def compute_c3d8_B_matrix(coords, elements, integral_point, device="cuda:0", dtype=torch.float32):
+    """`solver/element.py:1666-1694` -> [M,6,24]."""
+    return _iso_geom(coords, elements, "c3d8", integral_point, "B", device, dtype)
+
+
+def compute_c3d8_K_matrix(coords, elements, E, nu, integral_point=None, single=True, device="cuda:0",
+                          dtype=torch.float32):
+    """sum_ip w detJ B^T D B -> [M,24,24]; single=False -> [n_ip,M,24,24] without weights (Q6).
+    `solver/element.py:1754-1803`."""
+    p, w = _points_weights("c3d8", integral_point)
+    return _iso_ke(coords, elements, "c3d8", E, nu, p, w, C.ISO_SUM if single else C.ISO_STACK, device, dtype)
+
+
+def compute_c3d6_Jacobian(coords, elements, integral_point, device="cuda:0", dtype=torch.float32):
+    """`solver/element.py:2482-2509`."""
+    return _iso_geom(coords, elements, "c3d6", integral_point, "J", device, dtype)
+
+
+def compute_c3d6_shape_gradients(coords, elements, integral_point, device="cuda:0", dtype=torch.float32):
+    """`solver/element.py:2511-2539`."""
+    return _iso_geom(coords, elements, "c3d6", integral_point, "G", device, dtype)
+
+
+def compute_c3d6_B_matrix(coords, elements, integral_point, device="cuda:0", dtype=torch.float32):
+    """`solver/element.py:2541-2568`."""
+    return _iso_geom(coords, elements, "c3d6", integral_point, "B", device, dtype)
+
+
+def compute_wedge_volumes(coords, elements, device="cuda:0", dtype=torch.float32):
+    """Sum of the 3 sub-tet |volumes| (p0,p1,p2,p3), (p1,p2,p4,p3), (p2,p4,p5,p3). `solver/element.py:2198-2232`
+    (the sub-tet volumes come from the c3d4 geometry kernel)."""
+    el = torch.as_tensor(elements).to(LONG)
+    subs = torch.stack([el[:, [0, 1, 2, 3]], el[:, [1, 2, 4, 3]], el[:, [2, 4, 5, 3]]], 1).reshape(-1, 4)
+    v = compute_tetrahedral_volumes(coords, subs, device=device, dtype=F64).view(-1, 3)
+    return _out(v[:, 0] + v[:, 1] + v[:, 2], device, dtype)
+
+
+def compute_c3d6_K_matrix(coords, elements, E, nu, integral_point=None, single=True, device="cuda:0",
+                          dtype=torch.float32):
+    """single=True: B at (1/3,1/3,0) times the wedge volume; single=False: sum_ip w detJ B^T D B with the
+    reference's 6-point rule (weights sum to 2, Q3). Always [M,18,18]. `solver/element.py:2631-2676`."""
+    if single:
+        p = torch.tensor([[1 / 3, 1 / 3, 0.0]], dtype=F64)
+        return _iso_ke(coords, elements, "c3d6", E, nu, p, torch.ones(1, dtype=F64), C.ISO_VOLUME, device, dtype)
+    p, w = _points_weights("c3d6", integral_point)
+    return _iso_ke(coords, elements, "c3d6", E, nu, p, w, C.ISO_SUM, device, dtype)
+
+
+def compute_c3d10_Jacobian(coords, elements, integral_point, device="cuda:0", dtype=torch.float32):
+    """`solver/element.py:1026-1060`."""
+    return _iso_geom(coords, elements, "c3d10", integral_point, "J", device, dtype)
+
+
+def compute_c3d10_shape_gradients(coords, elements, integral_point, device="cuda:0", dtype=torch.float32):
+    """`solver/element.py:1062-1095`."""
+    return _iso_geom(coords, elements, "c3d10", integral_point, "G", device, dtype)
+
+
+def compute_c3d10_B_matrix(coords, elements, integral_point, device="cuda:0", dtype=torch.float32):
+    """`solver/element.py:1097-1125`."""
+    return _iso_geom(coords, elements, "c3d10", integral_point, "B", device, dtype)
+
+
+def compute_c3d10_K_matrix(coords, elements, E, nu, integral_point=None, single=True, device="cuda:0",
+                           dtype=torch.float32):
+    """sum_ip w signed-detJ B^T D B (11-point rule, Q2) -> [M,30,30]; single=False -> [n_ip,M,30,30] unweighted.
+    `solver/element.py:1191-1239`."""
+    p, w = _points_weights("c3d10", integral_point)
+    return _iso_ke(coords, elements, "c3d10", E, nu, p, w, C.ISO_SUM if single else C.ISO_STACK, device, dtype)
+
+
+# ============================================================================ dispatch (`solver/element.py:371-427`)
+def _unsupported(element_type):
+    raise ValueError(f"Unsupported element type: {element_type}")
+
+
+def integral_points(element_type, device="cuda:0"):
+    et = element_type.lower()
+    if et in ("c3d8", "c3d10", "c3d6"):
+        return _ISO[et][2](device=device)
+    _unsupported(et)
+
+
+def compute_Jacobian(coords, elements, element_type, integral_point=None, device="cuda:0"):
+    et = element_type.lower()
+    et = "c3d8" if et == "c3d8i" else et
+    if et in _ISO:
+        return _iso_geom(coords, elements, et, integral_point, "J", device, torch.float32)
+    _unsupported(et)
+
+
+def compute_shape_gradients(coords, elements, element_type, integral_point=None, device="cuda:0"):
+    et = element_type.lower()
+    if et in _ISO:
+        return _iso_geom(coords, elements, et, integral_point, "G", device, torch.float32)
+    _unsupported(et)
+
+
+def compute_B_matrix(coords, elements, integral_point, element_type, device="cuda:0", dtype=torch.float32):
+    et = element_type.lower()
+    if et == "c3d4":
+        return compute_c3d4_B_matrix(coords, elements, device, dtype)
+    if et in _ISO:
+        return _iso_geom(coords, elements, et, integral_point, "B", device, dtype)
+    _unsupported(et)
+
+
+def compute_K_matrix(coords, elements, element_type, E, nu, integral_point=None, single=True, device="cuda:0",
+                     dtype=torch.float32):
+    """String dispatch of `solver/element.py:419-427` (c3d20/c3d15 are broken in the reference: out of scope)."""
+    et = element_type.lower()
+    if et == "c3d4":
+        return compute_c3d4_K_matrix(coords, elements, E, nu, device, dtype)
+    if et == "c3d8":
+        return compute_c3d8_K_matrix(coords, elements, E, nu, integral_point, single, device, dtype)
+    if et == "c3d10":
+        return compute_c3d10_K_matrix(coords, elements, E, nu, integral_point, single, device, dtype)
+    if et == "c3d6":
+        return compute_c3d6_K_matrix(coords, elements, E, nu, integral_point, single, device, dtype)
+    _unsupported(et)
+
+
+# ============================================================================ element-by-element operator
+_INC_CACHE: "OrderedDict[tuple, tuple]" = OrderedDict()
+
+
+def _key(t: torch.Tensor, *extra):
+    return (t.data_ptr(), t._version, tuple(t.shape), str(t.device)) + extra
+
+
+def cached_incidence(elements: torch.Tensor, n_nodes: int):
+    k = _key(elements, n_nodes)
+    hit = _INC_CACHE.get(k)
+    if hit is not None:
+        _INC_CACHE.move_to_end(k)
+        return hit[1]
+    inc = _sys.incidence(elements, n_nodes)
+    _INC_CACHE[k] = (elements, inc)   # keep `elements` alive so its pointer is not reused while cached
+    while len(_INC_CACHE) > 8:
+        _INC_CACHE.popitem(last=False)
+    return inc
+
+
+def compute_nodal_forces(K, elements, displacement, device="cuda:0", dtype=torch.float32):
+    """y = sum_e P_e^T K_e P_e u without assembly -> [N, dpn]. `solver/element.py:429-464`.
+    dofs per node = K.shape[-1] / nodes per element (3 in the reference; 1 for the scalar Poisson K)."""
+    lib = C.lib()
+    dev = _dev(device)
+    elements = elements.to(device=dev, dtype=LONG).contiguous()
+    K = K.to(device=dev, dtype=F64).contiguous()
+    u = displacement.to(device=dev, dtype=F64).contiguous()
+    M, npe = elements.shape
+    dpn = K.shape[-1] // npe
+    N = u.shape[0]
+    inc_ptr, inc = cached_incidence(elements, N)
+    y = torch.empty((N, dpn), dtype=F64, device=dev)
+    C.check(lib.fem_ebe_apply(C.ptr(K), C.ptr(elements), npe, dpn, C.ptr(inc_ptr), C.ptr(inc), N, C.ptr(u), C.ptr(y),
+                              C.stream(dev)), "fem_ebe_apply")
+    return _out(y, device, dtype)

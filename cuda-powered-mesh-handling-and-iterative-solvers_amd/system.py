@@ -1,0 +1,288 @@
+"""Device-resident global operator: pattern build, assembly into SELL-64, SpMV and the (P)CG driver.
+
+This is the host runtime around the HIP kernels: it allocates device buffers with torch (plumbing only),
+calls the C-ABI on the current HIP stream, and owns nothing the kernels compute. The reference has no
+assembled operator (it is element-by-element, `solver/element.py:429-464`); the assembled matrix here is
+the coalesced COO of `subdivision.ipynb:118-139`, so `A @ p == compute_nodal_forces(K, elements, p)`.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _capi as C
+
+I32, I64, F64 = torch.int32, torch.int64, torch.float64
+
+
+def _dev_scalar(dev, dtype, value):
+    return torch.full((1,), value, dtype=dtype, device=dev)
+
+
+@dataclass
+class PcgResult:
+    x: torch.Tensor
+    iterations: int      # the reference's reported count (i+1 at the stop)
+    status: int          # _capi.PCG_*
+    rz: float            # last r.z (r.r in CG mode) — the "Residual norm" the reference prints (squared)
+    pq: float            # last p.Ap (printed on breakdown)
+    history: torch.Tensor = None
+
+
+@dataclass
+class Graph:
+    """Node graph of a mesh: incidence + CSR pattern + SELL-64 pattern, all on one device."""
+    n_nodes: int
+    npe: int
+    inc_ptr: torch.Tensor
+    inc: torch.Tensor
+    rowptr: torch.Tensor
+    colidx: torch.Tensor
+    diagpos: torch.Tensor
+    slice_ptr: torch.Tensor
+    cols: torch.Tensor
+    csr2sell: torch.Tensor
+
+    @property
+    def nnz(self):
+        return int(self.colidx.numel())
+
+    @property
+    def sell_entries(self):
+        return int(self.cols.numel())
+
+
+def incidence(elements: torch.Tensor, n_nodes: int):
+    """Deterministic node -> (element, local) incidence of a connectivity block [M, npe] (int64, device)."""
+    lib = C.lib()
+    dev = elements.device
+    M, npe = elements.shape
+    inc_ptr = torch.empty(n_nodes + 1, dtype=I32, device=dev)
+    inc = torch.empty(M * npe, dtype=I32, device=dev)
+    work = torch.empty(n_nodes + int(lib.fem_scan_work_len(n_nodes)), dtype=I32, device=dev)
+    C.check(lib.fem_incidence(C.ptr(elements), M, npe, n_nodes, C.ptr(inc_ptr), C.ptr(inc), C.ptr(work),
+                              C.stream(dev)), "fem_incidence")
+    return inc_ptr, inc
+
+
+def build_graph(elements: torch.Tensor, n_nodes: int) -> Graph:
+    """Node-graph CSR + SELL-64 pattern of `elements` (one element family, int64 [M, npe] on the device).
+    The rows are the coalesced pattern of the reference's COO assembly (`subdivision.ipynb:118-139`)."""
+    lib = C.lib()
+    dev = elements.device
+    elements = elements.contiguous()
+    M, npe = elements.shape
+    st = C.stream(dev)
+    inc_ptr, inc = incidence(elements, n_nodes)
+    row_len = torch.empty(n_nodes, dtype=I32, device=dev)
+    overflow = torch.zeros(1, dtype=I32, device=dev)
+    C.check(lib.fem_graph_count(C.ptr(elements), npe, C.ptr(inc_ptr), C.ptr(inc), n_nodes, C.ptr(row_len),
+                                C.ptr(overflow), st), "fem_graph_count")
+    rowptr = torch.empty(n_nodes + 1, dtype=I32, device=dev)
+    work = torch.empty(int(lib.fem_scan_work_len(n_nodes)) + 1, dtype=I32, device=dev)
+    C.check(lib.fem_scan_i32(C.ptr(row_len), n_nodes, C.ptr(rowptr), C.ptr(work), st), "fem_scan_i32")
+    ov = int(overflow.item())
+    if ov:
+        raise C.FemError(f"fem355: a node has {ov} element-neighbour candidates, above the pattern capacity")
+    nnz = int(rowptr[-1].item())
+    colidx = torch.empty(nnz, dtype=I32, device=dev)
+    diagpos = torch.empty(n_nodes, dtype=I32, device=dev)
+    C.check(lib.fem_graph_fill(C.ptr(elements), npe, C.ptr(inc_ptr), C.ptr(inc), n_nodes, C.ptr(rowptr),
+                               C.ptr(colidx), C.ptr(diagpos), st), "fem_graph_fill")
+    ns = (n_nodes + 63) // 64
+    width = torch.empty(ns, dtype=I64, device=dev)
+    C.check(lib.fem_sell_widths(C.ptr(rowptr), n_nodes, C.ptr(width), st), "fem_sell_widths")
+    slice_ptr = torch.empty(ns + 1, dtype=I64, device=dev)
+    work64 = torch.empty(int(lib.fem_scan_work_len(ns)) + 1, dtype=I64, device=dev)
+    C.check(lib.fem_scan_i64(C.ptr(width), ns, C.ptr(slice_ptr), C.ptr(work64), st), "fem_scan_i64")
+    ent = int(slice_ptr[-1].item())
+    cols = torch.empty(ent, dtype=I32, device=dev)
+    csr2sell = torch.empty(max(nnz, 1), dtype=I64, device=dev)
+    C.check(lib.fem_sell_fill(C.ptr(rowptr), C.ptr(colidx), n_nodes, C.ptr(slice_ptr), C.ptr(cols),
+                              C.ptr(csr2sell), st), "fem_sell_fill")
+    return Graph(n_nodes, npe, inc_ptr, inc, rowptr, colidx, diagpos, slice_ptr, cols, csr2sell)
+
+
+def pad_connectivity(blocks, npe_max):
+    """Concatenate element families into one [sum M, npe_max] block for the pattern (padding repeats node 0
+    of the element; duplicates vanish in the unique-neighbour pass)."""
+    out = []
+    for el in blocks:
+        if el.shape[1] < npe_max:
+            el = torch.cat([el, el[:, :1].expand(-1, npe_max - el.shape[1])], dim=1)
+        out.append(el)
+    return torch.cat(out, 0).contiguous()
+
+
+class SellMatrix:
+    """Assembled global operator in SELL-64 with bs x bs blocks (bs = dofs per node)."""
+
+    def __init__(self, graph: Graph, bs: int):
+        self.g = graph
+        self.bs = bs
+        self.device = graph.cols.device
+        self.vals = torch.zeros(max(graph.sell_entries, 1) * bs * bs, dtype=F64, device=self.device)
+
+    @property
+    def n_rows(self):
+        return self.g.n_nodes
+
+    @property
+    def n(self):
+        return self.g.n_nodes * self.bs
+
+    # ---------------------------------------------------------------- assembly
+    def add_element_matrices(self, Ke: torch.Tensor, elements: torch.Tensor, inc=None):
+        """vals += coalesce(P_e^T K_e P_e) of one element family (deterministic row-gather)."""
+        lib = C.lib()
+        elements = elements.contiguous()
+        Ke = Ke.to(F64).contiguous()
+        npe = elements.shape[1]
+        if Ke.shape[-1] != npe * self.bs:
+            raise ValueError(f"element matrix size {Ke.shape[-1]} != {npe}*{self.bs}")
+        inc_ptr, inc_ = inc if inc is not None else (
+            (self.g.inc_ptr, self.g.inc) if npe == self.g.npe and elements.shape[0] * npe == self.g.inc.numel()
+            else incidence(elements, self.g.n_nodes))
+        C.check(lib.fem_assemble_from_ke(C.ptr(Ke), C.ptr(elements), npe, self.bs, C.ptr(inc_ptr), C.ptr(inc_),
+                                         self.g.n_nodes, C.ptr(self.g.rowptr), C.ptr(self.g.colidx),
+                                         C.ptr(self.g.csr2sell), C.ptr(self.g.slice_ptr), C.ptr(self.vals),
+                                         C.stream(self.device)), "fem_assemble_from_ke")
+        return self
+
+    def add_tet4(self, coords: torch.Tensor, elements: torch.Tensor, E: float, nu: float = 0.0):
+        """vals += the c3d4 operator computed on the fly (bs=3: elasticity E, nu; bs=1: Poisson, kappa=E)."""
+        lib = C.lib()
+        bad = _dev_scalar(self.device, I64, elements.shape[0])
+        C.check(lib.fem_assemble_tet4(C.ptr(coords), C.ptr(elements), float(E), float(nu), self.bs,
+                                      C.ptr(self.g.inc_ptr), C.ptr(self.g.inc), self.g.n_nodes, C.ptr(self.g.rowptr),
+                                      C.ptr(self.g.colidx), C.ptr(self.g.csr2sell), C.ptr(self.g.slice_ptr),
+                                      C.ptr(self.vals), C.ptr(bad), C.stream(self.device)), "fem_assemble_tet4")
+        self._bad = (bad, elements.shape[0])
+        return self
+
+    def check_singular(self):
+        bad = getattr(self, "_bad", None)
+        if bad is not None and int(bad[0].item()) < bad[1]:
+            raise ValueError("Singular matrix encountered while computing B matrix.")
+
+    # ---------------------------------------------------------------- operators
+    def matvec(self, x: torch.Tensor, out: torch.Tensor = None):
+        lib = C.lib()
+        x = x.to(F64).contiguous()
+        y = out if out is not None else torch.empty(self.n, dtype=F64, device=self.device)
+        C.check(lib.fem_spmv(self.g.n_nodes, self.bs, C.ptr(self.g.slice_ptr), C.ptr(self.g.cols),
+                             C.ptr(self.vals), C.ptr(x), C.ptr(y), C.stream(self.device)), "fem_spmv")
+        return y
+
+    def jacobi(self, fixed_mask: torch.Tensor = None):
+        """w = 1/diag(A) (inf -> 0), zero on fixed DOFs (uint8 mask [n])."""
+        lib = C.lib()
+        w = torch.empty(self.n, dtype=F64, device=self.device)
+        C.check(lib.fem_jacobi(C.ptr(self.vals), self.bs, C.ptr(self.g.rowptr), C.ptr(self.g.diagpos),
+                               C.ptr(self.g.csr2sell), C.ptr(self.g.slice_ptr), self.g.n_nodes,
+                               C.ptr(fixed_mask), C.ptr(w), C.stream(self.device)), "fem_jacobi")
+        return w
+
+    def csr(self):
+        """(rowptr, colidx, vals[nnz, bs, bs]) in block-CSR (export / testing)."""
+        lib = C.lib()
+        out = torch.empty(max(self.g.nnz, 1) * self.bs * self.bs, dtype=F64, device=self.device)
+        C.check(lib.fem_sell_to_csr_vals(C.ptr(self.vals), self.bs, C.ptr(self.g.rowptr), self.g.n_nodes,
+                                         C.ptr(self.g.csr2sell), C.ptr(self.g.slice_ptr), C.ptr(out),
+                                         C.stream(self.device)), "fem_sell_to_csr_vals")
+        return self.g.rowptr, self.g.colidx, out[: self.g.nnz * self.bs * self.bs].view(-1, self.bs, self.bs)
+
+    def algorithmic_bytes_spmv(self):
+        """HBM bytes one SpMV must move: 12 nnz + 4 (n+1) + 16 n for scalar CSR,
+        76 nnzb + 4 (nb+1) + 16 n for 3x3 blocks (fp64 values, int32 indices)."""
+        nnzb, nb = self.g.nnz, self.g.n_nodes
+        if self.bs == 1:
+            return 12 * nnzb + 4 * (nb + 1) + 16 * nb
+        return (8 * self.bs * self.bs + 4) * nnzb + 4 * (nb + 1) + 16 * nb * self.bs
+
+    # ---------------------------------------------------------------- solver
+    def pcg(self, b, x0=None, w=None, mode=C.MODE_PCG, tol=1e-8, max_iter=1000, eps=1e-30, history=False,
+            chunk=32):
+        """Run the device (P)CG; returns (x, iterations, status, rz_last, hist or None)."""
+        lib = C.lib()
+        b = b.to(F64).contiguous().view(-1)
+        x = (torch.zeros(self.n, dtype=F64, device=self.device) if x0 is None
+             else x0.to(device=self.device, dtype=F64).clone().contiguous().view(-1))
+        w = w.to(F64).contiguous().view(-1)
+        hist = torch.full((max(max_iter, 1),), float("nan"), dtype=F64, device=self.device) if history else None
+        h = ctypes.c_void_p()
+        C.check(lib.fem_pcg_create(self.g.n_nodes, self.bs, C.ptr(self.g.slice_ptr), C.ptr(self.g.cols),
+                                   C.ptr(self.vals), C.ptr(b), C.ptr(x), C.ptr(w), mode, float(tol), float(eps),
+                                   C.ptr(hist), hist.numel() if hist is not None else 0, C.stream(self.device),
+                                   ctypes.byref(h)), "fem_pcg_create")
+        try:
+            it, stt, rz = ctypes.c_int(), ctypes.c_int(), ctypes.c_double()
+            C.check(lib.fem_pcg_solve(h, int(max_iter), int(chunk), ctypes.byref(it), ctypes.byref(stt),
+                                      ctypes.byref(rz)), "fem_pcg_solve")
+            sc = (ctypes.c_double * 6)()
+            C.check(lib.fem_pcg_scalars(h, sc), "fem_pcg_scalars")
+        finally:
+            lib.fem_pcg_destroy(h)
+        if hist is not None:
+            hist = hist[: min(it.value, hist.numel())]
+        return PcgResult(x, it.value, stt.value, rz.value, sc[1], hist)
+
+
+class PcgRunner:
+    """Persistent (P)CG context for fixed-iteration timing (bench.py): start once, iterate k, poll."""
+
+    def __init__(self, A: SellMatrix, b, w, x0=None, mode=C.MODE_PCG, tol=0.0, eps=1e-30):
+        self.lib = C.lib()
+        self.A = A
+        self.b = b.to(F64).contiguous().view(-1)
+        self.w = w.to(F64).contiguous().view(-1)
+        self.x = (torch.zeros(A.n, dtype=F64, device=A.device) if x0 is None
+                  else x0.to(F64).clone().contiguous().view(-1))
+        self.h = ctypes.c_void_p()
+        C.check(self.lib.fem_pcg_create(A.g.n_nodes, A.bs, C.ptr(A.g.slice_ptr), C.ptr(A.g.cols), C.ptr(A.vals),
+                                        C.ptr(self.b), C.ptr(self.x), C.ptr(self.w), mode, float(tol), float(eps),
+                                        None, 0, C.stream(A.device), ctypes.byref(self.h)), "fem_pcg_create")
+
+    def start(self):
+        C.check(self.lib.fem_pcg_start(self.h), "fem_pcg_start")
+
+    def use_graph(self, k):
+        C.check(self.lib.fem_pcg_use_graph(self.h, int(k)), "fem_pcg_use_graph")
+
+    def iterate(self, k):
+        C.check(self.lib.fem_pcg_iterate(self.h, int(k)), "fem_pcg_iterate")
+
+    def poll(self):
+        it, stt, rz = ctypes.c_int(), ctypes.c_int(), ctypes.c_double()
+        C.check(self.lib.fem_pcg_poll(self.h, ctypes.byref(it), ctypes.byref(stt), ctypes.byref(rz)), "fem_pcg_poll")
+        return it.value, stt.value, rz.value
+
+    def profile(self, k, every=1):
+        """k iterations with hip events around the kernels of every `every`-th one -> (ms sums, counts)."""
+        ms = (ctypes.c_double * 3)()
+        n = (ctypes.c_int * 3)()
+        C.check(self.lib.fem_pcg_profile(self.h, int(k), int(every), ms, n), "fem_pcg_profile")
+        return list(ms), list(n)
+
+    def close(self):
+        if self.h:
+            self.lib.fem_pcg_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def assemble_tet4_system(coords, elements, kind="poisson", E=1.0, nu=0.0, graph=None):
+    """Mesh -> assembled device operator in one pass (pattern + values; element matrices never stored).
+    kind: "poisson" (bs=1, kappa=E) or "elastic" (bs=3)."""
+    n_nodes = coords.shape[0]
+    g = graph if graph is not None else build_graph(elements, n_nodes)
+    bs = 1 if kind == "poisson" else 3
+    A = SellMatrix(g, bs).add_tet4(coords.to(F64).contiguous(), elements.contiguous(), E, nu)
+    return A

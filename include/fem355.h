@@ -1,0 +1,202 @@
+/*
+ * fem355 C-ABI — MI355X (gfx950) FEM assembly + Jacobi-PCG.
+ *
+ * Drop-in boundary for the hot path of sml2004/CUDA-powered-mesh-handling-and-Iterative-solvers
+ * (reference @ 2025-04-18; citations are reference-relative file:line). The reference is pure
+ * Python/PyTorch, so its "FFI" is its module-level function surface; each entry point below names the
+ * reference function whose device work it replaces. The Python mirror of that surface is
+ * `cuda-powered-mesh-handling-and-iterative-solvers_amd/{element,solver}.py` (ctypes, `_capi.py`).
+ *
+ * Conventions
+ *   - every pointer is caller-owned DEVICE memory (torch tensors' data_ptr()), except where marked [host];
+ *   - coordinates / values are fp64; connectivity is int64 row-major [M, npe] (torch.long, as the reference);
+ *   - graph indices (incidence, CSR/SELL pattern) are int32, offsets into value arrays int64;
+ *   - dof = dpn * node + component (`solver/element.py:451`); dpn (= block size bs) is 1 or 3;
+ *   - every call is asynchronous on `stream` (a hipStream_t; 0 = legacy default) unless marked [sync];
+ *   - return value: FEM_OK or one of the FEM_E* codes; fem_last_error() gives a message.
+ *
+ * Matrix format (the "ELL-blocked" global matrix): SELL-64 with bs x bs blocks. Rows (nodes) are cut into
+ * slices of 64; slice s has width w_s = max row length in the slice; entry (s, k, lane) holds block
+ * column cols[slice_ptr[s] + 64*k + lane] and its bs*bs values at
+ *   vals[bs*bs*slice_ptr[s] + 64*(bs*bs*k + rc) + lane],  rc = r*bs + c (row-major in the block).
+ * Padding entries have col = own row and zero values. Columns of a row are ascending.
+ */
+#ifndef FEM355_H
+#define FEM355_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* fem_stream_t; /* hipStream_t */
+
+enum {
+    FEM_OK = 0,
+    FEM_EBADTYPE = 1,   /* unsupported element type  -> ValueError (`solver/element.py:427`) */
+    FEM_ESINGULAR = 2,  /* singular element, index in *bad_idx -> ValueError (`solver/element.py:857-858`) */
+    FEM_EHIP = 3,       /* HIP runtime error -> RuntimeError */
+    FEM_ERCCL = 4,      /* RCCL error -> RuntimeError */
+    FEM_EARG = 5,       /* bad argument / capacity exceeded */
+};
+
+/* status words of the (P)CG state, mirrored on the host as the reference's print strings
+ * (`solver/solver.py:187-198,210-218,226-227,805-811`) */
+enum {
+    FEM_PCG_RUNNING = 0,
+    FEM_PCG_CONVERGED = 1,
+    FEM_PCG_MAXITER = 2,
+    FEM_PCG_BREAKDOWN = 3,  /* pAp < eps or pAp < 0  (`solver/solver.py:187-192`) */
+    FEM_PCG_ALPHA_NAN = 4,  /* (`solver/solver.py:196-198`) */
+    FEM_PCG_BETA_NAN = 5,   /* (`solver/solver.py:214-218`) */
+};
+
+enum { FEM_MODE_CG_STABLE = 0, FEM_MODE_PCG = 1 };
+enum { FEM_KIND_ELASTIC = 0, FEM_KIND_POISSON = 1, FEM_KIND_MASS = 2 };
+enum { FEM_ISO_SUM = 0, FEM_ISO_STACK = 1, FEM_ISO_VOLUME = 2 };
+
+const char* fem_last_error(void);                 /* [host] message of the last failing call */
+int fem_version(void);                            /* [host] ABI version (100 * major + minor) */
+
+/* ------------------------------------------------------------------ element stiffness (L1)
+ * fem_tet4_ke: c3d4 element matrices.
+ *   kind = FEM_KIND_ELASTIC: Ke [M,12,12] = B^T D B V   — replaces compute_c3d4_K_matrix
+ *          (`solver/element.py:883-903`, with B `:835-881`, D `:282-306`, V `:514-541`).
+ *   kind = FEM_KIND_POISSON: Ke [M,4,4] = kappa V G G^T (derived P1 Laplacian; no reference function,
+ *          SURVEY §8(a) a15); `E` is used as kappa.
+ *   Singular check |det[1 x y z]| < 1e-12 -> FEM_ESINGULAR, *bad_idx [device int64] = first bad element
+ *   (initialise it to M). */
+int fem_tet4_ke(const double* coords, const int64_t* conn, int64_t M, double E, double nu, int kind,
+                double* Ke, int64_t* bad_idx, fem_stream_t stream);
+
+/* c3d4 geometry: vol [M] = |det|/6 (compute_tetrahedral_volumes, `solver/element.py:514-541`), grads [M,4,3]
+ * (rows of inv([1 x y z]), `:851-866`), B [M,6,12] (compute_c3d4_B_matrix, `:835-881`); outputs may be NULL.
+ * kind FEM_KIND_MASS of fem_tet4_ke gives the consistent P1 mass [M,12,12] = rho V (1+delta_ab)/20 (x) I3 with
+ * E = rho (compute_c3d4_M_matrix, called at `solver_example.ipynb:221`; no source exists: parity unpinned). */
+int fem_tet4_geom(const double* coords, const int64_t* conn, int64_t M, double* vol, double* grads, double* B,
+                  int64_t* bad_idx, fem_stream_t stream);
+
+/* fem_iso_ke: isoparametric solids c3d8 / c3d6 / c3d10 (npe = 8 / 6 / 10). The natural derivatives dN
+ * [n_ip, npe, 3] and weights w [n_ip] are evaluated on the host exactly as the reference does (its quirks:
+ * c3d10 weights summing to 0.45, the float32 line points of c3d6), then
+ *   mode FEM_ISO_SUM    : Ke[M,d,d]      = sum_q w_q detJ_q B_q^T D B_q   (signed detJ)
+ *   mode FEM_ISO_STACK  : Ke[n_ip,M,d,d] = detJ_q B_q^T D B_q            (`single=False`, Q6)
+ *   mode FEM_ISO_VOLUME : Ke[M,d,d]      = B^T D B * wedge volume, one point (c3d6 single=True)
+ * Replaces compute_c3d8_K_matrix (`solver/element.py:1754-1803`), compute_c3d6_K_matrix (`:2631-2676`),
+ * compute_c3d10_K_matrix (`:1191-1239`). */
+int fem_iso_ke(const double* coords, const int64_t* conn, int64_t M, int npe, double E, double nu,
+               const double* dN, const double* w, int n_ip, int mode, double* Ke, fem_stream_t stream);
+/* J [M,3,3] (J[i][k] = sum_j dN[j][i] x_j[k]), global gradients [M,npe,3] and B [M,6,3npe] of an isoparametric
+ * element at one point with natural derivatives dN [npe,3]; outputs may be NULL. Replaces compute_c3d8_Jacobian /
+ * _shape_gradients / _B_matrix (`solver/element.py:1601-1694`) and the c3d6 (`:2482-2568`) / c3d10
+ * (`:1026-1125`) equivalents. */
+int fem_iso_geom(const double* coords, const int64_t* conn, int64_t M, int npe, const double* dN, double* J,
+                 double* grads, double* B, fem_stream_t stream);
+
+/* ------------------------------------------------------------------ mesh graph (pattern build)
+ * Node -> (element, local) incidence, deterministic (entries sorted ascending by e*npe+local).
+ * inc_ptr [N+1], inc [M*npe]; work: int32 [N + fem_scan_work_len(N)]. */
+int64_t fem_scan_work_len(int64_t n);
+int fem_incidence(const int64_t* conn, int64_t M, int npe, int64_t N, int32_t* inc_ptr, int32_t* inc,
+                  int32_t* work, fem_stream_t stream);
+
+/* Node-graph CSR pattern (block pattern for any dpn): the coalesced COO pattern of the reference's global
+ * assembly (`subdivision.ipynb:118-139`) at node granularity. Two passes:
+ *   fem_graph_count : row_len [N]  (unique neighbours incl. self); *overflow [device int] set on capacity
+ *   fem_graph_fill  : colidx [nnz] sorted per row, diagpos [N] (position of the diagonal)
+ * rowptr [N+1] is the exclusive scan of row_len (fem_scan_i32). */
+int fem_graph_count(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
+                    int32_t* row_len, int32_t* overflow, fem_stream_t stream);
+int fem_graph_fill(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
+                   const int32_t* rowptr, int32_t* colidx, int32_t* diagpos, fem_stream_t stream);
+/* exclusive scan of int32 counts -> out[n+1] (out[n] = total); work: int32 [fem_scan_work_len(n)] */
+int fem_scan_i32(const int32_t* in, int64_t n, int32_t* out, int32_t* work, fem_stream_t stream);
+
+/* CSR pattern -> SELL-64 pattern. slice_ptr [S+1] int64 (entries, i.e. 64*sum of widths); cols [slice_ptr[S]].
+ *   fem_sell_widths: width [S] int64 = 64 * max row length in the slice (scan it with fem_scan_i64)
+ *   fem_sell_fill  : cols (padding = own row) and the CSR->SELL entry map csr2sell [nnz] int64 */
+int fem_sell_widths(const int32_t* rowptr, int64_t nrows, int64_t* width, fem_stream_t stream);
+int fem_scan_i64(const int64_t* in, int64_t n, int64_t* out, int64_t* work, fem_stream_t stream);
+int fem_sell_fill(const int32_t* rowptr, const int32_t* colidx, int64_t nrows, const int64_t* slice_ptr,
+                  int32_t* cols, int64_t* csr2sell, fem_stream_t stream);
+
+/* ------------------------------------------------------------------ global assembly (values)
+ * Deterministic row-gather: every block row sums its contributions in ascending element order.
+ * fem_assemble_from_ke: values from element matrices Ke [M, npe*bs, npe*bs] (the solver-entry path: the
+ *   reference hands K[M,d,d] to its CG, `solver/solver.py:144`).
+ * fem_assemble_tet4  : values of the c3d4 elastic (bs=3) / Poisson (bs=1) operator computed on the fly
+ *   from coordinates (K_e never materialised). E is kappa for Poisson.
+ * Both write SELL values (vals must be zeroed by the caller). */
+int fem_assemble_from_ke(const double* Ke, const int64_t* conn, int npe, int bs, const int32_t* inc_ptr,
+                         const int32_t* inc, int64_t N, const int32_t* rowptr, const int32_t* colidx,
+                         const int64_t* csr2sell, const int64_t* slice_ptr, double* vals, fem_stream_t stream);
+int fem_assemble_tet4(const double* coords, const int64_t* conn, double E, double nu, int bs,
+                      const int32_t* inc_ptr, const int32_t* inc, int64_t N, const int32_t* rowptr,
+                      const int32_t* colidx, const int64_t* csr2sell, const int64_t* slice_ptr, double* vals,
+                      int64_t* bad_idx, fem_stream_t stream);
+
+/* SELL -> CSR values (export / testing): csr_vals [nnz*bs*bs] row-major blocks. */
+int fem_sell_to_csr_vals(const double* vals, int bs, const int32_t* rowptr, int64_t nrows,
+                         const int64_t* csr2sell, const int64_t* slice_ptr, double* csr_vals,
+                         fem_stream_t stream);
+
+/* Jacobi: w[i] = 1/A_ii (inf -> 0, `solver/solver.py:830-831`), w[i] = 0 where mask[i] != 0 (fixed DOFs);
+ * mask may be NULL. diag read through diagpos. */
+int fem_jacobi(const double* vals, int bs, const int32_t* rowptr, const int32_t* diagpos,
+               const int64_t* csr2sell, const int64_t* slice_ptr, int64_t nrows, const uint8_t* mask,
+               double* w, fem_stream_t stream);
+
+/* ------------------------------------------------------------------ element-by-element operator
+ * y = sum_e P_e^T K_e P_e u — replaces compute_nodal_forces (`solver/element.py:429-464`), deterministic
+ * (ascending element order per dof, like the CPU index_add). Ke [M, npe*dpn, npe*dpn]. */
+int fem_ebe_apply(const double* Ke, const int64_t* conn, int npe, int dpn, const int32_t* inc_ptr,
+                  const int32_t* inc, int64_t N, const double* u, double* y, fem_stream_t stream);
+/* diag_K of compute_diagonal_preconditioner (`solver/solver.py:814-833`) before inversion:
+ * colzero = 1 reproduces the reference's column-0 slice (`:828`, quirk Q1), 0 the true diagonal. */
+int fem_ebe_diag(const double* Ke, const int64_t* conn, int npe, int dpn, const int32_t* inc_ptr,
+                 const int32_t* inc, int64_t N, int colzero, double* diag, fem_stream_t stream);
+/* out[i] = 1/in[i], inf -> 0 */
+int fem_invert_diag(const double* in, int64_t n, double* out, fem_stream_t stream);
+
+/* ------------------------------------------------------------------ SpMV (L2)
+ * y = A x on the SELL-64 matrix (nrows block rows of size bs). */
+int fem_spmv(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_t* cols, const double* vals,
+             const double* x, double* y, fem_stream_t stream);
+
+/* ------------------------------------------------------------------ (P)CG (L3)
+ * One solve context over a SELL matrix. The whole iteration runs on the device: SpMV + p.q reduction,
+ * update + r.z reduction, p/x update; scalars, guards and the stop test live in a device state word,
+ * so the host only polls between chunks of iterations.
+ *   mode FEM_MODE_CG_STABLE: stable_conjugate_gradient_solver (`solver/solver.py:144-229`), w = free mask
+ *        (1 free / 0 fixed), alpha = rs/(pAp+eps), beta = rs_new/(rs_old+eps), stop sqrt(r.r) < tol
+ *   mode FEM_MODE_PCG: preconditioned_conjugate_gradient_solver (`solver/solver.py:766-812`), w = M_inv,
+ *        no eps, no guards, stop sqrt(r.z) < tol
+ * b, x, w are [n = nrows*bs]; x holds u_init on entry and u on exit. hist [max_iter] (may be NULL)
+ * receives sqrt(r.z) (sqrt(r.r) for CG) after each iteration. */
+typedef struct fem_pcg fem_pcg;   /* opaque */
+int fem_pcg_create(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_t* cols, const double* vals,
+                   const double* b, double* x, const double* w, int mode, double tol, double eps,
+                   double* hist, int64_t hist_len, fem_stream_t stream, fem_pcg** out);
+/* initial residual r0 = b - A x0 (+ masking in CG mode), z0, p0, r0.z0 */
+int fem_pcg_start(fem_pcg* s);
+/* enqueue k iterations (no host sync); iterations after a stop are no-ops on the device */
+int fem_pcg_iterate(fem_pcg* s, int k);
+/* [sync] read iteration count, status and last r.z (or r.r) */
+int fem_pcg_poll(fem_pcg* s, int* iters, int* status, double* rz);
+/* [sync] out6 = {rz (rs_old), pq (p.Ap), alpha, beta, rz_new, completed iterations} for the host messages */
+int fem_pcg_scalars(fem_pcg* s, double* out6);
+/* [sync] run to completion: start + chunks of `chunk` iterations until stop or max_iter */
+int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, double* rz);
+/* capture `k` iterations in a hipGraph and use it for fem_pcg_iterate calls with that k (0 disables) */
+int fem_pcg_use_graph(fem_pcg* s, int k);
+/* [sync] enqueue k iterations like fem_pcg_iterate, bracketing every `every`-th iteration's three kernels
+ * with hip events on the solver stream; ms[0..2] = summed device ms of SpMV+dot / update / p-x update over the
+ * n[0..2] sampled launches (bench.py's live per-kernel timing inside its timed region) */
+int fem_pcg_profile(fem_pcg* s, int k, int every, double* ms, int* n);
+void fem_pcg_destroy(fem_pcg* s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FEM355_H */

@@ -1,0 +1,97 @@
+"""Tier 1 (CPU): the oracle restatement against golden vectors produced by the reference itself
+(tools/gen_golden.py). Bit-exact where the op sequence is the reference's."""
+import torch
+
+from conftest import load_golden, rel
+from oracle import ref_cpu as R
+
+E, NU = 113.8e9, 0.342
+
+
+def test_tet4_element_algebra():
+    g = load_golden("tet4_cube_n4_jit")
+    c, t = g["coords"], g["tets"]
+    assert rel(R.tet_volumes(c, t), g["V"]) == 0.0
+    assert rel(R.tet4_B(c, t), g["B"]) == 0.0
+    assert rel(R.tet4_K(c, t, E, NU), g["K"]) == 0.0
+    assert rel(R.elasticity_matrix(E, NU), g["D"]) < 1e-15
+
+
+def test_ebe_operator_and_preconditioner():
+    g = load_golden("tet4_cube_n4_jit")
+    K, t = g["K"], g["tets"]
+    assert rel(R.nodal_forces(K, t, g["p"]), g["y"]) == 0.0
+    assert rel(R.diag_preconditioner(K, t, g["coords"].shape[0], compat_colzero=True), g["Minv_bug"]) == 0.0
+    g6 = load_golden("tet4_cube_n6")
+    K6 = R.tet4_K(g6["coords"], g6["tets"], E, NU)
+    assert rel(R.nodal_forces(K6, g6["tets"], g6["p"]), g6["y"]) < 1e-15
+
+
+def test_stable_cg_and_pcg_match_reference_iterations():
+    g = load_golden("tet4_cube_n4_jit")
+    K, t = g["K"], g["tets"]
+    hist = []
+    u, n, s = R.stable_cg(K, t, g["F"], g["fixed"], tol=float(g["tol"]), history=hist)
+    assert s == "converged" and n == int(g["n_cg"])
+    assert rel(u, g["u_cg"]) == 0.0
+    u, n, s = R.pcg(K, t, g["F"], g["Minv"], tol=1e-6)
+    assert n == int(g["n_pcg"]) and rel(u, g["u_pcg"]) == 0.0
+    assert str(g["cg_stdout"]).startswith(f"Converged after {int(g['n_cg'])} iterations.")
+
+
+def test_cg_residual_history_first_iterations():
+    """Contract: the true masked residual after k iterations matches the reference's."""
+    g = load_golden("tet4_cube_n4_jit")
+    K, t, F, fixed = g["K"], g["tets"], g["F"], g["fixed"]
+    ref = g["cg_hist"]
+    for k in (1, 5, 10, 20):
+        u, _, _ = R.stable_cg(K, t, F, fixed, tol=0.0, max_iter=k)
+        r = F - R.nodal_forces(K, t, u)
+        r[fixed] = 0.0
+        assert abs(float(torch.linalg.norm(r)) - float(ref[k - 1])) <= 1e-10 * float(ref[k - 1])
+
+
+def test_isoparametric_solids():
+    for et in ("c3d8", "c3d6", "c3d10"):
+        g = load_golden(f"{et}_cells")
+        c, e = g["coords"], g["elements"]
+        p, w = R.POINTS[et]()
+        assert rel(p, g["points"]) == 0.0 and rel(w, g["weights"]) == 0.0
+        assert rel(R.iso_K(c, e, et, E, NU), g["K_single"]) == 0.0, et
+        assert rel(R.iso_K(c, e, et, E, NU, single=False), g["K_multi"]) == 0.0, et
+        for q in range(p.shape[0]):
+            dN = R.DN[et](*[float(v) for v in p[q]])
+            assert rel(R.iso_jacobian(c, e, dN), g["J"][q]) < 1e-15
+            assert rel(R.iso_gradients(c, e, dN), g["grads"][q]) < 1e-14
+
+
+def test_poisson_derivation_and_solve():
+    g = load_golden("poisson_tet4_n4_jit")
+    c, t = g["coords"], g["tets"]
+    assert rel(R.tet4_poisson_K(c, t), g["KP"]) == 0.0
+    u, n, _ = R.pcg(g["KP"], t, g["f"].view(-1, 1), g["dinv"].view(-1, 1), tol=float(g["tol"]))
+    assert n == int(g["n_pcg"]) and rel(u[:, 0], g["u"]) < 1e-14
+    assert rel(R.nodal_forces(g["KP"], t, g["p"].view(-1, 1))[:, 0], g["y"]) < 1e-14
+
+
+def test_static_structure_mixed():
+    g = load_golden("mixed_static")
+    u, n, s = R.static_structure(g["coords"], g["force"], g["fixed"],
+                                 {"c3d4": g["c3d4"], "c3d6": g["c3d6"], "c3d8": g["c3d8"]}, E, NU, tol=1e-6,
+                                 max_iter=3000)
+    assert s == "converged" and n == int(g["n_iter"]) and rel(u, g["u"]) == 0.0
+
+
+def test_coo_coalesce_equals_ebe_and_partition_maps():
+    g = load_golden("tet4_cube_n4_jit")
+    K, t, p = g["K"], g["tets"], g["p"]
+    rp, ci, v = R.coo_to_csr(K, t, 3)
+    y = R.csr_matvec(rp, ci, v, p.reshape(-1)).view(-1, 3)
+    assert rel(y, g["y"]) < 1e-14
+    rpn, cin = R.node_pattern(t, g["coords"].shape[0])
+    # the dof pattern is the node pattern expanded by 3x3 blocks
+    assert int(rp[-1]) == 9 * int(rpn[-1])
+    pr = load_golden("partition_ref")
+    for k in range(4):
+        nodes, loc = R.partition_local_maps(pr["tets"], pr[f"ids{k}"])
+        assert torch.equal(nodes, pr[f"nodes{k}"]) and torch.equal(loc, pr[f"local{k}"])

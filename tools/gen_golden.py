@@ -164,8 +164,8 @@ def gen_solids(el, so):
             pts, w = el.c3d8_integration_points(device=CPU, dtype=F64)
         Js, Gs, Bs = [], [], []
         for q in range(pts.shape[0]):
-            Js.append(el.compute_Jacobian(coords, cells, etype, pts[q], device=CPU) if etype != "c3d6" else
-                      el.compute_c3d6_Jacobian(coords, cells, pts[q], device=CPU, dtype=F64))
+            Js.append({"c3d8": el.compute_c3d8_Jacobian, "c3d6": el.compute_c3d6_Jacobian,
+                       "c3d10": el.compute_c3d10_Jacobian}[etype](coords, cells, pts[q], device=CPU, dtype=F64))
             Gs.append({"c3d8": el.compute_c3d8_shape_gradients, "c3d6": el.compute_c3d6_shape_gradients,
                        "c3d10": el.compute_c3d10_shape_gradients}[etype](coords, cells, pts[q], device=CPU, dtype=F64))
             Bs.append({"c3d8": el.compute_c3d8_B_matrix, "c3d6": el.compute_c3d6_B_matrix,
