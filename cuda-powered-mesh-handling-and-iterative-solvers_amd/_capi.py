@@ -52,12 +52,16 @@ SIGNATURES = {
     "fem_ebe_diag": (_I, [_P, _P, _I, _I, _P, _P, _L, _I, _P, _P]),
     "fem_invert_diag": (_I, [_P, _L, _P, _P]),
     "fem_spmv": (_I, [_L, _I, _P, _P, _P, _P, _P, _P]),
+    "fem_spmv_variant": (_I, [_I, _I, _L, _I, _P, _P, _P, _P, _P, _P]),
+    "fem_stream_copy": (_I, [_P, _P, _L, _I, _P]),
     "fem_pcg_create": (_I, [_L, _I, _P, _P, _P, _P, _P, _P, _I, _D, _D, _P, _L, _P, ctypes.POINTER(_P)]),
     "fem_pcg_start": (_I, [_P]),
     "fem_pcg_iterate": (_I, [_P, _I]),
     "fem_pcg_poll": (_I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_D)]),
     "fem_pcg_solve": (_I, [_P, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_D)]),
     "fem_pcg_use_graph": (_I, [_P, _I]),
+    "fem_pcg_set_schedule": (_I, [_P, _I]),
+    "fem_pcg_finish": (_I, [_P]),
     "fem_pcg_profile": (_I, [_P, _I, _I, ctypes.POINTER(_D), ctypes.POINTER(_I)]),
     "fem_pcg_destroy": (None, [_P]),
 }

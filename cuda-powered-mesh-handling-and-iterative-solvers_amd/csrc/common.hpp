@@ -69,21 +69,20 @@ __device__ __forceinline__ int wave_max_i(int v) {
     return v;
 }
 
-// Last-block-done ticket (agent-scope release/acquire, MI355X_MICROARCH.md §visibility): every block
-// publishes `partial` into partials[blockIdx.x]; returns true in the block whose arrival was last, after an
-// acquire, so it may read every partial. The counter is re-armed by the last block.
+// Last-block-done ticket. Every block hands ONE 8-byte partial to the last-arriving block, in the write-through
+// form of MI355X_MICROARCH.md §visibility ("Valid forms", first table row): the partial is stored `sc1`
+// (relaxed agent-scope atomic store), the storing wave drains it with `s_waitcnt vmcnt(0)`, then one
+// agent-scope atomic add on the counter signals; the last block reads every partial with `sc1` loads
+// (sum_partials). No release fence: `buffer_wbl2` would write back every dirty line of the XCD's L2 (the
+// q / r streams this kernel just wrote) in every block. The counter is re-armed by the last block.
 __device__ __forceinline__ bool publish_partial(double partial, double* partials, unsigned* counter,
                                                 int* lds_flag) {
     if (threadIdx.x == 0) {
         __hip_atomic_store(&partials[blockIdx.x], partial, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         int last = (t == gridDim.x - 1);
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (last) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *lds_flag = last;
     }
     __syncthreads();
@@ -96,6 +95,54 @@ __device__ __forceinline__ double sum_partials(const double* partials, int n, do
     for (int i = threadIdx.x; i < n; i += 256)
         v += __hip_atomic_load(&partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return block_sum256(v, lds4);
+}
+
+// Two-level (sharded) grid reduction. One counter takes ~12 ns per arrival (MI355X_MICROARCH.md row
+// "fanin"), so 2048 arrivals on one word cost ~25 us. Blocks arrive on RED_SHARDS counters (blockIdx % shards,
+// each on its own 128-byte line); the last arriver of a shard sums its shard's partials (fixed order) and
+// arrives on the top counter; the last shard sums the shard sums (fixed order). Same `sc1` store / drain /
+// atomic / `sc1` load hand-off as publish_partial. Deterministic: the summation order never depends on arrival.
+// Layout of `counters`: (RED_SHARDS + 1) * 32 unsigned; `partials`: gridDim.x + RED_SHARDS doubles.
+constexpr int RED_SHARDS = 32;
+constexpr int RED_COUNTER_WORDS = (RED_SHARDS + 1) * 32;
+
+__device__ __forceinline__ bool reduce_grid(double partial, double* partials, unsigned* counters, double* total,
+                                            double* lds4, int* lds_flag) {
+    const unsigned G = gridDim.x;
+    const unsigned nsh = G < (unsigned)RED_SHARDS ? G : (unsigned)RED_SHARDS;
+    const unsigned sh = blockIdx.x % RED_SHARDS;
+    const unsigned in_shard = (G - sh + RED_SHARDS - 1) / RED_SHARDS;   // blocks b < G with b % shards == sh
+    double* shard_sums = partials + G;
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(&partials[blockIdx.x], partial, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned t = __hip_atomic_fetch_add(&counters[sh * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int last = (t == in_shard - 1);
+        if (last) __hip_atomic_store(&counters[sh * 32], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *lds_flag = last;
+    }
+    __syncthreads();
+    if (!*lds_flag) return false;
+    double v = 0.0;
+    for (unsigned i = threadIdx.x; i < in_shard; i += 256)
+        v += __hip_atomic_load(&partials[sh + i * RED_SHARDS], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    v = block_sum256(v, lds4);
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(&shard_sums[sh], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned* top = &counters[RED_SHARDS * 32];
+        unsigned t = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int last = (t == nsh - 1);
+        if (last) __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *lds_flag = last;
+    }
+    __syncthreads();
+    if (!*lds_flag) return false;
+    double s = (threadIdx.x < nsh)
+                   ? __hip_atomic_load(&shard_sums[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                   : 0.0;
+    *total = block_sum256(s, lds4);
+    return true;
 }
 
 }  // namespace fem

@@ -1,28 +1,52 @@
 // SELL-64 SpMV and the device-resident (P)CG iteration (L2 + L3 of the hot path).
 //
 // Replaces the reference's per-iteration op chain (`solver/solver.py:182-224` / `:798-810`): EBE matvec via
-// gather + bmm + index_add (`solver/element.py:429-464`), torch.sum dots and axpys, with three kernels per
-// iteration and no host synchronisation:
-//   K1 spmv_dot : q = A p (SELL-64, one wave per 64-row slice, XCD-contiguous slice ranges), p.q partials,
-//                 the last block forms pq, the breakdown guards and alpha
-//   K2 update   : r <- r - alpha q (masked in CG mode), z = w r, r.z partials; last block: stop test, beta
-//   K3 pupdate  : x <- x + alpha p ; p <- z + beta p  (x update deferred here so p is read once)
-// Scalars and the stop flag live in device memory; kernels after a stop are no-ops, so the host enqueues
-// chunks of iterations and polls once per chunk.
+// gather + bmm + index_add (`solver/element.py:429-464`), torch.sum dots and axpys. No host synchronisation
+// inside the iteration: scalars, guards and the stop flag live in a device state word, kernels after a stop
+// are no-ops, and the host polls once per chunk of iterations.
+//
+// Two kernel schedules (same arithmetic, same results up to fp rounding order; 3-kernel is the default):
+//   3-kernel  K1 spmv_dot : q = A p, p.q               -> alpha, guards
+//             K2 update   : r -= alpha q, z = w r, r.z -> stop test, beta
+//             K3 pupdate  : x += alpha p ; p = z + beta p
+//   fused     K1 spmv_dot : x += alpha' p' ; p = w r + beta p' computed on the fly for every gathered column
+//                           (double-buffered p), q = A p, p.q
+//             K2 update   (as above)                          -> 2 launches and 88 n bytes of vectors per iteration
+// Grid reductions are deterministic two-level trees (common.hpp reduce_grid).
 #include <vector>
 
 #include "common.hpp"
 
 namespace fem {
 
+template <typename T, bool NT>
+__device__ __forceinline__ T ld(const T* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+// Vector operands of the SpMV: a plain vector, or the fused p = w r + beta p_old evaluated per gathered dof.
+struct VecPlain {
+    const double* x;
+    __device__ __forceinline__ double operator()(int64_t i) const { return x[i]; }
+};
+struct VecFusedP {
+    const double* r;
+    const double* w;
+    const double* pold;
+    double beta;
+    __device__ __forceinline__ double operator()(int64_t i) const { return w[i] * r[i] + beta * pold[i]; }
+};
+
 // ---------------------------------------------------------------- SELL SpMV core
 // One wave = one slice of 64 block rows; lane = row. Row entries are strided by 64, so every load of the
 // wave (cols, each of the bs*bs value planes) is one contiguous 256/512-byte segment; on meshes numbered
-// along lines the x gathers of neighbouring lanes are contiguous too.
-template <int BS>
+// along lines the x gathers of neighbouring lanes are contiguous too. U entries per step: all U column loads,
+// then U value loads, then U gathers are in flight together; the tail step is predicated.
+template <int BS, int U, bool NT, typename X>
 __device__ __forceinline__ void sell_row(int64_t s, int lane, const int64_t* __restrict__ slice_ptr,
                                          const int32_t* __restrict__ cols, const double* __restrict__ vals,
-                                         const double* __restrict__ x, double out[BS]) {
+                                         const X& x, double out[BS]) {
     const int64_t p0 = slice_ptr[s];
     const int w = (int)((slice_ptr[s + 1] - p0) >> 6);
     const int32_t* c = cols + p0 + lane;
@@ -30,35 +54,38 @@ __device__ __forceinline__ void sell_row(int64_t s, int lane, const int64_t* __r
     for (int r = 0; r < BS; ++r) out[r] = 0.0;
     if (BS == 1) {
         const double* v = vals + p0 + lane;
-        int k = 0;
-        for (; k + 4 <= w; k += 4) {
-            int c0 = c[64 * k], c1 = c[64 * (k + 1)], c2 = c[64 * (k + 2)], c3 = c[64 * (k + 3)];
-            double v0 = v[64 * k], v1 = v[64 * (k + 1)], v2 = v[64 * (k + 2)], v3 = v[64 * (k + 3)];
-            double x0 = x[c0], x1 = x[c1], x2 = x[c2], x3 = x[c3];
-            out[0] += v0 * x0;
-            out[0] += v1 * x1;
-            out[0] += v2 * x2;
-            out[0] += v3 * x3;
+        for (int k0 = 0; k0 < w; k0 += U) {
+            int ci[U];
+            double vi[U], xi[U];
+#pragma unroll
+            for (int j = 0; j < U; ++j) ci[j] = (k0 + j < w) ? ld<int32_t, NT>(c + 64 * (k0 + j)) : 0;
+#pragma unroll
+            for (int j = 0; j < U; ++j) vi[j] = (k0 + j < w) ? ld<double, NT>(v + 64 * (k0 + j)) : 0.0;
+#pragma unroll
+            for (int j = 0; j < U; ++j) xi[j] = (k0 + j < w) ? x(ci[j]) : 0.0;
+#pragma unroll
+            for (int j = 0; j < U; ++j)
+                if (k0 + j < w) out[0] += vi[j] * xi[j];
         }
-        for (; k < w; ++k) out[0] += v[64 * k] * x[c[64 * k]];
     } else {
         const double* v = vals + p0 * (BS * BS) + lane;
         for (int k = 0; k < w; ++k) {
-            const int64_t cc = (int64_t)c[64 * k] * BS;
+            const int64_t cc = (int64_t)ld<int32_t, NT>(c + 64 * k) * BS;
             double xv[BS];
 #pragma unroll
-            for (int j = 0; j < BS; ++j) xv[j] = x[cc + j];
+            for (int j = 0; j < BS; ++j) xv[j] = x(cc + j);
             const double* vk = v + (int64_t)64 * BS * BS * k;
 #pragma unroll
             for (int r = 0; r < BS; ++r)
 #pragma unroll
-                for (int j = 0; j < BS; ++j) out[r] += vk[64 * (r * BS + j)] * xv[j];
+                for (int j = 0; j < BS; ++j) out[r] += ld<double, NT>(vk + 64 * (r * BS + j)) * xv[j];
         }
     }
 }
 
 // XCD-aware slice walk: XCD x (= blockIdx % 8 under the observed round-robin placement; speed only) owns the
-// contiguous slice range [x*spx, (x+1)*spx), walked 4 slices (one per wave) per block step.
+// contiguous slice range [x*spx, (x+1)*spx), walked 4 slices (one per wave) per block step, so the x-gather
+// window of an XCD stays in its own L2.
 struct SliceWalk {
     int64_t s, end, step;
 };
@@ -72,15 +99,18 @@ __device__ __forceinline__ SliceWalk slice_walk(int64_t nslices) {
     return SliceWalk{start + lb * 4 + (threadIdx.x >> 6), end, nlb * 4};
 }
 
-template <int BS>
+constexpr int SPMV_U = 8;   // tools/spmv_tune.py: U=8 beats 4 and 16 on the 10M Poisson matrix (gfx950)
+
+template <int BS, int U = SPMV_U, bool NT = false>
 __global__ void __launch_bounds__(256) k_spmv(int64_t nslices, int64_t nrows, const int64_t* __restrict__ slice_ptr,
                                               const int32_t* __restrict__ cols, const double* __restrict__ vals,
                                               const double* __restrict__ x, double* __restrict__ y) {
     const int lane = threadIdx.x & 63;
     SliceWalk wk = slice_walk(nslices);
+    const VecPlain xv{x};
     for (int64_t s = wk.s; s < wk.end; s += wk.step) {
         double o[BS];
-        sell_row<BS>(s, lane, slice_ptr, cols, vals, x, o);
+        sell_row<BS, U, NT>(s, lane, slice_ptr, cols, vals, xv, o);
         const int64_t row = s * 64 + lane;
         if (row < nrows) {
 #pragma unroll
@@ -93,82 +123,152 @@ __global__ void __launch_bounds__(256) k_spmv(int64_t nslices, int64_t nrows, co
 struct PcgState {
     double rz;        // r.z of the current iterate (rs_old)
     double pq;        // p.Ap of this iteration
-    double alpha, beta;
+    double alpha;     // alpha of this iteration (K1 -> K2)
+    double alpha_x;   // alpha of the last completed update, for the deferred x update (K2 -> next K1 / finish)
+    double beta;      // K2 -> next K1 / K3
     double rz_new;
     double tol, eps;
     int iter;         // completed iterations
     int status;       // FEM_PCG_*
-    int halt;         // 1: solve ended, K1/K2 are no-ops
-    int xupd;         // 1: K2 ran this iteration -> K3 applies x += alpha p
+    int halt;         // 1: solve ended, iteration kernels are no-ops
+    int xupd;         // 3-kernel: K2 ran this iteration -> K3 applies x += alpha p
+    int x_done;       // fused: 0 while an x update is pending (applied by the next K1 or by finish)
     int stop_iter;    // reported iteration of a guard stop (i+1 in the reference prints)
     int max_iter;
     int mode;
-    int pad_;
-    unsigned counter[4];
 };
 
 constexpr int PCG_BLOCK = 256;
-constexpr int MAX_PARTIALS = 4096;
+constexpr int MAX_PARTIALS = 4096;   // >= grid + RED_SHARDS for every reduction kernel
+enum { RED_K1 = 0, RED_K2 = 1, RED_INIT = 2, RED_N = 3 };
 
-template <int BS>
+// alpha and the breakdown guards from p.Ap (`solver/solver.py:185-198` / `:800`)
+__device__ __forceinline__ void finish_pq(PcgState* st, double pq) {
+    st->pq = pq;
+    if (st->mode == FEM_MODE_CG_STABLE) {
+        if (fabs(pq) < st->eps || pq < 0.0) {                 // `solver/solver.py:187`
+            st->status = FEM_PCG_BREAKDOWN;
+            st->halt = 1;
+            st->stop_iter = st->iter + 1;
+        } else {
+            const double a = st->rz / (pq + st->eps);          // `:194`
+            st->alpha = a;
+            if (isnan(a) || isinf(a)) {                        // `:196`
+                st->status = FEM_PCG_ALPHA_NAN;
+                st->halt = 1;
+                st->stop_iter = st->iter + 1;
+            }
+        }
+    } else {
+        st->alpha = st->rz / pq;                              // `:800` (no guards)
+    }
+}
+
+// stop test and beta from the new r.z (`solver/solver.py:208-222` / `:804-809`)
+__device__ __forceinline__ void finish_rz(PcgState* st, double rz_new, double* hist, int64_t hist_len) {
+    const bool cg = st->mode == FEM_MODE_CG_STABLE;
+    const int it = st->iter;
+    st->rz_new = rz_new;
+    st->xupd = 1;
+    st->x_done = 0;
+    st->alpha_x = st->alpha;
+    st->iter = it + 1;
+    const double nrm = sqrt(rz_new);
+    if (hist && it < hist_len) hist[it] = nrm;
+    if (nrm < st->tol) {                                      // `:210` / `:805`
+        st->status = FEM_PCG_CONVERGED;
+        st->halt = 1;
+        st->stop_iter = it + 1;
+    } else {
+        const double b = cg ? rz_new / (st->rz + st->eps) : rz_new / st->rz;   // `:213` / `:808`
+        st->beta = b;
+        if (cg && (isnan(b) || isinf(b))) {                   // `:214`
+            st->status = FEM_PCG_BETA_NAN;
+            st->halt = 1;
+            st->stop_iter = it + 1;
+        }
+        st->rz = rz_new;
+    }
+}
+
+struct RedBuf {
+    double* partials;    // [RED_N][MAX_PARTIALS]
+    unsigned* counters;  // [RED_N][RED_COUNTER_WORDS]
+    __device__ __forceinline__ double* part(int k) const { return partials + k * MAX_PARTIALS; }
+    __device__ __forceinline__ unsigned* cnt(int k) const { return counters + k * RED_COUNTER_WORDS; }
+};
+
+// K1. FUSED: p (in p_buf[iter & 1]) is formed on the fly from r, w and the previous p (p_buf[(iter+1) & 1]);
+// this kernel also applies the deferred x += alpha_x p_prev to its own rows.
+template <int BS, bool FUSED>
 __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_spmv_dot(int64_t nslices, int64_t nrows,
                                                             const int64_t* __restrict__ slice_ptr,
                                                             const int32_t* __restrict__ cols,
-                                                            const double* __restrict__ vals,
-                                                            const double* __restrict__ p, double* __restrict__ q,
-                                                            PcgState* __restrict__ st, double* __restrict__ partials) {
+                                                            const double* __restrict__ vals, double* __restrict__ p0,
+                                                            double* __restrict__ p1, const double* __restrict__ r,
+                                                            const double* __restrict__ w, double* __restrict__ x,
+                                                            double* __restrict__ q, PcgState* __restrict__ st,
+                                                            RedBuf red) {
     __shared__ double lds4[4];
-    __shared__ int last;
-    if (blockIdx.x == 0 && threadIdx.x == 0) st->xupd = 0;
-    if (st->halt || st->iter >= st->max_iter) return;
+    __shared__ int flag;
+    if (!FUSED && blockIdx.x == 0 && threadIdx.x == 0) st->xupd = 0;
+    const int iter = st->iter;
+    if (st->halt || iter >= st->max_iter) return;
     const int lane = threadIdx.x & 63;
     double dot = 0.0;
     SliceWalk wk = slice_walk(nslices);
-    for (int64_t s = wk.s; s < wk.end; s += wk.step) {
-        double o[BS];
-        sell_row<BS>(s, lane, slice_ptr, cols, vals, p, o);
-        const int64_t row = s * 64 + lane;
-        if (row < nrows) {
+    if (FUSED) {
+        double* pnew = (iter & 1) ? p1 : p0;
+        const double* pold = (iter & 1) ? p0 : p1;
+        const double beta = st->beta, ax = st->alpha_x;
+        const VecFusedP pv{r, w, pold, beta};
+        for (int64_t s = wk.s; s < wk.end; s += wk.step) {
+            double o[BS];
+            sell_row<BS, SPMV_U, false>(s, lane, slice_ptr, cols, vals, pv, o);
+            const int64_t row = s * 64 + lane;
+            if (row < nrows) {
 #pragma unroll
-            for (int r = 0; r < BS; ++r) {
-                q[row * BS + r] = o[r];
-                dot += p[row * BS + r] * o[r];
+                for (int c = 0; c < BS; ++c) {
+                    const int64_t i = row * BS + c;
+                    const double po = pold[i];
+                    const double pn = w[i] * r[i] + beta * po;
+                    x[i] += ax * po;
+                    pnew[i] = pn;
+                    q[i] = o[c];
+                    dot += pn * o[c];
+                }
+            }
+        }
+    } else {
+        const VecPlain pv{p0};
+        for (int64_t s = wk.s; s < wk.end; s += wk.step) {
+            double o[BS];
+            sell_row<BS, SPMV_U, false>(s, lane, slice_ptr, cols, vals, pv, o);
+            const int64_t row = s * 64 + lane;
+            if (row < nrows) {
+#pragma unroll
+                for (int c = 0; c < BS; ++c) {
+                    q[row * BS + c] = o[c];
+                    dot += p0[row * BS + c] * o[c];
+                }
             }
         }
     }
     dot = block_sum256(dot, lds4);
-    if (publish_partial(dot, partials, &st->counter[0], &last)) {
-        const double pq = sum_partials(partials, gridDim.x, lds4);
-        if (threadIdx.x == 0) {
-            st->pq = pq;
-            if (st->mode == FEM_MODE_CG_STABLE) {
-                if (fabs(pq) < st->eps || pq < 0.0) {                 // `solver/solver.py:187`
-                    st->status = FEM_PCG_BREAKDOWN;
-                    st->halt = 1;
-                    st->stop_iter = st->iter + 1;
-                } else {
-                    const double a = st->rz / (pq + st->eps);          // `:194`
-                    st->alpha = a;
-                    if (isnan(a) || isinf(a)) {                        // `:196`
-                        st->status = FEM_PCG_ALPHA_NAN;
-                        st->halt = 1;
-                        st->stop_iter = st->iter + 1;
-                    }
-                }
-            } else {
-                st->alpha = st->rz / pq;                              // `:800` (no guards)
-            }
-        }
+    double pq;
+    if (reduce_grid(dot, red.part(RED_K1), red.cnt(RED_K1), &pq, lds4, &flag) && threadIdx.x == 0) {
+        if (FUSED) st->x_done = 1;   // the pending x update was applied above by every block
+        finish_pq(st, pq);
     }
 }
 
 // K2: r <- r - alpha q (CG: masked), z = w r, partial r.z (CG: r.r since w is the 0/1 free mask)
 __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update(int64_t n, double* __restrict__ r,
                                                           const double* __restrict__ q, const double* __restrict__ w,
-                                                          PcgState* __restrict__ st, double* __restrict__ partials,
+                                                          PcgState* __restrict__ st, RedBuf red,
                                                           double* __restrict__ hist, int64_t hist_len) {
     __shared__ double lds4[4];
-    __shared__ int last;
+    __shared__ int flag;
     if (st->halt || st->iter >= st->max_iter) return;
     const double alpha = st->alpha;
     const bool cg = st->mode == FEM_MODE_CG_STABLE;
@@ -197,34 +297,12 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update(int64_t n, double* __r
         acc += rv * (w[i] * rv);
     }
     acc = block_sum256(acc, lds4);
-    if (publish_partial(acc, partials, &st->counter[1], &last)) {
-        const double rz_new = sum_partials(partials, gridDim.x, lds4);
-        if (threadIdx.x == 0) {
-            const int it = st->iter;
-            st->rz_new = rz_new;
-            st->xupd = 1;
-            st->iter = it + 1;
-            const double nrm = sqrt(rz_new);
-            if (hist && it < hist_len) hist[it] = nrm;
-            if (nrm < st->tol) {                                      // `:210` / `:805`
-                st->status = FEM_PCG_CONVERGED;
-                st->halt = 1;
-                st->stop_iter = it + 1;
-            } else {
-                const double b = cg ? rz_new / (st->rz + st->eps) : rz_new / st->rz;   // `:213` / `:808`
-                st->beta = b;
-                if (cg && (isnan(b) || isinf(b))) {                   // `:214`
-                    st->status = FEM_PCG_BETA_NAN;
-                    st->halt = 1;
-                    st->stop_iter = it + 1;
-                }
-                st->rz = rz_new;
-            }
-        }
-    }
+    double rz_new;
+    if (reduce_grid(acc, red.part(RED_K2), red.cnt(RED_K2), &rz_new, lds4, &flag) && threadIdx.x == 0)
+        finish_rz(st, rz_new, hist, hist_len);
 }
 
-// K3: x <- x + alpha p ; p <- w r + beta p (unless stopped in K2)
+// K3 (3-kernel schedule): x <- x + alpha p ; p <- w r + beta p (unless stopped in K2)
 __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_pupdate(int64_t n, double* __restrict__ x, double* __restrict__ p,
                                                            const double* __restrict__ r, const double* __restrict__ w,
                                                            const PcgState* __restrict__ st) {
@@ -255,13 +333,27 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_pupdate(int64_t n, double* __
     }
 }
 
-// start: (CG) x[fixed] = 0; r = b - q (q = A x computed before), (CG) r[fixed] = 0; p = z = w r; rz = r.z
+// fused schedule, end of solve: apply the pending x += alpha_x p_last once
+__global__ void __launch_bounds__(PCG_BLOCK) k_pcg_finish(int64_t n, double* __restrict__ x, const double* __restrict__ p0,
+                                                          const double* __restrict__ p1, const PcgState* __restrict__ st) {
+    if (st->x_done) return;
+    // the last completed iteration (st->iter - 1) wrote its p into p_buf[(st->iter - 1) & 1]
+    const double* p = ((st->iter - 1) & 1) ? p1 : p0;
+    const double a = st->alpha_x;
+    for (int64_t i = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * PCG_BLOCK)
+        x[i] += a * p[i];
+}
+
+__global__ void k_mark_x_done(PcgState* st) { st->x_done = 1; }
+
+// start: (CG) x[fixed] = 0 beforehand; r = b - q (q = A x), (CG) r[fixed] = 0; rz = r.z;
+// 3-kernel: p = z = w r.  fused: both p buffers = 0 and beta = alpha_x = 0, so the first K1 forms p = w r.
 __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_init(int64_t n, const double* __restrict__ b, double* __restrict__ r,
                                                         const double* __restrict__ q, const double* __restrict__ w,
-                                                        double* __restrict__ p, PcgState* __restrict__ st,
-                                                        double* __restrict__ partials) {
+                                                        double* __restrict__ p0, double* __restrict__ p1, int fused,
+                                                        PcgState* __restrict__ st, RedBuf red) {
     __shared__ double lds4[4];
-    __shared__ int last;
+    __shared__ int flag;
     const bool cg = st->mode == FEM_MODE_CG_STABLE;
     double acc = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * PCG_BLOCK) {
@@ -269,14 +361,23 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_init(int64_t n, const double*
         if (cg && w[i] == 0.0) rv = 0.0;
         r[i] = rv;
         const double z = w[i] * rv;
-        p[i] = z;
+        if (fused) {
+            p0[i] = 0.0;
+            p1[i] = 0.0;
+        } else {
+            p0[i] = z;
+        }
         acc += rv * z;
     }
     acc = block_sum256(acc, lds4);
-    if (publish_partial(acc, partials, &st->counter[2], &last)) {
-        const double rz = sum_partials(partials, gridDim.x, lds4);
-        if (threadIdx.x == 0) st->rz = rz;
-    }
+    double rz;
+    if (reduce_grid(acc, red.part(RED_INIT), red.cnt(RED_INIT), &rz, lds4, &flag) && threadIdx.x == 0) st->rz = rz;
+}
+
+// HBM ceiling probe: dst = src, 16 B per lane, grid-stride (the measured "STREAM copy" roof of SURVEY §8(d))
+__global__ void __launch_bounds__(256) k_stream_copy(const double2* __restrict__ src, double2* __restrict__ dst,
+                                                     int64_t n2) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n2; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
 }
 
 __global__ void k_zero_fixed(int64_t n, double* __restrict__ x, const double* __restrict__ w) {
@@ -303,11 +404,13 @@ struct fem_pcg {
     int mode;
     double tol, eps;
     hipStream_t stream;
+    int fused;          // kernel schedule (1 = fused, default)
     // owned device memory
     double* r;
-    double* p;
+    double* p0;
+    double* p1;
     double* q;
-    double* partials;
+    RedBuf red;
     PcgState* st;
     PcgState* st_host;  // pinned
     int grid_spmv, grid_vec;
@@ -317,25 +420,31 @@ struct fem_pcg {
 };
 
 static int launch_spmv_dot(fem_pcg* s) {
-    if (s->bs == 1)
-        hipLaunchKernelGGL(k_pcg_spmv_dot<1>, dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream, s->nslices, s->nrows,
-                           s->slice_ptr, s->cols, s->vals, s->p, s->q, s->st, s->partials);
-    else
-        hipLaunchKernelGGL(k_pcg_spmv_dot<3>, dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream, s->nslices, s->nrows,
-                           s->slice_ptr, s->cols, s->vals, s->p, s->q, s->st, s->partials);
+#define FEM_K1(B, F)                                                                                               \
+    hipLaunchKernelGGL((k_pcg_spmv_dot<B, F>), dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream, s->nslices,      \
+                       s->nrows, s->slice_ptr, s->cols, s->vals, s->p0, s->p1, s->r, s->w, s->x, s->q, s->st, s->red)
+    if (s->bs == 1) {
+        if (s->fused) FEM_K1(1, true);
+        else FEM_K1(1, false);
+    } else {
+        if (s->fused) FEM_K1(3, true);
+        else FEM_K1(3, false);
+    }
+#undef FEM_K1
     FEM_LAUNCHED();
     return FEM_OK;
 }
 
 static int launch_update(fem_pcg* s) {
     hipLaunchKernelGGL(k_pcg_update, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->r, s->q, s->w, s->st,
-                       s->partials + MAX_PARTIALS, s->hist, s->hist_len);
+                       s->red, s->hist, s->hist_len);
     FEM_LAUNCHED();
     return FEM_OK;
 }
 
 static int launch_pupdate(fem_pcg* s) {
-    hipLaunchKernelGGL(k_pcg_pupdate, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->x, s->p, s->r, s->w,
+    if (s->fused) return FEM_OK;
+    hipLaunchKernelGGL(k_pcg_pupdate, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->x, s->p0, s->r, s->w,
                        s->st);
     FEM_LAUNCHED();
     return FEM_OK;
@@ -377,6 +486,48 @@ int fem_spmv(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_t* col
     return FEM_OK;
 }
 
+// tuning entry: SpMV variants (unroll U in {4, 8, 16} x nontemporal matrix loads), grid override
+int fem_spmv_variant(int variant, int grid, int64_t nrows, int bs, const int64_t* slice_ptr, const int32_t* cols,
+                     const double* vals, const double* x, double* y, fem_stream_t stream) {
+    const int64_t ns = cdiv(nrows, 64);
+    if (ns == 0) return FEM_OK;
+    if (grid <= 0) grid = grid_multiple_of_xcd(cdiv(ns, 4), 2048);
+    grid = ((grid + NXCD - 1) / NXCD) * NXCD;
+    hipStream_t st = S(stream);
+#define FEM_SPMV_V(B, U, N) \
+    hipLaunchKernelGGL((k_spmv<B, U, N>), dim3(grid), dim3(256), 0, st, ns, nrows, slice_ptr, cols, vals, x, y)
+    if (bs == 1) {
+        switch (variant) {
+            case 0: FEM_SPMV_V(1, 4, false); break;
+            case 1: FEM_SPMV_V(1, 8, false); break;
+            case 2: FEM_SPMV_V(1, 16, false); break;
+            case 3: FEM_SPMV_V(1, 4, true); break;
+            case 4: FEM_SPMV_V(1, 8, true); break;
+            case 5: FEM_SPMV_V(1, 16, true); break;
+            default: set_error("fem_spmv_variant: unknown variant %d", variant); return FEM_EARG;
+        }
+    } else if (bs == 3) {
+        switch (variant) {
+            case 0: FEM_SPMV_V(3, 8, false); break;
+            case 3: FEM_SPMV_V(3, 8, true); break;
+            default: set_error("fem_spmv_variant: unknown variant %d", variant); return FEM_EARG;
+        }
+    } else {
+        set_error("fem_spmv_variant: block size %d unsupported", bs);
+        return FEM_EARG;
+    }
+#undef FEM_SPMV_V
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_stream_copy(const double* src, double* dst, int64_t n, int grid, fem_stream_t stream) {
+    if (grid <= 0) grid = 2048;
+    hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(256), 0, S(stream), (const double2*)src, (double2*)dst, n / 2);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
 int fem_pcg_create(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_t* cols, const double* vals,
                    const double* b, double* x, const double* w, int mode, double tol, double eps, double* hist,
                    int64_t hist_len, fem_stream_t stream, fem_pcg** out) {
@@ -409,6 +560,7 @@ int fem_pcg_create(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_
     s->tol = tol;
     s->eps = eps;
     s->stream = S(stream);
+    s->fused = 0;   // measured: 3-kernel 0.103 ms/it vs fused 0.121 on 10M Poisson (profiles/)
     s->graph = nullptr;
     s->graph_k = 0;
     s->max_iter = 0x7fffffff;
@@ -417,9 +569,12 @@ int fem_pcg_create(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_
     size_t vec = sizeof(double) * (size_t)(s->n + 2);
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = hipMalloc(&s->r, vec);
-    if (e == hipSuccess) e = hipMalloc(&s->p, vec);
+    if (e == hipSuccess) e = hipMalloc(&s->p0, vec);
+    if (e == hipSuccess) e = hipMalloc(&s->p1, vec);
     if (e == hipSuccess) e = hipMalloc(&s->q, vec);
-    if (e == hipSuccess) e = hipMalloc(&s->partials, sizeof(double) * 3 * MAX_PARTIALS);
+    if (e == hipSuccess) e = hipMalloc(&s->red.partials, sizeof(double) * RED_N * MAX_PARTIALS);
+    if (e == hipSuccess) e = hipMalloc(&s->red.counters, sizeof(unsigned) * RED_N * RED_COUNTER_WORDS);
+    if (e == hipSuccess) e = hipMemset(s->red.counters, 0, sizeof(unsigned) * RED_N * RED_COUNTER_WORDS);
     if (e == hipSuccess) e = hipMalloc(&s->st, sizeof(PcgState));
     if (e == hipSuccess) e = hipHostMalloc(&s->st_host, sizeof(PcgState), hipHostMallocDefault);
     if (e != hipSuccess) {
@@ -431,12 +586,22 @@ int fem_pcg_create(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_
     return FEM_OK;
 }
 
+int fem_pcg_set_schedule(fem_pcg* s, int fused) {
+    if (s->graph) {
+        set_error("fem_pcg_set_schedule: drop the captured graph first (fem_pcg_use_graph(s, 0))");
+        return FEM_EARG;
+    }
+    s->fused = fused ? 1 : 0;
+    return FEM_OK;
+}
+
 int fem_pcg_start(fem_pcg* s) {
     PcgState h{};
     h.tol = s->tol;
     h.eps = s->eps;
     h.mode = s->mode;
     h.max_iter = s->max_iter;
+    h.x_done = 1;
     *s->st_host = h;
     FEM_HIP(hipMemcpyAsync(s->st, s->st_host, sizeof(PcgState), hipMemcpyHostToDevice, s->stream));
     if (s->mode == FEM_MODE_CG_STABLE) {
@@ -445,8 +610,8 @@ int fem_pcg_start(fem_pcg* s) {
     }
     int rc = fem_spmv(s->nrows, s->bs, s->slice_ptr, s->cols, s->vals, s->x, s->q, s->stream);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_pcg_init, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->b, s->r, s->q, s->w, s->p,
-                       s->st, s->partials + 2 * MAX_PARTIALS);
+    hipLaunchKernelGGL(k_pcg_init, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->b, s->r, s->q, s->w, s->p0,
+                       s->p1, s->fused, s->st, s->red);
     FEM_LAUNCHED();
     return FEM_OK;
 }
@@ -458,6 +623,15 @@ int fem_pcg_iterate(fem_pcg* s, int k) {
         return FEM_OK;
     }
     return launch_iterations(s, k);
+}
+
+int fem_pcg_finish(fem_pcg* s) {
+    if (!s->fused) return FEM_OK;
+    hipLaunchKernelGGL(k_pcg_finish, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->x, s->p0, s->p1, s->st);
+    FEM_LAUNCHED();
+    hipLaunchKernelGGL(k_mark_x_done, dim3(1), dim3(1), 0, s->stream, s->st);
+    FEM_LAUNCHED();
+    return FEM_OK;
 }
 
 int fem_pcg_use_graph(fem_pcg* s, int k) {
@@ -528,6 +702,7 @@ int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, 
         if (stt != FEM_PCG_RUNNING) break;
         if (chunk < 256) chunk *= 2;   // poll less often once the solve is clearly long
     }
+    if ((rc = fem_pcg_finish(s))) return rc;
     if ((rc = fem_pcg_poll(s, &it, &stt, rz))) return rc;
     if (iters) *iters = it;
     if (status) *status = stt;
@@ -536,7 +711,7 @@ int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, 
 
 int fem_pcg_profile(fem_pcg* s, int k, int every, double* ms, int* n) {
     // k iterations enqueued on the solver stream; iterations i % every == 0 are bracketed by hip events
-    // around each of the three kernels (on the stream the kernels run on), the others launch bare.
+    // around each of their kernels (on the stream the kernels run on), the others launch bare.
     if (every < 1) every = 1;
     double acc[3] = {0, 0, 0};
     int rc = FEM_OK;
@@ -578,9 +753,11 @@ void fem_pcg_destroy(fem_pcg* s) {
     if (!s) return;
     if (s->graph) (void)hipGraphExecDestroy(s->graph);
     if (s->r) (void)hipFree(s->r);
-    if (s->p) (void)hipFree(s->p);
+    if (s->p0) (void)hipFree(s->p0);
+    if (s->p1) (void)hipFree(s->p1);
     if (s->q) (void)hipFree(s->q);
-    if (s->partials) (void)hipFree(s->partials);
+    if (s->red.partials) (void)hipFree(s->red.partials);
+    if (s->red.counters) (void)hipFree(s->red.counters);
     if (s->st) (void)hipFree(s->st);
     if (s->st_host) (void)hipHostFree(s->st_host);
     delete s;

@@ -204,7 +204,7 @@ class SellMatrix:
 
     # ---------------------------------------------------------------- solver
     def pcg(self, b, x0=None, w=None, mode=C.MODE_PCG, tol=1e-8, max_iter=1000, eps=1e-30, history=False,
-            chunk=32):
+            chunk=32, fused=False):
         """Run the device (P)CG; returns (x, iterations, status, rz_last, hist or None)."""
         lib = C.lib()
         b = b.to(F64).contiguous().view(-1)
@@ -218,6 +218,7 @@ class SellMatrix:
                                    C.ptr(hist), hist.numel() if hist is not None else 0, C.stream(self.device),
                                    ctypes.byref(h)), "fem_pcg_create")
         try:
+            C.check(lib.fem_pcg_set_schedule(h, 1 if fused else 0), "fem_pcg_set_schedule")
             it, stt, rz = ctypes.c_int(), ctypes.c_int(), ctypes.c_double()
             C.check(lib.fem_pcg_solve(h, int(max_iter), int(chunk), ctypes.byref(it), ctypes.byref(stt),
                                       ctypes.byref(rz)), "fem_pcg_solve")
@@ -233,17 +234,25 @@ class SellMatrix:
 class PcgRunner:
     """Persistent (P)CG context for fixed-iteration timing (bench.py): start once, iterate k, poll."""
 
-    def __init__(self, A: SellMatrix, b, w, x0=None, mode=C.MODE_PCG, tol=0.0, eps=1e-30):
+    def __init__(self, A: SellMatrix, b, w, x0=None, mode=C.MODE_PCG, tol=0.0, eps=1e-30, fused=False):
         self.lib = C.lib()
         self.A = A
         self.b = b.to(F64).contiguous().view(-1)
         self.w = w.to(F64).contiguous().view(-1)
         self.x = (torch.zeros(A.n, dtype=F64, device=A.device) if x0 is None
                   else x0.to(F64).clone().contiguous().view(-1))
+        # a dedicated stream: hipGraph capture is not allowed on the legacy default stream
+        self.stream = torch.cuda.Stream(device=A.device)
+        self.stream.wait_stream(torch.cuda.current_stream(A.device))
         self.h = ctypes.c_void_p()
         C.check(self.lib.fem_pcg_create(A.g.n_nodes, A.bs, C.ptr(A.g.slice_ptr), C.ptr(A.g.cols), C.ptr(A.vals),
                                         C.ptr(self.b), C.ptr(self.x), C.ptr(self.w), mode, float(tol), float(eps),
-                                        None, 0, C.stream(A.device), ctypes.byref(self.h)), "fem_pcg_create")
+                                        None, 0, ctypes.c_void_p(self.stream.cuda_stream), ctypes.byref(self.h)),
+                "fem_pcg_create")
+        C.check(self.lib.fem_pcg_set_schedule(self.h, 1 if fused else 0), "fem_pcg_set_schedule")
+
+    def finish(self):
+        C.check(self.lib.fem_pcg_finish(self.h), "fem_pcg_finish")
 
     def start(self):
         C.check(self.lib.fem_pcg_start(self.h), "fem_pcg_start")

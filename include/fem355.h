@@ -163,6 +163,11 @@ int fem_invert_diag(const double* in, int64_t n, double* out, fem_stream_t strea
  * y = A x on the SELL-64 matrix (nrows block rows of size bs). */
 int fem_spmv(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_t* cols, const double* vals,
              const double* x, double* y, fem_stream_t stream);
+/* tuning / measurement entry points (tools/spmv_tune.py): SpMV code variants and grid size (grid <= 0:
+ * default), and the HBM copy-ceiling probe dst = src over n doubles (n even, 16-byte aligned). */
+int fem_spmv_variant(int variant, int grid, int64_t nrows, int bs, const int64_t* slice_ptr, const int32_t* cols,
+                     const double* vals, const double* x, double* y, fem_stream_t stream);
+int fem_stream_copy(const double* src, double* dst, int64_t n, int grid, fem_stream_t stream);
 
 /* ------------------------------------------------------------------ (P)CG (L3)
  * One solve context over a SELL matrix. The whole iteration runs on the device: SpMV + p.q reduction,
@@ -188,6 +193,11 @@ int fem_pcg_poll(fem_pcg* s, int* iters, int* status, double* rz);
 int fem_pcg_scalars(fem_pcg* s, double* out6);
 /* [sync] run to completion: start + chunks of `chunk` iterations until stop or max_iter */
 int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, double* rz);
+/* kernel schedule: 0 = 3-kernel (default, faster on gfx950), 1 = fused (p formed inside the SpMV from r, w and
+ * the previous p at every gathered column; 2 kernels per iteration, 88n instead of 96n vector bytes) */
+int fem_pcg_set_schedule(fem_pcg* s, int fused);
+/* apply the deferred x update of the fused schedule after the last iteration (fem_pcg_solve does this) */
+int fem_pcg_finish(fem_pcg* s);
 /* capture `k` iterations in a hipGraph and use it for fem_pcg_iterate calls with that k (0 disables) */
 int fem_pcg_use_graph(fem_pcg* s, int k);
 /* [sync] enqueue k iterations like fem_pcg_iterate, bracketing every `every`-th iteration's three kernels

@@ -232,6 +232,31 @@ def test_cg_guard_breakdown(gpu, capsys):
     assert float(u.abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("kind", ["poisson", "elastic"])
+def test_fused_and_three_kernel_schedules_agree(gpu, kind):
+    _, mesh, solver, system = _mods()
+    c, t = mesh.kuhn_cube(7, jitter=0.1)
+    if kind == "poisson":
+        f, fixed = mesh.cube_poisson_case(c)
+    else:
+        f, fixed = mesh.cube_elasticity_case(c)
+    A = system.assemble_tet4_system(c.to(gpu), t.to(gpu), kind, 1.0 if kind == "poisson" else E, NU)
+    mask = torch.zeros((c.shape[0], A.bs), dtype=torch.uint8, device=gpu)
+    mask[fixed.to(gpu)] = 1
+    w = A.jacobi(mask.view(-1))
+    b = f.to(gpu).reshape(-1)
+    tol = 1e-9 * float(torch.sqrt(torch.dot(b, w * b)))
+    r1 = A.pcg(b, w=w, tol=tol, max_iter=2000, fused=True)
+    r0 = A.pcg(b, w=w, tol=tol, max_iter=2000, fused=False)
+    assert r1.status == r0.status == 1 and abs(r1.iterations - r0.iterations) <= 1
+    assert rel(r1.x, r0.x) < 1e-10
+    # CG mode, fixed max_iter (the deferred x update of the fused schedule is applied at the end)
+    wm = (mask.view(-1) == 0).to(F64)
+    c1 = A.pcg(b, w=wm, mode=0, tol=0.0, max_iter=25, fused=True)
+    c0 = A.pcg(b, w=wm, mode=0, tol=0.0, max_iter=25, fused=False)
+    assert c1.iterations == c0.iterations == 25 and rel(c1.x, c0.x) < 1e-12
+
+
 def test_pcg_history_and_fixed_iterations(gpu):
     _, mesh, solver, system = _mods()
     c, t = mesh.kuhn_cube(8)
