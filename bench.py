@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", type=int, default=0, help="capture k iterations per hipGraph (0 = plain launches)")
+    ap.add_argument("--force-dist", action="store_true", help="run the RCCL element-partitioned path even at N=1")
     return ap.parse_args()
 
 
@@ -90,7 +91,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 or a.force_dist:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("WORLD_SIZE", str(world))
+        os.environ.setdefault("RANK", str(rank))
         from fem355 import dist
         return dist.bench_main(a, METRIC)
     torch.cuda.set_device(local)

@@ -64,6 +64,19 @@ SIGNATURES = {
     "fem_pcg_finish": (_I, [_P]),
     "fem_pcg_profile": (_I, [_P, _I, _I, ctypes.POINTER(_D), ctypes.POINTER(_I)]),
     "fem_pcg_destroy": (None, [_P]),
+    "fem_sell_diag": (_I, [_P, _I, _P, _P, _L, _P, _P]),
+    "fem_jacobi_from_diag": (_I, [_P, _L, _P, _P, _P]),
+    "fem_comm_unique_id": (_I, [ctypes.c_char_p]),
+    "fem_comm_init": (_I, [_I, _I, ctypes.c_char_p, ctypes.POINTER(_P)]),
+    "fem_comm_destroy": (_I, [_P]),
+    "fem_allreduce_sum": (_I, [_P, _P, _L, _P]),
+    "fem_halo_sum": (_I, [_P, _P, _I, _P, _L, _P, _L, _P, _P]),
+    "fem_halo_pack": (_I, [_P, _I, _P, _L, _P, _P]),
+    "fem_halo_unpack": (_I, [_P, _I, _P, _L, _P, _P]),
+    "fem_pcg_set_dist": (_I, [_P, _I, _P, _L, _P, _P, _P]),
+    "fem_pcg_dist_phase": (_I, [_P, _I]),
+    "fem_pcg_dist_buffer": (_I, [_P, _I, ctypes.POINTER(_P), ctypes.POINTER(_L)]),
+    "fem_group_allreduce": (_I, [_P, _I, _L, _P]),
 }
 
 _lib = None

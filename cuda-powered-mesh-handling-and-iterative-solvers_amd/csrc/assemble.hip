@@ -426,6 +426,26 @@ __global__ void k_jacobi(const double* __restrict__ vals, int bs, const int32_t*
     }
 }
 
+__global__ void k_sell_diag(const double* __restrict__ vals, int bs, const int32_t* __restrict__ diagpos,
+                            const int64_t* __restrict__ csr2sell, int64_t nrows, double* __restrict__ out) {
+    const int64_t n = nrows * bs;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t node = i / bs;
+        const int r = (int)(i - node * bs);
+        out[i] = vals[sell_val(csr2sell[diagpos[node]], bs * bs, r * bs + r)];
+    }
+}
+
+__global__ void k_jacobi_from_diag(const double* __restrict__ d, int64_t n, const uint8_t* __restrict__ mask,
+                                   double* __restrict__ w) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        double v = 1.0 / d[i];
+        if (v == INFINITY) v = 0.0;
+        if (mask && mask[i]) v = 0.0;
+        w[i] = v;
+    }
+}
+
 // ---------------------------------------------------------------- element-by-element operator
 template <int DPN>
 __global__ void __launch_bounds__(256) k_ebe_apply(const double* __restrict__ Ke, const int64_t* __restrict__ conn,
@@ -608,6 +628,20 @@ int fem_jacobi(const double* vals, int bs, const int32_t* rowptr, const int32_t*
     (void)slice_ptr;
     hipLaunchKernelGGL(k_jacobi, dim3(stream_grid(nrows * bs, 256)), dim3(256), 0, S(stream), vals, bs, diagpos,
                        csr2sell, nrows, mask, w);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_sell_diag(const double* vals, int bs, const int32_t* diagpos, const int64_t* csr2sell, int64_t nrows,
+                  double* diag, fem_stream_t stream) {
+    hipLaunchKernelGGL(k_sell_diag, dim3(stream_grid(nrows * bs, 256)), dim3(256), 0, S(stream), vals, bs, diagpos,
+                       csr2sell, nrows, diag);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_jacobi_from_diag(const double* diag, int64_t n, const uint8_t* mask, double* w, fem_stream_t stream) {
+    hipLaunchKernelGGL(k_jacobi_from_diag, dim3(stream_grid(n, 256)), dim3(256), 0, S(stream), diag, n, mask, w);
     FEM_LAUNCHED();
     return FEM_OK;
 }

@@ -13,6 +13,9 @@
 //                           (double-buffered p), q = A p, p.q
 //             K2 update   (as above)                          -> 2 launches and 88 n bytes of vectors per iteration
 // Grid reductions are deterministic two-level trees (common.hpp reduce_grid).
+#include <rccl/rccl.h>
+#include <stddef.h>
+
 #include <vector>
 
 #include "common.hpp"
@@ -136,6 +139,8 @@ struct PcgState {
     int stop_iter;    // reported iteration of a guard stop (i+1 in the reference prints)
     int max_iter;
     int mode;
+    int dist;         // 1: element-partitioned; reductions land in red[] and are all-reduced (RCCL) first
+    double red[4];    // dist: rank-local partial sums p.q, r.z, r0.z0 (all-reduced in place)
 };
 
 constexpr int PCG_BLOCK = 256;
@@ -200,7 +205,7 @@ struct RedBuf {
 
 // K1. FUSED: p (in p_buf[iter & 1]) is formed on the fly from r, w and the previous p (p_buf[(iter+1) & 1]);
 // this kernel also applies the deferred x += alpha_x p_prev to its own rows.
-template <int BS, bool FUSED>
+template <int BS, bool FUSED, bool DOT = true>
 __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_spmv_dot(int64_t nslices, int64_t nrows,
                                                             const int64_t* __restrict__ slice_ptr,
                                                             const int32_t* __restrict__ cols,
@@ -249,11 +254,12 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_spmv_dot(int64_t nslices, int
 #pragma unroll
                 for (int c = 0; c < BS; ++c) {
                     q[row * BS + c] = o[c];
-                    dot += p0[row * BS + c] * o[c];
+                    if (DOT) dot += p0[row * BS + c] * o[c];
                 }
             }
         }
     }
+    if (!DOT) return;   // distributed: q is partial on interface rows; p.q is formed after the halo sum
     dot = block_sum256(dot, lds4);
     double pq;
     if (reduce_grid(dot, red.part(RED_K1), red.cnt(RED_K1), &pq, lds4, &flag) && threadIdx.x == 0) {
@@ -263,10 +269,12 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_spmv_dot(int64_t nslices, int
 }
 
 // K2: r <- r - alpha q (CG: masked), z = w r, partial r.z (CG: r.r since w is the 0/1 free mask)
+// own (distributed only, else null): 1 on the rows (nodes) this rank owns, so shared dofs count once in r.z
 __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update(int64_t n, double* __restrict__ r,
                                                           const double* __restrict__ q, const double* __restrict__ w,
                                                           PcgState* __restrict__ st, RedBuf red,
-                                                          double* __restrict__ hist, int64_t hist_len) {
+                                                          double* __restrict__ hist, int64_t hist_len,
+                                                          const uint8_t* __restrict__ own, int bs) {
     __shared__ double lds4[4];
     __shared__ int flag;
     if (st->halt || st->iter >= st->max_iter) return;
@@ -286,20 +294,27 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update(int64_t n, double* __r
             if (wv.y == 0.0) rv.y = 0.0;
         }
         r2[i] = rv;
-        acc += rv.x * (wv.x * rv.x);
-        acc += rv.y * (wv.y * rv.y);
+        if (own) {
+            if (own[(2 * i) / bs]) acc += rv.x * (wv.x * rv.x);
+            if (own[(2 * i + 1) / bs]) acc += rv.y * (wv.y * rv.y);
+        } else {
+            acc += rv.x * (wv.x * rv.x);
+            acc += rv.y * (wv.y * rv.y);
+        }
     }
     if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
         int64_t i = n - 1;
         double rv = r[i] - alpha * q[i];
         if (cg && w[i] == 0.0) rv = 0.0;
         r[i] = rv;
-        acc += rv * (w[i] * rv);
+        if (!own || own[i / bs]) acc += rv * (w[i] * rv);
     }
     acc = block_sum256(acc, lds4);
     double rz_new;
-    if (reduce_grid(acc, red.part(RED_K2), red.cnt(RED_K2), &rz_new, lds4, &flag) && threadIdx.x == 0)
-        finish_rz(st, rz_new, hist, hist_len);
+    if (reduce_grid(acc, red.part(RED_K2), red.cnt(RED_K2), &rz_new, lds4, &flag) && threadIdx.x == 0) {
+        if (st->dist) st->red[1] = rz_new;   // all-reduced, then k_fin_rz
+        else finish_rz(st, rz_new, hist, hist_len);
+    }
 }
 
 // K3 (3-kernel schedule): x <- x + alpha p ; p <- w r + beta p (unless stopped in K2)
@@ -351,7 +366,8 @@ __global__ void k_mark_x_done(PcgState* st) { st->x_done = 1; }
 __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_init(int64_t n, const double* __restrict__ b, double* __restrict__ r,
                                                         const double* __restrict__ q, const double* __restrict__ w,
                                                         double* __restrict__ p0, double* __restrict__ p1, int fused,
-                                                        PcgState* __restrict__ st, RedBuf red) {
+                                                        PcgState* __restrict__ st, RedBuf red,
+                                                        const uint8_t* __restrict__ own, int bs) {
     __shared__ double lds4[4];
     __shared__ int flag;
     const bool cg = st->mode == FEM_MODE_CG_STABLE;
@@ -367,12 +383,72 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_init(int64_t n, const double*
         } else {
             p0[i] = z;
         }
-        acc += rv * z;
+        if (!own || own[i / bs]) acc += rv * z;
     }
     acc = block_sum256(acc, lds4);
     double rz;
-    if (reduce_grid(acc, red.part(RED_INIT), red.cnt(RED_INIT), &rz, lds4, &flag) && threadIdx.x == 0) st->rz = rz;
+    if (reduce_grid(acc, red.part(RED_INIT), red.cnt(RED_INIT), &rz, lds4, &flag) && threadIdx.x == 0) {
+        if (st->dist) st->red[2] = rz;
+        else st->rz = rz;
+    }
 }
+
+// ---------------------------------------------------------------- distributed halo exchange + scalar finishing
+// Interface dofs (nodes shared by several ranks' elements) carry rank-partial sums after the local SpMV. Every
+// rank packs its partials into the compact global interface vector (zeros where it has no copy), RCCL sums it
+// over the ranks, and every rank reads the full sums back: q is then identical on all copies of a node.
+__device__ __forceinline__ bool halted(const PcgState* st) { return st && (st->halt || st->iter >= st->max_iter); }
+
+__global__ void __launch_bounds__(256) k_halo_pack(const double* __restrict__ v, int bs, const int32_t* __restrict__ map,
+                                                   int64_t nI, double* __restrict__ buf, const PcgState* __restrict__ st) {
+    if (halted(st)) return;
+    for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < nI * bs; t += (int64_t)gridDim.x * 256) {
+        const int64_t j = t / bs;
+        const int c = (int)(t - j * bs);
+        const int32_t l = map[j];
+        buf[t] = (l >= 0) ? v[(int64_t)l * bs + c] : 0.0;
+    }
+}
+
+// v[i] <- halo sum on interface rows; DOT: partial of p.v over owned rows -> st->red[slot]
+template <bool DOT>
+__global__ void __launch_bounds__(PCG_BLOCK) k_halo_unpack(int64_t nloc, int bs, const int32_t* __restrict__ pos,
+                                                           const double* __restrict__ buf, double* __restrict__ v,
+                                                           const double* __restrict__ p, const uint8_t* __restrict__ own,
+                                                           PcgState* __restrict__ st, RedBuf red, int slot) {
+    __shared__ double lds4[4];
+    __shared__ int flag;
+    if (halted(st)) return;
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; i < nloc * bs; i += (int64_t)gridDim.x * PCG_BLOCK) {
+        const int64_t node = i / bs;
+        const int32_t j = pos[node];
+        double vi;
+        if (j >= 0) {
+            vi = buf[(int64_t)j * bs + (i - node * bs)];
+            v[i] = vi;
+        } else {
+            vi = v[i];
+        }
+        if (DOT && own[node]) acc += p[i] * vi;
+    }
+    if (!DOT) return;
+    acc = block_sum256(acc, lds4);
+    double tot;
+    if (reduce_grid(acc, red.part(slot), red.cnt(slot), &tot, lds4, &flag) && threadIdx.x == 0) st->red[0] = tot;
+}
+
+__global__ void k_fin_pq(PcgState* st) {
+    if (halted(st)) return;
+    finish_pq(st, st->red[0]);
+}
+
+__global__ void k_fin_rz(PcgState* st, double* hist, int64_t hist_len) {
+    if (halted(st)) return;
+    finish_rz(st, st->red[1], hist, hist_len);
+}
+
+__global__ void k_set_rz(PcgState* st) { st->rz = st->red[2]; }
 
 // HBM ceiling probe: dst = src, 16 B per lane, grid-stride (the measured "STREAM copy" roof of SURVEY §8(d))
 __global__ void __launch_bounds__(256) k_stream_copy(const double2* __restrict__ src, double2* __restrict__ dst,
@@ -417,18 +493,43 @@ struct fem_pcg {
     hipGraphExec_t graph;
     int graph_k;
     int max_iter;       // device-side iteration cap armed by fem_pcg_start
+    // distributed (element-partitioned) mode: dist = 1; exchanges by RCCL on `comm`, or (comm == NULL) by the
+    // caller between fem_pcg_dist_phase calls (single-process multi-partition validation)
+    int dist;
+    ncclComm_t comm;
+    int64_t nI;         // global interface nodes
+    const int32_t* imap;  // [nI] local row of interface node j on this rank, -1 if absent
+    const int32_t* ipos;  // [nrows] interface index of a local row, -1 for interior rows
+    const uint8_t* own;   // [nrows] 1 where this rank owns the node (lowest rank touching it)
+    double* hbuf;         // [nI * bs] compact interface vector
 };
 
+#define FEM_NCCL(call)                                                                         \
+    do {                                                                                       \
+        ncclResult_t _r = (call);                                                              \
+        if (_r != ncclSuccess) {                                                               \
+            ::fem::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #call, ncclGetErrorString(_r)); \
+            return FEM_ERCCL;                                                                  \
+        }                                                                                      \
+    } while (0)
+
+static double* st_red(fem_pcg* s, int k) {
+    return reinterpret_cast<double*>(reinterpret_cast<char*>(s->st) + offsetof(PcgState, red)) + k;
+}
+
 static int launch_spmv_dot(fem_pcg* s) {
-#define FEM_K1(B, F)                                                                                               \
-    hipLaunchKernelGGL((k_pcg_spmv_dot<B, F>), dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream, s->nslices,      \
+#define FEM_K1(B, F, D)                                                                                            \
+    hipLaunchKernelGGL((k_pcg_spmv_dot<B, F, D>), dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream, s->nslices,   \
                        s->nrows, s->slice_ptr, s->cols, s->vals, s->p0, s->p1, s->r, s->w, s->x, s->q, s->st, s->red)
-    if (s->bs == 1) {
-        if (s->fused) FEM_K1(1, true);
-        else FEM_K1(1, false);
+    if (s->dist) {
+        if (s->bs == 1) FEM_K1(1, false, false);
+        else FEM_K1(3, false, false);
+    } else if (s->bs == 1) {
+        if (s->fused) FEM_K1(1, true, true);
+        else FEM_K1(1, false, true);
     } else {
-        if (s->fused) FEM_K1(3, true);
-        else FEM_K1(3, false);
+        if (s->fused) FEM_K1(3, true, true);
+        else FEM_K1(3, false, true);
     }
 #undef FEM_K1
     FEM_LAUNCHED();
@@ -437,7 +538,110 @@ static int launch_spmv_dot(fem_pcg* s) {
 
 static int launch_update(fem_pcg* s) {
     hipLaunchKernelGGL(k_pcg_update, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->r, s->q, s->w, s->st,
-                       s->red, s->hist, s->hist_len);
+                       s->red, s->hist, s->hist_len, s->dist ? s->own : nullptr, s->bs);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+static int launch_pupdate(fem_pcg* s);
+
+// ---------------------------------------------------------------- distributed iteration, phase by phase
+// iteration : [0] K1 (local A p) + pack q  | sum hbuf  | [1] unpack q + p.q (owned)     | sum red[0]
+//             [2] alpha (k_fin_pq) + K2    | sum red[1]| [3] beta/stop (k_fin_rz) + K3
+// start     : [10] (CG: x[fixed]=0) A x + pack | sum hbuf | [11] unpack + r0, r0.z0 | sum red[2] | [12] rz
+static int halo_pack(fem_pcg* s, const double* v, bool guarded) {
+    hipLaunchKernelGGL(k_halo_pack, dim3(stream_grid(s->nI * s->bs, 256)), dim3(256), 0, s->stream, v, s->bs, s->imap,
+                       s->nI, s->hbuf, guarded ? (const PcgState*)s->st : nullptr);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+static int dist_phase(fem_pcg* s, int phase) {
+    int rc = FEM_OK;
+    switch (phase) {
+        case 0:
+            if ((rc = launch_spmv_dot(s))) return rc;
+            return halo_pack(s, s->q, true);
+        case 1:
+            hipLaunchKernelGGL(k_halo_unpack<true>, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->nrows, s->bs,
+                               s->ipos, s->hbuf, s->q, s->p0, s->own, s->st, s->red, (int)RED_K1);
+            FEM_LAUNCHED();
+            return FEM_OK;
+        case 2:
+            hipLaunchKernelGGL(k_fin_pq, dim3(1), dim3(1), 0, s->stream, s->st);
+            FEM_LAUNCHED();
+            return launch_update(s);
+        case 3:
+            hipLaunchKernelGGL(k_fin_rz, dim3(1), dim3(1), 0, s->stream, s->st, s->hist, s->hist_len);
+            FEM_LAUNCHED();
+            return launch_pupdate(s);
+        case 10:
+            if (s->mode == FEM_MODE_CG_STABLE) {
+                hipLaunchKernelGGL(k_zero_fixed, dim3(stream_grid(s->n, 256)), dim3(256), 0, s->stream, s->n, s->x,
+                                   s->w);
+                FEM_LAUNCHED();
+            }
+            if ((rc = fem_spmv(s->nrows, s->bs, s->slice_ptr, s->cols, s->vals, s->x, s->q, s->stream))) return rc;
+            return halo_pack(s, s->q, false);
+        case 11:
+            hipLaunchKernelGGL(k_halo_unpack<false>, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->nrows, s->bs,
+                               s->ipos, s->hbuf, s->q, s->p0, s->own, (PcgState*)nullptr, s->red, (int)RED_K1);
+            FEM_LAUNCHED();
+            hipLaunchKernelGGL(k_pcg_init, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->b, s->r, s->q,
+                               s->w, s->p0, s->p1, 0, s->st, s->red, s->own, s->bs);
+            FEM_LAUNCHED();
+            return FEM_OK;
+        case 12:
+            hipLaunchKernelGGL(k_set_rz, dim3(1), dim3(1), 0, s->stream, s->st);
+            FEM_LAUNCHED();
+            return FEM_OK;
+        default:
+            set_error("dist_phase: unknown phase %d", phase);
+            return FEM_EARG;
+    }
+}
+
+// device buffer summed over the ranks after `phase`
+static void dist_buffer(fem_pcg* s, int phase, double** ptr, int64_t* n) {
+    *ptr = nullptr;
+    *n = 0;
+    if (phase == 0 || phase == 10) {
+        *ptr = s->hbuf;
+        *n = s->nI * s->bs;
+    } else if (phase == 1) {
+        *ptr = st_red(s, 0);
+        *n = 1;
+    } else if (phase == 2) {
+        *ptr = st_red(s, 1);
+        *n = 1;
+    } else if (phase == 11) {
+        *ptr = st_red(s, 2);
+        *n = 1;
+    }
+}
+
+static int dist_exchange(fem_pcg* s, int phase) {
+    double* p;
+    int64_t n;
+    dist_buffer(s, phase, &p, &n);
+    if (n <= 0) return FEM_OK;
+    if (!s->comm) {
+        set_error("distributed PCG without a communicator: drive it with fem_pcg_dist_phase");
+        return FEM_EARG;
+    }
+    FEM_NCCL(ncclAllReduce(p, p, (size_t)n, ncclFloat64, ncclSum, s->comm, s->stream));
+    return FEM_OK;
+}
+
+// the parts of one distributed iteration after the local SpMV (for fem_pcg_profile's kernel buckets)
+static int launch_exchange_dot(fem_pcg* s) {
+    if (!s->dist) return FEM_OK;
+    int rc;
+    if ((rc = halo_pack(s, s->q, true))) return rc;
+    if ((rc = dist_exchange(s, 0))) return rc;
+    if ((rc = dist_phase(s, 1))) return rc;
+    if ((rc = dist_exchange(s, 1))) return rc;
+    hipLaunchKernelGGL(k_fin_pq, dim3(1), dim3(1), 0, s->stream, s->st);
     FEM_LAUNCHED();
     return FEM_OK;
 }
@@ -450,11 +654,27 @@ static int launch_pupdate(fem_pcg* s) {
     return FEM_OK;
 }
 
+// K2, and in the distributed mode the r.z all-reduce and the stop test / beta that follow it
+static int launch_update_finish(fem_pcg* s) {
+    int rc;
+    if ((rc = launch_update(s))) return rc;
+    if (!s->dist) return FEM_OK;
+    if ((rc = dist_exchange(s, 2))) return rc;
+    hipLaunchKernelGGL(k_fin_rz, dim3(1), dim3(1), 0, s->stream, s->st, s->hist, s->hist_len);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
 static int launch_iterations(fem_pcg* s, int k) {
+    if (s->dist && !s->comm) {
+        set_error("distributed PCG without a communicator: drive it with fem_pcg_dist_phase");
+        return FEM_EARG;
+    }
     for (int i = 0; i < k; ++i) {
         int rc;
         if ((rc = launch_spmv_dot(s))) return rc;
-        if ((rc = launch_update(s))) return rc;
+        if ((rc = launch_exchange_dot(s))) return rc;
+        if ((rc = launch_update_finish(s))) return rc;
         if ((rc = launch_pupdate(s))) return rc;
     }
     return FEM_OK;
@@ -591,6 +811,10 @@ int fem_pcg_set_schedule(fem_pcg* s, int fused) {
         set_error("fem_pcg_set_schedule: drop the captured graph first (fem_pcg_use_graph(s, 0))");
         return FEM_EARG;
     }
+    if (fused && s->comm) {
+        set_error("fem_pcg_set_schedule: the distributed path runs the 3-kernel schedule");
+        return FEM_EARG;
+    }
     s->fused = fused ? 1 : 0;
     return FEM_OK;
 }
@@ -602,16 +826,124 @@ int fem_pcg_start(fem_pcg* s) {
     h.mode = s->mode;
     h.max_iter = s->max_iter;
     h.x_done = 1;
+    h.dist = s->dist;
     *s->st_host = h;
     FEM_HIP(hipMemcpyAsync(s->st, s->st_host, sizeof(PcgState), hipMemcpyHostToDevice, s->stream));
+    int rc;
+    if (s->dist) {
+        if (!s->comm) return FEM_OK;   // phase-driven by the caller from phase 10 on
+        if ((rc = dist_phase(s, 10)) || (rc = dist_exchange(s, 10)) || (rc = dist_phase(s, 11)) ||
+            (rc = dist_exchange(s, 11)) || (rc = dist_phase(s, 12)))
+            return rc;
+        return FEM_OK;
+    }
     if (s->mode == FEM_MODE_CG_STABLE) {
         hipLaunchKernelGGL(k_zero_fixed, dim3(stream_grid(s->n, 256)), dim3(256), 0, s->stream, s->n, s->x, s->w);
         FEM_LAUNCHED();
     }
-    int rc = fem_spmv(s->nrows, s->bs, s->slice_ptr, s->cols, s->vals, s->x, s->q, s->stream);
-    if (rc) return rc;
+    if ((rc = fem_spmv(s->nrows, s->bs, s->slice_ptr, s->cols, s->vals, s->x, s->q, s->stream))) return rc;
     hipLaunchKernelGGL(k_pcg_init, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->b, s->r, s->q, s->w, s->p0,
-                       s->p1, s->fused, s->st, s->red);
+                       s->p1, s->fused, s->st, s->red, (const uint8_t*)nullptr, s->bs);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_pcg_dist_phase(fem_pcg* s, int phase) {
+    if (!s->dist) {
+        set_error("fem_pcg_dist_phase: context is not in distributed mode");
+        return FEM_EARG;
+    }
+    return dist_phase(s, phase);
+}
+
+int fem_pcg_dist_buffer(fem_pcg* s, int phase, double** ptr, int64_t* n) {
+    dist_buffer(s, phase, ptr, n);
+    return FEM_OK;
+}
+
+// ---------------------------------------------------------------- RCCL bootstrap + distributed setup
+int fem_comm_unique_id(char* out128) {
+    ncclUniqueId id;
+    FEM_NCCL(ncclGetUniqueId(&id));
+    memcpy(out128, id.internal, sizeof(id.internal));
+    return FEM_OK;
+}
+
+int fem_comm_init(int nranks, int rank, const char* id128, void** comm) {
+    ncclUniqueId id;
+    memcpy(id.internal, id128, sizeof(id.internal));
+    ncclComm_t c;
+    FEM_NCCL(ncclCommInitRank(&c, nranks, id, rank));
+    *comm = c;
+    return FEM_OK;
+}
+
+int fem_comm_destroy(void* comm) {
+    if (comm) FEM_NCCL(ncclCommDestroy((ncclComm_t)comm));
+    return FEM_OK;
+}
+
+int fem_allreduce_sum(void* comm, double* buf, int64_t n, fem_stream_t stream) {
+    FEM_NCCL(ncclAllReduce(buf, buf, (size_t)n, ncclFloat64, ncclSum, (ncclComm_t)comm, S(stream)));
+    return FEM_OK;
+}
+
+int fem_halo_pack(const double* v, int bs, const int32_t* imap, int64_t nI, double* buf, fem_stream_t stream) {
+    if (nI <= 0) return FEM_OK;
+    hipLaunchKernelGGL(k_halo_pack, dim3(stream_grid(nI * bs, 256)), dim3(256), 0, S(stream), v, bs, imap, nI, buf,
+                       (const PcgState*)nullptr);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_halo_unpack(double* v, int bs, const int32_t* ipos, int64_t nrows, const double* buf, fem_stream_t stream) {
+    RedBuf none{nullptr, nullptr};
+    hipLaunchKernelGGL(k_halo_unpack<false>, dim3(stream_grid(nrows * bs, PCG_BLOCK)), dim3(PCG_BLOCK), 0, S(stream),
+                       nrows, bs, ipos, buf, v, (const double*)nullptr, (const uint8_t*)nullptr, (PcgState*)nullptr,
+                       none, 0);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_halo_sum(void* comm, double* v, int bs, const int32_t* imap, int64_t nI, const int32_t* ipos, int64_t nrows,
+                 double* buf, fem_stream_t stream) {
+    int rc;
+    if ((rc = fem_halo_pack(v, bs, imap, nI, buf, stream))) return rc;
+    if (nI > 0) FEM_NCCL(ncclAllReduce(buf, buf, (size_t)(nI * bs), ncclFloat64, ncclSum, (ncclComm_t)comm, S(stream)));
+    return fem_halo_unpack(v, bs, ipos, nrows, buf, stream);
+}
+
+int fem_pcg_set_dist(fem_pcg* s, int enable, void* comm, int64_t nI, const int32_t* imap, const int32_t* ipos,
+                     const uint8_t* own) {
+    if (enable && (s->graph || s->fused)) {
+        set_error("fem_pcg_set_dist: the distributed path runs the 3-kernel schedule without a captured graph");
+        return FEM_EARG;
+    }
+    if (s->hbuf) (void)hipFree(s->hbuf);
+    s->hbuf = nullptr;
+    s->dist = enable ? 1 : 0;
+    s->comm = enable ? (ncclComm_t)comm : nullptr;
+    s->nI = nI;
+    s->imap = imap;
+    s->ipos = ipos;
+    s->own = own;
+    if (enable) FEM_HIP(hipMalloc(&s->hbuf, sizeof(double) * (size_t)((nI > 0 ? nI : 1) * s->bs)));
+    return FEM_OK;
+}
+
+// single-process validation of the distributed iteration: sum P ranks' exchange buffers (rank order) and
+// write the sum back to every one of them (what ncclAllReduce does across processes)
+__global__ void k_group_sum(double* const* bufs, int P, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        double s = 0.0;
+        for (int r = 0; r < P; ++r) s += bufs[r][i];
+        for (int r = 0; r < P; ++r) bufs[r][i] = s;
+    }
+}
+
+int fem_group_allreduce(double* const* dev_ptr_array, int P, int64_t n, fem_stream_t stream) {
+    if (n <= 0) return FEM_OK;
+    hipLaunchKernelGGL(k_group_sum, dim3(stream_grid(n, 256)), dim3(256), 0, S(stream), dev_ptr_array, P, n);
     FEM_LAUNCHED();
     return FEM_OK;
 }
@@ -727,7 +1059,8 @@ int fem_pcg_profile(fem_pcg* s, int k, int every, double* ms, int* n) {
         (void)hipEventRecord(evs[4 * si + 0], s->stream);
         rc = launch_spmv_dot(s);
         (void)hipEventRecord(evs[4 * si + 1], s->stream);
-        if (!rc) rc = launch_update(s);
+        if (!rc) rc = launch_exchange_dot(s);
+        if (!rc) rc = launch_update_finish(s);
         (void)hipEventRecord(evs[4 * si + 2], s->stream);
         if (!rc) rc = launch_pupdate(s);
         (void)hipEventRecord(evs[4 * si + 3], s->stream);
@@ -758,6 +1091,7 @@ void fem_pcg_destroy(fem_pcg* s) {
     if (s->q) (void)hipFree(s->q);
     if (s->red.partials) (void)hipFree(s->red.partials);
     if (s->red.counters) (void)hipFree(s->red.counters);
+    if (s->hbuf) (void)hipFree(s->hbuf);
     if (s->st) (void)hipFree(s->st);
     if (s->st_host) (void)hipHostFree(s->st_host);
     delete s;

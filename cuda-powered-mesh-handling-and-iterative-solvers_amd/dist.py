@@ -1,0 +1,418 @@
+"""Multi-GPU path: element partition across the GPUs of one node, RCCL halo all-reduce inside each PCG iteration.
+
+The reference has no multi-device code; its only decomposition is the single-GPU, randomly seeded region growing
+of `subdivision.ipynb:194-297` (global->local node maps by `torch.unique`, `:254-259`). Here:
+  * partition: recursive coordinate bisection of element centroids (deterministic: every rank computes the same
+    split independently, no communication), RCB splits the longest axis at the element-count median;
+  * every rank keeps the GLOBAL node ids of its elements (`torch.unique`, sorted, as `subdivision.ipynb:254-259`),
+    assembles the SELL matrix of its own elements over them (unassembled at shared nodes), and knows the global
+    interface list (nodes touched by several ranks) and which rows it owns (lowest rank touching the node);
+  * per iteration: halo all-reduce of A p on the compact interface vector, p.q and r.z over owned rows with one
+    scalar all-reduce each (csrc/pcg.hip, distributed phases). All ranks hold bit-identical copies of shared dofs.
+
+The partition/halo bookkeeping is plain torch index work run on the mesh's device; it is also exercised on CPU by
+tests/test_dist_cpu.py (gloo, world size 2) against the oracle. The RCCL communicator is created in the C-ABI
+(fem_comm_init) from a unique id broadcast over torch.distributed.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import time
+from dataclasses import dataclass
+
+import torch
+
+from . import _capi as C
+from . import mesh as _mesh
+from . import system as _sys
+
+F64, I32, LONG = torch.float64, torch.int32, torch.long
+
+
+# ============================================================================ partition (host logic, any device)
+def element_centroids(coords, elements):
+    return coords[elements].mean(dim=1)
+
+
+def rcb_partition(centroids: torch.Tensor, nparts: int) -> torch.Tensor:
+    """Recursive coordinate bisection -> part id [M] (int64). Deterministic: stable sorts, ties by element id."""
+    M = centroids.shape[0]
+    part = torch.empty(M, dtype=LONG, device=centroids.device)
+
+    def split(ids, k, base):
+        if k == 1:
+            part[ids] = base
+            return
+        c = centroids[ids]
+        ext = c.amax(0) - c.amin(0)
+        axis = int(torch.argmax(ext))          # first maximal axis on ties
+        order = torch.sort(c[:, axis], stable=True).indices
+        kl = k // 2
+        nl = (ids.numel() * kl + k // 2) // k
+        left = torch.sort(ids[order[:nl]]).values
+        right = torch.sort(ids[order[nl:]]).values
+        split(left, kl, base)
+        split(right, k - kl, base + kl)
+
+    split(torch.arange(M, device=centroids.device), nparts, 0)
+    return part
+
+
+@dataclass
+class RankMesh:
+    rank: int
+    nparts: int
+    elem_ids: torch.Tensor    # global element ids of this rank
+    nodes: torch.Tensor       # global node ids of the local rows (sorted)
+    conn: torch.Tensor        # local connectivity [M_r, npe]
+    imap: torch.Tensor        # [nI] int32 local row of interface node j, -1 if absent
+    ipos: torch.Tensor        # [n_local] int32 interface index, -1 interior
+    own: torch.Tensor         # [n_local] uint8
+    n_iface: int
+
+
+def node_sharing(elements, part, nparts, n_nodes):
+    """(number of ranks touching each node, lowest rank touching it)."""
+    dev = elements.device
+    count = torch.zeros(n_nodes, dtype=I32, device=dev)
+    owner = torch.full((n_nodes,), nparts, dtype=LONG, device=dev)
+    for r in range(nparts):
+        m = torch.zeros(n_nodes, dtype=torch.bool, device=dev)
+        m[elements[part == r].reshape(-1)] = True
+        count += m.to(I32)
+        owner = torch.where(m & (owner > r), torch.full_like(owner, r), owner)
+    return count, owner
+
+
+def rank_mesh(elements, part, rank, nparts, n_nodes, sharing=None) -> RankMesh:
+    count, owner = sharing if sharing is not None else node_sharing(elements, part, nparts, n_nodes)
+    ids = torch.nonzero(part == rank, as_tuple=True)[0]
+    el = elements[ids]
+    nodes, inv = torch.unique(el, return_inverse=True)         # `subdivision.ipynb:254-259`
+    conn = inv.reshape(el.shape).contiguous()
+    iface = torch.nonzero(count > 1, as_tuple=True)[0]          # sorted global interface node ids
+    pos_in_local = torch.searchsorted(nodes, iface)
+    present = (pos_in_local < nodes.numel())
+    present &= nodes[pos_in_local.clamp(max=max(nodes.numel() - 1, 0))] == iface
+    imap = torch.where(present, pos_in_local, torch.full_like(pos_in_local, -1)).to(I32)
+    is_if = count[nodes] > 1
+    ipos = torch.where(is_if, torch.searchsorted(iface, nodes), torch.full_like(nodes, -1)).to(I32)
+    own = (owner[nodes] == rank).to(torch.uint8)
+    return RankMesh(rank, nparts, ids, nodes, conn, imap.contiguous(), ipos.contiguous(), own.contiguous(),
+                    int(iface.numel()))
+
+
+# ============================================================================ device side
+class DistSystem:
+    """One rank's share: local SELL operator + halo maps. `comm` = RCCL communicator (None: phase-driven)."""
+
+    def __init__(self, coords, elements, part, rank, nparts, kind="poisson", E=1.0, nu=0.0, comm=None,
+                 sharing=None):
+        self.lib = C.lib()
+        self.dev = coords.device
+        self.rm = rank_mesh(elements, part, rank, nparts, coords.shape[0], sharing)
+        self.comm = comm
+        lc = coords[self.rm.nodes].contiguous()
+        self.A = _sys.assemble_tet4_system(lc, self.rm.conn, kind, E, nu)
+        self.bs = self.A.bs
+        self.hbuf = torch.empty(max(self.rm.n_iface, 1) * self.bs, dtype=F64, device=self.dev)
+
+    @property
+    def n(self):
+        return self.A.n
+
+    def local(self, v_global):
+        """Restrict a global nodal field [N, bs] to this rank's rows (nodal values, not partial sums)."""
+        return v_global.reshape(-1, self.bs)[self.rm.nodes].reshape(-1).to(F64).contiguous()
+
+    def diag_local(self):
+        d = torch.empty(self.n, dtype=F64, device=self.dev)
+        g = self.A.g
+        C.check(self.lib.fem_sell_diag(C.ptr(self.A.vals), self.bs, C.ptr(g.diagpos), C.ptr(g.csr2sell), g.n_nodes,
+                                       C.ptr(d), C.stream(self.dev)), "fem_sell_diag")
+        return d
+
+    def halo_pack(self, v):
+        C.check(self.lib.fem_halo_pack(C.ptr(v), self.bs, C.ptr(self.rm.imap), self.rm.n_iface, C.ptr(self.hbuf),
+                                       C.stream(self.dev)), "fem_halo_pack")
+
+    def halo_unpack(self, v):
+        C.check(self.lib.fem_halo_unpack(C.ptr(v), self.bs, C.ptr(self.rm.ipos), self.A.g.n_nodes, C.ptr(self.hbuf),
+                                         C.stream(self.dev)), "fem_halo_unpack")
+
+    def jacobi_from(self, dsum, fixed_mask_local):
+        w = torch.empty(self.n, dtype=F64, device=self.dev)
+        C.check(self.lib.fem_jacobi_from_diag(C.ptr(dsum), self.n, C.ptr(fixed_mask_local), C.ptr(w),
+                                              C.stream(self.dev)), "fem_jacobi_from_diag")
+        return w
+
+    def jacobi(self, fixed_mask_local):
+        """M_inv of the ASSEMBLED global matrix: the local diagonals are halo-summed first (RCCL)."""
+        d = self.diag_local()
+        C.check(self.lib.fem_halo_sum(self.comm, C.ptr(d), self.bs, C.ptr(self.rm.imap), self.rm.n_iface,
+                                      C.ptr(self.rm.ipos), self.A.g.n_nodes, C.ptr(self.hbuf), C.stream(self.dev)),
+                "fem_halo_sum")
+        return self.jacobi_from(d, fixed_mask_local)
+
+    def runner(self, b, w, tol=0.0, mode=C.MODE_PCG, hist_len=0):
+        return DistRunner(self, b, w, tol, mode, hist_len)
+
+
+class DistRunner(_sys.PcgRunner):
+    """(P)CG context of one rank in distributed mode."""
+
+    def __init__(self, ds: DistSystem, b, w, tol, mode, hist_len=0):
+        super().__init__(ds.A, b, w, mode=mode, tol=tol)
+        self.ds = ds
+        self.hist = torch.full((max(hist_len, 1),), float("nan"), dtype=F64, device=ds.dev) if hist_len else None
+        C.check(self.lib.fem_pcg_set_dist(self.h, 1, ds.comm, ds.rm.n_iface, C.ptr(ds.rm.imap), C.ptr(ds.rm.ipos),
+                                          C.ptr(ds.rm.own)), "fem_pcg_set_dist")
+
+    def phase(self, k):
+        C.check(self.lib.fem_pcg_dist_phase(self.h, int(k)), "fem_pcg_dist_phase")
+
+    def buffer(self, k):
+        p, n = ctypes.c_void_p(), ctypes.c_int64()
+        C.check(self.lib.fem_pcg_dist_buffer(self.h, int(k), ctypes.byref(p), ctypes.byref(n)), "fem_pcg_dist_buffer")
+        return p.value, n.value
+
+
+# ============================================================================ single-process, multi-partition driver
+class PartitionGroup:
+    """All P partitions in ONE process on ONE GPU, exchanges summed by a group kernel in rank order: exercises the
+    distributed kernels, halo maps and ownership without RCCL (which refuses two ranks per device)."""
+
+    def __init__(self, coords, elements, nparts, kind="poisson", E=1.0, nu=0.0):
+        self.lib = C.lib()
+        part = rcb_partition(element_centroids(coords, elements), nparts)
+        sharing = node_sharing(elements, part, nparts, coords.shape[0])
+        self.part = part
+        self.ranks = [DistSystem(coords, elements, part, r, nparts, kind, E, nu, None, sharing)
+                      for r in range(nparts)]
+        self.dev = coords.device
+
+    def group_sum(self, ptrs, n):
+        arr = torch.tensor(ptrs, dtype=torch.int64, device=self.dev)
+        C.check(self.lib.fem_group_allreduce(C.ptr(arr), len(ptrs), int(n), C.stream(self.dev)), "fem_group_allreduce")
+        torch.cuda.current_stream(self.dev).synchronize()   # keep `arr` alive until the kernel ran
+
+    def jacobi(self, fixed_masks):
+        ds = [r.diag_local() for r in self.ranks]
+        for r, d in zip(self.ranks, ds):
+            r.halo_pack(d)
+        self.group_sum([r.hbuf.data_ptr() for r in self.ranks], self.ranks[0].hbuf.numel())
+        out = []
+        for r, d, m in zip(self.ranks, ds, fixed_masks):
+            r.halo_unpack(d)
+            out.append(r.jacobi_from(d, m))
+        return out
+
+    def solve(self, bs_local, ws, tol, max_iter, mode=C.MODE_PCG):
+        """Phase-driven (P)CG over the P partitions; returns (per-rank x, iterations, status)."""
+        # every context on the current stream: the phases of all ranks and the group sums serialise in order
+        runs = [_GroupRunner(r, b, w, tol, mode) for r, b, w in zip(self.ranks, bs_local, ws)]
+        for run in runs:
+            run.start_state()
+
+        def step(ph):
+            for run in runs:
+                run.phase(ph)
+            p0, n0 = runs[0].buffer(ph)
+            if n0:
+                self.group_sum([run.buffer(ph)[0] for run in runs], n0)
+
+        for ph in (10, 11, 12):
+            step(ph)
+        it = 0
+        for it in range(max_iter):
+            for ph in (0, 1, 2, 3):
+                step(ph)
+            if (it + 1) % 16 == 0:
+                i_, s_, _ = runs[0].poll()
+                if s_ != C.PCG_RUNNING:
+                    break
+        polls = [run.poll() for run in runs]
+        xs = [run.x for run in runs]
+        for run in runs:
+            run.close()
+        its = {p[0] for p in polls}
+        sts = {p[1] for p in polls}
+        assert len(its) == 1 and len(sts) == 1, f"ranks disagree: {polls}"
+        return xs, polls[0][0], polls[0][1]
+
+
+class _GroupRunner:
+    """Distributed (P)CG context on the current stream, driven phase by phase by PartitionGroup."""
+
+    def __init__(self, ds: DistSystem, b, w, tol, mode):
+        self.lib = C.lib()
+        A = ds.A
+        self.b = b.to(F64).contiguous()
+        self.w = w.to(F64).contiguous()
+        self.x = torch.zeros(A.n, dtype=F64, device=A.device)
+        self.h = ctypes.c_void_p()
+        C.check(self.lib.fem_pcg_create(A.g.n_nodes, A.bs, C.ptr(A.g.slice_ptr), C.ptr(A.g.cols), C.ptr(A.vals),
+                                        C.ptr(self.b), C.ptr(self.x), C.ptr(self.w), mode, float(tol), 1e-30, None,
+                                        0, C.stream(A.device), ctypes.byref(self.h)), "fem_pcg_create")
+        C.check(self.lib.fem_pcg_set_schedule(self.h, 0), "fem_pcg_set_schedule")
+        C.check(self.lib.fem_pcg_set_dist(self.h, 1, None, ds.rm.n_iface, C.ptr(ds.rm.imap), C.ptr(ds.rm.ipos),
+                                          C.ptr(ds.rm.own)), "fem_pcg_set_dist")
+
+    def start_state(self):
+        C.check(self.lib.fem_pcg_start(self.h), "fem_pcg_start")   # state only (phases do the work)
+
+    def phase(self, k):
+        C.check(self.lib.fem_pcg_dist_phase(self.h, int(k)), "fem_pcg_dist_phase")
+
+    def buffer(self, k):
+        p, n = ctypes.c_void_p(), ctypes.c_int64()
+        C.check(self.lib.fem_pcg_dist_buffer(self.h, int(k), ctypes.byref(p), ctypes.byref(n)), "fem_pcg_dist_buffer")
+        return p.value, n.value
+
+    def poll(self):
+        it, stt, rz = ctypes.c_int(), ctypes.c_int(), ctypes.c_double()
+        C.check(self.lib.fem_pcg_poll(self.h, ctypes.byref(it), ctypes.byref(stt), ctypes.byref(rz)), "fem_pcg_poll")
+        return it.value, stt.value, rz.value
+
+    def close(self):
+        if self.h:
+            self.lib.fem_pcg_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+
+def gather_solution(ranks, xs, n_nodes, bs):
+    """Assemble the global solution from the ranks' copies (owned rows)."""
+    dev = xs[0].device
+    out = torch.zeros(n_nodes * bs, dtype=F64, device=dev)
+    for r, x in zip(ranks, xs):
+        own = r.rm.own.bool()
+        rows = r.rm.nodes[own]
+        out.view(-1, bs)[rows] = x.view(-1, bs)[own]
+    return out.view(n_nodes, bs)
+
+
+# ============================================================================ RCCL bootstrap + bench
+def init_comm(rank, world):
+    """RCCL communicator for this rank on the current HIP device; the 128-byte id travels over torch.distributed."""
+    import torch.distributed as tdist
+    lib = C.lib()
+    buf = ctypes.create_string_buffer(128)
+    if rank == 0:
+        C.check(lib.fem_comm_unique_id(buf), "fem_comm_unique_id")
+    obj = [bytes(buf.raw) if rank == 0 else None]
+    tdist.broadcast_object_list(obj, src=0)
+    comm = ctypes.c_void_p()
+    C.check(lib.fem_comm_init(world, rank, obj[0], ctypes.byref(comm)), "fem_comm_init")
+    return comm
+
+
+def bench_main(a, metric):
+    """bench.py for N > 1 ranks (one per GPU): the 10M-tet system element-partitioned over the ranks (strong
+    scaling); value = CG iterations/s of the global system, max time over ranks."""
+    import torch.distributed as tdist
+    world = int(os.environ["WORLD_SIZE"])
+    rank = int(os.environ["RANK"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    C.lib()
+    comm = init_comm(rank, world)
+
+    def barrier_sync():
+        torch.cuda.synchronize()
+        tdist.barrier()
+
+    def tmax(v):
+        t = torch.tensor([v], dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        return float(t[0])
+
+    coords, tets = _mesh.kuhn_cube(a.n, device=dev)
+    N = coords.shape[0]
+    if a.kind == "poisson":
+        f, fixed = _mesh.cube_poisson_case(coords)
+        E, nu = 1.0, 0.0
+    else:
+        f, fixed = _mesh.cube_elasticity_case(coords)
+        E, nu = 113.8e9, 0.342
+    # warm the kernels and the RCCL connections (lazily set up on the first collective)
+    c0, t0_ = _mesh.kuhn_cube(6, device=dev)
+    _sys.assemble_tet4_system(c0, t0_, a.kind, E, nu)
+    wbuf = torch.ones(1 << 16, dtype=F64, device=dev)
+    C.check(C.lib().fem_allreduce_sum(comm, C.ptr(wbuf), wbuf.numel(), C.stream(dev)), "fem_allreduce_sum")
+    barrier_sync()
+
+    t0 = time.perf_counter()
+    part = rcb_partition(element_centroids(coords, tets), world)
+    ds = DistSystem(coords, tets, part, rank, world, a.kind, E, nu, comm)
+    bs = ds.bs
+    gmask = torch.zeros((N, bs), dtype=torch.uint8, device=dev)
+    gmask[fixed] = 1
+    mask = gmask[ds.rm.nodes].reshape(-1).contiguous()
+    w = ds.jacobi(mask)
+    barrier_sync()
+    t_asm = tmax(time.perf_counter() - t0)
+    b = ds.local(f)
+    # global tolerance: rtol * sqrt(b.Minv b) over owned rows
+    own = ds.rm.own.bool().repeat_interleave(bs)
+    bz = torch.tensor([float(torch.dot(b[own], (w * b)[own]))], dtype=torch.float64)
+    tdist.all_reduce(bz)
+    tol = a.rtol * float(bz[0]) ** 0.5
+
+    run = ds.runner(b, w, tol=tol)
+    barrier_sync()
+    t0 = time.perf_counter()
+    run.start()
+    done, it, stt = 0, 0, C.PCG_RUNNING
+    chunk = 64
+    while done < 20000:
+        run.iterate(chunk)
+        done += chunk
+        it, stt, _ = run.poll()
+        if stt != C.PCG_RUNNING:
+            break
+    barrier_sync()
+    t_solve = tmax(time.perf_counter() - t0)
+    run.close()
+
+    run = ds.runner(b, w, tol=0.0)
+    run.start()
+    run.iterate(a.warmup)
+    barrier_sync()
+    t0 = time.perf_counter()
+    ms, cnt = run.profile(a.steps, every=a.sample_every)
+    barrier_sync()
+    dt = tmax(time.perf_counter() - t0)
+    it2, _, _ = run.poll()
+    run.close()
+    spmv_ms = tmax(ms[0] / max(cnt[0], 1))
+    alg = ds.A.algorithmic_bytes_spmv()
+    alg_total = torch.tensor([float(alg)], dtype=torch.float64)
+    tdist.all_reduce(alg_total)
+    nI = ds.rm.n_iface
+    if rank == 0:
+        achieved = alg / (spmv_ms * 1e-3) / 1e9
+        out = {
+            "metric": metric, "value": a.steps / dt, "unit": "CG iterations/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"{tets.shape[0]:,}-tet P1 {a.kind} Kuhn cube n={a.n}, Jacobi-PCG fixed "
+                                   f"iterations, element-partitioned (RCB) over {world} GPUs, RCCL halo all-reduce",
+                       "tets": int(tets.shape[0]), "dofs": N * bs, "interface_nodes": nI,
+                       "parallelism": f"element partition x{world}"},
+            "dofs_per_s": N * bs / (t_asm + t_solve), "assembly_ms": t_asm * 1e3, "solve_ms": t_solve * 1e3,
+            "solve_iters": it, "solve_status": stt,
+            "kernel_ms": {"spmv_local_max": spmv_ms, "exchange_update": ms[1] / max(cnt[1], 1),
+                          "pupdate": ms[2] / max(cnt[2], 1)},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
+                         "frac": achieved / 8000.0, "traffic": None, "kernel": "k_pcg_spmv_dot (rank 0 local)",
+                         "algorithmic_bytes": alg},
+            "cpu_baseline": None,
+        }
+        print(json.dumps(out), flush=True)
+    C.check(C.lib().fem_comm_destroy(comm), "fem_comm_destroy")
+    tdist.barrier()
+    tdist.destroy_process_group()

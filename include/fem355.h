@@ -147,6 +147,12 @@ int fem_jacobi(const double* vals, int bs, const int32_t* rowptr, const int32_t*
                const int64_t* csr2sell, const int64_t* slice_ptr, int64_t nrows, const uint8_t* mask,
                double* w, fem_stream_t stream);
 
+/* diag [nrows*bs] = the block diagonals' diagonal entries; w = 1/diag (inf -> 0, 0 where mask) — the two halves
+ * of fem_jacobi, split so a distributed caller can halo-sum the diagonal in between (fem_halo_sum). */
+int fem_sell_diag(const double* vals, int bs, const int32_t* diagpos, const int64_t* csr2sell, int64_t nrows,
+                  double* diag, fem_stream_t stream);
+int fem_jacobi_from_diag(const double* diag, int64_t n, const uint8_t* mask, double* w, fem_stream_t stream);
+
 /* ------------------------------------------------------------------ element-by-element operator
  * y = sum_e P_e^T K_e P_e u — replaces compute_nodal_forces (`solver/element.py:429-464`), deterministic
  * (ascending element order per dof, like the CPU index_add). Ke [M, npe*dpn, npe*dpn]. */
@@ -205,6 +211,38 @@ int fem_pcg_use_graph(fem_pcg* s, int k);
  * n[0..2] sampled launches (bench.py's live per-kernel timing inside its timed region) */
 int fem_pcg_profile(fem_pcg* s, int k, int every, double* ms, int* n);
 void fem_pcg_destroy(fem_pcg* s);
+
+/* ------------------------------------------------------------------ multi-GPU (element partition, RCCL)
+ * One process per GPU. Every rank holds the SELL matrix of ITS elements over its local nodes (unassembled at
+ * nodes shared with other ranks) and the global interface list: imap [nI] = local row of global interface node j
+ * (-1 if the rank has no copy), ipos [nrows] = interface index of a local row (-1 interior), own [nrows] = 1 on
+ * the rows the rank owns (owner = lowest rank touching the node). Each iteration then adds, on the device
+ * stream: halo all-reduce of the compact interface vector of A p (nI*bs doubles), p.q over owned rows and its
+ * scalar all-reduce, r.z and its scalar all-reduce. The reference has no multi-device code; this replaces its
+ * single-GPU region-growing split (`subdivision.ipynb:194-297`) with a deterministic partition.
+ *   fem_comm_unique_id: [host] 128-byte RCCL id from rank 0 (broadcast it with any host transport)
+ *   fem_comm_init     : [sync] communicator of this rank on the current HIP device */
+int fem_comm_unique_id(char* out128);
+int fem_comm_init(int nranks, int rank, const char* id128, void** comm);
+int fem_comm_destroy(void* comm);
+int fem_allreduce_sum(void* comm, double* buf, int64_t n, fem_stream_t stream);
+/* v[interface rows] <- sum over ranks (buf: [nI*bs] scratch) = pack, all-reduce, unpack */
+int fem_halo_pack(const double* v, int bs, const int32_t* imap, int64_t nI, double* buf, fem_stream_t stream);
+int fem_halo_unpack(double* v, int bs, const int32_t* ipos, int64_t nrows, const double* buf, fem_stream_t stream);
+int fem_halo_sum(void* comm, double* v, int bs, const int32_t* imap, int64_t nI, const int32_t* ipos, int64_t nrows,
+                 double* buf, fem_stream_t stream);
+/* switch a (P)CG context to the distributed iteration (enable=1; 3-kernel schedule, no graph). With comm = NULL
+ * the exchanges are left to the caller, who drives the iteration phase by phase (below). */
+int fem_pcg_set_dist(fem_pcg* s, int enable, void* comm, int64_t nI, const int32_t* imap, const int32_t* ipos,
+                     const uint8_t* own);
+/* Phase-driven distributed iteration (what fem_pcg_start/iterate do around ncclAllReduce): phases 10, 11, 12
+ * start the solve, phases 0..3 are one iteration; after phases 10, 0, 11, 1, 2 the buffer reported by
+ * fem_pcg_dist_buffer must be summed over all ranks. Used to validate the distributed kernels with several
+ * partitions in ONE process on one GPU (RCCL refuses two ranks on one device). */
+int fem_pcg_dist_phase(fem_pcg* s, int phase);
+int fem_pcg_dist_buffer(fem_pcg* s, int phase, double** ptr, int64_t* n);
+/* dev_ptr_array: DEVICE array of P device pointers; sums the P buffers (rank order) into each of them */
+int fem_group_allreduce(double* const* dev_ptr_array, int P, int64_t n, fem_stream_t stream);
 
 #ifdef __cplusplus
 }

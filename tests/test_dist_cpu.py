@@ -1,0 +1,106 @@
+"""N>1 path on the CPU: world-size-2 gloo run of the element-partitioned PCG (oracle/dist_ref.py) on the product's
+RCB partition and halo maps (fem355.dist), against the serial oracle solve."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, kind, out_path):
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import fem355  # noqa: F401
+    from fem355 import dist as fd, mesh
+    from oracle import dist_ref
+    coords, tets = mesh.kuhn_cube(5, jitter=0.1)
+    if kind == "poisson":
+        f, fixed = mesh.cube_poisson_case(coords)
+        E, nu = 1.0, 0.0
+    else:
+        f, fixed = mesh.cube_elasticity_case(coords)
+        E, nu = 113.8e9, 0.342
+    part = fd.rcb_partition(fd.element_centroids(coords, tets), world)
+    rm = fd.rank_mesh(tets, part, rank, world, coords.shape[0])
+    x, it, st = dist_ref.dist_pcg(coords, tets, f, fixed, rm, kind, E, nu, tol=1e-9, max_iter=2000)
+    torch.save({"nodes": rm.nodes, "own": rm.own, "x": x, "it": it, "st": st, "nI": rm.n_iface},
+               f"{out_path}.{rank}")
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["poisson", "elastic"])
+def test_partitioned_pcg_matches_serial(tmp_path, kind):
+    from fem355 import mesh
+    from oracle import ref_cpu as R
+    world = 2
+    out = str(tmp_path / "res")
+    mp.spawn(_worker, args=(world, _free_port(), kind, out), nprocs=world, join=True)
+    res = [torch.load(f"{out}.{r}", weights_only=True) for r in range(world)]
+    coords, tets = mesh.kuhn_cube(5, jitter=0.1)
+    N = coords.shape[0]
+    if kind == "poisson":
+        f, fixed = mesh.cube_poisson_case(coords)
+        K, bs = R.tet4_poisson_K(coords, tets), 1
+    else:
+        f, fixed = mesh.cube_elasticity_case(coords)
+        K, bs = R.tet4_K(coords, tets, 113.8e9, 0.342), 3
+    Minv = R.diag_preconditioner(K, tets, N, dpn=bs)
+    Minv[fixed] = 0.0
+    u, it, st = R.pcg(K, tets, f.view(N, bs), Minv, tol=1e-9, max_iter=2000)
+    assert st == "converged"
+    assert all(r["st"] == "converged" for r in res)
+    assert abs(res[0]["it"] - it) <= 2 and res[0]["it"] == res[1]["it"]
+    assert res[0]["nI"] > 0
+    glob = torch.zeros(N, bs, dtype=torch.float64)
+    owned = torch.zeros(N, dtype=torch.int32)
+    for r in res:
+        o = r["own"].bool()
+        glob[r["nodes"][o]] = r["x"].view(-1, bs)[o]
+        owned[r["nodes"][o]] += 1
+    assert bool((owned == 1).all())                     # every node owned exactly once
+    assert float((glob - u).abs().max() / u.abs().max()) < 1e-10
+    # shared copies agree across ranks
+    common, i0, i1 = (lambda a, b: (lambda c: (c, torch.searchsorted(a, c), torch.searchsorted(b, c)))(
+        a[torch.isin(a, b)]))(res[0]["nodes"], res[1]["nodes"])
+    assert common.numel() > 0
+    assert torch.equal(res[0]["x"].view(-1, bs)[i0], res[1]["x"].view(-1, bs)[i1])
+
+
+def test_rcb_partition_properties():
+    from fem355 import dist as fd, mesh
+    coords, tets = mesh.kuhn_cube(8)
+    for P in (2, 3, 4, 8):
+        part = fd.rcb_partition(fd.element_centroids(coords, tets), P)
+        counts = torch.bincount(part, minlength=P)
+        assert int(counts.sum()) == tets.shape[0] and int(counts.min()) > 0
+        assert int(counts.max() - counts.min()) <= 1
+        # deterministic
+        assert torch.equal(part, fd.rcb_partition(fd.element_centroids(coords, tets), P))
+    part = fd.rcb_partition(fd.element_centroids(coords, tets), 8)
+    cnt, owner = fd.node_sharing(tets, part, 8, coords.shape[0])
+    rms = [fd.rank_mesh(tets, part, r, 8, coords.shape[0], (cnt, owner)) for r in range(8)]
+    nI = rms[0].n_iface
+    assert all(rm.n_iface == nI for rm in rms)
+    # each interface node is present on >= 2 ranks, its ipos/imap are mutually consistent
+    pres = torch.zeros(nI, dtype=torch.int32)
+    for rm in rms:
+        has = rm.imap >= 0
+        pres += has.int()
+        loc = rm.imap[has].long()
+        assert torch.equal(rm.ipos[loc].long(), torch.nonzero(has, as_tuple=True)[0])
+    assert bool((pres >= 2).all())
