@@ -141,6 +141,20 @@ struct PcgState {
     int mode;
     int dist;         // 1: element-partitioned; reductions land in red[] and are all-reduced (RCCL) first
     double red[4];    // dist: rank-local partial sums p.q, r.z, r0.z0 (all-reduced in place)
+    // deferred schedule: per-iteration state banked by the host's launch parity (see k_pcg_d*)
+    struct Bank {
+        double rz;        // r.z of the current iterate
+        double beta;      // beta to form this iteration's p (unused: p is formed in d3)
+        int iter;         // completed iterations
+        int halt;
+        int status;
+        int stop_iter;
+        int k2stop;       // set by d2 of this bank's iteration: FEM_PCG_BREAKDOWN / ALPHA_NAN
+        int pad_;
+        double alpha;     // written by d2 block 0 (read by d3)
+        double pq;
+        double rz_new;
+    } bank[2];
 };
 
 constexpr int PCG_BLOCK = 256;
@@ -348,6 +362,178 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_pupdate(int64_t n, double* __
     }
 }
 
+// ---------------------------------------------------------------- deferred schedule (3 kernels, no grid atomics)
+// d1: q = A p and one p.q partial per block (plain store).  d2: every block re-sums d1's partials in fixed order
+// (identical pq everywhere), alpha + guards, r update, one r.z partial per block.  d3: every block re-sums d2's
+// partials -> stop test, beta, x/p update; block 0 writes the NEXT bank. Bank = host launch parity, so no kernel
+// writes a state field its own blocks read.
+template <int BS>
+__global__ void __launch_bounds__(PCG_BLOCK) k_pcg_d1(int64_t nslices, int64_t nrows,
+                                                      const int64_t* __restrict__ slice_ptr,
+                                                      const int32_t* __restrict__ cols, const double* __restrict__ vals,
+                                                      const double* __restrict__ p, double* __restrict__ q,
+                                                      const PcgState* __restrict__ st, int par,
+                                                      double* __restrict__ partials) {
+    __shared__ double lds4[4];
+    const PcgState::Bank& bk = st->bank[par];
+    if (bk.halt || bk.iter >= st->max_iter) return;
+    const int lane = threadIdx.x & 63;
+    double dot = 0.0;
+    SliceWalk wk = slice_walk(nslices);
+    const VecPlain pv{p};
+    for (int64_t s = wk.s; s < wk.end; s += wk.step) {
+        double o[BS];
+        sell_row<BS, SPMV_U, false>(s, lane, slice_ptr, cols, vals, pv, o);
+        const int64_t row = s * 64 + lane;
+        if (row < nrows) {
+#pragma unroll
+            for (int c = 0; c < BS; ++c) {
+                q[row * BS + c] = o[c];
+                dot += p[row * BS + c] * o[c];
+            }
+        }
+    }
+    dot = block_sum256(dot, lds4);
+    if (threadIdx.x == 0) partials[blockIdx.x] = dot;
+}
+
+__device__ __forceinline__ double sum_prev_partials(const double* __restrict__ part, int n, double* lds4) {
+    double v = 0.0;
+    for (int i = threadIdx.x; i < n; i += PCG_BLOCK) v += part[i];
+    return block_sum256(v, lds4);
+}
+
+__global__ void __launch_bounds__(PCG_BLOCK) k_pcg_d2(int64_t n, double* __restrict__ r, const double* __restrict__ q,
+                                                      const double* __restrict__ w, PcgState* __restrict__ st, int par,
+                                                      const double* __restrict__ part1, int n1,
+                                                      double* __restrict__ part2) {
+    __shared__ double lds4[4];
+    PcgState::Bank& bk = st->bank[par];
+    if (bk.halt || bk.iter >= st->max_iter) return;
+    const double pq = sum_prev_partials(part1, n1, lds4);
+    const bool cg = st->mode == FEM_MODE_CG_STABLE;
+    double alpha = 0.0;
+    int stop = 0;
+    if (cg) {
+        if (fabs(pq) < st->eps || pq < 0.0) stop = FEM_PCG_BREAKDOWN;             // `solver/solver.py:187`
+        else {
+            alpha = bk.rz / (pq + st->eps);                                      // `:194`
+            if (isnan(alpha) || isinf(alpha)) stop = FEM_PCG_ALPHA_NAN;          // `:196`
+        }
+    } else {
+        alpha = bk.rz / pq;                                                      // `:800`
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        bk.pq = pq;
+        bk.alpha = alpha;
+        bk.k2stop = stop;
+    }
+    if (stop) return;
+    double acc = 0.0;
+    const int64_t n2 = n >> 1;
+    const double2* q2 = reinterpret_cast<const double2*>(q);
+    const double2* w2 = reinterpret_cast<const double2*>(w);
+    double2* r2 = reinterpret_cast<double2*>(r);
+    for (int64_t i = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; i < n2; i += (int64_t)gridDim.x * PCG_BLOCK) {
+        double2 rv = r2[i], qv = q2[i], wv = w2[i];
+        rv.x = rv.x - alpha * qv.x;
+        rv.y = rv.y - alpha * qv.y;
+        if (cg) {
+            if (wv.x == 0.0) rv.x = 0.0;
+            if (wv.y == 0.0) rv.y = 0.0;
+        }
+        r2[i] = rv;
+        acc += rv.x * (wv.x * rv.x);
+        acc += rv.y * (wv.y * rv.y);
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+        int64_t i = n - 1;
+        double rv = r[i] - alpha * q[i];
+        if (cg && w[i] == 0.0) rv = 0.0;
+        r[i] = rv;
+        acc += rv * (w[i] * rv);
+    }
+    acc = block_sum256(acc, lds4);
+    if (threadIdx.x == 0) part2[blockIdx.x] = acc;
+}
+
+__global__ void __launch_bounds__(PCG_BLOCK) k_pcg_d3(int64_t n, double* __restrict__ x, double* __restrict__ p,
+                                                      const double* __restrict__ r, const double* __restrict__ w,
+                                                      PcgState* __restrict__ st, int par,
+                                                      const double* __restrict__ part2, int n2p,
+                                                      double* __restrict__ hist, int64_t hist_len) {
+    __shared__ double lds4[4];
+    const PcgState::Bank bk = st->bank[par];
+    PcgState::Bank& nx = st->bank[par ^ 1];
+    const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+    if (bk.halt || bk.iter >= st->max_iter) {
+        if (lead) {
+            nx = bk;
+            nx.k2stop = 0;
+        }
+        return;
+    }
+    if (bk.k2stop) {   // guard stop in d2: the reference breaks before updating u (`solver/solver.py:187-198`)
+        if (lead) {
+            nx = bk;
+            nx.halt = 1;
+            nx.status = bk.k2stop;
+            nx.stop_iter = bk.iter + 1;
+            nx.k2stop = 0;
+        }
+        return;
+    }
+    const double rz_new = sum_prev_partials(part2, n2p, lds4);
+    const bool cg = st->mode == FEM_MODE_CG_STABLE;
+    const double nrm = sqrt(rz_new);
+    const bool conv = nrm < st->tol;                                             // `:210` / `:805`
+    double beta = 0.0;
+    bool bnan = false;
+    if (!conv) {
+        beta = cg ? rz_new / (bk.rz + st->eps) : rz_new / bk.rz;                 // `:213` / `:808`
+        bnan = cg && (isnan(beta) || isinf(beta));                               // `:214`
+    }
+    const bool upd_p = !conv && !bnan;
+    const double alpha = bk.alpha;
+    const int64_t nh = n >> 1;
+    double2* x2 = reinterpret_cast<double2*>(x);
+    double2* p2 = reinterpret_cast<double2*>(p);
+    const double2* r2 = reinterpret_cast<const double2*>(r);
+    const double2* w2 = reinterpret_cast<const double2*>(w);
+    for (int64_t i = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; i < nh; i += (int64_t)gridDim.x * PCG_BLOCK) {
+        double2 pv = p2[i], xv = x2[i];
+        xv.x += alpha * pv.x;
+        xv.y += alpha * pv.y;
+        x2[i] = xv;
+        if (upd_p) {
+            double2 rv = r2[i], wv = w2[i];
+            pv.x = wv.x * rv.x + beta * pv.x;
+            pv.y = wv.y * rv.y + beta * pv.y;
+            p2[i] = pv;
+        }
+    }
+    if ((n & 1) && lead) {
+        int64_t i = n - 1;
+        x[i] += alpha * p[i];
+        if (upd_p) p[i] = w[i] * r[i] + beta * p[i];
+    }
+    if (lead) {
+        nx = bk;
+        nx.iter = bk.iter + 1;
+        nx.rz_new = rz_new;
+        nx.beta = beta;
+        nx.k2stop = 0;
+        if (hist && bk.iter < hist_len) hist[bk.iter] = nrm;
+        if (conv || bnan) {
+            nx.halt = 1;
+            nx.status = conv ? FEM_PCG_CONVERGED : FEM_PCG_BETA_NAN;
+            nx.stop_iter = bk.iter + 1;
+        } else {
+            nx.rz = rz_new;
+        }
+    }
+}
+
 // fused schedule, end of solve: apply the pending x += alpha_x p_last once
 __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_finish(int64_t n, double* __restrict__ x, const double* __restrict__ p0,
                                                           const double* __restrict__ p1, const PcgState* __restrict__ st) {
@@ -450,6 +636,12 @@ __global__ void k_fin_rz(PcgState* st, double* hist, int64_t hist_len) {
 
 __global__ void k_set_rz(PcgState* st) { st->rz = st->red[2]; }
 
+// deferred schedule start: bank 0 holds the initial iterate's r.z
+__global__ void k_bank_init(PcgState* st) {
+    st->bank[0].rz = st->rz;
+    st->bank[0].rz_new = st->rz;
+}
+
 // HBM ceiling probe: dst = src, 16 B per lane, grid-stride (the measured "STREAM copy" roof of SURVEY §8(d))
 __global__ void __launch_bounds__(256) k_stream_copy(const double2* __restrict__ src, double2* __restrict__ dst,
                                                      int64_t n2) {
@@ -480,7 +672,9 @@ struct fem_pcg {
     int mode;
     double tol, eps;
     hipStream_t stream;
-    int fused;          // kernel schedule (1 = fused, default)
+    int fused;          // schedule 1: p formed inside the SpMV
+    int deferred;       // schedule 2: partial sums finished by the next kernel (banked state)
+    int64_t launched;   // iterations enqueued since start (the deferred schedule's bank parity)
     // owned device memory
     double* r;
     double* p0;
@@ -665,10 +859,38 @@ static int launch_update_finish(fem_pcg* s) {
     return FEM_OK;
 }
 
+static int launch_deferred(fem_pcg* s, int which) {
+    const int par = (int)(s->launched & 1);
+    if (which == 0) {
+        if (s->bs == 1)
+            hipLaunchKernelGGL(k_pcg_d1<1>, dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream, s->nslices, s->nrows,
+                               s->slice_ptr, s->cols, s->vals, s->p0, s->q, s->st, par, s->red.partials);
+        else
+            hipLaunchKernelGGL(k_pcg_d1<3>, dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream, s->nslices, s->nrows,
+                               s->slice_ptr, s->cols, s->vals, s->p0, s->q, s->st, par, s->red.partials);
+    } else if (which == 1) {
+        hipLaunchKernelGGL(k_pcg_d2, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->r, s->q, s->w, s->st,
+                           par, s->red.partials, s->grid_spmv, s->red.partials + MAX_PARTIALS);
+    } else {
+        hipLaunchKernelGGL(k_pcg_d3, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->x, s->p0, s->r, s->w,
+                           s->st, par, s->red.partials + MAX_PARTIALS, s->grid_vec, s->hist, s->hist_len);
+        s->launched++;
+    }
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
 static int launch_iterations(fem_pcg* s, int k) {
     if (s->dist && !s->comm) {
         set_error("distributed PCG without a communicator: drive it with fem_pcg_dist_phase");
         return FEM_EARG;
+    }
+    if (s->deferred && !s->dist) {
+        for (int i = 0; i < k; ++i) {
+            int rc;
+            if ((rc = launch_deferred(s, 0)) || (rc = launch_deferred(s, 1)) || (rc = launch_deferred(s, 2))) return rc;
+        }
+        return FEM_OK;
     }
     for (int i = 0; i < k; ++i) {
         int rc;
@@ -806,17 +1028,40 @@ int fem_pcg_create(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_
     return FEM_OK;
 }
 
-int fem_pcg_set_schedule(fem_pcg* s, int fused) {
+int fem_pcg_set_schedule(fem_pcg* s, int sched) {
     if (s->graph) {
         set_error("fem_pcg_set_schedule: drop the captured graph first (fem_pcg_use_graph(s, 0))");
         return FEM_EARG;
     }
-    if (fused && s->comm) {
+    if (sched < 0 || sched > 2) {
+        set_error("fem_pcg_set_schedule: unknown schedule %d", sched);
+        return FEM_EARG;
+    }
+    if (sched != 0 && s->dist) {
         set_error("fem_pcg_set_schedule: the distributed path runs the 3-kernel schedule");
         return FEM_EARG;
     }
-    s->fused = fused ? 1 : 0;
+    s->fused = sched == 1;
+    s->deferred = sched == 2;
     return FEM_OK;
+}
+
+// host view of the state: the deferred schedule keeps it in the bank of the current launch parity
+static PcgState state_view(const fem_pcg* s) {
+    PcgState h = *s->st_host;
+    if (s->deferred && !s->dist) {
+        const PcgState::Bank& b = h.bank[s->launched & 1];
+        h.iter = b.iter;
+        h.status = b.status;
+        h.halt = b.halt;
+        h.stop_iter = b.stop_iter;
+        h.rz = b.rz;
+        h.rz_new = b.rz_new;
+        h.pq = b.pq;
+        h.alpha = b.alpha;
+        h.beta = b.beta;
+    }
+    return h;
 }
 
 int fem_pcg_start(fem_pcg* s) {
@@ -845,6 +1090,11 @@ int fem_pcg_start(fem_pcg* s) {
     hipLaunchKernelGGL(k_pcg_init, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->b, s->r, s->q, s->w, s->p0,
                        s->p1, s->fused, s->st, s->red, (const uint8_t*)nullptr, s->bs);
     FEM_LAUNCHED();
+    s->launched = 0;
+    if (s->deferred) {
+        hipLaunchKernelGGL(k_bank_init, dim3(1), dim3(1), 0, s->stream, s->st);
+        FEM_LAUNCHED();
+    }
     return FEM_OK;
 }
 
@@ -950,8 +1200,11 @@ int fem_group_allreduce(double* const* dev_ptr_array, int P, int64_t n, fem_stre
 
 int fem_pcg_iterate(fem_pcg* s, int k) {
     if (k <= 0) return FEM_OK;
-    if (s->graph && s->graph_k > 0 && k % s->graph_k == 0) {
+    // the deferred schedule's graph was captured from bank parity 0 over an even number of iterations
+    const bool parity_ok = !s->deferred || ((s->launched & 1) == 0 && (s->graph_k & 1) == 0);
+    if (s->graph && s->graph_k > 0 && k % s->graph_k == 0 && parity_ok) {
         for (int i = 0; i < k / s->graph_k; ++i) FEM_HIP(hipGraphLaunch(s->graph, s->stream));
+        s->launched += k;
         return FEM_OK;
     }
     return launch_iterations(s, k);
@@ -974,9 +1227,12 @@ int fem_pcg_use_graph(fem_pcg* s, int k) {
     }
     if (k <= 0) return FEM_OK;
     hipGraph_t g;
+    const int64_t saved = s->launched;
+    s->launched = 0;
     FEM_HIP(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
     int rc = launch_iterations(s, k);
     hipError_t e = hipStreamEndCapture(s->stream, &g);
+    s->launched = saved;
     if (rc) return rc;
     if (e != hipSuccess) {
         set_error("fem_pcg_use_graph: capture failed: %s", hipGetErrorString(e));
@@ -996,7 +1252,7 @@ int fem_pcg_use_graph(fem_pcg* s, int k) {
 int fem_pcg_poll(fem_pcg* s, int* iters, int* status, double* rz) {
     FEM_HIP(hipMemcpyAsync(s->st_host, s->st, sizeof(PcgState), hipMemcpyDeviceToHost, s->stream));
     FEM_HIP(hipStreamSynchronize(s->stream));
-    const PcgState& h = *s->st_host;
+    const PcgState h = state_view(s);
     int stt = h.status;
     if (stt == FEM_PCG_RUNNING && h.iter >= h.max_iter) stt = FEM_PCG_MAXITER;
     if (iters) *iters = (stt == FEM_PCG_BREAKDOWN || stt == FEM_PCG_ALPHA_NAN) ? h.stop_iter : h.iter;
@@ -1008,7 +1264,7 @@ int fem_pcg_poll(fem_pcg* s, int* iters, int* status, double* rz) {
 int fem_pcg_scalars(fem_pcg* s, double* out6) {
     FEM_HIP(hipMemcpyAsync(s->st_host, s->st, sizeof(PcgState), hipMemcpyDeviceToHost, s->stream));
     FEM_HIP(hipStreamSynchronize(s->stream));
-    const PcgState& h = *s->st_host;
+    const PcgState h = state_view(s);
     out6[0] = h.rz;
     out6[1] = h.pq;
     out6[2] = h.alpha;
@@ -1056,13 +1312,14 @@ int fem_pcg_profile(fem_pcg* s, int k, int every, double* ms, int* n) {
             rc = launch_iterations(s, 1);
             continue;
         }
+        const bool dfr = s->deferred && !s->dist;
         (void)hipEventRecord(evs[4 * si + 0], s->stream);
-        rc = launch_spmv_dot(s);
+        rc = dfr ? launch_deferred(s, 0) : launch_spmv_dot(s);
         (void)hipEventRecord(evs[4 * si + 1], s->stream);
-        if (!rc) rc = launch_exchange_dot(s);
-        if (!rc) rc = launch_update_finish(s);
+        if (!rc && !dfr) rc = launch_exchange_dot(s);
+        if (!rc) rc = dfr ? launch_deferred(s, 1) : launch_update_finish(s);
         (void)hipEventRecord(evs[4 * si + 2], s->stream);
-        if (!rc) rc = launch_pupdate(s);
+        if (!rc) rc = dfr ? launch_deferred(s, 2) : launch_pupdate(s);
         (void)hipEventRecord(evs[4 * si + 3], s->stream);
         ++si;
     }

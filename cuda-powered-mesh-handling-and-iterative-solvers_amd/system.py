@@ -21,6 +21,18 @@ def _dev_scalar(dev, dtype, value):
     return torch.full((1,), value, dtype=dtype, device=dev)
 
 
+# (P)CG kernel schedules (csrc/pcg.hip): 0 = three kernels with in-kernel grid reductions, 1 = fused (p formed
+# inside the SpMV), 2 = deferred (partials summed by the next kernel, no grid atomics)
+SCHED_THREE, SCHED_FUSED, SCHED_DEFERRED = 0, 1, 2
+DEFAULT_SCHEDULE = SCHED_THREE
+
+
+def _schedule(fused, schedule):
+    if schedule is not None:
+        return int(schedule)
+    return SCHED_FUSED if fused else DEFAULT_SCHEDULE
+
+
 @dataclass
 class PcgResult:
     x: torch.Tensor
@@ -204,7 +216,7 @@ class SellMatrix:
 
     # ---------------------------------------------------------------- solver
     def pcg(self, b, x0=None, w=None, mode=C.MODE_PCG, tol=1e-8, max_iter=1000, eps=1e-30, history=False,
-            chunk=32, fused=False):
+            chunk=32, fused=False, schedule=None):
         """Run the device (P)CG; returns (x, iterations, status, rz_last, hist or None)."""
         lib = C.lib()
         b = b.to(F64).contiguous().view(-1)
@@ -218,7 +230,7 @@ class SellMatrix:
                                    C.ptr(hist), hist.numel() if hist is not None else 0, C.stream(self.device),
                                    ctypes.byref(h)), "fem_pcg_create")
         try:
-            C.check(lib.fem_pcg_set_schedule(h, 1 if fused else 0), "fem_pcg_set_schedule")
+            C.check(lib.fem_pcg_set_schedule(h, _schedule(fused, schedule)), "fem_pcg_set_schedule")
             it, stt, rz = ctypes.c_int(), ctypes.c_int(), ctypes.c_double()
             C.check(lib.fem_pcg_solve(h, int(max_iter), int(chunk), ctypes.byref(it), ctypes.byref(stt),
                                       ctypes.byref(rz)), "fem_pcg_solve")
@@ -234,7 +246,8 @@ class SellMatrix:
 class PcgRunner:
     """Persistent (P)CG context for fixed-iteration timing (bench.py): start once, iterate k, poll."""
 
-    def __init__(self, A: SellMatrix, b, w, x0=None, mode=C.MODE_PCG, tol=0.0, eps=1e-30, fused=False):
+    def __init__(self, A: SellMatrix, b, w, x0=None, mode=C.MODE_PCG, tol=0.0, eps=1e-30, fused=False,
+                 schedule=None):
         self.lib = C.lib()
         self.A = A
         self.b = b.to(F64).contiguous().view(-1)
@@ -249,7 +262,7 @@ class PcgRunner:
                                         C.ptr(self.b), C.ptr(self.x), C.ptr(self.w), mode, float(tol), float(eps),
                                         None, 0, ctypes.c_void_p(self.stream.cuda_stream), ctypes.byref(self.h)),
                 "fem_pcg_create")
-        C.check(self.lib.fem_pcg_set_schedule(self.h, 1 if fused else 0), "fem_pcg_set_schedule")
+        C.check(self.lib.fem_pcg_set_schedule(self.h, _schedule(fused, schedule)), "fem_pcg_set_schedule")
 
     def finish(self):
         C.check(self.lib.fem_pcg_finish(self.h), "fem_pcg_finish")

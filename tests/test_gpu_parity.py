@@ -246,15 +246,47 @@ def test_fused_and_three_kernel_schedules_agree(gpu, kind):
     w = A.jacobi(mask.view(-1))
     b = f.to(gpu).reshape(-1)
     tol = 1e-9 * float(torch.sqrt(torch.dot(b, w * b)))
-    r1 = A.pcg(b, w=w, tol=tol, max_iter=2000, fused=True)
-    r0 = A.pcg(b, w=w, tol=tol, max_iter=2000, fused=False)
-    assert r1.status == r0.status == 1 and abs(r1.iterations - r0.iterations) <= 1
-    assert rel(r1.x, r0.x) < 1e-10
-    # CG mode, fixed max_iter (the deferred x update of the fused schedule is applied at the end)
+    r0 = A.pcg(b, w=w, tol=tol, max_iter=2000, schedule=0)
     wm = (mask.view(-1) == 0).to(F64)
-    c1 = A.pcg(b, w=wm, mode=0, tol=0.0, max_iter=25, fused=True)
-    c0 = A.pcg(b, w=wm, mode=0, tol=0.0, max_iter=25, fused=False)
-    assert c1.iterations == c0.iterations == 25 and rel(c1.x, c0.x) < 1e-12
+    c0 = A.pcg(b, w=wm, mode=0, tol=0.0, max_iter=25, schedule=0)
+    for sched in (1, 2):
+        r1 = A.pcg(b, w=w, tol=tol, max_iter=2000, schedule=sched, history=True)
+        assert r1.status == r0.status == 1 and abs(r1.iterations - r0.iterations) <= 1, sched
+        assert rel(r1.x, r0.x) < 1e-10
+        # CG mode, fixed max_iter (the fused schedule's deferred x update is applied at the end)
+        c1 = A.pcg(b, w=wm, mode=0, tol=0.0, max_iter=25, schedule=sched)
+        assert c1.iterations == c0.iterations == 25 and c1.status == c0.status == 2 and rel(c1.x, c0.x) < 1e-12
+
+
+def test_deferred_schedule_guard_and_graph(gpu):
+    """Deferred schedule: breakdown stop on the indefinite c3d10 rule (Q2) at iteration 1, and graph replay from
+    even bank parity equals plain launches."""
+    el, mesh, solver, system = _mods()
+    c, t10 = mesh.tet10_cube(1)
+    K = el.compute_c3d10_K_matrix(c, t10, E, NU, device=gpu, dtype=F64)
+    A = solver.assemble(K, t10, c.shape[0], gpu)
+    F = torch.zeros(c.shape[0] * 3, dtype=F64, device=gpu)
+    F[2::3] = -1.0
+    fixed = mesh.face_nodes(c, 2, 0.0).to(gpu)
+    w = torch.ones(c.shape[0], 3, dtype=F64, device=gpu)
+    w[fixed] = 0.0
+    res = A.pcg(F, w=w.view(-1), mode=0, tol=1e-10, max_iter=50, schedule=2)
+    assert res.status == 3 and res.iterations == 1 and float(res.x.abs().max()) == 0.0
+    c4, t4 = mesh.kuhn_cube(6)
+    P = system.assemble_tet4_system(c4.to(gpu), t4.to(gpu), "poisson")
+    b = torch.ones(P.n, dtype=F64, device=gpu)
+    wj = P.jacobi(None)
+    runs = []
+    for g in (0, 4):
+        run = system.PcgRunner(P, b, wj, tol=0.0, schedule=2)
+        run.start()
+        if g:
+            run.use_graph(g)
+        run.iterate(12)
+        it, st, rz = run.poll()
+        runs.append((it, rz, run.x.clone()))
+        run.close()
+    assert runs[0][0] == runs[1][0] == 12 and runs[0][1] == runs[1][1] and torch.equal(runs[0][2], runs[1][2])
 
 
 def test_pcg_history_and_fixed_iterations(gpu):

@@ -85,9 +85,9 @@ def main():
     # PCG kernels, both schedules
     import time
     w = torch.ones(A.n, dtype=torch.float64, device=dev)
-    for fused in (True, False):
-        tag = "fused" if fused else "3k"
-        run = system.PcgRunner(A, x, w, tol=0.0, fused=fused)
+    for sched in (0, 1, 2):
+        tag = {0: "3k", 1: "fused", 2: "deferred"}[sched]
+        run = system.PcgRunner(A, x, w, tol=0.0, schedule=sched)
         run.start()
         run.iterate(20)
         ms, n = run.profile(200, every=1)
