@@ -53,6 +53,9 @@ SIGNATURES = {
     "fem_invert_diag": (_I, [_P, _L, _P, _P]),
     "fem_spmv": (_I, [_L, _I, _P, _P, _P, _P, _P, _P]),
     "fem_spmv_variant": (_I, [_I, _I, _L, _I, _P, _P, _P, _P, _P, _P]),
+    "fem_sell_delta16": (_I, [_P, _L, _P, _P, _P, _P]),
+    "fem_spmv16": (_I, [_L, _I, _P, _P, _P, _P, _P, _P]),
+    "fem_pcg_set_cols16": (_I, [_P, _P]),
     "fem_stream_copy": (_I, [_P, _P, _L, _I, _P]),
     "fem_pcg_create": (_I, [_L, _I, _P, _P, _P, _P, _P, _P, _I, _D, _D, _P, _L, _P, ctypes.POINTER(_P)]),
     "fem_pcg_start": (_I, [_P]),

@@ -140,7 +140,7 @@ __global__ void k_sell_fill(const int32_t* __restrict__ rowptr, const int32_t* _
             rp = rowptr[r];
             len = rowptr[r + 1] - rp;
         }
-        const int pad = (r < nrows) ? (int)r : 0;
+        const int pad = (r < nrows) ? (int)r : (int)(nrows - 1);   // near the row: 16-bit deltas stay small
         for (int k = 0; k < w; ++k) {
             int64_t e = e0 + (int64_t)k * 64;
             if (k < len) {
@@ -148,6 +148,26 @@ __global__ void k_sell_fill(const int32_t* __restrict__ rowptr, const int32_t* _
                 csr2sell[rp + k] = e;
             } else {
                 cols[e] = pad;
+            }
+        }
+    }
+}
+
+// 16-bit column deltas (col - row) of the SELL pattern; *overflow = 1 if any |delta| > 32767 (keep int32 then)
+__global__ void k_sell_delta16(const int32_t* __restrict__ cols, int64_t nslices, const int64_t* __restrict__ slice_ptr,
+                               int16_t* __restrict__ dcols, int32_t* __restrict__ overflow) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nslices * 64; r += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = r >> 6;
+        const int64_t e0 = slice_ptr[s] + (r & 63);
+        const int w = (int)((slice_ptr[s + 1] - slice_ptr[s]) >> 6);
+        for (int k = 0; k < w; ++k) {
+            const int64_t e = e0 + (int64_t)k * 64;
+            const int64_t d = (int64_t)cols[e] - r;
+            if (d > 32767 || d < -32767) {
+                atomicOr(overflow, 1);
+                dcols[e] = 0;
+            } else {
+                dcols[e] = (int16_t)d;
             }
         }
     }
@@ -200,6 +220,15 @@ int fem_graph_fill(const int64_t* conn, int npe, const int32_t* inc_ptr, const i
                    const int32_t* rowptr, int32_t* colidx, int32_t* diagpos, fem_stream_t stream) {
     hipLaunchKernelGGL(k_graph<true>, dim3(graph_grid(N)), dim3(256), 0, S(stream), conn, npe, inc_ptr, inc, N,
                        (int32_t*)nullptr, rowptr, colidx, diagpos, (int32_t*)nullptr);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_sell_delta16(const int32_t* cols, int64_t nrows, const int64_t* slice_ptr, int16_t* dcols, int32_t* overflow,
+                     fem_stream_t stream) {
+    int64_t ns = cdiv(nrows, 64);
+    hipLaunchKernelGGL(k_sell_delta16, dim3(stream_grid(ns * 64, 256)), dim3(256), 0, S(stream), cols, ns, slice_ptr,
+                       dcols, overflow);
     FEM_LAUNCHED();
     return FEM_OK;
 }

@@ -46,13 +46,15 @@ struct VecFusedP {
 // wave (cols, each of the bs*bs value planes) is one contiguous 256/512-byte segment; on meshes numbered
 // along lines the x gathers of neighbouring lanes are contiguous too. U entries per step: all U column loads,
 // then U value loads, then U gathers are in flight together; the tail step is predicated.
-template <int BS, int U, bool NT, typename X>
+// CI = int32_t: absolute block columns; CI = int16_t: 16-bit deltas col - row (half the index bytes)
+template <int BS, int U, bool NT, typename X, typename CI = int32_t>
 __device__ __forceinline__ void sell_row(int64_t s, int lane, const int64_t* __restrict__ slice_ptr,
-                                         const int32_t* __restrict__ cols, const double* __restrict__ vals,
+                                         const CI* __restrict__ cols, const double* __restrict__ vals,
                                          const X& x, double out[BS]) {
     const int64_t p0 = slice_ptr[s];
     const int w = (int)((slice_ptr[s + 1] - p0) >> 6);
-    const int32_t* c = cols + p0 + lane;
+    const CI* c = cols + p0 + lane;
+    const int base = (sizeof(CI) == 2) ? (int)(s * 64 + lane) : 0;
 #pragma unroll
     for (int r = 0; r < BS; ++r) out[r] = 0.0;
     if (BS == 1) {
@@ -61,7 +63,7 @@ __device__ __forceinline__ void sell_row(int64_t s, int lane, const int64_t* __r
             int ci[U];
             double vi[U], xi[U];
 #pragma unroll
-            for (int j = 0; j < U; ++j) ci[j] = (k0 + j < w) ? ld<int32_t, NT>(c + 64 * (k0 + j)) : 0;
+            for (int j = 0; j < U; ++j) ci[j] = (k0 + j < w) ? base + (int)ld<CI, NT>(c + 64 * (k0 + j)) : 0;
 #pragma unroll
             for (int j = 0; j < U; ++j) vi[j] = (k0 + j < w) ? ld<double, NT>(v + 64 * (k0 + j)) : 0.0;
 #pragma unroll
@@ -73,7 +75,7 @@ __device__ __forceinline__ void sell_row(int64_t s, int lane, const int64_t* __r
     } else {
         const double* v = vals + p0 * (BS * BS) + lane;
         for (int k = 0; k < w; ++k) {
-            const int64_t cc = (int64_t)ld<int32_t, NT>(c + 64 * k) * BS;
+            const int64_t cc = (int64_t)(base + (int)ld<CI, NT>(c + 64 * k)) * BS;
             double xv[BS];
 #pragma unroll
             for (int j = 0; j < BS; ++j) xv[j] = x(cc + j);
@@ -104,16 +106,16 @@ __device__ __forceinline__ SliceWalk slice_walk(int64_t nslices) {
 
 constexpr int SPMV_U = 8;   // tools/spmv_tune.py: U=8 beats 4 and 16 on the 10M Poisson matrix (gfx950)
 
-template <int BS, int U = SPMV_U, bool NT = false>
+template <int BS, int U = SPMV_U, bool NT = false, typename CI = int32_t>
 __global__ void __launch_bounds__(256) k_spmv(int64_t nslices, int64_t nrows, const int64_t* __restrict__ slice_ptr,
-                                              const int32_t* __restrict__ cols, const double* __restrict__ vals,
+                                              const CI* __restrict__ cols, const double* __restrict__ vals,
                                               const double* __restrict__ x, double* __restrict__ y) {
     const int lane = threadIdx.x & 63;
     SliceWalk wk = slice_walk(nslices);
     const VecPlain xv{x};
     for (int64_t s = wk.s; s < wk.end; s += wk.step) {
         double o[BS];
-        sell_row<BS, U, NT>(s, lane, slice_ptr, cols, vals, xv, o);
+        sell_row<BS, U, NT, VecPlain, CI>(s, lane, slice_ptr, cols, vals, xv, o);
         const int64_t row = s * 64 + lane;
         if (row < nrows) {
 #pragma unroll
@@ -219,10 +221,10 @@ struct RedBuf {
 
 // K1. FUSED: p (in p_buf[iter & 1]) is formed on the fly from r, w and the previous p (p_buf[(iter+1) & 1]);
 // this kernel also applies the deferred x += alpha_x p_prev to its own rows.
-template <int BS, bool FUSED, bool DOT = true>
+template <int BS, bool FUSED, bool DOT = true, typename CI = int32_t>
 __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_spmv_dot(int64_t nslices, int64_t nrows,
                                                             const int64_t* __restrict__ slice_ptr,
-                                                            const int32_t* __restrict__ cols,
+                                                            const CI* __restrict__ cols,
                                                             const double* __restrict__ vals, double* __restrict__ p0,
                                                             double* __restrict__ p1, const double* __restrict__ r,
                                                             const double* __restrict__ w, double* __restrict__ x,
@@ -243,7 +245,7 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_spmv_dot(int64_t nslices, int
         const VecFusedP pv{r, w, pold, beta};
         for (int64_t s = wk.s; s < wk.end; s += wk.step) {
             double o[BS];
-            sell_row<BS, SPMV_U, false>(s, lane, slice_ptr, cols, vals, pv, o);
+            sell_row<BS, SPMV_U, false, decltype(pv), CI>(s, lane, slice_ptr, cols, vals, pv, o);
             const int64_t row = s * 64 + lane;
             if (row < nrows) {
 #pragma unroll
@@ -262,7 +264,7 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_spmv_dot(int64_t nslices, int
         const VecPlain pv{p0};
         for (int64_t s = wk.s; s < wk.end; s += wk.step) {
             double o[BS];
-            sell_row<BS, SPMV_U, false>(s, lane, slice_ptr, cols, vals, pv, o);
+            sell_row<BS, SPMV_U, false, decltype(pv), CI>(s, lane, slice_ptr, cols, vals, pv, o);
             const int64_t row = s * 64 + lane;
             if (row < nrows) {
 #pragma unroll
@@ -273,12 +275,18 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_spmv_dot(int64_t nslices, int
             }
         }
     }
-    if (!DOT) return;   // distributed: q is partial on interface rows; p.q is formed after the halo sum
+    if (!DOT) return;
+    // distributed: q is this rank's partial on interface rows; p.q_partial over ALL local rows summed over the
+    // ranks is exactly p.q, so the rank sum rides in the halo all-reduce (k_halo_pack appends st->red[0])
     dot = block_sum256(dot, lds4);
     double pq;
     if (reduce_grid(dot, red.part(RED_K1), red.cnt(RED_K1), &pq, lds4, &flag) && threadIdx.x == 0) {
-        if (FUSED) st->x_done = 1;   // the pending x update was applied above by every block
-        finish_pq(st, pq);
+        if (st->dist) {
+            st->red[0] = pq;
+        } else {
+            if (FUSED) st->x_done = 1;   // the pending x update was applied above by every block
+            finish_pq(st, pq);
+        }
     }
 }
 
@@ -367,10 +375,10 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_pupdate(int64_t n, double* __
 // (identical pq everywhere), alpha + guards, r update, one r.z partial per block.  d3: every block re-sums d2's
 // partials -> stop test, beta, x/p update; block 0 writes the NEXT bank. Bank = host launch parity, so no kernel
 // writes a state field its own blocks read.
-template <int BS>
+template <int BS, typename CI = int32_t>
 __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_d1(int64_t nslices, int64_t nrows,
                                                       const int64_t* __restrict__ slice_ptr,
-                                                      const int32_t* __restrict__ cols, const double* __restrict__ vals,
+                                                      const CI* __restrict__ cols, const double* __restrict__ vals,
                                                       const double* __restrict__ p, double* __restrict__ q,
                                                       const PcgState* __restrict__ st, int par,
                                                       double* __restrict__ partials) {
@@ -383,7 +391,7 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_d1(int64_t nslices, int64_t n
     const VecPlain pv{p};
     for (int64_t s = wk.s; s < wk.end; s += wk.step) {
         double o[BS];
-        sell_row<BS, SPMV_U, false>(s, lane, slice_ptr, cols, vals, pv, o);
+        sell_row<BS, SPMV_U, false, decltype(pv), CI>(s, lane, slice_ptr, cols, vals, pv, o);
         const int64_t row = s * 64 + lane;
         if (row < nrows) {
 #pragma unroll
@@ -585,8 +593,10 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_init(int64_t n, const double*
 // over the ranks, and every rank reads the full sums back: q is then identical on all copies of a node.
 __device__ __forceinline__ bool halted(const PcgState* st) { return st && (st->halt || st->iter >= st->max_iter); }
 
+// scalar != 0: also append st->red[0] (this rank's p.q partial) at buf[nI * bs]
 __global__ void __launch_bounds__(256) k_halo_pack(const double* __restrict__ v, int bs, const int32_t* __restrict__ map,
-                                                   int64_t nI, double* __restrict__ buf, const PcgState* __restrict__ st) {
+                                                   int64_t nI, double* __restrict__ buf, const PcgState* __restrict__ st,
+                                                   int scalar) {
     if (halted(st)) return;
     for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < nI * bs; t += (int64_t)gridDim.x * 256) {
         const int64_t j = t / bs;
@@ -594,39 +604,21 @@ __global__ void __launch_bounds__(256) k_halo_pack(const double* __restrict__ v,
         const int32_t l = map[j];
         buf[t] = (l >= 0) ? v[(int64_t)l * bs + c] : 0.0;
     }
+    if (scalar && blockIdx.x == 0 && threadIdx.x == 0) buf[nI * bs] = st->red[0];
 }
 
-// v[i] <- halo sum on interface rows; DOT: partial of p.v over owned rows -> st->red[slot]
-template <bool DOT>
+// v[i] <- halo sum on interface rows; FIN: block 0 also finishes p.q (= buf[nI * bs]) into alpha / guards
+template <bool FIN>
 __global__ void __launch_bounds__(PCG_BLOCK) k_halo_unpack(int64_t nloc, int bs, const int32_t* __restrict__ pos,
                                                            const double* __restrict__ buf, double* __restrict__ v,
-                                                           const double* __restrict__ p, const uint8_t* __restrict__ own,
-                                                           PcgState* __restrict__ st, RedBuf red, int slot) {
-    __shared__ double lds4[4];
-    __shared__ int flag;
+                                                           int64_t nI, PcgState* __restrict__ st) {
     if (halted(st)) return;
-    double acc = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; i < nloc * bs; i += (int64_t)gridDim.x * PCG_BLOCK) {
         const int64_t node = i / bs;
         const int32_t j = pos[node];
-        double vi;
-        if (j >= 0) {
-            vi = buf[(int64_t)j * bs + (i - node * bs)];
-            v[i] = vi;
-        } else {
-            vi = v[i];
-        }
-        if (DOT && own[node]) acc += p[i] * vi;
+        if (j >= 0) v[i] = buf[(int64_t)j * bs + (i - node * bs)];
     }
-    if (!DOT) return;
-    acc = block_sum256(acc, lds4);
-    double tot;
-    if (reduce_grid(acc, red.part(slot), red.cnt(slot), &tot, lds4, &flag) && threadIdx.x == 0) st->red[0] = tot;
-}
-
-__global__ void k_fin_pq(PcgState* st) {
-    if (halted(st)) return;
-    finish_pq(st, st->red[0]);
+    if (FIN && blockIdx.x == 0 && threadIdx.x == 0) finish_pq(st, buf[nI * bs]);
 }
 
 __global__ void k_fin_rz(PcgState* st, double* hist, int64_t hist_len) {
@@ -675,6 +667,7 @@ struct fem_pcg {
     int fused;          // schedule 1: p formed inside the SpMV
     int deferred;       // schedule 2: partial sums finished by the next kernel (banked state)
     int64_t launched;   // iterations enqueued since start (the deferred schedule's bank parity)
+    const int16_t* cols16;  // optional 16-bit column deltas (fem_sell_delta16): used instead of cols when set
     // owned device memory
     double* r;
     double* p0;
@@ -712,12 +705,31 @@ static double* st_red(fem_pcg* s, int k) {
 }
 
 static int launch_spmv_dot(fem_pcg* s) {
+    if (s->cols16) {
+#define FEM_K1D(B, F, D)                                                                                           \
+    hipLaunchKernelGGL((k_pcg_spmv_dot<B, F, D, int16_t>), dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream,     \
+                       s->nslices, s->nrows, s->slice_ptr, s->cols16, s->vals, s->p0, s->p1, s->r, s->w, s->x, s->q, \
+                       s->st, s->red)
+        if (s->dist) {
+            if (s->bs == 1) FEM_K1D(1, false, true);
+            else FEM_K1D(3, false, true);
+        } else if (s->bs == 1) {
+            if (s->fused) FEM_K1D(1, true, true);
+            else FEM_K1D(1, false, true);
+        } else {
+            if (s->fused) FEM_K1D(3, true, true);
+            else FEM_K1D(3, false, true);
+        }
+#undef FEM_K1D
+        FEM_LAUNCHED();
+        return FEM_OK;
+    }
 #define FEM_K1(B, F, D)                                                                                            \
     hipLaunchKernelGGL((k_pcg_spmv_dot<B, F, D>), dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream, s->nslices,   \
                        s->nrows, s->slice_ptr, s->cols, s->vals, s->p0, s->p1, s->r, s->w, s->x, s->q, s->st, s->red)
     if (s->dist) {
-        if (s->bs == 1) FEM_K1(1, false, false);
-        else FEM_K1(3, false, false);
+        if (s->bs == 1) FEM_K1(1, false, true);
+        else FEM_K1(3, false, true);
     } else if (s->bs == 1) {
         if (s->fused) FEM_K1(1, true, true);
         else FEM_K1(1, false, true);
@@ -740,12 +752,13 @@ static int launch_update(fem_pcg* s) {
 static int launch_pupdate(fem_pcg* s);
 
 // ---------------------------------------------------------------- distributed iteration, phase by phase
-// iteration : [0] K1 (local A p) + pack q  | sum hbuf  | [1] unpack q + p.q (owned)     | sum red[0]
-//             [2] alpha (k_fin_pq) + K2    | sum red[1]| [3] beta/stop (k_fin_rz) + K3
+// iteration : [0] K1 (local A p, p.q partial over all local rows) + pack q and p.q | sum hbuf (nI*bs + 1)
+//             [1] unpack q, alpha + guards from the summed p.q | [2] K2 (r, r.z over owned rows) | sum red[1]
+//             [3] beta/stop (k_fin_rz) + K3                       -> two collectives per iteration
 // start     : [10] (CG: x[fixed]=0) A x + pack | sum hbuf | [11] unpack + r0, r0.z0 | sum red[2] | [12] rz
-static int halo_pack(fem_pcg* s, const double* v, bool guarded) {
-    hipLaunchKernelGGL(k_halo_pack, dim3(stream_grid(s->nI * s->bs, 256)), dim3(256), 0, s->stream, v, s->bs, s->imap,
-                       s->nI, s->hbuf, guarded ? (const PcgState*)s->st : nullptr);
+static int halo_pack(fem_pcg* s, const double* v, bool guarded, bool scalar) {
+    hipLaunchKernelGGL(k_halo_pack, dim3(stream_grid(s->nI * s->bs + 1, 256)), dim3(256), 0, s->stream, v, s->bs,
+                       s->imap, s->nI, s->hbuf, guarded ? (const PcgState*)s->st : nullptr, scalar ? 1 : 0);
     FEM_LAUNCHED();
     return FEM_OK;
 }
@@ -755,15 +768,13 @@ static int dist_phase(fem_pcg* s, int phase) {
     switch (phase) {
         case 0:
             if ((rc = launch_spmv_dot(s))) return rc;
-            return halo_pack(s, s->q, true);
+            return halo_pack(s, s->q, true, true);
         case 1:
             hipLaunchKernelGGL(k_halo_unpack<true>, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->nrows, s->bs,
-                               s->ipos, s->hbuf, s->q, s->p0, s->own, s->st, s->red, (int)RED_K1);
+                               s->ipos, s->hbuf, s->q, s->nI, s->st);
             FEM_LAUNCHED();
             return FEM_OK;
         case 2:
-            hipLaunchKernelGGL(k_fin_pq, dim3(1), dim3(1), 0, s->stream, s->st);
-            FEM_LAUNCHED();
             return launch_update(s);
         case 3:
             hipLaunchKernelGGL(k_fin_rz, dim3(1), dim3(1), 0, s->stream, s->st, s->hist, s->hist_len);
@@ -775,11 +786,12 @@ static int dist_phase(fem_pcg* s, int phase) {
                                    s->w);
                 FEM_LAUNCHED();
             }
-            if ((rc = fem_spmv(s->nrows, s->bs, s->slice_ptr, s->cols, s->vals, s->x, s->q, s->stream))) return rc;
-            return halo_pack(s, s->q, false);
+            if ((rc = (s->cols16 ? fem_spmv16(s->nrows, s->bs, s->slice_ptr, s->cols16, s->vals, s->x, s->q, s->stream)
+                          : fem_spmv(s->nrows, s->bs, s->slice_ptr, s->cols, s->vals, s->x, s->q, s->stream)))) return rc;
+            return halo_pack(s, s->q, false, false);
         case 11:
             hipLaunchKernelGGL(k_halo_unpack<false>, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->nrows, s->bs,
-                               s->ipos, s->hbuf, s->q, s->p0, s->own, (PcgState*)nullptr, s->red, (int)RED_K1);
+                               s->ipos, s->hbuf, s->q, s->nI, (PcgState*)nullptr);
             FEM_LAUNCHED();
             hipLaunchKernelGGL(k_pcg_init, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->b, s->r, s->q,
                                s->w, s->p0, s->p1, 0, s->st, s->red, s->own, s->bs);
@@ -799,12 +811,12 @@ static int dist_phase(fem_pcg* s, int phase) {
 static void dist_buffer(fem_pcg* s, int phase, double** ptr, int64_t* n) {
     *ptr = nullptr;
     *n = 0;
-    if (phase == 0 || phase == 10) {
+    if (phase == 0) {
+        *ptr = s->hbuf;
+        *n = s->nI * s->bs + 1;     // interface rows of q + this rank's p.q partial
+    } else if (phase == 10) {
         *ptr = s->hbuf;
         *n = s->nI * s->bs;
-    } else if (phase == 1) {
-        *ptr = st_red(s, 0);
-        *n = 1;
     } else if (phase == 2) {
         *ptr = st_red(s, 1);
         *n = 1;
@@ -831,13 +843,9 @@ static int dist_exchange(fem_pcg* s, int phase) {
 static int launch_exchange_dot(fem_pcg* s) {
     if (!s->dist) return FEM_OK;
     int rc;
-    if ((rc = halo_pack(s, s->q, true))) return rc;
+    if ((rc = halo_pack(s, s->q, true, true))) return rc;
     if ((rc = dist_exchange(s, 0))) return rc;
-    if ((rc = dist_phase(s, 1))) return rc;
-    if ((rc = dist_exchange(s, 1))) return rc;
-    hipLaunchKernelGGL(k_fin_pq, dim3(1), dim3(1), 0, s->stream, s->st);
-    FEM_LAUNCHED();
-    return FEM_OK;
+    return dist_phase(s, 1);
 }
 
 static int launch_pupdate(fem_pcg* s) {
@@ -862,7 +870,14 @@ static int launch_update_finish(fem_pcg* s) {
 static int launch_deferred(fem_pcg* s, int which) {
     const int par = (int)(s->launched & 1);
     if (which == 0) {
-        if (s->bs == 1)
+        if (s->cols16) {
+            if (s->bs == 1)
+                hipLaunchKernelGGL((k_pcg_d1<1, int16_t>), dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream, s->nslices,
+                                   s->nrows, s->slice_ptr, s->cols16, s->vals, s->p0, s->q, s->st, par, s->red.partials);
+            else
+                hipLaunchKernelGGL((k_pcg_d1<3, int16_t>), dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream, s->nslices,
+                                   s->nrows, s->slice_ptr, s->cols16, s->vals, s->p0, s->q, s->st, par, s->red.partials);
+        } else if (s->bs == 1)
             hipLaunchKernelGGL(k_pcg_d1<1>, dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream, s->nslices, s->nrows,
                                s->slice_ptr, s->cols, s->vals, s->p0, s->q, s->st, par, s->red.partials);
         else
@@ -925,6 +940,34 @@ int fem_spmv(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_t* col
         return FEM_EARG;
     }
     FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_spmv16(int64_t nrows, int bs, const int64_t* slice_ptr, const int16_t* dcols, const double* vals,
+               const double* x, double* y, fem_stream_t stream) {
+    const int64_t ns = cdiv(nrows, 64);
+    if (ns == 0) return FEM_OK;
+    const int grid = grid_multiple_of_xcd(cdiv(ns, 4), 2048);
+    if (bs == 1)
+        hipLaunchKernelGGL((k_spmv<1, SPMV_U, false, int16_t>), dim3(grid), dim3(256), 0, S(stream), ns, nrows,
+                           slice_ptr, dcols, vals, x, y);
+    else if (bs == 3)
+        hipLaunchKernelGGL((k_spmv<3, SPMV_U, false, int16_t>), dim3(grid), dim3(256), 0, S(stream), ns, nrows,
+                           slice_ptr, dcols, vals, x, y);
+    else {
+        set_error("fem_spmv16: block size %d unsupported", bs);
+        return FEM_EARG;
+    }
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_pcg_set_cols16(fem_pcg* s, const int16_t* dcols) {
+    if (s->graph) {
+        set_error("fem_pcg_set_cols16: drop the captured graph first");
+        return FEM_EARG;
+    }
+    s->cols16 = dcols;
     return FEM_OK;
 }
 
@@ -1086,7 +1129,8 @@ int fem_pcg_start(fem_pcg* s) {
         hipLaunchKernelGGL(k_zero_fixed, dim3(stream_grid(s->n, 256)), dim3(256), 0, s->stream, s->n, s->x, s->w);
         FEM_LAUNCHED();
     }
-    if ((rc = fem_spmv(s->nrows, s->bs, s->slice_ptr, s->cols, s->vals, s->x, s->q, s->stream))) return rc;
+    if ((rc = (s->cols16 ? fem_spmv16(s->nrows, s->bs, s->slice_ptr, s->cols16, s->vals, s->x, s->q, s->stream)
+                          : fem_spmv(s->nrows, s->bs, s->slice_ptr, s->cols, s->vals, s->x, s->q, s->stream)))) return rc;
     hipLaunchKernelGGL(k_pcg_init, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->b, s->r, s->q, s->w, s->p0,
                        s->p1, s->fused, s->st, s->red, (const uint8_t*)nullptr, s->bs);
     FEM_LAUNCHED();
@@ -1141,16 +1185,14 @@ int fem_allreduce_sum(void* comm, double* buf, int64_t n, fem_stream_t stream) {
 int fem_halo_pack(const double* v, int bs, const int32_t* imap, int64_t nI, double* buf, fem_stream_t stream) {
     if (nI <= 0) return FEM_OK;
     hipLaunchKernelGGL(k_halo_pack, dim3(stream_grid(nI * bs, 256)), dim3(256), 0, S(stream), v, bs, imap, nI, buf,
-                       (const PcgState*)nullptr);
+                       (const PcgState*)nullptr, 0);
     FEM_LAUNCHED();
     return FEM_OK;
 }
 
 int fem_halo_unpack(double* v, int bs, const int32_t* ipos, int64_t nrows, const double* buf, fem_stream_t stream) {
-    RedBuf none{nullptr, nullptr};
     hipLaunchKernelGGL(k_halo_unpack<false>, dim3(stream_grid(nrows * bs, PCG_BLOCK)), dim3(PCG_BLOCK), 0, S(stream),
-                       nrows, bs, ipos, buf, v, (const double*)nullptr, (const uint8_t*)nullptr, (PcgState*)nullptr,
-                       none, 0);
+                       nrows, bs, ipos, buf, v, (int64_t)0, (PcgState*)nullptr);
     FEM_LAUNCHED();
     return FEM_OK;
 }
@@ -1177,7 +1219,7 @@ int fem_pcg_set_dist(fem_pcg* s, int enable, void* comm, int64_t nI, const int32
     s->imap = imap;
     s->ipos = ipos;
     s->own = own;
-    if (enable) FEM_HIP(hipMalloc(&s->hbuf, sizeof(double) * (size_t)((nI > 0 ? nI : 1) * s->bs)));
+    if (enable) FEM_HIP(hipMalloc(&s->hbuf, sizeof(double) * (size_t)(nI * s->bs + 1)));
     return FEM_OK;
 }
 

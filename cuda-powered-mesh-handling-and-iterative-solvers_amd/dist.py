@@ -7,8 +7,9 @@ of `subdivision.ipynb:194-297` (global->local node maps by `torch.unique`, `:254
   * every rank keeps the GLOBAL node ids of its elements (`torch.unique`, sorted, as `subdivision.ipynb:254-259`),
     assembles the SELL matrix of its own elements over them (unassembled at shared nodes), and knows the global
     interface list (nodes touched by several ranks) and which rows it owns (lowest rank touching the node);
-  * per iteration: halo all-reduce of A p on the compact interface vector, p.q and r.z over owned rows with one
-    scalar all-reduce each (csrc/pcg.hip, distributed phases). All ranks hold bit-identical copies of shared dofs.
+  * per iteration: ONE all-reduce of [interface rows of A p | p.q partial] (each rank's p . q_rank over all its
+    local rows: the rank sum is p.q) and one scalar all-reduce of r.z over owned rows (csrc/pcg.hip, distributed
+    phases). All ranks hold bit-identical copies of shared dofs.
 
 The partition/halo bookkeeping is plain torch index work run on the mesh's device; it is also exercised on CPU by
 tests/test_dist_cpu.py (gloo, world size 2) against the oracle. The RCCL communicator is created in the C-ABI
@@ -160,7 +161,7 @@ class DistSystem:
         return DistRunner(self, b, w, tol, mode, hist_len)
 
 
-class DistRunner(_sys.PcgRunner):
+class DistRunner(_sys._DistMarker, _sys.PcgRunner):
     """(P)CG context of one rank in distributed mode."""
 
     def __init__(self, ds: DistSystem, b, w, tol, mode, hist_len=0):
@@ -257,6 +258,7 @@ class _GroupRunner:
                                         C.ptr(self.b), C.ptr(self.x), C.ptr(self.w), mode, float(tol), 1e-30, None,
                                         0, C.stream(A.device), ctypes.byref(self.h)), "fem_pcg_create")
         C.check(self.lib.fem_pcg_set_schedule(self.h, 0), "fem_pcg_set_schedule")
+        A.attach_cols16(self.h)
         C.check(self.lib.fem_pcg_set_dist(self.h, 1, None, ds.rm.n_iface, C.ptr(ds.rm.imap), C.ptr(ds.rm.ipos),
                                           C.ptr(ds.rm.own)), "fem_pcg_set_dist")
 

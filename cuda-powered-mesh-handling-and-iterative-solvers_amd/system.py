@@ -24,13 +24,15 @@ def _dev_scalar(dev, dtype, value):
 # (P)CG kernel schedules (csrc/pcg.hip): 0 = three kernels with in-kernel grid reductions, 1 = fused (p formed
 # inside the SpMV), 2 = deferred (partials summed by the next kernel, no grid atomics)
 SCHED_THREE, SCHED_FUSED, SCHED_DEFERRED = 0, 1, 2
-DEFAULT_SCHEDULE = SCHED_THREE
+# measured on MI355X (tools/spmv_tune.py, 10M-tet cube, 16-bit columns): scalar Poisson 0.0925 ms/it deferred vs
+# 0.0947 three-kernel; 3x3 elasticity 0.437 three-kernel vs 0.454 deferred
+DEFAULT_SCHEDULE = {1: SCHED_DEFERRED, 3: SCHED_THREE}
 
 
-def _schedule(fused, schedule):
+def _schedule(fused, schedule, bs=1):
     if schedule is not None:
         return int(schedule)
-    return SCHED_FUSED if fused else DEFAULT_SCHEDULE
+    return SCHED_FUSED if fused else DEFAULT_SCHEDULE.get(bs, SCHED_THREE)
 
 
 @dataclass
@@ -56,6 +58,7 @@ class Graph:
     slice_ptr: torch.Tensor
     cols: torch.Tensor
     csr2sell: torch.Tensor
+    dcols: torch.Tensor = None   # int16 col - row deltas, or None when the bandwidth exceeds 32767
 
     @property
     def nnz(self):
@@ -79,9 +82,10 @@ def incidence(elements: torch.Tensor, n_nodes: int):
     return inc_ptr, inc
 
 
-def build_graph(elements: torch.Tensor, n_nodes: int) -> Graph:
+def build_graph(elements: torch.Tensor, n_nodes: int, compress: bool = True) -> Graph:
     """Node-graph CSR + SELL-64 pattern of `elements` (one element family, int64 [M, npe] on the device).
-    The rows are the coalesced pattern of the reference's COO assembly (`subdivision.ipynb:118-139`)."""
+    The rows are the coalesced pattern of the reference's COO assembly (`subdivision.ipynb:118-139`).
+    compress: also derive 16-bit column deltas (used by the SpMV when every |col - row| <= 32767)."""
     lib = C.lib()
     dev = elements.device
     elements = elements.contiguous()
@@ -114,7 +118,15 @@ def build_graph(elements: torch.Tensor, n_nodes: int) -> Graph:
     csr2sell = torch.empty(max(nnz, 1), dtype=I64, device=dev)
     C.check(lib.fem_sell_fill(C.ptr(rowptr), C.ptr(colidx), n_nodes, C.ptr(slice_ptr), C.ptr(cols),
                               C.ptr(csr2sell), st), "fem_sell_fill")
-    return Graph(n_nodes, npe, inc_ptr, inc, rowptr, colidx, diagpos, slice_ptr, cols, csr2sell)
+    g = Graph(n_nodes, npe, inc_ptr, inc, rowptr, colidx, diagpos, slice_ptr, cols, csr2sell)
+    if compress:
+        dcols = torch.empty(max(ent, 1), dtype=torch.int16, device=dev)
+        ovf = torch.zeros(1, dtype=I32, device=dev)
+        C.check(lib.fem_sell_delta16(C.ptr(cols), n_nodes, C.ptr(slice_ptr), C.ptr(dcols), C.ptr(ovf), st),
+                "fem_sell_delta16")
+        if int(ovf.item()) == 0:
+            g.dcols = dcols
+    return g
 
 
 def pad_connectivity(blocks, npe_max):
@@ -136,6 +148,7 @@ class SellMatrix:
         self.bs = bs
         self.device = graph.cols.device
         self.vals = torch.zeros(max(graph.sell_entries, 1) * bs * bs, dtype=F64, device=self.device)
+        self.use16 = graph.dcols is not None   # 16-bit column deltas in every SpMV of this matrix
 
     @property
     def n_rows(self):
@@ -184,9 +197,18 @@ class SellMatrix:
         lib = C.lib()
         x = x.to(F64).contiguous()
         y = out if out is not None else torch.empty(self.n, dtype=F64, device=self.device)
-        C.check(lib.fem_spmv(self.g.n_nodes, self.bs, C.ptr(self.g.slice_ptr), C.ptr(self.g.cols),
-                             C.ptr(self.vals), C.ptr(x), C.ptr(y), C.stream(self.device)), "fem_spmv")
+        if self.use16:
+            C.check(lib.fem_spmv16(self.g.n_nodes, self.bs, C.ptr(self.g.slice_ptr), C.ptr(self.g.dcols),
+                                   C.ptr(self.vals), C.ptr(x), C.ptr(y), C.stream(self.device)), "fem_spmv16")
+        else:
+            C.check(lib.fem_spmv(self.g.n_nodes, self.bs, C.ptr(self.g.slice_ptr), C.ptr(self.g.cols),
+                                 C.ptr(self.vals), C.ptr(x), C.ptr(y), C.stream(self.device)), "fem_spmv")
         return y
+
+    def attach_cols16(self, h):
+        """Point a (P)CG context at the 16-bit column deltas when this matrix uses them."""
+        if self.use16:
+            C.check(C.lib().fem_pcg_set_cols16(h, C.ptr(self.g.dcols)), "fem_pcg_set_cols16")
 
     def jacobi(self, fixed_mask: torch.Tensor = None):
         """w = 1/diag(A) (inf -> 0), zero on fixed DOFs (uint8 mask [n])."""
@@ -206,13 +228,12 @@ class SellMatrix:
                                          C.stream(self.device)), "fem_sell_to_csr_vals")
         return self.g.rowptr, self.g.colidx, out[: self.g.nnz * self.bs * self.bs].view(-1, self.bs, self.bs)
 
-    def algorithmic_bytes_spmv(self):
-        """HBM bytes one SpMV must move: 12 nnz + 4 (n+1) + 16 n for scalar CSR,
-        76 nnzb + 4 (nb+1) + 16 n for 3x3 blocks (fp64 values, int32 indices)."""
+    def algorithmic_bytes_spmv(self, index_bytes=None):
+        """HBM bytes one SpMV must move (SURVEY §8(d)): (8 bs^2 + idx) nnzb + 4 (nb+1) + 16 n, fp64 values;
+        idx = 4 for int32 columns (the survey's 12 nnz + 4(n+1) + 16 n for bs=1), 2 for 16-bit deltas."""
+        idx = index_bytes if index_bytes is not None else (2 if self.use16 else 4)
         nnzb, nb = self.g.nnz, self.g.n_nodes
-        if self.bs == 1:
-            return 12 * nnzb + 4 * (nb + 1) + 16 * nb
-        return (8 * self.bs * self.bs + 4) * nnzb + 4 * (nb + 1) + 16 * nb * self.bs
+        return (8 * self.bs * self.bs + idx) * nnzb + 4 * (nb + 1) + 16 * nb * self.bs
 
     # ---------------------------------------------------------------- solver
     def pcg(self, b, x0=None, w=None, mode=C.MODE_PCG, tol=1e-8, max_iter=1000, eps=1e-30, history=False,
@@ -230,7 +251,8 @@ class SellMatrix:
                                    C.ptr(hist), hist.numel() if hist is not None else 0, C.stream(self.device),
                                    ctypes.byref(h)), "fem_pcg_create")
         try:
-            C.check(lib.fem_pcg_set_schedule(h, _schedule(fused, schedule)), "fem_pcg_set_schedule")
+            C.check(lib.fem_pcg_set_schedule(h, _schedule(fused, schedule, self.bs)), "fem_pcg_set_schedule")
+            self.attach_cols16(h)
             it, stt, rz = ctypes.c_int(), ctypes.c_int(), ctypes.c_double()
             C.check(lib.fem_pcg_solve(h, int(max_iter), int(chunk), ctypes.byref(it), ctypes.byref(stt),
                                       ctypes.byref(rz)), "fem_pcg_solve")
@@ -241,6 +263,10 @@ class SellMatrix:
         if hist is not None:
             hist = hist[: min(it.value, hist.numel())]
         return PcgResult(x, it.value, stt.value, rz.value, sc[1], hist)
+
+
+class _DistMarker:
+    """Mixin marking distributed runners (they run the 3-kernel schedule)."""
 
 
 class PcgRunner:
@@ -262,7 +288,9 @@ class PcgRunner:
                                         C.ptr(self.b), C.ptr(self.x), C.ptr(self.w), mode, float(tol), float(eps),
                                         None, 0, ctypes.c_void_p(self.stream.cuda_stream), ctypes.byref(self.h)),
                 "fem_pcg_create")
-        C.check(self.lib.fem_pcg_set_schedule(self.h, _schedule(fused, schedule)), "fem_pcg_set_schedule")
+        self.schedule = 0 if isinstance(self, _DistMarker) else _schedule(fused, schedule, A.bs)
+        C.check(self.lib.fem_pcg_set_schedule(self.h, self.schedule), "fem_pcg_set_schedule")
+        A.attach_cols16(self.h)
 
     def finish(self):
         C.check(self.lib.fem_pcg_finish(self.h), "fem_pcg_finish")

@@ -169,6 +169,13 @@ int fem_invert_diag(const double* in, int64_t n, double* out, fem_stream_t strea
  * y = A x on the SELL-64 matrix (nrows block rows of size bs). */
 int fem_spmv(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_t* cols, const double* vals,
              const double* x, double* y, fem_stream_t stream);
+/* 16-bit column deltas: dcols[e] = cols[e] - row (SELL layout); *overflow [device int32, zeroed] = 1 when a
+ * delta exceeds +-32767 (then keep the int32 columns). Halves the index stream of every SpMV: 10 instead of
+ * 12 bytes per scalar nonzero on banded (e.g. line-numbered or RCM-ordered) meshes. */
+int fem_sell_delta16(const int32_t* cols, int64_t nrows, const int64_t* slice_ptr, int16_t* dcols, int32_t* overflow,
+                     fem_stream_t stream);
+int fem_spmv16(int64_t nrows, int bs, const int64_t* slice_ptr, const int16_t* dcols, const double* vals,
+               const double* x, double* y, fem_stream_t stream);
 /* tuning / measurement entry points (tools/spmv_tune.py): SpMV code variants and grid size (grid <= 0:
  * default), and the HBM copy-ceiling probe dst = src over n doubles (n even, 16-byte aligned). */
 int fem_spmv_variant(int variant, int grid, int64_t nrows, int bs, const int64_t* slice_ptr, const int32_t* cols,
@@ -202,6 +209,8 @@ int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, 
 /* kernel schedule: 0 = 3-kernel (default, faster on gfx950), 1 = fused (p formed inside the SpMV from r, w and
  * the previous p at every gathered column; 2 kernels per iteration, 88n instead of 96n vector bytes) */
 int fem_pcg_set_schedule(fem_pcg* s, int fused);
+/* run the SpMV of this context on 16-bit column deltas (NULL: back to the int32 columns) */
+int fem_pcg_set_cols16(fem_pcg* s, const int16_t* dcols);
 /* apply the deferred x update of the fused schedule after the last iteration (fem_pcg_solve does this) */
 int fem_pcg_finish(fem_pcg* s);
 /* capture `k` iterations in a hipGraph and use it for fem_pcg_iterate calls with that k (0 disables) */
@@ -217,8 +226,9 @@ void fem_pcg_destroy(fem_pcg* s);
  * nodes shared with other ranks) and the global interface list: imap [nI] = local row of global interface node j
  * (-1 if the rank has no copy), ipos [nrows] = interface index of a local row (-1 interior), own [nrows] = 1 on
  * the rows the rank owns (owner = lowest rank touching the node). Each iteration then adds, on the device
- * stream: halo all-reduce of the compact interface vector of A p (nI*bs doubles), p.q over owned rows and its
- * scalar all-reduce, r.z and its scalar all-reduce. The reference has no multi-device code; this replaces its
+ * stream: ONE all-reduce of the compact interface vector of A p (nI*bs doubles) with this rank's p.q partial
+ * appended (p . q_rank over all local rows sums to p.q exactly), and one scalar all-reduce of r.z over owned
+ * rows. The reference has no multi-device code; this replaces its
  * single-GPU region-growing split (`subdivision.ipynb:194-297`) with a deterministic partition.
  *   fem_comm_unique_id: [host] 128-byte RCCL id from rank 0 (broadcast it with any host transport)
  *   fem_comm_init     : [sync] communicator of this rank on the current HIP device */
@@ -236,8 +246,8 @@ int fem_halo_sum(void* comm, double* v, int bs, const int32_t* imap, int64_t nI,
 int fem_pcg_set_dist(fem_pcg* s, int enable, void* comm, int64_t nI, const int32_t* imap, const int32_t* ipos,
                      const uint8_t* own);
 /* Phase-driven distributed iteration (what fem_pcg_start/iterate do around ncclAllReduce): phases 10, 11, 12
- * start the solve, phases 0..3 are one iteration; after phases 10, 0, 11, 1, 2 the buffer reported by
- * fem_pcg_dist_buffer must be summed over all ranks. Used to validate the distributed kernels with several
+ * start the solve, phases 0..3 are one iteration; after a phase whose fem_pcg_dist_buffer is non-empty (10, 11:
+ * start; 0: interface rows of A p + the p.q partial; 2: the r.z partial) that buffer must be summed over all ranks. Used to validate the distributed kernels with several
  * partitions in ONE process on one GPU (RCCL refuses two ranks on one device). */
 int fem_pcg_dist_phase(fem_pcg* s, int phase);
 int fem_pcg_dist_buffer(fem_pcg* s, int phase, double** ptr, int64_t* n);

@@ -145,6 +145,32 @@ def test_fused_tet4_assembly_matches_element_path(gpu):
         assert rel(A.matvec(xx.to(gpu)), y_ref) < 1e-12, kind
 
 
+def test_cols16_matches_int32_and_falls_back(gpu):
+    _, mesh, _, system = _mods()
+    c, t = mesh.kuhn_cube(12, jitter=0.1)
+    for kind, bs in (("poisson", 1), ("elastic", 3)):
+        A = system.assemble_tet4_system(c.to(gpu), t.to(gpu), kind, 1.0 if bs == 1 else E, NU)
+        assert A.use16
+        x = torch.randn(A.n, dtype=F64, device=gpu)
+        y16 = A.matvec(x)
+        A.use16 = False
+        y32 = A.matvec(x)
+        assert torch.equal(y16, y32)     # same arithmetic, only the index encoding differs
+        A.use16 = True
+        assert A.algorithmic_bytes_spmv() < A.algorithmic_bytes_spmv(index_bytes=4)
+    # a random node numbering on a 35,937-node mesh has |col - row| > 32767 somewhere -> int32 columns
+    c, t = mesh.kuhn_cube(32)
+    perm = torch.randperm(c.shape[0], generator=torch.Generator().manual_seed(3))
+    inv = torch.empty_like(perm)
+    inv[perm] = torch.arange(perm.numel())
+    cp, tp = c[perm], inv[t]
+    A = system.assemble_tet4_system(cp.to(gpu), tp.to(gpu), "poisson")
+    assert not A.use16
+    Ko = R.tet4_poisson_K(cp, tp)
+    x = torch.randn(A.n, dtype=F64)
+    assert rel(A.matvec(x.to(gpu)), R.nodal_forces(Ko, tp, x.view(-1, 1)).view(-1)) < 1e-12
+
+
 def test_spmv_large_cube_properties(gpu):
     """Full-size check without the oracle: the assembled Laplacian annihilates constants and is symmetric
     in the bilinear sense x.Ay == y.Ax (10M-tet scale runs in bench.py; here n=60)."""

@@ -66,6 +66,17 @@ def main():
                 torch.cuda.synchronize()
                 assert float((y - ref).abs().max()) <= 1e-12 * float(ref.abs().max()), v
     print(json.dumps({"stage": "variants"}), flush=True)
+    if A.g.dcols is not None:
+        t16 = []
+        for r in range(a.rounds):
+            def f16():
+                C.check(lib.fem_spmv16(A.g.n_nodes, A.bs, C.ptr(A.g.slice_ptr), C.ptr(A.g.dcols), C.ptr(A.vals),
+                                       C.ptr(x), C.ptr(y), st), "spmv16")
+            f16()
+            t16.append(timed(f16, a.reps))
+        alg16 = A.algorithmic_bytes_spmv(index_bytes=2)
+        med = sorted(t16)[len(t16) // 2]
+        out["spmv16_ms"] = {"min": min(t16), "med": med, "GBps_med": alg16 / (med * 1e-3) / 1e9, "alg_bytes": alg16}
     out["spmv_ms"] = {k: {"min": min(v), "med": sorted(v)[len(v) // 2],
                           "GBps_med": alg / (sorted(v)[len(v) // 2] * 1e-3) / 1e9} for k, v in res.items()}
     # HBM copy ceiling on 2 x 1 GiB
