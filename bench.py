@@ -2,13 +2,15 @@
 """fem355 benchmark: BASELINE.json metric "CG iterations/sec + DOFs/sec (assembly+solve), 10M P1-tet Poisson".
 
 Workload: Kuhn-cube mesh n=119 -> 10,110,954 P1 tets, 1,728,000 nodes/DOFs, scalar Poisson
-(kappa=1), z=0 face Dirichlet, unit nodal source; fp64 values, int32 indices, SELL-64 global matrix.
+(kappa=1), z=0 face Dirichlet, unit nodal source; fp64 values, SELL-64 global matrix with 16-bit column deltas
+(int32 columns when a delta does not fit).
   * a "step" = one Jacobi-PCG iteration (SpMV + 2 dots + vector updates) on that system, tol=0 (no early exit);
     `value` = steps/s of the whole job (for N>1: the same global system element-partitioned over the ranks,
     strong scaling), measured between barrier+synchronize brackets, max over ranks.
   * DOFs/s = n_DOF / (assembly incl. pattern build + PCG solve to rtol 1e-8 on sqrt(r.z)), reported beside.
-  * roofline: the SpMV+p.Ap kernel, algorithmic bytes 12 nnz + 4 (n+1) + 16 n per launch (§8(d)) over its
-    average device time, sampled live with hip events on the solver stream inside the timed region.
+  * roofline: the SpMV+p.Ap kernel (k_pcg_d1 in the default deferred schedule), algorithmic bytes
+    (8 + idx) nnz + 4 (n+1) + 16 n per launch (§8(d); idx = 2 for 16-bit deltas, 4 for int32) over its average
+    device time, sampled live with hip events on the solver stream inside the timed region.
   * cpu_baseline: the oracle (torch-CPU restatement of the reference's EBE PCG, oracle/ref_cpu.py) timed on the
     host cores on a bounded sample (assembly + a few iterations of the same 10M system), rank 0 at N=1 only.
 
@@ -147,6 +149,8 @@ def main():
     dt = time.perf_counter() - t0
     it, stt, _ = run.poll()
     assert it == a.warmup + a.steps, (it, stt)
+    kernel = {system.SCHED_THREE: "k_pcg_spmv_dot", system.SCHED_FUSED: "k_pcg_spmv_dot<FUSED>",
+              system.SCHED_DEFERRED: "k_pcg_d1"}[run.schedule]
     run.close()
 
     spmv_ms = ms[0] / max(cnt[0], 1)
@@ -167,7 +171,7 @@ def main():
         "dtype": "f64",
         "data": "synthetic",
         "config": {"workload": f"{M:,}-tet P1 {a.kind} Kuhn cube n={a.n}, Jacobi-PCG fixed iterations",
-                   "tets": M, "nodes": N, "dofs": A.n, "nnz_blocks": A.g.nnz, "format": "SELL-64 fp64 values, int32 cols",
+                   "tets": M, "nodes": N, "dofs": A.n, "nnz_blocks": A.g.nnz, "format": "SELL-64 fp64 values, " + ("int16 column deltas" if A.use16 else "int32 cols"),
                    "parallelism": "single GPU"},
         "dofs_per_s": A.n / (t_asm + t_solve),
         "assembly_ms": t_asm * 1e3,
@@ -178,7 +182,7 @@ def main():
                       "sampled_launches": cnt[0]},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic_from_profiles(workload_key),
-                     "kernel": "k_pcg_spmv_dot", "algorithmic_bytes": alg},
+                     "kernel": kernel, "algorithmic_bytes": alg},
         "cpu_baseline": None,
     }
     if not a.no_cpu_baseline and rank == 0:

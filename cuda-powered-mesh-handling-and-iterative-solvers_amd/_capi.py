@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("FEM355_LIB", os.path.join(PKG_DIR, "lib", "libfem355.
 
 FEM_OK, FEM_EBADTYPE, FEM_ESINGULAR, FEM_EHIP, FEM_ERCCL, FEM_EARG = range(6)
 PCG_RUNNING, PCG_CONVERGED, PCG_MAXITER, PCG_BREAKDOWN, PCG_ALPHA_NAN, PCG_BETA_NAN = range(6)
-MODE_CG_STABLE, MODE_PCG = 0, 1
+MODE_CG_STABLE, MODE_PCG, MODE_CG_CONSTRAINED = 0, 1, 2
 KIND_ELASTIC, KIND_POISSON, KIND_MASS = 0, 1, 2
 ISO_SUM, ISO_STACK, ISO_VOLUME = 0, 1, 2
 
@@ -64,6 +64,8 @@ SIGNATURES = {
     "fem_pcg_solve": (_I, [_P, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_D)]),
     "fem_pcg_use_graph": (_I, [_P, _I]),
     "fem_pcg_set_schedule": (_I, [_P, _I]),
+    "fem_pcg_set_constraints": (_I, [_P, _I, _L, _P, _P, _L, _P, _P, _L, _P, _P, _P, _P, _P]),
+    "fem_enforce_constraints": (_I, [_P, _P, _L, _I, _L, _P, _P, _L, _P, _P, _L, _P, _P, _P, _P, _P, _P]),
     "fem_pcg_finish": (_I, [_P]),
     "fem_pcg_profile": (_I, [_P, _I, _I, ctypes.POINTER(_D), ctypes.POINTER(_I)]),
     "fem_pcg_destroy": (None, [_P]),

@@ -166,7 +166,7 @@ enum { RED_K1 = 0, RED_K2 = 1, RED_INIT = 2, RED_N = 3 };
 // alpha and the breakdown guards from p.Ap (`solver/solver.py:185-198` / `:800`)
 __device__ __forceinline__ void finish_pq(PcgState* st, double pq) {
     st->pq = pq;
-    if (st->mode == FEM_MODE_CG_STABLE) {
+    if (st->mode != FEM_MODE_PCG) {
         if (fabs(pq) < st->eps || pq < 0.0) {                 // `solver/solver.py:187`
             st->status = FEM_PCG_BREAKDOWN;
             st->halt = 1;
@@ -187,7 +187,7 @@ __device__ __forceinline__ void finish_pq(PcgState* st, double pq) {
 
 // stop test and beta from the new r.z (`solver/solver.py:208-222` / `:804-809`)
 __device__ __forceinline__ void finish_rz(PcgState* st, double rz_new, double* hist, int64_t hist_len) {
-    const bool cg = st->mode == FEM_MODE_CG_STABLE;
+    const bool cg = st->mode != FEM_MODE_PCG;
     const int it = st->iter;
     st->rz_new = rz_new;
     st->xupd = 1;
@@ -301,7 +301,7 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update(int64_t n, double* __r
     __shared__ int flag;
     if (st->halt || st->iter >= st->max_iter) return;
     const double alpha = st->alpha;
-    const bool cg = st->mode == FEM_MODE_CG_STABLE;
+    const bool cg = st->mode != FEM_MODE_PCG;
     double acc = 0.0;
     const int64_t n2 = n >> 1;
     const double2* q2 = reinterpret_cast<const double2*>(q);
@@ -419,7 +419,7 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_d2(int64_t n, double* __restr
     PcgState::Bank& bk = st->bank[par];
     if (bk.halt || bk.iter >= st->max_iter) return;
     const double pq = sum_prev_partials(part1, n1, lds4);
-    const bool cg = st->mode == FEM_MODE_CG_STABLE;
+    const bool cg = st->mode != FEM_MODE_PCG;
     double alpha = 0.0;
     int stop = 0;
     if (cg) {
@@ -492,7 +492,7 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_d3(int64_t n, double* __restr
         return;
     }
     const double rz_new = sum_prev_partials(part2, n2p, lds4);
-    const bool cg = st->mode == FEM_MODE_CG_STABLE;
+    const bool cg = st->mode != FEM_MODE_PCG;
     const double nrm = sqrt(rz_new);
     const bool conv = nrm < st->tol;                                             // `:210` / `:805`
     double beta = 0.0;
@@ -564,7 +564,7 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_init(int64_t n, const double*
                                                         const uint8_t* __restrict__ own, int bs) {
     __shared__ double lds4[4];
     __shared__ int flag;
-    const bool cg = st->mode == FEM_MODE_CG_STABLE;
+    const bool cg = st->mode != FEM_MODE_PCG;
     double acc = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * PCG_BLOCK) {
         double rv = b[i] - q[i];
@@ -634,6 +634,101 @@ __global__ void k_bank_init(PcgState* st) {
     st->bank[0].rz_new = st->rz;
 }
 
+// ---------------------------------------------------------------- constraint projections (CG_CONSTRAINED)
+// `enforce_constraints` (`solver/solver.py:478-510`: RBE2 then SPC) and `new_enforce_constraints` (`:665-700`:
+// SPC, RBE2, then RBE3 sets in order) on the displacement after every update; the r-zeroing of SPC dofs and RBE2
+// slaves is the 0/1 mask w of the CG. One 256-thread block, phases separated by barriers so that each step sees the
+// previous one, RBE2 as gather-then-scatter (the reference's vectorised assignment), RBE3 groups sequential with a
+// fixed-order block sum. `always` = 1 at start (the reference enforces once before the loop).
+struct Constraints {
+    int64_t R, S, G;
+    const int64_t* rbe2_slave;   // [R] dofs
+    const int64_t* rbe2_master;  // [R]
+    double* tmp;                 // [R]
+    const int64_t* spc_dof;      // [S]
+    const double* spc_val;       // [S]
+    const int64_t* r3_ptr;       // [G+1] entry ranges of the groups (set-major, dof ascending)
+    const int64_t* r3_master;    // [G] master dof of the group
+    const double* r3_wsum;       // [G] weight sum of the group's set
+    const int64_t* r3_slave;     // [E] slave dofs
+    const double* r3_w;          // [E]
+    int order;                   // 0: RBE2, SPC (constrained_cg) ; 1: SPC, RBE2, RBE3 (new_constrained_cg)
+};
+
+// r (nullable): also zero the residual at SPC dofs and RBE2 slaves (the standalone enforce_* entry point; inside
+// the CG that masking is the weight vector w)
+// parts: bit 0 = the SPC / RBE2 copies, bit 1 = the RBE3 means (large SPC / RBE2 sets run as grid kernels)
+__global__ void __launch_bounds__(256) k_constraints(double* __restrict__ x, double* __restrict__ r, Constraints c,
+                                                     const PcgState* st, int always, int parts) {
+    __shared__ double lds4[4];
+    if (!always && !st->xupd) return;
+    if (!(parts & 1)) c.R = c.S = 0;
+    if (!(parts & 2)) c.G = 0;
+    const int t0 = threadIdx.x;
+    auto rbe2 = [&]() {
+        for (int64_t t = t0; t < c.R; t += 256) c.tmp[t] = x[c.rbe2_master[t]];
+        __syncthreads();
+        for (int64_t t = t0; t < c.R; t += 256) {
+            x[c.rbe2_slave[t]] = c.tmp[t];
+            if (r) r[c.rbe2_slave[t]] = 0.0;
+        }
+        __syncthreads();
+    };
+    auto spc = [&]() {
+        for (int64_t t = t0; t < c.S; t += 256) {
+            x[c.spc_dof[t]] = c.spc_val[t];
+            if (r) r[c.spc_dof[t]] = 0.0;
+        }
+        __syncthreads();
+    };
+    if (c.order == 0) {
+        rbe2();
+        spc();
+    } else {
+        spc();
+        rbe2();
+        for (int64_t g = 0; g < c.G; ++g) {
+            double v = 0.0;
+            for (int64_t e = c.r3_ptr[g] + t0; e < c.r3_ptr[g + 1]; e += 256) v += c.r3_w[e] * x[c.r3_slave[e]];
+            v = block_sum256(v, lds4);
+            if (t0 == 0) x[c.r3_master[g]] = v / (c.r3_wsum[g] + 1e-30);   // `:697-698`
+            __syncthreads();
+        }
+    }
+}
+
+// grid-wide variants of the two copy phases for large sets (one launch each keeps gather-before-scatter and the
+// reference's phase order)
+enum { CON_GATHER = 0, CON_SCATTER = 1, CON_SPC = 2 };
+template <int PH>
+__global__ void __launch_bounds__(256) k_con_phase(double* __restrict__ x, double* __restrict__ r, Constraints c,
+                                                   const PcgState* st, int always) {
+    if (!always && !st->xupd) return;
+    const int64_t m = PH == CON_SPC ? c.S : c.R;
+    for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < m; t += (int64_t)gridDim.x * 256) {
+        if (PH == CON_GATHER) {
+            c.tmp[t] = x[c.rbe2_master[t]];
+        } else if (PH == CON_SCATTER) {
+            x[c.rbe2_slave[t]] = c.tmp[t];
+            if (r) r[c.rbe2_slave[t]] = 0.0;
+        } else {
+            x[c.spc_dof[t]] = c.spc_val[t];
+            if (r) r[c.spc_dof[t]] = 0.0;
+        }
+    }
+}
+
+// set-up validation of caller index arrays (a bad index would otherwise be an out-of-bounds store)
+__global__ void k_check_range(const int64_t* __restrict__ v, int64_t m, int64_t lo, int64_t hi, int* __restrict__ bad) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
+        if (v[i] < lo || v[i] >= hi) atomicOr(bad, 1);
+}
+
+__global__ void k_check_ptr(const int64_t* __restrict__ ptr, int64_t g, int* __restrict__ bad) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < g; i += (int64_t)gridDim.x * blockDim.x)
+        if (ptr[i + 1] < ptr[i] || (i == 0 && ptr[0] != 0)) atomicOr(bad, 1);
+}
+
 // HBM ceiling probe: dst = src, 16 B per lane, grid-stride (the measured "STREAM copy" roof of SURVEY §8(d))
 __global__ void __launch_bounds__(256) k_stream_copy(const double2* __restrict__ src, double2* __restrict__ dst,
                                                      int64_t n2) {
@@ -668,6 +763,8 @@ struct fem_pcg {
     int deferred;       // schedule 2: partial sums finished by the next kernel (banked state)
     int64_t launched;   // iterations enqueued since start (the deferred schedule's bank parity)
     const int16_t* cols16;  // optional 16-bit column deltas (fem_sell_delta16): used instead of cols when set
+    int has_con;            // CG_CONSTRAINED projections set (fem_pcg_set_constraints)
+    Constraints con;
     // owned device memory
     double* r;
     double* p0;
@@ -848,11 +945,43 @@ static int launch_exchange_dot(fem_pcg* s) {
     return dist_phase(s, 1);
 }
 
+// projections on x: one block for small sets, else gather / scatter / SPC grid phases (+ one block for RBE3)
+static const int64_t CON_SMALL = 8192;
+static int launch_constraints(hipStream_t stream, double* x, double* r, const Constraints& c, const PcgState* st,
+                              int always) {
+    if (c.R + c.S <= CON_SMALL) {
+        hipLaunchKernelGGL(k_constraints, dim3(1), dim3(256), 0, stream, x, r, c, st, always, 3);
+        FEM_LAUNCHED();
+        return FEM_OK;
+    }
+    auto phase = [&](int ph) {
+        const int64_t m = ph == CON_SPC ? c.S : c.R;
+        if (m == 0) return;
+        const dim3 g(stream_grid(m, 256));
+        if (ph == CON_GATHER) hipLaunchKernelGGL(k_con_phase<CON_GATHER>, g, dim3(256), 0, stream, x, r, c, st, always);
+        if (ph == CON_SCATTER) hipLaunchKernelGGL(k_con_phase<CON_SCATTER>, g, dim3(256), 0, stream, x, r, c, st, always);
+        if (ph == CON_SPC) hipLaunchKernelGGL(k_con_phase<CON_SPC>, g, dim3(256), 0, stream, x, r, c, st, always);
+    };
+    if (c.order == 0) {
+        phase(CON_GATHER);
+        phase(CON_SCATTER);
+        phase(CON_SPC);
+    } else {
+        phase(CON_SPC);
+        phase(CON_GATHER);
+        phase(CON_SCATTER);
+        if (c.G) hipLaunchKernelGGL(k_constraints, dim3(1), dim3(256), 0, stream, x, r, c, st, always, 2);
+    }
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
 static int launch_pupdate(fem_pcg* s) {
     if (s->fused) return FEM_OK;
     hipLaunchKernelGGL(k_pcg_pupdate, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->x, s->p0, s->r, s->w,
                        s->st);
     FEM_LAUNCHED();
+    if (s->has_con) return launch_constraints(s->stream, s->x, nullptr, s->con, s->st, 0);
     return FEM_OK;
 }
 
@@ -962,6 +1091,105 @@ int fem_spmv16(int64_t nrows, int bs, const int64_t* slice_ptr, const int16_t* d
     return FEM_OK;
 }
 
+// validate the caller's constraint arrays against [0, n) on `stream` (one sync) and fill c (tmp not allocated)
+static int make_constraints(const char* fn, int64_t n, hipStream_t stream, int order, int64_t R,
+                            const int64_t* rbe2_slave, const int64_t* rbe2_master, int64_t S, const int64_t* spc_dof,
+                            const double* spc_val, int64_t G, const int64_t* r3_ptr, const int64_t* r3_master,
+                            const double* r3_wsum, const int64_t* r3_slave, const double* r3_w, Constraints* c) {
+    if (R < 0 || S < 0 || G < 0 || (R && (!rbe2_slave || !rbe2_master)) || (S && (!spc_dof || !spc_val)) ||
+        (G && (!r3_ptr || !r3_master || !r3_wsum)) || (order != 0 && order != 1) || (order == 0 && G)) {
+        set_error("%s: bad sizes / pointers / order", fn);
+        return FEM_EARG;
+    }
+    int* bad = nullptr;
+    FEM_HIP(hipMallocAsync((void**)&bad, sizeof(int) * 2, stream));
+    FEM_HIP(hipMemsetAsync(bad, 0, sizeof(int) * 2, stream));
+    auto chk = [&](const int64_t* v, int64_t m) {
+        if (m > 0)
+            hipLaunchKernelGGL(k_check_range, dim3(stream_grid(m, 256)), dim3(256), 0, stream, v, m, (int64_t)0, n, bad);
+    };
+    chk(rbe2_slave, R);
+    chk(rbe2_master, R);
+    chk(spc_dof, S);
+    chk(r3_master, G);
+    int64_t E = 0;
+    if (G) {
+        hipLaunchKernelGGL(k_check_ptr, dim3(stream_grid(G, 256)), dim3(256), 0, stream, r3_ptr, G, bad + 1);
+        FEM_HIP(hipMemcpyAsync(&E, r3_ptr + G, sizeof(int64_t), hipMemcpyDeviceToHost, stream));
+    }
+    int hbad[2] = {0, 0};
+    FEM_HIP(hipMemcpyAsync(hbad, bad, sizeof(hbad), hipMemcpyDeviceToHost, stream));
+    FEM_HIP(hipStreamSynchronize(stream));
+    if (!hbad[1] && E > 0) {
+        if (!r3_slave || !r3_w) hbad[1] = 1;
+        else {
+            chk(r3_slave, E);
+            FEM_HIP(hipMemcpyAsync(hbad, bad, sizeof(int), hipMemcpyDeviceToHost, stream));
+            FEM_HIP(hipStreamSynchronize(stream));
+        }
+    }
+    FEM_HIP(hipFreeAsync(bad, stream));
+    if (hbad[0] || hbad[1]) {
+        set_error("%s: %s", fn, hbad[0] ? "a constraint dof is outside [0, n)" : "RBE3 group pointer is not a CSR offset array");
+        return FEM_EARG;
+    }
+    *c = Constraints{};
+    c->R = R;
+    c->S = S;
+    c->G = G;
+    c->rbe2_slave = rbe2_slave;
+    c->rbe2_master = rbe2_master;
+    c->spc_dof = spc_dof;
+    c->spc_val = spc_val;
+    c->r3_ptr = r3_ptr;
+    c->r3_master = r3_master;
+    c->r3_wsum = r3_wsum;
+    c->r3_slave = r3_slave;
+    c->r3_w = r3_w;
+    c->order = order;
+    return FEM_OK;
+}
+
+int fem_pcg_set_constraints(fem_pcg* s, int order, int64_t R, const int64_t* rbe2_slave, const int64_t* rbe2_master,
+                            int64_t S, const int64_t* spc_dof, const double* spc_val, int64_t G, const int64_t* r3_ptr,
+                            const int64_t* r3_master, const double* r3_wsum, const int64_t* r3_slave,
+                            const double* r3_w) {
+    if (s->mode != FEM_MODE_CG_CONSTRAINED || s->dist || s->fused || s->deferred || s->graph) {
+        set_error("fem_pcg_set_constraints: needs a CG_CONSTRAINED, single-GPU, 3-kernel context without a graph");
+        return FEM_EARG;
+    }
+    Constraints c;
+    const int rc = make_constraints("fem_pcg_set_constraints", s->n, s->stream, order, R, rbe2_slave, rbe2_master, S,
+                                    spc_dof, spc_val, G, r3_ptr, r3_master, r3_wsum, r3_slave, r3_w, &c);
+    if (rc != FEM_OK) return rc;
+    if (s->con.tmp) (void)hipFree(s->con.tmp);
+    s->con.tmp = nullptr;
+    if (R > 0) FEM_HIP(hipMalloc(&c.tmp, sizeof(double) * (size_t)R));
+    s->con = c;
+    s->has_con = 1;
+    return FEM_OK;
+}
+
+int fem_enforce_constraints(double* x, double* r, int64_t n, int order, int64_t R, const int64_t* rbe2_slave,
+                            const int64_t* rbe2_master, int64_t S, const int64_t* spc_dof, const double* spc_val,
+                            int64_t G, const int64_t* r3_ptr, const int64_t* r3_master, const double* r3_wsum,
+                            const int64_t* r3_slave, const double* r3_w, fem_stream_t stream) {
+    if (!x || n < 0) {
+        set_error("fem_enforce_constraints: null x / negative n");
+        return FEM_EARG;
+    }
+    const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    Constraints c;
+    const int rc = make_constraints("fem_enforce_constraints", n, st, order, R, rbe2_slave, rbe2_master, S, spc_dof,
+                                    spc_val, G, r3_ptr, r3_master, r3_wsum, r3_slave, r3_w, &c);
+    if (rc != FEM_OK) return rc;
+    if (R > 0) FEM_HIP(hipMallocAsync((void**)&c.tmp, sizeof(double) * (size_t)R, st));
+    const int lrc = launch_constraints(st, x, r, c, nullptr, 1);
+    if (lrc != FEM_OK) return lrc;
+    if (c.tmp) FEM_HIP(hipFreeAsync(c.tmp, st));
+    return FEM_OK;
+}
+
 int fem_pcg_set_cols16(fem_pcg* s, const int16_t* dcols) {
     if (s->graph) {
         set_error("fem_pcg_set_cols16: drop the captured graph first");
@@ -1020,7 +1248,7 @@ int fem_pcg_create(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_
         set_error("fem_pcg_create: block size %d unsupported", bs);
         return FEM_EARG;
     }
-    if (mode != FEM_MODE_CG_STABLE && mode != FEM_MODE_PCG) {
+    if (mode != FEM_MODE_CG_STABLE && mode != FEM_MODE_PCG && mode != FEM_MODE_CG_CONSTRAINED) {
         set_error("fem_pcg_create: unknown mode %d", mode);
         return FEM_EARG;
     }
@@ -1084,6 +1312,10 @@ int fem_pcg_set_schedule(fem_pcg* s, int sched) {
         set_error("fem_pcg_set_schedule: the distributed path runs the 3-kernel schedule");
         return FEM_EARG;
     }
+    if (sched != 0 && s->mode == FEM_MODE_CG_CONSTRAINED) {
+        set_error("fem_pcg_set_schedule: the constrained CG runs the 3-kernel schedule (projection after K3)");
+        return FEM_EARG;
+    }
     s->fused = sched == 1;
     s->deferred = sched == 2;
     return FEM_OK;
@@ -1134,6 +1366,10 @@ int fem_pcg_start(fem_pcg* s) {
     hipLaunchKernelGGL(k_pcg_init, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->b, s->r, s->q, s->w, s->p0,
                        s->p1, s->fused, s->st, s->red, (const uint8_t*)nullptr, s->bs);
     FEM_LAUNCHED();
+    if (s->has_con) {   // the reference enforces once after r0 = F - K u0 (`solver/solver.py:548-553`)
+        const int rc = launch_constraints(s->stream, s->x, nullptr, s->con, s->st, 1);
+        if (rc != FEM_OK) return rc;
+    }
     s->launched = 0;
     if (s->deferred) {
         hipLaunchKernelGGL(k_bank_init, dim3(1), dim3(1), 0, s->stream, s->st);
@@ -1391,6 +1627,7 @@ void fem_pcg_destroy(fem_pcg* s) {
     if (s->red.partials) (void)hipFree(s->red.partials);
     if (s->red.counters) (void)hipFree(s->red.counters);
     if (s->hbuf) (void)hipFree(s->hbuf);
+    if (s->con.tmp) (void)hipFree(s->con.tmp);
     if (s->st) (void)hipFree(s->st);
     if (s->st_host) (void)hipHostFree(s->st_host);
     delete s;

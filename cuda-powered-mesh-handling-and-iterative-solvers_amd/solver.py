@@ -20,6 +20,8 @@ try:
     from .element import _dev, _key, cached_incidence, compute_c3d4_K_matrix, compute_c3d6_K_matrix, \
         compute_c3d8_K_matrix
     from .shell import *  # noqa: F401,F403
+    from .constraints import *  # noqa: F401,F403
+    from .constraints import ConstraintSet
 except ImportError:  # pragma: no cover - flat import from the package directory
     import _capi as C  # type: ignore
     import system as _sys  # type: ignore
@@ -27,6 +29,8 @@ except ImportError:  # pragma: no cover - flat import from the package directory
     from element import _dev, _key, cached_incidence, compute_c3d4_K_matrix, compute_c3d6_K_matrix, \
         compute_c3d8_K_matrix  # type: ignore
     from shell import *  # type: ignore # noqa
+    from constraints import *  # type: ignore # noqa
+    from constraints import ConstraintSet  # type: ignore
 
 from collections import OrderedDict
 
@@ -97,6 +101,57 @@ def stable_conjugate_gradient_solver(K, elements, F, rbe2, u_init=None, tol=1e-1
     _cg_messages(res, "stable")
     u = res.x.view(N, A.bs).to(device=torch.device(device), dtype=dtype)
     return (u, res) if return_info else u
+
+
+# ============================================================================ constrained CG (`solver/solver.py:394-759`)
+def _constrained_messages(res):
+    """`solver/solver.py:566-598` / `:735-757`."""
+    if res.status == C.PCG_CONVERGED:
+        print(f"[CG] Converged @ iter {res.iterations}, residual norm = {res.rz:.3e}")
+    elif res.status == C.PCG_BREAKDOWN:
+        print(f"[CG] Early terminate @ iter {res.iterations}: p^T K p = {res.pq:.3e}, not valid for SPD.")
+    elif res.status == C.PCG_ALPHA_NAN:
+        print(f"[CG] Terminate @ iter {res.iterations}: alpha is NaN/Inf.")
+    elif res.status == C.PCG_BETA_NAN:
+        print(f"[CG] Terminate @ iter {res.iterations}: beta is NaN/Inf.")
+    else:
+        print("[CG] Did not converge within max_iter.")
+
+
+def _constrained_solve(K, elements, F, cons_args, order, u_init, tol, max_iter, device, dtype, eps, return_info):
+    dev = _dev(device)
+    N = F.shape[0]
+    A = assemble(K, elements, N, dev)
+    if F.shape[1] != A.bs:
+        raise ValueError(f"F is [N, {F.shape[1]}] but the element matrices have {A.bs} dofs per node")
+    cs = ConstraintSet(N, A.bs, dev, *cons_args, order=order)
+    b = F.to(device=dev, dtype=F64).reshape(-1)
+    res = A.pcg(b, u_init, w=cs.mask(), mode=C.MODE_CG_CONSTRAINED, tol=tol, max_iter=max_iter, eps=eps,
+                schedule=_sys.SCHED_THREE, constraints=cs)
+    _constrained_messages(res)
+    u = res.x.view(N, A.bs).to(device=torch.device(device), dtype=dtype)
+    return (u, res) if return_info else u
+
+
+def constrained_conjugate_gradient_solver(K, elements, F, rbe2_list, spc_list, u_init=None, tol=1e-10, max_iter=1000,
+                                          device="cuda:0", dtype=torch.float64, eps=1e-30, return_info=False):
+    """CG on the assembled K with RBE2 (slave dofs follow the master) and SPC (prescribed values) enforced after
+    every update, residual zeroed on those dofs; r0 = F - K u0 is formed before the first projection, like the
+    reference (`solver/solver.py:512-600`). Stop when sqrt(r.r) < tol. Returns u [N, dpn] (fp64 arithmetic)."""
+    cons = (parse_spc_list(spc_list, "cpu"), parse_rbe2_list(rbe2_list, "cpu"))  # noqa: F405
+    return _constrained_solve(K, elements, F, cons, 0, u_init, tol, max_iter, device, dtype, eps, return_info)
+
+
+def new_constrained_conjugate_gradient_solver(K, elements, N, rbe2_list, rbe3_list, spc_list, load_list, u_init=None,
+                                              tol=1e-10, max_iter=1000, device="cuda:0", dtype=torch.float64,
+                                              eps=1e-30, return_info=False):
+    """F [N, 3] from the nodal loads, then the constrained CG with SPC, RBE2 and RBE3 (master = weighted mean of
+    its slaves per dof) enforced after every update (`solver/solver.py:702-759`)."""
+    F = torch.zeros((N, 3), dtype=F64)
+    apply_loads_to_F(F, load_list)  # noqa: F405
+    cons = (parse_spc_list(spc_list, "cpu"), parse_rbe2_list(rbe2_list, "cpu"),  # noqa: F405
+            parse_rbe3_list(rbe3_list, "cpu"))  # noqa: F405
+    return _constrained_solve(K, elements, F, cons, 1, u_init, tol, max_iter, device, dtype, eps, return_info)
 
 
 # ============================================================================ PCG (`solver/solver.py:766-833`)

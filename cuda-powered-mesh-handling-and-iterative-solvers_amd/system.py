@@ -237,8 +237,9 @@ class SellMatrix:
 
     # ---------------------------------------------------------------- solver
     def pcg(self, b, x0=None, w=None, mode=C.MODE_PCG, tol=1e-8, max_iter=1000, eps=1e-30, history=False,
-            chunk=32, fused=False, schedule=None):
-        """Run the device (P)CG; returns (x, iterations, status, rz_last, hist or None)."""
+            chunk=32, fused=False, schedule=None, constraints=None):
+        """Run the device (P)CG; returns a PcgResult. `constraints` (a constraints.ConstraintSet, mode
+        CG_CONSTRAINED, 3-kernel schedule) is projected onto x at start and after every x update."""
         lib = C.lib()
         b = b.to(F64).contiguous().view(-1)
         x = (torch.zeros(self.n, dtype=F64, device=self.device) if x0 is None
@@ -253,6 +254,8 @@ class SellMatrix:
         try:
             C.check(lib.fem_pcg_set_schedule(h, _schedule(fused, schedule, self.bs)), "fem_pcg_set_schedule")
             self.attach_cols16(h)
+            if constraints is not None:
+                C.check(lib.fem_pcg_set_constraints(h, *constraints.args()), "fem_pcg_set_constraints")
             it, stt, rz = ctypes.c_int(), ctypes.c_int(), ctypes.c_double()
             C.check(lib.fem_pcg_solve(h, int(max_iter), int(chunk), ctypes.byref(it), ctypes.byref(stt),
                                       ctypes.byref(rz)), "fem_pcg_solve")
@@ -273,7 +276,7 @@ class PcgRunner:
     """Persistent (P)CG context for fixed-iteration timing (bench.py): start once, iterate k, poll."""
 
     def __init__(self, A: SellMatrix, b, w, x0=None, mode=C.MODE_PCG, tol=0.0, eps=1e-30, fused=False,
-                 schedule=None):
+                 schedule=None, constraints=None):
         self.lib = C.lib()
         self.A = A
         self.b = b.to(F64).contiguous().view(-1)
@@ -291,6 +294,9 @@ class PcgRunner:
         self.schedule = 0 if isinstance(self, _DistMarker) else _schedule(fused, schedule, A.bs)
         C.check(self.lib.fem_pcg_set_schedule(self.h, self.schedule), "fem_pcg_set_schedule")
         A.attach_cols16(self.h)
+        self.constraints = constraints   # keeps the device arrays alive with the context
+        if constraints is not None:
+            C.check(self.lib.fem_pcg_set_constraints(self.h, *constraints.args()), "fem_pcg_set_constraints")
 
     def finish(self):
         C.check(self.lib.fem_pcg_finish(self.h), "fem_pcg_finish")

@@ -52,7 +52,10 @@ enum {
     FEM_PCG_BETA_NAN = 5,   /* (`solver/solver.py:214-218`) */
 };
 
-enum { FEM_MODE_CG_STABLE = 0, FEM_MODE_PCG = 1 };
+/* CG_CONSTRAINED: constrained_conjugate_gradient_solver / new_constrained_conjugate_gradient_solver
+ * (`solver/solver.py:512-600`, `:702-759`): the CG_STABLE arithmetic without zeroing x, plus the projections
+ * of fem_pcg_set_constraints after every x update */
+enum { FEM_MODE_CG_STABLE = 0, FEM_MODE_PCG = 1, FEM_MODE_CG_CONSTRAINED = 2 };
 enum { FEM_KIND_ELASTIC = 0, FEM_KIND_POISSON = 1, FEM_KIND_MASS = 2 };
 enum { FEM_ISO_SUM = 0, FEM_ISO_STACK = 1, FEM_ISO_VOLUME = 2 };
 
@@ -206,9 +209,31 @@ int fem_pcg_poll(fem_pcg* s, int* iters, int* status, double* rz);
 int fem_pcg_scalars(fem_pcg* s, double* out6);
 /* [sync] run to completion: start + chunks of `chunk` iterations until stop or max_iter */
 int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, double* rz);
-/* kernel schedule: 0 = 3-kernel (default, faster on gfx950), 1 = fused (p formed inside the SpMV from r, w and
- * the previous p at every gathered column; 2 kernels per iteration, 88n instead of 96n vector bytes) */
-int fem_pcg_set_schedule(fem_pcg* s, int fused);
+/* kernel schedule: 0 = 3-kernel (SpMV+p.q / r update+r.z / x,p update; the context default), 1 = fused (p formed
+ * inside the SpMV from r, w and the previous p; 2 kernels per iteration), 2 = deferred (each kernel finishes the
+ * previous kernel's block partials itself: no grid atomics, state banked by launch parity). Distributed and
+ * constrained contexts accept only 0. */
+int fem_pcg_set_schedule(fem_pcg* s, int sched);
+/* CG_CONSTRAINED projections applied to x once at fem_pcg_start (after r0 = b - A x0) and after every x update:
+ *   order 0 (`enforce_constraints`, `solver/solver.py:478-510`): x[rbe2_slave] = x[rbe2_master] (all gathered
+ *           before any is written), then x[spc_dof] = spc_val.  G must be 0.
+ *   order 1 (`new_enforce_constraints`, `:665-700`): SPC, then RBE2, then for every RBE3 group g in order
+ *           x[r3_master[g]] = sum_{e in [r3_ptr[g], r3_ptr[g+1])} r3_w[e] x[r3_slave[e]] / (r3_wsum[g] + 1e-30).
+ * All indices are flat dofs (node * dpn + dof) in [0, n); r3_ptr is a CSR offset array with r3_ptr[0] = 0 (one
+ * group per (RBE3, dof) pair: `:685-698`). The residual masking of SPC dofs and RBE2 slaves (`r[...] = 0`) is the
+ * context's 0/1 weight vector w. All arrays are device-resident and must outlive the context.
+ * [sync] validates every index once; FEM_EARG on a bad index, a non-constrained / distributed / graph context. */
+int fem_pcg_set_constraints(fem_pcg* s, int order, int64_t R, const int64_t* rbe2_slave, const int64_t* rbe2_master,
+                            int64_t S, const int64_t* spc_dof, const double* spc_val, int64_t G,
+                            const int64_t* r3_ptr, const int64_t* r3_master, const double* r3_wsum,
+                            const int64_t* r3_slave, const double* r3_w);
+/* [sync] the same projections applied once to x [n] (stream-ordered), and r [n] (nullable) zeroed at the SPC dofs
+ * and RBE2 slaves: `enforce_constraints` / `new_enforce_constraints` as standalone calls
+ * (`solver/solver.py:478-510`, `:665-700`). */
+int fem_enforce_constraints(double* x, double* r, int64_t n, int order, int64_t R, const int64_t* rbe2_slave,
+                            const int64_t* rbe2_master, int64_t S, const int64_t* spc_dof, const double* spc_val,
+                            int64_t G, const int64_t* r3_ptr, const int64_t* r3_master, const double* r3_wsum,
+                            const int64_t* r3_slave, const double* r3_w, fem_stream_t stream);
 /* run the SpMV of this context on 16-bit column deltas (NULL: back to the int32 columns) */
 int fem_pcg_set_cols16(fem_pcg* s, const int16_t* dcols);
 /* apply the deferred x update of the fused schedule after the last iteration (fem_pcg_solve does this) */

@@ -311,6 +311,84 @@ def pcg(K, elements, F, M_inv, u_init=None, tol=1e-8, max_iter=1000, history=Non
     return u, max_iter, "max_iter"
 
 
+# ---------------------------------------------------------------- constraints (`solver/solver.py:394-759`)
+def enforce(u, r, rbe2_list, spc_list, rbe3_list=None):
+    """`enforce_constraints` (:478-510, rbe3_list None: RBE2 then SPC) or `new_enforce_constraints`
+    (:665-700: SPC, RBE2, then every RBE3 per distinct dof in ascending order). u, r: [N, dpn], in place."""
+    # flattened in the order of `parse_rbe2_list` (:437-476: rbe2 -> slave -> dof) / `parse_spc_list` (:396-435)
+    rbe2 = [(sl, c["master"], d) for c in rbe2_list for sl in c["slaves"] for d in c["dofs"]]
+    spc = [(c["node"], d, float(c["value"])) for c in spc_list for d in c["dofs"]]
+
+    def _rbe2():
+        if rbe2:
+            s, m, d = (torch.tensor(v) for v in zip(*rbe2))
+            u[s, d] = u[m, d]
+            r[s, d] = 0.0
+
+    def _spc():
+        if spc:
+            n, d, v = zip(*spc)
+            n, d = torch.tensor(n), torch.tensor(d)
+            u[n, d] = torch.tensor(v, dtype=u.dtype)
+            r[n, d] = 0.0
+
+    if rbe3_list is None:
+        _rbe2()
+        _spc()
+        return
+    _spc()
+    _rbe2()
+    for c in rbe3_list:
+        w = torch.tensor([float(x) for x in c["weights"]], dtype=u.dtype)
+        w_sum = torch.tensor(float(sum(c["weights"])), dtype=u.dtype)
+        slaves = torch.tensor(c["slaves"])
+        for d in sorted(set(c["dofs"])):
+            u[c["master"], d] = torch.sum(w * u[slaves, d]) / (w_sum + 1e-30)
+
+
+def constrained_cg(K, elements, F, rbe2_list, spc_list, rbe3_list=None, u_init=None, tol=1e-10, max_iter=1000,
+                   eps=1e-30, history=None):
+    """`constrained_conjugate_gradient_solver` (:512-600; rbe3_list None) and the loop of
+    `new_constrained_conjugate_gradient_solver` (:702-759; rbe3_list given, F already built by the loads).
+    r0 = F - K u0 is formed BEFORE the first projection, as in the reference. Returns (u, iterations, status)."""
+    u = torch.zeros_like(F) if u_init is None else u_init.clone().to(F.dtype)
+    r = F - nodal_forces(K, elements, u)
+    enforce(u, r, rbe2_list, spc_list, rbe3_list)
+    p = r.clone()
+    rs_old = torch.sum(r * r)
+    for i in range(max_iter):
+        Ap = nodal_forces(K, elements, p)
+        pAp = torch.sum(p * Ap)
+        if pAp.abs() < eps or pAp < 0.0:
+            return u, i + 1, "breakdown_pAp"
+        alpha = rs_old / (pAp + eps)
+        if torch.isnan(alpha) or torch.isinf(alpha):
+            return u, i + 1, "alpha_nan"
+        u += alpha * p
+        r -= alpha * Ap
+        enforce(u, r, rbe2_list, spc_list, rbe3_list)
+        rs_new = torch.sum(r * r)
+        if history is not None:
+            history.append(float(torch.sqrt(rs_new)))
+        if torch.sqrt(rs_new) < tol:
+            return u, i + 1, "converged"
+        beta = rs_new / (rs_old + eps)
+        if torch.isnan(beta) or torch.isinf(beta):
+            return u, i + 1, "beta_nan"
+        p = r + beta * p
+        rs_old = rs_new
+    return u, max_iter, "max_iter"
+
+
+def loads_to_F(N, load_list, dtype=F64):
+    """`apply_loads_to_F` (:653-663) into a fresh [N, 3] array."""
+    F = torch.zeros((N, 3), dtype=dtype)
+    for ld in load_list:
+        for d in range(3):
+            F[ld["node"], d] += ld["force"][d]
+    return F
+
+
 def static_structure(coords, force, fixed, blocks, E, nu, u_init=None, tol=1e-10, max_iter=1000, eps=1e-30):
     """`static_structure_solver`, `solver/solver.py:11-135`, solid families only (shells are out of scope).
     `blocks` = {"c3d4": elems, "c3d8": elems, "c3d6": elems}; c3d8 uses the 8-point rule, c3d6 single=True.

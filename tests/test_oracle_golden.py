@@ -95,3 +95,22 @@ def test_coo_coalesce_equals_ebe_and_partition_maps():
     for k in range(4):
         nodes, loc = R.partition_local_maps(pr["tets"], pr[f"ids{k}"])
         assert torch.equal(nodes, pr[f"nodes{k}"]) and torch.equal(loc, pr[f"local{k}"])
+
+
+def constrained_fixture():
+    import json
+    g = load_golden("constrained_tet4")
+    return g, json.loads(str(g["constraints"]))
+
+
+def test_constrained_cg_oracle_matches_reference():
+    """`constrained_conjugate_gradient_solver` (RBE2 plate + SPC with a prescribed value) and
+    `new_constrained_conjugate_gradient_solver` (SPC, RBE2, weighted RBE3 sets, nodal loads)."""
+    g, c = constrained_fixture()
+    K = R.tet4_K(g["coords"], g["tets"], E, NU)
+    tol = float(g["tol"])
+    u, n, s = R.constrained_cg(K, g["tets"], g["F"], c["rbe2_a"], c["spc"], tol=tol, max_iter=3000)
+    assert s == "converged" and n == int(g["n_iter_a"]) and rel(u, g["u_a"]) == 0.0
+    Fb = R.loads_to_F(g["coords"].shape[0], c["loads_b"])
+    u, n, s = R.constrained_cg(K, g["tets"], Fb, c["rbe2_b"], c["spc"], c["rbe3_b"], tol=tol, max_iter=3000)
+    assert s == "converged" and n == int(g["n_iter_b"]) and rel(u, g["u_b"]) == 0.0

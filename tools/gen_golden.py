@@ -220,6 +220,44 @@ def gen_partition(el, so):
     save("partition_ref", **out)
 
 
+def constrained_case():
+    """Jittered n=4 c3d4 cube with an SPC'd base (one prescribed non-zero value), a rigid RBE2 top plate driven
+    from its centre node (case A), and an RBE2 side group + weighted RBE3 top master + nodal loads (case B)."""
+    coords, tets = mesh.kuhn_cube(4, jitter=0.15)
+    z = coords[:, 2]
+    base = torch.nonzero(z < 1e-9).view(-1).tolist()
+    top = torch.nonzero(z > 1 - 1e-9).view(-1).tolist()
+    master = top[len(top) // 2]
+    slaves = [t for t in top if t != master]
+    spc = [{"node": b, "dofs": [0, 1, 2], "value": 0.0} for b in base]
+    spc[0] = {"node": base[0], "dofs": [0], "value": 1e-5}
+    rbe2_a = [{"master": master, "slaves": slaves, "dofs": [0, 1, 2]}]
+    side = [s for s in torch.nonzero(coords[:, 0] > 1 - 1e-9).view(-1).tolist() if s not in base and s not in top]
+    rbe2_b = [{"master": side[0], "slaves": side[1:4], "dofs": [0, 2]}]
+    rbe3_b = [{"master": master, "slaves": slaves[:6], "dofs": [0, 1, 2], "weights": [1.0, 2.0, 1.0, 0.5, 1.5, 1.0]},
+              {"master": slaves[7], "slaves": slaves[8:11], "dofs": [2, 1], "weights": [1.0, 1.0, 2.0]}]
+    loads_b = [{"node": s, "force": [1e4, 0.0, -1e5]} for s in top]
+    return coords, tets, master, spc, rbe2_a, rbe2_b, rbe3_b, loads_b
+
+
+def gen_constrained(el, so):
+    import json
+    coords, tets, master, spc, rbe2_a, rbe2_b, rbe3_b, loads_b = constrained_case()
+    N = coords.shape[0]
+    K = el.compute_K_matrix(coords, tets, "c3d4", E, NU, device=CPU, dtype=F64)
+    F = torch.zeros((N, 3), dtype=F64)
+    F[master, 2] = -1e6
+    tol = 1e-3
+    ua, ta = run_quiet(so.constrained_conjugate_gradient_solver, K, tets, F, rbe2_a, spc, tol=tol, max_iter=3000,
+                       device=CPU)
+    ub, tb = run_quiet(so.new_constrained_conjugate_gradient_solver, K, tets, N, rbe2_b, rbe3_b, spc, loads_b, tol=tol,
+                       max_iter=3000, device=CPU)
+    it = [int(re.search(r"Converged @ iter (\d+)", t).group(1)) for t in (ta, tb)]
+    cons = json.dumps({"spc": spc, "rbe2_a": rbe2_a, "rbe2_b": rbe2_b, "rbe3_b": rbe3_b, "loads_b": loads_b})
+    save("constrained_tet4", coords=coords, tets=tets, F=F, u_a=ua, u_b=ub, n_iter_a=it[0], n_iter_b=it[1], tol=tol,
+         constraints=np.array(cons))
+
+
 def main():
     if not os.path.isdir(REF):
         print("reference not present; nothing to do")
@@ -233,6 +271,7 @@ def main():
     gen_solids(el, so)
     gen_mixed(el, so)
     gen_partition(el, so)
+    gen_constrained(el, so)
     return 0
 
 
