@@ -56,14 +56,17 @@ def sync():
     torch.cuda.synchronize()
 
 
-def traffic_from_profiles(workload_key):
-    """HBM bytes per SpMV launch from the committed PMC summary (tools/pmc_traffic.py), or None."""
+def traffic_from_profiles(workload_key, kernel, alg):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (tools/pmc_traffic.py), or None when the
+    summary was taken on another kernel / matrix format."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
-        d = json.load(open(path))
-        return d.get(workload_key, {}).get("bytes_per_launch")
+        d = json.load(open(path)).get(workload_key, {})
     except Exception:
         return None
+    if d.get("kernel") != kernel or d.get("algorithmic_bytes") != alg:
+        return None
+    return d.get("bytes_per_launch")
 
 
 def cpu_baseline(n, kind, iters):
@@ -181,7 +184,7 @@ def main():
         "kernel_ms": {"spmv_dot": spmv_ms, "update": ms[1] / max(cnt[1], 1), "pupdate": ms[2] / max(cnt[2], 1),
                       "sampled_launches": cnt[0]},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic_from_profiles(workload_key),
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic_from_profiles(workload_key, kernel, alg),
                      "kernel": kernel, "algorithmic_bytes": alg},
         "cpu_baseline": None,
     }

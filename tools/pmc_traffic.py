@@ -20,7 +20,19 @@ import shutil
 import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {"spmv_dot": "k_pcg_spmv_dot", "update": "k_pcg_update(", "pupdate": "k_pcg_pupdate"}
+KERNELS_3K = {"spmv_dot": "k_pcg_spmv_dot", "update": "k_pcg_update(", "pupdate": "k_pcg_pupdate"}
+KERNELS_DEFERRED = {"spmv_dot": "k_pcg_d1", "update": "k_pcg_d2", "pupdate": "k_pcg_d3"}
+
+
+def bench_line(prof):
+    """The bench.py JSON line of the trace pass (algorithmic bytes, kernel name), or {}."""
+    try:
+        for line in reversed(open(os.path.join(prof, "trace.log")).read().splitlines()):
+            if line.startswith("{"):
+                return json.loads(line)
+    except OSError:
+        pass
+    return {}
 
 
 def load_trace(path):
@@ -40,18 +52,24 @@ def main():
     ap.add_argument("--tag", default="r01")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--workload", default="kuhn119_poisson")
-    ap.add_argument("--alg-bytes", type=float, default=341470060.0)
+    ap.add_argument("--alg-bytes", type=float, default=None, help="default: from the bench line of the trace pass")
     a = ap.parse_args()
     prof = a.prof
+    bl = bench_line(prof)
+    if a.alg_bytes is None:
+        a.alg_bytes = float(bl["roofline"]["algorithmic_bytes"])
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     shutil.copy(os.path.join(prof, "trace", "run_kernel_stats.csv"),
                 os.path.join(ROOT, "profiles", f"{a.tag}_kernel_stats.csv"))
     trace = load_trace(os.path.join(prof, "trace", "run_kernel_trace.csv"))
-    out = {"workload": a.workload, "timed_dispatches": a.steps, "kernels": {}}
+    deferred = any("k_pcg_d1" in r["Kernel_Name"] for r in trace)
+    KERNELS = KERNELS_DEFERRED if deferred else KERNELS_3K
+    out = {"workload": a.workload, "timed_dispatches": a.steps, "kernels": {}, "bench_line": bl}
     for short, key in KERNELS.items():
         rows = last_n(trace, key, a.steps)
+        names = sorted({r["Kernel_Name"] for r in rows})
         durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
-        ent = {"dispatches": len(durs), "avg_us": statistics.mean(durs) if durs else None,
+        ent = {"kernel": names, "dispatches": len(durs), "avg_us": statistics.mean(durs) if durs else None,
                "median_us": statistics.median(durs) if durs else None}
         for counter, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
             p = os.path.join(prof, sub, "run_counter_collection.csv")
@@ -74,7 +92,7 @@ def main():
     tp = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     allt = json.load(open(tp)) if os.path.exists(tp) else {}
     allt[a.workload] = {"bytes_per_launch": k1.get("hbm_bytes_per_launch"), "source": f"profiles/{a.tag}_summary.json",
-                        "kernel": "k_pcg_spmv_dot"}
+                        "kernel": KERNELS["spmv_dot"], "algorithmic_bytes": a.alg_bytes}
     json.dump(allt, open(tp, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
