@@ -51,6 +51,13 @@ SIGNATURES = {
     "fem_ebe_apply": (_I, [_P, _P, _I, _I, _P, _P, _L, _P, _P, _P]),
     "fem_ebe_diag": (_I, [_P, _P, _I, _I, _P, _P, _L, _I, _P, _P]),
     "fem_invert_diag": (_I, [_P, _L, _P, _P]),
+    "fem_tet4_stress": (_I, [_P, _P, _L, _P, _D, _D, _P, _P, _P, _P]),
+    "fem_iso_stress": (_I, [_P, _P, _L, _I, _P, _D, _D, _P, _P, _I, _I, _P, _P, _P]),
+    "fem_voigt_to_tensor": (_I, [_P, _L, _P, _P]),
+    "fem_von_mises": (_I, [_P, _L, _P, _P]),
+    "fem_node_average": (_I, [_P, _I, _P, _P, _L, _P, _P]),
+    "fem_face_forces": (_I, [_P, _P, _L, _I, _P, _P]),
+    "fem_shared_face_sum": (_I, [_P, _P, _I, _L, _P, _P]),
     "fem_spmv": (_I, [_L, _I, _P, _P, _P, _P, _P, _P]),
     "fem_spmv_variant": (_I, [_I, _I, _L, _I, _P, _P, _P, _P, _P, _P]),
     "fem_sell_delta16": (_I, [_P, _L, _P, _P, _P, _P]),

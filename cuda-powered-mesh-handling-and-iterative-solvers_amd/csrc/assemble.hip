@@ -7,50 +7,9 @@
 // the same block formula per quadrature point with signed detJ (Q2), which is exactly B^T D B for the
 // isotropic D; only the rounding order differs from the reference's dense einsums.
 #include "common.hpp"
+#include "element.hpp"
 
 namespace fem {
-
-struct Lame {
-    double lam, mu;
-};
-
-__host__ __device__ inline Lame lame(double E, double nu) {
-    // same coefficient the reference forms: coef = E/((1+nu)(1-2nu)); D33 = coef*(1-2nu)/2
-    double c = E / ((1.0 + nu) * (1.0 - 2.0 * nu));
-    return Lame{c * nu, c * ((1.0 - 2.0 * nu) / 2.0)};
-}
-
-// gradients of the P1 shape functions (rows of inv([1 x y z]) 1..3) and signed det of the edge matrix
-__device__ __forceinline__ double tet4_grads(const double* __restrict__ X, const int64_t* __restrict__ c,
-                                             double g[4][3]) {
-    double p[4][3];
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-        const int64_t n = c[a];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) p[a][k] = X[3 * n + k];
-    }
-    double e1[3], e2[3], e3[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        e1[k] = p[1][k] - p[0][k];
-        e2[k] = p[2][k] - p[0][k];
-        e3[k] = p[3][k] - p[0][k];
-    }
-    double c23[3] = {e2[1] * e3[2] - e2[2] * e3[1], e2[2] * e3[0] - e2[0] * e3[2], e2[0] * e3[1] - e2[1] * e3[0]};
-    double c31[3] = {e3[1] * e1[2] - e3[2] * e1[1], e3[2] * e1[0] - e3[0] * e1[2], e3[0] * e1[1] - e3[1] * e1[0]};
-    double c12[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
-    double det = e1[0] * c23[0] + e1[1] * c23[1] + e1[2] * c23[2];
-    double inv = 1.0 / det;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        g[1][k] = c23[k] * inv;
-        g[2][k] = c31[k] * inv;
-        g[3][k] = c12[k] * inv;
-        g[0][k] = -(g[1][k] + g[2][k] + g[3][k]);
-    }
-    return det;
-}
 
 // ---------------------------------------------------------------- c3d4 element matrices
 // 64 elements per 256-thread block: 64 lanes form gradients into LDS, then all 256 threads write the

@@ -8,7 +8,7 @@ notebook call sites work unchanged. Differences, all deliberate:
     (there is no CPU code path in this package: see `_capi.lib()`);
   * integration-point tables are evaluated on the host exactly as the reference evaluates them (including its
     quirks: c3d10 weights summing to 0.45, the float32-rounded line points of c3d6), then handed to the kernels.
-Out of scope: shells, stress recovery, topology, visualisation, c3d20/c3d15.
+Out of scope: shells, topology, visualisation, c3d20/c3d15.
 """
 from __future__ import annotations
 
@@ -65,6 +65,7 @@ def _prep(coords, elements, device):
     dev = _dev(device)
     coords = coords.to(device=dev, dtype=F64).contiguous()
     elements = elements.to(device=dev, dtype=LONG).contiguous()
+    _sys.check_connectivity(elements, coords.shape[0])
     return dev, coords, elements
 
 
@@ -427,3 +428,170 @@ def compute_nodal_forces(K, elements, displacement, device="cuda:0", dtype=torch
     C.check(lib.fem_ebe_apply(C.ptr(K), C.ptr(elements), npe, dpn, C.ptr(inc_ptr), C.ptr(inc), N, C.ptr(u), C.ptr(y),
                               C.stream(dev)), "fem_ebe_apply")
     return _out(y, device, dtype)
+
+
+# ============================================================================ stress recovery
+def _disp(displacement, dev, N):
+    u = displacement.to(device=dev, dtype=F64).contiguous()
+    if u.dim() != 2 or u.shape[1] != 3 or u.shape[0] != N:
+        raise ValueError(f"displacement must be [N, 3] with N = {N} nodes, got {list(u.shape)}")
+    return u
+
+
+def compute_stress_tensor(stress_vector):
+    """Voigt [M,6] (xx, yy, zz, xy, yz, xz) -> symmetric [M,3,3] on the input's device / dtype.
+    `solver/element.py:308-330`."""
+    lib = C.lib()
+    dev = _dev(stress_vector.device)
+    v = stress_vector.to(device=dev, dtype=F64).contiguous()
+    M = v.shape[0]
+    out = torch.empty((M, 3, 3), dtype=F64, device=dev)
+    C.check(lib.fem_voigt_to_tensor(C.ptr(v), M, C.ptr(out), C.stream(dev)), "fem_voigt_to_tensor")
+    return out.to(device=stress_vector.device, dtype=stress_vector.dtype)
+
+
+def compute_von_mises_stress(stress_tensor):
+    """[M,3,3] -> sqrt(((sxx-syy)^2 + (syy-szz)^2 + (szz-sxx)^2 + 6 (sxy^2 + syz^2 + sxz^2)) / 2) [M], read from
+    the upper triangle. `solver/element.py:332-353`."""
+    lib = C.lib()
+    dev = _dev(stress_tensor.device)
+    t = stress_tensor.to(device=dev, dtype=F64).contiguous()
+    M = t.shape[0]
+    out = torch.empty(M, dtype=F64, device=dev)
+    C.check(lib.fem_von_mises(C.ptr(t), M, C.ptr(out), C.stream(dev)), "fem_von_mises")
+    return out.to(device=stress_tensor.device, dtype=stress_tensor.dtype)
+
+
+def compute_c3d4_element_stress(coords, elements, displacement, E, nu, device="cuda:0", dtype=torch.float32):
+    """(stress tensor [M,3,3], von Mises [M]) of P1 tets from nodal displacements [N,3]; ValueError on a
+    degenerate element like the reference's B matrix. `solver/element.py:905-937`."""
+    lib = C.lib()
+    dev, coords, elements = _prep(coords, elements, device)
+    u = _disp(displacement, dev, coords.shape[0])
+    M = elements.shape[0]
+    sig = torch.empty((M, 3, 3), dtype=F64, device=dev)
+    vm = torch.empty(M, dtype=F64, device=dev)
+    bad = _bad_scalar(dev, M)
+    C.check(lib.fem_tet4_stress(C.ptr(coords), C.ptr(elements), M, C.ptr(u), float(E), float(nu), C.ptr(sig),
+                                C.ptr(vm), C.ptr(bad), C.stream(dev)), "fem_tet4_stress")
+    _raise_if_singular(bad, M)
+    return _out(sig, device, dtype), _out(vm, device, dtype)
+
+
+def _iso_stress(coords, elements, displacement, E, nu, etype, integral_point, single, point_major, device, dtype):
+    lib = C.lib()
+    dev, coords, elements = _prep(coords, elements, device)
+    npe = _ISO[etype][0]
+    if elements.shape[1] != npe:
+        raise ValueError(f"{etype} expects {npe} nodes per element, got {elements.shape[1]}")
+    u = _disp(displacement, dev, coords.shape[0])
+    M = elements.shape[0]
+    p, w = _points_weights(etype, integral_point)
+    dN = _dn_table(etype, p, dev)
+    w = w.to(dev, F64).contiguous()
+    n_ip = dN.shape[0]
+    if single:
+        layout, shape = 0, (M,)
+    else:
+        layout, shape = (2, (n_ip, M)) if point_major else (1, (M, n_ip))
+    sig = torch.empty(shape + (3, 3), dtype=F64, device=dev)
+    vm = torch.empty(shape, dtype=F64, device=dev)
+    C.check(lib.fem_iso_stress(C.ptr(coords), C.ptr(elements), M, npe, C.ptr(u), float(E), float(nu), C.ptr(dN),
+                               C.ptr(w), n_ip, layout, C.ptr(sig), C.ptr(vm), C.stream(dev)), "fem_iso_stress")
+    return _out(sig, device, dtype), _out(vm, device, dtype)
+
+
+def compute_c3d8_element_stress(coords, elements, displacement, E, nu, integral_point=None, single=True,
+                                device="cuda:0", dtype=torch.float32):
+    """Per 2x2x2 Gauss point stress / von Mises; single=True -> sum_q w_q (tensor, vm) [M,3,3], [M], else
+    [M,n_ip,3,3], [M,n_ip]. `solver/element.py:1696-1752`."""
+    return _iso_stress(coords, elements, displacement, E, nu, "c3d8", integral_point, single, False, device, dtype)
+
+
+def compute_c3d6_element_stress(coords, elements, displacement, E, nu, integral_point=None, single=True,
+                                device="cuda:0", dtype=torch.float32):
+    """Wedge analogue of compute_c3d8_element_stress (6-point rule, weights 1/3: Q3). `solver/element.py:2570-2629`."""
+    return _iso_stress(coords, elements, displacement, E, nu, "c3d6", integral_point, single, False, device, dtype)
+
+
+def compute_c3d10_element_stress(coords, elements, displacement, E, nu, integral_point=None, single=True,
+                                 device="cuda:0", dtype=torch.float32):
+    """Quadratic tet, 11-point rule (weights sum to 0.45: Q2); single=False stacks point-major [n_ip,M,3,3],
+    [n_ip,M] like the reference's list stack. `solver/element.py:1127-1189`."""
+    return _iso_stress(coords, elements, displacement, E, nu, "c3d10", integral_point, single, True, device, dtype)
+
+
+def compute_element_stress(coords, elements, displacement, E, nu, element_type, integral_point=None, single=True,
+                           device="cuda:0", dtype=torch.float32):
+    """String dispatch of `solver/element.py:409-417` (c3d20 / c3d15 out of scope, as for compute_K_matrix)."""
+    et = element_type.lower()
+    if et == "c3d4":
+        return compute_c3d4_element_stress(coords, elements, displacement, E, nu, device, dtype)
+    if et == "c3d8":
+        return compute_c3d8_element_stress(coords, elements, displacement, E, nu, integral_point, single, device,
+                                           dtype)
+    if et == "c3d10":
+        return compute_c3d10_element_stress(coords, elements, displacement, E, nu, integral_point, single, device,
+                                            dtype)
+    if et == "c3d6":
+        return compute_c3d6_element_stress(coords, elements, displacement, E, nu, integral_point, single, device,
+                                           dtype)
+    _unsupported(et)
+
+
+def compute_node_vm_stress(coords, elements, element_vm_stress, device="cuda:0", dtype=torch.float32):
+    """Node value = mean of the element values over the elements touching it (0 for unused nodes), summed in
+    ascending element order. `solver/element.py:466-504`."""
+    lib = C.lib()
+    dev, coords, elements = _prep(coords, elements, device)
+    N = coords.shape[0]
+    M, npe = elements.shape
+    ev = element_vm_stress.to(device=dev, dtype=F64).contiguous().view(-1)
+    if ev.numel() != M:
+        raise ValueError(f"element_vm_stress must have one value per element ({M}), got {ev.numel()}")
+    inc_ptr, inc = cached_incidence(elements, N)
+    out = torch.empty(N, dtype=F64, device=dev)
+    C.check(lib.fem_node_average(C.ptr(ev), npe, C.ptr(inc_ptr), C.ptr(inc), N, C.ptr(out), C.stream(dev)),
+            "fem_node_average")
+    return _out(out, device, dtype)
+
+
+def compute_c3d4_surface_forces(normal_vectors, stress_tensors, device="cuda:0"):
+    """Face tractions sigma_e n_ef [M,F,3] from area-weighted face normals [M,F,3] and element stress [M,3,3].
+    `solver/element.py:3343-3362`."""
+    lib = C.lib()
+    dev = _dev(device)
+    out_dtype = torch.promote_types(normal_vectors.dtype, stress_tensors.dtype)
+    n = normal_vectors.to(device=dev, dtype=F64).contiguous()
+    s = stress_tensors.to(device=dev, dtype=F64).contiguous()
+    M, F = n.shape[0], n.shape[1]
+    if tuple(s.shape) != (M, 3, 3) or n.shape[2] != 3:
+        raise ValueError(f"normals [M,F,3] and stress [M,3,3] expected, got {list(n.shape)} / {list(s.shape)}")
+    out = torch.empty((M, F, 3), dtype=F64, device=dev)
+    C.check(lib.fem_face_forces(C.ptr(n), C.ptr(s), M, F, C.ptr(out), C.stream(dev)), "fem_face_forces")
+    return out.to(device=torch.device(device), dtype=out_dtype)
+
+
+def compute_c3d4_shared_face_forces_sum(shared_face_indices, element_forces, device="cuda:0"):
+    """f[e0,f0] + f[e1,f1] for every shared face [S,2,2] -> [S,3] (zero at equilibrium).
+    `solver/element.py:3364-3382`."""
+    lib = C.lib()
+    dev = _dev(device)
+    out_dtype = element_forces.dtype
+    idx = shared_face_indices.to(device=dev, dtype=LONG).contiguous()
+    ff = element_forces.to(device=dev, dtype=F64).contiguous()
+    M, F = ff.shape[0], ff.shape[1]
+    S = idx.shape[0]
+    if S and (int(idx[..., 0].min()) < 0 or int(idx[..., 0].max()) >= M or int(idx[..., 1].min()) < 0
+              or int(idx[..., 1].max()) >= F):
+        raise IndexError("shared_face_indices out of range of element_forces")
+    out = torch.empty((S, 3), dtype=F64, device=dev)
+    C.check(lib.fem_shared_face_sum(C.ptr(idx), C.ptr(ff), F, S, C.ptr(out), C.stream(dev)), "fem_shared_face_sum")
+    return out.to(device=torch.device(device), dtype=out_dtype)
+
+
+__all__ += [
+    "compute_stress_tensor", "compute_von_mises_stress", "compute_element_stress", "compute_c3d4_element_stress",
+    "compute_c3d8_element_stress", "compute_c3d6_element_stress", "compute_c3d10_element_stress",
+    "compute_node_vm_stress", "compute_c3d4_surface_forces", "compute_c3d4_shared_face_forces_sum",
+]

@@ -69,9 +69,20 @@ class Graph:
         return int(self.cols.numel())
 
 
+def check_connectivity(elements: torch.Tensor, n_nodes: int):
+    """IndexError for a node index outside [0, n_nodes) (the kernels gather without bounds checks; the
+    reference's torch indexing raises IndexError on such input). One device reduction + sync."""
+    if elements.numel() == 0:
+        return
+    lo, hi = int(elements.min()), int(elements.max())
+    if lo < 0 or hi >= n_nodes:
+        raise IndexError(f"element connectivity references node {lo if lo < 0 else hi}, outside [0, {n_nodes})")
+
+
 def incidence(elements: torch.Tensor, n_nodes: int):
     """Deterministic node -> (element, local) incidence of a connectivity block [M, npe] (int64, device)."""
     lib = C.lib()
+    check_connectivity(elements, n_nodes)
     dev = elements.device
     M, npe = elements.shape
     inc_ptr = torch.empty(n_nodes + 1, dtype=I32, device=dev)
@@ -89,6 +100,7 @@ def build_graph(elements: torch.Tensor, n_nodes: int, compress: bool = True) -> 
     lib = C.lib()
     dev = elements.device
     elements = elements.contiguous()
+    check_connectivity(elements, n_nodes)
     M, npe = elements.shape
     st = C.stream(dev)
     inc_ptr, inc = incidence(elements, n_nodes)

@@ -168,6 +168,35 @@ int fem_ebe_diag(const double* Ke, const int64_t* conn, int npe, int dpn, const 
 /* out[i] = 1/in[i], inf -> 0 */
 int fem_invert_diag(const double* in, int64_t n, double* out, fem_stream_t stream);
 
+/* ------------------------------------------------------------------ stress recovery (post-solve)
+ * strain = B u_e, stress = D strain (isotropic D of `solver/element.py:282-306`), tensor rows xx xy xz / xy yy yz /
+ * xz yz zz, von Mises. u [N,3]. Outputs sig [.., 3, 3] and vm [..] may each be NULL. */
+/* compute_c3d4_element_stress (`solver/element.py:905-937`): sig [M,3,3], vm [M]; bad_idx (nullable, preset to M)
+ * receives the lowest element index with |det| < 1e-12 (the reference's B-matrix ValueError, `:857-858`). */
+int fem_tet4_stress(const double* coords, const int64_t* conn, int64_t M, const double* u, double E, double nu,
+                    double* sig, double* vm, int64_t* bad_idx, fem_stream_t stream);
+/* compute_c3d8/c3d6/c3d10_element_stress (`:1696-1752`, `:2570-2629`, `:1127-1189`) at n_ip points with natural
+ * derivative tables dN [n_ip, npe, 3] (npe 6, 8, 10) and weights w [n_ip]. layout 0: sum_q w_q sig_q -> [M,3,3] and
+ * sum_q w_q vm_q -> [M] (single=True); 1: [M,n_ip,3,3] / [M,n_ip] (c3d8/c3d6 single=False); 2: [n_ip,M,3,3] /
+ * [n_ip,M] (c3d10 single=False). */
+int fem_iso_stress(const double* coords, const int64_t* conn, int64_t M, int npe, const double* u, double E, double nu,
+                   const double* dN, const double* w, int n_ip, int layout, double* sig, double* vm,
+                   fem_stream_t stream);
+/* compute_stress_tensor (`:308-330`): Voigt [M,6] (xx, yy, zz, xy, yz, xz) -> [M,3,3] */
+int fem_voigt_to_tensor(const double* voigt, int64_t M, double* tensor, fem_stream_t stream);
+/* compute_von_mises_stress (`:332-353`): [M,3,3] -> [M] */
+int fem_von_mises(const double* tensor, int64_t M, double* vm, fem_stream_t stream);
+/* compute_node_vm_stress (`:466-504`): out[n] = mean of ev[e] over the incidence of node n (0 if none), summed in
+ * ascending element order (the reference's sequential index_add); inc from fem_incidence of the same [M,npe] */
+int fem_node_average(const double* ev, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N, double* out,
+                     fem_stream_t stream);
+/* compute_c3d4_surface_forces (`:3343-3362`): out [M,F,3] = sig_e n_ef for normals [M,F,3], sig [M,3,3] */
+int fem_face_forces(const double* normals, const double* sig, int64_t M, int F, double* out, fem_stream_t stream);
+/* compute_c3d4_shared_face_forces_sum (`:3364-3382`): out [S,3] = ff[e0,f0] + ff[e1,f1], idx [S,2,2] (validated by
+ * the caller), ff [M,F,3] */
+int fem_shared_face_sum(const int64_t* idx, const double* face_forces, int F, int64_t S, double* out,
+                        fem_stream_t stream);
+
 /* ------------------------------------------------------------------ SpMV (L2)
  * y = A x on the SELL-64 matrix (nrows block rows of size bs). */
 int fem_spmv(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_t* cols, const double* vals,

@@ -212,6 +212,81 @@ def iso_K(coords, elements, etype, E, nu, points=None, weights=None, single=True
     return K if K is not None else torch.stack(out, 0)
 
 
+# ----------------------------------------------------------------------------- stress recovery
+def stress_tensor(v):
+    """Voigt [M,6] (xx, yy, zz, xy, yz, xz) -> [M,3,3]. `solver/element.py:308-330`."""
+    t = torch.zeros((v.shape[0], 3, 3), dtype=v.dtype)
+    for (i, j), k in (((0, 0), 0), ((1, 1), 1), ((2, 2), 2), ((0, 1), 3), ((1, 0), 3), ((0, 2), 5), ((2, 0), 5),
+                      ((1, 2), 4), ((2, 1), 4)):
+        t[:, i, j] = v[:, k]
+    return t
+
+
+def von_mises(t):
+    """`solver/element.py:332-353` (upper-triangle shears)."""
+    sxx, syy, szz = t[:, 0, 0], t[:, 1, 1], t[:, 2, 2]
+    sxy, sxz, syz = t[:, 0, 1], t[:, 0, 2], t[:, 1, 2]
+    return torch.sqrt(((sxx - syy) ** 2 + (syy - szz) ** 2 + (szz - sxx) ** 2 + 6 * (sxy ** 2 + syz ** 2 + sxz ** 2)) / 2)
+
+
+def _point_stress(B, ue, D):
+    strain = torch.bmm(B, ue.unsqueeze(2)).squeeze(2)     # [M,6]
+    s = stress_tensor(torch.matmul(strain, D.t()))
+    return s, von_mises(s)
+
+
+def tet4_stress(coords, elements, u, E, nu):
+    """`compute_c3d4_element_stress`, `solver/element.py:905-937` -> ([M,3,3], [M])."""
+    ue = u[elements].reshape(elements.shape[0], -1)
+    return _point_stress(tet4_B(coords, elements), ue, elasticity_matrix(E, nu))
+
+
+def iso_stress(coords, elements, u, etype, E, nu, points=None, weights=None, single=True):
+    """`compute_c3d8_element_stress` (`:1696-1752`), `compute_c3d6_element_stress` (`:2570-2629`): stack per point,
+    single -> einsum("i,mijk->mjk") weights; `compute_c3d10_element_stress` (`:1127-1189`): single -> running
+    `+= tensor * w` in point order, else a point-major stack."""
+    if points is None:
+        points, weights = POINTS[etype]()
+    D = elasticity_matrix(E, nu)
+    ue = u[elements].reshape(elements.shape[0], -1)
+    M, n = elements.shape[0], points.shape[0]
+    sig, vm = [], []
+    acc_s, acc_v = torch.zeros((M, 3, 3), dtype=F64), torch.zeros(M, dtype=F64)
+    for q in range(n):
+        dN = DN[etype](*[float(v) for v in points[q]])
+        s, v = _point_stress(_voigt_B(iso_gradients(coords, elements, dN)), ue, D)
+        if etype == "c3d10" and single:
+            acc_s += s * weights[q]
+            acc_v += v * weights[q]
+        sig.append(s)
+        vm.append(v)
+    if etype == "c3d10":
+        return (acc_s, acc_v) if single else (torch.stack(sig, 0), torch.stack(vm, 0))
+    S, V = torch.stack(sig, 1), torch.stack(vm, 1)     # [M,n,3,3], [M,n]
+    if single:
+        return torch.einsum("i,mijk->mjk", weights, S), torch.einsum("i,mi->m", weights, V)
+    return S, V
+
+
+def node_average(elements, ev, N):
+    """`compute_node_vm_stress`, `solver/element.py:466-504`: index_add sums / counts, 0 where unused."""
+    idx = elements.reshape(-1)
+    vals = ev.repeat_interleave(elements.shape[1])
+    s = torch.zeros(N, dtype=ev.dtype).index_add(0, idx, vals)
+    c = torch.zeros(N, dtype=ev.dtype).index_add(0, idx, torch.ones_like(vals))
+    return torch.where(c > 0, s / c, torch.zeros_like(s))
+
+
+def face_forces(normals, sig):
+    """`compute_c3d4_surface_forces`, `solver/element.py:3343-3362`."""
+    return torch.matmul(sig.unsqueeze(1), normals.unsqueeze(-1)).squeeze(-1)
+
+
+def shared_face_sum(idx, ff):
+    """`compute_c3d4_shared_face_forces_sum`, `solver/element.py:3364-3382`."""
+    return ff[idx[:, 0, 0], idx[:, 0, 1], :] + ff[idx[:, 1, 0], idx[:, 1, 1], :]
+
+
 # ----------------------------------------------------------------------------- operator / preconditioner
 def dof_map(elements, dpn):
     """dof = dpn*node + comp, element-major (`solver/element.py:451-452`)."""

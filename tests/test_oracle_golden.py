@@ -114,3 +114,25 @@ def test_constrained_cg_oracle_matches_reference():
     Fb = R.loads_to_F(g["coords"].shape[0], c["loads_b"])
     u, n, s = R.constrained_cg(K, g["tets"], Fb, c["rbe2_b"], c["spc"], c["rbe3_b"], tol=tol, max_iter=3000)
     assert s == "converged" and n == int(g["n_iter_b"]) and rel(u, g["u_b"]) == 0.0
+
+
+def test_stress_recovery_oracle_matches_reference():
+    """compute_*_element_stress / compute_node_vm_stress / surface + shared-face forces (§8(f) row 2)."""
+    s = load_golden("stress")
+    g = load_golden("tet4_cube_n4_jit")
+    c, t = g["coords"], g["tets"]
+    sig, vm = R.tet4_stress(c, t, g["u_cg"], E, NU)
+    assert rel(sig, s["c3d4_sig"]) == 0.0 and rel(vm, s["c3d4_vm"]) == 0.0
+    assert rel(R.node_average(t, vm, c.shape[0]), s["c3d4_node_vm"]) == 0.0
+    assert rel(R.face_forces(s["normals"], sig), s["face_forces"]) == 0.0
+    assert rel(R.shared_face_sum(s["shared_idx"], s["face_forces"]), s["shared_sum"]) == 0.0
+    T = R.stress_tensor(s["voigt"])
+    assert rel(T, s["voigt_tensor"]) == 0.0 and rel(R.von_mises(T), s["voigt_vm"]) == 0.0
+    for et in ("c3d8", "c3d6", "c3d10"):
+        cg = load_golden(f"{et}_cells")
+        cc, ce, u = cg["coords"], cg["elements"], s[f"{et}_u"]
+        s1, v1 = R.iso_stress(cc, ce, u, et, E, NU, single=True)
+        s0, v0 = R.iso_stress(cc, ce, u, et, E, NU, single=False)
+        assert rel(s1, s[f"{et}_sig1"]) < 1e-15 and rel(v1, s[f"{et}_vm1"]) < 1e-15, et
+        assert rel(s0, s[f"{et}_sig0"]) < 1e-15 and rel(v0, s[f"{et}_vm0"]) < 1e-15, et
+        assert rel(R.node_average(ce, s[f"{et}_vm1"], cc.shape[0]), s[f"{et}_node_vm"]) == 0.0, et

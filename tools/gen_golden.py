@@ -258,6 +258,38 @@ def gen_constrained(el, so):
          constraints=np.array(cons))
 
 
+def gen_stress(el, so):
+    """Stress recovery on the golden meshes with seeded displacements."""
+    g = np.load(os.path.join(OUT, "tet4_cube_n4_jit.npz"))
+    coords, tets = torch.from_numpy(g["coords"]), torch.from_numpy(g["tets"])
+    u = torch.from_numpy(g["u_cg"])
+    out = {}
+    s4, v4 = el.compute_element_stress(coords, tets, u, E, NU, "c3d4", device=CPU, dtype=F64)
+    out.update(c3d4_sig=s4, c3d4_vm=v4,
+               c3d4_node_vm=el.compute_node_vm_stress(coords, tets, v4, device=CPU, dtype=F64))
+    rng = np.random.default_rng(7)
+    normals = torch.from_numpy(rng.standard_normal((tets.shape[0], 4, 3)))
+    ff = el.compute_c3d4_surface_forces(normals, s4, device=CPU)
+    S = 40
+    sidx = torch.stack([torch.from_numpy(rng.integers(0, tets.shape[0], (S, 2))),
+                        torch.from_numpy(rng.integers(0, 4, (S, 2)))], dim=-1)   # [S, 2, (elem, face)]
+    out.update(normals=normals, face_forces=ff, shared_idx=sidx,
+               shared_sum=el.compute_c3d4_shared_face_forces_sum(sidx, ff, device=CPU))
+    voigt = torch.from_numpy(rng.standard_normal((16, 6)))
+    T = el.compute_stress_tensor(voigt)
+    out.update(voigt=voigt, voigt_tensor=T, voigt_vm=el.compute_von_mises_stress(T))
+    for etype in ("c3d8", "c3d6", "c3d10"):
+        c = np.load(os.path.join(OUT, f"{etype}_cells.npz"))
+        cc, ce = torch.from_numpy(c["coords"]), torch.from_numpy(c["elements"])
+        ue = torch.from_numpy(rng.standard_normal((cc.shape[0], 3))) * 1e-3
+        s1, v1 = el.compute_element_stress(cc, ce, ue, E, NU, etype, single=True, device=CPU, dtype=F64)
+        s0, v0 = el.compute_element_stress(cc, ce, ue, E, NU, etype, single=False, device=CPU, dtype=F64)
+        out.update({f"{etype}_u": ue, f"{etype}_sig1": s1, f"{etype}_vm1": v1, f"{etype}_sig0": s0,
+                    f"{etype}_vm0": v0, f"{etype}_node_vm": el.compute_node_vm_stress(cc, ce, v1, device=CPU,
+                                                                                        dtype=F64)})
+    save("stress", **out)
+
+
 def main():
     if not os.path.isdir(REF):
         print("reference not present; nothing to do")
@@ -272,6 +304,7 @@ def main():
     gen_mixed(el, so)
     gen_partition(el, so)
     gen_constrained(el, so)
+    gen_stress(el, so)
     return 0
 
 
