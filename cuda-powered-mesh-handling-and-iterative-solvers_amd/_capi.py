@@ -58,6 +58,15 @@ SIGNATURES = {
     "fem_node_average": (_I, [_P, _I, _P, _P, _L, _P, _P]),
     "fem_face_forces": (_I, [_P, _P, _L, _I, _P, _P]),
     "fem_shared_face_sum": (_I, [_P, _P, _I, _L, _P, _P]),
+    "fem_topo_create": (_I, [_P, _L, _I, _P, _I, _I, _L, _P, ctypes.POINTER(_P)]),
+    "fem_topo_counts": (_I, [_P, ctypes.POINTER(_L), ctypes.POINTER(_L), ctypes.POINTER(_L)]),
+    "fem_topo_pairs": (_I, [_P, _P]),
+    "fem_topo_unique": (_I, [_P, _P]),
+    "fem_topo_boundary": (_I, [_P, _P, _I, _P, _P, _P, _P, _P, ctypes.POINTER(_L)]),
+    "fem_topo_destroy": (None, [_P]),
+    "fem_sub_elements": (_I, [_P, _L, _I, _P, _I, _I, _P, _P]),
+    "fem_element_face_normals": (_I, [_P, _P, _L, _I, _P, _P, _P, _P, _I, _D, _I, _I, _P, _P]),
+    "fem_surface_normals": (_I, [_P, _P, _P, _L, _I, _I, _P, _P]),
     "fem_spmv": (_I, [_L, _I, _P, _P, _P, _P, _P, _P]),
     "fem_spmv_variant": (_I, [_I, _I, _L, _I, _P, _P, _P, _P, _P, _P]),
     "fem_sell_delta16": (_I, [_P, _L, _P, _P, _P, _P]),

@@ -595,3 +595,14 @@ __all__ += [
     "compute_c3d8_element_stress", "compute_c3d6_element_stress", "compute_c3d10_element_stress",
     "compute_node_vm_stress", "compute_c3d4_surface_forces", "compute_c3d4_shared_face_forces_sum",
 ]
+
+# mesh topology lives in topology.py; re-exported here because the reference keeps it in
+# element.py (`solver/element.py:543-762,963-993,1293-1581,2234-2446,2687-2713`)
+try:
+    from . import topology as _topo
+except ImportError:  # pragma: no cover - flat import from the package directory
+    import topology as _topo  # type: ignore
+from_topology = [n for n in _topo.__all__ if n != "FaceGroups"]
+globals().update({n: getattr(_topo, n) for n in from_topology})
+__all__ += from_topology
+del from_topology

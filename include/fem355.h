@@ -197,6 +197,43 @@ int fem_face_forces(const double* normals, const double* sig, int64_t M, int F, 
 int fem_shared_face_sum(const int64_t* idx, const double* face_forces, int F, int64_t S, double* out,
                         fem_stream_t stream);
 
+/* ------------------------------------------------------------------ mesh topology
+ * Face / edge grouping: every element face of table ftab [F, fpn] (local node indices, element-major flat id
+ * e * F + f) is keyed by its sorted node ids and radix-sorted once (stable), which reproduces torch.unique(dim=0)
+ * row order and the reference's pairing order (`solver/element.py:543-579,707-762,1293-1334,1474-1532,2234-2283,
+ * 2687-2713`). N bounds the node ids (< 2^32); F <= 12, fpn <= 4, M * F < 2^31. [sync] */
+typedef struct fem_topo fem_topo;
+int fem_topo_create(const int64_t* conn, int64_t M, int npe, const int32_t* ftab, int F, int fpn, int64_t N,
+                    fem_stream_t stream, fem_topo** out);
+/* number of distinct faces, of faces occurring once (surfaces) and of faces occurring exactly twice (shared) */
+int fem_topo_counts(const fem_topo* t, int64_t* n_unique, int64_t* n_single, int64_t* n_pair);
+/* shared faces [n_pair, 2, 2] = ((e0, f0), (e1, f1)) in key order, e0 * F + f0 < e1 * F + f1
+ * (identify_*_shared_faces) */
+int fem_topo_pairs(fem_topo* t, int64_t* out);
+/* distinct sorted node tuples [n_unique, fpn] in lexicographic order (element_to_edge) */
+int fem_topo_unique(fem_topo* t, int64_t* out);
+/* faces occurring once, in face-major order fs * M + e of a caller table of Fs rows: stab [Fs, fpn] gives the
+ * output node order, smap [Fs] the context row with the same node set, xtab [Fs] (nullable) the extra node
+ * (compute_*_surface_faces_with_*_node). faces [count, fpn], extra [count] may be NULL to only count. [sync] */
+int fem_topo_boundary(fem_topo* t, const int64_t* conn, int Fs, const int32_t* smap, const int32_t* stab,
+                      const int32_t* xtab, int64_t* faces, int64_t* extra, int64_t* count);
+void fem_topo_destroy(fem_topo* t);
+/* out [M * T, spe] = conn[:, tab] (c3d8_to_c3d4 `:1555-1581`, c3d6_to_c3d4 `:2424-2446`, c3d10_to_c3d4 `:963-993`) */
+int fem_sub_elements(const int64_t* conn, int64_t M, int npe, const int32_t* tab, int T, int spe, int64_t* out,
+                     fem_stream_t stream);
+/* per element face normals [M, F, 3]: (p[e1] - p[e0]) x (p[e2] - p[e0]) * scale for edges [F, 3]; unit: normalise;
+ * flip: negate when dot(n, x[extra] - mean(x[cen[f][0..ncen[f])])) > 0 (cen is [F, 4]).
+ * compute_tetrahedral_normals_and_area `:652-705`, compute_hexahedral_normals_and_area `:1418-1472`,
+ * compute_wedge_normals_and_area `:2377-2422` */
+int fem_element_face_normals(const double* coords, const int64_t* conn, int64_t M, int npe, const int32_t* edges,
+                             const int32_t* cen, const int32_t* ncen, const int32_t* extra, int F, double scale,
+                             int flip, int unit, double* out, fem_stream_t stream);
+/* outward unit normals of surface faces [K, fpn] with extra nodes [K]; second edge to vertex v2
+ * (compute_tetrahdral_surface_normals `:581-619`, compute_hexahedral_surface_normals `:1336-1374`,
+ * compute_wedge_surface_normals `:2285-2338`) */
+int fem_surface_normals(const double* coords, const int64_t* faces, const int64_t* extra, int64_t K, int fpn, int v2,
+                        double* out, fem_stream_t stream);
+
 /* ------------------------------------------------------------------ SpMV (L2)
  * y = A x on the SELL-64 matrix (nrows block rows of size bs). */
 int fem_spmv(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_t* cols, const double* vals,

@@ -555,3 +555,73 @@ def partition_local_maps(elements, element_ids):
     elems = elements[element_ids]
     g, inv = torch.unique(elems, return_inverse=True)
     return g, inv.reshape(elems.shape)
+
+
+# ----------------------------------------------------------------------------- mesh topology
+def boundary_faces(elements, table, extra):
+    """`compute_tetrahedral_surface_faces_with_fourth_node` (`solver/element.py:543-579`) and the hex / wedge
+    variants (`:1293-1334`, `:2234-2283`): faces seen once, face-major order, plus their extra node."""
+    faces = torch.cat([elements[:, list(r)] for r in table], 0)
+    xs = torch.cat([elements[:, x] for x in extra], 0)
+    _, inv, cnt = torch.unique(torch.sort(faces, dim=1)[0], dim=0, return_inverse=True, return_counts=True)
+    m = cnt[inv] == 1
+    return faces[m], xs[m]
+
+
+def shared_faces(elements, table):
+    """`identify_tetrahedral_shared_faces` (`:707-762`) / `identify_hexahedral_shared_faces` (`:1474-1532`)."""
+    M, F = elements.shape[0], len(table)
+    flat = torch.sort(elements[:, torch.tensor(table)], dim=2)[0].reshape(-1, len(table[0]))
+    eid = torch.arange(M).repeat_interleave(F)
+    fid = torch.tile(torch.arange(F), (M,))
+    _, inv, cnt = torch.unique(flat, return_inverse=True, return_counts=True, dim=0)
+    ids = torch.nonzero(cnt == 2, as_tuple=True)[0]
+    if ids.numel() == 0:
+        return torch.empty((0, 2, 2), dtype=torch.long)
+    sinv, order = torch.sort(inv)
+    pos = torch.searchsorted(sinv, ids)
+    e, f = eid[order], fid[order]
+    return torch.stack([torch.stack([e[pos], f[pos]], 1), torch.stack([e[pos + 1], f[pos + 1]], 1)], 1)
+
+
+def surface_normals(coords, faces, extra, v2):
+    """`compute_tetrahdral_surface_normals` (`:581-619`), hex (`:1336-1374`), wedge (`:2285-2338`)."""
+    p = coords[faces]
+    n = torch.cross(p[:, 1] - p[:, 0], p[:, v2] - p[:, 0], dim=1)
+    n = n / torch.norm(n, dim=1, keepdim=True)
+    t = coords[extra] - p.mean(dim=1)
+    t = t / torch.norm(t, dim=1, keepdim=True)
+    d = (n * t).sum(dim=1)
+    n[d > 0] = -n[d > 0]
+    return n
+
+
+def element_face_normals(coords, elements, table, edge_rows, extra=None, scale=1.0, unit=False):
+    """`compute_tetrahedral_normals_and_area` (`:652-705`, scale 1/2), hex (`:1418-1472`), wedge (`:2377-2422`,
+    unit, no orientation): (p[r1]-p[r0]) x (p[r2]-p[r0]) per face row."""
+    ce = coords[elements]
+    outs = []
+    for f, (a0, a1, a2) in enumerate(edge_rows):
+        n = torch.cross(ce[:, a1] - ce[:, a0], ce[:, a2] - ce[:, a0], dim=1)
+        if scale != 1.0:
+            n = n / (1.0 / scale)
+        outs.append(n)
+    n = torch.stack(outs, 1)
+    if unit:
+        n = n / torch.norm(n, dim=2, keepdim=True)
+    if extra is not None:
+        cen = torch.stack([ce[:, list(r)].mean(dim=1) for r in table], 1)
+        d = torch.sum(n * (coords[elements[:, list(extra)]] - cen), dim=2)
+        n[d > 0] = -n[d > 0]
+    return n
+
+
+def unique_edges(elements, edges):
+    """`element_to_edge`, `:2687-2713`."""
+    e = torch.sort(elements[:, torch.tensor(edges)].view(-1, 2), dim=1)[0]
+    return torch.unique(e, dim=0).t()
+
+
+def split_elements(elements, table):
+    """`c3d8_to_c3d4` (`:1555-1581`), `c3d6_to_c3d4` (`:2424-2446`), `c3d10_to_c3d4` (`:963-993`)."""
+    return elements[:, torch.tensor(table)].reshape(-1, len(table[0]))

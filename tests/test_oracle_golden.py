@@ -136,3 +136,34 @@ def test_stress_recovery_oracle_matches_reference():
         assert rel(s1, s[f"{et}_sig1"]) < 1e-15 and rel(v1, s[f"{et}_vm1"]) < 1e-15, et
         assert rel(s0, s[f"{et}_sig0"]) < 1e-15 and rel(v0, s[f"{et}_vm0"]) < 1e-15, et
         assert rel(R.node_average(ce, s[f"{et}_vm1"], cc.shape[0]), s[f"{et}_node_vm"]) == 0.0, et
+
+
+def test_topology_oracle_matches_reference():
+    """Surface faces / normals, shared faces, edges and element splits (§8(f) row 3)."""
+    from fem355 import topology as T
+    g = load_golden("topology")
+    c, t = g["tet_coords"], g["tets"]
+    f, x = R.boundary_faces(t, T.TET_SURFACE, T.TET_SURFACE_X)
+    assert torch.equal(f, g["tet_surf"]) and torch.equal(x, g["tet_surf_x"])
+    assert rel(R.surface_normals(c, f, x, 2), g["tet_surf_n"]) == 0.0
+    assert rel(R.element_face_normals(c, t, T.TET_SHARED, T.TET_SHARED, T.TET_SHARED_X, scale=0.5),
+               g["tet_area_n"]) == 0.0
+    assert torch.equal(R.shared_faces(t, T.TET_SHARED), g["tet_shared"])
+    assert torch.equal(R.unique_edges(t, T.EDGES), g["tet_edges"])
+    ch, h = g["hex_coords"], g["hexes"]
+    f, x = R.boundary_faces(h, T.HEX, T.HEX_SURFACE_X)
+    assert torch.equal(f, g["hex_surf"]) and torch.equal(x, g["hex_surf_x"])
+    assert rel(R.surface_normals(ch, f, x, 2), g["hex_surf_n"]) == 0.0
+    rows = [[r[0], r[1], r[3]] for r in T.HEX]
+    assert rel(R.element_face_normals(ch, h, T.HEX, rows, T.HEX_AREA_X), g["hex_area_n"]) == 0.0
+    assert torch.equal(R.shared_faces(h, T.HEX), g["hex_shared"])
+    cw, w = g["wedge_coords"], g["wedges"]
+    fq, xq = R.boundary_faces(w, T.WEDGE_QUAD, T.WEDGE_QUAD_X)
+    ft, xt = R.boundary_faces(w, T.WEDGE_TRI, T.WEDGE_TRI_X)
+    assert torch.equal(fq, g["wedge_surf_q"]) and torch.equal(ft, g["wedge_surf_t"])
+    assert torch.equal(xq, g["wedge_surf_xq"]) and torch.equal(xt, g["wedge_surf_xt"])
+    assert rel(R.surface_normals(cw, fq, xq, 3), g["wedge_surf_nq"]) == 0.0
+    assert rel(R.surface_normals(cw, ft, xt, 2), g["wedge_surf_nt"]) == 0.0
+    assert torch.equal(R.split_elements(h, T.SPLIT[8]), g["hex_tets"])
+    assert torch.equal(R.split_elements(w, T.SPLIT[6]), g["wedge_tets"])
+    assert torch.equal(R.split_elements(g["tet10"], T.SPLIT[10]), g["tet10_tets"])

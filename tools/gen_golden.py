@@ -290,6 +290,40 @@ def gen_stress(el, so):
     save("stress", **out)
 
 
+def gen_topology(el, so):
+    """Topology on small jittered meshes with some elements removed (holes -> inner
+    surfaces), tets / hexes / wedges / c3d10."""
+    out = {}
+    rng = np.random.default_rng(11)
+    ct, tt = mesh.kuhn_cube(3, jitter=0.15, seed=5)
+    tt = tt[torch.from_numpy(np.sort(rng.choice(tt.shape[0], tt.shape[0] - 9, replace=False)))]
+    f, x = el.compute_tetrahedral_surface_faces_with_fourth_node(tt, device=CPU)
+    out.update(tet_coords=ct, tets=tt, tet_surf=f, tet_surf_x=x,
+               tet_surf_n=el.compute_tetrahdral_surface_normals(ct, tt, device=CPU, dtype=F64),
+               tet_area_n=el.compute_tetrahedral_normals_and_area(ct, tt, device=CPU, dtype=F64),
+               tet_shared=el.identify_tetrahedral_shared_faces(tt, device=CPU),
+               tet_edges=el.element_to_edge(tt, device=CPU))
+    ch, hh = mesh.hex_box(3, jitter=0.15, seed=6)
+    hh = hh[torch.from_numpy(np.sort(rng.choice(hh.shape[0], hh.shape[0] - 3, replace=False)))]
+    f, x = el.compute_hexahedral_surface_faces_with_extra_node(hh, device=CPU)
+    out.update(hex_coords=ch, hexes=hh, hex_surf=f, hex_surf_x=x,
+               hex_surf_n=el.compute_hexahedral_surface_normals(ch, hh, device=CPU, dtype=F64),
+               hex_area_n=el.compute_hexahedral_normals_and_area(ch, hh, device=CPU, dtype=F64),
+               hex_shared=el.identify_hexahedral_shared_faces(hh, device=CPU),
+               hex_tets=el.c3d8_to_c3d4(hh, device=CPU))
+    cw, ww = mesh.wedge_box(2, jitter=0.1, seed=7)
+    # compute_wedge_normals_and_area raises in the reference itself (torch.cross(..., dim=3) on [M, 3, 3]
+    # tensors, `solver/element.py:2409,2415`): not a fixture
+    (fq, ft), (xq, xt) = el.compute_wedge_surface_faces_with_extra_node(ww, device=CPU)
+    nq, nt = el.compute_wedge_surface_normals(cw, ww, device=CPU, dtype=F64)
+    out.update(wedge_coords=cw, wedges=ww, wedge_surf_q=fq, wedge_surf_t=ft, wedge_surf_xq=xq, wedge_surf_xt=xt,
+               wedge_surf_nq=nq, wedge_surf_nt=nt,
+               wedge_tets=el.c3d6_to_c3d4(ww, device=CPU))
+    c10, t10 = mesh.tet10_cube(1)
+    out.update(tet10=t10, tet10_tets=el.c3d10_to_c3d4(t10, device=CPU))
+    save("topology", **out)
+
+
 def main():
     if not os.path.isdir(REF):
         print("reference not present; nothing to do")
@@ -305,6 +339,7 @@ def main():
     gen_partition(el, so)
     gen_constrained(el, so)
     gen_stress(el, so)
+    gen_topology(el, so)
     return 0
 
 
