@@ -67,6 +67,10 @@ SIGNATURES = {
     "fem_sub_elements": (_I, [_P, _L, _I, _P, _I, _I, _P, _P]),
     "fem_element_face_normals": (_I, [_P, _P, _L, _I, _P, _P, _P, _P, _I, _D, _I, _I, _P, _P]),
     "fem_surface_normals": (_I, [_P, _P, _P, _L, _I, _I, _P, _P]),
+    "fem_vtk_read": (_I, [ctypes.c_char_p, ctypes.POINTER(_P)]),
+    "fem_vtk_sizes": (_I, [_P, ctypes.POINTER(_L), ctypes.POINTER(_L), ctypes.POINTER(_L), ctypes.POINTER(_L)]),
+    "fem_vtk_copy": (_I, [_P, _P, _P, _P]),
+    "fem_vtk_free": (None, [_P]),
     "fem_spmv": (_I, [_L, _I, _P, _P, _P, _P, _P, _P]),
     "fem_spmv_variant": (_I, [_I, _I, _L, _I, _P, _P, _P, _P, _P, _P]),
     "fem_sell_delta16": (_I, [_P, _L, _P, _P, _P, _P]),

@@ -12,7 +12,9 @@ Out of scope: shells, topology, visualisation, c3d20/c3d15.
 """
 from __future__ import annotations
 
+import ctypes
 import math
+import os
 import warnings
 from collections import OrderedDict
 
@@ -29,7 +31,7 @@ F64 = torch.float64
 LONG = torch.long
 
 __all__ = [
-    "human_readable_number", "vtk_loader_to_torch", "compute_elasticity_matrix", "integral_points",
+    "human_readable_number", "vtk_loader_to_torch", "read_vtk", "compute_elasticity_matrix", "integral_points",
     "compute_Jacobian", "compute_shape_gradients", "compute_B_matrix", "compute_K_matrix", "compute_nodal_forces",
     "compute_tetrahedral_volumes", "compute_c3d4_B_matrix", "compute_c3d4_K_matrix", "compute_L_matrix",
     "compute_c3d4_M_matrix", "compute_c3d4_poisson_K_matrix",
@@ -51,10 +53,45 @@ def human_readable_number(num):
     return f"{num:.1f}"
 
 
-def vtk_loader_to_torch(file_path, element_type="c3d4", device="cuda:0", dtype=torch.float32):
-    """`solver/element.py:39-90` reads VTK through pyvista, which this image does not ship; the VTK reader is
-    a ranked next step, not part of this round's hot path."""
-    raise NotImplementedError("vtk_loader_to_torch: pyvista-free VTK reader not implemented yet (SURVEY §8(f)-4)")
+_VTK_NPE = {"c3d4": 4, "c3d10": 10, "c3d8": 8, "c3d20": 20, "c3d6": 6, "c3d15": 15, "s3": 3, "s6": 6, "s4": 4,
+            "s8": 8}
+
+
+def read_vtk(file_path):
+    """Parse a legacy VTK unstructured grid with the native reader (`csrc/vtk.cpp`, host only) ->
+    (points [N,3] float64 numpy, count-prefixed cell array int64 numpy, cell types int64 numpy)."""
+    import numpy as np
+    lib = C.load_library()
+    path = os.fspath(file_path)
+    if not os.path.exists(path):
+        raise FileNotFoundError(f"File '{path}' does not exist.")
+    h = ctypes.c_void_p()
+    C.check(lib.fem_vtk_read(path.encode(), ctypes.byref(h)), "fem_vtk_read")
+    try:
+        n = [ctypes.c_int64() for _ in range(4)]
+        lib.fem_vtk_sizes(h, *[ctypes.byref(v) for v in n])
+        npts, _, clen, ntyp = (v.value for v in n)
+        pts = np.empty((npts, 3), dtype=np.float64)
+        cells = np.empty(clen, dtype=np.int64)
+        types = np.empty(ntyp, dtype=np.int64)
+        lib.fem_vtk_copy(h, pts.ctypes.data_as(ctypes.c_void_p), cells.ctypes.data_as(ctypes.c_void_p),
+                         types.ctypes.data_as(ctypes.c_void_p))
+    finally:
+        lib.fem_vtk_free(h)
+    return pts, cells, types
+
+
+def vtk_loader_to_torch(file_path, element_type, device="cuda:0", dtype=torch.float32):
+    """(points [N,3], connectivity [M,npe]) from a VTK file: the count-prefixed cell array reshaped to
+    [-1, npe+1] with the count column dropped, exactly as `solver/element.py:39-90` does with pyvista's
+    mesh.cells (so mixed cell sizes fail the same way). ValueError("Invalid element type.") for other types."""
+    pts, cells, _ = read_vtk(file_path)
+    points = torch.tensor(pts, device=device, dtype=dtype)
+    if element_type not in _VTK_NPE:
+        raise ValueError("Invalid element type.")
+    npe = _VTK_NPE[element_type]
+    element = torch.tensor(cells.reshape(-1, npe + 1)[:, 1:], device=device, dtype=torch.long)
+    return points, element
 
 
 def _dev(device):

@@ -234,6 +234,16 @@ int fem_element_face_normals(const double* coords, const int64_t* conn, int64_t 
 int fem_surface_normals(const double* coords, const int64_t* faces, const int64_t* extra, int64_t K, int fpn, int v2,
                         double* out, fem_stream_t stream);
 
+/* ------------------------------------------------------------------ mesh input
+ * Legacy VTK unstructured grid (ASCII / BINARY, file versions 2.x-5.x) -> points [N,3] fp64, the count-prefixed
+ * cell array pyvista exposes as mesh.cells, and the VTK cell types: the file side of vtk_loader_to_torch
+ * (`solver/element.py:39-90`). [host] — plain host memory, no device needed. */
+typedef struct fem_vtk fem_vtk;
+int fem_vtk_read(const char* path, fem_vtk** out);
+int fem_vtk_sizes(const fem_vtk* v, int64_t* n_points, int64_t* n_cells, int64_t* cells_len, int64_t* n_types);
+int fem_vtk_copy(const fem_vtk* v, double* points, int64_t* cells, int64_t* types);
+void fem_vtk_free(fem_vtk* v);
+
 /* ------------------------------------------------------------------ SpMV (L2)
  * y = A x on the SELL-64 matrix (nrows block rows of size bs). */
 int fem_spmv(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_t* cols, const double* vals,
