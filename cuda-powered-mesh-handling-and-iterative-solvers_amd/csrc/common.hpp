@@ -45,6 +45,14 @@ inline int stream_grid(int64_t work_items, int block) {
     return (int)g;
 }
 
+// grid rounded to a multiple of the 8 XCDs (blockIdx % 8 selects the XCD), capped
+inline int grid_multiple_of_xcd(int64_t blocks, int cap) {
+    int64_t g = blocks;
+    if (g > cap) g = cap;
+    g = ((g + NXCD - 1) / NXCD) * NXCD;
+    return (int)(g < NXCD ? NXCD : g);
+}
+
 // ---------------------------------------------------------------- device reductions
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll

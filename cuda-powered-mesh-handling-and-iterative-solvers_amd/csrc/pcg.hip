@@ -18,7 +18,7 @@
 
 #include <vector>
 
-#include "common.hpp"
+#include "sell_pair.hpp"
 
 namespace fem {
 
@@ -92,7 +92,7 @@ __device__ __forceinline__ void sell_row(int64_t s, int lane, const int64_t* __r
 // contiguous slice range [x*spx, (x+1)*spx), walked 4 slices (one per wave) per block step, so the x-gather
 // window of an XCD stays in its own L2.
 struct SliceWalk {
-    int64_t s, end, step;
+    int64_t s, end, step, first;
 };
 
 __device__ __forceinline__ SliceWalk slice_walk(int64_t nslices) {
@@ -101,10 +101,11 @@ __device__ __forceinline__ SliceWalk slice_walk(int64_t nslices) {
     const int64_t spx = (nslices + NXCD - 1) / NXCD;
     const int64_t start = (int64_t)xcd * spx;
     const int64_t end = min(start + spx, nslices);
-    return SliceWalk{start + lb * 4 + (threadIdx.x >> 6), end, nlb * 4};
+    return SliceWalk{start + lb * 4 + (threadIdx.x >> 6), end, nlb * 4, start};
 }
 
 constexpr int SPMV_U = 8;   // tools/spmv_tune.py: U=8 beats 4 and 16 on the 10M Poisson matrix (gfx950)
+constexpr int SPMV_UP = 8;  // pairs in flight of the paired layout (tools/spmv_layout.py: 2, 4, 8 within 1 %)
 
 template <int BS, int U = SPMV_U, bool NT = false, typename CI = int32_t>
 __global__ void __launch_bounds__(256) k_spmv(int64_t nslices, int64_t nrows, const int64_t* __restrict__ slice_ptr,
@@ -221,7 +222,7 @@ struct RedBuf {
 
 // K1. FUSED: p (in p_buf[iter & 1]) is formed on the fly from r, w and the previous p (p_buf[(iter+1) & 1]);
 // this kernel also applies the deferred x += alpha_x p_prev to its own rows.
-template <int BS, bool FUSED, bool DOT = true, typename CI = int32_t>
+template <int BS, bool FUSED, bool DOT = true, typename CI = int32_t, bool PAIR = false>
 __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_spmv_dot(int64_t nslices, int64_t nrows,
                                                             const int64_t* __restrict__ slice_ptr,
                                                             const CI* __restrict__ cols,
@@ -229,7 +230,7 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_spmv_dot(int64_t nslices, int
                                                             double* __restrict__ p1, const double* __restrict__ r,
                                                             const double* __restrict__ w, double* __restrict__ x,
                                                             double* __restrict__ q, PcgState* __restrict__ st,
-                                                            RedBuf red) {
+                                                            RedBuf red, int tune_rev) {
     __shared__ double lds4[4];
     __shared__ int flag;
     if (!FUSED && blockIdx.x == 0 && threadIdx.x == 0) st->xupd = 0;
@@ -262,9 +263,14 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_spmv_dot(int64_t nslices, int
         }
     } else {
         const VecPlain pv{p0};
-        for (int64_t s = wk.s; s < wk.end; s += wk.step) {
+        // odd iterations sweep backwards (FEM_TUNE_REVERSE; parity from the device iteration count)
+        const bool rev = tune_rev && (iter & 1);
+        const int64_t mirror = wk.first + wk.end - 1;
+        for (int64_t s0 = wk.s; s0 < wk.end; s0 += wk.step) {
+            const int64_t s = rev ? mirror - s0 : s0;
             double o[BS];
-            sell_row<BS, SPMV_U, false, decltype(pv), CI>(s, lane, slice_ptr, cols, vals, pv, o);
+            if constexpr (PAIR) o[0] = sell_row_pair<SPMV_UP>(s, lane, slice_ptr, cols, vals, p0);
+            else sell_row<BS, SPMV_U, false, decltype(pv), CI>(s, lane, slice_ptr, cols, vals, pv, o);
             const int64_t row = s * 64 + lane;
             if (row < nrows) {
 #pragma unroll
@@ -375,12 +381,12 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_pupdate(int64_t n, double* __
 // (identical pq everywhere), alpha + guards, r update, one r.z partial per block.  d3: every block re-sums d2's
 // partials -> stop test, beta, x/p update; block 0 writes the NEXT bank. Bank = host launch parity, so no kernel
 // writes a state field its own blocks read.
-template <int BS, typename CI = int32_t>
+template <int BS, typename CI = int32_t, bool PAIR = false>
 __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_d1(int64_t nslices, int64_t nrows,
                                                       const int64_t* __restrict__ slice_ptr,
                                                       const CI* __restrict__ cols, const double* __restrict__ vals,
                                                       const double* __restrict__ p, double* __restrict__ q,
-                                                      const PcgState* __restrict__ st, int par,
+                                                      const PcgState* __restrict__ st, int par, int rev,
                                                       double* __restrict__ partials) {
     __shared__ double lds4[4];
     const PcgState::Bank& bk = st->bank[par];
@@ -389,9 +395,14 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_d1(int64_t nslices, int64_t n
     double dot = 0.0;
     SliceWalk wk = slice_walk(nslices);
     const VecPlain pv{p};
-    for (int64_t s = wk.s; s < wk.end; s += wk.step) {
+    // rev: this XCD's slice range is swept end -> start, so the slices the previous sweep touched last (still in
+    // the memory-side cache) are read first
+    const int64_t mirror = rev ? wk.first + wk.end - 1 : -1;
+    for (int64_t s0 = wk.s; s0 < wk.end; s0 += wk.step) {
+        const int64_t s = rev ? mirror - s0 : s0;
         double o[BS];
-        sell_row<BS, SPMV_U, false, decltype(pv), CI>(s, lane, slice_ptr, cols, vals, pv, o);
+        if constexpr (PAIR) o[0] = sell_row_pair<SPMV_UP>(s, lane, slice_ptr, cols, vals, p);
+        else sell_row<BS, SPMV_U, false, decltype(pv), CI>(s, lane, slice_ptr, cols, vals, pv, o);
         const int64_t row = s * 64 + lane;
         if (row < nrows) {
 #pragma unroll
@@ -764,6 +775,10 @@ struct fem_pcg {
     int64_t launched;   // iterations enqueued since start (the deferred schedule's bank parity)
     const int16_t* cols16;  // optional 16-bit column deltas (fem_sell_delta16): used instead of cols when set
     int has_con;            // CG_CONSTRAINED projections set (fem_pcg_set_constraints)
+    int tune;               // FEM_TUNE_* flags (fem_pcg_set_tuning)
+    int paired;             // the SpMV reads pvals / pcols16 (lane-paired copy, refreshed by fem_pcg_start)
+    double* pvals;
+    int16_t* pcols16;
     Constraints con;
     // owned device memory
     double* r;
@@ -806,8 +821,12 @@ static int launch_spmv_dot(fem_pcg* s) {
 #define FEM_K1D(B, F, D)                                                                                           \
     hipLaunchKernelGGL((k_pcg_spmv_dot<B, F, D, int16_t>), dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream,     \
                        s->nslices, s->nrows, s->slice_ptr, s->cols16, s->vals, s->p0, s->p1, s->r, s->w, s->x, s->q, \
-                       s->st, s->red)
-        if (s->dist) {
+                       s->st, s->red, s->tune & FEM_TUNE_REVERSE)
+        if (s->paired && !s->fused) {   // bs = 1, lane-paired copy of the matrix (sell_pair.hpp)
+            hipLaunchKernelGGL((k_pcg_spmv_dot<1, false, true, int16_t, true>), dim3(s->grid_spmv), dim3(PCG_BLOCK), 0,
+                               s->stream, s->nslices, s->nrows, s->slice_ptr, s->pcols16, s->pvals, s->p0, s->p1, s->r,
+                               s->w, s->x, s->q, s->st, s->red, s->tune & FEM_TUNE_REVERSE);
+        } else if (s->dist) {
             if (s->bs == 1) FEM_K1D(1, false, true);
             else FEM_K1D(3, false, true);
         } else if (s->bs == 1) {
@@ -823,7 +842,8 @@ static int launch_spmv_dot(fem_pcg* s) {
     }
 #define FEM_K1(B, F, D)                                                                                            \
     hipLaunchKernelGGL((k_pcg_spmv_dot<B, F, D>), dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream, s->nslices,   \
-                       s->nrows, s->slice_ptr, s->cols, s->vals, s->p0, s->p1, s->r, s->w, s->x, s->q, s->st, s->red)
+                       s->nrows, s->slice_ptr, s->cols, s->vals, s->p0, s->p1, s->r, s->w, s->x, s->q, s->st, s->red,  \
+                       s->tune & FEM_TUNE_REVERSE)
     if (s->dist) {
         if (s->bs == 1) FEM_K1(1, false, true);
         else FEM_K1(3, false, true);
@@ -998,20 +1018,25 @@ static int launch_update_finish(fem_pcg* s) {
 
 static int launch_deferred(fem_pcg* s, int which) {
     const int par = (int)(s->launched & 1);
+    const int rev = (s->tune & FEM_TUNE_REVERSE) ? par : 0;
     if (which == 0) {
-        if (s->cols16) {
+        if (s->paired) {
+            hipLaunchKernelGGL((k_pcg_d1<1, int16_t, true>), dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream,
+                               s->nslices, s->nrows, s->slice_ptr, s->pcols16, s->pvals, s->p0, s->q, s->st, par, rev,
+                               s->red.partials);
+        } else if (s->cols16) {
             if (s->bs == 1)
                 hipLaunchKernelGGL((k_pcg_d1<1, int16_t>), dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream, s->nslices,
-                                   s->nrows, s->slice_ptr, s->cols16, s->vals, s->p0, s->q, s->st, par, s->red.partials);
+                                   s->nrows, s->slice_ptr, s->cols16, s->vals, s->p0, s->q, s->st, par, rev, s->red.partials);
             else
                 hipLaunchKernelGGL((k_pcg_d1<3, int16_t>), dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream, s->nslices,
-                                   s->nrows, s->slice_ptr, s->cols16, s->vals, s->p0, s->q, s->st, par, s->red.partials);
+                                   s->nrows, s->slice_ptr, s->cols16, s->vals, s->p0, s->q, s->st, par, rev, s->red.partials);
         } else if (s->bs == 1)
             hipLaunchKernelGGL(k_pcg_d1<1>, dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream, s->nslices, s->nrows,
-                               s->slice_ptr, s->cols, s->vals, s->p0, s->q, s->st, par, s->red.partials);
+                               s->slice_ptr, s->cols, s->vals, s->p0, s->q, s->st, par, rev, s->red.partials);
         else
             hipLaunchKernelGGL(k_pcg_d1<3>, dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream, s->nslices, s->nrows,
-                               s->slice_ptr, s->cols, s->vals, s->p0, s->q, s->st, par, s->red.partials);
+                               s->slice_ptr, s->cols, s->vals, s->p0, s->q, s->st, par, rev, s->red.partials);
     } else if (which == 1) {
         hipLaunchKernelGGL(k_pcg_d2, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->r, s->q, s->w, s->st,
                            par, s->red.partials, s->grid_spmv, s->red.partials + MAX_PARTIALS);
@@ -1042,15 +1067,9 @@ static int launch_iterations(fem_pcg* s, int k) {
         if ((rc = launch_exchange_dot(s))) return rc;
         if ((rc = launch_update_finish(s))) return rc;
         if ((rc = launch_pupdate(s))) return rc;
+        s->launched++;
     }
     return FEM_OK;
-}
-
-static int grid_multiple_of_xcd(int64_t blocks, int cap) {
-    int64_t g = blocks;
-    if (g > cap) g = cap;
-    g = ((g + NXCD - 1) / NXCD) * NXCD;
-    return (int)(g < NXCD ? NXCD : g);
 }
 
 extern "C" {
@@ -1190,12 +1209,22 @@ int fem_enforce_constraints(double* x, double* r, int64_t n, int order, int64_t 
     return FEM_OK;
 }
 
+int fem_pcg_set_tuning(fem_pcg* s, int flags) {
+    if (s->graph) {
+        set_error("fem_pcg_set_tuning: drop the captured graph first");
+        return FEM_EARG;
+    }
+    s->tune = flags;
+    return FEM_OK;
+}
+
 int fem_pcg_set_cols16(fem_pcg* s, const int16_t* dcols) {
     if (s->graph) {
         set_error("fem_pcg_set_cols16: drop the captured graph first");
         return FEM_EARG;
     }
     s->cols16 = dcols;
+    if (!dcols) s->paired = 0;
     return FEM_OK;
 }
 
@@ -1257,6 +1286,7 @@ int fem_pcg_create(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_
         return FEM_EARG;
     }
     fem_pcg* s = new fem_pcg();
+    s->tune = FEM_TUNE_REVERSE | FEM_TUNE_PAIR;
     s->nrows = nrows;
     s->bs = bs;
     s->nslices = cdiv(nrows, 64);
@@ -1339,7 +1369,30 @@ static PcgState state_view(const fem_pcg* s) {
     return h;
 }
 
+// (re)build the lane-paired matrix copy used by the bs = 1 SpMV when FEM_TUNE_PAIR is set
+static int refresh_pairing(fem_pcg* s) {
+    const bool want = s->bs == 1 && s->cols16 && (s->tune & FEM_TUNE_PAIR) && !s->fused;
+    s->paired = 0;
+    if (!want || s->nslices == 0) return FEM_OK;
+    int64_t ent = 0;
+    FEM_HIP(hipMemcpyAsync(&ent, s->slice_ptr + s->nslices, sizeof(int64_t), hipMemcpyDeviceToHost, s->stream));
+    FEM_HIP(hipStreamSynchronize(s->stream));
+    if (!s->pvals) {
+        FEM_HIP(hipMalloc(&s->pvals, sizeof(double) * (size_t)ent));
+        FEM_HIP(hipMalloc(&s->pcols16, sizeof(int16_t) * (size_t)ent));
+    }
+    hipLaunchKernelGGL(k_sell_pair, dim3(stream_grid(s->nslices * 64, 256)), dim3(256), 0, s->stream, s->nslices,
+                       s->slice_ptr, s->vals, s->cols16, s->pvals, s->pcols16);
+    FEM_LAUNCHED();
+    s->paired = 1;
+    return FEM_OK;
+}
+
 int fem_pcg_start(fem_pcg* s) {
+    {
+        const int prc = refresh_pairing(s);
+        if (prc) return prc;
+    }
     PcgState h{};
     h.tol = s->tol;
     h.eps = s->eps;
@@ -1628,6 +1681,8 @@ void fem_pcg_destroy(fem_pcg* s) {
     if (s->red.counters) (void)hipFree(s->red.counters);
     if (s->hbuf) (void)hipFree(s->hbuf);
     if (s->con.tmp) (void)hipFree(s->con.tmp);
+    if (s->pvals) (void)hipFree(s->pvals);
+    if (s->pcols16) (void)hipFree(s->pcols16);
     if (s->st) (void)hipFree(s->st);
     if (s->st_host) (void)hipHostFree(s->st_host);
     delete s;

@@ -1,0 +1,113 @@
+// SpMV layout experiments (tools/spmv_layout.py): memory-instruction width probes and a lane-paired SELL-64
+// layout in which each lane loads two consecutive entries of its row with one 16-byte value load and one 4-byte
+// column load (the plain layout issues one 8-byte value and one 2-byte column load per entry).
+//
+// Paired layout of slice s (width w, base p0 = slice_ptr[s]): entry k < 2*(w/2) of lane l lives at
+//   p0 + (k/2)*128 + 2*l + (k%2), the odd tail entry (w odd) at p0 + (w/2)*128 + l;
+// same for the 16-bit column deltas. Footprint and slice_ptr are unchanged.
+#include "sell_pair.hpp"
+
+namespace fem {
+
+// copy probes: W bytes per lane per instruction (8, 16, 32)
+template <int W>
+__global__ void __launch_bounds__(256) k_copy_w(const double* __restrict__ src, double* __restrict__ dst, int64_t n) {
+    constexpr int D = W / 8;
+    const int64_t nv = n / D;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (int64_t)gridDim.x * 256) {
+        if constexpr (D == 1) {
+            dst[i] = src[i];
+        } else if constexpr (D == 2) {
+            reinterpret_cast<double2*>(dst)[i] = reinterpret_cast<const double2*>(src)[i];
+        } else {
+            const double2* s2 = reinterpret_cast<const double2*>(src) + 2 * i;
+            double2 a = s2[0], b = s2[1];
+            double2* d2 = reinterpret_cast<double2*>(dst) + 2 * i;
+            d2[0] = a;
+            d2[1] = b;
+        }
+    }
+}
+
+// read-only probe: sum of W-byte loads (no writes)
+template <int W>
+__global__ void __launch_bounds__(256) k_read_w(const double* __restrict__ src, int64_t n, double* __restrict__ out) {
+    constexpr int D = W / 8;
+    const int64_t nv = n / D;
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nv; i += (int64_t)gridDim.x * 256) {
+        if constexpr (D == 1) {
+            acc += src[i];
+        } else {
+            const double2 v = reinterpret_cast<const double2*>(src)[i];
+            acc += v.x + v.y;
+        }
+    }
+    if (acc == 12345.678) out[0] = acc;   // keep the loads alive
+}
+
+template <int U>
+__global__ void __launch_bounds__(256) k_spmv16_pair(int64_t nslices, int64_t nrows,
+                                                     const int64_t* __restrict__ slice_ptr,
+                                                     const int16_t* __restrict__ cols, const double* __restrict__ vals,
+                                                     const double* __restrict__ x, double* __restrict__ y) {
+    const int lane = threadIdx.x & 63;
+    const int xcd = blockIdx.x % NXCD;
+    const int64_t lb = blockIdx.x / NXCD, nlb = gridDim.x / NXCD;
+    const int64_t spx = (nslices + NXCD - 1) / NXCD;
+    const int64_t end = min((int64_t)(xcd + 1) * spx, nslices);
+    for (int64_t s = (int64_t)xcd * spx + lb * 4 + (threadIdx.x >> 6); s < end; s += nlb * 4) {
+        const double acc = sell_row_pair<U>(s, lane, slice_ptr, cols, vals, x);
+        const int64_t row = s * 64 + lane;
+        if (row < nrows) y[row] = acc;
+    }
+}
+
+}  // namespace fem
+
+using namespace fem;
+
+extern "C" {
+
+int fem_lab_copy(int width, int read_only, const double* src, double* dst, int64_t n, int grid, fem_stream_t stream) {
+    if (grid <= 0) grid = 2048;
+    const hipStream_t st = S(stream);
+    if (read_only) {
+        if (width == 8) hipLaunchKernelGGL(k_read_w<8>, dim3(grid), dim3(256), 0, st, src, n, dst);
+        else hipLaunchKernelGGL(k_read_w<16>, dim3(grid), dim3(256), 0, st, src, n, dst);
+    } else if (width == 8) {
+        hipLaunchKernelGGL(k_copy_w<8>, dim3(grid), dim3(256), 0, st, src, dst, n);
+    } else if (width == 16) {
+        hipLaunchKernelGGL(k_copy_w<16>, dim3(grid), dim3(256), 0, st, src, dst, n);
+    } else {
+        hipLaunchKernelGGL(k_copy_w<32>, dim3(grid), dim3(256), 0, st, src, dst, n);
+    }
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_lab_sell_pair(int64_t nrows, const int64_t* slice_ptr, const double* vals, const int16_t* dcols,
+                      double* vals_out, int16_t* dcols_out, fem_stream_t stream) {
+    const int64_t ns = cdiv(nrows, 64);
+    if (ns == 0) return FEM_OK;
+    hipLaunchKernelGGL(k_sell_pair, dim3(stream_grid(ns * 64, 256)), dim3(256), 0, S(stream), ns, slice_ptr, vals,
+                       dcols, vals_out, dcols_out);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_lab_spmv16_pair(int u, int grid, int64_t nrows, const int64_t* slice_ptr, const int16_t* dcols,
+                        const double* vals, const double* x, double* y, fem_stream_t stream) {
+    const int64_t ns = cdiv(nrows, 64);
+    if (ns == 0) return FEM_OK;
+    if (grid <= 0) grid = grid_multiple_of_xcd(cdiv(ns, 4), 2048);
+    grid = ((grid + NXCD - 1) / NXCD) * NXCD;
+    const hipStream_t st = S(stream);
+    if (u == 2) hipLaunchKernelGGL(k_spmv16_pair<2>, dim3(grid), dim3(256), 0, st, ns, nrows, slice_ptr, dcols, vals, x, y);
+    else if (u == 8) hipLaunchKernelGGL(k_spmv16_pair<8>, dim3(grid), dim3(256), 0, st, ns, nrows, slice_ptr, dcols, vals, x, y);
+    else hipLaunchKernelGGL(k_spmv16_pair<4>, dim3(grid), dim3(256), 0, st, ns, nrows, slice_ptr, dcols, vals, x, y);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+}  // extern "C"

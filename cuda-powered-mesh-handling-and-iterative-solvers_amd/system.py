@@ -310,6 +310,9 @@ class PcgRunner:
         if constraints is not None:
             C.check(self.lib.fem_pcg_set_constraints(self.h, *constraints.args()), "fem_pcg_set_constraints")
 
+    def set_tuning(self, flags):
+        C.check(self.lib.fem_pcg_set_tuning(self.h, int(flags)), "fem_pcg_set_tuning")
+
     def finish(self):
         C.check(self.lib.fem_pcg_finish(self.h), "fem_pcg_finish")
 

@@ -260,6 +260,13 @@ int fem_spmv16(int64_t nrows, int bs, const int64_t* slice_ptr, const int16_t* d
 int fem_spmv_variant(int variant, int grid, int64_t nrows, int bs, const int64_t* slice_ptr, const int32_t* cols,
                      const double* vals, const double* x, double* y, fem_stream_t stream);
 int fem_stream_copy(const double* src, double* dst, int64_t n, int grid, fem_stream_t stream);
+/* layout lab (tools/spmv_layout.py): W-byte-per-lane copy / read probes (W = 8, 16, 32), the lane-paired SELL-64
+ * layout (two consecutive entries of a row per 16-byte value load + 4-byte column load) and its SpMV */
+int fem_lab_copy(int width, int read_only, const double* src, double* dst, int64_t n, int grid, fem_stream_t stream);
+int fem_lab_sell_pair(int64_t nrows, const int64_t* slice_ptr, const double* vals, const int16_t* dcols,
+                      double* vals_out, int16_t* dcols_out, fem_stream_t stream);
+int fem_lab_spmv16_pair(int u, int grid, int64_t nrows, const int64_t* slice_ptr, const int16_t* dcols,
+                        const double* vals, const double* x, double* y, fem_stream_t stream);
 
 /* ------------------------------------------------------------------ (P)CG (L3)
  * One solve context over a SELL matrix. The whole iteration runs on the device: SpMV + p.q reduction,
@@ -310,6 +317,15 @@ int fem_enforce_constraints(double* x, double* r, int64_t n, int order, int64_t 
                             const int64_t* rbe2_master, int64_t S, const int64_t* spc_dof, const double* spc_val,
                             int64_t G, const int64_t* r3_ptr, const int64_t* r3_master, const double* r3_wsum,
                             const int64_t* r3_slave, const double* r3_w, fem_stream_t stream);
+/* tuning flags (default FEM_TUNE_REVERSE | FEM_TUNE_PAIR): the SpMV of every schedule sweeps each XCD's slice range backwards on
+ * odd iterations, so the matrix tail read last (still in the MI355X's 256 MB memory-side cache) is read first by
+ * the next sweep: 67 -> 57 us per SpMV on the 10M Poisson matrix. Results depend on the flags only through the
+ * order of the per-block p.q partials (deterministic for a given flag set). */
+enum { FEM_TUNE_REVERSE = 1, FEM_TUNE_PAIR = 2 };
+/* FEM_TUNE_PAIR (default): bs = 1 contexts with 16-bit columns keep a lane-paired copy of the matrix (two entries per
+ * 16-byte value load, sell_pair.hpp; +257 MB on the 10M Poisson matrix), rebuilt from vals / cols16 by every
+ * fem_pcg_start. Same products, same summation order per row as the plain layout. */
+int fem_pcg_set_tuning(fem_pcg* s, int flags);
 /* run the SpMV of this context on 16-bit column deltas (NULL: back to the int32 columns) */
 int fem_pcg_set_cols16(fem_pcg* s, const int16_t* dcols);
 /* apply the deferred x update of the fused schedule after the last iteration (fem_pcg_solve does this) */
