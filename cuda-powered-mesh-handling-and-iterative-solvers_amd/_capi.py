@@ -40,6 +40,9 @@ SIGNATURES = {
     "fem_incidence": (_I, [_P, _L, _I, _L, _P, _P, _P, _P]),
     "fem_graph_count": (_I, [_P, _I, _P, _P, _L, _P, _P, _P]),
     "fem_graph_fill": (_I, [_P, _I, _P, _P, _L, _P, _P, _P, _P]),
+    "fem_graph_tmp_len": (_L, [_L]),
+    "fem_graph_count2": (_I, [_P, _I, _P, _P, _L, _P, _P, _P, _P]),
+    "fem_graph_fill2": (_I, [_P, _I, _P, _P, _L, _P, _P, _P, _P, _P]),
     "fem_scan_i32": (_I, [_P, _L, _P, _P, _P]),
     "fem_scan_i64": (_I, [_P, _L, _P, _P, _P]),
     "fem_sell_widths": (_I, [_P, _L, _P, _P]),

@@ -6,6 +6,8 @@
 // block (a,b) of K_e is V (lambda g_a g_b^T + mu g_b g_a^T + mu (g_a.g_b) I). Isoparametric solids use
 // the same block formula per quadrature point with signed detJ (Q2), which is exactly B^T D B for the
 // isotropic D; only the rounding order differs from the reference's dense einsums.
+#include <algorithm>
+
 #include "common.hpp"
 #include "element.hpp"
 
@@ -359,6 +361,105 @@ __global__ void __launch_bounds__(256) k_assemble_tet4(const double* __restrict_
     }
 }
 
+// Wave per row, lanes = the row's incident elements (chunks of 64): every lane forms its element's gradients and
+// volume once and locates the element's 4 nodes in the row's column list (held in LDS); then each lane owns one
+// (column, block-row) output and sums the contributions of all incident elements in ascending incidence order,
+// starting from the stored value — the same additions in the same order as the thread-per-row kernel above, so
+// the result is bit-identical, with the row's loads issued by up to 64 lanes at once instead of one thread.
+constexpr int AW_WAVES = 4;
+
+template <int BS>
+__global__ void __launch_bounds__(256) k_assemble_tet4w(const double* __restrict__ X, const int64_t* __restrict__ conn,
+                                                        double E, double nu, const int32_t* __restrict__ inc_ptr,
+                                                        const int32_t* __restrict__ inc, int64_t N,
+                                                        const int32_t* __restrict__ rowptr,
+                                                        const int32_t* __restrict__ colidx,
+                                                        const int64_t* __restrict__ csr2sell, double* __restrict__ vals,
+                                                        int64_t* __restrict__ bad) {
+    __shared__ double g_s[AW_WAVES][64][4][3];
+    __shared__ double v_s[AW_WAVES][64];
+    __shared__ int8_t a_s[AW_WAVES][64];
+    __shared__ int8_t pos_s[AW_WAVES][64][4];   // column slot of node b in the current column group, -1 if outside
+    __shared__ int col_s[AW_WAVES][64];
+    constexpr int JG = 64 / BS;                 // columns per pass (one lane per column and block row)
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const Lame L = lame(E, nu);
+    const int64_t nwaves = (int64_t)gridDim.x * AW_WAVES;
+    for (int64_t i = (int64_t)blockIdx.x * AW_WAVES + wid; i < N; i += nwaves) {
+        const int lo = rowptr[i], len = rowptr[i + 1] - lo;
+        const int t0 = inc_ptr[i], C = inc_ptr[i + 1] - t0;
+        for (int j0 = 0; j0 < len; j0 += JG) {
+            const int nj = min(JG, len - j0);
+            if (lane < nj) col_s[wid][lane] = colidx[lo + j0 + lane];
+            // output owned by this lane: column j0 + jl, block row r
+            const int jl = lane / BS, r = lane - BS * (lane / BS);
+            const bool owner = lane < nj * BS;
+            double acc[BS];
+            int64_t Ei = 0;
+            if (owner) {
+                Ei = csr2sell[lo + j0 + jl];
+#pragma unroll
+                for (int c = 0; c < BS; ++c) acc[c] = vals[BS == 1 ? Ei : sell_val(Ei, BS * BS, r * BS + c)];
+            }
+            for (int k0 = 0; k0 < C; k0 += 64) {
+                const int nk = min(64, C - k0);
+                __builtin_amdgcn_wave_barrier();
+                if (lane < nk) {
+                    const int ea = inc[t0 + k0 + lane];
+                    const int64_t e = ea >> 2;
+                    const int64_t* c = conn + 4 * e;
+                    double g[4][3];
+                    const double det = tet4_grads(X, c, g);
+                    if (j0 == 0 && fabs(det) < 1e-12) atomicMin((unsigned long long*)bad, (unsigned long long)e);
+                    v_s[wid][lane] = fabs(det) / 6.0;
+                    a_s[wid][lane] = (int8_t)(ea & 3);
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+#pragma unroll
+                        for (int q = 0; q < 3; ++q) g_s[wid][lane][b][q] = g[b][q];
+                        const int j = (int)c[b];
+                        int p = -1;
+                        for (int u = 0; u < nj; ++u)
+                            if (col_s[wid][u] == j) p = u;
+                        pos_s[wid][lane][b] = (int8_t)p;
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                if (owner) {
+                    for (int k = 0; k < nk; ++k) {
+                        const int a = a_s[wid][k];
+                        const double V = v_s[wid][k];
+                        const double* ga = g_s[wid][k][a];
+#pragma unroll
+                        for (int b = 0; b < 4; ++b) {
+                            if (pos_s[wid][k][b] != jl) continue;
+                            const double* gb = g_s[wid][k][b];
+                            const double dot = ga[0] * gb[0] + ga[1] * gb[1] + ga[2] * gb[2];
+                            if (BS == 1) {
+                                acc[0] += E * dot * V;
+                            } else {
+#pragma unroll
+                                for (int kk = 0; kk < BS; ++kk) {
+                                    double s = L.lam * ga[r] * gb[kk] + L.mu * ga[kk] * gb[r];
+                                    if (r == kk) s += L.mu * dot;
+                                    acc[kk] += s * V;
+                                }
+                            }
+                        }
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+            if (owner) {
+#pragma unroll
+                for (int c = 0; c < BS; ++c) vals[BS == 1 ? Ei : sell_val(Ei, BS * BS, r * BS + c)] = acc[c];
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
 template <int BS>
 __global__ void k_sell_to_csr(const double* __restrict__ vals, const int32_t* __restrict__ rowptr, int64_t nrows,
                               const int64_t* __restrict__ csr2sell, double* __restrict__ out) {
@@ -557,11 +658,12 @@ int fem_assemble_tet4(const double* coords, const int64_t* conn, double E, doubl
                       const int64_t* csr2sell, const int64_t* slice_ptr, double* vals, int64_t* bad_idx,
                       fem_stream_t stream) {
     (void)slice_ptr;
-    dim3 g(stream_grid(N, 256));
+    // wave per row (k_assemble_tet4w); the thread-per-row k_assemble_tet4 is kept as the reference formulation
+    const dim3 g((unsigned)std::min<int64_t>(cdiv(N, AW_WAVES), 8192));
     if (bs == 1)
-        hipLaunchKernelGGL(k_assemble_tet4<1>, g, dim3(256), 0, S(stream), coords, conn, E, nu, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals, bad_idx);
+        hipLaunchKernelGGL(k_assemble_tet4w<1>, g, dim3(256), 0, S(stream), coords, conn, E, nu, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals, bad_idx);
     else if (bs == 3)
-        hipLaunchKernelGGL(k_assemble_tet4<3>, g, dim3(256), 0, S(stream), coords, conn, E, nu, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals, bad_idx);
+        hipLaunchKernelGGL(k_assemble_tet4w<3>, g, dim3(256), 0, S(stream), coords, conn, E, nu, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals, bad_idx);
     else {
         set_error("fem_assemble_tet4: block size %d unsupported", bs);
         return FEM_EARG;

@@ -4,6 +4,10 @@
 // its only global matrix is the COO of `subdivision.ipynb:118-139`, coalesced by torch. The pattern built here
 // is exactly coalesce(COO) at node granularity (bit-exact against oracle.ref_cpu.node_pattern): every row
 // lists the unique nodes sharing an element with it, ascending.
+#include <algorithm>
+
+#include <hipcub/hipcub.hpp>
+
 #include "common.hpp"
 
 namespace fem {
@@ -39,17 +43,117 @@ __global__ void k_inc_sort(const int32_t* __restrict__ ptr, int64_t N, int32_t* 
     }
 }
 
+// sort keys of the incidence: node id of every (element, local) slot, payload = slot
+__global__ void k_inc_keys(const int64_t* __restrict__ conn, int64_t total, int32_t* __restrict__ key,
+                           int32_t* __restrict__ slot) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        key[i] = (int32_t)conn[i];
+        slot[i] = (int32_t)i;
+    }
+}
+
+// inc_ptr[n] = first sorted position whose node is >= n (run boundaries of the sorted keys)
+__global__ void k_inc_ptr(const int32_t* __restrict__ key, int64_t total, int64_t N, int32_t* __restrict__ inc_ptr) {
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p <= total; p += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t prev = p == 0 ? -1 : key[p - 1];
+        const int64_t cur = p == total ? N : key[p];
+        for (int64_t n = prev + 1; n <= cur; ++n) inc_ptr[n] = (int32_t)p;
+    }
+}
+
 // ---------------------------------------------------------------- node graph (wave per node)
 constexpr int G_WAVES = 4;      // waves per block
 constexpr int G_CAP = 1536;     // candidate capacity per node (deg * npe)
 constexpr int G_UCAP = 512;     // unique-neighbour capacity per node
+constexpr int G_SCAP = 384;     // candidate capacity of the small-row kernel
+constexpr int G_TCAP = 32;      // rows of at most this many neighbours are produced by k_graph_small
+
+// Small rows in one pass (every P1 / Q1 / wedge row of ordinary meshes): wave per node, wave-private LDS (1.7 KB,
+// so occupancy is not LDS-bound), candidates gathered, first occurrences kept, rank-sorted and written to
+// tmp[node * G_TCAP + rank] with row_len[node]. Rows with more candidates or neighbours get tmp[node * G_TCAP] = -1
+// and are left to k_graph (count and fill passes, skipping the rows done here).
+__global__ void __launch_bounds__(256) k_graph_small(const int64_t* __restrict__ conn, int npe,
+                                                     const int32_t* __restrict__ inc_ptr,
+                                                     const int32_t* __restrict__ inc, int64_t N,
+                                                     int32_t* __restrict__ row_len, int32_t* __restrict__ tmp) {
+    __shared__ int cand[G_WAVES][G_SCAP];
+    __shared__ int uniq[G_WAVES][64];
+    const int wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int64_t node = (int64_t)blockIdx.x * G_WAVES + wid; node < N; node += (int64_t)gridDim.x * G_WAVES) {
+        const int start = inc_ptr[node];
+        const int C = (inc_ptr[node + 1] - start) * npe;
+        int32_t* trow = tmp + node * G_TCAP;
+        if (C > G_SCAP) {
+            if (lane == 0) trow[0] = -1;
+            continue;
+        }
+        for (int t = lane; t < C; t += 64) {
+            const int k = t / npe, b = t - k * npe;
+            const int e = inc[start + k] / npe;
+            cand[wid][t] = (int)conn[(int64_t)e * npe + b];
+        }
+        __builtin_amdgcn_wave_barrier();
+        int U = 0;
+        for (int cb = 0; cb < C; cb += 64) {
+            const int t = cb + lane;
+            bool first = false;
+            int v = 0;
+            if (t < C) {
+                v = cand[wid][t];
+                first = true;
+                for (int u = 0; u < t; ++u)
+                    if (cand[wid][u] == v) {
+                        first = false;
+                        break;
+                    }
+            }
+            const unsigned long long m = __ballot(first);
+            if (first) {
+                const int pos = U + __popcll(m & lt_mask);
+                if (pos < 64) uniq[wid][pos] = v;
+            }
+            U += __popcll(m);
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (U > G_TCAP) {
+            if (lane == 0) trow[0] = -1;
+            continue;
+        }
+        if (lane < U) {
+            const int v = uniq[wid][lane];
+            int rank = 0;
+            for (int u = 0; u < U; ++u) rank += (uniq[wid][u] < v);
+            trow[rank] = v;
+        }
+        if (lane == 0) row_len[node] = U;
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// rows of k_graph_small -> CSR colidx / diagpos
+__global__ void k_graph_copy(const int32_t* __restrict__ tmp, const int32_t* __restrict__ rowptr, int64_t N,
+                             int32_t* __restrict__ colidx, int32_t* __restrict__ diagpos) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < N * G_TCAP; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t node = t / G_TCAP;
+        const int j = (int)(t - node * G_TCAP);
+        if (tmp[node * G_TCAP] < 0) continue;
+        const int rp = rowptr[node], len = rowptr[node + 1] - rp;
+        if (j >= len) continue;
+        const int v = tmp[t];
+        colidx[rp + j] = v;
+        if (v == (int)node) diagpos[node] = rp + j;
+    }
+}
 
 template <bool FILL>
 __global__ void __launch_bounds__(256) k_graph(const int64_t* __restrict__ conn, int npe,
                                                const int32_t* __restrict__ inc_ptr, const int32_t* __restrict__ inc,
                                                int64_t N, int32_t* __restrict__ row_len,
                                                const int32_t* __restrict__ rowptr, int32_t* __restrict__ colidx,
-                                               int32_t* __restrict__ diagpos, int32_t* __restrict__ overflow) {
+                                               int32_t* __restrict__ diagpos, int32_t* __restrict__ overflow,
+                                               const int32_t* __restrict__ done) {
     __shared__ int cand[G_WAVES][G_CAP];
     __shared__ int uniq[G_WAVES][G_UCAP];
     const int wid = threadIdx.x >> 6;
@@ -58,7 +162,8 @@ __global__ void __launch_bounds__(256) k_graph(const int64_t* __restrict__ conn,
 
     for (int64_t base = (int64_t)blockIdx.x * G_WAVES; base < N; base += (int64_t)gridDim.x * G_WAVES) {
         const int64_t node = base + wid;
-        const bool active = node < N;
+        // rows already produced by k_graph_small (done[node * G_TCAP] >= 0) are skipped
+        const bool active = node < N && !(done && done[node * G_TCAP] >= 0);
         int C = 0, start = 0;
         if (active) {
             start = inc_ptr[node];
@@ -181,24 +286,38 @@ extern "C" {
 
 int fem_incidence(const int64_t* conn, int64_t M, int npe, int64_t N, int32_t* inc_ptr, int32_t* inc,
                   int32_t* work, fem_stream_t stream) {
+    (void)work;
     hipStream_t st = S(stream);
     const int64_t total = M * npe;
-    if (total >= (int64_t)1 << 31) {
-        set_error("fem_incidence: M*npe = %lld exceeds int32 range", (long long)total);
+    if (total >= (int64_t)1 << 31 || N >= (int64_t)1 << 31) {
+        set_error("fem_incidence: M*npe = %lld / N = %lld exceed int32 range", (long long)total, (long long)N);
         return FEM_EARG;
     }
-    int32_t* cnt = work;
-    int32_t* scan_work = work + N;
-    FEM_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t) * N, st));
-    hipLaunchKernelGGL(k_inc_count, dim3(stream_grid(total, 256)), dim3(256), 0, st, conn, total, cnt);
+    if (N <= 0) return FEM_OK;
+    if (total == 0) {
+        FEM_HIP(hipMemsetAsync(inc_ptr, 0, sizeof(int32_t) * (N + 1), st));
+        return FEM_OK;
+    }
+    // stable radix sort of (node, slot) pairs: the slots of a node come out ascending (deterministic incidence)
+    int bits = 1;
+    while (((int64_t)1 << bits) < N) ++bits;
+    int32_t *kin = nullptr, *kout = nullptr, *vin = nullptr;
+    FEM_HIP(hipMallocAsync((void**)&kin, sizeof(int32_t) * total, st));
+    FEM_HIP(hipMallocAsync((void**)&kout, sizeof(int32_t) * total, st));
+    FEM_HIP(hipMallocAsync((void**)&vin, sizeof(int32_t) * total, st));
+    hipLaunchKernelGGL(k_inc_keys, dim3(stream_grid(total, 256)), dim3(256), 0, st, conn, total, kin, vin);
     FEM_LAUNCHED();
-    int rc = fem_scan_i32(cnt, N, inc_ptr, scan_work, stream);
-    if (rc) return rc;
-    FEM_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t) * N, st));
-    hipLaunchKernelGGL(k_inc_fill, dim3(stream_grid(total, 256)), dim3(256), 0, st, conn, total, inc_ptr, cnt, inc);
+    size_t tb = 0;
+    FEM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kout, vin, inc, (int)total, 0, bits, st));
+    void* tmp = nullptr;
+    FEM_HIP(hipMallocAsync(&tmp, tb, st));
+    FEM_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb, kin, kout, vin, inc, (int)total, 0, bits, st));
+    hipLaunchKernelGGL(k_inc_ptr, dim3(stream_grid(total + 1, 256)), dim3(256), 0, st, kout, total, N, inc_ptr);
     FEM_LAUNCHED();
-    hipLaunchKernelGGL(k_inc_sort, dim3(stream_grid(N, 256)), dim3(256), 0, st, inc_ptr, N, inc);
-    FEM_LAUNCHED();
+    FEM_HIP(hipFreeAsync(tmp, st));
+    FEM_HIP(hipFreeAsync(kin, st));
+    FEM_HIP(hipFreeAsync(kout, st));
+    FEM_HIP(hipFreeAsync(vin, st));
     return FEM_OK;
 }
 
@@ -211,7 +330,37 @@ static int graph_grid(int64_t N) {
 int fem_graph_count(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
                     int32_t* row_len, int32_t* overflow, fem_stream_t stream) {
     hipLaunchKernelGGL(k_graph<false>, dim3(graph_grid(N)), dim3(256), 0, S(stream), conn, npe, inc_ptr, inc, N,
-                       row_len, (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, overflow);
+                       row_len, (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, overflow,
+                       (const int32_t*)nullptr);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int64_t fem_graph_tmp_len(int64_t N) { return N * G_TCAP; }
+
+int fem_graph_count2(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
+                     int32_t* row_len, int32_t* tmp, int32_t* overflow, fem_stream_t stream) {
+    if (N <= 0) return FEM_OK;
+    const int64_t grid = std::min<int64_t>(cdiv(N, G_WAVES), 16384);
+    hipLaunchKernelGGL(k_graph_small, dim3((unsigned)grid), dim3(256), 0, S(stream), conn, npe, inc_ptr, inc, N,
+                       row_len, tmp);
+    FEM_LAUNCHED();
+    hipLaunchKernelGGL(k_graph<false>, dim3(graph_grid(N)), dim3(256), 0, S(stream), conn, npe, inc_ptr, inc, N,
+                       row_len, (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, overflow,
+                       (const int32_t*)tmp);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_graph_fill2(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
+                    const int32_t* rowptr, const int32_t* tmp, int32_t* colidx, int32_t* diagpos,
+                    fem_stream_t stream) {
+    if (N <= 0) return FEM_OK;
+    hipLaunchKernelGGL(k_graph_copy, dim3(stream_grid(N * G_TCAP, 256)), dim3(256), 0, S(stream), tmp, rowptr, N,
+                       colidx, diagpos);
+    FEM_LAUNCHED();
+    hipLaunchKernelGGL(k_graph<true>, dim3(graph_grid(N)), dim3(256), 0, S(stream), conn, npe, inc_ptr, inc, N,
+                       (int32_t*)nullptr, rowptr, colidx, diagpos, (int32_t*)nullptr, tmp);
     FEM_LAUNCHED();
     return FEM_OK;
 }
@@ -219,7 +368,7 @@ int fem_graph_count(const int64_t* conn, int npe, const int32_t* inc_ptr, const 
 int fem_graph_fill(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
                    const int32_t* rowptr, int32_t* colidx, int32_t* diagpos, fem_stream_t stream) {
     hipLaunchKernelGGL(k_graph<true>, dim3(graph_grid(N)), dim3(256), 0, S(stream), conn, npe, inc_ptr, inc, N,
-                       (int32_t*)nullptr, rowptr, colidx, diagpos, (int32_t*)nullptr);
+                       (int32_t*)nullptr, rowptr, colidx, diagpos, (int32_t*)nullptr, (const int32_t*)nullptr);
     FEM_LAUNCHED();
     return FEM_OK;
 }

@@ -74,21 +74,21 @@ def check_connectivity(elements: torch.Tensor, n_nodes: int):
     reference's torch indexing raises IndexError on such input). One device reduction + sync."""
     if elements.numel() == 0:
         return
-    lo, hi = int(elements.min()), int(elements.max())
+    lo, hi = (int(v) for v in torch.aminmax(elements))
     if lo < 0 or hi >= n_nodes:
         raise IndexError(f"element connectivity references node {lo if lo < 0 else hi}, outside [0, {n_nodes})")
 
 
-def incidence(elements: torch.Tensor, n_nodes: int):
+def incidence(elements: torch.Tensor, n_nodes: int, checked: bool = False):
     """Deterministic node -> (element, local) incidence of a connectivity block [M, npe] (int64, device)."""
     lib = C.lib()
-    check_connectivity(elements, n_nodes)
+    if not checked:
+        check_connectivity(elements, n_nodes)
     dev = elements.device
     M, npe = elements.shape
     inc_ptr = torch.empty(n_nodes + 1, dtype=I32, device=dev)
     inc = torch.empty(M * npe, dtype=I32, device=dev)
-    work = torch.empty(n_nodes + int(lib.fem_scan_work_len(n_nodes)), dtype=I32, device=dev)
-    C.check(lib.fem_incidence(C.ptr(elements), M, npe, n_nodes, C.ptr(inc_ptr), C.ptr(inc), C.ptr(work),
+    C.check(lib.fem_incidence(C.ptr(elements), M, npe, n_nodes, C.ptr(inc_ptr), C.ptr(inc), None,
                               C.stream(dev)), "fem_incidence")
     return inc_ptr, inc
 
@@ -103,22 +103,23 @@ def build_graph(elements: torch.Tensor, n_nodes: int, compress: bool = True) -> 
     check_connectivity(elements, n_nodes)
     M, npe = elements.shape
     st = C.stream(dev)
-    inc_ptr, inc = incidence(elements, n_nodes)
+    inc_ptr, inc = incidence(elements, n_nodes, checked=True)
     row_len = torch.empty(n_nodes, dtype=I32, device=dev)
     overflow = torch.zeros(1, dtype=I32, device=dev)
-    C.check(lib.fem_graph_count(C.ptr(elements), npe, C.ptr(inc_ptr), C.ptr(inc), n_nodes, C.ptr(row_len),
-                                C.ptr(overflow), st), "fem_graph_count")
+    tmp = torch.empty(max(int(lib.fem_graph_tmp_len(n_nodes)), 1), dtype=I32, device=dev)
+    C.check(lib.fem_graph_count2(C.ptr(elements), npe, C.ptr(inc_ptr), C.ptr(inc), n_nodes, C.ptr(row_len),
+                                 C.ptr(tmp), C.ptr(overflow), st), "fem_graph_count2")
     rowptr = torch.empty(n_nodes + 1, dtype=I32, device=dev)
     work = torch.empty(int(lib.fem_scan_work_len(n_nodes)) + 1, dtype=I32, device=dev)
     C.check(lib.fem_scan_i32(C.ptr(row_len), n_nodes, C.ptr(rowptr), C.ptr(work), st), "fem_scan_i32")
-    ov = int(overflow.item())
+    ov, nnz = torch.stack([overflow[0], rowptr[-1]]).tolist()      # one sync
     if ov:
         raise C.FemError(f"fem355: a node has {ov} element-neighbour candidates, above the pattern capacity")
-    nnz = int(rowptr[-1].item())
     colidx = torch.empty(nnz, dtype=I32, device=dev)
     diagpos = torch.empty(n_nodes, dtype=I32, device=dev)
-    C.check(lib.fem_graph_fill(C.ptr(elements), npe, C.ptr(inc_ptr), C.ptr(inc), n_nodes, C.ptr(rowptr),
-                               C.ptr(colidx), C.ptr(diagpos), st), "fem_graph_fill")
+    C.check(lib.fem_graph_fill2(C.ptr(elements), npe, C.ptr(inc_ptr), C.ptr(inc), n_nodes, C.ptr(rowptr), C.ptr(tmp),
+                                C.ptr(colidx), C.ptr(diagpos), st), "fem_graph_fill2")
+    del tmp
     ns = (n_nodes + 63) // 64
     width = torch.empty(ns, dtype=I64, device=dev)
     C.check(lib.fem_sell_widths(C.ptr(rowptr), n_nodes, C.ptr(width), st), "fem_sell_widths")

@@ -98,7 +98,8 @@ int fem_iso_geom(const double* coords, const int64_t* conn, int64_t M, int npe, 
                  double* grads, double* B, fem_stream_t stream);
 
 /* ------------------------------------------------------------------ mesh graph (pattern build)
- * Node -> (element, local) incidence, deterministic (entries sorted ascending by e*npe+local).
+ * Node -> (element, local) incidence, deterministic (entries sorted ascending by e*npe+local; a stable radix sort
+ * of (node, slot) pairs; `work` is unused and kept for ABI compatibility).
  * inc_ptr [N+1], inc [M*npe]; work: int32 [N + fem_scan_work_len(N)]. */
 int64_t fem_scan_work_len(int64_t n);
 int fem_incidence(const int64_t* conn, int64_t M, int npe, int64_t N, int32_t* inc_ptr, int32_t* inc,
@@ -113,6 +114,15 @@ int fem_graph_count(const int64_t* conn, int npe, const int32_t* inc_ptr, const 
                     int32_t* row_len, int32_t* overflow, fem_stream_t stream);
 int fem_graph_fill(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
                    const int32_t* rowptr, int32_t* colidx, int32_t* diagpos, fem_stream_t stream);
+/* Same pattern in (typically) one pass: rows of at most 32 neighbours from at most 384 candidates are gathered,
+ * deduplicated and sorted once by a wave-private kernel into tmp [fem_graph_tmp_len(N)] (int32); the rest fall
+ * back to the two-pass kernels above. fem_graph_count2 writes row_len; fem_graph_fill2 copies / fills the rows. */
+int64_t fem_graph_tmp_len(int64_t N);
+int fem_graph_count2(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
+                     int32_t* row_len, int32_t* tmp, int32_t* overflow, fem_stream_t stream);
+int fem_graph_fill2(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
+                    const int32_t* rowptr, const int32_t* tmp, int32_t* colidx, int32_t* diagpos,
+                    fem_stream_t stream);
 /* exclusive scan of int32 counts -> out[n+1] (out[n] = total); work: int32 [fem_scan_work_len(n)] */
 int fem_scan_i32(const int32_t* in, int64_t n, int32_t* out, int32_t* work, fem_stream_t stream);
 
