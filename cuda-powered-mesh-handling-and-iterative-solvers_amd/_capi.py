@@ -37,6 +37,7 @@ SIGNATURES = {
     "fem_iso_geom": (_I, [_P, _P, _L, _I, _P, _P, _P, _P, _P]),
     "fem_pcg_scalars": (_I, [_P, ctypes.POINTER(_D)]),
     "fem_scan_work_len": (_L, [_L]),
+    "fem_incidence_work_bytes": (_L, [_L, _L]),
     "fem_incidence": (_I, [_P, _L, _I, _L, _P, _P, _P, _P]),
     "fem_graph_count": (_I, [_P, _I, _P, _P, _L, _P, _P, _P]),
     "fem_graph_fill": (_I, [_P, _I, _P, _P, _L, _P, _P, _P, _P]),

@@ -460,6 +460,175 @@ __global__ void __launch_bounds__(256) k_assemble_tet4w(const double* __restrict
     }
 }
 
+// bs = 1 (P1 Poisson): each element lane forms its 4 scalar contributions E (g_a . g_b) V itself and finds the 4
+// column slots by binary search in the row's LDS column list; an owner lane per column then adds the (at most one)
+// contribution of every element in ascending incidence order — 2 LDS reads per element instead of ~20.
+__global__ void __launch_bounds__(256) k_assemble_p1w(const double* __restrict__ X, const int64_t* __restrict__ conn,
+                                                      double kappa, const int32_t* __restrict__ inc_ptr,
+                                                      const int32_t* __restrict__ inc, int64_t N,
+                                                      const int32_t* __restrict__ rowptr,
+                                                      const int32_t* __restrict__ colidx,
+                                                      const int64_t* __restrict__ csr2sell, double* __restrict__ vals,
+                                                      int64_t* __restrict__ bad) {
+    __shared__ double c_s[AW_WAVES][64][4];
+    __shared__ uint32_t pos_s[AW_WAVES][64];    // 4 column slots (bytes), 0xff = outside this column group
+    __shared__ int col_s[AW_WAVES][64];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t nwaves = (int64_t)gridDim.x * AW_WAVES;
+    for (int64_t i = (int64_t)blockIdx.x * AW_WAVES + wid; i < N; i += nwaves) {
+        const int lo = rowptr[i], len = rowptr[i + 1] - lo;
+        const int t0 = inc_ptr[i], C = inc_ptr[i + 1] - t0;
+        for (int j0 = 0; j0 < len; j0 += 64) {
+            const int nj = min(64, len - j0);
+            if (lane < nj) col_s[wid][lane] = colidx[lo + j0 + lane];
+            const bool owner = lane < nj;
+            int64_t Ei = 0;
+            double acc = 0.0;
+            if (owner) {
+                Ei = csr2sell[lo + j0 + lane];
+                acc = vals[Ei];
+            }
+            for (int k0 = 0; k0 < C; k0 += 64) {
+                const int nk = min(64, C - k0);
+                __builtin_amdgcn_wave_barrier();
+                if (lane < nk) {
+                    const int ea = inc[t0 + k0 + lane];
+                    const int64_t e = ea >> 2;
+                    const int a = ea & 3;
+                    const int64_t* c = conn + 4 * e;
+                    double g[4][3];
+                    const double det = tet4_grads(X, c, g);
+                    if (j0 == 0 && fabs(det) < 1e-12) atomicMin((unsigned long long*)bad, (unsigned long long)e);
+                    const double V = fabs(det) / 6.0;
+                    uint32_t packed = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        const double dot = g[a][0] * g[b][0] + g[a][1] * g[b][1] + g[a][2] * g[b][2];
+                        c_s[wid][lane][b] = kappa * dot * V;
+                        const int j = (int)c[b];
+                        int l = 0, h = nj;   // binary search of j among the group's sorted columns
+                        while (l < h) {
+                            const int m = (l + h) >> 1;
+                            if (col_s[wid][m] < j) l = m + 1;
+                            else h = m;
+                        }
+                        const uint32_t p = (l < nj && col_s[wid][l] == j) ? (uint32_t)l : 0xffu;
+                        packed |= p << (8 * b);
+                    }
+                    pos_s[wid][lane] = packed;
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (owner) {
+                    for (int k = 0; k < nk; ++k) {
+                        const uint32_t pk = pos_s[wid][k];
+#pragma unroll
+                        for (int b = 0; b < 4; ++b)
+                            if (((pk >> (8 * b)) & 0xffu) == (uint32_t)lane) acc += c_s[wid][k][b];
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+            if (owner) vals[Ei] = acc;
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+// bs = 3 (c3d4 elasticity), same scheme with 3x3 blocks: element lanes (chunks of 32 elements) form the 4 blocks of
+// their element row V (lambda g_a g_b^T + mu g_b g_a^T + mu (g_a . g_b) I) in LDS; owner lanes (column, block row)
+// add their block row of every element in ascending incidence order.
+constexpr int AE_K = 32;
+
+__global__ void __launch_bounds__(256) k_assemble_el3w(const double* __restrict__ X, const int64_t* __restrict__ conn,
+                                                       double E, double nu, const int32_t* __restrict__ inc_ptr,
+                                                       const int32_t* __restrict__ inc, int64_t N,
+                                                       const int32_t* __restrict__ rowptr,
+                                                       const int32_t* __restrict__ colidx,
+                                                       const int64_t* __restrict__ csr2sell, double* __restrict__ vals,
+                                                       int64_t* __restrict__ bad) {
+    __shared__ double blk_s[AW_WAVES][AE_K][4][9];
+    __shared__ uint32_t pos_s[AW_WAVES][AE_K];
+    __shared__ int col_s[AW_WAVES][21];
+    constexpr int JG = 21;
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const Lame L = lame(E, nu);
+    const int64_t nwaves = (int64_t)gridDim.x * AW_WAVES;
+    for (int64_t i = (int64_t)blockIdx.x * AW_WAVES + wid; i < N; i += nwaves) {
+        const int lo = rowptr[i], len = rowptr[i + 1] - lo;
+        const int t0 = inc_ptr[i], C = inc_ptr[i + 1] - t0;
+        for (int j0 = 0; j0 < len; j0 += JG) {
+            const int nj = min(JG, len - j0);
+            if (lane < nj) col_s[wid][lane] = colidx[lo + j0 + lane];
+            const int jl = lane / 3, r = lane - 3 * (lane / 3);
+            const bool owner = lane < nj * 3;
+            int64_t Ei = 0;
+            double acc[3] = {0.0, 0.0, 0.0};
+            if (owner) {
+                Ei = csr2sell[lo + j0 + jl];
+#pragma unroll
+                for (int c = 0; c < 3; ++c) acc[c] = vals[sell_val(Ei, 9, r * 3 + c)];
+            }
+            for (int k0 = 0; k0 < C; k0 += AE_K) {
+                const int nk = min(AE_K, C - k0);
+                __builtin_amdgcn_wave_barrier();
+                if (lane < nk) {
+                    const int ea = inc[t0 + k0 + lane];
+                    const int64_t e = ea >> 2;
+                    const int a = ea & 3;
+                    const int64_t* c = conn + 4 * e;
+                    double g[4][3];
+                    const double det = tet4_grads(X, c, g);
+                    if (j0 == 0 && fabs(det) < 1e-12) atomicMin((unsigned long long*)bad, (unsigned long long)e);
+                    const double V = fabs(det) / 6.0;
+                    uint32_t packed = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        const double dot = g[a][0] * g[b][0] + g[a][1] * g[b][1] + g[a][2] * g[b][2];
+#pragma unroll
+                        for (int rr = 0; rr < 3; ++rr)
+#pragma unroll
+                            for (int kk = 0; kk < 3; ++kk) {
+                                double s = L.lam * g[a][rr] * g[b][kk] + L.mu * g[a][kk] * g[b][rr];
+                                if (rr == kk) s += L.mu * dot;
+                                blk_s[wid][lane][b][rr * 3 + kk] = s * V;
+                            }
+                        const int j = (int)c[b];
+                        int l = 0, h = nj;
+                        while (l < h) {
+                            const int m = (l + h) >> 1;
+                            if (col_s[wid][m] < j) l = m + 1;
+                            else h = m;
+                        }
+                        const uint32_t p = (l < nj && col_s[wid][l] == j) ? (uint32_t)l : 0xffu;
+                        packed |= p << (8 * b);
+                    }
+                    pos_s[wid][lane] = packed;
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (owner) {
+                    for (int k = 0; k < nk; ++k) {
+                        const uint32_t pk = pos_s[wid][k];
+#pragma unroll
+                        for (int b = 0; b < 4; ++b)
+                            if (((pk >> (8 * b)) & 0xffu) == (uint32_t)jl) {
+                                const double* br = &blk_s[wid][k][b][r * 3];
+                                acc[0] += br[0];
+                                acc[1] += br[1];
+                                acc[2] += br[2];
+                            }
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+            if (owner) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) vals[sell_val(Ei, 9, r * 3 + c)] = acc[c];
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
 template <int BS>
 __global__ void k_sell_to_csr(const double* __restrict__ vals, const int32_t* __restrict__ rowptr, int64_t nrows,
                               const int64_t* __restrict__ csr2sell, double* __restrict__ out) {
@@ -658,12 +827,13 @@ int fem_assemble_tet4(const double* coords, const int64_t* conn, double E, doubl
                       const int64_t* csr2sell, const int64_t* slice_ptr, double* vals, int64_t* bad_idx,
                       fem_stream_t stream) {
     (void)slice_ptr;
-    // wave per row (k_assemble_tet4w); the thread-per-row k_assemble_tet4 is kept as the reference formulation
+    // wave per row (k_assemble_p1w / k_assemble_el3w); the thread-per-row k_assemble_tet4 and the first wave
+    // version k_assemble_tet4w stay as reference formulations
     const dim3 g((unsigned)std::min<int64_t>(cdiv(N, AW_WAVES), 8192));
     if (bs == 1)
-        hipLaunchKernelGGL(k_assemble_tet4w<1>, g, dim3(256), 0, S(stream), coords, conn, E, nu, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals, bad_idx);
+        hipLaunchKernelGGL(k_assemble_p1w, g, dim3(256), 0, S(stream), coords, conn, E, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals, bad_idx);
     else if (bs == 3)
-        hipLaunchKernelGGL(k_assemble_tet4w<3>, g, dim3(256), 0, S(stream), coords, conn, E, nu, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals, bad_idx);
+        hipLaunchKernelGGL(k_assemble_el3w, g, dim3(256), 0, S(stream), coords, conn, E, nu, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals, bad_idx);
     else {
         set_error("fem_assemble_tet4: block size %d unsupported", bs);
         return FEM_EARG;

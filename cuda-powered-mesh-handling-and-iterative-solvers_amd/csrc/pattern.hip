@@ -68,15 +68,17 @@ constexpr int G_UCAP = 512;     // unique-neighbour capacity per node
 constexpr int G_SCAP = 384;     // candidate capacity of the small-row kernel
 constexpr int G_TCAP = 32;      // rows of at most this many neighbours are produced by k_graph_small
 
-// Small rows in one pass (every P1 / Q1 / wedge row of ordinary meshes): wave per node, wave-private LDS (1.7 KB,
-// so occupancy is not LDS-bound), candidates gathered, first occurrences kept, rank-sorted and written to
-// tmp[node * G_TCAP + rank] with row_len[node]. Rows with more candidates or neighbours get tmp[node * G_TCAP] = -1
-// and are left to k_graph (count and fill passes, skipping the rows done here).
+// Small rows in one pass (every P1 / Q1 / wedge row of ordinary meshes): wave per node, candidates deduplicated
+// through a wave-private LDS hash table (512 slots, linear probing, compare-and-swap), the unique set compacted
+// and rank-sorted, written to tmp[node * G_TCAP + rank] with row_len[node]. Rows with more than G_SCAP candidates or
+// G_TCAP neighbours get tmp[node * G_TCAP] = -1 and are left to k_graph (count and fill passes skip the rest).
+constexpr int G_HT = 512;
+
 __global__ void __launch_bounds__(256) k_graph_small(const int64_t* __restrict__ conn, int npe,
                                                      const int32_t* __restrict__ inc_ptr,
                                                      const int32_t* __restrict__ inc, int64_t N,
                                                      int32_t* __restrict__ row_len, int32_t* __restrict__ tmp) {
-    __shared__ int cand[G_WAVES][G_SCAP];
+    __shared__ int ht[G_WAVES][G_HT];
     __shared__ int uniq[G_WAVES][64];
     const int wid = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
@@ -89,28 +91,26 @@ __global__ void __launch_bounds__(256) k_graph_small(const int64_t* __restrict__
             if (lane == 0) trow[0] = -1;
             continue;
         }
+        for (int q = lane; q < G_HT; q += 64) ht[wid][q] = -1;
+        __builtin_amdgcn_wave_barrier();
         for (int t = lane; t < C; t += 64) {
             const int k = t / npe, b = t - k * npe;
             const int e = inc[start + k] / npe;
-            cand[wid][t] = (int)conn[(int64_t)e * npe + b];
+            const int v = (int)conn[(int64_t)e * npe + b];
+            unsigned h = ((unsigned)v * 2654435761u) >> 23;   // 9 bits
+            while (true) {
+                const int old = atomicCAS(&ht[wid][h], -1, v);
+                if (old == -1 || old == v) break;
+                h = (h + 1) & (G_HT - 1);
+            }
         }
         __builtin_amdgcn_wave_barrier();
         int U = 0;
-        for (int cb = 0; cb < C; cb += 64) {
-            const int t = cb + lane;
-            bool first = false;
-            int v = 0;
-            if (t < C) {
-                v = cand[wid][t];
-                first = true;
-                for (int u = 0; u < t; ++u)
-                    if (cand[wid][u] == v) {
-                        first = false;
-                        break;
-                    }
-            }
-            const unsigned long long m = __ballot(first);
-            if (first) {
+        for (int q0 = 0; q0 < G_HT; q0 += 64) {
+            const int v = ht[wid][q0 + lane];
+            const bool has = v >= 0;
+            const unsigned long long m = __ballot(has);
+            if (has) {
                 const int pos = U + __popcll(m & lt_mask);
                 if (pos < 64) uniq[wid][pos] = v;
             }
@@ -284,9 +284,28 @@ using namespace fem;
 
 extern "C" {
 
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static size_t inc_sort_temp_bytes(int64_t total, int bits) {
+    size_t tb = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const int32_t*)nullptr, (int32_t*)nullptr,
+                                             (const int32_t*)nullptr, (int32_t*)nullptr, (int)total, 0, bits);
+    return tb;
+}
+
+static int node_bits(int64_t N) {
+    int bits = 1;
+    while (((int64_t)1 << bits) < N) ++bits;
+    return bits;
+}
+
+int64_t fem_incidence_work_bytes(int64_t total, int64_t N) {
+    if (total <= 0 || N <= 0) return 0;
+    return (int64_t)(3 * align256(sizeof(int32_t) * total) + align256(inc_sort_temp_bytes(total, node_bits(N))));
+}
+
 int fem_incidence(const int64_t* conn, int64_t M, int npe, int64_t N, int32_t* inc_ptr, int32_t* inc,
                   int32_t* work, fem_stream_t stream) {
-    (void)work;
     hipStream_t st = S(stream);
     const int64_t total = M * npe;
     if (total >= (int64_t)1 << 31 || N >= (int64_t)1 << 31) {
@@ -299,25 +318,23 @@ int fem_incidence(const int64_t* conn, int64_t M, int npe, int64_t N, int32_t* i
         return FEM_OK;
     }
     // stable radix sort of (node, slot) pairs: the slots of a node come out ascending (deterministic incidence)
-    int bits = 1;
-    while (((int64_t)1 << bits) < N) ++bits;
-    int32_t *kin = nullptr, *kout = nullptr, *vin = nullptr;
-    FEM_HIP(hipMallocAsync((void**)&kin, sizeof(int32_t) * total, st));
-    FEM_HIP(hipMallocAsync((void**)&kout, sizeof(int32_t) * total, st));
-    FEM_HIP(hipMallocAsync((void**)&vin, sizeof(int32_t) * total, st));
+    const int bits = node_bits(N);
+    const size_t a4 = align256(sizeof(int32_t) * total);
+    const size_t tb = inc_sort_temp_bytes(total, bits);
+    char* base = reinterpret_cast<char*>(work);
+    const bool own = base == nullptr;   // no caller workspace: stream-ordered allocation
+    if (own) FEM_HIP(hipMallocAsync((void**)&base, 3 * a4 + align256(tb), st));
+    int32_t* kin = reinterpret_cast<int32_t*>(base);
+    int32_t* kout = reinterpret_cast<int32_t*>(base + a4);
+    int32_t* vin = reinterpret_cast<int32_t*>(base + 2 * a4);
+    void* tmp = base + 3 * a4;
     hipLaunchKernelGGL(k_inc_keys, dim3(stream_grid(total, 256)), dim3(256), 0, st, conn, total, kin, vin);
     FEM_LAUNCHED();
-    size_t tb = 0;
-    FEM_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kout, vin, inc, (int)total, 0, bits, st));
-    void* tmp = nullptr;
-    FEM_HIP(hipMallocAsync(&tmp, tb, st));
-    FEM_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb, kin, kout, vin, inc, (int)total, 0, bits, st));
+    size_t tb2 = tb;
+    FEM_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb2, kin, kout, vin, inc, (int)total, 0, bits, st));
     hipLaunchKernelGGL(k_inc_ptr, dim3(stream_grid(total + 1, 256)), dim3(256), 0, st, kout, total, N, inc_ptr);
     FEM_LAUNCHED();
-    FEM_HIP(hipFreeAsync(tmp, st));
-    FEM_HIP(hipFreeAsync(kin, st));
-    FEM_HIP(hipFreeAsync(kout, st));
-    FEM_HIP(hipFreeAsync(vin, st));
+    if (own) FEM_HIP(hipFreeAsync(base, st));
     return FEM_OK;
 }
 

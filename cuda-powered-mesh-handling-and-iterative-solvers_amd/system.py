@@ -88,7 +88,9 @@ def incidence(elements: torch.Tensor, n_nodes: int, checked: bool = False):
     M, npe = elements.shape
     inc_ptr = torch.empty(n_nodes + 1, dtype=I32, device=dev)
     inc = torch.empty(M * npe, dtype=I32, device=dev)
-    C.check(lib.fem_incidence(C.ptr(elements), M, npe, n_nodes, C.ptr(inc_ptr), C.ptr(inc), None,
+    # workspace from torch's caching allocator: it is reused by the pattern arrays allocated right after
+    work = torch.empty(max(int(lib.fem_incidence_work_bytes(M * npe, n_nodes)), 1), dtype=torch.uint8, device=dev)
+    C.check(lib.fem_incidence(C.ptr(elements), M, npe, n_nodes, C.ptr(inc_ptr), C.ptr(inc), C.ptr(work),
                               C.stream(dev)), "fem_incidence")
     return inc_ptr, inc
 

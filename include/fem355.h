@@ -99,9 +99,11 @@ int fem_iso_geom(const double* coords, const int64_t* conn, int64_t M, int npe, 
 
 /* ------------------------------------------------------------------ mesh graph (pattern build)
  * Node -> (element, local) incidence, deterministic (entries sorted ascending by e*npe+local; a stable radix sort
- * of (node, slot) pairs; `work` is unused and kept for ABI compatibility).
- * inc_ptr [N+1], inc [M*npe]; work: int32 [N + fem_scan_work_len(N)]. */
+ * of (node, slot) pairs). work: a device workspace of fem_incidence_work_bytes(M*npe, N) bytes (256-aligned), or
+ * NULL to allocate it stream-ordered inside the call. */
+int64_t fem_incidence_work_bytes(int64_t total, int64_t N);
 int64_t fem_scan_work_len(int64_t n);
+/* inc_ptr [N+1], inc [M*npe] */
 int fem_incidence(const int64_t* conn, int64_t M, int npe, int64_t N, int32_t* inc_ptr, int32_t* inc,
                   int32_t* work, fem_stream_t stream);
 
