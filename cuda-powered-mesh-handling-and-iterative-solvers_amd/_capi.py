@@ -71,6 +71,12 @@ SIGNATURES = {
     "fem_sub_elements": (_I, [_P, _L, _I, _P, _I, _I, _P, _P]),
     "fem_element_face_normals": (_I, [_P, _P, _L, _I, _P, _P, _P, _P, _I, _D, _I, _I, _P, _P]),
     "fem_surface_normals": (_I, [_P, _P, _P, _L, _I, _I, _P, _P]),
+    "fem_solid_ke": (_I, [_I, _P, _P, _L, _D, _D, _P, _P, _I, _I, _P, _P]),
+    "fem_csr_pattern": (_I, [_P, _L, _I, _I, _L, _P, _P, _P, ctypes.POINTER(_L), _P]),
+    "fem_csr_fill": (_I, [_P, _P, _L, _I, _I, _L, _P, _P, _P, _P]),
+    "fem_spmv_csr": (_I, [_P, _P, _P, _P, _P, _L, _P]),
+    "fem_pcg_csr": (_I, [_P, _P, _P, _L, _P, _P, _P, _P, _D, _I, _D, _I, ctypes.POINTER(_I), ctypes.POINTER(_I), _P,
+                         _P]),
     "fem_vtk_read": (_I, [ctypes.c_char_p, ctypes.POINTER(_P)]),
     "fem_vtk_sizes": (_I, [_P, ctypes.POINTER(_L), ctypes.POINTER(_L), ctypes.POINTER(_L), ctypes.POINTER(_L)]),
     "fem_vtk_copy": (_I, [_P, _P, _P, _P]),

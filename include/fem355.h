@@ -256,6 +256,32 @@ int fem_vtk_sizes(const fem_vtk* v, int64_t* n_points, int64_t* n_cells, int64_t
 int fem_vtk_copy(const fem_vtk* v, double* points, int64_t* cells, int64_t* types);
 void fem_vtk_free(fem_vtk* v);
 
+/* ------------------------------------------------------------------ dof-level CSR layer (SURVEY §8(b) names)
+ * The assembled-matrix view of the reference (`subdivision.ipynb:118-139`: rows dof_i, cols dof_j, K_e values
+ * row-major, coalesced), dof = dpn * node + comp. [sync] where noted; temporaries are stream-ordered.
+ * fem_solid_ke: c3d8 / c3d6 / c3d10 element matrices (type = nodes per element 8 / 6 / 10) from natural points
+ *   ip [n_ip,3] and weights w [n_ip] (device); single = 1: sum_q w_q detJ_q B^T D B (c3d6: B at (1/3,1/3,0) times
+ *   the wedge volume, ip ignored), single = 0: the per-point stack [n_ip,M,d,d] (c3d6: the weighted sum)
+ *   (`solver/element.py:1754-1803`, `:2631-2676`, `:1191-1239`). */
+int fem_solid_ke(int type, const double* coords, const int64_t* conn, int64_t M, double E, double nu, const double* ip,
+                 const double* w, int n_ip, int single, double* Ke, fem_stream_t stream);
+/* [sync] dof CSR pattern: rowptr [n_nodes*dpn+1], *nnz_out; with colidx (nnz, sorted per row) and diagpos
+ * [n_nodes*dpn] (nullable) also the columns. Call once with colidx = NULL to size colidx. */
+int fem_csr_pattern(const int64_t* conn, int64_t M, int npe, int dofs_per_node, int64_t n_nodes, int32_t* rowptr,
+                    int32_t* colidx, int32_t* diagpos, int64_t* nnz_out, fem_stream_t stream);
+/* vals += coalesce(P_e^T K_e P_e), Ke [M, npe*dpn, npe*dpn], summed per entry in ascending (element, local) order */
+int fem_csr_fill(const double* Ke, const int64_t* conn, int64_t M, int npe, int dpn, int64_t n_nodes,
+                 const int32_t* rowptr, const int32_t* colidx, double* vals, fem_stream_t stream);
+/* y = A x on the dof CSR (n rows) */
+int fem_spmv_csr(const int32_t* rowptr, const int32_t* colidx, const double* vals, const double* x, double* y,
+                 int64_t n, fem_stream_t stream);
+/* [sync] one-shot solve on the dof CSR: mode FEM_MODE_CG_STABLE (`solver/solver.py:144-229`; fixed_mask dofs held
+ * at zero) or FEM_MODE_PCG (`:766-812`; z = dinv r, fixed_mask dofs get dinv = 0). x: initial guess in, solution out;
+ * res_hist_out [max_iter] (nullable) receives sqrt(r.z) per iteration. */
+int fem_pcg_csr(const int32_t* rowptr, const int32_t* colidx, const double* vals, int64_t n, const double* b,
+                double* x, const double* dinv, const uint8_t* fixed_mask, double tol, int max_iter, double eps,
+                int mode, int* iters_out, int* status_out, double* res_hist_out, fem_stream_t stream);
+
 /* ------------------------------------------------------------------ SpMV (L2)
  * y = A x on the SELL-64 matrix (nrows block rows of size bs). */
 int fem_spmv(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_t* cols, const double* vals,
