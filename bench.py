@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", type=int, default=0, help="capture k iterations per hipGraph (0 = plain launches)")
     ap.add_argument("--force-dist", action="store_true", help="run the RCCL element-partitioned path even at N=1")
+    ap.add_argument("--dist-graph", type=int, default=50,
+                    help="distributed path: capture k iterations (kernels + RCCL) per hipGraph, 0 = plain launches")
     return ap.parse_args()
 
 

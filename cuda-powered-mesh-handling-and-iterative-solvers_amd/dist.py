@@ -20,6 +20,7 @@ from __future__ import annotations
 import ctypes
 import json
 import os
+import sys
 import time
 from dataclasses import dataclass
 
@@ -340,16 +341,25 @@ def bench_main(a, metric):
     else:
         f, fixed = _mesh.cube_elasticity_case(coords)
         E, nu = 113.8e9, 0.342
-    # warm the kernels and the RCCL connections (lazily set up on the first collective)
-    c0, t0_ = _mesh.kuhn_cube(6, device=dev)
-    _sys.assemble_tet4_system(c0, t0_, a.kind, E, nu)
+    # warm the kernels (HIP modules and the torch ops of the setup load lazily on first use) and the RCCL
+    # connections (set up on the first collective) with the whole setup on a small cube
+    c0, t0_ = _mesh.kuhn_cube(8, device=dev)
+    p0 = rcb_partition(element_centroids(c0, t0_), world)
+    d0 = DistSystem(c0, t0_, p0, rank, world, a.kind, E, nu, comm)
+    d0.jacobi(torch.zeros(d0.n, dtype=torch.uint8, device=dev))
     wbuf = torch.ones(1 << 16, dtype=F64, device=dev)
     C.check(C.lib().fem_allreduce_sum(comm, C.ptr(wbuf), wbuf.numel(), C.stream(dev)), "fem_allreduce_sum")
+    del d0, p0
     barrier_sync()
 
+    stages = {}
     t0 = time.perf_counter()
     part = rcb_partition(element_centroids(coords, tets), world)
+    torch.cuda.synchronize()
+    stages["partition_ms"] = (time.perf_counter() - t0) * 1e3
     ds = DistSystem(coords, tets, part, rank, world, a.kind, E, nu, comm)
+    torch.cuda.synchronize()
+    stages["rank_mesh_assembly_ms"] = (time.perf_counter() - t0) * 1e3 - stages["partition_ms"]
     bs = ds.bs
     gmask = torch.zeros((N, bs), dtype=torch.uint8, device=dev)
     gmask[fixed] = 1
@@ -364,12 +374,26 @@ def bench_main(a, metric):
     tdist.all_reduce(bz)
     tol = a.rtol * float(bz[0]) ** 0.5
 
+    # hipGraph-captured iterations (RCCL collectives captured with the kernels): at N = 8 the host cost of ~8
+    # launches + 2 collectives per iteration would otherwise exceed the device time of an iteration
+    gk = int(getattr(a, "dist_graph", 0) or 0)
+
+    def use_graph(r, k):
+        if k <= 0:
+            return 0
+        try:
+            r.use_graph(k)
+            return k
+        except C.FemError as e:   # capture unsupported: plain launches, reported in the JSON
+            print(f"[rank {rank}] graph capture failed, plain launches: {e}", file=sys.stderr, flush=True)
+            return 0
+
     run = ds.runner(b, w, tol=tol)
     barrier_sync()
     t0 = time.perf_counter()
     run.start()
+    chunk = use_graph(run, gk) or 64
     done, it, stt = 0, 0, C.PCG_RUNNING
-    chunk = 64
     while done < 20000:
         run.iterate(chunk)
         done += chunk
@@ -382,13 +406,21 @@ def bench_main(a, metric):
 
     run = ds.runner(b, w, tol=0.0)
     run.start()
+    import math
+    graph_k = use_graph(run, math.gcd(math.gcd(gk, a.steps), a.warmup) if gk > 0 else 0)
     run.iterate(a.warmup)
     barrier_sync()
     t0 = time.perf_counter()
-    ms, cnt = run.profile(a.steps, every=a.sample_every)
+    if graph_k:
+        run.iterate(a.steps)
+    else:
+        ms, cnt = run.profile(a.steps, every=a.sample_every)
     barrier_sync()
     dt = tmax(time.perf_counter() - t0)
     it2, _, _ = run.poll()
+    if graph_k:   # kernel times sampled after the timed region (event brackets cannot sit inside a graph)
+        run.use_graph(0)
+        ms, cnt = run.profile(max(a.sample_every, 20), every=1)
     run.close()
     spmv_ms = tmax(ms[0] / max(cnt[0], 1))
     alg = ds.A.algorithmic_bytes_spmv()
@@ -404,8 +436,9 @@ def bench_main(a, metric):
             "config": {"workload": f"{tets.shape[0]:,}-tet P1 {a.kind} Kuhn cube n={a.n}, Jacobi-PCG fixed "
                                    f"iterations, element-partitioned (RCB) over {world} GPUs, RCCL halo all-reduce",
                        "tets": int(tets.shape[0]), "dofs": N * bs, "interface_nodes": nI,
-                       "parallelism": f"element partition x{world}"},
+                       "parallelism": f"element partition x{world}", "graph_iterations": graph_k},
             "dofs_per_s": N * bs / (t_asm + t_solve), "assembly_ms": t_asm * 1e3, "solve_ms": t_solve * 1e3,
+            "assembly_stages_rank0": stages,
             "solve_iters": it, "solve_status": stt,
             "kernel_ms": {"spmv_local_max": spmv_ms, "exchange_update": ms[1] / max(cnt[1], 1),
                           "pupdate": ms[2] / max(cnt[2], 1)},
