@@ -318,6 +318,100 @@ __global__ void __launch_bounds__(256) k_assemble_from_ke(const double* __restri
     }
 }
 
+// Wave-per-row version of k_assemble_from_ke. The chunk's element nodes are staged in LDS; each owner lane
+// (column, block row) builds, per incident element, the bit mask of element-local nodes equal to its column by
+// broadcast compares, then issues the element-row loads KU elements at a time (independent, all in flight) before
+// adding them in ascending (incidence, b) order onto the stored value — the additions and order of the
+// thread-per-row kernel (bit-identical). Repeated nodes inside one element (degenerate input) take the exact
+// extra-bit loop.
+constexpr int AW_WAVES = 4;   // waves per 256-thread block of the wave-per-row assembly kernels
+
+template <int BS, int NPE>
+__global__ void __launch_bounds__(256) k_assemble_ke_w(const double* __restrict__ Ke, const int64_t* __restrict__ conn,
+                                                       const int32_t* __restrict__ inc_ptr,
+                                                       const int32_t* __restrict__ inc, int64_t N,
+                                                       const int32_t* __restrict__ rowptr,
+                                                       const int32_t* __restrict__ colidx,
+                                                       const int64_t* __restrict__ csr2sell,
+                                                       double* __restrict__ vals) {
+    constexpr int JG = 64 / BS;
+    constexpr int D = NPE * BS;
+    constexpr int KU = 8;
+    __shared__ int node_s[AW_WAVES][64 * NPE];
+    __shared__ int64_t krow_s[AW_WAVES][64];   // offset of the element's block row a in Ke
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int jl = lane / BS, r = lane - BS * (lane / BS);
+    const int64_t nwaves = (int64_t)gridDim.x * AW_WAVES;
+    for (int64_t i = (int64_t)blockIdx.x * AW_WAVES + wid; i < N; i += nwaves) {
+        const int lo = rowptr[i], len = rowptr[i + 1] - lo;
+        const int t0 = inc_ptr[i], C = inc_ptr[i + 1] - t0;
+        for (int j0 = 0; j0 < len; j0 += JG) {
+            const int nj = min(JG, len - j0);
+            const bool owner = jl < nj;
+            int myj = -1;
+            int64_t Ei = 0;
+            double acc[BS];
+            if (owner) {
+                myj = colidx[lo + j0 + jl];
+                Ei = csr2sell[lo + j0 + jl];
+#pragma unroll
+                for (int c = 0; c < BS; ++c) acc[c] = vals[BS == 1 ? Ei : sell_val(Ei, BS * BS, r * BS + c)];
+            }
+            for (int k0 = 0; k0 < C; k0 += 64) {
+                const int nk = min(64, C - k0);
+                if (j0 == 0 || C > 64) {   // one chunk: staged once per row, reused by every column group
+                    __builtin_amdgcn_wave_barrier();
+                    if (lane < nk) {
+                        const int ea = inc[t0 + k0 + lane];
+                        const int e = ea / NPE;
+                        krow_s[wid][lane] = (int64_t)e * D * D + (int64_t)((ea - e * NPE) * BS) * D;
+                    }
+                    for (int q = lane; q < nk * NPE; q += 64) {
+                        const int k = q / NPE;
+                        const int e = inc[t0 + k0 + k] / NPE;
+                        node_s[wid][q] = (int)conn[(int64_t)e * NPE + (q - k * NPE)];
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
+                if (owner) {
+                    for (int kk = 0; kk < nk; kk += KU) {
+                        unsigned m[KU];
+                        double v[KU][BS];
+#pragma unroll
+                        for (int u = 0; u < KU; ++u) {
+                            const int k = min(kk + u, nk - 1);
+                            unsigned mm = 0;
+#pragma unroll
+                            for (int b = 0; b < NPE; ++b) mm |= (unsigned)(node_s[wid][k * NPE + b] == myj) << b;
+                            m[u] = (kk + u < nk) ? mm : 0u;
+                            const double* p = Ke + krow_s[wid][k] + (int64_t)r * D + (m[u] ? __builtin_ctz(m[u]) : 0) * BS;
+#pragma unroll
+                            for (int c = 0; c < BS; ++c) v[u][c] = m[u] ? p[c] : 0.0;
+                        }
+#pragma unroll
+                        for (int u = 0; u < KU; ++u) {
+                            if (!m[u]) continue;
+#pragma unroll
+                            for (int c = 0; c < BS; ++c) acc[c] += v[u][c];
+                            unsigned rest = m[u] & (m[u] - 1);
+                            while (rest) {   // the same node twice in one element
+                                const double* p = Ke + krow_s[wid][kk + u] + (int64_t)r * D + __builtin_ctz(rest) * BS;
+#pragma unroll
+                                for (int c = 0; c < BS; ++c) acc[c] += p[c];
+                                rest &= rest - 1;
+                            }
+                        }
+                    }
+                }
+            }
+            if (owner) {
+#pragma unroll
+                for (int c = 0; c < BS; ++c) vals[BS == 1 ? Ei : sell_val(Ei, BS * BS, r * BS + c)] = acc[c];
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------- fused c3d4 assembly (K_e never stored)
 template <int BS>
 __global__ void __launch_bounds__(256) k_assemble_tet4(const double* __restrict__ X, const int64_t* __restrict__ conn,
@@ -366,7 +460,6 @@ __global__ void __launch_bounds__(256) k_assemble_tet4(const double* __restrict_
 // (column, block-row) output and sums the contributions of all incident elements in ascending incidence order,
 // starting from the stored value — the same additions in the same order as the thread-per-row kernel above, so
 // the result is bit-identical, with the row's loads issued by up to 64 lanes at once instead of one thread.
-constexpr int AW_WAVES = 4;
 
 template <int BS>
 __global__ void __launch_bounds__(256) k_assemble_tet4w(const double* __restrict__ X, const int64_t* __restrict__ conn,
@@ -809,6 +902,18 @@ int fem_assemble_from_ke(const double* Ke, const int64_t* conn, int npe, int bs,
                          const int32_t* inc, int64_t N, const int32_t* rowptr, const int32_t* colidx,
                          const int64_t* csr2sell, const int64_t* slice_ptr, double* vals, fem_stream_t stream) {
     (void)slice_ptr;
+    if ((bs == 1 || bs == 3) && (npe == 4 || npe == 6 || npe == 8 || npe == 10)) {   // wave per row
+        const dim3 g((unsigned)std::min<int64_t>(cdiv(N, AW_WAVES), 8192));
+#define FEM_KE_W(B, P)                                                                                          \
+    if (bs == B && npe == P)                                                                                    \
+        hipLaunchKernelGGL((k_assemble_ke_w<B, P>), g, dim3(256), 0, S(stream), Ke, conn, inc_ptr, inc, N, rowptr, \
+                           colidx, csr2sell, vals);
+        FEM_KE_W(1, 4) FEM_KE_W(1, 6) FEM_KE_W(1, 8) FEM_KE_W(1, 10)
+        FEM_KE_W(3, 4) FEM_KE_W(3, 6) FEM_KE_W(3, 8) FEM_KE_W(3, 10)
+#undef FEM_KE_W
+        FEM_LAUNCHED();
+        return FEM_OK;
+    }
     dim3 g(stream_grid(N, 256));
     if (bs == 1)
         hipLaunchKernelGGL(k_assemble_from_ke<1>, g, dim3(256), 0, S(stream), Ke, conn, npe, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals);

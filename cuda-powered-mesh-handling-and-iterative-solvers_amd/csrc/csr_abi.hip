@@ -163,24 +163,17 @@ static int node_graph(const int64_t* conn, int64_t M, int npe, int64_t N, hipStr
     FEM_HIP(hipMallocAsync((void**)&g->inc, sizeof(int32_t) * (M * npe > 0 ? M * npe : 1), st));
     int rc = fem_incidence(conn, M, npe, N, g->inc_ptr, g->inc, nullptr, fs);
     if (rc) return rc;
-    int32_t *row_len = nullptr, *tmp = nullptr, *ovf = nullptr, *work = nullptr;
+    int32_t *row_len = nullptr, *tmp = nullptr, *work = nullptr;
     FEM_HIP(hipMallocAsync((void**)&row_len, sizeof(int32_t) * N, st));
     FEM_HIP(hipMallocAsync((void**)&tmp, sizeof(int32_t) * fem_graph_tmp_len(N), st));
-    FEM_HIP(hipMallocAsync((void**)&ovf, sizeof(int32_t), st));
-    FEM_HIP(hipMemsetAsync(ovf, 0, sizeof(int32_t), st));
     FEM_HIP(hipMallocAsync((void**)&g->rowptr, sizeof(int32_t) * (N + 1), st));
     FEM_HIP(hipMallocAsync((void**)&work, sizeof(int32_t) * (fem_scan_work_len(N) + 1), st));
-    if ((rc = fem_graph_count2(conn, npe, g->inc_ptr, g->inc, N, row_len, tmp, ovf, fs))) return rc;
+    if ((rc = fem_graph_count2(conn, npe, g->inc_ptr, g->inc, N, row_len, tmp, nullptr, fs))) return rc;
     if ((rc = fem_scan_i32(row_len, N, g->rowptr, work, fs))) return rc;
-    int32_t h[2] = {0, 0};
-    FEM_HIP(hipMemcpyAsync(&h[0], ovf, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    FEM_HIP(hipMemcpyAsync(&h[1], g->rowptr + N, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    int32_t nnz = 0;
+    FEM_HIP(hipMemcpyAsync(&nnz, g->rowptr + N, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     FEM_HIP(hipStreamSynchronize(st));
-    if (h[0]) {
-        set_error("node graph: a node has %d element-neighbour candidates, above the pattern capacity", h[0]);
-        return FEM_EARG;
-    }
-    g->nnz = h[1];
+    g->nnz = nnz;
     if (cols) {
         int32_t* diag = nullptr;
         FEM_HIP(hipMallocAsync((void**)&g->colidx, sizeof(int32_t) * (g->nnz > 0 ? g->nnz : 1), st));
@@ -190,7 +183,6 @@ static int node_graph(const int64_t* conn, int64_t M, int npe, int64_t N, hipStr
     }
     FEM_HIP(hipFreeAsync(row_len, st));
     FEM_HIP(hipFreeAsync(tmp, st));
-    FEM_HIP(hipFreeAsync(ovf, st));
     FEM_HIP(hipFreeAsync(work, st));
     return FEM_OK;
 }

@@ -63,8 +63,7 @@ __global__ void k_inc_ptr(const int32_t* __restrict__ key, int64_t total, int64_
 
 // ---------------------------------------------------------------- node graph (wave per node)
 constexpr int G_WAVES = 4;      // waves per block
-constexpr int G_CAP = 1536;     // candidate capacity per node (deg * npe)
-constexpr int G_UCAP = 512;     // unique-neighbour capacity per node
+constexpr int G_UCAP = 512;     // unique-neighbour capacity of k_graph (larger rows: k_graph_big)
 constexpr int G_SCAP = 384;     // candidate capacity of the small-row kernel
 constexpr int G_TCAP = 32;      // rows of at most this many neighbours are produced by k_graph_small
 
@@ -147,77 +146,130 @@ __global__ void k_graph_copy(const int32_t* __restrict__ tmp, const int32_t* __r
     }
 }
 
+// Rows beyond k_graph_small (c3d10 corner rows, dense fans): wave per node, candidates streamed from the incidence
+// list straight into a wave-private 2048-slot LDS hash (no candidate-count limit), the unique set compacted and
+// rank-sorted. A row whose unique count passes G_UCAP stops inserting (the table never holds more than
+// G_UCAP + 64 keys, so probing always ends) and is marked row_len = -1 for k_graph_big; the fill pass recognises
+// those rows by their length. Rows finished by k_graph_small (done[node * G_TCAP] >= 0) are skipped.
+constexpr int G_HT2 = 2048;
+
 template <bool FILL>
 __global__ void __launch_bounds__(256) k_graph(const int64_t* __restrict__ conn, int npe,
                                                const int32_t* __restrict__ inc_ptr, const int32_t* __restrict__ inc,
                                                int64_t N, int32_t* __restrict__ row_len,
                                                const int32_t* __restrict__ rowptr, int32_t* __restrict__ colidx,
-                                               int32_t* __restrict__ diagpos, int32_t* __restrict__ overflow,
-                                               const int32_t* __restrict__ done) {
-    __shared__ int cand[G_WAVES][G_CAP];
+                                               int32_t* __restrict__ diagpos, const int32_t* __restrict__ done) {
+    __shared__ int ht[G_WAVES][G_HT2];
     __shared__ int uniq[G_WAVES][G_UCAP];
+    __shared__ int cnt_s[G_WAVES];
     const int wid = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-
-    for (int64_t base = (int64_t)blockIdx.x * G_WAVES; base < N; base += (int64_t)gridDim.x * G_WAVES) {
-        const int64_t node = base + wid;
-        // rows already produced by k_graph_small (done[node * G_TCAP] >= 0) are skipped
-        const bool active = node < N && !(done && done[node * G_TCAP] >= 0);
-        int C = 0, start = 0;
-        if (active) {
-            start = inc_ptr[node];
-            C = (inc_ptr[node + 1] - start) * npe;
-        }
-        const bool ok = active && C <= G_CAP;
-        if (active && !ok) atomicMax(overflow, C);
-        // phase A: gather candidate neighbour nodes of all incident elements into LDS
-        if (ok) {
-            for (int t = lane; t < C; t += 64) {
-                int k = t / npe, b = t - k * npe;
-                int e = inc[start + k] / npe;
-                cand[wid][t] = (int)conn[(int64_t)e * npe + b];
+    for (int64_t node = (int64_t)blockIdx.x * G_WAVES + wid; node < N; node += (int64_t)gridDim.x * G_WAVES) {
+        if (done && done[node * G_TCAP] >= 0) continue;
+        if (FILL && rowptr[node + 1] - rowptr[node] > G_UCAP) continue;   // k_graph_big's row
+        const int start = inc_ptr[node];
+        const int C = (inc_ptr[node + 1] - start) * npe;
+        for (int q = lane; q < G_HT2; q += 64) ht[wid][q] = -1;
+        if (lane == 0) cnt_s[wid] = 0;
+        __builtin_amdgcn_wave_barrier();
+        for (int t0 = 0; t0 < C; t0 += 64) {
+            if (cnt_s[wid] > G_UCAP) break;                      // wave-uniform: read after the barrier below
+            const int t = t0 + lane;
+            if (t < C) {
+                const int k = t / npe, b = t - k * npe;
+                const int e = inc[start + k] / npe;
+                const int v = (int)conn[(int64_t)e * npe + b];
+                unsigned h = ((unsigned)v * 2654435761u) >> 21;   // 11 bits
+                while (true) {
+                    const int old = atomicCAS(&ht[wid][h], -1, v);
+                    if (old == -1) {
+                        atomicAdd(&cnt_s[wid], 1);
+                        break;
+                    }
+                    if (old == v) break;
+                    h = (h + 1) & (G_HT2 - 1);
+                }
             }
+            __builtin_amdgcn_wave_barrier();
         }
-        __syncthreads();
-        // phase B: first occurrences -> compact unique list
+        if (cnt_s[wid] > G_UCAP) {
+            if (!FILL && lane == 0) row_len[node] = -1;
+            __builtin_amdgcn_wave_barrier();
+            continue;
+        }
         int U = 0;
-        if (ok) {
-            for (int cb = 0; cb < C; cb += 64) {
-                int t = cb + lane;
-                bool first = false;
-                int v = 0;
-                if (t < C) {
-                    v = cand[wid][t];
-                    first = true;
-                    for (int u = 0; u < t; ++u)
-                        if (cand[wid][u] == v) { first = false; break; }
-                }
-                unsigned long long m = __ballot(first);
-                if (FILL && first) {
-                    int pos = U + __popcll(m & lt_mask);
-                    if (pos < G_UCAP) uniq[wid][pos] = v;
-                }
-                U += __popcll(m);
-            }
-            if (!FILL && lane == 0) row_len[node] = (U <= G_UCAP) ? U : 0;
-            if (U > G_UCAP && lane == 0) atomicMax(overflow, U);
-        } else if (active && !FILL && lane == 0) {
-            row_len[node] = 0;
+        for (int q0 = 0; q0 < G_HT2; q0 += 64) {
+            const int v = ht[wid][q0 + lane];
+            const bool has = v >= 0;
+            const unsigned long long m = __ballot(has);
+            if (FILL && has) uniq[wid][U + __popcll(m & lt_mask)] = v;
+            U += __popcll(m);
         }
-        __syncthreads();
-        // phase C (fill): rank-sort the unique list and write the row
-        if (FILL && ok && U <= G_UCAP) {
+        if (!FILL) {
+            if (lane == 0) row_len[node] = U;
+        } else {
+            __builtin_amdgcn_wave_barrier();
             const int32_t rp = rowptr[node];
             for (int j = lane; j < U; j += 64) {
-                int v = uniq[wid][j];
+                const int v = uniq[wid][j];
                 int rank = 0;
                 for (int u = 0; u < U; ++u) rank += (uniq[wid][u] < v);
                 colidx[rp + rank] = v;
                 if (v == (int)node) diagpos[node] = rp + rank;
             }
         }
-        __syncthreads();
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// Rows of more than G_UCAP neighbours (no limit): wave per row, ascending selection straight from the incidence
+// list — each step takes the wave-wide minimum candidate above the previous one. O(U * C / 64) per row; such rows
+// are rare (a node shared by hundreds of elements). Nodes are found 64 at a time by a ballot over the flags.
+__device__ __forceinline__ int wave_min_i32(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+    return v;
+}
+
+template <bool FILL>
+__global__ void __launch_bounds__(256) k_graph_big(const int64_t* __restrict__ conn, int npe,
+                                                   const int32_t* __restrict__ inc_ptr,
+                                                   const int32_t* __restrict__ inc, int64_t N,
+                                                   int32_t* __restrict__ row_len, const int32_t* __restrict__ rowptr,
+                                                   int32_t* __restrict__ colidx, int32_t* __restrict__ diagpos) {
+    const int wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    for (int64_t base = ((int64_t)blockIdx.x * G_WAVES + wid) * 64; base < N;
+         base += (int64_t)gridDim.x * G_WAVES * 64) {
+        const int64_t me = base + lane;
+        const bool big = me < N && (FILL ? rowptr[me + 1] - rowptr[me] > G_UCAP : row_len[me] < 0);
+        unsigned long long m = __ballot(big);
+        while (m) {
+            const int64_t node = base + (__ffsll((long long)m) - 1);
+            m &= m - 1;
+            const int start = inc_ptr[node];
+            const int C = (inc_ptr[node + 1] - start) * npe;
+            const int32_t rp = FILL ? rowptr[node] : 0;
+            int prev = -1, U = 0;
+            while (true) {
+                int best = INT_MAX;
+                for (int t = lane; t < C; t += 64) {
+                    const int k = t / npe, b = t - k * npe;
+                    const int v = (int)conn[(int64_t)(inc[start + k] / npe) * npe + b];
+                    if (v > prev && v < best) best = v;
+                }
+                best = wave_min_i32(best);
+                if (best == INT_MAX) break;
+                if (FILL && lane == 0) {
+                    colidx[rp + U] = best;
+                    if (best == (int)node) diagpos[node] = rp + U;
+                }
+                ++U;
+                prev = best;
+            }
+            if (!FILL && lane == 0) row_len[node] = U;
+        }
     }
 }
 
@@ -344,13 +396,42 @@ static int graph_grid(int64_t N) {
     return (int)(g < 1 ? 1 : g);
 }
 
-int fem_graph_count(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
-                    int32_t* row_len, int32_t* overflow, fem_stream_t stream) {
-    hipLaunchKernelGGL(k_graph<false>, dim3(graph_grid(N)), dim3(256), 0, S(stream), conn, npe, inc_ptr, inc, N,
-                       row_len, (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, overflow,
-                       (const int32_t*)nullptr);
+static int big_grid(int64_t N) {
+    int64_t g = cdiv(N, (int64_t)G_WAVES * 64);
+    if (g > 2048) g = 2048;
+    return (int)(g < 1 ? 1 : g);
+}
+
+// count: k_graph for every row (done = null) or for the rows k_graph_small left, then k_graph_big for the rows
+// k_graph flagged; row_len ends exact for every node. *overflow is kept for ABI compatibility and set to 0 (no
+// capacity limit remains).
+static int graph_count(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
+                       int32_t* row_len, const int32_t* done, int32_t* overflow, hipStream_t st) {
+    if (overflow) FEM_HIP(hipMemsetAsync(overflow, 0, sizeof(int32_t), st));
+    hipLaunchKernelGGL(k_graph<false>, dim3(graph_grid(N)), dim3(256), 0, st, conn, npe, inc_ptr, inc, N, row_len,
+                       (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, done);
+    FEM_LAUNCHED();
+    hipLaunchKernelGGL(k_graph_big<false>, dim3(big_grid(N)), dim3(256), 0, st, conn, npe, inc_ptr, inc, N, row_len,
+                       (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr);
     FEM_LAUNCHED();
     return FEM_OK;
+}
+
+static int graph_fill(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
+                      const int32_t* rowptr, int32_t* colidx, int32_t* diagpos, const int32_t* done, hipStream_t st) {
+    hipLaunchKernelGGL(k_graph<true>, dim3(graph_grid(N)), dim3(256), 0, st, conn, npe, inc_ptr, inc, N,
+                       (int32_t*)nullptr, rowptr, colidx, diagpos, done);
+    FEM_LAUNCHED();
+    hipLaunchKernelGGL(k_graph_big<true>, dim3(big_grid(N)), dim3(256), 0, st, conn, npe, inc_ptr, inc, N,
+                       (int32_t*)nullptr, rowptr, colidx, diagpos);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_graph_count(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
+                    int32_t* row_len, int32_t* overflow, fem_stream_t stream) {
+    if (N <= 0) return FEM_OK;
+    return graph_count(conn, npe, inc_ptr, inc, N, row_len, nullptr, overflow, S(stream));
 }
 
 int64_t fem_graph_tmp_len(int64_t N) { return N * G_TCAP; }
@@ -362,11 +443,7 @@ int fem_graph_count2(const int64_t* conn, int npe, const int32_t* inc_ptr, const
     hipLaunchKernelGGL(k_graph_small, dim3((unsigned)grid), dim3(256), 0, S(stream), conn, npe, inc_ptr, inc, N,
                        row_len, tmp);
     FEM_LAUNCHED();
-    hipLaunchKernelGGL(k_graph<false>, dim3(graph_grid(N)), dim3(256), 0, S(stream), conn, npe, inc_ptr, inc, N,
-                       row_len, (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, overflow,
-                       (const int32_t*)tmp);
-    FEM_LAUNCHED();
-    return FEM_OK;
+    return graph_count(conn, npe, inc_ptr, inc, N, row_len, tmp, overflow, S(stream));
 }
 
 int fem_graph_fill2(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
@@ -376,18 +453,13 @@ int fem_graph_fill2(const int64_t* conn, int npe, const int32_t* inc_ptr, const 
     hipLaunchKernelGGL(k_graph_copy, dim3(stream_grid(N * G_TCAP, 256)), dim3(256), 0, S(stream), tmp, rowptr, N,
                        colidx, diagpos);
     FEM_LAUNCHED();
-    hipLaunchKernelGGL(k_graph<true>, dim3(graph_grid(N)), dim3(256), 0, S(stream), conn, npe, inc_ptr, inc, N,
-                       (int32_t*)nullptr, rowptr, colidx, diagpos, (int32_t*)nullptr, tmp);
-    FEM_LAUNCHED();
-    return FEM_OK;
+    return graph_fill(conn, npe, inc_ptr, inc, N, rowptr, colidx, diagpos, tmp, S(stream));
 }
 
 int fem_graph_fill(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
                    const int32_t* rowptr, int32_t* colidx, int32_t* diagpos, fem_stream_t stream) {
-    hipLaunchKernelGGL(k_graph<true>, dim3(graph_grid(N)), dim3(256), 0, S(stream), conn, npe, inc_ptr, inc, N,
-                       (int32_t*)nullptr, rowptr, colidx, diagpos, (int32_t*)nullptr, (const int32_t*)nullptr);
-    FEM_LAUNCHED();
-    return FEM_OK;
+    if (N <= 0) return FEM_OK;
+    return graph_fill(conn, npe, inc_ptr, inc, N, rowptr, colidx, diagpos, nullptr, S(stream));
 }
 
 int fem_sell_delta16(const int32_t* cols, int64_t nrows, const int64_t* slice_ptr, int16_t* dcols, int32_t* overflow,

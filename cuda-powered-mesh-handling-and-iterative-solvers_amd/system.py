@@ -107,16 +107,13 @@ def build_graph(elements: torch.Tensor, n_nodes: int, compress: bool = True) -> 
     st = C.stream(dev)
     inc_ptr, inc = incidence(elements, n_nodes, checked=True)
     row_len = torch.empty(n_nodes, dtype=I32, device=dev)
-    overflow = torch.zeros(1, dtype=I32, device=dev)
     tmp = torch.empty(max(int(lib.fem_graph_tmp_len(n_nodes)), 1), dtype=I32, device=dev)
     C.check(lib.fem_graph_count2(C.ptr(elements), npe, C.ptr(inc_ptr), C.ptr(inc), n_nodes, C.ptr(row_len),
-                                 C.ptr(tmp), C.ptr(overflow), st), "fem_graph_count2")
+                                 C.ptr(tmp), None, st), "fem_graph_count2")
     rowptr = torch.empty(n_nodes + 1, dtype=I32, device=dev)
     work = torch.empty(int(lib.fem_scan_work_len(n_nodes)) + 1, dtype=I32, device=dev)
     C.check(lib.fem_scan_i32(C.ptr(row_len), n_nodes, C.ptr(rowptr), C.ptr(work), st), "fem_scan_i32")
-    ov, nnz = torch.stack([overflow[0], rowptr[-1]]).tolist()      # one sync
-    if ov:
-        raise C.FemError(f"fem355: a node has {ov} element-neighbour candidates, above the pattern capacity")
+    nnz = int(rowptr[-1])                                          # the one sync of the pattern build
     colidx = torch.empty(nnz, dtype=I32, device=dev)
     diagpos = torch.empty(n_nodes, dtype=I32, device=dev)
     C.check(lib.fem_graph_fill2(C.ptr(elements), npe, C.ptr(inc_ptr), C.ptr(inc), n_nodes, C.ptr(rowptr), C.ptr(tmp),

@@ -109,7 +109,8 @@ int fem_incidence(const int64_t* conn, int64_t M, int npe, int64_t N, int32_t* i
 
 /* Node-graph CSR pattern (block pattern for any dpn): the coalesced COO pattern of the reference's global
  * assembly (`subdivision.ipynb:118-139`) at node granularity. Two passes:
- *   fem_graph_count : row_len [N]  (unique neighbours incl. self); *overflow [device int] set on capacity
+ *   fem_graph_count : row_len [N]  (unique neighbours incl. self); *overflow [device int] is written 0 (kept
+ *                     for ABI stability: rows of any length are handled, the widest by a selection kernel)
  *   fem_graph_fill  : colidx [nnz] sorted per row, diagpos [N] (position of the diagonal)
  * rowptr [N+1] is the exclusive scan of row_len (fem_scan_i32). */
 int fem_graph_count(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
@@ -118,7 +119,7 @@ int fem_graph_fill(const int64_t* conn, int npe, const int32_t* inc_ptr, const i
                    const int32_t* rowptr, int32_t* colidx, int32_t* diagpos, fem_stream_t stream);
 /* Same pattern in (typically) one pass: rows of at most 32 neighbours from at most 384 candidates are gathered,
  * deduplicated and sorted once by a wave-private kernel into tmp [fem_graph_tmp_len(N)] (int32); the rest fall
- * back to the two-pass kernels above. fem_graph_count2 writes row_len; fem_graph_fill2 copies / fills the rows. */
+ * back to the two-pass kernels above (LDS hash up to 512 neighbours, selection beyond). fem_graph_count2 writes row_len; fem_graph_fill2 copies / fills the rows. */
 int64_t fem_graph_tmp_len(int64_t N);
 int fem_graph_count2(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
                      int32_t* row_len, int32_t* tmp, int32_t* overflow, fem_stream_t stream);

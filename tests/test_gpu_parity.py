@@ -110,6 +110,22 @@ def test_pattern_bit_exact_vs_oracle(gpu):
         assert torch.equal(t.reshape(-1)[inc], seg)                               # entry belongs to its node
 
 
+def test_pattern_wide_rows_vs_oracle(gpu):
+    """Rows past every LDS tier: > 2048 candidates (c3d10 x9 repeats, hash tier) and > 512 unique neighbours
+    (a fan of 700 tets around node 0, selection tier); bit-exact against the oracle, also through the CSR C-ABI."""
+    _, mesh, _, system = _mods()
+    c10, t10 = mesh.tet10_cube(3)
+    a = torch.arange(1, 701)
+    fan = torch.stack([torch.zeros_like(a), a, a + 1, a + 2], 1)
+    fan = torch.cat([fan, torch.tensor([[5, 9, 400, 702]])])             # a short row next to the fan
+    for t, N in ((t10.repeat(9, 1), c10.shape[0]), (fan, 703)):
+        gph = system.build_graph(t.to(gpu), N)
+        rp, ci = R.node_pattern(t, N)
+        assert torch.equal(gph.rowptr.cpu().long(), rp) and torch.equal(gph.colidx.cpu().long(), ci)
+        assert torch.equal(gph.colidx.cpu().long()[gph.diagpos.cpu().long()], torch.arange(N))
+    assert int(rp[1] - rp[0]) == 703
+
+
 def test_assembled_operator_equals_ebe_and_coo(gpu):
     el, mesh, solver, system = _mods()
     g = load_golden("tet4_cube_n4_jit")
@@ -332,3 +348,24 @@ def test_pcg_history_and_fixed_iterations(gpu):
     h = res.history.cpu()
     for k in range(20):
         assert abs(float(h[k]) - hist[k]) <= 1e-10 * hist[k], k
+
+
+@pytest.mark.parametrize("etype,n", [("c3d8", 5), ("c3d6", 4), ("c3d10", 3)])
+def test_assembly_from_element_matrices_wide_rows(gpu, etype, n):
+    """Assembly from stored K_e (wave-per-row kernel) across column groups and >64 incident elements per row:
+    assembled matvec == element-by-element product of the same K_e (bs=3 and the scalar bs=1 sub-block)."""
+    el, mesh, _, system = _mods()
+    gen = {"c3d8": mesh.hex_box, "c3d6": mesh.wedge_box, "c3d10": mesh.tet10_cube}[etype]
+    c, t = gen(n, jitter=0.1)
+    t = t.repeat(9, 1)                      # each element nine times: rows see > 64 incident elements
+    N = c.shape[0]
+    K = el.compute_K_matrix(c.to(gpu), t.to(gpu), etype, E, NU, device=gpu, dtype=F64)
+    g = system.build_graph(t.to(gpu), N)
+    inc_ptr = g.inc_ptr.cpu()
+    assert int((inc_ptr[1:] - inc_ptr[:-1]).max()) > 64
+    for bs in (3, 1):
+        Kb = K if bs == 3 else K[:, 0::3, 0::3].contiguous()
+        A = system.SellMatrix(g, bs).add_element_matrices(Kb, t.to(gpu))
+        x = torch.randn(N * bs, dtype=F64, generator=torch.Generator().manual_seed(3))
+        y_ref = R.nodal_forces(Kb.cpu(), t, x.view(N, bs)).reshape(-1)
+        assert rel(A.matvec(x.to(gpu)), y_ref) < 1e-12, (etype, bs)
