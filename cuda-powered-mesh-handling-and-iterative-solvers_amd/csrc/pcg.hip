@@ -416,6 +416,8 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_d1(int64_t nslices, int64_t n
     if (threadIdx.x == 0) partials[blockIdx.x] = dot;
 }
 
+constexpr int VPF = 4;   // double2 elements per thread loaded ahead of the partial re-sum in d2 / d3
+
 __device__ __forceinline__ double sum_prev_partials(const double* __restrict__ part, int n, double* lds4) {
     double v = 0.0;
     for (int i = threadIdx.x; i < n; i += PCG_BLOCK) v += part[i];
@@ -429,6 +431,22 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_d2(int64_t n, double* __restr
     __shared__ double lds4[4];
     PcgState::Bank& bk = st->bank[par];
     if (bk.halt || bk.iter >= st->max_iter) return;
+    // this thread's first VPF elements are loaded before the partial re-sum, so its latency hides behind them
+    const int64_t n2 = n >> 1;
+    const int64_t i0 = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x, istep = (int64_t)gridDim.x * PCG_BLOCK;
+    const double2* q2 = reinterpret_cast<const double2*>(q);
+    const double2* w2 = reinterpret_cast<const double2*>(w);
+    double2* r2 = reinterpret_cast<double2*>(r);
+    double2 rp[VPF], qp[VPF], wp[VPF];
+#pragma unroll
+    for (int u = 0; u < VPF; ++u) {
+        const int64_t i = i0 + u * istep;
+        if (i < n2) {
+            rp[u] = r2[i];
+            qp[u] = q2[i];
+            wp[u] = w2[i];
+        }
+    }
     const double pq = sum_prev_partials(part1, n1, lds4);
     const bool cg = st->mode != FEM_MODE_PCG;
     double alpha = 0.0;
@@ -449,12 +467,7 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_d2(int64_t n, double* __restr
     }
     if (stop) return;
     double acc = 0.0;
-    const int64_t n2 = n >> 1;
-    const double2* q2 = reinterpret_cast<const double2*>(q);
-    const double2* w2 = reinterpret_cast<const double2*>(w);
-    double2* r2 = reinterpret_cast<double2*>(r);
-    for (int64_t i = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; i < n2; i += (int64_t)gridDim.x * PCG_BLOCK) {
-        double2 rv = r2[i], qv = q2[i], wv = w2[i];
+    auto step = [&](int64_t i, double2 rv, const double2 qv, const double2 wv) {
         rv.x = rv.x - alpha * qv.x;
         rv.y = rv.y - alpha * qv.y;
         if (cg) {
@@ -464,7 +477,11 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_d2(int64_t n, double* __restr
         r2[i] = rv;
         acc += rv.x * (wv.x * rv.x);
         acc += rv.y * (wv.y * rv.y);
-    }
+    };
+#pragma unroll
+    for (int u = 0; u < VPF; ++u)
+        if (i0 + u * istep < n2) step(i0 + u * istep, rp[u], qp[u], wp[u]);
+    for (int64_t i = i0 + VPF * istep; i < n2; i += istep) step(i, r2[i], q2[i], w2[i]);
     if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
         int64_t i = n - 1;
         double rv = r[i] - alpha * q[i];
@@ -502,6 +519,23 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_d3(int64_t n, double* __restr
         }
         return;
     }
+    const int64_t nh = n >> 1;
+    const int64_t i0 = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x, istep = (int64_t)gridDim.x * PCG_BLOCK;
+    double2* x2 = reinterpret_cast<double2*>(x);
+    double2* p2 = reinterpret_cast<double2*>(p);
+    const double2* r2 = reinterpret_cast<const double2*>(r);
+    const double2* w2 = reinterpret_cast<const double2*>(w);
+    double2 xp[VPF], pp[VPF], rp[VPF], wp[VPF];
+#pragma unroll
+    for (int u = 0; u < VPF; ++u) {   // loaded ahead of the partial re-sum (as in d2)
+        const int64_t i = i0 + u * istep;
+        if (i < nh) {
+            xp[u] = x2[i];
+            pp[u] = p2[i];
+            rp[u] = r2[i];
+            wp[u] = w2[i];
+        }
+    }
     const double rz_new = sum_prev_partials(part2, n2p, lds4);
     const bool cg = st->mode != FEM_MODE_PCG;
     const double nrm = sqrt(rz_new);
@@ -514,23 +548,20 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_d3(int64_t n, double* __restr
     }
     const bool upd_p = !conv && !bnan;
     const double alpha = bk.alpha;
-    const int64_t nh = n >> 1;
-    double2* x2 = reinterpret_cast<double2*>(x);
-    double2* p2 = reinterpret_cast<double2*>(p);
-    const double2* r2 = reinterpret_cast<const double2*>(r);
-    const double2* w2 = reinterpret_cast<const double2*>(w);
-    for (int64_t i = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; i < nh; i += (int64_t)gridDim.x * PCG_BLOCK) {
-        double2 pv = p2[i], xv = x2[i];
+    auto step = [&](int64_t i, double2 xv, double2 pv, const double2 rv, const double2 wv) {
         xv.x += alpha * pv.x;
         xv.y += alpha * pv.y;
         x2[i] = xv;
         if (upd_p) {
-            double2 rv = r2[i], wv = w2[i];
             pv.x = wv.x * rv.x + beta * pv.x;
             pv.y = wv.y * rv.y + beta * pv.y;
             p2[i] = pv;
         }
-    }
+    };
+#pragma unroll
+    for (int u = 0; u < VPF; ++u)
+        if (i0 + u * istep < nh) step(i0 + u * istep, xp[u], pp[u], rp[u], wp[u]);
+    for (int64_t i = i0 + VPF * istep; i < nh; i += istep) step(i, x2[i], p2[i], r2[i], w2[i]);
     if ((n & 1) && lead) {
         int64_t i = n - 1;
         x[i] += alpha * p[i];
