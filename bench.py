@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--rtol", type=float, default=1e-8)
     ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--schedule", type=int, default=None, help="PCG kernel schedule (0 three-kernel, 1 fused, 2 deferred; "
+                    "default: deferred for bs=1, three-kernel for bs=3)")
     ap.add_argument("--graph", type=int, default=0, help="capture k iterations per hipGraph (0 = plain launches)")
     ap.add_argument("--force-dist", action="store_true", help="run the RCCL element-partitioned path even at N=1")
     ap.add_argument("--dist-graph", type=int, default=50,
@@ -69,6 +71,34 @@ def traffic_from_profiles(workload_key, kernel, alg):
     if d.get("kernel") != kernel or d.get("algorithmic_bytes") != alg:
         return None
     return d.get("bytes_per_launch")
+
+
+def stream_ceiling(dev, gib=2.0, reps=5):
+    """Measured HBM ceilings on this box (report the fraction of the measured STREAM ceiling too):
+    16-byte-per-lane read-only sweep and copy over buffers far larger than the 256 MB memory-side cache, best of
+    `reps`, timed with hip events on the stream the probes run on."""
+    lib = C.lib()
+    n = int(gib * (1 << 30) / 8)
+    src = torch.ones(n, dtype=torch.float64, device=dev)
+    dst = torch.empty(n // 2, dtype=torch.float64, device=dev)
+    out = torch.zeros(1, dtype=torch.float64, device=dev)
+    st = torch.cuda.current_stream(dev)
+    res = {}
+    for name, fn, nbytes in (("read", lambda: lib.fem_lab_copy(16, 1, C.ptr(src), C.ptr(out), n, 4096, C.stream(dev)), n * 8),
+                             ("copy", lambda: lib.fem_stream_copy(C.ptr(src), C.ptr(dst), n // 2, 4096, C.stream(dev)), n * 8)):
+        best = None
+        for _ in range(reps + 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            C.check(fn(), "stream probe")
+            e1.record(st)
+            e1.synchronize()
+            t = e0.elapsed_time(e1) * 1e-3
+            best = t if best is None else min(best, t)
+        res[name] = nbytes / best / 1e9
+    del src, dst
+    torch.cuda.empty_cache()
+    return res
 
 
 def cpu_baseline(n, kind, iters):
@@ -142,7 +172,7 @@ def main():
     t_solve = time.perf_counter() - t0
 
     # ---- fixed-iteration timing (the metric)
-    run = system.PcgRunner(A, b, w, tol=0.0)
+    run = system.PcgRunner(A, b, w, tol=0.0, schedule=a.schedule)
     run.start()
     if a.graph:
         run.use_graph(a.graph)
@@ -161,6 +191,7 @@ def main():
     spmv_ms = ms[0] / max(cnt[0], 1)
     alg = A.algorithmic_bytes_spmv()
     achieved = alg / (spmv_ms * 1e-3) / 1e9
+    ceiling = stream_ceiling(dev)
     workload_key = f"kuhn{a.n}_{a.kind}"
     out = {
         "metric": METRIC,
@@ -187,7 +218,8 @@ def main():
                       "sampled_launches": cnt[0]},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic_from_profiles(workload_key, kernel, alg),
-                     "kernel": kernel, "algorithmic_bytes": alg},
+                     "kernel": kernel, "algorithmic_bytes": alg,
+                     "stream_ceiling_GBps": ceiling, "frac_of_stream_read": achieved / ceiling["read"]},
         "cpu_baseline": None,
     }
     if not a.no_cpu_baseline and rank == 0:

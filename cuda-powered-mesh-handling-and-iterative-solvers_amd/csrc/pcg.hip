@@ -47,6 +47,16 @@ struct VecFusedP {
 // along lines the x gathers of neighbouring lanes are contiguous too. U entries per step: all U column loads,
 // then U value loads, then U gathers are in flight together; the tail step is predicated.
 // CI = int32_t: absolute block columns; CI = int16_t: 16-bit deltas col - row (half the index bytes)
+#ifndef FEM_SPMV_UB
+#define FEM_SPMV_UB 1
+#endif
+constexpr int SPMV_UB = FEM_SPMV_UB;   // bs > 1: blocks in flight per lane
+#ifndef FEM_SPMV_NT3
+#define FEM_SPMV_NT3 1
+#endif
+constexpr bool SPMV_NT3 = FEM_SPMV_NT3;   // bs > 1 in the PCG kernels: nontemporal matrix loads keep the p
+                                          // gather window in L2 (10M elastic K1 420 -> 406 us, PMC 1.115x alg)
+
 template <int BS, int U, bool NT, typename X, typename CI = int32_t>
 __device__ __forceinline__ void sell_row(int64_t s, int lane, const int64_t* __restrict__ slice_ptr,
                                          const CI* __restrict__ cols, const double* __restrict__ vals,
@@ -73,17 +83,34 @@ __device__ __forceinline__ void sell_row(int64_t s, int lane, const int64_t* __r
                 if (k0 + j < w) out[0] += vi[j] * xi[j];
         }
     } else {
+        // UB blocks in flight: UB column loads, UB*bs^2 plane loads, UB*bs gathers, then the FMAs in (k, r, j)
+        // order — the same per-row order as one block at a time
+        constexpr int UB = SPMV_UB;
         const double* v = vals + p0 * (BS * BS) + lane;
-        for (int k = 0; k < w; ++k) {
-            const int64_t cc = (int64_t)(base + (int)ld<CI, NT>(c + 64 * k)) * BS;
-            double xv[BS];
+        for (int k0 = 0; k0 < w; k0 += UB) {
+            int64_t cc[UB];
+            double vv[UB][BS * BS], xv[UB][BS];
 #pragma unroll
-            for (int j = 0; j < BS; ++j) xv[j] = x(cc + j);
-            const double* vk = v + (int64_t)64 * BS * BS * k;
+            for (int u = 0; u < UB; ++u)
+                cc[u] = (k0 + u < w) ? (int64_t)(base + (int)ld<CI, NT>(c + 64 * (k0 + u))) * BS : 0;
 #pragma unroll
-            for (int r = 0; r < BS; ++r)
+            for (int u = 0; u < UB; ++u) {
+                const double* vk = v + (int64_t)64 * BS * BS * (k0 + u);
 #pragma unroll
-                for (int j = 0; j < BS; ++j) out[r] += ld<double, NT>(vk + 64 * (r * BS + j)) * xv[j];
+                for (int e = 0; e < BS * BS; ++e) vv[u][e] = (k0 + u < w) ? ld<double, NT>(vk + 64 * e) : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < UB; ++u)
+#pragma unroll
+                for (int j = 0; j < BS; ++j) xv[u][j] = (k0 + u < w) ? x(cc[u] + j) : 0.0;
+#pragma unroll
+            for (int u = 0; u < UB; ++u)
+                if (k0 + u < w) {
+#pragma unroll
+                    for (int r = 0; r < BS; ++r)
+#pragma unroll
+                        for (int j = 0; j < BS; ++j) out[r] += vv[u][r * BS + j] * xv[u][j];
+                }
         }
     }
 }
@@ -246,7 +273,7 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_spmv_dot(int64_t nslices, int
         const VecFusedP pv{r, w, pold, beta};
         for (int64_t s = wk.s; s < wk.end; s += wk.step) {
             double o[BS];
-            sell_row<BS, SPMV_U, false, decltype(pv), CI>(s, lane, slice_ptr, cols, vals, pv, o);
+            sell_row<BS, SPMV_U, (BS > 1 && SPMV_NT3), decltype(pv), CI>(s, lane, slice_ptr, cols, vals, pv, o);
             const int64_t row = s * 64 + lane;
             if (row < nrows) {
 #pragma unroll
@@ -270,7 +297,7 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_spmv_dot(int64_t nslices, int
             const int64_t s = rev ? mirror - s0 : s0;
             double o[BS];
             if constexpr (PAIR) o[0] = sell_row_pair<SPMV_UP>(s, lane, slice_ptr, cols, vals, p0);
-            else sell_row<BS, SPMV_U, false, decltype(pv), CI>(s, lane, slice_ptr, cols, vals, pv, o);
+            else sell_row<BS, SPMV_U, (BS > 1 && SPMV_NT3), decltype(pv), CI>(s, lane, slice_ptr, cols, vals, pv, o);
             const int64_t row = s * 64 + lane;
             if (row < nrows) {
 #pragma unroll
@@ -402,7 +429,7 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_d1(int64_t nslices, int64_t n
         const int64_t s = rev ? mirror - s0 : s0;
         double o[BS];
         if constexpr (PAIR) o[0] = sell_row_pair<SPMV_UP>(s, lane, slice_ptr, cols, vals, p);
-        else sell_row<BS, SPMV_U, false, decltype(pv), CI>(s, lane, slice_ptr, cols, vals, pv, o);
+        else sell_row<BS, SPMV_U, (BS > 1 && SPMV_NT3), decltype(pv), CI>(s, lane, slice_ptr, cols, vals, pv, o);
         const int64_t row = s * 64 + lane;
         if (row < nrows) {
 #pragma unroll
