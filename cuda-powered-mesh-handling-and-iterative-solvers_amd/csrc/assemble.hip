@@ -318,6 +318,23 @@ __global__ void __launch_bounds__(256) k_assemble_from_ke(const double* __restri
     }
 }
 
+// XCD-aware row walk of the wave-per-row assembly kernels: SELL slice c (64 rows) belongs to XCD c % 8
+// (blockIdx % 8 under the observed round-robin placement), whose blocks take its slices in order. All 64 rows of a
+// slice are then written through ONE L2, where their partial value lines merge instead of reaching HBM from eight
+// L2s, and heavy row ranges (c3d10 corner nodes, numbered first) stay spread over all XCDs.
+// Needs gridDim.x % 8 == 0 (grid_multiple_of_xcd).
+struct RowWalk {
+    int64_t k, step;
+    int xcd;
+    __device__ __forceinline__ int64_t row(int64_t kk) const { return ((kk >> 6) * NXCD + xcd) * 64 + (kk & 63); }
+};
+
+__device__ __forceinline__ RowWalk row_walk(int waves) {
+    const int xcd = blockIdx.x % NXCD;
+    const int64_t lb = blockIdx.x / NXCD, nlb = gridDim.x / NXCD;
+    return RowWalk{lb * waves + (threadIdx.x >> 6), nlb * waves, xcd};
+}
+
 // Wave-per-row version of k_assemble_from_ke. The chunk's element nodes are staged in LDS; each owner lane
 // (column, block row) builds, per incident element, the bit mask of element-local nodes equal to its column by
 // broadcast compares, then issues the element-row loads KU elements at a time (independent, all in flight) before
@@ -341,8 +358,8 @@ __global__ void __launch_bounds__(256) k_assemble_ke_w(const double* __restrict_
     __shared__ int64_t krow_s[AW_WAVES][64];   // offset of the element's block row a in Ke
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int jl = lane / BS, r = lane - BS * (lane / BS);
-    const int64_t nwaves = (int64_t)gridDim.x * AW_WAVES;
-    for (int64_t i = (int64_t)blockIdx.x * AW_WAVES + wid; i < N; i += nwaves) {
+    const RowWalk rw = row_walk(AW_WAVES);
+    for (int64_t k = rw.k, i; (i = rw.row(k)) < N; k += rw.step) {
         const int lo = rowptr[i], len = rowptr[i + 1] - lo;
         const int t0 = inc_ptr[i], C = inc_ptr[i + 1] - t0;
         for (int j0 = 0; j0 < len; j0 += JG) {
@@ -567,8 +584,8 @@ __global__ void __launch_bounds__(256) k_assemble_p1w(const double* __restrict__
     __shared__ uint32_t pos_s[AW_WAVES][64];    // 4 column slots (bytes), 0xff = outside this column group
     __shared__ int col_s[AW_WAVES][64];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t nwaves = (int64_t)gridDim.x * AW_WAVES;
-    for (int64_t i = (int64_t)blockIdx.x * AW_WAVES + wid; i < N; i += nwaves) {
+    const RowWalk rw = row_walk(AW_WAVES);
+    for (int64_t k = rw.k, i; (i = rw.row(k)) < N; k += rw.step) {
         const int lo = rowptr[i], len = rowptr[i + 1] - lo;
         const int t0 = inc_ptr[i], C = inc_ptr[i + 1] - t0;
         for (int j0 = 0; j0 < len; j0 += 64) {
@@ -645,8 +662,8 @@ __global__ void __launch_bounds__(256) k_assemble_el3w(const double* __restrict_
     constexpr int JG = 21;
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const Lame L = lame(E, nu);
-    const int64_t nwaves = (int64_t)gridDim.x * AW_WAVES;
-    for (int64_t i = (int64_t)blockIdx.x * AW_WAVES + wid; i < N; i += nwaves) {
+    const RowWalk rw = row_walk(AW_WAVES);
+    for (int64_t k = rw.k, i; (i = rw.row(k)) < N; k += rw.step) {
         const int lo = rowptr[i], len = rowptr[i + 1] - lo;
         const int t0 = inc_ptr[i], C = inc_ptr[i + 1] - t0;
         for (int j0 = 0; j0 < len; j0 += JG) {
@@ -903,7 +920,7 @@ int fem_assemble_from_ke(const double* Ke, const int64_t* conn, int npe, int bs,
                          const int64_t* csr2sell, const int64_t* slice_ptr, double* vals, fem_stream_t stream) {
     (void)slice_ptr;
     if ((bs == 1 || bs == 3) && (npe == 4 || npe == 6 || npe == 8 || npe == 10)) {   // wave per row
-        const dim3 g((unsigned)std::min<int64_t>(cdiv(N, AW_WAVES), 8192));
+        const dim3 g((unsigned)grid_multiple_of_xcd(cdiv(N, AW_WAVES), 8192));
 #define FEM_KE_W(B, P)                                                                                          \
     if (bs == B && npe == P)                                                                                    \
         hipLaunchKernelGGL((k_assemble_ke_w<B, P>), g, dim3(256), 0, S(stream), Ke, conn, inc_ptr, inc, N, rowptr, \
@@ -934,7 +951,7 @@ int fem_assemble_tet4(const double* coords, const int64_t* conn, double E, doubl
     (void)slice_ptr;
     // wave per row (k_assemble_p1w / k_assemble_el3w); the thread-per-row k_assemble_tet4 and the first wave
     // version k_assemble_tet4w stay as reference formulations
-    const dim3 g((unsigned)std::min<int64_t>(cdiv(N, AW_WAVES), 8192));
+    const dim3 g((unsigned)grid_multiple_of_xcd(cdiv(N, AW_WAVES), 8192));
     if (bs == 1)
         hipLaunchKernelGGL(k_assemble_p1w, g, dim3(256), 0, S(stream), coords, conn, E, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals, bad_idx);
     else if (bs == 3)
