@@ -51,6 +51,8 @@ def parse():
                     "default: deferred for bs=1, three-kernel for bs=3)")
     ap.add_argument("--graph", type=int, default=0, help="capture k iterations per hipGraph (0 = plain launches)")
     ap.add_argument("--force-dist", action="store_true", help="run the RCCL element-partitioned path even at N=1")
+    ap.add_argument("--dist-variant", type=int, default=1,
+                    help="N>1: 1 = single-reduction PCG (one all-reduce per iteration), 0 = two reductions")
     ap.add_argument("--dist-graph", type=int, default=50,
                     help="distributed path: capture k iterations (kernels + RCCL) per hipGraph, 0 = plain launches")
     return ap.parse_args()

@@ -703,6 +703,184 @@ __global__ void k_bank_init(PcgState* st) {
     st->bank[0].rz_new = st->rz;
 }
 
+// ---------------------------------------------------------------- single-reduction distributed iteration
+// Chronopoulos–Gear form of the same preconditioned CG (the "single reduction" CG): with u = z = w r and
+// v = A u carried alongside r, an iteration's two dot products g = r.z (owned rows) and d = u.v (all local rows;
+// rank partials of an operator sum, like p.q above) are formed back to back and ride in ONE all-reduce together
+// with the interface rows of v:
+//     beta = g / g_prev,  p.Ap = d - beta g / alpha_prev,  alpha = g / p.Ap
+//     p = u + beta p,  s = v + beta s (= A p),  x += alpha p,  r -= alpha s,  u = w r,  v = A u
+// One collective and three kernels per iteration instead of two collectives and six kernels. Same stop test
+// (sqrt(r.z) < tol, `solver/solver.py:210` / `:805`) and guards (`:187-198`, `:214`); the rounding differs from
+// the two-reduction form, which the N>1 contract allows (1e-10 on u, +-2 iterations).
+// The all-reduce is out of place: `send` keeps zeros at the interface nodes this rank has no copy of.
+//   k_cg1_step   (1 thread) : stop test on g of the last update, beta, p.Ap, alpha, guards; iter += 1
+//   k_cg1_update (grid)     : p, s, x, r, u; g partial of the new iterate -> st->red[1]
+//   k_cg1_spmv   (grid)     : v = A u (local), d partial; interface rows of v and [g, d] -> send
+__global__ void k_cg1_step(PcgState* st, const double* __restrict__ recv, int64_t off, double* hist,
+                           int64_t hist_len) {
+    st->xupd = 0;
+    if (st->halt) return;
+    const int it = st->iter;
+    const bool cg = st->mode != FEM_MODE_PCG;
+    const double g = recv[off], d = recv[off + 1];
+    double beta = 0.0;
+    if (it > 0) {
+        st->rz_new = g;
+        const double nrm = sqrt(g);
+        if (hist && it - 1 < hist_len) hist[it - 1] = nrm;
+        if (nrm < st->tol) {
+            st->status = FEM_PCG_CONVERGED;
+            st->halt = 1;
+            st->stop_iter = it;
+            return;
+        }
+        beta = cg ? g / (st->rz + st->eps) : g / st->rz;
+        if (cg && (isnan(beta) || isinf(beta))) {
+            st->status = FEM_PCG_BETA_NAN;
+            st->halt = 1;
+            st->stop_iter = it;
+            return;
+        }
+    }
+    if (it >= st->max_iter) {   // poll reports FEM_PCG_MAXITER
+        st->halt = 1;
+        return;
+    }
+    const double pq = (it == 0) ? d : d - beta * g / st->alpha;
+    st->pq = pq;
+    double alpha;
+    if (cg) {
+        if (fabs(pq) < st->eps || pq < 0.0) {
+            st->status = FEM_PCG_BREAKDOWN;
+            st->halt = 1;
+            st->stop_iter = it + 1;
+            return;
+        }
+        alpha = g / (pq + st->eps);
+        if (isnan(alpha) || isinf(alpha)) {
+            st->status = FEM_PCG_ALPHA_NAN;
+            st->halt = 1;
+            st->stop_iter = it + 1;
+            return;
+        }
+    } else {
+        alpha = g / pq;
+    }
+    st->rz = g;
+    st->alpha = alpha;
+    st->beta = beta;
+    st->iter = it + 1;
+    st->xupd = 1;
+}
+
+__global__ void __launch_bounds__(PCG_BLOCK) k_cg1_update(int64_t n, int bs, double* __restrict__ x,
+                                                          double* __restrict__ r, double* __restrict__ p,
+                                                          double* __restrict__ sv, double* __restrict__ u,
+                                                          const double* __restrict__ v, const double* __restrict__ w,
+                                                          const double* __restrict__ recv,
+                                                          const int32_t* __restrict__ ipos,
+                                                          const uint8_t* __restrict__ own, PcgState* __restrict__ st,
+                                                          RedBuf red) {
+    __shared__ double lds4[4];
+    __shared__ int flag;
+    if (!st->xupd) return;
+    const double alpha = st->alpha, beta = st->beta;
+    const bool cg = st->mode != FEM_MODE_PCG;
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * PCG_BLOCK) {
+        const int64_t node = i / bs;
+        const int32_t j = ipos ? ipos[node] : -1;
+        const double vi = (j >= 0) ? recv[(int64_t)j * bs + (i - node * bs)] : v[i];
+        const double pi = u[i] + beta * p[i];
+        const double si = vi + beta * sv[i];
+        p[i] = pi;
+        sv[i] = si;
+        x[i] += alpha * pi;
+        double ri = r[i] - alpha * si;
+        if (cg && w[i] == 0.0) ri = 0.0;
+        r[i] = ri;
+        const double ui = w[i] * ri;
+        u[i] = ui;
+        if (!own || own[node]) acc += ri * ui;
+    }
+    acc = block_sum256(acc, lds4);
+    double g;
+    if (reduce_grid(acc, red.part(RED_K2), red.cnt(RED_K2), &g, lds4, &flag) && threadIdx.x == 0) st->red[1] = g;
+}
+
+// r0 = b - A x0 (A x0 halo-summed in q; CG: masked), u0 = w r0, p = s = 0; g0 partial -> st->red[1]
+__global__ void __launch_bounds__(PCG_BLOCK) k_cg1_init(int64_t n, int bs, const double* __restrict__ b,
+                                                        double* __restrict__ r, const double* __restrict__ q,
+                                                        const double* __restrict__ w, double* __restrict__ p,
+                                                        double* __restrict__ sv, double* __restrict__ u,
+                                                        const uint8_t* __restrict__ own, PcgState* __restrict__ st,
+                                                        RedBuf red) {
+    __shared__ double lds4[4];
+    __shared__ int flag;
+    const bool cg = st->mode != FEM_MODE_PCG;
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * PCG_BLOCK) {
+        double rv = b[i] - q[i];
+        if (cg && w[i] == 0.0) rv = 0.0;
+        r[i] = rv;
+        const double z = w[i] * rv;
+        u[i] = z;
+        p[i] = 0.0;
+        sv[i] = 0.0;
+        if (!own || own[i / bs]) acc += rv * z;
+    }
+    acc = block_sum256(acc, lds4);
+    double g;
+    if (reduce_grid(acc, red.part(RED_INIT), red.cnt(RED_INIT), &g, lds4, &flag) && threadIdx.x == 0) {
+        st->red[1] = g;
+        st->rz = g;
+    }
+}
+
+template <int BS, typename CI, bool PAIR>
+__global__ void __launch_bounds__(PCG_BLOCK) k_cg1_spmv(int64_t nslices, int64_t nrows,
+                                                        const int64_t* __restrict__ slice_ptr,
+                                                        const CI* __restrict__ cols, const double* __restrict__ vals,
+                                                        const double* __restrict__ u, double* __restrict__ v,
+                                                        const int32_t* __restrict__ ipos, double* __restrict__ send,
+                                                        int64_t off, PcgState* __restrict__ st, RedBuf red,
+                                                        int always, int tune_rev) {
+    __shared__ double lds4[4];
+    __shared__ int flag;
+    if (!always && !st->xupd) return;
+    const int lane = threadIdx.x & 63;
+    double dot = 0.0;
+    const SliceWalk wk = slice_walk(nslices);
+    const VecPlain uv{u};
+    // sweep direction alternating with the iteration parity (FEM_TUNE_REVERSE, as k_pcg_spmv_dot)
+    const bool rev = tune_rev && (st->iter & 1);
+    const int64_t mirror = wk.first + wk.end - 1;
+    for (int64_t s0 = wk.s; s0 < wk.end; s0 += wk.step) {
+        const int64_t s = rev ? mirror - s0 : s0;
+        double o[BS];
+        if constexpr (PAIR) o[0] = sell_row_pair<SPMV_UP>(s, lane, slice_ptr, cols, vals, u);
+        else sell_row<BS, SPMV_U, (BS > 1 && SPMV_NT3), decltype(uv), CI>(s, lane, slice_ptr, cols, vals, uv, o);
+        const int64_t row = s * 64 + lane;
+        if (row < nrows) {
+            const int32_t j = ipos ? ipos[row] : -1;
+#pragma unroll
+            for (int c = 0; c < BS; ++c) {
+                v[row * BS + c] = o[c];
+                dot += u[row * BS + c] * o[c];
+                if (j >= 0) send[(int64_t)j * BS + c] = o[c];
+            }
+        }
+    }
+    dot = block_sum256(dot, lds4);
+    double d;
+    if (reduce_grid(dot, red.part(RED_K1), red.cnt(RED_K1), &d, lds4, &flag) && threadIdx.x == 0) {
+        st->red[0] = d;
+        send[off] = st->red[1];
+        send[off + 1] = d;
+    }
+}
+
 // ---------------------------------------------------------------- constraint projections (CG_CONSTRAINED)
 // `enforce_constraints` (`solver/solver.py:478-510`: RBE2 then SPC) and `new_enforce_constraints` (`:665-700`:
 // SPC, RBE2, then RBE3 sets in order) on the displacement after every update; the r-zeroing of SPC dofs and RBE2
@@ -859,6 +1037,12 @@ struct fem_pcg {
     const int32_t* ipos;  // [nrows] interface index of a local row, -1 for interior rows
     const uint8_t* own;   // [nrows] 1 where this rank owns the node (lowest rank touching it)
     double* hbuf;         // [nI * bs] compact interface vector
+    // single-reduction variant (k_cg1_*): s = A p, u = w r, and the out-of-place exchange [v interface | g | d]
+    int cg1;
+    double* cg1_s;
+    double* cg1_u;
+    double* cg1_send;
+    double* cg1_recv;
 };
 
 #define FEM_NCCL(call)                                                                         \
@@ -938,6 +1122,41 @@ static int halo_pack(fem_pcg* s, const double* v, bool guarded, bool scalar) {
     return FEM_OK;
 }
 
+// single-reduction pieces (k_cg1_*); the group path (comm == NULL) copies send -> recv so the caller's in-place
+// group sum sees this rank's buffer, the RCCL path all-reduces send -> recv out of place
+static int64_t cg1_len(const fem_pcg* s) { return s->nI * s->bs + 2; }
+
+static int cg1_spmv(fem_pcg* s, int always) {
+    const int64_t off = s->nI * s->bs;
+    const int32_t* ipos = s->nI > 0 ? s->ipos : nullptr;
+#define FEM_CG1(B, CI, PR, C, V)                                                                                   \
+    hipLaunchKernelGGL((k_cg1_spmv<B, CI, PR>), dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream, s->nslices,     \
+                       s->nrows, s->slice_ptr, C, V, s->cg1_u, s->q, ipos, s->cg1_send, off, s->st, s->red, always, \
+                       s->tune & FEM_TUNE_REVERSE)
+    if (s->paired) FEM_CG1(1, int16_t, true, s->pcols16, s->pvals);
+    else if (s->cols16 && s->bs == 1) FEM_CG1(1, int16_t, false, s->cols16, s->vals);
+    else if (s->cols16) FEM_CG1(3, int16_t, false, s->cols16, s->vals);
+    else if (s->bs == 1) FEM_CG1(1, int32_t, false, s->cols, s->vals);
+    else FEM_CG1(3, int32_t, false, s->cols, s->vals);
+#undef FEM_CG1
+    FEM_LAUNCHED();
+    if (!s->comm)
+        FEM_HIP(hipMemcpyAsync(s->cg1_recv, s->cg1_send, sizeof(double) * (size_t)cg1_len(s), hipMemcpyDeviceToDevice,
+                               s->stream));
+    return FEM_OK;
+}
+
+static int cg1_step_update(fem_pcg* s) {
+    hipLaunchKernelGGL(k_cg1_step, dim3(1), dim3(1), 0, s->stream, s->st, s->cg1_recv, s->nI * s->bs, s->hist,
+                       s->hist_len);
+    FEM_LAUNCHED();
+    hipLaunchKernelGGL(k_cg1_update, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->bs, s->x, s->r, s->p0,
+                       s->cg1_s, s->cg1_u, s->q, s->w, s->cg1_recv, s->nI > 0 ? s->ipos : nullptr, s->own, s->st,
+                       s->red);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
 static int dist_phase(fem_pcg* s, int phase) {
     int rc = FEM_OK;
     switch (phase) {
@@ -976,10 +1195,24 @@ static int dist_phase(fem_pcg* s, int phase) {
             hipLaunchKernelGGL(k_set_rz, dim3(1), dim3(1), 0, s->stream, s->st);
             FEM_LAUNCHED();
             return FEM_OK;
+        case 4:   // single-reduction iteration: step + update + v = A u and pack | sum [v interface | g | d]
+            if (!s->cg1) break;
+            if ((rc = cg1_step_update(s))) return rc;
+            return cg1_spmv(s, 0);
+        case 20:  // single-reduction start (after 10): unpack A x0, r0, u0, g0; v0 = A u0 and pack | sum
+            if (!s->cg1) break;
+            hipLaunchKernelGGL(k_halo_unpack<false>, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->nrows, s->bs,
+                               s->ipos, s->hbuf, s->q, s->nI, (PcgState*)nullptr);
+            FEM_LAUNCHED();
+            hipLaunchKernelGGL(k_cg1_init, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->bs, s->b, s->r,
+                               s->q, s->w, s->p0, s->cg1_s, s->cg1_u, s->own, s->st, s->red);
+            FEM_LAUNCHED();
+            return cg1_spmv(s, 1);
         default:
-            set_error("dist_phase: unknown phase %d", phase);
-            return FEM_EARG;
+            break;
     }
+    set_error("dist_phase: unknown phase %d%s", phase, s->cg1 ? " (single-reduction: 10, 20, then 4)" : "");
+    return FEM_EARG;
 }
 
 // device buffer summed over the ranks after `phase`
@@ -998,6 +1231,9 @@ static void dist_buffer(fem_pcg* s, int phase, double** ptr, int64_t* n) {
     } else if (phase == 11) {
         *ptr = st_red(s, 2);
         *n = 1;
+    } else if (s->cg1 && (phase == 4 || phase == 20)) {
+        *ptr = s->cg1_recv;       // group path: summed in place (cg1_spmv copied send -> recv)
+        *n = cg1_len(s);
     }
 }
 
@@ -1010,7 +1246,10 @@ static int dist_exchange(fem_pcg* s, int phase) {
         set_error("distributed PCG without a communicator: drive it with fem_pcg_dist_phase");
         return FEM_EARG;
     }
-    FEM_NCCL(ncclAllReduce(p, p, (size_t)n, ncclFloat64, ncclSum, s->comm, s->stream));
+    if (s->cg1 && (phase == 4 || phase == 20))
+        FEM_NCCL(ncclAllReduce(s->cg1_send, s->cg1_recv, (size_t)n, ncclFloat64, ncclSum, s->comm, s->stream));
+    else
+        FEM_NCCL(ncclAllReduce(p, p, (size_t)n, ncclFloat64, ncclSum, s->comm, s->stream));
     return FEM_OK;
 }
 
@@ -1116,6 +1355,14 @@ static int launch_iterations(fem_pcg* s, int k) {
         for (int i = 0; i < k; ++i) {
             int rc;
             if ((rc = launch_deferred(s, 0)) || (rc = launch_deferred(s, 1)) || (rc = launch_deferred(s, 2))) return rc;
+        }
+        return FEM_OK;
+    }
+    if (s->dist && s->cg1) {
+        for (int i = 0; i < k; ++i) {
+            int rc;
+            if ((rc = dist_phase(s, 4)) || (rc = dist_exchange(s, 4))) return rc;
+            s->launched++;
         }
         return FEM_OK;
     }
@@ -1463,6 +1710,12 @@ int fem_pcg_start(fem_pcg* s) {
     int rc;
     if (s->dist) {
         if (!s->comm) return FEM_OK;   // phase-driven by the caller from phase 10 on
+        if (s->cg1) {
+            if ((rc = dist_phase(s, 10)) || (rc = dist_exchange(s, 10)) || (rc = dist_phase(s, 20)) ||
+                (rc = dist_exchange(s, 20)))
+                return rc;
+            return FEM_OK;
+        }
         if ((rc = dist_phase(s, 10)) || (rc = dist_exchange(s, 10)) || (rc = dist_phase(s, 11)) ||
             (rc = dist_exchange(s, 11)) || (rc = dist_phase(s, 12)))
             return rc;
@@ -1560,6 +1813,11 @@ int fem_pcg_set_dist(fem_pcg* s, int enable, void* comm, int64_t nI, const int32
     }
     if (s->hbuf) (void)hipFree(s->hbuf);
     s->hbuf = nullptr;
+    for (double** b : {&s->cg1_s, &s->cg1_u, &s->cg1_send, &s->cg1_recv}) {   // sized by nI: set the variant after
+        if (*b) (void)hipFree(*b);
+        *b = nullptr;
+    }
+    s->cg1 = 0;
     s->dist = enable ? 1 : 0;
     s->comm = enable ? (ncclComm_t)comm : nullptr;
     s->nI = nI;
@@ -1567,6 +1825,27 @@ int fem_pcg_set_dist(fem_pcg* s, int enable, void* comm, int64_t nI, const int32
     s->ipos = ipos;
     s->own = own;
     if (enable) FEM_HIP(hipMalloc(&s->hbuf, sizeof(double) * (size_t)(nI * s->bs + 1)));
+    return FEM_OK;
+}
+
+int fem_pcg_set_dist_variant(fem_pcg* s, int variant) {
+    if (!s->dist || s->graph || (variant != 0 && variant != 1)) {
+        set_error("fem_pcg_set_dist_variant: needs a distributed context without a captured graph, variant 0 or 1");
+        return FEM_EARG;
+    }
+    for (double** b : {&s->cg1_s, &s->cg1_u, &s->cg1_send, &s->cg1_recv}) {
+        if (*b) (void)hipFree(*b);
+        *b = nullptr;
+    }
+    s->cg1 = variant;
+    if (variant == 1) {
+        FEM_HIP(hipMalloc(&s->cg1_s, sizeof(double) * (size_t)s->n));
+        FEM_HIP(hipMalloc(&s->cg1_u, sizeof(double) * (size_t)s->n));
+        FEM_HIP(hipMalloc(&s->cg1_send, sizeof(double) * (size_t)cg1_len(s)));
+        FEM_HIP(hipMalloc(&s->cg1_recv, sizeof(double) * (size_t)cg1_len(s)));
+        FEM_HIP(hipMemset(s->cg1_send, 0, sizeof(double) * (size_t)cg1_len(s)));   // non-local interface nodes
+        FEM_HIP(hipMemset(s->cg1_recv, 0, sizeof(double) * (size_t)cg1_len(s)));
+    }
     return FEM_OK;
 }
 
@@ -1643,7 +1922,8 @@ int fem_pcg_poll(fem_pcg* s, int* iters, int* status, double* rz) {
     FEM_HIP(hipStreamSynchronize(s->stream));
     const PcgState h = state_view(s);
     int stt = h.status;
-    if (stt == FEM_PCG_RUNNING && h.iter >= h.max_iter) stt = FEM_PCG_MAXITER;
+    // single reduction: the stop test of the last update runs in the next step, which also sets halt
+    if (stt == FEM_PCG_RUNNING && h.iter >= h.max_iter && (!(s->dist && s->cg1) || h.halt)) stt = FEM_PCG_MAXITER;
     if (iters) *iters = (stt == FEM_PCG_BREAKDOWN || stt == FEM_PCG_ALPHA_NAN) ? h.stop_iter : h.iter;
     if (status) *status = stt;
     if (rz) *rz = (h.iter > 0) ? h.rz_new : h.rz;
@@ -1701,6 +1981,18 @@ int fem_pcg_profile(fem_pcg* s, int k, int every, double* ms, int* n) {
             rc = launch_iterations(s, 1);
             continue;
         }
+        if (s->dist && s->cg1) {   // buckets: [0] v = A u + pack, [1] all-reduce, [2] step + update
+            (void)hipEventRecord(evs[4 * si + 3], s->stream);
+            rc = cg1_step_update(s);
+            (void)hipEventRecord(evs[4 * si + 0], s->stream);
+            if (!rc) rc = cg1_spmv(s, 0);
+            (void)hipEventRecord(evs[4 * si + 1], s->stream);
+            if (!rc) rc = dist_exchange(s, 4);
+            (void)hipEventRecord(evs[4 * si + 2], s->stream);
+            s->launched++;
+            ++si;
+            continue;
+        }
         const bool dfr = s->deferred && !s->dist;
         (void)hipEventRecord(evs[4 * si + 0], s->stream);
         rc = dfr ? launch_deferred(s, 0) : launch_spmv_dot(s);
@@ -1716,7 +2008,9 @@ int fem_pcg_profile(fem_pcg* s, int k, int every, double* ms, int* n) {
     for (int i = 0; i < si; ++i) {
         float t;
         for (int j = 0; j < 3; ++j) {
-            (void)hipEventElapsedTime(&t, evs[4 * i + j], evs[4 * i + j + 1]);
+            // single-reduction: events 3 -> 0 bracket step + update (bucket 2)
+            const bool c1 = s->dist && s->cg1;
+            (void)hipEventElapsedTime(&t, evs[4 * i + (c1 && j == 2 ? 3 : j)], evs[4 * i + (c1 && j == 2 ? 0 : j + 1)]);
             acc[j] += t;
         }
     }
@@ -1738,6 +2032,10 @@ void fem_pcg_destroy(fem_pcg* s) {
     if (s->red.partials) (void)hipFree(s->red.partials);
     if (s->red.counters) (void)hipFree(s->red.counters);
     if (s->hbuf) (void)hipFree(s->hbuf);
+    if (s->cg1_s) (void)hipFree(s->cg1_s);
+    if (s->cg1_u) (void)hipFree(s->cg1_u);
+    if (s->cg1_send) (void)hipFree(s->cg1_send);
+    if (s->cg1_recv) (void)hipFree(s->cg1_recv);
     if (s->con.tmp) (void)hipFree(s->con.tmp);
     if (s->pvals) (void)hipFree(s->pvals);
     if (s->pcols16) (void)hipFree(s->pcols16);

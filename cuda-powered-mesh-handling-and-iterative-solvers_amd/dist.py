@@ -31,6 +31,9 @@ from . import mesh as _mesh
 from . import system as _sys
 
 F64, I32, LONG = torch.float64, torch.int32, torch.long
+# distributed iteration: 0 = two reductions (halo + p.q, then r.z), 1 = single reduction (Chronopoulos-Gear form,
+# one all-reduce of [interface rows of A u | r.z | u.Au] per iteration; csrc/pcg.hip k_cg1_*)
+VARIANT_TWO, VARIANT_SINGLE = 0, 1
 
 
 # ============================================================================ partition (host logic, any device)
@@ -158,19 +161,21 @@ class DistSystem:
                 "fem_halo_sum")
         return self.jacobi_from(d, fixed_mask_local)
 
-    def runner(self, b, w, tol=0.0, mode=C.MODE_PCG, hist_len=0):
-        return DistRunner(self, b, w, tol, mode, hist_len)
+    def runner(self, b, w, tol=0.0, mode=C.MODE_PCG, hist_len=0, variant=VARIANT_SINGLE):
+        return DistRunner(self, b, w, tol, mode, hist_len, variant)
 
 
 class DistRunner(_sys._DistMarker, _sys.PcgRunner):
     """(P)CG context of one rank in distributed mode."""
 
-    def __init__(self, ds: DistSystem, b, w, tol, mode, hist_len=0):
+    def __init__(self, ds: DistSystem, b, w, tol, mode, hist_len=0, variant=None):
         super().__init__(ds.A, b, w, mode=mode, tol=tol)
         self.ds = ds
         self.hist = torch.full((max(hist_len, 1),), float("nan"), dtype=F64, device=ds.dev) if hist_len else None
         C.check(self.lib.fem_pcg_set_dist(self.h, 1, ds.comm, ds.rm.n_iface, C.ptr(ds.rm.imap), C.ptr(ds.rm.ipos),
                                           C.ptr(ds.rm.own)), "fem_pcg_set_dist")
+        self.variant = VARIANT_SINGLE if variant is None else int(variant)
+        C.check(self.lib.fem_pcg_set_dist_variant(self.h, self.variant), "fem_pcg_set_dist_variant")
 
     def phase(self, k):
         C.check(self.lib.fem_pcg_dist_phase(self.h, int(k)), "fem_pcg_dist_phase")
@@ -211,10 +216,11 @@ class PartitionGroup:
             out.append(r.jacobi_from(d, m))
         return out
 
-    def solve(self, bs_local, ws, tol, max_iter, mode=C.MODE_PCG):
+    def solve(self, bs_local, ws, tol, max_iter, mode=C.MODE_PCG, variant=None):
         """Phase-driven (P)CG over the P partitions; returns (per-rank x, iterations, status)."""
         # every context on the current stream: the phases of all ranks and the group sums serialise in order
-        runs = [_GroupRunner(r, b, w, tol, mode) for r, b, w in zip(self.ranks, bs_local, ws)]
+        variant = VARIANT_SINGLE if variant is None else int(variant)
+        runs = [_GroupRunner(r, b, w, tol, mode, variant) for r, b, w in zip(self.ranks, bs_local, ws)]
         for run in runs:
             run.start_state()
 
@@ -225,11 +231,13 @@ class PartitionGroup:
             if n0:
                 self.group_sum([run.buffer(ph)[0] for run in runs], n0)
 
-        for ph in (10, 11, 12):
+        start, iteration = ((10, 20), (4,)) if variant == VARIANT_SINGLE else ((10, 11, 12), (0, 1, 2, 3))
+        for ph in start:
             step(ph)
         it = 0
-        for it in range(max_iter):
-            for ph in (0, 1, 2, 3):
+        # the single-reduction form tests convergence at the start of the next iteration: one extra pass
+        for it in range(max_iter + (1 if variant == VARIANT_SINGLE else 0)):
+            for ph in iteration:
                 step(ph)
             if (it + 1) % 16 == 0:
                 i_, s_, _ = runs[0].poll()
@@ -248,7 +256,7 @@ class PartitionGroup:
 class _GroupRunner:
     """Distributed (P)CG context on the current stream, driven phase by phase by PartitionGroup."""
 
-    def __init__(self, ds: DistSystem, b, w, tol, mode):
+    def __init__(self, ds: DistSystem, b, w, tol, mode, variant=0):
         self.lib = C.lib()
         A = ds.A
         self.b = b.to(F64).contiguous()
@@ -262,6 +270,7 @@ class _GroupRunner:
         A.attach_cols16(self.h)
         C.check(self.lib.fem_pcg_set_dist(self.h, 1, None, ds.rm.n_iface, C.ptr(ds.rm.imap), C.ptr(ds.rm.ipos),
                                           C.ptr(ds.rm.own)), "fem_pcg_set_dist")
+        C.check(self.lib.fem_pcg_set_dist_variant(self.h, int(variant)), "fem_pcg_set_dist_variant")
 
     def start_state(self):
         C.check(self.lib.fem_pcg_start(self.h), "fem_pcg_start")   # state only (phases do the work)
@@ -388,7 +397,8 @@ def bench_main(a, metric):
             print(f"[rank {rank}] graph capture failed, plain launches: {e}", file=sys.stderr, flush=True)
             return 0
 
-    run = ds.runner(b, w, tol=tol)
+    variant = int(getattr(a, "dist_variant", VARIANT_SINGLE))
+    run = ds.runner(b, w, tol=tol, variant=variant)
     barrier_sync()
     t0 = time.perf_counter()
     run.start()
@@ -404,7 +414,7 @@ def bench_main(a, metric):
     t_solve = tmax(time.perf_counter() - t0)
     run.close()
 
-    run = ds.runner(b, w, tol=0.0)
+    run = ds.runner(b, w, tol=0.0, variant=variant)
     run.start()
     import math
     graph_k = use_graph(run, math.gcd(math.gcd(gk, a.steps), a.warmup) if gk > 0 else 0)
@@ -434,16 +444,22 @@ def bench_main(a, metric):
             "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": f"{tets.shape[0]:,}-tet P1 {a.kind} Kuhn cube n={a.n}, Jacobi-PCG fixed "
-                                   f"iterations, element-partitioned (RCB) over {world} GPUs, RCCL halo all-reduce",
+                                   f"iterations, element-partitioned (RCB) over {world} GPUs, RCCL halo all-reduce"
+                                   + (" (single reduction: one all-reduce per iteration)" if variant else
+                                      " + r.z all-reduce"),
                        "tets": int(tets.shape[0]), "dofs": N * bs, "interface_nodes": nI,
-                       "parallelism": f"element partition x{world}", "graph_iterations": graph_k},
+                       "parallelism": f"element partition x{world}", "graph_iterations": graph_k,
+                       "dist_variant": "single-reduction" if variant else "two-reduction"},
             "dofs_per_s": N * bs / (t_asm + t_solve), "assembly_ms": t_asm * 1e3, "solve_ms": t_solve * 1e3,
             "assembly_stages_rank0": stages,
             "solve_iters": it, "solve_status": stt,
-            "kernel_ms": {"spmv_local_max": spmv_ms, "exchange_update": ms[1] / max(cnt[1], 1),
-                          "pupdate": ms[2] / max(cnt[2], 1)},
+            "kernel_ms": ({"spmv_local_max": spmv_ms, "allreduce": ms[1] / max(cnt[1], 1),
+                           "step_update": ms[2] / max(cnt[2], 1)} if variant else
+                          {"spmv_local_max": spmv_ms, "exchange_update": ms[1] / max(cnt[1], 1),
+                           "pupdate": ms[2] / max(cnt[2], 1)}),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
-                         "frac": achieved / 8000.0, "traffic": None, "kernel": "k_pcg_spmv_dot (rank 0 local)",
+                         "frac": achieved / 8000.0, "traffic": None,
+                         "kernel": ("k_cg1_spmv" if variant else "k_pcg_spmv_dot") + " (rank 0 local)",
                          "algorithmic_bytes": alg},
             "cpu_baseline": None,
         }

@@ -401,6 +401,13 @@ int fem_halo_sum(void* comm, double* v, int bs, const int32_t* imap, int64_t nI,
  * the exchanges are left to the caller, who drives the iteration phase by phase (below). */
 int fem_pcg_set_dist(fem_pcg* s, int enable, void* comm, int64_t nI, const int32_t* imap, const int32_t* ipos,
                      const uint8_t* own);
+/* Distributed iteration variant (call after fem_pcg_set_dist; resets on every fem_pcg_set_dist):
+ *   0: the two-reduction PCG above (halo + p.q all-reduce, then the r.z all-reduce; six kernels per iteration)
+ *   1: single reduction (Chronopoulos-Gear form of the same PCG): v = A u with u = z carried alongside r, so r.z,
+ *      u.v and the interface rows of v ride in ONE all-reduce per iteration (three kernels). Same stop test and
+ *      guards; rounding differs from variant 0 (N>1 contract: u within 1e-10, iterations within +-2).
+ *      Phases: start 10 | sum | 20 | sum; iteration 4 | sum (buffer: fem_pcg_dist_buffer of that phase). */
+int fem_pcg_set_dist_variant(fem_pcg* s, int variant);
 /* Phase-driven distributed iteration (what fem_pcg_start/iterate do around ncclAllReduce): phases 10, 11, 12
  * start the solve, phases 0..3 are one iteration; after a phase whose fem_pcg_dist_buffer is non-empty (10, 11:
  * start; 0: interface rows of A p + the p.q partial; 2: the r.z partial) that buffer must be summed over all ranks. Used to validate the distributed kernels with several

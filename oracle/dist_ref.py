@@ -38,8 +38,8 @@ def gdot(a, b, own_rows):
     return t[0]
 
 
-def dist_pcg(coords, elements, f, fixed, rm, kind="poisson", E=1.0, nu=0.0, tol=1e-8, max_iter=1000):
-    """One rank's share of the partitioned PCG. Returns (x_local, iterations, status)."""
+def _setup(coords, rm, f, fixed, kind, E, nu):
+    """Local operator (halo-summed), Jacobi inverse of the assembled diagonal, local rhs and owned-dof mask."""
     lc = coords[rm.nodes]
     if kind == "poisson":
         K = E * R.tet4_poisson_K(lc, rm.conn)
@@ -63,6 +63,12 @@ def dist_pcg(coords, elements, f, fixed, rm, kind="poisson", E=1.0, nu=0.0, tol=
     Minv.view(-1, bs)[gfix[rm.nodes]] = 0.0
     b = f.reshape(-1, bs)[rm.nodes].reshape(-1).to(F64)
     own = rm.own.bool().repeat_interleave(bs)
+    return A, Minv, b, own
+
+
+def dist_pcg(coords, elements, f, fixed, rm, kind="poisson", E=1.0, nu=0.0, tol=1e-8, max_iter=1000):
+    """One rank's share of the partitioned PCG. Returns (x_local, iterations, status)."""
+    A, Minv, b, own = _setup(coords, rm, f, fixed, kind, E, nu)
     x = torch.zeros_like(b)
     r = b - A(x)
     z = Minv * r
@@ -79,4 +85,39 @@ def dist_pcg(coords, elements, f, fixed, rm, kind="poisson", E=1.0, nu=0.0, tol=
             return x, i + 1, "converged"
         p = z + (rz_new / rz) * p
         rz = rz_new
+    return x, max_iter, "max_iter"
+
+
+def dist_pcg_single(coords, elements, f, fixed, rm, kind="poisson", E=1.0, nu=0.0, tol=1e-8, max_iter=1000):
+    """The single-reduction (Chronopoulos-Gear) form of the same PCG, as csrc/pcg.hip k_cg1_* runs it on N>1 GPUs:
+    u = M r and v = A u carried alongside r, beta = g/g_prev, p.Ap = d - beta g/alpha_prev, alpha = g/p.Ap with
+    g = r.u and d = u.v; p = u + beta p, s = v + beta s, x += alpha p, r -= alpha s. Stop test sqrt(r.z) < tol as
+    `solver/solver.py:805`, evaluated at the top of the next pass. Returns (x_local, iterations, status)."""
+    A, Minv, b, own = _setup(coords, rm, f, fixed, kind, E, nu)
+    x = torch.zeros_like(b)
+    r = b - A(x)
+    u = Minv * r
+    v = A(u)
+    g, d = gdot(r, u, own), gdot(u, v, own)
+    p = torch.zeros_like(b)
+    s = torch.zeros_like(b)
+    g_prev = alpha_prev = None
+    for i in range(max_iter + 1):
+        beta = 0.0
+        if i > 0:
+            if torch.sqrt(g) < tol:
+                return x, i, "converged"
+            beta = g / g_prev
+        if i == max_iter:
+            break
+        pq = d if i == 0 else d - beta * g / alpha_prev
+        alpha = g / pq
+        p = u + beta * p
+        s = v + beta * s
+        x += alpha * p
+        r -= alpha * s
+        u = Minv * r
+        v = A(u)
+        g_prev, alpha_prev = g, alpha
+        g, d = gdot(r, u, own), gdot(u, v, own)
     return x, max_iter, "max_iter"

@@ -18,7 +18,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, kind, out_path):
+def _worker(rank, world, port, kind, out_path, variant):
     import sys
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
@@ -37,19 +37,22 @@ def _worker(rank, world, port, kind, out_path):
         E, nu = 113.8e9, 0.342
     part = fd.rcb_partition(fd.element_centroids(coords, tets), world)
     rm = fd.rank_mesh(tets, part, rank, world, coords.shape[0])
-    x, it, st = dist_ref.dist_pcg(coords, tets, f, fixed, rm, kind, E, nu, tol=1e-9, max_iter=2000)
+    solve = dist_ref.dist_pcg_single if variant == "single" else dist_ref.dist_pcg
+    x, it, st = solve(coords, tets, f, fixed, rm, kind, E, nu, tol=1e-9, max_iter=2000)
     torch.save({"nodes": rm.nodes, "own": rm.own, "x": x, "it": it, "st": st, "nI": rm.n_iface},
                f"{out_path}.{rank}")
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("variant", ["two", "single"])
 @pytest.mark.parametrize("kind", ["poisson", "elastic"])
-def test_partitioned_pcg_matches_serial(tmp_path, kind):
+def test_partitioned_pcg_matches_serial(tmp_path, kind, variant):
+    """Both distributed forms: two reductions per iteration, and the single-reduction (Chronopoulos-Gear) form."""
     from fem355 import mesh
     from oracle import ref_cpu as R
     world = 2
     out = str(tmp_path / "res")
-    mp.spawn(_worker, args=(world, _free_port(), kind, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), kind, out, variant), nprocs=world, join=True)
     res = [torch.load(f"{out}.{r}", weights_only=True) for r in range(world)]
     coords, tets = mesh.kuhn_cube(5, jitter=0.1)
     N = coords.shape[0]

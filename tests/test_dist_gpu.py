@@ -10,8 +10,10 @@ pytestmark = pytest.mark.gpu
 F64 = torch.float64
 
 
-@pytest.mark.parametrize("kind,P", [("poisson", 2), ("poisson", 8), ("elastic", 3)])
-def test_partition_group_matches_single_gpu(gpu, kind, P):
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("kind,P", [("poisson", 1), ("poisson", 2), ("poisson", 8), ("elastic", 3)])
+def test_partition_group_matches_single_gpu(gpu, kind, P, variant):
+    """variant 0: two reductions per iteration; 1: single reduction (Chronopoulos-Gear form, one exchange)."""
     import fem355  # noqa: F401
     from fem355 import dist as fd, mesh, system
     coords, tets = mesh.kuhn_cube(10, jitter=0.1)
@@ -40,7 +42,7 @@ def test_partition_group_matches_single_gpu(gpu, kind, P):
     for r, wl in zip(grp.ranks, ws):
         assert rel(wl, w.view(-1, bs)[r.rm.nodes].reshape(-1)) < 1e-14
     bl = [r.local(f) for r in grp.ranks]
-    xs, it, st = grp.solve(bl, ws, tol, 3000)
+    xs, it, st = grp.solve(bl, ws, tol, 3000, variant=variant)
     assert st == 1 and abs(it - ref.iterations) <= 2, (it, ref.iterations)
     u = fd.gather_solution(grp.ranks, xs, N, bs)
     assert rel(u.reshape(-1), ref.x) < 1e-10
