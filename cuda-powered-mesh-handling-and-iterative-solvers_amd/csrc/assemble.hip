@@ -152,18 +152,30 @@ __global__ void __launch_bounds__(256) k_iso_geom(const double* __restrict__ X, 
 
 // ---------------------------------------------------------------- isoparametric solids (wave per element)
 constexpr int ISO_MAX_IP = 32;
+constexpr int ISO_IPC = 16;   // points whose geometry is staged in LDS at once
 
 template <int NPE>
 __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, const int64_t* __restrict__ conn,
                                                 int64_t M, double E, double nu, const double* __restrict__ dN,
                                                 const double* __restrict__ w, int n_ip, int mode,
                                                 double* __restrict__ Ke) {
+    // Wave per element, 4 per block. Per chunk of up to ISO_IPC points, lane q of a wave forms the Jacobian,
+    // detJ and the global gradients of point q (`einsum("ji,mjk->mik")`, `einsum("mij,nj->mni")`) into LDS —
+    // all points of the chunk at once, one barrier — then lane (a,b), a <= b, adds the 3x3 block of every point
+    // in point order. c3d10 (100 blocks > 64 lanes): only a <= b, block (b,a) written as its transpose (K_e =
+    // sum B^T D B is symmetric; mirrored entries equal the directly formed ones up to the order of two products),
+    // 55 blocks, one per lane. c3d8 / c3d6 (<= 64 blocks): every block formed directly.
     constexpr int D = 3 * NPE;
-    constexpr int NB = NPE * NPE;
+    constexpr bool SYM = NPE * NPE > 64;
+    constexpr int NS = SYM ? NPE * (NPE + 1) / 2 : NPE * NPE;
+    static_assert(NS <= 64, "one block per lane");
     __shared__ double dn_s[ISO_MAX_IP * NPE * 3];
     __shared__ double x_s[4][NPE][3];
-    __shared__ double g_s[4][NPE][3];
-    __shared__ double J_s[4][9];
+    // point gradients of the current chunk; after the last chunk the same space stages the element matrix so
+    // that the wave writes it out as contiguous 16-byte stores
+    constexpr int GK = (ISO_IPC * NPE * 3 > D * D) ? ISO_IPC * NPE * 3 : D * D;
+    __shared__ double gk_s[4][GK];
+    __shared__ double c_s[4][ISO_IPC];
     for (int t = threadIdx.x; t < n_ip * NPE * 3; t += 256) dn_s[t] = dN[t];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t e = (int64_t)blockIdx.x * 4 + wid;
@@ -174,11 +186,23 @@ __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, co
     }
     __syncthreads();
     const Lame L = lame(E, nu);
-    double acc[2][9];
+    int ba = 0, bb = 0;   // this lane's block (SYM: ba <= bb), lane < NS
+    if (SYM) {
+        int t = lane;
+        while (ba < NPE && t >= NPE - ba) {
+            t -= NPE - ba;
+            ++ba;
+        }
+        bb = ba + t;
+    } else {
+        ba = lane / NPE;
+        bb = lane - NPE * (lane / NPE);
+    }
+    const bool mirror = SYM && ba != bb;
+    const bool blk_lane = lane < NS;
+    double acc[9];
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int t = 0; t < 9; ++t) acc[q][t] = 0.0;
+    for (int t = 0; t < 9; ++t) acc[t] = 0.0;
 
     double vol = 0.0;
     if (mode == FEM_ISO_VOLUME) {  // wedge volume: 3 sub-tets (`solver/element.py:2198-2232`)
@@ -195,38 +219,42 @@ __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, co
         }
     }
 
-    for (int q = 0; q < n_ip; ++q) {
-        const double* dq = dn_s + q * NPE * 3;
-        // J[i][k] = sum_j dN[j][i] x[j][k]  (`einsum("ji,mjk->mik")`)
-        if (lane < 9) {
-            int i = lane / 3, k = lane - 3 * (lane / 3);
-            double s = 0.0;
+    for (int q0 = 0; q0 < n_ip; q0 += ISO_IPC) {
+        const int nq = min(ISO_IPC, n_ip - q0);
+        if (lane < nq) {
+            const int q = q0 + lane;
+            const double* dq = dn_s + q * NPE * 3;
+            double J[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll 1
+            for (int j = 0; j < NPE; ++j) {   // node order j ascending for every entry, as the einsum loop
+                const double d[3] = {dq[j * 3], dq[j * 3 + 1], dq[j * 3 + 2]};
+                const double xx[3] = {x_s[wid][j][0], x_s[wid][j][1], x_s[wid][j][2]};
 #pragma unroll
-            for (int j = 0; j < NPE; ++j) s += dq[j * 3 + i] * x_s[wid][j][k];
-            J_s[wid][lane] = s;
+                for (int i = 0; i < 3; ++i)
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) J[3 * i + k] += d[i] * xx[k];
+            }
+            const double c00 = J[4] * J[8] - J[5] * J[7], c01 = J[5] * J[6] - J[3] * J[8],
+                         c02 = J[3] * J[7] - J[4] * J[6];
+            const double det = J[0] * c00 + J[1] * c01 + J[2] * c02;
+            const double id = 1.0 / det;
+            const double Ji[9] = {c00 * id, (J[2] * J[7] - J[1] * J[8]) * id, (J[1] * J[5] - J[2] * J[4]) * id,
+                                  c01 * id, (J[0] * J[8] - J[2] * J[6]) * id, (J[2] * J[3] - J[0] * J[5]) * id,
+                                  c02 * id, (J[1] * J[6] - J[0] * J[7]) * id, (J[0] * J[4] - J[1] * J[3]) * id};
+#pragma unroll 1
+            for (int n = 0; n < NPE; ++n)
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+                    gk_s[wid][(lane * NPE + n) * 3 + i] =
+                        Ji[3 * i] * dq[n * 3] + Ji[3 * i + 1] * dq[n * 3 + 1] + Ji[3 * i + 2] * dq[n * 3 + 2];
+            c_s[wid][lane] = (mode == FEM_ISO_SUM) ? det * w[q] : (mode == FEM_ISO_STACK ? det : vol);
         }
         __syncthreads();
-        const double* J = J_s[wid];
-        double c00 = J[4] * J[8] - J[5] * J[7], c01 = J[5] * J[6] - J[3] * J[8], c02 = J[3] * J[7] - J[4] * J[6];
-        double det = J[0] * c00 + J[1] * c01 + J[2] * c02;
-        double id = 1.0 / det;
-        double Ji[9] = {c00 * id, (J[2] * J[7] - J[1] * J[8]) * id, (J[1] * J[5] - J[2] * J[4]) * id,
-                        c01 * id, (J[0] * J[8] - J[2] * J[6]) * id, (J[2] * J[3] - J[0] * J[5]) * id,
-                        c02 * id, (J[1] * J[6] - J[0] * J[7]) * id, (J[0] * J[4] - J[1] * J[3]) * id};
-        // global gradients g_n = Jinv dN_n (`einsum("mij,nj->mni")`)
-        if (lane < NPE * 3) {
-            int n = lane / 3, i = lane - 3 * (lane / 3);
-            g_s[wid][n][i] = Ji[3 * i] * dq[n * 3] + Ji[3 * i + 1] * dq[n * 3 + 1] + Ji[3 * i + 2] * dq[n * 3 + 2];
-        }
-        __syncthreads();
-        const double coef = (mode == FEM_ISO_SUM) ? det * w[q] : (mode == FEM_ISO_STACK ? det : vol);
-#pragma unroll
-        for (int slot = 0; slot < 2; ++slot) {
-            const int blk = lane + 64 * slot;
-            if (blk < NB) {
-                const int a = blk / NPE, b = blk - NPE * (blk / NPE);
-                const double* ga = g_s[wid][a];
-                const double* gb = g_s[wid][b];
+        for (int ql = 0; ql < nq; ++ql) {
+            const double coef = c_s[wid][ql];
+            if (blk_lane) {
+                const double* ga = &gk_s[wid][(ql * NPE + ba) * 3];
+                const double* gb = &gk_s[wid][(ql * NPE + bb) * 3];
                 const double dot = ga[0] * gb[0] + ga[1] * gb[1] + ga[2] * gb[2];
 #pragma unroll
                 for (int i = 0; i < 3; ++i)
@@ -234,40 +262,39 @@ __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, co
                     for (int k = 0; k < 3; ++k) {
                         double s = L.lam * ga[i] * gb[k] + L.mu * ga[k] * gb[i];
                         if (i == k) s += L.mu * dot;
-                        if (mode == FEM_ISO_STACK) acc[slot][3 * i + k] = s * coef;
-                        else acc[slot][3 * i + k] += s * coef;
+                        if (mode == FEM_ISO_STACK) acc[3 * i + k] = s * coef;
+                        else acc[3 * i + k] += s * coef;
                     }
             }
-        }
-        if (mode == FEM_ISO_STACK && active) {
-            double* out = Ke + ((int64_t)q * M + e) * D * D;
+            if (mode == FEM_ISO_STACK && active && blk_lane) {
+                double* out = Ke + ((int64_t)(q0 + ql) * M + e) * D * D;
 #pragma unroll
-            for (int slot = 0; slot < 2; ++slot) {
-                const int blk = lane + 64 * slot;
-                if (blk < NB) {
-                    const int a = blk / NPE, b = blk - NPE * (blk / NPE);
+                for (int i = 0; i < 3; ++i)
 #pragma unroll
-                    for (int i = 0; i < 3; ++i)
-#pragma unroll
-                        for (int k = 0; k < 3; ++k) out[(3 * a + i) * D + 3 * b + k] = acc[slot][3 * i + k];
-                }
+                    for (int k = 0; k < 3; ++k) {
+                        out[(3 * ba + i) * D + 3 * bb + k] = acc[3 * i + k];
+                        if (mirror) out[(3 * bb + k) * D + 3 * ba + i] = acc[3 * i + k];
+                    }
             }
         }
         __syncthreads();
     }
-    if (mode != FEM_ISO_STACK && active) {
-        double* out = Ke + e * D * D;
+    if (mode != FEM_ISO_STACK && active) {   // (the loop above ended on a barrier: gk_s is free)
+        double* ks = gk_s[wid];
+        if (blk_lane) {
 #pragma unroll
-        for (int slot = 0; slot < 2; ++slot) {
-            const int blk = lane + 64 * slot;
-            if (blk < NB) {
-                const int a = blk / NPE, b = blk - NPE * (blk / NPE);
+            for (int i = 0; i < 3; ++i)
 #pragma unroll
-                for (int i = 0; i < 3; ++i)
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) out[(3 * a + i) * D + 3 * b + k] = acc[slot][3 * i + k];
-            }
+                for (int k = 0; k < 3; ++k) {
+                    ks[(3 * ba + i) * D + 3 * bb + k] = acc[3 * i + k];
+                    if (mirror) ks[(3 * bb + k) * D + 3 * ba + i] = acc[3 * i + k];
+                }
         }
+        __builtin_amdgcn_wave_barrier();
+        // D*D is even for every NPE here, and e * D * D * 8 bytes is 16-byte aligned
+        double2* out2 = reinterpret_cast<double2*>(Ke + e * D * D);
+        const double2* ks2 = reinterpret_cast<const double2*>(ks);
+        for (int t = lane; t < D * D / 2; t += 64) out2[t] = ks2[t];
     }
 }
 
