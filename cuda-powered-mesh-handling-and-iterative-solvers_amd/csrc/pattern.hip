@@ -73,10 +73,18 @@ constexpr int G_TCAP = 32;      // rows of at most this many neighbours are prod
 // G_TCAP neighbours get tmp[node * G_TCAP] = -1 and are left to k_graph (count and fill passes skip the rest).
 constexpr int G_HT = 512;
 
+// hash table of a row: the smallest power of two >= 2 C slots (at least 128, at most 1 << maxbits), so clearing
+// and compacting it costs ~C, not the table capacity (P1 rows: 96 candidates -> 256 slots instead of 512)
+__device__ __forceinline__ int ht_bits(int C, int maxbits) {
+    const int b = (C <= 64) ? 7 : 32 - __clz(2 * C - 1);
+    return b > maxbits ? maxbits : b;
+}
+
 __global__ void __launch_bounds__(256) k_graph_small(const int64_t* __restrict__ conn, int npe,
                                                      const int32_t* __restrict__ inc_ptr,
                                                      const int32_t* __restrict__ inc, int64_t N,
-                                                     int32_t* __restrict__ row_len, int32_t* __restrict__ tmp) {
+                                                     int32_t* __restrict__ row_len, int32_t* __restrict__ tmp,
+                                                     uint8_t* __restrict__ defer) {
     __shared__ int ht[G_WAVES][G_HT];
     __shared__ int uniq[G_WAVES][64];
     const int wid = threadIdx.x >> 6;
@@ -87,25 +95,26 @@ __global__ void __launch_bounds__(256) k_graph_small(const int64_t* __restrict__
         const int C = (inc_ptr[node + 1] - start) * npe;
         int32_t* trow = tmp + node * G_TCAP;
         if (C > G_SCAP) {
-            if (lane == 0) trow[0] = -1;
+            if (lane == 0) defer[node] = 1;
             continue;
         }
-        for (int q = lane; q < G_HT; q += 64) ht[wid][q] = -1;
+        const int hb = ht_bits(C, 9), HS = 1 << hb;
+        for (int q = lane; q < HS; q += 64) ht[wid][q] = -1;
         __builtin_amdgcn_wave_barrier();
         for (int t = lane; t < C; t += 64) {
             const int k = t / npe, b = t - k * npe;
             const int e = inc[start + k] / npe;
             const int v = (int)conn[(int64_t)e * npe + b];
-            unsigned h = ((unsigned)v * 2654435761u) >> 23;   // 9 bits
+            unsigned h = ((unsigned)v * 2654435761u) >> (32 - hb);
             while (true) {
                 const int old = atomicCAS(&ht[wid][h], -1, v);
                 if (old == -1 || old == v) break;
-                h = (h + 1) & (G_HT - 1);
+                h = (h + 1) & (HS - 1);
             }
         }
         __builtin_amdgcn_wave_barrier();
         int U = 0;
-        for (int q0 = 0; q0 < G_HT; q0 += 64) {
+        for (int q0 = 0; q0 < HS; q0 += 64) {
             const int v = ht[wid][q0 + lane];
             const bool has = v >= 0;
             const unsigned long long m = __ballot(has);
@@ -117,7 +126,7 @@ __global__ void __launch_bounds__(256) k_graph_small(const int64_t* __restrict__
         }
         __builtin_amdgcn_wave_barrier();
         if (U > G_TCAP) {
-            if (lane == 0) trow[0] = -1;
+            if (lane == 0) defer[node] = 1;
             continue;
         }
         if (lane < U) {
@@ -126,18 +135,22 @@ __global__ void __launch_bounds__(256) k_graph_small(const int64_t* __restrict__
             for (int u = 0; u < U; ++u) rank += (uniq[wid][u] < v);
             trow[rank] = v;
         }
-        if (lane == 0) row_len[node] = U;
+        if (lane == 0) {
+            row_len[node] = U;
+            defer[node] = 0;
+        }
         __builtin_amdgcn_wave_barrier();
     }
 }
 
-// rows of k_graph_small -> CSR colidx / diagpos
-__global__ void k_graph_copy(const int32_t* __restrict__ tmp, const int32_t* __restrict__ rowptr, int64_t N,
-                             int32_t* __restrict__ colidx, int32_t* __restrict__ diagpos) {
+// rows of k_graph_small -> CSR colidx / diagpos (only the row's own entries of tmp are read)
+__global__ void k_graph_copy(const int32_t* __restrict__ tmp, const uint8_t* __restrict__ defer,
+                             const int32_t* __restrict__ rowptr, int64_t N, int32_t* __restrict__ colidx,
+                             int32_t* __restrict__ diagpos) {
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < N * G_TCAP; t += (int64_t)gridDim.x * blockDim.x) {
         const int64_t node = t / G_TCAP;
         const int j = (int)(t - node * G_TCAP);
-        if (tmp[node * G_TCAP] < 0) continue;
+        if (defer[node]) continue;
         const int rp = rowptr[node], len = rowptr[node + 1] - rp;
         if (j >= len) continue;
         const int v = tmp[t];
@@ -150,7 +163,7 @@ __global__ void k_graph_copy(const int32_t* __restrict__ tmp, const int32_t* __r
 // list straight into a wave-private 2048-slot LDS hash (no candidate-count limit), the unique set compacted and
 // rank-sorted. A row whose unique count passes G_UCAP stops inserting (the table never holds more than
 // G_UCAP + 64 keys, so probing always ends) and is marked row_len = -1 for k_graph_big; the fill pass recognises
-// those rows by their length. Rows finished by k_graph_small (done[node * G_TCAP] >= 0) are skipped.
+// those rows by their length. Rows finished by k_graph_small (defer[node] == 0) are skipped.
 constexpr int G_HT2 = 2048;
 
 template <bool FILL>
@@ -158,19 +171,28 @@ __global__ void __launch_bounds__(256) k_graph(const int64_t* __restrict__ conn,
                                                const int32_t* __restrict__ inc_ptr, const int32_t* __restrict__ inc,
                                                int64_t N, int32_t* __restrict__ row_len,
                                                const int32_t* __restrict__ rowptr, int32_t* __restrict__ colidx,
-                                               int32_t* __restrict__ diagpos, const int32_t* __restrict__ done) {
+                                               int32_t* __restrict__ diagpos, const uint8_t* __restrict__ defer) {
     __shared__ int ht[G_WAVES][G_HT2];
     __shared__ int uniq[G_WAVES][G_UCAP];
     __shared__ int cnt_s[G_WAVES];
     const int wid = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (int64_t node = (int64_t)blockIdx.x * G_WAVES + wid; node < N; node += (int64_t)gridDim.x * G_WAVES) {
-        if (done && done[node * G_TCAP] >= 0) continue;
-        if (FILL && rowptr[node + 1] - rowptr[node] > G_UCAP) continue;   // k_graph_big's row
+    // 64 candidate nodes per wave step (node = wave + nwaves * (64 c + lane): heavy rows numbered together, like
+    // c3d10 corner nodes, stay spread over the waves): one look at the flags, then only this kernel's rows
+    const int64_t wv = (int64_t)blockIdx.x * G_WAVES + wid, nw = (int64_t)gridDim.x * G_WAVES;
+    for (int64_t c0 = 0; wv + nw * c0 < N; c0 += 64) {
+      const int64_t me = wv + nw * (c0 + lane);
+      bool mine = me < N && (!defer || defer[me]);
+      if (FILL && mine) mine = rowptr[me + 1] - rowptr[me] <= G_UCAP;   // longer rows: k_graph_big
+      unsigned long long todo = __ballot(mine);
+      while (todo) {
+        const int64_t node = wv + nw * (c0 + __ffsll((long long)todo) - 1);
+        todo &= todo - 1;
         const int start = inc_ptr[node];
         const int C = (inc_ptr[node + 1] - start) * npe;
-        for (int q = lane; q < G_HT2; q += 64) ht[wid][q] = -1;
+        const int hb = ht_bits(C, 11), HS = 1 << hb;   // >= 2 C slots, or 2048 >= G_UCAP + 64 keys
+        for (int q = lane; q < HS; q += 64) ht[wid][q] = -1;
         if (lane == 0) cnt_s[wid] = 0;
         __builtin_amdgcn_wave_barrier();
         for (int t0 = 0; t0 < C; t0 += 64) {
@@ -180,7 +202,7 @@ __global__ void __launch_bounds__(256) k_graph(const int64_t* __restrict__ conn,
                 const int k = t / npe, b = t - k * npe;
                 const int e = inc[start + k] / npe;
                 const int v = (int)conn[(int64_t)e * npe + b];
-                unsigned h = ((unsigned)v * 2654435761u) >> 21;   // 11 bits
+                unsigned h = ((unsigned)v * 2654435761u) >> (32 - hb);
                 while (true) {
                     const int old = atomicCAS(&ht[wid][h], -1, v);
                     if (old == -1) {
@@ -188,7 +210,7 @@ __global__ void __launch_bounds__(256) k_graph(const int64_t* __restrict__ conn,
                         break;
                     }
                     if (old == v) break;
-                    h = (h + 1) & (G_HT2 - 1);
+                    h = (h + 1) & (HS - 1);
                 }
             }
             __builtin_amdgcn_wave_barrier();
@@ -199,7 +221,7 @@ __global__ void __launch_bounds__(256) k_graph(const int64_t* __restrict__ conn,
             continue;
         }
         int U = 0;
-        for (int q0 = 0; q0 < G_HT2; q0 += 64) {
+        for (int q0 = 0; q0 < HS; q0 += 64) {
             const int v = ht[wid][q0 + lane];
             const bool has = v >= 0;
             const unsigned long long m = __ballot(has);
@@ -220,6 +242,7 @@ __global__ void __launch_bounds__(256) k_graph(const int64_t* __restrict__ conn,
             }
         }
         __builtin_amdgcn_wave_barrier();
+      }
     }
 }
 
@@ -284,29 +307,42 @@ __global__ void k_sell_widths(const int32_t* __restrict__ rowptr, int64_t nrows,
     }
 }
 
-__global__ void k_sell_fill(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ colidx, int64_t nrows,
-                            int64_t nslices, const int64_t* __restrict__ slice_ptr, int32_t* __restrict__ cols,
-                            int64_t* __restrict__ csr2sell) {
-    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nslices * 64; r += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t s = r >> 6;
-        const int lane = (int)(r & 63);
-        const int64_t e0 = slice_ptr[s] + lane;
-        const int w = (int)((slice_ptr[s + 1] - slice_ptr[s]) >> 6);
+// Wave per slice. Pass 1, lane = row: cols of column slot k, one contiguous 256-byte store per k (the CSR reads
+// are strided but the slice's CSR segment is a few KB, cache-resident after the first touch). Pass 2, lane = CSR
+// position of the slice's contiguous segment: csr2sell written contiguously, the row of a position found by a
+// binary search over the slice's 65 row starts in LDS.
+__global__ void __launch_bounds__(256) k_sell_fill(const int32_t* __restrict__ rowptr,
+                                                   const int32_t* __restrict__ colidx, int64_t nrows, int64_t nslices,
+                                                   const int64_t* __restrict__ slice_ptr, int32_t* __restrict__ cols,
+                                                   int64_t* __restrict__ csr2sell) {
+    __shared__ int32_t rp_s[4][65];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int64_t s = (int64_t)blockIdx.x * 4 + wid; s < nslices; s += (int64_t)gridDim.x * 4) {
+        const int64_t r = s * 64 + lane;
+        const int64_t e0 = slice_ptr[s];
+        const int w = (int)((slice_ptr[s + 1] - e0) >> 6);
+        const int64_t rlast = min(s * 64 + 64, nrows);
+        rp_s[wid][lane] = rowptr[min(r, rlast)];
+        if (lane == 0) rp_s[wid][64] = rowptr[rlast];
+        __builtin_amdgcn_wave_barrier();
         int len = 0, rp = 0;
         if (r < nrows) {
-            rp = rowptr[r];
-            len = rowptr[r + 1] - rp;
+            rp = rp_s[wid][lane];
+            len = rp_s[wid][lane + 1] - rp;
         }
         const int pad = (r < nrows) ? (int)r : (int)(nrows - 1);   // near the row: 16-bit deltas stay small
-        for (int k = 0; k < w; ++k) {
-            int64_t e = e0 + (int64_t)k * 64;
-            if (k < len) {
-                cols[e] = colidx[rp + k];
-                csr2sell[rp + k] = e;
-            } else {
-                cols[e] = pad;
+        for (int k = 0; k < w; ++k) cols[e0 + (int64_t)k * 64 + lane] = (k < len) ? colidx[rp + k] : pad;
+        const int p0 = rp_s[wid][0], p1 = rp_s[wid][64];
+        for (int p = p0 + lane; p < p1; p += 64) {
+            int lo = 0, hi = 64;   // last row l with rp_s[l] <= p
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (rp_s[wid][mid] <= p) lo = mid;
+                else hi = mid;
             }
+            csr2sell[p] = e0 + (int64_t)(p - rp_s[wid][lo]) * 64 + lo;
         }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -317,16 +353,17 @@ __global__ void k_sell_delta16(const int32_t* __restrict__ cols, int64_t nslices
         const int64_t s = r >> 6;
         const int64_t e0 = slice_ptr[s] + (r & 63);
         const int w = (int)((slice_ptr[s + 1] - slice_ptr[s]) >> 6);
+        bool far = false;
         for (int k = 0; k < w; ++k) {
             const int64_t e = e0 + (int64_t)k * 64;
             const int64_t d = (int64_t)cols[e] - r;
-            if (d > 32767 || d < -32767) {
-                atomicOr(overflow, 1);
-                dcols[e] = 0;
-            } else {
-                dcols[e] = (int16_t)d;
-            }
+            const bool f = d > 32767 || d < -32767;
+            far |= f;
+            dcols[e] = f ? (int16_t)0 : (int16_t)d;
         }
+        // one flag write per row at most (a numbering with many far columns, c3d10 mid-edge nodes after the
+        // corners, made one atomic per entry cost milliseconds)
+        if (far && !*overflow) atomicOr(overflow, 1);
     }
 }
 
@@ -406,10 +443,10 @@ static int big_grid(int64_t N) {
 // k_graph flagged; row_len ends exact for every node. *overflow is kept for ABI compatibility and set to 0 (no
 // capacity limit remains).
 static int graph_count(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
-                       int32_t* row_len, const int32_t* done, int32_t* overflow, hipStream_t st) {
+                       int32_t* row_len, const uint8_t* defer, int32_t* overflow, hipStream_t st) {
     if (overflow) FEM_HIP(hipMemsetAsync(overflow, 0, sizeof(int32_t), st));
     hipLaunchKernelGGL(k_graph<false>, dim3(graph_grid(N)), dim3(256), 0, st, conn, npe, inc_ptr, inc, N, row_len,
-                       (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, done);
+                       (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, defer);
     FEM_LAUNCHED();
     hipLaunchKernelGGL(k_graph_big<false>, dim3(big_grid(N)), dim3(256), 0, st, conn, npe, inc_ptr, inc, N, row_len,
                        (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr);
@@ -418,9 +455,9 @@ static int graph_count(const int64_t* conn, int npe, const int32_t* inc_ptr, con
 }
 
 static int graph_fill(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
-                      const int32_t* rowptr, int32_t* colidx, int32_t* diagpos, const int32_t* done, hipStream_t st) {
+                      const int32_t* rowptr, int32_t* colidx, int32_t* diagpos, const uint8_t* defer, hipStream_t st) {
     hipLaunchKernelGGL(k_graph<true>, dim3(graph_grid(N)), dim3(256), 0, st, conn, npe, inc_ptr, inc, N,
-                       (int32_t*)nullptr, rowptr, colidx, diagpos, done);
+                       (int32_t*)nullptr, rowptr, colidx, diagpos, defer);
     FEM_LAUNCHED();
     hipLaunchKernelGGL(k_graph_big<true>, dim3(big_grid(N)), dim3(256), 0, st, conn, npe, inc_ptr, inc, N,
                        (int32_t*)nullptr, rowptr, colidx, diagpos);
@@ -434,26 +471,31 @@ int fem_graph_count(const int64_t* conn, int npe, const int32_t* inc_ptr, const 
     return graph_count(conn, npe, inc_ptr, inc, N, row_len, nullptr, overflow, S(stream));
 }
 
-int64_t fem_graph_tmp_len(int64_t N) { return N * G_TCAP; }
+// tmp: [N * G_TCAP] rows of k_graph_small, then N bytes of deferral flags (rows left to k_graph / k_graph_big)
+int64_t fem_graph_tmp_len(int64_t N) { return N * G_TCAP + (N + 3) / 4; }
+static uint8_t* defer_flags(int32_t* tmp, int64_t N) { return reinterpret_cast<uint8_t*>(tmp + N * G_TCAP); }
+static const uint8_t* defer_flags(const int32_t* tmp, int64_t N) {
+    return reinterpret_cast<const uint8_t*>(tmp + N * G_TCAP);
+}
 
 int fem_graph_count2(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
                      int32_t* row_len, int32_t* tmp, int32_t* overflow, fem_stream_t stream) {
     if (N <= 0) return FEM_OK;
     const int64_t grid = std::min<int64_t>(cdiv(N, G_WAVES), 16384);
     hipLaunchKernelGGL(k_graph_small, dim3((unsigned)grid), dim3(256), 0, S(stream), conn, npe, inc_ptr, inc, N,
-                       row_len, tmp);
+                       row_len, tmp, defer_flags(tmp, N));
     FEM_LAUNCHED();
-    return graph_count(conn, npe, inc_ptr, inc, N, row_len, tmp, overflow, S(stream));
+    return graph_count(conn, npe, inc_ptr, inc, N, row_len, defer_flags(tmp, N), overflow, S(stream));
 }
 
 int fem_graph_fill2(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
                     const int32_t* rowptr, const int32_t* tmp, int32_t* colidx, int32_t* diagpos,
                     fem_stream_t stream) {
     if (N <= 0) return FEM_OK;
-    hipLaunchKernelGGL(k_graph_copy, dim3(stream_grid(N * G_TCAP, 256)), dim3(256), 0, S(stream), tmp, rowptr, N,
-                       colidx, diagpos);
+    hipLaunchKernelGGL(k_graph_copy, dim3(stream_grid(N * G_TCAP, 256)), dim3(256), 0, S(stream), tmp,
+                       defer_flags(tmp, N), rowptr, N, colidx, diagpos);
     FEM_LAUNCHED();
-    return graph_fill(conn, npe, inc_ptr, inc, N, rowptr, colidx, diagpos, tmp, S(stream));
+    return graph_fill(conn, npe, inc_ptr, inc, N, rowptr, colidx, diagpos, defer_flags(tmp, N), S(stream));
 }
 
 int fem_graph_fill(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
@@ -481,8 +523,9 @@ int fem_sell_widths(const int32_t* rowptr, int64_t nrows, int64_t* width, fem_st
 int fem_sell_fill(const int32_t* rowptr, const int32_t* colidx, int64_t nrows, const int64_t* slice_ptr,
                   int32_t* cols, int64_t* csr2sell, fem_stream_t stream) {
     int64_t ns = cdiv(nrows, 64);
-    hipLaunchKernelGGL(k_sell_fill, dim3(stream_grid(ns * 64, 256)), dim3(256), 0, S(stream), rowptr, colidx, nrows,
-                       ns, slice_ptr, cols, csr2sell);
+    if (ns == 0) return FEM_OK;
+    hipLaunchKernelGGL(k_sell_fill, dim3((unsigned)std::min<int64_t>(cdiv(ns, 4), 16384)), dim3(256), 0, S(stream),
+                       rowptr, colidx, nrows, ns, slice_ptr, cols, csr2sell);
     FEM_LAUNCHED();
     return FEM_OK;
 }
