@@ -369,8 +369,11 @@ __device__ __forceinline__ RowWalk row_walk(int waves) {
 // thread-per-row kernel (bit-identical). Repeated nodes inside one element (degenerate input) take the exact
 // extra-bit loop.
 constexpr int AW_WAVES = 4;   // waves per 256-thread block of the wave-per-row assembly kernels
+#ifndef FEM_KE_RPL3
+#define FEM_KE_RPL3 1   // bs = 3 assembly from K_e: block rows per lane (3, one lane per column: c3d8 4.2 -> 5.1 ms)
+#endif
 
-template <int BS, int NPE>
+template <int BS, int NPE, int RPL>
 __global__ void __launch_bounds__(256) k_assemble_ke_w(const double* __restrict__ Ke, const int64_t* __restrict__ conn,
                                                        const int32_t* __restrict__ inc_ptr,
                                                        const int32_t* __restrict__ inc, int64_t N,
@@ -378,13 +381,15 @@ __global__ void __launch_bounds__(256) k_assemble_ke_w(const double* __restrict_
                                                        const int32_t* __restrict__ colidx,
                                                        const int64_t* __restrict__ csr2sell,
                                                        double* __restrict__ vals) {
-    constexpr int JG = 64 / BS;
+    // RPL block rows per lane: BS / RPL lanes per column, 64 RPL / BS columns per group
+    constexpr int LPC = BS / RPL;
+    constexpr int JG = 64 / LPC;
     constexpr int D = NPE * BS;
-    constexpr int KU = 8;
+    constexpr int KU = (RPL == 1) ? 8 : 4;
     __shared__ int node_s[AW_WAVES][64 * NPE];
     __shared__ int64_t krow_s[AW_WAVES][64];   // offset of the element's block row a in Ke
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int jl = lane / BS, r = lane - BS * (lane / BS);
+    const int jl = lane / LPC, r0 = (lane - LPC * (lane / LPC)) * RPL;
     const RowWalk rw = row_walk(AW_WAVES);
     for (int64_t k = rw.k, i; (i = rw.row(k)) < N; k += rw.step) {
         const int lo = rowptr[i], len = rowptr[i + 1] - lo;
@@ -394,12 +399,15 @@ __global__ void __launch_bounds__(256) k_assemble_ke_w(const double* __restrict_
             const bool owner = jl < nj;
             int myj = -1;
             int64_t Ei = 0;
-            double acc[BS];
+            double acc[RPL][BS];
             if (owner) {
                 myj = colidx[lo + j0 + jl];
                 Ei = csr2sell[lo + j0 + jl];
 #pragma unroll
-                for (int c = 0; c < BS; ++c) acc[c] = vals[BS == 1 ? Ei : sell_val(Ei, BS * BS, r * BS + c)];
+                for (int rr = 0; rr < RPL; ++rr)
+#pragma unroll
+                    for (int c = 0; c < BS; ++c)
+                        acc[rr][c] = vals[BS == 1 ? Ei : sell_val(Ei, BS * BS, (r0 + rr) * BS + c)];
             }
             for (int k0 = 0; k0 < C; k0 += 64) {
                 const int nk = min(64, C - k0);
@@ -420,7 +428,7 @@ __global__ void __launch_bounds__(256) k_assemble_ke_w(const double* __restrict_
                 if (owner) {
                     for (int kk = 0; kk < nk; kk += KU) {
                         unsigned m[KU];
-                        double v[KU][BS];
+                        double v[KU][RPL][BS];
 #pragma unroll
                         for (int u = 0; u < KU; ++u) {
                             const int k = min(kk + u, nk - 1);
@@ -428,20 +436,28 @@ __global__ void __launch_bounds__(256) k_assemble_ke_w(const double* __restrict_
 #pragma unroll
                             for (int b = 0; b < NPE; ++b) mm |= (unsigned)(node_s[wid][k * NPE + b] == myj) << b;
                             m[u] = (kk + u < nk) ? mm : 0u;
-                            const double* p = Ke + krow_s[wid][k] + (int64_t)r * D + (m[u] ? __builtin_ctz(m[u]) : 0) * BS;
+                            const double* p =
+                                Ke + krow_s[wid][k] + (int64_t)r0 * D + (m[u] ? __builtin_ctz(m[u]) : 0) * BS;
 #pragma unroll
-                            for (int c = 0; c < BS; ++c) v[u][c] = m[u] ? p[c] : 0.0;
+                            for (int rr = 0; rr < RPL; ++rr)
+#pragma unroll
+                                for (int c = 0; c < BS; ++c) v[u][rr][c] = m[u] ? p[rr * D + c] : 0.0;
                         }
 #pragma unroll
                         for (int u = 0; u < KU; ++u) {
                             if (!m[u]) continue;
 #pragma unroll
-                            for (int c = 0; c < BS; ++c) acc[c] += v[u][c];
+                            for (int rr = 0; rr < RPL; ++rr)
+#pragma unroll
+                                for (int c = 0; c < BS; ++c) acc[rr][c] += v[u][rr][c];
                             unsigned rest = m[u] & (m[u] - 1);
                             while (rest) {   // the same node twice in one element
-                                const double* p = Ke + krow_s[wid][kk + u] + (int64_t)r * D + __builtin_ctz(rest) * BS;
+                                const double* p =
+                                    Ke + krow_s[wid][kk + u] + (int64_t)r0 * D + __builtin_ctz(rest) * BS;
 #pragma unroll
-                                for (int c = 0; c < BS; ++c) acc[c] += p[c];
+                                for (int rr = 0; rr < RPL; ++rr)
+#pragma unroll
+                                    for (int c = 0; c < BS; ++c) acc[rr][c] += p[rr * D + c];
                                 rest &= rest - 1;
                             }
                         }
@@ -450,7 +466,10 @@ __global__ void __launch_bounds__(256) k_assemble_ke_w(const double* __restrict_
             }
             if (owner) {
 #pragma unroll
-                for (int c = 0; c < BS; ++c) vals[BS == 1 ? Ei : sell_val(Ei, BS * BS, r * BS + c)] = acc[c];
+                for (int rr = 0; rr < RPL; ++rr)
+#pragma unroll
+                    for (int c = 0; c < BS; ++c)
+                        vals[BS == 1 ? Ei : sell_val(Ei, BS * BS, (r0 + rr) * BS + c)] = acc[rr][c];
             }
         }
     }
@@ -950,8 +969,8 @@ int fem_assemble_from_ke(const double* Ke, const int64_t* conn, int npe, int bs,
         const dim3 g((unsigned)grid_multiple_of_xcd(cdiv(N, AW_WAVES), 8192));
 #define FEM_KE_W(B, P)                                                                                          \
     if (bs == B && npe == P)                                                                                    \
-        hipLaunchKernelGGL((k_assemble_ke_w<B, P>), g, dim3(256), 0, S(stream), Ke, conn, inc_ptr, inc, N, rowptr, \
-                           colidx, csr2sell, vals);
+        hipLaunchKernelGGL((k_assemble_ke_w<B, P, (B == 3 ? FEM_KE_RPL3 : 1)>), g, dim3(256), 0, S(stream), Ke,  \
+                           conn, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals);
         FEM_KE_W(1, 4) FEM_KE_W(1, 6) FEM_KE_W(1, 8) FEM_KE_W(1, 10)
         FEM_KE_W(3, 4) FEM_KE_W(3, 6) FEM_KE_W(3, 8) FEM_KE_W(3, 10)
 #undef FEM_KE_W
