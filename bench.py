@@ -75,34 +75,6 @@ def traffic_from_profiles(workload_key, kernel, alg):
     return d.get("bytes_per_launch")
 
 
-def stream_ceiling(dev, gib=2.0, reps=5):
-    """Measured HBM ceilings on this box (report the fraction of the measured STREAM ceiling too):
-    16-byte-per-lane read-only sweep and copy over buffers far larger than the 256 MB memory-side cache, best of
-    `reps`, timed with hip events on the stream the probes run on."""
-    lib = C.lib()
-    n = int(gib * (1 << 30) / 8)
-    src = torch.ones(n, dtype=torch.float64, device=dev)
-    dst = torch.empty(n // 2, dtype=torch.float64, device=dev)
-    out = torch.zeros(1, dtype=torch.float64, device=dev)
-    st = torch.cuda.current_stream(dev)
-    res = {}
-    for name, fn, nbytes in (("read", lambda: lib.fem_lab_copy(16, 1, C.ptr(src), C.ptr(out), n, 4096, C.stream(dev)), n * 8),
-                             ("copy", lambda: lib.fem_stream_copy(C.ptr(src), C.ptr(dst), n // 2, 4096, C.stream(dev)), n * 8)):
-        best = None
-        for _ in range(reps + 1):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(st)
-            C.check(fn(), "stream probe")
-            e1.record(st)
-            e1.synchronize()
-            t = e0.elapsed_time(e1) * 1e-3
-            best = t if best is None else min(best, t)
-        res[name] = nbytes / best / 1e9
-    del src, dst
-    torch.cuda.empty_cache()
-    return res
-
-
 def cpu_baseline(n, kind, iters):
     """Oracle (reference op sequence on torch-CPU) on the same mesh: assembly + `iters` EBE-PCG iterations."""
     from oracle import ref_cpu as R
@@ -193,7 +165,7 @@ def main():
     spmv_ms = ms[0] / max(cnt[0], 1)
     alg = A.algorithmic_bytes_spmv()
     achieved = alg / (spmv_ms * 1e-3) / 1e9
-    ceiling = stream_ceiling(dev)
+    ceiling = system.stream_ceiling(dev)
     workload_key = f"kuhn{a.n}_{a.kind}"
     out = {
         "metric": METRIC,

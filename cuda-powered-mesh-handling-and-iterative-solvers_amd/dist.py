@@ -439,6 +439,7 @@ def bench_main(a, metric):
     nI = ds.rm.n_iface
     if rank == 0:
         achieved = alg / (spmv_ms * 1e-3) / 1e9
+        ceiling = _sys.stream_ceiling(dev)   # after the timed region, rank 0's GPU only
         out = {
             "metric": metric, "value": a.steps / dt, "unit": "CG iterations/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "strong",
@@ -460,7 +461,8 @@ def bench_main(a, metric):
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                          "frac": achieved / 8000.0, "traffic": None,
                          "kernel": ("k_cg1_spmv" if variant else "k_pcg_spmv_dot") + " (rank 0 local)",
-                         "algorithmic_bytes": alg},
+                         "algorithmic_bytes": alg, "stream_ceiling_GBps": ceiling,
+                         "frac_of_stream_read": achieved / ceiling["read"]},
             "cpu_baseline": None,
         }
         print(json.dumps(out), flush=True)

@@ -357,3 +357,31 @@ def assemble_tet4_system(coords, elements, kind="poisson", E=1.0, nu=0.0, graph=
     bs = 1 if kind == "poisson" else 3
     A = SellMatrix(g, bs).add_tet4(coords.to(F64).contiguous(), elements.contiguous(), E, nu)
     return A
+
+
+def stream_ceiling(dev, gib=2.0, reps=5):
+    """Measured HBM ceilings on this box (report the fraction of the measured STREAM ceiling too):
+    16-byte-per-lane read-only sweep and copy over buffers far larger than the 256 MB memory-side cache, best of
+    `reps`, timed with hip events on the stream the probes run on."""
+    lib = C.lib()
+    n = int(gib * (1 << 30) / 8)
+    src = torch.ones(n, dtype=torch.float64, device=dev)
+    dst = torch.empty(n // 2, dtype=torch.float64, device=dev)
+    out = torch.zeros(1, dtype=torch.float64, device=dev)
+    st = torch.cuda.current_stream(dev)
+    res = {}
+    for name, fn, nbytes in (("read", lambda: lib.fem_lab_copy(16, 1, C.ptr(src), C.ptr(out), n, 4096, C.stream(dev)), n * 8),
+                             ("copy", lambda: lib.fem_stream_copy(C.ptr(src), C.ptr(dst), n // 2, 4096, C.stream(dev)), n * 8)):
+        best = None
+        for _ in range(reps + 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            C.check(fn(), "stream probe")
+            e1.record(st)
+            e1.synchronize()
+            t = e0.elapsed_time(e1) * 1e-3
+            best = t if best is None else min(best, t)
+        res[name] = nbytes / best / 1e9
+    del src, dst
+    torch.cuda.empty_cache()
+    return res
