@@ -356,10 +356,10 @@ struct RowWalk {
     __device__ __forceinline__ int64_t row(int64_t kk) const { return ((kk >> 6) * NXCD + xcd) * 64 + (kk & 63); }
 };
 
-__device__ __forceinline__ RowWalk row_walk(int waves) {
+__device__ __forceinline__ RowWalk row_walk(int waves, int rows_per_wave = 1, int sub = 0) {
     const int xcd = blockIdx.x % NXCD;
     const int64_t lb = blockIdx.x / NXCD, nlb = gridDim.x / NXCD;
-    return RowWalk{lb * waves + (threadIdx.x >> 6), nlb * waves, xcd};
+    return RowWalk{(lb * waves + (threadIdx.x >> 6)) * rows_per_wave + sub, nlb * waves * rows_per_wave, xcd};
 }
 
 // Wave-per-row version of k_assemble_from_ke. The chunk's element nodes are staged in LDS; each owner lane
@@ -369,6 +369,9 @@ __device__ __forceinline__ RowWalk row_walk(int waves) {
 // thread-per-row kernel (bit-identical). Repeated nodes inside one element (degenerate input) take the exact
 // extra-bit loop.
 constexpr int AW_WAVES = 4;   // waves per 256-thread block of the wave-per-row assembly kernels
+#ifndef FEM_P1_LPR
+#define FEM_P1_LPR 16   // P1 assembly: lanes per row (four rows per wave; 64: 2.95 ms, 32: 1.52, 16: 1.11 on 10M tets)
+#endif
 #ifndef FEM_KE_RPL3
 #define FEM_KE_RPL3 1   // bs = 3 assembly from K_e: block rows per lane (3, one lane per column: c3d8 4.2 -> 5.1 ms)
 #endif
@@ -619,6 +622,9 @@ __global__ void __launch_bounds__(256) k_assemble_tet4w(const double* __restrict
 // bs = 1 (P1 Poisson): each element lane forms its 4 scalar contributions E (g_a . g_b) V itself and finds the 4
 // column slots by binary search in the row's LDS column list; an owner lane per column then adds the (at most one)
 // contribution of every element in ascending incidence order — 2 LDS reads per element instead of ~20.
+// LPR lanes per row (64 or 32): with 32, each half-wave assembles its own row — P1 rows (~15 columns, ~24
+// incident tets) fill half a wave, so two rows' dependent loads are in flight per wave. Chunk loops cover longer rows.
+template <int LPR>
 __global__ void __launch_bounds__(256) k_assemble_p1w(const double* __restrict__ X, const int64_t* __restrict__ conn,
                                                       double kappa, const int32_t* __restrict__ inc_ptr,
                                                       const int32_t* __restrict__ inc, int64_t N,
@@ -626,29 +632,31 @@ __global__ void __launch_bounds__(256) k_assemble_p1w(const double* __restrict__
                                                       const int32_t* __restrict__ colidx,
                                                       const int64_t* __restrict__ csr2sell, double* __restrict__ vals,
                                                       int64_t* __restrict__ bad) {
+    constexpr int RPW = 64 / LPR;
     __shared__ double c_s[AW_WAVES][64][4];
     __shared__ uint32_t pos_s[AW_WAVES][64];    // 4 column slots (bytes), 0xff = outside this column group
     __shared__ int col_s[AW_WAVES][64];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const RowWalk rw = row_walk(AW_WAVES);
+    const int sub = lane / LPR, sl = lane - LPR * sub, base = LPR * sub;
+    const RowWalk rw = row_walk(AW_WAVES, RPW, sub);
     for (int64_t k = rw.k, i; (i = rw.row(k)) < N; k += rw.step) {
         const int lo = rowptr[i], len = rowptr[i + 1] - lo;
         const int t0 = inc_ptr[i], C = inc_ptr[i + 1] - t0;
-        for (int j0 = 0; j0 < len; j0 += 64) {
-            const int nj = min(64, len - j0);
-            if (lane < nj) col_s[wid][lane] = colidx[lo + j0 + lane];
-            const bool owner = lane < nj;
+        for (int j0 = 0; j0 < len; j0 += LPR) {
+            const int nj = min(LPR, len - j0);
+            if (sl < nj) col_s[wid][base + sl] = colidx[lo + j0 + sl];
+            const bool owner = sl < nj;
             int64_t Ei = 0;
             double acc = 0.0;
             if (owner) {
-                Ei = csr2sell[lo + j0 + lane];
+                Ei = csr2sell[lo + j0 + sl];
                 acc = vals[Ei];
             }
-            for (int k0 = 0; k0 < C; k0 += 64) {
-                const int nk = min(64, C - k0);
+            for (int k0 = 0; k0 < C; k0 += LPR) {
+                const int nk = min(LPR, C - k0);
                 __builtin_amdgcn_wave_barrier();
-                if (lane < nk) {
-                    const int ea = inc[t0 + k0 + lane];
+                if (sl < nk) {
+                    const int ea = inc[t0 + k0 + sl];
                     const int64_t e = ea >> 2;
                     const int a = ea & 3;
                     const int64_t* c = conn + 4 * e;
@@ -660,26 +668,26 @@ __global__ void __launch_bounds__(256) k_assemble_p1w(const double* __restrict__
 #pragma unroll
                     for (int b = 0; b < 4; ++b) {
                         const double dot = g[a][0] * g[b][0] + g[a][1] * g[b][1] + g[a][2] * g[b][2];
-                        c_s[wid][lane][b] = kappa * dot * V;
+                        c_s[wid][base + sl][b] = kappa * dot * V;
                         const int j = (int)c[b];
                         int l = 0, h = nj;   // binary search of j among the group's sorted columns
                         while (l < h) {
                             const int m = (l + h) >> 1;
-                            if (col_s[wid][m] < j) l = m + 1;
+                            if (col_s[wid][base + m] < j) l = m + 1;
                             else h = m;
                         }
-                        const uint32_t p = (l < nj && col_s[wid][l] == j) ? (uint32_t)l : 0xffu;
+                        const uint32_t p = (l < nj && col_s[wid][base + l] == j) ? (uint32_t)l : 0xffu;
                         packed |= p << (8 * b);
                     }
-                    pos_s[wid][lane] = packed;
+                    pos_s[wid][base + sl] = packed;
                 }
                 __builtin_amdgcn_wave_barrier();
                 if (owner) {
-                    for (int k = 0; k < nk; ++k) {
-                        const uint32_t pk = pos_s[wid][k];
+                    for (int kk = 0; kk < nk; ++kk) {
+                        const uint32_t pk = pos_s[wid][base + kk];
 #pragma unroll
                         for (int b = 0; b < 4; ++b)
-                            if (((pk >> (8 * b)) & 0xffu) == (uint32_t)lane) acc += c_s[wid][k][b];
+                            if (((pk >> (8 * b)) & 0xffu) == (uint32_t)sl) acc += c_s[wid][base + kk][b];
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
@@ -999,7 +1007,7 @@ int fem_assemble_tet4(const double* coords, const int64_t* conn, double E, doubl
     // version k_assemble_tet4w stay as reference formulations
     const dim3 g((unsigned)grid_multiple_of_xcd(cdiv(N, AW_WAVES), 8192));
     if (bs == 1)
-        hipLaunchKernelGGL(k_assemble_p1w, g, dim3(256), 0, S(stream), coords, conn, E, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals, bad_idx);
+        hipLaunchKernelGGL(k_assemble_p1w<FEM_P1_LPR>, g, dim3(256), 0, S(stream), coords, conn, E, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals, bad_idx);
     else if (bs == 3)
         hipLaunchKernelGGL(k_assemble_el3w, g, dim3(256), 0, S(stream), coords, conn, E, nu, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals, bad_idx);
     else {
