@@ -72,6 +72,9 @@ constexpr int G_TCAP = 32;      // rows of at most this many neighbours are prod
 // and rank-sorted, written to tmp[node * G_TCAP + rank] with row_len[node]. Rows with more than G_SCAP candidates or
 // G_TCAP neighbours get tmp[node * G_TCAP] = -1 and are left to k_graph (count and fill passes skip the rest).
 constexpr int G_HT = 512;
+#ifndef FEM_GRAPH_LPN
+#define FEM_GRAPH_LPN 32   // k_graph_small lanes per node (two rows per wave)
+#endif
 
 // hash table of a row: the smallest power of two >= 2 C slots (at least 128, at most 1 << maxbits), so clearing
 // and compacting it costs ~C, not the table capacity (P1 rows: 96 candidates -> 256 slots instead of 512)
@@ -80,62 +83,74 @@ __device__ __forceinline__ int ht_bits(int C, int maxbits) {
     return b > maxbits ? maxbits : b;
 }
 
+// LPN lanes per node (64 or 32): with 32 each half-wave builds its own row in half the wave's table, so two rows'
+// dependent incidence / connectivity loads are in flight per wave; rows over LPN / 64 * G_SCAP candidates defer.
+template <int LPN>
 __global__ void __launch_bounds__(256) k_graph_small(const int64_t* __restrict__ conn, int npe,
                                                      const int32_t* __restrict__ inc_ptr,
                                                      const int32_t* __restrict__ inc, int64_t N,
                                                      int32_t* __restrict__ row_len, int32_t* __restrict__ tmp,
                                                      uint8_t* __restrict__ defer) {
+    constexpr int NPW = 64 / LPN;                 // nodes per wave
+    constexpr int HTS = G_HT / NPW;               // table slots per node
+    constexpr int SCAP = G_SCAP * LPN / 64;       // candidates per node (load <= 3/4 of the table)
+    constexpr int MAXB = (HTS == 512) ? 9 : (HTS == 256 ? 8 : 7);
     __shared__ int ht[G_WAVES][G_HT];
     __shared__ int uniq[G_WAVES][64];
     const int wid = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
-    const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (int64_t node = (int64_t)blockIdx.x * G_WAVES + wid; node < N; node += (int64_t)gridDim.x * G_WAVES) {
+    const int sub = lane / LPN, sl = lane - LPN * sub, base = LPN * sub;
+    int* const tab = &ht[wid][HTS * sub];
+    int* const uq = &uniq[wid][base];
+    const unsigned long long lt_mask = (sl == 0) ? 0ull : (~0ull >> (64 - sl));
+    const unsigned long long my_bits = (LPN == 64) ? ~0ull : (((1ull << LPN) - 1) << base);
+    for (int64_t node = ((int64_t)blockIdx.x * G_WAVES + wid) * NPW + sub; node < N;
+         node += (int64_t)gridDim.x * G_WAVES * NPW) {
         const int start = inc_ptr[node];
         const int C = (inc_ptr[node + 1] - start) * npe;
         int32_t* trow = tmp + node * G_TCAP;
-        if (C > G_SCAP) {
-            if (lane == 0) defer[node] = 1;
+        if (C > SCAP) {
+            if (sl == 0) defer[node] = 1;
             continue;
         }
-        const int hb = ht_bits(C, 9), HS = 1 << hb;
-        for (int q = lane; q < HS; q += 64) ht[wid][q] = -1;
+        const int hb = ht_bits(C, MAXB), HS = 1 << hb;
+        for (int q = sl; q < HS; q += LPN) tab[q] = -1;
         __builtin_amdgcn_wave_barrier();
-        for (int t = lane; t < C; t += 64) {
+        for (int t = sl; t < C; t += LPN) {
             const int k = t / npe, b = t - k * npe;
             const int e = inc[start + k] / npe;
             const int v = (int)conn[(int64_t)e * npe + b];
             unsigned h = ((unsigned)v * 2654435761u) >> (32 - hb);
             while (true) {
-                const int old = atomicCAS(&ht[wid][h], -1, v);
+                const int old = atomicCAS(&tab[h], -1, v);
                 if (old == -1 || old == v) break;
                 h = (h + 1) & (HS - 1);
             }
         }
         __builtin_amdgcn_wave_barrier();
         int U = 0;
-        for (int q0 = 0; q0 < HS; q0 += 64) {
-            const int v = ht[wid][q0 + lane];
+        for (int q0 = 0; q0 < HS; q0 += LPN) {
+            const int v = tab[q0 + sl];
             const bool has = v >= 0;
-            const unsigned long long m = __ballot(has);
+            const unsigned long long m = (__ballot(has) & my_bits) >> base;
             if (has) {
                 const int pos = U + __popcll(m & lt_mask);
-                if (pos < 64) uniq[wid][pos] = v;
+                if (pos < LPN) uq[pos] = v;
             }
             U += __popcll(m);
         }
         __builtin_amdgcn_wave_barrier();
-        if (U > G_TCAP) {
-            if (lane == 0) defer[node] = 1;
+        if (U > G_TCAP || U > LPN) {
+            if (sl == 0) defer[node] = 1;
             continue;
         }
-        if (lane < U) {
-            const int v = uniq[wid][lane];
+        if (sl < U) {
+            const int v = uq[sl];
             int rank = 0;
-            for (int u = 0; u < U; ++u) rank += (uniq[wid][u] < v);
+            for (int u = 0; u < U; ++u) rank += (uq[u] < v);
             trow[rank] = v;
         }
-        if (lane == 0) {
+        if (sl == 0) {
             row_len[node] = U;
             defer[node] = 0;
         }
@@ -482,7 +497,7 @@ int fem_graph_count2(const int64_t* conn, int npe, const int32_t* inc_ptr, const
                      int32_t* row_len, int32_t* tmp, int32_t* overflow, fem_stream_t stream) {
     if (N <= 0) return FEM_OK;
     const int64_t grid = std::min<int64_t>(cdiv(N, G_WAVES), 16384);
-    hipLaunchKernelGGL(k_graph_small, dim3((unsigned)grid), dim3(256), 0, S(stream), conn, npe, inc_ptr, inc, N,
+    hipLaunchKernelGGL(k_graph_small<FEM_GRAPH_LPN>, dim3((unsigned)grid), dim3(256), 0, S(stream), conn, npe, inc_ptr, inc, N,
                        row_len, tmp, defer_flags(tmp, N));
     FEM_LAUNCHED();
     return graph_count(conn, npe, inc_ptr, inc, N, row_len, defer_flags(tmp, N), overflow, S(stream));
