@@ -113,7 +113,9 @@ def build_graph(elements: torch.Tensor, n_nodes: int, compress: bool = True) -> 
     rowptr = torch.empty(n_nodes + 1, dtype=I32, device=dev)
     work = torch.empty(int(lib.fem_scan_work_len(n_nodes)) + 1, dtype=I32, device=dev)
     C.check(lib.fem_scan_i32(C.ptr(row_len), n_nodes, C.ptr(rowptr), C.ptr(work), st), "fem_scan_i32")
-    nnz = int(rowptr[-1])                                          # the one sync of the pattern build
+    nnz = int(row_len.sum(dtype=I64))                              # the one sync of the pattern build
+    if nnz >= 2**31:   # int32 row pointers / column slots
+        raise ValueError(f"fem355: {nnz} node-graph entries exceed the int32 pattern (split the mesh over GPUs)")
     colidx = torch.empty(nnz, dtype=I32, device=dev)
     diagpos = torch.empty(n_nodes, dtype=I32, device=dev)
     C.check(lib.fem_graph_fill2(C.ptr(elements), npe, C.ptr(inc_ptr), C.ptr(inc), n_nodes, C.ptr(rowptr), C.ptr(tmp),
