@@ -5,13 +5,16 @@
 // inside the iteration: scalars, guards and the stop flag live in a device state word, kernels after a stop
 // are no-ops, and the host polls once per chunk of iterations.
 //
-// Two kernel schedules (same arithmetic, same results up to fp rounding order; 3-kernel is the default):
-//   3-kernel  K1 spmv_dot : q = A p, p.q               -> alpha, guards
+// Kernel schedules (same arithmetic, same results up to fp rounding order):
+//   3-kernel  K1 spmv_dot : q = A p, p.q               -> alpha, guards            (default for bs = 3, dist)
 //             K2 update   : r -= alpha q, z = w r, r.z -> stop test, beta
 //             K3 pupdate  : x += alpha p ; p = z + beta p
 //   fused     K1 spmv_dot : x += alpha' p' ; p = w r + beta p' computed on the fly for every gathered column
 //                           (double-buffered p), q = A p, p.q
 //             K2 update   (as above)                          -> 2 launches and 88 n bytes of vectors per iteration
+//   deferred  d1 / d2 / d3: the 3-kernel work without grid atomics, each kernel re-summing the previous kernel's
+//             per-block partials (default for bs = 1)
+//   distributed single reduction: k_cg1_step / k_cg1_update / k_cg1_spmv, one all-reduce per iteration (N > 1)
 // Grid reductions are deterministic two-level trees (common.hpp reduce_grid).
 #include <rccl/rccl.h>
 #include <stddef.h>
