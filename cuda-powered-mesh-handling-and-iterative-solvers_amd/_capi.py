@@ -91,6 +91,8 @@ SIGNATURES = {
     "fem_lab_copy": (_I, [_I, _I, _P, _P, _L, _I, _P]),
     "fem_lab_sell_pair": (_I, [_L, _P, _P, _P, _P, _P, _P]),
     "fem_lab_spmv16_pair": (_I, [_I, _I, _L, _P, _P, _P, _P, _P, _P]),
+    "fem_lab_sell3_layout": (_I, [_I, _L, _P, _P, _P, _P, _P, _P]),
+    "fem_lab_spmv3": (_I, [_I, _I, _I, _I, _L, _P, _P, _P, _P, _P, _P]),
     "fem_pcg_create": (_I, [_L, _I, _P, _P, _P, _P, _P, _P, _I, _D, _D, _P, _L, _P, ctypes.POINTER(_P)]),
     "fem_pcg_start": (_I, [_P]),
     "fem_pcg_iterate": (_I, [_P, _I]),

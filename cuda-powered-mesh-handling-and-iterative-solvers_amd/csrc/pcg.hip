@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "sell_pair.hpp"
+#include "sell_pair3.hpp"
 
 namespace fem {
 
@@ -136,6 +137,17 @@ __device__ __forceinline__ SliceWalk slice_walk(int64_t nslices) {
 
 constexpr int SPMV_U = 8;   // tools/spmv_tune.py: U=8 beats 4 and 16 on the 10M Poisson matrix (gfx950)
 constexpr int SPMV_UP = 8;  // pairs in flight of the paired layout (tools/spmv_layout.py: 2, 4, 8 within 1 %)
+
+// SpMV row of the 16-byte-value copy of the matrix: bs = 1 lane-paired layout (sell_pair.hpp), bs = 3 plane-paired
+// layout A (sell_pair3.hpp: 4 sixteen-byte + 1 eight-byte value loads per block, nontemporal; tools/spmv3_layout.py:
+// 10M elastic 369 -> 348 us stand-alone). Both keep the plain layout's per-row summation order.
+template <int BS>
+__device__ __forceinline__ void sell_row_paired(int64_t s, int lane, const int64_t* __restrict__ slice_ptr,
+                                                const int16_t* __restrict__ cols, const double* __restrict__ vals,
+                                                const double* __restrict__ x, double out[BS]) {
+    if constexpr (BS == 1) out[0] = sell_row_pair<SPMV_UP>(s, lane, slice_ptr, cols, vals, x);
+    else sell3_row_a<1, SPMV_NT3>(s, lane, slice_ptr, cols, vals, x, out);
+}
 
 template <int BS, int U = SPMV_U, bool NT = false, typename CI = int32_t>
 __global__ void __launch_bounds__(256) k_spmv(int64_t nslices, int64_t nrows, const int64_t* __restrict__ slice_ptr,
@@ -299,7 +311,7 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_spmv_dot(int64_t nslices, int
         for (int64_t s0 = wk.s; s0 < wk.end; s0 += wk.step) {
             const int64_t s = rev ? mirror - s0 : s0;
             double o[BS];
-            if constexpr (PAIR) o[0] = sell_row_pair<SPMV_UP>(s, lane, slice_ptr, cols, vals, p0);
+            if constexpr (PAIR) sell_row_paired<BS>(s, lane, slice_ptr, cols, vals, p0, o);
             else sell_row<BS, SPMV_U, (BS > 1 && SPMV_NT3), decltype(pv), CI>(s, lane, slice_ptr, cols, vals, pv, o);
             const int64_t row = s * 64 + lane;
             if (row < nrows) {
@@ -431,7 +443,7 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_d1(int64_t nslices, int64_t n
     for (int64_t s0 = wk.s; s0 < wk.end; s0 += wk.step) {
         const int64_t s = rev ? mirror - s0 : s0;
         double o[BS];
-        if constexpr (PAIR) o[0] = sell_row_pair<SPMV_UP>(s, lane, slice_ptr, cols, vals, p);
+        if constexpr (PAIR) sell_row_paired<BS>(s, lane, slice_ptr, cols, vals, p, o);
         else sell_row<BS, SPMV_U, (BS > 1 && SPMV_NT3), decltype(pv), CI>(s, lane, slice_ptr, cols, vals, pv, o);
         const int64_t row = s * 64 + lane;
         if (row < nrows) {
@@ -862,7 +874,7 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_spmv(int64_t nslices, int64_t
     for (int64_t s0 = wk.s; s0 < wk.end; s0 += wk.step) {
         const int64_t s = rev ? mirror - s0 : s0;
         double o[BS];
-        if constexpr (PAIR) o[0] = sell_row_pair<SPMV_UP>(s, lane, slice_ptr, cols, vals, u);
+        if constexpr (PAIR) sell_row_paired<BS>(s, lane, slice_ptr, cols, vals, u, o);
         else sell_row<BS, SPMV_U, (BS > 1 && SPMV_NT3), decltype(uv), CI>(s, lane, slice_ptr, cols, vals, uv, o);
         const int64_t row = s * 64 + lane;
         if (row < nrows) {
@@ -1057,6 +1069,9 @@ struct fem_pcg {
         }                                                                                      \
     } while (0)
 
+// columns of the paired matrix copy: bs = 1 pairs its columns, bs = 3 (layout A) keeps cols16
+static const int16_t* pcols(const fem_pcg* s) { return s->bs == 1 ? s->pcols16 : s->cols16; }
+
 static double* st_red(fem_pcg* s, int k) {
     return reinterpret_cast<double*>(reinterpret_cast<char*>(s->st) + offsetof(PcgState, red)) + k;
 }
@@ -1067,10 +1082,15 @@ static int launch_spmv_dot(fem_pcg* s) {
     hipLaunchKernelGGL((k_pcg_spmv_dot<B, F, D, int16_t>), dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream,     \
                        s->nslices, s->nrows, s->slice_ptr, s->cols16, s->vals, s->p0, s->p1, s->r, s->w, s->x, s->q, \
                        s->st, s->red, s->tune & FEM_TUNE_REVERSE)
-        if (s->paired && !s->fused) {   // bs = 1, lane-paired copy of the matrix (sell_pair.hpp)
-            hipLaunchKernelGGL((k_pcg_spmv_dot<1, false, true, int16_t, true>), dim3(s->grid_spmv), dim3(PCG_BLOCK), 0,
-                               s->stream, s->nslices, s->nrows, s->slice_ptr, s->pcols16, s->pvals, s->p0, s->p1, s->r,
-                               s->w, s->x, s->q, s->st, s->red, s->tune & FEM_TUNE_REVERSE);
+        if (s->paired && !s->fused) {   // 16-byte-value copy of the matrix (sell_pair.hpp / sell_pair3.hpp)
+            if (s->bs == 1)
+                hipLaunchKernelGGL((k_pcg_spmv_dot<1, false, true, int16_t, true>), dim3(s->grid_spmv), dim3(PCG_BLOCK),
+                                   0, s->stream, s->nslices, s->nrows, s->slice_ptr, pcols(s), s->pvals, s->p0, s->p1,
+                                   s->r, s->w, s->x, s->q, s->st, s->red, s->tune & FEM_TUNE_REVERSE);
+            else
+                hipLaunchKernelGGL((k_pcg_spmv_dot<3, false, true, int16_t, true>), dim3(s->grid_spmv), dim3(PCG_BLOCK),
+                                   0, s->stream, s->nslices, s->nrows, s->slice_ptr, pcols(s), s->pvals, s->p0, s->p1,
+                                   s->r, s->w, s->x, s->q, s->st, s->red, s->tune & FEM_TUNE_REVERSE);
         } else if (s->dist) {
             if (s->bs == 1) FEM_K1D(1, false, true);
             else FEM_K1D(3, false, true);
@@ -1136,7 +1156,8 @@ static int cg1_spmv(fem_pcg* s, int always) {
     hipLaunchKernelGGL((k_cg1_spmv<B, CI, PR>), dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream, s->nslices,     \
                        s->nrows, s->slice_ptr, C, V, s->cg1_u, s->q, ipos, s->cg1_send, off, s->st, s->red, always, \
                        s->tune & FEM_TUNE_REVERSE)
-    if (s->paired) FEM_CG1(1, int16_t, true, s->pcols16, s->pvals);
+    if (s->paired && s->bs == 1) FEM_CG1(1, int16_t, true, pcols(s), s->pvals);
+    else if (s->paired) FEM_CG1(3, int16_t, true, pcols(s), s->pvals);
     else if (s->cols16 && s->bs == 1) FEM_CG1(1, int16_t, false, s->cols16, s->vals);
     else if (s->cols16) FEM_CG1(3, int16_t, false, s->cols16, s->vals);
     else if (s->bs == 1) FEM_CG1(1, int32_t, false, s->cols, s->vals);
@@ -1320,9 +1341,13 @@ static int launch_deferred(fem_pcg* s, int which) {
     const int par = (int)(s->launched & 1);
     const int rev = (s->tune & FEM_TUNE_REVERSE) ? par : 0;
     if (which == 0) {
-        if (s->paired) {
+        if (s->paired && s->bs == 1) {
             hipLaunchKernelGGL((k_pcg_d1<1, int16_t, true>), dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream,
-                               s->nslices, s->nrows, s->slice_ptr, s->pcols16, s->pvals, s->p0, s->q, s->st, par, rev,
+                               s->nslices, s->nrows, s->slice_ptr, pcols(s), s->pvals, s->p0, s->q, s->st, par, rev,
+                               s->red.partials);
+        } else if (s->paired) {
+            hipLaunchKernelGGL((k_pcg_d1<3, int16_t, true>), dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream,
+                               s->nslices, s->nrows, s->slice_ptr, pcols(s), s->pvals, s->p0, s->q, s->st, par, rev,
                                s->red.partials);
         } else if (s->cols16) {
             if (s->bs == 1)
@@ -1677,14 +1702,24 @@ static PcgState state_view(const fem_pcg* s) {
     return h;
 }
 
-// (re)build the lane-paired matrix copy used by the bs = 1 SpMV when FEM_TUNE_PAIR is set
+// (re)build the 16-byte-value matrix copy used by the SpMV when FEM_TUNE_PAIR is set: bs = 1 lane-paired values and
+// columns (sell_pair.hpp), bs = 3 plane-paired values (sell_pair3.hpp layout A; columns stay cols16)
 static int refresh_pairing(fem_pcg* s) {
-    const bool want = s->bs == 1 && s->cols16 && (s->tune & FEM_TUNE_PAIR) && !s->fused;
+    const bool want = (s->bs == 1 || s->bs == 3) && s->cols16 && (s->tune & FEM_TUNE_PAIR) && !s->fused;
     s->paired = 0;
     if (!want || s->nslices == 0) return FEM_OK;
     int64_t ent = 0;
     FEM_HIP(hipMemcpyAsync(&ent, s->slice_ptr + s->nslices, sizeof(int64_t), hipMemcpyDeviceToHost, s->stream));
     FEM_HIP(hipStreamSynchronize(s->stream));
+    if (s->bs == 3) {
+        if (!s->pvals) FEM_HIP(hipMalloc(&s->pvals, sizeof(double) * 9 * (size_t)ent));
+        s->pcols16 = nullptr;
+        hipLaunchKernelGGL(k_sell3_to_a, dim3(stream_grid(s->nslices * 64, 256)), dim3(256), 0, s->stream, s->nslices,
+                           s->slice_ptr, s->vals, s->pvals);
+        FEM_LAUNCHED();
+        s->paired = 1;
+        return FEM_OK;
+    }
     if (!s->pvals) {
         FEM_HIP(hipMalloc(&s->pvals, sizeof(double) * (size_t)ent));
         FEM_HIP(hipMalloc(&s->pcols16, sizeof(int16_t) * (size_t)ent));

@@ -6,6 +6,7 @@
 //   p0 + (k/2)*128 + 2*l + (k%2), the odd tail entry (w odd) at p0 + (w/2)*128 + l;
 // same for the 16-bit column deltas. Footprint and slice_ptr are unchanged.
 #include "sell_pair.hpp"
+#include "sell_pair3.hpp"
 
 namespace fem {
 
@@ -63,6 +64,32 @@ __global__ void __launch_bounds__(256) k_spmv16_pair(int64_t nslices, int64_t nr
     }
 }
 
+// bs = 3 layout probes (sell_pair3.hpp): L = 0 plain, 1 plane-paired (A), 2 entry-paired (B)
+template <int L, int U, bool NT>
+__global__ void __launch_bounds__(256) k_spmv3_lab(int64_t nslices, int64_t nrows,
+                                                   const int64_t* __restrict__ slice_ptr,
+                                                   const int16_t* __restrict__ cols, const double* __restrict__ vals,
+                                                   const double* __restrict__ x, double* __restrict__ y) {
+    const int lane = threadIdx.x & 63;
+    const int xcd = blockIdx.x % NXCD;
+    const int64_t lb = blockIdx.x / NXCD, nlb = gridDim.x / NXCD;
+    const int64_t spx = (nslices + NXCD - 1) / NXCD;
+    const int64_t end = min((int64_t)(xcd + 1) * spx, nslices);
+    for (int64_t s = (int64_t)xcd * spx + lb * 4 + (threadIdx.x >> 6); s < end; s += nlb * 4) {
+        double o[3];
+        if constexpr (L == 0) sell3_row_plain<U, NT>(s, lane, slice_ptr, cols, vals, x, o);
+        else if constexpr (L == 1) sell3_row_a<U, NT>(s, lane, slice_ptr, cols, vals, x, o);
+        else if constexpr (L == 3) sell3_row_a<U, NT, 1>(s, lane, slice_ptr, cols, vals, x, o);
+        else sell3_row_b<U, NT>(s, lane, slice_ptr, cols, vals, x, o);
+        const int64_t row = s * 64 + lane;
+        if (row < nrows) {
+            y[3 * row] = o[0];
+            y[3 * row + 1] = o[1];
+            y[3 * row + 2] = o[2];
+        }
+    }
+}
+
 }  // namespace fem
 
 using namespace fem;
@@ -106,6 +133,43 @@ int fem_lab_spmv16_pair(int u, int grid, int64_t nrows, const int64_t* slice_ptr
     if (u == 2) hipLaunchKernelGGL(k_spmv16_pair<2>, dim3(grid), dim3(256), 0, st, ns, nrows, slice_ptr, dcols, vals, x, y);
     else if (u == 8) hipLaunchKernelGGL(k_spmv16_pair<8>, dim3(grid), dim3(256), 0, st, ns, nrows, slice_ptr, dcols, vals, x, y);
     else hipLaunchKernelGGL(k_spmv16_pair<4>, dim3(grid), dim3(256), 0, st, ns, nrows, slice_ptr, dcols, vals, x, y);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_lab_sell3_layout(int layout, int64_t nrows, const int64_t* slice_ptr, const double* vals,
+                         const int16_t* dcols, double* vals_out, int16_t* dcols_out, fem_stream_t stream) {
+    const int64_t ns = cdiv(nrows, 64);
+    if (ns == 0) return FEM_OK;
+    const int g = stream_grid(ns * 64, 256);
+    if (layout == 1) hipLaunchKernelGGL(k_sell3_to_a, dim3(g), dim3(256), 0, S(stream), ns, slice_ptr, vals, vals_out);
+    else hipLaunchKernelGGL(k_sell3_to_b, dim3(g), dim3(256), 0, S(stream), ns, slice_ptr, vals, dcols, vals_out, dcols_out);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_lab_spmv3(int layout, int u, int nt, int grid, int64_t nrows, const int64_t* slice_ptr, const int16_t* dcols,
+                  const double* vals, const double* x, double* y, fem_stream_t stream) {
+    const int64_t ns = cdiv(nrows, 64);
+    if (ns == 0) return FEM_OK;
+    if (grid <= 0) grid = grid_multiple_of_xcd(cdiv(ns, 4), 2048);
+    grid = ((grid + NXCD - 1) / NXCD) * NXCD;
+    const hipStream_t st = S(stream);
+#define L3(LL, UU, NN) \
+    hipLaunchKernelGGL((k_spmv3_lab<LL, UU, NN>), dim3(grid), dim3(256), 0, st, ns, nrows, slice_ptr, dcols, vals, x, y)
+#define L3U(LL, NN)              \
+    if (u == 2) L3(LL, 2, NN);   \
+    else L3(LL, 1, NN);
+#define L3N(LL)              \
+    if (nt) { L3U(LL, true) } \
+    else { L3U(LL, false) }
+    if (layout == 0) { L3N(0) }
+    else if (layout == 1) { L3N(1) }
+    else if (layout == 3) { L3N(3) }
+    else { L3N(2) }
+#undef L3N
+#undef L3U
+#undef L3
     FEM_LAUNCHED();
     return FEM_OK;
 }

@@ -306,6 +306,11 @@ int fem_lab_sell_pair(int64_t nrows, const int64_t* slice_ptr, const double* val
                       double* vals_out, int16_t* dcols_out, fem_stream_t stream);
 int fem_lab_spmv16_pair(int u, int grid, int64_t nrows, const int64_t* slice_ptr, const int16_t* dcols,
                         const double* vals, const double* x, double* y, fem_stream_t stream);
+// bs = 3 layout probes (sell_pair3.hpp): layout 1 plane-paired values, 2 entry-paired values + int32 column pairs
+int fem_lab_sell3_layout(int layout, int64_t nrows, const int64_t* slice_ptr, const double* vals,
+                         const int16_t* dcols, double* vals_out, int16_t* dcols_out, fem_stream_t stream);
+int fem_lab_spmv3(int layout, int u, int nt, int grid, int64_t nrows, const int64_t* slice_ptr, const int16_t* dcols,
+                  const double* vals, const double* x, double* y, fem_stream_t stream);
 
 /* ------------------------------------------------------------------ (P)CG (L3)
  * One solve context over a SELL matrix. The whole iteration runs on the device: SpMV + p.q reduction,
@@ -361,9 +366,10 @@ int fem_enforce_constraints(double* x, double* r, int64_t n, int order, int64_t 
  * the next sweep: 67 -> 57 us per SpMV on the 10M Poisson matrix. Results depend on the flags only through the
  * order of the per-block p.q partials (deterministic for a given flag set). */
 enum { FEM_TUNE_REVERSE = 1, FEM_TUNE_PAIR = 2 };
-/* FEM_TUNE_PAIR (default): bs = 1 contexts with 16-bit columns keep a lane-paired copy of the matrix (two entries per
- * 16-byte value load, sell_pair.hpp; +257 MB on the 10M Poisson matrix), rebuilt from vals / cols16 by every
- * fem_pcg_start. Same products, same summation order per row as the plain layout. */
+/* FEM_TUNE_PAIR (default): contexts with 16-bit columns keep a copy of the matrix read with 16-byte value loads,
+ * rebuilt from vals / cols16 by every fem_pcg_start: bs = 1 lane-paired (two entries per load, sell_pair.hpp; +257 MB
+ * on the 10M Poisson matrix), bs = 3 plane-paired (values 0..7 of a block as four 16-byte loads, sell_pair3.hpp
+ * layout A; +1.85 GB on the 10M elasticity matrix). Same products, same summation order per row as the plain layout. */
 int fem_pcg_set_tuning(fem_pcg* s, int flags);
 /* run the SpMV of this context on 16-bit column deltas (NULL: back to the int32 columns) */
 int fem_pcg_set_cols16(fem_pcg* s, const int16_t* dcols);

@@ -369,3 +369,27 @@ def test_assembly_from_element_matrices_wide_rows(gpu, etype, n):
         x = torch.randn(N * bs, dtype=F64, generator=torch.Generator().manual_seed(3))
         y_ref = R.nodal_forces(Kb.cpu(), t, x.view(N, bs)).reshape(-1)
         assert rel(A.matvec(x.to(gpu)), y_ref) < 1e-12, (etype, bs)
+
+
+@pytest.mark.parametrize("kind", ["poisson", "elastic"])
+def test_paired_matrix_copy_is_bit_identical(gpu, kind):
+    """FEM_TUNE_PAIR (16-byte-value copy: bs = 1 lane-paired, bs = 3 plane-paired layout A) keeps every row's
+    summation order, so fixed-iteration PCG iterates equal the plain layout's bit for bit, in every schedule."""
+    _, mesh, _, system = _mods()
+    c, t = mesh.kuhn_cube(9, jitter=0.1)
+    A = system.assemble_tet4_system(c.to(gpu), t.to(gpu), kind, 1.0 if kind == "poisson" else E, NU)
+    assert A.use16
+    b = torch.randn(A.n, dtype=F64, device=gpu)
+    w = A.jacobi(None)
+    for sched in (0, 2):
+        xs = []
+        for flags in (1, 3):   # FEM_TUNE_REVERSE, FEM_TUNE_REVERSE | FEM_TUNE_PAIR
+            run = system.PcgRunner(A, b, w, tol=0.0, schedule=sched)
+            run.set_tuning(flags)
+            run.start()
+            run.iterate(30)
+            it, _, _ = run.poll()
+            assert it == 30
+            xs.append(run.x.clone())
+            run.close()
+        assert torch.equal(xs[0], xs[1]), (kind, sched)
