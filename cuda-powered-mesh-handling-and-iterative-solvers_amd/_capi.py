@@ -17,7 +17,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FEM355_LIB", os.path.join(PKG_DIR, "lib", "libfem355.so"))
 
 FEM_OK, FEM_EBADTYPE, FEM_ESINGULAR, FEM_EHIP, FEM_ERCCL, FEM_EARG = range(6)
-PCG_RUNNING, PCG_CONVERGED, PCG_MAXITER, PCG_BREAKDOWN, PCG_ALPHA_NAN, PCG_BETA_NAN = range(6)
+PCG_RUNNING, PCG_CONVERGED, PCG_MAXITER, PCG_BREAKDOWN, PCG_ALPHA_NAN, PCG_BETA_NAN, PCG_SYNC_TIMEOUT = range(7)
 MODE_CG_STABLE, MODE_PCG, MODE_CG_CONSTRAINED = 0, 1, 2
 KIND_ELASTIC, KIND_POISSON, KIND_MASS = 0, 1, 2
 ISO_SUM, ISO_STACK, ISO_VOLUME = 0, 1, 2
@@ -92,6 +92,7 @@ SIGNATURES = {
     "fem_lab_sell_pair": (_I, [_L, _P, _P, _P, _P, _P, _P]),
     "fem_lab_spmv16_pair": (_I, [_I, _I, _L, _P, _P, _P, _P, _P, _P]),
     "fem_lab_sell3_layout": (_I, [_I, _L, _P, _P, _P, _P, _P, _P]),
+    "fem_lab_spmv_persist": (_I, [_I, _I, _I, _L, _L, _P, _P, _P, _P, _P, _P]),
     "fem_lab_spmv3": (_I, [_I, _I, _I, _I, _L, _P, _P, _P, _P, _P, _P]),
     "fem_pcg_create": (_I, [_L, _I, _P, _P, _P, _P, _P, _P, _I, _D, _D, _P, _L, _P, ctypes.POINTER(_P)]),
     "fem_pcg_start": (_I, [_P]),
@@ -100,6 +101,8 @@ SIGNATURES = {
     "fem_pcg_solve": (_I, [_P, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_D)]),
     "fem_pcg_use_graph": (_I, [_P, _I]),
     "fem_pcg_set_schedule": (_I, [_P, _I]),
+    "fem_pcg_get_schedule": (_I, [_P]),
+    "fem_pcg_persist_profile": (_I, [_P, _I, _P, ctypes.POINTER(_I)]),
     "fem_pcg_set_constraints": (_I, [_P, _I, _L, _P, _P, _L, _P, _P, _L, _P, _P, _P, _P, _P]),
     "fem_enforce_constraints": (_I, [_P, _P, _L, _I, _L, _P, _P, _L, _P, _P, _L, _P, _P, _P, _P, _P, _P]),
     "fem_pcg_finish": (_I, [_P]),

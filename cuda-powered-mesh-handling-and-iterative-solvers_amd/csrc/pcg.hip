@@ -896,6 +896,10 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_spmv(int64_t nslices, int64_t
     }
 }
 
+}  // namespace fem
+#include "pcg_persist.hpp"
+namespace fem {
+
 // ---------------------------------------------------------------- constraint projections (CG_CONSTRAINED)
 // `enforce_constraints` (`solver/solver.py:478-510`: RBE2 then SPC) and `new_enforce_constraints` (`:665-700`:
 // SPC, RBE2, then RBE3 sets in order) on the displacement after every update; the r-zeroing of SPC dofs and RBE2
@@ -1058,6 +1062,14 @@ struct fem_pcg {
     double* cg1_u;
     double* cg1_send;
     double* cg1_recv;
+    // persistent schedule (3): requested by fem_pcg_set_schedule, active after fem_pcg_start when supported
+    int persist_req;
+    int persist;
+    int pk_grid;          // workgroups (one per CU, multiple of 8)
+    int pk_win_ok;        // gather windows computed for this matrix
+    int32_t* pk_win;      // [2 G]: first workgroups, then last workgroups of the gather windows
+    double* pk_part;      // [2][2][G]
+    unsigned* pk_sync;    // (18 + G) lines, zeroed before every launch
 };
 
 #define FEM_NCCL(call)                                                                         \
@@ -1374,11 +1386,14 @@ static int launch_deferred(fem_pcg* s, int which) {
     return FEM_OK;
 }
 
+static int launch_persist(fem_pcg* s, int k, unsigned long long* prof = nullptr);
+
 static int launch_iterations(fem_pcg* s, int k) {
     if (s->dist && !s->comm) {
         set_error("distributed PCG without a communicator: drive it with fem_pcg_dist_phase");
         return FEM_EARG;
     }
+    if (s->persist) return launch_persist(s, k);
     if (s->deferred && !s->dist) {
         for (int i = 0; i < k; ++i) {
             int rc;
@@ -1667,7 +1682,7 @@ int fem_pcg_set_schedule(fem_pcg* s, int sched) {
         set_error("fem_pcg_set_schedule: drop the captured graph first (fem_pcg_use_graph(s, 0))");
         return FEM_EARG;
     }
-    if (sched < 0 || sched > 2) {
+    if (sched < 0 || sched > 3) {
         set_error("fem_pcg_set_schedule: unknown schedule %d", sched);
         return FEM_EARG;
     }
@@ -1680,14 +1695,127 @@ int fem_pcg_set_schedule(fem_pcg* s, int sched) {
         return FEM_EARG;
     }
     s->fused = sched == 1;
-    s->deferred = sched == 2;
+    s->deferred = sched == 2 || sched == 3;   // 3 falls back to the deferred schedule when unsupported
+    s->persist_req = sched == 3;
+    s->persist = 0;
+    return FEM_OK;
+}
+
+int fem_pcg_persist_profile(fem_pcg* s, int k, unsigned long long* host_out, int* grid) {
+    if (!s->persist || k <= 0) {
+        set_error("fem_pcg_persist_profile: the context does not run the persistent schedule (start it first)");
+        return FEM_EARG;
+    }
+    const size_t nb = sizeof(unsigned long long) * (size_t)s->pk_grid * PK_NPROF;
+    unsigned long long* d = nullptr;
+    FEM_HIP(hipMalloc(&d, nb));
+    FEM_HIP(hipMemsetAsync(d, 0, nb, s->stream));
+    int rc = launch_persist(s, k, d);
+    if (!rc) {
+        const hipError_t e1 = hipMemcpyAsync(host_out, d, nb, hipMemcpyDeviceToHost, s->stream);
+        const hipError_t e2 = hipStreamSynchronize(s->stream);
+        if (e1 != hipSuccess || e2 != hipSuccess) {
+            set_error("fem_pcg_persist_profile: %s", hipGetErrorString(e1 != hipSuccess ? e1 : e2));
+            rc = FEM_EHIP;
+        }
+    }
+    (void)hipFree(d);
+    if (grid) *grid = s->pk_grid;
+    return rc;
+}
+
+int fem_pcg_get_schedule(fem_pcg* s) {
+    if (s->persist) return 3;
+    if (s->fused) return 1;
+    return s->deferred ? 2 : 0;
+}
+
+static size_t pk_sync_words(int G) { return (size_t)(18 + G) * PK_LINE; }
+
+// schedule 3 prerequisites: bs = 1, 16-bit columns + lane-paired copy, single GPU, no projections, capacity
+// (every wave <= PK_MAXS slices), one resident PK_T-thread workgroup per CU
+static int persist_setup(fem_pcg* s) {
+    s->persist = 0;
+    if (!s->persist_req) return FEM_OK;
+    if (s->bs != 1 || !s->paired || s->dist || s->mode == FEM_MODE_CG_CONSTRAINED || s->nslices == 0) return FEM_OK;
+    int dev = 0, ncu = 0;
+    FEM_HIP(hipGetDevice(&dev));
+    FEM_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    const int G = (ncu / NXCD) * NXCD;
+    if (G < NXCD || s->nslices > (int64_t)G * PK_WAVES * PK_MAXS) return FEM_OK;
+    int nb = 0, nbp = 0;
+    for (const void* f : {(const void*)k_pcg_persist<PK_MAXS, false>, (const void*)k_pcg_persist<PK_MAXS, true>})
+        FEM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)PK_LDS));
+    FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pcg_persist<PK_MAXS, false>, PK_T, PK_LDS));
+    FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nbp, k_pcg_persist<PK_MAXS, true>, PK_T, PK_LDS));
+    if (nb < 1 || nbp < 1) return FEM_OK;
+    if (s->pk_grid != G) {
+        if (s->pk_win) (void)hipFree(s->pk_win);
+        if (s->pk_part) (void)hipFree(s->pk_part);
+        if (s->pk_sync) (void)hipFree(s->pk_sync);
+        s->pk_win = nullptr;
+        s->pk_part = nullptr;
+        s->pk_sync = nullptr;
+        FEM_HIP(hipMalloc(&s->pk_win, sizeof(int32_t) * 2 * G));
+        FEM_HIP(hipMalloc(&s->pk_part, sizeof(double) * 4 * G));
+        FEM_HIP(hipMalloc(&s->pk_sync, sizeof(unsigned) * pk_sync_words(G)));
+        s->pk_grid = G;
+        s->pk_win_ok = 0;
+    }
+    if (!s->pk_win_ok) {   // [lo | hi] per logical workgroup, from the matrix columns
+        std::vector<int32_t> lohi(2 * (size_t)G);
+        for (int i = 0; i < G; ++i) {
+            lohi[i] = G;
+            lohi[G + i] = -1;
+        }
+        FEM_HIP(hipMemcpyAsync(s->pk_win, lohi.data(), sizeof(int32_t) * 2 * G, hipMemcpyHostToDevice, s->stream));
+        hipLaunchKernelGGL(k_pk_window, dim3(stream_grid(s->nslices * 64, 256)), dim3(256), 0, s->stream, s->nslices,
+                           s->nrows, s->slice_ptr, s->cols16, G, s->pk_win, s->pk_win + G);
+        FEM_LAUNCHED();
+        FEM_HIP(hipStreamSynchronize(s->stream));   // lohi must outlive the copy
+        s->pk_win_ok = 1;
+    }
+    s->persist = 1;
+    return FEM_OK;
+}
+
+// one persistent launch of k iterations (schedule 3); prof (device, [G][PK_NPROF]) selects the instrumented build
+static int launch_persist(fem_pcg* s, int k, unsigned long long* prof) {
+    const int G = s->pk_grid;
+    FEM_HIP(hipMemsetAsync(s->pk_sync, 0, sizeof(unsigned) * pk_sync_words(G), s->stream));
+    PkArgs a;
+    a.nslices = s->nslices;
+    a.nrows = s->nrows;
+    a.slice_ptr = s->slice_ptr;
+    a.cols = s->pcols16;
+    a.vals = s->pvals;
+    a.x = s->x;
+    a.r = s->r;
+    a.p = s->p0;
+    a.s = s->p1;
+    a.u = s->q;
+    a.w = s->w;
+    a.win = s->pk_win;
+    a.part = s->pk_part;
+    a.sync = s->pk_sync;
+    a.st = s->st;
+    a.hist = s->hist;
+    a.hist_len = s->hist_len;
+    a.kmax = k;
+    a.rev = (s->tune & FEM_TUNE_REVERSE) ? 1 : 0;
+    a.prof = prof;
+    void* args[] = {&a};
+    const void* fn = prof ? (const void*)k_pcg_persist<PK_MAXS, true> : (const void*)k_pcg_persist<PK_MAXS, false>;
+    FEM_HIP(hipLaunchCooperativeKernel(fn, dim3(G), dim3(PK_T), args, PK_LDS, s->stream));
+    FEM_LAUNCHED();
+    s->launched += k;
     return FEM_OK;
 }
 
 // host view of the state: the deferred schedule keeps it in the bank of the current launch parity
 static PcgState state_view(const fem_pcg* s) {
     PcgState h = *s->st_host;
-    if (s->deferred && !s->dist) {
+    if (s->deferred && !s->dist && !s->persist) {
         const PcgState::Bank& b = h.bank[s->launched & 1];
         h.iter = b.iter;
         h.status = b.status;
@@ -1733,7 +1861,8 @@ static int refresh_pairing(fem_pcg* s) {
 
 int fem_pcg_start(fem_pcg* s) {
     {
-        const int prc = refresh_pairing(s);
+        int prc = refresh_pairing(s);
+        if (!prc) prc = persist_setup(s);
         if (prc) return prc;
     }
     PcgState h{};
@@ -1765,6 +1894,13 @@ int fem_pcg_start(fem_pcg* s) {
     }
     if ((rc = (s->cols16 ? fem_spmv16(s->nrows, s->bs, s->slice_ptr, s->cols16, s->vals, s->x, s->q, s->stream)
                           : fem_spmv(s->nrows, s->bs, s->slice_ptr, s->cols, s->vals, s->x, s->q, s->stream)))) return rc;
+    if (s->persist) {   // single-reduction start: r0 = b - A x0, u0 = w r0 (in q), p = s = 0, g0 -> red[1]
+        hipLaunchKernelGGL(k_cg1_init, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->bs, s->b, s->r,
+                           s->q, s->w, s->p0, s->p1, s->q, (const uint8_t*)nullptr, s->st, s->red);
+        FEM_LAUNCHED();
+        s->launched = 0;
+        return FEM_OK;
+    }
     hipLaunchKernelGGL(k_pcg_init, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->b, s->r, s->q, s->w, s->p0,
                        s->p1, s->fused, s->st, s->red, (const uint8_t*)nullptr, s->bs);
     FEM_LAUNCHED();
@@ -1908,7 +2044,7 @@ int fem_pcg_iterate(fem_pcg* s, int k) {
     if (k <= 0) return FEM_OK;
     // the deferred schedule's graph was captured from bank parity 0 over an even number of iterations
     const bool parity_ok = !s->deferred || ((s->launched & 1) == 0 && (s->graph_k & 1) == 0);
-    if (s->graph && s->graph_k > 0 && k % s->graph_k == 0 && parity_ok) {
+    if (s->graph && s->graph_k > 0 && k % s->graph_k == 0 && parity_ok && !s->persist) {
         for (int i = 0; i < k / s->graph_k; ++i) FEM_HIP(hipGraphLaunch(s->graph, s->stream));
         s->launched += k;
         return FEM_OK;
@@ -1931,7 +2067,7 @@ int fem_pcg_use_graph(fem_pcg* s, int k) {
         s->graph = nullptr;
         s->graph_k = 0;
     }
-    if (k <= 0) return FEM_OK;
+    if (k <= 0 || s->persist) return FEM_OK;   // the persistent schedule is one launch per chunk already
     hipGraph_t g;
     const int64_t saved = s->launched;
     s->launched = 0;
@@ -2014,6 +2150,27 @@ int fem_pcg_profile(fem_pcg* s, int k, int every, double* ms, int* n) {
     std::vector<hipEvent_t> evs((size_t)ns * 4);
     for (auto& e : evs) FEM_HIP(hipEventCreate(&e));
     int si = 0;
+    if (s->persist) {   // bucket 0: persistent launches of `every` iterations (per-iteration time = ms / n)
+        for (int i = 0; i < k && !rc; i += every) {
+            const int kk = every < k - i ? every : k - i;
+            (void)hipEventRecord(evs[4 * si + 0], s->stream);
+            rc = launch_persist(s, kk);
+            (void)hipEventRecord(evs[4 * si + 1], s->stream);
+            ++si;
+        }
+        FEM_HIP(hipStreamSynchronize(s->stream));
+        int iters = 0;
+        for (int i = 0; i < si; ++i) {
+            float t;
+            (void)hipEventElapsedTime(&t, evs[4 * i + 0], evs[4 * i + 1]);
+            acc[0] += t;
+        }
+        iters = k;
+        for (auto& e : evs) (void)hipEventDestroy(e);
+        if (ms) ms[0] = acc[0], ms[1] = 0.0, ms[2] = 0.0;
+        if (n) n[0] = iters, n[1] = 0, n[2] = 0;
+        return rc;
+    }
     for (int i = 0; i < k && !rc; ++i) {
         if (i % every) {
             rc = launch_iterations(s, 1);
@@ -2077,6 +2234,9 @@ void fem_pcg_destroy(fem_pcg* s) {
     if (s->con.tmp) (void)hipFree(s->con.tmp);
     if (s->pvals) (void)hipFree(s->pvals);
     if (s->pcols16) (void)hipFree(s->pcols16);
+    if (s->pk_win) (void)hipFree(s->pk_win);
+    if (s->pk_part) (void)hipFree(s->pk_part);
+    if (s->pk_sync) (void)hipFree(s->pk_sync);
     if (s->st) (void)hipFree(s->st);
     if (s->st_host) (void)hipHostFree(s->st_host);
     delete s;

@@ -1,0 +1,473 @@
+// Persistent register-resident Jacobi-PCG (schedule 3, bs = 1 with the lane-paired matrix copy).
+//
+// The single-reduction (Chronopoulos–Gear) form of k_cg1_* run as ONE launch per chunk of iterations: every wave
+// owns a fixed contiguous range of at most PK_MAXS slices for the whole launch and keeps its rows' CG state on the
+// chip — r, p, s = A p, v = A u and its own u in registers, x and w in LDS — so an iteration moves the matrix once,
+// gathers u, and writes u: (8 + 2) nnz + 16 n bytes instead of the deferred schedule's (8 + 2) nnz + 96 n.
+//
+//   per iteration (epoch e = local iteration + 1):
+//     wait   : one wave polls the u-flags of the workgroups whose rows this workgroup's columns reach
+//              (gather window, computed once per matrix), then ONE agent acquire (L1) for the workgroup
+//     SpMV   : v = A u over the own slices (paired layout, plain u gathers), d partial = u.v
+//     reduce : workgroup partials of d (and g of the last update) stored sc1 into a parity bank; hierarchical
+//              grid barrier (8 group counters -> top counter -> group generation words), every wave then sums
+//              the G partials in the same fixed order -> identical scalars in every workgroup
+//     step   : stop test on g (`solver/solver.py:210` / `:805`), beta, p.Ap = d - beta g / alpha_prev, alpha,
+//              guards (`:187-198`, `:214`) -- k_cg1_step's arithmetic, evaluated redundantly by every thread
+//     update : p = u + beta p, s = v + beta s, x += alpha p, r -= alpha s (CG: masked), u = w r stored sc1,
+//              g partial; every wave drains its stores, then one lane raises the workgroup's u-flag to e
+// The hand-offs follow MI355X_MICROARCH.md "Valid forms" (sc1 stores + drain + relaxed flag / counter; sc1 loads
+// of the partials; agent acquire before the plain u gathers). Every spin is bounded: a give-up sets a word all
+// spinners check, the launch then ends with status FEM_PCG_SYNC_TIMEOUT instead of hanging.
+// Exactly one workgroup of PK_T threads per CU (LDS pins it): the grid is resident by construction (the host
+// checks the occupancy query and launches cooperatively).
+#pragma once
+#include "sell_pair.hpp"
+
+namespace fem {
+
+constexpr int PK_T = 1024;               // threads per workgroup (16 waves, 4 per SIMD)
+constexpr int PK_WAVES = PK_T / 64;
+constexpr int PK_MAXS = 7;               // slices per wave (10M Poisson: 27,000 slices over 4,096 waves -> 7)
+constexpr int PK_U = 2;                  // pairs in flight per lane (4 spills the slot state; persist_probe: 4 = 8)
+constexpr int PK_LINE = 32;              // unsigned words per 128-byte line
+// sync words (zeroed before every launch), in lines: [0, 8) group arrivals, 8 top, [9, 17) group generations,
+// 17 give-up word, 18 + L: u-flag of workgroup L
+enum { PK_GRP = 0, PK_TOP = 8 * PK_LINE, PK_GEN = 9 * PK_LINE, PK_TMO = 17 * PK_LINE, PK_UFLAG = 18 * PK_LINE };
+constexpr unsigned PK_SPIN_LIMIT = 1u << 22;
+constexpr int PK_NPROF = 6;   // phases: u wait, SpMV, block sum, barrier + sums, step, update + drain + flag
+// dynamic LDS (statics would shift the dynamic base off 16 B, cdna_hip_programming.md Guideline 17): 16 wave sums,
+// the barrier verdict (own 16-byte slot), then x and w of the workgroup's rows
+constexpr size_t PK_LDS_HEAD = 256;
+constexpr int PK_VL = 5;                 // slots of v = A u kept in LDS (the rest in registers): fills the LDS left
+                                         // by x and w, frees 2 PK_VL VGPRs for the SpMV (no spills at PK_U = 2)
+constexpr size_t PK_LDS = PK_LDS_HEAD + sizeof(double) * (2 * PK_MAXS + PK_VL) * PK_WAVES * 64;
+static_assert(PK_LDS <= 160 * 1024, "persistent PCG: LDS over the 160 KB of a CU");
+
+__device__ __forceinline__ unsigned pk_ld(const unsigned* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void pk_st(unsigned* p, unsigned v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one lane spins until *p >= target; false on give-up (own or another spinner's)
+__device__ __noinline__ bool pk_wait_ge(const unsigned* p, unsigned target, unsigned* tmo) {
+    for (unsigned spins = 0;; ++spins) {
+        if (pk_ld(p) >= target) return true;
+        if ((spins & 63) == 63 && pk_ld(tmo)) return false;
+        if (spins >= PK_SPIN_LIMIT) {
+            pk_st(tmo, 1u);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+// fixed-order sum of n sc1-loaded partials by one wave (identical result in every lane)
+__device__ __forceinline__ double pk_sum(const double* part, int n) {
+    const int lane = threadIdx.x & 63;
+    double v = 0.0;
+    for (int i = lane; i < n; i += 64) v += __hip_atomic_load(part + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return wave_sum(v);
+}
+
+// grid barrier of epoch e over 8 groups of nper workgroups, then the fixed-order sums of the partial vectors pd
+// (and pg when given) by wave 0 alone, handed to the other waves through LDS (out[0], out[1]). One wave per
+// workgroup reads the G partials instead of all 16 (4,096 waves loading the same 4 KB with sc1 loads queue on the
+// memory channels that hold those lines).
+__device__ __forceinline__ bool pk_barrier(unsigned* sy, int grp, unsigned nper, unsigned e, int* lds_ok,
+                                           const double* pd, const double* pg, int G, double* out) {
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        int okv = 0;
+        if (threadIdx.x == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            unsigned* tmo = sy + PK_TMO;
+            bool ok;
+            const unsigned old = __hip_atomic_fetch_add(sy + PK_GRP + grp * PK_LINE, 1u, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+            if (old == e * nper - 1) {   // last of its group: arrive on top, wait for all groups, release the group
+                __hip_atomic_fetch_add(sy + PK_TOP, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = pk_wait_ge(sy + PK_TOP, e * NXCD, tmo);
+                pk_st(sy + PK_GEN + grp * PK_LINE, e);
+            } else {
+                ok = pk_wait_ge(sy + PK_GEN + grp * PK_LINE, e, tmo);
+            }
+            okv = ok ? 1 : 0;
+        }
+        okv = __builtin_amdgcn_readfirstlane(okv);
+        if (okv && pd) {
+            const double d = pk_sum(pd, G);
+            const double g = pg ? pk_sum(pg, G) : 0.0;
+            if (threadIdx.x == 0) {
+                out[0] = d;
+                out[1] = g;
+            }
+        }
+        if (threadIdx.x == 0) *lds_ok = okv;
+    }
+    __syncthreads();
+    return *lds_ok != 0;
+}
+
+// fixed-order workgroup sum (PK_WAVES waves), valid in thread 0
+__device__ __forceinline__ double pk_block_sum(double v, double* lds16) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) lds16[w] = v;
+    __syncthreads();
+    double t = 0.0;
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 0; i < PK_WAVES; ++i) t += lds16[i];
+    }
+    return t;
+}
+
+struct PkArgs {
+    int64_t nslices, nrows;
+    const int64_t* slice_ptr;
+    const int16_t* cols;    // lane-paired copy (sell_pair.hpp)
+    const double* vals;
+    double* x;
+    double* r;
+    double* p;
+    double* s;
+    double* u;              // gathered by the SpMV: the hand-off between workgroups
+    const double* w;
+    const int32_t* win;     // [2 G] gather window per logical workgroup: first workgroups, then last ones
+    double* part;           // [2 banks][2 (d, g)][G]
+    unsigned* sync;
+    PcgState* st;
+    double* hist;
+    int64_t hist_len;
+    int kmax;               // iterations of this launch
+    int rev;                // FEM_TUNE_REVERSE: odd iterations walk the own slices backwards
+    unsigned long long* prof;   // PROF instantiation: [G][PK_NPROF] shader-clock sums per phase (thread 0 of each WG)
+};
+
+// the 64 rows of slot j of this wave: row = rb + 64 j (32-bit; the host checks nrows < 2^31); `lim` = rows of the
+// slot that exist (wave-uniform; < 64 only in the matrix's last slice)
+#define PK_ON(j) ((j) < nsl && lane < nrows - (s0 + (j)) * 64)
+
+template <int MAXS, bool PROF>
+__global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
+    unsigned long long pacc[PROF ? PK_NPROF : 1] = {};
+    unsigned long long pt = 0;
+// phase boundary: a scheduling barrier in every build (instructions hoisted across phases lengthen the live ranges
+// of the slot arrays: ~180 spilled VGPRs without it), plus the phase clock in the PROF build
+#define PK_MARK(i)                                                         \
+    __builtin_amdgcn_sched_barrier(0);                                     \
+    if constexpr (PROF) {                                                  \
+        const unsigned long long now = __builtin_amdgcn_s_memtime();       \
+        pacc[i] += now - pt;                                               \
+        pt = now;                                                          \
+    }
+    extern __shared__ __attribute__((aligned(16))) double pk_lds_raw[];
+    double* lds16 = pk_lds_raw;
+    int& lds_ok = *reinterpret_cast<int*>(pk_lds_raw + PK_WAVES);
+    double* lds_dg = pk_lds_raw + PK_WAVES + 2;   // barrier sums (bytes 144..159 of the 256-byte head)
+    double* pk_lds = pk_lds_raw + PK_LDS_HEAD / sizeof(double);
+    const int G = gridDim.x;
+    const unsigned nper = (unsigned)(G / NXCD);
+    const int L = (blockIdx.x % NXCD) * (G / NXCD) + blockIdx.x / NXCD;   // XCD-contiguous logical order
+    const int grp = L / (int)nper;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform -> scalar slot bounds
+    const int64_t W = (int64_t)G * PK_WAVES;
+    const int64_t gw = (int64_t)L * PK_WAVES + wv;
+    const int s0 = (int)(gw * a.nslices / W);
+    const int nsl = (int)((gw + 1) * a.nslices / W) - s0;   // <= MAXS (host check)
+    const int nrows = (int)a.nrows;
+    const unsigned rb = (unsigned)s0 * 64u + (unsigned)lane;
+    double* xl = pk_lds + wv * MAXS * 64 + lane;
+    double* wl = pk_lds + PK_WAVES * MAXS * 64 + wv * MAXS * 64 + lane;
+    double* vl = pk_lds + 2 * PK_WAVES * MAXS * 64 + wv * PK_VL * 64 + lane;   // v of slots j < PK_VL
+    unsigned* sy = a.sync;
+    PcgState* st = a.st;
+
+    // scalars (every thread; WG 0 thread 0 writes them back)
+    const bool cg = st->mode != FEM_MODE_PCG;
+    const double tol = st->tol, eps = st->eps;
+    const int max_iter = st->max_iter;
+    int it = st->iter, halt = st->halt, status = st->status, stop_iter = st->stop_iter;
+    double rz = st->rz, alpha_prev = st->alpha, beta = st->beta, pq = st->pq, rz_new = st->rz_new;
+    double g = st->red[1];   // r.z of the current iterate (init or the last launch's last update)
+
+    double rr[MAXS], pp[MAXS], ss[MAXS], vv[MAXS], uo[MAXS];
+#pragma unroll
+    for (int j = 0; j < MAXS; ++j) {
+        const unsigned row = rb + 64u * j;
+        const bool on = PK_ON(j);
+        rr[j] = on ? a.r[row] : 0.0;
+        pp[j] = on ? a.p[row] : 0.0;
+        ss[j] = on ? a.s[row] : 0.0;
+        uo[j] = on ? a.u[row] : 0.0;
+        vv[j] = 0.0;
+        if (j < PK_VL) vl[j * 64] = 0.0;
+        xl[j * 64] = on ? a.x[row] : 0.0;
+        wl[j * 64] = on ? a.w[row] : 0.0;
+    }
+    const int wlo = a.win[L], whi = a.win[G + L];
+    bool fail = false;
+    int k = 0;
+    if (!halt) {
+        if constexpr (PROF) pt = __builtin_amdgcn_s_memtime();
+        for (k = 0; k < a.kmax; ++k) {
+            const unsigned e = (unsigned)k + 1;
+            // ---- wait for the u of the gather window (written by the previous update of this launch)
+            if (k > 0) {
+                if (wv == 0) {
+                    bool ok = true;
+                    for (int b0 = wlo; b0 <= whi && ok; b0 += 64) {
+                        const int jw = b0 + lane;
+                        bool done = jw > whi;
+                        for (unsigned spins = 0; !__all(done); ++spins) {
+                            if (!done) done = pk_ld(sy + PK_UFLAG + jw * PK_LINE) >= e - 1;
+                            if ((spins & 63) == 63 && pk_ld(sy + PK_TMO)) {
+                                ok = false;
+                                break;
+                            }
+                            if (spins >= PK_SPIN_LIMIT) {
+                                pk_st(sy + PK_TMO, 1u);
+                                ok = false;
+                                break;
+                            }
+                            __builtin_amdgcn_s_sleep(1);
+                        }
+                    }
+                    if (lane == 0) {
+                        lds_ok = ok;
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    }
+                }
+                __syncthreads();
+                if (!lds_ok) {
+                    fail = true;
+                    break;
+                }
+            }
+            PK_MARK(0);
+            // ---- v = A u over the own slices, d partial. Slots unrolled (register-resident state needs
+            // compile-time indices); the empty asm keeps the compiler from interleaving slots (register blow-up)
+            const bool rv = a.rev && ((it & 1) != 0);
+            // launder the matrix pointers every iteration: otherwise the per-slot addresses are hoisted out of the
+            // k loop and held in VGPRs across it (7 slots x ~6 registers -> spills)
+            const int64_t* slp = a.slice_ptr;
+            const int16_t* cop = a.cols;
+            const double* vap = a.vals;
+            const double* uvp = a.u;
+            asm volatile("" : "+s"(slp), "+s"(cop), "+s"(vap), "+s"(uvp));
+            if (!rv) {
+#pragma unroll
+                for (int j = 0; j < MAXS; ++j) {
+                    if (j < nsl) {
+                        const double v = sell_row_pair<PK_U>(s0 + j, lane, slp, cop, vap, uvp);
+                        if (j < PK_VL) vl[j * 64] = v; else vv[j] = v;
+                    }
+                    asm volatile("" ::: "memory");
+                }
+            } else {
+#pragma unroll
+                for (int jj = 0; jj < MAXS; ++jj) {
+                    const int j = MAXS - 1 - jj;
+                    if (j < nsl) {
+                        const double v = sell_row_pair<PK_U>(s0 + j, lane, slp, cop, vap, uvp);
+                        if (j < PK_VL) vl[j * 64] = v; else vv[j] = v;
+                    }
+                    asm volatile("" ::: "memory");
+                }
+            }
+            double dp = 0.0;
+#pragma unroll
+            for (int j = 0; j < MAXS; ++j) dp += uo[j] * (j < PK_VL ? vl[j * 64] : vv[j]);   // absent rows: uo = 0
+            // ---- publish d (and g of the last update), grid barrier, fixed-order sums
+            const int bank = k & 1;
+            double* pd = a.part + (size_t)bank * 2 * G;
+            PK_MARK(1);
+            const double dsum = pk_block_sum(dp, lds16);
+            PK_MARK(2);
+            if (threadIdx.x == 0) __hip_atomic_store(pd + L, dsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (!pk_barrier(sy, grp, nper, e, &lds_ok, pd, k > 0 ? pd + G : nullptr, G, lds_dg)) {
+                fail = true;
+                break;
+            }
+            const double d = lds_dg[0];
+            if (k > 0) g = lds_dg[1];
+            PK_MARK(3);
+            // ---- step (k_cg1_step)
+            double bnew = 0.0;
+            bool stop = false;
+            if (it > 0) {
+                rz_new = g;
+                const double nrm = sqrt(g);
+                if (L == 0 && threadIdx.x == 0 && a.hist && it - 1 < a.hist_len) a.hist[it - 1] = nrm;
+                if (nrm < tol) {
+                    status = FEM_PCG_CONVERGED;
+                    stop_iter = it;
+                    stop = true;
+                } else {
+                    bnew = cg ? g / (rz + eps) : g / rz;
+                    if (cg && (isnan(bnew) || isinf(bnew))) {
+                        status = FEM_PCG_BETA_NAN;
+                        stop_iter = it;
+                        stop = true;
+                    }
+                }
+            }
+            if (!stop && it >= max_iter) stop = true;   // poll reports FEM_PCG_MAXITER
+            double al = 0.0;
+            if (!stop) {
+                pq = (it == 0) ? d : d - bnew * g / alpha_prev;
+                if (cg) {
+                    if (fabs(pq) < eps || pq < 0.0) {
+                        status = FEM_PCG_BREAKDOWN;
+                        stop_iter = it + 1;
+                        stop = true;
+                    } else {
+                        al = g / (pq + eps);
+                        if (isnan(al) || isinf(al)) {
+                            status = FEM_PCG_ALPHA_NAN;
+                            stop_iter = it + 1;
+                            stop = true;
+                        }
+                    }
+                } else {
+                    al = g / pq;
+                }
+            }
+            if (stop) {
+                halt = 1;
+                break;
+            }
+            rz = g;
+            alpha_prev = al;
+            beta = bnew;
+            it += 1;
+            PK_MARK(4);
+            // ---- update the own rows, publish u and the g partial (bank of the next iteration)
+            double gp = 0.0;
+            // per-slot store addresses recomputed every iteration (hoisted out of the k loop they are spilled)
+            unsigned rbi = rb;
+            double* ust = a.u;
+            asm volatile("" : "+v"(rbi), "+s"(ust));
+#pragma unroll
+            for (int j = 0; j < MAXS; ++j) {
+                // branch-free over the lanes (rows past nrows hold zeros: their SpMV rows are zero padding); only
+                // the u store is masked. Exec-masked updates of the loop-carried arrays cost register copies.
+                if (j < nsl) {
+                    const double pi = uo[j] + bnew * pp[j];
+                    const double si = (j < PK_VL ? vl[j * 64] : vv[j]) + bnew * ss[j];
+                    pp[j] = pi;
+                    ss[j] = si;
+                    xl[j * 64] += al * pi;
+                    double ri = rr[j] - al * si;
+                    const double wi = wl[j * 64];
+                    if (cg && wi == 0.0) ri = 0.0;
+                    rr[j] = ri;
+                    const double ui = wi * ri;
+                    uo[j] = ui;
+                    if (PK_ON(j)) __hip_atomic_store(ust + (rbi + 64u * j), ui, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    gp += ri * ui;
+                }
+            }
+            const double gsum = pk_block_sum(gp, lds16);
+            if (threadIdx.x == 0)
+                __hip_atomic_store(a.part + (size_t)(bank ^ 1) * 2 * G + G + L, gsum, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave drains its u stores
+            __syncthreads();
+            if (threadIdx.x == 0) pk_st(sy + PK_UFLAG + L * PK_LINE, e);
+            PK_MARK(5);
+        }
+    }
+    // ---- chunk end without a stop: one more barrier makes the last g partials visible; stop test of that g
+    if (!fail && !halt && k == a.kmax && a.kmax > 0) {
+        const unsigned e = (unsigned)a.kmax + 1;
+        if (!pk_barrier(sy, grp, nper, e, &lds_ok, a.part + (size_t)(a.kmax & 1) * 2 * G + G, nullptr, G, lds_dg)) {
+            fail = true;
+        } else {
+            g = lds_dg[0];
+            if (it > 0) {
+                const double nrm = sqrt(g);
+                const bool conv = nrm < tol;
+                if (conv || it >= max_iter) {
+                    rz_new = g;
+                    if (L == 0 && threadIdx.x == 0 && a.hist && it - 1 < a.hist_len) a.hist[it - 1] = nrm;
+                    if (conv) {
+                        status = FEM_PCG_CONVERGED;
+                        stop_iter = it;
+                    }
+                    halt = 1;
+                }
+            }
+        }
+    }
+    // ---- state back to memory (u is already there)
+#pragma unroll
+    for (int j = 0; j < MAXS; ++j) {
+        if (PK_ON(j)) {
+            const unsigned row = rb + 64u * j;
+            a.r[row] = rr[j];
+            a.p[row] = pp[j];
+            a.s[row] = ss[j];
+            a.x[row] = xl[j * 64];
+        }
+    }
+    if constexpr (PROF) {
+        if (threadIdx.x == 0)
+            for (int i = 0; i < PK_NPROF; ++i) a.prof[(size_t)L * PK_NPROF + i] = pacc[i];
+    }
+    if (L == 0 && threadIdx.x == 0) {
+        if (fail) {
+            status = FEM_PCG_SYNC_TIMEOUT;
+            halt = 1;
+        }
+        st->iter = it;
+        st->halt = halt;
+        st->status = status;
+        st->stop_iter = stop_iter;
+        st->rz = rz;
+        st->rz_new = rz_new;
+        st->alpha = alpha_prev;
+        st->beta = beta;
+        st->pq = pq;
+        st->red[1] = g;
+    }
+}
+#undef PK_ON
+#undef PK_MARK
+
+// gather window per logical workgroup: the first and last workgroup owning a column of its rows
+__global__ void k_pk_window(int64_t nslices, int64_t nrows, const int64_t* __restrict__ slice_ptr,
+                            const int16_t* __restrict__ dcols, int G, int* __restrict__ lo, int* __restrict__ hi) {
+    const int64_t W = (int64_t)G * PK_WAVES;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nslices * 64;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = t >> 6;
+        const int l = (int)(t & 63);
+        const int64_t row = s * 64 + l;
+        const int64_t p0 = slice_ptr[s];
+        const int w = (int)((slice_ptr[s + 1] - p0) >> 6);
+        int64_t cmin = row, cmax = row;
+        for (int kk = 0; kk < w; ++kk) {
+            const int64_t c = row + dcols[p0 + 64 * kk + l];
+            cmin = c < cmin ? c : cmin;
+            cmax = c > cmax ? c : cmax;
+        }
+        if (cmax >= nrows) cmax = nrows - 1;
+        if (cmin < 0) cmin = 0;
+        auto owner = [&](int64_t r) {   // logical workgroup owning row r: largest wave gw with gw S / W <= slice
+            const int64_t sl = r >> 6;
+            const int64_t gw = ((sl + 1) * W - 1) / nslices;
+            return (int)(gw / PK_WAVES);
+        };
+        const int me = owner(row);
+        atomicMin(lo + me, owner(cmin));
+        atomicMax(hi + me, owner(cmax));
+    }
+}
+
+}  // namespace fem

@@ -90,6 +90,29 @@ __global__ void __launch_bounds__(256) k_spmv3_lab(int64_t nslices, int64_t nrow
     }
 }
 
+// persistent-geometry probe: one workgroup of T threads per CU (occupancy pinned by dynamic LDS), wave g owns the
+// contiguous slice range [g S / W, (g+1) S / W) (XCD-contiguous logical order), U pairs in flight (paired layout)
+template <int T, int U>
+__global__ void __launch_bounds__(T) k_spmv_persist_lab(int64_t nslices, int64_t nrows,
+                                                        const int64_t* __restrict__ slice_ptr,
+                                                        const int16_t* __restrict__ cols,
+                                                        const double* __restrict__ vals,
+                                                        const double* __restrict__ x, double* __restrict__ y) {
+    extern __shared__ double pad_lds[];
+    const int lane = threadIdx.x & 63;
+    const int G = gridDim.x;
+    const int L = (blockIdx.x % NXCD) * (G / NXCD) + blockIdx.x / NXCD;
+    const int64_t W = (int64_t)G * (T / 64);
+    const int64_t g = (int64_t)L * (T / 64) + (threadIdx.x >> 6);
+    const int64_t s0 = g * nslices / W, s1 = (g + 1) * nslices / W;
+    for (int64_t s = s0; s < s1; ++s) {
+        const double acc = sell_row_pair<U>(s, lane, slice_ptr, cols, vals, x);
+        const int64_t row = s * 64 + lane;
+        if (row < nrows) y[row] = acc;
+    }
+    if (nrows < 0) pad_lds[threadIdx.x] = 0.0;
+}
+
 }  // namespace fem
 
 using namespace fem;
@@ -133,6 +156,26 @@ int fem_lab_spmv16_pair(int u, int grid, int64_t nrows, const int64_t* slice_ptr
     if (u == 2) hipLaunchKernelGGL(k_spmv16_pair<2>, dim3(grid), dim3(256), 0, st, ns, nrows, slice_ptr, dcols, vals, x, y);
     else if (u == 8) hipLaunchKernelGGL(k_spmv16_pair<8>, dim3(grid), dim3(256), 0, st, ns, nrows, slice_ptr, dcols, vals, x, y);
     else hipLaunchKernelGGL(k_spmv16_pair<4>, dim3(grid), dim3(256), 0, st, ns, nrows, slice_ptr, dcols, vals, x, y);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_lab_spmv_persist(int threads, int u, int grid, int64_t lds_bytes, int64_t nrows, const int64_t* slice_ptr,
+                         const int16_t* dcols, const double* vals, const double* x, double* y, fem_stream_t stream) {
+    const int64_t ns = cdiv(nrows, 64);
+    if (ns == 0) return FEM_OK;
+    const hipStream_t st = S(stream);
+#define LP(TT, UU)                                                                                              \
+    hipLaunchKernelGGL((k_spmv_persist_lab<TT, UU>), dim3(grid), dim3(TT), (size_t)lds_bytes, st, ns, nrows, \
+                       slice_ptr, dcols, vals, x, y)
+    if (threads == 512) {
+        if (u == 4) LP(512, 4); else LP(512, 8);
+    } else if (threads == 1024) {
+        if (u == 4) LP(1024, 4); else LP(1024, 8);
+    } else {
+        if (u == 4) LP(256, 4); else LP(256, 8);
+    }
+#undef LP
     FEM_LAUNCHED();
     return FEM_OK;
 }

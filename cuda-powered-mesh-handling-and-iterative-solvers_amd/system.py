@@ -22,8 +22,10 @@ def _dev_scalar(dev, dtype, value):
 
 
 # (P)CG kernel schedules (csrc/pcg.hip): 0 = three kernels with in-kernel grid reductions, 1 = fused (p formed
-# inside the SpMV), 2 = deferred (partials summed by the next kernel, no grid atomics)
-SCHED_THREE, SCHED_FUSED, SCHED_DEFERRED = 0, 1, 2
+# inside the SpMV), 2 = deferred (partials summed by the next kernel, no grid atomics), 3 = persistent (one
+# cooperative launch per chunk of single-reduction iterations, csrc/pcg_persist.hpp; falls back to 2 where its
+# prerequisites do not hold)
+SCHED_THREE, SCHED_FUSED, SCHED_DEFERRED, SCHED_PERSIST = 0, 1, 2, 3
 # measured on MI355X (tools/spmv_tune.py, 10M-tet cube, 16-bit columns): scalar Poisson 0.0925 ms/it deferred vs
 # 0.0947 three-kernel; 3x3 elasticity 0.437 three-kernel vs 0.454 deferred
 DEFAULT_SCHEDULE = {1: SCHED_DEFERRED, 3: SCHED_THREE}
@@ -275,11 +277,18 @@ class SellMatrix:
                                       ctypes.byref(rz)), "fem_pcg_solve")
             sc = (ctypes.c_double * 6)()
             C.check(lib.fem_pcg_scalars(h, sc), "fem_pcg_scalars")
+            _check_sync(stt.value)
         finally:
             lib.fem_pcg_destroy(h)
         if hist is not None:
             hist = hist[: min(it.value, hist.numel())]
         return PcgResult(x, it.value, stt.value, rz.value, sc[1], hist)
+
+
+def _check_sync(status):
+    if status == C.PCG_SYNC_TIMEOUT:
+        raise RuntimeError("persistent PCG: an in-launch wait gave up (grid synchronisation timed out); "
+                           "the iterate is not meaningful")
 
 
 class _DistMarker:
@@ -330,7 +339,12 @@ class PcgRunner:
     def poll(self):
         it, stt, rz = ctypes.c_int(), ctypes.c_int(), ctypes.c_double()
         C.check(self.lib.fem_pcg_poll(self.h, ctypes.byref(it), ctypes.byref(stt), ctypes.byref(rz)), "fem_pcg_poll")
+        _check_sync(stt.value)
         return it.value, stt.value, rz.value
+
+    def effective_schedule(self):
+        """The schedule the context runs (after start(): SCHED_PERSIST may have fallen back to SCHED_DEFERRED)."""
+        return int(self.lib.fem_pcg_get_schedule(self.h))
 
     def profile(self, k, every=1):
         """k iterations with hip events around the kernels of every `every`-th one -> (ms sums, counts)."""

@@ -50,6 +50,8 @@ enum {
     FEM_PCG_BREAKDOWN = 3,  /* pAp < eps or pAp < 0  (`solver/solver.py:187-192`) */
     FEM_PCG_ALPHA_NAN = 4,  /* (`solver/solver.py:196-198`) */
     FEM_PCG_BETA_NAN = 5,   /* (`solver/solver.py:214-218`) */
+    FEM_PCG_SYNC_TIMEOUT = 6, /* persistent schedule: an in-launch wait gave up (seconds without progress); the
+                               * iterate is not meaningful -> RuntimeError */
 };
 
 /* CG_CONSTRAINED: constrained_conjugate_gradient_solver / new_constrained_conjugate_gradient_solver
@@ -306,6 +308,10 @@ int fem_lab_sell_pair(int64_t nrows, const int64_t* slice_ptr, const double* val
                       double* vals_out, int16_t* dcols_out, fem_stream_t stream);
 int fem_lab_spmv16_pair(int u, int grid, int64_t nrows, const int64_t* slice_ptr, const int16_t* dcols,
                         const double* vals, const double* x, double* y, fem_stream_t stream);
+// persistent-geometry SpMV probe (paired bs = 1 layout): one workgroup of `threads` per CU pinned by lds_bytes of
+// dynamic LDS, contiguous slice ranges per wave
+int fem_lab_spmv_persist(int threads, int u, int grid, int64_t lds_bytes, int64_t nrows, const int64_t* slice_ptr,
+                         const int16_t* dcols, const double* vals, const double* x, double* y, fem_stream_t stream);
 // bs = 3 layout probes (sell_pair3.hpp): layout 1 plane-paired values, 2 entry-paired values + int32 column pairs
 int fem_lab_sell3_layout(int layout, int64_t nrows, const int64_t* slice_ptr, const double* vals,
                          const int16_t* dcols, double* vals_out, int16_t* dcols_out, fem_stream_t stream);
@@ -338,9 +344,16 @@ int fem_pcg_scalars(fem_pcg* s, double* out6);
 int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, double* rz);
 /* kernel schedule: 0 = 3-kernel (SpMV+p.q / r update+r.z / x,p update; the context default), 1 = fused (p formed
  * inside the SpMV from r, w and the previous p; 2 kernels per iteration), 2 = deferred (each kernel finishes the
- * previous kernel's block partials itself: no grid atomics, state banked by launch parity). Distributed and
- * constrained contexts accept only 0. */
+ * previous kernel's block partials itself: no grid atomics, state banked by launch parity), 3 = persistent
+ * (pcg_persist.hpp: the single-reduction iteration as one cooperative launch per chunk, CG state of every row held in
+ * registers / LDS of its owning wave; bs = 1 with 16-bit columns and FEM_TUNE_PAIR, single GPU, at most 7 slices
+ * per wave; otherwise fem_pcg_start falls back to 2). Distributed and constrained contexts accept only 0. */
 int fem_pcg_set_schedule(fem_pcg* s, int sched);
+/* the schedule the context runs (valid after fem_pcg_start: 3 may have fallen back to 2) */
+int fem_pcg_get_schedule(fem_pcg* s);
+/* persistent schedule only: k iterations of the instrumented kernel build; host_out[G * 6] = per-workgroup shader-clock
+ * sums of the phases (u wait, SpMV, block sum, barrier + partial sums, step, update + drain + flag), *grid = G */
+int fem_pcg_persist_profile(fem_pcg* s, int k, unsigned long long* host_out, int* grid);
 /* CG_CONSTRAINED projections applied to x once at fem_pcg_start (after r0 = b - A x0) and after every x update:
  *   order 0 (`enforce_constraints`, `solver/solver.py:478-510`): x[rbe2_slave] = x[rbe2_master] (all gathered
  *           before any is written), then x[spc_dof] = spc_val.  G must be 0.

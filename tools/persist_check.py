@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Persistent PCG (schedule 3) against the deferred schedule (2) on the GPU box: solve-to-tolerance parity (iteration
+count, status, x) and fixed-iteration throughput on Kuhn-cube Poisson meshes.
+
+    python tools/persist_check.py [--n 20 119] [--iters 500] [--chunk 500]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import fem355  # noqa: E402,F401
+from fem355 import _capi as C, mesh, system  # noqa: E402
+
+
+def case(n, dev):
+    coords, tets = mesh.kuhn_cube(n, device=dev)
+    A = system.assemble_tet4_system(coords, tets, "poisson", 1.0, 0.0)
+    f, fixed = mesh.cube_poisson_case(coords)
+    mask = torch.zeros((coords.shape[0], 1), dtype=torch.uint8, device=dev)
+    mask[fixed] = 1
+    w = A.jacobi(mask.view(-1))
+    b = f.reshape(-1).to(torch.float64).contiguous()
+    return A, b, w
+
+
+def rate(A, b, w, sched, warm, iters, chunk):
+    run = system.PcgRunner(A, b, w, tol=0.0, schedule=sched)
+    run.start()
+    eff = run.effective_schedule()
+    run.iterate(warm)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    done = 0
+    while done < iters:
+        k = min(chunk, iters - done)
+        run.iterate(k)
+        done += k
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    it, stt, rz = run.poll()
+    x = run.x.clone()
+    run.close()
+    return {"sched": eff, "it_per_s": iters / dt, "us_per_it": dt / iters * 1e6, "iter": it, "status": stt,
+            "rz": rz}, x
+
+
+PHASES = ("u_wait", "spmv", "block_sum", "barrier_sums", "step", "update_flag")
+
+
+def phase_profile(A, b, w, warm, iters, ghz=2.4):
+    """Per-iteration phase times (us at `ghz` shader clock) of the instrumented persistent kernel: mean and max over
+    workgroups."""
+    import ctypes
+    run = system.PcgRunner(A, b, w, tol=0.0, schedule=3)
+    run.start()
+    assert run.effective_schedule() == 3
+    run.iterate(warm)
+    G = 256
+    buf = (ctypes.c_ulonglong * (G * len(PHASES)))()
+    g = ctypes.c_int()
+    C.check(run.lib.fem_pcg_persist_profile(run.h, int(iters), buf, ctypes.byref(g)), "fem_pcg_persist_profile")
+    run.close()
+    t = torch.tensor(list(buf), dtype=torch.float64).view(G, len(PHASES))[: g.value] / iters / (ghz * 1e3)
+    return {p: {"mean_us": float(t[:, i].mean()), "max_us": float(t[:, i].max()), "min_us": float(t[:, i].min())}
+            for i, p in enumerate(PHASES)} | {"total_mean_us": float(t.sum(1).mean())}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, nargs="+", default=[20, 119])
+    ap.add_argument("--iters", type=int, default=500)
+    ap.add_argument("--warm", type=int, default=50)
+    ap.add_argument("--chunk", type=int, default=500)
+    ap.add_argument("--prof", action="store_true", help="phase breakdown of the instrumented persistent kernel")
+    ap.add_argument("--skip-solve", action="store_true")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    for n in a.n:
+        A, b, w = case(n, dev)
+        out = {"n": n, "rows": A.n}
+        tol = 1e-8 * float(torch.sqrt(torch.dot(b, w * b)))
+        if a.prof:
+            out["prof"] = phase_profile(A, b, w, a.warm, a.iters)
+        sol = {}
+        for sched in (() if a.skip_solve else (2, 3)):
+            t0 = time.perf_counter()
+            r = A.pcg(b, None, w=w, mode=C.MODE_PCG, tol=tol, max_iter=20000, chunk=64, schedule=sched)
+            torch.cuda.synchronize()
+            out[f"solve{sched}"] = {"iters": r.iterations, "status": r.status, "rz": r.rz,
+                                    "ms": (time.perf_counter() - t0) * 1e3}
+            sol[sched] = r.x
+        if sol:
+            out["solve_dx_rel"] = float((sol[2] - sol[3]).norm() / sol[2].norm())
+        xs = {}
+        for sched in (2, 3):
+            out[f"rate{sched}"], xs[sched] = rate(A, b, w, sched, a.warm, a.iters, a.chunk)
+        out["rate_dx_rel"] = float((xs[2] - xs[3]).norm() / xs[2].norm())
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
