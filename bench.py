@@ -8,9 +8,11 @@ Workload: Kuhn-cube mesh n=119 -> 10,110,954 P1 tets, 1,728,0
     `value` = steps/s of the whole job (for N>1: the same global system element-partitioned over the ranks,
     strong scaling), measured between barrier+synchronize brackets, max over ranks.
   * DOFs/s = n_DOF / (assembly incl. pattern build + PCG solve to rtol 1e-8 on sqrt(r.z)), reported beside.
-  * roofline: the SpMV+p.Ap kernel (k_pcg_d1 in the default deferred schedule), algorithmic bytes
-    (8 + idx) nnz + 4 (n+1) + 16 n per launch (§8(d); idx = 2 for 16-bit deltas, 4 for int32) over its average
-    device time, sampled live with hip events on the solver stream inside the timed region.
+  * roofline: the dominant kernel of the active schedule, algorithmic bytes (8 + idx) nnz + 4 (n+1) + 16 n
+    (§8(d); idx = 2 for 16-bit deltas, 4 for int32) over its device time measured live with hip events on the
+    solver stream inside the timed region. bs=1 default (persistent schedule, k_pcg_persist): per ITERATION —
+    the whole PCG iteration moves just those bytes (matrix, u gather, u store); other schedules: per SpMV launch
+    (k_pcg_d1 deferred, k_pcg_spmv_dot three-kernel).
   * cpu_baseline: the oracle (torch-CPU restatement of the reference's EBE PCG, oracle/ref_cpu.py) timed on the
     host cores on a bounded sample (assembly + a few iterations of the same 10M system), rank 0 at N=1 only.
 
@@ -47,8 +49,8 @@ def parse():
     ap.add_argument("--rtol", type=float, default=1e-8)
     ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--schedule", type=int, default=None, help="PCG kernel schedule (0 three-kernel, 1 fused, 2 deferred; "
-                    "default: deferred for bs=1, three-kernel for bs=3)")
+    ap.add_argument("--schedule", type=int, default=None, help="PCG kernel schedule (0 three-kernel, 1 fused, 2 deferred, 3 persistent; "
+                    "default: persistent for bs=1, three-kernel for bs=3)")
     ap.add_argument("--graph", type=int, default=0, help="capture k iterations per hipGraph (0 = plain launches)")
     ap.add_argument("--force-dist", action="store_true", help="run the RCCL element-partitioned path even at N=1")
     ap.add_argument("--dist-variant", type=int, default=1,
@@ -153,15 +155,20 @@ def main():
     run.iterate(a.warmup)
     sync()
     t0 = time.perf_counter()
-    ms, cnt = run.profile(a.steps, every=a.sample_every)
+    persist = run.effective_schedule() == system.SCHED_PERSIST
+    # persistent schedule: the K steps are ONE cooperative launch (the kernel stops itself on convergence, so a
+    # solve needs no host polling either); hip events around it give the per-iteration time of the whole iteration
+    ms, cnt = run.profile(a.steps, every=a.steps if persist else a.sample_every)
     sync()
     dt = time.perf_counter() - t0
     it, stt, _ = run.poll()
     assert it == a.warmup + a.steps, (it, stt)
     kernel = {system.SCHED_THREE: "k_pcg_spmv_dot", system.SCHED_FUSED: "k_pcg_spmv_dot<FUSED>",
-              system.SCHED_DEFERRED: "k_pcg_d1"}[run.schedule]
+              system.SCHED_DEFERRED: "k_pcg_d1", system.SCHED_PERSIST: "k_pcg_persist"}[run.effective_schedule()]
     run.close()
 
+    # per launch of the measured kernel: one SpMV (3-kernel / deferred) or one whole iteration (persistent: the
+    # matrix, the u gather and the u store are all it moves; r, p, s, x, w stay in registers and LDS)
     spmv_ms = ms[0] / max(cnt[0], 1)
     alg = A.algorithmic_bytes_spmv()
     achieved = alg / (spmv_ms * 1e-3) / 1e9
@@ -188,11 +195,13 @@ def main():
         "solve_ms": t_solve * 1e3,
         "solve_iters": res.iterations,
         "solve_status": res.status,
-        "kernel_ms": {"spmv_dot": spmv_ms, "update": ms[1] / max(cnt[1], 1), "pupdate": ms[2] / max(cnt[2], 1),
-                      "sampled_launches": cnt[0]},
+        "kernel_ms": ({"persist_iteration": spmv_ms, "iterations_per_launch": a.steps} if persist else
+                      {"spmv_dot": spmv_ms, "update": ms[1] / max(cnt[1], 1), "pupdate": ms[2] / max(cnt[2], 1),
+                       "sampled_launches": cnt[0]}),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic_from_profiles(workload_key, kernel, alg),
                      "kernel": kernel, "algorithmic_bytes": alg,
+                     "per": "iteration (whole PCG iteration in the persistent kernel)" if persist else "SpMV launch",
                      "stream_ceiling_GBps": ceiling, "frac_of_stream_read": achieved / ceiling["read"]},
         "cpu_baseline": None,
     }

@@ -1806,7 +1806,7 @@ static int launch_persist(fem_pcg* s, int k, unsigned long long* prof) {
     a.prof = prof;
     void* args[] = {&a};
     const void* fn = prof ? (const void*)k_pcg_persist<PK_MAXS, true> : (const void*)k_pcg_persist<PK_MAXS, false>;
-    FEM_HIP(hipLaunchCooperativeKernel(fn, dim3(G), dim3(PK_T), args, PK_LDS, s->stream));
+    FEM_HIP(hipLaunchKernel(fn, dim3(G), dim3(PK_T), args, PK_LDS, s->stream));
     FEM_LAUNCHED();
     s->launched += k;
     return FEM_OK;
@@ -2123,6 +2123,7 @@ int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, 
     s->max_iter = 0x7fffffff;
     if (rc) return rc;
     if (chunk <= 0) chunk = 32;
+    if (s->persist) chunk = max_iter;   // the persistent kernel stops itself on convergence: one launch, one poll
     int done = 0;
     int it = 0, stt = FEM_PCG_RUNNING;
     while (done < max_iter) {

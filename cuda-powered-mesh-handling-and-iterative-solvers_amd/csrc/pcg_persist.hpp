@@ -20,7 +20,7 @@
 // of the partials; agent acquire before the plain u gathers). Every spin is bounded: a give-up sets a word all
 // spinners check, the launch then ends with status FEM_PCG_SYNC_TIMEOUT instead of hanging.
 // Exactly one workgroup of PK_T threads per CU (LDS pins it): the grid is resident by construction (the host
-// checks the occupancy query and launches cooperatively).
+// checks the occupancy query; a plain launch: a cooperative one adds ~17 us per launch and buys only that check).
 #pragma once
 #include "sell_pair.hpp"
 
@@ -393,8 +393,8 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
             if (it > 0) {
                 const double nrm = sqrt(g);
                 const bool conv = nrm < tol;
+                rz_new = g;   // r.z of the current iterate, what fem_pcg_poll reports between chunks
                 if (conv || it >= max_iter) {
-                    rz_new = g;
                     if (L == 0 && threadIdx.x == 0 && a.hist && it - 1 < a.hist_len) a.hist[it - 1] = nrm;
                     if (conv) {
                         status = FEM_PCG_CONVERGED;
@@ -464,9 +464,19 @@ __global__ void k_pk_window(int64_t nslices, int64_t nrows, const int64_t* __res
             const int64_t gw = ((sl + 1) * W - 1) / nslices;
             return (int)(gw / PK_WAVES);
         };
+        // the 64 lanes of a wave hold the 64 rows of one slice (same owner): reduce, then one atomic pair per
+        // wave (1.7M-thread atomics on 2 G words cost 4.4 ms)
         const int me = owner(row);
-        atomicMin(lo + me, owner(cmin));
-        atomicMax(hi + me, owner(cmax));
+        int olo = owner(cmin), ohi = owner(cmax);
+        for (int off = 32; off > 0; off >>= 1) {
+            const int a2 = __shfl_xor(olo, off), b2 = __shfl_xor(ohi, off);
+            olo = a2 < olo ? a2 : olo;
+            ohi = b2 > ohi ? b2 : ohi;
+        }
+        if (l == 0) {
+            atomicMin(lo + me, olo);
+            atomicMax(hi + me, ohi);
+        }
     }
 }
 

@@ -26,9 +26,9 @@ def _dev_scalar(dev, dtype, value):
 # cooperative launch per chunk of single-reduction iterations, csrc/pcg_persist.hpp; falls back to 2 where its
 # prerequisites do not hold)
 SCHED_THREE, SCHED_FUSED, SCHED_DEFERRED, SCHED_PERSIST = 0, 1, 2, 3
-# measured on MI355X (tools/spmv_tune.py, 10M-tet cube, 16-bit columns): scalar Poisson 0.0925 ms/it deferred vs
-# 0.0947 three-kernel; 3x3 elasticity 0.437 three-kernel vs 0.454 deferred
-DEFAULT_SCHEDULE = {1: SCHED_DEFERRED, 3: SCHED_THREE}
+# measured on MI355X (10M-tet cube, 16-bit columns, paired layout; tools/persist_check.py, tools/spmv_tune.py):
+# scalar Poisson 59.4 us/it persistent vs 79.4 deferred; 3x3 elasticity three-kernel (the persistent kernel is bs=1)
+DEFAULT_SCHEDULE = {1: SCHED_PERSIST, 3: SCHED_THREE}
 
 
 def _schedule(fused, schedule, bs=1):

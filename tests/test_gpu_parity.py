@@ -393,3 +393,101 @@ def test_paired_matrix_copy_is_bit_identical(gpu, kind):
             xs.append(run.x.clone())
             run.close()
         assert torch.equal(xs[0], xs[1]), (kind, sched)
+
+
+# ------------------------------------------------------------------ persistent schedule (csrc/pcg_persist.hpp)
+def _poisson_case(system, mesh, n, gpu, jitter=0.0):
+    c, t = mesh.kuhn_cube(n, jitter=jitter, device=gpu) if jitter == 0.0 else mesh.kuhn_cube(n, jitter=jitter)
+    f, fixed = mesh.cube_poisson_case(c)
+    A = system.assemble_tet4_system(c.to(gpu), t.to(gpu), "poisson")
+    mask = torch.zeros(A.n, dtype=torch.uint8, device=gpu)
+    mask[fixed.to(gpu)] = 1
+    return A, f.to(gpu).reshape(-1).to(F64), mask
+
+
+@pytest.mark.parametrize("n,jitter", [(7, 0.1), (40, 0.0)])
+def test_persistent_schedule_matches_three_kernel(gpu, n, jitter):
+    """Schedule 3 (single-reduction iteration in one cooperative launch) against the 3-kernel schedule: PCG to
+    tolerance (iterations +-1, x 1e-10), CG mode with masked rows at fixed iterations (x 1e-12), history."""
+    _, mesh, _, system = _mods()
+    A, b, mask = _poisson_case(system, mesh, n, gpu, jitter)
+    w = A.jacobi(mask)
+    run = system.PcgRunner(A, b, w, tol=0.0, schedule=3)
+    run.start()
+    assert run.effective_schedule() == 3
+    run.close()
+    tol = 1e-9 * float(torch.sqrt(torch.dot(b, w * b)))
+    r0 = A.pcg(b, w=w, tol=tol, max_iter=5000, schedule=0, history=True)
+    r3 = A.pcg(b, w=w, tol=tol, max_iter=5000, schedule=3, history=True)
+    assert r0.status == r3.status == 1 and abs(r0.iterations - r3.iterations) <= 1
+    assert rel(r3.x, r0.x) < 1e-10
+    k = min(r0.iterations, r3.iterations) - 1
+    assert rel(r3.history[:k], r0.history[:k]) < 1e-8
+    wm = (mask == 0).to(F64)
+    c0 = A.pcg(b, w=wm, mode=0, tol=0.0, max_iter=25, schedule=0)
+    c3 = A.pcg(b, w=wm, mode=0, tol=0.0, max_iter=25, schedule=3)
+    assert c0.iterations == c3.iterations == 25 and c0.status == c3.status == 2 and rel(c3.x, c0.x) < 1e-12
+
+
+def test_persistent_chunks_are_bit_identical(gpu):
+    """Chunk boundaries add no arithmetic: 4 launches of 9 iterations == one launch of 36, bit for bit, and the
+    poll reports the same state."""
+    _, mesh, _, system = _mods()
+    A, b, mask = _poisson_case(system, mesh, 24, gpu)
+    w = A.jacobi(mask)
+    outs = []
+    for chunks in ((36,), (9, 9, 9, 9)):
+        run = system.PcgRunner(A, b, w, tol=0.0, schedule=3)
+        run.start()
+        for k in chunks:
+            run.iterate(k)
+        outs.append((run.poll(), run.x.clone()))
+        run.close()
+    assert outs[0][0] == outs[1][0] and outs[0][0][0] == 36 and torch.equal(outs[0][1], outs[1][1])
+
+
+def test_persistent_full_geometry_10m(gpu):
+    """The 10M-tet bench system (27,000 slices: 6-7 slots per wave, every register slot and the LDS v slots in use):
+    50 fixed iterations equal the deferred schedule's to 1e-12; a solve to tolerance stops mid-launch at the
+    same iteration count."""
+    _, mesh, _, system = _mods()
+    A, b, mask = _poisson_case(system, mesh, 119, gpu)
+    w = A.jacobi(mask)
+    xs = []
+    for sched in (2, 3):
+        run = system.PcgRunner(A, b, w, tol=0.0, schedule=sched)
+        run.start()
+        assert run.effective_schedule() == sched
+        run.iterate(50)
+        it, st, rz = run.poll()
+        assert it == 50 and st == 0
+        xs.append((rz, run.x.clone()))
+        run.close()
+    assert rel(xs[1][1], xs[0][1]) < 1e-12 and abs(xs[1][0] - xs[0][0]) <= 1e-10 * abs(xs[0][0])
+    tol = 1e-8 * float(torch.sqrt(torch.dot(b, w * b)))
+    r2 = A.pcg(b, w=w, tol=tol, max_iter=3000, schedule=2)
+    r3 = A.pcg(b, w=w, tol=tol, max_iter=3000, schedule=3)
+    assert r2.status == r3.status == 1 and abs(r2.iterations - r3.iterations) <= 1 and rel(r3.x, r2.x) < 1e-10
+
+
+def test_persistent_falls_back_and_guards(gpu):
+    """bs = 3 falls back to the deferred schedule; a guard stop (CG breakdown on the scalar block
+    of the indefinite c3d10 rule) reports the same status and iteration as the 3-kernel schedule."""
+    el, mesh, solver, system = _mods()
+    c, t = mesh.kuhn_cube(6)
+    Ael = system.assemble_tet4_system(c.to(gpu), t.to(gpu), "elastic", E, NU)
+    run = system.PcgRunner(Ael, torch.ones(Ael.n, dtype=F64, device=gpu), Ael.jacobi(None), tol=0.0, schedule=3)
+    run.start()
+    assert run.effective_schedule() == 2
+    run.close()
+    c10, t10 = mesh.tet10_cube(1)
+    K = el.compute_c3d10_K_matrix(c10, t10, E, NU, device=gpu, dtype=F64)[:, 0::3, 0::3].contiguous()
+    g = system.build_graph(t10.to(gpu), c10.shape[0])
+    A = system.SellMatrix(g, 1).add_element_matrices(K, t10.to(gpu))
+    F = -torch.ones(A.n, dtype=F64, device=gpu)
+    fixed = mesh.face_nodes(c10, 2, 0.0).to(gpu)
+    wv = torch.ones(A.n, dtype=F64, device=gpu)
+    wv[fixed] = 0.0
+    res = [A.pcg(F, w=wv, mode=0, tol=1e-10, max_iter=50, schedule=s) for s in (0, 3)]
+    assert res[0].status == res[1].status and res[0].iterations == res[1].iterations
+    assert rel(res[1].x, res[0].x) < 1e-10 or float(res[0].x.abs().max()) == float(res[1].x.abs().max()) == 0.0

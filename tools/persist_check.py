@@ -53,7 +53,7 @@ def rate(A, b, w, sched, warm, iters, chunk):
 PHASES = ("u_wait", "spmv", "block_sum", "barrier_sums", "step", "update_flag")
 
 
-def phase_profile(A, b, w, warm, iters, ghz=2.4):
+def phase_profile(A, b, w, warm, iters, ghz=2.4, per_wg=False):
     """Per-iteration phase times (us at `ghz` shader clock) of the instrumented persistent kernel: mean and max over
     workgroups."""
     import ctypes
@@ -67,8 +67,19 @@ def phase_profile(A, b, w, warm, iters, ghz=2.4):
     C.check(run.lib.fem_pcg_persist_profile(run.h, int(iters), buf, ctypes.byref(g)), "fem_pcg_persist_profile")
     run.close()
     t = torch.tensor(list(buf), dtype=torch.float64).view(G, len(PHASES))[: g.value] / iters / (ghz * 1e3)
-    return {p: {"mean_us": float(t[:, i].mean()), "max_us": float(t[:, i].max()), "min_us": float(t[:, i].min())}
-            for i, p in enumerate(PHASES)} | {"total_mean_us": float(t.sum(1).mean())}
+    out = {p: {"mean_us": float(t[:, i].mean()), "max_us": float(t[:, i].max()), "min_us": float(t[:, i].min())}
+           for i, p in enumerate(PHASES)} | {"total_mean_us": float(t.sum(1).mean())}
+    if per_wg:   # logical workgroup L owns waves [16 L, 16 L + 16) of the contiguous slice split
+        G = g.value
+        sp = A.g.slice_ptr.cpu()
+        S = sp.numel() - 1
+        W = G * 16
+        ent = []
+        for L in range(G):
+            s0, s1 = (16 * L) * S // W, (16 * L + 16) * S // W
+            ent.append(int(sp[s1] - sp[s0]))
+        out["per_wg"] = {"spmv_us": [round(float(v), 3) for v in t[:, 1]], "entries": ent}
+    return out
 
 
 def main():
@@ -79,6 +90,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=500)
     ap.add_argument("--prof", action="store_true", help="phase breakdown of the instrumented persistent kernel")
     ap.add_argument("--skip-solve", action="store_true")
+    ap.add_argument("--per-wg", action="store_true", help="with --prof: SpMV time and matrix entries per workgroup")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     for n in a.n:
@@ -86,7 +98,7 @@ def main():
         out = {"n": n, "rows": A.n}
         tol = 1e-8 * float(torch.sqrt(torch.dot(b, w * b)))
         if a.prof:
-            out["prof"] = phase_profile(A, b, w, a.warm, a.iters)
+            out["prof"] = phase_profile(A, b, w, a.warm, a.iters, per_wg=a.per_wg)
         sol = {}
         for sched in (() if a.skip_solve else (2, 3)):
             t0 = time.perf_counter()

@@ -3,8 +3,9 @@
 
   * profiles/<tag>_kernel_stats.csv   : rocprofv3 --kernel-trace --stats summary (copied)
   * profiles/<tag>_summary.json       : per hot kernel, the average duration over the bench's timed region
-                                        (the last --steps dispatches) from the trace pass, and the HBM bytes per
-                                        launch from the separate FETCH_SIZE / WRITE_SIZE passes
+                                        (the last --steps dispatches; persistent schedule: the last dispatch,
+                                        divided by --steps iterations) from the trace pass, and the HBM bytes per
+                                        launch (per iteration) from the separate FETCH_SIZE / WRITE_SIZE passes
   * profiles/pmc_traffic.json         : {workload: {"bytes_per_launch": ...}} read by bench.py (roofline.traffic)
 
 HBM bytes per the MI355X guide's rocprofv3 recipe: FETCH_SIZE and WRITE_SIZE are kilobytes; on gfx950 FETCH_SIZE
@@ -22,6 +23,8 @@ import statistics
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS_3K = {"spmv_dot": "k_pcg_spmv_dot", "update": "k_pcg_update(", "pupdate": "k_pcg_pupdate"}
 KERNELS_DEFERRED = {"spmv_dot": "k_pcg_d1", "update": "k_pcg_d2", "pupdate": "k_pcg_d3"}
+# persistent schedule: the bench's K timed steps are ONE dispatch; durations and bytes are divided by K (per iteration)
+KERNELS_PERSIST = {"spmv_dot": "k_pcg_persist"}
 
 
 def bench_line(prof):
@@ -63,12 +66,16 @@ def main():
                 os.path.join(ROOT, "profiles", f"{a.tag}_kernel_stats.csv"))
     trace = load_trace(os.path.join(prof, "trace", "run_kernel_trace.csv"))
     deferred = any("k_pcg_d1" in r["Kernel_Name"] for r in trace)
-    KERNELS = KERNELS_DEFERRED if deferred else KERNELS_3K
-    out = {"workload": a.workload, "timed_dispatches": a.steps, "kernels": {}, "bench_line": bl}
+    persist = any("k_pcg_persist" in r["Kernel_Name"] for r in trace)
+    KERNELS = KERNELS_PERSIST if persist else (KERNELS_DEFERRED if deferred else KERNELS_3K)
+    ndisp = 1 if persist else a.steps      # dispatches of the timed region
+    per = a.steps if persist else 1        # iterations per dispatch
+    out = {"workload": a.workload, "timed_dispatches": ndisp, "iterations_per_dispatch": per, "kernels": {},
+           "bench_line": bl}
     for short, key in KERNELS.items():
-        rows = last_n(trace, key, a.steps)
+        rows = last_n(trace, key, ndisp)
         names = sorted({r["Kernel_Name"] for r in rows})
-        durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
+        durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 / per for r in rows]
         ent = {"kernel": names, "dispatches": len(durs), "avg_us": statistics.mean(durs) if durs else None,
                "median_us": statistics.median(durs) if durs else None}
         for counter, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
@@ -77,7 +84,7 @@ def main():
                 continue
             crow = [r for r in csv.DictReader(open(p)) if key in r["Kernel_Name"] and r["Counter_Name"] == counter]
             crow.sort(key=lambda r: int(r["Dispatch_Id"]))
-            vals = [float(r["Counter_Value"]) for r in crow[-a.steps:]]
+            vals = [float(r["Counter_Value"]) / per for r in crow[-ndisp:]]
             ent[counter + "_KB_avg"] = statistics.mean(vals) if vals else None
         if ent.get("FETCH_SIZE_KB_avg") is not None and ent.get("WRITE_SIZE_KB_avg") is not None:
             ent["hbm_bytes_per_launch"] = 2 * 1024 * ent["FETCH_SIZE_KB_avg"] + 1024 * ent["WRITE_SIZE_KB_avg"]
