@@ -1634,7 +1634,7 @@ int fem_pcg_create(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_
         return FEM_EARG;
     }
     fem_pcg* s = new fem_pcg();
-    s->tune = FEM_TUNE_REVERSE | FEM_TUNE_PAIR;
+    s->tune = FEM_TUNE_REVERSE | FEM_TUNE_PAIR | FEM_TUNE_PK_SC1;
     s->nrows = nrows;
     s->bs = bs;
     s->nslices = cdiv(nrows, 64);
@@ -1732,6 +1732,11 @@ int fem_pcg_get_schedule(fem_pcg* s) {
 
 static size_t pk_sync_words(int G) { return (size_t)(18 + G) * PK_LINE; }
 
+static const void* persist_fn(bool prof, bool gsc1) {
+    if (prof) return gsc1 ? (const void*)k_pcg_persist<PK_MAXS, true, true> : (const void*)k_pcg_persist<PK_MAXS, true, false>;
+    return gsc1 ? (const void*)k_pcg_persist<PK_MAXS, false, true> : (const void*)k_pcg_persist<PK_MAXS, false, false>;
+}
+
 // schedule 3 prerequisites: bs = 1, 16-bit columns + lane-paired copy, single GPU, no projections, capacity
 // (every wave <= PK_MAXS slices), one resident PK_T-thread workgroup per CU
 static int persist_setup(fem_pcg* s) {
@@ -1743,12 +1748,13 @@ static int persist_setup(fem_pcg* s) {
     FEM_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     const int G = (ncu / NXCD) * NXCD;
     if (G < NXCD || s->nslices > (int64_t)G * PK_WAVES * PK_MAXS) return FEM_OK;
-    int nb = 0, nbp = 0;
-    for (const void* f : {(const void*)k_pcg_persist<PK_MAXS, false>, (const void*)k_pcg_persist<PK_MAXS, true>})
+    for (int v = 0; v < 4; ++v) {
+        const void* f = persist_fn(v & 1, v & 2);
         FEM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)PK_LDS));
-    FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pcg_persist<PK_MAXS, false>, PK_T, PK_LDS));
-    FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nbp, k_pcg_persist<PK_MAXS, true>, PK_T, PK_LDS));
-    if (nb < 1 || nbp < 1) return FEM_OK;
+        int nb = 0;
+        FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, PK_T, PK_LDS));
+        if (nb < 1) return FEM_OK;
+    }
     if (s->pk_grid != G) {
         if (s->pk_win) (void)hipFree(s->pk_win);
         if (s->pk_part) (void)hipFree(s->pk_part);
@@ -1805,7 +1811,7 @@ static int launch_persist(fem_pcg* s, int k, unsigned long long* prof) {
     a.rev = (s->tune & FEM_TUNE_REVERSE) ? 1 : 0;
     a.prof = prof;
     void* args[] = {&a};
-    const void* fn = prof ? (const void*)k_pcg_persist<PK_MAXS, true> : (const void*)k_pcg_persist<PK_MAXS, false>;
+    const void* fn = persist_fn(prof != nullptr, (s->tune & FEM_TUNE_PK_SC1) != 0);
     FEM_HIP(hipLaunchKernel(fn, dim3(G), dim3(PK_T), args, PK_LDS, s->stream));
     FEM_LAUNCHED();
     s->launched += k;

@@ -151,7 +151,9 @@ struct PkArgs {
 // slot that exist (wave-uniform; < 64 only in the matrix's last slice)
 #define PK_ON(j) ((j) < nsl && lane < nrows - (s0 + (j)) * 64)
 
-template <int MAXS, bool PROF>
+// GSC1: the u gathers are sc1 loads and the u-flag wait needs no agent acquire (whose L2 invalidation by every
+// workgroup of an XCD can drop the gather window other workgroups are still reading)
+template <int MAXS, bool PROF, bool GSC1>
 __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
     unsigned long long pacc[PROF ? PK_NPROF : 1] = {};
     unsigned long long pt = 0;
@@ -239,7 +241,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
                     }
                     if (lane == 0) {
                         lds_ok = ok;
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                        if constexpr (!GSC1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     }
                 }
@@ -264,7 +266,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
 #pragma unroll
                 for (int j = 0; j < MAXS; ++j) {
                     if (j < nsl) {
-                        const double v = sell_row_pair<PK_U>(s0 + j, lane, slp, cop, vap, uvp);
+                        const double v = sell_row_pair<PK_U, GSC1>(s0 + j, lane, slp, cop, vap, uvp);
                         if (j < PK_VL) vl[j * 64] = v; else vv[j] = v;
                     }
                     asm volatile("" ::: "memory");
@@ -274,7 +276,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
                 for (int jj = 0; jj < MAXS; ++jj) {
                     const int j = MAXS - 1 - jj;
                     if (j < nsl) {
-                        const double v = sell_row_pair<PK_U>(s0 + j, lane, slp, cop, vap, uvp);
+                        const double v = sell_row_pair<PK_U, GSC1>(s0 + j, lane, slp, cop, vap, uvp);
                         if (j < PK_VL) vl[j * 64] = v; else vv[j] = v;
                     }
                     asm volatile("" ::: "memory");

@@ -28,8 +28,16 @@ static __global__ void k_sell_pair(int64_t nslices, const int64_t* __restrict__ 
 }
 
 
+// gathered x element: plain load, or (SC1) an agent-scope relaxed load (global_load sc1): the coherent form that
+// may replace the consumer's acquire when every producer store was sc1 (MI355X_MICROARCH.md, Valid forms)
+template <bool SC1>
+__device__ __forceinline__ double ldx(const double* p) {
+    if constexpr (SC1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *p;
+}
+
 // y_row (bs = 1) of one slice row in the paired layout; U pairs in flight
-template <int U>
+template <int U, bool SC1 = false>
 __device__ __forceinline__ double sell_row_pair(int64_t s, int lane, const int64_t* __restrict__ slice_ptr,
                                                 const int16_t* __restrict__ cols, const double* __restrict__ vals,
                                                 const double* __restrict__ x) {
@@ -51,8 +59,8 @@ __device__ __forceinline__ double sell_row_pair(int64_t s, int lane, const int64
 #pragma unroll
         for (int j = 0; j < U; ++j) {
             const int lo = (int)(int16_t)(cc[j] & 0xffff), hi = (int)(int16_t)(cc[j] >> 16);
-            x0[j] = (j0 + j < np) ? x[base + lo] : 0.0;
-            x1[j] = (j0 + j < np) ? x[base + hi] : 0.0;
+            x0[j] = (j0 + j < np) ? ldx<SC1>(x + (base + lo)) : 0.0;
+            x1[j] = (j0 + j < np) ? ldx<SC1>(x + (base + hi)) : 0.0;
         }
 #pragma unroll
         for (int j = 0; j < U; ++j)
@@ -63,7 +71,7 @@ __device__ __forceinline__ double sell_row_pair(int64_t s, int lane, const int64
     }
     if (w & 1) {
         const int64_t t = p0 + (int64_t)np * 128 + lane;
-        acc += vals[t] * x[base + (int)cols[t]];
+        acc += vals[t] * ldx<SC1>(x + (base + (int)cols[t]));
     }
     return acc;
 }

@@ -431,19 +431,21 @@ def test_persistent_schedule_matches_three_kernel(gpu, n, jitter):
 
 def test_persistent_chunks_are_bit_identical(gpu):
     """Chunk boundaries add no arithmetic: 4 launches of 9 iterations == one launch of 36, bit for bit, and the
-    poll reports the same state."""
+    poll reports the same state; both u hand-off forms (sc1 gathers, acquire + plain gathers) agree bit for bit."""
     _, mesh, _, system = _mods()
     A, b, mask = _poisson_case(system, mesh, 24, gpu)
     w = A.jacobi(mask)
     outs = []
-    for chunks in ((36,), (9, 9, 9, 9)):
+    for chunks, flags in (((36,), 7), ((9, 9, 9, 9), 7), ((36,), 3)):
         run = system.PcgRunner(A, b, w, tol=0.0, schedule=3)
+        run.set_tuning(flags)   # 7: sc1 gathers (default), 3: agent acquire + plain gathers
         run.start()
         for k in chunks:
             run.iterate(k)
         outs.append((run.poll(), run.x.clone()))
         run.close()
-    assert outs[0][0] == outs[1][0] and outs[0][0][0] == 36 and torch.equal(outs[0][1], outs[1][1])
+    assert outs[0][0] == outs[1][0] == outs[2][0] and outs[0][0][0] == 36
+    assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][1], outs[2][1])
 
 
 def test_persistent_full_geometry_10m(gpu):
@@ -464,6 +466,13 @@ def test_persistent_full_geometry_10m(gpu):
         xs.append((rz, run.x.clone()))
         run.close()
     assert rel(xs[1][1], xs[0][1]) < 1e-12 and abs(xs[1][0] - xs[0][0]) <= 1e-10 * abs(xs[0][0])
+    # the u hand-off through an agent acquire + plain gathers (FEM_TUNE_PK_SC1 off) gives the same bits
+    run = system.PcgRunner(A, b, w, tol=0.0, schedule=3)
+    run.set_tuning(3)
+    run.start()
+    run.iterate(50)
+    assert run.poll()[0] == 50 and torch.equal(run.x, xs[1][1])
+    run.close()
     tol = 1e-8 * float(torch.sqrt(torch.dot(b, w * b)))
     r2 = A.pcg(b, w=w, tol=tol, max_iter=3000, schedule=2)
     r3 = A.pcg(b, w=w, tol=tol, max_iter=3000, schedule=3)

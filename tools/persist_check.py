@@ -29,8 +29,10 @@ def case(n, dev):
     return A, b, w
 
 
-def rate(A, b, w, sched, warm, iters, chunk):
+def rate(A, b, w, sched, warm, iters, chunk, tune=None):
     run = system.PcgRunner(A, b, w, tol=0.0, schedule=sched)
+    if tune is not None:
+        run.set_tuning(tune)
     run.start()
     eff = run.effective_schedule()
     run.iterate(warm)
@@ -53,11 +55,13 @@ def rate(A, b, w, sched, warm, iters, chunk):
 PHASES = ("u_wait", "spmv", "block_sum", "barrier_sums", "step", "update_flag")
 
 
-def phase_profile(A, b, w, warm, iters, ghz=2.4, per_wg=False):
+def phase_profile(A, b, w, warm, iters, ghz=2.4, per_wg=False, tune=None):
     """Per-iteration phase times (us at `ghz` shader clock) of the instrumented persistent kernel: mean and max over
     workgroups."""
     import ctypes
     run = system.PcgRunner(A, b, w, tol=0.0, schedule=3)
+    if tune is not None:
+        run.set_tuning(tune)
     run.start()
     assert run.effective_schedule() == 3
     run.iterate(warm)
@@ -90,6 +94,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=500)
     ap.add_argument("--prof", action="store_true", help="phase breakdown of the instrumented persistent kernel")
     ap.add_argument("--skip-solve", action="store_true")
+    ap.add_argument("--tune", type=int, nargs="*", default=[], help="extra FEM_TUNE_* flag sets for schedule 3")
     ap.add_argument("--per-wg", action="store_true", help="with --prof: SpMV time and matrix entries per workgroup")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -113,6 +118,12 @@ def main():
         for sched in (2, 3):
             out[f"rate{sched}"], xs[sched] = rate(A, b, w, sched, a.warm, a.iters, a.chunk)
         out["rate_dx_rel"] = float((xs[2] - xs[3]).norm() / xs[2].norm())
+        for t in a.tune:   # extra tuning-flag sets of the persistent schedule (FEM_TUNE_*), x compared bitwise
+            out[f"rate3_t{t}"], xt = rate(A, b, w, 3, a.warm, a.iters, a.chunk, tune=t)
+            out[f"rate3_t{t}"]["x_equal"] = bool(torch.equal(xt, xs[3]))
+            out[f"rate3_t{t}"]["dx_rel"] = float((xt - xs[3]).norm() / xs[3].norm())
+            if a.prof:
+                out[f"prof_t{t}"] = phase_profile(A, b, w, a.warm, a.iters, tune=t)
         print(json.dumps(out), flush=True)
 
 
