@@ -44,6 +44,16 @@ constexpr int PK_VL = 5;                 // slots of v = A u kept in LDS (the re
 constexpr size_t PK_LDS = PK_LDS_HEAD + sizeof(double) * (2 * PK_MAXS + PK_VL) * PK_WAVES * 64;
 static_assert(PK_LDS <= 160 * 1024, "persistent PCG: LDS over the 160 KB of a CU");
 
+// an opaque copy of a global pointer (the compiler cannot hoist address arithmetic on it out of the iteration loop)
+// that keeps its address space: laundering a generic pointer turns every access through it into a FLAT access
+// (lgkmcnt-coupled, and `flat_` sc1 loads are not a valid hand-off form, MI355X_MICROARCH.md)
+template <class T>
+__device__ __forceinline__ T* pk_launder(T* p) {
+    __attribute__((address_space(1))) T* q = (__attribute__((address_space(1))) T*)p;
+    asm volatile("" : "+s"(q));
+    return (T*)q;
+}
+
 __device__ __forceinline__ unsigned pk_ld(const unsigned* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -257,11 +267,10 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
             const bool rv = a.rev && ((it & 1) != 0);
             // launder the matrix pointers every iteration: otherwise the per-slot addresses are hoisted out of the
             // k loop and held in VGPRs across it (7 slots x ~6 registers -> spills)
-            const int64_t* slp = a.slice_ptr;
-            const int16_t* cop = a.cols;
-            const double* vap = a.vals;
-            const double* uvp = a.u;
-            asm volatile("" : "+s"(slp), "+s"(cop), "+s"(vap), "+s"(uvp));
+            const int64_t* slp = pk_launder(a.slice_ptr);
+            const int16_t* cop = pk_launder(a.cols);
+            const double* vap = pk_launder(a.vals);
+            const double* uvp = pk_launder(a.u);
             if (!rv) {
 #pragma unroll
                 for (int j = 0; j < MAXS; ++j) {
@@ -353,8 +362,8 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
             double gp = 0.0;
             // per-slot store addresses recomputed every iteration (hoisted out of the k loop they are spilled)
             unsigned rbi = rb;
-            double* ust = a.u;
-            asm volatile("" : "+v"(rbi), "+s"(ust));
+            double* ust = pk_launder(a.u);
+            asm volatile("" : "+v"(rbi));
 #pragma unroll
             for (int j = 0; j < MAXS; ++j) {
                 // branch-free over the lanes (rows past nrows hold zeros: their SpMV rows are zero padding); only
