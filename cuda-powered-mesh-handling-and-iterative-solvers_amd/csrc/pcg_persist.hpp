@@ -62,7 +62,7 @@ __device__ __forceinline__ void pk_st(unsigned* p, unsigned v) {
 }
 
 // one lane spins until *p >= target; false on give-up (own or another spinner's)
-__device__ __noinline__ bool pk_wait_ge(const unsigned* p, unsigned target, unsigned* tmo) {
+__device__ __forceinline__ bool pk_wait_ge(const unsigned* p, unsigned target, unsigned* tmo) {
     for (unsigned spins = 0;; ++spins) {
         if (pk_ld(p) >= target) return true;
         if ((spins & 63) == 63 && pk_ld(tmo)) return false;
