@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--force-dist", action="store_true", help="run the RCCL element-partitioned path even at N=1")
     ap.add_argument("--dist-variant", type=int, default=1,
                     help="N>1: 1 = single-reduction PCG (one all-reduce per iteration), 0 = two reductions")
+    ap.add_argument("--dist-exchange", default="p2p", choices=["p2p", "allreduce"],
+                    help="N>1 single-reduction exchange: grouped ncclSend/Recv with every other rank + fixed-order sum "
+                         "(p2p), or one all-reduce over the global interface vector")
     ap.add_argument("--dist-graph", type=int, default=50,
                     help="distributed path: capture k iterations (kernels + RCCL) per hipGraph, 0 = plain launches")
     return ap.parse_args()

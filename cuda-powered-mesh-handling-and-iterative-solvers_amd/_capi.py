@@ -119,6 +119,9 @@ SIGNATURES = {
     "fem_halo_unpack": (_I, [_P, _I, _P, _L, _P, _P]),
     "fem_pcg_set_dist": (_I, [_P, _I, _P, _L, _P, _P, _P]),
     "fem_pcg_set_dist_variant": (_I, [_P, _I]),
+    "fem_pcg_set_p2p": (_I, [_P, _I, _I, _P, _P, _P, _P]),
+    "fem_pcg_p2p_buffers": (_I, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_L)]),
+    "fem_p2p_deliver": (_I, [_P, _I, _P]),
     "fem_pcg_dist_phase": (_I, [_P, _I]),
     "fem_pcg_dist_buffer": (_I, [_P, _I, ctypes.POINTER(_P), ctypes.POINTER(_L)]),
     "fem_group_allreduce": (_I, [_P, _I, _L, _P]),

@@ -732,13 +732,37 @@ __global__ void k_bank_init(PcgState* st) {
 //   k_cg1_step   (1 thread) : stop test on g of the last update, beta, p.Ap, alpha, guards; iter += 1
 //   k_cg1_update (grid)     : p, s, x, r, u; g partial of the new iterate -> st->red[1]
 //   k_cg1_spmv   (grid)     : v = A u (local), d partial; interface rows of v and [g, d] -> send
-__global__ void k_cg1_step(PcgState* st, const double* __restrict__ recv, int64_t off, double* hist,
-                           int64_t hist_len) {
+// neighbour exchange (fem_pcg_set_p2p) seen by the single-reduction kernels; P = 0: all-reduce path. Message
+// slots are symmetric (the slot for peer r holds the same nodes in the same order in psend and precv), so one table
+// serves both directions: csrc[J P + r] = offset of node J's component 0 in rank r's slot (-1: this rank, -2: r does
+// not touch J), ssrc[r] = offset of rank r's [g, d] (-1: this rank).
+struct P2PArgs {
+    int P;
+    const int32_t* csrc;
+    const int32_t* ssrc;
+    double* psend;
+    const double* precv;
+};
+
+// rank-ordered sum of the [g, d] pairs (p2p) or the all-reduced pair
+__device__ __forceinline__ double cg1_scalar(const double* recv, const double* send, int64_t off, int k,
+                                             const P2PArgs& x) {
+    if (!x.P) return recv[off + k];
+    double acc = 0.0;
+    for (int r = 0; r < x.P; ++r) {
+        const int src = x.ssrc[r];
+        acc += (src < 0) ? send[off + k] : x.precv[src + k];
+    }
+    return acc;
+}
+
+__global__ void k_cg1_step(PcgState* st, const double* __restrict__ recv, const double* __restrict__ send,
+                           int64_t off, double* hist, int64_t hist_len, P2PArgs x) {
     st->xupd = 0;
     if (st->halt) return;
     const int it = st->iter;
     const bool cg = st->mode != FEM_MODE_PCG;
-    const double g = recv[off], d = recv[off + 1];
+    const double g = cg1_scalar(recv, send, off, 0, x), d = cg1_scalar(recv, send, off, 1, x);
     double beta = 0.0;
     if (it > 0) {
         st->rz_new = g;
@@ -796,7 +820,7 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_update(int64_t n, int bs, dou
                                                           const double* __restrict__ recv,
                                                           const int32_t* __restrict__ ipos,
                                                           const uint8_t* __restrict__ own, PcgState* __restrict__ st,
-                                                          RedBuf red) {
+                                                          RedBuf red, P2PArgs xp) {
     __shared__ double lds4[4];
     __shared__ int flag;
     if (!st->xupd) return;
@@ -806,7 +830,21 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_update(int64_t n, int bs, dou
     for (int64_t i = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * PCG_BLOCK) {
         const int64_t node = i / bs;
         const int32_t j = ipos ? ipos[node] : -1;
-        const double vi = (j >= 0) ? recv[(int64_t)j * bs + (i - node * bs)] : v[i];
+        double vi = v[i];
+        if (j >= 0) {
+            const int c = (int)(i - node * bs);
+            if (xp.P) {   // rank-ordered sum of the partials (own partial = the local row itself)
+                double acc = 0.0;
+                for (int r = 0; r < xp.P; ++r) {
+                    const int src = xp.csrc[(int64_t)j * xp.P + r];
+                    if (src == -1) acc += vi;
+                    else if (src >= 0) acc += xp.precv[src + c];
+                }
+                vi = acc;
+            } else {
+                vi = recv[(int64_t)j * bs + c];
+            }
+        }
         const double pi = u[i] + beta * p[i];
         const double si = vi + beta * sv[i];
         p[i] = pi;
@@ -860,7 +898,7 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_spmv(int64_t nslices, int64_t
                                                         const double* __restrict__ u, double* __restrict__ v,
                                                         const int32_t* __restrict__ ipos, double* __restrict__ send,
                                                         int64_t off, PcgState* __restrict__ st, RedBuf red,
-                                                        int always, int tune_rev) {
+                                                        int always, int tune_rev, P2PArgs xp) {
     __shared__ double lds4[4];
     __shared__ int flag;
     if (!always && !st->xupd) return;
@@ -883,7 +921,16 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_spmv(int64_t nslices, int64_t
             for (int c = 0; c < BS; ++c) {
                 v[row * BS + c] = o[c];
                 dot += u[row * BS + c] * o[c];
-                if (j >= 0) send[(int64_t)j * BS + c] = o[c];
+                if (j >= 0) {
+                    if (xp.P) {   // straight into every peer's message slot for this node
+                        for (int r = 0; r < xp.P; ++r) {
+                            const int dst = xp.csrc[(int64_t)j * xp.P + r];
+                            if (dst >= 0) xp.psend[dst + c] = o[c];
+                        }
+                    } else {
+                        send[(int64_t)j * BS + c] = o[c];
+                    }
+                }
             }
         }
     }
@@ -893,6 +940,13 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_spmv(int64_t nslices, int64_t
         st->red[0] = d;
         send[off] = st->red[1];
         send[off + 1] = d;
+        for (int r = 0; r < xp.P; ++r) {
+            const int dst = xp.ssrc[r];
+            if (dst >= 0) {
+                xp.psend[dst] = st->red[1];
+                xp.psend[dst + 1] = d;
+            }
+        }
     }
 }
 
@@ -1062,6 +1116,17 @@ struct fem_pcg {
     double* cg1_u;
     double* cg1_send;
     double* cg1_recv;
+    // neighbour exchange (fem_pcg_set_p2p): the single-reduction all-reduce replaced by grouped send/recv with every
+    // other rank ([g, d | shared interface rows] per peer) and a fixed-rank-order sum into cg1_recv
+    int p2p;
+    int p2p_nranks;
+    std::vector<int> peer_rank;
+    std::vector<int64_t> peer_off, peer_cnt;   // doubles, into psend / precv
+    int64_t p2p_total;
+    const int32_t* p2p_csrc;   // [nI][nranks] slot offset of node J's component 0 for rank r, -1 own, -2 absent
+    const int32_t* p2p_ssrc;   // [nranks] precv offset of rank r's [g, d], -1 own
+    double* psend;
+    double* precv;
     // persistent schedule (3): requested by fem_pcg_set_schedule, active after fem_pcg_start when supported
     int persist_req;
     int persist;
@@ -1161,13 +1226,25 @@ static int halo_pack(fem_pcg* s, const double* v, bool guarded, bool scalar) {
 // group sum sees this rank's buffer, the RCCL path all-reduces send -> recv out of place
 static int64_t cg1_len(const fem_pcg* s) { return s->nI * s->bs + 2; }
 
+static P2PArgs p2p_args(const fem_pcg* s) {
+    P2PArgs x{};
+    if (s->p2p) {
+        x.P = s->p2p_nranks;
+        x.csrc = s->p2p_csrc;
+        x.ssrc = s->p2p_ssrc;
+        x.psend = s->psend;
+        x.precv = s->precv;
+    }
+    return x;
+}
+
 static int cg1_spmv(fem_pcg* s, int always) {
     const int64_t off = s->nI * s->bs;
     const int32_t* ipos = s->nI > 0 ? s->ipos : nullptr;
 #define FEM_CG1(B, CI, PR, C, V)                                                                                   \
     hipLaunchKernelGGL((k_cg1_spmv<B, CI, PR>), dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream, s->nslices,     \
                        s->nrows, s->slice_ptr, C, V, s->cg1_u, s->q, ipos, s->cg1_send, off, s->st, s->red, always, \
-                       s->tune & FEM_TUNE_REVERSE)
+                       s->tune & FEM_TUNE_REVERSE, p2p_args(s))
     if (s->paired && s->bs == 1) FEM_CG1(1, int16_t, true, pcols(s), s->pvals);
     else if (s->paired) FEM_CG1(3, int16_t, true, pcols(s), s->pvals);
     else if (s->cols16 && s->bs == 1) FEM_CG1(1, int16_t, false, s->cols16, s->vals);
@@ -1176,6 +1253,7 @@ static int cg1_spmv(fem_pcg* s, int always) {
     else FEM_CG1(3, int32_t, false, s->cols, s->vals);
 #undef FEM_CG1
     FEM_LAUNCHED();
+    if (!s->comm && s->p2p) return FEM_OK;   // group path: the caller moves psend -> peers' precv
     if (!s->comm)
         FEM_HIP(hipMemcpyAsync(s->cg1_recv, s->cg1_send, sizeof(double) * (size_t)cg1_len(s), hipMemcpyDeviceToDevice,
                                s->stream));
@@ -1183,12 +1261,12 @@ static int cg1_spmv(fem_pcg* s, int always) {
 }
 
 static int cg1_step_update(fem_pcg* s) {
-    hipLaunchKernelGGL(k_cg1_step, dim3(1), dim3(1), 0, s->stream, s->st, s->cg1_recv, s->nI * s->bs, s->hist,
-                       s->hist_len);
+    hipLaunchKernelGGL(k_cg1_step, dim3(1), dim3(1), 0, s->stream, s->st, s->cg1_recv, s->cg1_send, s->nI * s->bs,
+                       s->hist, s->hist_len, p2p_args(s));
     FEM_LAUNCHED();
     hipLaunchKernelGGL(k_cg1_update, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->bs, s->x, s->r, s->p0,
                        s->cg1_s, s->cg1_u, s->q, s->w, s->cg1_recv, s->nI > 0 ? s->ipos : nullptr, s->own, s->st,
-                       s->red);
+                       s->red, p2p_args(s));
     FEM_LAUNCHED();
     return FEM_OK;
 }
@@ -1267,13 +1345,30 @@ static void dist_buffer(fem_pcg* s, int phase, double** ptr, int64_t* n) {
     } else if (phase == 11) {
         *ptr = st_red(s, 2);
         *n = 1;
-    } else if (s->cg1 && (phase == 4 || phase == 20)) {
+    } else if (s->cg1 && !s->p2p && (phase == 4 || phase == 20)) {
         *ptr = s->cg1_recv;       // group path: summed in place (cg1_spmv copied send -> recv)
         *n = cg1_len(s);
     }
 }
 
 static int dist_exchange(fem_pcg* s, int phase) {
+    if (s->cg1 && s->p2p && (phase == 4 || phase == 20)) {
+        if (!s->comm) {
+            set_error("distributed PCG without a communicator: drive it with fem_pcg_dist_phase");
+            return FEM_EARG;
+        }
+        if (!s->peer_rank.empty()) {
+            FEM_NCCL(ncclGroupStart());
+            for (size_t i = 0; i < s->peer_rank.size(); ++i) {
+                FEM_NCCL(ncclSend(s->psend + s->peer_off[i], (size_t)s->peer_cnt[i], ncclFloat64, s->peer_rank[i],
+                                  s->comm, s->stream));
+                FEM_NCCL(ncclRecv(s->precv + s->peer_off[i], (size_t)s->peer_cnt[i], ncclFloat64, s->peer_rank[i],
+                                  s->comm, s->stream));
+            }
+            FEM_NCCL(ncclGroupEnd());
+        }
+        return FEM_OK;   // the next step / update kernels sum the messages in rank order
+    }
     double* p;
     int64_t n;
     dist_buffer(s, phase, &p, &n);
@@ -1998,6 +2093,7 @@ int fem_pcg_set_dist(fem_pcg* s, int enable, void* comm, int64_t nI, const int32
         *b = nullptr;
     }
     s->cg1 = 0;
+    s->p2p = 0;
     s->dist = enable ? 1 : 0;
     s->comm = enable ? (ncclComm_t)comm : nullptr;
     s->nI = nI;
@@ -2018,6 +2114,7 @@ int fem_pcg_set_dist_variant(fem_pcg* s, int variant) {
         *b = nullptr;
     }
     s->cg1 = variant;
+    s->p2p = 0;   // maps refer to the single-reduction buffers: set them again after the variant
     if (variant == 1) {
         FEM_HIP(hipMalloc(&s->cg1_s, sizeof(double) * (size_t)s->n));
         FEM_HIP(hipMalloc(&s->cg1_u, sizeof(double) * (size_t)s->n));
@@ -2026,6 +2123,69 @@ int fem_pcg_set_dist_variant(fem_pcg* s, int variant) {
         FEM_HIP(hipMemset(s->cg1_send, 0, sizeof(double) * (size_t)cg1_len(s)));   // non-local interface nodes
         FEM_HIP(hipMemset(s->cg1_recv, 0, sizeof(double) * (size_t)cg1_len(s)));
     }
+    return FEM_OK;
+}
+
+int fem_pcg_set_p2p(fem_pcg* s, int nranks, int npeer, const int* peer_rank, const int64_t* peer_cnt,
+                    const int32_t* csrc, const int32_t* ssrc) {
+    if (!s->dist || !s->cg1 || s->graph || nranks < 1 || npeer < 0 || npeer >= nranks) {
+        set_error("fem_pcg_set_p2p: needs a single-reduction distributed context without a captured graph");
+        return FEM_EARG;
+    }
+    if (s->psend) (void)hipFree(s->psend);
+    if (s->precv) (void)hipFree(s->precv);
+    s->psend = s->precv = nullptr;
+    s->peer_rank.assign(peer_rank, peer_rank + npeer);
+    s->peer_cnt.assign(peer_cnt, peer_cnt + npeer);
+    s->peer_off.resize(npeer);
+    int64_t tot = 0;
+    for (int i = 0; i < npeer; ++i) {
+        if (peer_cnt[i] < 2) {
+            set_error("fem_pcg_set_p2p: every message carries the [g, d] pair (count >= 2)");
+            return FEM_EARG;
+        }
+        s->peer_off[i] = tot;
+        tot += peer_cnt[i];
+    }
+    s->p2p_total = tot;
+    s->p2p_nranks = nranks;
+    s->p2p_csrc = csrc;
+    s->p2p_ssrc = ssrc;
+    if (tot > 0) {
+        FEM_HIP(hipMalloc(&s->psend, sizeof(double) * (size_t)tot));
+        FEM_HIP(hipMalloc(&s->precv, sizeof(double) * (size_t)tot));
+    }
+    s->p2p = 1;
+    return FEM_OK;
+}
+
+int fem_p2p_deliver(fem_pcg* const* ctx, int P, fem_stream_t stream) {
+    for (int a = 0; a < P; ++a) {
+        const fem_pcg* A = ctx[a];
+        if (!A->p2p || A->p2p_nranks != P) {
+            set_error("fem_p2p_deliver: context %d has no neighbour exchange over %d ranks", a, P);
+            return FEM_EARG;
+        }
+        for (size_t i = 0; i < A->peer_rank.size(); ++i) {
+            const int b = A->peer_rank[i];
+            const fem_pcg* B = ctx[b];
+            size_t j = 0;
+            while (j < B->peer_rank.size() && B->peer_rank[j] != a) ++j;
+            if (j == B->peer_rank.size() || B->peer_cnt[j] != A->peer_cnt[i]) {
+                set_error("fem_p2p_deliver: ranks %d and %d disagree on their message", a, b);
+                return FEM_EARG;
+            }
+            FEM_HIP(hipMemcpyAsync(B->precv + B->peer_off[j], A->psend + A->peer_off[i],
+                                   sizeof(double) * (size_t)A->peer_cnt[i], hipMemcpyDeviceToDevice, S(stream)));
+        }
+    }
+    return FEM_OK;
+}
+
+int fem_pcg_p2p_buffers(fem_pcg* s, double** psend, double** precv, int64_t* total) {
+    *psend = s->psend;
+    *precv = s->precv;
+    *total = s->p2p_total;
     return FEM_OK;
 }
 
@@ -2238,6 +2398,8 @@ void fem_pcg_destroy(fem_pcg* s) {
     if (s->cg1_u) (void)hipFree(s->cg1_u);
     if (s->cg1_send) (void)hipFree(s->cg1_send);
     if (s->cg1_recv) (void)hipFree(s->cg1_recv);
+    if (s->psend) (void)hipFree(s->psend);
+    if (s->precv) (void)hipFree(s->precv);
     if (s->con.tmp) (void)hipFree(s->con.tmp);
     if (s->pvals) (void)hipFree(s->pvals);
     if (s->pcols16) (void)hipFree(s->pcols16);

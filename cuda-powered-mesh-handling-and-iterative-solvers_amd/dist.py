@@ -34,6 +34,9 @@ F64, I32, LONG = torch.float64, torch.int32, torch.long
 # distributed iteration: 0 = two reductions (halo + p.q, then r.z), 1 = single reduction (Chronopoulos-Gear form,
 # one all-reduce of [interface rows of A u | r.z | u.Au] per iteration; csrc/pcg.hip k_cg1_*)
 VARIANT_TWO, VARIANT_SINGLE = 0, 1
+# exchange of the single-reduction variant: the all-reduce over the GLOBAL interface vector, or grouped
+# ncclSend/ncclRecv of [g, d | rows shared with that rank] with every other rank + a fixed-rank-order sum
+EXCHANGE_ALLREDUCE, EXCHANGE_P2P = "allreduce", "p2p"
 
 
 # ============================================================================ partition (host logic, any device)
@@ -91,6 +94,52 @@ def node_sharing(elements, part, nparts, n_nodes):
     return count, owner
 
 
+def touch_masks(elements, part, nparts, n_nodes):
+    """[nparts, n_nodes] bool: rank r has an element on the node."""
+    dev = elements.device
+    t = torch.zeros((nparts, n_nodes), dtype=torch.bool, device=dev)
+    for r in range(nparts):
+        t[r, elements[part == r].reshape(-1)] = True
+    return t
+
+
+@dataclass
+class P2PMaps:
+    """Neighbour-exchange maps of one rank (fem_pcg_set_p2p): messages to/from every other rank, ascending."""
+    nranks: int
+    peer_rank: list
+    peer_cnt: list            # doubles per message: 2 + bs * shared nodes
+    csrc: torch.Tensor        # int32 [nI, nranks] slot offset of node J's component 0 for rank r (-1 own, -2 absent)
+    ssrc: torch.Tensor        # int32 [nranks] slot offset of rank r's [g, d] (-1 own)
+
+
+def p2p_maps(rm: RankMesh, touch: torch.Tensor, bs: int) -> P2PMaps:
+    """Messages of rank rm.rank to/from each other rank b: [g, d] then bs values per node shared by both, nodes in
+    ascending global interface index J (the same order on both sides, so one slot layout serves sending and
+    receiving). For every J this rank holds: the slot offset of each other rank that also holds it (rank order is
+    the summation order on every rank: shared dofs stay bit-identical)."""
+    a, P = rm.rank, rm.nparts
+    dev = touch.device
+    iface = torch.nonzero(touch.sum(0) > 1, as_tuple=True)[0]          # global interface nodes, J order
+    tif = touch[:, iface]                                               # [P, nI]
+    nI = int(iface.numel())
+    peers = [b for b in range(P) if b != a]
+    csrc = torch.full((nI, P), -2, dtype=LONG, device=dev)
+    csrc[tif[a], a] = -1
+    ssrc = torch.full((P,), -1, dtype=LONG, device=dev)
+    cnt = []
+    tot = 0
+    for b in peers:
+        S = torch.nonzero(tif[a] & tif[b], as_tuple=True)[0]           # J, ascending
+        csrc[S, b] = tot + 2 + bs * torch.arange(S.numel(), device=dev)
+        ssrc[b] = tot
+        cnt.append(2 + bs * int(S.numel()))
+        tot += cnt[-1]
+    if tot >= 2 ** 31:
+        raise ValueError("neighbour exchange: message offsets overflow int32")
+    return P2PMaps(P, peers, cnt, csrc.to(I32).contiguous(), ssrc.to(I32).contiguous())
+
+
 def rank_mesh(elements, part, rank, nparts, n_nodes, sharing=None) -> RankMesh:
     count, owner = sharing if sharing is not None else node_sharing(elements, part, nparts, n_nodes)
     ids = torch.nonzero(part == rank, as_tuple=True)[0]
@@ -114,10 +163,13 @@ class DistSystem:
     """One rank's share: local SELL operator + halo maps. `comm` = RCCL communicator (None: phase-driven)."""
 
     def __init__(self, coords, elements, part, rank, nparts, kind="poisson", E=1.0, nu=0.0, comm=None,
-                 sharing=None):
+                 sharing=None, touch=None):
         self.lib = C.lib()
         self.dev = coords.device
         self.rm = rank_mesh(elements, part, rank, nparts, coords.shape[0], sharing)
+        self._touch = touch
+        self._elements, self._part, self._n_nodes = elements, part, coords.shape[0]
+        self._p2p = None
         self.comm = comm
         lc = coords[self.rm.nodes].contiguous()
         self.A = _sys.assemble_tet4_system(lc, self.rm.conn, kind, E, nu)
@@ -161,14 +213,22 @@ class DistSystem:
                 "fem_halo_sum")
         return self.jacobi_from(d, fixed_mask_local)
 
-    def runner(self, b, w, tol=0.0, mode=C.MODE_PCG, hist_len=0, variant=VARIANT_SINGLE):
-        return DistRunner(self, b, w, tol, mode, hist_len, variant)
+    def p2p(self):
+        """Neighbour-exchange maps of this rank (built once; device int32 tensors kept alive here)."""
+        if self._p2p is None:
+            t = self._touch if self._touch is not None else touch_masks(self._elements, self._part, self.rm.nparts,
+                                                                        self._n_nodes)
+            self._p2p = p2p_maps(self.rm, t, self.bs)
+        return self._p2p
+
+    def runner(self, b, w, tol=0.0, mode=C.MODE_PCG, hist_len=0, variant=VARIANT_SINGLE, exchange=EXCHANGE_ALLREDUCE):
+        return DistRunner(self, b, w, tol, mode, hist_len, variant, exchange)
 
 
 class DistRunner(_sys._DistMarker, _sys.PcgRunner):
     """(P)CG context of one rank in distributed mode."""
 
-    def __init__(self, ds: DistSystem, b, w, tol, mode, hist_len=0, variant=None):
+    def __init__(self, ds: DistSystem, b, w, tol, mode, hist_len=0, variant=None, exchange=EXCHANGE_ALLREDUCE):
         super().__init__(ds.A, b, w, mode=mode, tol=tol)
         self.ds = ds
         self.hist = torch.full((max(hist_len, 1),), float("nan"), dtype=F64, device=ds.dev) if hist_len else None
@@ -176,6 +236,11 @@ class DistRunner(_sys._DistMarker, _sys.PcgRunner):
                                           C.ptr(ds.rm.own)), "fem_pcg_set_dist")
         self.variant = VARIANT_SINGLE if variant is None else int(variant)
         C.check(self.lib.fem_pcg_set_dist_variant(self.h, self.variant), "fem_pcg_set_dist_variant")
+        self.exchange = exchange
+        if exchange == EXCHANGE_P2P:
+            if self.variant != VARIANT_SINGLE:
+                raise ValueError("the neighbour exchange needs the single-reduction variant")
+            set_p2p(self.lib, self.h, ds.p2p())
 
     def phase(self, k):
         C.check(self.lib.fem_pcg_dist_phase(self.h, int(k)), "fem_pcg_dist_phase")
@@ -195,8 +260,9 @@ class PartitionGroup:
         self.lib = C.lib()
         part = rcb_partition(element_centroids(coords, elements), nparts)
         sharing = node_sharing(elements, part, nparts, coords.shape[0])
+        touch = touch_masks(elements, part, nparts, coords.shape[0])
         self.part = part
-        self.ranks = [DistSystem(coords, elements, part, r, nparts, kind, E, nu, None, sharing)
+        self.ranks = [DistSystem(coords, elements, part, r, nparts, kind, E, nu, None, sharing, touch)
                       for r in range(nparts)]
         self.dev = coords.device
 
@@ -216,17 +282,26 @@ class PartitionGroup:
             out.append(r.jacobi_from(d, m))
         return out
 
-    def solve(self, bs_local, ws, tol, max_iter, mode=C.MODE_PCG, variant=None):
+    def deliver(self, runs):
+        """Neighbour exchange without RCCL: every rank's message to b lands in b's receive slot for it."""
+        arr = (ctypes.c_void_p * len(runs))(*[run.h.value for run in runs])
+        C.check(self.lib.fem_p2p_deliver(arr, len(runs), C.stream(self.dev)), "fem_p2p_deliver")
+
+    def solve(self, bs_local, ws, tol, max_iter, mode=C.MODE_PCG, variant=None, exchange=EXCHANGE_ALLREDUCE):
         """Phase-driven (P)CG over the P partitions; returns (per-rank x, iterations, status)."""
         # every context on the current stream: the phases of all ranks and the group sums serialise in order
         variant = VARIANT_SINGLE if variant is None else int(variant)
-        runs = [_GroupRunner(r, b, w, tol, mode, variant) for r, b, w in zip(self.ranks, bs_local, ws)]
+        runs = [_GroupRunner(r, b, w, tol, mode, variant, exchange) for r, b, w in zip(self.ranks, bs_local, ws)]
         for run in runs:
             run.start_state()
+        p2p = exchange == EXCHANGE_P2P
 
         def step(ph):
             for run in runs:
                 run.phase(ph)
+            if p2p and ph in (4, 20):
+                self.deliver(runs)
+                return
             p0, n0 = runs[0].buffer(ph)
             if n0:
                 self.group_sum([run.buffer(ph)[0] for run in runs], n0)
@@ -256,7 +331,7 @@ class PartitionGroup:
 class _GroupRunner:
     """Distributed (P)CG context on the current stream, driven phase by phase by PartitionGroup."""
 
-    def __init__(self, ds: DistSystem, b, w, tol, mode, variant=0):
+    def __init__(self, ds: DistSystem, b, w, tol, mode, variant=0, exchange=EXCHANGE_ALLREDUCE):
         self.lib = C.lib()
         A = ds.A
         self.b = b.to(F64).contiguous()
@@ -271,6 +346,8 @@ class _GroupRunner:
         C.check(self.lib.fem_pcg_set_dist(self.h, 1, None, ds.rm.n_iface, C.ptr(ds.rm.imap), C.ptr(ds.rm.ipos),
                                           C.ptr(ds.rm.own)), "fem_pcg_set_dist")
         C.check(self.lib.fem_pcg_set_dist_variant(self.h, int(variant)), "fem_pcg_set_dist_variant")
+        if exchange == EXCHANGE_P2P:
+            set_p2p(self.lib, self.h, ds.p2p())
 
     def start_state(self):
         C.check(self.lib.fem_pcg_start(self.h), "fem_pcg_start")   # state only (phases do the work)
@@ -292,6 +369,13 @@ class _GroupRunner:
         if self.h:
             self.lib.fem_pcg_destroy(self.h)
             self.h = ctypes.c_void_p()
+
+
+def set_p2p(lib, h, m: P2PMaps):
+    npeer = len(m.peer_rank)
+    ranks = (ctypes.c_int * max(npeer, 1))(*m.peer_rank)
+    cnts = (ctypes.c_int64 * max(npeer, 1))(*m.peer_cnt)
+    C.check(lib.fem_pcg_set_p2p(h, m.nranks, npeer, ranks, cnts, C.ptr(m.csrc), C.ptr(m.ssrc)), "fem_pcg_set_p2p")
 
 
 def gather_solution(ranks, xs, n_nodes, bs):
@@ -398,7 +482,8 @@ def bench_main(a, metric):
             return 0
 
     variant = int(getattr(a, "dist_variant", VARIANT_SINGLE))
-    run = ds.runner(b, w, tol=tol, variant=variant)
+    exchange = getattr(a, "dist_exchange", EXCHANGE_ALLREDUCE) if variant == VARIANT_SINGLE else EXCHANGE_ALLREDUCE
+    run = ds.runner(b, w, tol=tol, variant=variant, exchange=exchange)
     barrier_sync()
     t0 = time.perf_counter()
     run.start()
@@ -414,7 +499,7 @@ def bench_main(a, metric):
     t_solve = tmax(time.perf_counter() - t0)
     run.close()
 
-    run = ds.runner(b, w, tol=0.0, variant=variant)
+    run = ds.runner(b, w, tol=0.0, variant=variant, exchange=exchange)
     run.start()
     import math
     graph_k = use_graph(run, math.gcd(math.gcd(gk, a.steps), a.warmup) if gk > 0 else 0)
@@ -445,16 +530,20 @@ def bench_main(a, metric):
             "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": f"{tets.shape[0]:,}-tet P1 {a.kind} Kuhn cube n={a.n}, Jacobi-PCG fixed "
-                                   f"iterations, element-partitioned (RCB) over {world} GPUs, RCCL halo all-reduce"
-                                   + (" (single reduction: one all-reduce per iteration)" if variant else
-                                      " + r.z all-reduce"),
+                                   f"iterations, element-partitioned (RCB) over {world} GPUs, "
+                                   + ("RCCL neighbour send/recv of [r.z, u.Au | shared rows] with every other rank"
+                                      " (single reduction: one grouped exchange per iteration)"
+                                      if variant and exchange == EXCHANGE_P2P else
+                                      "RCCL halo all-reduce (single reduction: one all-reduce per iteration)"
+                                      if variant else "RCCL halo all-reduce + r.z all-reduce"),
                        "tets": int(tets.shape[0]), "dofs": N * bs, "interface_nodes": nI,
                        "parallelism": f"element partition x{world}", "graph_iterations": graph_k,
-                       "dist_variant": "single-reduction" if variant else "two-reduction"},
+                       "dist_variant": "single-reduction" if variant else "two-reduction",
+                       "dist_exchange": exchange},
             "dofs_per_s": N * bs / (t_asm + t_solve), "assembly_ms": t_asm * 1e3, "solve_ms": t_solve * 1e3,
             "assembly_stages_rank0": stages,
             "solve_iters": it, "solve_status": stt,
-            "kernel_ms": ({"spmv_local_max": spmv_ms, "allreduce": ms[1] / max(cnt[1], 1),
+            "kernel_ms": ({"spmv_local_max": spmv_ms, "exchange": ms[1] / max(cnt[1], 1),
                            "step_update": ms[2] / max(cnt[2], 1)} if variant else
                           {"spmv_local_max": spmv_ms, "exchange_update": ms[1] / max(cnt[1], 1),
                            "pupdate": ms[2] / max(cnt[2], 1)}),

@@ -430,6 +430,22 @@ int fem_pcg_set_dist(fem_pcg* s, int enable, void* comm, int64_t nI, const int32
  *      guards; rounding differs from variant 0 (N>1 contract: u within 1e-10, iterations within +-2).
  *      Phases: start 10 | sum | 20 | sum; iteration 4 | sum (buffer: fem_pcg_dist_buffer of that phase). */
 int fem_pcg_set_dist_variant(fem_pcg* s, int variant);
+/* neighbour exchange for the single-reduction variant (call after fem_pcg_set_dist_variant(s, 1)): the per-iteration
+ * all-reduce of [interface rows | g | d] becomes ONE grouped ncclSend/ncclRecv with each of the npeer other ranks
+ * (every other rank: the [g, d] pair travels to all). Message i (to and from peer_rank[i], peer_cnt[i] doubles) =
+ * [g, d | bs values of each node shared with that rank, ascending global interface index]; the slot layout is the
+ * same in both directions. csrc[J * nranks + r] (device int32, J over the nI global interface nodes) = offset of node
+ * J's component 0 in the slot of rank r (-1: this rank, -2: r does not touch J or this rank does not); ssrc[r]
+ * (device int32) = offset of rank r's [g, d] pair (-1: this rank). The SpMV kernel writes straight into the send
+ * slots, the step/update kernels sum the received slots in rank order 0..nranks-1, so shared dofs stay
+ * bit-identical across ranks. The maps stay owned by the caller (fem355.dist.p2p_maps builds them). */
+int fem_pcg_set_p2p(fem_pcg* s, int nranks, int npeer, const int* peer_rank, const int64_t* peer_cnt,
+                    const int32_t* csrc, const int32_t* ssrc);
+/* the neighbour-exchange staging buffers (psend / precv, total doubles) */
+int fem_pcg_p2p_buffers(fem_pcg* s, double** psend, double** precv, int64_t* total);
+/* group path (all P ranks' contexts in one process, ctx[r] = rank r): every rank's message to each peer copied into
+ * that peer's receive slot (what the grouped ncclSend/ncclRecv moves) */
+int fem_p2p_deliver(fem_pcg* const* ctx, int P, fem_stream_t stream);
 /* Phase-driven distributed iteration (what fem_pcg_start/iterate do around ncclAllReduce): phases 10, 11, 12
  * start the solve, phases 0..3 are one iteration; after a phase whose fem_pcg_dist_buffer is non-empty (10, 11:
  * start; 0: interface rows of A p + the p.q partial; 2: the r.z partial) that buffer must be summed over all ranks. Used to validate the distributed kernels with several

@@ -107,3 +107,71 @@ def test_rcb_partition_properties():
         loc = rm.imap[has].long()
         assert torch.equal(rm.ipos[loc].long(), torch.nonzero(has, as_tuple=True)[0])
     assert bool((pres >= 2).all())
+
+
+@pytest.mark.parametrize("P,bs", [(2, 1), (3, 3), (8, 1)])
+def test_p2p_maps_sum_like_the_allreduce(P, bs):
+    """Neighbour-exchange maps (fem355.dist.p2p_maps) on CPU, with the kernels' rules: the SpMV scatters each
+    interface row into every peer slot of csrc (>= 0) and the [g, d] pair into ssrc; the slots are delivered;
+    the update sums in rank order (-1: own row, -2: skip). Every rank's sum of a shared row equals the rank-ordered
+    sum of all holders' partials bit for bit (so copies agree across ranks), and [g, d] the rank-ordered sum."""
+    from fem355 import dist as fd, mesh
+    coords, tets = mesh.kuhn_cube(6, jitter=0.1)
+    N = coords.shape[0]
+    part = fd.rcb_partition(fd.element_centroids(coords, tets), P)
+    touch = fd.touch_masks(tets, part, P, N)
+    sharing = fd.node_sharing(tets, part, P, N)
+    rms = [fd.rank_mesh(tets, part, r, P, N, sharing) for r in range(P)]
+    maps = [fd.p2p_maps(rm, touch, bs) for rm in rms]
+    nI = rms[0].n_iface
+    iface = torch.nonzero(sharing[0] > 1, as_tuple=True)[0]
+    g = torch.Generator().manual_seed(7)
+    part_rows = torch.randn(P, nI, bs, generator=g, dtype=torch.float64)   # rank r's partial of node J
+    pairs = torch.randn(P, 2, generator=g, dtype=torch.float64)
+    psend = []
+    for a, m in enumerate(maps):
+        buf = torch.full((sum(m.peer_cnt),), float("nan"), dtype=torch.float64)
+        for J in range(nI):
+            for r in range(P):
+                dst = int(m.csrc[J, r])
+                if dst >= 0:
+                    buf[dst:dst + bs] = part_rows[a, J]
+        for r in range(P):
+            dst = int(m.ssrc[r])
+            if dst >= 0:
+                buf[dst:dst + 2] = pairs[a]
+        psend.append(buf)
+    assert all(not bool(torch.isnan(b).any()) for b in psend)   # every slot element written
+    offs = [[sum(m.peer_cnt[:i]) for i in range(len(m.peer_cnt))] for m in maps]
+    precv = [torch.zeros_like(b) for b in psend]
+    for a, m in enumerate(maps):
+        for i, b in enumerate(m.peer_rank):
+            j = maps[b].peer_rank.index(a)
+            assert maps[b].peer_cnt[j] == m.peer_cnt[i]
+            precv[b][offs[b][j]: offs[b][j] + m.peer_cnt[i]] = psend[a][offs[a][i]: offs[a][i] + m.peer_cnt[i]]
+    for a, m in enumerate(maps):
+        held = touch[a, iface]
+        for J in range(nI):
+            if not bool(held[J]):
+                assert bool((m.csrc[J] == -2).all())
+                continue
+            for c in range(bs):
+                acc, ref = 0.0, 0.0
+                for r in range(P):
+                    src = int(m.csrc[J, r])
+                    if src == -1:
+                        acc += float(part_rows[a, J, c])
+                    elif src >= 0:
+                        acc += float(precv[a][src + c])
+                    if bool(touch[r, iface[J]]):
+                        ref += float(part_rows[r, J, c])
+                assert acc == ref, (a, J, c)
+        for c in range(2):
+            acc = 0.0
+            for r in range(P):
+                src = int(m.ssrc[r])
+                acc += float(pairs[a, c]) if src < 0 else float(precv[a][src + c])
+            ref = 0.0
+            for r in range(P):
+                ref += float(pairs[r, c])
+            assert acc == ref
