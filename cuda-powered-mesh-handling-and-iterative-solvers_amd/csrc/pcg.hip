@@ -14,7 +14,7 @@
 //             K2 update   (as above)                          -> 2 launches and 88 n bytes of vectors per iteration
 //   deferred  d1 / d2 / d3: the 3-kernel work without grid atomics, each kernel re-summing the previous kernel's
 //             per-block partials (default for bs = 1)
-//   distributed single reduction: k_cg1_step / k_cg1_update / k_cg1_spmv, one all-reduce per iteration (N > 1)
+//   distributed single reduction: k_cg1_update / k_cg1_spmv (step evaluated in both), one exchange per iteration
 // Grid reductions are deterministic two-level trees (common.hpp reduce_grid).
 #include <rccl/rccl.h>
 #include <stddef.h>
@@ -729,7 +729,8 @@ __global__ void k_bank_init(PcgState* st) {
 // (sqrt(r.z) < tol, `solver/solver.py:210` / `:805`) and guards (`:187-198`, `:214`); the rounding differs from
 // the two-reduction form, which the N>1 contract allows (1e-10 on u, +-2 iterations).
 // The all-reduce is out of place: `send` keeps zeros at the interface nodes this rank has no copy of.
-//   k_cg1_step   (1 thread) : stop test on g of the last update, beta, p.Ap, alpha, guards; iter += 1
+//   step (every block of the next two kernels, cg1_eval): stop test on g of the last update, beta, p.Ap, alpha,
+//                             guards; committed (iter += 1, ...) by the last block of k_cg1_spmv
 //   k_cg1_update (grid)     : p, s, x, r, u; g partial of the new iterate -> st->red[1]
 //   k_cg1_spmv   (grid)     : v = A u (local), d partial; interface rows of v and [g, d] -> send
 // neighbour exchange (fem_pcg_set_p2p) seen by the single-reduction kernels; P = 0: all-reduce path. Message
@@ -756,61 +757,93 @@ __device__ __forceinline__ double cg1_scalar(const double* recv, const double* s
     return acc;
 }
 
-__global__ void k_cg1_step(PcgState* st, const double* __restrict__ recv, const double* __restrict__ send,
-                           int64_t off, double* hist, int64_t hist_len, P2PArgs x) {
-    st->xupd = 0;
-    if (st->halt) return;
-    const int it = st->iter;
+// the single-reduction step as a value: every block of k_cg1_update and k_cg1_spmv evaluates it from the unchanged
+// state and the exchanged [g, d] (identical result everywhere), the last block of k_cg1_spmv commits it
+struct Cg1Step {
+    int go;          // 1: update + SpMV run this iteration
+    int stop;        // 1: a stop decision to commit (status / halt / stop_iter below)
+    int status, stop_iter;
+    int it;
+    double g, d, alpha, beta, pq;
+    int has_pq;
+};
+
+__device__ __forceinline__ Cg1Step cg1_eval(const PcgState* st, double g, double d) {
+    Cg1Step k{};
+    k.it = st->iter;
+    k.g = g;
+    k.d = d;
+    k.status = st->status;
+    k.stop_iter = st->stop_iter;
+    if (st->halt) return k;
     const bool cg = st->mode != FEM_MODE_PCG;
-    const double g = cg1_scalar(recv, send, off, 0, x), d = cg1_scalar(recv, send, off, 1, x);
+    const int it = k.it;
     double beta = 0.0;
     if (it > 0) {
-        st->rz_new = g;
-        const double nrm = sqrt(g);
-        if (hist && it - 1 < hist_len) hist[it - 1] = nrm;
-        if (nrm < st->tol) {
-            st->status = FEM_PCG_CONVERGED;
-            st->halt = 1;
-            st->stop_iter = it;
-            return;
+        if (sqrt(g) < st->tol) {
+            k.stop = 1;
+            k.status = FEM_PCG_CONVERGED;
+            k.stop_iter = it;
+            return k;
         }
         beta = cg ? g / (st->rz + st->eps) : g / st->rz;
         if (cg && (isnan(beta) || isinf(beta))) {
-            st->status = FEM_PCG_BETA_NAN;
-            st->halt = 1;
-            st->stop_iter = it;
-            return;
+            k.stop = 1;
+            k.status = FEM_PCG_BETA_NAN;
+            k.stop_iter = it;
+            return k;
         }
     }
     if (it >= st->max_iter) {   // poll reports FEM_PCG_MAXITER
-        st->halt = 1;
-        return;
+        k.stop = 1;
+        return k;
     }
     const double pq = (it == 0) ? d : d - beta * g / st->alpha;
-    st->pq = pq;
+    k.pq = pq;
+    k.has_pq = 1;
     double alpha;
     if (cg) {
         if (fabs(pq) < st->eps || pq < 0.0) {
-            st->status = FEM_PCG_BREAKDOWN;
-            st->halt = 1;
-            st->stop_iter = it + 1;
-            return;
+            k.stop = 1;
+            k.status = FEM_PCG_BREAKDOWN;
+            k.stop_iter = it + 1;
+            return k;
         }
         alpha = g / (pq + st->eps);
         if (isnan(alpha) || isinf(alpha)) {
-            st->status = FEM_PCG_ALPHA_NAN;
-            st->halt = 1;
-            st->stop_iter = it + 1;
-            return;
+            k.stop = 1;
+            k.status = FEM_PCG_ALPHA_NAN;
+            k.stop_iter = it + 1;
+            return k;
         }
     } else {
         alpha = g / pq;
     }
-    st->rz = g;
-    st->alpha = alpha;
-    st->beta = beta;
-    st->iter = it + 1;
-    st->xupd = 1;
+    k.alpha = alpha;
+    k.beta = beta;
+    k.go = 1;
+    return k;
+}
+
+// the step's state writes (one thread)
+__device__ __forceinline__ void cg1_commit(PcgState* st, const Cg1Step& k, double* hist, int64_t hist_len) {
+    st->xupd = k.go;
+    if (!k.go && !k.stop) return;   // halted before this pass
+    if (k.it > 0) {
+        st->rz_new = k.g;
+        if (hist && k.it - 1 < hist_len) hist[k.it - 1] = sqrt(k.g);
+    }
+    if (k.has_pq) st->pq = k.pq;
+    if (k.stop) {
+        st->status = k.status;
+        st->stop_iter = k.stop_iter;
+        st->halt = 1;
+        return;
+    }
+    st->rz = k.g;
+    st->alpha = k.alpha;
+    st->beta = k.beta;
+    st->iter = k.it + 1;
 }
 
 __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_update(int64_t n, int bs, double* __restrict__ x,
@@ -820,11 +853,13 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_update(int64_t n, int bs, dou
                                                           const double* __restrict__ recv,
                                                           const int32_t* __restrict__ ipos,
                                                           const uint8_t* __restrict__ own, PcgState* __restrict__ st,
-                                                          RedBuf red, P2PArgs xp) {
+                                                          RedBuf red, P2PArgs xp, const double* __restrict__ send,
+                                                          int64_t off) {
     __shared__ double lds4[4];
     __shared__ int flag;
-    if (!st->xupd) return;
-    const double alpha = st->alpha, beta = st->beta;
+    const Cg1Step k = cg1_eval(st, cg1_scalar(recv, send, off, 0, xp), cg1_scalar(recv, send, off, 1, xp));
+    if (!k.go) return;
+    const double alpha = k.alpha, beta = k.beta;
     const bool cg = st->mode != FEM_MODE_PCG;
     double acc = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * PCG_BLOCK) {
@@ -898,16 +933,26 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_spmv(int64_t nslices, int64_t
                                                         const double* __restrict__ u, double* __restrict__ v,
                                                         const int32_t* __restrict__ ipos, double* __restrict__ send,
                                                         int64_t off, PcgState* __restrict__ st, RedBuf red,
-                                                        int always, int tune_rev, P2PArgs xp) {
+                                                        int always, int tune_rev, P2PArgs xp,
+                                                        const double* __restrict__ recv, double* hist,
+                                                        int64_t hist_len) {
     __shared__ double lds4[4];
     __shared__ int flag;
-    if (!always && !st->xupd) return;
+    Cg1Step k{};
+    if (!always) {   // the step of this pass (read before the last block commits it)
+        k = cg1_eval(st, cg1_scalar(recv, send, off, 0, xp), cg1_scalar(recv, send, off, 1, xp));
+        if (!k.go) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) cg1_commit(st, k, hist, hist_len);
+            return;
+        }
+    }
     const int lane = threadIdx.x & 63;
     double dot = 0.0;
     const SliceWalk wk = slice_walk(nslices);
     const VecPlain uv{u};
-    // sweep direction alternating with the iteration parity (FEM_TUNE_REVERSE, as k_pcg_spmv_dot)
-    const bool rev = tune_rev && (st->iter & 1);
+    // sweep direction alternating with the iteration parity (FEM_TUNE_REVERSE, as k_pcg_spmv_dot): the iteration
+    // count after this pass's step
+    const bool rev = tune_rev && ((always ? st->iter : k.it + 1) & 1);
     const int64_t mirror = wk.first + wk.end - 1;
     for (int64_t s0 = wk.s; s0 < wk.end; s0 += wk.step) {
         const int64_t s = rev ? mirror - s0 : s0;
@@ -937,6 +982,7 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_spmv(int64_t nslices, int64_t
     dot = block_sum256(dot, lds4);
     double d;
     if (reduce_grid(dot, red.part(RED_K1), red.cnt(RED_K1), &d, lds4, &flag) && threadIdx.x == 0) {
+        if (!always) cg1_commit(st, k, hist, hist_len);   // every block has read the state by now
         st->red[0] = d;
         send[off] = st->red[1];
         send[off + 1] = d;
@@ -1244,7 +1290,7 @@ static int cg1_spmv(fem_pcg* s, int always) {
 #define FEM_CG1(B, CI, PR, C, V)                                                                                   \
     hipLaunchKernelGGL((k_cg1_spmv<B, CI, PR>), dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream, s->nslices,     \
                        s->nrows, s->slice_ptr, C, V, s->cg1_u, s->q, ipos, s->cg1_send, off, s->st, s->red, always, \
-                       s->tune & FEM_TUNE_REVERSE, p2p_args(s))
+                       s->tune & FEM_TUNE_REVERSE, p2p_args(s), s->cg1_recv, s->hist, s->hist_len)
     if (s->paired && s->bs == 1) FEM_CG1(1, int16_t, true, pcols(s), s->pvals);
     else if (s->paired) FEM_CG1(3, int16_t, true, pcols(s), s->pvals);
     else if (s->cols16 && s->bs == 1) FEM_CG1(1, int16_t, false, s->cols16, s->vals);
@@ -1261,12 +1307,9 @@ static int cg1_spmv(fem_pcg* s, int always) {
 }
 
 static int cg1_step_update(fem_pcg* s) {
-    hipLaunchKernelGGL(k_cg1_step, dim3(1), dim3(1), 0, s->stream, s->st, s->cg1_recv, s->cg1_send, s->nI * s->bs,
-                       s->hist, s->hist_len, p2p_args(s));
-    FEM_LAUNCHED();
     hipLaunchKernelGGL(k_cg1_update, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->bs, s->x, s->r, s->p0,
                        s->cg1_s, s->cg1_u, s->q, s->w, s->cg1_recv, s->nI > 0 ? s->ipos : nullptr, s->own, s->st,
-                       s->red, p2p_args(s));
+                       s->red, p2p_args(s), s->cg1_send, s->nI * s->bs);
     FEM_LAUNCHED();
     return FEM_OK;
 }
