@@ -107,9 +107,23 @@ __device__ __forceinline__ bool pk_barrier(unsigned* sy, int grp, unsigned nper,
             okv = ok ? 1 : 0;
         }
         okv = __builtin_amdgcn_readfirstlane(okv);
-        if (okv && pd) {
-            const double d = pk_sum(pd, G);
-            const double g = pg ? pk_sum(pg, G) : 0.0;
+        if (okv && pd) {   // both partial vectors in one round of loads (same per-lane order as two pk_sums)
+            const int lane = threadIdx.x & 63;
+            double vd = 0.0, vg = 0.0;
+            if (pg) {
+#pragma unroll 4
+                for (int i = lane; i < G; i += 64) {
+                    const double a = __hip_atomic_load(pd + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const double b = __hip_atomic_load(pg + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    vd += a;
+                    vg += b;
+                }
+            } else {
+#pragma unroll 4
+                for (int i = lane; i < G; i += 64) vd += __hip_atomic_load(pd + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            const double d = wave_sum(vd);
+            const double g = pg ? wave_sum(vg) : 0.0;
             if (threadIdx.x == 0) {
                 out[0] = d;
                 out[1] = g;
