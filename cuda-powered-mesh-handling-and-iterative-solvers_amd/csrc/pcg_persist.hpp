@@ -10,7 +10,7 @@
 //              (gather window, computed once per matrix), then ONE agent acquire (L1) for the workgroup
 //     SpMV   : v = A u over the own slices (paired layout, plain u gathers), d partial = u.v
 //     reduce : workgroup partials of d (and g of the last update) stored sc1 into a parity bank; hierarchical
-//              grid barrier (8 group counters -> top counter -> group generation words), every wave then sums
+//              grid barrier (8 group counters -> 8 replicas of the top counter), wave 0 then sums
 //              the G partials in the same fixed order -> identical scalars in every workgroup
 //     step   : stop test on g (`solver/solver.py:210` / `:805`), beta, p.Ap = d - beta g / alpha_prev, alpha,
 //              guards (`:187-198`, `:214`) -- k_cg1_step's arithmetic, evaluated redundantly by every thread
@@ -31,7 +31,8 @@ constexpr int PK_WAVES = PK_T / 64;
 constexpr int PK_MAXS = 7;               // slices per wave (10M Poisson: 27,000 slices over 4,096 waves -> 7)
 constexpr int PK_U = 2;                  // pairs in flight per lane (4 spills the slot state; persist_probe: 4 = 8)
 constexpr int PK_LINE = 32;              // unsigned words per 128-byte line
-// sync words (zeroed before every launch), in lines: [0, 8) group arrivals, 8 top, [9, 17) group generations,
+// sync words (zeroed before every launch), in lines: [0, 8) group arrivals, 8 (unused), [9, 17) replicas of the
+// top counter (one per group),
 // 17 give-up word, 18 + L: u-flag of workgroup L
 enum { PK_GRP = 0, PK_TOP = 8 * PK_LINE, PK_GEN = 9 * PK_LINE, PK_TMO = 17 * PK_LINE, PK_UFLAG = 18 * PK_LINE };
 constexpr unsigned PK_SPIN_LIMIT = 1u << 22;
@@ -97,13 +98,12 @@ __device__ __forceinline__ bool pk_barrier(unsigned* sy, int grp, unsigned nper,
             bool ok;
             const unsigned old = __hip_atomic_fetch_add(sy + PK_GRP + grp * PK_LINE, 1u, __ATOMIC_RELAXED,
                                                         __HIP_MEMORY_SCOPE_AGENT);
-            if (old == e * nper - 1) {   // last of its group: arrive on top, wait for all groups, release the group
-                __hip_atomic_fetch_add(sy + PK_TOP, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok = pk_wait_ge(sy + PK_TOP, e * NXCD, tmo);
-                pk_st(sy + PK_GEN + grp * PK_LINE, e);
-            } else {
-                ok = pk_wait_ge(sy + PK_GEN + grp * PK_LINE, e, tmo);
-            }
+            // last of its group: arrive on all 8 replicas of the top counter (one line each); every workgroup polls
+            // its group's replica (32 pollers per line, no leader -> generation hop)
+            if (old == e * nper - 1)
+                for (int r = 0; r < NXCD; ++r)
+                    __hip_atomic_fetch_add(sy + PK_GEN + r * PK_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = pk_wait_ge(sy + PK_GEN + grp * PK_LINE, e * NXCD, tmo);
             okv = ok ? 1 : 0;
         }
         okv = __builtin_amdgcn_readfirstlane(okv);
