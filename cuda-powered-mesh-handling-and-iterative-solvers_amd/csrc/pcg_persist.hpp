@@ -2,22 +2,25 @@
 //
 // The single-reduction (Chronopoulos–Gear) form of k_cg1_* run as ONE launch per chunk of iterations: every wave
 // owns a fixed contiguous range of at most PK_MAXS slices for the whole launch and keeps its rows' CG state on the
-// chip — r, p, s = A p, v = A u and its own u in registers, x and w in LDS — so an iteration moves the matrix once,
+// chip — r, p, s = A p, its own u and 2 of 7 v = A u slots in registers, x, w and 5 v slots in LDS — so an
+// iteration moves the matrix once,
 // gathers u, and writes u: (8 + 2) nnz + 16 n bytes instead of the deferred schedule's (8 + 2) nnz + 96 n.
 //
 //   per iteration (epoch e = local iteration + 1):
 //     wait   : one wave polls the u-flags of the workgroups whose rows this workgroup's columns reach
-//              (gather window, computed once per matrix), then ONE agent acquire (L1) for the workgroup
-//     SpMV   : v = A u over the own slices (paired layout, plain u gathers), d partial = u.v
+//              (gather window, computed once per matrix); workgroup barrier (GSC1 = 0: one agent acquire first)
+//     SpMV   : v = A u over the own slices (paired layout; u gathers as global sc1 loads, GSC1 = 1, the default),
+//              d partial = u.v
 //     reduce : workgroup partials of d (and g of the last update) stored sc1 into a parity bank; hierarchical
 //              grid barrier (8 group counters -> 8 replicas of the top counter), wave 0 then sums
 //              the G partials in the same fixed order -> identical scalars in every workgroup
 //     step   : stop test on g (`solver/solver.py:210` / `:805`), beta, p.Ap = d - beta g / alpha_prev, alpha,
-//              guards (`:187-198`, `:214`) -- k_cg1_step's arithmetic, evaluated redundantly by every thread
+//              guards (`:187-198`, `:214`) -- the single-reduction step (pcg.hip cg1_eval), by every thread
 //     update : p = u + beta p, s = v + beta s, x += alpha p, r -= alpha s (CG: masked), u = w r stored sc1,
 //              g partial; every wave drains its stores, then one lane raises the workgroup's u-flag to e
-// The hand-offs follow MI355X_MICROARCH.md "Valid forms" (sc1 stores + drain + relaxed flag / counter; sc1 loads
-// of the partials; agent acquire before the plain u gathers). Every spin is bounded: a give-up sets a word all
+// The hand-offs follow MI355X_MICROARCH.md "Valid forms" (sc1 stores + drain + relaxed flag / counter; global sc1
+// loads of the partials and of the u gathers, or an agent acquire before plain gathers). Every spin is bounded: a
+// give-up sets a word all
 // spinners check, the launch then ends with status FEM_PCG_SYNC_TIMEOUT instead of hanging.
 // Exactly one workgroup of PK_T threads per CU (LDS pins it): the grid is resident by construction (the host
 // checks the occupancy query; a plain launch: a cooperative one adds ~17 us per launch and buys only that check).
