@@ -1772,7 +1772,7 @@ int fem_pcg_create(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_
         return FEM_EARG;
     }
     fem_pcg* s = new fem_pcg();
-    s->tune = FEM_TUNE_REVERSE | FEM_TUNE_PAIR | FEM_TUNE_PK_SC1;
+    s->tune = FEM_TUNE_REVERSE | FEM_TUNE_PAIR | FEM_TUNE_PK_SC1 | FEM_TUNE_PK_PACK;
     s->nrows = nrows;
     s->bs = bs;
     s->nslices = cdiv(nrows, 64);
@@ -1948,6 +1948,10 @@ static int launch_persist(fem_pcg* s, int k, unsigned long long* prof) {
     a.kmax = k;
     a.rev = (s->tune & FEM_TUNE_REVERSE) ? 1 : 0;
     a.prof = prof;
+    {   // packed slice assignment: m = ceil(max slices of a workgroup / waves) per wave
+        const int64_t maxL = (s->nslices + G - 1) / G;
+        a.pack = (s->tune & FEM_TUNE_PK_PACK) ? (int)((maxL + PK_WAVES - 1) / PK_WAVES) : 0;
+    }
     void* args[] = {&a};
     const void* fn = persist_fn(prof != nullptr, (s->tune & FEM_TUNE_PK_SC1) != 0);
     FEM_HIP(hipLaunchKernel(fn, dim3(G), dim3(PK_T), args, PK_LDS, s->stream));

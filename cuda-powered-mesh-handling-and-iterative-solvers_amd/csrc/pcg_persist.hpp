@@ -171,6 +171,7 @@ struct PkArgs {
     int64_t hist_len;
     int kmax;               // iterations of this launch
     int rev;                // FEM_TUNE_REVERSE: odd iterations walk the own slices backwards
+    int pack;               // FEM_TUNE_PK_PACK: slices per wave in order (0: spread; see k_pcg_persist)
     unsigned long long* prof;   // PROF instantiation: [G][PK_NPROF] shader-clock sums per phase (thread 0 of each WG)
 };
 
@@ -204,10 +205,24 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
     const int grp = L / (int)nper;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform -> scalar slot bounds
-    const int64_t W = (int64_t)G * PK_WAVES;
-    const int64_t gw = (int64_t)L * PK_WAVES + wv;
-    const int s0 = (int)(gw * a.nslices / W);
-    const int nsl = (int)((gw + 1) * a.nslices / W) - s0;   // <= MAXS (host check)
+    // slices of this wave (wave-uniform): workgroup L owns [L S / G, (L+1) S / G) either way; spread: the
+    // workgroup's slices evenly over its 16 waves (6 or 7 each at 10M); packed (FEM_TUNE_PK_PACK): a.pack =
+    // ceil(max slices per workgroup / 16) per wave in order, the remainder on the last busy wave (10M: 15 waves x 7
+    // + 0 or 1 -- every busy wave streams to the end of the phase instead of 41 % of them idling through the 7th)
+    int s0, nsl;
+    if (a.pack) {
+        const int m = a.pack;   // <= MAXS (host)
+        const int sL0 = (int)((int64_t)L * a.nslices / G);
+        const int nL = (int)((int64_t)(L + 1) * a.nslices / G) - sL0;
+        const int lo = wv * m < nL ? wv * m : nL;
+        s0 = sL0 + lo;
+        nsl = nL - lo < m ? nL - lo : m;
+    } else {
+        const int64_t W = (int64_t)G * PK_WAVES;
+        const int64_t gw = (int64_t)L * PK_WAVES + wv;
+        s0 = (int)(gw * a.nslices / W);
+        nsl = (int)((gw + 1) * a.nslices / W) - s0;   // <= MAXS (host check)
+    }
     const int nrows = (int)a.nrows;
     const unsigned rb = (unsigned)s0 * 64u + (unsigned)lane;
     double* xl = pk_lds + wv * MAXS * 64 + lane;

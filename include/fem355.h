@@ -374,11 +374,16 @@ int fem_enforce_constraints(double* x, double* r, int64_t n, int order, int64_t 
                             const int64_t* rbe2_master, int64_t S, const int64_t* spc_dof, const double* spc_val,
                             int64_t G, const int64_t* r3_ptr, const int64_t* r3_master, const double* r3_wsum,
                             const int64_t* r3_slave, const double* r3_w, fem_stream_t stream);
-/* tuning flags (default FEM_TUNE_REVERSE | FEM_TUNE_PAIR | FEM_TUNE_PK_SC1): the SpMV of every schedule sweeps each XCD's slice range backwards on
+/* tuning flags (default FEM_TUNE_REVERSE | FEM_TUNE_PAIR | FEM_TUNE_PK_SC1 | FEM_TUNE_PK_PACK): the SpMV of every schedule sweeps each XCD's slice range backwards on
  * odd iterations, so the matrix tail read last (still in the MI355X's 256 MB memory-side cache) is read first by
  * the next sweep: 67 -> 57 us per SpMV on the 10M Poisson matrix. Results depend on the flags only through the
  * order of the per-block p.q partials (deterministic for a given flag set). */
-enum { FEM_TUNE_REVERSE = 1, FEM_TUNE_PAIR = 2, FEM_TUNE_PK_SC1 = 4 };
+enum { FEM_TUNE_REVERSE = 1, FEM_TUNE_PAIR = 2, FEM_TUNE_PK_SC1 = 4, FEM_TUNE_PK_PACK = 8 };
+/* FEM_TUNE_PK_PACK (default): persistent schedule only — each workgroup gives its waves ceil(max slices per
+ * workgroup / 16) slices each in order (the last busy wave takes the remainder) instead of spreading them evenly:
+ * at 10M 15 waves x 7 slices all stream to the end of the SpMV phase instead of 7-slice waves finishing alone
+ * (54.0 -> 51.6 us per iteration; 3M tets 21.6 -> 19.3; equal at 1M and 6M). Same per-row arithmetic, so the
+ * iterates change only through the order of the u.v partials. */
 /* FEM_TUNE_PK_SC1 (default): persistent schedule only — the u gathers are sc1 (agent-coherent) loads instead of
  * plain loads behind an agent acquire per workgroup and iteration (whose L2 invalidations cost the other workgroups
  * of the XCD their gather window): 58.8 -> 55.9 us per 10M Poisson iteration, bit-identical iterates. */

@@ -429,6 +429,24 @@ def test_persistent_schedule_matches_three_kernel(gpu, n, jitter):
     assert c0.iterations == c3.iterations == 25 and c0.status == c3.status == 2 and rel(c3.x, c0.x) < 1e-12
 
 
+def test_persistent_initial_guess(gpu):
+    """Non-zero x0 (r0 = b - A x0 before the first launch; x carried in LDS): schedule 3 equals the 3-kernel
+    schedule in PCG and CG (masked) modes."""
+    _, mesh, _, system = _mods()
+    A, b, mask = _poisson_case(system, mesh, 16, gpu, jitter=0.1)
+    w = A.jacobi(mask)
+    x0 = torch.randn(A.n, dtype=F64, generator=torch.Generator().manual_seed(5)).to(gpu)
+    x0[mask.bool()] = 0.0
+    tol = 1e-9 * float(torch.sqrt(torch.dot(b, w * b)))
+    r0 = A.pcg(b, x0, w=w, tol=tol, max_iter=3000, schedule=0)
+    r3 = A.pcg(b, x0, w=w, tol=tol, max_iter=3000, schedule=3)
+    assert r0.status == r3.status == 1 and abs(r0.iterations - r3.iterations) <= 1 and rel(r3.x, r0.x) < 1e-10
+    wm = (mask == 0).to(F64)
+    c0 = A.pcg(b, x0, w=wm, mode=0, tol=0.0, max_iter=30, schedule=0)
+    c3 = A.pcg(b, x0, w=wm, mode=0, tol=0.0, max_iter=30, schedule=3)
+    assert c0.iterations == c3.iterations == 30 and rel(c3.x, c0.x) < 1e-12
+
+
 def test_persistent_chunks_are_bit_identical(gpu):
     """Chunk boundaries add no arithmetic: 4 launches of 9 iterations == one launch of 36, bit for bit, and the
     poll reports the same state; both u hand-off forms (sc1 gathers, acquire + plain gathers) agree bit for bit."""
