@@ -454,9 +454,9 @@ def test_persistent_chunks_are_bit_identical(gpu):
     A, b, mask = _poisson_case(system, mesh, 24, gpu)
     w = A.jacobi(mask)
     outs = []
-    for chunks, flags in (((36,), 7), ((9, 9, 9, 9), 7), ((36,), 3)):
+    for chunks, flags in (((36,), 15), ((9, 9, 9, 9), 15), ((36,), 11)):
         run = system.PcgRunner(A, b, w, tol=0.0, schedule=3)
-        run.set_tuning(flags)   # 7: sc1 gathers (default), 3: agent acquire + plain gathers
+        run.set_tuning(flags)   # 15: sc1 gathers (default), 11: agent acquire + plain gathers
         run.start()
         for k in chunks:
             run.iterate(k)
@@ -486,7 +486,7 @@ def test_persistent_full_geometry_10m(gpu):
     assert rel(xs[1][1], xs[0][1]) < 1e-12 and abs(xs[1][0] - xs[0][0]) <= 1e-10 * abs(xs[0][0])
     # the u hand-off through an agent acquire + plain gathers (FEM_TUNE_PK_SC1 off) gives the same bits
     run = system.PcgRunner(A, b, w, tol=0.0, schedule=3)
-    run.set_tuning(3)
+    run.set_tuning(1 | 2 | 8)   # REVERSE | PAIR | PK_PACK, without PK_SC1
     run.start()
     run.iterate(50)
     assert run.poll()[0] == 50 and torch.equal(run.x, xs[1][1])
