@@ -416,13 +416,24 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
                     gp += ri * ui;
                 }
             }
-            const double gsum = pk_block_sum(gp, lds16);
-            if (threadIdx.x == 0)
-                __hip_atomic_store(a.part + (size_t)(bank ^ 1) * 2 * G + G + L, gsum, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+            // one workgroup barrier for both the g block sum and the u hand-off: every wave leaves its g wave sum
+            // in LDS and drains its u stores, then thread 0 sums (wave order, as pk_block_sum), stores the g
+            // partial and raises the u-flag (the g partial is covered by the next grid barrier's drain, not by
+            // this flag)
+            {
+                const double gw = wave_sum(gp);
+                if (lane == 0) lds16[wv] = gw;
+            }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave drains its u stores
             __syncthreads();
-            if (threadIdx.x == 0) pk_st(sy + PK_UFLAG + L * PK_LINE, e);
+            if (threadIdx.x == 0) {
+                double gsum = 0.0;
+#pragma unroll
+                for (int i = 0; i < PK_WAVES; ++i) gsum += lds16[i];
+                __hip_atomic_store(a.part + (size_t)(bank ^ 1) * 2 * G + G + L, gsum, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                pk_st(sy + PK_UFLAG + L * PK_LINE, e);
+            }
             PK_MARK(5);
         }
     }
