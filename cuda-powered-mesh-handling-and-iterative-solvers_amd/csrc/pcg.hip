@@ -1181,6 +1181,8 @@ struct fem_pcg {
     int32_t* pk_win;      // [2 G]: first workgroups, then last workgroups of the gather windows
     double* pk_part;      // [2][2][G]
     unsigned* pk_sync;    // (18 + G) lines, zeroed before every launch
+    int pk_ovf;           // overflow build (more than PK_MAXS slices per wave)
+    double* pk_v;         // [n] v of the overflow rows
 };
 
 #define FEM_NCCL(call)                                                                         \
@@ -1840,8 +1842,8 @@ int fem_pcg_set_schedule(fem_pcg* s, int sched) {
 }
 
 int fem_pcg_persist_profile(fem_pcg* s, int k, unsigned long long* host_out, int* grid) {
-    if (!s->persist || k <= 0) {
-        set_error("fem_pcg_persist_profile: the context does not run the persistent schedule (start it first)");
+    if (!s->persist || s->pk_ovf || k <= 0) {
+        set_error("fem_pcg_persist_profile: the context does not run the (register-resident) persistent schedule");
         return FEM_EARG;
     }
     const size_t nb = sizeof(unsigned long long) * (size_t)s->pk_grid * PK_NPROF;
@@ -1870,7 +1872,9 @@ int fem_pcg_get_schedule(fem_pcg* s) {
 
 static size_t pk_sync_words(int G) { return (size_t)(18 + G) * PK_LINE; }
 
-static const void* persist_fn(bool prof, bool gsc1) {
+static const void* persist_fn(bool prof, bool gsc1, bool ovf = false) {
+    if (ovf) return gsc1 ? (const void*)k_pcg_persist<PK_MAXS, false, true, true>
+                         : (const void*)k_pcg_persist<PK_MAXS, false, false, true>;
     if (prof) return gsc1 ? (const void*)k_pcg_persist<PK_MAXS, true, true> : (const void*)k_pcg_persist<PK_MAXS, true, false>;
     return gsc1 ? (const void*)k_pcg_persist<PK_MAXS, false, true> : (const void*)k_pcg_persist<PK_MAXS, false, false>;
 }
@@ -1885,9 +1889,12 @@ static int persist_setup(fem_pcg* s) {
     FEM_HIP(hipGetDevice(&dev));
     FEM_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     const int G = (ncu / NXCD) * NXCD;
-    if (G < NXCD || s->nslices > (int64_t)G * PK_WAVES * PK_MAXS) return FEM_OK;
-    for (int v = 0; v < 4; ++v) {
-        const void* f = persist_fn(v & 1, v & 2);
+    if (G < NXCD) return FEM_OK;
+    // past MAXS slices per wave: the overflow build (packed assignment only; overflow rows streamed from HBM)
+    const bool ovf = s->nslices > (int64_t)G * PK_WAVES * PK_MAXS;
+    if (ovf && !(s->tune & FEM_TUNE_PK_PACK)) return FEM_OK;
+    for (int v = 0; v < 6; ++v) {
+        const void* f = persist_fn((v & 1) && v < 4, v & 2, v >= 4);
         FEM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)PK_LDS));
         int nb = 0;
         FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, PK_T, PK_LDS));
@@ -1919,6 +1926,8 @@ static int persist_setup(fem_pcg* s) {
         FEM_HIP(hipStreamSynchronize(s->stream));   // lohi must outlive the copy
         s->pk_win_ok = 1;
     }
+    if (ovf && !s->pk_v) FEM_HIP(hipMalloc(&s->pk_v, sizeof(double) * (size_t)s->n));
+    s->pk_ovf = ovf ? 1 : 0;
     s->persist = 1;
     return FEM_OK;
 }
@@ -1948,12 +1957,13 @@ static int launch_persist(fem_pcg* s, int k, unsigned long long* prof) {
     a.kmax = k;
     a.rev = (s->tune & FEM_TUNE_REVERSE) ? 1 : 0;
     a.prof = prof;
+    a.v = s->pk_ovf ? s->pk_v : nullptr;
     {   // packed slice assignment: m = ceil(max slices of a workgroup / waves) per wave
         const int64_t maxL = (s->nslices + G - 1) / G;
         a.pack = (s->tune & FEM_TUNE_PK_PACK) ? (int)((maxL + PK_WAVES - 1) / PK_WAVES) : 0;
     }
     void* args[] = {&a};
-    const void* fn = persist_fn(prof != nullptr, (s->tune & FEM_TUNE_PK_SC1) != 0);
+    const void* fn = persist_fn(prof != nullptr && !s->pk_ovf, (s->tune & FEM_TUNE_PK_SC1) != 0, s->pk_ovf != 0);
     FEM_HIP(hipLaunchKernel(fn, dim3(G), dim3(PK_T), args, PK_LDS, s->stream));
     FEM_LAUNCHED();
     s->launched += k;
@@ -2453,6 +2463,7 @@ void fem_pcg_destroy(fem_pcg* s) {
     if (s->pk_win) (void)hipFree(s->pk_win);
     if (s->pk_part) (void)hipFree(s->pk_part);
     if (s->pk_sync) (void)hipFree(s->pk_sync);
+    if (s->pk_v) (void)hipFree(s->pk_v);
     if (s->st) (void)hipFree(s->st);
     if (s->st_host) (void)hipHostFree(s->st_host);
     delete s;

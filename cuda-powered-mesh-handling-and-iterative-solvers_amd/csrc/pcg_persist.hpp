@@ -172,16 +172,20 @@ struct PkArgs {
     int kmax;               // iterations of this launch
     int rev;                // FEM_TUNE_REVERSE: odd iterations walk the own slices backwards
     int pack;               // FEM_TUNE_PK_PACK: slices per wave in order (0: spread; see k_pcg_persist)
+    double* v;              // OVF: v = A u of the overflow rows (their state stays in r, p, s, x, u, w in HBM)
     unsigned long long* prof;   // PROF instantiation: [G][PK_NPROF] shader-clock sums per phase (thread 0 of each WG)
 };
 
 // the 64 rows of slot j of this wave: row = rb + 64 j (32-bit; the host checks nrows < 2^31); `lim` = rows of the
 // slot that exist (wave-uniform; < 64 only in the matrix's last slice)
-#define PK_ON(j) ((j) < nsl && lane < nrows - (s0 + (j)) * 64)
+#define PK_ON(j) ((j) < nreg && lane < nrows - (s0 + (j)) * 64)
 
 // GSC1: the u gathers are sc1 loads and the u-flag wait needs no agent acquire (whose L2 invalidation by every
 // workgroup of an XCD can drop the gather window other workgroups are still reading)
-template <int MAXS, bool PROF, bool GSC1>
+// OVF: meshes past MAXS slices per wave (packed assignment only): a wave's slices beyond its MAXS register slots keep
+// their CG state in HBM (the r, p, s, x, u, w arrays, v in a.v) and are streamed every iteration like the deferred
+// schedule's rows, inside the same launch and the same barriers
+template <int MAXS, bool PROF, bool GSC1, bool OVF = false>
 __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
     unsigned long long pacc[PROF ? PK_NPROF : 1] = {};
     unsigned long long pt = 0;
@@ -223,6 +227,8 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
         s0 = (int)(gw * a.nslices / W);
         nsl = (int)((gw + 1) * a.nslices / W) - s0;   // <= MAXS (host check)
     }
+    const int nreg = (OVF && nsl > MAXS) ? MAXS : nsl;   // register / LDS slots
+    const int nov = nsl - nreg;                          // overflow slices (OVF only; host-checked 0 otherwise)
     const int nrows = (int)a.nrows;
     const unsigned rb = (unsigned)s0 * 64u + (unsigned)lane;
     double* xl = pk_lds + wv * MAXS * 64 + lane;
@@ -306,7 +312,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
             if (!rv) {
 #pragma unroll
                 for (int j = 0; j < MAXS; ++j) {
-                    if (j < nsl) {
+                    if (j < nreg) {
                         const double v = sell_row_pair<PK_U, GSC1>(s0 + j, lane, slp, cop, vap, uvp);
                         if (j < PK_VL) vl[j * 64] = v; else vv[j] = v;
                     }
@@ -316,7 +322,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
 #pragma unroll
                 for (int jj = 0; jj < MAXS; ++jj) {
                     const int j = MAXS - 1 - jj;
-                    if (j < nsl) {
+                    if (j < nreg) {
                         const double v = sell_row_pair<PK_U, GSC1>(s0 + j, lane, slp, cop, vap, uvp);
                         if (j < PK_VL) vl[j * 64] = v; else vv[j] = v;
                     }
@@ -326,6 +332,18 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
             double dp = 0.0;
 #pragma unroll
             for (int j = 0; j < MAXS; ++j) dp += uo[j] * (j < PK_VL ? vl[j * 64] : vv[j]);   // absent rows: uo = 0
+            if constexpr (OVF) {   // overflow slices: v to HBM, u.v from the own u (this lane stored it last update)
+                __builtin_amdgcn_sched_barrier(0);
+                for (int q = 0; q < nov; ++q) {
+                    const int sq = s0 + MAXS + q;
+                    const double v = sell_row_pair<PK_U, GSC1>(sq, lane, slp, cop, vap, uvp);
+                    const int row = sq * 64 + lane;
+                    if (row < nrows) {
+                        a.v[row] = v;
+                        dp += a.u[row] * v;
+                    }
+                }
+            }
             // ---- publish d (and g of the last update), grid barrier, fixed-order sums
             const int bank = k & 1;
             double* pd = a.part + (size_t)bank * 2 * G;
@@ -400,7 +418,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
             for (int j = 0; j < MAXS; ++j) {
                 // branch-free over the lanes (rows past nrows hold zeros: their SpMV rows are zero padding); only
                 // the u store is masked. Exec-masked updates of the loop-carried arrays cost register copies.
-                if (j < nsl) {
+                if (j < nreg) {
                     const double pi = uo[j] + bnew * pp[j];
                     const double si = (j < PK_VL ? vl[j * 64] : vv[j]) + bnew * ss[j];
                     pp[j] = pi;
@@ -414,6 +432,26 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
                     uo[j] = ui;
                     if (PK_ON(j)) __hip_atomic_store(ust + (rbi + 64u * j), ui, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     gp += ri * ui;
+                }
+            }
+            if constexpr (OVF) {   // overflow rows: the same update on the HBM-resident state
+                __builtin_amdgcn_sched_barrier(0);
+                for (int q = 0; q < nov; ++q) {
+                    const int row = (s0 + MAXS + q) * 64 + lane;
+                    if (row < nrows) {
+                        const double pi = a.u[row] + bnew * a.p[row];
+                        const double si = a.v[row] + bnew * a.s[row];
+                        a.p[row] = pi;
+                        a.s[row] = si;
+                        a.x[row] += al * pi;
+                        double ri = a.r[row] - al * si;
+                        const double wi = a.w[row];
+                        if (cg && wi == 0.0) ri = 0.0;
+                        a.r[row] = ri;
+                        const double ui = wi * ri;
+                        __hip_atomic_store(ust + row, ui, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        gp += ri * ui;
+                    }
                 }
             }
             // one workgroup barrier for both the g block sum and the u hand-off: every wave leaves its g wave sum

@@ -346,8 +346,9 @@ int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, 
  * inside the SpMV from r, w and the previous p; 2 kernels per iteration), 2 = deferred (each kernel finishes the
  * previous kernel's block partials itself: no grid atomics, state banked by launch parity), 3 = persistent
  * (pcg_persist.hpp: the single-reduction iteration as one cooperative launch per chunk, CG state of every row held in
- * registers / LDS of its owning wave; bs = 1 with 16-bit columns and FEM_TUNE_PAIR, single GPU, at most 7 slices
- * per wave; otherwise fem_pcg_start falls back to 2). Distributed and constrained contexts accept only 0. */
+ * registers / LDS of its owning wave, slices past 7 per wave streamed from HBM in the same launch; bs = 1 with
+ * 16-bit columns and FEM_TUNE_PAIR, single GPU; otherwise fem_pcg_start falls back to 2). Distributed and
+ * constrained contexts accept only 0. */
 int fem_pcg_set_schedule(fem_pcg* s, int sched);
 /* the schedule the context runs (valid after fem_pcg_start: 3 may have fallen back to 2) */
 int fem_pcg_get_schedule(fem_pcg* s);

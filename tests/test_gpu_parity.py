@@ -497,6 +497,29 @@ def test_persistent_full_geometry_10m(gpu):
     assert r2.status == r3.status == 1 and abs(r2.iterations - r3.iterations) <= 1 and rel(r3.x, r2.x) < 1e-10
 
 
+def test_persistent_overflow_past_register_capacity(gpu):
+    """A 13.2M-tet mesh (2.25M rows: more than 7 slices per wave): the overflow build keeps the rows past the register
+    slots in HBM inside the same launch; fixed iterations equal the deferred schedule's to 1e-12, a solve to
+    tolerance stops at the same iteration."""
+    _, mesh, _, system = _mods()
+    A, b, mask = _poisson_case(system, mesh, 130, gpu)
+    w = A.jacobi(mask)
+    xs = []
+    for sched in (2, 3):
+        run = system.PcgRunner(A, b, w, tol=0.0, schedule=sched)
+        run.start()
+        assert run.effective_schedule() == sched
+        run.iterate(30)
+        assert run.poll()[0] == 30
+        xs.append(run.x.clone())
+        run.close()
+    assert rel(xs[1], xs[0]) < 1e-12
+    tol = 1e-8 * float(torch.sqrt(torch.dot(b, w * b)))
+    r2 = A.pcg(b, w=w, tol=tol, max_iter=3000, schedule=2)
+    r3 = A.pcg(b, w=w, tol=tol, max_iter=3000, schedule=3)
+    assert r2.status == r3.status == 1 and abs(r2.iterations - r3.iterations) <= 1 and rel(r3.x, r2.x) < 1e-10
+
+
 def test_persistent_falls_back_and_guards(gpu):
     """bs = 3 falls back to the deferred schedule; a guard stop (CG breakdown on the scalar block
     of the indefinite c3d10 rule) reports the same status and iteration as the 3-kernel schedule."""
