@@ -2346,7 +2346,9 @@ int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, 
     s->max_iter = 0x7fffffff;
     if (rc) return rc;
     if (chunk <= 0) chunk = 32;
-    if (s->persist) chunk = max_iter;   // the persistent kernel stops itself on convergence: one launch, one poll
+    // the persistent kernel stops itself on convergence: one launch and one poll per 8192 iterations (~0.4 s at
+    // 10M tets; bounded launches keep a non-converging solve interruptible between them)
+    if (s->persist) chunk = max_iter < 8192 ? max_iter : 8192;
     int done = 0;
     int it = 0, stt = FEM_PCG_RUNNING;
     while (done < max_iter) {
@@ -2355,7 +2357,7 @@ int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, 
         done += k;
         if ((rc = fem_pcg_poll(s, &it, &stt, rz))) return rc;
         if (stt != FEM_PCG_RUNNING) break;
-        if (chunk < 256) chunk *= 2;   // poll less often once the solve is clearly long
+        if (chunk < 256 && !s->persist) chunk *= 2;   // poll less often once the solve is clearly long
     }
     if ((rc = fem_pcg_finish(s))) return rc;
     if ((rc = fem_pcg_poll(s, &it, &stt, rz))) return rc;
