@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--dist-exchange", default="p2p", choices=["p2p", "allreduce"],
                     help="N>1 single-reduction exchange: grouped ncclSend/Recv with every other rank + fixed-order sum "
                          "(p2p), or one all-reduce over the global interface vector")
+    ap.add_argument("--dist-fused", type=int, default=0,
+                    help="N>1 single reduction: 1 = one launch per iteration (k_cg1_fused), 0 = update + SpMV kernels")
     ap.add_argument("--dist-graph", type=int, default=50,
                     help="distributed path: capture k iterations (kernels + RCCL) per hipGraph, 0 = plain launches")
     return ap.parse_args()

@@ -996,6 +996,265 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_spmv(int64_t nslices, int64_t
     }
 }
 
+
+// ---------------------------------------------------------------- distributed single-reduction iteration, fused
+// One launch per iteration between two exchanges (N > 1): step, update of the own rows, u hand-off to the
+// neighbouring workgroups by flags (no grid barrier: only the workgroups whose rows the SpMV reaches), SpMV of the
+// same rows, pack, and ONE two-value grid reduction (g, d) whose last block commits the step and writes [g, d].
+// Replaces k_cg1_update + k_cg1_spmv (two launches and two reduction tails). Every workgroup must be resident
+// (the host sizes the grid from the occupancy query); a flag wait that exceeds the spin limit ends the solve with
+// FEM_PCG_SYNC_TIMEOUT. Hand-off: u stores sc1 + drain + workgroup barrier + relaxed flag; consumer: relaxed poll,
+// one agent acquire, plain gathers (MI355X_MICROARCH.md "Valid forms").
+constexpr int C1F_BLOCK = 256;
+constexpr unsigned C1F_SPIN_LIMIT = 1u << 22;
+
+__device__ __forceinline__ bool reduce_grid_pair(double a, double b, double* pa, double* pb, unsigned* counters,
+                                                 double* ta, double* tb, double* lds4, int* lds_flag) {
+    const unsigned G = gridDim.x;
+    const unsigned nsh = G < (unsigned)RED_SHARDS ? G : (unsigned)RED_SHARDS;
+    const unsigned sh = blockIdx.x % RED_SHARDS;
+    const unsigned in_shard = (G - sh + RED_SHARDS - 1) / RED_SHARDS;
+    double* sa = pa + G;
+    double* sb = pb + G;
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(&pa[blockIdx.x], a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&pb[blockIdx.x], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned t = __hip_atomic_fetch_add(&counters[sh * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = (t == in_shard - 1);
+        if (last) __hip_atomic_store(&counters[sh * 32], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *lds_flag = last;
+    }
+    __syncthreads();
+    if (!*lds_flag) return false;
+    double va = 0.0, vb = 0.0;
+    for (unsigned i = threadIdx.x; i < in_shard; i += C1F_BLOCK) {
+        va += __hip_atomic_load(&pa[sh + i * RED_SHARDS], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        vb += __hip_atomic_load(&pb[sh + i * RED_SHARDS], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    va = block_sum256(va, lds4);
+    vb = block_sum256(vb, lds4);
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(&sa[sh], va, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&sb[sh], vb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned* top = &counters[RED_SHARDS * 32];
+        const unsigned t = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = (t == nsh - 1);
+        if (last) __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *lds_flag = last;
+    }
+    __syncthreads();
+    if (!*lds_flag) return false;
+    const double s1 = (threadIdx.x < nsh) ? __hip_atomic_load(&sa[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+    const double s2 = (threadIdx.x < nsh) ? __hip_atomic_load(&sb[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+    *ta = block_sum256(s1, lds4);
+    *tb = block_sum256(s2, lds4);
+    return true;
+}
+
+struct Cg1FArgs {
+    int64_t nslices, nrows;
+    const int64_t* slice_ptr;
+    const void* cols;
+    const double* vals;
+    double *x, *r, *p, *sv, *u, *v;
+    const double* w;
+    const int32_t* ipos;
+    const uint8_t* own;
+    double* send;
+    const double* recv;
+    int64_t off;
+    PcgState* st;
+    RedBuf red;
+    P2PArgs xp;
+    double* hist;
+    int64_t hist_len;
+    const int32_t* win;   // [2 G]: first / last logical workgroup of each workgroup's gather window
+    unsigned* flags;      // [G lines] u-flags (epochs = iteration numbers), then the give-up word; zeroed at start
+    int tune_rev;
+};
+
+template <int BS, typename CI, bool PAIR>
+__global__ void __launch_bounds__(C1F_BLOCK) k_cg1_fused(Cg1FArgs a) {
+    __shared__ double lds4[4];
+    __shared__ int flag;
+    __shared__ int ok_lds;
+    PcgState* st = a.st;
+    const Cg1Step k = cg1_eval(st, cg1_scalar(a.recv, a.send, a.off, 0, a.xp), cg1_scalar(a.recv, a.send, a.off, 1, a.xp));
+    if (!k.go) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) cg1_commit(st, k, a.hist, a.hist_len);
+        return;
+    }
+    const int G = gridDim.x;
+    const int L = (blockIdx.x % NXCD) * (G / NXCD) + blockIdx.x / NXCD;   // XCD-contiguous logical order
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const int64_t sA = (int64_t)L * a.nslices / G, sB = (int64_t)(L + 1) * a.nslices / G;
+    const bool cg = st->mode != FEM_MODE_PCG;
+    const double alpha = k.alpha, beta = k.beta;
+    const unsigned e = (unsigned)k.it + 1;
+    unsigned* tmo = a.flags + (size_t)G * 32;
+    // ---- update of the own rows (as k_cg1_update), u stored sc1 for the hand-off
+    double gp = 0.0;
+    for (int64_t sl = sA + wv; sl < sB; sl += C1F_BLOCK / 64) {
+        const int64_t node = sl * 64 + lane;
+        if (node >= a.nrows) continue;
+        const int32_t j = a.ipos ? a.ipos[node] : -1;
+#pragma unroll
+        for (int c = 0; c < BS; ++c) {
+            const int64_t i = node * BS + c;
+            double vi = a.v[i];
+            if (j >= 0) {
+                if (a.xp.P) {
+                    double acc = 0.0;
+                    for (int r = 0; r < a.xp.P; ++r) {
+                        const int src = a.xp.csrc[(int64_t)j * a.xp.P + r];
+                        if (src == -1) acc += vi;
+                        else if (src >= 0) acc += a.xp.precv[src + c];
+                    }
+                    vi = acc;
+                } else {
+                    vi = a.recv[(int64_t)j * BS + c];
+                }
+            }
+            const double pi = a.u[i] + beta * a.p[i];
+            const double si = vi + beta * a.sv[i];
+            a.p[i] = pi;
+            a.sv[i] = si;
+            a.x[i] += alpha * pi;
+            double ri = a.r[i] - alpha * si;
+            const double wi = a.w[i];
+            if (cg && wi == 0.0) ri = 0.0;
+            a.r[i] = ri;
+            const double ui = wi * ri;
+            __hip_atomic_store(a.u + i, ui, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (!a.own || a.own[node]) gp += ri * ui;
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave drains its u stores
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(a.flags + (size_t)L * 32, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // ---- wait for the u of the gather window
+    if (wv == 0) {
+        const int wlo = a.win[L], whi = a.win[G + L];
+        bool ok = true;
+        for (int b0 = wlo; b0 <= whi && ok; b0 += 64) {
+            const int jw = b0 + lane;
+            bool done = jw > whi;
+            for (unsigned spins = 0; !__all(done); ++spins) {
+                if (!done) done = __hip_atomic_load(a.flags + (size_t)jw * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= e;
+                if ((spins & 63) == 63 && __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    ok = false;
+                    break;
+                }
+                if (spins >= C1F_SPIN_LIMIT) {
+                    __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        if (lane == 0) {
+            ok_lds = ok;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (!ok_lds) {   // a neighbour never arrived: end the solve (the reduction below is abandoned)
+        if (threadIdx.x == 0) {
+            st->status = FEM_PCG_SYNC_TIMEOUT;
+            st->halt = 1;
+        }
+        return;
+    }
+    // ---- v = A u over the own slices, interface rows packed, d partial
+    const CI* cols = reinterpret_cast<const CI*>(a.cols);
+    const VecPlain uv{a.u};
+    const bool rev = a.tune_rev && ((k.it + 1) & 1);
+    double dot = 0.0;
+    for (int64_t t = sA + wv; t < sB; t += C1F_BLOCK / 64) {
+        const int64_t sl = rev ? sA + sB - 1 - t : t;
+        double o[BS];
+        if constexpr (PAIR) sell_row_paired<BS>(sl, lane, a.slice_ptr, cols, a.vals, a.u, o);
+        else sell_row<BS, SPMV_U, (BS > 1 && SPMV_NT3), decltype(uv), CI>(sl, lane, a.slice_ptr, cols, a.vals, uv, o);
+        const int64_t row = sl * 64 + lane;
+        if (row < a.nrows) {
+            const int32_t j = a.ipos ? a.ipos[row] : -1;
+#pragma unroll
+            for (int c = 0; c < BS; ++c) {
+                a.v[row * BS + c] = o[c];
+                dot += a.u[row * BS + c] * o[c];
+                if (j >= 0) {
+                    if (a.xp.P) {
+                        for (int r = 0; r < a.xp.P; ++r) {
+                            const int dst = a.xp.csrc[(int64_t)j * a.xp.P + r];
+                            if (dst >= 0) a.xp.psend[dst + c] = o[c];
+                        }
+                    } else {
+                        a.send[(int64_t)j * BS + c] = o[c];
+                    }
+                }
+            }
+        }
+    }
+    gp = block_sum256(gp, lds4);
+    dot = block_sum256(dot, lds4);
+    double gt, dt;
+    if (reduce_grid_pair(gp, dot, a.red.part(RED_K2), a.red.part(RED_K1), a.red.cnt(RED_K1), &gt, &dt, lds4, &flag) &&
+        threadIdx.x == 0) {
+        cg1_commit(st, k, a.hist, a.hist_len);   // every block has evaluated the step by now
+        st->red[1] = gt;
+        st->red[0] = dt;
+        a.send[a.off] = gt;
+        a.send[a.off + 1] = dt;
+        for (int r = 0; r < a.xp.P; ++r) {
+            const int dst = a.xp.ssrc[r];
+            if (dst >= 0) {
+                a.xp.psend[dst] = gt;
+                a.xp.psend[dst + 1] = dt;
+            }
+        }
+    }
+}
+
+// gather window per logical workgroup of a G-workgroup slice split (generic column type)
+template <typename CI>
+__global__ void k_c1f_window(int64_t nslices, int64_t nrows, const int64_t* __restrict__ slice_ptr,
+                             const CI* __restrict__ cols, int G, int* __restrict__ lo, int* __restrict__ hi) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nslices * 64;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t sl = t >> 6;
+        const int l = (int)(t & 63);
+        const int64_t row = sl * 64 + l;
+        const int64_t p0 = slice_ptr[sl];
+        const int w = (int)((slice_ptr[sl + 1] - p0) >> 6);
+        int64_t cmin = row < nrows ? row : nrows - 1, cmax = cmin;
+        for (int kk = 0; kk < w; ++kk) {
+            int64_t c = (int64_t)cols[p0 + 64 * kk + l];
+            if constexpr (sizeof(CI) == 2) c += row;
+            cmin = c < cmin ? c : cmin;
+            cmax = c > cmax ? c : cmax;
+        }
+        if (cmax >= nrows) cmax = nrows - 1;
+        if (cmin < 0) cmin = 0;
+        auto owner = [&](int64_t r) { return (int)((((r >> 6) + 1) * G - 1) / nslices); };
+        const int me = owner(row < nrows ? row : nrows - 1);
+        int olo = owner(cmin), ohi = owner(cmax);
+        for (int off = 32; off > 0; off >>= 1) {
+            const int a2 = __shfl_xor(olo, off), b2 = __shfl_xor(ohi, off);
+            olo = a2 < olo ? a2 : olo;
+            ohi = b2 > ohi ? b2 : ohi;
+        }
+        if (l == 0) {
+            atomicMin(lo + me, olo);
+            atomicMax(hi + me, ohi);
+        }
+    }
+}
+
 }  // namespace fem
 #include "pcg_persist.hpp"
 namespace fem {
@@ -1173,6 +1432,12 @@ struct fem_pcg {
     const int32_t* p2p_ssrc;   // [nranks] precv offset of rank r's [g, d], -1 own
     double* psend;
     double* precv;
+    // fused distributed iteration (FEM_TUNE_C1F): one launch per iteration, u hand-off by flags
+    int c1f;
+    int c1f_grid;
+    int c1f_win_ok;
+    int32_t* c1f_win;      // [2 G]
+    unsigned* c1f_flags;   // (G + 1) lines
     // persistent schedule (3): requested by fem_pcg_set_schedule, active after fem_pcg_start when supported
     int persist_req;
     int persist;
@@ -1316,6 +1581,104 @@ static int cg1_step_update(fem_pcg* s) {
     return FEM_OK;
 }
 
+// fused iteration setup (at fem_pcg_start of a single-reduction distributed context with FEM_TUNE_C1F): the grid
+// (resident by the occupancy query), the gather windows of this matrix, zeroed flags
+static const void* c1f_fn(const fem_pcg* s) {
+    if (s->paired && s->bs == 1) return (const void*)k_cg1_fused<1, int16_t, true>;
+    if (s->paired) return (const void*)k_cg1_fused<3, int16_t, true>;
+    if (s->cols16 && s->bs == 1) return (const void*)k_cg1_fused<1, int16_t, false>;
+    if (s->cols16) return (const void*)k_cg1_fused<3, int16_t, false>;
+    if (s->bs == 1) return (const void*)k_cg1_fused<1, int32_t, false>;
+    return (const void*)k_cg1_fused<3, int32_t, false>;
+}
+
+static int c1f_setup(fem_pcg* s) {
+    s->c1f = 0;
+    if (!(s->tune & FEM_TUNE_C1F) || !s->dist || !s->cg1 || s->nslices == 0) return FEM_OK;
+    int dev = 0, ncu = 0, nb = 0;
+    FEM_HIP(hipGetDevice(&dev));
+    FEM_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, c1f_fn(s), C1F_BLOCK, 0));
+    if (nb < 1 || ncu < NXCD) return FEM_OK;
+    const int per = nb < 2 ? nb : 2;   // 8 waves per CU (4 per CU: 10M 103 -> 93 us, 1.2M tets 21.6 -> 25.1 us)
+    int G = (ncu / NXCD) * NXCD * per;
+    while (G > NXCD && (int64_t)G > s->nslices) G -= NXCD;   // at least one slice per workgroup
+    if (G != s->c1f_grid) {
+        if (s->c1f_win) (void)hipFree(s->c1f_win);
+        if (s->c1f_flags) (void)hipFree(s->c1f_flags);
+        s->c1f_win = nullptr;
+        s->c1f_flags = nullptr;
+        FEM_HIP(hipMalloc(&s->c1f_win, sizeof(int32_t) * 2 * G));
+        FEM_HIP(hipMalloc(&s->c1f_flags, sizeof(unsigned) * 32 * (size_t)(G + 1)));
+        s->c1f_grid = G;
+        s->c1f_win_ok = 0;
+    }
+    if (!s->c1f_win_ok) {
+        std::vector<int32_t> lohi(2 * (size_t)G);
+        for (int i = 0; i < G; ++i) {
+            lohi[i] = G;
+            lohi[G + i] = -1;
+        }
+        FEM_HIP(hipMemcpyAsync(s->c1f_win, lohi.data(), sizeof(int32_t) * 2 * G, hipMemcpyHostToDevice, s->stream));
+        if (s->cols16)
+            hipLaunchKernelGGL(k_c1f_window<int16_t>, dim3(stream_grid(s->nslices * 64, 256)), dim3(256), 0, s->stream,
+                               s->nslices, s->nrows, s->slice_ptr, s->cols16, G, s->c1f_win, s->c1f_win + G);
+        else
+            hipLaunchKernelGGL(k_c1f_window<int32_t>, dim3(stream_grid(s->nslices * 64, 256)), dim3(256), 0, s->stream,
+                               s->nslices, s->nrows, s->slice_ptr, s->cols, G, s->c1f_win, s->c1f_win + G);
+        FEM_LAUNCHED();
+        FEM_HIP(hipStreamSynchronize(s->stream));   // lohi must outlive the copy
+        s->c1f_win_ok = 1;
+    }
+    FEM_HIP(hipMemsetAsync(s->c1f_flags, 0, sizeof(unsigned) * 32 * (size_t)(G + 1), s->stream));
+    s->c1f = 1;
+    return FEM_OK;
+}
+
+static int c1f_launch(fem_pcg* s) {
+    Cg1FArgs a{};
+    a.nslices = s->nslices;
+    a.nrows = s->nrows;
+    a.slice_ptr = s->slice_ptr;
+    if (s->paired) {
+        a.cols = pcols(s);
+        a.vals = s->pvals;
+    } else if (s->cols16) {
+        a.cols = s->cols16;
+        a.vals = s->vals;
+    } else {
+        a.cols = s->cols;
+        a.vals = s->vals;
+    }
+    a.x = s->x;
+    a.r = s->r;
+    a.p = s->p0;
+    a.sv = s->cg1_s;
+    a.u = s->cg1_u;
+    a.v = s->q;
+    a.w = s->w;
+    a.ipos = s->nI > 0 ? s->ipos : nullptr;
+    a.own = s->own;
+    a.send = s->cg1_send;
+    a.recv = s->cg1_recv;
+    a.off = s->nI * s->bs;
+    a.st = s->st;
+    a.red = s->red;
+    a.xp = p2p_args(s);
+    a.hist = s->hist;
+    a.hist_len = s->hist_len;
+    a.win = s->c1f_win;
+    a.flags = s->c1f_flags;
+    a.tune_rev = (s->tune & FEM_TUNE_REVERSE) ? 1 : 0;
+    void* args[] = {&a};
+    FEM_HIP(hipLaunchKernel(c1f_fn(s), dim3(s->c1f_grid), dim3(C1F_BLOCK), args, 0, s->stream));
+    FEM_LAUNCHED();
+    if (!s->comm && !s->p2p)   // group path: the caller sums recv in place
+        FEM_HIP(hipMemcpyAsync(s->cg1_recv, s->cg1_send, sizeof(double) * (size_t)cg1_len(s), hipMemcpyDeviceToDevice,
+                               s->stream));
+    return FEM_OK;
+}
+
 static int dist_phase(fem_pcg* s, int phase) {
     int rc = FEM_OK;
     switch (phase) {
@@ -1356,6 +1719,7 @@ static int dist_phase(fem_pcg* s, int phase) {
             return FEM_OK;
         case 4:   // single-reduction iteration: step + update + v = A u and pack | sum [v interface | g | d]
             if (!s->cg1) break;
+            if (s->c1f) return c1f_launch(s);
             if ((rc = cg1_step_update(s))) return rc;
             return cg1_spmv(s, 0);
         case 20:  // single-reduction start (after 10): unpack A x0, r0, u0, g0; v0 = A u0 and pack | sum
@@ -2021,6 +2385,7 @@ int fem_pcg_start(fem_pcg* s) {
     {
         int prc = refresh_pairing(s);
         if (!prc) prc = persist_setup(s);
+        if (!prc) prc = c1f_setup(s);
         if (prc) return prc;
     }
     PcgState h{};
@@ -2459,6 +2824,8 @@ void fem_pcg_destroy(fem_pcg* s) {
     if (s->cg1_recv) (void)hipFree(s->cg1_recv);
     if (s->psend) (void)hipFree(s->psend);
     if (s->precv) (void)hipFree(s->precv);
+    if (s->c1f_win) (void)hipFree(s->c1f_win);
+    if (s->c1f_flags) (void)hipFree(s->c1f_flags);
     if (s->con.tmp) (void)hipFree(s->con.tmp);
     if (s->pvals) (void)hipFree(s->pvals);
     if (s->pcols16) (void)hipFree(s->pcols16);

@@ -37,6 +37,9 @@ VARIANT_TWO, VARIANT_SINGLE = 0, 1
 # exchange of the single-reduction variant: the all-reduce over the GLOBAL interface vector, or grouped
 # ncclSend/ncclRecv of [g, d | rows shared with that rank] with every other rank + a fixed-rank-order sum
 EXCHANGE_ALLREDUCE, EXCHANGE_P2P = "allreduce", "p2p"
+# tuning flags of the distributed contexts (include/fem355.h FEM_TUNE_*): the single-GPU defaults, plus FEM_TUNE_C1F
+# for the fused one-launch iteration (k_cg1_fused)
+TUNE_DEFAULT, TUNE_C1F = 1 | 2 | 4 | 8, 16
 
 
 # ============================================================================ partition (host logic, any device)
@@ -216,14 +219,16 @@ class DistSystem:
             self._p2p = p2p_maps(self.rm, t, self.bs)
         return self._p2p
 
-    def runner(self, b, w, tol=0.0, mode=C.MODE_PCG, hist_len=0, variant=VARIANT_SINGLE, exchange=EXCHANGE_ALLREDUCE):
-        return DistRunner(self, b, w, tol, mode, hist_len, variant, exchange)
+    def runner(self, b, w, tol=0.0, mode=C.MODE_PCG, hist_len=0, variant=VARIANT_SINGLE, exchange=EXCHANGE_ALLREDUCE,
+               fused=False):
+        return DistRunner(self, b, w, tol, mode, hist_len, variant, exchange, fused)
 
 
 class DistRunner(_sys._DistMarker, _sys.PcgRunner):
     """(P)CG context of one rank in distributed mode."""
 
-    def __init__(self, ds: DistSystem, b, w, tol, mode, hist_len=0, variant=None, exchange=EXCHANGE_ALLREDUCE):
+    def __init__(self, ds: DistSystem, b, w, tol, mode, hist_len=0, variant=None, exchange=EXCHANGE_ALLREDUCE,
+                 fused=False):
         super().__init__(ds.A, b, w, mode=mode, tol=tol)
         self.ds = ds
         self.hist = torch.full((max(hist_len, 1),), float("nan"), dtype=F64, device=ds.dev) if hist_len else None
@@ -236,6 +241,8 @@ class DistRunner(_sys._DistMarker, _sys.PcgRunner):
             if self.variant != VARIANT_SINGLE:
                 raise ValueError("the neighbour exchange needs the single-reduction variant")
             set_p2p(self.lib, self.h, ds.p2p())
+        if fused:
+            C.check(self.lib.fem_pcg_set_tuning(self.h, TUNE_DEFAULT | TUNE_C1F), "fem_pcg_set_tuning")
 
     def phase(self, k):
         C.check(self.lib.fem_pcg_dist_phase(self.h, int(k)), "fem_pcg_dist_phase")
@@ -282,11 +289,13 @@ class PartitionGroup:
         arr = (ctypes.c_void_p * len(runs))(*[run.h.value for run in runs])
         C.check(self.lib.fem_p2p_deliver(arr, len(runs), C.stream(self.dev)), "fem_p2p_deliver")
 
-    def solve(self, bs_local, ws, tol, max_iter, mode=C.MODE_PCG, variant=None, exchange=EXCHANGE_ALLREDUCE):
+    def solve(self, bs_local, ws, tol, max_iter, mode=C.MODE_PCG, variant=None, exchange=EXCHANGE_ALLREDUCE,
+              fused=False):
         """Phase-driven (P)CG over the P partitions; returns (per-rank x, iterations, status)."""
         # every context on the current stream: the phases of all ranks and the group sums serialise in order
         variant = VARIANT_SINGLE if variant is None else int(variant)
-        runs = [_GroupRunner(r, b, w, tol, mode, variant, exchange) for r, b, w in zip(self.ranks, bs_local, ws)]
+        runs = [_GroupRunner(r, b, w, tol, mode, variant, exchange, fused)
+                for r, b, w in zip(self.ranks, bs_local, ws)]
         for run in runs:
             run.start_state()
         p2p = exchange == EXCHANGE_P2P
@@ -326,7 +335,7 @@ class PartitionGroup:
 class _GroupRunner:
     """Distributed (P)CG context on the current stream, driven phase by phase by PartitionGroup."""
 
-    def __init__(self, ds: DistSystem, b, w, tol, mode, variant=0, exchange=EXCHANGE_ALLREDUCE):
+    def __init__(self, ds: DistSystem, b, w, tol, mode, variant=0, exchange=EXCHANGE_ALLREDUCE, fused=False):
         self.lib = C.lib()
         A = ds.A
         self.b = b.to(F64).contiguous()
@@ -343,6 +352,8 @@ class _GroupRunner:
         C.check(self.lib.fem_pcg_set_dist_variant(self.h, int(variant)), "fem_pcg_set_dist_variant")
         if exchange == EXCHANGE_P2P:
             set_p2p(self.lib, self.h, ds.p2p())
+        if fused:
+            C.check(self.lib.fem_pcg_set_tuning(self.h, TUNE_DEFAULT | TUNE_C1F), "fem_pcg_set_tuning")
 
     def start_state(self):
         C.check(self.lib.fem_pcg_start(self.h), "fem_pcg_start")   # state only (phases do the work)
@@ -480,7 +491,8 @@ def bench_main(a, metric):
 
     variant = int(getattr(a, "dist_variant", VARIANT_SINGLE))
     exchange = getattr(a, "dist_exchange", EXCHANGE_ALLREDUCE) if variant == VARIANT_SINGLE else EXCHANGE_ALLREDUCE
-    run = ds.runner(b, w, tol=tol, variant=variant, exchange=exchange)
+    fused = bool(getattr(a, "dist_fused", 0)) and variant == VARIANT_SINGLE
+    run = ds.runner(b, w, tol=tol, variant=variant, exchange=exchange, fused=fused)
     barrier_sync()
     t0 = time.perf_counter()
     run.start()
@@ -496,7 +508,7 @@ def bench_main(a, metric):
     t_solve = tmax(time.perf_counter() - t0)
     run.close()
 
-    run = ds.runner(b, w, tol=0.0, variant=variant, exchange=exchange)
+    run = ds.runner(b, w, tol=0.0, variant=variant, exchange=exchange, fused=fused)
     run.start()
     import math
     graph_k = use_graph(run, math.gcd(math.gcd(gk, a.steps), a.warmup) if gk > 0 else 0)
@@ -536,7 +548,7 @@ def bench_main(a, metric):
                        "tets": int(tets.shape[0]), "dofs": N * bs, "interface_nodes": nI,
                        "parallelism": f"element partition x{world}", "graph_iterations": graph_k,
                        "dist_variant": "single-reduction" if variant else "two-reduction",
-                       "dist_exchange": exchange},
+                       "dist_exchange": exchange, "dist_fused_iteration": fused},
             "dofs_per_s": N * bs / (t_asm + t_solve), "assembly_ms": t_asm * 1e3, "solve_ms": t_solve * 1e3,
             "assembly_stages_rank0": stages,
             "solve_iters": it, "solve_status": stt,

@@ -379,7 +379,10 @@ int fem_enforce_constraints(double* x, double* r, int64_t n, int order, int64_t 
  * odd iterations, so the matrix tail read last (still in the MI355X's 256 MB memory-side cache) is read first by
  * the next sweep: 67 -> 57 us per SpMV on the 10M Poisson matrix. Results depend on the flags only through the
  * order of the per-block p.q partials (deterministic for a given flag set). */
-enum { FEM_TUNE_REVERSE = 1, FEM_TUNE_PAIR = 2, FEM_TUNE_PK_SC1 = 4, FEM_TUNE_PK_PACK = 8 };
+enum { FEM_TUNE_REVERSE = 1, FEM_TUNE_PAIR = 2, FEM_TUNE_PK_SC1 = 4, FEM_TUNE_PK_PACK = 8, FEM_TUNE_C1F = 16 };
+/* FEM_TUNE_C1F: distributed single-reduction contexts run each iteration as ONE launch (k_cg1_fused: step, update,
+ * u hand-off to the neighbouring workgroups by flags, SpMV, pack, one two-value grid reduction) instead of
+ * k_cg1_update + k_cg1_spmv. */
 /* FEM_TUNE_PK_PACK (default): persistent schedule only — each workgroup gives its waves ceil(max slices per
  * workgroup / 16) slices each in order (the last busy wave takes the remainder) instead of spreading them evenly:
  * at 10M 15 waves x 7 slices all stream to the end of the SpMV phase instead of 7-slice waves finishing alone

@@ -10,11 +10,13 @@ pytestmark = pytest.mark.gpu
 F64 = torch.float64
 
 
-@pytest.mark.parametrize("variant,exchange", [(0, "allreduce"), (1, "allreduce"), (1, "p2p")])
+@pytest.mark.parametrize("variant,exchange,fused", [(0, "allreduce", False), (1, "allreduce", False),
+                                                    (1, "p2p", False), (1, "allreduce", True), (1, "p2p", True)])
 @pytest.mark.parametrize("kind,P", [("poisson", 1), ("poisson", 2), ("poisson", 8), ("elastic", 3)])
-def test_partition_group_matches_single_gpu(gpu, kind, P, variant, exchange):
+def test_partition_group_matches_single_gpu(gpu, kind, P, variant, exchange, fused):
     """variant 0: two reductions per iteration; 1: single reduction (Chronopoulos-Gear form, one exchange: the
-    all-reduce over the global interface vector, or the neighbour exchange with a fixed-rank-order sum)."""
+    all-reduce over the global interface vector, or the neighbour exchange with a fixed-rank-order sum), with the
+    iteration as two kernels or as one fused launch (u hand-off between workgroups by flags)."""
     import fem355  # noqa: F401
     from fem355 import dist as fd, mesh, system
     coords, tets = mesh.kuhn_cube(10, jitter=0.1)
@@ -43,7 +45,7 @@ def test_partition_group_matches_single_gpu(gpu, kind, P, variant, exchange):
     for r, wl in zip(grp.ranks, ws):
         assert rel(wl, w.view(-1, bs)[r.rm.nodes].reshape(-1)) < 1e-14
     bl = [r.local(f) for r in grp.ranks]
-    xs, it, st = grp.solve(bl, ws, tol, 3000, variant=variant, exchange=exchange)
+    xs, it, st = grp.solve(bl, ws, tol, 3000, variant=variant, exchange=exchange, fused=fused)
     assert st == 1 and abs(it - ref.iterations) <= 2, (it, ref.iterations)
     u = fd.gather_solution(grp.ranks, xs, N, bs)
     assert rel(u.reshape(-1), ref.x) < 1e-10
