@@ -372,6 +372,9 @@ constexpr int AW_WAVES = 4;   // waves per 256-thread block of the wave-per-row 
 #ifndef FEM_P1_LPR
 #define FEM_P1_LPR 16   // P1 assembly: lanes per row (four rows per wave; 64: 2.95 ms, 32: 1.52, 16: 1.11 on 10M tets)
 #endif
+#ifndef FEM_KE_KU
+#define FEM_KE_KU 8     // bs = 3 / bs = 1 assembly from K_e: incident elements whose loads are in flight per batch
+#endif
 #ifndef FEM_KE_RPL3
 #define FEM_KE_RPL3 1   // bs = 3 assembly from K_e: block rows per lane (3, one lane per column: c3d8 4.2 -> 5.1 ms)
 #endif
@@ -388,7 +391,7 @@ __global__ void __launch_bounds__(256) k_assemble_ke_w(const double* __restrict_
     constexpr int LPC = BS / RPL;
     constexpr int JG = 64 / LPC;
     constexpr int D = NPE * BS;
-    constexpr int KU = (RPL == 1) ? 8 : 4;
+    constexpr int KU = (RPL == 1) ? FEM_KE_KU : 4;
     __shared__ int node_s[AW_WAVES][64 * NPE];
     __shared__ int64_t krow_s[AW_WAVES][64];   // offset of the element's block row a in Ke
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
