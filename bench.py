@@ -121,8 +121,13 @@ def main():
     C.lib()
 
     # ---- warm the kernels (module load, first-launch costs) on a small mesh
-    c0, t0_ = mesh.kuhn_cube(8, device=dev)
-    system.assemble_tet4_system(c0, t0_, a.kind, 1.0, 0.3).matvec(torch.ones(c0.shape[0] * (1 if a.kind == "poisson" else 3), dtype=torch.float64, device=dev))
+    c0, t0_ = mesh.kuhn_cube(20, device=dev)   # 9k rows: enough slices for the persistent kernel's grid
+    A0 = system.assemble_tet4_system(c0, t0_, a.kind, 1.0, 0.3)
+    b0 = torch.ones(A0.n, dtype=torch.float64, device=dev)
+    A0.matvec(b0)
+    A0.pcg(b0, None, w=A0.jacobi(torch.zeros(A0.n, dtype=torch.uint8, device=dev)), mode=C.MODE_PCG, tol=0.0,
+           max_iter=4, chunk=4)   # the solver kernels (the persistent one included)
+    del A0, b0
     sync()
 
     coords, tets = mesh.kuhn_cube(a.n, device=dev)
