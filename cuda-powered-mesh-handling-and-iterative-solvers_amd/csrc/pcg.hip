@@ -1593,11 +1593,12 @@ static const void* c1f_fn(const fem_pcg* s) {
     return (const void*)k_cg1_fused<3, int32_t, false>;
 }
 
-// Context buffers of the solve (vectors, reduction words, the paired matrix copy, persistent-kernel words) are
+// Context buffers of bs = 1 solves (vectors, reduction words, the paired matrix copy, persistent-kernel words) are
 // recycled through a process-wide cache keyed by (device, exact size) instead of hipFree'd: tearing down a 10M
 // context cost 1.4 ms (4 % of a 682-iteration solve) with hipFree and with the stream-ordered pool alike, and
 // repeated solves on one matrix ask for the same sizes. At most PCG_CACHE_KEEP bytes are kept (oldest freed first).
-// RCCL buffers keep plain hipMalloc.
+// RCCL buffers and bs = 3 contexts keep plain hipMalloc: with recycled buffers the 10M elastic SpMV ran 311 -> 367 us
+// (whatever the match order; cause not found), for 1 ms less teardown.
 #ifndef FEM_PCG_POOL
 #define FEM_PCG_POOL 1
 #endif
@@ -1615,13 +1616,14 @@ std::vector<DevBuf> dev_live;    // handed out by pool_alloc
 size_t dev_cache_bytes = 0;
 }  // namespace
 
-static hipError_t pool_alloc(void** p, size_t bytes, hipStream_t) {
-    if (!FEM_PCG_POOL) return hipMalloc(p, bytes);
+static hipError_t pool_alloc(void** p, size_t bytes, hipStream_t, bool cached) {
+    if (!FEM_PCG_POOL || !cached) return hipMalloc(p, bytes);
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     std::lock_guard<std::mutex> g(dev_cache_mu);
-    for (size_t i = dev_cache.size(); i-- > 0;) {
+    // oldest first: a context created after another one's teardown gets the same buffers in the same roles
+    for (size_t i = 0; i < dev_cache.size(); ++i) {
         if (dev_cache[i].bytes == bytes && dev_cache[i].dev == dev) {
             *p = dev_cache[i].p;
             dev_cache_bytes -= bytes;
@@ -2253,15 +2255,16 @@ int fem_pcg_create(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_
     s->grid_vec = grid_multiple_of_xcd(cdiv(s->n / 2 + 1, PCG_BLOCK), 1024);
     size_t vec = sizeof(double) * (size_t)(s->n + 2);
     hipError_t e = hipSuccess;
-    if (e == hipSuccess) e = pool_alloc((void**)&s->r, vec, s->stream);
-    if (e == hipSuccess) e = pool_alloc((void**)&s->p0, vec, s->stream);
-    if (e == hipSuccess) e = pool_alloc((void**)&s->p1, vec, s->stream);
-    if (e == hipSuccess) e = pool_alloc((void**)&s->q, vec, s->stream);
-    if (e == hipSuccess) e = pool_alloc((void**)&s->red.partials, sizeof(double) * RED_N * MAX_PARTIALS, s->stream);
+    if (e == hipSuccess) e = pool_alloc((void**)&s->r, vec, s->stream, s->bs == 1);
+    if (e == hipSuccess) e = pool_alloc((void**)&s->p0, vec, s->stream, s->bs == 1);
+    if (e == hipSuccess) e = pool_alloc((void**)&s->p1, vec, s->stream, s->bs == 1);
+    if (e == hipSuccess) e = pool_alloc((void**)&s->q, vec, s->stream, s->bs == 1);
     if (e == hipSuccess)
-        e = pool_alloc((void**)&s->red.counters, sizeof(unsigned) * RED_N * RED_COUNTER_WORDS, s->stream);
+        e = pool_alloc((void**)&s->red.partials, sizeof(double) * RED_N * MAX_PARTIALS, s->stream, s->bs == 1);
+    if (e == hipSuccess)
+        e = pool_alloc((void**)&s->red.counters, sizeof(unsigned) * RED_N * RED_COUNTER_WORDS, s->stream, s->bs == 1);
     if (e == hipSuccess) e = hipMemsetAsync(s->red.counters, 0, sizeof(unsigned) * RED_N * RED_COUNTER_WORDS, s->stream);
-    if (e == hipSuccess) e = pool_alloc((void**)&s->st, sizeof(PcgState), s->stream);
+    if (e == hipSuccess) e = pool_alloc((void**)&s->st, sizeof(PcgState), s->stream, s->bs == 1);
     if (e == hipSuccess) e = host_state_alloc((void**)&s->st_host, sizeof(PcgState));
     if (e != hipSuccess) {
         set_error("fem_pcg_create: allocation failed: %s", hipGetErrorString(e));
@@ -2362,9 +2365,9 @@ static int persist_setup(fem_pcg* s) {
         s->pk_win = nullptr;
         s->pk_part = nullptr;
         s->pk_sync = nullptr;
-        FEM_HIP(pool_alloc((void**)&s->pk_win, sizeof(int32_t) * 2 * G, s->stream));
-        FEM_HIP(pool_alloc((void**)&s->pk_part, sizeof(double) * 4 * G, s->stream));
-        FEM_HIP(pool_alloc((void**)&s->pk_sync, sizeof(unsigned) * pk_sync_words(G), s->stream));
+        FEM_HIP(pool_alloc((void**)&s->pk_win, sizeof(int32_t) * 2 * G, s->stream, s->bs == 1));
+        FEM_HIP(pool_alloc((void**)&s->pk_part, sizeof(double) * 4 * G, s->stream, s->bs == 1));
+        FEM_HIP(pool_alloc((void**)&s->pk_sync, sizeof(unsigned) * pk_sync_words(G), s->stream, s->bs == 1));
         s->pk_grid = G;
         s->pk_win_ok = 0;
     }
@@ -2381,7 +2384,7 @@ static int persist_setup(fem_pcg* s) {
         FEM_HIP(hipStreamSynchronize(s->stream));   // lohi must outlive the copy
         s->pk_win_ok = 1;
     }
-    if (ovf && !s->pk_v) FEM_HIP(pool_alloc((void**)&s->pk_v, sizeof(double) * (size_t)s->n, s->stream));
+    if (ovf && !s->pk_v) FEM_HIP(pool_alloc((void**)&s->pk_v, sizeof(double) * (size_t)s->n, s->stream, s->bs == 1));
     s->pk_ovf = ovf ? 1 : 0;
     s->persist = 1;
     return FEM_OK;
@@ -2453,7 +2456,7 @@ static int refresh_pairing(fem_pcg* s) {
     FEM_HIP(hipMemcpyAsync(&ent, s->slice_ptr + s->nslices, sizeof(int64_t), hipMemcpyDeviceToHost, s->stream));
     FEM_HIP(hipStreamSynchronize(s->stream));
     if (s->bs == 3) {
-        if (!s->pvals) FEM_HIP(pool_alloc((void**)&s->pvals, sizeof(double) * 9 * (size_t)ent, s->stream));
+        if (!s->pvals) FEM_HIP(pool_alloc((void**)&s->pvals, sizeof(double) * 9 * (size_t)ent, s->stream, s->bs == 1));
         s->pcols16 = nullptr;
         hipLaunchKernelGGL(k_sell3_to_a, dim3(stream_grid(s->nslices * 64, 256)), dim3(256), 0, s->stream, s->nslices,
                            s->slice_ptr, s->vals, s->pvals);
@@ -2462,8 +2465,8 @@ static int refresh_pairing(fem_pcg* s) {
         return FEM_OK;
     }
     if (!s->pvals) {
-        FEM_HIP(pool_alloc((void**)&s->pvals, sizeof(double) * (size_t)ent, s->stream));
-        FEM_HIP(pool_alloc((void**)&s->pcols16, sizeof(int16_t) * (size_t)ent, s->stream));
+        FEM_HIP(pool_alloc((void**)&s->pvals, sizeof(double) * (size_t)ent, s->stream, s->bs == 1));
+        FEM_HIP(pool_alloc((void**)&s->pcols16, sizeof(int16_t) * (size_t)ent, s->stream, s->bs == 1));
     }
     hipLaunchKernelGGL(k_sell_pair, dim3(stream_grid(s->nslices * 64, 256)), dim3(256), 0, s->stream, s->nslices,
                        s->slice_ptr, s->vals, s->cols16, s->pvals, s->pcols16);
