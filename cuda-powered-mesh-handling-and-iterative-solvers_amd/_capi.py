@@ -7,7 +7,10 @@ streams are valid in both.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
+import functools
+import inspect
 import os
 import threading
 
@@ -108,6 +111,7 @@ SIGNATURES = {
     "fem_pcg_finish": (_I, [_P]),
     "fem_pcg_profile": (_I, [_P, _I, _I, ctypes.POINTER(_D), ctypes.POINTER(_I)]),
     "fem_pcg_destroy": (None, [_P]),
+    "fem_pcg_release_cache": (_I, []),
     "fem_sell_diag": (_I, [_P, _I, _P, _P, _L, _P, _P]),
     "fem_jacobi_from_diag": (_I, [_P, _L, _P, _P, _P]),
     "fem_comm_unique_id": (_I, [ctypes.c_char_p]),
@@ -170,8 +174,13 @@ def check(rc: int, what: str = ""):
 
 
 def ptr(t):
-    """Device pointer of a tensor (None -> NULL)."""
-    return None if t is None else ctypes.c_void_p(t.data_ptr())
+    """Device pointer of a tensor (None -> NULL). A host tensor is refused here: its address handed to a kernel
+    would be a memory fault (XNACK off), not an exception."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise FemError(f"fem355: a {t.device} tensor was passed where device memory is required")
+    return ctypes.c_void_p(t.data_ptr())
 
 
 def stream(dev=None):
@@ -185,3 +194,69 @@ def compute_device(device=None) -> torch.device:
         if d.type == "cuda":
             return d if d.index is not None else torch.device("cuda", torch.cuda.current_device())
     return torch.device("cuda", torch.cuda.current_device())
+
+
+def device_scope(dev):
+    """Context that makes `dev` the current HIP device for the calls inside it: the library allocates its
+    workspace on, and launches on the null stream of, the CURRENT device, so every public entry point runs its
+    C calls inside the scope of the device its tensors live on."""
+    d = torch.device(dev)
+    if d.type != "cuda" or d.index is None or d.index == torch.cuda.current_device():
+        return _NULL_SCOPE
+    return torch.cuda.device(d)
+
+
+class _NullScope:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NULL_SCOPE = _NullScope()
+
+
+def on_device(fn):
+    """Decorator for the reference-named public functions: run `fn` with the current HIP device set to the one
+    its `device` argument names (`device="cuda:1"` with current device 0 must not launch on GPU 0)."""
+    sig = inspect.signature(fn)
+    if "device" not in sig.parameters:
+        return fn
+    default = sig.parameters["device"].default
+
+    @functools.wraps(fn)
+    def wrapper(*args, **kwargs):
+        if not torch.cuda.is_available():
+            return fn(*args, **kwargs)
+        dev = kwargs.get("device", default)
+        if "device" not in kwargs:
+            try:
+                dev = sig.bind_partial(*args, **kwargs).arguments.get("device", default)
+            except TypeError:
+                return fn(*args, **kwargs)   # let the call itself raise the reference's TypeError
+        try:
+            d = compute_device(dev)
+        except Exception:
+            return fn(*args, **kwargs)
+        with device_scope(d):
+            return fn(*args, **kwargs)
+
+    return wrapper
+
+
+def scope_module(namespace: dict):
+    """Wrap every public function with a `device` parameter defined in `namespace` (a module's globals())."""
+    mod = namespace.get("__name__")
+    for name, obj in list(namespace.items()):
+        if name.startswith("_") or not inspect.isfunction(obj) or obj.__module__ != mod:
+            continue
+        namespace[name] = on_device(obj)
+
+
+def release_cache() -> int:
+    """Free the solver buffers the library keeps for reuse (MB released)."""
+    return int(_lib.fem_pcg_release_cache()) if _lib is not None else 0
+
+
+atexit.register(release_cache)

@@ -181,3 +181,6 @@ def new_enforce_constraints(u, r, spc_nodes, spc_dofs, spc_values, rbe2_slaves, 
 
 __all__ = ["parse_spc_list", "parse_rbe2_list", "parse_rbe3_list", "apply_loads_to_F", "enforce_constraints",
            "new_enforce_constraints", "ConstraintSet"]
+
+# every public function runs in the scope of the device its `device` argument names (_capi.on_device)
+C.scope_module(globals())

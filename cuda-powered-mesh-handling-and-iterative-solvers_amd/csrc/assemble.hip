@@ -814,7 +814,9 @@ __global__ void k_jacobi(const double* __restrict__ vals, int bs, const int32_t*
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t node = i / bs;
         const int r = (int)(i - node * bs);
-        const double dg = vals[sell_val(csr2sell[diagpos[node]], bs * bs, r * bs + r)];
+        // diagpos < 0: a node no element touches (diagonal 0 -> 1/0 = inf -> 0, `solver/solver.py:828-831`)
+        const int32_t dp = diagpos[node];
+        const double dg = dp < 0 ? 0.0 : vals[sell_val(csr2sell[dp], bs * bs, r * bs + r)];
         double v = 1.0 / dg;
         if (v == INFINITY) v = 0.0;  // `solver/solver.py:831` (only +inf)
         if (mask && mask[i]) v = 0.0;
@@ -828,7 +830,8 @@ __global__ void k_sell_diag(const double* __restrict__ vals, int bs, const int32
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t node = i / bs;
         const int r = (int)(i - node * bs);
-        out[i] = vals[sell_val(csr2sell[diagpos[node]], bs * bs, r * bs + r)];
+        const int32_t dp = diagpos[node];   // < 0: no diagonal entry (unused node)
+        out[i] = dp < 0 ? 0.0 : vals[sell_val(csr2sell[dp], bs * bs, r * bs + r)];
     }
 }
 

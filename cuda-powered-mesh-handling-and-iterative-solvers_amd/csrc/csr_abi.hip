@@ -252,6 +252,8 @@ int fem_csr_pattern(const int64_t* conn, int64_t M, int npe, int dofs_per_node, 
         const int64_t nr = n_nodes * dpn;
         hipLaunchKernelGGL(k_dof_rowptr, dim3(stream_grid(nr + 1, 256)), dim3(256), 0, st, g.rowptr, n_nodes, dpn,
                            rowptr);
+        if (colidx && diagpos && hipMemsetAsync(diagpos, 0xff, sizeof(int32_t) * (size_t)nr, st) != hipSuccess)
+            rc = FEM_EHIP;   // -1 = no diagonal (a node no element touches)
         if (colidx)
             hipLaunchKernelGGL(k_dof_cols, dim3(stream_grid(nr, 256)), dim3(256), 0, st, g.rowptr, g.colidx, n_nodes,
                                dpn, rowptr, colidx, diagpos);

@@ -507,6 +507,9 @@ int fem_graph_fill2(const int64_t* conn, int npe, const int32_t* inc_ptr, const 
                     const int32_t* rowptr, const int32_t* tmp, int32_t* colidx, int32_t* diagpos,
                     fem_stream_t stream) {
     if (N <= 0) return FEM_OK;
+    // a node no element touches has no diagonal: -1 (fem_jacobi then gives w = 0, like the reference's 1/0 -> inf
+    // -> 0, `solver/solver.py:828-831`)
+    FEM_HIP(hipMemsetAsync(diagpos, 0xff, sizeof(int32_t) * (size_t)N, S(stream)));
     hipLaunchKernelGGL(k_graph_copy, dim3(stream_grid(N * G_TCAP, 256)), dim3(256), 0, S(stream), tmp,
                        defer_flags(tmp, N), rowptr, N, colidx, diagpos);
     FEM_LAUNCHED();
@@ -516,6 +519,7 @@ int fem_graph_fill2(const int64_t* conn, int npe, const int32_t* inc_ptr, const 
 int fem_graph_fill(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
                    const int32_t* rowptr, int32_t* colidx, int32_t* diagpos, fem_stream_t stream) {
     if (N <= 0) return FEM_OK;
+    FEM_HIP(hipMemsetAsync(diagpos, 0xff, sizeof(int32_t) * (size_t)N, S(stream)));   // -1: no diagonal
     return graph_fill(conn, npe, inc_ptr, inc, N, rowptr, colidx, diagpos, nullptr, S(stream));
 }
 

@@ -1449,6 +1449,7 @@ struct fem_pcg {
     unsigned* pk_sync;    // (18 + G) lines, zeroed before every launch
     int pk_ovf;           // overflow build (more than PK_MAXS slices per wave)
     double* pk_v;         // [n] v of the overflow rows
+    int pk_coop;          // launch through hipLaunchCooperativeKernel (fem_pcg_solve; FEM_TUNE_PK_COOP elsewhere)
 };
 
 #define FEM_NCCL(call)                                                                         \
@@ -1602,7 +1603,17 @@ static const void* c1f_fn(const fem_pcg* s) {
 #ifndef FEM_PCG_POOL
 #define FEM_PCG_POOL 1
 #endif
-static constexpr size_t PCG_CACHE_KEEP = size_t(8) << 30;
+// cap of the cache (FEM355_PCG_CACHE_MB, default 1024 MB: a 10M-row bs = 1 context with its paired matrix copy is
+// ~330 MB); fem_pcg_release_cache() hands everything back to the driver (the Python layer calls it at exit and
+// before retrying a failed allocation)
+static size_t pcg_cache_keep() {
+    static const size_t keep = [] {
+        const char* e = getenv("FEM355_PCG_CACHE_MB");
+        const long long mb = e ? atoll(e) : 1024;
+        return (size_t)(mb < 0 ? 0 : mb) << 20;
+    }();
+    return keep;
+}
 
 namespace {
 struct DevBuf {
@@ -1651,7 +1662,7 @@ static void pool_free(void* p, hipStream_t st) {
         dev_cache.push_back(dev_live[i]);
         dev_cache_bytes += dev_live[i].bytes;
         dev_live.erase(dev_live.begin() + (ptrdiff_t)i);
-        while (dev_cache_bytes > PCG_CACHE_KEEP && !dev_cache.empty()) {
+        while (dev_cache_bytes > pcg_cache_keep() && !dev_cache.empty()) {
             (void)hipFree(dev_cache.front().p);
             dev_cache_bytes -= dev_cache.front().bytes;
             dev_cache.erase(dev_cache.begin());
@@ -1659,6 +1670,18 @@ static void pool_free(void* p, hipStream_t st) {
         return;
     }
     (void)hipFree(p);
+}
+
+static size_t pool_release_all() {
+    std::lock_guard<std::mutex> g(dev_cache_mu);
+    size_t freed = 0;
+    for (const DevBuf& b : dev_cache) {
+        (void)hipFree(b.p);
+        freed += b.bytes;
+    }
+    dev_cache.clear();
+    dev_cache_bytes = 0;
+    return freed;
 }
 
 // Pinned host status words are recycled too: hipHostFree synchronises the device and unpins (1.4 ms per context).
@@ -2422,7 +2445,15 @@ static int launch_persist(fem_pcg* s, int k, unsigned long long* prof) {
     }
     void* args[] = {&a};
     const void* fn = persist_fn(prof != nullptr && !s->pk_ovf, (s->tune & FEM_TUNE_PK_SC1) != 0, s->pk_ovf != 0);
-    FEM_HIP(hipLaunchKernel(fn, dim3(G), dim3(PK_T), args, PK_LDS, s->stream));
+    // the grid spins on inter-workgroup flags, so all G workgroups must be resident together: one per CU is
+    // what the occupancy query promised, and a cooperative launch makes the runtime guarantee it (or fail) even
+    // when other streams / processes hold CUs. A plain launch (the bench's fixed-iteration runs) relies on the
+    // occupancy check; should residency still fail, every spin is bounded and the launch ends with
+    // FEM_PCG_SYNC_TIMEOUT (fem_pcg_solve then re-solves on the deferred schedule).
+    if (s->pk_coop || (s->tune & FEM_TUNE_PK_COOP))
+        FEM_HIP(hipLaunchCooperativeKernel(fn, dim3(G), dim3(PK_T), args, PK_LDS, s->stream));
+    else
+        FEM_HIP(hipLaunchKernel(fn, dim3(G), dim3(PK_T), args, PK_LDS, s->stream));
     FEM_LAUNCHED();
     s->launched += k;
     return FEM_OK;
@@ -2773,7 +2804,12 @@ int fem_pcg_use_graph(fem_pcg* s, int k) {
     return FEM_OK;
 }
 
-int fem_pcg_poll(fem_pcg* s, int* iters, int* status, double* rz) {
+static int fem_pcg_poll_raw(fem_pcg* s, int* iters, int* status, double* rz);
+int fem_pcg_poll(fem_pcg* s, int* iters, int* status, double* rz) { return fem_pcg_poll_raw(s, iters, status, rz); }
+
+int fem_pcg_release_cache(void) { return (int)(pool_release_all() >> 20); }
+
+static int fem_pcg_poll_raw(fem_pcg* s, int* iters, int* status, double* rz) {
     FEM_HIP(hipMemcpyAsync(s->st_host, s->st, sizeof(PcgState), hipMemcpyDeviceToHost, s->stream));
     FEM_HIP(hipStreamSynchronize(s->stream));
     const PcgState h = state_view(s);
@@ -2799,7 +2835,8 @@ int fem_pcg_scalars(fem_pcg* s, double* out6) {
     return FEM_OK;
 }
 
-int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, double* rz) {
+// one solve attempt from the x currently in s->x
+static int pcg_solve_once(fem_pcg* s, int max_iter, int chunk, int* it, int* stt, double* rz) {
     s->max_iter = max_iter;
     int rc = fem_pcg_start(s);
     s->max_iter = 0x7fffffff;
@@ -2809,15 +2846,42 @@ int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, 
     // 10M tets; bounded launches keep a non-converging solve interruptible between them)
     if (s->persist) chunk = max_iter < 8192 ? max_iter : 8192;
     int done = 0;
-    int it = 0, stt = FEM_PCG_RUNNING;
+    *it = 0;
+    *stt = FEM_PCG_RUNNING;
     while (done < max_iter) {
         int k = chunk < max_iter - done ? chunk : max_iter - done;
         if ((rc = fem_pcg_iterate(s, k))) return rc;
         done += k;
-        if ((rc = fem_pcg_poll(s, &it, &stt, rz))) return rc;
-        if (stt != FEM_PCG_RUNNING) break;
+        if ((rc = fem_pcg_poll_raw(s, it, stt, rz))) return rc;
+        if (*stt != FEM_PCG_RUNNING) break;
         if (chunk < 256 && !s->persist) chunk *= 2;   // poll less often once the solve is clearly long
     }
+    return FEM_OK;
+}
+
+int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, double* rz) {
+    // the persistent schedule: cooperative launches, and a copy of x0 so that a launch whose grid synchronisation
+    // gave up (FEM_PCG_SYNC_TIMEOUT: the workgroups were not all resident) is re-solved on the deferred schedule
+    // from the same start instead of returning a meaningless iterate
+    double* x0 = nullptr;
+    const bool may_persist = s->persist_req && s->bs == 1 && !s->dist && s->mode != FEM_MODE_CG_CONSTRAINED;
+    if (may_persist) {
+        FEM_HIP(pool_alloc((void**)&x0, sizeof(double) * (size_t)(s->n + 2), s->stream, true));
+        FEM_HIP(hipMemcpyAsync(x0, s->x, sizeof(double) * (size_t)s->n, hipMemcpyDeviceToDevice, s->stream));
+    }
+    s->pk_coop = 1;
+    int it = 0, stt = FEM_PCG_RUNNING;
+    int rc = pcg_solve_once(s, max_iter, chunk, &it, &stt, rz);
+    s->pk_coop = 0;
+    if (!rc && stt == FEM_PCG_SYNC_TIMEOUT && x0) {
+        rc = hipMemcpyAsync(s->x, x0, sizeof(double) * (size_t)s->n, hipMemcpyDeviceToDevice, s->stream) == hipSuccess
+                 ? FEM_OK : FEM_EHIP;
+        s->persist_req = 0;   // fem_pcg_start now sets up the deferred schedule (set_schedule(3) implied deferred)
+        if (!rc) rc = pcg_solve_once(s, max_iter, chunk, &it, &stt, rz);
+        s->persist_req = 1;
+    }
+    pool_free(x0, s->stream);
+    if (rc) return rc;
     if ((rc = fem_pcg_finish(s))) return rc;
     if ((rc = fem_pcg_poll(s, &it, &stt, rz))) return rc;
     if (iters) *iters = it;

@@ -633,6 +633,9 @@ __all__ += [
     "compute_node_vm_stress", "compute_c3d4_surface_forces", "compute_c3d4_shared_face_forces_sum",
 ]
 
+# every public function runs in the scope of the device its `device` argument names (_capi.on_device)
+C.scope_module(globals())
+
 # mesh topology lives in topology.py; re-exported here because the reference keeps it in
 # element.py (`solver/element.py:543-762,963-993,1293-1581,2234-2446,2687-2713`)
 try:

@@ -263,3 +263,6 @@ def solve_tet4(coords, elements, f, fixed, kind="poisson", E=1.0, nu=0.0, tol=1e
         tol = float(rtol) * float(torch.sqrt(torch.dot(b, w * b)))
     res = A.pcg(b, None, w=w, mode=C.MODE_PCG, tol=tol, max_iter=max_iter)
     return res.x.view(N, A.bs), res, A
+
+# every public function runs in the scope of the device its `device` argument names (_capi.on_device)
+C.scope_module(globals())

@@ -17,6 +17,32 @@ from . import _capi as C
 I32, I64, F64 = torch.int32, torch.int64, torch.float64
 
 
+def _scoped(cls):
+    """Class decorator: every public method (and __init__) runs with the current HIP device set to the object's
+    device (`self.device`, or for __init__ the device of the first tensor argument's matrix), so the library's
+    allocations and null-stream launches land where the tensors live (`_capi.device_scope`)."""
+    import functools
+
+    def wrap(fn):
+        @functools.wraps(fn)
+        def w(self, *args, **kwargs):
+            dev = getattr(self, "device", None)
+            if dev is None:   # __init__: SellMatrix(graph, bs) / PcgRunner(A, ...)
+                a0 = args[0] if args else None
+                dev = getattr(a0, "device", None) or getattr(getattr(a0, "cols", None), "device", None)
+            if dev is None or not torch.cuda.is_available():
+                return fn(self, *args, **kwargs)
+            with C.device_scope(dev):
+                return fn(self, *args, **kwargs)
+        return w
+
+    for name, fn in list(vars(cls).items()):
+        if callable(fn) and (name == "__init__" or not name.startswith("_")) and not isinstance(fn, (staticmethod,
+                                                                                                    classmethod, property)):
+            setattr(cls, name, wrap(fn))
+    return cls
+
+
 def _dev_scalar(dev, dtype, value):
     return torch.full((1,), value, dtype=dtype, device=dev)
 
@@ -83,6 +109,11 @@ def check_connectivity(elements: torch.Tensor, n_nodes: int):
 
 def incidence(elements: torch.Tensor, n_nodes: int, checked: bool = False):
     """Deterministic node -> (element, local) incidence of a connectivity block [M, npe] (int64, device)."""
+    with C.device_scope(elements.device):
+        return _incidence(elements, n_nodes, checked)
+
+
+def _incidence(elements, n_nodes, checked):
     lib = C.lib()
     if not checked:
         check_connectivity(elements, n_nodes)
@@ -101,6 +132,11 @@ def build_graph(elements: torch.Tensor, n_nodes: int, compress: bool = True) -> 
     """Node-graph CSR + SELL-64 pattern of `elements` (one element family, int64 [M, npe] on the device).
     The rows are the coalesced pattern of the reference's COO assembly (`subdivision.ipynb:118-139`).
     compress: also derive 16-bit column deltas (used by the SpMV when every |col - row| <= 32767)."""
+    with C.device_scope(elements.device):
+        return _build_graph(elements, n_nodes, compress)
+
+
+def _build_graph(elements, n_nodes, compress):
     lib = C.lib()
     dev = elements.device
     elements = elements.contiguous()
@@ -156,6 +192,7 @@ def pad_connectivity(blocks, npe_max):
     return torch.cat(out, 0).contiguous()
 
 
+@_scoped
 class SellMatrix:
     """Assembled global operator in SELL-64 with bs x bs blocks (bs = dofs per node)."""
 
@@ -257,16 +294,21 @@ class SellMatrix:
         """Run the device (P)CG; returns a PcgResult. `constraints` (a constraints.ConstraintSet, mode
         CG_CONSTRAINED, 3-kernel schedule) is projected onto x at start and after every x update."""
         lib = C.lib()
-        b = b.to(F64).contiguous().view(-1)
+        b = b.to(device=self.device, dtype=F64).contiguous().view(-1)
         x = (torch.zeros(self.n, dtype=F64, device=self.device) if x0 is None
              else x0.to(device=self.device, dtype=F64).clone().contiguous().view(-1))
-        w = w.to(F64).contiguous().view(-1)
+        w = w.to(device=self.device, dtype=F64).contiguous().view(-1)
         hist = torch.full((max(max_iter, 1),), float("nan"), dtype=F64, device=self.device) if history else None
         h = ctypes.c_void_p()
-        C.check(lib.fem_pcg_create(self.g.n_nodes, self.bs, C.ptr(self.g.slice_ptr), C.ptr(self.g.cols),
-                                   C.ptr(self.vals), C.ptr(b), C.ptr(x), C.ptr(w), mode, float(tol), float(eps),
-                                   C.ptr(hist), hist.numel() if hist is not None else 0, C.stream(self.device),
-                                   ctypes.byref(h)), "fem_pcg_create")
+        args = (self.g.n_nodes, self.bs, C.ptr(self.g.slice_ptr), C.ptr(self.g.cols), C.ptr(self.vals), C.ptr(b),
+                C.ptr(x), C.ptr(w), mode, float(tol), float(eps), C.ptr(hist), hist.numel() if hist is not None else 0,
+                C.stream(self.device), ctypes.byref(h))
+        rc = lib.fem_pcg_create(*args)
+        if rc == C.FEM_EHIP:   # out of memory: hand the library's recycled buffers and torch's cache back, retry once
+            C.release_cache()
+            torch.cuda.empty_cache()
+            rc = lib.fem_pcg_create(*args)
+        C.check(rc, "fem_pcg_create")
         try:
             C.check(lib.fem_pcg_set_schedule(h, _schedule(fused, schedule, self.bs)), "fem_pcg_set_schedule")
             self.attach_cols16(h)
@@ -295,6 +337,7 @@ class _DistMarker:
     """Mixin marking distributed runners (they run the 3-kernel schedule)."""
 
 
+@_scoped
 class PcgRunner:
     """Persistent (P)CG context for fixed-iteration timing (bench.py): start once, iterate k, poll."""
 
@@ -302,10 +345,11 @@ class PcgRunner:
                  schedule=None, constraints=None):
         self.lib = C.lib()
         self.A = A
-        self.b = b.to(F64).contiguous().view(-1)
-        self.w = w.to(F64).contiguous().view(-1)
+        self.device = A.device
+        self.b = b.to(device=A.device, dtype=F64).contiguous().view(-1)
+        self.w = w.to(device=A.device, dtype=F64).contiguous().view(-1)
         self.x = (torch.zeros(A.n, dtype=F64, device=A.device) if x0 is None
-                  else x0.to(F64).clone().contiguous().view(-1))
+                  else x0.to(device=A.device, dtype=F64).clone().contiguous().view(-1))
         # a dedicated stream: hipGraph capture is not allowed on the legacy default stream
         self.stream = torch.cuda.Stream(device=A.device)
         self.stream.wait_stream(torch.cuda.current_stream(A.device))

@@ -320,3 +320,6 @@ __all__ = [
     "identify_tetrahedral_shared_faces", "identify_hexahedral_shared_faces", "element_adjacency", "element_to_edge",
     "c3d8_to_c3d4", "c3d6_to_c3d4", "c3d10_to_c3d4", "to_c3d4", "FaceGroups",
 ]
+
+# every public function runs in the scope of the device its `device` argument names (_capi.on_device)
+C.scope_module(globals())

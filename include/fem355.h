@@ -113,7 +113,7 @@ int fem_incidence(const int64_t* conn, int64_t M, int npe, int64_t N, int32_t* i
  * assembly (`subdivision.ipynb:118-139`) at node granularity. Two passes:
  *   fem_graph_count : row_len [N]  (unique neighbours incl. self); *overflow [device int] is written 0 (kept
  *                     for ABI stability: rows of any length are handled, the widest by a selection kernel)
- *   fem_graph_fill  : colidx [nnz] sorted per row, diagpos [N] (position of the diagonal)
+ *   fem_graph_fill  : colidx [nnz] sorted per row, diagpos [N] (position of the diagonal; -1 for a node no element touches)
  * rowptr [N+1] is the exclusive scan of row_len (fem_scan_i32). */
 int fem_graph_count(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
                     int32_t* row_len, int32_t* overflow, fem_stream_t stream);
@@ -160,7 +160,7 @@ int fem_sell_to_csr_vals(const double* vals, int bs, const int32_t* rowptr, int6
                          fem_stream_t stream);
 
 /* Jacobi: w[i] = 1/A_ii (inf -> 0, `solver/solver.py:830-831`), w[i] = 0 where mask[i] != 0 (fixed DOFs);
- * mask may be NULL. diag read through diagpos. */
+ * mask may be NULL. diag read through diagpos (diagpos < 0: diagonal 0, so w = 0 as the reference's inf -> 0). */
 int fem_jacobi(const double* vals, int bs, const int32_t* rowptr, const int32_t* diagpos,
                const int64_t* csr2sell, const int64_t* slice_ptr, int64_t nrows, const uint8_t* mask,
                double* w, fem_stream_t stream);
@@ -340,7 +340,8 @@ int fem_pcg_iterate(fem_pcg* s, int k);
 int fem_pcg_poll(fem_pcg* s, int* iters, int* status, double* rz);
 /* [sync] out6 = {rz (rs_old), pq (p.Ap), alpha, beta, rz_new, completed iterations} for the host messages */
 int fem_pcg_scalars(fem_pcg* s, double* out6);
-/* [sync] run to completion: start + chunks of `chunk` iterations until stop or max_iter */
+/* [sync] run to completion: start + chunks of `chunk` iterations until stop or max_iter (persistent schedule:
+ * cooperative launches, deferred-schedule re-solve from x0 after a FEM_PCG_SYNC_TIMEOUT) */
 int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, double* rz);
 /* kernel schedule: 0 = 3-kernel (SpMV+p.q / r update+r.z / x,p update; the context default), 1 = fused (p formed
  * inside the SpMV from r, w and the previous p; 2 kernels per iteration), 2 = deferred (each kernel finishes the
@@ -379,7 +380,13 @@ int fem_enforce_constraints(double* x, double* r, int64_t n, int order, int64_t 
  * odd iterations, so the matrix tail read last (still in the MI355X's 256 MB memory-side cache) is read first by
  * the next sweep: 67 -> 57 us per SpMV on the 10M Poisson matrix. Results depend on the flags only through the
  * order of the per-block p.q partials (deterministic for a given flag set). */
-enum { FEM_TUNE_REVERSE = 1, FEM_TUNE_PAIR = 2, FEM_TUNE_PK_SC1 = 4, FEM_TUNE_PK_PACK = 8, FEM_TUNE_C1F = 16 };
+enum { FEM_TUNE_REVERSE = 1, FEM_TUNE_PAIR = 2, FEM_TUNE_PK_SC1 = 4, FEM_TUNE_PK_PACK = 8, FEM_TUNE_C1F = 16,
+       FEM_TUNE_PK_COOP = 32 };
+/* FEM_TUNE_PK_COOP: persistent schedule — every launch is a hipLaunchCooperativeKernel (the runtime guarantees that
+ * all workgroups are resident at once, or fails the launch). fem_pcg_solve always launches cooperatively and, should
+ * a launch still end with FEM_PCG_SYNC_TIMEOUT, re-solves from the saved x0 on the deferred schedule; without the
+ * flag fem_pcg_iterate / fem_pcg_profile use plain launches (residency from the occupancy check) and report the
+ * timeout status. */
 /* FEM_TUNE_C1F: distributed single-reduction contexts run each iteration as ONE launch (k_cg1_fused: step, update,
  * u hand-off to the neighbouring workgroups by flags, SpMV, pack, one two-value grid reduction) instead of
  * k_cg1_update + k_cg1_spmv. */
@@ -407,6 +414,9 @@ int fem_pcg_use_graph(fem_pcg* s, int k);
  * n[0..2] sampled launches (bench.py's live per-kernel timing inside its timed region) */
 int fem_pcg_profile(fem_pcg* s, int k, int every, double* ms, int* n);
 void fem_pcg_destroy(fem_pcg* s);
+/* [host] free the buffers that destroyed bs = 1 contexts left in the library's recycling cache (capped at
+ * FEM355_PCG_CACHE_MB, default 1024 MB; invisible to torch's allocator); returns the MB released */
+int fem_pcg_release_cache(void);
 
 /* ------------------------------------------------------------------ multi-GPU (element partition, RCCL)
  * One process per GPU. Every rank holds the SELL matrix of ITS elements over its local nodes (unassembled at

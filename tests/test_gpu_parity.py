@@ -242,6 +242,29 @@ def test_diagonal_preconditioner_quirk_and_exact(gpu):
     assert rel(Me[free], Mref[free]) < 1e-15
 
 
+def test_unused_node_gets_zero_jacobi_weight(gpu):
+    """A point no element touches (common in VTK files): its row is empty, its diagonal 0, so w = 1/0 -> inf -> 0
+    as in the reference (`solver/solver.py:828-831`); the solve equals the oracle's on the same system."""
+    _, mesh, solver, system = _mods()
+    c, t = mesh.kuhn_cube(5, jitter=0.1)
+    c2 = torch.cat([c[:17], torch.tensor([[4.0, 4.0, 4.0]], dtype=c.dtype), c[17:]])   # point 17: unused
+    t2 = t + (t >= 17).to(t.dtype)
+    N = c2.shape[0]
+    A = system.assemble_tet4_system(c2.to(gpu), t2.to(gpu), "poisson")
+    assert int(A.g.diagpos[17]) == -1
+    w = A.jacobi(None)
+    assert float(w[17]) == 0.0 and bool(torch.isfinite(w).all())
+    KP = R.tet4_poisson_K(c2, t2)
+    assert torch.equal(w.cpu(), R.diag_preconditioner(KP, t2, N, dpn=1).view(-1))
+    f, fixed = mesh.cube_poisson_case(c2)
+    u, res, _ = solver.solve_tet4(c2, t2, f, fixed, kind="poisson", tol=1e-10, device=gpu)
+    dinv = R.diag_preconditioner(KP, t2, N, dpn=1)
+    dinv[fixed] = 0.0
+    u_ref, it_ref, _ = R.pcg(KP, t2, f, dinv, tol=1e-10)
+    assert abs(res.iterations - it_ref) <= 2 and rel(u, u_ref) < 1e-10
+    assert float(u[17].abs().max()) == 0.0
+
+
 def test_poisson_pcg_vs_reference(gpu):
     _, _, solver, _ = _mods()
     g = load_golden("poisson_tet4_n4_jit")
