@@ -162,10 +162,15 @@ def main():
     run.start()
     if a.graph:
         run.use_graph(a.graph)
-    run.iterate(a.warmup)
+    persist = run.effective_schedule() == system.SCHED_PERSIST
+    # the W warm-up steps go through the same launch path as the timed steps (persistent: one launch, events of the
+    # context created here rather than next to the timed launch)
+    if persist and a.warmup > 0:
+        run.profile(a.warmup, every=a.warmup)
+    else:
+        run.iterate(a.warmup)
     sync()
     t0 = time.perf_counter()
-    persist = run.effective_schedule() == system.SCHED_PERSIST
     # persistent schedule: the K steps are ONE cooperative launch (the kernel stops itself on convergence, so a
     # solve needs no host polling either); hip events around it give the per-iteration time of the whole iteration
     ms, cnt = run.profile(a.steps, every=a.steps if persist else a.sample_every)

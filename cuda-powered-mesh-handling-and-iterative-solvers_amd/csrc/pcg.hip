@@ -201,6 +201,11 @@ struct PcgState {
         double pq;
         double rz_new;
     } bank[2];
+    // persistent schedule: grid-barrier epochs completed so far. The sync words (group counters, top replicas,
+    // u-flags) count monotonically across launches from this base, so a launch needs no memset of them first
+    // (zeroed by fem_pcg_start, and by the host before the counters could wrap)
+    unsigned pk_epoch;
+    unsigned pk_pad_;
 };
 
 constexpr int PCG_BLOCK = 256;
@@ -1450,6 +1455,8 @@ struct fem_pcg {
     int pk_ovf;           // overflow build (more than PK_MAXS slices per wave)
     double* pk_v;         // [n] v of the overflow rows
     int pk_coop;          // launch through hipLaunchCooperativeKernel (fem_pcg_solve; FEM_TUNE_PK_COOP elsewhere)
+    int64_t pk_epochs;    // upper bound of the barrier epochs enqueued since the sync words were last zeroed
+    hipEvent_t pev[2];    // fem_pcg_profile's events of the persistent launch (created once per context)
 };
 
 #define FEM_NCCL(call)                                                                         \
@@ -2414,9 +2421,22 @@ static int persist_setup(fem_pcg* s) {
 }
 
 // one persistent launch of k iterations (schedule 3); prof (device, [G][PK_NPROF]) selects the instrumented build
+static int persist_reset_sync(fem_pcg* s) {
+    FEM_HIP(hipMemsetAsync(s->pk_sync, 0, sizeof(unsigned) * pk_sync_words(s->pk_grid), s->stream));
+    FEM_HIP(hipMemsetAsync(&s->st->pk_epoch, 0, sizeof(unsigned), s->stream));
+    s->pk_epochs = 0;
+    return FEM_OK;
+}
+
 static int launch_persist(fem_pcg* s, int k, unsigned long long* prof) {
     const int G = s->pk_grid;
-    FEM_HIP(hipMemsetAsync(s->pk_sync, 0, sizeof(unsigned) * pk_sync_words(G), s->stream));
+    // the sync words count epochs across launches (no memset per launch); zero them long before the group counters
+    // (epoch * G / 8) could wrap 32 bits
+    if (s->pk_epochs + k + 1 > (int64_t(1) << 24)) {
+        const int rc = persist_reset_sync(s);
+        if (rc) return rc;
+    }
+    s->pk_epochs += k + 1;
     PkArgs a;
     a.nslices = s->nslices;
     a.nrows = s->nrows;
@@ -2543,6 +2563,8 @@ int fem_pcg_start(fem_pcg* s) {
     if ((rc = (s->cols16 ? fem_spmv16(s->nrows, s->bs, s->slice_ptr, s->cols16, s->vals, s->x, s->q, s->stream)
                           : fem_spmv(s->nrows, s->bs, s->slice_ptr, s->cols, s->vals, s->x, s->q, s->stream)))) return rc;
     if (s->persist) {   // single-reduction start: r0 = b - A x0, u0 = w r0 (in q), p = s = 0, g0 -> red[1]
+        const int zrc = persist_reset_sync(s);   // after the state upload: zeroes st->pk_epoch too
+        if (zrc) return zrc;
         hipLaunchKernelGGL(k_cg1_init, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->bs, s->b, s->r,
                            s->q, s->w, s->p0, s->p1, s->q, (const uint8_t*)nullptr, s->st, s->red);
         FEM_LAUNCHED();
@@ -2869,7 +2891,13 @@ int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, 
         FEM_HIP(pool_alloc((void**)&x0, sizeof(double) * (size_t)(s->n + 2), s->stream, true));
         FEM_HIP(hipMemcpyAsync(x0, s->x, sizeof(double) * (size_t)s->n, hipMemcpyDeviceToDevice, s->stream));
     }
-    s->pk_coop = 1;
+    // FEM355_PK_COOP=0 turns the cooperative launch off (rocprofv3 7.2 segfaults in its exit handler after a
+    // process made one: profiling runs of bench.py set it; the bench's timed launches are plain either way)
+    static const int coop = [] {
+        const char* e = getenv("FEM355_PK_COOP");
+        return e ? atoi(e) : 1;
+    }();
+    s->pk_coop = coop;
     int it = 0, stt = FEM_PCG_RUNNING;
     int rc = pcg_solve_once(s, max_iter, chunk, &it, &stt, rz);
     s->pk_coop = 0;
@@ -2895,31 +2923,30 @@ int fem_pcg_profile(fem_pcg* s, int k, int every, double* ms, int* n) {
     if (every < 1) every = 1;
     double acc[3] = {0, 0, 0};
     int rc = FEM_OK;
+    if (s->persist) {   // bucket 0: persistent launches of `every` iterations (per-iteration time = ms / n); the
+                        // two events live with the context (no event creation next to a timed launch)
+        if (!s->pev[0]) {
+            FEM_HIP(hipEventCreate(&s->pev[0]));
+            FEM_HIP(hipEventCreate(&s->pev[1]));
+        }
+        for (int i = 0; i < k && !rc; i += every) {
+            const int kk = every < k - i ? every : k - i;
+            FEM_HIP(hipEventRecord(s->pev[0], s->stream));
+            rc = launch_persist(s, kk);
+            FEM_HIP(hipEventRecord(s->pev[1], s->stream));
+            FEM_HIP(hipEventSynchronize(s->pev[1]));   // launches of `every` < k are timed one by one
+            float t = 0.f;
+            FEM_HIP(hipEventElapsedTime(&t, s->pev[0], s->pev[1]));
+            acc[0] += t;
+        }
+        if (ms) ms[0] = acc[0], ms[1] = 0.0, ms[2] = 0.0;
+        if (n) n[0] = k, n[1] = 0, n[2] = 0;
+        return rc;
+    }
     const int ns = (k + every - 1) / every;
     std::vector<hipEvent_t> evs((size_t)ns * 4);
     for (auto& e : evs) FEM_HIP(hipEventCreate(&e));
     int si = 0;
-    if (s->persist) {   // bucket 0: persistent launches of `every` iterations (per-iteration time = ms / n)
-        for (int i = 0; i < k && !rc; i += every) {
-            const int kk = every < k - i ? every : k - i;
-            (void)hipEventRecord(evs[4 * si + 0], s->stream);
-            rc = launch_persist(s, kk);
-            (void)hipEventRecord(evs[4 * si + 1], s->stream);
-            ++si;
-        }
-        FEM_HIP(hipStreamSynchronize(s->stream));
-        int iters = 0;
-        for (int i = 0; i < si; ++i) {
-            float t;
-            (void)hipEventElapsedTime(&t, evs[4 * i + 0], evs[4 * i + 1]);
-            acc[0] += t;
-        }
-        iters = k;
-        for (auto& e : evs) (void)hipEventDestroy(e);
-        if (ms) ms[0] = acc[0], ms[1] = 0.0, ms[2] = 0.0;
-        if (n) n[0] = iters, n[1] = 0, n[2] = 0;
-        return rc;
-    }
     for (int i = 0; i < k && !rc; ++i) {
         if (i % every) {
             rc = launch_iterations(s, 1);
@@ -2968,6 +2995,8 @@ int fem_pcg_profile(fem_pcg* s, int k, int every, double* ms, int* n) {
 
 void fem_pcg_destroy(fem_pcg* s) {
     if (!s) return;
+    if (s->pev[0]) (void)hipEventDestroy(s->pev[0]);
+    if (s->pev[1]) (void)hipEventDestroy(s->pev[1]);
     if (s->graph) (void)hipGraphExecDestroy(s->graph);
     pool_free(s->r, s->stream);
     pool_free(s->p0, s->stream);

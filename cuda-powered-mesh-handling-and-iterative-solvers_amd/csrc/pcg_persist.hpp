@@ -34,12 +34,13 @@ constexpr int PK_WAVES = PK_T / 64;
 constexpr int PK_MAXS = 7;               // slices per wave (10M Poisson: 27,000 slices over 4,096 waves -> 7)
 constexpr int PK_U = 2;                  // pairs in flight per lane (4 spills the slot state; persist_probe: 4 = 8)
 constexpr int PK_LINE = 32;              // unsigned words per 128-byte line
-// sync words (zeroed before every launch), in lines: [0, 8) group arrivals, 8 (unused), [9, 17) replicas of the
+// sync words (zeroed by fem_pcg_start; epochs continue across launches from PcgState::pk_epoch), in lines: [0, 8) group arrivals, 8 (unused), [9, 17) replicas of the
 // top counter (one per group),
 // 17 give-up word, 18 + L: u-flag of workgroup L
 enum { PK_GRP = 0, PK_TOP = 8 * PK_LINE, PK_GEN = 9 * PK_LINE, PK_TMO = 17 * PK_LINE, PK_UFLAG = 18 * PK_LINE };
 constexpr unsigned PK_SPIN_LIMIT = 1u << 22;
-constexpr int PK_NPROF = 6;   // phases: u wait, SpMV, block sum, barrier + sums, step, update + drain + flag
+constexpr int PK_NPROF = 8;   // phases: u wait, SpMV, block sum, barrier + sums, step, update + drain + flag,
+                               // prologue (state loads), epilogue (chunk-end barrier + state stores)
 // dynamic LDS (statics would shift the dynamic base off 16 B, cdna_hip_programming.md Guideline 17): 16 wave sums,
 // the barrier verdict (own 16-byte slot), then x and w of the workgroup's rows
 constexpr size_t PK_LDS_HEAD = 256;
@@ -189,6 +190,7 @@ template <int MAXS, bool PROF, bool GSC1, bool OVF = false>
 __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
     unsigned long long pacc[PROF ? PK_NPROF : 1] = {};
     unsigned long long pt = 0;
+    if constexpr (PROF) pt = __builtin_amdgcn_s_memtime();
 // phase boundary: a scheduling barrier in every build (instructions hoisted across phases lengthen the live ranges
 // of the slot arrays: ~180 spilled VGPRs without it), plus the phase clock in the PROF build
 #define PK_MARK(i)                                                         \
@@ -244,6 +246,8 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
     int it = st->iter, halt = st->halt, status = st->status, stop_iter = st->stop_iter;
     double rz = st->rz, alpha_prev = st->alpha, beta = st->beta, pq = st->pq, rz_new = st->rz_new;
     double g = st->red[1];   // r.z of the current iterate (init or the last launch's last update)
+    const unsigned ebase = st->pk_epoch;   // barriers of earlier launches (sync words count on from there)
+    unsigned elast = ebase;                // last barrier epoch of this launch
 
     double rr[MAXS], pp[MAXS], ss[MAXS], vv[MAXS], uo[MAXS];
 #pragma unroll
@@ -253,19 +257,25 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
         rr[j] = on ? a.r[row] : 0.0;
         pp[j] = on ? a.p[row] : 0.0;
         ss[j] = on ? a.s[row] : 0.0;
-        uo[j] = on ? a.u[row] : 0.0;
         vv[j] = 0.0;
         if (j < PK_VL) vl[j * 64] = 0.0;
         xl[j * 64] = on ? a.x[row] : 0.0;
-        wl[j * 64] = on ? a.w[row] : 0.0;
+        const double wj = on ? a.w[row] : 0.0;
+        wl[j * 64] = wj;
+        uo[j] = wj * rr[j];   // u = w r is how every u was formed (k_cg1_init, the update): bit-identical, no load
     }
     const int wlo = a.win[L], whi = a.win[G + L];
     bool fail = false;
     int k = 0;
+    if constexpr (PROF) {
+        __syncthreads();
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        pacc[6] += now - pt;
+        pt = now;
+    }
     if (!halt) {
-        if constexpr (PROF) pt = __builtin_amdgcn_s_memtime();
         for (k = 0; k < a.kmax; ++k) {
-            const unsigned e = (unsigned)k + 1;
+            const unsigned e = ebase + (unsigned)k + 1;
             // ---- wait for the u of the gather window (written by the previous update of this launch)
             if (k > 0) {
                 if (wv == 0) {
@@ -355,6 +365,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
                 fail = true;
                 break;
             }
+            elast = e;
             const double d = lds_dg[0];
             if (k > 0) g = lds_dg[1];
             PK_MARK(3);
@@ -477,10 +488,11 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
     }
     // ---- chunk end without a stop: one more barrier makes the last g partials visible; stop test of that g
     if (!fail && !halt && k == a.kmax && a.kmax > 0) {
-        const unsigned e = (unsigned)a.kmax + 1;
+        const unsigned e = ebase + (unsigned)a.kmax + 1;
         if (!pk_barrier(sy, grp, nper, e, &lds_ok, a.part + (size_t)(a.kmax & 1) * 2 * G + G, nullptr, G, lds_dg)) {
             fail = true;
         } else {
+            elast = e;
             g = lds_dg[0];
             if (it > 0) {
                 const double nrm = sqrt(g);
@@ -509,6 +521,9 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
         }
     }
     if constexpr (PROF) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        pacc[7] += __builtin_amdgcn_s_memtime() - pt;
         if (threadIdx.x == 0)
             for (int i = 0; i < PK_NPROF; ++i) a.prof[(size_t)L * PK_NPROF + i] = pacc[i];
     }
@@ -527,6 +542,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
         st->beta = beta;
         st->pq = pq;
         st->red[1] = g;
+        st->pk_epoch = elast;   // every workgroup read the base before its first barrier of this launch
     }
 }
 #undef PK_ON

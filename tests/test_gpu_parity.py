@@ -255,7 +255,7 @@ def test_unused_node_gets_zero_jacobi_weight(gpu):
     w = A.jacobi(None)
     assert float(w[17]) == 0.0 and bool(torch.isfinite(w).all())
     KP = R.tet4_poisson_K(c2, t2)
-    assert torch.equal(w.cpu(), R.diag_preconditioner(KP, t2, N, dpn=1).view(-1))
+    assert rel(w, R.diag_preconditioner(KP, t2, N, dpn=1).view(-1)) < 1e-14   # sums in another order
     f, fixed = mesh.cube_poisson_case(c2)
     u, res, _ = solver.solve_tet4(c2, t2, f, fixed, kind="poisson", tol=1e-10, device=gpu)
     dinv = R.diag_preconditioner(KP, t2, N, dpn=1)

@@ -52,7 +52,8 @@ def rate(A, b, w, sched, warm, iters, chunk, tune=None):
             "rz": rz}, x
 
 
-PHASES = ("u_wait", "spmv", "block_sum", "barrier_sums", "step", "update_flag")
+PHASES = ("u_wait", "spmv", "block_sum", "barrier_sums", "step", "update_flag", "prologue_per_launch",
+          "epilogue_per_launch")
 
 
 def phase_profile(A, b, w, warm, iters, ghz=2.4, per_wg=False, tune=None):
@@ -70,7 +71,8 @@ def phase_profile(A, b, w, warm, iters, ghz=2.4, per_wg=False, tune=None):
     g = ctypes.c_int()
     C.check(run.lib.fem_pcg_persist_profile(run.h, int(iters), buf, ctypes.byref(g)), "fem_pcg_persist_profile")
     run.close()
-    t = torch.tensor(list(buf), dtype=torch.float64).view(G, len(PHASES))[: g.value] / iters / (ghz * 1e3)
+    t = torch.tensor(list(buf), dtype=torch.float64).view(G, len(PHASES))[: g.value] / (ghz * 1e3)
+    t[:, :6] /= iters   # per iteration; prologue / epilogue stay per launch
     out = {p: {"mean_us": float(t[:, i].mean()), "max_us": float(t[:, i].max()), "min_us": float(t[:, i].min())}
            for i, p in enumerate(PHASES)} | {"total_mean_us": float(t.sum(1).mean())}
     if per_wg:   # logical workgroup L owns waves [16 L, 16 L + 16) of the contiguous slice split

@@ -8,6 +8,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT
+export FEM355_PK_COOP=0   # rocprofv3 segfaults at exit after a cooperative launch (the timed launches are plain)
 ARGS=${PROF_ARGS:-"--steps 100 --warmup 10 --no-cpu-baseline"}
 set -o pipefail
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/trace.log 2>&1 || exit $?
