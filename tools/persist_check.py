@@ -56,15 +56,20 @@ PHASES = ("u_wait", "spmv", "block_sum", "barrier_sums", "step", "update_flag", 
           "epilogue_per_launch")
 
 
-def phase_profile(A, b, w, warm, iters, ghz=2.4, per_wg=False, tune=None):
-    """Per-iteration phase times (us at `ghz` shader clock) of the instrumented persistent kernel: mean and max over
-    workgroups."""
+PIPE_PHASES = ("m_wait", "spmv", "reduce", "unused", "step", "update_publish", "prologue_per_launch",
+               "epilogue_per_launch")
+
+
+def phase_profile(A, b, w, warm, iters, ghz=2.4, per_wg=False, tune=None, sched=3):
+    """Per-iteration phase times (us at `ghz` shader clock) of the instrumented persistent kernel (schedule 3 or the
+    pipelined 4): mean and max over workgroups."""
     import ctypes
-    run = system.PcgRunner(A, b, w, tol=0.0, schedule=3)
+    run = system.PcgRunner(A, b, w, tol=0.0, schedule=sched)
     if tune is not None:
         run.set_tuning(tune)
     run.start()
-    assert run.effective_schedule() == 3
+    assert run.effective_schedule() == sched
+    names = PHASES if sched == 3 else PIPE_PHASES
     run.iterate(warm)
     G = 256
     buf = (ctypes.c_ulonglong * (G * len(PHASES)))()
@@ -74,7 +79,7 @@ def phase_profile(A, b, w, warm, iters, ghz=2.4, per_wg=False, tune=None):
     t = torch.tensor(list(buf), dtype=torch.float64).view(G, len(PHASES))[: g.value] / (ghz * 1e3)
     t[:, :6] /= iters   # per iteration; prologue / epilogue stay per launch
     out = {p: {"mean_us": float(t[:, i].mean()), "max_us": float(t[:, i].max()), "min_us": float(t[:, i].min())}
-           for i, p in enumerate(PHASES)} | {"total_mean_us": float(t.sum(1).mean())}
+           for i, p in enumerate(names)} | {"total_mean_us": float(t[:, :6].sum(1).mean())}
     if per_wg:   # logical workgroup L owns waves [16 L, 16 L + 16) of the contiguous slice split
         G = g.value
         sp = A.g.slice_ptr.cpu()
@@ -98,6 +103,8 @@ def main():
     ap.add_argument("--skip-solve", action="store_true")
     ap.add_argument("--tune", type=int, nargs="*", default=[], help="extra FEM_TUNE_* flag sets for schedule 3")
     ap.add_argument("--per-wg", action="store_true", help="with --prof: SpMV time and matrix entries per workgroup")
+    ap.add_argument("--scheds", type=int, nargs="+", default=[2, 3], help="schedules to solve / rate")
+    ap.add_argument("--prof-scheds", type=int, nargs="+", default=[3], help="schedules to phase-profile (3, 4)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     for n in a.n:
@@ -105,21 +112,27 @@ def main():
         out = {"n": n, "rows": A.n}
         tol = 1e-8 * float(torch.sqrt(torch.dot(b, w * b)))
         if a.prof:
-            out["prof"] = phase_profile(A, b, w, a.warm, a.iters, per_wg=a.per_wg)
+            for ps in a.prof_scheds:
+                out["prof" if ps == 3 else f"prof{ps}"] = phase_profile(A, b, w, a.warm, a.iters, per_wg=a.per_wg,
+                                                                         sched=ps)
         sol = {}
-        for sched in (() if a.skip_solve else (2, 3)):
+        for sched in (() if a.skip_solve else a.scheds):
             t0 = time.perf_counter()
             r = A.pcg(b, None, w=w, mode=C.MODE_PCG, tol=tol, max_iter=20000, chunk=64, schedule=sched)
             torch.cuda.synchronize()
             out[f"solve{sched}"] = {"iters": r.iterations, "status": r.status, "rz": r.rz,
                                     "ms": (time.perf_counter() - t0) * 1e3}
             sol[sched] = r.x
-        if sol:
-            out["solve_dx_rel"] = float((sol[2] - sol[3]).norm() / sol[2].norm())
+        s0 = a.scheds[0]
+        for sched in sol:
+            if sched != s0:
+                out[f"solve_dx_rel_{sched}"] = float((sol[s0] - sol[sched]).norm() / sol[s0].norm())
         xs = {}
-        for sched in (2, 3):
+        for sched in a.scheds:
             out[f"rate{sched}"], xs[sched] = rate(A, b, w, sched, a.warm, a.iters, a.chunk)
-        out["rate_dx_rel"] = float((xs[2] - xs[3]).norm() / xs[2].norm())
+        for sched in xs:
+            if sched != s0:
+                out[f"rate_dx_rel_{sched}"] = float((xs[s0] - xs[sched]).norm() / xs[s0].norm())
         for t in a.tune:   # extra tuning-flag sets of the persistent schedule (FEM_TUNE_*), x compared bitwise
             out[f"rate3_t{t}"], xt = rate(A, b, w, 3, a.warm, a.iters, a.chunk, tune=t)
             out[f"rate3_t{t}"]["x_equal"] = bool(torch.equal(xt, xs[3]))
