@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--rtol", type=float, default=1e-8)
     ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--schedule", type=int, default=None, help="PCG kernel schedule (0 three-kernel, 1 fused, 2 deferred, 3 persistent, 4 pipelined persistent; "
+    ap.add_argument("--schedule", type=int, default=None, help="PCG kernel schedule (0 three-kernel, 1 fused, 2 deferred, 3 persistent; "
                     "default: persistent for bs=1, three-kernel for bs=3)")
     ap.add_argument("--graph", type=int, default=0, help="capture k iterations per hipGraph (0 = plain launches)")
     ap.add_argument("--force-dist", action="store_true", help="run the RCCL element-partitioned path even at N=1")
@@ -162,7 +162,7 @@ def main():
     run.start()
     if a.graph:
         run.use_graph(a.graph)
-    persist = run.effective_schedule() in system.PERSISTENT
+    persist = run.effective_schedule() == system.SCHED_PERSIST
     # the W warm-up steps go through the same launch path as the timed steps (persistent: one launch, events of the
     # context created here rather than next to the timed launch)
     if persist and a.warmup > 0:
@@ -179,8 +179,7 @@ def main():
     it, stt, _ = run.poll()
     assert it == a.warmup + a.steps, (it, stt)
     kernel = {system.SCHED_THREE: "k_pcg_spmv_dot", system.SCHED_FUSED: "k_pcg_spmv_dot<FUSED>",
-              system.SCHED_DEFERRED: "k_pcg_d1", system.SCHED_PERSIST: "k_pcg_persist",
-              system.SCHED_PIPE: "k_pcg_pipe"}[run.effective_schedule()]
+              system.SCHED_DEFERRED: "k_pcg_d1", system.SCHED_PERSIST: "k_pcg_persist"}[run.effective_schedule()]
     run.close()
 
     # per launch of the measured kernel: one SpMV (3-kernel / deferred) or one whole iteration (persistent: the

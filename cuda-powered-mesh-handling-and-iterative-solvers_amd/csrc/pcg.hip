@@ -1263,7 +1263,6 @@ __global__ void k_c1f_window(int64_t nslices, int64_t nrows, const int64_t* __re
 
 }  // namespace fem
 #include "pcg_persist.hpp"
-#include "pcg_pipe.hpp"
 namespace fem {
 
 // ---------------------------------------------------------------- constraint projections (CG_CONSTRAINED)
@@ -1458,14 +1457,6 @@ struct fem_pcg {
     int pk_coop;          // launch through hipLaunchCooperativeKernel (fem_pcg_solve; FEM_TUNE_PK_COOP elsewhere)
     int64_t pk_epochs;    // upper bound of the barrier epochs enqueued since the sync words were last zeroed
     hipEvent_t pev[2];    // fem_pcg_profile's events of the persistent launch (created once per context)
-    // pipelined persistent schedule (4, pcg_pipe.hpp): persist = 1 and pipe = 1; its geometry and extra vectors
-    int pipe;
-    int pp_cfg;           // index into pipe_cfgs()
-    double* pp_a;         // a = A u
-    double* pp_z;
-    double* pp_m0;        // m = w a, double-buffered by epoch parity
-    double* pp_m1;
-    double* pp_gd;        // [2 * init blocks] init partials
 };
 
 #define FEM_NCCL(call)                                                                         \
@@ -2319,7 +2310,7 @@ int fem_pcg_set_schedule(fem_pcg* s, int sched) {
         set_error("fem_pcg_set_schedule: drop the captured graph first (fem_pcg_use_graph(s, 0))");
         return FEM_EARG;
     }
-    if (sched < 0 || sched > 4) {
+    if (sched < 0 || sched > 3) {
         set_error("fem_pcg_set_schedule: unknown schedule %d", sched);
         return FEM_EARG;
     }
@@ -2332,10 +2323,9 @@ int fem_pcg_set_schedule(fem_pcg* s, int sched) {
         return FEM_EARG;
     }
     s->fused = sched == 1;
-    s->deferred = sched >= 2;   // 3 / 4 fall back to the deferred schedule when unsupported
-    s->persist_req = sched == 3 ? 1 : sched == 4 ? 2 : 0;
+    s->deferred = sched == 2 || sched == 3;   // 3 falls back to the deferred schedule when unsupported
+    s->persist_req = sched == 3;
     s->persist = 0;
-    s->pipe = 0;
     return FEM_OK;
 }
 
@@ -2344,7 +2334,7 @@ int fem_pcg_persist_profile(fem_pcg* s, int k, unsigned long long* host_out, int
         set_error("fem_pcg_persist_profile: the context does not run the (register-resident) persistent schedule");
         return FEM_EARG;
     }
-    const size_t nb = sizeof(unsigned long long) * (size_t)s->pk_grid * (s->pipe ? PP_NPROF : PK_NPROF);
+    const size_t nb = sizeof(unsigned long long) * (size_t)s->pk_grid * PK_NPROF;
     unsigned long long* d = nullptr;
     FEM_HIP(hipMalloc(&d, nb));
     FEM_HIP(hipMemsetAsync(d, 0, nb, s->stream));
@@ -2363,7 +2353,7 @@ int fem_pcg_persist_profile(fem_pcg* s, int k, unsigned long long* host_out, int
 }
 
 int fem_pcg_get_schedule(fem_pcg* s) {
-    if (s->persist) return s->pipe ? 4 : 3;
+    if (s->persist) return 3;
     if (s->fused) return 1;
     return s->deferred ? 2 : 0;
 }
@@ -2375,37 +2365,6 @@ static const void* persist_fn(bool prof, bool gsc1, bool ovf = false) {
                          : (const void*)k_pcg_persist<PK_MAXS, false, false, true>;
     if (prof) return gsc1 ? (const void*)k_pcg_persist<PK_MAXS, true, true> : (const void*)k_pcg_persist<PK_MAXS, true, false>;
     return gsc1 ? (const void*)k_pcg_persist<PK_MAXS, false, true> : (const void*)k_pcg_persist<PK_MAXS, false, false>;
-}
-
-// schedule 4 geometries (waves per workgroup, register slots per wave, n slots in LDS, pairs in flight): one
-// workgroup per CU, NW * MAXS slices of capacity per CU; none spills (hipcc -Rpass-analysis=kernel-resource-usage)
-struct PipeCfg {
-    int nw, maxs;
-    size_t lds;
-    const void* fn;
-    const void* fn_prof;
-};
-static const PipeCfg* pipe_cfgs(int* n) {
-    static const PipeCfg cfgs[] = {
-        {8, 14, pp_lds_bytes<8, 14, 11>(), (const void*)k_pcg_pipe<8, 14, 11, 4, false>,
-         (const void*)k_pcg_pipe<8, 14, 11, 4, true>},
-        {12, 9, pp_lds_bytes<12, 9, 8>(), (const void*)k_pcg_pipe<12, 9, 8, 2, false>,
-         (const void*)k_pcg_pipe<12, 9, 8, 2, true>},
-        {8, 14, pp_lds_bytes<8, 14, 11>(), (const void*)k_pcg_pipe<8, 14, 11, 3, false>,
-         (const void*)k_pcg_pipe<8, 14, 11, 3, true>},
-    };
-    *n = (int)(sizeof(cfgs) / sizeof(cfgs[0]));
-    return cfgs;
-}
-
-static int pipe_buffers(fem_pcg* s) {
-    const size_t vec = sizeof(double) * (size_t)(s->n + 2);
-    if (!s->pp_a) FEM_HIP(pool_alloc((void**)&s->pp_a, vec, s->stream, true));
-    if (!s->pp_z) FEM_HIP(pool_alloc((void**)&s->pp_z, vec, s->stream, true));
-    if (!s->pp_m0) FEM_HIP(pool_alloc((void**)&s->pp_m0, vec, s->stream, true));
-    if (!s->pp_m1) FEM_HIP(pool_alloc((void**)&s->pp_m1, vec, s->stream, true));
-    if (!s->pp_gd) FEM_HIP(pool_alloc((void**)&s->pp_gd, sizeof(double) * 2 * 1024, s->stream, true));
-    return FEM_OK;
 }
 
 // schedule 3 prerequisites: bs = 1, 16-bit columns + lane-paired copy, single GPU, no projections, capacity
@@ -2457,32 +2416,6 @@ static int persist_setup(fem_pcg* s) {
     }
     if (ovf && !s->pk_v) FEM_HIP(pool_alloc((void**)&s->pk_v, sizeof(double) * (size_t)s->n, s->stream, s->bs == 1));
     s->pk_ovf = ovf ? 1 : 0;
-    s->pipe = 0;
-    if (s->persist_req == 2) {   // pipelined: its own geometry, no overflow build (falls back to schedule 3)
-        int nc = 0;
-        const PipeCfg* cf = pipe_cfgs(&nc);
-        static const int env_cfg = [] {
-            const char* e = getenv("FEM355_PIPE_CFG");
-            return e ? atoi(e) : 0;
-        }();
-        const int sel = (s->tune >> 6) & 3;   // FEM_TUNE_PIPE_CFG bits: 0 = default (FEM355_PIPE_CFG, else 0)
-        const int c = sel ? (sel - 1 < nc ? sel - 1 : 0) : (env_cfg >= 0 && env_cfg < nc ? env_cfg : 0);
-        const int64_t maxL = (s->nslices + G - 1) / G;
-        bool ok = maxL <= (int64_t)cf[c].nw * cf[c].maxs;
-        for (int v = 0; v < 2 && ok; ++v) {
-            const void* f = v ? cf[c].fn_prof : cf[c].fn;
-            FEM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)cf[c].lds));
-            int nb = 0;
-            FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, cf[c].nw * 64, cf[c].lds));
-            ok = nb >= 1;
-        }
-        if (ok) {
-            const int rc = pipe_buffers(s);
-            if (rc) return rc;
-            s->pipe = 1;
-            s->pp_cfg = c;
-        }
-    }
     s->persist = 1;
     return FEM_OK;
 }
@@ -2495,54 +2428,7 @@ static int persist_reset_sync(fem_pcg* s) {
     return FEM_OK;
 }
 
-static int launch_pipe(fem_pcg* s, int k, unsigned long long* prof) {
-    const int G = s->pk_grid;
-    int nc = 0;
-    const PipeCfg& cf = pipe_cfgs(&nc)[s->pp_cfg];
-    PpArgs a;
-    a.nslices = s->nslices;
-    a.nrows = s->nrows;
-    a.slice_ptr = s->slice_ptr;
-    a.cols = s->pcols16;
-    a.vals = s->pvals;
-    a.x = s->x;
-    a.r = s->r;
-    a.av = s->pp_a;
-    a.s = s->p1;
-    a.p = s->p0;
-    a.z = s->pp_z;
-    a.m0 = s->pp_m0;
-    a.m1 = s->pp_m1;
-    a.w = s->w;
-    a.win = s->pk_win;
-    a.part = s->pk_part;
-    a.tmo = s->pk_sync;                 // line 0
-    a.flag = s->pk_sync + PK_LINE;      // lines 1 .. G
-    a.st = s->st;
-    a.hist = s->hist;
-    a.hist_len = s->hist_len;
-    a.kmax = k;
-    a.rev = (s->tune & FEM_TUNE_REVERSE) ? 1 : 0;
-    a.prof = prof;
-    {
-        const int64_t maxL = (s->nslices + G - 1) / G;
-        a.pack = (int)((maxL + cf.nw - 1) / cf.nw);
-    }
-    void* args[] = {&a};
-    const void* fn = prof ? cf.fn_prof : cf.fn;
-    // flags hold epochs themselves (no counters): 2^32 iterations before they wrap, so no periodic reset (which
-    // would also break the epoch parity of the m buffer)
-    if (s->pk_coop || (s->tune & FEM_TUNE_PK_COOP))
-        FEM_HIP(hipLaunchCooperativeKernel(fn, dim3(G), dim3(cf.nw * 64), args, cf.lds, s->stream));
-    else
-        FEM_HIP(hipLaunchKernel(fn, dim3(G), dim3(cf.nw * 64), args, cf.lds, s->stream));
-    FEM_LAUNCHED();
-    s->launched += k;
-    return FEM_OK;
-}
-
 static int launch_persist(fem_pcg* s, int k, unsigned long long* prof) {
-    if (s->pipe) return launch_pipe(s, k, prof);
     const int G = s->pk_grid;
     // the sync words count epochs across launches (no memset per launch); zero them long before the group counters
     // (epoch * G / 8) could wrap 32 bits
@@ -2676,22 +2562,6 @@ int fem_pcg_start(fem_pcg* s) {
     }
     if ((rc = (s->cols16 ? fem_spmv16(s->nrows, s->bs, s->slice_ptr, s->cols16, s->vals, s->x, s->q, s->stream)
                           : fem_spmv(s->nrows, s->bs, s->slice_ptr, s->cols, s->vals, s->x, s->q, s->stream)))) return rc;
-    if (s->persist && s->pipe) {   // pipelined start: r0 = b - A x0, u0 = w r0, a0 = A u0, m0 = w a0, gamma0, delta0
-        const int zrc = persist_reset_sync(s);   // flags, give-up word and st->pk_epoch
-        if (zrc) return zrc;
-        hipLaunchKernelGGL(k_pipe_init1, dim3(stream_grid(s->n, 256)), dim3(256), 0, s->stream, s->n, s->b, s->q, s->w,
-                           s->r, s->pp_m1, s->p0, s->p1, s->pp_z, s->mode != FEM_MODE_PCG ? 1 : 0);
-        FEM_LAUNCHED();
-        if ((rc = fem_spmv16(s->nrows, s->bs, s->slice_ptr, s->cols16, s->vals, s->pp_m1, s->q, s->stream))) return rc;
-        const int nb = (int)std::min<int64_t>(1024, std::max<int64_t>(1, cdiv(s->n, 256)));
-        hipLaunchKernelGGL(k_pipe_init2, dim3(nb), dim3(256), 0, s->stream, s->n, s->q, s->w, s->r, s->pp_a, s->pp_m0,
-                           s->pp_gd);
-        FEM_LAUNCHED();
-        hipLaunchKernelGGL(k_pipe_init3, dim3(1), dim3(64), 0, s->stream, s->pp_gd, nb, s->pk_part, s->pk_grid, s->st);
-        FEM_LAUNCHED();
-        s->launched = 0;
-        return FEM_OK;
-    }
     if (s->persist) {   // single-reduction start: r0 = b - A x0, u0 = w r0 (in q), p = s = 0, g0 -> red[1]
         const int zrc = persist_reset_sync(s);   // after the state upload: zeroes st->pk_epoch too
         if (zrc) return zrc;
@@ -3034,10 +2904,9 @@ int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, 
     if (!rc && stt == FEM_PCG_SYNC_TIMEOUT && x0) {
         rc = hipMemcpyAsync(s->x, x0, sizeof(double) * (size_t)s->n, hipMemcpyDeviceToDevice, s->stream) == hipSuccess
                  ? FEM_OK : FEM_EHIP;
-        const int req = s->persist_req;
-        s->persist_req = 0;   // fem_pcg_start now sets up the deferred schedule (set_schedule(3/4) implied deferred)
+        s->persist_req = 0;   // fem_pcg_start now sets up the deferred schedule (set_schedule(3) implied deferred)
         if (!rc) rc = pcg_solve_once(s, max_iter, chunk, &it, &stt, rz);
-        s->persist_req = req;
+        s->persist_req = 1;
     }
     pool_free(x0, s->stream);
     if (rc) return rc;
@@ -3151,11 +3020,6 @@ void fem_pcg_destroy(fem_pcg* s) {
     pool_free(s->pk_part, s->stream);
     pool_free(s->pk_sync, s->stream);
     pool_free(s->pk_v, s->stream);
-    pool_free(s->pp_a, s->stream);
-    pool_free(s->pp_z, s->stream);
-    pool_free(s->pp_m0, s->stream);
-    pool_free(s->pp_m1, s->stream);
-    pool_free(s->pp_gd, s->stream);
     pool_free(s->st, s->stream);
     host_state_free(s->st_host, s->stream);
     delete s;

@@ -50,10 +50,8 @@ def _dev_scalar(dev, dtype, value):
 # (P)CG kernel schedules (csrc/pcg.hip): 0 = three kernels with in-kernel grid reductions, 1 = fused (p formed
 # inside the SpMV), 2 = deferred (partials summed by the next kernel, no grid atomics), 3 = persistent (one
 # cooperative launch per chunk of single-reduction iterations, csrc/pcg_persist.hpp; falls back to 2 where its
-# prerequisites do not hold), 4 = pipelined persistent (csrc/pcg_pipe.hpp: the grid-wide sums overlap the SpMV; falls
-# back to 3, then 2)
-SCHED_THREE, SCHED_FUSED, SCHED_DEFERRED, SCHED_PERSIST, SCHED_PIPE = 0, 1, 2, 3, 4
-PERSISTENT = (SCHED_PERSIST, SCHED_PIPE)
+# prerequisites do not hold)
+SCHED_THREE, SCHED_FUSED, SCHED_DEFERRED, SCHED_PERSIST = 0, 1, 2, 3
 # measured on MI355X (10M-tet cube, 16-bit columns, paired layout; tools/persist_check.py, tools/spmv_tune.py):
 # scalar Poisson 59.4 us/it persistent vs 79.4 deferred; 3x3 elasticity three-kernel (the persistent kernel is bs=1)
 DEFAULT_SCHEDULE = {1: SCHED_PERSIST, 3: SCHED_THREE}

@@ -343,17 +343,13 @@ int fem_pcg_scalars(fem_pcg* s, double* out6);
 /* [sync] run to completion: start + chunks of `chunk` iterations until stop or max_iter (persistent schedule:
  * cooperative launches, deferred-schedule re-solve from x0 after a FEM_PCG_SYNC_TIMEOUT) */
 int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, double* rz);
-/* kernel schedule (4 = pipelined persistent, below): 0 = 3-kernel (SpMV+p.q / r update+r.z / x,p update; the context default), 1 = fused (p formed
+/* kernel schedule: 0 = 3-kernel (SpMV+p.q / r update+r.z / x,p update; the context default), 1 = fused (p formed
  * inside the SpMV from r, w and the previous p; 2 kernels per iteration), 2 = deferred (each kernel finishes the
  * previous kernel's block partials itself: no grid atomics, state banked by launch parity), 3 = persistent
  * (pcg_persist.hpp: the single-reduction iteration as one cooperative launch per chunk, CG state of every row held in
  * registers / LDS of its owning wave, slices past 7 per wave streamed from HBM in the same launch; bs = 1 with
  * 16-bit columns and FEM_TUNE_PAIR, single GPU; otherwise fem_pcg_start falls back to 2). Distributed and
  * constrained contexts accept only 0. */
-/* 4 = pipelined persistent (pcg_pipe.hpp): the same Jacobi-PCG in the pipelined (Ghysels-Vanroose) form — a = A u
- * carried by recurrence, so the two dot products of an iteration come from the previous update and their grid-wide
- * sum overlaps the SpMV: no grid barrier per iteration, only flag hand-offs. bs = 1, same prerequisites as 3 and
- * capacity without overflow (otherwise 3, else 2). */
 int fem_pcg_set_schedule(fem_pcg* s, int sched);
 /* the schedule the context runs (valid after fem_pcg_start: 3 may have fallen back to 2) */
 int fem_pcg_get_schedule(fem_pcg* s);
@@ -385,10 +381,7 @@ int fem_enforce_constraints(double* x, double* r, int64_t n, int order, int64_t 
  * the next sweep: 67 -> 57 us per SpMV on the 10M Poisson matrix. Results depend on the flags only through the
  * order of the per-block p.q partials (deterministic for a given flag set). */
 enum { FEM_TUNE_REVERSE = 1, FEM_TUNE_PAIR = 2, FEM_TUNE_PK_SC1 = 4, FEM_TUNE_PK_PACK = 8, FEM_TUNE_C1F = 16,
-       FEM_TUNE_PK_COOP = 32, FEM_TUNE_PIPE_CFG_SHIFT = 6 };
-/* bits 6-7 (value c << FEM_TUNE_PIPE_CFG_SHIFT): pipelined schedule geometry c - 1 (0 = default: env
- * FEM355_PIPE_CFG, else 0): 0 = 8 waves x 14 slots, 4 pairs in flight; 1 = 12 waves x 9 slots, 2 pairs; 2 = 8 waves
- * x 14 slots, 3 pairs. Same arithmetic per row; the iterates differ only through the partial-sum grouping. */
+       FEM_TUNE_PK_COOP = 32 };
 /* FEM_TUNE_PK_COOP: persistent schedule — every launch is a hipLaunchCooperativeKernel (the runtime guarantees that
  * all workgroups are resident at once, or fails the launch). fem_pcg_solve always launches cooperatively and, should
  * a launch still end with FEM_PCG_SYNC_TIMEOUT, re-solves from the saved x0 on the deferred schedule; without the

@@ -56,20 +56,16 @@ PHASES = ("u_wait", "spmv", "block_sum", "barrier_sums", "step", "update_flag", 
           "epilogue_per_launch")
 
 
-PIPE_PHASES = ("m_wait", "spmv", "reduce", "unused", "step", "update_publish", "prologue_per_launch",
-               "epilogue_per_launch")
-
-
 def phase_profile(A, b, w, warm, iters, ghz=2.4, per_wg=False, tune=None, sched=3):
     """Per-iteration phase times (us at `ghz` shader clock) of the instrumented persistent kernel (schedule 3 or the
-    pipelined 4): mean and max over workgroups."""
+    a variant): mean and max over workgroups."""
     import ctypes
     run = system.PcgRunner(A, b, w, tol=0.0, schedule=sched)
     if tune is not None:
         run.set_tuning(tune)
     run.start()
     assert run.effective_schedule() == sched
-    names = PHASES if sched == 3 else PIPE_PHASES
+    names = PHASES
     run.iterate(warm)
     G = 256
     buf = (ctypes.c_ulonglong * (G * len(PHASES)))()
