@@ -2334,7 +2334,7 @@ int fem_pcg_persist_profile(fem_pcg* s, int k, unsigned long long* host_out, int
         set_error("fem_pcg_persist_profile: the context does not run the (register-resident) persistent schedule");
         return FEM_EARG;
     }
-    const size_t nb = sizeof(unsigned long long) * (size_t)s->pk_grid * PK_NPROF;
+    const size_t nb = sizeof(unsigned long long) * (size_t)s->pk_grid * (PK_NPROF + PK_WAVES);
     unsigned long long* d = nullptr;
     FEM_HIP(hipMalloc(&d, nb));
     FEM_HIP(hipMemsetAsync(d, 0, nb, s->stream));

@@ -174,7 +174,8 @@ struct PkArgs {
     int rev;                // FEM_TUNE_REVERSE: odd iterations walk the own slices backwards
     int pack;               // FEM_TUNE_PK_PACK: slices per wave in order (0: spread; see k_pcg_persist)
     double* v;              // OVF: v = A u of the overflow rows (their state stays in r, p, s, x, u, w in HBM)
-    unsigned long long* prof;   // PROF instantiation: [G][PK_NPROF] shader-clock sums per phase (thread 0 of each WG)
+    unsigned long long* prof;   // PROF instantiation: [G][PK_NPROF] shader-clock sums per phase (thread 0 of each WG),
+                                // then [G][PK_WAVES] SpMV-phase clock sums of every wave (its own slices only)
 };
 
 // the 64 rows of slot j of this wave: row = rb + 64 j (32-bit; the host checks nrows < 2^31); `lim` = rows of the
@@ -189,7 +190,7 @@ struct PkArgs {
 template <int MAXS, bool PROF, bool GSC1, bool OVF = false>
 __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
     unsigned long long pacc[PROF ? PK_NPROF : 1] = {};
-    unsigned long long pt = 0;
+    unsigned long long pt = 0, wspmv = 0;
     if constexpr (PROF) pt = __builtin_amdgcn_s_memtime();
 // phase boundary: a scheduling barrier in every build (instructions hoisted across phases lengthen the live ranges
 // of the slot arrays: ~180 spilled VGPRs without it), plus the phase clock in the PROF build
@@ -313,6 +314,8 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
             // ---- v = A u over the own slices, d partial. Slots unrolled (register-resident state needs
             // compile-time indices); the empty asm keeps the compiler from interleaving slots (register blow-up)
             const bool rv = a.rev && ((it & 1) != 0);
+            unsigned long long tw0 = 0;
+            if constexpr (PROF) tw0 = __builtin_amdgcn_s_memtime();
             // launder the matrix pointers every iteration: otherwise the per-slot addresses are hoisted out of the
             // k loop and held in VGPRs across it (7 slots x ~6 registers -> spills)
             const int64_t* slp = pk_launder(a.slice_ptr);
@@ -338,6 +341,10 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
                     }
                     asm volatile("" ::: "memory");
                 }
+            }
+            if constexpr (PROF) {   // this wave's own SpMV time (results back: the v slots are written)
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                wspmv += __builtin_amdgcn_s_memtime() - tw0;
             }
             double dp = 0.0;
 #pragma unroll
@@ -526,6 +533,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
         pacc[7] += __builtin_amdgcn_s_memtime() - pt;
         if (threadIdx.x == 0)
             for (int i = 0; i < PK_NPROF; ++i) a.prof[(size_t)L * PK_NPROF + i] = pacc[i];
+        if (lane == 0) a.prof[(size_t)G * PK_NPROF + (size_t)L * PK_WAVES + wv] = wspmv;
     }
     if (L == 0 && threadIdx.x == 0) {
         if (fail) {

@@ -353,8 +353,9 @@ int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, 
 int fem_pcg_set_schedule(fem_pcg* s, int sched);
 /* the schedule the context runs (valid after fem_pcg_start: 3 may have fallen back to 2) */
 int fem_pcg_get_schedule(fem_pcg* s);
-/* persistent schedule only: k iterations of the instrumented kernel build; host_out[G * 6] = per-workgroup shader-clock
- * sums of the phases (u wait, SpMV, block sum, barrier + partial sums, step, update + drain + flag), *grid = G */
+/* persistent schedule only: k iterations of the instrumented kernel build; host_out[G * 8] = per-workgroup shader-clock
+ * sums of the phases (u wait, SpMV, block sum, barrier + partial sums, step, update + drain + flag, launch prologue,
+ * launch epilogue), then host_out[G * 8 + G * 16] = every wave's own SpMV clock sum; *grid = G */
 int fem_pcg_persist_profile(fem_pcg* s, int k, unsigned long long* host_out, int* grid);
 /* CG_CONSTRAINED projections applied to x once at fem_pcg_start (after r0 = b - A x0) and after every x update:
  *   order 0 (`enforce_constraints`, `solver/solver.py:478-510`): x[rbe2_slave] = x[rbe2_master] (all gathered

@@ -68,24 +68,35 @@ def phase_profile(A, b, w, warm, iters, ghz=2.4, per_wg=False, tune=None, sched=
     names = PHASES
     run.iterate(warm)
     G = 256
-    buf = (ctypes.c_ulonglong * (G * len(PHASES)))()
+    buf = (ctypes.c_ulonglong * (G * (len(PHASES) + 16)))()
     g = ctypes.c_int()
     C.check(run.lib.fem_pcg_persist_profile(run.h, int(iters), buf, ctypes.byref(g)), "fem_pcg_persist_profile")
     run.close()
-    t = torch.tensor(list(buf), dtype=torch.float64).view(G, len(PHASES))[: g.value] / (ghz * 1e3)
+    allv = torch.tensor(list(buf), dtype=torch.float64) / (ghz * 1e3)
+    t = allv[: G * len(PHASES)].view(G, len(PHASES))[: g.value].clone()
+    tw = allv[G * len(PHASES):].view(G, 16)[: g.value] / iters   # per-wave own SpMV, us per iteration
     t[:, :6] /= iters   # per iteration; prologue / epilogue stay per launch
     out = {p: {"mean_us": float(t[:, i].mean()), "max_us": float(t[:, i].max()), "min_us": float(t[:, i].min())}
            for i, p in enumerate(names)} | {"total_mean_us": float(t[:, :6].sum(1).mean())}
-    if per_wg:   # logical workgroup L owns waves [16 L, 16 L + 16) of the contiguous slice split
+    busy = tw > 0
+    out["wave_spmv_us"] = {"mean_busy": float(tw[busy].mean()), "max": float(tw.max()),
+                           "min_busy": float(tw[busy].min()),
+                           "wg_max_mean": float(tw.max(1).values.mean()), "wg_max_max": float(tw.max(1).values.max())}
+    if per_wg:   # packed assignment: WG L owns [L S / G, (L+1) S / G), its waves ceil(maxL / 16) slices each in order
         G = g.value
         sp = A.g.slice_ptr.cpu()
         S = sp.numel() - 1
-        W = G * 16
-        ent = []
+        pack = (-(-S // G) + 15) // 16
+        ent, went = [], []
         for L in range(G):
-            s0, s1 = (16 * L) * S // W, (16 * L + 16) * S // W
-            ent.append(int(sp[s1] - sp[s0]))
-        out["per_wg"] = {"spmv_us": [round(float(v), 3) for v in t[:, 1]], "entries": ent}
+            a0, a1 = L * S // G, (L + 1) * S // G
+            ent.append(int(sp[a1] - sp[a0]))
+            for wv in range(16):
+                lo = min(a0 + wv * pack, a1)
+                hi = min(lo + pack, a1)
+                went.append(int(sp[hi] - sp[lo]))
+        out["per_wg"] = {"spmv_us": [round(float(v), 3) for v in t[:, 1]], "entries": ent,
+                         "wave_spmv_us": [round(float(v), 3) for v in tw.reshape(-1)], "wave_entries": went}
     return out
 
 
