@@ -112,6 +112,13 @@ SIGNATURES = {
     "fem_pcg_profile": (_I, [_P, _I, _I, ctypes.POINTER(_D), ctypes.POINTER(_I)]),
     "fem_pcg_destroy": (None, [_P]),
     "fem_pcg_release_cache": (_I, []),
+    "fem_pcg_set_rows": (_I, [_P, _I, _I, _P, _I]),
+    "fem_pcg_comm_block": (_I, [_P, ctypes.POINTER(_P), ctypes.POINTER(_L)]),
+    "fem_pcg_col_window": (_I, [_P, ctypes.POINTER(_L), ctypes.POINTER(_L)]),
+    "fem_pcg_set_peers": (_I, [_P, _P, _P, _P]),
+    "fem_ipc_handle": (_I, [_P, ctypes.c_char_p]),
+    "fem_ipc_open": (_I, [ctypes.c_char_p, ctypes.POINTER(_P)]),
+    "fem_ipc_close": (_I, [_P]),
     "fem_sell_diag": (_I, [_P, _I, _P, _P, _L, _P, _P]),
     "fem_jacobi_from_diag": (_I, [_P, _L, _P, _P, _P]),
     "fem_comm_unique_id": (_I, [ctypes.c_char_p]),

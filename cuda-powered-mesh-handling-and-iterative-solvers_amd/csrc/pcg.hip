@@ -1457,6 +1457,17 @@ struct fem_pcg {
     int pk_coop;          // launch through hipLaunchCooperativeKernel (fem_pcg_solve; FEM_TUNE_PK_COOP elsewhere)
     int64_t pk_epochs;    // upper bound of the barrier epochs enqueued since the sync words were last zeroed
     hipEvent_t pev[2];    // fem_pcg_profile's events of the persistent launch (created once per context)
+    // distributed persistent schedule (fem_pcg_set_rows): rows partitioned over ranks, one persistent launch per
+    // rank, u hand-offs and rank sums through the ranks' comm blocks (pcg_persist.hpp DIST build)
+    int pd;
+    int pd_rank, pd_nranks, pd_grid_req;
+    int64_t pd_split[PK_MAX_RANKS + 1];   // global slice bounds of the ranks
+    char* pd_block;                       // this rank's comm block (hipMalloc: exportable through IPC)
+    int64_t pd_block_bytes, pd_off_flag, pd_off_red, pd_off_rflag;
+    char* pd_peer[PK_MAX_RANKS];          // comm blocks of all ranks (own included), set by fem_pcg_set_peers
+    int pd_peers_ok;
+    int32_t* pd_pub;                      // [G][nranks][2] rows of each local workgroup gathered by each rank
+    int pd_init_pending;                  // the next launch runs the distributed init (r0, u0, r0.u0)
 };
 
 #define FEM_NCCL(call)                                                                         \
@@ -2360,6 +2371,22 @@ int fem_pcg_get_schedule(fem_pcg* s) {
 
 static size_t pk_sync_words(int G) { return (size_t)(18 + G) * PK_LINE; }
 
+// distributed builds: 4 register slots per wave when the rank's slices fit (every rank of a 10M-tet system at
+// N >= 2: fewer loop-carried registers, no spills), else 7
+constexpr int PK_MAXS_DIST = 4;
+static const void* persist_fn_dist(bool prof, int maxs) {
+    if (maxs <= PK_MAXS_DIST)
+        return prof ? (const void*)k_pcg_persist<PK_MAXS_DIST, true, true, false, true>
+                    : (const void*)k_pcg_persist<PK_MAXS_DIST, false, true, false, true>;
+    return prof ? (const void*)k_pcg_persist<PK_MAXS, true, true, false, true>
+                : (const void*)k_pcg_persist<PK_MAXS, false, true, false, true>;
+}
+static int dist_maxs(const fem_pcg* s) {
+    const int64_t nloc = s->pd_split[s->pd_rank + 1] - s->pd_split[s->pd_rank];
+    const int64_t maxL = (nloc + s->pk_grid - 1) / s->pk_grid;
+    return (int)((maxL + PK_WAVES - 1) / PK_WAVES);
+}
+
 static const void* persist_fn(bool prof, bool gsc1, bool ovf = false) {
     if (ovf) return gsc1 ? (const void*)k_pcg_persist<PK_MAXS, false, true, true>
                          : (const void*)k_pcg_persist<PK_MAXS, false, false, true>;
@@ -2369,8 +2396,11 @@ static const void* persist_fn(bool prof, bool gsc1, bool ovf = false) {
 
 // schedule 3 prerequisites: bs = 1, 16-bit columns + lane-paired copy, single GPU, no projections, capacity
 // (every wave <= PK_MAXS slices), one resident PK_T-thread workgroup per CU
+static int persist_setup_dist(fem_pcg* s);
+
 static int persist_setup(fem_pcg* s) {
     s->persist = 0;
+    if (s->pd) return persist_setup_dist(s);
     if (!s->persist_req) return FEM_OK;
     if (s->bs != 1 || !s->paired || s->dist || s->mode == FEM_MODE_CG_CONSTRAINED || s->nslices == 0) return FEM_OK;
     int dev = 0, ncu = 0;
@@ -2420,6 +2450,41 @@ static int persist_setup(fem_pcg* s) {
     return FEM_OK;
 }
 
+// schedule 3 over a row-partitioned multi-rank system (fem_pcg_set_rows / fem_pcg_set_peers already ran): the
+// prerequisites of the single-GPU schedule, this rank's slices within the register capacity (no overflow build),
+// one resident workgroup per CU for the chosen grid
+static int persist_setup_dist(fem_pcg* s) {
+    if (s->bs != 1 || !s->paired || s->dist || s->mode == FEM_MODE_CG_CONSTRAINED) {
+        set_error("distributed persistent PCG: needs bs = 1, 16-bit columns with the paired copy, no element "
+                  "partition, no constraints");
+        return FEM_EARG;
+    }
+    if (!s->pd_peers_ok) {
+        set_error("distributed persistent PCG: fem_pcg_set_peers first");
+        return FEM_EARG;
+    }
+    const int G = s->pk_grid;
+    const int64_t nloc = s->pd_split[s->pd_rank + 1] - s->pd_split[s->pd_rank];
+    if ((nloc + G - 1) / G > (int64_t)PK_WAVES * PK_MAXS) {
+        set_error("distributed persistent PCG: %lld slices on this rank exceed the register capacity of %d workgroups",
+                  (long long)nloc, G);
+        return FEM_EARG;
+    }
+    for (int v = 0; v < 2; ++v) {
+        const void* f = persist_fn_dist(v == 1, dist_maxs(s));
+        FEM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)PK_LDS));
+        int nb = 0;
+        FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, PK_T, PK_LDS));
+        if (nb < 1) {
+            set_error("distributed persistent PCG: kernel does not fit one workgroup per CU");
+            return FEM_EARG;
+        }
+    }
+    s->pk_ovf = 0;
+    s->persist = 1;
+    return FEM_OK;
+}
+
 // one persistent launch of k iterations (schedule 3); prof (device, [G][PK_NPROF]) selects the instrumented build
 static int persist_reset_sync(fem_pcg* s) {
     FEM_HIP(hipMemsetAsync(s->pk_sync, 0, sizeof(unsigned) * pk_sync_words(s->pk_grid), s->stream));
@@ -2433,6 +2498,10 @@ static int launch_persist(fem_pcg* s, int k, unsigned long long* prof) {
     // the sync words count epochs across launches (no memset per launch); zero them long before the group counters
     // (epoch * G / 8) could wrap 32 bits
     if (s->pk_epochs + k + 1 > (int64_t(1) << 24)) {
+        if (s->pd) {   // the other ranks write into this rank's words: only fem_pcg_start (+ a host barrier) resets
+            set_error("distributed persistent PCG: 2^24 iterations since fem_pcg_start; restart the solve");
+            return FEM_EARG;
+        }
         const int rc = persist_reset_sync(s);
         if (rc) return rc;
     }
@@ -2463,8 +2532,34 @@ static int launch_persist(fem_pcg* s, int k, unsigned long long* prof) {
         const int64_t maxL = (s->nslices + G - 1) / G;
         a.pack = (s->tune & FEM_TUNE_PK_PACK) ? (int)((maxL + PK_WAVES - 1) / PK_WAVES) : 0;
     }
+    a.sbase = 0;
+    a.rank = 0;
+    a.nranks = 1;
+    for (int q = 0; q < PK_MAX_RANKS; ++q) a.peer[q] = nullptr;
+    a.off_flag = a.off_red = a.off_rflag = 0;
+    a.pub = nullptr;
+    a.b = s->b;
+    a.init = 0;
+    if (s->pd) {   // distributed: this rank's slices, comm blocks, the init on the first launch after start
+        const int64_t S0 = s->pd_split[s->pd_rank], S1 = s->pd_split[s->pd_rank + 1];
+        a.nslices = S1 - S0;
+        a.sbase = S0;
+        a.rank = s->pd_rank;
+        a.nranks = s->pd_nranks;
+        for (int q = 0; q < s->pd_nranks; ++q) a.peer[q] = s->pd_peer[q];
+        a.off_flag = s->pd_off_flag;
+        a.off_red = s->pd_off_red;
+        a.off_rflag = s->pd_off_rflag;
+        a.pub = s->pd_pub;
+        a.u = reinterpret_cast<double*>(s->pd_block);
+        a.init = s->pd_init_pending;
+        s->pd_init_pending = 0;
+        const int64_t maxL = (a.nslices + G - 1) / G;
+        a.pack = (int)((maxL + PK_WAVES - 1) / PK_WAVES);
+    }
     void* args[] = {&a};
-    const void* fn = persist_fn(prof != nullptr && !s->pk_ovf, (s->tune & FEM_TUNE_PK_SC1) != 0, s->pk_ovf != 0);
+    const void* fn = s->pd ? persist_fn_dist(prof != nullptr, a.pack)
+                           : persist_fn(prof != nullptr && !s->pk_ovf, (s->tune & FEM_TUNE_PK_SC1) != 0, s->pk_ovf != 0);
     // the grid spins on inter-workgroup flags, so all G workgroups must be resident together: one per CU is
     // what the occupancy query promised, and a cooperative launch makes the runtime guarantee it (or fail) even
     // when other streams / processes hold CUs. A plain launch (the bench's fixed-iteration runs) relies on the
@@ -2559,6 +2654,20 @@ int fem_pcg_start(fem_pcg* s) {
     if (s->mode == FEM_MODE_CG_STABLE) {
         hipLaunchKernelGGL(k_zero_fixed, dim3(stream_grid(s->n, 256)), dim3(256), 0, s->stream, s->n, s->x, s->w);
         FEM_LAUNCHED();
+    }
+    if (s->pd) {   // distributed persistent: the first launch forms r0, u0 and r0.u0 itself (k_pcg_persist DIST init)
+        if (!s->persist) {
+            set_error("distributed persistent PCG: setup failed");
+            return FEM_EARG;
+        }
+        FEM_HIP(hipMemsetAsync(s->pk_sync, 0, sizeof(unsigned) * pk_sync_words(s->pk_grid), s->stream));
+        FEM_HIP(hipMemsetAsync(s->pd_block + s->pd_off_flag, 0, (size_t)(s->pd_block_bytes - s->pd_off_flag),
+                               s->stream));
+        FEM_HIP(hipMemsetAsync(&s->st->pk_epoch, 0, sizeof(unsigned), s->stream));
+        s->pk_epochs = 0;
+        s->pd_init_pending = 1;
+        s->launched = 0;
+        return FEM_OK;   // every rank must finish its start before any rank launches (a host barrier)
     }
     if ((rc = (s->cols16 ? fem_spmv16(s->nrows, s->bs, s->slice_ptr, s->cols16, s->vals, s->x, s->q, s->stream)
                           : fem_spmv(s->nrows, s->bs, s->slice_ptr, s->cols, s->vals, s->x, s->q, s->stream)))) return rc;
@@ -2886,6 +2995,10 @@ int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, 
     // gave up (FEM_PCG_SYNC_TIMEOUT: the workgroups were not all resident) is re-solved on the deferred schedule
     // from the same start instead of returning a meaningless iterate
     double* x0 = nullptr;
+    if (s->pd) {   // ranks must pass a host barrier between their starts and their first launches
+        set_error("fem_pcg_solve: a distributed persistent context is driven by start / iterate / poll per rank");
+        return FEM_EARG;
+    }
     const bool may_persist = s->persist_req && s->bs == 1 && !s->dist && s->mode != FEM_MODE_CG_CONSTRAINED;
     if (may_persist) {
         FEM_HIP(pool_alloc((void**)&x0, sizeof(double) * (size_t)(s->n + 2), s->stream, true));
@@ -2993,9 +3106,161 @@ int fem_pcg_profile(fem_pcg* s, int k, int every, double* ms, int* n) {
     return rc;
 }
 
+// ------------------------------------------------------------------ distributed persistent schedule
+int fem_pcg_set_rows(fem_pcg* s, int nranks, int rank, const int64_t* slice_split, int grid) {
+    if (nranks < 1 || nranks > PK_MAX_RANKS || rank < 0 || rank >= nranks || !slice_split) {
+        set_error("fem_pcg_set_rows: nranks %d (1..%d), rank %d", nranks, PK_MAX_RANKS, rank);
+        return FEM_EARG;
+    }
+    if (s->bs != 1 || s->dist || s->mode == FEM_MODE_CG_CONSTRAINED || s->pd) {
+        set_error("fem_pcg_set_rows: bs = 1, not element-partitioned, not constrained, once per context");
+        return FEM_EARG;
+    }
+    if (slice_split[0] != 0 || slice_split[nranks] != s->nslices) {
+        set_error("fem_pcg_set_rows: the split must cover slices [0, %lld)", (long long)s->nslices);
+        return FEM_EARG;
+    }
+    for (int q = 0; q < nranks; ++q)
+        if (slice_split[q + 1] <= slice_split[q]) {
+            set_error("fem_pcg_set_rows: rank %d owns no slice", q);
+            return FEM_EARG;
+        }
+    int dev = 0, ncu = 0;
+    FEM_HIP(hipGetDevice(&dev));
+    FEM_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    const int G = grid > 0 ? grid : (ncu / NXCD) * NXCD;
+    if (G < NXCD || G % NXCD || G > ncu) {
+        set_error("fem_pcg_set_rows: grid %d must be a multiple of %d within %d CUs", G, NXCD, ncu);
+        return FEM_EARG;
+    }
+    s->pd_rank = rank;
+    s->pd_nranks = nranks;
+    for (int q = 0; q <= nranks; ++q) s->pd_split[q] = slice_split[q];
+    // comm block: u (global length) | u-flags of all nranks * G workgroups | rank sums | rank epoch lines
+    const int64_t line = sizeof(unsigned) * PK_LINE;
+    s->pd_off_flag = (int64_t)cdiv(sizeof(double) * (s->n + 2), 256) * 256;
+    s->pd_off_red = s->pd_off_flag + (int64_t)nranks * G * line;
+    s->pd_off_rflag = s->pd_off_red + 256;
+    s->pd_block_bytes = s->pd_off_rflag + PK_MAX_RANKS * line;
+    FEM_HIP(hipMalloc((void**)&s->pd_block, (size_t)s->pd_block_bytes));
+    FEM_HIP(hipMemsetAsync(s->pd_block, 0, (size_t)s->pd_block_bytes, s->stream));
+    // the single-GPU persistent buffers for this grid, and the gather windows in global workgroup ids
+    pool_free(s->pk_win, s->stream);
+    pool_free(s->pk_part, s->stream);
+    pool_free(s->pk_sync, s->stream);
+    FEM_HIP(pool_alloc((void**)&s->pk_win, sizeof(int32_t) * (2 * G + 2), s->stream, true));
+    FEM_HIP(pool_alloc((void**)&s->pk_part, sizeof(double) * 4 * G, s->stream, true));
+    FEM_HIP(pool_alloc((void**)&s->pk_sync, sizeof(unsigned) * pk_sync_words(G), s->stream, true));
+    s->pk_grid = G;
+    std::vector<int32_t> lohi(2 * (size_t)G + 2);
+    for (int i = 0; i < G; ++i) {
+        lohi[i] = nranks * G;
+        lohi[G + i] = -1;
+    }
+    lohi[2 * G] = 0x7fffffff;
+    lohi[2 * G + 1] = -1;
+    FEM_HIP(hipMemcpyAsync(s->pk_win, lohi.data(), sizeof(int32_t) * lohi.size(), hipMemcpyHostToDevice, s->stream));
+    PkSplit sp{};
+    for (int q = 0; q <= nranks; ++q) sp.b[q] = slice_split[q];
+    const int64_t nloc = slice_split[rank + 1] - slice_split[rank];
+    hipLaunchKernelGGL(k_pk_window_dist, dim3(stream_grid(nloc * 64, 256)), dim3(256), 0, s->stream, slice_split[rank],
+                       nloc, s->nrows, s->slice_ptr, s->cols, G, sp, nranks, s->pk_win, s->pk_win + G,
+                       s->pk_win + 2 * G);
+    FEM_LAUNCHED();
+    FEM_HIP(hipStreamSynchronize(s->stream));   // lohi must outlive the copy
+    s->pk_win_ok = 1;
+    s->pd = 1;
+    s->pd_peers_ok = 0;
+    s->persist_req = 1;
+    s->deferred = 1;
+    s->fused = 0;
+    return FEM_OK;
+}
+
+int fem_pcg_comm_block(fem_pcg* s, void** base, int64_t* bytes) {
+    if (!s->pd) {
+        set_error("fem_pcg_comm_block: fem_pcg_set_rows first");
+        return FEM_EARG;
+    }
+    if (base) *base = s->pd_block;
+    if (bytes) *bytes = s->pd_block_bytes;
+    return FEM_OK;
+}
+
+int fem_pcg_col_window(fem_pcg* s, int64_t* lo, int64_t* hi) {
+    if (!s->pd) {
+        set_error("fem_pcg_col_window: fem_pcg_set_rows first");
+        return FEM_EARG;
+    }
+    int32_t w[2];
+    FEM_HIP(hipMemcpyAsync(w, s->pk_win + 2 * s->pk_grid, sizeof w, hipMemcpyDeviceToHost, s->stream));
+    FEM_HIP(hipStreamSynchronize(s->stream));
+    *lo = w[0];
+    *hi = w[1];
+    return FEM_OK;
+}
+
+int fem_pcg_set_peers(fem_pcg* s, void* const* bases, const int64_t* need_lo, const int64_t* need_hi) {
+    if (!s->pd) {
+        set_error("fem_pcg_set_peers: fem_pcg_set_rows first");
+        return FEM_EARG;
+    }
+    const int N = s->pd_nranks, G = s->pk_grid, r = s->pd_rank;
+    for (int q = 0; q < N; ++q) {
+        s->pd_peer[q] = q == r ? s->pd_block : (char*)bases[q];
+        if (!s->pd_peer[q]) {
+            set_error("fem_pcg_set_peers: no comm block for rank %d", q);
+            return FEM_EARG;
+        }
+    }
+    // rows of each local workgroup that rank q gathers: its rows within q's column window
+    const int64_t S0 = s->pd_split[r], nloc = s->pd_split[r + 1] - S0;
+    std::vector<int32_t> pub((size_t)G * N * 2, 0);
+    for (int L = 0; L < G; ++L) {
+        const int64_t rlo = (S0 + (int64_t)L * nloc / G) * 64;
+        const int64_t rhi = std::min<int64_t>((S0 + (int64_t)(L + 1) * nloc / G) * 64, s->nrows);
+        for (int q = 0; q < N; ++q) {
+            if (q == r) continue;
+            const int64_t lo = std::max<int64_t>(rlo, need_lo[q]), hi = std::min<int64_t>(rhi, need_hi[q] + 1);
+            if (lo < hi) {
+                pub[((size_t)L * N + q) * 2] = (int32_t)lo;
+                pub[((size_t)L * N + q) * 2 + 1] = (int32_t)hi;
+            }
+        }
+    }
+    if (!s->pd_pub) FEM_HIP(hipMalloc((void**)&s->pd_pub, sizeof(int32_t) * pub.size()));
+    FEM_HIP(hipMemcpyAsync(s->pd_pub, pub.data(), sizeof(int32_t) * pub.size(), hipMemcpyHostToDevice, s->stream));
+    FEM_HIP(hipStreamSynchronize(s->stream));
+    s->pd_peers_ok = 1;
+    return FEM_OK;
+}
+
+int fem_ipc_handle(void* ptr, char* out64) {
+    hipIpcMemHandle_t h;
+    FEM_HIP(hipIpcGetMemHandle(&h, ptr));
+    static_assert(sizeof(h) <= 64, "IPC handle size");
+    memset(out64, 0, 64);
+    memcpy(out64, &h, sizeof h);
+    return FEM_OK;
+}
+
+int fem_ipc_open(const char* h64, void** ptr) {
+    hipIpcMemHandle_t h;
+    memcpy(&h, h64, sizeof h);
+    FEM_HIP(hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess));
+    return FEM_OK;
+}
+
+int fem_ipc_close(void* ptr) {
+    FEM_HIP(hipIpcCloseMemHandle(ptr));
+    return FEM_OK;
+}
+
 void fem_pcg_destroy(fem_pcg* s) {
     if (!s) return;
     if (s->pev[0]) (void)hipEventDestroy(s->pev[0]);
+    if (s->pd_block) (void)hipFree(s->pd_block);
+    if (s->pd_pub) (void)hipFree(s->pd_pub);
     if (s->pev[1]) (void)hipEventDestroy(s->pev[1]);
     if (s->graph) (void)hipGraphExecDestroy(s->graph);
     pool_free(s->r, s->stream);

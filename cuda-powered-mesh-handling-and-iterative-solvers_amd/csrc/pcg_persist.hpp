@@ -153,6 +153,8 @@ __device__ __forceinline__ double pk_block_sum(double v, double* lds16) {
     return t;
 }
 
+constexpr int PK_MAX_RANKS = 8;
+
 struct PkArgs {
     int64_t nslices, nrows;
     const int64_t* slice_ptr;
@@ -176,7 +178,99 @@ struct PkArgs {
     double* v;              // OVF: v = A u of the overflow rows (their state stays in r, p, s, x, u, w in HBM)
     unsigned long long* prof;   // PROF instantiation: [G][PK_NPROF] shader-clock sums per phase (thread 0 of each WG),
                                 // then [G][PK_WAVES] SpMV-phase clock sums of every wave (its own slices only)
+    // DIST build (one rank per GPU, rows partitioned): this rank owns the global slices [sbase, sbase + nslices) of
+    // a matrix whose rows are global; every vector is global-length. Each rank's comm block (peer[rank]; the other
+    // ranks' blocks mapped through IPC) holds: u at offset 0 (the gathered vector: own rows written here, the rows
+    // other ranks gather from this rank also written into THEIR blocks), the u-flags of all nranks * G workgroups
+    // (off_flag, one line each, written by the owning workgroup wherever its rows are gathered), the rank sums
+    // [2 banks][PK_MAX_RANKS][d, g] (off_red) and one epoch line per rank announcing them (off_rflag).
+    int64_t sbase;
+    int rank, nranks;
+    char* peer[PK_MAX_RANKS];
+    int64_t off_flag, off_red, off_rflag;
+    const int32_t* pub;     // [G][nranks][2]: rows [lo, hi) of logical workgroup L gathered by rank Q (lo >= hi: none)
+    const double* b;        // init launch: r0 = b - A x0 over the own rows (x0 global-length, the same on every rank)
+    int init;
 };
+
+// DIST: after the local grid barrier every workgroup holds this rank's sums (out[0] = d, out[1] = g); wave 0 of
+// logical workgroup 0 announces them to every rank (system-scope stores into each rank's comm block, a system
+// release, then the epoch line), and wave 0 of every workgroup waits for all ranks' epoch e and sums the ranks'
+// values in rank order 0..N-1 -- identical bits on every rank. Banked by epoch parity (a rank reaches epoch e + 2
+// only after every rank announced e + 1, i.e. after every reader of bank e is done with it).
+__device__ __forceinline__ bool pk_rank_sum(const PkArgs& a, int L, unsigned e, unsigned* tmo, double* out,
+                                            int* lds_ok) {
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        const int bank = (int)(e & 1u);
+        int okv = 1;
+        if (L == 0) {
+            const double d = out[0], g = out[1];
+            if (lane < a.nranks) {
+                double* red = reinterpret_cast<double*>(a.peer[lane] + a.off_red) + (bank * PK_MAX_RANKS + a.rank) * 2;
+                __hip_atomic_store(red, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(red + 1, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane < a.nranks)
+                __hip_atomic_store(reinterpret_cast<unsigned*>(a.peer[lane] + a.off_rflag) + a.rank * PK_LINE, e,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        const unsigned* rf = reinterpret_cast<const unsigned*>(a.peer[a.rank] + a.off_rflag);
+        bool done = lane >= a.nranks;
+        for (unsigned spins = 0; !__all(done); ++spins) {
+            if (!done) done = __hip_atomic_load(rf + lane * PK_LINE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= e;
+            if ((spins & 63) == 63 && pk_ld(tmo)) {
+                okv = 0;
+                break;
+            }
+            if (spins >= 4 * PK_SPIN_LIMIT) {   // ranks start their launches up to milliseconds apart
+                pk_st(tmo, 1u);
+                okv = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (okv) {
+            const double* red = reinterpret_cast<const double*>(a.peer[a.rank] + a.off_red) + bank * PK_MAX_RANKS * 2;
+            double d = 0.0, g = 0.0;
+            for (int q = 0; q < a.nranks; ++q) {   // rank order: the same sum on every rank
+                d += __hip_atomic_load(red + 2 * q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                g += __hip_atomic_load(red + 2 * q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            if (lane == 0) {
+                out[0] = d;
+                out[1] = g;
+            }
+        }
+        if (lane == 0) *lds_ok = okv;
+    }
+    __syncthreads();
+    return *lds_ok != 0;
+}
+
+// DIST: row `row` of this rank's u also lands in the comm block of every rank in pubmask whose gathered range holds it
+__device__ __forceinline__ void pk_publish_row(const PkArgs& a, int L, unsigned pubmask, unsigned row, double v) {
+    for (int q = 0; q < a.nranks; ++q) {
+        if (!(pubmask & (1u << q))) continue;
+        const int32_t* pr = a.pub + (L * a.nranks + q) * 2;
+        if ((int)row >= pr[0] && (int)row < pr[1])
+            __hip_atomic_store(reinterpret_cast<double*>(a.peer[q]) + row, v, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// DIST: after every wave drained its stores (and, where it published rows to other ranks, ran a system release),
+// thread 0 raises this workgroup's u-flag in every rank that gathers its rows
+__device__ __forceinline__ void pk_publish_flag(const PkArgs& a, int Lg, unsigned pubmask, unsigned e) {
+    for (int q = 0; q < a.nranks; ++q)
+        if (pubmask & (1u << q))
+            __hip_atomic_store(reinterpret_cast<unsigned*>(a.peer[q] + a.off_flag) + Lg * PK_LINE, e, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 
 // the 64 rows of slot j of this wave: row = rb + 64 j (32-bit; the host checks nrows < 2^31); `lim` = rows of the
 // slot that exist (wave-uniform; < 64 only in the matrix's last slice)
@@ -187,8 +281,10 @@ struct PkArgs {
 // OVF: meshes past MAXS slices per wave (packed assignment only): a wave's slices beyond its MAXS register slots keep
 // their CG state in HBM (the r, p, s, x, u, w arrays, v in a.v) and are streamed every iteration like the deferred
 // schedule's rows, inside the same launch and the same barriers
-template <int MAXS, bool PROF, bool GSC1, bool OVF = false>
+// DIST: see PkArgs (GSC1 and !OVF implied)
+template <int MAXS, bool PROF, bool GSC1, bool OVF = false, bool DIST = false>
 __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
+    static_assert(!DIST || (GSC1 && !OVF), "distributed persistent PCG: sc1 gathers, no overflow build");
     unsigned long long pacc[PROF ? PK_NPROF : 1] = {};
     unsigned long long pt = 0, wspmv = 0;
     if constexpr (PROF) pt = __builtin_amdgcn_s_memtime();
@@ -219,7 +315,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
     int s0, nsl;
     if (a.pack) {
         const int m = a.pack;   // <= MAXS (host)
-        const int sL0 = (int)((int64_t)L * a.nslices / G);
+        const int sL0 = (int)((int64_t)L * a.nslices / G) + (DIST ? (int)a.sbase : 0);
         const int nL = (int)((int64_t)(L + 1) * a.nslices / G) - sL0;
         const int lo = wv * m < nL ? wv * m : nL;
         s0 = sL0 + lo;
@@ -239,6 +335,16 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
     double* vl = pk_lds + 2 * PK_WAVES * MAXS * 64 + wv * PK_VL * 64 + lane;   // v of slots j < PK_VL
     unsigned* sy = a.sync;
     PcgState* st = a.st;
+    // u-flags: this rank's own lines (single GPU), or the comm block's lines of all ranks' workgroups (DIST)
+    unsigned* uf = DIST ? reinterpret_cast<unsigned*>(a.peer[a.rank] + a.off_flag) : sy + PK_UFLAG;
+    const int Lg = DIST ? a.rank * G + L : L;   // global logical workgroup
+    unsigned pubmask = 0;                       // DIST: ranks that gather rows of this workgroup
+    bool ghost = false;                         // DIST: this workgroup gathers rows of other ranks
+    if constexpr (DIST) {
+        for (int q = 0; q < a.nranks; ++q)
+            if (q != a.rank && a.pub[(L * a.nranks + q) * 2] < a.pub[(L * a.nranks + q) * 2 + 1]) pubmask |= 1u << q;
+        ghost = a.win[L] < a.rank * G || a.win[G + L] >= (a.rank + 1) * G;
+    }
 
     // scalars (every thread; WG 0 thread 0 writes them back)
     const bool cg = st->mode != FEM_MODE_PCG;
@@ -247,7 +353,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
     int it = st->iter, halt = st->halt, status = st->status, stop_iter = st->stop_iter;
     double rz = st->rz, alpha_prev = st->alpha, beta = st->beta, pq = st->pq, rz_new = st->rz_new;
     double g = st->red[1];   // r.z of the current iterate (init or the last launch's last update)
-    const unsigned ebase = st->pk_epoch;   // barriers of earlier launches (sync words count on from there)
+    unsigned ebase = st->pk_epoch;         // barriers of earlier launches (sync words count on from there)
     unsigned elast = ebase;                // last barrier epoch of this launch
 
     double rr[MAXS], pp[MAXS], ss[MAXS], vv[MAXS], uo[MAXS];
@@ -268,24 +374,88 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
     const int wlo = a.win[L], whi = a.win[G + L];
     bool fail = false;
     int k = 0;
+    if constexpr (DIST) {
+        // first launch of a distributed solve: r0 = b - A x0 over the own rows (x0 global-length, identical on every
+        // rank), u0 = w r0 published like an update (epoch ebase + 1), r0.u0 summed by a full barrier (local, then
+        // across ranks) -- the distributed counterpart of k_cg1_init
+        if (a.init && !halt) {
+            const int64_t* slp = pk_launder(a.slice_ptr);
+            const int16_t* cop = pk_launder(a.cols);
+            const double* vap = pk_launder(a.vals);
+            const double* xvp = pk_launder(a.x);
+            double gp = 0.0;
+#pragma unroll
+            for (int j = 0; j < MAXS; ++j) {
+                if (j < nreg) {
+                    const double q = sell_row_pair<PK_U, 0>(s0 + j, lane, slp, cop, vap, xvp);
+                    const unsigned row = rb + 64u * j;
+                    const bool on = PK_ON(j);
+                    double rv = on ? a.b[row] - q : 0.0;
+                    const double wj = wl[j * 64];
+                    if (cg && wj == 0.0) rv = 0.0;
+                    rr[j] = rv;
+                    pp[j] = 0.0;
+                    ss[j] = 0.0;
+                    const double ui = wj * rv;
+                    uo[j] = ui;
+                    gp += rv * ui;
+                    if (on) {
+                        __hip_atomic_store(a.u + row, ui, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (pubmask) pk_publish_row(a, L, pubmask, row, ui);
+                    }
+                }
+                asm volatile("" ::: "memory");
+            }
+            {
+                const double gw = wave_sum(gp);
+                if (lane == 0) lds16[wv] = gw;
+            }
+            if (pubmask) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            const unsigned e0 = ebase + 1;
+            double* pg0 = a.part + 2 * (size_t)G;   // bank 1's d slots: first written at local iteration 1
+            if (threadIdx.x == 0) {
+                double gsum = 0.0;
+#pragma unroll
+                for (int i = 0; i < PK_WAVES; ++i) gsum += lds16[i];
+                __hip_atomic_store(pg0 + L, gsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                pk_st(uf + Lg * PK_LINE, e0);
+                pk_publish_flag(a, Lg, pubmask, e0);
+            }
+            if (!pk_barrier(sy, grp, nper, e0, &lds_ok, pg0, nullptr, G, lds_dg) ||
+                !pk_rank_sum(a, L, e0, sy + PK_TMO, lds_dg, &lds_ok)) {
+                fail = true;
+            } else {
+                g = lds_dg[0];
+                rz = g;
+                ebase = e0;
+                elast = e0;
+            }
+        }
+    }
     if constexpr (PROF) {
         __syncthreads();
         const unsigned long long now = __builtin_amdgcn_s_memtime();
         pacc[6] += now - pt;
         pt = now;
     }
-    if (!halt) {
+    if (!halt && !fail) {
         for (k = 0; k < a.kmax; ++k) {
             const unsigned e = ebase + (unsigned)k + 1;
-            // ---- wait for the u of the gather window (written by the previous update of this launch)
-            if (k > 0) {
+            // ---- wait for the u of the gather window (written by the previous update of this launch, or by the
+            // distributed init above)
+            if (k > 0 || (DIST && a.init)) {
                 if (wv == 0) {
                     bool ok = true;
                     for (int b0 = wlo; b0 <= whi && ok; b0 += 64) {
                         const int jw = b0 + lane;
                         bool done = jw > whi;
                         for (unsigned spins = 0; !__all(done); ++spins) {
-                            if (!done) done = pk_ld(sy + PK_UFLAG + jw * PK_LINE) >= e - 1;
+                            if (!done)
+                                done = (DIST ? __hip_atomic_load(uf + jw * PK_LINE, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_SYSTEM)
+                                             : pk_ld(uf + jw * PK_LINE)) >= e - 1;
                             if ((spins & 63) == 63 && pk_ld(sy + PK_TMO)) {
                                 ok = false;
                                 break;
@@ -322,26 +492,33 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
             const int16_t* cop = pk_launder(a.cols);
             const double* vap = pk_launder(a.vals);
             const double* uvp = pk_launder(a.u);
-            if (!rv) {
-#pragma unroll
-                for (int j = 0; j < MAXS; ++j) {
-                    if (j < nreg) {
-                        const double v = sell_row_pair<PK_U, GSC1>(s0 + j, lane, slp, cop, vap, uvp);
-                        if (j < PK_VL) vl[j * 64] = v; else vv[j] = v;
-                    }
-                    asm volatile("" ::: "memory");
-                }
+#define PK_SPMV(MODE)                                                                              \
+    if (!rv) {                                                                                     \
+        _Pragma("unroll") for (int j = 0; j < MAXS; ++j) {                                         \
+            if (j < nreg) {                                                                        \
+                const double v = sell_row_pair<PK_U, MODE>(s0 + j, lane, slp, cop, vap, uvp);      \
+                if (j < PK_VL) vl[j * 64] = v; else vv[j] = v;                                     \
+            }                                                                                      \
+            asm volatile("" ::: "memory");                                                         \
+        }                                                                                          \
+    } else {                                                                                       \
+        _Pragma("unroll") for (int jj = 0; jj < MAXS; ++jj) {                                      \
+            const int j = MAXS - 1 - jj;                                                           \
+            if (j < nreg) {                                                                        \
+                const double v = sell_row_pair<PK_U, MODE>(s0 + j, lane, slp, cop, vap, uvp);      \
+                if (j < PK_VL) vl[j * 64] = v; else vv[j] = v;                                     \
+            }                                                                                      \
+            asm volatile("" ::: "memory");                                                         \
+        }                                                                                          \
+    }
+            // DIST: a workgroup whose gather window reaches other ranks reads u past this GPU's L2 (those rows
+            // arrive from other GPUs; the L2 may hold the previous iteration's copy)
+            if (DIST && ghost) {
+                PK_SPMV(2)
             } else {
-#pragma unroll
-                for (int jj = 0; jj < MAXS; ++jj) {
-                    const int j = MAXS - 1 - jj;
-                    if (j < nreg) {
-                        const double v = sell_row_pair<PK_U, GSC1>(s0 + j, lane, slp, cop, vap, uvp);
-                        if (j < PK_VL) vl[j * 64] = v; else vv[j] = v;
-                    }
-                    asm volatile("" ::: "memory");
-                }
+                PK_SPMV((GSC1 ? 1 : 0))
             }
+#undef PK_SPMV
             if constexpr (PROF) {   // this wave's own SpMV time (results back: the v slots are written)
                 asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
                 wspmv += __builtin_amdgcn_s_memtime() - tw0;
@@ -371,6 +548,12 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
             if (!pk_barrier(sy, grp, nper, e, &lds_ok, pd, k > 0 ? pd + G : nullptr, G, lds_dg)) {
                 fail = true;
                 break;
+            }
+            if constexpr (DIST) {
+                if (!pk_rank_sum(a, L, e, sy + PK_TMO, lds_dg, &lds_ok)) {
+                    fail = true;
+                    break;
+                }
             }
             elast = e;
             const double d = lds_dg[0];
@@ -448,7 +631,12 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
                     rr[j] = ri;
                     const double ui = wi * ri;
                     uo[j] = ui;
-                    if (PK_ON(j)) __hip_atomic_store(ust + (rbi + 64u * j), ui, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (PK_ON(j)) {
+                        __hip_atomic_store(ust + (rbi + 64u * j), ui, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if constexpr (DIST) {
+                            if (pubmask) pk_publish_row(a, L, pubmask, rbi + 64u * j, ui);
+                        }
+                    }
                     gp += ri * ui;
                 }
             }
@@ -480,6 +668,9 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
                 const double gw = wave_sum(gp);
                 if (lane == 0) lds16[wv] = gw;
             }
+            if constexpr (DIST) {   // rows published to other GPUs: system release before the flags
+                if (pubmask) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave drains its u stores
             __syncthreads();
             if (threadIdx.x == 0) {
@@ -488,7 +679,8 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
                 for (int i = 0; i < PK_WAVES; ++i) gsum += lds16[i];
                 __hip_atomic_store(a.part + (size_t)(bank ^ 1) * 2 * G + G + L, gsum, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
-                pk_st(sy + PK_UFLAG + L * PK_LINE, e);
+                pk_st(uf + Lg * PK_LINE, e);
+                if constexpr (DIST) pk_publish_flag(a, Lg, pubmask, e);
             }
             PK_MARK(5);
         }
@@ -496,7 +688,9 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
     // ---- chunk end without a stop: one more barrier makes the last g partials visible; stop test of that g
     if (!fail && !halt && k == a.kmax && a.kmax > 0) {
         const unsigned e = ebase + (unsigned)a.kmax + 1;
-        if (!pk_barrier(sy, grp, nper, e, &lds_ok, a.part + (size_t)(a.kmax & 1) * 2 * G + G, nullptr, G, lds_dg)) {
+        bool okb = pk_barrier(sy, grp, nper, e, &lds_ok, a.part + (size_t)(a.kmax & 1) * 2 * G + G, nullptr, G, lds_dg);
+        if constexpr (DIST) okb = okb && pk_rank_sum(a, L, e, sy + PK_TMO, lds_dg, &lds_ok);
+        if (!okb) {
             fail = true;
         } else {
             elast = e;
@@ -592,6 +786,56 @@ __global__ void k_pk_window(int64_t nslices, int64_t nrows, const int64_t* __res
         if (l == 0) {
             atomicMin(lo + me, olo);
             atomicMax(hi + me, ohi);
+        }
+    }
+}
+
+// DIST gather windows: for every own slice of this rank (global slices [sbase, sbase + nloc)), the first and last
+// GLOBAL logical workgroup (rank * G + L) owning a column of its rows; ranks own the slice ranges split[r..r+1)
+struct PkSplit {
+    int64_t b[PK_MAX_RANKS + 1];
+};
+__global__ void k_pk_window_dist(int64_t sbase, int64_t nloc, int64_t nrows, const int64_t* __restrict__ slice_ptr,
+                                 const int32_t* __restrict__ cols, int G, PkSplit split, int nranks,
+                                 int* __restrict__ lo, int* __restrict__ hi, int* __restrict__ cwin) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nloc * 64; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = sbase + (t >> 6);
+        const int l = (int)(t & 63);
+        const int64_t row = s * 64 + l;
+        const int64_t p0 = slice_ptr[s];
+        const int w = (int)((slice_ptr[s + 1] - p0) >> 6);
+        int64_t cmin = row < nrows ? row : nrows - 1, cmax = cmin;
+        if (row < nrows)
+            for (int kk = 0; kk < w; ++kk) {
+                const int64_t c = cols[p0 + 64 * kk + l];
+                cmin = c < cmin ? c : cmin;
+                cmax = c > cmax ? c : cmax;
+            }
+        auto owner = [&](int64_t r) {   // global logical workgroup owning row r
+            const int64_t sl = r >> 6;
+            int q = 0;
+            while (q + 1 < nranks && split.b[q + 1] <= sl) ++q;
+            const int64_t S = split.b[q + 1] - split.b[q];
+            const int64_t tl = sl - split.b[q];
+            const int64_t L = S > 0 ? ((tl + 1) * G - 1) / S : 0;
+            return (int)(q * G + (L < G ? L : G - 1));
+        };
+        const int me = owner(s * 64) - (int)(owner(sbase * 64) / G) * G;   // local logical workgroup of slice s
+        int olo = owner(cmin), ohi = owner(cmax);
+        int clo = (int)cmin, chi = (int)cmax;
+        for (int off = 32; off > 0; off >>= 1) {
+            const int a2 = __shfl_xor(olo, off), b2 = __shfl_xor(ohi, off);
+            const int c2 = __shfl_xor(clo, off), d2 = __shfl_xor(chi, off);
+            olo = a2 < olo ? a2 : olo;
+            ohi = b2 > ohi ? b2 : ohi;
+            clo = c2 < clo ? c2 : clo;
+            chi = d2 > chi ? d2 : chi;
+        }
+        if (l == 0) {
+            atomicMin(lo + me, olo);
+            atomicMax(hi + me, ohi);
+            atomicMin(cwin, clo);   // the rank's column window: rows of other ranks it gathers
+            atomicMax(cwin + 1, chi);
         }
     }
 }

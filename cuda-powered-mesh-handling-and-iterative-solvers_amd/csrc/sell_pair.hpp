@@ -28,16 +28,18 @@ static __global__ void k_sell_pair(int64_t nslices, const int64_t* __restrict__ 
 }
 
 
-// gathered x element: plain load, or (SC1) an agent-scope relaxed load (global_load sc1): the coherent form that
-// may replace the consumer's acquire when every producer store was sc1 (MI355X_MICROARCH.md, Valid forms)
-template <bool SC1>
+// gathered x element: plain load (SC1 = 0), an agent-scope relaxed load (1: global_load sc1, the coherent form that
+// may replace the consumer's acquire when every producer store was sc1, MI355X_MICROARCH.md, Valid forms), or a
+// system-scope relaxed load (2: sc0 sc1, past this GPU's L2 -- rows another GPU wrote into this GPU's memory)
+template <int SC1>
 __device__ __forceinline__ double ldx(const double* p) {
-    if constexpr (SC1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (SC1 == 2) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else if constexpr (SC1 == 1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else return *p;
 }
 
 // y_row (bs = 1) of one slice row in the paired layout; U pairs in flight
-template <int U, bool SC1 = false>
+template <int U, int SC1 = 0>
 __device__ __forceinline__ double sell_row_pair(int64_t s, int lane, const int64_t* __restrict__ slice_ptr,
                                                 const int16_t* __restrict__ cols, const double* __restrict__ vals,
                                                 const double* __restrict__ x) {

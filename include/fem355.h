@@ -415,6 +415,31 @@ int fem_pcg_use_graph(fem_pcg* s, int k);
  * n[0..2] sampled launches (bench.py's live per-kernel timing inside its timed region) */
 int fem_pcg_profile(fem_pcg* s, int k, int every, double* ms, int* n);
 void fem_pcg_destroy(fem_pcg* s);
+/* ------------------------------------------------------------------ multi-GPU persistent schedule (rows partitioned)
+ * The persistent schedule across ranks (one process per GPU, or several contexts of one process on one GPU for
+ * validation): every rank holds the SELL rows of the global matrix it owns (global row / column numbering, all
+ * vectors global-length) and runs ONE persistent launch per chunk over its own slices; the u rows another rank
+ * gathers are written straight into that rank's comm block (system-scope stores over xGMI + a system release +
+ * an epoch flag per workgroup), and the per-iteration sums go rank -> every rank the same way, summed in rank
+ * order (bit-identical scalars everywhere). No collective library call inside an iteration. bs = 1 only.
+ *   fem_pcg_set_rows  : rank `rank` of `nranks` (<= 8) owns the global slices [split[rank], split[rank+1]) of the
+ *                       context's matrix; grid = workgroups of this rank's launches (0: one per CU; a multiple of
+ *                       8: several ranks sharing one GPU); allocates the comm block and the gather windows.
+ *   fem_pcg_comm_block: [host] the rank's comm block (device memory from hipMalloc: exportable with fem_ipc_handle)
+ *   fem_pcg_col_window: [sync] min / max global column of the own rows (exchange between the ranks)
+ *   fem_pcg_set_peers : every rank's comm block as mapped in THIS process (own entry ignored) and column window
+ *   then fem_pcg_start on EVERY rank, a host barrier over the ranks, and fem_pcg_iterate / fem_pcg_profile /
+ *   fem_pcg_poll with the same k on every rank (the first launch after a start forms r0 = b - A x0, u0 and r0.u0
+ *   itself). fem_pcg_solve refuses such a context (it cannot place the barrier).
+ * fem_ipc_handle / fem_ipc_open / fem_ipc_close: 64-byte hipIpcMemHandle of a device allocation, and its mapping in
+ * another process (hipIpcMemLazyEnablePeerAccess). */
+int fem_pcg_set_rows(fem_pcg* s, int nranks, int rank, const int64_t* slice_split, int grid);
+int fem_pcg_comm_block(fem_pcg* s, void** base, int64_t* bytes);
+int fem_pcg_col_window(fem_pcg* s, int64_t* lo, int64_t* hi);
+int fem_pcg_set_peers(fem_pcg* s, void* const* bases, const int64_t* need_lo, const int64_t* need_hi);
+int fem_ipc_handle(void* ptr, char* out64);
+int fem_ipc_open(const char* h64, void** ptr);
+int fem_ipc_close(void* ptr);
 /* [host] free the buffers that destroyed bs = 1 contexts left in the library's recycling cache (capped at
  * FEM355_PCG_CACHE_MB, default 1024 MB; invisible to torch's allocator); returns the MB released */
 int fem_pcg_release_cache(void);

