@@ -2947,7 +2947,9 @@ static int fem_pcg_poll_raw(fem_pcg* s, int* iters, int* status, double* rz) {
     int stt = h.status;
     // single reduction: the stop test of the last update runs in the next step, which also sets halt
     if (stt == FEM_PCG_RUNNING && h.iter >= h.max_iter && (!(s->dist && s->cg1) || h.halt)) stt = FEM_PCG_MAXITER;
-    if (iters) *iters = (stt == FEM_PCG_BREAKDOWN || stt == FEM_PCG_ALPHA_NAN) ? h.stop_iter : h.iter;
+    if (iters)
+        *iters = (stt == FEM_PCG_BREAKDOWN || stt == FEM_PCG_ALPHA_NAN || stt == FEM_PCG_SYNC_TIMEOUT) ? h.stop_iter
+                                                                                                      : h.iter;
     if (status) *status = stt;
     if (rz) *rz = (h.iter > 0) ? h.rz_new : h.rz;
     return FEM_OK;
@@ -3213,25 +3215,66 @@ int fem_pcg_set_peers(fem_pcg* s, void* const* bases, const int64_t* need_lo, co
             return FEM_EARG;
         }
     }
-    // rows of each local workgroup that rank q gathers: its rows within q's column window
+    // for each local workgroup and rank q: {-1, -1} when q never waits on it, else the rows [lo, hi) of it that q
+    // gathers (possibly none). q waits on the contiguous range of global workgroups between the owners of its
+    // column window's ends -- a workgroup in that range without rows (fewer slices than workgroups) still raises
+    // its flag there
     const int64_t S0 = s->pd_split[r], nloc = s->pd_split[r + 1] - S0;
-    std::vector<int32_t> pub((size_t)G * N * 2, 0);
-    for (int L = 0; L < G; ++L) {
-        const int64_t rlo = (S0 + (int64_t)L * nloc / G) * 64;
-        const int64_t rhi = std::min<int64_t>((S0 + (int64_t)(L + 1) * nloc / G) * 64, s->nrows);
-        for (int q = 0; q < N; ++q) {
-            if (q == r) continue;
+    auto owner = [&](int64_t row) {   // global logical workgroup owning a row (k_pk_window_dist's owner)
+        const int64_t sl = row >> 6;
+        int q = 0;
+        while (q + 1 < N && s->pd_split[q + 1] <= sl) ++q;
+        const int64_t S = s->pd_split[q + 1] - s->pd_split[q], tl = sl - s->pd_split[q];
+        const int64_t L = ((tl + 1) * G - 1) / S;
+        return (int64_t)q * G + (L < G ? L : G - 1);
+    };
+    std::vector<int32_t> pub((size_t)G * N * 2, -1);
+    for (int q = 0; q < N; ++q) {
+        if (q == r || need_hi[q] < need_lo[q]) continue;
+        const int64_t glo = owner(need_lo[q]), ghi = owner(need_hi[q]);
+        for (int L = 0; L < G; ++L) {
+            const int64_t Lg = (int64_t)r * G + L;
+            if (Lg < glo || Lg > ghi) continue;
+            const int64_t rlo = (S0 + (int64_t)L * nloc / G) * 64;
+            const int64_t rhi = std::min<int64_t>((S0 + (int64_t)(L + 1) * nloc / G) * 64, s->nrows);
             const int64_t lo = std::max<int64_t>(rlo, need_lo[q]), hi = std::min<int64_t>(rhi, need_hi[q] + 1);
-            if (lo < hi) {
-                pub[((size_t)L * N + q) * 2] = (int32_t)lo;
-                pub[((size_t)L * N + q) * 2 + 1] = (int32_t)hi;
-            }
+            pub[((size_t)L * N + q) * 2] = (int32_t)std::max<int64_t>(lo, 0);
+            pub[((size_t)L * N + q) * 2 + 1] = (int32_t)std::max<int64_t>(hi, std::max<int64_t>(lo, 0));
         }
     }
     if (!s->pd_pub) FEM_HIP(hipMalloc((void**)&s->pd_pub, sizeof(int32_t) * pub.size()));
     FEM_HIP(hipMemcpyAsync(s->pd_pub, pub.data(), sizeof(int32_t) * pub.size(), hipMemcpyHostToDevice, s->stream));
     FEM_HIP(hipStreamSynchronize(s->stream));
     s->pd_peers_ok = 1;
+    return FEM_OK;
+}
+
+int fem_pcg_dist_debug(fem_pcg* s, int which, int32_t* host_out, int64_t n) {
+    if (!s->pd) {
+        set_error("fem_pcg_dist_debug: not a distributed persistent context");
+        return FEM_EARG;
+    }
+    const int G = s->pk_grid, N = s->pd_nranks;
+    if (which == 0) {   // gather windows [G] lo, [G] hi (global workgroups), then the column window
+        FEM_HIP(hipMemcpyAsync(host_out, s->pk_win, sizeof(int32_t) * std::min<int64_t>(n, 2 * G + 2),
+                               hipMemcpyDeviceToHost, s->stream));
+    } else if (which == 1) {   // the u-flag of every global workgroup in this rank's comm block
+        for (int64_t i = 0; i < std::min<int64_t>(n, (int64_t)N * G); ++i)
+            FEM_HIP(hipMemcpyAsync(host_out + i, s->pd_block + s->pd_off_flag + i * sizeof(unsigned) * PK_LINE,
+                                   sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
+    } else if (which == 2) {   // pub [G][N][2]
+        FEM_HIP(hipMemcpyAsync(host_out, s->pd_pub, sizeof(int32_t) * std::min<int64_t>(n, (int64_t)G * N * 2),
+                               hipMemcpyDeviceToHost, s->stream));
+    } else if (which == 3) {   // the rank epoch lines
+        for (int64_t i = 0; i < std::min<int64_t>(n, N); ++i)
+            FEM_HIP(hipMemcpyAsync(host_out + i, s->pd_block + s->pd_off_rflag + i * sizeof(unsigned) * PK_LINE,
+                                   sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
+    } else if (which == 4) {   // local sync words: group counters, top replicas, give-up word
+        for (int64_t i = 0; i < std::min<int64_t>(n, 18); ++i)
+            FEM_HIP(hipMemcpyAsync(host_out + i, s->pk_sync + i * PK_LINE, sizeof(int32_t), hipMemcpyDeviceToHost,
+                                   s->stream));
+    }
+    FEM_HIP(hipStreamSynchronize(s->stream));
     return FEM_OK;
 }
 

@@ -67,12 +67,15 @@ __device__ __forceinline__ void pk_st(unsigned* p, unsigned v) {
 }
 
 // one lane spins until *p >= target; false on give-up (own or another spinner's)
+// the give-up word holds the site of the first give-up (diagnostics, reported by fem_pcg_poll as the iteration
+// count of a FEM_PCG_SYNC_TIMEOUT): 1 + 16 * epoch local grid barrier, 2 + 16 * epoch u-flag window, 3 + 16 * epoch
+// rank sums (DIST)
 __device__ __forceinline__ bool pk_wait_ge(const unsigned* p, unsigned target, unsigned* tmo) {
     for (unsigned spins = 0;; ++spins) {
         if (pk_ld(p) >= target) return true;
         if ((spins & 63) == 63 && pk_ld(tmo)) return false;
         if (spins >= PK_SPIN_LIMIT) {
-            pk_st(tmo, 1u);
+            pk_st(tmo, 1u + 16u * (target / NXCD));
             return false;
         }
         __builtin_amdgcn_s_sleep(2);
@@ -188,7 +191,8 @@ struct PkArgs {
     int rank, nranks;
     char* peer[PK_MAX_RANKS];
     int64_t off_flag, off_red, off_rflag;
-    const int32_t* pub;     // [G][nranks][2]: rows [lo, hi) of logical workgroup L gathered by rank Q (lo >= hi: none)
+    const int32_t* pub;     // [G][nranks][2]: rows [lo, hi) of logical workgroup L gathered by rank Q; lo < 0: Q
+                            // never waits on L (lo >= 0 with lo == hi: L raises its flag in Q, no rows)
     const double* b;        // init launch: r0 = b - A x0 over the own rows (x0 global-length, the same on every rank)
     int init;
 };
@@ -227,7 +231,7 @@ __device__ __forceinline__ bool pk_rank_sum(const PkArgs& a, int L, unsigned e, 
                 break;
             }
             if (spins >= 4 * PK_SPIN_LIMIT) {   // ranks start their launches up to milliseconds apart
-                pk_st(tmo, 1u);
+                pk_st(tmo, 3u + 16u * e);
                 okv = 0;
                 break;
             }
@@ -315,10 +319,10 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
     int s0, nsl;
     if (a.pack) {
         const int m = a.pack;   // <= MAXS (host)
-        const int sL0 = (int)((int64_t)L * a.nslices / G) + (DIST ? (int)a.sbase : 0);
+        const int sL0 = (int)((int64_t)L * a.nslices / G);
         const int nL = (int)((int64_t)(L + 1) * a.nslices / G) - sL0;
         const int lo = wv * m < nL ? wv * m : nL;
-        s0 = sL0 + lo;
+        s0 = sL0 + lo + (DIST ? (int)a.sbase : 0);   // DIST: this rank's slices start at global slice sbase
         nsl = nL - lo < m ? nL - lo : m;
     } else {
         const int64_t W = (int64_t)G * PK_WAVES;
@@ -342,7 +346,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
     bool ghost = false;                         // DIST: this workgroup gathers rows of other ranks
     if constexpr (DIST) {
         for (int q = 0; q < a.nranks; ++q)
-            if (q != a.rank && a.pub[(L * a.nranks + q) * 2] < a.pub[(L * a.nranks + q) * 2 + 1]) pubmask |= 1u << q;
+            if (q != a.rank && a.pub[(L * a.nranks + q) * 2] >= 0) pubmask |= 1u << q;
         ghost = a.win[L] < a.rank * G || a.win[G + L] >= (a.rank + 1) * G;
     }
 
@@ -461,7 +465,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
                                 break;
                             }
                             if (spins >= PK_SPIN_LIMIT) {
-                                pk_st(sy + PK_TMO, 1u);
+                                pk_st(sy + PK_TMO, 2u + 16u * e);
                                 ok = false;
                                 break;
                             }
@@ -732,6 +736,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
     if (L == 0 && threadIdx.x == 0) {
         if (fail) {
             status = FEM_PCG_SYNC_TIMEOUT;
+            stop_iter = (int)pk_ld(sy + PK_TMO);   // where the first give-up happened (see pk_wait_ge)
             halt = 1;
         }
         st->iter = it;

@@ -141,6 +141,12 @@ class RankRunner:
     def effective_schedule(self):
         return int(self.lib.fem_pcg_get_schedule(self.h))
 
+    def debug(self, which, n):
+        buf = (ctypes.c_int32 * n)()
+        with C.device_scope(self.device):
+            C.check(self.lib.fem_pcg_dist_debug(self.h, int(which), buf, int(n)), "fem_pcg_dist_debug")
+        return list(buf)
+
     def own_x(self):
         lo, hi = self.rs.lo, self.rs.hi
         return self.x[lo:hi]

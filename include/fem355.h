@@ -437,6 +437,10 @@ int fem_pcg_set_rows(fem_pcg* s, int nranks, int rank, const int64_t* slice_spli
 int fem_pcg_comm_block(fem_pcg* s, void** base, int64_t* bytes);
 int fem_pcg_col_window(fem_pcg* s, int64_t* lo, int64_t* hi);
 int fem_pcg_set_peers(fem_pcg* s, void* const* bases, const int64_t* need_lo, const int64_t* need_hi);
+/* [sync] diagnostics of a distributed persistent context into host_out[n]: which 0 = gather windows [G] first /
+ * [G] last global workgroup + the column window, 1 = u-flag of every global workgroup in this rank's comm block,
+ * 2 = publication table [G][nranks][2], 3 = rank epoch lines, 4 = local sync words (18 lines' first words) */
+int fem_pcg_dist_debug(fem_pcg* s, int which, int32_t* host_out, int64_t n);
 int fem_ipc_handle(void* ptr, char* out64);
 int fem_ipc_open(const char* h64, void** ptr);
 int fem_ipc_close(void* ptr);

@@ -3,7 +3,8 @@ comm blocks; dist_persist.py, pcg_persist.hpp DIST build), validated on ONE GPU:
 process on separate streams, sharing the CUs (EmulatedGroup) -- the same kernel and hand-off code as one process
 per GPU, with the comm blocks as plain device pointers instead of IPC mappings. Against the single-GPU persistent
 schedule: solutions within 1e-10 and iterations within +-1 (only the grouping of the partial sums differs: rank
-sums, then rank order), fixed-iteration iterates within 1e-12, chunk boundaries bit-identical."""
+sums, then rank order), fixed-iteration iterates within 1e-12, chunk boundaries bit-identical. At most 3 emulated
+ranks: each needs a hardware queue of its own to run concurrently (GPU_MAX_HW_QUEUES = 4 on the box)."""
 import pytest
 import torch
 
@@ -30,7 +31,7 @@ def _case(mesh, system, n, gpu, jitter=0.0):
     return c, t, f.reshape(-1).to(F64), mask, A, w
 
 
-@pytest.mark.parametrize("nranks,n,jitter", [(2, 24, 0.1), (4, 40, 0.0), (3, 30, 0.05)])
+@pytest.mark.parametrize("nranks,n,jitter", [(2, 24, 0.1), (2, 40, 0.0), (3, 30, 0.05)])
 def test_dist_persist_solve_matches_single_gpu(gpu, nranks, n, jitter):
     C, DP, mesh, system = _mods()
     c, t, b, mask, A, w = _case(mesh, system, n, gpu, jitter)
@@ -38,7 +39,6 @@ def test_dist_persist_solve_matches_single_gpu(gpu, nranks, n, jitter):
     r3 = A.pcg(b, w=w, tol=tol, max_iter=5000, schedule=3)
     grp = DP.EmulatedGroup(c, t, nranks, b, fixed_mask=mask, tol=tol)
     try:
-        assert all(rr.effective_schedule() == 3 for rr in grp.ranks) or True
         it, stt = grp.solve(max_iter=5000, chunk=97)
         assert stt == C.PCG_CONVERGED and r3.status == C.PCG_CONVERGED
         assert abs(it - r3.iterations) <= 1, (it, r3.iterations)
