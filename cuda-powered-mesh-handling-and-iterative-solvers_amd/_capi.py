@@ -117,6 +117,9 @@ SIGNATURES = {
     "fem_pcg_col_window": (_I, [_P, ctypes.POINTER(_L), ctypes.POINTER(_L)]),
     "fem_pcg_set_peers": (_I, [_P, _P, _P, _P]),
     "fem_pcg_dist_debug": (_I, [_P, _I, _P, _L]),
+    "fem_stream_create_cu": (_I, [_I, _I, ctypes.POINTER(_P)]),
+    "fem_stream_destroy": (_I, [_P]),
+    "fem_pcg_set_prof": (_I, [_P, _P]),
     "fem_ipc_handle": (_I, [_P, ctypes.c_char_p]),
     "fem_ipc_open": (_I, [ctypes.c_char_p, ctypes.POINTER(_P)]),
     "fem_ipc_close": (_I, [_P]),

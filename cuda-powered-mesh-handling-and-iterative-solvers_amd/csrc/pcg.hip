@@ -1468,6 +1468,7 @@ struct fem_pcg {
     int pd_peers_ok;
     int32_t* pd_pub;                      // [G][nranks][2] rows of each local workgroup gathered by each rank
     int pd_init_pending;                  // the next launch runs the distributed init (r0, u0, r0.u0)
+    unsigned long long* pd_prof;          // fem_pcg_set_prof: launches run the phase-clock build into this buffer
 };
 
 #define FEM_NCCL(call)                                                                         \
@@ -2558,6 +2559,7 @@ static int launch_persist(fem_pcg* s, int k, unsigned long long* prof) {
         a.pack = (int)((maxL + PK_WAVES - 1) / PK_WAVES);
     }
     void* args[] = {&a};
+    if (s->pd && !prof && s->pd_prof) a.prof = prof = s->pd_prof;
     const void* fn = s->pd ? persist_fn_dist(prof != nullptr, a.pack)
                            : persist_fn(prof != nullptr && !s->pk_ovf, (s->tune & FEM_TUNE_PK_SC1) != 0, s->pk_ovf != 0);
     // the grid spins on inter-workgroup flags, so all G workgroups must be resident together: one per CU is
@@ -3275,6 +3277,37 @@ int fem_pcg_dist_debug(fem_pcg* s, int which, int32_t* host_out, int64_t n) {
                                    s->stream));
     }
     FEM_HIP(hipStreamSynchronize(s->stream));
+    return FEM_OK;
+}
+
+int fem_stream_create_cu(int part, int nparts, void** stream) {
+    int dev = 0, ncu = 0;
+    FEM_HIP(hipGetDevice(&dev));
+    FEM_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    if (nparts < 1 || part < 0 || part >= nparts) {
+        set_error("fem_stream_create_cu: part %d of %d", part, nparts);
+        return FEM_EARG;
+    }
+    std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+    for (int cu = 0; cu < ncu; ++cu)
+        if (cu % nparts == part) mask[(size_t)cu / 32] |= 1u << (cu % 32);
+    hipStream_t st = nullptr;
+    FEM_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+    *stream = st;
+    return FEM_OK;
+}
+
+int fem_stream_destroy(void* stream) {
+    FEM_HIP(hipStreamDestroy(reinterpret_cast<hipStream_t>(stream)));
+    return FEM_OK;
+}
+
+int fem_pcg_set_prof(fem_pcg* s, unsigned long long* dev_buf) {
+    if (!s->pd) {
+        set_error("fem_pcg_set_prof: distributed persistent contexts only (single GPU: fem_pcg_persist_profile)");
+        return FEM_EARG;
+    }
+    s->pd_prof = dev_buf;
     return FEM_OK;
 }
 

@@ -147,6 +147,10 @@ class RankRunner:
             C.check(self.lib.fem_pcg_dist_debug(self.h, int(which), buf, int(n)), "fem_pcg_dist_debug")
         return list(buf)
 
+    def set_prof(self, buf):
+        with C.device_scope(self.device):
+            C.check(self.lib.fem_pcg_set_prof(self.h, C.ptr(buf)), "fem_pcg_set_prof")
+
     def own_x(self):
         lo, hi = self.rs.lo, self.rs.hi
         return self.x[lo:hi]
@@ -176,9 +180,19 @@ class EmulatedGroup:
         N = coords.shape[0]
         self.split = slice_split(N, nranks)
         self.ranks = []
+        self._raw_streams = []
+        lib = C.lib()
         for r in range(nranks):
+            # a CU-masked stream per rank: its own hardware queue and its own CUs, so the ranks' launches run side by
+            # side (plain streams may share a queue and then serialise: the first rank would wait for the second)
+            raw = ctypes.c_void_p()
+            with C.device_scope(dev):
+                C.check(lib.fem_stream_create_cu(r, nranks, ctypes.byref(raw)), "fem_stream_create_cu")
+            self._raw_streams.append(raw.value)
+            st = torch.cuda.ExternalStream(raw.value, device=dev)
             rs = assemble_rank(coords, elements, self.split, r, kind, E, nu, fixed_mask)
-            self.ranks.append(RankRunner(rs, b, self.split, r, nranks, tol=tol, mode=mode, grid=grid, x0=x0))
+            self.ranks.append(RankRunner(rs, b, self.split, r, nranks, tol=tol, mode=mode, grid=grid, x0=x0,
+                                         stream=st))
         torch.cuda.synchronize(dev)
         bases = [rr.block for rr in self.ranks]
         windows = [rr.col_window for rr in self.ranks]
@@ -224,3 +238,7 @@ class EmulatedGroup:
     def close(self):
         for rr in self.ranks:
             rr.close()
+        torch.cuda.synchronize()
+        for raw in self._raw_streams:
+            C.lib().fem_stream_destroy(ctypes.c_void_p(raw))
+        self._raw_streams = []

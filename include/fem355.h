@@ -441,6 +441,13 @@ int fem_pcg_set_peers(fem_pcg* s, void* const* bases, const int64_t* need_lo, co
  * [G] last global workgroup + the column window, 1 = u-flag of every global workgroup in this rank's comm block,
  * 2 = publication table [G][nranks][2], 3 = rank epoch lines, 4 = local sync words (18 lines' first words) */
 int fem_pcg_dist_debug(fem_pcg* s, int which, int32_t* host_out, int64_t n);
+/* [host] a stream whose kernels run only on the CUs with cu % nparts == part (hipExtStreamCreateWithCUMask: its own
+ * hardware queue) -- several emulated ranks of one process then run their persistent launches side by side */
+int fem_stream_create_cu(int part, int nparts, void** stream);
+int fem_stream_destroy(void* stream);
+/* distributed persistent contexts: every later launch runs the phase-clock build (pcg_persist.hpp PROF) into dev_buf
+ * ([G][8] phase sums, then [G][16] per-wave SpMV sums, as fem_pcg_persist_profile); NULL turns it off */
+int fem_pcg_set_prof(fem_pcg* s, unsigned long long* dev_buf);
 int fem_ipc_handle(void* ptr, char* out64);
 int fem_ipc_open(const char* h64, void** ptr);
 int fem_ipc_close(void* ptr);

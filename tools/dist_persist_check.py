@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--iters", type=int, nargs="+", default=[1, 5, 50])
     ap.add_argument("--rtol", type=float, default=1e-9)
     ap.add_argument("--time-iters", type=int, default=0)
+    ap.add_argument("--prof", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     c, t = mesh.kuhn_cube(a.n, device=dev)
@@ -84,6 +85,24 @@ def main():
             t0 = time.perf_counter()
             grp.iterate(a.time_iters)
             res["us_per_it"] = (time.perf_counter() - t0) / a.time_iters * 1e6
+            if a.prof:   # phase clocks of the distributed kernel (PROF build), per rank: mean / max over workgroups
+                G = 256 // P // 8 * 8
+                bufs = []
+                for rr in grp.ranks:
+                    buf = torch.zeros(G * 24, dtype=torch.int64, device=dev)
+                    rr.set_prof(buf)
+                    bufs.append(buf)
+                grp.iterate(a.time_iters)
+                phases = ("u_wait", "spmv", "block_sum", "barrier_ranksum", "step", "update_flag", "prologue",
+                          "epilogue")
+                prof = []
+                for buf in bufs:
+                    v = buf.cpu().to(torch.float64) / 2.4e3
+                    ph = v[: G * 8].view(G, 8)
+                    ph[:, :6] /= a.time_iters
+                    prof.append({n: [round(float(ph[:, i].mean()), 2), round(float(ph[:, i].max()), 2)]
+                                 for i, n in enumerate(phases)})
+                res["prof"] = prof
             grp.close()
         out[f"P{P}"] = res
         print(json.dumps(out), flush=True)
