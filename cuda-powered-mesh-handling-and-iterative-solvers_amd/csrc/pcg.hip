@@ -3145,7 +3145,7 @@ int fem_pcg_set_rows(fem_pcg* s, int nranks, int rank, const int64_t* slice_spli
     s->pd_off_flag = (int64_t)cdiv(sizeof(double) * (s->n + 2), 256) * 256;
     s->pd_off_red = s->pd_off_flag + (int64_t)nranks * G * line;
     s->pd_off_rflag = s->pd_off_red + 256;
-    s->pd_block_bytes = s->pd_off_rflag + PK_MAX_RANKS * line;
+    s->pd_block_bytes = s->pd_off_rflag + PK_MAX_RANKS * NXCD * line;   // [rank][XCD group] epoch lines
     FEM_HIP(hipMalloc((void**)&s->pd_block, (size_t)s->pd_block_bytes));
     FEM_HIP(hipMemsetAsync(s->pd_block, 0, (size_t)s->pd_block_bytes, s->stream));
     // the single-GPU persistent buffers for this grid, and the gather windows in global workgroup ids
@@ -3267,8 +3267,8 @@ int fem_pcg_dist_debug(fem_pcg* s, int which, int32_t* host_out, int64_t n) {
     } else if (which == 2) {   // pub [G][N][2]
         FEM_HIP(hipMemcpyAsync(host_out, s->pd_pub, sizeof(int32_t) * std::min<int64_t>(n, (int64_t)G * N * 2),
                                hipMemcpyDeviceToHost, s->stream));
-    } else if (which == 3) {   // the rank epoch lines
-        for (int64_t i = 0; i < std::min<int64_t>(n, N); ++i)
+    } else if (which == 3) {   // the rank epoch lines [rank][XCD group]
+        for (int64_t i = 0; i < std::min<int64_t>(n, (int64_t)N * NXCD); ++i)
             FEM_HIP(hipMemcpyAsync(host_out + i, s->pd_block + s->pd_off_rflag + i * sizeof(unsigned) * PK_LINE,
                                    sizeof(int32_t), hipMemcpyDeviceToHost, s->stream));
     } else if (which == 4) {   // local sync words: group counters, top replicas, give-up word

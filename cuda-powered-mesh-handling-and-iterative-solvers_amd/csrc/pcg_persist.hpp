@@ -197,20 +197,40 @@ struct PkArgs {
     int init;
 };
 
-// DIST: after the local grid barrier every workgroup holds this rank's sums (out[0] = d, out[1] = g); wave 0 of
-// logical workgroup 0 announces them to every rank (system-scope stores into each rank's comm block, a system
-// release, then the epoch line), and wave 0 of every workgroup waits for all ranks' epoch e and sums the ranks'
-// values in rank order 0..N-1 -- identical bits on every rank. Banked by epoch parity (a rank reaches epoch e + 2
-// only after every rank announced e + 1, i.e. after every reader of bank e is done with it).
-__device__ __forceinline__ bool pk_rank_sum(const PkArgs& a, int L, unsigned e, unsigned* tmo, double* out,
-                                            int* lds_ok) {
+// DIST grid barrier with the rank exchange folded in. Arrivals as in pk_barrier (group counter, the last of a group
+// adds to ONE top counter); the add on the top counter that returns e * 8 - 1 tells its workgroup that the whole
+// rank has arrived: its wave 0 alone sums the G partials (fixed order) and announces the rank's (d, g) to every
+// rank -- system-scope stores into bank e & 1 of each rank's comm block, a system release, then epoch e on the
+// rank's 8 replica lines there (one per XCD group: 32 pollers per line). Every workgroup's wave 0 waits for epoch e
+// from all ranks on its group's replicas and sums the ranks' pairs in rank order 0..N-1 (identical bits on every
+// rank). Banked by epoch parity: a rank announces e + 2 only after all ranks announced e + 1, i.e. after every
+// reader of bank e is done. The give-up word records 3 + 16 e.
+__device__ __forceinline__ bool pk_barrier_dist(const PkArgs& a, unsigned* sy, int grp, unsigned nper, unsigned e,
+                                                int* lds_ok, const double* pd, const double* pg, int G, double* out) {
     __syncthreads();
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
+        unsigned* tmo = sy + PK_TMO;
+        int last = 0;
+        if (lane == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned old = __hip_atomic_fetch_add(sy + PK_GRP + grp * PK_LINE, 1u, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+            if (old == e * nper - 1) {
+                const unsigned old2 = __hip_atomic_fetch_add(sy + PK_GEN, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                last = old2 == e * NXCD - 1;
+            }
+        }
+        last = __builtin_amdgcn_readfirstlane(last);
         const int bank = (int)(e & 1u);
-        int okv = 1;
-        if (L == 0) {
-            const double d = out[0], g = out[1];
+        if (last) {
+            double vd = 0.0, vg = 0.0;
+#pragma unroll 4
+            for (int i = lane; i < G; i += 64) {
+                vd += __hip_atomic_load(pd + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (pg) vg += __hip_atomic_load(pg + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            const double d = wave_sum(vd), g = wave_sum(vg);
             if (lane < a.nranks) {
                 double* red = reinterpret_cast<double*>(a.peer[lane] + a.off_red) + (bank * PK_MAX_RANKS + a.rank) * 2;
                 __hip_atomic_store(red, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -218,14 +238,18 @@ __device__ __forceinline__ bool pk_rank_sum(const PkArgs& a, int L, unsigned e, 
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane < a.nranks)
-                __hip_atomic_store(reinterpret_cast<unsigned*>(a.peer[lane] + a.off_rflag) + a.rank * PK_LINE, e,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (lane < a.nranks * NXCD)   // rank (lane / 8)'s replica (lane % 8) of this rank's epoch line
+                __hip_atomic_store(reinterpret_cast<unsigned*>(a.peer[lane / NXCD] + a.off_rflag) +
+                                       (a.rank * NXCD + lane % NXCD) * PK_LINE,
+                                   e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         const unsigned* rf = reinterpret_cast<const unsigned*>(a.peer[a.rank] + a.off_rflag);
+        int okv = 1;
         bool done = lane >= a.nranks;
         for (unsigned spins = 0; !__all(done); ++spins) {
-            if (!done) done = __hip_atomic_load(rf + lane * PK_LINE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= e;
+            if (!done)
+                done = __hip_atomic_load(rf + (lane * NXCD + grp) * PK_LINE, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_SYSTEM) >= e;
             if ((spins & 63) == 63 && pk_ld(tmo)) {
                 okv = 0;
                 break;
@@ -342,6 +366,8 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
     // u-flags: this rank's own lines (single GPU), or the comm block's lines of all ranks' workgroups (DIST)
     unsigned* uf = DIST ? reinterpret_cast<unsigned*>(a.peer[a.rank] + a.off_flag) : sy + PK_UFLAG;
     const int Lg = DIST ? a.rank * G + L : L;   // global logical workgroup
+    const int olo = DIST ? (int)(a.sbase * 64) : 0;                         // this rank's rows [olo, ohi)
+    const int ohi = DIST ? (int)((a.sbase + a.nslices) * 64 < a.nrows ? (a.sbase + a.nslices) * 64 : a.nrows) : 0;
     unsigned pubmask = 0;                       // DIST: ranks that gather rows of this workgroup
     bool ghost = false;                         // DIST: this workgroup gathers rows of other ranks
     if constexpr (DIST) {
@@ -427,8 +453,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
                 pk_st(uf + Lg * PK_LINE, e0);
                 pk_publish_flag(a, Lg, pubmask, e0);
             }
-            if (!pk_barrier(sy, grp, nper, e0, &lds_ok, pg0, nullptr, G, lds_dg) ||
-                !pk_rank_sum(a, L, e0, sy + PK_TMO, lds_dg, &lds_ok)) {
+            if (!pk_barrier_dist(a, sy, grp, nper, e0, &lds_ok, pg0, nullptr, G, lds_dg)) {
                 fail = true;
             } else {
                 g = lds_dg[0];
@@ -500,7 +525,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
     if (!rv) {                                                                                     \
         _Pragma("unroll") for (int j = 0; j < MAXS; ++j) {                                         \
             if (j < nreg) {                                                                        \
-                const double v = sell_row_pair<PK_U, MODE>(s0 + j, lane, slp, cop, vap, uvp);      \
+                const double v = sell_row_pair<PK_U, MODE>(s0 + j, lane, slp, cop, vap, uvp, olo, ohi); \
                 if (j < PK_VL) vl[j * 64] = v; else vv[j] = v;                                     \
             }                                                                                      \
             asm volatile("" ::: "memory");                                                         \
@@ -509,16 +534,17 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
         _Pragma("unroll") for (int jj = 0; jj < MAXS; ++jj) {                                      \
             const int j = MAXS - 1 - jj;                                                           \
             if (j < nreg) {                                                                        \
-                const double v = sell_row_pair<PK_U, MODE>(s0 + j, lane, slp, cop, vap, uvp);      \
+                const double v = sell_row_pair<PK_U, MODE>(s0 + j, lane, slp, cop, vap, uvp, olo, ohi); \
                 if (j < PK_VL) vl[j * 64] = v; else vv[j] = v;                                     \
             }                                                                                      \
             asm volatile("" ::: "memory");                                                         \
         }                                                                                          \
     }
-            // DIST: a workgroup whose gather window reaches other ranks reads u past this GPU's L2 (those rows
-            // arrive from other GPUs; the L2 may hold the previous iteration's copy)
+            // DIST: a workgroup whose gather window reaches other ranks reads the rows of other ranks past this GPU's
+            // L2 (they arrive from other GPUs; the L2 may hold the previous iteration's copy), its own rank's rows
+            // as usual (mode 3 picks per element)
             if (DIST && ghost) {
-                PK_SPMV(2)
+                PK_SPMV(3)
             } else {
                 PK_SPMV((GSC1 ? 1 : 0))
             }
@@ -549,15 +575,10 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
             const double dsum = pk_block_sum(dp, lds16);
             PK_MARK(2);
             if (threadIdx.x == 0) __hip_atomic_store(pd + L, dsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (!pk_barrier(sy, grp, nper, e, &lds_ok, pd, k > 0 ? pd + G : nullptr, G, lds_dg)) {
+            if (!(DIST ? pk_barrier_dist(a, sy, grp, nper, e, &lds_ok, pd, k > 0 ? pd + G : nullptr, G, lds_dg)
+                       : pk_barrier(sy, grp, nper, e, &lds_ok, pd, k > 0 ? pd + G : nullptr, G, lds_dg))) {
                 fail = true;
                 break;
-            }
-            if constexpr (DIST) {
-                if (!pk_rank_sum(a, L, e, sy + PK_TMO, lds_dg, &lds_ok)) {
-                    fail = true;
-                    break;
-                }
             }
             elast = e;
             const double d = lds_dg[0];
@@ -692,8 +713,9 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
     // ---- chunk end without a stop: one more barrier makes the last g partials visible; stop test of that g
     if (!fail && !halt && k == a.kmax && a.kmax > 0) {
         const unsigned e = ebase + (unsigned)a.kmax + 1;
-        bool okb = pk_barrier(sy, grp, nper, e, &lds_ok, a.part + (size_t)(a.kmax & 1) * 2 * G + G, nullptr, G, lds_dg);
-        if constexpr (DIST) okb = okb && pk_rank_sum(a, L, e, sy + PK_TMO, lds_dg, &lds_ok);
+        const double* pgl = a.part + (size_t)(a.kmax & 1) * 2 * G + G;
+        const bool okb = DIST ? pk_barrier_dist(a, sy, grp, nper, e, &lds_ok, pgl, nullptr, G, lds_dg)
+                              : pk_barrier(sy, grp, nper, e, &lds_ok, pgl, nullptr, G, lds_dg);
         if (!okb) {
             fail = true;
         } else {

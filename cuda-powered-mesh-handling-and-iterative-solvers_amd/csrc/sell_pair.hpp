@@ -38,11 +38,23 @@ __device__ __forceinline__ double ldx(const double* p) {
     else return *p;
 }
 
+// SC1 = 3: per element, 2 (system scope) for columns outside [own_lo, own_hi) -- rows another GPU wrote into this
+// GPU's memory, never cached here -- and 1 for the rest (this GPU's rows, L2-served)
+template <int SC1>
+__device__ __forceinline__ double ldx_col(const double* x, int col, int own_lo, int own_hi) {
+    if constexpr (SC1 == 3) {
+        if (col < own_lo || col >= own_hi) return ldx<2>(x + col);
+        return ldx<1>(x + col);
+    } else {
+        return ldx<SC1>(x + col);
+    }
+}
+
 // y_row (bs = 1) of one slice row in the paired layout; U pairs in flight
 template <int U, int SC1 = 0>
 __device__ __forceinline__ double sell_row_pair(int64_t s, int lane, const int64_t* __restrict__ slice_ptr,
                                                 const int16_t* __restrict__ cols, const double* __restrict__ vals,
-                                                const double* __restrict__ x) {
+                                                const double* __restrict__ x, int own_lo = 0, int own_hi = 0) {
     const int64_t p0 = slice_ptr[s];
     const int w = (int)((slice_ptr[s + 1] - p0) >> 6);
     const int np = w >> 1;
@@ -61,8 +73,8 @@ __device__ __forceinline__ double sell_row_pair(int64_t s, int lane, const int64
 #pragma unroll
         for (int j = 0; j < U; ++j) {
             const int lo = (int)(int16_t)(cc[j] & 0xffff), hi = (int)(int16_t)(cc[j] >> 16);
-            x0[j] = (j0 + j < np) ? ldx<SC1>(x + (base + lo)) : 0.0;
-            x1[j] = (j0 + j < np) ? ldx<SC1>(x + (base + hi)) : 0.0;
+            x0[j] = (j0 + j < np) ? ldx_col<SC1>(x, base + lo, own_lo, own_hi) : 0.0;
+            x1[j] = (j0 + j < np) ? ldx_col<SC1>(x, base + hi, own_lo, own_hi) : 0.0;
         }
 #pragma unroll
         for (int j = 0; j < U; ++j)
@@ -73,7 +85,7 @@ __device__ __forceinline__ double sell_row_pair(int64_t s, int lane, const int64
     }
     if (w & 1) {
         const int64_t t = p0 + (int64_t)np * 128 + lane;
-        acc += vals[t] * ldx<SC1>(x + (base + (int)cols[t]));
+        acc += vals[t] * ldx_col<SC1>(x, base + (int)cols[t], own_lo, own_hi);
     }
     return acc;
 }

@@ -176,7 +176,9 @@ class EmulatedGroup:
                  mode=C.MODE_PCG, x0=None):
         dev = coords.device
         ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-        grid = (ncu // nranks) // 8 * 8
+        # a multiple of 8 workgroups per rank within its CU-mask share (at 3+ ranks leave headroom: the masks are
+        # laid over the CU numbering, which need not split evenly into usable CUs)
+        grid = (ncu // nranks) // 8 * 8 if nranks <= 2 else int(ncu / nranks * 0.85) // 8 * 8
         N = coords.shape[0]
         self.split = slice_split(N, nranks)
         self.ranks = []
