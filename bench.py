@@ -60,6 +60,9 @@ def parse():
                          "(p2p), or one all-reduce over the global interface vector")
     ap.add_argument("--dist-fused", type=int, default=0,
                     help="N>1 single reduction: 1 = one launch per iteration (k_cg1_fused), 0 = update + SpMV kernels")
+    ap.add_argument("--dist-path", default="auto", choices=["auto", "persist", "rccl"],
+                    help="N>1: the persistent multi-GPU schedule (rows partitioned, in-kernel hand-offs over xGMI; "
+                         "Poisson; auto falls back to RCCL if its self-check fails) or the RCCL element partition")
     ap.add_argument("--dist-graph", type=int, default=50,
                     help="distributed path: capture k iterations (kernels + RCCL) per hipGraph, 0 = plain launches")
     return ap.parse_args()

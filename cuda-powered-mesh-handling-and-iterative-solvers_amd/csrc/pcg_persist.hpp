@@ -440,7 +440,6 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
                 const double gw = wave_sum(gp);
                 if (lane == 0) lds16[wv] = gw;
             }
-            if (pubmask) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             const unsigned e0 = ebase + 1;
@@ -451,7 +450,11 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
                 for (int i = 0; i < PK_WAVES; ++i) gsum += lds16[i];
                 __hip_atomic_store(pg0 + L, gsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 pk_st(uf + Lg * PK_LINE, e0);
-                pk_publish_flag(a, Lg, pubmask, e0);
+                if (pubmask) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    pk_publish_flag(a, Lg, pubmask, e0);
+                }
             }
             if (!pk_barrier_dist(a, sy, grp, nper, e0, &lds_ok, pg0, nullptr, G, lds_dg)) {
                 fail = true;
@@ -693,9 +696,6 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
                 const double gw = wave_sum(gp);
                 if (lane == 0) lds16[wv] = gw;
             }
-            if constexpr (DIST) {   // rows published to other GPUs: system release before the flags
-                if (pubmask) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-            }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave drains its u stores
             __syncthreads();
             if (threadIdx.x == 0) {
@@ -705,7 +705,13 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
                 __hip_atomic_store(a.part + (size_t)(bank ^ 1) * 2 * G + G + L, gsum, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
                 pk_st(uf + Lg * PK_LINE, e);
-                if constexpr (DIST) pk_publish_flag(a, Lg, pubmask, e);
+                if constexpr (DIST) {
+                    if (pubmask) {   // rows published to other GPUs (every wave drained them): one system release
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // for the XCD's L2, then the flags there
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        pk_publish_flag(a, Lg, pubmask, e);
+                    }
+                }
             }
             PK_MARK(5);
         }

@@ -417,10 +417,24 @@ def bench_main(a, metric):
     world = int(os.environ["WORLD_SIZE"])
     rank = int(os.environ["RANK"])
     local = int(os.environ.get("LOCAL_RANK", rank))
+    # FEM355_DIST_SAME_GPU=1: every rank on GPU 0, each on its own CU share (validates the multi-process path of
+    # the persistent schedule on a one-GPU box; RCCL refuses two ranks per GPU, so there is no RCCL fallback then)
+    same_gpu = os.environ.get("FEM355_DIST_SAME_GPU", "0") == "1"
+    if same_gpu:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     tdist.init_process_group("gloo", rank=rank, world_size=world)
     C.lib()
+    path = getattr(a, "dist_path", "auto")
+    if a.kind == "poisson" and path in ("auto", "persist"):
+        from . import dist_persist
+        if dist_persist.bench_persist(a, metric, rank, world, dev, tdist, same_gpu=same_gpu):
+            tdist.barrier()
+            tdist.destroy_process_group()
+            return
+        if same_gpu:
+            raise RuntimeError("persistent multi-GPU self-check failed (ranks on one GPU: no RCCL fallback)")
     comm = init_comm(rank, world)
 
     def barrier_sync():

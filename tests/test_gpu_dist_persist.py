@@ -3,8 +3,9 @@ comm blocks; dist_persist.py, pcg_persist.hpp DIST build), validated on ONE GPU:
 process on separate streams, sharing the CUs (EmulatedGroup) -- the same kernel and hand-off code as one process
 per GPU, with the comm blocks as plain device pointers instead of IPC mappings. Against the single-GPU persistent
 schedule: solutions within 1e-10 and iterations within +-1 (only the grouping of the partial sums differs: rank
-sums, then rank order), fixed-iteration iterates within 1e-12, chunk boundaries bit-identical. At most 3 emulated
-ranks: each needs a hardware queue of its own to run concurrently (GPU_MAX_HW_QUEUES = 4 on the box)."""
+sums, then rank order), fixed-iteration iterates within 1e-12, chunk boundaries bit-identical. Two emulated ranks:
+each gets a CU-masked stream (a hardware queue and half the CUs of its own); three shares of the 256 CUs did not
+always co-schedule on the box (a give-up, not a hang: every spin is bounded)."""
 import pytest
 import torch
 
@@ -31,7 +32,7 @@ def _case(mesh, system, n, gpu, jitter=0.0):
     return c, t, f.reshape(-1).to(F64), mask, A, w
 
 
-@pytest.mark.parametrize("nranks,n,jitter", [(2, 24, 0.1), (2, 40, 0.0), (3, 30, 0.05)])
+@pytest.mark.parametrize("nranks,n,jitter", [(2, 24, 0.1), (2, 40, 0.0), (2, 30, 0.05)])
 def test_dist_persist_solve_matches_single_gpu(gpu, nranks, n, jitter):
     C, DP, mesh, system = _mods()
     c, t, b, mask, A, w = _case(mesh, system, n, gpu, jitter)
