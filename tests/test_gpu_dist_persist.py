@@ -54,6 +54,7 @@ def test_dist_persist_fixed_iterations_and_chunks(gpu):
     run = system.PcgRunner(A, b, w, tol=0.0, schedule=3)
     run.start()
     run.iterate(40)
+    assert run.poll()[0] == 40   # (syncs the runner's stream)
     x1 = run.x.clone()
     run.close()
     xs = []
@@ -108,6 +109,7 @@ def test_dist_persist_10m_two_ranks(gpu):
     run = system.PcgRunner(A, b, w, tol=0.0, schedule=3)
     run.start()
     run.iterate(50)
+    assert run.poll()[0] == 50
     x1 = run.x.clone()
     run.close()
     del A
