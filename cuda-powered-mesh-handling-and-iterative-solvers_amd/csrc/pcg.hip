@@ -3146,7 +3146,10 @@ int fem_pcg_set_rows(fem_pcg* s, int nranks, int rank, const int64_t* slice_spli
     s->pd_off_red = s->pd_off_flag + (int64_t)nranks * G * line;
     s->pd_off_rflag = s->pd_off_red + 256;
     s->pd_block_bytes = s->pd_off_rflag + PK_MAX_RANKS * NXCD * line;   // [rank][XCD group] epoch lines
-    FEM_HIP(hipMalloc((void**)&s->pd_block, (size_t)s->pd_block_bytes));
+    if (s->tune & FEM_TUNE_DIST_FINE)   // fine-grained device memory: coherent for the other GPUs' accesses
+        FEM_HIP(hipExtMallocWithFlags((void**)&s->pd_block, (size_t)s->pd_block_bytes, hipDeviceMallocFinegrained));
+    else
+        FEM_HIP(hipMalloc((void**)&s->pd_block, (size_t)s->pd_block_bytes));
     FEM_HIP(hipMemsetAsync(s->pd_block, 0, (size_t)s->pd_block_bytes, s->stream));
     // the single-GPU persistent buffers for this grid, and the gather windows in global workgroup ids
     pool_free(s->pk_win, s->stream);

@@ -73,8 +73,10 @@ def assemble_rank(coords, elements, split, rank, kind="poisson", E=1.0, nu=0.0, 
 class RankRunner:
     """One rank's persistent PCG context over its rows of the global system (vectors global-length)."""
 
+    TUNE_DEFAULT, TUNE_DIST_FINE = 1 | 2 | 4 | 8, 64
+
     def __init__(self, rs: RankSetup, b, split, rank, nranks, tol=0.0, mode=C.MODE_PCG, eps=1e-30, grid=0,
-                 stream=None, x0=None):
+                 stream=None, x0=None, fine=False):
         self.lib = C.lib()
         A = rs.A
         self.A, self.rs, self.rank, self.nranks = A, rs, rank, nranks
@@ -92,6 +94,9 @@ class RankRunner:
                                             None, 0, ctypes.c_void_p(self.stream.cuda_stream), ctypes.byref(self.h)),
                     "fem_pcg_create")
             A.attach_cols16(self.h)
+            if fine:   # comm block in fine-grained memory (the fallback variant for the real multi-GPU transport)
+                C.check(self.lib.fem_pcg_set_tuning(self.h, self.TUNE_DEFAULT | self.TUNE_DIST_FINE),
+                        "fem_pcg_set_tuning")
             sp = (ctypes.c_int64 * (nranks + 1))(*split)
             C.check(self.lib.fem_pcg_set_rows(self.h, nranks, rank, sp, int(grid)), "fem_pcg_set_rows")
             base, nbytes = ctypes.c_void_p(), ctypes.c_int64()
@@ -173,7 +178,7 @@ class EmulatedGroup:
     launches run concurrently; the comm blocks are plain device pointers (no IPC)."""
 
     def __init__(self, coords, elements, nranks, b, fixed_mask=None, kind="poisson", E=1.0, nu=0.0, tol=0.0,
-                 mode=C.MODE_PCG, x0=None):
+                 mode=C.MODE_PCG, x0=None, fine=False):
         dev = coords.device
         ncu = torch.cuda.get_device_properties(dev).multi_processor_count
         # a multiple of 8 workgroups per rank within its CU-mask share (at 3+ ranks leave headroom: the masks are
@@ -194,7 +199,7 @@ class EmulatedGroup:
             st = torch.cuda.ExternalStream(raw.value, device=dev)
             rs = assemble_rank(coords, elements, self.split, r, kind, E, nu, fixed_mask)
             self.ranks.append(RankRunner(rs, b, self.split, r, nranks, tol=tol, mode=mode, grid=grid, x0=x0,
-                                         stream=st))
+                                         stream=st, fine=fine))
         torch.cuda.synchronize(dev)
         bases = [rr.block for rr in self.ranks]
         windows = [rr.col_window for rr in self.ranks]
@@ -313,6 +318,8 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False):
     def stream():
         return torch.cuda.ExternalStream(raw_stream, device=dev) if raw_stream else torch.cuda.Stream(device=dev)
 
+    fine = False   # comm blocks from hipMalloc first; fine-grained memory if that fails the self-check
+
     def solve(coords, tets, b, gmask, rtol, max_iter=20000, chunk=8192):
         N = coords.shape[0]
         split = slice_split(N, world)
@@ -320,7 +327,7 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False):
         lo, hi = rs.lo, rs.hi
         bz = tsum(float(torch.dot(b[lo:hi], (rs.w * b)[lo:hi])))
         tol = rtol * bz ** 0.5
-        run = RankRunner(rs, b, split, rank, world, tol=tol, grid=grid, stream=stream())
+        run = RankRunner(rs, b, split, rank, world, tol=tol, grid=grid, stream=stream(), fine=fine)
         opened = connect(run, tdist, rank, world)
         barrier_sync()
         t0 = time.perf_counter()
@@ -363,36 +370,44 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False):
     barrier_sync()
     t_asm = tmax(time.perf_counter() - t0)
     del rs
-    rs, x_own, it, stt, t_solve, split = solve(coords, tets, b, gmask, a.rtol)
-
     # self-check against the single-GPU persistent solve on rank 0's GPU (the iterates may differ only by the
-    # grouping of the partial sums): a mapping or coherence problem of the real transport shows up here
-    parts = [None] * world
-    tdist.all_gather_object(parts, (rs.lo, rs.hi, x_own.cpu()))
-    ok, why = 1, ""
+    # grouping of the partial sums): a mapping or coherence problem of the real transport shows up here. First
+    # with the comm blocks in hipMalloc memory, then in fine-grained memory; then the caller falls back to RCCL.
+    ref_x = None
     if rank == 0:
-        x = torch.empty(N, dtype=F64)
-        for lo, hi, xp in parts:
-            x[lo:hi] = xp
         from . import system as _system
         A = _system.assemble_tet4_system(coords, tets, "poisson", 1.0, 0.0)
         w = A.jacobi(gmask)
         tol = a.rtol * float(torch.sqrt(torch.dot(b, w * b)))
         ref = A.pcg(b, w=w, tol=tol, max_iter=20000, schedule=3)
-        err = float((x - ref.x.cpu()).abs().max() / ref.x.abs().max().cpu())
-        ok = int(stt == C.PCG_CONVERGED and ref.status == C.PCG_CONVERGED and abs(it - ref.iterations) <= 1
-                 and err < 1e-10)
-        why = f"status {stt} / {ref.status}, iterations {it} / {ref.iterations}, x rel diff {err:.3e}"
+        ref_x, ref_it, ref_st = ref.x.cpu(), ref.iterations, ref.status
         del A, w, ref
-    verdict = [ok, why]
-    tdist.broadcast_object_list(verdict, src=0)
+    verdict = [0, "not run"]
+    for attempt in ("coarse-grained", "fine-grained"):
+        fine = attempt == "fine-grained"
+        rs, x_own, it, stt, t_solve, split = solve(coords, tets, b, gmask, a.rtol)
+        parts = [None] * world
+        tdist.all_gather_object(parts, (rs.lo, rs.hi, x_own.cpu()))
+        ok, why = 1, ""
+        if rank == 0:
+            x = torch.empty(N, dtype=F64)
+            for lo, hi, xp in parts:
+                x[lo:hi] = xp
+            err = float((x - ref_x).abs().max() / ref_x.abs().max())
+            ok = int(stt == C.PCG_CONVERGED and ref_st == C.PCG_CONVERGED and abs(it - ref_it) <= 1 and err < 1e-10)
+            why = f"{attempt} comm blocks: status {stt} / {ref_st}, iterations {it} / {ref_it}, x rel diff {err:.3e}"
+        verdict = [ok, why]
+        tdist.broadcast_object_list(verdict, src=0)
+        if verdict[0]:
+            break
+        print(f"[rank {rank}] persistent multi-GPU schedule failed its self-check ({verdict[1]})", file=sys.stderr,
+              flush=True)
     if not verdict[0]:
-        print(f"[rank {rank}] persistent multi-GPU schedule failed its self-check ({verdict[1]}); "
-              "measuring the RCCL path instead", file=sys.stderr, flush=True)
+        print(f"[rank {rank}] measuring the RCCL path instead", file=sys.stderr, flush=True)
         return False
 
     # fixed-iteration timing: W warm-up steps, then exactly K steps as one launch per rank, max over ranks
-    run = RankRunner(rs, b, split, rank, world, tol=0.0, grid=grid, stream=stream())
+    run = RankRunner(rs, b, split, rank, world, tol=0.0, grid=grid, stream=stream(), fine=fine)
     opened = connect(run, tdist, rank, world)
     barrier_sync()
     run.start()

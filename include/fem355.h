@@ -382,7 +382,10 @@ int fem_enforce_constraints(double* x, double* r, int64_t n, int order, int64_t 
  * the next sweep: 67 -> 57 us per SpMV on the 10M Poisson matrix. Results depend on the flags only through the
  * order of the per-block p.q partials (deterministic for a given flag set). */
 enum { FEM_TUNE_REVERSE = 1, FEM_TUNE_PAIR = 2, FEM_TUNE_PK_SC1 = 4, FEM_TUNE_PK_PACK = 8, FEM_TUNE_C1F = 16,
-       FEM_TUNE_PK_COOP = 32 };
+       FEM_TUNE_PK_COOP = 32, FEM_TUNE_DIST_FINE = 64 };
+/* FEM_TUNE_DIST_FINE (set before fem_pcg_set_rows): the distributed persistent comm block (u, flags, rank sums) in
+ * fine-grained device memory (hipDeviceMallocFinegrained) instead of hipMalloc's coarse-grained memory -- the
+ * variant bench.py tries when the coarse-grained one fails its self-check on a multi-GPU node. */
 /* FEM_TUNE_PK_COOP: persistent schedule — every launch is a hipLaunchCooperativeKernel (the runtime guarantees that
  * all workgroups are resident at once, or fails the launch). fem_pcg_solve always launches cooperatively and, should
  * a launch still end with FEM_PCG_SYNC_TIMEOUT, re-solves from the saved x0 on the deferred schedule; without the

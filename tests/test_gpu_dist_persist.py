@@ -32,13 +32,14 @@ def _case(mesh, system, n, gpu, jitter=0.0):
     return c, t, f.reshape(-1).to(F64), mask, A, w
 
 
-@pytest.mark.parametrize("nranks,n,jitter", [(2, 24, 0.1), (2, 40, 0.0), (2, 30, 0.05)])
-def test_dist_persist_solve_matches_single_gpu(gpu, nranks, n, jitter):
+@pytest.mark.parametrize("nranks,n,jitter,fine", [(2, 24, 0.1, False), (2, 40, 0.0, False), (2, 30, 0.05, True)])
+def test_dist_persist_solve_matches_single_gpu(gpu, nranks, n, jitter, fine):
+    """fine: the comm blocks in fine-grained device memory (bench.py's second attempt on a multi-GPU node)."""
     C, DP, mesh, system = _mods()
     c, t, b, mask, A, w = _case(mesh, system, n, gpu, jitter)
     tol = 1e-9 * float(torch.sqrt(torch.dot(b, w * b)))
     r3 = A.pcg(b, w=w, tol=tol, max_iter=5000, schedule=3)
-    grp = DP.EmulatedGroup(c, t, nranks, b, fixed_mask=mask, tol=tol)
+    grp = DP.EmulatedGroup(c, t, nranks, b, fixed_mask=mask, tol=tol, fine=fine)
     try:
         it, stt = grp.solve(max_iter=5000, chunk=97)
         assert stt == C.PCG_CONVERGED and r3.status == C.PCG_CONVERGED
