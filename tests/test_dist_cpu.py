@@ -175,3 +175,24 @@ def test_p2p_maps_sum_like_the_allreduce(P, bs):
             for r in range(P):
                 ref += float(pairs[r, c])
             assert acc == ref
+
+
+def test_row_partition_helpers():
+    """dist_persist's row partition (host logic): contiguous slice ranges within one slice of each other, covering
+    every row once; a rank's elements are exactly those touching its rows."""
+    import torch
+    from fem355 import dist_persist as DP, mesh
+    for n_rows, P in ((1000, 2), (64 * 27000, 8), (65, 1), (64 * 8 + 3, 8)):
+        sp = DP.slice_split(n_rows, P)
+        assert sp[0] == 0 and sp[-1] == (n_rows + 63) // 64 and len(sp) == P + 1
+        sizes = [sp[i + 1] - sp[i] for i in range(P)]
+        assert min(sizes) >= 1 and max(sizes) - min(sizes) <= 1
+        rows = [DP.rank_rows(n_rows, sp, r) for r in range(P)]
+        assert rows[0][0] == 0 and rows[-1][1] == n_rows
+        assert all(rows[i][1] == rows[i + 1][0] for i in range(P - 1))
+    c, t = mesh.kuhn_cube(5)
+    sp = DP.slice_split(c.shape[0], 2)
+    lo, hi = DP.rank_rows(c.shape[0], sp, 1)
+    el = DP.rank_elements(t, lo, hi)
+    touch = ((t >= lo) & (t < hi)).any(1)
+    assert el.shape[0] == int(touch.sum()) and torch.equal(el, t[touch])
