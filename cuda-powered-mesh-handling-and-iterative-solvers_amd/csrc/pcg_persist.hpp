@@ -395,14 +395,15 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
         pp[j] = on ? a.p[row] : 0.0;
         ss[j] = on ? a.s[row] : 0.0;
         vv[j] = 0.0;
-        if (j < PK_VL) vl[j * 64] = 0.0;
         xl[j * 64] = on ? a.x[row] : 0.0;
+        if (j < PK_VL) vl[j * 64] = 0.0;
         const double wj = on ? a.w[row] : 0.0;
         wl[j * 64] = wj;
         uo[j] = wj * rr[j];   // u = w r is how every u was formed (k_cg1_init, the update): bit-identical, no load
     }
     const int wlo = a.win[L], whi = a.win[G + L];
     bool fail = false;
+    bool st_loaded = !halt;   // the state is on chip and may have changed (nothing to store after a halt)
     int k = 0;
     if constexpr (DIST) {
         // first launch of a distributed solve: r0 = b - A x0 over the own rows (x0 global-length, identical on every
@@ -426,6 +427,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
                     rr[j] = rv;
                     pp[j] = 0.0;
                     ss[j] = 0.0;
+                    xl[j * 64] = on ? a.x[row] : 0.0;
                     const double ui = wj * rv;
                     uo[j] = ui;
                     gp += rv * ui;
@@ -456,6 +458,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
                     pk_publish_flag(a, Lg, pubmask, e0);
                 }
             }
+            st_loaded = true;
             if (!pk_barrier_dist(a, sy, grp, nper, e0, &lds_ok, pg0, nullptr, G, lds_dg)) {
                 fail = true;
             } else {
@@ -716,6 +719,23 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
             PK_MARK(5);
         }
     }
+    // ---- state back to memory (u is already there; nothing to store when no iteration ran). The chunk-end barrier
+    // below changes none of it, so every wave but wave 0 (which arrives for its workgroup after draining its own
+    // stores) writes it before the barrier and the traffic drains under the barrier's latency
+    auto store_state = [&]() {
+        if (!st_loaded) return;
+#pragma unroll
+        for (int j = 0; j < MAXS; ++j) {
+            if (PK_ON(j)) {
+                const unsigned row = rb + 64u * j;
+                a.r[row] = rr[j];
+                a.p[row] = pp[j];
+                a.s[row] = ss[j];
+                a.x[row] = xl[j * 64];
+            }
+        }
+    };
+    if (wv != 0) store_state();
     // ---- chunk end without a stop: one more barrier makes the last g partials visible; stop test of that g
     if (!fail && !halt && k == a.kmax && a.kmax > 0) {
         const unsigned e = ebase + (unsigned)a.kmax + 1;
@@ -742,17 +762,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
             }
         }
     }
-    // ---- state back to memory (u is already there)
-#pragma unroll
-    for (int j = 0; j < MAXS; ++j) {
-        if (PK_ON(j)) {
-            const unsigned row = rb + 64u * j;
-            a.r[row] = rr[j];
-            a.p[row] = pp[j];
-            a.s[row] = ss[j];
-            a.x[row] = xl[j * 64];
-        }
-    }
+    if (wv == 0) store_state();
     if constexpr (PROF) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
