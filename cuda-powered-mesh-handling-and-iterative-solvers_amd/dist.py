@@ -429,12 +429,17 @@ def bench_main(a, metric):
     path = getattr(a, "dist_path", "auto")
     if a.kind == "poisson" and path in ("auto", "persist"):
         from . import dist_persist
-        if dist_persist.bench_persist(a, metric, rank, world, dev, tdist, same_gpu=same_gpu):
+        try:
+            done = dist_persist.bench_persist(a, metric, rank, world, dev, tdist, same_gpu=same_gpu)
+        except C.FemError as e:   # raised on every rank alike (dist_persist.connect agrees before raising)
+            print(f"[rank {rank}] persistent multi-GPU schedule unavailable: {e}", file=sys.stderr, flush=True)
+            done = False
+        if done:
             tdist.barrier()
             tdist.destroy_process_group()
             return
-        if same_gpu:
-            raise RuntimeError("persistent multi-GPU self-check failed (ranks on one GPU: no RCCL fallback)")
+        if same_gpu or path == "persist":
+            raise RuntimeError("persistent multi-GPU schedule failed (no RCCL fallback requested / possible)")
     comm = init_comm(rank, world)
 
     def barrier_sync():

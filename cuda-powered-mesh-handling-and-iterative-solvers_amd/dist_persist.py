@@ -259,16 +259,25 @@ def connect(run: RankRunner, tdist, rank: int, world: int):
     allv = [None] * world
     tdist.all_gather_object(allv, mine)
     lib = C.lib()
-    bases, opened = [], []
+    bases, opened, err = [], [], ""
     with C.device_scope(run.device):
         for q, (h, _) in enumerate(allv):
             if q == rank:
                 bases.append(run.block)
                 continue
             p = ctypes.c_void_p()
-            C.check(lib.fem_ipc_open(h, ctypes.byref(p)), "fem_ipc_open")
+            rc = lib.fem_ipc_open(h, ctypes.byref(p))
+            if rc != C.FEM_OK:   # e.g. no peer access between these GPUs
+                err = f"rank {rank}: fem_ipc_open of rank {q}'s block: {(lib.fem_last_error() or b'').decode()}"
+                break
             bases.append(p.value)
             opened.append(p.value)
+    # every rank learns whether every rank could map every block, so they all leave (or all stay) together
+    fail = torch.tensor([1 if err else 0], dtype=torch.int32)
+    tdist.all_reduce(fail, op=tdist.ReduceOp.MAX)
+    if int(fail[0]):
+        disconnect(opened, run.device)
+        raise C.FemError(err or "another rank could not map the comm blocks")
     run.set_peers(bases, [w for _, w in allv])
     return opened
 
