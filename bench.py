@@ -166,6 +166,7 @@ def main():
     if a.graph:
         run.use_graph(a.graph)
     persist = run.effective_schedule() == system.SCHED_PERSIST
+    n_uni, n_sl, idx_total = run.uniform_slices()
     # the W warm-up steps go through the same launch path as the timed steps (persistent: one launch, events of the
     # context created here rather than next to the timed launch)
     if persist and a.warmup > 0:
@@ -188,7 +189,9 @@ def main():
     # per launch of the measured kernel: one SpMV (3-kernel / deferred) or one whole iteration (persistent: the
     # matrix, the u gather and the u store are all it moves; r, p, s, x, w stay in registers and LDS)
     spmv_ms = ms[0] / max(cnt[0], 1)
-    alg = A.algorithmic_bytes_spmv()
+    # column-index bytes of the stored format: slice-uniform slices read one delta list per slice (persistent
+    # schedule), the others 2 (int16) or 4 bytes per entry incl. padding
+    alg = A.algorithmic_bytes_spmv(index_total=idx_total if (persist and n_uni) else None)
     achieved = alg / (spmv_ms * 1e-3) / 1e9
     ceiling = system.stream_ceiling(dev)
     workload_key = f"kuhn{a.n}_{a.kind}"
@@ -206,7 +209,8 @@ def main():
         "dtype": "f64",
         "data": "synthetic",
         "config": {"workload": f"{M:,}-tet P1 {a.kind} Kuhn cube n={a.n}, Jacobi-PCG fixed iterations",
-                   "tets": M, "nodes": N, "dofs": A.n, "nnz_blocks": A.g.nnz, "format": "SELL-64 fp64 values, " + ("int16 column deltas" if A.use16 else "int32 cols"),
+                   "tets": M, "nodes": N, "dofs": A.n, "nnz_blocks": A.g.nnz, "format": "SELL-64 fp64 values, " + ("int16 column deltas" if A.use16 else "int32 cols")
+                   + (f", slice-uniform deltas in {n_uni} of {n_sl} slices" if (persist and n_uni) else ""),
                    "parallelism": "single GPU"},
         "dofs_per_s": A.n / (t_asm + t_solve),
         "assembly_ms": t_asm * 1e3,

@@ -1399,6 +1399,8 @@ struct fem_pcg {
     int paired;             // the SpMV reads pvals / pcols16 (lane-paired copy, refreshed by fem_pcg_start)
     double* pvals;
     int16_t* pcols16;
+    int32_t* puoff;         // FEM_TUNE_PK_UNI (bs = 1): per-slice offset into pucol, -1 = per-lane deltas
+    int16_t* pucol;
     Constraints con;
     // owned device memory
     double* r;
@@ -2272,7 +2274,7 @@ int fem_pcg_create(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_
         return FEM_EARG;
     }
     fem_pcg* s = new fem_pcg();
-    s->tune = FEM_TUNE_REVERSE | FEM_TUNE_PAIR | FEM_TUNE_PK_SC1 | FEM_TUNE_PK_PACK;
+    s->tune = FEM_TUNE_REVERSE | FEM_TUNE_PAIR | FEM_TUNE_PK_SC1 | FEM_TUNE_PK_PACK | FEM_TUNE_PK_UNI;
     s->nrows = nrows;
     s->bs = bs;
     s->nslices = cdiv(nrows, 64);
@@ -2368,6 +2370,33 @@ int fem_pcg_get_schedule(fem_pcg* s) {
     if (s->persist) return 3;
     if (s->fused) return 1;
     return s->deferred ? 2 : 0;
+}
+
+int fem_pcg_uniform_slices(fem_pcg* s, int64_t* uniform, int64_t* nslices, int64_t* index_bytes) {
+    *uniform = 0;
+    *nslices = s->nslices;
+    *index_bytes = 0;
+    if (s->nslices == 0) return FEM_OK;
+    std::vector<int64_t> sp((size_t)s->nslices + 1);
+    std::vector<int32_t> h((size_t)s->nslices, -1);
+    FEM_HIP(hipMemcpyAsync(sp.data(), s->slice_ptr, sizeof(int64_t) * sp.size(), hipMemcpyDeviceToHost, s->stream));
+    const bool uni = s->paired && s->puoff && (s->tune & FEM_TUNE_PK_UNI) && s->bs == 1;
+    if (uni) FEM_HIP(hipMemcpyAsync(h.data(), s->puoff, sizeof(int32_t) * h.size(), hipMemcpyDeviceToHost, s->stream));
+    FEM_HIP(hipStreamSynchronize(s->stream));
+    const int64_t idx = s->cols16 ? 2 : 4;
+    int64_t c = 0, ib = 0;
+    for (int64_t i = 0; i < s->nslices; ++i) {
+        const int64_t wdt = (sp[i + 1] - sp[i]) / 64;
+        if (h[i] >= 0) {
+            ++c;
+            ib += 2 * ((wdt + 1) & ~int64_t(1));
+        } else {
+            ib += idx * 64 * wdt;
+        }
+    }
+    *uniform = c;
+    *index_bytes = ib;
+    return FEM_OK;
 }
 
 static size_t pk_sync_words(int G) { return (size_t)(18 + G) * PK_LINE; }
@@ -2513,6 +2542,9 @@ static int launch_persist(fem_pcg* s, int k, unsigned long long* prof) {
     a.slice_ptr = s->slice_ptr;
     a.cols = s->pcols16;
     a.vals = s->pvals;
+    const bool uni = (s->tune & FEM_TUNE_PK_UNI) && s->puoff;
+    a.uoff = uni ? s->puoff : nullptr;
+    a.ucol = uni ? s->pucol : nullptr;
     a.x = s->x;
     a.r = s->r;
     a.p = s->p0;
@@ -2620,6 +2652,17 @@ static int refresh_pairing(fem_pcg* s) {
                        s->slice_ptr, s->vals, s->cols16, s->pvals, s->pcols16);
     FEM_LAUNCHED();
     s->paired = 1;
+    // slice-uniform deltas (sell_pair.hpp): read by the persistent schedule; the rewritten paired copy stays valid
+    // for every other reader
+    if ((s->tune & FEM_TUNE_PK_UNI) && 2 * (ent / 64) + 2 < (int64_t)INT32_MAX) {
+        if (!s->puoff) {
+            FEM_HIP(pool_alloc((void**)&s->puoff, sizeof(int32_t) * (size_t)s->nslices, s->stream, true));
+            FEM_HIP(pool_alloc((void**)&s->pucol, sizeof(int16_t) * (size_t)(2 * (ent / 64) + 2), s->stream, true));
+        }
+        hipLaunchKernelGGL(k_sell_uniform, dim3((unsigned)cdiv(s->nslices, 4)), dim3(256), 0, s->stream, s->nslices,
+                           s->nrows, s->slice_ptr, s->vals, s->cols16, s->pvals, s->pcols16, s->pucol, s->puoff);
+        FEM_LAUNCHED();
+    }
     return FEM_OK;
 }
 
@@ -3360,6 +3403,8 @@ void fem_pcg_destroy(fem_pcg* s) {
     if (s->con.tmp) (void)hipFree(s->con.tmp);
     pool_free(s->pvals, s->stream);
     pool_free(s->pcols16, s->stream);
+    pool_free(s->puoff, s->stream);
+    pool_free(s->pucol, s->stream);
     pool_free(s->pk_win, s->stream);
     pool_free(s->pk_part, s->stream);
     pool_free(s->pk_sync, s->stream);

@@ -163,6 +163,8 @@ struct PkArgs {
     const int64_t* slice_ptr;
     const int16_t* cols;    // lane-paired copy (sell_pair.hpp)
     const double* vals;
+    const int32_t* uoff;    // slice-uniform deltas (k_sell_uniform; nullptr: per-lane deltas everywhere)
+    const int16_t* ucol;
     double* x;
     double* r;
     double* p;
@@ -418,7 +420,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
 #pragma unroll
             for (int j = 0; j < MAXS; ++j) {
                 if (j < nreg) {
-                    const double q = sell_row_pair<PK_U, 0>(s0 + j, lane, slp, cop, vap, xvp);
+                    const double q = sell_row_pair<PK_U, 0>(s0 + j, lane, slp, cop, vap, xvp, 0, 0, a.uoff, a.ucol);
                     const unsigned row = rb + 64u * j;
                     const bool on = PK_ON(j);
                     double rv = on ? a.b[row] - q : 0.0;
@@ -527,11 +529,13 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
             const int16_t* cop = pk_launder(a.cols);
             const double* vap = pk_launder(a.vals);
             const double* uvp = pk_launder(a.u);
+            const int32_t* uop = a.uoff ? pk_launder(a.uoff) : nullptr;
+            const int16_t* ucp = a.uoff ? pk_launder(a.ucol) : nullptr;
 #define PK_SPMV(MODE)                                                                              \
     if (!rv) {                                                                                     \
         _Pragma("unroll") for (int j = 0; j < MAXS; ++j) {                                         \
             if (j < nreg) {                                                                        \
-                const double v = sell_row_pair<PK_U, MODE>(s0 + j, lane, slp, cop, vap, uvp, olo, ohi); \
+                const double v = sell_row_pair<PK_U, MODE>(s0 + j, lane, slp, cop, vap, uvp, olo, ohi, uop, ucp); \
                 if (j < PK_VL) vl[j * 64] = v; else vv[j] = v;                                     \
             }                                                                                      \
             asm volatile("" ::: "memory");                                                         \
@@ -540,7 +544,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
         _Pragma("unroll") for (int jj = 0; jj < MAXS; ++jj) {                                      \
             const int j = MAXS - 1 - jj;                                                           \
             if (j < nreg) {                                                                        \
-                const double v = sell_row_pair<PK_U, MODE>(s0 + j, lane, slp, cop, vap, uvp, olo, ohi); \
+                const double v = sell_row_pair<PK_U, MODE>(s0 + j, lane, slp, cop, vap, uvp, olo, ohi, uop, ucp); \
                 if (j < PK_VL) vl[j * 64] = v; else vv[j] = v;                                     \
             }                                                                                      \
             asm volatile("" ::: "memory");                                                         \
@@ -566,7 +570,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
                 __builtin_amdgcn_sched_barrier(0);
                 for (int q = 0; q < nov; ++q) {
                     const int sq = s0 + MAXS + q;
-                    const double v = sell_row_pair<PK_U, GSC1>(sq, lane, slp, cop, vap, uvp);
+                    const double v = sell_row_pair<PK_U, GSC1>(sq, lane, slp, cop, vap, uvp, 0, 0, uop, ucp);
                     const int row = sq * 64 + lane;
                     if (row < nrows) {
                         a.v[row] = v;

@@ -50,24 +50,112 @@ __device__ __forceinline__ double ldx_col(const double* x, int col, int own_lo, 
     }
 }
 
-// y_row (bs = 1) of one slice row in the paired layout; U pairs in flight
-template <int U, int SC1 = 0>
-__device__ __forceinline__ double sell_row_pair(int64_t s, int lane, const int64_t* __restrict__ slice_ptr,
-                                                const int16_t* __restrict__ cols, const double* __restrict__ vals,
-                                                const double* __restrict__ x, int own_lo = 0, int own_hi = 0) {
+// Slice-uniform column deltas (FEM_TUNE_PK_UNI). When the 64 rows of a slice take their columns at the same
+// offsets from the row (every row's deltas a subset of one sorted list of `w` deltas -- FEM meshes numbered along a
+// structured sweep, e.g. every slice of the Kuhn cubes), the slice stores that list ONCE: ucol[uoff[s] + k] = delta of
+// entry k for every lane, and rows lacking an offset hold a zero value there (the lane-paired value layout is kept,
+// entries in list order). The SpMV then reads the deltas with wave-uniform loads: 10 -> 8 bytes per entry on the
+// matrix stream. Real entries keep their order within the row (ascending column), so every row sum adds the same
+// products in the same order, with +-0 terms interleaved. Other slices: uoff[s] = -1, per-lane deltas as before.
+// k_sell_uniform runs after k_sell_pair; it rewrites the paired values / deltas of the uniform slices (pcols16 stays a
+// valid per-lane copy: kernels that ignore uoff read the same entries). A slice qualifies when: it is full (no rows
+// past nrows), width <= SU_MAXW, the row of greatest length has exactly w entries (no extra padding), every other
+// row's real deltas are a subsequence of that row's, every padded column row + delta lies in [0, nrows), and the
+// trailing SELL padding entries of every row are (delta 0, value 0).
+constexpr int SU_MAXW = 64;
+__attribute__((unused)) static __global__ void __launch_bounds__(256) k_sell_uniform(int64_t nslices, int64_t nrows,
+                                                             const int64_t* __restrict__ slice_ptr,
+                                                             const double* __restrict__ vin,
+                                                             const int16_t* __restrict__ cin, double* __restrict__ vout,
+                                                             int16_t* __restrict__ cout, int16_t* __restrict__ ucol,
+                                                             int32_t* __restrict__ uoff) {
+    __shared__ int cand_all[4][SU_MAXW];
+    const int64_t s = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;   // one wave per slice
+    const int l = threadIdx.x & 63;
+    int* cand = cand_all[(threadIdx.x >> 6) & 3];
+    if (s >= nslices) return;   // wave-uniform
     const int64_t p0 = slice_ptr[s];
     const int w = (int)((slice_ptr[s + 1] - p0) >> 6);
+    const int64_t row = s * 64 + l;
+    bool ok = (s + 1) * 64 <= nrows && w > 0 && w <= SU_MAXW;
+    // real entries of this row: the strictly increasing prefix of its deltas; the rest must be (0, 0.0) padding
+    int len = 0;
+    if (ok) {
+        int prev = -(1 << 30);
+        for (int k = 0; k < w; ++k) {
+            const int d = cin[p0 + 64 * k + l];
+            if (len == k && d > prev) {
+                ++len;
+                prev = d;
+            } else if (d != 0 || vin[p0 + 64 * k + l] != 0.0) {
+                ok = false;
+            }
+        }
+    }
+    ok = __all(ok);
+    const unsigned long long full = __ballot(ok && len == w);
+    if (ok && full) {
+        const int c = __builtin_ctzll(full);   // the lowest full-length row supplies the delta list
+        for (int k = 0; k < w; ++k) {
+            const int d = __shfl((int)cin[p0 + 64 * k + l], c, 64);
+            if (l == 0) cand[k] = d;
+            const int64_t col = row + d;
+            if (col < 0 || col >= nrows) ok = false;
+        }
+        // cand (written by lane 0) visible to the whole wave
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        int i = 0;
+        for (int k = 0; k < len && ok; ++k) {   // subsequence check
+            const int d = cin[p0 + 64 * k + l];
+            while (i < w && cand[i] < d) ++i;
+            if (i == w || cand[i] != d) ok = false;
+            ++i;
+        }
+    } else {
+        ok = false;
+    }
+    ok = __all(ok);
+    const int32_t uo = (int32_t)(2 * (p0 >> 6));   // even: the deltas are read as int32 pairs
+    if (!ok) {
+        if (l == 0) uoff[s] = -1;
+        return;
+    }
     const int np = w >> 1;
-    const int base = (int)(s * 64 + lane);
+    int kr = 0;   // next real entry of this row
+    for (int k = 0; k < w; ++k) {
+        const int d = cand[k];
+        double v = 0.0;
+        if (kr < len && (int)cin[p0 + 64 * kr + l] == d) {
+            v = vin[p0 + 64 * kr + l];
+            ++kr;
+        }
+        const int64_t dst = k < 2 * np ? p0 + (int64_t)(k >> 1) * 128 + 2 * l + (k & 1) : p0 + (int64_t)np * 128 + l;
+        vout[dst] = v;
+        cout[dst] = (int16_t)d;
+    }
+    for (int k = l; k < w; k += 64) ucol[uo + k] = (int16_t)cand[k];
+    if (l == 0) uoff[s] = uo;
+}
+
+// y_row (bs = 1) of one slice row in the paired layout; U pairs in flight. UNI: the slice's deltas from the
+// wave-uniform list ucl (k_sell_uniform), else per lane from cols.
+template <int U, int SC1, bool UNI>
+__device__ __forceinline__ double sell_row_pair_body(int64_t p0, int w, int base, int lane,
+                                                     const int16_t* __restrict__ cols, const int16_t* __restrict__ ucl,
+                                                     const double* __restrict__ vals, const double* __restrict__ x,
+                                                     int own_lo, int own_hi) {
+    const int np = w >> 1;
     const double2* v2 = reinterpret_cast<const double2*>(vals + p0) + lane;
-    const int32_t* c2 = reinterpret_cast<const int32_t*>(cols + p0) + lane;
+    const int32_t* c2 = UNI ? reinterpret_cast<const int32_t*>(ucl) : reinterpret_cast<const int32_t*>(cols + p0) + lane;
     double acc = 0.0;
     for (int j0 = 0; j0 < np; j0 += U) {
         int32_t cc[U];
         double2 vv[U];
         double x0[U], x1[U];
 #pragma unroll
-        for (int j = 0; j < U; ++j) cc[j] = (j0 + j < np) ? c2[64 * (j0 + j)] : 0;
+        for (int j = 0; j < U; ++j) cc[j] = (j0 + j < np) ? c2[UNI ? (j0 + j) : 64 * (j0 + j)] : 0;
 #pragma unroll
         for (int j = 0; j < U; ++j) vv[j] = (j0 + j < np) ? v2[64 * (j0 + j)] : double2{0.0, 0.0};
 #pragma unroll
@@ -85,9 +173,27 @@ __device__ __forceinline__ double sell_row_pair(int64_t s, int lane, const int64
     }
     if (w & 1) {
         const int64_t t = p0 + (int64_t)np * 128 + lane;
-        acc += vals[t] * ldx_col<SC1>(x, base + (int)cols[t], own_lo, own_hi);
+        const int d = UNI ? (int)ucl[w - 1] : (int)cols[t];
+        acc += vals[t] * ldx_col<SC1>(x, base + d, own_lo, own_hi);
     }
     return acc;
+}
+
+// uoff / ucol (nullable): the slice-uniform deltas of k_sell_uniform
+template <int U, int SC1 = 0>
+__device__ __forceinline__ double sell_row_pair(int64_t s, int lane, const int64_t* __restrict__ slice_ptr,
+                                                const int16_t* __restrict__ cols, const double* __restrict__ vals,
+                                                const double* __restrict__ x, int own_lo = 0, int own_hi = 0,
+                                                const int32_t* __restrict__ uoff = nullptr,
+                                                const int16_t* __restrict__ ucol = nullptr) {
+    const int64_t p0 = slice_ptr[s];
+    const int w = (int)((slice_ptr[s + 1] - p0) >> 6);
+    const int base = (int)(s * 64 + lane);
+    if (uoff) {
+        const int uo = __builtin_amdgcn_readfirstlane(uoff[s]);
+        if (uo >= 0) return sell_row_pair_body<U, SC1, true>(p0, w, base, lane, cols, ucol + uo, vals, x, own_lo, own_hi);
+    }
+    return sell_row_pair_body<U, SC1, false>(p0, w, base, lane, cols, nullptr, vals, x, own_lo, own_hi);
 }
 
 }  // namespace fem

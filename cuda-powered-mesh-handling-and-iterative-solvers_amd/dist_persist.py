@@ -73,7 +73,7 @@ def assemble_rank(coords, elements, split, rank, kind="poisson", E=1.0, nu=0.0, 
 class RankRunner:
     """One rank's persistent PCG context over its rows of the global system (vectors global-length)."""
 
-    TUNE_DEFAULT, TUNE_DIST_FINE = 1 | 2 | 4 | 8, 64
+    TUNE_DEFAULT, TUNE_DIST_FINE = 1 | 2 | 4 | 8 | 128, 64
 
     def __init__(self, rs: RankSetup, b, split, rank, nranks, tol=0.0, mode=C.MODE_PCG, eps=1e-30, grid=0,
                  stream=None, x0=None, fine=False):

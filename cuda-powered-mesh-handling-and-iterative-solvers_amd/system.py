@@ -281,12 +281,15 @@ class SellMatrix:
                                          C.stream(self.device)), "fem_sell_to_csr_vals")
         return self.g.rowptr, self.g.colidx, out[: self.g.nnz * self.bs * self.bs].view(-1, self.bs, self.bs)
 
-    def algorithmic_bytes_spmv(self, index_bytes=None):
+    def algorithmic_bytes_spmv(self, index_bytes=None, index_total=None):
         """HBM bytes one SpMV must move (SURVEY §8(d)): (8 bs^2 + idx) nnzb + 4 (nb+1) + 16 n, fp64 values;
-        idx = 4 for int32 columns (the survey's 12 nnz + 4(n+1) + 16 n for bs=1), 2 for 16-bit deltas."""
+        idx = 4 for int32 columns (the survey's 12 nnz + 4(n+1) + 16 n for bs=1), 2 for 16-bit deltas.
+        index_total: the column-index bytes of the stored format instead of idx nnzb (slice-uniform deltas:
+        PcgRunner.uniform_slices())."""
         idx = index_bytes if index_bytes is not None else (2 if self.use16 else 4)
         nnzb, nb = self.g.nnz, self.g.n_nodes
-        return (8 * self.bs * self.bs + idx) * nnzb + 4 * (nb + 1) + 16 * nb * self.bs
+        ib = idx * nnzb if index_total is None else int(index_total)
+        return 8 * self.bs * self.bs * nnzb + ib + 4 * (nb + 1) + 16 * nb * self.bs
 
     # ---------------------------------------------------------------- solver
     def pcg(self, b, x0=None, w=None, mode=C.MODE_PCG, tol=1e-8, max_iter=1000, eps=1e-30, history=False,
@@ -389,6 +392,14 @@ class PcgRunner:
     def effective_schedule(self):
         """The schedule the context runs (after start(): SCHED_PERSIST may have fallen back to SCHED_DEFERRED)."""
         return int(self.lib.fem_pcg_get_schedule(self.h))
+
+    def uniform_slices(self):
+        """(slices stored with slice-uniform deltas, all slices, column-index bytes per SpMV) of the context's matrix
+        copy (after start())."""
+        u, n, ib = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        C.check(self.lib.fem_pcg_uniform_slices(self.h, ctypes.byref(u), ctypes.byref(n), ctypes.byref(ib)),
+                "fem_pcg_uniform_slices")
+        return u.value, n.value, ib.value
 
     def profile(self, k, every=1):
         """k iterations with hip events around the kernels of every `every`-th one -> (ms sums, counts)."""

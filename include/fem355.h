@@ -353,6 +353,9 @@ int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, 
 int fem_pcg_set_schedule(fem_pcg* s, int sched);
 /* the schedule the context runs (valid after fem_pcg_start: 3 may have fallen back to 2) */
 int fem_pcg_get_schedule(fem_pcg* s);
+/* [sync] slices stored with slice-uniform deltas (FEM_TUNE_PK_UNI; valid after fem_pcg_start), the slice count, and
+ * the column-index bytes one SpMV over the context's matrix reads (padding included) */
+int fem_pcg_uniform_slices(fem_pcg* s, int64_t* uniform, int64_t* nslices, int64_t* index_bytes);
 /* persistent schedule only: k iterations of the instrumented kernel build; host_out[G * 8] = per-workgroup shader-clock
  * sums of the phases (u wait, SpMV, block sum, barrier + partial sums, step, update + drain + flag, launch prologue,
  * launch epilogue), then host_out[G * 8 + G * 16] = every wave's own SpMV clock sum; *grid = G */
@@ -377,12 +380,16 @@ int fem_enforce_constraints(double* x, double* r, int64_t n, int order, int64_t 
                             const int64_t* rbe2_master, int64_t S, const int64_t* spc_dof, const double* spc_val,
                             int64_t G, const int64_t* r3_ptr, const int64_t* r3_master, const double* r3_wsum,
                             const int64_t* r3_slave, const double* r3_w, fem_stream_t stream);
-/* tuning flags (default FEM_TUNE_REVERSE | FEM_TUNE_PAIR | FEM_TUNE_PK_SC1 | FEM_TUNE_PK_PACK): the SpMV of every schedule sweeps each XCD's slice range backwards on
+/* tuning flags (default FEM_TUNE_REVERSE | FEM_TUNE_PAIR | FEM_TUNE_PK_SC1 | FEM_TUNE_PK_PACK | FEM_TUNE_PK_UNI): the SpMV of every schedule sweeps each XCD's slice range backwards on
  * odd iterations, so the matrix tail read last (still in the MI355X's 256 MB memory-side cache) is read first by
  * the next sweep: 67 -> 57 us per SpMV on the 10M Poisson matrix. Results depend on the flags only through the
  * order of the per-block p.q partials (deterministic for a given flag set). */
 enum { FEM_TUNE_REVERSE = 1, FEM_TUNE_PAIR = 2, FEM_TUNE_PK_SC1 = 4, FEM_TUNE_PK_PACK = 8, FEM_TUNE_C1F = 16,
-       FEM_TUNE_PK_COOP = 32, FEM_TUNE_DIST_FINE = 64 };
+       FEM_TUNE_PK_COOP = 32, FEM_TUNE_DIST_FINE = 64, FEM_TUNE_PK_UNI = 128 };
+/* FEM_TUNE_PK_UNI (default): bs = 1 paired copies also record, per 64-row slice whose rows take their columns at one
+ * common sorted list of offsets (rows lacking an offset get a zero value there), that list once (sell_pair.hpp
+ * k_sell_uniform); the persistent schedule then reads those slices' deltas with wave-uniform loads: 10 -> 8 bytes
+ * per matrix entry (every slice of the Kuhn cubes). Same products in the same order per row (+-0 terms between). */
 /* FEM_TUNE_DIST_FINE (set before fem_pcg_set_rows): the distributed persistent comm block (u, flags, rank sums) in
  * fine-grained device memory (hipDeviceMallocFinegrained) instead of hipMalloc's coarse-grained memory -- the
  * variant bench.py tries when the coarse-grained one fails its self-check on a multi-GPU node. */

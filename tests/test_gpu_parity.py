@@ -489,6 +489,58 @@ def test_persistent_chunks_are_bit_identical(gpu):
     assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][1], outs[2][1])
 
 
+def _fixed_iterates(system, A, b, w, sched, flags, k):
+    run = system.PcgRunner(A, b, w, tol=0.0, schedule=sched)
+    if flags is not None:
+        run.set_tuning(flags)
+    run.start()
+    uni = run.uniform_slices()
+    run.iterate(k)
+    it, st, rz = run.poll()
+    assert it == k and st == 0
+    x = run.x.clone()
+    run.close()
+    return uni, rz, x
+
+
+@pytest.mark.parametrize("case", ["kuhn", "kuhn_unused_node", "permuted"])
+def test_slice_uniform_deltas_are_bit_identical(gpu, case):
+    """FEM_TUNE_PK_UNI (default): slices whose rows share one sorted delta list store it once and hold zeros where
+    a row lacks an offset. Every row adds the same products in the same order, so the persistent and the deferred
+    schedules give the same iterates bit for bit with and without it. Kuhn cubes: every full slice qualifies (the
+    partial last slice never does); an unused node (empty row) and a random node numbering (no common lists) fall
+    back per slice."""
+    _, mesh, _, system = _mods()
+    c, t = mesh.kuhn_cube(13, jitter=0.1)
+    N = c.shape[0]
+    if case == "kuhn_unused_node":
+        c = torch.cat([c[:700], torch.tensor([[4.0, 4.0, 4.0]], dtype=c.dtype), c[700:]])
+        t = t + (t >= 700).to(t.dtype)
+        N += 1
+    elif case == "permuted":
+        perm = torch.randperm(N, generator=torch.Generator().manual_seed(11))
+        inv = torch.empty_like(perm)
+        inv[perm] = torch.arange(N)
+        c, t = c[perm], inv[t]
+    A = system.assemble_tet4_system(c.to(gpu), t.to(gpu), "poisson")
+    b = torch.randn(A.n, dtype=F64, generator=torch.Generator().manual_seed(2)).to(gpu)
+    w = A.jacobi(None)
+    for sched in (3, 2):
+        uni, rz1, x1 = _fixed_iterates(system, A, b, w, sched, None, 40)        # defaults (PK_UNI on)
+        off, rz0, x0 = _fixed_iterates(system, A, b, w, sched, 1 | 2 | 4 | 8, 40)
+        nsl = (N + 63) // 64
+        assert uni[1] == off[1] == nsl and off[0] == 0
+        if case == "permuted":
+            assert uni[0] <= nsl // 10
+        elif case == "kuhn":
+            # all but the slices near either end (a padded column row + delta would leave [0, N)) and the partial one
+            assert nsl - 9 <= uni[0] < nsl
+        else:
+            assert 0 < uni[0] < nsl   # slices whose rows' offsets change at the inserted node fall back
+        assert uni[2] < off[2] or uni[0] == 0
+        assert torch.equal(x1, x0) and rz1 == rz0, (case, sched)
+
+
 def test_persistent_full_geometry_10m(gpu):
     """The 10M-tet bench system (27,000 slices: 6-7 slots per wave, every register slot and the LDS v slots in use):
     50 fixed iterations equal the deferred schedule's to 1e-12; a solve to tolerance stops mid-launch at the

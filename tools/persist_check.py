@@ -35,6 +35,7 @@ def rate(A, b, w, sched, warm, iters, chunk, tune=None):
         run.set_tuning(tune)
     run.start()
     eff = run.effective_schedule()
+    uni = run.uniform_slices()[:2]
     run.iterate(warm)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -48,7 +49,7 @@ def rate(A, b, w, sched, warm, iters, chunk, tune=None):
     it, stt, rz = run.poll()
     x = run.x.clone()
     run.close()
-    return {"sched": eff, "it_per_s": iters / dt, "us_per_it": dt / iters * 1e6, "iter": it, "status": stt,
+    return {"sched": eff, "uniform_slices": list(uni), "it_per_s": iters / dt, "us_per_it": dt / iters * 1e6, "iter": it, "status": stt,
             "rz": rz}, x
 
 
