@@ -113,6 +113,99 @@ __global__ void __launch_bounds__(T) k_spmv_persist_lab(int64_t nslices, int64_t
     if (nrows < 0) pad_lds[threadIdx.x] = 0.0;
 }
 
+// the persistent-geometry probe on the production bs = 1 format: lane-paired values, slice-uniform deltas where
+// k_sell_uniform found them (U = 2 pairs in flight, 1024 threads, as k_pcg_persist)
+__global__ void __launch_bounds__(1024) k_spmv_persist_uni_lab(int64_t nslices, int64_t nrows,
+                                                               const int64_t* __restrict__ slice_ptr,
+                                                               const int16_t* __restrict__ cols,
+                                                               const double* __restrict__ vals,
+                                                               const int32_t* __restrict__ uoff,
+                                                               const int16_t* __restrict__ ucol,
+                                                               const double* __restrict__ x, double* __restrict__ y) {
+    extern __shared__ double pad_lds[];
+    const int lane = threadIdx.x & 63;
+    const int G = gridDim.x;
+    const int L = (blockIdx.x % NXCD) * (G / NXCD) + blockIdx.x / NXCD;
+    const int64_t W = (int64_t)G * 16;
+    const int64_t g = (int64_t)L * 16 + (threadIdx.x >> 6);
+    const int64_t s0 = g * nslices / W, s1 = (g + 1) * nslices / W;
+    for (int64_t s = s0; s < s1; ++s) {
+        const double acc = sell_row_pair<2>(s, lane, slice_ptr, cols, vals, x, 0, 0, uoff, ucol);
+        const int64_t row = s * 64 + lane;
+        if (row < nrows) y[row] = acc;
+    }
+    if (nrows < 0) pad_lds[threadIdx.x] = 0.0;
+}
+
+// symmetric-storage probe (bs = 1): only the upper triangle (col >= row) is stored, plain SELL-64 layout with a
+// slice-uniform delta list per slice; the lower entries of a row are re-read from the upper storage of the rows
+// they mirror: for lower delta d of slice s, lanes l >= d % 64 read slice s - d / 64 at base_a + l - d % 64, the
+// others slice s - d / 64 - 1 at base_b + l - d % 64 + 64 (bases: slice offset + 64 k of delta +d there; -1: none).
+// Same persistent geometry as above. x must be readable at [row - 32768, row + 32768) for every slice row.
+__global__ void __launch_bounds__(1024) k_spmv_sym_lab(int64_t nslices, int64_t nrows, const int64_t* __restrict__ uptr,
+                                                       const int32_t* __restrict__ ulist,
+                                                       const int16_t* __restrict__ udel,
+                                                       const int32_t* __restrict__ lptr,
+                                                       const int32_t* __restrict__ ldel,
+                                                       const int32_t* __restrict__ lbase,
+                                                       const double* __restrict__ uvals, const double* __restrict__ x,
+                                                       double* __restrict__ y) {
+    extern __shared__ double pad_lds[];
+    const int lane = threadIdx.x & 63;
+    const int G = gridDim.x;
+    const int L = (blockIdx.x % NXCD) * (G / NXCD) + blockIdx.x / NXCD;
+    const int64_t W = (int64_t)G * 16;
+    const int64_t g = (int64_t)L * 16 + (threadIdx.x >> 6);
+    const int64_t s0 = g * nslices / W, s1 = (g + 1) * nslices / W;
+    for (int64_t s = s0; s < s1; ++s) {
+        const int64_t p0 = uptr[s];
+        const int w = (int)((uptr[s + 1] - p0) >> 6);
+        const int16_t* ud = udel + ulist[s];
+        const int base = (int)(s * 64 + lane);
+        const double* uv = uvals + p0 + lane;
+        double acc = 0.0;
+        int k = 0;
+        for (; k + 4 <= w; k += 4) {
+            double v[4], xv[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = uv[64 * (k + j)];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) xv[j] = x[base + ud[k + j]];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc += v[j] * xv[j];
+        }
+        for (; k < w; ++k) acc += uv[64 * k] * x[base + ud[k]];
+        const int m0 = lptr[s], m1 = lptr[s + 1];
+        int m = m0;
+        for (; m + 2 <= m1; m += 2) {
+            double v[2], xv[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int d = ldel[m + j];
+                const int r = d & 63;
+                const int ba = lbase[2 * (m + j)], bb = lbase[2 * (m + j) + 1];
+                const int lp = lane - r;
+                const int pos = lp >= 0 ? (ba >= 0 ? ba + lp : -1) : (bb >= 0 ? bb + lp + 64 : -1);
+                v[j] = pos >= 0 ? uvals[pos] : 0.0;
+                xv[j] = x[base - d];
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc += v[j] * xv[j];
+        }
+        for (; m < m1; ++m) {
+            const int d = ldel[m];
+            const int r = d & 63;
+            const int ba = lbase[2 * m], bb = lbase[2 * m + 1];
+            const int lp = lane - r;
+            const int pos = lp >= 0 ? (ba >= 0 ? ba + lp : -1) : (bb >= 0 ? bb + lp + 64 : -1);
+            acc += (pos >= 0 ? uvals[pos] : 0.0) * x[base - d];
+        }
+        const int64_t row = s * 64 + lane;
+        if (row < nrows) y[row] = acc;
+    }
+    if (nrows < 0) pad_lds[threadIdx.x] = 0.0;
+}
+
 }  // namespace fem
 
 using namespace fem;
@@ -213,6 +306,41 @@ int fem_lab_spmv3(int layout, int u, int nt, int grid, int64_t nrows, const int6
 #undef L3N
 #undef L3U
 #undef L3
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_lab_sell_uniform(int64_t nrows, const int64_t* slice_ptr, const double* vals, const int16_t* dcols,
+                         double* vals_out, int16_t* dcols_out, int16_t* ucol, int32_t* uoff, fem_stream_t stream) {
+    const int64_t ns = cdiv(nrows, 64);
+    if (ns == 0) return FEM_OK;
+    hipLaunchKernelGGL(k_sell_pair, dim3(stream_grid(ns * 64, 256)), dim3(256), 0, S(stream), ns, slice_ptr, vals,
+                       dcols, vals_out, dcols_out);
+    FEM_LAUNCHED();
+    hipLaunchKernelGGL(k_sell_uniform, dim3((unsigned)cdiv(ns, 4)), dim3(256), 0, S(stream), ns, nrows, slice_ptr, vals,
+                       dcols, vals_out, dcols_out, ucol, uoff);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_lab_spmv_persist_uni(int grid, int64_t lds_bytes, int64_t nrows, const int64_t* slice_ptr,
+                             const int16_t* pcols, const double* pvals, const int32_t* uoff, const int16_t* ucol,
+                             const double* x, double* y, fem_stream_t stream) {
+    const int64_t ns = cdiv(nrows, 64);
+    if (ns == 0) return FEM_OK;
+    hipLaunchKernelGGL(k_spmv_persist_uni_lab, dim3(grid), dim3(1024), (size_t)lds_bytes, S(stream), ns, nrows,
+                       slice_ptr, pcols, pvals, uoff, ucol, x, y);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_lab_spmv_sym(int grid, int64_t lds_bytes, int64_t nrows, const int64_t* uptr, const int32_t* ulist,
+                     const int16_t* udel, const int32_t* lptr, const int32_t* ldel, const int32_t* lbase,
+                     const double* uvals, const double* x, double* y, fem_stream_t stream) {
+    const int64_t ns = cdiv(nrows, 64);
+    if (ns == 0) return FEM_OK;
+    hipLaunchKernelGGL(k_spmv_sym_lab, dim3(grid), dim3(1024), (size_t)lds_bytes, S(stream), ns, nrows, uptr, ulist,
+                       udel, lptr, ldel, lbase, uvals, x, y);
     FEM_LAUNCHED();
     return FEM_OK;
 }

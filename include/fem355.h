@@ -317,6 +317,17 @@ int fem_lab_sell3_layout(int layout, int64_t nrows, const int64_t* slice_ptr, co
                          const int16_t* dcols, double* vals_out, int16_t* dcols_out, fem_stream_t stream);
 int fem_lab_spmv3(int layout, int u, int nt, int grid, int64_t nrows, const int64_t* slice_ptr, const int16_t* dcols,
                   const double* vals, const double* x, double* y, fem_stream_t stream);
+/* probes (tools/sym_probe.py): the production bs = 1 paired copy with slice-uniform deltas (k_sell_pair +
+ * k_sell_uniform) and the persistent-geometry SpMV over it; a symmetric-storage SpMV (upper triangle only, lower
+ * entries re-read from the rows they mirror) in the same geometry */
+int fem_lab_sell_uniform(int64_t nrows, const int64_t* slice_ptr, const double* vals, const int16_t* dcols,
+                         double* vals_out, int16_t* dcols_out, int16_t* ucol, int32_t* uoff, fem_stream_t stream);
+int fem_lab_spmv_persist_uni(int grid, int64_t lds_bytes, int64_t nrows, const int64_t* slice_ptr,
+                             const int16_t* pcols, const double* pvals, const int32_t* uoff, const int16_t* ucol,
+                             const double* x, double* y, fem_stream_t stream);
+int fem_lab_spmv_sym(int grid, int64_t lds_bytes, int64_t nrows, const int64_t* uptr, const int32_t* ulist,
+                     const int16_t* udel, const int32_t* lptr, const int32_t* ldel, const int32_t* lbase,
+                     const double* uvals, const double* x, double* y, fem_stream_t stream);
 
 /* ------------------------------------------------------------------ (P)CG (L3)
  * One solve context over a SELL matrix. The whole iteration runs on the device: SpMV + p.q reduction,
