@@ -99,6 +99,7 @@ SIGNATURES = {
     "fem_lab_spmv3": (_I, [_I, _I, _I, _I, _L, _P, _P, _P, _P, _P, _P]),
     "fem_lab_sell_uniform": (_I, [_L, _P, _P, _P, _P, _P, _P, _P, _P]),
     "fem_lab_spmv_persist_uni": (_I, [_I, _L, _L, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "fem_lab_spmv_gather": (_I, [_I, _I, _L, _L, _P, _P, _P, _P, _P, _P, _P]),
     "fem_lab_spmv_sym": (_I, [_I, _L, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "fem_pcg_create": (_I, [_L, _I, _P, _P, _P, _P, _P, _P, _I, _D, _D, _P, _L, _P, ctypes.POINTER(_P)]),
     "fem_pcg_start": (_I, [_P]),

@@ -206,6 +206,69 @@ __global__ void __launch_bounds__(1024) k_spmv_sym_lab(int64_t nslices, int64_t 
     if (nrows < 0) pad_lds[threadIdx.x] = 0.0;
 }
 
+// gather-volume probe: the uniform-slice SpMV with the odd entry of every pair taking the even entry's gathered x
+// (MODE 1: WRONG result, 8 instead of 15 gathers per row on the Kuhn stencil) or with no gathers at all (MODE 2:
+// x = 1) -- how much of the SpMV time the L2-served x gathers cost
+template <int MODE>
+__global__ void __launch_bounds__(1024) k_spmv_gather_lab(int64_t nslices, int64_t nrows,
+                                                          const int64_t* __restrict__ slice_ptr,
+                                                          const double* __restrict__ vals,
+                                                          const int32_t* __restrict__ uoff,
+                                                          const int16_t* __restrict__ ucol,
+                                                          const double* __restrict__ x, double* __restrict__ y) {
+    extern __shared__ double pad_lds[];
+    const int lane = threadIdx.x & 63;
+    const int G = gridDim.x;
+    const int L = (blockIdx.x % NXCD) * (G / NXCD) + blockIdx.x / NXCD;
+    const int64_t W = (int64_t)G * 16;
+    const int64_t g = (int64_t)L * 16 + (threadIdx.x >> 6);
+    const int64_t s0 = g * nslices / W, s1 = (g + 1) * nslices / W;
+    for (int64_t s = s0; s < s1; ++s) {
+        const int uo = __builtin_amdgcn_readfirstlane(uoff[s]);
+        if (uo < 0) continue;
+        const int64_t p0 = slice_ptr[s];
+        const int w = (int)((slice_ptr[s + 1] - p0) >> 6);
+        const int np = w >> 1;
+        const int base = (int)(s * 64 + lane);
+        const double2* v2 = reinterpret_cast<const double2*>(vals + p0) + lane;
+        const int32_t* c2 = reinterpret_cast<const int32_t*>(ucol + uo);
+        double acc = 0.0;
+        for (int j0 = 0; j0 < np; j0 += 2) {
+            int32_t cc[2];
+            double2 vv[2];
+            double x0[2], x1[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) cc[j] = (j0 + j < np) ? c2[j0 + j] : 0;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) vv[j] = (j0 + j < np) ? v2[64 * (j0 + j)] : double2{0.0, 0.0};
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int lo = (int)(int16_t)(cc[j] & 0xffff);
+                if constexpr (MODE == 2) {
+                    x0[j] = 1.0 + lo;
+                    x1[j] = 1.0;
+                } else {
+                    x0[j] = (j0 + j < np) ? x[base + lo] : 0.0;
+                    x1[j] = x0[j];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                if (j0 + j < np) {
+                    acc += vv[j].x * x0[j];
+                    acc += vv[j].y * x1[j];
+                }
+        }
+        if (w & 1) {
+            const int64_t t = p0 + (int64_t)np * 128 + lane;
+            acc += vals[t] * (MODE == 2 ? 1.0 : x[base + (int)ucol[uo + w - 1]]);
+        }
+        const int64_t row = s * 64 + lane;
+        if (row < nrows) y[row] = acc;
+    }
+    if (nrows < 0) pad_lds[threadIdx.x] = 0.0;
+}
+
 }  // namespace fem
 
 using namespace fem;
@@ -341,6 +404,21 @@ int fem_lab_spmv_sym(int grid, int64_t lds_bytes, int64_t nrows, const int64_t* 
     if (ns == 0) return FEM_OK;
     hipLaunchKernelGGL(k_spmv_sym_lab, dim3(grid), dim3(1024), (size_t)lds_bytes, S(stream), ns, nrows, uptr, ulist,
                        udel, lptr, ldel, lbase, uvals, x, y);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_lab_spmv_gather(int mode, int grid, int64_t lds_bytes, int64_t nrows, const int64_t* slice_ptr,
+                        const double* pvals, const int32_t* uoff, const int16_t* ucol, const double* x, double* y,
+                        fem_stream_t stream) {
+    const int64_t ns = cdiv(nrows, 64);
+    if (ns == 0) return FEM_OK;
+    if (mode == 2)
+        hipLaunchKernelGGL(k_spmv_gather_lab<2>, dim3(grid), dim3(1024), (size_t)lds_bytes, S(stream), ns, nrows,
+                           slice_ptr, pvals, uoff, ucol, x, y);
+    else
+        hipLaunchKernelGGL(k_spmv_gather_lab<1>, dim3(grid), dim3(1024), (size_t)lds_bytes, S(stream), ns, nrows,
+                           slice_ptr, pvals, uoff, ucol, x, y);
     FEM_LAUNCHED();
     return FEM_OK;
 }

@@ -325,6 +325,9 @@ int fem_lab_sell_uniform(int64_t nrows, const int64_t* slice_ptr, const double* 
 int fem_lab_spmv_persist_uni(int grid, int64_t lds_bytes, int64_t nrows, const int64_t* slice_ptr,
                              const int16_t* pcols, const double* pvals, const int32_t* uoff, const int16_t* ucol,
                              const double* x, double* y, fem_stream_t stream);
+int fem_lab_spmv_gather(int mode, int grid, int64_t lds_bytes, int64_t nrows, const int64_t* slice_ptr,
+                        const double* pvals, const int32_t* uoff, const int16_t* ucol, const double* x, double* y,
+                        fem_stream_t stream);
 int fem_lab_spmv_sym(int grid, int64_t lds_bytes, int64_t nrows, const int64_t* uptr, const int32_t* ulist,
                      const int16_t* udel, const int32_t* lptr, const int32_t* ldel, const int32_t* lbase,
                      const double* uvals, const double* x, double* y, fem_stream_t stream);

@@ -117,6 +117,12 @@ def main():
     out = {"n": a.n, "rows": N, "nnz": g.nnz, "uniform_slices": int((uoff >= 0).sum()),
            "full_err": float((y[:N] - ref).abs().max() / ref.abs().max())}
     out["full_us"] = timed(full, a.reps) * 1e3
+    for mode in (1, 2):   # gather-volume probe (wrong results by design): half the gathers / none
+        def gth(mode=mode):
+            C.check(lib.fem_lab_spmv_gather(mode, ncu, lds, N, C.ptr(g.slice_ptr), C.ptr(pv), C.ptr(uoff), C.ptr(ucol),
+                                            C.ptr(x), C.ptr(y), st), "gather")
+        gth()
+        out[f"gather_mode{mode}_us"] = timed(gth, a.reps) * 1e3
     sym = build_sym(rowptr, colidx, vals, N, dev)
     out["upper_entries"] = sym["upper_entries"]
 
