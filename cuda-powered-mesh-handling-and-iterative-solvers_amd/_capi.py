@@ -109,7 +109,7 @@ SIGNATURES = {
     "fem_pcg_use_graph": (_I, [_P, _I]),
     "fem_pcg_set_schedule": (_I, [_P, _I]),
     "fem_pcg_get_schedule": (_I, [_P]),
-    "fem_pcg_uniform_slices": (_I, [_P, _P, _P, _P]),
+    "fem_pcg_uniform_slices": (_I, [_P, _L, _L, _P, _P, _P]),
     "fem_pcg_persist_profile": (_I, [_P, _I, _P, ctypes.POINTER(_I)]),
     "fem_pcg_set_constraints": (_I, [_P, _I, _L, _P, _P, _L, _P, _P, _L, _P, _P, _P, _P, _P]),
     "fem_enforce_constraints": (_I, [_P, _P, _L, _I, _L, _P, _P, _L, _P, _P, _L, _P, _P, _P, _P, _P, _P]),

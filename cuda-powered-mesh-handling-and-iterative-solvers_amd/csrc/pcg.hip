@@ -2372,9 +2372,13 @@ int fem_pcg_get_schedule(fem_pcg* s) {
     return s->deferred ? 2 : 0;
 }
 
-int fem_pcg_uniform_slices(fem_pcg* s, int64_t* uniform, int64_t* nslices, int64_t* index_bytes) {
+int fem_pcg_uniform_slices(fem_pcg* s, int64_t s_begin, int64_t s_end, int64_t* uniform, int64_t* nslices,
+                           int64_t* index_bytes) {
+    if (s_end < 0 || s_end > s->nslices) s_end = s->nslices;
+    if (s_begin < 0) s_begin = 0;
+    if (s_begin > s_end) s_begin = s_end;
     *uniform = 0;
-    *nslices = s->nslices;
+    *nslices = s_end - s_begin;
     *index_bytes = 0;
     if (s->nslices == 0) return FEM_OK;
     std::vector<int64_t> sp((size_t)s->nslices + 1);
@@ -2385,7 +2389,7 @@ int fem_pcg_uniform_slices(fem_pcg* s, int64_t* uniform, int64_t* nslices, int64
     FEM_HIP(hipStreamSynchronize(s->stream));
     const int64_t idx = s->cols16 ? 2 : 4;
     int64_t c = 0, ib = 0;
-    for (int64_t i = 0; i < s->nslices; ++i) {
+    for (int64_t i = s_begin; i < s_end; ++i) {
         const int64_t wdt = (sp[i + 1] - sp[i]) / 64;
         if (h[i] >= 0) {
             ++c;

@@ -430,13 +430,16 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False):
     dt = tmax(time.perf_counter() - t0)
     it2, stt2, _ = run.poll()
     ms_max = tmax(ms)
+    # column-index bytes of this rank's slices as stored (slice-uniform delta lists where they qualify)
+    n_uni, _, idx_own = _sys.uniform_slices(run.lib, run.h, split[rank], split[rank + 1])
     barrier_sync()
     disconnect(opened, dev)
     A = rs.A
     lo, hi = rs.lo, rs.hi
     nnz_own = int(A.g.rowptr[hi] - A.g.rowptr[lo])
     n_own = hi - lo
-    alg_own = (8 + 2) * nnz_own + 4 * (n_own + 1) + 16 * n_own   # this rank's bytes per iteration
+    # this rank's bytes per iteration (with the stored format's index bytes)
+    alg_own = 8 * nnz_own + (idx_own if n_uni else 2 * nnz_own) + 4 * (n_own + 1) + 16 * n_own
     alg_total = tsum(float(alg_own))
     run.close()
     ok_steps = it2 == a.warmup + a.steps and stt2 == C.PCG_RUNNING

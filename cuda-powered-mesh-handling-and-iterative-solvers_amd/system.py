@@ -192,6 +192,14 @@ def pad_connectivity(blocks, npe_max):
     return torch.cat(out, 0).contiguous()
 
 
+def uniform_slices(lib, h, s_begin=0, s_end=-1):
+    """fem_pcg_uniform_slices of a solver context handle: (uniform slices, slices, column-index bytes per SpMV)."""
+    u, n, ib = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    C.check(lib.fem_pcg_uniform_slices(h, int(s_begin), int(s_end), ctypes.byref(u), ctypes.byref(n),
+                                       ctypes.byref(ib)), "fem_pcg_uniform_slices")
+    return u.value, n.value, ib.value
+
+
 @_scoped
 class SellMatrix:
     """Assembled global operator in SELL-64 with bs x bs blocks (bs = dofs per node)."""
@@ -393,13 +401,10 @@ class PcgRunner:
         """The schedule the context runs (after start(): SCHED_PERSIST may have fallen back to SCHED_DEFERRED)."""
         return int(self.lib.fem_pcg_get_schedule(self.h))
 
-    def uniform_slices(self):
-        """(slices stored with slice-uniform deltas, all slices, column-index bytes per SpMV) of the context's matrix
-        copy (after start())."""
-        u, n, ib = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
-        C.check(self.lib.fem_pcg_uniform_slices(self.h, ctypes.byref(u), ctypes.byref(n), ctypes.byref(ib)),
-                "fem_pcg_uniform_slices")
-        return u.value, n.value, ib.value
+    def uniform_slices(self, s_begin=0, s_end=-1):
+        """(slices stored with slice-uniform deltas, slices, column-index bytes per SpMV) over the slices
+        [s_begin, s_end) of the context's matrix copy (after start())."""
+        return uniform_slices(self.lib, self.h, s_begin, s_end)
 
     def profile(self, k, every=1):
         """k iterations with hip events around the kernels of every `every`-th one -> (ms sums, counts)."""

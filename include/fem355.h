@@ -367,9 +367,11 @@ int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, 
 int fem_pcg_set_schedule(fem_pcg* s, int sched);
 /* the schedule the context runs (valid after fem_pcg_start: 3 may have fallen back to 2) */
 int fem_pcg_get_schedule(fem_pcg* s);
-/* [sync] slices stored with slice-uniform deltas (FEM_TUNE_PK_UNI; valid after fem_pcg_start), the slice count, and
- * the column-index bytes one SpMV over the context's matrix reads (padding included) */
-int fem_pcg_uniform_slices(fem_pcg* s, int64_t* uniform, int64_t* nslices, int64_t* index_bytes);
+/* [sync] over the slices [s_begin, s_end) of the context's matrix (s_end < 0: to the last): the slices stored with
+ * slice-uniform deltas (FEM_TUNE_PK_UNI; valid after fem_pcg_start), the slice count, and the column-index bytes one
+ * SpMV over those slices reads (padding included) */
+int fem_pcg_uniform_slices(fem_pcg* s, int64_t s_begin, int64_t s_end, int64_t* uniform, int64_t* nslices,
+                           int64_t* index_bytes);
 /* persistent schedule only: k iterations of the instrumented kernel build; host_out[G * 8] = per-workgroup shader-clock
  * sums of the phases (u wait, SpMV, block sum, barrier + partial sums, step, update + drain + flag, launch prologue,
  * launch epilogue), then host_out[G * 8 + G * 16] = every wave's own SpMV clock sum; *grid = G */
