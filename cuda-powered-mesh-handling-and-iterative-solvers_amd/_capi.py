@@ -23,7 +23,7 @@ FEM_OK, FEM_EBADTYPE, FEM_ESINGULAR, FEM_EHIP, FEM_ERCCL, FEM_EARG = range(6)
 PCG_RUNNING, PCG_CONVERGED, PCG_MAXITER, PCG_BREAKDOWN, PCG_ALPHA_NAN, PCG_BETA_NAN, PCG_SYNC_TIMEOUT = range(7)
 MODE_CG_STABLE, MODE_PCG, MODE_CG_CONSTRAINED = 0, 1, 2
 KIND_ELASTIC, KIND_POISSON, KIND_MASS = 0, 1, 2
-ISO_SUM, ISO_STACK, ISO_VOLUME = 0, 1, 2
+ISO_SUM, ISO_STACK, ISO_VOLUME, ISO_MASS = 0, 1, 2, 3
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -38,6 +38,7 @@ SIGNATURES = {
     "fem_tet4_geom": (_I, [_P, _P, _L, _P, _P, _P, _P, _P]),
     "fem_iso_ke": (_I, [_P, _P, _L, _I, _D, _D, _P, _P, _I, _I, _P, _P]),
     "fem_iso_geom": (_I, [_P, _P, _L, _I, _P, _P, _P, _P, _P]),
+    "fem_iso_mass": (_I, [_P, _P, _L, _I, _D, _P, _P, _P, _I, _P, _P]),
     "fem_pcg_scalars": (_I, [_P, ctypes.POINTER(_D)]),
     "fem_scan_work_len": (_L, [_L]),
     "fem_incidence_work_bytes": (_L, [_L, _L]),

@@ -158,13 +158,14 @@ template <int NPE>
 __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, const int64_t* __restrict__ conn,
                                                 int64_t M, double E, double nu, const double* __restrict__ dN,
                                                 const double* __restrict__ w, int n_ip, int mode,
-                                                double* __restrict__ Ke) {
+                                                double* __restrict__ Ke, const double* __restrict__ Nv = nullptr) {
     // Wave per element, 4 per block. Per chunk of up to ISO_IPC points, lane q of a wave forms the Jacobian,
     // detJ and the global gradients of point q (`einsum("ji,mjk->mik")`, `einsum("mij,nj->mni")`) into LDS —
     // all points of the chunk at once, one barrier — then lane (a,b), a <= b, adds the 3x3 block of every point
     // in point order. c3d10 (100 blocks > 64 lanes): only a <= b, block (b,a) written as its transpose (K_e =
     // sum B^T D B is symmetric; mirrored entries equal the directly formed ones up to the order of two products),
     // 55 blocks, one per lane. c3d8 / c3d6 (<= 64 blocks): every block formed directly.
+    // mode FEM_ISO_MASS (E = rho, Nv = shape values [n_ip][NPE]): block (a,b) = rho sum_q w_q |detJ_q| N_a N_b I3.
     constexpr int D = 3 * NPE;
     constexpr bool SYM = NPE * NPE > 64;
     constexpr int NS = SYM ? NPE * (NPE + 1) / 2 : NPE * NPE;
@@ -176,7 +177,11 @@ __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, co
     constexpr int GK = (ISO_IPC * NPE * 3 > D * D) ? ISO_IPC * NPE * 3 : D * D;
     __shared__ double gk_s[4][GK];
     __shared__ double c_s[4][ISO_IPC];
+    __shared__ double nv_s[ISO_MAX_IP * NPE];
+    const bool mass = mode == FEM_ISO_MASS;
     for (int t = threadIdx.x; t < n_ip * NPE * 3; t += 256) dn_s[t] = dN[t];
+    if (mass)
+        for (int t = threadIdx.x; t < n_ip * NPE; t += 256) nv_s[t] = Nv[t];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t e = (int64_t)blockIdx.x * 4 + wid;
     const bool active = e < M;
@@ -247,12 +252,20 @@ __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, co
                 for (int i = 0; i < 3; ++i)
                     gk_s[wid][(lane * NPE + n) * 3 + i] =
                         Ji[3 * i] * dq[n * 3] + Ji[3 * i + 1] * dq[n * 3 + 1] + Ji[3 * i + 2] * dq[n * 3 + 2];
-            c_s[wid][lane] = (mode == FEM_ISO_SUM) ? det * w[q] : (mode == FEM_ISO_STACK ? det : vol);
+            c_s[wid][lane] = mass ? fabs(det) * w[q] * E
+                                  : (mode == FEM_ISO_SUM) ? det * w[q] : (mode == FEM_ISO_STACK ? det : vol);
         }
         __syncthreads();
         for (int ql = 0; ql < nq; ++ql) {
             const double coef = c_s[wid][ql];
-            if (blk_lane) {
+            if (mass) {
+                if (blk_lane) {
+                    const double s = nv_s[(q0 + ql) * NPE + ba] * nv_s[(q0 + ql) * NPE + bb] * coef;
+                    acc[0] += s;
+                    acc[4] += s;
+                    acc[8] += s;
+                }
+            } else if (blk_lane) {
                 const double* ga = &gk_s[wid][(ql * NPE + ba) * 3];
                 const double* gb = &gk_s[wid][(ql * NPE + bb) * 3];
                 const double dot = ga[0] * gb[0] + ga[1] * gb[1] + ga[2] * gb[2];
@@ -959,6 +972,10 @@ int fem_iso_geom(const double* coords, const int64_t* conn, int64_t M, int npe, 
 
 int fem_iso_ke(const double* coords, const int64_t* conn, int64_t M, int npe, double E, double nu, const double* dN,
                const double* w, int n_ip, int mode, double* Ke, fem_stream_t stream) {
+    if (mode != FEM_ISO_SUM && mode != FEM_ISO_STACK && mode != FEM_ISO_VOLUME) {
+        set_error("fem_iso_ke: unknown mode %d", mode);
+        return FEM_EARG;
+    }
     if (M <= 0) return FEM_OK;
     if (n_ip < 1 || n_ip > ISO_MAX_IP) {
         set_error("fem_iso_ke: n_ip = %d out of range [1, %d]", n_ip, ISO_MAX_IP);
@@ -970,6 +987,25 @@ int fem_iso_ke(const double* coords, const int64_t* conn, int64_t M, int npe, do
         case 8: hipLaunchKernelGGL(k_iso_ke<8>, g, dim3(256), 0, S(stream), coords, conn, M, E, nu, dN, w, n_ip, mode, Ke); break;
         case 10: hipLaunchKernelGGL(k_iso_ke<10>, g, dim3(256), 0, S(stream), coords, conn, M, E, nu, dN, w, n_ip, mode, Ke); break;
         default: set_error("fem_iso_ke: unsupported nodes per element %d", npe); return FEM_EBADTYPE;
+    }
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_iso_mass(const double* coords, const int64_t* conn, int64_t M, int npe, double rho, const double* Nv,
+                 const double* dN, const double* w, int n_ip, double* Me, fem_stream_t stream) {
+    if (M <= 0) return FEM_OK;
+    if (n_ip < 1 || n_ip > ISO_MAX_IP) {
+        set_error("fem_iso_mass: n_ip = %d out of range [1, %d]", n_ip, ISO_MAX_IP);
+        return FEM_EARG;
+    }
+    dim3 g((unsigned)cdiv(M, 4));
+    const int mode = FEM_ISO_MASS;
+    switch (npe) {
+        case 6: hipLaunchKernelGGL(k_iso_ke<6>, g, dim3(256), 0, S(stream), coords, conn, M, rho, 0.0, dN, w, n_ip, mode, Me, Nv); break;
+        case 8: hipLaunchKernelGGL(k_iso_ke<8>, g, dim3(256), 0, S(stream), coords, conn, M, rho, 0.0, dN, w, n_ip, mode, Me, Nv); break;
+        case 10: hipLaunchKernelGGL(k_iso_ke<10>, g, dim3(256), 0, S(stream), coords, conn, M, rho, 0.0, dN, w, n_ip, mode, Me, Nv); break;
+        default: set_error("fem_iso_mass: unsupported nodes per element %d", npe); return FEM_EBADTYPE;
     }
     FEM_LAUNCHED();
     return FEM_OK;

@@ -41,6 +41,8 @@ __all__ = [
     "compute_c3d6_K_matrix", "compute_wedge_volumes",
     "c3d10_integration_points", "compute_c3d10_Jacobian", "compute_c3d10_shape_gradients", "compute_c3d10_B_matrix",
     "compute_c3d10_K_matrix",
+    "mass_integration_points", "compute_c3d8_M_matrix", "compute_c3d6_M_matrix", "compute_c3d10_M_matrix",
+    "compute_M_matrix",
 ]
 
 
@@ -243,8 +245,63 @@ def _dn_c3d10(xi, eta, zeta):
             [-4 * zeta, -4 * zeta, 4 * (1 - xi - eta - 2 * zeta)]]
 
 
+def _n_c3d8(xi, eta, zeta):
+    # shape values matching _dn_c3d8's node order
+    return [0.125 * (1 + a * xi) * (1 + b * eta) * (1 + c * zeta)
+            for (a, b, c) in ((-1, -1, -1), (1, -1, -1), (1, 1, -1), (-1, 1, -1), (-1, -1, 1), (1, -1, 1), (1, 1, 1),
+                              (-1, 1, 1))]
+
+
+def _n_c3d6(r, s, t):
+    # shape values matching _dn_c3d6
+    L = 1 - r - s
+    return [0.5 * L * (1 - t), 0.5 * r * (1 - t), 0.5 * s * (1 - t), 0.5 * L * (1 + t), 0.5 * r * (1 + t),
+            0.5 * s * (1 + t)]
+
+
+def _n_c3d10(xi, eta, zeta):
+    # shape values matching _dn_c3d10 (corners xi, eta, zeta, L; mid-edges (0,1), (1,2), (2,0), (0,3), (1,3), (2,3))
+    L = 1 - xi - eta - zeta
+    return [xi * (2 * xi - 1), eta * (2 * eta - 1), zeta * (2 * zeta - 1), L * (2 * L - 1), 4 * xi * eta,
+            4 * eta * zeta, 4 * zeta * xi, 4 * xi * L, 4 * eta * L, 4 * zeta * L]
+
+
+def mass_integration_points(element_type, dtype=F64):
+    """Quadrature of the consistent mass (no reference: parity unpinned), exact for N_a N_b on affine elements:
+    c3d8 the 2x2x2 Gauss rule (w = 1, volume 8); c3d6 the degree-2 triangle rule (1/6, 1/6), (2/3, 1/6), (1/6, 2/3)
+    with weight 1/6 (sum = the triangle's 1/2, not the stiffness rule's 1/3 each, Q3) times 2-point Gauss in t;
+    c3d10 the 14-point degree-5 tetrahedron rule (weights sum to 1/6). Returns (points [n,3], weights [n])."""
+    et = element_type.lower()
+    if et == "c3d8":
+        return c3d8_integration_points(device="cpu", dtype=dtype)
+    if et == "c3d6":
+        g = 1.0 / 3.0 ** 0.5
+        tri = [(1 / 6, 1 / 6), (2 / 3, 1 / 6), (1 / 6, 2 / 3)]
+        pts = [(r, s_, t) for t in (-g, g) for (r, s_) in tri]
+        return torch.tensor(pts, dtype=dtype), torch.full((6,), 1.0 / 6.0, dtype=dtype)
+    if et == "c3d10":
+        a, b, c = 0.0927352503108912, 0.3108859192633006, 0.0455037041256496
+        wa, wb, wc = 0.0734930431163619 / 6, 0.1126879257180159 / 6, 0.0425460207770815 / 6
+        pts, ws = [], []
+        for x, wx in ((a, wa), (b, wb)):
+            for k in range(4):
+                bary = [x] * 4
+                bary[k] = 1 - 3 * x
+                pts.append(bary[:3])
+                ws.append(wx)
+        for i in range(4):
+            for j in range(i + 1, 4):
+                bary = [c] * 4
+                bary[i] = bary[j] = 0.5 - c
+                pts.append(bary[:3])
+                ws.append(wc)
+        return torch.tensor(pts, dtype=dtype), torch.tensor(ws, dtype=dtype)
+    _unsupported(element_type)
+
+
 _ISO = {"c3d8": (8, _dn_c3d8, c3d8_integration_points), "c3d6": (6, _dn_c3d6, c3d6_integration_points),
         "c3d10": (10, _dn_c3d10, c3d10_integration_points)}
+_N = {"c3d8": _n_c3d8, "c3d6": _n_c3d6, "c3d10": _n_c3d10}
 
 
 def _points_weights(etype, integral_point):
@@ -279,6 +336,52 @@ def _iso_ke(coords, elements, etype, E, nu, points, weights, mode, device, dtype
     C.check(lib.fem_iso_ke(C.ptr(coords), C.ptr(elements), M, npe, float(E), float(nu), C.ptr(dN), C.ptr(w), n_ip,
                            mode, C.ptr(K), C.stream(dev)), "fem_iso_ke")
     return _out(K, device, dtype)
+
+
+def _iso_mass(coords, elements, etype, rho, device, dtype):
+    lib = C.lib()
+    dev, coords, elements = _prep(coords, elements, device)
+    npe = _ISO[etype][0]
+    if elements.shape[1] != npe:
+        raise ValueError(f"{etype} expects {npe} nodes per element, got {elements.shape[1]}")
+    M = elements.shape[0]
+    p, w = mass_integration_points(etype)
+    dN = _dn_table(etype, p, dev)
+    Nv = torch.tensor([_N[etype](*[float(v) for v in p[q]]) for q in range(p.shape[0])], dtype=F64).to(dev)
+    w = w.to(dev, F64).contiguous()
+    d = 3 * npe
+    Me = torch.empty((M, d, d), dtype=F64, device=dev)
+    C.check(lib.fem_iso_mass(C.ptr(coords), C.ptr(elements), M, npe, float(rho), C.ptr(Nv.contiguous()), C.ptr(dN),
+                             C.ptr(w), p.shape[0], C.ptr(Me), C.stream(dev)), "fem_iso_mass")
+    return _out(Me, device, dtype)
+
+
+def compute_c3d8_M_matrix(coords, elements, rho, device="cuda:0", dtype=torch.float32):
+    """Consistent hex mass [M,24,24] = rho sum_q w_q |detJ_q| N_a N_b (x) I3, 2x2x2 Gauss. No reference function
+    (the notebook's `compute_c3d4_M_matrix`, `solver_example.ipynb:221`, is the only mass call): parity unpinned."""
+    return _iso_mass(coords, elements, "c3d8", rho, device, dtype)
+
+
+def compute_c3d6_M_matrix(coords, elements, rho, device="cuda:0", dtype=torch.float32):
+    """Consistent wedge mass [M,18,18] (3-point triangle x 2-point Gauss, mass_integration_points). Parity
+    unpinned."""
+    return _iso_mass(coords, elements, "c3d6", rho, device, dtype)
+
+
+def compute_c3d10_M_matrix(coords, elements, rho, device="cuda:0", dtype=torch.float32):
+    """Consistent P2 tet mass [M,30,30] (14-point degree-5 rule, |detJ|: the reference's node convention makes
+    detJ negative on VTK-positive tets, Q2). Parity unpinned."""
+    return _iso_mass(coords, elements, "c3d10", rho, device, dtype)
+
+
+def compute_M_matrix(coords, elements, element_type, rho, device="cuda:0", dtype=torch.float32):
+    """Consistent mass dispatch over c3d4 / c3d6 / c3d8 / c3d10 (ValueError otherwise, like compute_K_matrix)."""
+    et = element_type.lower()
+    if et == "c3d4":
+        return compute_c3d4_M_matrix(coords, elements, rho, device=device, dtype=dtype)
+    if et in _N:
+        return _iso_mass(coords, elements, et, rho, device, dtype)
+    _unsupported(element_type)
 
 
 def _iso_geom(coords, elements, etype, integral_point, what, device, dtype):

@@ -59,7 +59,7 @@ enum {
  * of fem_pcg_set_constraints after every x update */
 enum { FEM_MODE_CG_STABLE = 0, FEM_MODE_PCG = 1, FEM_MODE_CG_CONSTRAINED = 2 };
 enum { FEM_KIND_ELASTIC = 0, FEM_KIND_POISSON = 1, FEM_KIND_MASS = 2 };
-enum { FEM_ISO_SUM = 0, FEM_ISO_STACK = 1, FEM_ISO_VOLUME = 2 };
+enum { FEM_ISO_SUM = 0, FEM_ISO_STACK = 1, FEM_ISO_VOLUME = 2, FEM_ISO_MASS = 3 };
 
 const char* fem_last_error(void);                 /* [host] message of the last failing call */
 int fem_version(void);                            /* [host] ABI version (100 * major + minor) */
@@ -92,6 +92,13 @@ int fem_tet4_geom(const double* coords, const int64_t* conn, int64_t M, double* 
  * compute_c3d10_K_matrix (`:1191-1239`). */
 int fem_iso_ke(const double* coords, const int64_t* conn, int64_t M, int npe, double E, double nu,
                const double* dN, const double* w, int n_ip, int mode, double* Ke, fem_stream_t stream);
+/* fem_iso_mass: consistent mass of c3d8 / c3d6 / c3d10 (npe = 8 / 6 / 10) — no reference function exists (the
+ * reference notebook calls a compute_c3d4_M_matrix defined nowhere, `solver_example.ipynb:221`): parity unpinned.
+ *   Me[M, 3 npe, 3 npe], block (a,b) = rho sum_q w_q |detJ_q| N_a(q) N_b(q) I3
+ * Nv [n_ip, npe] shape values and dN [n_ip, npe, 3] natural derivatives at the n_ip (<= 32) points, w [n_ip] weights
+ * (element.py picks rules exact for N_a N_b on affine elements). */
+int fem_iso_mass(const double* coords, const int64_t* conn, int64_t M, int npe, double rho, const double* Nv,
+                 const double* dN, const double* w, int n_ip, double* Me, fem_stream_t stream);
 /* J [M,3,3] (J[i][k] = sum_j dN[j][i] x_j[k]), global gradients [M,npe,3] and B [M,6,3npe] of an isoparametric
  * element at one point with natural derivatives dN [npe,3]; outputs may be NULL. Replaces compute_c3d8_Jacobian /
  * _shape_gradients / _B_matrix (`solver/element.py:1601-1694`) and the c3d6 (`:2482-2568`) / c3d10

@@ -212,6 +212,21 @@ def iso_K(coords, elements, etype, E, nu, points=None, weights=None, single=True
     return K if K is not None else torch.stack(out, 0)
 
 
+def iso_mass(coords, elements, shape_values, shape_derivs, points, weights, rho):
+    """Consistent mass of an isoparametric element family (no reference function: parity unpinned; the GPU kernel's
+    specification restated): M_e = rho sum_q w_q |detJ_q| (N N^T)(q) (x) I3 -> [M, 3 npe, 3 npe]. shape_values /
+    shape_derivs: callables (xi, eta, zeta) -> N [npe] / dN [npe, 3] in the element's node order."""
+    M, npe = elements.shape
+    m = torch.zeros((M, npe, npe), dtype=F64)
+    for q in range(points.shape[0]):
+        pq = [float(v) for v in points[q]]
+        Nq = torch.tensor(shape_values(*pq), dtype=F64)
+        dN = torch.as_tensor(shape_derivs(*pq), dtype=F64)
+        detJ = torch.det(iso_jacobian(coords, elements, dN)).abs()
+        m = m + (float(weights[q]) * rho) * detJ.view(-1, 1, 1) * torch.outer(Nq, Nq).view(1, npe, npe)
+    return torch.kron(m, torch.eye(3, dtype=F64).view(1, 3, 3))
+
+
 # ----------------------------------------------------------------------------- stress recovery
 def stress_tensor(v):
     """Voigt [M,6] (xx, yy, zz, xy, yz, xz) -> [M,3,3]. `solver/element.py:308-330`."""

@@ -4,8 +4,9 @@
 Three separate boxes (P2/linear faces are nonconforming): c3d8 88^3 = 681,472 hexes, c3d6 2*70^3 =
 686,000 wedges, c3d10 6*48^3 = 663,552 quadratic tets (jittered). Per family: element stiffness through the
 reference API (compute_K_matrix, default rule, single=True) timed with events, then the global assembly (pattern +
-row-gather) of those matrices; plus the c3d4 consistent mass of the 10M cube (compute_c3d4_M_matrix, the only mass
-the reference calls). Output bytes per family give the write bandwidth; the oracle (reference op sequence on
+row-gather) of those matrices, then the consistent mass (compute_M_matrix: no reference function, parity unpinned)
+and its global assembly on the same pattern; plus the c3d4 consistent mass of the 10M cube (compute_c3d4_M_matrix,
+the only mass the reference's notebook calls). Output bytes per family give the write bandwidth; the oracle (reference op sequence on
 torch-CPU) element stiffness on a bounded sample gives the CPU baseline.
 
     python tools/bench_mixed.py [--cpu-sample 20000]
@@ -54,14 +55,18 @@ def main():
             ms_k, K = ev_ms(lambda: element.compute_K_matrix(c, el, et, E, NU, device=dev, dtype=F64))
             ms_g, g = ev_ms(lambda: system.build_graph(el, c.shape[0]))
             ms_a, A = ev_ms(lambda: system.SellMatrix(g, 3).add_element_matrices(K, el))
-            reps.append((ms_k, ms_g, ms_a))
+            del K
+            ms_m, Me = ev_ms(lambda: element.compute_M_matrix(c, el, et, RHO, device=dev, dtype=F64))
+            ms_ma, Am = ev_ms(lambda: system.SellMatrix(g, 3).add_element_matrices(Me, el))
+            reps.append((ms_k, ms_g, ms_a, ms_m, ms_ma))
             if len(reps) < 4:
-                del K, A, g
-        ms_k, ms_g, ms_a = (min(r[i] for r in reps[1:]) for i in range(3))
+                del Me, A, Am, g
+        ms_k, ms_g, ms_a, ms_m, ms_ma = (min(r[i] for r in reps[1:]) for i in range(5))
         out[et] = {"elements": int(el.shape[0]), "nodes": int(c.shape[0]), "Ke_ms": ms_k,
-                   "Ke_write_GBps": K.numel() * 8 / (ms_k * 1e-3) / 1e9, "pattern_ms": ms_g, "assemble_ms": ms_a,
-                   "nnz_blocks": g.nnz}
-        del K, A, g
+                   "Ke_write_GBps": Me.numel() * 8 / (ms_k * 1e-3) / 1e9, "pattern_ms": ms_g, "assemble_ms": ms_a,
+                   "Me_ms": ms_m, "Me_write_GBps": Me.numel() * 8 / (ms_m * 1e-3) / 1e9, "mass_assemble_ms": ms_ma,
+                   "total_mass": float(Am.vals.sum()) / 3, "nnz_blocks": g.nnz}
+        del Me, A, Am, g
         torch.cuda.empty_cache()
         print(json.dumps(out), flush=True)
     c, t = mesh.kuhn_cube(119, device=dev)
