@@ -392,7 +392,10 @@ constexpr int AW_WAVES = 4;   // waves per 256-thread block of the wave-per-row 
 #define FEM_KE_RPL3 1   // bs = 3 assembly from K_e: block rows per lane (3, one lane per column: c3d8 4.2 -> 5.1 ms)
 #endif
 
-template <int BS, int NPE, int RPL>
+// CSRW: the row sums (from zero) go to out in row-contiguous block-CSR order (block j of row i at
+// (rowptr[i] + j) BS^2, row-major) -- every wave writes a contiguous range -- and k_csr_add_sell adds them into the SELL
+// planes slice by slice; otherwise each owner lane read-modify-writes its SELL entry in place.
+template <int BS, int NPE, int RPL, bool CSRW = false>
 __global__ void __launch_bounds__(256) k_assemble_ke_w(const double* __restrict__ Ke, const int64_t* __restrict__ conn,
                                                        const int32_t* __restrict__ inc_ptr,
                                                        const int32_t* __restrict__ inc, int64_t N,
@@ -421,12 +424,19 @@ __global__ void __launch_bounds__(256) k_assemble_ke_w(const double* __restrict_
             double acc[RPL][BS];
             if (owner) {
                 myj = colidx[lo + j0 + jl];
-                Ei = csr2sell[lo + j0 + jl];
+                if constexpr (CSRW) {
 #pragma unroll
-                for (int rr = 0; rr < RPL; ++rr)
+                    for (int rr = 0; rr < RPL; ++rr)
 #pragma unroll
-                    for (int c = 0; c < BS; ++c)
-                        acc[rr][c] = vals[BS == 1 ? Ei : sell_val(Ei, BS * BS, (r0 + rr) * BS + c)];
+                        for (int c = 0; c < BS; ++c) acc[rr][c] = 0.0;
+                } else {
+                    Ei = csr2sell[lo + j0 + jl];
+#pragma unroll
+                    for (int rr = 0; rr < RPL; ++rr)
+#pragma unroll
+                        for (int c = 0; c < BS; ++c)
+                            acc[rr][c] = vals[BS == 1 ? Ei : sell_val(Ei, BS * BS, (r0 + rr) * BS + c)];
+                }
             }
             for (int k0 = 0; k0 < C; k0 += 64) {
                 const int nk = min(64, C - k0);
@@ -487,9 +497,43 @@ __global__ void __launch_bounds__(256) k_assemble_ke_w(const double* __restrict_
 #pragma unroll
                 for (int rr = 0; rr < RPL; ++rr)
 #pragma unroll
-                    for (int c = 0; c < BS; ++c)
-                        vals[BS == 1 ? Ei : sell_val(Ei, BS * BS, (r0 + rr) * BS + c)] = acc[rr][c];
+                    for (int c = 0; c < BS; ++c) {
+                        if constexpr (CSRW)
+                            vals[(int64_t)(lo + j0 + jl) * BS * BS + (r0 + rr) * BS + c] = acc[rr][c];
+                        else
+                            vals[BS == 1 ? Ei : sell_val(Ei, BS * BS, (r0 + rr) * BS + c)] = acc[rr][c];
+                    }
             }
+        }
+    }
+}
+
+// SELL planes += block-CSR row sums (k_assemble_ke_w<..., CSRW>): wave per slice, lane = row; for every (entry k,
+// block value rc) the 64 rows of the slice write one contiguous 512-byte plane segment, and each lane reads its own
+// row's blocks in order (row-contiguous in the block-CSR buffer). Padding entries are left untouched.
+template <int BS>
+__global__ void __launch_bounds__(256) k_csr_add_sell(const double* __restrict__ csr, const int32_t* __restrict__ rowptr,
+                                                      int64_t N, int64_t nslices, const int64_t* __restrict__ slice_ptr,
+                                                      double* __restrict__ vals) {
+    constexpr int B2 = BS * BS;
+    const int lane = threadIdx.x & 63;
+    for (int64_t s = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; s < nslices;
+         s += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+        const int64_t row = s * 64 + lane;
+        const int64_t p0 = slice_ptr[s];
+        int len = 0, rp = 0;
+        if (row < N) {
+            rp = rowptr[row];
+            len = rowptr[row + 1] - rp;
+        }
+        const double* src = csr + (int64_t)rp * B2;
+        double* dst = vals + p0 * B2 + lane;
+        for (int k = 0; k < len; ++k) {
+            double v[B2];
+#pragma unroll
+            for (int rc = 0; rc < B2; ++rc) v[rc] = src[(int64_t)k * B2 + rc];
+#pragma unroll
+            for (int rc = 0; rc < B2; ++rc) dst[((int64_t)k * B2 + rc) * 64] += v[rc];
         }
     }
 }
@@ -1014,9 +1058,33 @@ int fem_iso_mass(const double* coords, const int64_t* conn, int64_t M, int npe, 
 int fem_assemble_from_ke(const double* Ke, const int64_t* conn, int npe, int bs, const int32_t* inc_ptr,
                          const int32_t* inc, int64_t N, const int32_t* rowptr, const int32_t* colidx,
                          const int64_t* csr2sell, const int64_t* slice_ptr, double* vals, fem_stream_t stream) {
-    (void)slice_ptr;
     if ((bs == 1 || bs == 3) && (npe == 4 || npe == 6 || npe == 8 || npe == 10)) {   // wave per row
         const dim3 g((unsigned)grid_multiple_of_xcd(cdiv(N, AW_WAVES), 8192));
+        // bs = 3: row sums to a block-CSR buffer with contiguous per-wave writes, then one slice-coalesced add into
+        // the SELL planes (the in-place variant's scattered 8-byte plane updates measured 4.6x their bytes in
+        // WRITE_SIZE on c3d10); FEM355_KE_DIRECT=1 keeps the in-place kernel
+        static const bool direct = getenv("FEM355_KE_DIRECT") != nullptr;
+        if (bs == 3 && !direct && N > 0) {
+            int64_t nnz = 0;
+            FEM_HIP(hipMemcpyAsync(&nnz, rowptr + N, sizeof(int32_t), hipMemcpyDeviceToHost, S(stream)));
+            FEM_HIP(hipStreamSynchronize(S(stream)));
+            nnz &= 0xffffffffLL;
+            double* tmp = nullptr;
+            FEM_HIP(hipMallocAsync((void**)&tmp, sizeof(double) * 9 * (size_t)(nnz > 0 ? nnz : 1), S(stream)));
+#define FEM_KE_C(P)                                                                                             \
+    if (npe == P)                                                                                               \
+        hipLaunchKernelGGL((k_assemble_ke_w<3, P, FEM_KE_RPL3, true>), g, dim3(256), 0, S(stream), Ke, conn,     \
+                           inc_ptr, inc, N, rowptr, colidx, csr2sell, tmp);
+            FEM_KE_C(4) FEM_KE_C(6) FEM_KE_C(8) FEM_KE_C(10)
+#undef FEM_KE_C
+            FEM_LAUNCHED();
+            const int64_t ns = cdiv(N, 64);
+            hipLaunchKernelGGL(k_csr_add_sell<3>, dim3((unsigned)std::min<int64_t>(cdiv(ns, 4), 16384)), dim3(256), 0,
+                               S(stream), tmp, rowptr, N, ns, slice_ptr, vals);
+            FEM_LAUNCHED();
+            FEM_HIP(hipFreeAsync(tmp, S(stream)));
+            return FEM_OK;
+        }
 #define FEM_KE_W(B, P)                                                                                          \
     if (bs == B && npe == P)                                                                                    \
         hipLaunchKernelGGL((k_assemble_ke_w<B, P, (B == 3 ? FEM_KE_RPL3 : 1)>), g, dim3(256), 0, S(stream), Ke,  \
@@ -1044,13 +1112,13 @@ int fem_assemble_tet4(const double* coords, const int64_t* conn, double E, doubl
                       const int32_t* inc, int64_t N, const int32_t* rowptr, const int32_t* colidx,
                       const int64_t* csr2sell, const int64_t* slice_ptr, double* vals, int64_t* bad_idx,
                       fem_stream_t stream) {
-    (void)slice_ptr;
     // wave per row (k_assemble_p1w / k_assemble_el3w); the thread-per-row k_assemble_tet4 and the first wave
     // version k_assemble_tet4w stay as reference formulations
     const dim3 g((unsigned)grid_multiple_of_xcd(cdiv(N, AW_WAVES), 8192));
     if (bs == 1)
         hipLaunchKernelGGL(k_assemble_p1w<FEM_P1_LPR>, g, dim3(256), 0, S(stream), coords, conn, E, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals, bad_idx);
-    else if (bs == 3)
+    else if (bs == 3)   // in place: the block-CSR staging of fem_assemble_from_ke measured slower here (6.7 vs 6.1
+                        // ms on 10M tets: this kernel is bound by forming the element blocks, not by its writes)
         hipLaunchKernelGGL(k_assemble_el3w, g, dim3(256), 0, S(stream), coords, conn, E, nu, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals, bad_idx);
     else {
         set_error("fem_assemble_tet4: block size %d unsupported", bs);

@@ -44,9 +44,10 @@ def main():
         e3 = ev()
         w = A.jacobi(torch.zeros(A.n, dtype=torch.uint8, device=dev))
         torch.cuda.synchronize()
+        bits = int(A.vals.view(torch.int64).sum())
         wall = (time.perf_counter() - h0) * 1e3
         out.append({"graph_ms": e0.elapsed_time(e1), "alloc_ms": e1.elapsed_time(e2), "assemble_ms": e2.elapsed_time(e3),
-                    "wall_ms_incl_jacobi": wall})
+                    "wall_ms_incl_jacobi": wall, "vals_bits": bits})
         del w
         del A, g
     print(json.dumps(out))
