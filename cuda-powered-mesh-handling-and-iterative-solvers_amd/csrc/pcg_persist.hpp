@@ -94,9 +94,11 @@ __device__ __forceinline__ double pk_sum(const double* part, int n) {
 // (and pg when given) by wave 0 alone, handed to the other waves through LDS (out[0], out[1]). One wave per
 // workgroup reads the G partials instead of all 16 (4,096 waves loading the same 4 KB with sc1 loads queue on the
 // memory channels that hold those lines).
+// entry_sync = false: the caller's own workgroup barrier (pk_block_sum's) already separates every wave's prior work
 __device__ __forceinline__ bool pk_barrier(unsigned* sy, int grp, unsigned nper, unsigned e, int* lds_ok,
-                                           const double* pd, const double* pg, int G, double* out) {
-    __syncthreads();
+                                           const double* pd, const double* pg, int G, double* out,
+                                           bool entry_sync = true) {
+    if (entry_sync) __syncthreads();
     if (threadIdx.x < 64) {
         int okv = 0;
         if (threadIdx.x == 0) {
@@ -208,8 +210,9 @@ struct PkArgs {
 // rank). Banked by epoch parity: a rank announces e + 2 only after all ranks announced e + 1, i.e. after every
 // reader of bank e is done. The give-up word records 3 + 16 e.
 __device__ __forceinline__ bool pk_barrier_dist(const PkArgs& a, unsigned* sy, int grp, unsigned nper, unsigned e,
-                                                int* lds_ok, const double* pd, const double* pg, int G, double* out) {
-    __syncthreads();
+                                                int* lds_ok, const double* pd, const double* pg, int G, double* out,
+                                                bool entry_sync = true) {
+    if (entry_sync) __syncthreads();
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
         unsigned* tmo = sy + PK_TMO;
@@ -585,8 +588,9 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
             const double dsum = pk_block_sum(dp, lds16);
             PK_MARK(2);
             if (threadIdx.x == 0) __hip_atomic_store(pd + L, dsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (!(DIST ? pk_barrier_dist(a, sy, grp, nper, e, &lds_ok, pd, k > 0 ? pd + G : nullptr, G, lds_dg)
-                       : pk_barrier(sy, grp, nper, e, &lds_ok, pd, k > 0 ? pd + G : nullptr, G, lds_dg))) {
+            // (pk_block_sum ended on a workgroup barrier: the grid barrier needs no entry barrier of its own)
+            if (!(DIST ? pk_barrier_dist(a, sy, grp, nper, e, &lds_ok, pd, k > 0 ? pd + G : nullptr, G, lds_dg, false)
+                       : pk_barrier(sy, grp, nper, e, &lds_ok, pd, k > 0 ? pd + G : nullptr, G, lds_dg, false))) {
                 fail = true;
                 break;
             }

@@ -102,7 +102,7 @@ def check_connectivity(elements: torch.Tensor, n_nodes: int):
     reference's torch indexing raises IndexError on such input). One device reduction + sync."""
     if elements.numel() == 0:
         return
-    lo, hi = (int(v) for v in torch.aminmax(elements))
+    lo, hi = (int(v) for v in torch.stack(torch.aminmax(elements)).cpu())   # one device-to-host copy
     if lo < 0 or hi >= n_nodes:
         raise IndexError(f"element connectivity references node {lo if lo < 0 else hi}, outside [0, {n_nodes})")
 
@@ -151,21 +151,24 @@ def _build_graph(elements, n_nodes, compress):
     rowptr = torch.empty(n_nodes + 1, dtype=I32, device=dev)
     work = torch.empty(int(lib.fem_scan_work_len(n_nodes)) + 1, dtype=I32, device=dev)
     C.check(lib.fem_scan_i32(C.ptr(row_len), n_nodes, C.ptr(rowptr), C.ptr(work), st), "fem_scan_i32")
-    nnz = int(row_len.sum(dtype=I64))                              # the one sync of the pattern build
-    if nnz >= 2**31:   # int32 row pointers / column slots
-        raise ValueError(f"fem355: {nnz} node-graph entries exceed the int32 pattern (split the mesh over GPUs)")
-    colidx = torch.empty(nnz, dtype=I32, device=dev)
-    diagpos = torch.empty(n_nodes, dtype=I32, device=dev)
-    C.check(lib.fem_graph_fill2(C.ptr(elements), npe, C.ptr(inc_ptr), C.ptr(inc), n_nodes, C.ptr(rowptr), C.ptr(tmp),
-                                C.ptr(colidx), C.ptr(diagpos), st), "fem_graph_fill2")
-    del tmp
+    # the SELL slice widths need only the row lengths: both sizes come back in ONE device-to-host copy
     ns = (n_nodes + 63) // 64
     width = torch.empty(ns, dtype=I64, device=dev)
     C.check(lib.fem_sell_widths(C.ptr(rowptr), n_nodes, C.ptr(width), st), "fem_sell_widths")
     slice_ptr = torch.empty(ns + 1, dtype=I64, device=dev)
     work64 = torch.empty(int(lib.fem_scan_work_len(ns)) + 1, dtype=I64, device=dev)
     C.check(lib.fem_scan_i64(C.ptr(width), ns, C.ptr(slice_ptr), C.ptr(work64), st), "fem_scan_i64")
-    ent = int(slice_ptr[-1].item())
+    nnz, ent = (int(v) for v in torch.stack([rowptr[-1].to(I64), slice_ptr[-1]]).cpu())   # the sync of the build
+    # int32 row pointers / column slots: the int32 scan would wrap past 2^31 entries; the int64 slice scan cannot
+    # (per-row lengths stay exact under wrap-around), and nnz <= ent
+    if ent >= 2**31:
+        raise ValueError(f"fem355: {ent} SELL entries (>= node-graph entries) exceed the int32 pattern "
+                         "(split the mesh over GPUs)")
+    colidx = torch.empty(nnz, dtype=I32, device=dev)
+    diagpos = torch.empty(n_nodes, dtype=I32, device=dev)
+    C.check(lib.fem_graph_fill2(C.ptr(elements), npe, C.ptr(inc_ptr), C.ptr(inc), n_nodes, C.ptr(rowptr), C.ptr(tmp),
+                                C.ptr(colidx), C.ptr(diagpos), st), "fem_graph_fill2")
+    del tmp
     cols = torch.empty(ent, dtype=I32, device=dev)
     csr2sell = torch.empty(max(nnz, 1), dtype=I64, device=dev)
     C.check(lib.fem_sell_fill(C.ptr(rowptr), C.ptr(colidx), n_nodes, C.ptr(slice_ptr), C.ptr(cols),
