@@ -51,6 +51,12 @@ def parse():
     ap.add_argument("--rtol", type=float, default=1e-8)
     ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--elastic", type=int, default=1,
+                    help="poisson runs: also measure the 10M-tet linear-elasticity system (BASELINE configs[2]/[3]) "
+                         "with the same steps, reported under \"elasticity\" in the same JSON line")
+    ap.add_argument("--elastic-timeout", type=float, default=240.0,
+                    help="seconds the elasticity companion may take before the line is printed without it")
+    ap.add_argument("--cpu-iters-elastic", type=int, default=2)
     ap.add_argument("--schedule", type=int, default=None, help="PCG kernel schedule (0 three-kernel, 1 fused, 2 deferred, 3 persistent; "
                     "default: persistent for bs=1, three-kernel for bs=3)")
     ap.add_argument("--graph", type=int, default=0, help="capture k iterations per hipGraph (0 = plain launches)")
@@ -136,8 +142,28 @@ def main():
     sync()
 
     coords, tets = mesh.kuhn_cube(a.n, device=dev)
+    out = measure(a, a.kind, coords, tets, dev)
+    if not a.no_cpu_baseline and rank == 0:
+        out["cpu_baseline"] = cpu_baseline(a.n, a.kind, a.cpu_iters)
+    # BASELINE configs[2] beside the metric: the same steps on the 10M-tet linear-elasticity system (north_star:
+    # CG it/s on elasticity at 1/2/4/8 GPUs), its own CPU-oracle sample; a failure is reported, never fatal
+    if a.kind == "poisson" and a.elastic:
+        from fem355 import dist
+
+        def companion():
+            d = measure(a, "elastic", coords, tets, dev)
+            if not a.no_cpu_baseline:
+                d["cpu_baseline"] = cpu_baseline(a.n, "elastic", a.cpu_iters_elastic)
+            return d
+        out = dist.guarded_companion(out, "elasticity", companion, rank=0, timeout=a.elastic_timeout)
+    print(json.dumps(out), flush=True)
+
+
+def measure(a, kind, coords, tets, dev):
+    """One single-GPU measurement of `kind` on the mesh: DOFs/s (assembly + solve to rtol, two passes) and the
+    fixed-iteration CG it/s with its roofline. Returns the bench dict (cpu_baseline None)."""
     M, N = tets.shape[0], coords.shape[0]
-    if a.kind == "poisson":
+    if kind == "poisson":
         f, fixed = mesh.cube_poisson_case(coords)
         E, nu = 1.0, 0.0
     else:
@@ -151,7 +177,7 @@ def main():
     # pattern, the values, the Jacobi weights and the whole solve are recomputed from the mesh)
     def assemble_and_solve():
         t0 = time.perf_counter()
-        A = system.assemble_tet4_system(coords, tets, a.kind, E, nu)
+        A = system.assemble_tet4_system(coords, tets, kind, E, nu)
         mask = torch.zeros((N, A.bs), dtype=torch.uint8, device=dev)
         mask[fixed] = 1
         w = A.jacobi(mask.view(-1))
@@ -206,7 +232,7 @@ def main():
     alg = A.algorithmic_bytes_spmv(index_total=idx_total if (persist and n_uni) else None)
     achieved = alg / (spmv_ms * 1e-3) / 1e9
     ceiling = system.stream_ceiling(dev)
-    workload_key = f"kuhn{a.n}_{a.kind}"
+    workload_key = f"kuhn{a.n}_{kind}"
     out = {
         "metric": METRIC,
         "value": a.steps / dt,
@@ -220,7 +246,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
-        "config": {"workload": f"{M:,}-tet P1 {a.kind} Kuhn cube n={a.n}, Jacobi-PCG fixed iterations",
+        "config": {"workload": f"{M:,}-tet P1 {kind} Kuhn cube n={a.n}, Jacobi-PCG fixed iterations",
                    "tets": M, "nodes": N, "dofs": A.n, "nnz_blocks": A.g.nnz, "format": "SELL-64 fp64 values, " + ("int16 column deltas" if A.use16 else "int32 cols")
                    + (f", slice-uniform deltas in {n_uni} of {n_sl} slices" if (persist and n_uni) else ""),
                    "parallelism": "single GPU"},
@@ -242,9 +268,7 @@ def main():
                      "stream_ceiling_GBps": ceiling, "frac_of_stream_read": achieved / ceiling["read"]},
         "cpu_baseline": None,
     }
-    if not a.no_cpu_baseline and rank == 0:
-        out["cpu_baseline"] = cpu_baseline(a.n, a.kind, a.cpu_iters)
-    print(json.dumps(out), flush=True)
+    return out
 
 
 if __name__ == "__main__":

@@ -410,9 +410,45 @@ def init_comm(rank, world):
     return comm
 
 
+COMPANION_DROP = ("metric", "n_gpus", "higher_is_better", "scaling", "vs_baseline", "dtype", "data")
+
+
+def guarded_companion(out, key, fn, rank=0, timeout=240.0):
+    """out[key] = fn() minus the line-level keys (a companion measurement inside the ONE bench JSON line). An
+    exception is recorded as {"error": ...}; a watchdog bounds the time: when fn() has not returned after `timeout`
+    seconds (e.g. a collective that never completes), rank 0 prints `out` as it stands (the metric measured before
+    the companion) and every rank exits, so the companion can never cost the metric line."""
+    import threading
+
+    def fire():
+        if rank == 0 and out is not None:
+            out[key] = {"error": f"timed out after {timeout:.0f} s"}
+            print(json.dumps(out), flush=True)
+        sys.stderr.write(f"[rank {rank}] {key} companion timed out after {timeout:.0f} s\n")
+        sys.stderr.flush()
+        os._exit(0)
+
+    timer = threading.Timer(timeout, fire)
+    timer.daemon = True
+    timer.start()
+    try:
+        d = fn()
+        sub = None if d is None else {k: v for k, v in d.items() if k not in COMPANION_DROP}
+    except Exception as e:   # noqa: BLE001 -- reported in the line; the metric above it stands
+        sub = {"error": f"{type(e).__name__}: {e}"}
+        sys.stderr.write(f"[rank {rank}] {key} companion failed: {sub['error']}\n")
+    finally:
+        timer.cancel()
+    if out is not None:
+        out[key] = sub
+    return out
+
+
 def bench_main(a, metric):
-    """bench.py for N > 1 ranks (one per GPU): the 10M-tet system element-partitioned over the ranks (strong
-    scaling); value = CG iterations/s of the global system, max time over ranks."""
+    """bench.py for N > 1 ranks (one per GPU), strong scaling of the 10M-tet system: Poisson on the persistent
+    multi-GPU schedule (rows partitioned, in-kernel hand-offs; RCCL element partition if its self-check fails),
+    elasticity on the RCCL element partition; value = CG iterations/s of the global system, max time over ranks.
+    Poisson runs also measure the elasticity system (BASELINE configs[3]) under "elasticity" in the same line."""
     import torch.distributed as tdist
     world = int(os.environ["WORLD_SIZE"])
     rank = int(os.environ["RANK"])
@@ -427,21 +463,38 @@ def bench_main(a, metric):
     tdist.init_process_group("gloo", rank=rank, world_size=world)
     C.lib()
     path = getattr(a, "dist_path", "auto")
+    out, comm, done = None, None, False
     if a.kind == "poisson" and path in ("auto", "persist"):
         from . import dist_persist
         try:
-            done = dist_persist.bench_persist(a, metric, rank, world, dev, tdist, same_gpu=same_gpu)
+            done, out = dist_persist.bench_persist(a, metric, rank, world, dev, tdist, same_gpu=same_gpu)
         except C.FemError as e:   # raised on every rank alike (dist_persist.connect agrees before raising)
             print(f"[rank {rank}] persistent multi-GPU schedule unavailable: {e}", file=sys.stderr, flush=True)
             done = False
-        if done:
-            tdist.barrier()
-            tdist.destroy_process_group()
-            return
-        if same_gpu or path == "persist":
+        if not done and (same_gpu or path == "persist"):
             raise RuntimeError("persistent multi-GPU schedule failed (no RCCL fallback requested / possible)")
-    comm = init_comm(rank, world)
+    if not done:
+        comm = init_comm(rank, world)
+        out = rccl_measure(a, a.kind, comm, rank, world, dev, tdist, metric)
+    if a.kind == "poisson" and getattr(a, "elastic", 0) and not same_gpu:
+        def companion():
+            nonlocal comm
+            if comm is None:
+                comm = init_comm(rank, world)
+            return rccl_measure(a, "elastic", comm, rank, world, dev, tdist, metric)
+        out = guarded_companion(out, "elasticity", companion, rank=rank,
+                                timeout=float(getattr(a, "elastic_timeout", 240.0)))
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if comm is not None:
+        C.check(C.lib().fem_comm_destroy(comm), "fem_comm_destroy")
+    tdist.barrier()
+    tdist.destroy_process_group()
 
+
+def rccl_measure(a, kind, comm, rank, world, dev, tdist, metric):
+    """The RCCL element-partition measurement of `kind` on the n-cube (every rank calls it); returns the bench
+    dict on rank 0, None elsewhere."""
     def barrier_sync():
         torch.cuda.synchronize()
         tdist.barrier()
@@ -453,7 +506,7 @@ def bench_main(a, metric):
 
     coords, tets = _mesh.kuhn_cube(a.n, device=dev)
     N = coords.shape[0]
-    if a.kind == "poisson":
+    if kind == "poisson":
         f, fixed = _mesh.cube_poisson_case(coords)
         E, nu = 1.0, 0.0
     else:
@@ -463,7 +516,7 @@ def bench_main(a, metric):
     # connections (set up on the first collective) with the whole setup on a small cube
     c0, t0_ = _mesh.kuhn_cube(8, device=dev)
     p0 = rcb_partition(element_centroids(c0, t0_), world)
-    d0 = DistSystem(c0, t0_, p0, rank, world, a.kind, E, nu, comm)
+    d0 = DistSystem(c0, t0_, p0, rank, world, kind, E, nu, comm)
     d0.jacobi(torch.zeros(d0.n, dtype=torch.uint8, device=dev))
     wbuf = torch.ones(1 << 16, dtype=F64, device=dev)
     C.check(C.lib().fem_allreduce_sum(comm, C.ptr(wbuf), wbuf.numel(), C.stream(dev)), "fem_allreduce_sum")
@@ -477,7 +530,7 @@ def bench_main(a, metric):
     sharing = node_sharing(tets, part, world, N, touch)
     torch.cuda.synchronize()
     stages["partition_ms"] = (time.perf_counter() - t0) * 1e3
-    ds = DistSystem(coords, tets, part, rank, world, a.kind, E, nu, comm, sharing, touch)
+    ds = DistSystem(coords, tets, part, rank, world, kind, E, nu, comm, sharing, touch)
     torch.cuda.synchronize()
     stages["rank_mesh_assembly_ms"] = (time.perf_counter() - t0) * 1e3 - stages["partition_ms"]
     bs = ds.bs
@@ -570,7 +623,7 @@ def bench_main(a, metric):
             "metric": metric, "value": a.steps / dt, "unit": "CG iterations/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": f"{tets.shape[0]:,}-tet P1 {a.kind} Kuhn cube n={a.n}, Jacobi-PCG fixed "
+            "config": {"workload": f"{tets.shape[0]:,}-tet P1 {kind} Kuhn cube n={a.n}, Jacobi-PCG fixed "
                                    f"iterations, element-partitioned (RCB) over {world} GPUs, "
                                    + ("RCCL neighbour send/recv of [r.z, u.Au | shared rows] with every other rank"
                                       " (single reduction: one grouped exchange per iteration)"
@@ -596,7 +649,5 @@ def bench_main(a, metric):
                          "frac_of_stream_read": achieved / ceiling["read"]},
             "cpu_baseline": None,
         }
-        print(json.dumps(out), flush=True)
-    C.check(C.lib().fem_comm_destroy(comm), "fem_comm_destroy")
-    tdist.barrier()
-    tdist.destroy_process_group()
+        return out
+    return None

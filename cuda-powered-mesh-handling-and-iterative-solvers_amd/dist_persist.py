@@ -292,8 +292,8 @@ def disconnect(opened, dev):
 def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False):
     """bench.py at N > 1 on the persistent multi-GPU schedule: the 10M-tet Poisson system row-partitioned over the
     ranks (strong scaling), self-checked against the single-GPU solve on rank 0's GPU before it is timed. Returns
-    False (nothing printed) when the check fails, so the caller can measure the RCCL path instead."""
-    import json
+    (True, the bench dict on rank 0 / None elsewhere), or (False, None) when the check fails, so the caller can
+    measure the RCCL path instead."""
     import os
     import sys
     import time
@@ -413,7 +413,7 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False):
               flush=True)
     if not verdict[0]:
         print(f"[rank {rank}] measuring the RCCL path instead", file=sys.stderr, flush=True)
-        return False
+        return False, None
 
     # fixed-iteration timing: W warm-up steps, then exactly K steps as one launch per rank, max over ranks
     run = RankRunner(rs, b, split, rank, world, tol=0.0, grid=grid, stream=stream(), fine=fine)
@@ -443,6 +443,7 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False):
     alg_total = tsum(float(alg_own))
     run.close()
     ok_steps = it2 == a.warmup + a.steps and stt2 == C.PCG_RUNNING
+    out = None
     if rank == 0:
         per_it = ms_max * 1e-3 / a.steps
         achieved = alg_own / per_it / 1e9
@@ -470,8 +471,7 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False):
                          "stream_ceiling_GBps": ceiling, "frac_of_stream_read": achieved / ceiling["read"]},
             "cpu_baseline": None,
         }
-        print(json.dumps(out), flush=True)
     if raw_stream:
         torch.cuda.synchronize(dev)
         lib.fem_stream_destroy(ctypes.c_void_p(raw_stream))
-    return True
+    return True, out
