@@ -154,7 +154,7 @@ __global__ void __launch_bounds__(256) k_iso_geom(const double* __restrict__ X, 
 constexpr int ISO_MAX_IP = 32;
 constexpr int ISO_IPC = 16;   // points whose geometry is staged in LDS at once
 
-template <int NPE>
+template <int NPE, bool MASS>
 __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, const int64_t* __restrict__ conn,
                                                 int64_t M, double E, double nu, const double* __restrict__ dN,
                                                 const double* __restrict__ w, int n_ip, int mode,
@@ -170,15 +170,17 @@ __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, co
     constexpr bool SYM = NPE * NPE > 64;
     constexpr int NS = SYM ? NPE * (NPE + 1) / 2 : NPE * NPE;
     static_assert(NS <= 64, "one block per lane");
-    __shared__ double dn_s[ISO_MAX_IP * NPE * 3];
+    // rule tables in dynamic LDS sized to the rule (n_ip NPE 3 natural derivatives, then n_ip NPE shape values)
+    extern __shared__ double iso_dyn[];
+    double* dn_s = iso_dyn;
+    double* nv_s = iso_dyn + n_ip * NPE * 3;
     __shared__ double x_s[4][NPE][3];
     // point gradients of the current chunk; after the last chunk the same space stages the element matrix so
     // that the wave writes it out as contiguous 16-byte stores
     constexpr int GK = (ISO_IPC * NPE * 3 > D * D) ? ISO_IPC * NPE * 3 : D * D;
     __shared__ double gk_s[4][GK];
     __shared__ double c_s[4][ISO_IPC];
-    __shared__ double nv_s[ISO_MAX_IP * NPE];
-    const bool mass = mode == FEM_ISO_MASS;
+    constexpr bool mass = MASS;   // mode == FEM_ISO_MASS
     for (int t = threadIdx.x; t < n_ip * NPE * 3; t += 256) dn_s[t] = dN[t];
     if (mass)
         for (int t = threadIdx.x; t < n_ip * NPE; t += 256) nv_s[t] = Nv[t];
@@ -511,7 +513,9 @@ __global__ void __launch_bounds__(256) k_assemble_ke_w(const double* __restrict_
 // SELL planes += block-CSR row sums (k_assemble_ke_w<..., CSRW>): wave per slice, lane = row; for every (entry k,
 // block value rc) the 64 rows of the slice write one contiguous 512-byte plane segment, and each lane reads its own
 // row's blocks in order (row-contiguous in the block-CSR buffer). Padding entries are left untouched.
-template <int BS>
+// STORE: the SELL values were never written (fresh matrix): the row sums are stored (0 + s == s bit for bit: the
+// sums start from +0.0, so none is -0.0) and the padding entries zeroed -- no memset of the matrix, no read of it.
+template <int BS, bool STORE = false>
 __global__ void __launch_bounds__(256) k_csr_add_sell(const double* __restrict__ csr, const int32_t* __restrict__ rowptr,
                                                       int64_t N, int64_t nslices, const int64_t* __restrict__ slice_ptr,
                                                       double* __restrict__ vals) {
@@ -533,7 +537,16 @@ __global__ void __launch_bounds__(256) k_csr_add_sell(const double* __restrict__
 #pragma unroll
             for (int rc = 0; rc < B2; ++rc) v[rc] = src[(int64_t)k * B2 + rc];
 #pragma unroll
-            for (int rc = 0; rc < B2; ++rc) dst[((int64_t)k * B2 + rc) * 64] += v[rc];
+            for (int rc = 0; rc < B2; ++rc) {
+                if constexpr (STORE) dst[((int64_t)k * B2 + rc) * 64] = v[rc];
+                else dst[((int64_t)k * B2 + rc) * 64] += v[rc];
+            }
+        }
+        if constexpr (STORE) {
+            const int w = (int)((slice_ptr[s + 1] - p0) >> 6);
+            for (int k = len; k < w; ++k)
+#pragma unroll
+                for (int rc = 0; rc < B2; ++rc) dst[((int64_t)k * B2 + rc) * 64] = 0.0;
         }
     }
 }
@@ -1026,10 +1039,11 @@ int fem_iso_ke(const double* coords, const int64_t* conn, int64_t M, int npe, do
         return FEM_EARG;
     }
     dim3 g((unsigned)cdiv(M, 4));
+    const size_t lds = sizeof(double) * (size_t)n_ip * npe * 3;
     switch (npe) {
-        case 6: hipLaunchKernelGGL(k_iso_ke<6>, g, dim3(256), 0, S(stream), coords, conn, M, E, nu, dN, w, n_ip, mode, Ke); break;
-        case 8: hipLaunchKernelGGL(k_iso_ke<8>, g, dim3(256), 0, S(stream), coords, conn, M, E, nu, dN, w, n_ip, mode, Ke); break;
-        case 10: hipLaunchKernelGGL(k_iso_ke<10>, g, dim3(256), 0, S(stream), coords, conn, M, E, nu, dN, w, n_ip, mode, Ke); break;
+        case 6: hipLaunchKernelGGL((k_iso_ke<6, false>), g, dim3(256), lds, S(stream), coords, conn, M, E, nu, dN, w, n_ip, mode, Ke); break;
+        case 8: hipLaunchKernelGGL((k_iso_ke<8, false>), g, dim3(256), lds, S(stream), coords, conn, M, E, nu, dN, w, n_ip, mode, Ke); break;
+        case 10: hipLaunchKernelGGL((k_iso_ke<10, false>), g, dim3(256), lds, S(stream), coords, conn, M, E, nu, dN, w, n_ip, mode, Ke); break;
         default: set_error("fem_iso_ke: unsupported nodes per element %d", npe); return FEM_EBADTYPE;
     }
     FEM_LAUNCHED();
@@ -1045,10 +1059,11 @@ int fem_iso_mass(const double* coords, const int64_t* conn, int64_t M, int npe, 
     }
     dim3 g((unsigned)cdiv(M, 4));
     const int mode = FEM_ISO_MASS;
+    const size_t lds = sizeof(double) * (size_t)n_ip * npe * 4;
     switch (npe) {
-        case 6: hipLaunchKernelGGL(k_iso_ke<6>, g, dim3(256), 0, S(stream), coords, conn, M, rho, 0.0, dN, w, n_ip, mode, Me, Nv); break;
-        case 8: hipLaunchKernelGGL(k_iso_ke<8>, g, dim3(256), 0, S(stream), coords, conn, M, rho, 0.0, dN, w, n_ip, mode, Me, Nv); break;
-        case 10: hipLaunchKernelGGL(k_iso_ke<10>, g, dim3(256), 0, S(stream), coords, conn, M, rho, 0.0, dN, w, n_ip, mode, Me, Nv); break;
+        case 6: hipLaunchKernelGGL((k_iso_ke<6, true>), g, dim3(256), lds, S(stream), coords, conn, M, rho, 0.0, dN, w, n_ip, mode, Me, Nv); break;
+        case 8: hipLaunchKernelGGL((k_iso_ke<8, true>), g, dim3(256), lds, S(stream), coords, conn, M, rho, 0.0, dN, w, n_ip, mode, Me, Nv); break;
+        case 10: hipLaunchKernelGGL((k_iso_ke<10, true>), g, dim3(256), lds, S(stream), coords, conn, M, rho, 0.0, dN, w, n_ip, mode, Me, Nv); break;
         default: set_error("fem_iso_mass: unsupported nodes per element %d", npe); return FEM_EBADTYPE;
     }
     FEM_LAUNCHED();
@@ -1058,17 +1073,34 @@ int fem_iso_mass(const double* coords, const int64_t* conn, int64_t M, int npe, 
 int fem_assemble_from_ke(const double* Ke, const int64_t* conn, int npe, int bs, const int32_t* inc_ptr,
                          const int32_t* inc, int64_t N, const int32_t* rowptr, const int32_t* colidx,
                          const int64_t* csr2sell, const int64_t* slice_ptr, double* vals, fem_stream_t stream) {
+    return fem_assemble_from_ke_ex(Ke, conn, npe, bs, inc_ptr, inc, N, rowptr, colidx, csr2sell, slice_ptr, -1, -1, 0,
+                                   vals, stream);
+}
+
+int fem_assemble_from_ke_ex(const double* Ke, const int64_t* conn, int npe, int bs, const int32_t* inc_ptr,
+                            const int32_t* inc, int64_t N, const int32_t* rowptr, const int32_t* colidx,
+                            const int64_t* csr2sell, const int64_t* slice_ptr, int64_t nnz, int64_t ent, int store,
+                            double* vals, fem_stream_t stream) {
+    if (store && ent < 0) {
+        set_error("fem_assemble_from_ke_ex: store mode needs the SELL entry count");
+        return FEM_EARG;
+    }
+    const bool csrw = bs == 3 && getenv("FEM355_KE_DIRECT") == nullptr && N > 0 &&
+                      (npe == 4 || npe == 6 || npe == 8 || npe == 10);
+    // store mode on the paths that add in place: zero the matrix first (the block-CSR path stores every entry)
+    if (store && !csrw && ent > 0) FEM_HIP(hipMemsetAsync(vals, 0, sizeof(double) * bs * bs * (size_t)ent, S(stream)));
     if ((bs == 1 || bs == 3) && (npe == 4 || npe == 6 || npe == 8 || npe == 10)) {   // wave per row
         const dim3 g((unsigned)grid_multiple_of_xcd(cdiv(N, AW_WAVES), 8192));
         // bs = 3: row sums to a block-CSR buffer with contiguous per-wave writes, then one slice-coalesced add into
         // the SELL planes (the in-place variant's scattered 8-byte plane updates measured 4.6x their bytes in
         // WRITE_SIZE on c3d10); FEM355_KE_DIRECT=1 keeps the in-place kernel
-        static const bool direct = getenv("FEM355_KE_DIRECT") != nullptr;
-        if (bs == 3 && !direct && N > 0) {
-            int64_t nnz = 0;
-            FEM_HIP(hipMemcpyAsync(&nnz, rowptr + N, sizeof(int32_t), hipMemcpyDeviceToHost, S(stream)));
-            FEM_HIP(hipStreamSynchronize(S(stream)));
-            nnz &= 0xffffffffLL;
+        if (csrw) {
+            if (nnz < 0) {   // not given: one device-to-host read of rowptr[N]
+                nnz = 0;
+                FEM_HIP(hipMemcpyAsync(&nnz, rowptr + N, sizeof(int32_t), hipMemcpyDeviceToHost, S(stream)));
+                FEM_HIP(hipStreamSynchronize(S(stream)));
+                nnz &= 0xffffffffLL;
+            }
             double* tmp = nullptr;
             FEM_HIP(hipMallocAsync((void**)&tmp, sizeof(double) * 9 * (size_t)(nnz > 0 ? nnz : 1), S(stream)));
 #define FEM_KE_C(P)                                                                                             \
@@ -1079,8 +1111,12 @@ int fem_assemble_from_ke(const double* Ke, const int64_t* conn, int npe, int bs,
 #undef FEM_KE_C
             FEM_LAUNCHED();
             const int64_t ns = cdiv(N, 64);
-            hipLaunchKernelGGL(k_csr_add_sell<3>, dim3((unsigned)std::min<int64_t>(cdiv(ns, 4), 16384)), dim3(256), 0,
-                               S(stream), tmp, rowptr, N, ns, slice_ptr, vals);
+            if (store)
+                hipLaunchKernelGGL((k_csr_add_sell<3, true>), dim3((unsigned)std::min<int64_t>(cdiv(ns, 4), 16384)),
+                                   dim3(256), 0, S(stream), tmp, rowptr, N, ns, slice_ptr, vals);
+            else
+                hipLaunchKernelGGL(k_csr_add_sell<3>, dim3((unsigned)std::min<int64_t>(cdiv(ns, 4), 16384)), dim3(256),
+                                   0, S(stream), tmp, rowptr, N, ns, slice_ptr, vals);
             FEM_LAUNCHED();
             FEM_HIP(hipFreeAsync(tmp, S(stream)));
             return FEM_OK;

@@ -314,10 +314,28 @@ def _points_weights(etype, integral_point):
     return p, w
 
 
+_CONST = OrderedDict()   # device copies of the per-rule tables (natural derivatives, shape values, weights)
+
+
+def _dev_const(key, make, dev):
+    """Cached device copy of a small host table: forming the tables by Python polynomial evaluation and copying them
+    host-to-device on every call cost more host time than the c3d6 / c3d8 element kernels themselves."""
+    k = key + (str(dev),)
+    t = _CONST.get(k)
+    if t is None:
+        t = make().to(dev).contiguous()
+        _CONST[k] = t
+        if len(_CONST) > 64:
+            _CONST.popitem(last=False)
+    return t
+
+
 def _dn_table(etype, points, dev):
     fn = _ISO[etype][1]
-    rows = [fn(*[float(v) for v in points[q]]) for q in range(points.shape[0])]
-    return torch.tensor(rows, dtype=F64).to(dev).contiguous()   # [n_ip, npe, 3]
+    pts = points.detach().to("cpu", F64).contiguous()
+    return _dev_const((etype, "dN", pts.numpy().tobytes()),
+                      lambda: torch.tensor([fn(*[float(v) for v in pts[q]]) for q in range(pts.shape[0])],
+                                           dtype=F64), dev)   # [n_ip, npe, 3]
 
 
 def _iso_ke(coords, elements, etype, E, nu, points, weights, mode, device, dtype):
@@ -328,7 +346,8 @@ def _iso_ke(coords, elements, etype, E, nu, points, weights, mode, device, dtype
         raise ValueError(f"{etype} expects {npe} nodes per element, got {elements.shape[1]}")
     M = elements.shape[0]
     dN = _dn_table(etype, points, dev)
-    w = weights.to(dev, F64).contiguous()
+    wh = weights.detach().to("cpu", F64).contiguous()
+    w = _dev_const(("w", wh.numpy().tobytes()), lambda: wh, dev)
     n_ip = dN.shape[0]
     d = 3 * npe
     shape = (n_ip, M, d, d) if mode == C.ISO_STACK else (M, d, d)
@@ -347,8 +366,10 @@ def _iso_mass(coords, elements, etype, rho, device, dtype):
     M = elements.shape[0]
     p, w = mass_integration_points(etype)
     dN = _dn_table(etype, p, dev)
-    Nv = torch.tensor([_N[etype](*[float(v) for v in p[q]]) for q in range(p.shape[0])], dtype=F64).to(dev)
-    w = w.to(dev, F64).contiguous()
+    Nv = _dev_const((etype, "N", p.numpy().tobytes()),
+                    lambda: torch.tensor([_N[etype](*[float(v) for v in p[q]]) for q in range(p.shape[0])], dtype=F64),
+                    dev)
+    w = _dev_const(("w", w.to("cpu", F64).contiguous().numpy().tobytes()), lambda: w.to("cpu", F64), dev)
     d = 3 * npe
     Me = torch.empty((M, d, d), dtype=F64, device=dev)
     C.check(lib.fem_iso_mass(C.ptr(coords), C.ptr(elements), M, npe, float(rho), C.ptr(Nv.contiguous()), C.ptr(dN),

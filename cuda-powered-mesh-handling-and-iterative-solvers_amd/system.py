@@ -211,8 +211,19 @@ class SellMatrix:
         self.g = graph
         self.bs = bs
         self.device = graph.cols.device
-        self.vals = torch.zeros(max(graph.sell_entries, 1) * bs * bs, dtype=F64, device=self.device)
+        # values are zeroed lazily: the first add_element_matrices of a fresh matrix STORES every value (padding
+        # included) instead of adding onto a zeroed buffer -- one memset and one read of the matrix fewer
+        self._vals = torch.empty(max(graph.sell_entries, 1) * bs * bs, dtype=F64, device=self.device)
+        self._fresh = True
         self.use16 = graph.dcols is not None   # 16-bit column deltas in every SpMV of this matrix
+
+    @property
+    def vals(self):
+        """SELL values [entries * bs * bs] (plane layout); zero until something was added."""
+        if self._fresh:
+            self._vals.zero_()
+            self._fresh = False
+        return self._vals
 
     @property
     def n_rows(self):
@@ -234,10 +245,13 @@ class SellMatrix:
         inc_ptr, inc_ = inc if inc is not None else (
             (self.g.inc_ptr, self.g.inc) if npe == self.g.npe and elements.shape[0] * npe == self.g.inc.numel()
             else incidence(elements, self.g.n_nodes))
-        C.check(lib.fem_assemble_from_ke(C.ptr(Ke), C.ptr(elements), npe, self.bs, C.ptr(inc_ptr), C.ptr(inc_),
-                                         self.g.n_nodes, C.ptr(self.g.rowptr), C.ptr(self.g.colidx),
-                                         C.ptr(self.g.csr2sell), C.ptr(self.g.slice_ptr), C.ptr(self.vals),
-                                         C.stream(self.device)), "fem_assemble_from_ke")
+        store = self._fresh
+        self._fresh = False
+        C.check(lib.fem_assemble_from_ke_ex(C.ptr(Ke), C.ptr(elements), npe, self.bs, C.ptr(inc_ptr), C.ptr(inc_),
+                                            self.g.n_nodes, C.ptr(self.g.rowptr), C.ptr(self.g.colidx),
+                                            C.ptr(self.g.csr2sell), C.ptr(self.g.slice_ptr), self.g.nnz,
+                                            self.g.sell_entries, 1 if store else 0, C.ptr(self._vals),
+                                            C.stream(self.device)), "fem_assemble_from_ke_ex")
         return self
 
     def add_tet4(self, coords: torch.Tensor, elements: torch.Tensor, E: float, nu: float = 0.0):

@@ -156,6 +156,14 @@ int fem_sell_fill(const int32_t* rowptr, const int32_t* colidx, int64_t nrows, c
 int fem_assemble_from_ke(const double* Ke, const int64_t* conn, int npe, int bs, const int32_t* inc_ptr,
                          const int32_t* inc, int64_t N, const int32_t* rowptr, const int32_t* colidx,
                          const int64_t* csr2sell, const int64_t* slice_ptr, double* vals, fem_stream_t stream);
+/* fem_assemble_from_ke with the sizes the caller already knows (nnz = block-CSR entries, ent = SELL entries; -1:
+ * read from the device) and store != 0 for a matrix whose values were never written: every SELL value is written
+ * (padding zeroed), so the caller skips zeroing the matrix and the kernels skip reading it. Same values bit for bit
+ * as zeroing + fem_assemble_from_ke (`solver/solver.py:144`'s K handoff, as above). */
+int fem_assemble_from_ke_ex(const double* Ke, const int64_t* conn, int npe, int bs, const int32_t* inc_ptr,
+                            const int32_t* inc, int64_t N, const int32_t* rowptr, const int32_t* colidx,
+                            const int64_t* csr2sell, const int64_t* slice_ptr, int64_t nnz, int64_t ent, int store,
+                            double* vals, fem_stream_t stream);
 int fem_assemble_tet4(const double* coords, const int64_t* conn, double E, double nu, int bs,
                       const int32_t* inc_ptr, const int32_t* inc, int64_t N, const int32_t* rowptr,
                       const int32_t* colidx, const int64_t* csr2sell, const int64_t* slice_ptr, double* vals,

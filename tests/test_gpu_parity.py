@@ -419,6 +419,33 @@ def test_assembly_from_element_matrices_wide_rows(gpu, etype, n):
         assert rel(A.matvec(x.to(gpu)), y_ref) < 1e-12, (etype, bs)
 
 
+@pytest.mark.parametrize("etype,n", [("c3d8", 4), ("c3d6", 4), ("c3d10", 3)])
+def test_fresh_matrix_store_equals_zero_and_add(gpu, etype, n):
+    """A fresh SellMatrix's first add_element_matrices stores every value (no memset, no read of the matrix): the
+    whole value buffer -- padding entries included -- equals zeroing + adding bit for bit, for bs = 3 (block-CSR
+    store path) and bs = 1 (in-place path behind a memset); a second family adds on top exactly as before."""
+    el, mesh, _, system = _mods()
+    gen = {"c3d8": mesh.hex_box, "c3d6": mesh.wedge_box, "c3d10": mesh.tet10_cube}[etype]
+    c, t = gen(n, jitter=0.1)
+    tg = t.to(gpu)
+    K = el.compute_K_matrix(c.to(gpu), tg, etype, E, NU, device=gpu, dtype=F64)
+    Me = el.compute_M_matrix(c.to(gpu), tg, etype, 4.47e-3, device=gpu, dtype=F64)
+    g = system.build_graph(tg, c.shape[0])
+    for bs in (3, 1):
+        Kb = K if bs == 3 else K[:, 0::3, 0::3].contiguous()
+        Mb = Me if bs == 3 else Me[:, 0::3, 0::3].contiguous()
+        fresh = system.SellMatrix(g, bs)
+        fresh._vals.fill_(float("nan"))          # garbage: every value must be written by the store pass
+        fresh.add_element_matrices(Kb, tg)
+        zeroed = system.SellMatrix(g, bs)
+        zeroed.vals                               # zero first, then the add path
+        zeroed.add_element_matrices(Kb, tg)
+        assert torch.equal(fresh.vals, zeroed.vals), (etype, bs)
+        fresh.add_element_matrices(Mb, tg)
+        zeroed.add_element_matrices(Mb, tg)
+        assert torch.equal(fresh.vals, zeroed.vals), (etype, bs, "second family")
+
+
 @pytest.mark.parametrize("kind", ["poisson", "elastic"])
 def test_paired_matrix_copy_is_bit_identical(gpu, kind):
     """FEM_TUNE_PAIR (16-byte-value copy: bs = 1 lane-paired, bs = 3 plane-paired layout A) keeps every row's
