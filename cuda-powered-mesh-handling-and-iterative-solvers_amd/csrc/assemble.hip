@@ -510,6 +510,119 @@ __global__ void __launch_bounds__(256) k_assemble_ke_w(const double* __restrict_
     }
 }
 
+// Element-row form of the bs = 3 block-CSR row sums (default for fem_assemble_from_ke): wave per row, and per
+// incident element the wave loads that element's whole block row a of K_e -- 3 D contiguous doubles (rows 3a..3a+2
+// of the row-major K_e), one coalesced segment, lane = value -- as soon as the incidence entry is known (no wait for
+// the element's nodes); lanes (u, b) meanwhile look up the slot of node b of incidence u in the row's sorted column
+// list (LDS binary search), and the values are added into LDS accumulators [slot][r][c] one incidence after the
+// other. Every slot therefore sums its contributions in ascending (incidence, b) order from +0.0, exactly as
+// k_assemble_ke_w<..., CSRW>: the row sums are bit-identical. Columns are taken KR_LMAX at a time (wider rows: one
+// more pass over the incidences per window); an element listing one node twice adds its b's in ascending order.
+constexpr int KR_LMAX = 64;
+template <int NPE>
+__global__ void __launch_bounds__(256) k_assemble_ke_rows3(const double* __restrict__ Ke, const int64_t* __restrict__ conn,
+                                                           const int32_t* __restrict__ inc_ptr,
+                                                           const int32_t* __restrict__ inc, int64_t N,
+                                                           const int32_t* __restrict__ rowptr,
+                                                           const int32_t* __restrict__ colidx, double* __restrict__ out) {
+    constexpr int BS = 3, B2 = 9, D = NPE * BS, RV = BS * D;
+    constexpr int NL = (RV + 63) / 64;    // K_e loads per lane per incidence
+    constexpr int KU = 64 / NPE;          // incidences per batch: one lane per (incidence, element node)
+    __shared__ int cols_s[AW_WAVES][KR_LMAX];
+    __shared__ double acc_s[AW_WAVES][KR_LMAX * B2];
+    __shared__ int slot_s[AW_WAVES][64];
+    __shared__ int64_t koff_s[AW_WAVES][64];
+    __shared__ int eid_s[AW_WAVES][64];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int vb[NL], vo[NL];   // per loaded value: element node b of its column, offset r*3 + c in the 3x3 block
+    bool vv[NL];
+#pragma unroll
+    for (int m = 0; m < NL; ++m) {
+        const int idx = lane + 64 * m;
+        vv[m] = idx < RV;
+        const int r = idx / D, col = idx - D * (idx / D);
+        vb[m] = col / BS;
+        vo[m] = r * BS + (col - BS * (col / BS));
+    }
+    int* cs = cols_s[wid];
+    double* acc = acc_s[wid];
+    const RowWalk rw = row_walk(AW_WAVES);
+    for (int64_t kk = rw.k, i; (i = rw.row(kk)) < N; kk += rw.step) {
+        const int lo = rowptr[i], len = rowptr[i + 1] - lo;
+        const int t0 = inc_ptr[i], C = inc_ptr[i + 1] - t0;
+        for (int j0 = 0; j0 < len; j0 += KR_LMAX) {
+            const int nj = min(KR_LMAX, len - j0);
+            __builtin_amdgcn_wave_barrier();
+            if (lane < nj) cs[lane] = colidx[lo + j0 + lane];
+            for (int t = lane; t < nj * B2; t += 64) acc[t] = 0.0;
+            for (int k0 = 0; k0 < C; k0 += 64) {
+                const int nk = min(64, C - k0);
+                __builtin_amdgcn_wave_barrier();
+                if (lane < nk) {
+                    const int ea = inc[t0 + k0 + lane];
+                    const int e = ea / NPE;
+                    koff_s[wid][lane] = (int64_t)e * D * D + (int64_t)(ea - e * NPE) * RV;
+                    eid_s[wid][lane] = e;
+                }
+                __builtin_amdgcn_wave_barrier();
+                for (int kb = 0; kb < nk; kb += KU) {
+                    const int nu = min(KU, nk - kb);
+                    double v[KU][NL];
+#pragma unroll
+                    for (int u = 0; u < KU; ++u) {
+                        const int64_t ko = koff_s[wid][kb + (u < nu ? u : 0)];
+#pragma unroll
+                        for (int m = 0; m < NL; ++m) v[u][m] = (u < nu && vv[m]) ? Ke[ko + lane + 64 * m] : 0.0;
+                    }
+                    int dup = 0;
+                    if (lane < nu * NPE) {   // slot of node b of incidence u in this column window (-1: outside)
+                        const int u = lane / NPE, b = lane - NPE * (lane / NPE);
+                        const int64_t eb = (int64_t)eid_s[wid][kb + u] * NPE;
+                        const int node = (int)conn[eb + b];
+                        int l = 0, h = nj;
+                        while (l < h) {
+                            const int mid = (l + h) >> 1;
+                            if (cs[mid] < node) l = mid + 1;
+                            else h = mid;
+                        }
+                        slot_s[wid][lane] = (l < nj && cs[l] == node) ? l : -1;
+                        for (int b2 = 0; b2 < b; ++b2) dup |= (int)conn[eb + b2] == node;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    if (!__any(dup)) {
+#pragma unroll
+                        for (int u = 0; u < KU; ++u) {
+                            if (u >= nu) break;
+#pragma unroll
+                            for (int m = 0; m < NL; ++m) {
+                                if (!vv[m]) continue;
+                                const int s = slot_s[wid][u * NPE + vb[m]];
+                                if (s >= 0) acc[s * B2 + vo[m]] += v[u][m];
+                            }
+                            __builtin_amdgcn_wave_barrier();
+                        }
+                    } else {   // an element lists a node twice: its b's one after the other
+                        for (int u = 0; u < nu; ++u)
+                            for (int bb = 0; bb < NPE; ++bb) {
+#pragma unroll
+                                for (int m = 0; m < NL; ++m) {
+                                    if (!vv[m] || vb[m] != bb) continue;
+                                    const int s = slot_s[wid][u * NPE + bb];
+                                    if (s >= 0) acc[s * B2 + vo[m]] += v[u][m];
+                                }
+                                __builtin_amdgcn_wave_barrier();
+                            }
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            double* o = out + (int64_t)(lo + j0) * B2;
+            for (int t = lane; t < nj * B2; t += 64) o[t] = acc[t];
+        }
+    }
+}
+
 // SELL planes += block-CSR row sums (k_assemble_ke_w<..., CSRW>): wave per slice, lane = row; for every (entry k,
 // block value rc) the 64 rows of the slice write one contiguous 512-byte plane segment, and each lane reads its own
 // row's blocks in order (row-contiguous in the block-CSR buffer). Padding entries are left untouched.
@@ -1103,10 +1216,16 @@ int fem_assemble_from_ke_ex(const double* Ke, const int64_t* conn, int npe, int 
             }
             double* tmp = nullptr;
             FEM_HIP(hipMallocAsync((void**)&tmp, sizeof(double) * 9 * (size_t)(nnz > 0 ? nnz : 1), S(stream)));
+            // FEM355_KE_COLS set: the column-owner form (k_assemble_ke_w) instead of the element-row form (read per
+            // call: the parity test compares both in one process)
+            const bool colform = getenv("FEM355_KE_COLS") != nullptr;
 #define FEM_KE_C(P)                                                                                             \
-    if (npe == P)                                                                                               \
+    if (npe == P && colform)                                                                                    \
         hipLaunchKernelGGL((k_assemble_ke_w<3, P, FEM_KE_RPL3, true>), g, dim3(256), 0, S(stream), Ke, conn,     \
-                           inc_ptr, inc, N, rowptr, colidx, csr2sell, tmp);
+                           inc_ptr, inc, N, rowptr, colidx, csr2sell, tmp);                                     \
+    else if (npe == P)                                                                                          \
+        hipLaunchKernelGGL(k_assemble_ke_rows3<P>, g, dim3(256), 0, S(stream), Ke, conn, inc_ptr, inc, N,       \
+                           rowptr, colidx, tmp);
             FEM_KE_C(4) FEM_KE_C(6) FEM_KE_C(8) FEM_KE_C(10)
 #undef FEM_KE_C
             FEM_LAUNCHED();

@@ -668,3 +668,29 @@ def test_persistent_falls_back_and_guards(gpu):
     res = [A.pcg(F, w=wv, mode=0, tol=1e-10, max_iter=50, schedule=s) for s in (0, 3)]
     assert res[0].status == res[1].status and res[0].iterations == res[1].iterations
     assert rel(res[1].x, res[0].x) < 1e-10 or float(res[0].x.abs().max()) == float(res[1].x.abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("etype,n,rep", [("c3d8", 5, 1), ("c3d6", 4, 1), ("c3d10", 4, 1), ("c3d10", 3, 9)])
+def test_element_row_assembly_bit_identical_to_column_form(gpu, etype, n, rep, monkeypatch):
+    """bs = 3 assembly from stored K_e: the element-row kernel (k_assemble_ke_rows3, default) and the column-owner
+    kernel (k_assemble_ke_w, FEM355_KE_COLS) give the same SELL values bit for bit -- also with every element
+    repeated (rows past 64 incident elements and past the 64-column window) and with a node listed twice in one
+    element (the ordered duplicate path)."""
+    el, mesh, _, system = _mods()
+    gen = {"c3d8": mesh.hex_box, "c3d6": mesh.wedge_box, "c3d10": mesh.tet10_cube}[etype]
+    c, t = gen(n, jitter=0.1)
+    t = t.repeat(rep, 1)
+    K = el.compute_K_matrix(c.to(gpu), t.to(gpu), etype, E, NU, device=gpu, dtype=F64)
+    if rep == 1:   # assembled over a connectivity where element 3 lists its first node twice
+        t = t.clone()
+        t[3, -1] = t[3, 0]
+    tg = t.to(gpu)
+    g = system.build_graph(tg, c.shape[0])
+    if rep > 1:
+        rp = g.rowptr.cpu()
+        assert int((rp[1:] - rp[:-1]).max()) > 64 or int((g.inc_ptr[1:] - g.inc_ptr[:-1]).max()) > 64
+    monkeypatch.delenv("FEM355_KE_COLS", raising=False)
+    a = system.SellMatrix(g, 3).add_element_matrices(K, tg).vals.clone()
+    monkeypatch.setenv("FEM355_KE_COLS", "1")
+    b = system.SellMatrix(g, 3).add_element_matrices(K, tg).vals.clone()
+    assert torch.equal(a, b), etype
