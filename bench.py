@@ -155,8 +155,12 @@ def main():
             if not a.no_cpu_baseline:
                 d["cpu_baseline"] = cpu_baseline(a.n, "elastic", a.cpu_iters_elastic)
             return d
-        out = dist.guarded_companion(out, "elasticity", companion, rank=0, timeout=a.elastic_timeout)
-    print(json.dumps(out), flush=True)
+        guard = dist.CompanionGuard(out, "elasticity", rank=0, timeout=a.elastic_timeout)
+        guard.run(companion)
+        guard.emit()
+        guard.close()
+    else:
+        print(json.dumps(out), flush=True)
 
 
 def measure(a, kind, coords, tets, dev):

@@ -413,35 +413,53 @@ def init_comm(rank, world):
 COMPANION_DROP = ("metric", "n_gpus", "higher_is_better", "scaling", "vs_baseline", "dtype", "data")
 
 
-def guarded_companion(out, key, fn, rank=0, timeout=240.0):
-    """out[key] = fn() minus the line-level keys (a companion measurement inside the ONE bench JSON line). An
-    exception is recorded as {"error": ...}; a watchdog bounds the time: when fn() has not returned after `timeout`
-    seconds (e.g. a collective that never completes), rank 0 prints `out` as it stands (the metric measured before
-    the companion) and every rank exits, so the companion can never cost the metric line."""
-    import threading
+class CompanionGuard:
+    """A companion measurement inside the ONE bench JSON line, under a watchdog that stays armed until `close()`
+    (after the line is printed and, at N > 1, after the final barrier). `run(fn)` stores fn() minus the line-level
+    keys under out[key] (an exception as {"error": ...}); `emit()` prints the line once (rank 0). If the watchdog
+    fires first -- a collective that never completes, in the companion or in the teardown after it -- rank 0 prints
+    the line as it stands (the metric measured before the companion; key = {"error": "timed out ..."}) unless it was
+    printed already, and the process exits with status 0: the companion can never cost the metric line."""
 
-    def fire():
-        if rank == 0 and out is not None:
-            out[key] = {"error": f"timed out after {timeout:.0f} s"}
-            print(json.dumps(out), flush=True)
-        sys.stderr.write(f"[rank {rank}] {key} companion timed out after {timeout:.0f} s\n")
-        sys.stderr.flush()
-        os._exit(0)
+    def __init__(self, out, key, rank=0, timeout=240.0):
+        import threading
+        self.out, self.key, self.rank, self.timeout = out, key, rank, timeout
+        self._lock = threading.Lock()
+        self._printed = False
+        self._timer = threading.Timer(timeout, self._fire)
+        self._timer.daemon = True
+        self._timer.start()
 
-    timer = threading.Timer(timeout, fire)
-    timer.daemon = True
-    timer.start()
-    try:
-        d = fn()
-        sub = None if d is None else {k: v for k, v in d.items() if k not in COMPANION_DROP}
-    except Exception as e:   # noqa: BLE001 -- reported in the line; the metric above it stands
-        sub = {"error": f"{type(e).__name__}: {e}"}
-        sys.stderr.write(f"[rank {rank}] {key} companion failed: {sub['error']}\n")
-    finally:
-        timer.cancel()
-    if out is not None:
-        out[key] = sub
-    return out
+    def _fire(self):
+        with self._lock:
+            if self.rank == 0 and self.out is not None and not self._printed:
+                if not isinstance(self.out.get(self.key), dict):
+                    self.out[self.key] = {"error": f"timed out after {self.timeout:.0f} s"}
+                print(json.dumps(self.out), flush=True)
+                self._printed = True
+            sys.stderr.write(f"[rank {self.rank}] {self.key} companion watchdog fired after {self.timeout:.0f} s\n")
+            sys.stderr.flush()
+            os._exit(0)
+
+    def run(self, fn):
+        try:
+            d = fn()
+            sub = None if d is None else {k: v for k, v in d.items() if k not in COMPANION_DROP}
+        except Exception as e:   # noqa: BLE001 -- reported in the line; the metric above it stands
+            sub = {"error": f"{type(e).__name__}: {e}"}
+            sys.stderr.write(f"[rank {self.rank}] {self.key} companion failed: {sub['error']}\n")
+        if self.out is not None:
+            self.out[self.key] = sub
+        return self.out
+
+    def emit(self):
+        with self._lock:
+            if self.rank == 0 and self.out is not None and not self._printed:
+                print(json.dumps(self.out), flush=True)
+            self._printed = True
+
+    def close(self):
+        self._timer.cancel()
 
 
 def bench_main(a, metric):
@@ -476,20 +494,25 @@ def bench_main(a, metric):
     if not done:
         comm = init_comm(rank, world)
         out = rccl_measure(a, a.kind, comm, rank, world, dev, tdist, metric)
+    guard = None
     if a.kind == "poisson" and getattr(a, "elastic", 0) and not same_gpu:
         def companion():
             nonlocal comm
             if comm is None:
                 comm = init_comm(rank, world)
             return rccl_measure(a, "elastic", comm, rank, world, dev, tdist, metric)
-        out = guarded_companion(out, "elasticity", companion, rank=rank,
-                                timeout=float(getattr(a, "elastic_timeout", 240.0)))
-    if rank == 0:
+        guard = CompanionGuard(out, "elasticity", rank=rank, timeout=float(getattr(a, "elastic_timeout", 240.0)))
+        out = guard.run(companion)
+        guard.emit()
+    elif rank == 0:
         print(json.dumps(out), flush=True)
+    # teardown under the same watchdog: a rank stuck in the companion must not hold the others in this barrier
     if comm is not None:
         C.check(C.lib().fem_comm_destroy(comm), "fem_comm_destroy")
     tdist.barrier()
     tdist.destroy_process_group()
+    if guard is not None:
+        guard.close()
 
 
 def rccl_measure(a, kind, comm, rank, world, dev, tdist, metric):
