@@ -1263,6 +1263,7 @@ __global__ void k_c1f_window(int64_t nslices, int64_t nrows, const int64_t* __re
 
 }  // namespace fem
 #include "pcg_persist.hpp"
+#include "pcg_persist3.hpp"
 namespace fem {
 
 // ---------------------------------------------------------------- constraint projections (CG_CONSTRAINED)
@@ -1448,6 +1449,7 @@ struct fem_pcg {
     unsigned* c1f_flags;   // (G + 1) lines
     // persistent schedule (3): requested by fem_pcg_set_schedule, active after fem_pcg_start when supported
     int persist_req;
+    int persist_fit_only;   // schedule 4 (auto) on bs = 3: no overflow build (the 3-kernel schedule instead)
     int persist;
     int pk_grid;          // workgroups (one per CU, multiple of 8)
     int pk_win_ok;        // gather windows computed for this matrix
@@ -2324,10 +2326,15 @@ int fem_pcg_set_schedule(fem_pcg* s, int sched) {
         set_error("fem_pcg_set_schedule: drop the captured graph first (fem_pcg_use_graph(s, 0))");
         return FEM_EARG;
     }
-    if (sched < 0 || sched > 3) {
+    if (sched < 0 || sched > 4) {
         set_error("fem_pcg_set_schedule: unknown schedule %d", sched);
         return FEM_EARG;
     }
+    // 4 = auto: the persistent schedule when it applies -- for bs = 3 only while every wave's slices fit on chip (the
+    // overflow build streams most of the 10M-tet elastic state and measured 633 vs 436 us per iteration), else the
+    // 3-kernel schedule; for bs = 1 schedule 3 (its overflow build beats the deferred fallback)
+    const bool auto3 = sched == 4 && s->bs == 3;
+    if (sched == 4) sched = (s->dist || s->mode == FEM_MODE_CG_CONSTRAINED) ? 0 : 3;
     if (sched != 0 && s->dist) {
         set_error("fem_pcg_set_schedule: the distributed path runs the 3-kernel schedule");
         return FEM_EARG;
@@ -2337,8 +2344,9 @@ int fem_pcg_set_schedule(fem_pcg* s, int sched) {
         return FEM_EARG;
     }
     s->fused = sched == 1;
-    s->deferred = sched == 2 || sched == 3;   // 3 falls back to the deferred schedule when unsupported
+    s->deferred = (sched == 2 || sched == 3) && !auto3;   // 3 falls back to the deferred schedule when unsupported
     s->persist_req = sched == 3;
+    s->persist_fit_only = auto3 ? 1 : 0;
     s->persist = 0;
     return FEM_OK;
 }
@@ -2428,28 +2436,38 @@ static const void* persist_fn(bool prof, bool gsc1, bool ovf = false) {
     return gsc1 ? (const void*)k_pcg_persist<PK_MAXS, false, true> : (const void*)k_pcg_persist<PK_MAXS, false, false>;
 }
 
-// schedule 3 prerequisites: bs = 1, 16-bit columns + lane-paired copy, single GPU, no projections, capacity
-// (every wave <= PK_MAXS slices), one resident PK_T-thread workgroup per CU
+// bs = 3 (pcg_persist3.hpp): P3_MAXS slices per wave on chip, the overflow build past that (single GPU), the DIST
+// build when the rank's slices fit
+static const void* persist3_fn(bool ovf, bool dist) {
+    if (dist) return (const void*)k_pcg_persist3<P3_MAXS, false, true>;
+    return ovf ? (const void*)k_pcg_persist3<P3_MAXS, true> : (const void*)k_pcg_persist3<P3_MAXS, false>;
+}
+static size_t persist_lds(const fem_pcg* s) { return s->bs == 3 ? P3_LDS : PK_LDS; }
+static int persist_maxs(const fem_pcg* s) { return s->bs == 3 ? P3_MAXS : PK_MAXS; }
+
+// schedule 3 prerequisites: bs = 1 (lane-paired copy) or bs = 3 (plane-paired copy), 16-bit columns, single GPU, no
+// projections, capacity (every wave <= MAXS slices, else the overflow build), one resident PK_T-thread workgroup per CU
 static int persist_setup_dist(fem_pcg* s);
 
 static int persist_setup(fem_pcg* s) {
     s->persist = 0;
     if (s->pd) return persist_setup_dist(s);
     if (!s->persist_req) return FEM_OK;
-    if (s->bs != 1 || !s->paired || s->dist || s->mode == FEM_MODE_CG_CONSTRAINED || s->nslices == 0) return FEM_OK;
+    if ((s->bs != 1 && s->bs != 3) || !s->paired || s->dist || s->mode == FEM_MODE_CG_CONSTRAINED || s->nslices == 0)
+        return FEM_OK;
     int dev = 0, ncu = 0;
     FEM_HIP(hipGetDevice(&dev));
     FEM_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     const int G = (ncu / NXCD) * NXCD;
     if (G < NXCD) return FEM_OK;
     // past MAXS slices per wave: the overflow build (packed assignment only; overflow rows streamed from HBM)
-    const bool ovf = s->nslices > (int64_t)G * PK_WAVES * PK_MAXS;
-    if (ovf && !(s->tune & FEM_TUNE_PK_PACK)) return FEM_OK;
-    for (int v = 0; v < 6; ++v) {
-        const void* f = persist_fn((v & 1) && v < 4, v & 2, v >= 4);
-        FEM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)PK_LDS));
+    const bool ovf = s->nslices > (int64_t)G * PK_WAVES * persist_maxs(s);
+    if (ovf && (!(s->tune & FEM_TUNE_PK_PACK) || s->persist_fit_only)) return FEM_OK;
+    for (int v = 0; v < (s->bs == 3 ? 2 : 6); ++v) {
+        const void* f = s->bs == 3 ? persist3_fn(v == 1, false) : persist_fn((v & 1) && v < 4, v & 2, v >= 4);
+        FEM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist_lds(s)));
         int nb = 0;
-        FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, PK_T, PK_LDS));
+        FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, PK_T, persist_lds(s)));
         if (nb < 1) return FEM_OK;
     }
     if (s->pk_grid != G) {
@@ -2488,8 +2506,8 @@ static int persist_setup(fem_pcg* s) {
 // prerequisites of the single-GPU schedule, this rank's slices within the register capacity (no overflow build),
 // one resident workgroup per CU for the chosen grid
 static int persist_setup_dist(fem_pcg* s) {
-    if (s->bs != 1 || !s->paired || s->dist || s->mode == FEM_MODE_CG_CONSTRAINED) {
-        set_error("distributed persistent PCG: needs bs = 1, 16-bit columns with the paired copy, no element "
+    if ((s->bs != 1 && s->bs != 3) || !s->paired || s->dist || s->mode == FEM_MODE_CG_CONSTRAINED) {
+        set_error("distributed persistent PCG: needs bs = 1 or 3, 16-bit columns with the paired copy, no element "
                   "partition, no constraints");
         return FEM_EARG;
     }
@@ -2499,16 +2517,16 @@ static int persist_setup_dist(fem_pcg* s) {
     }
     const int G = s->pk_grid;
     const int64_t nloc = s->pd_split[s->pd_rank + 1] - s->pd_split[s->pd_rank];
-    if ((nloc + G - 1) / G > (int64_t)PK_WAVES * PK_MAXS) {
+    if ((nloc + G - 1) / G > (int64_t)PK_WAVES * persist_maxs(s)) {
         set_error("distributed persistent PCG: %lld slices on this rank exceed the register capacity of %d workgroups",
                   (long long)nloc, G);
         return FEM_EARG;
     }
-    for (int v = 0; v < 2; ++v) {
-        const void* f = persist_fn_dist(v == 1, dist_maxs(s));
-        FEM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)PK_LDS));
+    for (int v = 0; v < (s->bs == 3 ? 1 : 2); ++v) {
+        const void* f = s->bs == 3 ? persist3_fn(false, true) : persist_fn_dist(v == 1, dist_maxs(s));
+        FEM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist_lds(s)));
         int nb = 0;
-        FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, PK_T, PK_LDS));
+        FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, PK_T, persist_lds(s)));
         if (nb < 1) {
             set_error("distributed persistent PCG: kernel does not fit one workgroup per CU");
             return FEM_EARG;
@@ -2596,7 +2614,22 @@ static int launch_persist(fem_pcg* s, int k, unsigned long long* prof) {
     }
     void* args[] = {&a};
     if (s->pd && !prof && s->pd_prof) a.prof = prof = s->pd_prof;
-    const void* fn = s->pd ? persist_fn_dist(prof != nullptr, a.pack)
+    if (s->bs == 3) {   // plane-paired values, per-lane 16-bit node deltas; no instrumented build
+        if (prof && !s->pd) {
+            set_error("persistent PCG: no instrumented (PROF) build for bs = 3");
+            return FEM_EARG;
+        }
+        a.cols = s->cols16;
+        a.uoff = nullptr;
+        a.ucol = nullptr;
+        a.prof = nullptr;
+        if (!s->pd) {   // k_pcg_persist3 always takes the packed assignment
+            const int64_t maxL = (s->nslices + G - 1) / G;
+            a.pack = (int)((maxL + PK_WAVES - 1) / PK_WAVES);
+        }
+    }
+    const void* fn = s->bs == 3 ? persist3_fn(s->pk_ovf != 0, s->pd != 0)
+                   : s->pd ? persist_fn_dist(prof != nullptr, a.pack)
                            : persist_fn(prof != nullptr && !s->pk_ovf, (s->tune & FEM_TUNE_PK_SC1) != 0, s->pk_ovf != 0);
     // the grid spins on inter-workgroup flags, so all G workgroups must be resident together: one per CU is
     // what the occupancy query promised, and a cooperative launch makes the runtime guarantee it (or fail) even
@@ -2604,9 +2637,9 @@ static int launch_persist(fem_pcg* s, int k, unsigned long long* prof) {
     // occupancy check; should residency still fail, every spin is bounded and the launch ends with
     // FEM_PCG_SYNC_TIMEOUT (fem_pcg_solve then re-solves on the deferred schedule).
     if (s->pk_coop || (s->tune & FEM_TUNE_PK_COOP))
-        FEM_HIP(hipLaunchCooperativeKernel(fn, dim3(G), dim3(PK_T), args, PK_LDS, s->stream));
+        FEM_HIP(hipLaunchCooperativeKernel(fn, dim3(G), dim3(PK_T), args, persist_lds(s), s->stream));
     else
-        FEM_HIP(hipLaunchKernel(fn, dim3(G), dim3(PK_T), args, PK_LDS, s->stream));
+        FEM_HIP(hipLaunchKernel(fn, dim3(G), dim3(PK_T), args, persist_lds(s), s->stream));
     FEM_LAUNCHED();
     s->launched += k;
     return FEM_OK;
@@ -3050,7 +3083,8 @@ int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, 
         set_error("fem_pcg_solve: a distributed persistent context is driven by start / iterate / poll per rank");
         return FEM_EARG;
     }
-    const bool may_persist = s->persist_req && s->bs == 1 && !s->dist && s->mode != FEM_MODE_CG_CONSTRAINED;
+    const bool may_persist = s->persist_req && (s->bs == 1 || s->bs == 3) && !s->dist &&
+                             s->mode != FEM_MODE_CG_CONSTRAINED;
     if (may_persist) {
         FEM_HIP(pool_alloc((void**)&x0, sizeof(double) * (size_t)(s->n + 2), s->stream, true));
         FEM_HIP(hipMemcpyAsync(x0, s->x, sizeof(double) * (size_t)s->n, hipMemcpyDeviceToDevice, s->stream));
@@ -3163,8 +3197,8 @@ int fem_pcg_set_rows(fem_pcg* s, int nranks, int rank, const int64_t* slice_spli
         set_error("fem_pcg_set_rows: nranks %d (1..%d), rank %d", nranks, PK_MAX_RANKS, rank);
         return FEM_EARG;
     }
-    if (s->bs != 1 || s->dist || s->mode == FEM_MODE_CG_CONSTRAINED || s->pd) {
-        set_error("fem_pcg_set_rows: bs = 1, not element-partitioned, not constrained, once per context");
+    if ((s->bs != 1 && s->bs != 3) || s->dist || s->mode == FEM_MODE_CG_CONSTRAINED || s->pd) {
+        set_error("fem_pcg_set_rows: bs = 1 or 3, not element-partitioned, not constrained, once per context");
         return FEM_EARG;
     }
     if (slice_split[0] != 0 || slice_split[nranks] != s->nslices) {

@@ -57,9 +57,8 @@ class RankSetup:
 
 def assemble_rank(coords, elements, split, rank, kind="poisson", E=1.0, nu=0.0, fixed_mask=None) -> RankSetup:
     """The global rows [lo, hi) of rank `rank`: pattern + values from the elements touching them, Jacobi weights
-    (zero on fixed dofs, uint8 mask over the global rows)."""
-    if kind != "poisson":
-        raise ValueError("the distributed persistent schedule is bs = 1 (Poisson); elasticity uses dist.py")
+    (zero on fixed dofs, uint8 mask over the global dofs). kind "poisson" (bs = 1) or "elastic" (bs = 3: the block
+    rows of the rank's nodes, k_pcg_persist3)."""
     N = coords.shape[0]
     lo, hi = rank_rows(N, split, rank)
     el = rank_elements(elements, lo, hi)
@@ -89,7 +88,7 @@ class RankRunner:
         self.stream.wait_stream(torch.cuda.current_stream(A.device))
         self.h = ctypes.c_void_p()
         with C.device_scope(A.device):
-            C.check(self.lib.fem_pcg_create(A.g.n_nodes, 1, C.ptr(A.g.slice_ptr), C.ptr(A.g.cols), C.ptr(A.vals),
+            C.check(self.lib.fem_pcg_create(A.g.n_nodes, A.bs, C.ptr(A.g.slice_ptr), C.ptr(A.g.cols), C.ptr(A.vals),
                                             C.ptr(self.b), C.ptr(self.x), C.ptr(self.w), mode, float(tol), float(eps),
                                             None, 0, ctypes.c_void_p(self.stream.cuda_stream), ctypes.byref(self.h)),
                     "fem_pcg_create")
@@ -157,8 +156,8 @@ class RankRunner:
             C.check(self.lib.fem_pcg_set_prof(self.h, C.ptr(buf)), "fem_pcg_set_prof")
 
     def own_x(self):
-        lo, hi = self.rs.lo, self.rs.hi
-        return self.x[lo:hi]
+        bs = self.A.bs
+        return self.x[self.rs.lo * bs:self.rs.hi * bs]
 
     def close(self):
         if self.h:
@@ -237,9 +236,10 @@ class EmulatedGroup:
         return it, stt
 
     def x(self):
-        out = torch.empty(self.n, dtype=F64, device=self.ranks[0].x.device)
+        bs = self.ranks[0].A.bs
+        out = torch.empty(self.n * bs, dtype=F64, device=self.ranks[0].x.device)
         for rr in self.ranks:
-            out[rr.rs.lo:rr.rs.hi] = rr.own_x()
+            out[rr.rs.lo * bs:rr.rs.hi * bs] = rr.own_x()
         return out
 
     def close(self):

@@ -51,10 +51,12 @@ def _dev_scalar(dev, dtype, value):
 # inside the SpMV), 2 = deferred (partials summed by the next kernel, no grid atomics), 3 = persistent (one
 # cooperative launch per chunk of single-reduction iterations, csrc/pcg_persist.hpp; falls back to 2 where its
 # prerequisites do not hold)
-SCHED_THREE, SCHED_FUSED, SCHED_DEFERRED, SCHED_PERSIST = 0, 1, 2, 3
+SCHED_THREE, SCHED_FUSED, SCHED_DEFERRED, SCHED_PERSIST, SCHED_AUTO = 0, 1, 2, 3, 4
 # measured on MI355X (10M-tet cube, 16-bit columns, paired layout; tools/persist_check.py, tools/spmv_tune.py):
-# scalar Poisson 59.4 us/it persistent vs 79.4 deferred; 3x3 elasticity three-kernel (the persistent kernel is bs=1)
-DEFAULT_SCHEDULE = {1: SCHED_PERSIST, 3: SCHED_THREE}
+# scalar Poisson 44.0 us/it persistent vs 79.4 deferred; 3x3 elasticity: the bs = 3 persistent kernel while the state
+# fits on chip (1.2M tets: 43.8 vs 63.2 us three-kernel), the three-kernel schedule past that (10M: 436 vs 633 us for
+# the overflow build) -- SCHED_AUTO picks per matrix
+DEFAULT_SCHEDULE = {1: SCHED_PERSIST, 3: SCHED_AUTO}
 
 
 def _schedule(fused, schedule, bs=1):

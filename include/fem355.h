@@ -377,8 +377,9 @@ int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, 
  * previous kernel's block partials itself: no grid atomics, state banked by launch parity), 3 = persistent
  * (pcg_persist.hpp: the single-reduction iteration as one cooperative launch per chunk, CG state of every row held in
  * registers / LDS of its owning wave, slices past 7 per wave streamed from HBM in the same launch; bs = 1 with
- * 16-bit columns and FEM_TUNE_PAIR, single GPU; otherwise fem_pcg_start falls back to 2). Distributed and
- * constrained contexts accept only 0. */
+ * 16-bit columns and FEM_TUNE_PAIR, single GPU; otherwise fem_pcg_start falls back to 2; bs = 3: pcg_persist3.hpp,
+ * 2 slices per wave on chip, past that the same overflow build), 4 = auto (3 where it applies -- for bs = 3 only
+ * while the state fits on chip, else 0). Element-partitioned and constrained contexts accept only 0 (4 maps to 0). */
 int fem_pcg_set_schedule(fem_pcg* s, int sched);
 /* the schedule the context runs (valid after fem_pcg_start: 3 may have fallen back to 2) */
 int fem_pcg_get_schedule(fem_pcg* s);

@@ -123,3 +123,51 @@ def test_dist_persist_10m_two_ranks(gpu):
         assert rel(grp.x(), x1) < 1e-12
     finally:
         grp.close()
+
+
+def _elastic_case(mesh, system, n, gpu, jitter=0.0):
+    c, t = mesh.kuhn_cube(n, jitter=jitter)
+    c, t = c.to(gpu), t.to(gpu)
+    f, fixed = mesh.cube_elasticity_case(c)
+    mask = torch.zeros((c.shape[0], 3), dtype=torch.uint8, device=gpu)
+    mask[fixed] = 1
+    A = system.assemble_tet4_system(c, t, "elastic", 113.8e9, 0.342)
+    w = A.jacobi(mask.view(-1))
+    return c, t, f.reshape(-1).to(F64), mask.view(-1), A, w
+
+
+@pytest.mark.parametrize("n,jitter", [(20, 0.1), (36, 0.0)])
+def test_dist_persist_elastic_matches_single_gpu(gpu, n, jitter):
+    """bs = 3 (k_pcg_persist3 DIST build, three dofs per hand-off row) over 2 emulated ranks: solve to tolerance
+    against the single-GPU bs = 3 persistent schedule (iterations +-1, x 1e-10), fixed iterations 1e-12, chunk
+    boundaries bit-identical."""
+    C, DP, mesh, system = _mods()
+    c, t, b, mask, A, w = _elastic_case(mesh, system, n, gpu, jitter)
+    tol = 1e-9 * float(torch.sqrt(torch.dot(b, w * b)))
+    r3 = A.pcg(b, w=w, tol=tol, max_iter=20000, schedule=3)
+    grp = DP.EmulatedGroup(c, t, 2, b, fixed_mask=mask, kind="elastic", E=113.8e9, nu=0.342, tol=tol)
+    try:
+        it, stt = grp.solve(max_iter=20000, chunk=301)
+        assert stt == C.PCG_CONVERGED and r3.status == C.PCG_CONVERGED
+        assert abs(it - r3.iterations) <= 1, (it, r3.iterations)
+        assert rel(grp.x(), r3.x) < 1e-10
+    finally:
+        grp.close()
+    run = system.PcgRunner(A, b, w, tol=0.0, schedule=3)
+    run.start()
+    run.iterate(40)
+    assert run.poll()[0] == 40
+    x1 = run.x.clone()
+    run.close()
+    xs = []
+    for chunks in ((40,), (15, 25)):
+        grp = DP.EmulatedGroup(c, t, 2, b, fixed_mask=mask, kind="elastic", E=113.8e9, nu=0.342, tol=0.0)
+        try:
+            grp.start()
+            for k in chunks:
+                grp.iterate(k)
+            assert grp.poll()[0] == 40
+            xs.append(grp.x())
+        finally:
+            grp.close()
+    assert rel(xs[0], x1) < 1e-12 and torch.equal(xs[0], xs[1])

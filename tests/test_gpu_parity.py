@@ -648,15 +648,18 @@ def test_persistent_overflow_past_register_capacity(gpu):
 
 
 def test_persistent_falls_back_and_guards(gpu):
-    """bs = 3 falls back to the deferred schedule; a guard stop (CG breakdown on the scalar block
-    of the indefinite c3d10 rule) reports the same status and iteration as the 3-kernel schedule."""
+    """bs = 3 runs the persistent schedule when asked (3) and by default while its state fits on chip (auto, 4); a
+    guard stop (CG breakdown on the scalar block of the indefinite c3d10 rule) reports the same status and
+    iteration as the 3-kernel schedule."""
     el, mesh, solver, system = _mods()
     c, t = mesh.kuhn_cube(6)
     Ael = system.assemble_tet4_system(c.to(gpu), t.to(gpu), "elastic", E, NU)
-    run = system.PcgRunner(Ael, torch.ones(Ael.n, dtype=F64, device=gpu), Ael.jacobi(None), tol=0.0, schedule=3)
-    run.start()
-    assert run.effective_schedule() == 2
-    run.close()
+    for sched in (3, None):
+        run = system.PcgRunner(Ael, torch.ones(Ael.n, dtype=F64, device=gpu), Ael.jacobi(None), tol=0.0,
+                               schedule=sched)
+        run.start()
+        assert run.effective_schedule() == 3, sched
+        run.close()
     c10, t10 = mesh.tet10_cube(1)
     K = el.compute_c3d10_K_matrix(c10, t10, E, NU, device=gpu, dtype=F64)[:, 0::3, 0::3].contiguous()
     g = system.build_graph(t10.to(gpu), c10.shape[0])
@@ -694,3 +697,63 @@ def test_element_row_assembly_bit_identical_to_column_form(gpu, etype, n, rep, m
     monkeypatch.setenv("FEM355_KE_COLS", "1")
     b = system.SellMatrix(g, 3).add_element_matrices(K, tg).vals.clone()
     assert torch.equal(a, b), etype
+
+
+def _elastic_case(system, mesh, n, gpu, jitter=0.1):
+    c, t = mesh.kuhn_cube(n, jitter=jitter, device=gpu)
+    f, fixed = mesh.cube_elasticity_case(c)
+    A = system.assemble_tet4_system(c, t, "elastic", E, NU)
+    mask = torch.zeros((c.shape[0], 3), dtype=torch.uint8, device=gpu)
+    mask[fixed] = 1
+    return A, f.reshape(-1).to(F64).contiguous(), mask.view(-1)
+
+
+@pytest.mark.parametrize("n", [7, 24])
+def test_persistent_elastic_matches_three_kernel(gpu, n):
+    """bs = 3 persistent schedule (k_pcg_persist3: 3x3 blocks, state on chip) against the 3-kernel schedule on the
+    elasticity system: PCG to tolerance (iterations +-1, x 1e-10, residual history 1e-8), CG mode with masked rows at
+    fixed iterations (x 1e-12), and chunked launches continue the same iteration."""
+    _, mesh, _, system = _mods()
+    A, b, mask = _elastic_case(system, mesh, n, gpu)
+    w = A.jacobi(mask)
+    run = system.PcgRunner(A, b, w, tol=0.0, schedule=3)
+    run.start()
+    assert run.effective_schedule() == 3
+    run.close()
+    tol = 1e-9 * float(torch.sqrt(torch.dot(b, w * b)))
+    r0 = A.pcg(b, w=w, tol=tol, max_iter=20000, schedule=0, history=True)
+    r3 = A.pcg(b, w=w, tol=tol, max_iter=20000, schedule=3, history=True)
+    assert r0.status == r3.status == 1 and abs(r0.iterations - r3.iterations) <= 1, (r0.iterations, r3.iterations)
+    assert rel(r3.x, r0.x) < 1e-10
+    k = min(r0.iterations, r3.iterations) - 1
+    assert rel(r3.history[:k], r0.history[:k]) < 1e-8
+    wm = (mask == 0).to(F64)
+    c0 = A.pcg(b, w=wm, mode=0, tol=0.0, max_iter=25, schedule=0)
+    c3 = A.pcg(b, w=wm, mode=0, tol=0.0, max_iter=25, schedule=3)
+    assert c0.iterations == c3.iterations == 25 and c0.status == c3.status == 2 and rel(c3.x, c0.x) < 1e-12
+    # 3 launches of 10 == 1 launch of 30, bit for bit
+    xs = []
+    for chunks in ((30,), (10, 10, 10)):
+        run = system.PcgRunner(A, b, w, tol=0.0, schedule=3)
+        run.start()
+        for kk in chunks:
+            run.iterate(kk)
+        assert run.poll()[0] == 30
+        torch.cuda.synchronize()
+        xs.append(run.x.clone())
+        run.close()
+    assert torch.equal(xs[0], xs[1])
+
+
+def test_persistent_elastic_overflow(gpu):
+    """Past 2 on-chip slices per wave (n = 80: 8,438 slices > 256 x 16 x 2) the overflow build streams the rest of
+    each wave's slices from HBM inside the same launch: equal to the 3-kernel schedule (iterations +-1, x 1e-10)."""
+    _, mesh, _, system = _mods()
+    A, b, mask = _elastic_case(system, mesh, 80, gpu, jitter=0.0)
+    assert (A.g.n_nodes + 63) // 64 > 256 * 16 * 2
+    w = A.jacobi(mask)
+    tol = 1e-9 * float(torch.sqrt(torch.dot(b, w * b)))
+    r0 = A.pcg(b, w=w, tol=tol, max_iter=20000, schedule=0)
+    r3 = A.pcg(b, w=w, tol=tol, max_iter=20000, schedule=3)
+    assert r0.status == r3.status == 1 and abs(r0.iterations - r3.iterations) <= 1, (r0.iterations, r3.iterations)
+    assert rel(r3.x, r0.x) < 1e-10
