@@ -45,7 +45,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--n", type=int, default=119, help="Kuhn cube size (119 -> 10.1M tets)")
+    ap.add_argument("--n", "--cube-n", dest="n", type=int, default=119,
+                    help="Kuhn cube size (119 -> 10.1M tets); --cube-n under torch.distributed.run (--n is ambiguous there)")
     ap.add_argument("--kind", default="poisson", choices=["poisson", "elastic"])
     ap.add_argument("--sample-every", type=int, default=10, help="event-sample every k-th step")
     ap.add_argument("--rtol", type=float, default=1e-8)

@@ -495,9 +495,23 @@ def bench_main(a, metric):
         comm = init_comm(rank, world)
         out = rccl_measure(a, a.kind, comm, rank, world, dev, tdist, metric)
     guard = None
-    if a.kind == "poisson" and getattr(a, "elastic", 0) and not same_gpu:
+    if a.kind == "poisson" and getattr(a, "elastic", 0):
         def companion():
+            # the persistent multi-GPU schedule for 3x3 blocks (k_pcg_persist3 DIST) where every rank's slices fit
+            # on chip (N >= 4 at 10M tets); else, or when its self-check fails, the RCCL element partition
             nonlocal comm
+            if path in ("auto", "persist"):
+                from . import dist_persist
+                try:
+                    ok, d = dist_persist.bench_persist(a, metric, rank, world, dev, tdist, same_gpu=same_gpu,
+                                                       kind="elastic")
+                    if ok:
+                        return d
+                except C.FemError as e:   # raised on every rank alike (capacity, IPC mapping)
+                    print(f"[rank {rank}] persistent multi-GPU elasticity unavailable: {e}", file=sys.stderr,
+                          flush=True)
+                if same_gpu:
+                    raise RuntimeError("persistent multi-GPU elasticity failed (no RCCL fallback on one GPU)")
             if comm is None:
                 comm = init_comm(rank, world)
             return rccl_measure(a, "elastic", comm, rank, world, dev, tdist, metric)

@@ -289,11 +289,12 @@ def disconnect(opened, dev):
             lib.fem_ipc_close(ctypes.c_void_p(p))
 
 
-def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False):
-    """bench.py at N > 1 on the persistent multi-GPU schedule: the 10M-tet Poisson system row-partitioned over the
-    ranks (strong scaling), self-checked against the single-GPU solve on rank 0's GPU before it is timed. Returns
-    (True, the bench dict on rank 0 / None elsewhere), or (False, None) when the check fails, so the caller can
-    measure the RCCL path instead."""
+def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False, kind="poisson"):
+    """bench.py at N > 1 on the persistent multi-GPU schedule: the 10M-tet Poisson (bs = 1, k_pcg_persist) or
+    elasticity (bs = 3, k_pcg_persist3) system row-partitioned over the ranks (strong scaling), self-checked against
+    the single-GPU persistent solve on rank 0's GPU before it is timed. Returns (True, the bench dict on rank 0 / None
+    elsewhere), or (False, None) when the check fails, so the caller can measure the RCCL path instead; raises
+    C.FemError on every rank alike when the schedule does not apply (a rank's slices past the on-chip capacity)."""
     import os
     import sys
     import time
@@ -329,11 +330,26 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False):
 
     fine = False   # comm blocks from hipMalloc first; fine-grained memory if that fails the self-check
 
+    bs = 1 if kind == "poisson" else 3
+    E, nu = (1.0, 0.0) if kind == "poisson" else (113.8e9, 0.342)
+    if bs == 3:   # on-chip capacity of k_pcg_persist3 (no overflow build across ranks): decided alike on every rank
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+        ns = ((a.n + 1) ** 3 + 63) // 64
+        cap = (grid or (ncu // 8) * 8) * 16 * 2
+        if (ns + world - 1) // world > cap:
+            raise C.FemError(f"{(ns + world - 1) // world} slices per rank exceed the bs = 3 on-chip capacity {cap}")
+
+    def case(coords):
+        f, fixed = _mesh.cube_poisson_case(coords) if kind == "poisson" else _mesh.cube_elasticity_case(coords)
+        gm = torch.zeros((coords.shape[0], bs), dtype=torch.uint8, device=dev)
+        gm[fixed] = 1
+        return f.reshape(-1).to(F64).contiguous(), gm.view(-1)
+
     def solve(coords, tets, b, gmask, rtol, max_iter=20000, chunk=8192):
         N = coords.shape[0]
         split = slice_split(N, world)
-        rs = assemble_rank(coords, tets, split, rank, fixed_mask=gmask)
-        lo, hi = rs.lo, rs.hi
+        rs = assemble_rank(coords, tets, split, rank, kind, E, nu, fixed_mask=gmask)
+        lo, hi = rs.lo * bs, rs.hi * bs
         bz = tsum(float(torch.dot(b[lo:hi], (rs.w * b)[lo:hi])))
         tol = rtol * bz ** 0.5
         run = RankRunner(rs, b, split, rank, world, tol=tol, grid=grid, stream=stream(), fine=fine)
@@ -360,22 +376,17 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False):
 
     # warm-up of the whole pipeline on a small cube (module loads, IPC mapping, the distributed kernel)
     c0, t0_ = _mesh.kuhn_cube(20, device=dev)
-    f0, fx0 = _mesh.cube_poisson_case(c0)
-    m0 = torch.zeros(c0.shape[0], dtype=torch.uint8, device=dev)
-    m0[fx0] = 1
-    solve(c0, t0_, f0.reshape(-1).to(F64), m0, 1e-6)
-    del c0, t0_, f0, fx0, m0
+    b0, m0 = case(c0)
+    solve(c0, t0_, b0, m0, 1e-6)
+    del c0, t0_, b0, m0
 
     coords, tets = _mesh.kuhn_cube(a.n, device=dev)
     N = coords.shape[0]
-    f, fixed = _mesh.cube_poisson_case(coords)
-    b = f.reshape(-1).to(F64).contiguous()
-    gmask = torch.zeros(N, dtype=torch.uint8, device=dev)
-    gmask[fixed] = 1
+    b, gmask = case(coords)
     barrier_sync()
     t0 = time.perf_counter()
     split = slice_split(N, world)
-    rs = assemble_rank(coords, tets, split, rank, fixed_mask=gmask)
+    rs = assemble_rank(coords, tets, split, rank, kind, E, nu, fixed_mask=gmask)
     barrier_sync()
     t_asm = tmax(time.perf_counter() - t0)
     del rs
@@ -385,7 +396,7 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False):
     ref_x = None
     if rank == 0:
         from . import system as _system
-        A = _system.assemble_tet4_system(coords, tets, "poisson", 1.0, 0.0)
+        A = _system.assemble_tet4_system(coords, tets, kind, E, nu)
         w = A.jacobi(gmask)
         tol = a.rtol * float(torch.sqrt(torch.dot(b, w * b)))
         ref = A.pcg(b, w=w, tol=tol, max_iter=20000, schedule=3)
@@ -399,9 +410,9 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False):
         tdist.all_gather_object(parts, (rs.lo, rs.hi, x_own.cpu()))
         ok, why = 1, ""
         if rank == 0:
-            x = torch.empty(N, dtype=F64)
+            x = torch.empty(N * bs, dtype=F64)
             for lo, hi, xp in parts:
-                x[lo:hi] = xp
+                x[lo * bs:hi * bs] = xp
             err = float((x - ref_x).abs().max() / ref_x.abs().max())
             ok = int(stt == C.PCG_CONVERGED and ref_st == C.PCG_CONVERGED and abs(it - ref_it) <= 1 and err < 1e-10)
             why = f"{attempt} comm blocks: status {stt} / {ref_st}, iterations {it} / {ref_it}, x rel diff {err:.3e}"
@@ -439,7 +450,7 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False):
     nnz_own = int(A.g.rowptr[hi] - A.g.rowptr[lo])
     n_own = hi - lo
     # this rank's bytes per iteration (with the stored format's index bytes)
-    alg_own = 8 * nnz_own + (idx_own if n_uni else 2 * nnz_own) + 4 * (n_own + 1) + 16 * n_own
+    alg_own = 8 * bs * bs * nnz_own + (idx_own if n_uni else 2 * nnz_own) + 4 * (n_own + 1) + 16 * n_own * bs
     alg_total = tsum(float(alg_own))
     run.close()
     ok_steps = it2 == a.warmup + a.steps and stt2 == C.PCG_RUNNING
@@ -453,18 +464,19 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False):
             "metric": metric, "value": a.steps / dt, "unit": "CG iterations/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": f"{tets.shape[0]:,}-tet P1 poisson Kuhn cube n={a.n}, Jacobi-PCG fixed "
+            "config": {"workload": f"{tets.shape[0]:,}-tet P1 {kind} Kuhn cube n={a.n}, Jacobi-PCG fixed "
                                    f"iterations, rows partitioned over {world} GPUs, persistent schedule per GPU with "
                                    "in-kernel hand-offs over xGMI (IPC-mapped comm blocks), no collective per "
                                    "iteration" + (" [ranks emulated on ONE GPU]" if same_gpu else ""),
-                       "tets": int(tets.shape[0]), "dofs": N, "parallelism": f"row partition x{world}",
+                       "tets": int(tets.shape[0]), "dofs": N * bs, "parallelism": f"row partition x{world}",
                        "steps_completed": bool(ok_steps), "self_check": verdict[1]},
-            "dofs_per_s": N / (t_asm + t_solve), "assembly_ms": t_asm * 1e3, "solve_ms": t_solve * 1e3,
+            "dofs_per_s": N * bs / (t_asm + t_solve), "assembly_ms": t_asm * 1e3, "solve_ms": t_solve * 1e3,
             "solve_iters": it, "solve_status": stt,
             "kernel_ms": {"persist_iteration_max_over_ranks": per_it * 1e3, "iterations_per_launch": a.steps},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                          "frac": achieved / 8000.0, "traffic": None,
-                         "kernel": "k_pcg_persist<DIST> (rank 0's rows; per GPU)", "algorithmic_bytes": alg_own,
+                         "kernel": ("k_pcg_persist" if bs == 1 else "k_pcg_persist3") + "<DIST> (rank 0's rows; per GPU)",
+                         "algorithmic_bytes": alg_own,
                          "algorithmic_bytes_all_ranks": alg_total,
                          "aggregate_GBps": alg_total / per_it / 1e9,
                          "per": "iteration (whole PCG iteration in the persistent kernel)",
