@@ -752,6 +752,10 @@ def test_persistent_elastic_overflow(gpu):
     A, b, mask = _elastic_case(system, mesh, 80, gpu, jitter=0.0)
     assert (A.g.n_nodes + 63) // 64 > 256 * 16 * 2
     w = A.jacobi(mask)
+    run = system.PcgRunner(A, b, w, tol=0.0)   # default (auto): past the on-chip capacity -> three-kernel
+    run.start()
+    assert run.effective_schedule() == 0
+    run.close()
     tol = 1e-9 * float(torch.sqrt(torch.dot(b, w * b)))
     r0 = A.pcg(b, w=w, tol=tol, max_iter=20000, schedule=0)
     r3 = A.pcg(b, w=w, tol=tol, max_iter=20000, schedule=3)
