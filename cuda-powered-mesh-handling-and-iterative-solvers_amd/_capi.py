@@ -110,6 +110,7 @@ SIGNATURES = {
     "fem_pcg_solve": (_I, [_P, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_D)]),
     "fem_pcg_use_graph": (_I, [_P, _I]),
     "fem_pcg_set_schedule": (_I, [_P, _I]),
+    "fem_pcg_set_entries": (_I, [_P, _L]),
     "fem_pcg_get_schedule": (_I, [_P]),
     "fem_pcg_uniform_slices": (_I, [_P, _L, _L, _P, _P, _P]),
     "fem_pcg_persist_profile": (_I, [_P, _I, _P, ctypes.POINTER(_I)]),

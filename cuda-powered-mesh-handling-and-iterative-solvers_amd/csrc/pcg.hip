@@ -1394,6 +1394,7 @@ struct fem_pcg {
     int fused;          // schedule 1: p formed inside the SpMV
     int deferred;       // schedule 2: partial sums finished by the next kernel (banked state)
     int64_t launched;   // iterations enqueued since start (the deferred schedule's bank parity)
+    int64_t sell_ent;   // SELL entries (slice_ptr[nslices]) when the caller gave it (fem_pcg_set_entries), else -1
     const int16_t* cols16;  // optional 16-bit column deltas (fem_sell_delta16): used instead of cols when set
     int has_con;            // CG_CONSTRAINED projections set (fem_pcg_set_constraints)
     int tune;               // FEM_TUNE_* flags (fem_pcg_set_tuning)
@@ -2281,6 +2282,7 @@ int fem_pcg_create(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_
     s->bs = bs;
     s->nslices = cdiv(nrows, 64);
     s->n = nrows * bs;
+    s->sell_ent = -1;
     s->slice_ptr = slice_ptr;
     s->cols = cols;
     s->vals = vals;
@@ -2318,6 +2320,15 @@ int fem_pcg_create(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_
         return FEM_EHIP;
     }
     *out = s;
+    return FEM_OK;
+}
+
+int fem_pcg_set_entries(fem_pcg* s, int64_t entries) {
+    if (entries < 0) {
+        set_error("fem_pcg_set_entries: negative entry count %lld", (long long)entries);
+        return FEM_EARG;
+    }
+    s->sell_ent = entries;
     return FEM_OK;
 }
 
@@ -2463,13 +2474,20 @@ static int persist_setup(fem_pcg* s) {
     // past MAXS slices per wave: the overflow build (packed assignment only; overflow rows streamed from HBM)
     const bool ovf = s->nslices > (int64_t)G * PK_WAVES * persist_maxs(s);
     if (ovf && (!(s->tune & FEM_TUNE_PK_PACK) || s->persist_fit_only)) return FEM_OK;
-    for (int v = 0; v < (s->bs == 3 ? 2 : 6); ++v) {
-        const void* f = s->bs == 3 ? persist3_fn(v == 1, false) : persist_fn((v & 1) && v < 4, v & 2, v >= 4);
-        FEM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist_lds(s)));
-        int nb = 0;
-        FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, PK_T, persist_lds(s)));
-        if (nb < 1) return FEM_OK;
+    // residency of every build, queried once per device and block size (host calls of ~tens of us per solve)
+    static int occ_cache[2][64] = {};   // 0 unknown, 1 resident, 2 not
+    int& occ = occ_cache[s->bs == 3][dev & 63];
+    if (occ == 0) {
+        occ = 1;
+        for (int v = 0; v < (s->bs == 3 ? 2 : 6) && occ == 1; ++v) {
+            const void* f = s->bs == 3 ? persist3_fn(v == 1, false) : persist_fn((v & 1) && v < 4, v & 2, v >= 4);
+            FEM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist_lds(s)));
+            int nb = 0;
+            FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, PK_T, persist_lds(s)));
+            if (nb < 1) occ = 2;
+        }
     }
+    if (occ != 1) return FEM_OK;
     if (s->pk_grid != G) {
         pool_free(s->pk_win, s->stream);
         pool_free(s->pk_part, s->stream);
@@ -2483,17 +2501,12 @@ static int persist_setup(fem_pcg* s) {
         s->pk_grid = G;
         s->pk_win_ok = 0;
     }
-    if (!s->pk_win_ok) {   // [lo | hi] per logical workgroup, from the matrix columns
-        std::vector<int32_t> lohi(2 * (size_t)G);
-        for (int i = 0; i < G; ++i) {
-            lohi[i] = G;
-            lohi[G + i] = -1;
-        }
-        FEM_HIP(hipMemcpyAsync(s->pk_win, lohi.data(), sizeof(int32_t) * 2 * G, hipMemcpyHostToDevice, s->stream));
+    if (!s->pk_win_ok) {   // [lo | hi] per logical workgroup, from the matrix columns (no host round trip)
+        hipLaunchKernelGGL(k_pk_window_init, dim3(cdiv(G, 256)), dim3(256), 0, s->stream, G, G, s->pk_win);
+        FEM_LAUNCHED();
         hipLaunchKernelGGL(k_pk_window, dim3(stream_grid(s->nslices * 64, 256)), dim3(256), 0, s->stream, s->nslices,
                            s->nrows, s->slice_ptr, s->cols16, G, s->pk_win, s->pk_win + G);
         FEM_LAUNCHED();
-        FEM_HIP(hipStreamSynchronize(s->stream));   // lohi must outlive the copy
         s->pk_win_ok = 1;
     }
     if (ovf && !s->pk_v) FEM_HIP(pool_alloc((void**)&s->pk_v, sizeof(double) * (size_t)s->n, s->stream, s->bs == 1));
@@ -2669,9 +2682,11 @@ static int refresh_pairing(fem_pcg* s) {
     const bool want = (s->bs == 1 || s->bs == 3) && s->cols16 && (s->tune & FEM_TUNE_PAIR) && !s->fused;
     s->paired = 0;
     if (!want || s->nslices == 0) return FEM_OK;
-    int64_t ent = 0;
-    FEM_HIP(hipMemcpyAsync(&ent, s->slice_ptr + s->nslices, sizeof(int64_t), hipMemcpyDeviceToHost, s->stream));
-    FEM_HIP(hipStreamSynchronize(s->stream));
+    int64_t ent = s->sell_ent;
+    if (ent < 0) {   // not given by the caller: one device-to-host read (a host sync)
+        FEM_HIP(hipMemcpyAsync(&ent, s->slice_ptr + s->nslices, sizeof(int64_t), hipMemcpyDeviceToHost, s->stream));
+        FEM_HIP(hipStreamSynchronize(s->stream));
+    }
     if (s->bs == 3) {
         if (!s->pvals) FEM_HIP(pool_alloc((void**)&s->pvals, sizeof(double) * 9 * (size_t)ent, s->stream, s->bs == 1));
         s->pcols16 = nullptr;

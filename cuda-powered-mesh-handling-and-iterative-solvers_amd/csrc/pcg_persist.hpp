@@ -801,6 +801,15 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
 #undef PK_ON
 #undef PK_MARK
 
+// empty gather windows before k_pk_window: lo = lo_empty, hi = -1 for every logical workgroup
+__global__ void k_pk_window_init(int G, int lo_empty, int* __restrict__ win) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < G) {
+        win[i] = lo_empty;
+        win[G + i] = -1;
+    }
+}
+
 // gather window per logical workgroup: the first and last workgroup owning a column of its rows
 __global__ void k_pk_window(int64_t nslices, int64_t nrows, const int64_t* __restrict__ slice_ptr,
                             const int16_t* __restrict__ dcols, int G, int* __restrict__ lo, int* __restrict__ hi) {

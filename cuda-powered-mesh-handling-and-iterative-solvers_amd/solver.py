@@ -103,6 +103,26 @@ def stable_conjugate_gradient_solver(K, elements, F, rbe2, u_init=None, tol=1e-1
     return (u, res) if return_info else u
 
 
+# ============================================================================ final_solver (`solver/solver.py:231-295`)
+def final_solver(K, elements, F, rbe2, u_init=None, tol=1e-10, max_iter=1000, device="cuda:0", dtype=torch.float64,
+                 eps=1e-30, return_info=False):
+    """The reference's out-of-place CG: the iteration of `stable_conjugate_gradient_solver` (the nodes `rbe2` held
+    at zero through a 0/1 mask, alpha = rs/(pAp+eps), beta = rs_new/(rs_old+eps), stop when sqrt(r.r) < tol), the
+    same early-stop prints, and no message when max_iter is reached (`:231-295` has no for-else). Runs the same
+    device CG (mode CG_STABLE). The reference builds u with requires_grad for autograd through its torch ops; the
+    device solve returns a plain tensor."""
+    dev = _dev(device)
+    N = F.shape[0]
+    A = assemble(K, elements, N, dev)
+    w = _free_mask(N, A.bs, rbe2, dev)
+    b = F.to(device=dev, dtype=F64).reshape(-1)
+    res = A.pcg(b, u_init, w=w, mode=C.MODE_CG_STABLE, tol=tol, max_iter=max_iter, eps=eps)
+    if res.status != C.PCG_MAXITER:
+        _cg_messages(res, "stable")
+    u = res.x.view(N, A.bs).to(device=torch.device(device), dtype=dtype)
+    return (u, res) if return_info else u
+
+
 # ============================================================================ constrained CG (`solver/solver.py:394-759`)
 def _constrained_messages(res):
     """`solver/solver.py:566-598` / `:735-757`."""

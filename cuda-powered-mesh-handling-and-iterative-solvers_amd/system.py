@@ -341,6 +341,7 @@ class SellMatrix:
         C.check(rc, "fem_pcg_create")
         try:
             C.check(lib.fem_pcg_set_schedule(h, _schedule(fused, schedule, self.bs)), "fem_pcg_set_schedule")
+            C.check(lib.fem_pcg_set_entries(h, self.g.sell_entries), "fem_pcg_set_entries")
             self.attach_cols16(h)
             if constraints is not None:
                 C.check(lib.fem_pcg_set_constraints(h, *constraints.args()), "fem_pcg_set_constraints")
@@ -390,6 +391,7 @@ class PcgRunner:
                 "fem_pcg_create")
         self.schedule = 0 if isinstance(self, _DistMarker) else _schedule(fused, schedule, A.bs)
         C.check(self.lib.fem_pcg_set_schedule(self.h, self.schedule), "fem_pcg_set_schedule")
+        C.check(self.lib.fem_pcg_set_entries(self.h, A.g.sell_entries), "fem_pcg_set_entries")
         A.attach_cols16(self.h)
         self.constraints = constraints   # keeps the device arrays alive with the context
         if constraints is not None:

@@ -93,5 +93,5 @@ def test_public_functions_enter_the_named_device(monkeypatch):
     assert probe(1, "cuda:0") == 2 and seen == [("call", "cuda:0")]
     # the reference-named API is wrapped (functools.wraps keeps the name / signature for the notebooks)
     for fn in (element.compute_c3d4_K_matrix, element.compute_nodal_forces, solver.preconditioned_conjugate_gradient_solver,
-               solver.stable_conjugate_gradient_solver, solver.static_structure_solver):
+               solver.stable_conjugate_gradient_solver, solver.static_structure_solver, solver.final_solver):
         assert hasattr(fn, "__wrapped__"), fn.__name__

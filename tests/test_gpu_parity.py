@@ -246,6 +246,25 @@ def test_stable_cg_vs_reference(gpu, capsys):
     assert r5.iterations == 20
 
 
+def test_final_solver_is_stable_cg_without_maxiter_message(gpu, capsys):
+    """`final_solver` (`solver/solver.py:231-295`): the stable CG iteration out of place; the same stop prints, none
+    at max_iter (no for-else in the reference)."""
+    _, _, solver, _ = _mods()
+    g = load_golden("tet4_cube_n4_jit")
+    u, res = solver.final_solver(g["K"], g["tets"], g["F"], g["fixed"], tol=float(g["tol"]), device=gpu,
+                                 return_info=True)
+    out = capsys.readouterr().out
+    us, rs = solver.stable_conjugate_gradient_solver(g["K"], g["tets"], g["F"], g["fixed"], tol=float(g["tol"]),
+                                                     device=gpu, return_info=True)
+    capsys.readouterr()
+    assert res.iterations == rs.iterations and torch.equal(u, us)
+    assert abs(res.iterations - int(g["n_cg"])) <= 2 and rel(u, g["u_cg"]) < 1e-10
+    assert out.startswith(f"Converged after {res.iterations} iterations. Residual norm:")
+    _, r5 = solver.final_solver(g["K"], g["tets"], g["F"], g["fixed"], tol=0.0, max_iter=20, device=gpu,
+                                return_info=True)
+    assert capsys.readouterr().out == "" and r5.iterations == 20
+
+
 def test_pcg_vs_reference(gpu, capsys):
     _, _, solver, _ = _mods()
     g = load_golden("tet4_cube_n4_jit")
