@@ -381,8 +381,9 @@ int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, 
  * 2 slices per wave on chip, past that the same overflow build), 4 = auto (3 where it applies -- for bs = 3 only
  * while the state fits on chip, else 0). Element-partitioned and constrained contexts accept only 0 (4 maps to 0). */
 int fem_pcg_set_schedule(fem_pcg* s, int sched);
-/* the SELL entry count of the context's matrix (slice_ptr[nslices], known to the caller from the pattern build):
- * spares fem_pcg_start the device-to-host read (a host sync) before it builds the paired copy. Optional. */
+/* the SELL entry count of the context's matrix, which MUST equal slice_ptr[nslices] (known to the caller from the
+ * pattern build; the paired copy is sized from it): spares fem_pcg_start the device-to-host read (a host sync)
+ * before it builds that copy. Optional; without it fem_pcg_start reads the count itself. */
 int fem_pcg_set_entries(fem_pcg* s, int64_t entries);
 /* the schedule the context runs (valid after fem_pcg_start: 3 may have fallen back to 2) */
 int fem_pcg_get_schedule(fem_pcg* s);
