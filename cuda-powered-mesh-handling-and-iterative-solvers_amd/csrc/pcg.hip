@@ -2700,21 +2700,22 @@ static int refresh_pairing(fem_pcg* s) {
         FEM_HIP(pool_alloc((void**)&s->pvals, sizeof(double) * (size_t)ent, s->stream, s->bs == 1));
         FEM_HIP(pool_alloc((void**)&s->pcols16, sizeof(int16_t) * (size_t)ent, s->stream, s->bs == 1));
     }
-    hipLaunchKernelGGL(k_sell_pair, dim3(stream_grid(s->nslices * 64, 256)), dim3(256), 0, s->stream, s->nslices,
-                       s->slice_ptr, s->vals, s->cols16, s->pvals, s->pcols16);
-    FEM_LAUNCHED();
     s->paired = 1;
-    // slice-uniform deltas (sell_pair.hpp): read by the persistent schedule; the rewritten paired copy stays valid
-    // for every other reader
+    // slice-uniform deltas (sell_pair.hpp): read by the persistent schedule; the paired copy of the uniform slices
+    // stays valid for every other reader. One pass writes both (the other slices get k_sell_pair's copy)
     if ((s->tune & FEM_TUNE_PK_UNI) && 2 * (ent / 64) + 2 < (int64_t)INT32_MAX) {
         if (!s->puoff) {
             FEM_HIP(pool_alloc((void**)&s->puoff, sizeof(int32_t) * (size_t)s->nslices, s->stream, true));
             FEM_HIP(pool_alloc((void**)&s->pucol, sizeof(int16_t) * (size_t)(2 * (ent / 64) + 2), s->stream, true));
         }
         hipLaunchKernelGGL(k_sell_uniform, dim3((unsigned)cdiv(s->nslices, 4)), dim3(256), 0, s->stream, s->nslices,
-                           s->nrows, s->slice_ptr, s->vals, s->cols16, s->pvals, s->pcols16, s->pucol, s->puoff);
+                           s->nrows, s->slice_ptr, s->vals, s->cols16, s->pvals, s->pcols16, s->pucol, s->puoff, 1);
         FEM_LAUNCHED();
+        return FEM_OK;
     }
+    hipLaunchKernelGGL(k_sell_pair, dim3(stream_grid(s->nslices * 64, 256)), dim3(256), 0, s->stream, s->nslices,
+                       s->slice_ptr, s->vals, s->cols16, s->pvals, s->pcols16);
+    FEM_LAUNCHED();
     return FEM_OK;
 }
 

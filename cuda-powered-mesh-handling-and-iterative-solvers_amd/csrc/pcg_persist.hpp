@@ -822,7 +822,8 @@ __global__ void k_pk_window(int64_t nslices, int64_t nrows, const int64_t* __res
         const int64_t p0 = slice_ptr[s];
         const int w = (int)((slice_ptr[s + 1] - p0) >> 6);
         int64_t cmin = row, cmax = row;
-        for (int kk = 0; kk < w; ++kk) {
+#pragma unroll 8
+        for (int kk = 0; kk < w; ++kk) {   // unrolled: the delta loads of a row in flight together
             const int64_t c = row + dcols[p0 + 64 * kk + l];
             cmin = c < cmin ? c : cmin;
             cmax = c > cmax ? c : cmax;

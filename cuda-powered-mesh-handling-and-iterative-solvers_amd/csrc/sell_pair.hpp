@@ -57,8 +57,9 @@ __device__ __forceinline__ double ldx_col(const double* x, int col, int own_lo, 
 // entries in list order). The SpMV then reads the deltas with wave-uniform loads: 10 -> 8 bytes per entry on the
 // matrix stream. Real entries keep their order within the row (ascending column), so every row sum adds the same
 // products in the same order, with +-0 terms interleaved. Other slices: uoff[s] = -1, per-lane deltas as before.
-// k_sell_uniform runs after k_sell_pair; it rewrites the paired values / deltas of the uniform slices (pcols16 stays a
-// valid per-lane copy: kernels that ignore uoff read the same entries). A slice qualifies when: it is full (no rows
+// k_sell_uniform writes the paired values / deltas of the uniform slices (pcols16 stays a valid per-lane copy: kernels
+// that ignore uoff read the same entries) and, with pair_rest, the plain lane-paired copy (k_sell_pair) of every other
+// slice -- one pass over the matrix instead of k_sell_pair followed by a rewrite of nearly every slice. A slice qualifies when: it is full (no rows
 // past nrows), width <= SU_MAXW, the row of greatest length has exactly w entries (no extra padding), every other
 // row's real deltas are a subsequence of that row's, every padded column row + delta lies in [0, nrows), and the
 // trailing SELL padding entries of every row are (delta 0, value 0).
@@ -68,7 +69,7 @@ __attribute__((unused)) static __global__ void __launch_bounds__(256) k_sell_uni
                                                              const double* __restrict__ vin,
                                                              const int16_t* __restrict__ cin, double* __restrict__ vout,
                                                              int16_t* __restrict__ cout, int16_t* __restrict__ ucol,
-                                                             int32_t* __restrict__ uoff) {
+                                                             int32_t* __restrict__ uoff, int pair_rest) {
     __shared__ int cand_all[4][SU_MAXW];
     const int64_t s = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;   // one wave per slice
     const int l = threadIdx.x & 63;
@@ -118,11 +119,19 @@ __attribute__((unused)) static __global__ void __launch_bounds__(256) k_sell_uni
     }
     ok = __all(ok);
     const int32_t uo = (int32_t)(2 * (p0 >> 6));   // even: the deltas are read as int32 pairs
+    const int np = w >> 1;
     if (!ok) {
         if (l == 0) uoff[s] = -1;
+        if (pair_rest) {   // k_sell_pair's copy of this slice
+            for (int k = 0; k < w; ++k) {
+                const int64_t src = p0 + 64 * k + l;
+                const int64_t dst = k < 2 * np ? p0 + (int64_t)(k >> 1) * 128 + 2 * l + (k & 1) : p0 + (int64_t)np * 128 + l;
+                vout[dst] = vin[src];
+                cout[dst] = cin[src];
+            }
+        }
         return;
     }
-    const int np = w >> 1;
     int kr = 0;   // next real entry of this row
     for (int k = 0; k < w; ++k) {
         const int d = cand[k];

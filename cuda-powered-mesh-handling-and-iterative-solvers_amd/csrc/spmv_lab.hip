@@ -377,11 +377,8 @@ int fem_lab_sell_uniform(int64_t nrows, const int64_t* slice_ptr, const double* 
                          double* vals_out, int16_t* dcols_out, int16_t* ucol, int32_t* uoff, fem_stream_t stream) {
     const int64_t ns = cdiv(nrows, 64);
     if (ns == 0) return FEM_OK;
-    hipLaunchKernelGGL(k_sell_pair, dim3(stream_grid(ns * 64, 256)), dim3(256), 0, S(stream), ns, slice_ptr, vals,
-                       dcols, vals_out, dcols_out);
-    FEM_LAUNCHED();
     hipLaunchKernelGGL(k_sell_uniform, dim3((unsigned)cdiv(ns, 4)), dim3(256), 0, S(stream), ns, nrows, slice_ptr, vals,
-                       dcols, vals_out, dcols_out, ucol, uoff);
+                       dcols, vals_out, dcols_out, ucol, uoff, 1);
     FEM_LAUNCHED();
     return FEM_OK;
 }
