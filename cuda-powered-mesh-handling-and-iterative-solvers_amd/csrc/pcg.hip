@@ -2428,6 +2428,8 @@ static size_t pk_sync_words(int G) { return (size_t)(18 + G) * PK_LINE; }
 // N >= 2: fewer loop-carried registers, no spills), else 7
 constexpr int PK_MAXS_DIST = 4;
 static const void* persist_fn_dist(bool prof, int maxs) {
+    if (!prof && maxs <= 1) return (const void*)k_pcg_persist<1, false, true, false, true>;   // 8 pairs in flight
+    if (!prof && maxs == 2) return (const void*)k_pcg_persist<2, false, true, false, true>;   // 4 pairs in flight
     if (maxs <= PK_MAXS_DIST)
         return prof ? (const void*)k_pcg_persist<PK_MAXS_DIST, true, true, false, true>
                     : (const void*)k_pcg_persist<PK_MAXS_DIST, false, true, false, true>;
@@ -2440,7 +2442,13 @@ static int dist_maxs(const fem_pcg* s) {
     return (int)((maxL + PK_WAVES - 1) / PK_WAVES);
 }
 
-static const void* persist_fn(bool prof, bool gsc1, bool ovf = false) {
+// small: slices per wave of the packed assignment (1, 2, 3-4 select the one-, two-, four-slot build with 8, 4, 4 lane
+// pairs in flight; 0 the 7-slot build with 2)
+static const void* persist_fn(bool prof, bool gsc1, bool ovf = false, int small = 0) {
+    if (small >= 1 && small <= 4 && !prof && !ovf && gsc1)
+        return small == 1 ? (const void*)k_pcg_persist<1, false, true>
+             : small == 2 ? (const void*)k_pcg_persist<2, false, true>
+                          : (const void*)k_pcg_persist<4, false, true>;
     if (ovf) return gsc1 ? (const void*)k_pcg_persist<PK_MAXS, false, true, true>
                          : (const void*)k_pcg_persist<PK_MAXS, false, false, true>;
     if (prof) return gsc1 ? (const void*)k_pcg_persist<PK_MAXS, true, true> : (const void*)k_pcg_persist<PK_MAXS, true, false>;
@@ -2479,8 +2487,10 @@ static int persist_setup(fem_pcg* s) {
     int& occ = occ_cache[s->bs == 3][dev & 63];
     if (occ == 0) {
         occ = 1;
-        for (int v = 0; v < (s->bs == 3 ? 2 : 6) && occ == 1; ++v) {
-            const void* f = s->bs == 3 ? persist3_fn(v == 1, false) : persist_fn((v & 1) && v < 4, v & 2, v >= 4);
+        for (int v = 0; v < (s->bs == 3 ? 2 : 9) && occ == 1; ++v) {
+            const void* f = s->bs == 3 ? persist3_fn(v == 1, false)
+                          : v >= 6 ? persist_fn(false, true, false, v == 8 ? 4 : v - 5)
+                                   : persist_fn((v & 1) && v < 4, v & 2, v >= 4);
             FEM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist_lds(s)));
             int nb = 0;
             FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, PK_T, persist_lds(s)));
@@ -2643,7 +2653,8 @@ static int launch_persist(fem_pcg* s, int k, unsigned long long* prof) {
     }
     const void* fn = s->bs == 3 ? persist3_fn(s->pk_ovf != 0, s->pd != 0)
                    : s->pd ? persist_fn_dist(prof != nullptr, a.pack)
-                           : persist_fn(prof != nullptr && !s->pk_ovf, (s->tune & FEM_TUNE_PK_SC1) != 0, s->pk_ovf != 0);
+                           : persist_fn(prof != nullptr && !s->pk_ovf, (s->tune & FEM_TUNE_PK_SC1) != 0, s->pk_ovf != 0,
+                                        (a.pack <= 4 && !(s->tune & FEM_TUNE_PK_WIDE)) ? a.pack : 0);
     // the grid spins on inter-workgroup flags, so all G workgroups must be resident together: one per CU is
     // what the occupancy query promised, and a cooperative launch makes the runtime guarantee it (or fail) even
     // when other streams / processes hold CUs. A plain launch (the bench's fixed-iteration runs) relies on the

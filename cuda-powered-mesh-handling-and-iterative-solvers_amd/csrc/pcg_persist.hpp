@@ -33,6 +33,11 @@ constexpr int PK_T = 1024;               // threads per workgroup (16 waves, 4 p
 constexpr int PK_WAVES = PK_T / 64;
 constexpr int PK_MAXS = 7;               // slices per wave (10M Poisson: 27,000 slices over 4,096 waves -> 7)
 constexpr int PK_U = 2;                  // pairs in flight per lane (4 spills the slot state; persist_probe: 4 = 8)
+// pairs in flight of a build: one slot per wave (small systems: every wave owns at most one slice, e.g. 1M tets or
+// a rank's share at N = 8) leaves the registers for 8 pairs, so a slice's loads go out in one round instead of 4;
+// up to four slots for 4 pairs (the instrumented builds keep PK_U there: their clock registers would spill)
+template <int MAXS, bool PROF>
+constexpr int pk_u() { return MAXS <= 1 ? 8 : (MAXS <= 4 && !PROF) ? 4 : PK_U; }
 constexpr int PK_LINE = 32;              // unsigned words per 128-byte line
 // sync words (zeroed by fem_pcg_start; epochs continue across launches from PcgState::pk_epoch), in lines: [0, 8) group arrivals, 8 (unused), [9, 17) replicas of the
 // top counter (one per group),
@@ -423,7 +428,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
 #pragma unroll
             for (int j = 0; j < MAXS; ++j) {
                 if (j < nreg) {
-                    const double q = sell_row_pair<PK_U, 0>(s0 + j, lane, slp, cop, vap, xvp, 0, 0, a.uoff, a.ucol);
+                    const double q = sell_row_pair<pk_u<MAXS, PROF>(), 0>(s0 + j, lane, slp, cop, vap, xvp, 0, 0, a.uoff, a.ucol);
                     const unsigned row = rb + 64u * j;
                     const bool on = PK_ON(j);
                     double rv = on ? a.b[row] - q : 0.0;
@@ -538,7 +543,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
     if (!rv) {                                                                                     \
         _Pragma("unroll") for (int j = 0; j < MAXS; ++j) {                                         \
             if (j < nreg) {                                                                        \
-                const double v = sell_row_pair<PK_U, MODE>(s0 + j, lane, slp, cop, vap, uvp, olo, ohi, uop, ucp); \
+                const double v = sell_row_pair<pk_u<MAXS, PROF>(), MODE>(s0 + j, lane, slp, cop, vap, uvp, olo, ohi, uop, ucp); \
                 if (j < PK_VL) vl[j * 64] = v; else vv[j] = v;                                     \
             }                                                                                      \
             asm volatile("" ::: "memory");                                                         \
@@ -547,7 +552,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
         _Pragma("unroll") for (int jj = 0; jj < MAXS; ++jj) {                                      \
             const int j = MAXS - 1 - jj;                                                           \
             if (j < nreg) {                                                                        \
-                const double v = sell_row_pair<PK_U, MODE>(s0 + j, lane, slp, cop, vap, uvp, olo, ohi, uop, ucp); \
+                const double v = sell_row_pair<pk_u<MAXS, PROF>(), MODE>(s0 + j, lane, slp, cop, vap, uvp, olo, ohi, uop, ucp); \
                 if (j < PK_VL) vl[j * 64] = v; else vv[j] = v;                                     \
             }                                                                                      \
             asm volatile("" ::: "memory");                                                         \
@@ -573,7 +578,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
                 __builtin_amdgcn_sched_barrier(0);
                 for (int q = 0; q < nov; ++q) {
                     const int sq = s0 + MAXS + q;
-                    const double v = sell_row_pair<PK_U, GSC1>(sq, lane, slp, cop, vap, uvp, 0, 0, uop, ucp);
+                    const double v = sell_row_pair<pk_u<MAXS, PROF>(), GSC1>(sq, lane, slp, cop, vap, uvp, 0, 0, uop, ucp);
                     const int row = sq * 64 + lane;
                     if (row < nrows) {
                         a.v[row] = v;

@@ -421,7 +421,9 @@ int fem_enforce_constraints(double* x, double* r, int64_t n, int order, int64_t 
  * the next sweep: 67 -> 57 us per SpMV on the 10M Poisson matrix. Results depend on the flags only through the
  * order of the per-block p.q partials (deterministic for a given flag set). */
 enum { FEM_TUNE_REVERSE = 1, FEM_TUNE_PAIR = 2, FEM_TUNE_PK_SC1 = 4, FEM_TUNE_PK_PACK = 8, FEM_TUNE_C1F = 16,
-       FEM_TUNE_PK_COOP = 32, FEM_TUNE_DIST_FINE = 64, FEM_TUNE_PK_UNI = 128 };
+       FEM_TUNE_PK_COOP = 32, FEM_TUNE_DIST_FINE = 64, FEM_TUNE_PK_UNI = 128, FEM_TUNE_PK_WIDE = 256 };
+/* FEM_TUNE_PK_WIDE: persistent schedule (bs = 1, single GPU) -- keep the 7-slot build when every wave owns at most
+ * one slice (by default such systems, e.g. 1M tets, run a one-slot build with 8 lane pairs in flight; A/B switch) */
 /* FEM_TUNE_PK_UNI (default): bs = 1 paired copies also record, per 64-row slice whose rows take their columns at one
  * common sorted list of offsets (rows lacking an offset get a zero value there), that list once (sell_pair.hpp
  * k_sell_uniform); the persistent schedule then reads those slices' deltas with wave-uniform loads: 10 -> 8 bytes
