@@ -245,7 +245,8 @@ def measure(a, kind, coords, tets, dev):
     it, stt, _ = run.poll()
     assert it == a.warmup + a.steps, (it, stt)
     kernel = {system.SCHED_THREE: "k_pcg_spmv_dot", system.SCHED_FUSED: "k_pcg_spmv_dot<FUSED>",
-              system.SCHED_DEFERRED: "k_pcg_d1", system.SCHED_PERSIST: "k_pcg_persist"}[run.effective_schedule()]
+              system.SCHED_DEFERRED: "k_pcg_d1",
+              system.SCHED_PERSIST: "k_pcg_persist3" if A.bs == 3 else "k_pcg_persist"}[run.effective_schedule()]
     run.close()
 
     # per launch of the measured kernel: one SpMV (3-kernel / deferred) or one whole iteration (persistent: the
