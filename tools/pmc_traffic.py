@@ -65,8 +65,11 @@ def main():
     shutil.copy(os.path.join(prof, "trace", "run_kernel_stats.csv"),
                 os.path.join(ROOT, "profiles", f"{a.tag}_kernel_stats.csv"))
     trace = load_trace(os.path.join(prof, "trace", "run_kernel_trace.csv"))
-    deferred = any("k_pcg_d1" in r["Kernel_Name"] for r in trace)
-    persist = any("k_pcg_persist" in r["Kernel_Name"] for r in trace)
+    # the schedule of the timed region from the bench line's roofline kernel (the warm-up on a small mesh may have
+    # run another schedule), else from the trace
+    rk = bl.get("roofline", {}).get("kernel", "")
+    deferred = rk.startswith("k_pcg_d1") if rk else any("k_pcg_d1" in r["Kernel_Name"] for r in trace)
+    persist = rk.startswith("k_pcg_persist") if rk else any("k_pcg_persist" in r["Kernel_Name"] for r in trace)
     KERNELS = KERNELS_PERSIST if persist else (KERNELS_DEFERRED if deferred else KERNELS_3K)
     ndisp = 1 if persist else a.steps      # dispatches of the timed region
     per = a.steps if persist else 1        # iterations per dispatch
