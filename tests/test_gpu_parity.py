@@ -612,6 +612,23 @@ def test_slice_uniform_deltas_are_bit_identical(gpu, case):
         assert torch.equal(x1, x0) and rz1 == rz0, (case, sched)
 
 
+@pytest.mark.parametrize("n,jitter", [(20, 0.1), (66, 0.0), (80, 0.05)])
+def test_persistent_slot_builds_are_bit_identical(gpu, n, jitter):
+    """When every wave owns at most 1 / 2 / 4 slices the persistent schedule runs a one- / two- / four-slot build with
+    8 / 4 / 4 lane pairs in flight instead of the 7-slot build's 2 (n = 20: 145 slices, 1 per wave; n = 66: 4,714
+    slices, 2; n = 80: 8,303 slices, 3). Only the loads in flight differ: 60 fixed iterations equal the 7-slot build's
+    (FEM_TUNE_PK_WIDE) bit for bit."""
+    _, mesh, _, system = _mods()
+    c, t = mesh.kuhn_cube(n, jitter=jitter)
+    A = system.assemble_tet4_system(c.to(gpu), t.to(gpu), "poisson")
+    b = torch.randn(A.n, dtype=F64, generator=torch.Generator().manual_seed(5)).to(gpu)
+    w = A.jacobi(None)
+    dflt = 1 | 2 | 4 | 8 | 128
+    _, rz1, x1 = _fixed_iterates(system, A, b, w, 3, dflt, 60)
+    _, rz0, x0 = _fixed_iterates(system, A, b, w, 3, dflt | 256, 60)   # FEM_TUNE_PK_WIDE
+    assert torch.equal(x1, x0) and rz1 == rz0, n
+
+
 def test_persistent_full_geometry_10m(gpu):
     """The 10M-tet bench system (27,000 slices: 6-7 slots per wave, every register slot and the LDS v slots in use):
     50 fixed iterations equal the deferred schedule's to 1e-12; a solve to tolerance stops mid-launch at the
