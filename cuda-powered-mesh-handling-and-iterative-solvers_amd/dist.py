@@ -346,6 +346,7 @@ class _GroupRunner:
                                         C.ptr(self.b), C.ptr(self.x), C.ptr(self.w), mode, float(tol), 1e-30, None,
                                         0, C.stream(A.device), ctypes.byref(self.h)), "fem_pcg_create")
         C.check(self.lib.fem_pcg_set_schedule(self.h, 0), "fem_pcg_set_schedule")
+        C.check(self.lib.fem_pcg_set_entries(self.h, A.g.sell_entries), "fem_pcg_set_entries")
         A.attach_cols16(self.h)
         C.check(self.lib.fem_pcg_set_dist(self.h, 1, None, ds.rm.n_iface, C.ptr(ds.rm.imap), C.ptr(ds.rm.ipos),
                                           C.ptr(ds.rm.own)), "fem_pcg_set_dist")

@@ -92,6 +92,7 @@ class RankRunner:
                                             C.ptr(self.b), C.ptr(self.x), C.ptr(self.w), mode, float(tol), float(eps),
                                             None, 0, ctypes.c_void_p(self.stream.cuda_stream), ctypes.byref(self.h)),
                     "fem_pcg_create")
+            C.check(self.lib.fem_pcg_set_entries(self.h, A.g.sell_entries), "fem_pcg_set_entries")
             A.attach_cols16(self.h)
             if fine:   # comm block in fine-grained memory (the fallback variant for the real multi-GPU transport)
                 C.check(self.lib.fem_pcg_set_tuning(self.h, self.TUNE_DEFAULT | self.TUNE_DIST_FINE),
