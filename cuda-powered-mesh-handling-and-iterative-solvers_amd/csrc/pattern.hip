@@ -13,36 +13,6 @@
 namespace fem {
 
 // ---------------------------------------------------------------- incidence
-__global__ void k_inc_count(const int64_t* __restrict__ conn, int64_t total, int32_t* __restrict__ cnt) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x)
-        atomicAdd(&cnt[conn[i]], 1);
-}
-
-__global__ void k_inc_fill(const int64_t* __restrict__ conn, int64_t total, const int32_t* __restrict__ ptr,
-                           int32_t* __restrict__ cursor, int32_t* __restrict__ inc) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        int64_t node = conn[i];
-        int pos = atomicAdd(&cursor[node], 1);
-        inc[ptr[node] + pos] = (int32_t)i;
-    }
-}
-
-// Each node's segment is short (~24 for Kuhn tets): insertion sort makes the incidence deterministic.
-__global__ void k_inc_sort(const int32_t* __restrict__ ptr, int64_t N, int32_t* __restrict__ inc) {
-    for (int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; n < N; n += (int64_t)gridDim.x * blockDim.x) {
-        int b = ptr[n], e = ptr[n + 1];
-        for (int i = b + 1; i < e; ++i) {
-            int v = inc[i];
-            int j = i - 1;
-            while (j >= b && inc[j] > v) {
-                inc[j + 1] = inc[j];
-                --j;
-            }
-            inc[j + 1] = v;
-        }
-    }
-}
-
 // sort keys of the incidence: node id of every (element, local) slot, payload = slot
 __global__ void k_inc_keys(const int64_t* __restrict__ conn, int64_t total, int32_t* __restrict__ key,
                            int32_t* __restrict__ slot) {
