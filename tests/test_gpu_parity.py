@@ -797,3 +797,25 @@ def test_persistent_elastic_overflow(gpu):
     r3 = A.pcg(b, w=w, tol=tol, max_iter=20000, schedule=3)
     assert r0.status == r3.status == 1 and abs(r0.iterations - r3.iterations) <= 1, (r0.iterations, r3.iterations)
     assert rel(r3.x, r0.x) < 1e-10
+
+
+def test_empty_mesh(gpu, capsys):
+    """No elements (M = 0): element matrices [0, 12, 12], a zero operator, and the stable CG stops at iteration 1 on
+    p.Kp = 0 with the reference's breakdown message. (The reference itself raises RuntimeError in
+    compute_nodal_forces there -- `dofs.view(M, -1)` of an empty tensor, `solver/element.py:452` -- a deliberate
+    difference: nothing faults or reads out of bounds.)"""
+    element, _, solver, system = _mods()
+    coords = torch.rand(10, 3, dtype=F64, generator=torch.Generator().manual_seed(3))
+    el = torch.zeros((0, 4), dtype=torch.long)
+    K = element.compute_c3d4_K_matrix(coords, el, 1e9, 0.3, device=gpu, dtype=F64)
+    assert K.shape == (0, 12, 12)
+    y = element.compute_nodal_forces(K, el, torch.rand(10, 3, dtype=F64), device=gpu, dtype=F64)
+    assert y.shape == (10, 3) and float(y.abs().max()) == 0.0
+    capsys.readouterr()
+    F = torch.rand(10, 3, dtype=F64)
+    u, res = solver.stable_conjugate_gradient_solver(K, el, F, torch.tensor([0]), device=gpu, max_iter=5,
+                                                     return_info=True)
+    assert res.iterations == 1 and float(u.abs().max()) == 0.0
+    assert capsys.readouterr().out.startswith("Terminating early at iteration 1: p^T K p = 0.000e+00")
+    A = system.assemble_tet4_system(coords.to(gpu), el.to(gpu), "poisson")
+    assert float(A.matvec(torch.ones(10, dtype=F64, device=gpu)).abs().max()) == 0.0
