@@ -815,7 +815,9 @@ __global__ void k_pk_window_init(int G, int lo_empty, int* __restrict__ win) {
     }
 }
 
-// gather window per logical workgroup: the first and last workgroup owning a column of its rows
+// gather window per logical workgroup: the first and last workgroup owning a column of its rows. Taken from the
+// per-lane deltas: in a slice-uniform slice (sell_pair.hpp) a lane also gathers at the offsets it lacks, up to 63 rows
+// past this window, but those entries hold value 0, so whatever (finite) u it reads there adds nothing
 __global__ void k_pk_window(int64_t nslices, int64_t nrows, const int64_t* __restrict__ slice_ptr,
                             const int16_t* __restrict__ dcols, int G, int* __restrict__ lo, int* __restrict__ hi) {
     const int64_t W = (int64_t)G * PK_WAVES;
