@@ -87,26 +87,17 @@ SIGNATURES = {
     "fem_vtk_copy": (_I, [_P, _P, _P, _P]),
     "fem_vtk_free": (None, [_P]),
     "fem_spmv": (_I, [_L, _I, _P, _P, _P, _P, _P, _P]),
-    "fem_spmv_variant": (_I, [_I, _I, _L, _I, _P, _P, _P, _P, _P, _P]),
     "fem_sell_delta16": (_I, [_P, _L, _P, _P, _P, _P]),
     "fem_spmv16": (_I, [_L, _I, _P, _P, _P, _P, _P, _P]),
     "fem_pcg_set_cols16": (_I, [_P, _P]),
     "fem_pcg_set_tuning": (_I, [_P, _I]),
     "fem_stream_copy": (_I, [_P, _P, _L, _I, _P]),
-    "fem_lab_copy": (_I, [_I, _I, _P, _P, _L, _I, _P]),
-    "fem_lab_sell_pair": (_I, [_L, _P, _P, _P, _P, _P, _P]),
-    "fem_lab_spmv16_pair": (_I, [_I, _I, _L, _P, _P, _P, _P, _P, _P]),
-    "fem_lab_sell3_layout": (_I, [_I, _L, _P, _P, _P, _P, _P, _P]),
-    "fem_lab_spmv_persist": (_I, [_I, _I, _I, _L, _L, _P, _P, _P, _P, _P, _P]),
-    "fem_lab_spmv3": (_I, [_I, _I, _I, _I, _L, _P, _P, _P, _P, _P, _P]),
-    "fem_lab_sell_uniform": (_I, [_L, _P, _P, _P, _P, _P, _P, _P, _P]),
-    "fem_lab_spmv_persist_uni": (_I, [_I, _L, _L, _P, _P, _P, _P, _P, _P, _P, _P]),
-    "fem_lab_spmv_gather": (_I, [_I, _I, _L, _L, _P, _P, _P, _P, _P, _P, _P]),
-    "fem_lab_spmv_sym": (_I, [_I, _L, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "fem_stream_read": (_I, [_P, _P, _L, _I, _P]),
     "fem_pcg_create": (_I, [_L, _I, _P, _P, _P, _P, _P, _P, _I, _D, _D, _P, _L, _P, ctypes.POINTER(_P)]),
     "fem_pcg_start": (_I, [_P]),
     "fem_pcg_iterate": (_I, [_P, _I]),
     "fem_pcg_poll": (_I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_D)]),
+    "fem_pcg_sync_site": (_I, [_P, ctypes.POINTER(_I)]),
     "fem_pcg_solve": (_I, [_P, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_D)]),
     "fem_pcg_use_graph": (_I, [_P, _I]),
     "fem_pcg_set_schedule": (_I, [_P, _I]),

@@ -1367,6 +1367,16 @@ __global__ void __launch_bounds__(256) k_stream_copy(const double2* __restrict__
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n2; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
 }
 
+// read-only sweep: 16-byte loads summed; the store happens only for an impossible sum (keeps the loads alive)
+__global__ void __launch_bounds__(256) k_stream_read(const double2* __restrict__ src, int64_t n2, double* __restrict__ out) {
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n2; i += (int64_t)gridDim.x * 256) {
+        const double2 v = src[i];
+        acc += v.x + v.y;
+    }
+    if (acc == 12345.678) out[0] = acc;
+}
+
 __global__ void k_zero_fixed(int64_t n, double* __restrict__ x, const double* __restrict__ w) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         if (w[i] == 0.0) x[i] = 0.0;
@@ -2219,44 +2229,16 @@ int fem_pcg_set_cols16(fem_pcg* s, const int16_t* dcols) {
     return FEM_OK;
 }
 
-// tuning entry: SpMV variants (unroll U in {4, 8, 16} x nontemporal matrix loads), grid override
-int fem_spmv_variant(int variant, int grid, int64_t nrows, int bs, const int64_t* slice_ptr, const int32_t* cols,
-                     const double* vals, const double* x, double* y, fem_stream_t stream) {
-    const int64_t ns = cdiv(nrows, 64);
-    if (ns == 0) return FEM_OK;
-    if (grid <= 0) grid = grid_multiple_of_xcd(cdiv(ns, 4), 2048);
-    grid = ((grid + NXCD - 1) / NXCD) * NXCD;
-    hipStream_t st = S(stream);
-#define FEM_SPMV_V(B, U, N) \
-    hipLaunchKernelGGL((k_spmv<B, U, N>), dim3(grid), dim3(256), 0, st, ns, nrows, slice_ptr, cols, vals, x, y)
-    if (bs == 1) {
-        switch (variant) {
-            case 0: FEM_SPMV_V(1, 4, false); break;
-            case 1: FEM_SPMV_V(1, 8, false); break;
-            case 2: FEM_SPMV_V(1, 16, false); break;
-            case 3: FEM_SPMV_V(1, 4, true); break;
-            case 4: FEM_SPMV_V(1, 8, true); break;
-            case 5: FEM_SPMV_V(1, 16, true); break;
-            default: set_error("fem_spmv_variant: unknown variant %d", variant); return FEM_EARG;
-        }
-    } else if (bs == 3) {
-        switch (variant) {
-            case 0: FEM_SPMV_V(3, 8, false); break;
-            case 3: FEM_SPMV_V(3, 8, true); break;
-            default: set_error("fem_spmv_variant: unknown variant %d", variant); return FEM_EARG;
-        }
-    } else {
-        set_error("fem_spmv_variant: block size %d unsupported", bs);
-        return FEM_EARG;
-    }
-#undef FEM_SPMV_V
+int fem_stream_copy(const double* src, double* dst, int64_t n, int grid, fem_stream_t stream) {
+    if (grid <= 0) grid = 2048;
+    hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(256), 0, S(stream), (const double2*)src, (double2*)dst, n / 2);
     FEM_LAUNCHED();
     return FEM_OK;
 }
 
-int fem_stream_copy(const double* src, double* dst, int64_t n, int grid, fem_stream_t stream) {
-    if (grid <= 0) grid = 2048;
-    hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(256), 0, S(stream), (const double2*)src, (double2*)dst, n / 2);
+int fem_stream_read(const double* src, double* out, int64_t n, int grid, fem_stream_t stream) {
+    if (grid <= 0) grid = 4096;
+    hipLaunchKernelGGL(k_stream_read, dim3(grid), dim3(256), 0, S(stream), (const double2*)src, n / 2, out);
     FEM_LAUNCHED();
     return FEM_OK;
 }
@@ -2483,19 +2465,28 @@ static int persist_setup(fem_pcg* s) {
     const bool ovf = s->nslices > (int64_t)G * PK_WAVES * persist_maxs(s);
     if (ovf && (!(s->tune & FEM_TUNE_PK_PACK) || s->persist_fit_only)) return FEM_OK;
     // residency of every build, queried once per device and block size (host calls of ~tens of us per solve)
+    // (the entry is published only after every build's attribute call succeeded, under a lock: a setup that fails
+    // midway, or a second thread, must not find "resident" before the LDS attribute of every build is set)
+    static std::mutex occ_mu;
     static int occ_cache[2][64] = {};   // 0 unknown, 1 resident, 2 not
-    int& occ = occ_cache[s->bs == 3][dev & 63];
-    if (occ == 0) {
-        occ = 1;
-        for (int v = 0; v < (s->bs == 3 ? 2 : 9) && occ == 1; ++v) {
-            const void* f = s->bs == 3 ? persist3_fn(v == 1, false)
-                          : v >= 6 ? persist_fn(false, true, false, v == 8 ? 4 : v - 5)
-                                   : persist_fn((v & 1) && v < 4, v & 2, v >= 4);
-            FEM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist_lds(s)));
-            int nb = 0;
-            FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, PK_T, persist_lds(s)));
-            if (nb < 1) occ = 2;
+    int occ;
+    {
+        std::lock_guard<std::mutex> lk(occ_mu);
+        int& slot = occ_cache[s->bs == 3][dev & 63];
+        if (slot == 0) {
+            int res = 1;
+            for (int v = 0; v < (s->bs == 3 ? 2 : 9) && res == 1; ++v) {
+                const void* f = s->bs == 3 ? persist3_fn(v == 1, false)
+                              : v >= 6 ? persist_fn(false, true, false, v == 8 ? 4 : v - 5)
+                                       : persist_fn((v & 1) && v < 4, v & 2, v >= 4);
+                FEM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)persist_lds(s)));
+                int nb = 0;
+                FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, PK_T, persist_lds(s)));
+                if (nb < 1) res = 2;
+            }
+            slot = res;
         }
+        occ = slot;
     }
     if (occ != 1) return FEM_OK;
     if (s->pk_grid != G) {
@@ -2770,8 +2761,8 @@ int fem_pcg_start(fem_pcg* s) {
             return FEM_EARG;
         }
         FEM_HIP(hipMemsetAsync(s->pk_sync, 0, sizeof(unsigned) * pk_sync_words(s->pk_grid), s->stream));
-        FEM_HIP(hipMemsetAsync(s->pd_block + s->pd_off_flag, 0, (size_t)(s->pd_block_bytes - s->pd_off_flag),
-                               s->stream));
+        // the whole comm block, u included: no row of an earlier solve (or a non-finite one) survives into this one
+        FEM_HIP(hipMemsetAsync(s->pd_block, 0, (size_t)s->pd_block_bytes, s->stream));
         FEM_HIP(hipMemsetAsync(&s->st->pk_epoch, 0, sizeof(unsigned), s->stream));
         s->pk_epochs = 0;
         s->pd_init_pending = 1;
@@ -3056,11 +3047,19 @@ static int fem_pcg_poll_raw(fem_pcg* s, int* iters, int* status, double* rz) {
     int stt = h.status;
     // single reduction: the stop test of the last update runs in the next step, which also sets halt
     if (stt == FEM_PCG_RUNNING && h.iter >= h.max_iter && (!(s->dist && s->cg1) || h.halt)) stt = FEM_PCG_MAXITER;
-    if (iters)
-        *iters = (stt == FEM_PCG_BREAKDOWN || stt == FEM_PCG_ALPHA_NAN || stt == FEM_PCG_SYNC_TIMEOUT) ? h.stop_iter
-                                                                                                      : h.iter;
+    // a guard stop reports the reference's printed iteration (i+1); a synchronisation give-up reports the last
+    // committed iteration (its stop_iter holds the give-up site code: fem_pcg_sync_site)
+    if (iters) *iters = (stt == FEM_PCG_BREAKDOWN || stt == FEM_PCG_ALPHA_NAN) ? h.stop_iter : h.iter;
     if (status) *status = stt;
     if (rz) *rz = (h.iter > 0) ? h.rz_new : h.rz;
+    return FEM_OK;
+}
+
+int fem_pcg_sync_site(fem_pcg* s, int* site) {
+    FEM_HIP(hipMemcpyAsync(s->st_host, s->st, sizeof(PcgState), hipMemcpyDeviceToHost, s->stream));
+    FEM_HIP(hipStreamSynchronize(s->stream));
+    const PcgState h = state_view(s);
+    *site = h.status == FEM_PCG_SYNC_TIMEOUT ? h.stop_iter : 0;
     return FEM_OK;
 }
 
@@ -3342,7 +3341,9 @@ int fem_pcg_set_peers(fem_pcg* s, void* const* bases, const int64_t* need_lo, co
         return (int64_t)q * G + (L < G ? L : G - 1);
     };
     std::vector<int32_t> pub((size_t)G * N * 2, -1);
-    for (int q = 0; q < N; ++q) {
+    // FEM_TUNE_DIST_DROP (fault injection, tests only): this rank publishes nothing, so the ranks that gather its
+    // rows give up on their u-flags and the launch ends with FEM_PCG_SYNC_TIMEOUT on every rank
+    for (int q = 0; q < N && !(s->tune & FEM_TUNE_DIST_DROP); ++q) {
         if (q == r || need_hi[q] < need_lo[q]) continue;
         const int64_t glo = owner(need_lo[q]), ghi = owner(need_hi[q]);
         for (int L = 0; L < G; ++L) {

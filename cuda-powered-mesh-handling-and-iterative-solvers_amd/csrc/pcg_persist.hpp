@@ -43,7 +43,15 @@ constexpr int PK_LINE = 32;              // unsigned words per 128-byte line
 // top counter (one per group),
 // 17 give-up word, 18 + L: u-flag of workgroup L
 enum { PK_GRP = 0, PK_TOP = 8 * PK_LINE, PK_GEN = 9 * PK_LINE, PK_TMO = 17 * PK_LINE, PK_UFLAG = 18 * PK_LINE };
-constexpr unsigned PK_SPIN_LIMIT = 1u << 22;
+// every spin is bounded in TIME (s_memrealtime, 100 MHz on gfx9 parts: hipDeviceAttributeWallClockRate), checked
+// every 64 polls: 2 s for a wait inside one GPU (the longest legitimate one is a grid barrier behind one ~50 us
+// SpMV phase), 5 s for the rank exchange of the DIST build (ranks start their launches up to milliseconds apart).
+// A give-up therefore costs at most ~5 s per launch whatever the poll latency (xGMI system-scope loads included);
+// the spin-count bound this replaces scaled with that latency (4M polls: 4-50 s)
+constexpr uint64_t PK_WAIT_TICKS = 200000000ull;
+constexpr uint64_t PK_RANK_WAIT_TICKS = 500000000ull;
+__device__ __forceinline__ uint64_t pk_now() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ bool pk_expired(uint64_t t0, uint64_t ticks) { return pk_now() - t0 > ticks; }
 constexpr int PK_NPROF = 8;   // phases: u wait, SpMV, block sum, barrier + sums, step, update + drain + flag,
                                // prologue (state loads), epilogue (chunk-end barrier + state stores)
 // dynamic LDS (statics would shift the dynamic base off 16 B, cdna_hip_programming.md Guideline 17): 16 wave sums,
@@ -72,14 +80,15 @@ __device__ __forceinline__ void pk_st(unsigned* p, unsigned v) {
 }
 
 // one lane spins until *p >= target; false on give-up (own or another spinner's)
-// the give-up word holds the site of the first give-up (diagnostics, reported by fem_pcg_poll as the iteration
-// count of a FEM_PCG_SYNC_TIMEOUT): 1 + 16 * epoch local grid barrier, 2 + 16 * epoch u-flag window, 3 + 16 * epoch
+// the give-up word holds the site of the first give-up (diagnostics, reported by fem_pcg_sync_site for a
+// FEM_PCG_SYNC_TIMEOUT): 1 + 16 * epoch local grid barrier, 2 + 16 * epoch u-flag window, 3 + 16 * epoch
 // rank sums (DIST)
 __device__ __forceinline__ bool pk_wait_ge(const unsigned* p, unsigned target, unsigned* tmo) {
+    const uint64_t t0 = pk_now();
     for (unsigned spins = 0;; ++spins) {
         if (pk_ld(p) >= target) return true;
         if ((spins & 63) == 63 && pk_ld(tmo)) return false;
-        if (spins >= PK_SPIN_LIMIT) {
+        if ((spins & 63) == 63 && pk_expired(t0, PK_WAIT_TICKS)) {
             pk_st(tmo, 1u + 16u * (target / NXCD));
             return false;
         }
@@ -256,6 +265,7 @@ __device__ __forceinline__ bool pk_barrier_dist(const PkArgs& a, unsigned* sy, i
         const unsigned* rf = reinterpret_cast<const unsigned*>(a.peer[a.rank] + a.off_rflag);
         int okv = 1;
         bool done = lane >= a.nranks;
+        const uint64_t t0 = pk_now();
         for (unsigned spins = 0; !__all(done); ++spins) {
             if (!done)
                 done = __hip_atomic_load(rf + (lane * NXCD + grp) * PK_LINE, __ATOMIC_RELAXED,
@@ -264,7 +274,7 @@ __device__ __forceinline__ bool pk_barrier_dist(const PkArgs& a, unsigned* sy, i
                 okv = 0;
                 break;
             }
-            if (spins >= 4 * PK_SPIN_LIMIT) {   // ranks start their launches up to milliseconds apart
+            if ((spins & 63) == 63 && pk_expired(t0, PK_RANK_WAIT_TICKS)) {
                 pk_st(tmo, 3u + 16u * e);
                 okv = 0;
                 break;
@@ -496,6 +506,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
                     for (int b0 = wlo; b0 <= whi && ok; b0 += 64) {
                         const int jw = b0 + lane;
                         bool done = jw > whi;
+                        const uint64_t t0 = pk_now();
                         for (unsigned spins = 0; !__all(done); ++spins) {
                             if (!done)
                                 done = (DIST ? __hip_atomic_load(uf + jw * PK_LINE, __ATOMIC_RELAXED,
@@ -505,7 +516,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
                                 ok = false;
                                 break;
                             }
-                            if (spins >= PK_SPIN_LIMIT) {
+                            if ((spins & 63) == 63 && pk_expired(t0, PK_WAIT_TICKS)) {
                                 pk_st(sy + PK_TMO, 2u + 16u * e);
                                 ok = false;
                                 break;
@@ -815,9 +826,25 @@ __global__ void k_pk_window_init(int G, int lo_empty, int* __restrict__ win) {
     }
 }
 
-// gather window per logical workgroup: the first and last workgroup owning a column of its rows. Taken from the
-// per-lane deltas: in a slice-uniform slice (sell_pair.hpp) a lane also gathers at the offsets it lacks, up to 63 rows
-// past this window, but those entries hold value 0, so whatever (finite) u it reads there adds nothing
+// gather window per logical workgroup: the first and last workgroup owning a column of its rows. A slice-uniform
+// slice (sell_pair.hpp) makes every lane gather at the whole slice's delta list, i.e. also at offsets its own row
+// lacks (value 0 there). So the window of a slice is taken over the UNION of its rows' deltas applied to every row
+// of the slice: [s*64 + min delta, s*64 + 63 + max delta]. Every column any lane reads is then inside a window the
+// workgroup waits on -- no read of an unsynchronised u, whose value (0 * Inf = NaN) would otherwise matter.
+__device__ __forceinline__ void pk_slice_span(int64_t s, int64_t nrows, int dmin, int dmax, int64_t* cmin, int64_t* cmax) {
+    for (int off = 32; off > 0; off >>= 1) {
+        const int a2 = __shfl_xor(dmin, off), b2 = __shfl_xor(dmax, off);
+        dmin = a2 < dmin ? a2 : dmin;
+        dmax = b2 > dmax ? b2 : dmax;
+    }
+    int64_t lo = s * 64 + dmin, hi = s * 64 + 63 + dmax;
+    if (hi >= nrows) hi = nrows - 1;
+    if (lo < 0) lo = 0;
+    if (lo > hi) lo = hi;
+    *cmin = lo;
+    *cmax = hi;
+}
+
 __global__ void k_pk_window(int64_t nslices, int64_t nrows, const int64_t* __restrict__ slice_ptr,
                             const int16_t* __restrict__ dcols, int G, int* __restrict__ lo, int* __restrict__ hi) {
     const int64_t W = (int64_t)G * PK_WAVES;
@@ -828,32 +855,28 @@ __global__ void k_pk_window(int64_t nslices, int64_t nrows, const int64_t* __res
         const int64_t row = s * 64 + l;
         const int64_t p0 = slice_ptr[s];
         const int w = (int)((slice_ptr[s + 1] - p0) >> 6);
-        int64_t cmin = row, cmax = row;
+        int dmin = 0, dmax = 0;
+        if (row < nrows) {
 #pragma unroll 8
-        for (int kk = 0; kk < w; ++kk) {   // unrolled: the delta loads of a row in flight together
-            const int64_t c = row + dcols[p0 + 64 * kk + l];
-            cmin = c < cmin ? c : cmin;
-            cmax = c > cmax ? c : cmax;
+            for (int kk = 0; kk < w; ++kk) {   // unrolled: the delta loads of a row in flight together
+                const int d = dcols[p0 + 64 * kk + l];
+                dmin = d < dmin ? d : dmin;
+                dmax = d > dmax ? d : dmax;
+            }
         }
-        if (cmax >= nrows) cmax = nrows - 1;
-        if (cmin < 0) cmin = 0;
+        int64_t cmin, cmax;
+        pk_slice_span(s, nrows, dmin, dmax, &cmin, &cmax);   // wave-uniform
         auto owner = [&](int64_t r) {   // logical workgroup owning row r: largest wave gw with gw S / W <= slice
             const int64_t sl = r >> 6;
             const int64_t gw = ((sl + 1) * W - 1) / nslices;
             return (int)(gw / PK_WAVES);
         };
-        // the 64 lanes of a wave hold the 64 rows of one slice (same owner): reduce, then one atomic pair per
-        // wave (1.7M-thread atomics on 2 G words cost 4.4 ms)
-        const int me = owner(row);
-        int olo = owner(cmin), ohi = owner(cmax);
-        for (int off = 32; off > 0; off >>= 1) {
-            const int a2 = __shfl_xor(olo, off), b2 = __shfl_xor(ohi, off);
-            olo = a2 < olo ? a2 : olo;
-            ohi = b2 > ohi ? b2 : ohi;
-        }
+        // the 64 lanes of a wave hold the 64 rows of one slice (same owner): one atomic pair per wave (1.7M-thread
+        // atomics on 2 G words cost 4.4 ms)
         if (l == 0) {
-            atomicMin(lo + me, olo);
-            atomicMax(hi + me, ohi);
+            const int me = owner(row);
+            atomicMin(lo + me, owner(cmin));
+            atomicMax(hi + me, owner(cmax));
         }
     }
 }
@@ -872,13 +895,15 @@ __global__ void k_pk_window_dist(int64_t sbase, int64_t nloc, int64_t nrows, con
         const int64_t row = s * 64 + l;
         const int64_t p0 = slice_ptr[s];
         const int w = (int)((slice_ptr[s + 1] - p0) >> 6);
-        int64_t cmin = row < nrows ? row : nrows - 1, cmax = cmin;
+        int dmin = 0, dmax = 0;   // the slice's delta union (k_pk_window)
         if (row < nrows)
             for (int kk = 0; kk < w; ++kk) {
-                const int64_t c = cols[p0 + 64 * kk + l];
-                cmin = c < cmin ? c : cmin;
-                cmax = c > cmax ? c : cmax;
+                const int d = (int)(cols[p0 + 64 * kk + l] - row);
+                dmin = d < dmin ? d : dmin;
+                dmax = d > dmax ? d : dmax;
             }
+        int64_t cmin, cmax;
+        pk_slice_span(s, nrows, dmin, dmax, &cmin, &cmax);
         auto owner = [&](int64_t r) {   // global logical workgroup owning row r
             const int64_t sl = r >> 6;
             int q = 0;
@@ -889,21 +914,11 @@ __global__ void k_pk_window_dist(int64_t sbase, int64_t nloc, int64_t nrows, con
             return (int)(q * G + (L < G ? L : G - 1));
         };
         const int me = owner(s * 64) - (int)(owner(sbase * 64) / G) * G;   // local logical workgroup of slice s
-        int olo = owner(cmin), ohi = owner(cmax);
-        int clo = (int)cmin, chi = (int)cmax;
-        for (int off = 32; off > 0; off >>= 1) {
-            const int a2 = __shfl_xor(olo, off), b2 = __shfl_xor(ohi, off);
-            const int c2 = __shfl_xor(clo, off), d2 = __shfl_xor(chi, off);
-            olo = a2 < olo ? a2 : olo;
-            ohi = b2 > ohi ? b2 : ohi;
-            clo = c2 < clo ? c2 : clo;
-            chi = d2 > chi ? d2 : chi;
-        }
         if (l == 0) {
-            atomicMin(lo + me, olo);
-            atomicMax(hi + me, ohi);
-            atomicMin(cwin, clo);   // the rank's column window: rows of other ranks it gathers
-            atomicMax(cwin + 1, chi);
+            atomicMin(lo + me, owner(cmin));
+            atomicMax(hi + me, owner(cmax));
+            atomicMin(cwin, (int)cmin);   // the rank's column window: rows of other ranks it gathers
+            atomicMax(cwin + 1, (int)cmax);
         }
     }
 }

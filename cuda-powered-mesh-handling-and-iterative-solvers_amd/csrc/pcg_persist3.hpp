@@ -230,6 +230,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist3(PkArgs a) {
                     for (int b0 = wlo; b0 <= whi && ok; b0 += 64) {
                         const int jw = b0 + lane;
                         bool done = jw > whi;
+                        const uint64_t t0 = pk_now();
                         for (unsigned spins = 0; !__all(done); ++spins) {
                             if (!done)
                                 done = (DIST ? __hip_atomic_load(uf + jw * PK_LINE, __ATOMIC_RELAXED,
@@ -239,7 +240,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist3(PkArgs a) {
                                 ok = false;
                                 break;
                             }
-                            if (spins >= PK_SPIN_LIMIT) {
+                            if ((spins & 63) == 63 && pk_expired(t0, PK_WAIT_TICKS)) {
                                 pk_st(sy + PK_TMO, 2u + 16u * e);
                                 ok = false;
                                 break;

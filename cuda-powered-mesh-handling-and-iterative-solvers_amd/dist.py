@@ -463,6 +463,28 @@ class CompanionGuard:
         self._timer.cancel()
 
 
+def run_chain(path, same_gpu, persist_fn, rccl_fn, rank=0, log=None):
+    """The N > 1 measurement decision (bench.py): returns (bench dict or None, "persist" | "rccl").
+    path "auto": the persistent multi-GPU schedule (`persist_fn() -> (ok, out)`, raising C.FemError on every rank
+    alike when it does not apply), the RCCL element partition (`rccl_fn() -> out`) when it raised or returned not ok;
+    "persist": the persistent schedule or a RuntimeError; "rccl": RCCL only. same_gpu (all ranks on one GPU, a
+    validation mode): RCCL refuses two ranks per GPU, so a failed persistent schedule is a RuntimeError there too."""
+    log = log or (lambda m: print(f"[rank {rank}] {m}", file=sys.stderr, flush=True))
+    if path in ("auto", "persist"):
+        try:
+            ok, out = persist_fn()
+        except C.FemError as e:
+            log(f"persistent multi-GPU schedule unavailable: {e}")
+            ok, out = False, None
+        if ok:
+            return out, "persist"
+        if same_gpu or path == "persist":
+            raise RuntimeError("persistent multi-GPU schedule failed (no RCCL fallback "
+                               + ("possible: all ranks on one GPU)" if same_gpu else "requested)"))
+        log("falling back to the RCCL element partition")
+    return rccl_fn(), "rccl"
+
+
 def bench_main(a, metric):
     """bench.py for N > 1 ranks (one per GPU), strong scaling of the 10M-tet system: Poisson on the persistent
     multi-GPU schedule (rows partitioned, in-kernel hand-offs; RCCL element partition if its self-check fails),
@@ -482,40 +504,29 @@ def bench_main(a, metric):
     tdist.init_process_group("gloo", rank=rank, world_size=world)
     C.lib()
     path = getattr(a, "dist_path", "auto")
-    out, comm, done = None, None, False
-    if a.kind == "poisson" and path in ("auto", "persist"):
+    comm = None
+
+    def rccl(kind):
+        nonlocal comm
+        if comm is None:
+            comm = init_comm(rank, world)
+        return rccl_measure(a, kind, comm, rank, world, dev, tdist, metric)
+
+    def persist(kind):
         from . import dist_persist
-        try:
-            done, out = dist_persist.bench_persist(a, metric, rank, world, dev, tdist, same_gpu=same_gpu)
-        except C.FemError as e:   # raised on every rank alike (dist_persist.connect agrees before raising)
-            print(f"[rank {rank}] persistent multi-GPU schedule unavailable: {e}", file=sys.stderr, flush=True)
-            done = False
-        if not done and (same_gpu or path == "persist"):
-            raise RuntimeError("persistent multi-GPU schedule failed (no RCCL fallback requested / possible)")
-    if not done:
-        comm = init_comm(rank, world)
-        out = rccl_measure(a, a.kind, comm, rank, world, dev, tdist, metric)
+        return dist_persist.bench_persist(a, metric, rank, world, dev, tdist, same_gpu=same_gpu, kind=kind)
+
+    # Poisson: the persistent multi-GPU schedule first (rows partitioned, in-kernel hand-offs), RCCL if it does not
+    # apply or fails its checks. The elasticity companion the same way: the bs = 3 DIST build where every rank's
+    # slices fit on chip (N >= 4 at 10M tets), else the RCCL element partition (BASELINE configs[3])
+    if a.kind == "poisson":
+        out, _ = run_chain(path, same_gpu, lambda: persist("poisson"), lambda: rccl("poisson"), rank)
+    else:
+        out = rccl(a.kind)
     guard = None
     if a.kind == "poisson" and getattr(a, "elastic", 0):
         def companion():
-            # the persistent multi-GPU schedule for 3x3 blocks (k_pcg_persist3 DIST) where every rank's slices fit
-            # on chip (N >= 4 at 10M tets); else, or when its self-check fails, the RCCL element partition
-            nonlocal comm
-            if path in ("auto", "persist"):
-                from . import dist_persist
-                try:
-                    ok, d = dist_persist.bench_persist(a, metric, rank, world, dev, tdist, same_gpu=same_gpu,
-                                                       kind="elastic")
-                    if ok:
-                        return d
-                except C.FemError as e:   # raised on every rank alike (capacity, IPC mapping)
-                    print(f"[rank {rank}] persistent multi-GPU elasticity unavailable: {e}", file=sys.stderr,
-                          flush=True)
-                if same_gpu:
-                    raise RuntimeError("persistent multi-GPU elasticity failed (no RCCL fallback on one GPU)")
-            if comm is None:
-                comm = init_comm(rank, world)
-            return rccl_measure(a, "elastic", comm, rank, world, dev, tdist, metric)
+            return run_chain(path, same_gpu, lambda: persist("elastic"), lambda: rccl("elastic"), rank)[0]
         guard = CompanionGuard(out, "elasticity", rank=rank, timeout=float(getattr(a, "elastic_timeout", 240.0)))
         out = guard.run(companion)
         guard.emit()

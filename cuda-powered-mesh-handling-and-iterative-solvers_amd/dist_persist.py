@@ -20,6 +20,7 @@ for the bs = 1 (Poisson) system, designed for the strong-scaling target of SURVE
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import torch
@@ -72,10 +73,10 @@ def assemble_rank(coords, elements, split, rank, kind="poisson", E=1.0, nu=0.0, 
 class RankRunner:
     """One rank's persistent PCG context over its rows of the global system (vectors global-length)."""
 
-    TUNE_DEFAULT, TUNE_DIST_FINE = 1 | 2 | 4 | 8 | 128, 64
+    TUNE_DEFAULT, TUNE_DIST_FINE, TUNE_DIST_DROP = 1 | 2 | 4 | 8 | 128, 64, 512
 
     def __init__(self, rs: RankSetup, b, split, rank, nranks, tol=0.0, mode=C.MODE_PCG, eps=1e-30, grid=0,
-                 stream=None, x0=None, fine=False):
+                 stream=None, x0=None, fine=False, drop=None):
         self.lib = C.lib()
         A = rs.A
         self.A, self.rs, self.rank, self.nranks = A, rs, rank, nranks
@@ -94,9 +95,14 @@ class RankRunner:
                     "fem_pcg_create")
             C.check(self.lib.fem_pcg_set_entries(self.h, A.g.sell_entries), "fem_pcg_set_entries")
             A.attach_cols16(self.h)
-            if fine:   # comm block in fine-grained memory (the fallback variant for the real multi-GPU transport)
-                C.check(self.lib.fem_pcg_set_tuning(self.h, self.TUNE_DEFAULT | self.TUNE_DIST_FINE),
-                        "fem_pcg_set_tuning")
+            # fine: comm block in fine-grained memory (coherent for the other GPUs' accesses; the default until a
+            # real multi-GPU run has shown hipMalloc memory coherent there too). drop: fault injection (tests) --
+            # this rank publishes nothing; FEM355_DIST_DROP_RANK=r selects rank r from the environment
+            if drop is None:
+                drop = os.environ.get("FEM355_DIST_DROP_RANK", "") == str(rank)
+            if fine or drop:
+                C.check(self.lib.fem_pcg_set_tuning(self.h, self.TUNE_DEFAULT | (self.TUNE_DIST_FINE if fine else 0)
+                                                    | (self.TUNE_DIST_DROP if drop else 0)), "fem_pcg_set_tuning")
             sp = (ctypes.c_int64 * (nranks + 1))(*split)
             C.check(self.lib.fem_pcg_set_rows(self.h, nranks, rank, sp, int(grid)), "fem_pcg_set_rows")
             base, nbytes = ctypes.c_void_p(), ctypes.c_int64()
@@ -143,6 +149,12 @@ class RankRunner:
                     "fem_pcg_poll")
         return it.value, stt.value, rz.value
 
+    def sync_site(self):
+        v = ctypes.c_int()
+        with C.device_scope(self.device):
+            C.check(self.lib.fem_pcg_sync_site(self.h, ctypes.byref(v)), "fem_pcg_sync_site")
+        return v.value
+
     def effective_schedule(self):
         return int(self.lib.fem_pcg_get_schedule(self.h))
 
@@ -178,7 +190,7 @@ class EmulatedGroup:
     launches run concurrently; the comm blocks are plain device pointers (no IPC)."""
 
     def __init__(self, coords, elements, nranks, b, fixed_mask=None, kind="poisson", E=1.0, nu=0.0, tol=0.0,
-                 mode=C.MODE_PCG, x0=None, fine=False):
+                 mode=C.MODE_PCG, x0=None, fine=False, drop_rank=-1):
         dev = coords.device
         ncu = torch.cuda.get_device_properties(dev).multi_processor_count
         # a multiple of 8 workgroups per rank within its CU-mask share (at 3+ ranks leave headroom: the masks are
@@ -199,7 +211,7 @@ class EmulatedGroup:
             st = torch.cuda.ExternalStream(raw.value, device=dev)
             rs = assemble_rank(coords, elements, self.split, r, kind, E, nu, fixed_mask)
             self.ranks.append(RankRunner(rs, b, self.split, r, nranks, tol=tol, mode=mode, grid=grid, x0=x0,
-                                         stream=st, fine=fine))
+                                         stream=st, fine=fine, drop=(r == drop_rank)))
         torch.cuda.synchronize(dev)
         bases = [rr.block for rr in self.ranks]
         windows = [rr.col_window for rr in self.ranks]
@@ -217,8 +229,11 @@ class EmulatedGroup:
             rr.iterate(k)
         torch.cuda.synchronize()
 
+    def poll_ranks(self):
+        return [rr.poll() for rr in self.ranks]
+
     def poll(self):
-        polls = [rr.poll() for rr in self.ranks]
+        polls = self.poll_ranks()
         its = {p[0] for p in polls}
         sts = {p[1] for p in polls}
         assert len(its) == 1 and len(sts) == 1, f"ranks disagree: {polls}"
@@ -290,6 +305,11 @@ def disconnect(opened, dev):
             lib.fem_ipc_close(ctypes.c_void_p(p))
 
 
+# comm-block variants tried in order by bench_persist: fine-grained device memory first (coherent for peer GPUs by
+# construction), hipMalloc memory second (faster local polls, coherence across GPUs not yet shown on hardware)
+ATTEMPTS = ("fine-grained", "coarse-grained")
+
+
 def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False, kind="poisson"):
     """bench.py at N > 1 on the persistent multi-GPU schedule: the 10M-tet Poisson (bs = 1, k_pcg_persist) or
     elasticity (bs = 3, k_pcg_persist3) system row-partitioned over the ranks (strong scaling), self-checked against
@@ -308,6 +328,11 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False, kind="pois
     def tmax(v):
         t = torch.tensor([v], dtype=torch.float64)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        return float(t[0])
+
+    def tmin(v):
+        t = torch.tensor([v], dtype=torch.float64)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MIN)
         return float(t[0])
 
     def tsum(v):
@@ -329,7 +354,12 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False, kind="pois
     def stream():
         return torch.cuda.ExternalStream(raw_stream, device=dev) if raw_stream else torch.cuda.Stream(device=dev)
 
-    fine = False   # comm blocks from hipMalloc first; fine-grained memory if that fails the self-check
+    def release_stream():
+        if raw_stream:
+            torch.cuda.synchronize(dev)
+            lib.fem_stream_destroy(ctypes.c_void_p(raw_stream))
+
+    fine = True   # comm-block variant of the current attempt (see ATTEMPTS)
 
     bs = 1 if kind == "poisson" else 3
     E, nu = (1.0, 0.0) if kind == "poisson" else (113.8e9, 0.342)
@@ -365,7 +395,7 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False, kind="pois
             run.iterate(k)
             done += k
             it, stt, _ = run.poll()
-            if stt != C.PCG_RUNNING:
+            if stt != C.PCG_RUNNING:   # converged, or a bounded wait gave up (FEM_PCG_SYNC_TIMEOUT): one launch
                 break
         barrier_sync()
         t_solve = tmax(time.perf_counter() - t0)
@@ -375,11 +405,10 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False, kind="pois
         run.close()
         return rs, x_own, it, stt, t_solve, split
 
-    # warm-up of the whole pipeline on a small cube (module loads, IPC mapping, the distributed kernel)
+    # warm the rank-local kernels (module loads, first-launch costs) before the assembly is timed
     c0, t0_ = _mesh.kuhn_cube(20, device=dev)
     b0, m0 = case(c0)
-    solve(c0, t0_, b0, m0, 1e-6)
-    del c0, t0_, b0, m0
+    assemble_rank(c0, t0_, slice_split(c0.shape[0], world), rank, kind, E, nu, fixed_mask=m0)
 
     coords, tets = _mesh.kuhn_cube(a.n, device=dev)
     N = coords.shape[0]
@@ -392,8 +421,9 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False, kind="pois
     t_asm = tmax(time.perf_counter() - t0)
     del rs
     # self-check against the single-GPU persistent solve on rank 0's GPU (the iterates may differ only by the
-    # grouping of the partial sums): a mapping or coherence problem of the real transport shows up here. First
-    # with the comm blocks in hipMalloc memory, then in fine-grained memory; then the caller falls back to RCCL.
+    # grouping of the partial sums): a mapping or coherence problem of the real transport shows up here. Attempts
+    # in ATTEMPTS order; each first solves the small warm-up cube (a transport that does not work gives up there,
+    # within one bounded launch: DESIGN.md §6.1 budget), then the full system. All fail -> the caller measures RCCL.
     ref_x = None
     if rank == 0:
         from . import system as _system
@@ -404,27 +434,38 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False, kind="pois
         ref_x, ref_it, ref_st = ref.x.cpu(), ref.iterations, ref.status
         del A, w, ref
     verdict = [0, "not run"]
-    for attempt in ("coarse-grained", "fine-grained"):
+    attempts_log = []
+    for attempt in ATTEMPTS:
         fine = attempt == "fine-grained"
-        rs, x_own, it, stt, t_solve, split = solve(coords, tets, b, gmask, a.rtol)
-        parts = [None] * world
-        tdist.all_gather_object(parts, (rs.lo, rs.hi, x_own.cpu()))
-        ok, why = 1, ""
-        if rank == 0:
-            x = torch.empty(N * bs, dtype=F64)
-            for lo, hi, xp in parts:
-                x[lo * bs:hi * bs] = xp
-            err = float((x - ref_x).abs().max() / ref_x.abs().max())
-            ok = int(stt == C.PCG_CONVERGED and ref_st == C.PCG_CONVERGED and abs(it - ref_it) <= 1 and err < 1e-10)
-            why = f"{attempt} comm blocks: status {stt} / {ref_st}, iterations {it} / {ref_it}, x rel diff {err:.3e}"
-        verdict = [ok, why]
-        tdist.broadcast_object_list(verdict, src=0)
+        ta = time.perf_counter()
+        _, _, it0, st0, _, _ = solve(c0, t0_, b0, m0, 1e-6)
+        warm_ok = tmin(1.0 if st0 == C.PCG_CONVERGED else 0.0) > 0
+        if not warm_ok:
+            verdict = [0, f"{attempt} comm blocks: warm-up solve status {st0} after {it0} iterations"]
+        else:
+            rs, x_own, it, stt, t_solve, split = solve(coords, tets, b, gmask, a.rtol)
+            parts = [None] * world
+            tdist.all_gather_object(parts, (rs.lo, rs.hi, x_own.cpu()))
+            ok, why = 1, ""
+            if rank == 0:
+                x = torch.empty(N * bs, dtype=F64)
+                for lo, hi, xp in parts:
+                    x[lo * bs:hi * bs] = xp
+                err = float((x - ref_x).abs().max() / ref_x.abs().max())
+                ok = int(stt == C.PCG_CONVERGED and ref_st == C.PCG_CONVERGED and abs(it - ref_it) <= 1 and err < 1e-10)
+                why = f"{attempt} comm blocks: status {stt} / {ref_st}, iterations {it} / {ref_it}, x rel diff {err:.3e}"
+            verdict = [ok, why]
+            tdist.broadcast_object_list(verdict, src=0)
+        attempts_log.append({"comm_block": attempt, "ok": bool(verdict[0]), "why": verdict[1],
+                             "seconds": round(tmax(time.perf_counter() - ta), 3)})
         if verdict[0]:
             break
         print(f"[rank {rank}] persistent multi-GPU schedule failed its self-check ({verdict[1]})", file=sys.stderr,
               flush=True)
+    del c0, t0_, b0, m0
     if not verdict[0]:
         print(f"[rank {rank}] measuring the RCCL path instead", file=sys.stderr, flush=True)
+        release_stream()
         return False, None
 
     # fixed-iteration timing: W warm-up steps, then exactly K steps as one launch per rank, max over ranks
@@ -454,7 +495,14 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False, kind="pois
     alg_own = 8 * bs * bs * nnz_own + (idx_own if n_uni else 2 * nnz_own) + 4 * (n_own + 1) + 16 * n_own * bs
     alg_total = tsum(float(alg_own))
     run.close()
-    ok_steps = it2 == a.warmup + a.steps and stt2 == C.PCG_RUNNING
+    # every rank must have run exactly the W + K iterations of the timed launches: a launch that gave up
+    # (FEM_PCG_SYNC_TIMEOUT) or stopped early on any rank publishes nothing; the caller measures RCCL instead
+    ok_steps = tmin(1.0 if (it2 == a.warmup + a.steps and stt2 == C.PCG_RUNNING) else 0.0) > 0
+    if not ok_steps:
+        print(f"[rank {rank}] persistent multi-GPU timed launch did not complete its steps (iterations {it2}, "
+              f"status {stt2}); measuring the RCCL path instead", file=sys.stderr, flush=True)
+        release_stream()
+        return False, None
     out = None
     if rank == 0:
         per_it = ms_max * 1e-3 / a.steps
@@ -470,7 +518,8 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False, kind="pois
                                    "in-kernel hand-offs over xGMI (IPC-mapped comm blocks), no collective per "
                                    "iteration" + (" [ranks emulated on ONE GPU]" if same_gpu else ""),
                        "tets": int(tets.shape[0]), "dofs": N * bs, "parallelism": f"row partition x{world}",
-                       "steps_completed": bool(ok_steps), "self_check": verdict[1]},
+                       "comm_block": "fine-grained" if fine else "coarse-grained (hipMalloc)",
+                       "self_check": verdict[1], "attempts": attempts_log},
             "dofs_per_s": N * bs / (t_asm + t_solve), "assembly_ms": t_asm * 1e3, "solve_ms": t_solve * 1e3,
             "solve_iters": it, "solve_status": stt,
             "kernel_ms": {"persist_iteration_max_over_ranks": per_it * 1e3, "iterations_per_launch": a.steps},
@@ -484,7 +533,5 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False, kind="pois
                          "stream_ceiling_GBps": ceiling, "frac_of_stream_read": achieved / ceiling["read"]},
             "cpu_baseline": None,
         }
-    if raw_stream:
-        torch.cuda.synchronize(dev)
-        lib.fem_stream_destroy(ctypes.c_void_p(raw_stream))
+    release_stream()
     return True, out

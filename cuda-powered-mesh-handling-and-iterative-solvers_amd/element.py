@@ -57,6 +57,8 @@ def human_readable_number(num):
 
 _VTK_NPE = {"c3d4": 4, "c3d10": 10, "c3d8": 8, "c3d20": 20, "c3d6": 6, "c3d15": 15, "s3": 3, "s6": 6, "s4": 4,
             "s8": 8}
+_VTK_CODE = {10: "c3d4", 24: "c3d10", 12: "c3d8", 25: "c3d20", 13: "c3d6", 26: "c3d15", 5: "s3", 22: "s6", 9: "s4",
+             23: "s8"}
 
 
 def read_vtk(file_path):
@@ -83,11 +85,30 @@ def read_vtk(file_path):
     return pts, cells, types
 
 
-def vtk_loader_to_torch(file_path, element_type, device="cuda:0", dtype=torch.float32):
+def infer_vtk_element_type(cell_types):
+    """Element type name of a homogeneous VTK cell-type array (VTK codes: 10 tetra, 24 quadratic tetra, 12
+    hexahedron, 25 quadratic hexahedron, 13 wedge, 26 quadratic wedge, 5 triangle, 22 quadratic triangle, 9 quad,
+    23 quadratic quad). ValueError for an empty, mixed or unsupported cell set."""
+    import numpy as np
+    kinds = np.unique(np.asarray(cell_types, dtype=np.int64))
+    if kinds.size != 1:
+        raise ValueError("Cannot infer the element type: the file holds "
+                         + ("no cells." if kinds.size == 0 else f"mixed VTK cell types {kinds.tolist()}."))
+    code = int(kinds[0])
+    if code not in _VTK_CODE:
+        raise ValueError(f"Cannot infer the element type: unsupported VTK cell type {code}.")
+    return _VTK_CODE[code]
+
+
+def vtk_loader_to_torch(file_path, element_type=None, device="cuda:0", dtype=torch.float32):
     """(points [N,3], connectivity [M,npe]) from a VTK file: the count-prefixed cell array reshaped to
     [-1, npe+1] with the count column dropped, exactly as `solver/element.py:39-90` does with pyvista's
-    mesh.cells (so mixed cell sizes fail the same way). ValueError("Invalid element type.") for other types."""
-    pts, cells, _ = read_vtk(file_path)
+    mesh.cells (so mixed cell sizes fail the same way). ValueError("Invalid element type.") for other types.
+    `element_type=None` (the one-argument call of `solver_example.ipynb:82`, written against an older
+    reference API) takes the type from the file's homogeneous cell types (`infer_vtk_element_type`)."""
+    pts, cells, types = read_vtk(file_path)
+    if element_type is None:
+        element_type = infer_vtk_element_type(types)
     points = torch.tensor(pts, device=device, dtype=dtype)
     if element_type not in _VTK_NPE:
         raise ValueError("Invalid element type.")

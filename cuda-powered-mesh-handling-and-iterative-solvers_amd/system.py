@@ -73,6 +73,7 @@ class PcgResult:
     rz: float            # last r.z (r.r in CG mode) — the "Residual norm" the reference prints (squared)
     pq: float            # last p.Ap (printed on breakdown)
     history: torch.Tensor = None
+    schedule: int = -1   # the kernel schedule the solve ran (SCHED_*; after any fallback)
 
 
 @dataclass
@@ -350,12 +351,13 @@ class SellMatrix:
                                       ctypes.byref(rz)), "fem_pcg_solve")
             sc = (ctypes.c_double * 6)()
             C.check(lib.fem_pcg_scalars(h, sc), "fem_pcg_scalars")
+            ran = int(lib.fem_pcg_get_schedule(h))
             _check_sync(stt.value)
         finally:
             lib.fem_pcg_destroy(h)
         if hist is not None:
             hist = hist[: min(it.value, hist.numel())]
-        return PcgResult(x, it.value, stt.value, rz.value, sc[1], hist)
+        return PcgResult(x, it.value, stt.value, rz.value, sc[1], hist, ran)
 
 
 def _check_sync(status):
@@ -467,7 +469,7 @@ def stream_ceiling(dev, gib=2.0, reps=5):
     out = torch.zeros(1, dtype=torch.float64, device=dev)
     st = torch.cuda.current_stream(dev)
     res = {}
-    for name, fn, nbytes in (("read", lambda: lib.fem_lab_copy(16, 1, C.ptr(src), C.ptr(out), n, 4096, C.stream(dev)), n * 8),
+    for name, fn, nbytes in (("read", lambda: lib.fem_stream_read(C.ptr(src), C.ptr(out), n, 4096, C.stream(dev)), n * 8),
                              ("copy", lambda: lib.fem_stream_copy(C.ptr(src), C.ptr(dst), n // 2, 4096, C.stream(dev)), n * 8)):
         best = None
         for _ in range(reps + 1):

@@ -311,41 +311,11 @@ int fem_sell_delta16(const int32_t* cols, int64_t nrows, const int64_t* slice_pt
                      fem_stream_t stream);
 int fem_spmv16(int64_t nrows, int bs, const int64_t* slice_ptr, const int16_t* dcols, const double* vals,
                const double* x, double* y, fem_stream_t stream);
-/* tuning / measurement entry points (tools/spmv_tune.py): SpMV code variants and grid size (grid <= 0:
- * default), and the HBM copy-ceiling probe dst = src over n doubles (n even, 16-byte aligned). */
-int fem_spmv_variant(int variant, int grid, int64_t nrows, int bs, const int64_t* slice_ptr, const int32_t* cols,
-                     const double* vals, const double* x, double* y, fem_stream_t stream);
+/* measurement entry points (bench.py stream_ceiling): the HBM copy-ceiling probe dst = src and the read-only
+ * probe (16-byte loads summed, *out written only to keep the loads alive) over n doubles (n even, 16-byte
+ * aligned); grid <= 0: default. */
 int fem_stream_copy(const double* src, double* dst, int64_t n, int grid, fem_stream_t stream);
-/* layout lab (tools/spmv_layout.py): W-byte-per-lane copy / read probes (W = 8, 16, 32), the lane-paired SELL-64
- * layout (two consecutive entries of a row per 16-byte value load + 4-byte column load) and its SpMV */
-int fem_lab_copy(int width, int read_only, const double* src, double* dst, int64_t n, int grid, fem_stream_t stream);
-int fem_lab_sell_pair(int64_t nrows, const int64_t* slice_ptr, const double* vals, const int16_t* dcols,
-                      double* vals_out, int16_t* dcols_out, fem_stream_t stream);
-int fem_lab_spmv16_pair(int u, int grid, int64_t nrows, const int64_t* slice_ptr, const int16_t* dcols,
-                        const double* vals, const double* x, double* y, fem_stream_t stream);
-// persistent-geometry SpMV probe (paired bs = 1 layout): one workgroup of `threads` per CU pinned by lds_bytes of
-// dynamic LDS, contiguous slice ranges per wave
-int fem_lab_spmv_persist(int threads, int u, int grid, int64_t lds_bytes, int64_t nrows, const int64_t* slice_ptr,
-                         const int16_t* dcols, const double* vals, const double* x, double* y, fem_stream_t stream);
-// bs = 3 layout probes (sell_pair3.hpp): layout 1 plane-paired values, 2 entry-paired values + int32 column pairs
-int fem_lab_sell3_layout(int layout, int64_t nrows, const int64_t* slice_ptr, const double* vals,
-                         const int16_t* dcols, double* vals_out, int16_t* dcols_out, fem_stream_t stream);
-int fem_lab_spmv3(int layout, int u, int nt, int grid, int64_t nrows, const int64_t* slice_ptr, const int16_t* dcols,
-                  const double* vals, const double* x, double* y, fem_stream_t stream);
-/* probes (tools/sym_probe.py): the production bs = 1 paired copy with slice-uniform deltas (k_sell_pair +
- * k_sell_uniform) and the persistent-geometry SpMV over it; a symmetric-storage SpMV (upper triangle only, lower
- * entries re-read from the rows they mirror) in the same geometry */
-int fem_lab_sell_uniform(int64_t nrows, const int64_t* slice_ptr, const double* vals, const int16_t* dcols,
-                         double* vals_out, int16_t* dcols_out, int16_t* ucol, int32_t* uoff, fem_stream_t stream);
-int fem_lab_spmv_persist_uni(int grid, int64_t lds_bytes, int64_t nrows, const int64_t* slice_ptr,
-                             const int16_t* pcols, const double* pvals, const int32_t* uoff, const int16_t* ucol,
-                             const double* x, double* y, fem_stream_t stream);
-int fem_lab_spmv_gather(int mode, int grid, int64_t lds_bytes, int64_t nrows, const int64_t* slice_ptr,
-                        const double* pvals, const int32_t* uoff, const int16_t* ucol, const double* x, double* y,
-                        fem_stream_t stream);
-int fem_lab_spmv_sym(int grid, int64_t lds_bytes, int64_t nrows, const int64_t* uptr, const int32_t* ulist,
-                     const int16_t* udel, const int32_t* lptr, const int32_t* ldel, const int32_t* lbase,
-                     const double* uvals, const double* x, double* y, fem_stream_t stream);
+int fem_stream_read(const double* src, double* out, int64_t n, int grid, fem_stream_t stream);
 
 /* ------------------------------------------------------------------ (P)CG (L3)
  * One solve context over a SELL matrix. The whole iteration runs on the device: SpMV + p.q reduction,
@@ -365,8 +335,12 @@ int fem_pcg_create(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_
 int fem_pcg_start(fem_pcg* s);
 /* enqueue k iterations (no host sync); iterations after a stop are no-ops on the device */
 int fem_pcg_iterate(fem_pcg* s, int k);
-/* [sync] read iteration count, status and last r.z (or r.r) */
+/* [sync] read iteration count, status and last r.z (or r.r). Guard stops (FEM_PCG_BREAKDOWN / _ALPHA_NAN) report
+ * the reference's printed iteration; every other status the completed iterations */
 int fem_pcg_poll(fem_pcg* s, int* iters, int* status, double* rz);
+/* [sync] diagnostic of a FEM_PCG_SYNC_TIMEOUT: the persistent kernel's give-up site code (1 grid barrier,
+ * 2 u-flag window, 3 rank sums of the DIST build; + 16 * epoch), 0 for any other status */
+int fem_pcg_sync_site(fem_pcg* s, int* site);
 /* [sync] out6 = {rz (rs_old), pq (p.Ap), alpha, beta, rz_new, completed iterations} for the host messages */
 int fem_pcg_scalars(fem_pcg* s, double* out6);
 /* [sync] run to completion: start + chunks of `chunk` iterations until stop or max_iter (persistent schedule:
@@ -421,7 +395,10 @@ int fem_enforce_constraints(double* x, double* r, int64_t n, int order, int64_t 
  * the next sweep: 67 -> 57 us per SpMV on the 10M Poisson matrix. Results depend on the flags only through the
  * order of the per-block p.q partials (deterministic for a given flag set). */
 enum { FEM_TUNE_REVERSE = 1, FEM_TUNE_PAIR = 2, FEM_TUNE_PK_SC1 = 4, FEM_TUNE_PK_PACK = 8, FEM_TUNE_C1F = 16,
-       FEM_TUNE_PK_COOP = 32, FEM_TUNE_DIST_FINE = 64, FEM_TUNE_PK_UNI = 128, FEM_TUNE_PK_WIDE = 256 };
+       FEM_TUNE_PK_COOP = 32, FEM_TUNE_DIST_FINE = 64, FEM_TUNE_PK_UNI = 128, FEM_TUNE_PK_WIDE = 256,
+       FEM_TUNE_DIST_DROP = 512 };
+/* FEM_TUNE_DIST_DROP: fault injection for the multi-GPU failure chain (tests only): the rank publishes no u row and
+ * no flag to the other ranks, so their launches give up (FEM_PCG_SYNC_TIMEOUT) within the bounded waits */
 /* FEM_TUNE_PK_WIDE: persistent schedule (bs = 1, single GPU) -- keep the 7-slot build when every wave owns at most
  * one slice (by default such systems, e.g. 1M tets, run a one-slot build with 8 lane pairs in flight; A/B switch) */
 /* FEM_TUNE_PK_UNI (default): bs = 1 paired copies also record, per 64-row slice whose rows take their columns at one

@@ -171,3 +171,76 @@ def test_dist_persist_elastic_matches_single_gpu(gpu, n, jitter):
         finally:
             grp.close()
     assert rel(xs[0], x1) < 1e-12 and torch.equal(xs[0], xs[1])
+
+
+# ---------------------------------------------------------------------------- the N > 1 failure chain
+def test_dist_persist_drop_publish_gives_up(gpu):
+    """Fault injection (FEM_TUNE_DIST_DROP on rank 1: it publishes no u row and no flag): every rank's launch ends
+    with FEM_PCG_SYNC_TIMEOUT within the bounded waits (2 s per in-GPU wait, 5 s for the rank exchange), each with a
+    give-up site -- never a hang."""
+    import time
+    C, DP, mesh, system = _mods()
+    c, t, b, mask, A, w = _case(mesh, system, 24, gpu)
+    grp = DP.EmulatedGroup(c, t, 2, b, fixed_mask=mask, tol=1e-12, drop_rank=1)
+    try:
+        t0 = time.perf_counter()
+        grp.start()
+        grp.iterate(200)
+        dt = time.perf_counter() - t0
+        polls = grp.poll_ranks()
+        assert all(p[1] == C.PCG_SYNC_TIMEOUT for p in polls), polls
+        sites = [rr.sync_site() for rr in grp.ranks]
+        assert all(s % 16 in (1, 2, 3) for s in sites), sites
+        assert all(0 <= p[0] < 200 for p in polls), polls   # completed iterations, not a site code
+        assert dt < 15.0, dt
+    finally:
+        grp.close()
+
+
+def _bench_two_ranks(extra_env, n=40, timeout=300):
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, FEM355_DIST_SAME_GPU="1", MASTER_ADDR="127.0.0.1", **extra_env)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", "--cube-n", str(n),
+           "--steps", "20", "--warmup", "5", "--elastic", "0", "--no-cpu-baseline"]
+    t0 = time.perf_counter()
+    p = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=timeout)
+    dt = time.perf_counter() - t0
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    return p, lines, dt
+
+
+def test_bench_two_ranks_same_gpu_prints_one_line(gpu):
+    """`bench.py --gpus 2` with both ranks on this GPU (FEM355_DIST_SAME_GPU=1): the persistent multi-GPU schedule
+    passes its self-check on the first attempt (fine-grained comm blocks) and rank 0 prints exactly one JSON line
+    whose timed launch completed its steps, within the stated budget (120 s on one GPU)."""
+    p, lines, dt = _bench_two_ranks({})
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert len(lines) == 1, p.stdout[-2000:]
+    cfg = lines[0]["config"]
+    assert lines[0]["value"] > 0 and lines[0]["n_gpus"] == 2
+    assert cfg["comm_block"] == "fine-grained" and cfg["attempts"][0]["ok"], cfg
+    assert dt < 120.0, dt
+
+
+def test_bench_two_ranks_drop_publish(gpu):
+    """The failure chain with rank 1 publishing nothing (FEM355_DIST_DROP_RANK=1): both comm-block attempts fail
+    their warm-up solve with a bounded give-up, and -- RCCL refusing two ranks per GPU -- the run ends with the
+    documented error instead of a line or a hang, within the stated budget (90 s on one GPU). On a
+    multi-GPU node the same chain continues with the RCCL element partition (`tests/test_dist_chain.py`)."""
+    p, lines, dt = _bench_two_ranks({"FEM355_DIST_DROP_RANK": "1"})
+    assert p.returncode != 0 and not lines
+    err = p.stderr
+    assert err.count("fine-grained comm blocks: warm-up solve status 6") >= 1, err[-3000:]
+    assert err.count("coarse-grained comm blocks: warm-up solve status 6") >= 1, err[-3000:]
+    assert "no RCCL fallback possible" in err, err[-3000:]
+    assert dt < 90.0, dt

@@ -327,6 +327,39 @@ def test_static_structure_mixed_vs_reference(gpu):
     assert abs(res.iterations - int(g["n_iter"])) <= 2 and rel(u, g["u"]) < 1e-10
 
 
+@pytest.mark.parametrize("sched", ["three_kernel", "default"])
+def test_golden_solvers_per_schedule(gpu, sched, monkeypatch, capsys):
+    """The reference-API solvers on the golden fixtures under each schedule the library can pick: the three-kernel
+    schedule (0) and the default -- the persistent kernels (k_pcg_persist for bs = 1, k_pcg_persist3 for these
+    bs = 3 systems, which fit on chip). Both against the reference's own outputs (`solver/solver.py:11-229`,
+    `:766-812`)."""
+    _, _, solver, system = _mods()
+    if sched == "three_kernel":
+        monkeypatch.setattr(system, "DEFAULT_SCHEDULE", {1: system.SCHED_THREE, 3: system.SCHED_THREE})
+    want = system.SCHED_THREE if sched == "three_kernel" else system.SCHED_PERSIST
+    g = load_golden("tet4_cube_n4_jit")
+    u, res = solver.stable_conjugate_gradient_solver(g["K"], g["tets"], g["F"], g["fixed"], tol=float(g["tol"]),
+                                                     device=gpu, return_info=True)
+    assert res.schedule == want, res.schedule
+    assert abs(res.iterations - int(g["n_cg"])) <= 2 and rel(u, g["u_cg"]) < 1e-10
+    u, res = solver.preconditioned_conjugate_gradient_solver(g["K"], g["tets"], g["F"], g["Minv"], tol=1e-6,
+                                                             device=gpu, dtype=F64, return_info=True)
+    assert res.schedule == want, res.schedule
+    assert abs(res.iterations - int(g["n_pcg"])) <= 2 and rel(u, g["u_pcg"]) < 1e-10
+    m = load_golden("mixed_static")
+    u, res = solver.static_structure_solver(m["coords"], m["force"], m["fixed"], c3d4=m["c3d4"], c3d6=m["c3d6"],
+                                            c3d8=m["c3d8"], material={"E": E, "nu": NU}, tol=1e-6, max_iter=3000,
+                                            device=gpu, return_info=True)
+    assert res.schedule == want, res.schedule
+    assert abs(res.iterations - int(m["n_iter"])) <= 2 and rel(u, m["u"]) < 1e-10
+    p = load_golden("poisson_tet4_n4_jit")
+    u, res, _ = solver.solve_tet4(p["coords"], p["tets"], p["f"].view(-1, 1), p["fixed"], kind="poisson",
+                                  tol=float(p["tol"]), device=gpu)
+    assert res.schedule == want, res.schedule
+    assert abs(res.iterations - int(p["n_pcg"])) <= 2 and rel(u[:, 0], p["u"]) < 1e-10
+    capsys.readouterr()
+
+
 def test_cg_guard_breakdown(gpu, capsys):
     """pAp <= 0 on an indefinite operator (the reference's negative-definite c3d10 rule, Q2) stops at iteration 1."""
     el, mesh, solver, _ = _mods()

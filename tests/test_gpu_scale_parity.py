@@ -1,0 +1,87 @@
+"""GPU tier at the BASELINE.json configuration sizes: the HIP path against the oracle (`oracle/ref_cpu.py`, the
+reference's op sequence on torch-CPU, pinned bit-exactly to the reference's golden vectors by
+`tests/test_oracle_golden.py`) on the full benchmark meshes, not on stand-ins. Ordered cheapest first (the driver
+runs `pytest -x`).
+
+  * configs[4] (2M-element c3d8 / c3d6 / c3d10 set): `compute_K_matrix` on each whole family mesh, a seeded
+    10,000-element sample checked against `R.iso_K` (`solver/element.py:1754-1803`, `:2631-2676`, `:1191-1239`);
+  * configs[1] (1M-tet P1 Poisson, n = 55): `solve_tet4` to rtol 1e-8 against `R.pcg` over the oracle's element
+    matrices (`solver/solver.py:766-812`): iterations within +-2, u within 1e-10;
+  * configs[2] (10M-tet P1 elasticity, n = 119): the assembled SELL operator applied to a seeded vector against the
+    oracle's EBE product `R.nodal_forces(R.tet4_K(...))` (`solver/element.py:429-464`, `:883-903`) to 1e-12, and the
+    first 5 Jacobi-PCG iterates of the default bs = 3 schedule against `R.pcg` to 1e-10.
+The oracle's element matrices at 10M tets take ~12 GB of host memory and ~10 s on the box's 16 cores."""
+import pytest
+import torch
+
+from conftest import rel
+from oracle import ref_cpu as R
+
+pytestmark = pytest.mark.gpu
+E, NU = 113.8e9, 0.342
+F64 = torch.float64
+
+
+def _mods():
+    import fem355  # noqa: F401
+    from fem355 import element, mesh, solver, system
+    return element, mesh, solver, system
+
+
+@pytest.mark.parametrize("etype,n", [("c3d6", 70), ("c3d8", 88), ("c3d10", 48)])
+def test_config4_family_stiffness_sample_vs_oracle(gpu, etype, n):
+    """BASELINE configs[4]: 686,000 wedges (2 x 70^3), 681,472 hexes (88^3), 663,552 P2 tets (6 x 48^3), jittered."""
+    el, mesh, _, _ = _mods()
+    gen = {"c3d8": mesh.hex_box, "c3d6": mesh.wedge_box, "c3d10": mesh.tet10_cube}[etype]
+    c, e = gen(n, jitter=0.1)
+    K = el.compute_K_matrix(c, e, etype, E, NU, device=gpu, dtype=F64)
+    assert K.shape == (e.shape[0], 3 * e.shape[1], 3 * e.shape[1])
+    idx = torch.randperm(e.shape[0], generator=torch.Generator().manual_seed(20250418))[:10000].sort().values
+    Ks = K[idx.to(gpu)].cpu()
+    del K
+    assert rel(Ks, R.iso_K(c, e[idx], etype, E, NU)) < 1e-12
+
+
+def test_config1_poisson_1m_solve_vs_oracle(gpu):
+    """BASELINE configs[1]: 998,250 tets, 175,616 DOFs, Jacobi-PCG to rtol 1e-8 (the bench's DOFs/s solve)."""
+    _, mesh, solver, _ = _mods()
+    c, t = mesh.kuhn_cube(55)
+    f, fixed = mesh.cube_poisson_case(c)
+    u, res, _ = solver.solve_tet4(c, t, f, fixed, kind="poisson", rtol=1e-8, device=gpu)
+    KP = R.tet4_poisson_K(c, t)
+    N = c.shape[0]
+    dinv = R.diag_preconditioner(KP, t, N, dpn=1)
+    dinv[fixed] = 0.0
+    b = f.reshape(N, 1).to(F64)
+    tol = 1e-8 * float(torch.sqrt(torch.sum(b * dinv * b)))
+    u_ref, it_ref, st = R.pcg(KP, t, b, dinv, tol=tol, max_iter=5000)
+    assert st == "converged" and abs(res.iterations - it_ref) <= 2, (res.iterations, it_ref)
+    assert rel(u, u_ref) < 1e-10
+
+
+def test_config2_elasticity_10m_operator_and_iterates_vs_oracle(gpu):
+    """BASELINE configs[2]: 10,110,954 tets, 5,184,000 DOFs. The assembled operator (fused on-the-fly assembly into
+    SELL-64 with 16-bit deltas, the bench's) equals the reference's EBE operator over its own element matrices, and
+    the default bs = 3 schedule's first 5 PCG iterates equal the reference PCG's."""
+    _, mesh, _, system = _mods()
+    c, t = mesh.kuhn_cube(119)
+    N = c.shape[0]
+    assert t.shape[0] == 10_110_954
+    f, fixed = mesh.cube_elasticity_case(c)
+    A = system.assemble_tet4_system(c.to(gpu), t.to(gpu), "elastic", E, NU)
+    assert A.use16
+    p = torch.randn(N, 3, dtype=F64, generator=torch.Generator().manual_seed(11))
+    y = A.matvec(p.reshape(-1).to(gpu)).cpu()
+    K = R.tet4_K(c, t, E, NU)
+    assert rel(y, R.nodal_forces(K, t, p).reshape(-1)) < 1e-12
+    mask = torch.zeros((N, 3), dtype=torch.uint8, device=gpu)
+    mask[fixed.to(gpu)] = 1
+    w = A.jacobi(mask.view(-1))
+    b = f.reshape(-1).to(F64)
+    res = A.pcg(b, w=w, tol=0.0, max_iter=5)
+    assert res.iterations == 5
+    dinv = R.diag_preconditioner(K, t, N, dpn=3)
+    dinv[fixed] = 0.0
+    assert rel(w.cpu(), dinv.reshape(-1)) < 1e-14
+    u_ref, it_ref, _ = R.pcg(K, t, b.view(N, 3), dinv, tol=0.0, max_iter=5)
+    assert it_ref == 5 and rel(res.x.cpu(), u_ref.reshape(-1)) < 1e-10

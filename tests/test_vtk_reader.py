@@ -85,6 +85,36 @@ def test_other_solids(tmp_path, etype, gen):
     assert cells.shape[0] == e.shape[0] * (e.shape[1] + 1) and set(types.tolist()) == {VTK_TYPE[e.shape[1]]}
 
 
+@pytest.mark.parametrize("etype,gen", [("c3d4", mesh.kuhn_cube), ("c3d8", mesh.hex_box), ("c3d6", mesh.wedge_box),
+                                       ("c3d10", mesh.tet10_cube)])
+def test_one_argument_call_infers_type(tmp_path, etype, gen):
+    """`coords, elements = solver.vtk_loader_to_torch(path)` (`solver_example.ipynb:82`): the element type comes
+    from the file's cell types; the result equals the explicit-type call."""
+    c, e = gen(2)
+    p = tmp_path / f"{etype}.vtk"
+    write_vtk(p, c, e, "4.2", True)
+    if torch.cuda.is_available():
+        pts, el = element.vtk_loader_to_torch(str(p))          # literally the notebook's call
+    else:
+        pts, el = element.vtk_loader_to_torch(str(p), device="cpu")
+    pts2, el2 = element.vtk_loader_to_torch(p, etype, device=pts.device)
+    assert torch.equal(el, el2) and torch.equal(pts, pts2) and pts.dtype == torch.float32
+    assert torch.equal(el.cpu(), e)
+
+
+def test_one_argument_call_rejects_mixed_cells(tmp_path):
+    c, t = mesh.kuhn_cube(1)
+    p = tmp_path / "mixed.vtk"
+    write_vtk(p, c, [list(t[0]), [0, 1, 2, 3, 4, 5, 6, 7]])
+    with pytest.raises(ValueError, match="mixed VTK cell types"):
+        element.vtk_loader_to_torch(p, device="cpu")
+    assert element.infer_vtk_element_type(np.array([10, 10])) == "c3d4"
+    with pytest.raises(ValueError, match="no cells"):
+        element.infer_vtk_element_type(np.array([], dtype=np.int64))
+    with pytest.raises(ValueError, match="unsupported VTK cell type 42"):
+        element.infer_vtk_element_type(np.array([42]))
+
+
 def test_reference_error_behaviour(tmp_path):
     c, t = mesh.kuhn_cube(1)
     p = tmp_path / "m.vtk"

@@ -18,7 +18,7 @@ step() {  # name, seconds, command...
 rm -f gpurun_out/steps.log
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
-  step pytest_gpu 900 python -m pytest tests -m gpu -q -x
+  step pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread -p no:cacheprovider --durations=20
   step smoke 300 python __graft_entry__.py smoke
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then

@@ -7,6 +7,7 @@
 // same for the 16-bit column deltas. Footprint and slice_ptr are unchanged.
 #include "sell_pair.hpp"
 #include "sell_pair3.hpp"
+#include "fem355_lab.h"
 
 namespace fem {
 

@@ -16,6 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import fem355  # noqa: E402
 from fem355 import _capi as C, mesh, system  # noqa: E402
+import lab as lab_lib  # noqa: E402  (tools/lab: probe kernels, not part of libfem355)
 
 
 def timed(fn, reps, pre=None):
@@ -38,6 +39,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     lib = C.lib()
+    lab = lab_lib.load()
     dev = torch.device("cuda", 0)
     st = C.stream(dev)
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
@@ -49,16 +51,16 @@ def main():
     alg = A.algorithmic_bytes_spmv(index_bytes=2)
     vp = torch.empty_like(A.vals)
     cp = torch.empty_like(g.dcols)
-    C.check(lib.fem_lab_sell_pair(g.n_nodes, C.ptr(g.slice_ptr), C.ptr(A.vals), C.ptr(g.dcols), C.ptr(vp), C.ptr(cp),
+    C.check(lab.fem_lab_sell_pair(g.n_nodes, C.ptr(g.slice_ptr), C.ptr(A.vals), C.ptr(g.dcols), C.ptr(vp), C.ptr(cp),
                                   st), "pair")
     pol = torch.empty(140 * (1 << 20) // 8, dtype=torch.float64, device=dev)
     pol2 = torch.empty_like(pol)
 
     def pollute():
-        C.check(lib.fem_lab_copy(16, 0, C.ptr(pol), C.ptr(pol2), pol.numel(), 2048, st), "pollute")
+        C.check(lab.fem_lab_copy(16, 0, C.ptr(pol), C.ptr(pol2), pol.numel(), 2048, st), "pollute")
 
     def base():
-        C.check(lib.fem_lab_spmv16_pair(8, 0, g.n_nodes, C.ptr(g.slice_ptr), C.ptr(cp), C.ptr(vp), C.ptr(x), C.ptr(y),
+        C.check(lab.fem_lab_spmv16_pair(8, 0, g.n_nodes, C.ptr(g.slice_ptr), C.ptr(cp), C.ptr(vp), C.ptr(x), C.ptr(y),
                                         st), "pair spmv")
     base()
     torch.cuda.synchronize()
@@ -68,7 +70,7 @@ def main():
                           (512, 64 << 10, 2)):
         for u in (4, 8):
             def run(thr=thr, lds=lds, u=u, wgs=wgs):
-                C.check(lib.fem_lab_spmv_persist(thr, u, ncu * wgs, lds, g.n_nodes, C.ptr(g.slice_ptr), C.ptr(cp),
+                C.check(lab.fem_lab_spmv_persist(thr, u, ncu * wgs, lds, g.n_nodes, C.ptr(g.slice_ptr), C.ptr(cp),
                                                  C.ptr(vp), C.ptr(x), C.ptr(y), st), "persist")
             y.zero_()
             run()

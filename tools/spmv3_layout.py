@@ -18,6 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import fem355  # noqa: E402
 from fem355 import _capi as C, mesh, system  # noqa: E402
+import lab as lab_lib  # noqa: E402  (tools/lab: probe kernels, not part of libfem355)
 
 
 def timed(fn, reps):
@@ -38,6 +39,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     lib = C.lib()
+    lab = lab_lib.load()
     dev = torch.device("cuda", 0)
     st = C.stream(dev)
     coords, tets = mesh.kuhn_cube(a.n, device=dev)
@@ -60,7 +62,7 @@ def main():
     for L in (1, 2):
         v = torch.empty_like(A.vals)
         c = torch.empty_like(g.dcols) if L == 2 else g.dcols
-        C.check(lib.fem_lab_sell3_layout(L, g.n_nodes, C.ptr(g.slice_ptr), C.ptr(A.vals), C.ptr(g.dcols), C.ptr(v),
+        C.check(lab.fem_lab_sell3_layout(L, g.n_nodes, C.ptr(g.slice_ptr), C.ptr(A.vals), C.ptr(g.dcols), C.ptr(v),
                                          C.ptr(c), st), "layout")
         lay[L] = (v, c)
     torch.cuda.synchronize()
@@ -70,7 +72,7 @@ def main():
         for u in (1, 2):
             for nt in (0, 1):
                 def run(L=L, u=u, nt=nt, v=v, c=c):
-                    C.check(lib.fem_lab_spmv3(L, u, nt, 0, g.n_nodes, C.ptr(g.slice_ptr), C.ptr(c), C.ptr(v),
+                    C.check(lab.fem_lab_spmv3(L, u, nt, 0, g.n_nodes, C.ptr(g.slice_ptr), C.ptr(c), C.ptr(v),
                                               C.ptr(x), C.ptr(y), st), "spmv3")
                 y.zero_()
                 run()

@@ -20,6 +20,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import fem355  # noqa: E402
 from fem355 import _capi as C, mesh, system  # noqa: E402
+import lab as lab_lib  # noqa: E402  (tools/lab: probe kernels, not part of libfem355)
 
 
 def timed(fn, reps, pre=None):
@@ -45,6 +46,7 @@ def main():
     ap.add_argument("--tunes", default="0,1")
     a = ap.parse_args()
     lib = C.lib()
+    lab = lab_lib.load()
     dev = torch.device("cuda", 0)
     st = C.stream(dev)
     out = {}
@@ -55,10 +57,10 @@ def main():
     dst = torch.empty_like(src)
     for w in (8, 16, 32):
         for g in (2048, 8192):
-            ms = timed(lambda: C.check(lib.fem_lab_copy(w, 0, C.ptr(src), C.ptr(dst), nb, g, st), "copy"), 5)
+            ms = timed(lambda: C.check(lab.fem_lab_copy(w, 0, C.ptr(src), C.ptr(dst), nb, g, st), "copy"), 5)
             out[f"copy{w}_g{g}_GBps"] = 2 * nb * 8 / (ms * 1e-3) / 1e9
     for w in (8, 16):
-        ms = timed(lambda: C.check(lib.fem_lab_copy(w, 1, C.ptr(src), C.ptr(dst), nb, 4096, st), "read"), 5)
+        ms = timed(lambda: C.check(lab.fem_lab_copy(w, 1, C.ptr(src), C.ptr(dst), nb, 4096, st), "read"), 5)
         out[f"read{w}_GBps"] = nb * 8 / (ms * 1e-3) / 1e9
     del src, dst
     print(json.dumps(out), flush=True)
@@ -73,7 +75,7 @@ def main():
     ref = A.matvec(x).clone()
     vp = torch.empty_like(A.vals)
     cp = torch.empty_like(g.dcols)
-    C.check(lib.fem_lab_sell_pair(g.n_nodes, C.ptr(g.slice_ptr), C.ptr(A.vals), C.ptr(g.dcols), C.ptr(vp), C.ptr(cp),
+    C.check(lab.fem_lab_sell_pair(g.n_nodes, C.ptr(g.slice_ptr), C.ptr(A.vals), C.ptr(g.dcols), C.ptr(vp), C.ptr(cp),
                                   st), "pair")
 
     def plain():
@@ -86,7 +88,7 @@ def main():
     res["plain_ms"] = ms
     for u in (2, 4, 8):
         def pair(u=u):
-            C.check(lib.fem_lab_spmv16_pair(u, 0, g.n_nodes, C.ptr(g.slice_ptr), C.ptr(cp), C.ptr(vp), C.ptr(x),
+            C.check(lab.fem_lab_spmv16_pair(u, 0, g.n_nodes, C.ptr(g.slice_ptr), C.ptr(cp), C.ptr(vp), C.ptr(x),
                                             C.ptr(y), st), "pair spmv")
         pair()
         torch.cuda.synchronize()
@@ -98,17 +100,17 @@ def main():
     pol2 = torch.empty_like(pol)
 
     def pollute():
-        C.check(lib.fem_lab_copy(16, 0, C.ptr(pol), C.ptr(pol2), pol.numel(), 2048, st), "pollute")
+        C.check(lab.fem_lab_copy(16, 0, C.ptr(pol), C.ptr(pol2), pol.numel(), 2048, st), "pollute")
     res["plain_after_140MB_ms"] = timed(plain, a.reps, pre=pollute)
     bigp = torch.empty(600 * (1 << 20) // 8, dtype=torch.float64, device=dev)
     bigp2 = torch.empty_like(bigp)
 
     def flush():
-        C.check(lib.fem_lab_copy(16, 0, C.ptr(bigp), C.ptr(bigp2), bigp.numel(), 2048, st), "flush")
+        C.check(lab.fem_lab_copy(16, 0, C.ptr(bigp), C.ptr(bigp2), bigp.numel(), 2048, st), "flush")
     res["plain_after_1200MB_ms"] = timed(plain, a.reps, pre=flush)
 
     def pair4():
-        C.check(lib.fem_lab_spmv16_pair(4, 0, g.n_nodes, C.ptr(g.slice_ptr), C.ptr(cp), C.ptr(vp), C.ptr(x),
+        C.check(lab.fem_lab_spmv16_pair(4, 0, g.n_nodes, C.ptr(g.slice_ptr), C.ptr(cp), C.ptr(vp), C.ptr(x),
                                         C.ptr(y), st), "pair spmv")
     res["pair_u4_after_1200MB_ms"] = timed(pair4, a.reps, pre=flush)
     for k in list(res):

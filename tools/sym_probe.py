@@ -17,6 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import fem355  # noqa: E402
 from fem355 import _capi as C, mesh, system  # noqa: E402
+import lab as lab_lib  # noqa: E402  (tools/lab: probe kernels, not part of libfem355)
 
 I32, I64, F64 = torch.int32, torch.int64, torch.float64
 
@@ -84,6 +85,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     lib = C.lib()
+    lab = lab_lib.load()
     dev = torch.device("cuda", 0)
     st = C.stream(dev)
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
@@ -104,13 +106,13 @@ def main():
     pc = torch.empty(ent, dtype=torch.int16, device=dev)
     ucol = torch.zeros(2 * (ent // 64) + 2, dtype=torch.int16, device=dev)
     uoff = torch.empty((N + 63) // 64, dtype=I32, device=dev)
-    C.check(lib.fem_lab_sell_uniform(N, C.ptr(g.slice_ptr), C.ptr(A.vals), C.ptr(g.dcols), C.ptr(pv), C.ptr(pc),
+    C.check(lab.fem_lab_sell_uniform(N, C.ptr(g.slice_ptr), C.ptr(A.vals), C.ptr(g.dcols), C.ptr(pv), C.ptr(pc),
                                      C.ptr(ucol), C.ptr(uoff), st), "uniform")
     ref = A.matvec(x)
     lds = 96 << 10
 
     def full():
-        C.check(lib.fem_lab_spmv_persist_uni(ncu, lds, N, C.ptr(g.slice_ptr), C.ptr(pc), C.ptr(pv), C.ptr(uoff),
+        C.check(lab.fem_lab_spmv_persist_uni(ncu, lds, N, C.ptr(g.slice_ptr), C.ptr(pc), C.ptr(pv), C.ptr(uoff),
                                              C.ptr(ucol), C.ptr(x), C.ptr(y), st), "full")
     full()
     torch.cuda.synchronize()
@@ -119,7 +121,7 @@ def main():
     out["full_us"] = timed(full, a.reps) * 1e3
     for mode in (1, 2):   # gather-volume probe (wrong results by design): half the gathers / none
         def gth(mode=mode):
-            C.check(lib.fem_lab_spmv_gather(mode, ncu, lds, N, C.ptr(g.slice_ptr), C.ptr(pv), C.ptr(uoff), C.ptr(ucol),
+            C.check(lab.fem_lab_spmv_gather(mode, ncu, lds, N, C.ptr(g.slice_ptr), C.ptr(pv), C.ptr(uoff), C.ptr(ucol),
                                             C.ptr(x), C.ptr(y), st), "gather")
         gth()
         out[f"gather_mode{mode}_us"] = timed(gth, a.reps) * 1e3
@@ -127,7 +129,7 @@ def main():
     out["upper_entries"] = sym["upper_entries"]
 
     def symm():
-        C.check(lib.fem_lab_spmv_sym(ncu, lds, N, C.ptr(sym["uptr"]), C.ptr(sym["ulist"]), C.ptr(sym["udel"]),
+        C.check(lab.fem_lab_spmv_sym(ncu, lds, N, C.ptr(sym["uptr"]), C.ptr(sym["ulist"]), C.ptr(sym["udel"]),
                                      C.ptr(sym["lptr"]), C.ptr(sym["ldel"]), C.ptr(sym["lbase"]), C.ptr(sym["uvals"]),
                                      C.ptr(x), C.ptr(y), st), "sym")
     y.zero_()
