@@ -107,6 +107,17 @@ def cpu_model():
     return None
 
 
+def s8d_models(n, nnz, spmv_ms, iter_ms, persist):
+    """SURVEY §8(d) byte models for n rows / nnz scalar nonzeros: B_spmv over the SpMV launch (persistent schedule:
+    the whole iteration, which contains it) and B_iter over the whole iteration, each as a fraction of 8 TB/s."""
+    b_spmv = 12 * nnz + 4 * (n + 1) + 16 * n
+    b_iter = b_spmv + 88 * n
+    return {"B_spmv": b_spmv, "B_iter": b_iter, "iteration_ms": iter_ms,
+            "spmv_ms": spmv_ms, "spmv_time_is": "whole iteration" if persist else "SpMV launch",
+            "frac_spmv": b_spmv / (spmv_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+            "frac_iter": b_iter / (iter_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+
+
 def cpu_baseline(n, kind, iters):
     """Oracle (reference op sequence on torch-CPU) on the same mesh: assembly + `iters` EBE-PCG iterations."""
     from oracle import ref_cpu as R
@@ -256,6 +267,11 @@ def measure(a, kind, coords, tets, dev):
     # schedule), the others 2 (int16) or 4 bytes per entry incl. padding
     alg = A.algorithmic_bytes_spmv(index_total=idx_total if (persist and n_uni) else None)
     achieved = alg / (spmv_ms * 1e-3) / 1e9
+    # SURVEY §8(d)'s byte models beside the stored-format one: B_spmv = 12 nnz + 4 (n+1) + 16 n (scalar CSR, int32
+    # columns) and B_iter = B_spmv + 88 n (11 vector streams of a three-pass Jacobi-PCG iteration), both over the
+    # measured iteration time; the SpMV frac uses the SpMV launch alone where the schedule has one
+    iter_ms = spmv_ms if persist else spmv_ms + ms[1] / max(cnt[1], 1) + ms[2] / max(cnt[2], 1)
+    s8d = s8d_models(A.n, A.g.nnz * A.bs * A.bs, spmv_ms, iter_ms, persist)
     ceiling = system.stream_ceiling(dev)
     workload_key = f"kuhn{a.n}_{kind}"
     out = {
@@ -291,7 +307,8 @@ def measure(a, kind, coords, tets, dev):
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic_from_profiles(workload_key, kernel, alg),
                      "kernel": kernel, "algorithmic_bytes": alg,
                      "per": "iteration (whole PCG iteration in the persistent kernel)" if persist else "SpMV launch",
-                     "stream_ceiling_GBps": ceiling, "frac_of_stream_read": achieved / ceiling["read"]},
+                     "stream_ceiling_GBps": ceiling, "frac_of_stream_read": achieved / ceiling["read"],
+                     "s8d": s8d},
         "cpu_baseline": None,
     }
     return out
