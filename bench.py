@@ -63,6 +63,11 @@ def parse():
     ap.add_argument("--schedule", type=int, default=None, help="PCG kernel schedule (0 three-kernel, 1 fused, 2 deferred, 3 persistent; "
                     "default: persistent for bs=1, three-kernel for bs=3)")
     ap.add_argument("--graph", type=int, default=0, help="capture k iterations per hipGraph (0 = plain launches)")
+    ap.add_argument("--permute", type=int, default=0,
+                    help="seed > 0: randomly renumber the cube's nodes first (a mesh in file order, untimed)")
+    ap.add_argument("--reorder", default="none", choices=["none", "rcm"],
+                    help="rcm: renumber the nodes by device reverse Cuthill-McKee inside every assembly pass "
+                         "(timed with it; reported as reorder_ms)")
     ap.add_argument("--force-dist", action="store_true", help="run the RCCL element-partitioned path even at N=1")
     ap.add_argument("--dist-variant", type=int, default=1,
                     help="N>1: 1 = single-reduction PCG (one all-reduce per iteration), 0 = two reductions")
@@ -167,6 +172,8 @@ def main():
     sync()
 
     coords, tets = mesh.kuhn_cube(a.n, device=dev)
+    if a.permute:
+        coords, tets = permute_nodes(coords, tets, a.permute)
     out = measure(a, a.kind, coords, tets, dev)
     if not a.no_cpu_baseline and rank == 0:
         out["cpu_baseline"] = cpu_baseline(a.n, a.kind, a.cpu_iters)
@@ -188,6 +195,14 @@ def main():
         print(json.dumps(out), flush=True)
 
 
+def permute_nodes(coords, tets, seed):
+    """The cube under a random node numbering (what a mesh file's order looks like to the pattern)."""
+    perm = torch.randperm(coords.shape[0], generator=torch.Generator().manual_seed(seed)).to(coords.device)
+    inv = torch.empty_like(perm)
+    inv[perm] = torch.arange(perm.numel(), device=coords.device)
+    return coords[perm].contiguous(), inv[tets].contiguous()
+
+
 def measure(a, kind, coords, tets, dev):
     """One single-GPU measurement of `kind` on the mesh: DOFs/s (assembly + solve to rtol, two passes) and the
     fixed-iteration CG it/s with its roofline. Returns the bench dict (cpu_baseline None)."""
@@ -205,16 +220,25 @@ def measure(a, kind, coords, tets, dev):
     # dofs_per_s_cold; the --dof-passes passes after it, timed the same way, give the steady-state dofs_per_s (their
     # median; same work every pass: the pattern, the values, the Jacobi weights and the whole solve are recomputed
     # from the mesh)
+    reorder_ms = []
+
     def assemble_and_solve():
         t0 = time.perf_counter()
-        A = system.assemble_tet4_system(coords, tets, kind, E, nu)
+        c, t, ff, fx = coords, tets, f, fixed
+        if a.reorder == "rcm":   # renumbered mesh, load and constraints (u maps back through inv)
+            perm, inv = system.rcm_order(tets, N)
+            c, t = system.renumber(coords, tets, perm, inv)
+            ff, fx = f[perm], inv[fixed]
+            sync()
+            reorder_ms.append((time.perf_counter() - t0) * 1e3)
+        A = system.assemble_tet4_system(c, t, kind, E, nu)
         mask = torch.zeros((N, A.bs), dtype=torch.uint8, device=dev)
-        mask[fixed] = 1
+        mask[fx] = 1
         w = A.jacobi(mask.view(-1))
         sync()
         t_asm = time.perf_counter() - t0
         A.check_singular()
-        b = f.reshape(-1).to(torch.float64).contiguous()
+        b = ff.reshape(-1).to(torch.float64).contiguous()
         tol = a.rtol * float(torch.sqrt(torch.dot(b, w * b)))
         sync()
         t0 = time.perf_counter()
@@ -299,6 +323,9 @@ def measure(a, kind, coords, tets, dev):
         "assembly_ms_cold": t_asm_cold * 1e3,
         "solve_ms_cold": t_solve_cold * 1e3,
         "solve_iters": res.iterations,
+        "mesh_numbering": ("random (seed %d)" % a.permute if a.permute else "lexicographic")
+        + (", device RCM renumbering in every assembly pass" if a.reorder == "rcm" else ""),
+        "reorder_ms": (sorted(reorder_ms)[len(reorder_ms) // 2] if reorder_ms else None),
         "solve_status": res.status,
         "kernel_ms": ({"persist_iteration": spmv_ms, "iterations_per_launch": a.steps} if persist else
                       {"spmv_dot": spmv_ms, "update": ms[1] / max(cnt[1], 1), "pupdate": ms[2] / max(cnt[2], 1),

@@ -43,6 +43,9 @@ SIGNATURES = {
     "fem_scan_work_len": (_L, [_L]),
     "fem_incidence_work_bytes": (_L, [_L, _L]),
     "fem_incidence": (_I, [_P, _L, _I, _L, _P, _P, _P, _P]),
+    "fem_incidence_checked": (_I, [_P, _L, _I, _L, _P, _P, _P, _P, _P]),
+    "fem_rcm_work_len": (_L, [_L]),
+    "fem_rcm": (_I, [_P, _P, _L, _P, _P, _P, _P, _P]),
     "fem_graph_count": (_I, [_P, _I, _P, _P, _L, _P, _P, _P]),
     "fem_graph_fill": (_I, [_P, _I, _P, _P, _L, _P, _P, _P, _P]),
     "fem_graph_tmp_len": (_L, [_L]),
@@ -55,6 +58,7 @@ SIGNATURES = {
     "fem_assemble_from_ke": (_I, [_P, _P, _I, _I, _P, _P, _L, _P, _P, _P, _P, _P, _P]),
     "fem_assemble_from_ke_ex": (_I, [_P, _P, _I, _I, _P, _P, _L, _P, _P, _P, _P, _L, _L, _I, _P, _P]),
     "fem_assemble_tet4": (_I, [_P, _P, _D, _D, _I, _P, _P, _L, _P, _P, _P, _P, _P, _P, _P]),
+    "fem_assemble_tet4_ex": (_I, [_P, _P, _D, _D, _I, _P, _P, _L, _P, _P, _P, _P, _I, _P, _P, _P]),
     "fem_sell_to_csr_vals": (_I, [_P, _I, _P, _L, _P, _P, _P, _P]),
     "fem_jacobi": (_I, [_P, _I, _P, _P, _P, _P, _L, _P, _P, _P]),
     "fem_ebe_apply": (_I, [_P, _P, _I, _I, _P, _P, _L, _P, _P, _P]),

@@ -665,142 +665,381 @@ __global__ void __launch_bounds__(256) k_csr_add_sell(const double* __restrict__
 }
 
 // ---------------------------------------------------------------- fused c3d4 assembly (K_e never stored)
-template <int BS>
-__global__ void __launch_bounds__(256) k_assemble_tet4(const double* __restrict__ X, const int64_t* __restrict__ conn,
+// Two forms, both straight into SELL (addresses from the slice pointer, no csr2sell reads; a fresh matrix is stored
+// whole, padding zeroed, without a memset), both with the additions and order of the wave-per-row kernels below
+// (k_assemble_p1w / k_assemble_el3w, FEM355_ASM_ROWS; bit for bit, tests/test_gpu_parity.py): the accumulator form
+// (k_asm_tet4_acc) for bs = 1 and the owner form (k_asm_tet4_tile) for bs = 3.
+//
+// Owner form: one 256-thread workgroup per R consecutive rows of one SELL slice. Per batch of 256 of the
+// tile's incidences (one per thread, the tile's incidence range is contiguous): element gradients and volume, and
+// the row's column slots of the element's 4 nodes (binary search in the tile's CSR segment, staged in LDS), all
+// staged in LDS. Then every output -- (row, column) entry, bs x bs block -- is owned by one thread, which adds its
+// contributions over the row's incidences in ascending order onto zero (STORE, fresh matrix; SELL padding written
+// as zeros) or onto the stored value: the additions, their order and the value formulas of k_assemble_p1w /
+// k_assemble_el3w, and one wave's stores of a block plane cover 64 consecutive owners = whole 128-byte lines.
+constexpr int AT_TB = 256;       // incidences per batch (one per thread)
+constexpr int AT_SEGCAP = 1024;  // CSR entries of a tile staged in LDS (larger tiles search colidx in memory)
+
+// a + b never fused with the product that formed b (the row kernels store the product to LDS before adding it)
+__device__ __forceinline__ double add_nc(double a, double b) {
+#pragma clang fp contract(off)
+    return a + b;
+}
+
+// entry (rr, kk) of the elastic block (a, b) of a c3d4 element, V (lambda g_a g_b^T + mu g_b g_a^T + mu (g_a . g_b)
+// I), evaluated without contractions so the two assembly forms that evaluate it in different code agree bit for bit
+__device__ __forceinline__ double el_dot(const double* ga, const double* gb) {
+#pragma clang fp contract(off)
+    return ga[0] * gb[0] + ga[1] * gb[1] + ga[2] * gb[2];
+}
+__device__ __forceinline__ double el_value(const Lame& L, const double* ga, const double* gb, int rr, int kk,
+                                           double dot, double V) {
+#pragma clang fp contract(off)
+    double s = L.lam * ga[rr] * gb[kk] + L.mu * ga[kk] * gb[rr];
+    if (rr == kk) s += L.mu * dot;
+    return s * V;
+}
+
+__device__ __forceinline__ double p1_value(const double ga[3], const double gb[3], double kappa, double V) {
+    const double dot = ga[0] * gb[0] + ga[1] * gb[1] + ga[2] * gb[2];
+    return kappa * dot * V;
+}
+
+// zero the SELL values of slices [0, ns) (slice_ptr on the device)
+__global__ void k_sell_zero(const int64_t* __restrict__ slice_ptr, int64_t ns, int bs2, double* __restrict__ vals) {
+    const int64_t n = slice_ptr[ns] * bs2;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        vals[i] = 0.0;
+}
+
+template <int BS, int R, int OPT, bool STORE>
+__global__ void __launch_bounds__(256) k_asm_tet4_tile(const double* __restrict__ X, const int64_t* __restrict__ conn,
                                                        double E, double nu, const int32_t* __restrict__ inc_ptr,
                                                        const int32_t* __restrict__ inc, int64_t N,
                                                        const int32_t* __restrict__ rowptr,
                                                        const int32_t* __restrict__ colidx,
-                                                       const int64_t* __restrict__ csr2sell, double* __restrict__ vals,
-                                                       int64_t* __restrict__ bad) {
+                                                       const int64_t* __restrict__ slice_ptr,
+                                                       double* __restrict__ vals, int64_t* __restrict__ bad,
+                                                       int64_t ntiles) {
+    static_assert(64 % R == 0, "a tile lies inside one slice");
+    constexpr int B2 = BS * BS;
+    constexpr int ND = BS == 1 ? 4 : 13;   // per incidence: bs = 1 the 4 values of the element row; bs = 3 g, V
+    __shared__ int ip_s[R + 1];
+    __shared__ int rp_s[R + 1];
+    __shared__ int col_s[AT_SEGCAP];
+    __shared__ uint2 pos_s[AT_TB];         // the 4 nodes' column slots in the row, 16 bits each (0xffff: none)
+    __shared__ double dat_s[ND][AT_TB];   // structure of arrays: conflict-free stores by the incidence threads
+    __shared__ int8_t a_s[AT_TB];
+    const int tid = threadIdx.x;
+    const int64_t per = (ntiles + NXCD - 1) / NXCD;   // XCD-contiguous tile ranges (shared gathers stay in one L2)
+    const int64_t tile = (int64_t)(blockIdx.x % NXCD) * per + blockIdx.x / NXCD;
+    if (tile >= ntiles) return;
+    const int64_t r0 = tile * R;
+    const int64_t s = r0 >> 6;
+    const int l0 = (int)(r0 & 63);
+    const int64_t e0 = slice_ptr[s];
+    const int W = (int)((slice_ptr[s + 1] - e0) >> 6);
+    if (tid <= R) {
+        const int64_t r = r0 + tid < N ? r0 + tid : N;
+        ip_s[tid] = inc_ptr[r];
+        rp_s[tid] = rowptr[r];
+    }
+    __syncthreads();
+    const int seg0 = rp_s[0], segn = rp_s[R] - seg0;
+    const bool staged = segn <= AT_SEGCAP;
+    if (staged)
+        for (int q = tid; q < segn; q += 256) col_s[q] = colidx[seg0 + q];
+    const int T0 = ip_s[0], T1 = ip_s[R];
     const Lame L = lame(E, nu);
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
-        const int lo = rowptr[i], hi = rowptr[i + 1];
-        for (int t = inc_ptr[i]; t < inc_ptr[i + 1]; ++t) {
-            const int ea = inc[t];
-            const int64_t e = ea >> 2;
-            const int a = ea & 3;
-            const int64_t* c = conn + 4 * e;
-            double g[4][3];
-            const double det = tet4_grads(X, c, g);
-            if (fabs(det) < 1e-12) atomicMin((unsigned long long*)bad, (unsigned long long)e);
-            const double V = fabs(det) / 6.0;
-            for (int b = 0; b < 4; ++b) {
-                const int j = (int)c[b];
-                const int p = find_col(colidx, lo, hi, j);
-                const int64_t Ei = csr2sell[p];
-                const double dot = g[a][0] * g[b][0] + g[a][1] * g[b][1] + g[a][2] * g[b][2];
-                if (BS == 1) {
-                    vals[Ei] += E * dot * V;
-                } else {
+    const int nout = R * W;
+    for (int o0 = 0; o0 < nout; o0 += 256 * OPT) {
+        double acc[OPT][B2];
 #pragma unroll
-                    for (int r = 0; r < 3; ++r)
+        for (int q = 0; q < OPT; ++q) {
+            const int o = o0 + q * 256 + tid, r = o % R, k = o / R;
 #pragma unroll
-                        for (int k = 0; k < 3; ++k) {
-                            double s = L.lam * g[a][r] * g[b][k] + L.mu * g[a][k] * g[b][r];
-                            if (r == k) s += L.mu * dot;
-                            vals[sell_val(Ei, 9, r * 3 + k)] += s * V;
-                        }
+            for (int c = 0; c < B2; ++c) acc[q][c] = 0.0;
+            if (!STORE && o < nout && k < rp_s[r + 1] - rp_s[r]) {
+                const int64_t Ei = e0 + (int64_t)k * 64 + l0 + r;
+#pragma unroll
+                for (int c = 0; c < B2; ++c) acc[q][c] = vals[BS == 1 ? Ei : sell_val(Ei, B2, c)];
+            }
+        }
+        for (int b0 = T0; b0 < T1; b0 += AT_TB) {
+            __syncthreads();   // col_s staged / previous batch consumed
+            const int t = b0 + tid;
+            if (t < T1) {
+                int lo = 0, hi = R;   // row of incidence t: last r with ip_s[r] <= t
+                while (hi - lo > 1) {
+                    const int m = (lo + hi) >> 1;
+                    if (ip_s[m] <= t) lo = m;
+                    else hi = m;
+                }
+                const int r = lo;
+                const int ea = inc[t];
+                const int64_t e = ea >> 2;
+                const int a = ea & 3;
+                const int64_t* c = conn + 4 * e;
+                double g[4][3];
+                const double det = tet4_grads(X, c, g);
+                if (o0 == 0 && fabs(det) < 1e-12) atomicMin((unsigned long long*)bad, (unsigned long long)e);
+                const double V = fabs(det) / 6.0;
+                const int cl = rp_s[r] - seg0, cn = rp_s[r + 1] - rp_s[r];
+                const int32_t* cs = staged ? col_s + cl : colidx + seg0 + cl;
+                uint32_t pk[2] = {0u, 0u};
+#pragma unroll
+                for (int bb = 0; bb < 4; ++bb) {
+                    const int j = (int)c[bb];
+                    int l = 0, h = cn;
+                    while (l < h) {
+                        const int m = (l + h) >> 1;
+                        if (cs[m] < j) l = m + 1;
+                        else h = m;
+                    }
+                    const uint32_t p = (l < cn && cs[l] == j) ? (uint32_t)l : 0xffffu;
+                    pk[bb >> 1] |= p << (16 * (bb & 1));
+                    if constexpr (BS == 1) dat_s[bb][tid] = p1_value(g[a], g[bb], E, V);
+                }
+                pos_s[tid] = make_uint2(pk[0], pk[1]);
+                if constexpr (BS == 3) {
+#pragma unroll
+                    for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+                        for (int q = 0; q < 3; ++q) dat_s[3 * bb + q][tid] = g[bb][q];
+                    dat_s[12][tid] = V;
+                    a_s[tid] = (int8_t)a;
                 }
             }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < OPT; ++q) {
+                const int o = o0 + q * 256 + tid, r = o % R, k = o / R;
+                if (o >= nout || k >= rp_s[r + 1] - rp_s[r]) continue;
+                const int j0 = max(ip_s[r], b0) - b0, j1 = min(ip_s[r + 1], b0 + AT_TB) - b0;
+                for (int jj = j0; jj < j1; ++jj) {
+                    const uint2 pp = pos_s[jj];
+#pragma unroll
+                    for (int bb = 0; bb < 4; ++bb) {
+                        const uint32_t p = ((bb < 2 ? pp.x : pp.y) >> (16 * (bb & 1))) & 0xffffu;
+                        if (p != (uint32_t)k) continue;
+                        if constexpr (BS == 1) {
+                            acc[q][0] += dat_s[bb][jj];
+                        } else {
+                            const int aa = a_s[jj];
+                            const double ga[3] = {dat_s[3 * aa][jj], dat_s[3 * aa + 1][jj], dat_s[3 * aa + 2][jj]};
+                            const double gb[3] = {dat_s[3 * bb][jj], dat_s[3 * bb + 1][jj], dat_s[3 * bb + 2][jj]};
+                            const double V = dat_s[12][jj];
+                            const double dot = el_dot(ga, gb);
+#pragma unroll
+                            for (int rr = 0; rr < 3; ++rr)
+#pragma unroll
+                                for (int kk = 0; kk < 3; ++kk)
+                                    acc[q][rr * 3 + kk] =
+                                        add_nc(acc[q][rr * 3 + kk], el_value(L, ga, gb, rr, kk, dot, V));
+                        }
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < OPT; ++q) {
+            const int o = o0 + q * 256 + tid, r = o % R, k = o / R;
+            if (o >= nout) continue;
+            if (!STORE && k >= rp_s[r + 1] - rp_s[r]) continue;   // adding: padding stays as stored
+            const int64_t Ei = e0 + (int64_t)k * 64 + l0 + r;
+#pragma unroll
+            for (int c = 0; c < B2; ++c) vals[BS == 1 ? Ei : sell_val(Ei, B2, c)] = acc[q][c];
         }
     }
 }
 
-// Wave per row, lanes = the row's incident elements (chunks of 64): every lane forms its element's gradients and
-// volume once and locates the element's 4 nodes in the row's column list (held in LDS); then each lane owns one
-// (column, block-row) output and sums the contributions of all incident elements in ascending incidence order,
-// starting from the stored value — the same additions in the same order as the thread-per-row kernel above, so
-// the result is bit-identical, with the row's loads issued by up to 64 lanes at once instead of one thread.
+// Accumulator form (default): one workgroup per R rows of a slice, the rows' block values accumulated in LDS.
+// Items = (row, j-th incident element of the row); per batch the j0..j0+J-1 items of every row are formed by one
+// thread each (gradients, volume, the column slots of the element's nodes in the row) and staged in LDS; then
+// every row is swept by its own lanes in lockstep -- lane (row, b[, rr]) takes the row's items in ascending order
+// and adds element node b's contribution (block row rr) into the accumulator of b's column: within one step the
+// row's lanes hit distinct columns (an element lists a node once; elements that do not are swept node by node), so
+// every accumulator receives its contributions in ascending incidence order -- the sums of k_assemble_p1w /
+// k_assemble_el3w bit for bit, without their owner loops (whose lanes stepped through every item to find their
+// few matches). The rows' accumulators are written out whole slice columns at a time (coalesced SELL stores).
+// Columns past ACC_W per row: the accumulators cover the row's columns in windows of ACC_W, one sweep per window.
+template <int R_, int J_, int LPR_, int W_, int SEG_>
+struct AccCfg {
+    static constexpr int R = R_, J = J_, LPR = LPR_, W = W_, SEG = SEG_;
+};
+// bs = 1: lanes (row, b), 64 rows (a slice), 4 items per row per batch, 32 accumulated columns per row (10M cube:
+// 0.86 ms; 16 columns 0.79 ms but two sweeps for rows past 16 columns, 8 items per row 1.16 ms at 3 waves per SIMD).
+// bs = 3 runs the owner form (k_asm_tet4_tile): the accumulator form with lanes (row, b, rr) measured 5.7-6.2 ms
+// against 3.85 ms there (16-row tiles, 3-4 workgroups per CU: each batch's dependent element loads are exposed).
+using AccP1 = AccCfg<64, 4, 4, 32, 1024>;
 
-template <int BS>
-__global__ void __launch_bounds__(256) k_assemble_tet4w(const double* __restrict__ X, const int64_t* __restrict__ conn,
-                                                        double E, double nu, const int32_t* __restrict__ inc_ptr,
-                                                        const int32_t* __restrict__ inc, int64_t N,
-                                                        const int32_t* __restrict__ rowptr,
-                                                        const int32_t* __restrict__ colidx,
-                                                        const int64_t* __restrict__ csr2sell, double* __restrict__ vals,
-                                                        int64_t* __restrict__ bad) {
-    __shared__ double g_s[AW_WAVES][64][4][3];
-    __shared__ double v_s[AW_WAVES][64];
-    __shared__ int8_t a_s[AW_WAVES][64];
-    __shared__ int8_t pos_s[AW_WAVES][64][4];   // column slot of node b in the current column group, -1 if outside
-    __shared__ int col_s[AW_WAVES][64];
-    constexpr int JG = 64 / BS;                 // columns per pass (one lane per column and block row)
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+template <int BS, class Cfg, bool STORE>
+__global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__ X, const int64_t* __restrict__ conn,
+                                                      double E, double nu, const int32_t* __restrict__ inc_ptr,
+                                                      const int32_t* __restrict__ inc, int64_t N,
+                                                      const int32_t* __restrict__ rowptr,
+                                                      const int32_t* __restrict__ colidx,
+                                                      const int64_t* __restrict__ slice_ptr,
+                                                      double* __restrict__ vals, int64_t* __restrict__ bad,
+                                                      int64_t ntiles) {
+    constexpr int R = Cfg::R, J = Cfg::J, LPR = Cfg::LPR, AW = Cfg::W, SEG = Cfg::SEG;
+    constexpr int B2 = BS * BS;
+    constexpr int NI = R * J;
+    constexpr int ND = BS == 1 ? 4 : 13;
+    static_assert(64 % R == 0 && NI % 256 == 0 || NI < 256, "items per batch");
+    static_assert(64 % R == 0 && R * LPR == 256 && 64 % LPR == 0, "tile geometry");
+    __shared__ int ip_s[R + 1];
+    __shared__ int rp_s[R + 1];
+    __shared__ int col_s[SEG];
+    __shared__ double dat_s[ND][NI];
+    __shared__ uint2 pos_s[NI];
+    __shared__ uint8_t a_s[NI];             // local index of the row's node; bit 7: the element repeats a node
+    __shared__ double acc_s[AW * B2][R];
+    __shared__ int maxc_s;
+    const int tid = threadIdx.x;
+    const int64_t per = (ntiles + NXCD - 1) / NXCD;
+    const int64_t tile = (int64_t)(blockIdx.x % NXCD) * per + blockIdx.x / NXCD;
+    if (tile >= ntiles) return;
+    const int64_t r0 = tile * R;
+    const int l0 = (int)(r0 & 63);
+    const int64_t e0 = slice_ptr[r0 >> 6];
+    const int W = (int)((slice_ptr[(r0 >> 6) + 1] - e0) >> 6);
+    if (tid == 0) maxc_s = 0;
+    __syncthreads();
+    if (tid <= R) {
+        const int64_t r = r0 + tid < N ? r0 + tid : N;
+        ip_s[tid] = inc_ptr[r];
+        rp_s[tid] = rowptr[r];
+        if (tid < R) {
+            const int64_t r1 = r0 + tid + 1 < N ? r0 + tid + 1 : N;
+            atomicMax(&maxc_s, inc_ptr[r1] - ip_s[tid]);
+        }
+    }
+    __syncthreads();
+    const int seg0 = rp_s[0], segn = rp_s[R] - seg0;
+    const bool staged = segn <= SEG;
+    if (staged)
+        for (int q = tid; q < segn; q += 256) col_s[q] = colidx[seg0 + q];
+    const int maxc = maxc_s;
     const Lame L = lame(E, nu);
-    const int64_t nwaves = (int64_t)gridDim.x * AW_WAVES;
-    for (int64_t i = (int64_t)blockIdx.x * AW_WAVES + wid; i < N; i += nwaves) {
-        const int lo = rowptr[i], len = rowptr[i + 1] - lo;
-        const int t0 = inc_ptr[i], C = inc_ptr[i + 1] - t0;
-        for (int j0 = 0; j0 < len; j0 += JG) {
-            const int nj = min(JG, len - j0);
-            if (lane < nj) col_s[wid][lane] = colidx[lo + j0 + lane];
-            // output owned by this lane: column j0 + jl, block row r
-            const int jl = lane / BS, r = lane - BS * (lane / BS);
-            const bool owner = lane < nj * BS;
-            double acc[BS];
-            int64_t Ei = 0;
-            if (owner) {
-                Ei = csr2sell[lo + j0 + jl];
+    // phase-2 lane: row lr, element node lb, block row lrr
+    const int lr = tid / LPR, lb = (tid % LPR) / (BS == 1 ? 1 : 4), lrr = BS == 1 ? 0 : tid % 4;
+    const bool lactive = BS == 1 || lrr < 3;
+    for (int c0 = 0; c0 < W; c0 += AW) {
+        const int cw = min(AW, W - c0);
+        __syncthreads();
+        for (int q = tid; q < AW * B2 * R; q += 256) {
+            const int r = q % R, kc = q / R, k = kc / B2, c = kc - k * B2;
+            double v = 0.0;
+            if (!STORE && k < cw && c0 + k < rp_s[r + 1] - rp_s[r])
+                v = vals[BS == 1 ? e0 + (int64_t)(c0 + k) * 64 + l0 + r
+                                 : sell_val(e0 + (int64_t)(c0 + k) * 64 + l0 + r, B2, c)];
+            acc_s[kc][r] = v;
+        }
+        for (int j0 = 0; j0 < maxc; j0 += J) {
+            __syncthreads();   // accumulators initialised / previous batch swept
 #pragma unroll
-                for (int c = 0; c < BS; ++c) acc[c] = vals[BS == 1 ? Ei : sell_val(Ei, BS * BS, r * BS + c)];
-            }
-            for (int k0 = 0; k0 < C; k0 += 64) {
-                const int nk = min(64, C - k0);
-                __builtin_amdgcn_wave_barrier();
-                if (lane < nk) {
-                    const int ea = inc[t0 + k0 + lane];
+            for (int i0 = 0; i0 < NI; i0 += 256) {
+                const int it0 = i0 + tid;
+                if (it0 >= NI) break;
+                const int r = it0 / J, jj = it0 - r * J;
+                const int t = ip_s[r] + j0 + jj;
+                uint32_t pk[2] = {0xffffffffu, 0xffffffffu};
+                uint8_t aflag = 0;
+                if (t < ip_s[r + 1]) {
+                    const int ea = inc[t];
                     const int64_t e = ea >> 2;
+                    const int a = ea & 3;
                     const int64_t* c = conn + 4 * e;
                     double g[4][3];
                     const double det = tet4_grads(X, c, g);
-                    if (j0 == 0 && fabs(det) < 1e-12) atomicMin((unsigned long long*)bad, (unsigned long long)e);
-                    v_s[wid][lane] = fabs(det) / 6.0;
-                    a_s[wid][lane] = (int8_t)(ea & 3);
+                    if (c0 == 0 && fabs(det) < 1e-12) atomicMin((unsigned long long*)bad, (unsigned long long)e);
+                    const double V = fabs(det) / 6.0;
+                    const int cl = rp_s[r] - seg0, cn = rp_s[r + 1] - rp_s[r];
+                    const int32_t* cs = staged ? col_s + cl : colidx + seg0 + cl;
+                    int nodes[4];
+                    pk[0] = pk[1] = 0u;
 #pragma unroll
-                    for (int b = 0; b < 4; ++b) {
+                    for (int bb = 0; bb < 4; ++bb) {
+                        const int j = (int)c[bb];
+                        nodes[bb] = j;
+                        int l = 0, h = cn;
+                        while (l < h) {
+                            const int m = (l + h) >> 1;
+                            if (cs[m] < j) l = m + 1;
+                            else h = m;
+                        }
+                        const uint32_t p = (l < cn && cs[l] == j) ? (uint32_t)l : 0xffffu;
+                        pk[bb >> 1] |= p << (16 * (bb & 1));
+                        if constexpr (BS == 1) dat_s[bb][it0] = p1_value(g[a], g[bb], E, V);
+                    }
+                    const bool rep = nodes[0] == nodes[1] || nodes[0] == nodes[2] || nodes[0] == nodes[3] ||
+                                     nodes[1] == nodes[2] || nodes[1] == nodes[3] || nodes[2] == nodes[3];
+                    aflag = (uint8_t)(a | (rep ? 0x80 : 0));
+                    if constexpr (BS == 3) {
 #pragma unroll
-                        for (int q = 0; q < 3; ++q) g_s[wid][lane][b][q] = g[b][q];
-                        const int j = (int)c[b];
-                        int p = -1;
-                        for (int u = 0; u < nj; ++u)
-                            if (col_s[wid][u] == j) p = u;
-                        pos_s[wid][lane][b] = (int8_t)p;
+                        for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+                            for (int q = 0; q < 3; ++q) dat_s[3 * bb + q][it0] = g[bb][q];
+                        dat_s[12][it0] = V;
                     }
                 }
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                if (owner) {
-                    for (int k = 0; k < nk; ++k) {
-                        const int a = a_s[wid][k];
-                        const double V = v_s[wid][k];
-                        const double* ga = g_s[wid][k][a];
+                pos_s[it0] = make_uint2(pk[0], pk[1]);
+                a_s[it0] = aflag;
+            }
+            __syncthreads();
+            // sweep: lanes of one row are consecutive lanes of one wave, in lockstep
+            for (int jj = 0; jj < J; ++jj) {
+                const int it = lr * J + jj;
+                const uint2 pp = pos_s[it];
+                const uint32_t praw = ((lb < 2 ? pp.x : pp.y) >> (16 * (lb & 1))) & 0xffffu;
+                const int k = (int)praw - c0;
+                const bool hit = lactive && praw != 0xffffu && k >= 0 && k < cw;
+                const uint8_t af = a_s[it];
+                double v[BS];
+                if (hit) {
+                    if constexpr (BS == 1) {
+                        v[0] = dat_s[lb][it];
+                    } else {
+                        const int aa = af & 3;
+                        const double ga[3] = {dat_s[3 * aa][it], dat_s[3 * aa + 1][it], dat_s[3 * aa + 2][it]};
+                        const double gb[3] = {dat_s[3 * lb][it], dat_s[3 * lb + 1][it], dat_s[3 * lb + 2][it]};
+                        const double V = dat_s[12][it];
+                        const double dot = el_dot(ga, gb);
 #pragma unroll
-                        for (int b = 0; b < 4; ++b) {
-                            if (pos_s[wid][k][b] != jl) continue;
-                            const double* gb = g_s[wid][k][b];
-                            const double dot = ga[0] * gb[0] + ga[1] * gb[1] + ga[2] * gb[2];
-                            if (BS == 1) {
-                                acc[0] += E * dot * V;
-                            } else {
+                        for (int cc = 0; cc < 3; ++cc) v[cc] = el_value(L, ga, gb, lrr, cc, dot, V);
+                    }
+                }
+                const bool any_rep = __ballot(hit && (af & 0x80)) != 0;
+                if (!any_rep) {
+                    if (hit) {
 #pragma unroll
-                                for (int kk = 0; kk < BS; ++kk) {
-                                    double s = L.lam * ga[r] * gb[kk] + L.mu * ga[kk] * gb[r];
-                                    if (r == kk) s += L.mu * dot;
-                                    acc[kk] += s * V;
-                                }
-                            }
+                        for (int cc = 0; cc < BS; ++cc) {
+                            double* ap = &acc_s[k * B2 + lrr * BS + cc][lr];
+                            *ap = add_nc(*ap, v[cc]);
                         }
                     }
-                }
-                __builtin_amdgcn_wave_barrier();
-            }
-            if (owner) {
+                } else {   // an element repeating a node: its nodes' contributions one after the other (b order)
+                    for (int b = 0; b < 4; ++b) {
+                        if (hit && lb == b) {
 #pragma unroll
-                for (int c = 0; c < BS; ++c) vals[BS == 1 ? Ei : sell_val(Ei, BS * BS, r * BS + c)] = acc[c];
+                            for (int cc = 0; cc < BS; ++cc) {
+                                double* ap = &acc_s[k * B2 + lrr * BS + cc][lr];
+                                *ap = add_nc(*ap, v[cc]);
+                            }
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    }
+                }
             }
-            __builtin_amdgcn_wave_barrier();
+        }
+        __syncthreads();
+        for (int q = tid; q < cw * B2 * R; q += 256) {
+            const int r = q % R, kc = q / R, k = kc / B2, c = kc - k * B2;
+            if (!STORE && c0 + k >= rp_s[r + 1] - rp_s[r]) continue;   // adding: padding stays as stored
+            const int64_t Ei = e0 + (int64_t)(c0 + k) * 64 + l0 + r;
+            vals[BS == 1 ? Ei : sell_val(Ei, B2, c)] = acc_s[kc][r];
         }
     }
 }
@@ -933,15 +1172,12 @@ __global__ void __launch_bounds__(256) k_assemble_el3w(const double* __restrict_
                     uint32_t packed = 0;
 #pragma unroll
                     for (int b = 0; b < 4; ++b) {
-                        const double dot = g[a][0] * g[b][0] + g[a][1] * g[b][1] + g[a][2] * g[b][2];
+                        const double dot = el_dot(g[a], g[b]);
 #pragma unroll
                         for (int rr = 0; rr < 3; ++rr)
 #pragma unroll
-                            for (int kk = 0; kk < 3; ++kk) {
-                                double s = L.lam * g[a][rr] * g[b][kk] + L.mu * g[a][kk] * g[b][rr];
-                                if (rr == kk) s += L.mu * dot;
-                                blk_s[wid][lane][b][rr * 3 + kk] = s * V;
-                            }
+                            for (int kk = 0; kk < 3; ++kk)
+                                blk_s[wid][lane][b][rr * 3 + kk] = el_value(L, g[a], g[b], rr, kk, dot, V);
                         const int j = (int)c[b];
                         int l = 0, h = nj;
                         while (l < h) {
@@ -1263,24 +1499,63 @@ int fem_assemble_from_ke_ex(const double* Ke, const int64_t* conn, int npe, int 
     return FEM_OK;
 }
 
+int fem_assemble_tet4_ex(const double* coords, const int64_t* conn, double E, double nu, int bs,
+                         const int32_t* inc_ptr, const int32_t* inc, int64_t N, const int32_t* rowptr,
+                         const int32_t* colidx, const int64_t* csr2sell, const int64_t* slice_ptr, int store,
+                         double* vals, int64_t* bad_idx, fem_stream_t stream) {
+    if (bs != 1 && bs != 3) {
+        set_error("fem_assemble_tet4: block size %d unsupported", bs);
+        return FEM_EARG;
+    }
+    if (N <= 0) return FEM_OK;
+    hipStream_t st = S(stream);
+    if (getenv("FEM355_ASM_ROWS") != nullptr) {
+        // wave per row (k_assemble_p1w / k_assemble_el3w, CSR-addressed through csr2sell; the tile kernel's bits):
+        // kept as the reference formulation of the tile kernel's summation order
+        if (store) {
+            hipLaunchKernelGGL(k_sell_zero, dim3(2048), dim3(256), 0, st, slice_ptr, cdiv(N, 64), bs * bs, vals);
+            FEM_LAUNCHED();
+        }
+        const dim3 g((unsigned)grid_multiple_of_xcd(cdiv(N, AW_WAVES), 8192));
+        if (bs == 1)
+            hipLaunchKernelGGL(k_assemble_p1w<FEM_P1_LPR>, g, dim3(256), 0, st, coords, conn, E, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals, bad_idx);
+        else
+            hipLaunchKernelGGL(k_assemble_el3w, g, dim3(256), 0, st, coords, conn, E, nu, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals, bad_idx);
+        FEM_LAUNCHED();
+        return FEM_OK;
+    }
+    if (bs == 1) {
+#define AA_LAUNCH(BS_, CFG_, ST_)                                                                                   \
+    do {                                                                                                            \
+        const int64_t nt = cdiv(N, 64) * (64 / CFG_::R);                                                            \
+        hipLaunchKernelGGL((k_asm_tet4_acc<BS_, CFG_, ST_>), dim3((unsigned)(cdiv(nt, NXCD) * NXCD)), dim3(256), 0,  \
+                           st, coords, conn, E, nu, inc_ptr, inc, N, rowptr, colidx, slice_ptr, vals, bad_idx, nt); \
+    } while (0)
+        if (store) AA_LAUNCH(1, AccP1, true);
+        else AA_LAUNCH(1, AccP1, false);
+#undef AA_LAUNCH
+        FEM_LAUNCHED();
+        return FEM_OK;
+    }
+    constexpr int R = 32;
+    const int64_t ntiles = cdiv(N, 64) * (64 / R);   // every lane of the last slice (padding rows: zeros)
+    const dim3 g((unsigned)(cdiv(ntiles, NXCD) * NXCD));
+#define AT_LAUNCH(BS_, OPT_, ST_)                                                                                   \
+    hipLaunchKernelGGL((k_asm_tet4_tile<BS_, R, OPT_, ST_>), g, dim3(256), 0, st, coords, conn, E, nu, inc_ptr, inc, N, \
+                       rowptr, colidx, slice_ptr, vals, bad_idx, ntiles)
+    if (store) AT_LAUNCH(3, 3, true);
+    else AT_LAUNCH(3, 3, false);
+#undef AT_LAUNCH
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
 int fem_assemble_tet4(const double* coords, const int64_t* conn, double E, double nu, int bs, const int32_t* inc_ptr,
                       const int32_t* inc, int64_t N, const int32_t* rowptr, const int32_t* colidx,
                       const int64_t* csr2sell, const int64_t* slice_ptr, double* vals, int64_t* bad_idx,
                       fem_stream_t stream) {
-    // wave per row (k_assemble_p1w / k_assemble_el3w); the thread-per-row k_assemble_tet4 and the first wave
-    // version k_assemble_tet4w stay as reference formulations
-    const dim3 g((unsigned)grid_multiple_of_xcd(cdiv(N, AW_WAVES), 8192));
-    if (bs == 1)
-        hipLaunchKernelGGL(k_assemble_p1w<FEM_P1_LPR>, g, dim3(256), 0, S(stream), coords, conn, E, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals, bad_idx);
-    else if (bs == 3)   // in place: the block-CSR staging of fem_assemble_from_ke measured slower here (6.7 vs 6.1
-                        // ms on 10M tets: this kernel is bound by forming the element blocks, not by its writes)
-        hipLaunchKernelGGL(k_assemble_el3w, g, dim3(256), 0, S(stream), coords, conn, E, nu, inc_ptr, inc, N, rowptr, colidx, csr2sell, vals, bad_idx);
-    else {
-        set_error("fem_assemble_tet4: block size %d unsupported", bs);
-        return FEM_EARG;
-    }
-    FEM_LAUNCHED();
-    return FEM_OK;
+    return fem_assemble_tet4_ex(coords, conn, E, nu, bs, inc_ptr, inc, N, rowptr, colidx, csr2sell, slice_ptr, 0,
+                                vals, bad_idx, stream);
 }
 
 int fem_sell_to_csr_vals(const double* vals, int bs, const int32_t* rowptr, int64_t nrows, const int64_t* csr2sell,

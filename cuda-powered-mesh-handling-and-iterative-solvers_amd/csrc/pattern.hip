@@ -13,16 +13,24 @@
 namespace fem {
 
 // ---------------------------------------------------------------- incidence
-// sort keys of the incidence: node id of every (element, local) slot, payload = slot
-__global__ void k_inc_keys(const int64_t* __restrict__ conn, int64_t total, int32_t* __restrict__ key,
-                           int32_t* __restrict__ slot) {
+// Stable radix sort of (node, slot) pairs, slot = e * npe + local: every node's slots come out ascending. An
+// out-of-range node id raises *bad and is keyed N (sorted past every node, outside every inc_ptr range). Measured
+// against a counting sort (atomic counts, scan, atomic scatter, per-node segment sort): 2.1 ms vs 1.2 ms on the 10M
+// cube -- 40M scattered device atomics twice (count + scatter) cost more than the three sort passes.
+__global__ void k_inc_keys(const int64_t* __restrict__ conn, int64_t total, int64_t N, int32_t* __restrict__ key,
+                           int32_t* __restrict__ slot, int32_t* __restrict__ bad) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        key[i] = (int32_t)conn[i];
+        int64_t v = conn[i];
+        if (v < 0 || v >= N) {
+            if (bad) *bad = 1;
+            v = N;
+        }
+        key[i] = (int32_t)v;
         slot[i] = (int32_t)i;
     }
 }
 
-// inc_ptr[n] = first sorted position whose node is >= n (run boundaries of the sorted keys)
+// inc_ptr[n] = first sorted position whose node is >= n (run boundaries of the sorted keys; keys N = bad slots)
 __global__ void k_inc_ptr(const int32_t* __restrict__ key, int64_t total, int64_t N, int32_t* __restrict__ inc_ptr) {
     for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p <= total; p += (int64_t)gridDim.x * blockDim.x) {
         const int64_t prev = p == 0 ? -1 : key[p - 1];
@@ -367,9 +375,9 @@ static size_t inc_sort_temp_bytes(int64_t total, int bits) {
     return tb;
 }
 
-static int node_bits(int64_t N) {
+static int node_bits(int64_t N) {   // bits of the keys 0..N (N = an out-of-range slot)
     int bits = 1;
-    while (((int64_t)1 << bits) < N) ++bits;
+    while (((int64_t)1 << bits) <= N) ++bits;
     return bits;
 }
 
@@ -378,20 +386,20 @@ int64_t fem_incidence_work_bytes(int64_t total, int64_t N) {
     return (int64_t)(3 * align256(sizeof(int32_t) * total) + align256(inc_sort_temp_bytes(total, node_bits(N))));
 }
 
-int fem_incidence(const int64_t* conn, int64_t M, int npe, int64_t N, int32_t* inc_ptr, int32_t* inc,
-                  int32_t* work, fem_stream_t stream) {
+int fem_incidence_checked(const int64_t* conn, int64_t M, int npe, int64_t N, int32_t* inc_ptr, int32_t* inc,
+                          int32_t* work, int32_t* bad, fem_stream_t stream) {
     hipStream_t st = S(stream);
     const int64_t total = M * npe;
     if (total >= (int64_t)1 << 31 || N >= (int64_t)1 << 31) {
         set_error("fem_incidence: M*npe = %lld / N = %lld exceed int32 range", (long long)total, (long long)N);
         return FEM_EARG;
     }
+    if (bad) FEM_HIP(hipMemsetAsync(bad, 0, sizeof(int32_t), st));
     if (N <= 0) return FEM_OK;
     if (total == 0) {
         FEM_HIP(hipMemsetAsync(inc_ptr, 0, sizeof(int32_t) * (N + 1), st));
         return FEM_OK;
     }
-    // stable radix sort of (node, slot) pairs: the slots of a node come out ascending (deterministic incidence)
     const int bits = node_bits(N);
     const size_t a4 = align256(sizeof(int32_t) * total);
     const size_t tb = inc_sort_temp_bytes(total, bits);
@@ -402,7 +410,7 @@ int fem_incidence(const int64_t* conn, int64_t M, int npe, int64_t N, int32_t* i
     int32_t* kout = reinterpret_cast<int32_t*>(base + a4);
     int32_t* vin = reinterpret_cast<int32_t*>(base + 2 * a4);
     void* tmp = base + 3 * a4;
-    hipLaunchKernelGGL(k_inc_keys, dim3(stream_grid(total, 256)), dim3(256), 0, st, conn, total, kin, vin);
+    hipLaunchKernelGGL(k_inc_keys, dim3(stream_grid(total, 256)), dim3(256), 0, st, conn, total, N, kin, vin, bad);
     FEM_LAUNCHED();
     size_t tb2 = tb;
     FEM_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb2, kin, kout, vin, inc, (int)total, 0, bits, st));
@@ -410,6 +418,11 @@ int fem_incidence(const int64_t* conn, int64_t M, int npe, int64_t N, int32_t* i
     FEM_LAUNCHED();
     if (own) FEM_HIP(hipFreeAsync(base, st));
     return FEM_OK;
+}
+
+int fem_incidence(const int64_t* conn, int64_t M, int npe, int64_t N, int32_t* inc_ptr, int32_t* inc,
+                  int32_t* work, fem_stream_t stream) {
+    return fem_incidence_checked(conn, M, npe, N, inc_ptr, inc, work, nullptr, stream);
 }
 
 static int graph_grid(int64_t N) {

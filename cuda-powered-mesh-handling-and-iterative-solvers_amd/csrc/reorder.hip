@@ -1,0 +1,300 @@
+// Reverse Cuthill-McKee node renumbering on the device (opt-in; SURVEY §7: meshes arrive in file order through
+// `vtk_loader_to_torch`, `solver/element.py:39-90`, and a file-ordered numbering gives the SELL slices scattered
+// gathers and int32 columns).
+//
+// Level-synchronous Cuthill-McKee over the node graph (CSR rowptr / colidx, diagonal included): the next level is
+// every unvisited neighbour of the current level; each such node's parent is its visited neighbour with the
+// smallest CM index (atomicMin -> order-independent), and the children of a parent are numbered in their CSR
+// order (ascending node id -- the id stands in for CM's degree key, so no sort is needed and the order is unique).
+// Per level two launches: k_cm_expand (all blocks: marks the next level and its parents) and k_cm_emit (one
+// workgroup: counts every frontier node's children, scans the counts in CM order, writes the children). Levels run
+// in batches without host round trips; the state words say when the last component is done. The start node is
+// pseudo-peripheral (George-Liu: one BFS from the lowest-degree node, then the lowest-degree node of its last
+// level); further components start at their lowest-id node; nodes no element touches go last. RCM = the reversed
+// CM order.
+#include <algorithm>
+
+#include "common.hpp"
+
+namespace fem {
+
+enum { CM_B = 0, CM_E, CM_L, CM_CURSOR, CM_DONE, CM_LASTB, CM_LASTE, CM_STOP_FIRST, CM_WORDS = 16 };
+
+__device__ __forceinline__ int cm_deg(const int32_t* rowptr, int64_t i) { return rowptr[i + 1] - rowptr[i]; }
+
+__global__ void __launch_bounds__(256) k_cm_expand(const int32_t* __restrict__ rowptr,
+                                                   const int32_t* __restrict__ colidx,
+                                                   const int32_t* __restrict__ order, int32_t* __restrict__ level,
+                                                   int32_t* __restrict__ par, const int32_t* __restrict__ st) {
+    if (st[CM_DONE]) return;
+    const int b = st[CM_B], e = st[CM_E], L = st[CM_L];
+    // wave per frontier node: the row's neighbours in parallel
+    const int lane = threadIdx.x & 63;
+    for (int64_t p = b + ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)); p < e; p += (int64_t)gridDim.x * 4) {
+        const int u = order[p];
+        for (int q = rowptr[u] + lane; q < rowptr[u + 1]; q += 64) {
+            const int v = colidx[q];
+            const int lv = level[v];
+            if (lv == -1 || lv == L + 1) {
+                level[v] = L + 1;
+                atomicMin(&par[v], (int)p);
+            }
+        }
+    }
+}
+
+// block-wide exclusive scan of one int per thread (1024 threads), total in *tot
+__device__ __forceinline__ int cm_scan1024(int v, int* lds, int* tot) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    __syncthreads();
+    if (lane == 63) lds[w] = x;
+    __syncthreads();
+    if (t < 16) {
+        int s = lds[t];
+        for (int o = 1; o < 16; o <<= 1) {
+            const int y = __shfl_up(s, o, 64);
+            if (t >= o) s += y;
+        }
+        lds[16 + t] = s;
+    }
+    __syncthreads();
+    *tot = lds[31];
+    return x - v + (w > 0 ? lds[16 + w - 1] : 0);
+}
+
+__global__ void __launch_bounds__(1024) k_cm_emit(const int32_t* __restrict__ rowptr,
+                                                  const int32_t* __restrict__ colidx, int64_t N,
+                                                  int32_t* __restrict__ order, int32_t* __restrict__ cm,
+                                                  int32_t* __restrict__ level, const int32_t* __restrict__ par,
+                                                  int32_t* __restrict__ st) {
+    __shared__ int lds[32];
+    __shared__ int found;
+    if (st[CM_DONE]) return;
+    const int b = st[CM_B], e = st[CM_E], L = st[CM_L];
+    const int t = threadIdx.x;
+    if (e == b) {   // the component is finished: record its last level, start the next one (or finish)
+        if (st[CM_STOP_FIRST]) {
+            if (t == 0) st[CM_DONE] = 1;
+            return;
+        }
+        if (t == 0) found = INT_MAX;
+        __syncthreads();
+        for (int64_t c = st[CM_CURSOR]; c < N; c += 16 * 1024) {
+#pragma unroll 4
+            for (int j = 0; j < 16; ++j) {
+                const int64_t i = c + j * 1024 + t;
+                if (i < N && level[i] == -1 && cm_deg(rowptr, i) > 0) atomicMin(&found, (int)i);
+            }
+            __syncthreads();
+            const bool hit = found != INT_MAX;
+            __syncthreads();   // every thread has read `found` before the next round's atomics
+            if (hit) break;
+        }
+        __syncthreads();
+        if (t == 0) {
+            const int r = found;
+            if (r == INT_MAX) {
+                st[CM_DONE] = 1;
+            } else {
+                order[e] = r;
+                cm[r] = e;
+                level[r] = 0;
+                st[CM_CURSOR] = r + 1;
+                st[CM_E] = e + 1;
+                st[CM_L] = 0;
+            }
+        }
+        return;
+    }
+    int running = 0;
+    for (int c0 = b; c0 < e; c0 += 1024) {
+        const int p = c0 + t;
+        int cnt = 0, u = 0;
+        if (p < e) {
+            u = order[p];
+            for (int q = rowptr[u]; q < rowptr[u + 1]; ++q) {
+                const int v = colidx[q];
+                cnt += (level[v] == L + 1 && par[v] == p);
+            }
+        }
+        int tot;
+        const int ex = cm_scan1024(cnt, lds, &tot);
+        if (p < e && cnt) {
+            int k = e + running + ex;
+            for (int q = rowptr[u]; q < rowptr[u + 1]; ++q) {
+                const int v = colidx[q];
+                if (level[v] == L + 1 && par[v] == p) {
+                    order[k] = v;
+                    cm[v] = k;
+                    ++k;
+                }
+            }
+        }
+        running += tot;
+        __syncthreads();
+    }
+    if (t == 0) {
+        if (running == 0) {
+            st[CM_LASTB] = b;
+            st[CM_LASTE] = e;
+        }
+        st[CM_B] = e;
+        st[CM_E] = e + running;
+        st[CM_L] = L + 1;
+    }
+}
+
+// the lowest-degree node (then lowest id) among order[lo, hi) (the pseudo-peripheral pick) -> *key
+__global__ void k_cm_pick(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ order,
+                          const int32_t* __restrict__ st, unsigned long long* __restrict__ key) {
+    const int lo = st[CM_LASTB], hi = st[CM_LASTE];
+    for (int p = lo + blockIdx.x * blockDim.x + threadIdx.x; p < hi; p += gridDim.x * blockDim.x) {
+        const int u = order[p];
+        atomicMin(key, ((unsigned long long)(unsigned)cm_deg(rowptr, u) << 32) | (unsigned)u);
+    }
+}
+
+// lowest-degree non-isolated node (then lowest id) of the whole graph -> *key
+__global__ void k_cm_min_degree(const int32_t* __restrict__ rowptr, int64_t N, unsigned long long* __restrict__ key) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
+        const int d = cm_deg(rowptr, i);
+        if (d > 0) atomicMin(key, ((unsigned long long)(unsigned)d << 32) | (unsigned)i);
+    }
+}
+
+__global__ void k_cm_reset(int32_t* __restrict__ level, int32_t* __restrict__ par, int32_t* __restrict__ cm,
+                           int64_t N, int32_t* __restrict__ order, int32_t* __restrict__ st,
+                           const unsigned long long* __restrict__ key, int stop_first) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
+        level[i] = -1;
+        par[i] = INT_MAX;
+        cm[i] = -1;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const unsigned long long k = *key;
+        for (int w = 0; w < CM_WORDS; ++w) st[w] = 0;
+        st[CM_STOP_FIRST] = stop_first;
+        if (k == ~0ull) {   // no edges at all
+            st[CM_DONE] = 1;
+            return;
+        }
+        const int r = (int)(k & 0xffffffffu);
+        order[0] = r;
+        st[CM_E] = 1;
+    }
+}
+
+// the start node must be marked after the reset has covered it (separate launch, one thread)
+__global__ void k_cm_seed(int32_t* __restrict__ level, int32_t* __restrict__ cm, const int32_t* __restrict__ order,
+                          const int32_t* __restrict__ st) {
+    if (st[CM_DONE]) return;
+    const int r = order[0];
+    level[r] = 0;
+    cm[r] = 0;
+}
+
+// isolated nodes (no element) after the components, ascending id; flags -> positions by the caller's scan
+__global__ void k_cm_isolated_flags(const int32_t* __restrict__ rowptr, int64_t N, int32_t* __restrict__ flag) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x)
+        flag[i] = cm_deg(rowptr, i) == 0;
+}
+
+// RCM: node order[k] gets new id N - 1 - k; isolated node i gets base + pos[i]
+__global__ void k_cm_finish(const int32_t* __restrict__ rowptr, int64_t N, const int32_t* __restrict__ order,
+                            const int32_t* __restrict__ pos, const int32_t* __restrict__ st, int32_t* __restrict__ perm,
+                            int32_t* __restrict__ inv) {
+    const int ncm = st[CM_E];   // nodes numbered by the CM sweeps
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
+        if (i < ncm) {
+            const int v = order[i];
+            const int64_t nw = ncm - 1 - i;
+            perm[nw] = v;
+            inv[v] = (int32_t)nw;
+        }
+        if (cm_deg(rowptr, i) == 0) {
+            const int64_t nw = ncm + pos[i];
+            perm[nw] = (int32_t)i;
+            inv[i] = (int32_t)nw;
+        }
+    }
+}
+
+}  // namespace fem
+
+using namespace fem;
+
+extern "C" {
+
+// per-array stride of the workspace: a multiple of 64 ints, so every array (and the 8-byte key) stays aligned
+static int64_t rcm_stride(int64_t N) { return (N + 64 + 63) & ~(int64_t)63; }
+
+int64_t fem_rcm_work_len(int64_t N) { return 5 * rcm_stride(N) + CM_WORDS + 8 + fem_scan_work_len(N); }
+
+int fem_rcm(const int32_t* rowptr, const int32_t* colidx, int64_t N, int32_t* perm, int32_t* inv, int32_t* work,
+            int* levels_out, fem_stream_t stream) {
+    hipStream_t st = S(stream);
+    if (N <= 0) return FEM_OK;
+    if (N >= (int64_t)1 << 31) {
+        set_error("fem_rcm: %lld nodes exceed int32", (long long)N);
+        return FEM_EARG;
+    }
+    if (reinterpret_cast<uintptr_t>(work) & 7) {
+        set_error("fem_rcm: work must be 8-byte aligned");
+        return FEM_EARG;
+    }
+    const int64_t S = rcm_stride(N);
+    int32_t* level = work;
+    int32_t* par = level + S;
+    int32_t* cm = par + S;
+    int32_t* order = cm + S;
+    int32_t* pos = order + S;
+    int32_t* sw = pos + S;
+    unsigned long long* key = reinterpret_cast<unsigned long long*>(sw + CM_WORDS);   // 8-byte aligned: S % 64 == 0
+    int32_t* swork = sw + CM_WORDS + 8;
+    const int g = stream_grid(N, 256);
+    const int ge = 1024;   // expand grid: 4096 waves, one frontier node each
+    constexpr int BATCH = 48;
+    int state[CM_WORDS];
+    int levels = 0;
+    FEM_HIP(hipMemsetAsync(key, 0xff, sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_cm_min_degree, dim3(g), dim3(256), 0, st, rowptr, N, key);
+    FEM_LAUNCHED();
+    for (int pass = 0; pass < 2; ++pass) {   // pass 0: BFS from the lowest-degree node (first component only)
+        hipLaunchKernelGGL(k_cm_reset, dim3(g), dim3(256), 0, st, level, par, cm, N, order, sw, key, pass == 0);
+        FEM_LAUNCHED();
+        hipLaunchKernelGGL(k_cm_seed, dim3(1), dim3(1), 0, st, level, cm, order, sw);
+        FEM_LAUNCHED();
+        for (;;) {
+            for (int k = 0; k < BATCH; ++k) {
+                hipLaunchKernelGGL(k_cm_expand, dim3(ge), dim3(256), 0, st, rowptr, colidx, order, level, par, sw);
+                hipLaunchKernelGGL(k_cm_emit, dim3(1), dim3(1024), 0, st, rowptr, colidx, N, order, cm, level, par, sw);
+            }
+            FEM_LAUNCHED();
+            FEM_HIP(hipMemcpyAsync(state, sw, sizeof(state), hipMemcpyDeviceToHost, st));
+            FEM_HIP(hipStreamSynchronize(st));
+            levels += BATCH;
+            if (state[CM_DONE]) break;
+        }
+        if (pass == 0) {   // pseudo-peripheral start: lowest-degree node of the last level
+            FEM_HIP(hipMemsetAsync(key, 0xff, sizeof(unsigned long long), st));
+            hipLaunchKernelGGL(k_cm_pick, dim3(64), dim3(256), 0, st, rowptr, order, sw, key);
+            FEM_LAUNCHED();
+        }
+    }
+    hipLaunchKernelGGL(k_cm_isolated_flags, dim3(g), dim3(256), 0, st, rowptr, N, level);   // level reused
+    FEM_LAUNCHED();
+    const int rc = fem_scan_i32(level, N, pos, swork, stream);
+    if (rc != FEM_OK) return rc;
+    hipLaunchKernelGGL(k_cm_finish, dim3(g), dim3(256), 0, st, rowptr, N, order, pos, sw, perm, inv);
+    FEM_LAUNCHED();
+    if (levels_out) *levels_out = levels;
+    return FEM_OK;
+}
+
+}  // extern "C"

@@ -264,25 +264,41 @@ def static_structure_solver(coords, force, fixed, c3d4=None, c3d6=None, c3d8=Non
 
 # ============================================================================ fused mesh -> solution pipeline
 def solve_tet4(coords, elements, f, fixed, kind="poisson", E=1.0, nu=0.0, tol=1e-8, max_iter=10000, device="cuda:0",
-               rtol=None):
+               rtol=None, reorder=None):
     """Assembly + Jacobi-PCG straight from the mesh (the benchmark pipeline; no element matrices stored):
     c3d4 Poisson (dpn 1, kappa = E) or elasticity (dpn 3), Dirichlet zero on `fixed` nodes via zeros in the
     exact Jacobi M_inv, reference PCG semantics (absolute tol on sqrt(r.z); `rtol` scales it by sqrt(r0.z0)).
+    reorder="rcm": solve on the reverse Cuthill-McKee renumbering of the nodes (system.rcm_order; for meshes in
+    file order) and return u in the caller's numbering (the returned SellMatrix is the renumbered one).
     Returns (u [N, dpn], PcgResult, SellMatrix)."""
     dev = _dev(device)
     coords = coords.to(device=dev, dtype=F64).contiguous()
     elements = elements.to(device=dev, dtype=LONG).contiguous()
     N = coords.shape[0]
+    dpn = 1 if kind == "poisson" else 3
+    fixed_mask = torch.zeros(N, dtype=torch.bool, device=dev)
+    fixed_mask[torch.as_tensor(fixed).to(device=dev)] = True
+    b = f.to(device=dev, dtype=F64).reshape(N, dpn)
+    inv = None
+    if reorder is not None:
+        if reorder != "rcm":
+            raise ValueError(f"unknown reorder {reorder!r} (supported: 'rcm')")
+        perm, inv = _sys.rcm_order(elements, N)
+        coords, elements = _sys.renumber(coords, elements, perm, inv)
+        fixed_mask, b = fixed_mask[perm], b[perm]
     A = _sys.assemble_tet4_system(coords, elements, kind, E, nu)
     A.check_singular()
     mask = torch.zeros((N, A.bs), dtype=torch.uint8, device=dev)
-    mask[torch.as_tensor(fixed).to(device=dev, dtype=LONG)] = 1
+    mask[fixed_mask] = 1
     w = A.jacobi(mask.view(-1))
-    b = f.to(device=dev, dtype=F64).reshape(-1).clone()
+    b = b.reshape(-1).contiguous().clone()
     if rtol is not None:
         tol = float(rtol) * float(torch.sqrt(torch.dot(b, w * b)))
     res = A.pcg(b, None, w=w, mode=C.MODE_PCG, tol=tol, max_iter=max_iter)
-    return res.x.view(N, A.bs), res, A
+    u = res.x.view(N, A.bs)
+    if inv is not None:
+        u = u[inv]
+    return u, res, A
 
 # every public function runs in the scope of the device its `device` argument names (_capi.on_device)
 C.scope_module(globals())

@@ -143,10 +143,17 @@ def _build_graph(elements, n_nodes, compress):
     lib = C.lib()
     dev = elements.device
     elements = elements.contiguous()
-    check_connectivity(elements, n_nodes)
     M, npe = elements.shape
     st = C.stream(dev)
-    inc_ptr, inc = incidence(elements, n_nodes, checked=True)
+    # the connectivity check rides on the incidence's count pass (out-of-range slots are left out; the kernels
+    # below only compare node ids, never index by them) and is read back with the sizes in the one sync below
+    inc_ptr = torch.empty(n_nodes + 1, dtype=I32, device=dev)
+    inc = torch.empty(M * npe, dtype=I32, device=dev)
+    bad = torch.empty(1, dtype=I32, device=dev)
+    work = torch.empty(max(int(lib.fem_incidence_work_bytes(M * npe, n_nodes)), 1), dtype=torch.uint8, device=dev)
+    C.check(lib.fem_incidence_checked(C.ptr(elements), M, npe, n_nodes, C.ptr(inc_ptr), C.ptr(inc), C.ptr(work),
+                                      C.ptr(bad), st), "fem_incidence_checked")
+    del work
     row_len = torch.empty(n_nodes, dtype=I32, device=dev)
     tmp = torch.empty(max(int(lib.fem_graph_tmp_len(n_nodes)), 1), dtype=I32, device=dev)
     C.check(lib.fem_graph_count2(C.ptr(elements), npe, C.ptr(inc_ptr), C.ptr(inc), n_nodes, C.ptr(row_len),
@@ -161,7 +168,9 @@ def _build_graph(elements, n_nodes, compress):
     slice_ptr = torch.empty(ns + 1, dtype=I64, device=dev)
     work64 = torch.empty(int(lib.fem_scan_work_len(ns)) + 1, dtype=I64, device=dev)
     C.check(lib.fem_scan_i64(C.ptr(width), ns, C.ptr(slice_ptr), C.ptr(work64), st), "fem_scan_i64")
-    nnz, ent = (int(v) for v in torch.stack([rowptr[-1].to(I64), slice_ptr[-1]]).cpu())   # the sync of the build
+    nnz, ent, nbad = (int(v) for v in torch.stack([rowptr[-1].to(I64), slice_ptr[-1], bad[0].to(I64)]).cpu())
+    if nbad:   # the sync of the build; the message names the offending node like check_connectivity
+        check_connectivity(elements, n_nodes)
     # int32 row pointers / column slots: the int32 scan would wrap past 2^31 entries; the int64 slice scan cannot
     # (per-row lengths stay exact under wrap-around), and nnz <= ent
     if ent >= 2**31:
@@ -185,6 +194,30 @@ def _build_graph(elements, n_nodes, compress):
         if int(ovf.item()) == 0:
             g.dcols = dcols
     return g
+
+
+def rcm_order(elements: torch.Tensor, n_nodes: int, graph: Graph = None):
+    """Reverse Cuthill-McKee renumbering of the mesh nodes, computed on the device (csrc/reorder.hip) ->
+    (perm, inv), int64 on the elements' device: new node k is old node perm[k], old node v becomes inv[v].
+    Opt-in: meshes read in file order (`vtk_loader_to_torch`, `solver/element.py:39-90`) scatter the SELL slices'
+    gathers and can need int32 columns; the renumbered mesh's operator is the same matrix under a symmetric
+    permutation, so solutions map back exactly up to summation order."""
+    with C.device_scope(elements.device):
+        lib = C.lib()
+        g = graph if graph is not None else build_graph(elements, n_nodes, compress=False)
+        dev = elements.device
+        perm = torch.empty(n_nodes, dtype=I32, device=dev)
+        inv = torch.empty(n_nodes, dtype=I32, device=dev)
+        work = torch.empty(max(int(lib.fem_rcm_work_len(n_nodes)), 1), dtype=I32, device=dev)
+        lv = ctypes.c_int(0)
+        C.check(lib.fem_rcm(C.ptr(g.rowptr), C.ptr(g.colidx), n_nodes, C.ptr(perm), C.ptr(inv), C.ptr(work),
+                            ctypes.byref(lv), C.stream(dev)), "fem_rcm")
+        return perm.long(), inv.long()
+
+
+def renumber(coords: torch.Tensor, elements: torch.Tensor, perm: torch.Tensor, inv: torch.Tensor):
+    """The mesh under a node renumbering (rcm_order): coordinates in the new order, connectivity in new ids."""
+    return coords[perm], inv[elements]
 
 
 def pad_connectivity(blocks, npe_max):
@@ -261,10 +294,13 @@ class SellMatrix:
         """vals += the c3d4 operator computed on the fly (bs=3: elasticity E, nu; bs=1: Poisson, kappa=E)."""
         lib = C.lib()
         bad = _dev_scalar(self.device, I64, elements.shape[0])
-        C.check(lib.fem_assemble_tet4(C.ptr(coords), C.ptr(elements), float(E), float(nu), self.bs,
-                                      C.ptr(self.g.inc_ptr), C.ptr(self.g.inc), self.g.n_nodes, C.ptr(self.g.rowptr),
-                                      C.ptr(self.g.colidx), C.ptr(self.g.csr2sell), C.ptr(self.g.slice_ptr),
-                                      C.ptr(self.vals), C.ptr(bad), C.stream(self.device)), "fem_assemble_tet4")
+        store = self._fresh   # a fresh matrix is stored whole (padding zeroed): no memset, no read of the values
+        self._fresh = False
+        C.check(lib.fem_assemble_tet4_ex(C.ptr(coords), C.ptr(elements), float(E), float(nu), self.bs,
+                                         C.ptr(self.g.inc_ptr), C.ptr(self.g.inc), self.g.n_nodes,
+                                         C.ptr(self.g.rowptr), C.ptr(self.g.colidx), C.ptr(self.g.csr2sell),
+                                         C.ptr(self.g.slice_ptr), 1 if store else 0, C.ptr(self._vals), C.ptr(bad),
+                                         C.stream(self.device)), "fem_assemble_tet4_ex")
         self._bad = (bad, elements.shape[0])
         return self
 

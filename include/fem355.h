@@ -108,13 +108,17 @@ int fem_iso_geom(const double* coords, const int64_t* conn, int64_t M, int npe, 
 
 /* ------------------------------------------------------------------ mesh graph (pattern build)
  * Node -> (element, local) incidence, deterministic (entries sorted ascending by e*npe+local; a stable radix sort
- * of (node, slot) pairs). work: a device workspace of fem_incidence_work_bytes(M*npe, N) bytes (256-aligned), or
- * NULL to allocate it stream-ordered inside the call. */
+ * of (node, slot) pairs). work: a device workspace of fem_incidence_work_bytes(M*npe, N)
+ * bytes (256-aligned), or NULL to allocate it stream-ordered inside the call. */
 int64_t fem_incidence_work_bytes(int64_t total, int64_t N);
 int64_t fem_scan_work_len(int64_t n);
 /* inc_ptr [N+1], inc [M*npe] */
 int fem_incidence(const int64_t* conn, int64_t M, int npe, int64_t N, int32_t* inc_ptr, int32_t* inc,
                   int32_t* work, fem_stream_t stream);
+/* the same with the connectivity check of the reference's indexing (IndexError in torch) folded in: *bad [device
+ * int32] = 1 if any node id is outside [0, N) (such slots are left out), else 0 -- read it before using the result */
+int fem_incidence_checked(const int64_t* conn, int64_t M, int npe, int64_t N, int32_t* inc_ptr, int32_t* inc,
+                          int32_t* work, int32_t* bad, fem_stream_t stream);
 
 /* Node-graph CSR pattern (block pattern for any dpn): the coalesced COO pattern of the reference's global
  * assembly (`subdivision.ipynb:118-139`) at node granularity. Two passes:
@@ -146,6 +150,17 @@ int fem_scan_i64(const int64_t* in, int64_t n, int64_t* out, int64_t* work, fem_
 int fem_sell_fill(const int32_t* rowptr, const int32_t* colidx, int64_t nrows, const int64_t* slice_ptr,
                   int32_t* cols, int64_t* csr2sell, fem_stream_t stream);
 
+/* Reverse Cuthill-McKee renumbering of the nodes (opt-in; no reference counterpart -- the reference keeps the file
+ * order of `vtk_loader_to_torch`, `solver/element.py:39-90`, which this undoes for the assembled operator) over the
+ * node-graph CSR pattern rowptr / colidx above: perm [N] (new -> old), inv [N] (old -> new). Deterministic: level-
+ * synchronous Cuthill-McKee from a pseudo-peripheral node (George-Liu), a level's nodes grouped by their parent's
+ * CM index, a parent's children in ascending id; further components from their lowest-id node; nodes no element
+ * touches last; the CM order reversed. work: int32 [fem_rcm_work_len(N)]; *levels_out (may be NULL): level steps
+ * launched. One host round trip per 48 levels. */
+int64_t fem_rcm_work_len(int64_t N);
+int fem_rcm(const int32_t* rowptr, const int32_t* colidx, int64_t N, int32_t* perm, int32_t* inv, int32_t* work,
+            int* levels_out, fem_stream_t stream);
+
 /* ------------------------------------------------------------------ global assembly (values)
  * Deterministic row-gather: every block row sums its contributions in ascending element order.
  * fem_assemble_from_ke: values from element matrices Ke [M, npe*bs, npe*bs] (the solver-entry path: the
@@ -168,6 +183,13 @@ int fem_assemble_tet4(const double* coords, const int64_t* conn, double E, doubl
                       const int32_t* inc_ptr, const int32_t* inc, int64_t N, const int32_t* rowptr,
                       const int32_t* colidx, const int64_t* csr2sell, const int64_t* slice_ptr, double* vals,
                       int64_t* bad_idx, fem_stream_t stream);
+/* fem_assemble_tet4 with store != 0 for a matrix whose values were never written: every SELL value is written
+ * (padding zeroed) and nothing is read, so the caller skips zeroing it. Same values bit for bit as zeroing +
+ * fem_assemble_tet4 (csr2sell is not read by the default row-tile kernel; pass it for FEM355_ASM_ROWS). */
+int fem_assemble_tet4_ex(const double* coords, const int64_t* conn, double E, double nu, int bs,
+                         const int32_t* inc_ptr, const int32_t* inc, int64_t N, const int32_t* rowptr,
+                         const int32_t* colidx, const int64_t* csr2sell, const int64_t* slice_ptr, int store,
+                         double* vals, int64_t* bad_idx, fem_stream_t stream);
 
 /* SELL -> CSR values (export / testing): csr_vals [nnz*bs*bs] row-major blocks. */
 int fem_sell_to_csr_vals(const double* vals, int bs, const int32_t* rowptr, int64_t nrows,

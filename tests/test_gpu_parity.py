@@ -768,6 +768,57 @@ def test_element_row_assembly_bit_identical_to_column_form(gpu, etype, n, rep, m
     assert torch.equal(a, b), etype
 
 
+def _helix_fan(m):
+    """m non-degenerate tets [0, a, a+1, a+2] around node 0 (a row of m + 3 columns) on a helix of nodes."""
+    th = torch.arange(1, m + 3, dtype=F64) * 0.3
+    pts = torch.stack([torch.cos(th), torch.sin(th), 0.05 * th], 1)
+    c = torch.cat([torch.zeros(1, 3, dtype=F64), pts])
+    a = torch.arange(1, m + 1)
+    return c, torch.stack([torch.zeros_like(a), a, a + 1, a + 2], 1)
+
+
+@pytest.mark.parametrize("case", ["kuhn", "permuted", "fan"])
+def test_tile_assembly_bit_identical_to_row_kernels(gpu, case, monkeypatch):
+    """c3d4 / P1 assembly straight into SELL: the row-tile kernel (k_asm_tet4_tile, default; fresh matrices stored
+    whole without a memset) gives the SELL values -- padding included -- of the wave-per-row kernels
+    (k_assemble_p1w / k_assemble_el3w onto a zeroed matrix, FEM355_ASM_ROWS) bit for bit, and adding a second time
+    onto stored values too. Cases: a jittered cube, a randomly renumbered cube (wide slices), and a 1,500-tet fan (a
+    row of 1,503 columns: the CSR segment searched in memory, many output passes)."""
+    _, mesh, _, system = _mods()
+    if case == "fan":
+        c, t = _helix_fan(1500)
+    else:
+        c, t = mesh.kuhn_cube(7, jitter=0.12)
+        if case == "permuted":
+            perm = torch.randperm(c.shape[0], generator=torch.Generator().manual_seed(11))
+            inv = torch.empty_like(perm)
+            inv[perm] = torch.arange(perm.numel())
+            c, t = c[perm], inv[t]
+    cg, tg = c.to(gpu), t.to(gpu)
+    g = system.build_graph(tg, c.shape[0])
+    for kind, bs, Ek in (("poisson", 1, 2.5), ("elastic", 3, E)):
+        out = []
+        for rows in (False, True):
+            if rows:
+                monkeypatch.setenv("FEM355_ASM_ROWS", "1")
+            else:
+                monkeypatch.delenv("FEM355_ASM_ROWS", raising=False)
+            A = system.SellMatrix(g, bs)
+            A._vals.fill_(float("nan"))    # a fresh matrix's buffer is never read by the store path
+            A.add_tet4(cg, tg, Ek, NU)
+            first = A.vals.clone()
+            A.add_tet4(cg, tg, Ek, NU)
+            out.append((first, A.vals.clone()))
+        monkeypatch.delenv("FEM355_ASM_ROWS", raising=False)
+        assert not bool(torch.isnan(out[0][0]).any())
+        assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1]), (case, kind)
+        Ko = R.tet4_K(c, t, E, NU) if bs == 3 else 2.5 * R.tet4_poisson_K(c, t)
+        x = torch.randn(c.shape[0] * bs, dtype=F64, generator=torch.Generator().manual_seed(5))
+        A.check_singular()
+        y = system.SellMatrix.matvec(A, x.to(gpu))
+        assert rel(y, 2 * R.nodal_forces(Ko, t, x.view(-1, bs)).reshape(-1)) < 1e-12, (case, kind)
+
+
 def _elastic_case(system, mesh, n, gpu, jitter=0.1):
     c, t = mesh.kuhn_cube(n, jitter=jitter, device=gpu)
     f, fixed = mesh.cube_elasticity_case(c)
