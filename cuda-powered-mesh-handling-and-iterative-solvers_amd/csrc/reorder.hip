@@ -6,19 +6,19 @@
 // every unvisited neighbour of the current level; each such node's parent is its visited neighbour with the
 // smallest CM index (atomicMin -> order-independent), and the children of a parent are numbered in their CSR
 // order (ascending node id -- the id stands in for CM's degree key, so no sort is needed and the order is unique).
-// Per level two launches: k_cm_expand (all blocks: marks the next level and its parents) and k_cm_emit (one
-// workgroup: counts every frontier node's children, scans the counts in CM order, writes the children). Levels run
-// in batches without host round trips; the state words say when the last component is done. The start node is
-// pseudo-peripheral (George-Liu: one BFS from the lowest-degree node, then the lowest-degree node of its last
-// level); further components start at their lowest-id node; nodes no element touches go last. RCM = the reversed
-// CM order.
+// Per level four launches, a wave per frontier node where a node's row is walked: k_cm_expand marks the next level
+// and its parents, k_cm_count counts every frontier node's children, k_cm_scan (one workgroup) scans the counts in
+// CM order and advances the level (or starts the next component), k_cm_write numbers the children. Levels run in
+// batches without host round trips; the state words say when the last component is done. The sweep starts at the
+// lowest-(degree, id) node (a boundary node: fewest neighbours); further components start at their lowest-id node;
+// nodes no element touches go last. RCM = the reversed CM order.
 #include <algorithm>
 
 #include "common.hpp"
 
 namespace fem {
 
-enum { CM_B = 0, CM_E, CM_L, CM_CURSOR, CM_DONE, CM_LASTB, CM_LASTE, CM_STOP_FIRST, CM_WORDS = 16 };
+enum { CM_B = 0, CM_E, CM_L, CM_CURSOR, CM_DONE, CM_LASTB, CM_WORDS = 16 };
 
 __device__ __forceinline__ int cm_deg(const int32_t* rowptr, int64_t i) { return rowptr[i + 1] - rowptr[i]; }
 
@@ -68,21 +68,43 @@ __device__ __forceinline__ int cm_scan1024(int v, int* lds, int* tot) {
     return x - v + (w > 0 ? lds[16 + w - 1] : 0);
 }
 
-__global__ void __launch_bounds__(1024) k_cm_emit(const int32_t* __restrict__ rowptr,
-                                                  const int32_t* __restrict__ colidx, int64_t N,
+// children of frontier node p (CM index): unvisited-at-L neighbours whose parent is p; wave per frontier node
+__global__ void __launch_bounds__(256) k_cm_count(const int32_t* __restrict__ rowptr,
+                                                  const int32_t* __restrict__ colidx,
+                                                  const int32_t* __restrict__ order,
+                                                  const int32_t* __restrict__ level, const int32_t* __restrict__ par,
+                                                  int32_t* __restrict__ cnt, const int32_t* __restrict__ st) {
+    if (st[CM_DONE]) return;
+    const int b = st[CM_B], e = st[CM_E], L = st[CM_L];
+    const int lane = threadIdx.x & 63;
+    for (int64_t p = b + ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)); p < e; p += (int64_t)gridDim.x * 4) {
+        const int u = order[p];
+        int c = 0;
+        for (int q0 = rowptr[u]; q0 < rowptr[u + 1]; q0 += 64) {
+            const int q = q0 + lane;
+            bool ch = false;
+            if (q < rowptr[u + 1]) {
+                const int v = colidx[q];
+                ch = level[v] == L + 1 && par[v] == (int)p;
+            }
+            c += __popcll(__ballot(ch));
+        }
+        if (lane == 0) cnt[p - b] = c;
+    }
+}
+
+// one workgroup: exclusive scan of the frontier's child counts (CM order) -> off, next level's bounds; an empty
+// frontier starts the next component (lowest-id unvisited node with neighbours) or finishes
+__global__ void __launch_bounds__(1024) k_cm_scan(const int32_t* __restrict__ rowptr, int64_t N,
                                                   int32_t* __restrict__ order, int32_t* __restrict__ cm,
-                                                  int32_t* __restrict__ level, const int32_t* __restrict__ par,
-                                                  int32_t* __restrict__ st) {
+                                                  int32_t* __restrict__ level, const int32_t* __restrict__ cnt,
+                                                  int32_t* __restrict__ off, int32_t* __restrict__ st) {
     __shared__ int lds[32];
     __shared__ int found;
     if (st[CM_DONE]) return;
     const int b = st[CM_B], e = st[CM_E], L = st[CM_L];
     const int t = threadIdx.x;
-    if (e == b) {   // the component is finished: record its last level, start the next one (or finish)
-        if (st[CM_STOP_FIRST]) {
-            if (t == 0) st[CM_DONE] = 1;
-            return;
-        }
+    if (e == b) {
         if (t == 0) found = INT_MAX;
         __syncthreads();
         for (int64_t c = st[CM_CURSOR]; c < N; c += 16 * 1024) {
@@ -112,51 +134,57 @@ __global__ void __launch_bounds__(1024) k_cm_emit(const int32_t* __restrict__ ro
         }
         return;
     }
+    const int nf = e - b;
     int running = 0;
-    for (int c0 = b; c0 < e; c0 += 1024) {
-        const int p = c0 + t;
-        int cnt = 0, u = 0;
-        if (p < e) {
-            u = order[p];
-            for (int q = rowptr[u]; q < rowptr[u + 1]; ++q) {
-                const int v = colidx[q];
-                cnt += (level[v] == L + 1 && par[v] == p);
-            }
-        }
+    for (int c0 = 0; c0 < nf; c0 += 1024) {
+        const int v = c0 + t < nf ? cnt[c0 + t] : 0;
         int tot;
-        const int ex = cm_scan1024(cnt, lds, &tot);
-        if (p < e && cnt) {
-            int k = e + running + ex;
-            for (int q = rowptr[u]; q < rowptr[u + 1]; ++q) {
-                const int v = colidx[q];
-                if (level[v] == L + 1 && par[v] == p) {
-                    order[k] = v;
-                    cm[v] = k;
-                    ++k;
-                }
-            }
-        }
+        const int ex = cm_scan1024(v, lds, &tot);
+        if (c0 + t < nf) off[c0 + t] = running + ex;
         running += tot;
         __syncthreads();
     }
     if (t == 0) {
-        if (running == 0) {
-            st[CM_LASTB] = b;
-            st[CM_LASTE] = e;
-        }
         st[CM_B] = e;
         st[CM_E] = e + running;
         st[CM_L] = L + 1;
+        st[CM_LASTB] = b;   // the level just numbered from (k_cm_write's parents)
     }
 }
 
-// the lowest-degree node (then lowest id) among order[lo, hi) (the pseudo-peripheral pick) -> *key
-__global__ void k_cm_pick(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ order,
-                          const int32_t* __restrict__ st, unsigned long long* __restrict__ key) {
-    const int lo = st[CM_LASTB], hi = st[CM_LASTE];
-    for (int p = lo + blockIdx.x * blockDim.x + threadIdx.x; p < hi; p += gridDim.x * blockDim.x) {
+// the children of frontier node p in CSR order at CM indices [e + off[p - b], ...); wave per frontier node
+__global__ void __launch_bounds__(256) k_cm_write(const int32_t* __restrict__ rowptr,
+                                                  const int32_t* __restrict__ colidx, int32_t* __restrict__ order,
+                                                  int32_t* __restrict__ cm, const int32_t* __restrict__ level,
+                                                  const int32_t* __restrict__ par, const int32_t* __restrict__ off,
+                                                  const int32_t* __restrict__ st) {
+    if (st[CM_DONE]) return;
+    // k_cm_scan has advanced the state: parents are [LASTB, B), children start at B; a new component (L == 0) has
+    // nothing to write
+    const int L = st[CM_L];
+    if (L == 0) return;
+    const int b = st[CM_LASTB], e = st[CM_B];
+    const int lane = threadIdx.x & 63;
+    const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    for (int64_t p = b + ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)); p < e; p += (int64_t)gridDim.x * 4) {
         const int u = order[p];
-        atomicMin(key, ((unsigned long long)(unsigned)cm_deg(rowptr, u) << 32) | (unsigned)u);
+        int k = e + off[p - b];
+        for (int q0 = rowptr[u]; q0 < rowptr[u + 1]; q0 += 64) {
+            const int q = q0 + lane;
+            bool ch = false;
+            int v = 0;
+            if (q < rowptr[u + 1]) {
+                v = colidx[q];
+                ch = level[v] == L && par[v] == (int)p;
+            }
+            const unsigned long long m = __ballot(ch);
+            if (ch) {
+                const int kk = k + __popcll(m & lt);
+                order[kk] = v;
+                cm[v] = kk;
+            }
+            k += __popcll(m);
+        }
     }
 }
 
@@ -170,7 +198,7 @@ __global__ void k_cm_min_degree(const int32_t* __restrict__ rowptr, int64_t N, u
 
 __global__ void k_cm_reset(int32_t* __restrict__ level, int32_t* __restrict__ par, int32_t* __restrict__ cm,
                            int64_t N, int32_t* __restrict__ order, int32_t* __restrict__ st,
-                           const unsigned long long* __restrict__ key, int stop_first) {
+                           const unsigned long long* __restrict__ key) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (int64_t)gridDim.x * blockDim.x) {
         level[i] = -1;
         par[i] = INT_MAX;
@@ -179,7 +207,6 @@ __global__ void k_cm_reset(int32_t* __restrict__ level, int32_t* __restrict__ pa
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         const unsigned long long k = *key;
         for (int w = 0; w < CM_WORDS; ++w) st[w] = 0;
-        st[CM_STOP_FIRST] = stop_first;
         if (k == ~0ull) {   // no edges at all
             st[CM_DONE] = 1;
             return;
@@ -234,7 +261,7 @@ extern "C" {
 // per-array stride of the workspace: a multiple of 64 ints, so every array (and the 8-byte key) stays aligned
 static int64_t rcm_stride(int64_t N) { return (N + 64 + 63) & ~(int64_t)63; }
 
-int64_t fem_rcm_work_len(int64_t N) { return 5 * rcm_stride(N) + CM_WORDS + 8 + fem_scan_work_len(N); }
+int64_t fem_rcm_work_len(int64_t N) { return 7 * rcm_stride(N) + CM_WORDS + 8 + fem_scan_work_len(N); }
 
 int fem_rcm(const int32_t* rowptr, const int32_t* colidx, int64_t N, int32_t* perm, int32_t* inv, int32_t* work,
             int* levels_out, fem_stream_t stream) {
@@ -254,7 +281,9 @@ int fem_rcm(const int32_t* rowptr, const int32_t* colidx, int64_t N, int32_t* pe
     int32_t* cm = par + S;
     int32_t* order = cm + S;
     int32_t* pos = order + S;
-    int32_t* sw = pos + S;
+    int32_t* cnt = pos + S;
+    int32_t* off = cnt + S;
+    int32_t* sw = off + S;
     unsigned long long* key = reinterpret_cast<unsigned long long*>(sw + CM_WORDS);   // 8-byte aligned: S % 64 == 0
     int32_t* swork = sw + CM_WORDS + 8;
     const int g = stream_grid(N, 256);
@@ -265,27 +294,22 @@ int fem_rcm(const int32_t* rowptr, const int32_t* colidx, int64_t N, int32_t* pe
     FEM_HIP(hipMemsetAsync(key, 0xff, sizeof(unsigned long long), st));
     hipLaunchKernelGGL(k_cm_min_degree, dim3(g), dim3(256), 0, st, rowptr, N, key);
     FEM_LAUNCHED();
-    for (int pass = 0; pass < 2; ++pass) {   // pass 0: BFS from the lowest-degree node (first component only)
-        hipLaunchKernelGGL(k_cm_reset, dim3(g), dim3(256), 0, st, level, par, cm, N, order, sw, key, pass == 0);
-        FEM_LAUNCHED();
-        hipLaunchKernelGGL(k_cm_seed, dim3(1), dim3(1), 0, st, level, cm, order, sw);
-        FEM_LAUNCHED();
-        for (;;) {
-            for (int k = 0; k < BATCH; ++k) {
-                hipLaunchKernelGGL(k_cm_expand, dim3(ge), dim3(256), 0, st, rowptr, colidx, order, level, par, sw);
-                hipLaunchKernelGGL(k_cm_emit, dim3(1), dim3(1024), 0, st, rowptr, colidx, N, order, cm, level, par, sw);
-            }
-            FEM_LAUNCHED();
-            FEM_HIP(hipMemcpyAsync(state, sw, sizeof(state), hipMemcpyDeviceToHost, st));
-            FEM_HIP(hipStreamSynchronize(st));
-            levels += BATCH;
-            if (state[CM_DONE]) break;
+    hipLaunchKernelGGL(k_cm_reset, dim3(g), dim3(256), 0, st, level, par, cm, N, order, sw, key);
+    FEM_LAUNCHED();
+    hipLaunchKernelGGL(k_cm_seed, dim3(1), dim3(1), 0, st, level, cm, order, sw);
+    FEM_LAUNCHED();
+    for (;;) {
+        for (int k = 0; k < BATCH; ++k) {
+            hipLaunchKernelGGL(k_cm_expand, dim3(ge), dim3(256), 0, st, rowptr, colidx, order, level, par, sw);
+            hipLaunchKernelGGL(k_cm_count, dim3(ge), dim3(256), 0, st, rowptr, colidx, order, level, par, cnt, sw);
+            hipLaunchKernelGGL(k_cm_scan, dim3(1), dim3(1024), 0, st, rowptr, N, order, cm, level, cnt, off, sw);
+            hipLaunchKernelGGL(k_cm_write, dim3(ge), dim3(256), 0, st, rowptr, colidx, order, cm, level, par, off, sw);
         }
-        if (pass == 0) {   // pseudo-peripheral start: lowest-degree node of the last level
-            FEM_HIP(hipMemsetAsync(key, 0xff, sizeof(unsigned long long), st));
-            hipLaunchKernelGGL(k_cm_pick, dim3(64), dim3(256), 0, st, rowptr, order, sw, key);
-            FEM_LAUNCHED();
-        }
+        FEM_LAUNCHED();
+        FEM_HIP(hipMemcpyAsync(state, sw, sizeof(state), hipMemcpyDeviceToHost, st));
+        FEM_HIP(hipStreamSynchronize(st));
+        levels += BATCH;
+        if (state[CM_DONE]) break;
     }
     hipLaunchKernelGGL(k_cm_isolated_flags, dim3(g), dim3(256), 0, st, rowptr, N, level);   // level reused
     FEM_LAUNCHED();

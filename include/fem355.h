@@ -153,9 +153,9 @@ int fem_sell_fill(const int32_t* rowptr, const int32_t* colidx, int64_t nrows, c
 /* Reverse Cuthill-McKee renumbering of the nodes (opt-in; no reference counterpart -- the reference keeps the file
  * order of `vtk_loader_to_torch`, `solver/element.py:39-90`, which this undoes for the assembled operator) over the
  * node-graph CSR pattern rowptr / colidx above: perm [N] (new -> old), inv [N] (old -> new). Deterministic: level-
- * synchronous Cuthill-McKee from a pseudo-peripheral node (George-Liu), a level's nodes grouped by their parent's
- * CM index, a parent's children in ascending id; further components from their lowest-id node; nodes no element
- * touches last; the CM order reversed. work: int32 [fem_rcm_work_len(N)]; *levels_out (may be NULL): level steps
+ * synchronous Cuthill-McKee from the lowest-(degree, id) node, a level's nodes grouped by their parent's CM index,
+ * a parent's children in ascending id; further components from their lowest-id node; nodes no element touches last;
+ * the CM order reversed. work: int32 [fem_rcm_work_len(N)]; *levels_out (may be NULL): level steps
  * launched. One host round trip per 48 levels. */
 int64_t fem_rcm_work_len(int64_t N);
 int fem_rcm(const int32_t* rowptr, const int32_t* colidx, int64_t N, int32_t* perm, int32_t* inv, int32_t* work,

@@ -7,20 +7,18 @@ with this oracle is exact (same permutation); its quality is pinned against scip
 
 Rule (deterministic): level-synchronous Cuthill-McKee over the node graph; a next-level node's parent is its
 neighbour in the current level with the smallest CM index; nodes are numbered parent by parent in CM order, a
-parent's children in ascending node id. Start: the lowest-(degree, id) node; one BFS of its component; the
-lowest-(degree, id) node of that BFS's last level is the start of the real sweep. A finished component is followed
-by the lowest-id unvisited node that has neighbours; nodes without any (no element) come last in id order. The CM
-order of the swept nodes is reversed."""
+parent's children in ascending node id. Start: the lowest-(degree, id) node (a boundary node). A finished
+component is followed by the lowest-id unvisited node that has neighbours; nodes without any (no element) come last
+in id order. The CM order of the swept nodes is reversed."""
 import numpy as np
 
 
 def _sweep(rowptr, colidx, order, level, cm, start, n_done):
-    """CM sweep of the component of `start`; appends to `order`; returns the last level's nodes."""
+    """CM sweep of the component of `start`; appends to `order`."""
     order.append(start)
     cm[start] = n_done
     level[start] = 0
     b, e, L = n_done, n_done + 1, 0
-    last = [start]
     while b < e:
         par = {}
         for p in range(b, e):
@@ -39,10 +37,7 @@ def _sweep(rowptr, colidx, order, level, cm, start, n_done):
                     order.append(v)
                     cm[v] = k
                     k += 1
-        if k == e:
-            last = order[b:e]
         b, e, L = e, k, L + 1
-    return last
 
 
 def rcm(rowptr, colidx, n):
@@ -59,12 +54,7 @@ def rcm(rowptr, colidx, n):
         r0 = int(live[np.argmin(key)])
         level = np.full(n, -1, dtype=np.int64)
         cm = np.full(n, -1, dtype=np.int64)
-        last = _sweep(rowptr, colidx, [], level, cm, r0, 0)
-        last = np.asarray(last, dtype=np.int64)
-        r1 = int(last[np.argmin(deg[last] * (1 << 32) + last)])
-        level[:] = -1
-        cm[:] = -1
-        _sweep(rowptr, colidx, order, level, cm, r1, 0)
+        _sweep(rowptr, colidx, order, level, cm, r0, 0)
         cursor = 0
         while True:
             cand = np.nonzero((level[cursor:] == -1) & (deg[cursor:] > 0))[0]
