@@ -19,6 +19,7 @@
 #include <rccl/rccl.h>
 #include <stddef.h>
 
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -206,6 +207,9 @@ struct PcgState {
     // (zeroed by fem_pcg_start, and by the host before the counters could wrap)
     unsigned pk_epoch;
     unsigned pk_pad_;
+    // merged update (k_pcg_update2): launches completed since fem_pcg_start (the epoch its release word counts)
+    unsigned u2_epoch;
+    unsigned u2_pad_;
 };
 
 constexpr int PCG_BLOCK = 256;
@@ -422,6 +426,156 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_pupdate(int64_t n, double* __
         x[i] += alpha * p[i];
         if (upd_p) p[i] = w[i] * r[i] + beta * p[i];
     }
+}
+
+// K2 + K3 as ONE launch (3-kernel schedule, FEM_TUNE_UPD1): r <- r - alpha q, z = w r and the r.z partials; the
+// last-arriving workgroup finishes r.z (stop test, beta: finish_rz) and releases the others through a write-through
+// broadcast + an epoch word (MI355X_MICROARCH.md visibility table: sc1 stores drained before the releasing atomic,
+// sc1 loads after the poll); then x <- x + alpha p and p <- z + beta p. Each thread keeps the z of its first U2_NPT
+// elements in registers across the wait, so r and w are read once per iteration (8 vector streams instead of the
+// two kernels' 10) and one launch boundary fewer. Every workgroup must be resident at once: the grid is sized from
+// the occupancy query (u2_setup); the wait is bounded in time (FEM_PCG_SYNC_TIMEOUT, never a hang).
+constexpr int U2_NPT = 8;                 // double2 elements per thread whose z stays in registers
+enum { U2_REL = 0, U2_BC = 32, U2_TMO = 64, U2_WORDS = 96 };   // release word, broadcast (beta, halt), give-up
+constexpr uint64_t U2_WAIT_TICKS = 200000000ull;   // 2 s of s_memrealtime (100 MHz)
+
+__global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update2(int64_t n, double* __restrict__ x, double* __restrict__ p,
+                                                           double* __restrict__ r, const double* __restrict__ q,
+                                                           const double* __restrict__ w, PcgState* __restrict__ st,
+                                                           RedBuf red, double* __restrict__ hist, int64_t hist_len,
+                                                           unsigned* __restrict__ sync) {
+    __shared__ double lds4[4];
+    __shared__ int flag;
+    __shared__ double bc_s[2];
+    if (st->halt || st->iter >= st->max_iter) return;
+    const unsigned e = st->u2_epoch + 1;
+    const double alpha = st->alpha;
+    const bool cg = st->mode != FEM_MODE_PCG;
+    const int64_t n2 = n >> 1, stride = (int64_t)gridDim.x * PCG_BLOCK;
+    const int64_t i0 = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x;
+    const double2* q2 = reinterpret_cast<const double2*>(q);
+    const double2* w2 = reinterpret_cast<const double2*>(w);
+    double2* r2 = reinterpret_cast<double2*>(r);
+    double2 z[U2_NPT];
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < U2_NPT; ++k) {
+        const int64_t i = i0 + k * stride;
+        z[k] = make_double2(0.0, 0.0);
+        if (i < n2) {
+            double2 rv = r2[i], qv = q2[i], wv = w2[i];
+            rv.x = rv.x - alpha * qv.x;
+            rv.y = rv.y - alpha * qv.y;
+            if (cg) {
+                if (wv.x == 0.0) rv.x = 0.0;
+                if (wv.y == 0.0) rv.y = 0.0;
+            }
+            r2[i] = rv;
+            z[k] = make_double2(wv.x * rv.x, wv.y * rv.y);
+            acc += rv.x * z[k].x;
+            acc += rv.y * z[k].y;
+        }
+    }
+    for (int64_t i = i0 + U2_NPT * stride; i < n2; i += stride) {   // past the register capacity
+        double2 rv = r2[i], qv = q2[i], wv = w2[i];
+        rv.x = rv.x - alpha * qv.x;
+        rv.y = rv.y - alpha * qv.y;
+        if (cg) {
+            if (wv.x == 0.0) rv.x = 0.0;
+            if (wv.y == 0.0) rv.y = 0.0;
+        }
+        r2[i] = rv;
+        acc += rv.x * (wv.x * rv.x);
+        acc += rv.y * (wv.y * rv.y);
+    }
+    double ztail = 0.0;
+    const bool tail = (n & 1) && blockIdx.x == 0 && threadIdx.x == 0;
+    if (tail) {
+        const int64_t i = n - 1;
+        double rv = r[i] - alpha * q[i];
+        if (cg && w[i] == 0.0) rv = 0.0;
+        r[i] = rv;
+        ztail = w[i] * rv;
+        acc += rv * ztail;
+    }
+    acc = block_sum256(acc, lds4);
+    double rz_new;
+    const bool last = reduce_grid(acc, red.part(RED_K2), red.cnt(RED_K2), &rz_new, lds4, &flag);
+    if (threadIdx.x == 0) {
+        double beta = 0.0, halt = 0.0;
+        bool ok = true;
+        if (last) {
+            finish_rz(st, rz_new, hist, hist_len);
+            beta = st->beta;
+            halt = st->halt ? 1.0 : 0.0;
+            __hip_atomic_store(reinterpret_cast<double*>(sync + U2_BC), beta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(reinterpret_cast<double*>(sync + U2_BC) + 1, halt, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(sync + U2_REL, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            for (unsigned spins = 0;; ++spins) {
+                if (__hip_atomic_load(sync + U2_REL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= e) break;
+                if ((spins & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > U2_WAIT_TICKS) {
+                    ok = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            if (ok) {
+                beta = __hip_atomic_load(reinterpret_cast<const double*>(sync + U2_BC), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+                halt = __hip_atomic_load(reinterpret_cast<const double*>(sync + U2_BC) + 1, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+            } else {   // a workgroup that never became resident: stop the solve instead of hanging
+                __hip_atomic_store(sync + U2_TMO, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                st->status = FEM_PCG_SYNC_TIMEOUT;
+                st->halt = 1;
+            }
+        }
+        bc_s[0] = beta;
+        bc_s[1] = ok ? halt : -1.0;
+    }
+    __syncthreads();
+    const double beta = bc_s[0];
+    if (bc_s[1] < 0.0) return;
+    const bool upd_p = bc_s[1] == 0.0;
+    double2* x2 = reinterpret_cast<double2*>(x);
+    double2* p2 = reinterpret_cast<double2*>(p);
+#pragma unroll
+    for (int k = 0; k < U2_NPT; ++k) {
+        const int64_t i = i0 + k * stride;
+        if (i < n2) {
+            double2 pv = p2[i], xv = x2[i];
+            xv.x += alpha * pv.x;
+            xv.y += alpha * pv.y;
+            x2[i] = xv;
+            if (upd_p) {
+                pv.x = z[k].x + beta * pv.x;
+                pv.y = z[k].y + beta * pv.y;
+                p2[i] = pv;
+            }
+        }
+    }
+    for (int64_t i = i0 + U2_NPT * stride; i < n2; i += stride) {
+        double2 pv = p2[i], xv = x2[i];
+        xv.x += alpha * pv.x;
+        xv.y += alpha * pv.y;
+        x2[i] = xv;
+        if (upd_p) {
+            const double2 rv = r2[i], wv = w2[i];
+            pv.x = wv.x * rv.x + beta * pv.x;
+            pv.y = wv.y * rv.y + beta * pv.y;
+            p2[i] = pv;
+        }
+    }
+    if (tail) {
+        const int64_t i = n - 1;
+        x[i] += alpha * p[i];
+        if (upd_p) p[i] = ztail + beta * p[i];
+    }
+    if (last && threadIdx.x == 0) st->u2_epoch = e;   // every workgroup read the epoch before the release
 }
 
 // ---------------------------------------------------------------- deferred schedule (3 kernels, no grid atomics)
@@ -1484,6 +1638,10 @@ struct fem_pcg {
     int32_t* pd_pub;                      // [G][nranks][2] rows of each local workgroup gathered by each rank
     int pd_init_pending;                  // the next launch runs the distributed init (r0, u0, r0.u0)
     unsigned long long* pd_prof;          // fem_pcg_set_prof: launches run the phase-clock build into this buffer
+    // merged update (FEM_TUNE_UPD1, 3-kernel schedule): K2 + K3 as one launch of u2_grid resident workgroups
+    int upd1;
+    int u2_grid;
+    unsigned* u2_sync;                    // [U2_WORDS]: release epoch, broadcast (beta, halt), give-up
 };
 
 #define FEM_NCCL(call)                                                                         \
@@ -1784,6 +1942,46 @@ static int c1f_setup(fem_pcg* s) {
     return FEM_OK;
 }
 
+// merged update (k_pcg_update2) for the single-GPU 3-kernel schedule: grid = every workgroup resident at once
+// (occupancy query, cached per device; the value is idempotent, so a racing first query only repeats the work)
+static int u2_setup(fem_pcg* s) {
+    s->upd1 = 0;
+    if (!(s->tune & FEM_TUNE_UPD1) || s->dist || s->fused || s->deferred || s->persist || s->has_con || s->n < 2)
+        return FEM_OK;
+    static std::atomic<int> occ[64];
+    int dev = 0;
+    FEM_HIP(hipGetDevice(&dev));
+    int per_cu = occ[dev & 63].load();
+    if (per_cu == 0) {
+        int ncu = 0, nb = 0;
+        FEM_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+        FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pcg_update2, PCG_BLOCK, 0));
+        per_cu = (nb < 1 || ncu < NXCD) ? -1 : ((ncu / NXCD) * NXCD) * (nb < 8 ? nb : 8);
+        occ[dev & 63].store(per_cu);
+    }
+    if (per_cu < 0) return FEM_OK;   // no resident grid: the two-kernel update stays
+    int64_t want = cdiv(s->n / 2 + 1, PCG_BLOCK);
+    want = cdiv(want, NXCD) * NXCD;
+    s->u2_grid = (int)(want < per_cu ? want : per_cu);
+    if (!s->u2_sync) {
+        hipError_t e = pool_alloc((void**)&s->u2_sync, sizeof(unsigned) * U2_WORDS, s->stream, s->bs == 1);
+        if (e != hipSuccess) {
+            set_error("u2_setup: %s", hipGetErrorString(e));
+            return FEM_EHIP;
+        }
+    }
+    FEM_HIP(hipMemsetAsync(s->u2_sync, 0, sizeof(unsigned) * U2_WORDS, s->stream));
+    s->upd1 = 1;
+    return FEM_OK;
+}
+
+static int launch_update2(fem_pcg* s) {
+    hipLaunchKernelGGL(k_pcg_update2, dim3(s->u2_grid), dim3(PCG_BLOCK), 0, s->stream, s->n, s->x, s->p0, s->r, s->q,
+                       s->w, s->st, s->red, s->hist, s->hist_len, s->u2_sync);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
 static int c1f_launch(fem_pcg* s) {
     Cg1FArgs a{};
     a.nslices = s->nslices;
@@ -2065,9 +2263,13 @@ static int launch_iterations(fem_pcg* s, int k) {
     for (int i = 0; i < k; ++i) {
         int rc;
         if ((rc = launch_spmv_dot(s))) return rc;
-        if ((rc = launch_exchange_dot(s))) return rc;
-        if ((rc = launch_update_finish(s))) return rc;
-        if ((rc = launch_pupdate(s))) return rc;
+        if (s->upd1) {
+            if ((rc = launch_update2(s))) return rc;
+        } else {
+            if ((rc = launch_exchange_dot(s))) return rc;
+            if ((rc = launch_update_finish(s))) return rc;
+            if ((rc = launch_pupdate(s))) return rc;
+        }
         s->launched++;
     }
     return FEM_OK;
@@ -2259,7 +2461,7 @@ int fem_pcg_create(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_
         return FEM_EARG;
     }
     fem_pcg* s = new fem_pcg();
-    s->tune = FEM_TUNE_REVERSE | FEM_TUNE_PAIR | FEM_TUNE_PK_SC1 | FEM_TUNE_PK_PACK | FEM_TUNE_PK_UNI;
+    s->tune = FEM_TUNE_REVERSE | FEM_TUNE_PAIR | FEM_TUNE_PK_SC1 | FEM_TUNE_PK_PACK | FEM_TUNE_PK_UNI | FEM_TUNE_UPD1;
     s->nrows = nrows;
     s->bs = bs;
     s->nslices = cdiv(nrows, 64);
@@ -2726,6 +2928,7 @@ int fem_pcg_start(fem_pcg* s) {
         int prc = refresh_pairing(s);
         if (!prc) prc = persist_setup(s);
         if (!prc) prc = c1f_setup(s);
+        if (!prc) prc = u2_setup(s);
         if (prc) return prc;
     }
     PcgState h{};
@@ -3189,6 +3392,17 @@ int fem_pcg_profile(fem_pcg* s, int k, int every, double* ms, int* n) {
             continue;
         }
         const bool dfr = s->deferred && !s->dist;
+        if (s->upd1) {   // buckets: [0] SpMV, [1] merged update, [2] empty
+            (void)hipEventRecord(evs[4 * si + 0], s->stream);
+            rc = launch_spmv_dot(s);
+            (void)hipEventRecord(evs[4 * si + 1], s->stream);
+            if (!rc) rc = launch_update2(s);
+            (void)hipEventRecord(evs[4 * si + 2], s->stream);
+            (void)hipEventRecord(evs[4 * si + 3], s->stream);
+            s->launched++;
+            ++si;
+            continue;
+        }
         (void)hipEventRecord(evs[4 * si + 0], s->stream);
         rc = dfr ? launch_deferred(s, 0) : launch_spmv_dot(s);
         (void)hipEventRecord(evs[4 * si + 1], s->stream);
@@ -3475,6 +3689,7 @@ void fem_pcg_destroy(fem_pcg* s) {
     pool_free(s->pk_part, s->stream);
     pool_free(s->pk_sync, s->stream);
     pool_free(s->pk_v, s->stream);
+    pool_free(s->u2_sync, s->stream);
     pool_free(s->st, s->stream);
     host_state_free(s->st_host, s->stream);
     delete s;

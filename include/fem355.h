@@ -412,13 +412,18 @@ int fem_enforce_constraints(double* x, double* r, int64_t n, int order, int64_t 
                             const int64_t* rbe2_master, int64_t S, const int64_t* spc_dof, const double* spc_val,
                             int64_t G, const int64_t* r3_ptr, const int64_t* r3_master, const double* r3_wsum,
                             const int64_t* r3_slave, const double* r3_w, fem_stream_t stream);
-/* tuning flags (default FEM_TUNE_REVERSE | FEM_TUNE_PAIR | FEM_TUNE_PK_SC1 | FEM_TUNE_PK_PACK | FEM_TUNE_PK_UNI): the SpMV of every schedule sweeps each XCD's slice range backwards on
+/* tuning flags (default FEM_TUNE_REVERSE | FEM_TUNE_PAIR | FEM_TUNE_PK_SC1 | FEM_TUNE_PK_PACK | FEM_TUNE_PK_UNI |
+ * FEM_TUNE_UPD1): the SpMV of every schedule sweeps each XCD's slice range backwards on
  * odd iterations, so the matrix tail read last (still in the MI355X's 256 MB memory-side cache) is read first by
  * the next sweep: 67 -> 57 us per SpMV on the 10M Poisson matrix. Results depend on the flags only through the
  * order of the per-block p.q partials (deterministic for a given flag set). */
 enum { FEM_TUNE_REVERSE = 1, FEM_TUNE_PAIR = 2, FEM_TUNE_PK_SC1 = 4, FEM_TUNE_PK_PACK = 8, FEM_TUNE_C1F = 16,
        FEM_TUNE_PK_COOP = 32, FEM_TUNE_DIST_FINE = 64, FEM_TUNE_PK_UNI = 128, FEM_TUNE_PK_WIDE = 256,
-       FEM_TUNE_DIST_DROP = 512 };
+       FEM_TUNE_DIST_DROP = 512, FEM_TUNE_UPD1 = 1024 };
+/* FEM_TUNE_UPD1 (default): single-GPU 3-kernel schedule (bs = 3 past the persistent kernel's capacity) -- the r / z
+ * update and the x / p update run as ONE launch with every workgroup resident (k_pcg_update2: the last workgroup
+ * finishes r.z and releases the others), z kept in registers in between: 8 vector streams per iteration instead of
+ * 10. Same recurrences; p = z + beta p rounds z before the add (the two-kernel form may fuse it). */
 /* FEM_TUNE_DIST_DROP: fault injection for the multi-GPU failure chain (tests only): the rank publishes no u row and
  * no flag to the other ranks, so their launches give up (FEM_PCG_SYNC_TIMEOUT) within the bounded waits */
 /* FEM_TUNE_PK_WIDE: persistent schedule (bs = 1, single GPU) -- keep the 7-slot build when every wave owns at most
