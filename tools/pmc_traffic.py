@@ -22,6 +22,8 @@ import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS_3K = {"spmv_dot": "k_pcg_spmv_dot", "update": "k_pcg_update(", "pupdate": "k_pcg_pupdate"}
+# 3-kernel schedule with the merged update (FEM_TUNE_UPD1, default): two dispatches per iteration
+KERNELS_3K_MERGED = {"spmv_dot": "k_pcg_spmv_dot", "update": "k_pcg_update2"}
 KERNELS_DEFERRED = {"spmv_dot": "k_pcg_d1", "update": "k_pcg_d2", "pupdate": "k_pcg_d3"}
 # persistent schedule: the bench's K timed steps are ONE dispatch; durations and bytes are divided by K (per iteration)
 KERNELS_PERSIST = {"spmv_dot": "k_pcg_persist"}
@@ -71,6 +73,8 @@ def main():
     deferred = rk.startswith("k_pcg_d1") if rk else any("k_pcg_d1" in r["Kernel_Name"] for r in trace)
     persist = rk.startswith("k_pcg_persist") if rk else any("k_pcg_persist" in r["Kernel_Name"] for r in trace)
     KERNELS = KERNELS_PERSIST if persist else (KERNELS_DEFERRED if deferred else KERNELS_3K)
+    if KERNELS is KERNELS_3K and any("k_pcg_update2" in r["Kernel_Name"] for r in trace):
+        KERNELS = KERNELS_3K_MERGED
     ndisp = 1 if persist else a.steps      # dispatches of the timed region
     per = a.steps if persist else 1        # iterations per dispatch
     out = {"workload": a.workload, "timed_dispatches": ndisp, "iterations_per_dispatch": per, "kernels": {},

@@ -6,7 +6,7 @@
 # No sys/runtime/hip/hsa/memory-copy traces are combined with --pmc.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/prof
+OUT=${OUT:-gpurun_out/prof}
 mkdir -p $OUT
 export FEM355_PK_COOP=0   # rocprofv3 segfaults at exit after a cooperative launch (the timed launches are plain)
 ARGS=${PROF_ARGS:-"--steps 100 --warmup 10 --no-cpu-baseline"}
