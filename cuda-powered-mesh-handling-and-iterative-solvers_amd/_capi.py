@@ -22,6 +22,9 @@ LIB_PATH = os.environ.get("FEM355_LIB", os.path.join(PKG_DIR, "lib", "libfem355.
 FEM_OK, FEM_EBADTYPE, FEM_ESINGULAR, FEM_EHIP, FEM_ERCCL, FEM_EARG = range(6)
 PCG_RUNNING, PCG_CONVERGED, PCG_MAXITER, PCG_BREAKDOWN, PCG_ALPHA_NAN, PCG_BETA_NAN, PCG_SYNC_TIMEOUT = range(7)
 MODE_CG_STABLE, MODE_PCG, MODE_CG_CONSTRAINED = 0, 1, 2
+# include/fem355.h FEM_TUNE_*: the library's default set for a new context, and the merged-update flag
+TUNE_UPD1 = 1024
+TUNE_DEFAULT = 1 | 2 | 4 | 8 | 128 | TUNE_UPD1
 KIND_ELASTIC, KIND_POISSON, KIND_MASS = 0, 1, 2
 ISO_SUM, ISO_STACK, ISO_VOLUME, ISO_MASS = 0, 1, 2, 3
 

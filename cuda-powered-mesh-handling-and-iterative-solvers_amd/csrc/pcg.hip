@@ -143,12 +143,18 @@ constexpr int SPMV_UP = 8;  // pairs in flight of the paired layout (tools/spmv_
 // SpMV row of the 16-byte-value copy of the matrix: bs = 1 lane-paired layout (sell_pair.hpp), bs = 3 plane-paired
 // layout A (sell_pair3.hpp: 4 sixteen-byte + 1 eight-byte value loads per block, nontemporal; tools/spmv3_layout.py:
 // 10M elastic 369 -> 348 us stand-alone). Both keep the plain layout's per-row summation order.
+#ifndef FEM_K1_U3
+#define FEM_K1_U3 1   // bs = 3 blocks in flight per lane (layout A)
+#endif
+#ifndef FEM_K1_G3
+#define FEM_K1_G3 0   // bs = 3 gathers: 0 = three 8-byte loads, 1 = 8 + 16 bytes
+#endif
 template <int BS>
 __device__ __forceinline__ void sell_row_paired(int64_t s, int lane, const int64_t* __restrict__ slice_ptr,
                                                 const int16_t* __restrict__ cols, const double* __restrict__ vals,
                                                 const double* __restrict__ x, double out[BS]) {
     if constexpr (BS == 1) out[0] = sell_row_pair<SPMV_UP>(s, lane, slice_ptr, cols, vals, x);
-    else sell3_row_a<1, SPMV_NT3>(s, lane, slice_ptr, cols, vals, x, out);
+    else sell3_row_a<FEM_K1_U3, SPMV_NT3, FEM_K1_G3>(s, lane, slice_ptr, cols, vals, x, out);
 }
 
 template <int BS, int U = SPMV_U, bool NT = false, typename CI = int32_t>

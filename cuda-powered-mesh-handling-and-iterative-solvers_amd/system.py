@@ -357,9 +357,10 @@ class SellMatrix:
 
     # ---------------------------------------------------------------- solver
     def pcg(self, b, x0=None, w=None, mode=C.MODE_PCG, tol=1e-8, max_iter=1000, eps=1e-30, history=False,
-            chunk=32, fused=False, schedule=None, constraints=None):
+            chunk=32, fused=False, schedule=None, constraints=None, tune=None):
         """Run the device (P)CG; returns a PcgResult. `constraints` (a constraints.ConstraintSet, mode
-        CG_CONSTRAINED, 3-kernel schedule) is projected onto x at start and after every x update."""
+        CG_CONSTRAINED, 3-kernel schedule) is projected onto x at start and after every x update. `tune`: the
+        context's FEM_TUNE_* flags instead of the library default (A/B checks)."""
         lib = C.lib()
         b = b.to(device=self.device, dtype=F64).contiguous().view(-1)
         x = (torch.zeros(self.n, dtype=F64, device=self.device) if x0 is None
@@ -378,6 +379,8 @@ class SellMatrix:
         C.check(rc, "fem_pcg_create")
         try:
             C.check(lib.fem_pcg_set_schedule(h, _schedule(fused, schedule, self.bs)), "fem_pcg_set_schedule")
+            if tune is not None:
+                C.check(lib.fem_pcg_set_tuning(h, int(tune)), "fem_pcg_set_tuning")
             C.check(lib.fem_pcg_set_entries(h, self.g.sell_entries), "fem_pcg_set_entries")
             self.attach_cols16(h)
             if constraints is not None:

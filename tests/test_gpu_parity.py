@@ -14,6 +14,14 @@ E, NU = 113.8e9, 0.342
 F64 = torch.float64
 
 
+def CAPI():
+    from fem355 import _capi
+    return _capi
+
+
+C_MODE = {"cg": 0, "pcg": 1}
+
+
 def _mods():
     import fem355  # noqa: F401
     from fem355 import element, mesh, solver, system
@@ -766,6 +774,38 @@ def test_element_row_assembly_bit_identical_to_column_form(gpu, etype, n, rep, m
     monkeypatch.setenv("FEM355_KE_COLS", "1")
     b = system.SellMatrix(g, 3).add_element_matrices(K, tg).vals.clone()
     assert torch.equal(a, b), etype
+
+
+@pytest.mark.parametrize("kind,mode", [("elastic", "cg"), ("elastic", "pcg"), ("poisson", "pcg")])
+def test_merged_update_matches_two_kernel_update(gpu, kind, mode):
+    """3-kernel schedule: the merged r/z + x/p update (k_pcg_update2, FEM_TUNE_UPD1, default) against the two
+    vector kernels it replaces, on an odd number of dofs (the scalar tail), stable CG with its history and PCG: same
+    stop, iterations +-1, x 1e-12, the first 20 residual norms 1e-12 (p = z + beta p rounds z first, so the bits may
+    differ)."""
+    _, mesh, _, system = _mods()
+    c, t = mesh.kuhn_cube(10, jitter=0.1)        # 1,331 nodes: n odd for both kinds
+    N = c.shape[0]
+    if kind == "elastic":
+        f, fixed = mesh.cube_elasticity_case(c)
+        A = system.assemble_tet4_system(c.to(gpu), t.to(gpu), "elastic", E, NU)
+    else:
+        f, fixed = mesh.cube_poisson_case(c)
+        A = system.assemble_tet4_system(c.to(gpu), t.to(gpu), "poisson")
+    mask = torch.zeros((N, A.bs), dtype=torch.uint8, device=gpu)
+    mask[fixed.to(gpu)] = 1
+    w = A.jacobi(mask.view(-1))
+    if mode == "cg":
+        w = (w != 0).to(F64)   # CG_STABLE: w is the 0/1 free mask
+    md = C_MODE[mode]
+    b = f.reshape(-1).to(gpu, F64)
+    tol = 1e-9 * float(torch.linalg.norm(b))
+    runs = [A.pcg(b, w=w, mode=md, tol=tol, max_iter=5000, history=True, schedule=0, tune=tn)
+            for tn in (CAPI().TUNE_DEFAULT, CAPI().TUNE_DEFAULT & ~CAPI().TUNE_UPD1)]
+    a, o = runs
+    assert A.n % 2 == 1 and a.schedule == 0 and o.schedule == 0
+    assert a.status == o.status == CAPI().PCG_CONVERGED and abs(a.iterations - o.iterations) <= 1
+    assert rel(a.x, o.x) < 1e-12
+    assert rel(a.history[:20], o.history[:20]) < 1e-12
 
 
 def _helix_fan(m):
