@@ -54,10 +54,12 @@ SIGNATURES = {
     "fem_graph_tmp_len": (_L, [_L]),
     "fem_graph_count2": (_I, [_P, _I, _P, _P, _L, _P, _P, _P, _P]),
     "fem_graph_fill2": (_I, [_P, _I, _P, _P, _L, _P, _P, _P, _P, _P]),
+    "fem_graph_sell_fill": (_I, [_P, _I, _P, _P, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "fem_scan_i32": (_I, [_P, _L, _P, _P, _P]),
     "fem_scan_i64": (_I, [_P, _L, _P, _P, _P]),
     "fem_sell_widths": (_I, [_P, _L, _P, _P]),
     "fem_sell_fill": (_I, [_P, _P, _L, _P, _P, _P, _P]),
+    "fem_sell_csr2sell": (_I, [_P, _L, _P, _P, _P]),
     "fem_assemble_from_ke": (_I, [_P, _P, _I, _I, _P, _P, _L, _P, _P, _P, _P, _P, _P]),
     "fem_assemble_from_ke_ex": (_I, [_P, _P, _I, _I, _P, _P, _L, _P, _P, _P, _P, _L, _L, _I, _P, _P]),
     "fem_assemble_tet4": (_I, [_P, _P, _D, _D, _I, _P, _P, _L, _P, _P, _P, _P, _P, _P, _P]),

@@ -886,7 +886,7 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
     constexpr int B2 = BS * BS;
     constexpr int NI = R * J;
     constexpr int ND = BS == 1 ? 4 : 13;
-    static_assert(64 % R == 0 && NI % 256 == 0 || NI < 256, "items per batch");
+    static_assert(NI <= 256, "one item per thread per batch");
     static_assert(64 % R == 0 && R * LPR == 256 && 64 % LPR == 0, "tile geometry");
     __shared__ int ip_s[R + 1];
     __shared__ int rp_s[R + 1];
@@ -936,23 +936,44 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                                  : sell_val(e0 + (int64_t)(c0 + k) * 64 + l0 + r, B2, c)];
             acc_s[kc][r] = v;
         }
+        // software pipeline over the batches: a thread's next incidence entry is loaded before the current batch
+        // is swept and its element's node ids right after, so a batch waits only for its coordinates
+        const int ir = tid / J, ij = tid - (tid / J) * J;   // this thread's item: row ir, j-th element of the batch
+        int ea_n = 0;
+        bool v_n = false;
+        int64_t cn_n[4] = {0, 0, 0, 0};
+        if (tid < NI) {
+            const int t = ip_s[ir] + ij;
+            v_n = t < ip_s[ir + 1];
+            if (v_n) ea_n = inc[t];
+        }
+        if (v_n) {
+#pragma unroll
+            for (int b = 0; b < 4; ++b) cn_n[b] = conn[4 * (int64_t)(ea_n >> 2) + b];
+        }
         for (int j0 = 0; j0 < maxc; j0 += J) {
             __syncthreads();   // accumulators initialised / previous batch swept
-#pragma unroll
-            for (int i0 = 0; i0 < NI; i0 += 256) {
-                const int it0 = i0 + tid;
-                if (it0 >= NI) break;
-                const int r = it0 / J, jj = it0 - r * J;
-                const int t = ip_s[r] + j0 + jj;
+            const bool vcur = v_n;
+            const int eacur = ea_n;
+            const int64_t cncur[4] = {cn_n[0], cn_n[1], cn_n[2], cn_n[3]};
+            v_n = false;
+            if (tid < NI && j0 + J < maxc) {
+                const int t = ip_s[ir] + j0 + J + ij;
+                v_n = t < ip_s[ir + 1];
+                if (v_n) ea_n = inc[t];
+            }
+            {
+                const int it0 = tid;
+                const int r = ir;
                 uint32_t pk[2] = {0xffffffffu, 0xffffffffu};
                 uint8_t aflag = 0;
-                if (t < ip_s[r + 1]) {
-                    const int ea = inc[t];
+                if (tid < NI && vcur) {
+                    const int ea = eacur;
                     const int64_t e = ea >> 2;
                     const int a = ea & 3;
-                    const int64_t* c = conn + 4 * e;
+                    const int64_t* c = cncur;
                     double g[4][3];
-                    const double det = tet4_grads(X, c, g);
+                    const double det = tet4_grads_n(X, cncur, g);
                     if (c0 == 0 && fabs(det) < 1e-12) atomicMin((unsigned long long*)bad, (unsigned long long)e);
                     const double V = fabs(det) / 6.0;
                     const int cl = rp_s[r] - seg0, cn = rp_s[r + 1] - rp_s[r];
@@ -984,10 +1005,16 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                         dat_s[12][it0] = V;
                     }
                 }
-                pos_s[it0] = make_uint2(pk[0], pk[1]);
-                a_s[it0] = aflag;
+                if (tid < NI) {
+                    pos_s[it0] = make_uint2(pk[0], pk[1]);
+                    a_s[it0] = aflag;
+                }
             }
             __syncthreads();
+            if (v_n) {   // the next batch's element node ids (its incidence entry was loaded above)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) cn_n[b] = conn[4 * (int64_t)(ea_n >> 2) + b];
+            }
             // sweep: lanes of one row are consecutive lanes of one wave, in lockstep
             for (int jj = 0; jj < J; ++jj) {
                 const int it = lr * J + jj;
@@ -1226,8 +1253,10 @@ __global__ void k_sell_to_csr(const double* __restrict__ vals, const int32_t* __
         }
 }
 
-__global__ void k_jacobi(const double* __restrict__ vals, int bs, const int32_t* __restrict__ diagpos,
-                         const int64_t* __restrict__ csr2sell, int64_t nrows, const uint8_t* __restrict__ mask,
+// csr2sell == nullptr: the SELL entry of the diagonal from the slice pointer (slot dp - rowptr[node] of the row)
+__global__ void k_jacobi(const double* __restrict__ vals, int bs, const int32_t* __restrict__ rowptr,
+                         const int32_t* __restrict__ diagpos, const int64_t* __restrict__ csr2sell,
+                         const int64_t* __restrict__ slice_ptr, int64_t nrows, const uint8_t* __restrict__ mask,
                          double* __restrict__ w) {
     const int64_t n = nrows * bs;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -1235,7 +1264,10 @@ __global__ void k_jacobi(const double* __restrict__ vals, int bs, const int32_t*
         const int r = (int)(i - node * bs);
         // diagpos < 0: a node no element touches (diagonal 0 -> 1/0 = inf -> 0, `solver/solver.py:828-831`)
         const int32_t dp = diagpos[node];
-        const double dg = dp < 0 ? 0.0 : vals[sell_val(csr2sell[dp], bs * bs, r * bs + r)];
+        const int64_t E = dp < 0 ? 0
+                          : csr2sell ? csr2sell[dp]
+                                     : slice_ptr[node >> 6] + (int64_t)(dp - rowptr[node]) * 64 + (node & 63);
+        const double dg = dp < 0 ? 0.0 : vals[sell_val(E, bs * bs, r * bs + r)];
         double v = 1.0 / dg;
         if (v == INFINITY) v = 0.0;  // `solver/solver.py:831` (only +inf)
         if (mask && mask[i]) v = 0.0;
@@ -1510,6 +1542,10 @@ int fem_assemble_tet4_ex(const double* coords, const int64_t* conn, double E, do
     if (N <= 0) return FEM_OK;
     hipStream_t st = S(stream);
     if (getenv("FEM355_ASM_ROWS") != nullptr) {
+        if (!csr2sell) {
+            set_error("fem_assemble_tet4: the row kernels (FEM355_ASM_ROWS) need csr2sell");
+            return FEM_EARG;
+        }
         // wave per row (k_assemble_p1w / k_assemble_el3w, CSR-addressed through csr2sell; the tile kernel's bits):
         // kept as the reference formulation of the tile kernel's summation order
         if (store) {
@@ -1571,10 +1607,8 @@ int fem_sell_to_csr_vals(const double* vals, int bs, const int32_t* rowptr, int6
 
 int fem_jacobi(const double* vals, int bs, const int32_t* rowptr, const int32_t* diagpos, const int64_t* csr2sell,
                const int64_t* slice_ptr, int64_t nrows, const uint8_t* mask, double* w, fem_stream_t stream) {
-    (void)rowptr;
-    (void)slice_ptr;
-    hipLaunchKernelGGL(k_jacobi, dim3(stream_grid(nrows * bs, 256)), dim3(256), 0, S(stream), vals, bs, diagpos,
-                       csr2sell, nrows, mask, w);
+    hipLaunchKernelGGL(k_jacobi, dim3(stream_grid(nrows * bs, 256)), dim3(256), 0, S(stream), vals, bs, rowptr,
+                       diagpos, csr2sell, slice_ptr, nrows, mask, w);
     FEM_LAUNCHED();
     return FEM_OK;
 }

@@ -14,9 +14,9 @@ __host__ __device__ inline Lame lame(double E, double nu) {
     return Lame{c * nu, c * ((1.0 - 2.0 * nu) / 2.0)};
 }
 
-// gradients of the P1 shape functions (rows of inv([1 x y z]) 1..3) and signed det of the edge matrix
-__device__ __forceinline__ double tet4_grads(const double* __restrict__ X, const int64_t* __restrict__ c,
-                                             double g[4][3]) {
+// gradients of the P1 shape functions (rows of inv([1 x y z]) 1..3) and signed det of the edge matrix, from the
+// element's node ids (already loaded)
+__device__ __forceinline__ double tet4_grads_n(const double* __restrict__ X, const int64_t c[4], double g[4][3]) {
     double p[4][3];
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
@@ -44,6 +44,12 @@ __device__ __forceinline__ double tet4_grads(const double* __restrict__ X, const
         g[0][k] = -(g[1][k] + g[2][k] + g[3][k]);
     }
     return det;
+}
+
+__device__ __forceinline__ double tet4_grads(const double* __restrict__ X, const int64_t* __restrict__ c,
+                                             double g[4][3]) {
+    const int64_t n[4] = {c[0], c[1], c[2], c[3]};
+    return tet4_grads_n(X, n, g);
 }
 
 // inverse of a row-major 3x3 Jacobian (cofactors), returns det

@@ -92,12 +92,26 @@ __global__ void __launch_bounds__(256) k_graph_small(const int64_t* __restrict__
             continue;
         }
         const int hb = ht_bits(C, MAXB), HS = 1 << hb;
+        // all of the lane's candidates loaded before any insert (the incidence loads, then the connectivity loads,
+        // in flight together instead of one dependent pair per insert)
+        constexpr int CPL = (SCAP + LPN - 1) / LPN;
+        int cand[CPL];
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) {
+            const int t = sl + u * LPN;
+            cand[u] = t < C ? inc[start + t / npe] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) {
+            const int t = sl + u * LPN;
+            cand[u] = t < C ? (int)conn[(int64_t)(cand[u] / npe) * npe + (t - (t / npe) * npe)] : -1;
+        }
         for (int q = sl; q < HS; q += LPN) tab[q] = -1;
         __builtin_amdgcn_wave_barrier();
-        for (int t = sl; t < C; t += LPN) {
-            const int k = t / npe, b = t - k * npe;
-            const int e = inc[start + k] / npe;
-            const int v = (int)conn[(int64_t)e * npe + b];
+#pragma unroll
+        for (int u = 0; u < CPL; ++u) {
+            const int v = cand[u];
+            if (v < 0) continue;
             unsigned h = ((unsigned)v * 2654435761u) >> (32 - hb);
             while (true) {
                 const int old = atomicCAS(&tab[h], -1, v);
@@ -339,6 +353,102 @@ __global__ void __launch_bounds__(256) k_sell_fill(const int32_t* __restrict__ r
     }
 }
 
+// The SELL-64 pattern straight from the graph kernels' rows, one wave per slice (fem_graph_fill2 + fem_sell_fill +
+// fem_sell_delta16 in one pass). Lane = row: column slot k of the 64 rows is one contiguous store of cols and of the
+// 16-bit deltas; a row comes from k_graph_small's tmp (32 slots per node) or, for the rows it deferred, from colidx
+// (already filled by k_graph / k_graph_big). Lane = CSR position of the slice's contiguous segment: csr2sell, and
+// colidx of the tmp rows, written contiguously (the row of a position by binary search over the slice's row starts).
+__global__ void __launch_bounds__(256) k_sell_fill_graph(const int32_t* __restrict__ rowptr,
+                                                         const int32_t* __restrict__ tmp,
+                                                         const uint8_t* __restrict__ defer, int64_t nrows,
+                                                         int64_t nslices, const int64_t* __restrict__ slice_ptr,
+                                                         int32_t* __restrict__ colidx, int32_t* __restrict__ diagpos,
+                                                         int32_t* __restrict__ cols, int16_t* __restrict__ dcols,
+                                                         int64_t* __restrict__ csr2sell, int32_t* __restrict__ overflow) {
+    __shared__ int32_t rp_s[4][65];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int64_t s = (int64_t)blockIdx.x * 4 + wid; s < nslices; s += (int64_t)gridDim.x * 4) {
+        const int64_t r = s * 64 + lane;
+        const int64_t e0 = slice_ptr[s];
+        const int w = (int)((slice_ptr[s + 1] - e0) >> 6);
+        const int64_t rlast = min(s * 64 + 64, nrows);
+        rp_s[wid][lane] = rowptr[min(r, rlast)];
+        if (lane == 0) rp_s[wid][64] = rowptr[rlast];
+        __builtin_amdgcn_wave_barrier();
+        int len = 0, rp = 0;
+        bool dfr = true;
+        if (r < nrows) {
+            rp = rp_s[wid][lane];
+            len = rp_s[wid][lane + 1] - rp;
+            dfr = defer[r] != 0;
+        }
+        const int32_t* src = dfr ? colidx + rp : tmp + r * G_TCAP;
+        const int pad = (r < nrows) ? (int)r : (int)(nrows - 1);   // near the row: 16-bit deltas stay small
+        bool far = false;
+        for (int k0 = 0; k0 < w; k0 += 8) {
+            int cv[8];   // the row's next 8 columns loaded before any store (src may alias nothing written here,
+                         // but the compiler cannot know: without the staging every load waits for the stores)
+#pragma unroll
+            for (int u = 0; u < 8; ++u) cv[u] = (k0 + u < len) ? src[k0 + u] : pad;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int k = k0 + u;
+                if (k >= w) break;
+                const int c = cv[u];
+                const int64_t e = e0 + (int64_t)k * 64 + lane;
+                cols[e] = c;
+                const int64_t d = (int64_t)c - r;
+                const bool f = d > 32767 || d < -32767;
+                far |= f;
+                dcols[e] = f ? (int16_t)0 : (int16_t)d;
+                if (k < len && c == (int)r) diagpos[r] = rp + k;
+            }
+        }
+        if (__ballot(far) && lane == 0 && !*overflow) atomicOr(overflow, 1);
+        const int p0 = rp_s[wid][0], p1 = rp_s[wid][64];
+        for (int p = p0 + lane; p < p1; p += 64) {
+            int lo = 0, hi = 64;   // last row l with rp_s[l] <= p
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (rp_s[wid][mid] <= p) lo = mid;
+                else hi = mid;
+            }
+            const int k = p - rp_s[wid][lo];
+            if (csr2sell) csr2sell[p] = e0 + (int64_t)k * 64 + lo;
+            const int64_t row = s * 64 + lo;
+            if (!defer[row]) colidx[p] = tmp[row * G_TCAP + k];
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// csr2sell of a SELL pattern from its row and slice pointers alone (wave per slice; the map fem_sell_fill writes)
+__global__ void __launch_bounds__(256) k_sell_csr2sell(const int32_t* __restrict__ rowptr, int64_t nrows,
+                                                       int64_t nslices, const int64_t* __restrict__ slice_ptr,
+                                                       int64_t* __restrict__ csr2sell) {
+    __shared__ int32_t rp_s[4][65];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int64_t s = (int64_t)blockIdx.x * 4 + wid; s < nslices; s += (int64_t)gridDim.x * 4) {
+        const int64_t r = s * 64 + lane;
+        const int64_t e0 = slice_ptr[s];
+        const int64_t rlast = min(s * 64 + 64, nrows);
+        rp_s[wid][lane] = rowptr[min(r, rlast)];
+        if (lane == 0) rp_s[wid][64] = rowptr[rlast];
+        __builtin_amdgcn_wave_barrier();
+        const int p0 = rp_s[wid][0], p1 = rp_s[wid][64];
+        for (int p = p0 + lane; p < p1; p += 64) {
+            int lo = 0, hi = 64;
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (rp_s[wid][mid] <= p) lo = mid;
+                else hi = mid;
+            }
+            csr2sell[p] = e0 + (int64_t)(p - rp_s[wid][lo]) * 64 + lo;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // 16-bit column deltas (col - row) of the SELL pattern; *overflow = 1 if any |delta| > 32767 (keep int32 then)
 __global__ void k_sell_delta16(const int32_t* __restrict__ cols, int64_t nslices, const int64_t* __restrict__ slice_ptr,
                                int16_t* __restrict__ dcols, int32_t* __restrict__ overflow) {
@@ -499,6 +609,25 @@ int fem_graph_fill2(const int64_t* conn, int npe, const int32_t* inc_ptr, const 
     return graph_fill(conn, npe, inc_ptr, inc, N, rowptr, colidx, diagpos, defer_flags(tmp, N), S(stream));
 }
 
+int fem_graph_sell_fill(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
+                        const int32_t* rowptr, const int32_t* tmp, const int64_t* slice_ptr, int32_t* colidx,
+                        int32_t* diagpos, int32_t* cols, int16_t* dcols, int64_t* csr2sell, int32_t* overflow,
+                        fem_stream_t stream) {
+    if (N <= 0) return FEM_OK;
+    hipStream_t st = S(stream);
+    FEM_HIP(hipMemsetAsync(diagpos, 0xff, sizeof(int32_t) * (size_t)N, st));   // -1: no diagonal
+    FEM_HIP(hipMemsetAsync(overflow, 0, sizeof(int32_t), st));
+    // rows k_graph_small deferred: straight into colidx / diagpos (k_graph, k_graph_big), before the slice pass
+    const int rc = graph_fill(conn, npe, inc_ptr, inc, N, rowptr, colidx, diagpos, defer_flags(tmp, N), st);
+    if (rc != FEM_OK) return rc;
+    const int64_t ns = cdiv(N, 64);
+    hipLaunchKernelGGL(k_sell_fill_graph, dim3((unsigned)std::min<int64_t>(cdiv(ns, 4), 16384)), dim3(256), 0, st,
+                       rowptr, tmp, defer_flags(tmp, N), N, ns, slice_ptr, colidx, diagpos, cols, dcols, csr2sell,
+                       overflow);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
 int fem_graph_fill(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
                    const int32_t* rowptr, int32_t* colidx, int32_t* diagpos, fem_stream_t stream) {
     if (N <= 0) return FEM_OK;
@@ -511,6 +640,16 @@ int fem_sell_delta16(const int32_t* cols, int64_t nrows, const int64_t* slice_pt
     int64_t ns = cdiv(nrows, 64);
     hipLaunchKernelGGL(k_sell_delta16, dim3(stream_grid(ns * 64, 256)), dim3(256), 0, S(stream), cols, ns, slice_ptr,
                        dcols, overflow);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_sell_csr2sell(const int32_t* rowptr, int64_t nrows, const int64_t* slice_ptr, int64_t* csr2sell,
+                      fem_stream_t stream) {
+    const int64_t ns = cdiv(nrows, 64);
+    if (ns == 0) return FEM_OK;
+    hipLaunchKernelGGL(k_sell_csr2sell, dim3((unsigned)std::min<int64_t>(cdiv(ns, 4), 16384)), dim3(256), 0,
+                       S(stream), rowptr, nrows, ns, slice_ptr, csr2sell);
     FEM_LAUNCHED();
     return FEM_OK;
 }

@@ -8,6 +8,7 @@ the coalesced COO of `subdivision.ipynb:118-139`, so `A @ p == compute_nodal_for
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import torch
@@ -88,8 +89,21 @@ class Graph:
     diagpos: torch.Tensor
     slice_ptr: torch.Tensor
     cols: torch.Tensor
-    csr2sell: torch.Tensor
+    c2s: torch.Tensor = None     # CSR -> SELL entry map, formed on first use (csr2sell)
     dcols: torch.Tensor = None   # int16 col - row deltas, or None when the bandwidth exceeds 32767
+
+    @property
+    def csr2sell(self):
+        """CSR position -> SELL entry (int64 [nnz]). The fused pattern pass skips it (the c3d4 assembly, Jacobi and
+        the solvers address SELL through the slice pointer); the stored-K_e assembly and the CSR export form it
+        here on first use, on the graph's device and current stream."""
+        if self.c2s is None:
+            with C.device_scope(self.rowptr.device):
+                c2s = torch.empty(max(self.nnz, 1), dtype=I64, device=self.rowptr.device)
+                C.check(C.lib().fem_sell_csr2sell(C.ptr(self.rowptr), self.n_nodes, C.ptr(self.slice_ptr),
+                                                  C.ptr(c2s), C.stream(self.rowptr.device)), "fem_sell_csr2sell")
+                self.c2s = c2s
+        return self.c2s
 
     @property
     def nnz(self):
@@ -178,21 +192,16 @@ def _build_graph(elements, n_nodes, compress):
                          "(split the mesh over GPUs)")
     colidx = torch.empty(nnz, dtype=I32, device=dev)
     diagpos = torch.empty(n_nodes, dtype=I32, device=dev)
-    C.check(lib.fem_graph_fill2(C.ptr(elements), npe, C.ptr(inc_ptr), C.ptr(inc), n_nodes, C.ptr(rowptr), C.ptr(tmp),
-                                C.ptr(colidx), C.ptr(diagpos), st), "fem_graph_fill2")
-    del tmp
     cols = torch.empty(ent, dtype=I32, device=dev)
-    csr2sell = torch.empty(max(nnz, 1), dtype=I64, device=dev)
-    C.check(lib.fem_sell_fill(C.ptr(rowptr), C.ptr(colidx), n_nodes, C.ptr(slice_ptr), C.ptr(cols),
-                              C.ptr(csr2sell), st), "fem_sell_fill")
-    g = Graph(n_nodes, npe, inc_ptr, inc, rowptr, colidx, diagpos, slice_ptr, cols, csr2sell)
-    if compress:
-        dcols = torch.empty(max(ent, 1), dtype=torch.int16, device=dev)
-        ovf = torch.zeros(1, dtype=I32, device=dev)
-        C.check(lib.fem_sell_delta16(C.ptr(cols), n_nodes, C.ptr(slice_ptr), C.ptr(dcols), C.ptr(ovf), st),
-                "fem_sell_delta16")
-        if int(ovf.item()) == 0:
-            g.dcols = dcols
+    dcols = torch.empty(max(ent, 1), dtype=torch.int16, device=dev)
+    ovf = torch.empty(1, dtype=I32, device=dev)
+    C.check(lib.fem_graph_sell_fill(C.ptr(elements), npe, C.ptr(inc_ptr), C.ptr(inc), n_nodes, C.ptr(rowptr),
+                                    C.ptr(tmp), C.ptr(slice_ptr), C.ptr(colidx), C.ptr(diagpos), C.ptr(cols),
+                                    C.ptr(dcols), None, C.ptr(ovf), st), "fem_graph_sell_fill")
+    del tmp
+    g = Graph(n_nodes, npe, inc_ptr, inc, rowptr, colidx, diagpos, slice_ptr, cols)
+    if compress and int(ovf.item()) == 0:
+        g.dcols = dcols
     return g
 
 
@@ -298,7 +307,8 @@ class SellMatrix:
         self._fresh = False
         C.check(lib.fem_assemble_tet4_ex(C.ptr(coords), C.ptr(elements), float(E), float(nu), self.bs,
                                          C.ptr(self.g.inc_ptr), C.ptr(self.g.inc), self.g.n_nodes,
-                                         C.ptr(self.g.rowptr), C.ptr(self.g.colidx), C.ptr(self.g.csr2sell),
+                                         C.ptr(self.g.rowptr), C.ptr(self.g.colidx),
+                                         C.ptr(self.g.csr2sell) if os.environ.get("FEM355_ASM_ROWS") else None,
                                          C.ptr(self.g.slice_ptr), 1 if store else 0, C.ptr(self._vals), C.ptr(bad),
                                          C.stream(self.device)), "fem_assemble_tet4_ex")
         self._bad = (bad, elements.shape[0])
@@ -332,7 +342,7 @@ class SellMatrix:
         lib = C.lib()
         w = torch.empty(self.n, dtype=F64, device=self.device)
         C.check(lib.fem_jacobi(C.ptr(self.vals), self.bs, C.ptr(self.g.rowptr), C.ptr(self.g.diagpos),
-                               C.ptr(self.g.csr2sell), C.ptr(self.g.slice_ptr), self.g.n_nodes,
+                               None, C.ptr(self.g.slice_ptr), self.g.n_nodes,
                                C.ptr(fixed_mask), C.ptr(w), C.stream(self.device)), "fem_jacobi")
         return w
 

@@ -139,6 +139,14 @@ int fem_graph_count2(const int64_t* conn, int npe, const int32_t* inc_ptr, const
 int fem_graph_fill2(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
                     const int32_t* rowptr, const int32_t* tmp, int32_t* colidx, int32_t* diagpos,
                     fem_stream_t stream);
+/* fem_graph_fill2 + fem_sell_fill + fem_sell_delta16 in one pass over the slices (slice_ptr from fem_sell_widths +
+ * fem_scan_i64): colidx, diagpos, SELL cols, the 16-bit deltas dcols [slice_ptr[S]] (0 where they do not fit,
+ * *overflow [device int] = 1 then: keep the int32 cols) and csr2sell (may be NULL: fem_sell_csr2sell forms it on
+ * demand) -- the same arrays as the three calls. */
+int fem_graph_sell_fill(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
+                        const int32_t* rowptr, const int32_t* tmp, const int64_t* slice_ptr, int32_t* colidx,
+                        int32_t* diagpos, int32_t* cols, int16_t* dcols, int64_t* csr2sell, int32_t* overflow,
+                        fem_stream_t stream);
 /* exclusive scan of int32 counts -> out[n+1] (out[n] = total); work: int32 [fem_scan_work_len(n)] */
 int fem_scan_i32(const int32_t* in, int64_t n, int32_t* out, int32_t* work, fem_stream_t stream);
 
@@ -146,6 +154,9 @@ int fem_scan_i32(const int32_t* in, int64_t n, int32_t* out, int32_t* work, fem_
  *   fem_sell_widths: width [S] int64 = 64 * max row length in the slice (scan it with fem_scan_i64)
  *   fem_sell_fill  : cols (padding = own row) and the CSR->SELL entry map csr2sell [nnz] int64 */
 int fem_sell_widths(const int32_t* rowptr, int64_t nrows, int64_t* width, fem_stream_t stream);
+/* the CSR -> SELL entry map (as fem_sell_fill writes it) from rowptr and slice_ptr alone */
+int fem_sell_csr2sell(const int32_t* rowptr, int64_t nrows, const int64_t* slice_ptr, int64_t* csr2sell,
+                      fem_stream_t stream);
 int fem_scan_i64(const int64_t* in, int64_t n, int64_t* out, int64_t* work, fem_stream_t stream);
 int fem_sell_fill(const int32_t* rowptr, const int32_t* colidx, int64_t nrows, const int64_t* slice_ptr,
                   int32_t* cols, int64_t* csr2sell, fem_stream_t stream);
@@ -197,7 +208,8 @@ int fem_sell_to_csr_vals(const double* vals, int bs, const int32_t* rowptr, int6
                          fem_stream_t stream);
 
 /* Jacobi: w[i] = 1/A_ii (inf -> 0, `solver/solver.py:830-831`), w[i] = 0 where mask[i] != 0 (fixed DOFs);
- * mask may be NULL. diag read through diagpos (diagpos < 0: diagonal 0, so w = 0 as the reference's inf -> 0). */
+ * mask may be NULL. diag read through diagpos (diagpos < 0: diagonal 0, so w = 0 as the reference's inf -> 0);
+ * csr2sell may be NULL (the diagonal's SELL entry is then formed from rowptr and slice_ptr). */
 int fem_jacobi(const double* vals, int bs, const int32_t* rowptr, const int32_t* diagpos,
                const int64_t* csr2sell, const int64_t* slice_ptr, int64_t nrows, const uint8_t* mask,
                double* w, fem_stream_t stream);
