@@ -3320,7 +3320,9 @@ int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, 
     }
     const bool may_persist = s->persist_req && (s->bs == 1 || s->bs == 3) && !s->dist &&
                              s->mode != FEM_MODE_CG_CONSTRAINED;
-    if (may_persist) {
+    // the merged update (k_pcg_update2) waits on every workgroup of its grid as well: same recovery
+    const bool may_upd = (s->tune & FEM_TUNE_UPD1) && !s->dist && s->mode != FEM_MODE_CG_CONSTRAINED;
+    if (may_persist || may_upd) {
         FEM_HIP(pool_alloc((void**)&x0, sizeof(double) * (size_t)(s->n + 2), s->stream, true));
         FEM_HIP(hipMemcpyAsync(x0, s->x, sizeof(double) * (size_t)s->n, hipMemcpyDeviceToDevice, s->stream));
     }
@@ -3337,9 +3339,12 @@ int fem_pcg_solve(fem_pcg* s, int max_iter, int chunk, int* iters, int* status, 
     if (!rc && stt == FEM_PCG_SYNC_TIMEOUT && x0) {
         rc = hipMemcpyAsync(s->x, x0, sizeof(double) * (size_t)s->n, hipMemcpyDeviceToDevice, s->stream) == hipSuccess
                  ? FEM_OK : FEM_EHIP;
+        const int req0 = s->persist_req, tune0 = s->tune;
         s->persist_req = 0;   // fem_pcg_start now sets up the deferred schedule (set_schedule(3) implied deferred)
+        s->tune &= ~FEM_TUNE_UPD1;   // and the two-kernel update
         if (!rc) rc = pcg_solve_once(s, max_iter, chunk, &it, &stt, rz);
-        s->persist_req = 1;
+        s->persist_req = req0;
+        s->tune = tune0;
     }
     pool_free(x0, s->stream);
     if (rc) return rc;

@@ -143,6 +143,32 @@ def test_pattern_bit_exact_vs_oracle(gpu):
         assert torch.equal(t.reshape(-1)[inc], seg)                               # entry belongs to its node
 
 
+def test_incidence_bucket_sort_equals_radix_sort(gpu, monkeypatch):
+    """The incidence by the two-level bucket sort (default) is the radix sort's (FEM355_INC_RADIX) entry for entry:
+    a randomly numbered cube, c3d10 elements repeated 9 times (buckets past the LDS capacity: the global path), a
+    700-tet fan (one node in every element) and a mesh with unused nodes."""
+    _, mesh, _, system = _mods()
+    c, t = mesh.kuhn_cube(9)
+    perm = torch.randperm(c.shape[0], generator=torch.Generator().manual_seed(2))
+    inv = torch.empty_like(perm)
+    inv[perm] = torch.arange(perm.numel())
+    _, t10 = mesh.tet10_cube(3)
+    a = torch.arange(1, 701)
+    fan = torch.stack([torch.zeros_like(a), a, a + 1, a + 2], 1)
+    cases = [(inv[t], c.shape[0]), (t10.repeat(9, 1), int(t10.max()) + 1), (fan, 703), (t + 5, c.shape[0] + 9)]
+    for el, N in cases:
+        eg = el.to(gpu).contiguous()
+        monkeypatch.delenv("FEM355_INC_RADIX", raising=False)
+        ip1, in1 = system.incidence(eg, N)
+        monkeypatch.setenv("FEM355_INC_RADIX", "1")
+        ip2, in2 = system.incidence(eg, N)
+        monkeypatch.delenv("FEM355_INC_RADIX", raising=False)
+        assert torch.equal(ip1, ip2) and torch.equal(in1, in2), (el.shape, N)
+    bad = torch.tensor([[0, 1, 2, 3], [1, 2, 3, 9]])
+    with pytest.raises(IndexError):
+        system.build_graph(bad.to(gpu), 5)
+
+
 def test_pattern_wide_rows_vs_oracle(gpu):
     """Rows past every LDS tier: > 2048 candidates (c3d10 x9 repeats, hash tier) and > 512 unique neighbours
     (a fan of 700 tets around node 0, selection tier); bit-exact against the oracle, also through the CSR C-ABI."""
