@@ -275,7 +275,7 @@ __global__ void __launch_bounds__(256) k_graph_small(const int64_t* __restrict__
                                                      const int32_t* __restrict__ inc_ptr,
                                                      const int32_t* __restrict__ inc, int64_t N,
                                                      int32_t* __restrict__ row_len, int32_t* __restrict__ tmp,
-                                                     uint8_t* __restrict__ defer) {
+                                                     uint8_t* __restrict__ defer, int32_t* __restrict__ far) {
     constexpr int NPW = 64 / LPN;                 // nodes per wave
     constexpr int HTS = G_HT / NPW;               // table slots per node
     constexpr int SCAP = G_SCAP * LPN / 64;       // candidates per node (load <= 3/4 of the table)
@@ -312,6 +312,12 @@ __global__ void __launch_bounds__(256) k_graph_small(const int64_t* __restrict__
         for (int u = 0; u < CPL; ++u) {
             const int t = sl + u * LPN;
             cand[u] = t < C ? (int)conn[(int64_t)(cand[u] / npe) * npe + (t - (t / npe) * npe)] : -1;
+        }
+        if (far) {   // a neighbour farther than 16-bit deltas reach (the SELL keeps int32 columns then)
+            bool f = false;
+#pragma unroll
+            for (int u = 0; u < CPL; ++u) f |= cand[u] >= 0 && (cand[u] - node > 32767 || node - cand[u] > 32767);
+            if (__ballot(f) && lane == 0 && !*far) atomicOr(far, 1);
         }
         for (int q = sl; q < HS; q += LPN) tab[q] = -1;
         __builtin_amdgcn_wave_barrier();
@@ -385,7 +391,8 @@ __global__ void __launch_bounds__(256) k_graph(const int64_t* __restrict__ conn,
                                                const int32_t* __restrict__ inc_ptr, const int32_t* __restrict__ inc,
                                                int64_t N, int32_t* __restrict__ row_len,
                                                const int32_t* __restrict__ rowptr, int32_t* __restrict__ colidx,
-                                               int32_t* __restrict__ diagpos, const uint8_t* __restrict__ defer) {
+                                               int32_t* __restrict__ diagpos, const uint8_t* __restrict__ defer,
+                                               int32_t* __restrict__ far) {
     __shared__ int ht[G_WAVES][G_HT2];
     __shared__ int uniq[G_WAVES][G_UCAP];
     __shared__ int cnt_s[G_WAVES];
@@ -416,6 +423,7 @@ __global__ void __launch_bounds__(256) k_graph(const int64_t* __restrict__ conn,
                 const int k = t / npe, b = t - k * npe;
                 const int e = inc[start + k] / npe;
                 const int v = (int)conn[(int64_t)e * npe + b];
+                if (!FILL && far && (v - node > 32767 || node - v > 32767) && !*far) atomicOr(far, 1);
                 unsigned h = ((unsigned)v * 2654435761u) >> (32 - hb);
                 while (true) {
                     const int old = atomicCAS(&ht[wid][h], -1, v);
@@ -474,7 +482,8 @@ __global__ void __launch_bounds__(256) k_graph_big(const int64_t* __restrict__ c
                                                    const int32_t* __restrict__ inc_ptr,
                                                    const int32_t* __restrict__ inc, int64_t N,
                                                    int32_t* __restrict__ row_len, const int32_t* __restrict__ rowptr,
-                                                   int32_t* __restrict__ colidx, int32_t* __restrict__ diagpos) {
+                                                   int32_t* __restrict__ colidx, int32_t* __restrict__ diagpos,
+                                                   int32_t* __restrict__ far) {
     const int wid = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     for (int64_t base = ((int64_t)blockIdx.x * G_WAVES + wid) * 64; base < N;
@@ -498,6 +507,8 @@ __global__ void __launch_bounds__(256) k_graph_big(const int64_t* __restrict__ c
                 }
                 best = wave_min_i32(best);
                 if (best == INT_MAX) break;
+                if (!FILL && far && lane == 0 && (best - node > 32767 || node - best > 32767) && !*far)
+                    atomicOr(far, 1);
                 if (FILL && lane == 0) {
                     colidx[rp + U] = best;
                     if (best == (int)node) diagpos[node] = rp + U;
@@ -607,11 +618,11 @@ __global__ void __launch_bounds__(256) k_sell_fill_graph(const int32_t* __restri
                 const int64_t d = (int64_t)c - r;
                 const bool f = d > 32767 || d < -32767;
                 far |= f;
-                dcols[e] = f ? (int16_t)0 : (int16_t)d;
+                if (dcols) dcols[e] = f ? (int16_t)0 : (int16_t)d;
                 if (k < len && c == (int)r) diagpos[r] = rp + k;
             }
         }
-        if (__ballot(far) && lane == 0 && !*overflow) atomicOr(overflow, 1);
+        if (overflow && __ballot(far) && lane == 0 && !*overflow) atomicOr(overflow, 1);
         const int p0 = rp_s[wid][0], p1 = rp_s[wid][64];
         for (int p = p0 + lane; p < p1; p += 64) {
             int lo = 0, hi = 64;   // last row l with rp_s[l] <= p
@@ -800,16 +811,15 @@ static int big_grid(int64_t N) {
 }
 
 // count: k_graph for every row (done = null) or for the rows k_graph_small left, then k_graph_big for the rows
-// k_graph flagged; row_len ends exact for every node. *overflow is kept for ABI compatibility and set to 0 (no
-// capacity limit remains).
+// k_graph flagged; row_len ends exact for every node. *overflow (zeroed by the caller's entry point): 1 if some
+// row has a neighbour farther than 32767 rows (the SELL pattern then keeps int32 columns).
 static int graph_count(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
                        int32_t* row_len, const uint8_t* defer, int32_t* overflow, hipStream_t st) {
-    if (overflow) FEM_HIP(hipMemsetAsync(overflow, 0, sizeof(int32_t), st));
     hipLaunchKernelGGL(k_graph<false>, dim3(graph_grid(N)), dim3(256), 0, st, conn, npe, inc_ptr, inc, N, row_len,
-                       (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, defer);
+                       (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, defer, overflow);
     FEM_LAUNCHED();
     hipLaunchKernelGGL(k_graph_big<false>, dim3(big_grid(N)), dim3(256), 0, st, conn, npe, inc_ptr, inc, N, row_len,
-                       (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr);
+                       (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, overflow);
     FEM_LAUNCHED();
     return FEM_OK;
 }
@@ -817,16 +827,17 @@ static int graph_count(const int64_t* conn, int npe, const int32_t* inc_ptr, con
 static int graph_fill(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
                       const int32_t* rowptr, int32_t* colidx, int32_t* diagpos, const uint8_t* defer, hipStream_t st) {
     hipLaunchKernelGGL(k_graph<true>, dim3(graph_grid(N)), dim3(256), 0, st, conn, npe, inc_ptr, inc, N,
-                       (int32_t*)nullptr, rowptr, colidx, diagpos, defer);
+                       (int32_t*)nullptr, rowptr, colidx, diagpos, defer, (int32_t*)nullptr);
     FEM_LAUNCHED();
     hipLaunchKernelGGL(k_graph_big<true>, dim3(big_grid(N)), dim3(256), 0, st, conn, npe, inc_ptr, inc, N,
-                       (int32_t*)nullptr, rowptr, colidx, diagpos);
+                       (int32_t*)nullptr, rowptr, colidx, diagpos, (int32_t*)nullptr);
     FEM_LAUNCHED();
     return FEM_OK;
 }
 
 int fem_graph_count(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
                     int32_t* row_len, int32_t* overflow, fem_stream_t stream) {
+    if (overflow) FEM_HIP(hipMemsetAsync(overflow, 0, sizeof(int32_t), S(stream)));
     if (N <= 0) return FEM_OK;
     return graph_count(conn, npe, inc_ptr, inc, N, row_len, nullptr, overflow, S(stream));
 }
@@ -840,10 +851,11 @@ static const uint8_t* defer_flags(const int32_t* tmp, int64_t N) {
 
 int fem_graph_count2(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
                      int32_t* row_len, int32_t* tmp, int32_t* overflow, fem_stream_t stream) {
+    if (overflow) FEM_HIP(hipMemsetAsync(overflow, 0, sizeof(int32_t), S(stream)));
     if (N <= 0) return FEM_OK;
     const int64_t grid = std::min<int64_t>(cdiv(N, G_WAVES), 16384);
     hipLaunchKernelGGL(k_graph_small<FEM_GRAPH_LPN>, dim3((unsigned)grid), dim3(256), 0, S(stream), conn, npe, inc_ptr, inc, N,
-                       row_len, tmp, defer_flags(tmp, N));
+                       row_len, tmp, defer_flags(tmp, N), overflow);
     FEM_LAUNCHED();
     return graph_count(conn, npe, inc_ptr, inc, N, row_len, defer_flags(tmp, N), overflow, S(stream));
 }
@@ -868,7 +880,7 @@ int fem_graph_sell_fill(const int64_t* conn, int npe, const int32_t* inc_ptr, co
     if (N <= 0) return FEM_OK;
     hipStream_t st = S(stream);
     FEM_HIP(hipMemsetAsync(diagpos, 0xff, sizeof(int32_t) * (size_t)N, st));   // -1: no diagonal
-    FEM_HIP(hipMemsetAsync(overflow, 0, sizeof(int32_t), st));
+    if (overflow) FEM_HIP(hipMemsetAsync(overflow, 0, sizeof(int32_t), st));
     // rows k_graph_small deferred: straight into colidx / diagpos (k_graph, k_graph_big), before the slice pass
     const int rc = graph_fill(conn, npe, inc_ptr, inc, N, rowptr, colidx, diagpos, defer_flags(tmp, N), st);
     if (rc != FEM_OK) return rc;

@@ -170,8 +170,9 @@ def _build_graph(elements, n_nodes, compress):
     del work
     row_len = torch.empty(n_nodes, dtype=I32, device=dev)
     tmp = torch.empty(max(int(lib.fem_graph_tmp_len(n_nodes)), 1), dtype=I32, device=dev)
+    ovf = torch.empty(1, dtype=I32, device=dev)   # 1: some neighbour is > 32767 rows away (no 16-bit deltas)
     C.check(lib.fem_graph_count2(C.ptr(elements), npe, C.ptr(inc_ptr), C.ptr(inc), n_nodes, C.ptr(row_len),
-                                 C.ptr(tmp), None, st), "fem_graph_count2")
+                                 C.ptr(tmp), C.ptr(ovf), st), "fem_graph_count2")
     rowptr = torch.empty(n_nodes + 1, dtype=I32, device=dev)
     work = torch.empty(int(lib.fem_scan_work_len(n_nodes)) + 1, dtype=I32, device=dev)
     C.check(lib.fem_scan_i32(C.ptr(row_len), n_nodes, C.ptr(rowptr), C.ptr(work), st), "fem_scan_i32")
@@ -182,7 +183,8 @@ def _build_graph(elements, n_nodes, compress):
     slice_ptr = torch.empty(ns + 1, dtype=I64, device=dev)
     work64 = torch.empty(int(lib.fem_scan_work_len(ns)) + 1, dtype=I64, device=dev)
     C.check(lib.fem_scan_i64(C.ptr(width), ns, C.ptr(slice_ptr), C.ptr(work64), st), "fem_scan_i64")
-    nnz, ent, nbad = (int(v) for v in torch.stack([rowptr[-1].to(I64), slice_ptr[-1], bad[0].to(I64)]).cpu())
+    nnz, ent, nbad, far = (int(v) for v in torch.stack([rowptr[-1].to(I64), slice_ptr[-1], bad[0].to(I64),
+                                                          ovf[0].to(I64)]).cpu())
     if nbad:   # the sync of the build; the message names the offending node like check_connectivity
         check_connectivity(elements, n_nodes)
     # int32 row pointers / column slots: the int32 scan would wrap past 2^31 entries; the int64 slice scan cannot
@@ -193,15 +195,13 @@ def _build_graph(elements, n_nodes, compress):
     colidx = torch.empty(nnz, dtype=I32, device=dev)
     diagpos = torch.empty(n_nodes, dtype=I32, device=dev)
     cols = torch.empty(ent, dtype=I32, device=dev)
-    dcols = torch.empty(max(ent, 1), dtype=torch.int16, device=dev)
-    ovf = torch.empty(1, dtype=I32, device=dev)
+    dcols = torch.empty(max(ent, 1), dtype=torch.int16, device=dev) if compress and not far else None
     C.check(lib.fem_graph_sell_fill(C.ptr(elements), npe, C.ptr(inc_ptr), C.ptr(inc), n_nodes, C.ptr(rowptr),
                                     C.ptr(tmp), C.ptr(slice_ptr), C.ptr(colidx), C.ptr(diagpos), C.ptr(cols),
-                                    C.ptr(dcols), None, C.ptr(ovf), st), "fem_graph_sell_fill")
+                                    C.ptr(dcols), None, None, st), "fem_graph_sell_fill")
     del tmp
     g = Graph(n_nodes, npe, inc_ptr, inc, rowptr, colidx, diagpos, slice_ptr, cols)
-    if compress and int(ovf.item()) == 0:
-        g.dcols = dcols
+    g.dcols = dcols
     return g
 
 

@@ -122,8 +122,9 @@ int fem_incidence_checked(const int64_t* conn, int64_t M, int npe, int64_t N, in
 
 /* Node-graph CSR pattern (block pattern for any dpn): the coalesced COO pattern of the reference's global
  * assembly (`subdivision.ipynb:118-139`) at node granularity. Two passes:
- *   fem_graph_count : row_len [N]  (unique neighbours incl. self); *overflow [device int] is written 0 (kept
- *                     for ABI stability: rows of any length are handled, the widest by a selection kernel)
+ *   fem_graph_count : row_len [N]  (unique neighbours incl. self; rows of any length, the widest by a selection
+ *                     kernel); *overflow [device int, may be NULL] = 1 if some row has a neighbour more than 32767
+ *                     rows away (16-bit column deltas do not fit), else 0
  *   fem_graph_fill  : colidx [nnz] sorted per row, diagpos [N] (position of the diagonal; -1 for a node no element touches)
  * rowptr [N+1] is the exclusive scan of row_len (fem_scan_i32). */
 int fem_graph_count(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
@@ -142,7 +143,8 @@ int fem_graph_fill2(const int64_t* conn, int npe, const int32_t* inc_ptr, const 
 /* fem_graph_fill2 + fem_sell_fill + fem_sell_delta16 in one pass over the slices (slice_ptr from fem_sell_widths +
  * fem_scan_i64): colidx, diagpos, SELL cols, the 16-bit deltas dcols [slice_ptr[S]] (0 where they do not fit,
  * *overflow [device int] = 1 then: keep the int32 cols) and csr2sell (may be NULL: fem_sell_csr2sell forms it on
- * demand) -- the same arrays as the three calls. */
+ * demand) -- the same arrays as the three calls. dcols / overflow may be NULL (fem_graph_count2's overflow already
+ * told the caller whether the deltas fit). */
 int fem_graph_sell_fill(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
                         const int32_t* rowptr, const int32_t* tmp, const int64_t* slice_ptr, int32_t* colidx,
                         int32_t* diagpos, int32_t* cols, int16_t* dcols, int64_t* csr2sell, int32_t* overflow,

@@ -843,6 +843,25 @@ def _helix_fan(m):
     return c, torch.stack([torch.zeros_like(a), a, a + 1, a + 2], 1)
 
 
+@pytest.mark.parametrize("m,gap", [(60, 0), (60, 40000), (300, 0), (300, 40000), (32700, 0), (33000, 0)])
+def test_cols16_flag_from_graph_count_matches_bandwidth(gpu, m, gap):
+    """The 16-bit delta decision is taken in the node-graph count kernels (read back in the build's single sync):
+    16-bit columns iff every |col - row| <= 32767, for rows in each count kernel -- hashed in registers (60-tet fan,
+    63 columns), hashed in LDS (300 tets, 303 columns) and selected in memory (32,700 / 33,000 tets: bandwidth just
+    under / over the limit). gap: the hub node is moved 40,000 ids away from its fan."""
+    _, _, _, system = _mods()
+    c, t = _helix_fan(m)
+    if gap:
+        c = torch.cat([c, torch.zeros(gap, 3, dtype=F64)])
+        t = torch.where(t == 0, torch.full_like(t, c.shape[0] - 1), t)
+        c[-1] = 0.0
+    g = system.build_graph(t.to(gpu), c.shape[0], compress=True)
+    rp = g.rowptr.long().cpu()
+    rows = torch.repeat_interleave(torch.arange(c.shape[0]), rp[1:] - rp[:-1])
+    bw = int((g.colidx.long().cpu() - rows).abs().max())
+    assert (g.dcols is not None) == (bw <= 32767), (m, gap, bw)
+
+
 @pytest.mark.parametrize("case", ["kuhn", "permuted", "fan"])
 def test_tile_assembly_bit_identical_to_row_kernels(gpu, case, monkeypatch):
     """c3d4 / P1 assembly straight into SELL: the row-tile kernel (k_asm_tet4_tile, default; fresh matrices stored
