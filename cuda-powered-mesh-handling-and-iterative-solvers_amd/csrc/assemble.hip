@@ -665,20 +665,12 @@ __global__ void __launch_bounds__(256) k_csr_add_sell(const double* __restrict__
 }
 
 // ---------------------------------------------------------------- fused c3d4 assembly (K_e never stored)
-// Two forms, both straight into SELL (addresses from the slice pointer, no csr2sell reads; a fresh matrix is stored
-// whole, padding zeroed, without a memset), both with the additions and order of the wave-per-row kernels below
-// (k_assemble_p1w / k_assemble_el3w, FEM355_ASM_ROWS; bit for bit, tests/test_gpu_parity.py): the accumulator form
-// (k_asm_tet4_acc) for bs = 1 and the owner form (k_asm_tet4_tile) for bs = 3.
-//
-// Owner form: one 256-thread workgroup per R consecutive rows of one SELL slice. Per batch of 256 of the
-// tile's incidences (one per thread, the tile's incidence range is contiguous): element gradients and volume, and
-// the row's column slots of the element's 4 nodes (binary search in the tile's CSR segment, staged in LDS), all
-// staged in LDS. Then every output -- (row, column) entry, bs x bs block -- is owned by one thread, which adds its
-// contributions over the row's incidences in ascending order onto zero (STORE, fresh matrix; SELL padding written
-// as zeros) or onto the stored value: the additions, their order and the value formulas of k_assemble_p1w /
-// k_assemble_el3w, and one wave's stores of a block plane cover 64 consecutive owners = whole 128-byte lines.
-constexpr int AT_TB = 256;       // incidences per batch (one per thread)
-constexpr int AT_SEGCAP = 1024;  // CSR entries of a tile staged in LDS (larger tiles search colidx in memory)
+// Straight into SELL (addresses from the slice pointer, no csr2sell reads; a fresh matrix is stored whole, padding
+// zeroed, without a memset), with the additions and order of the wave-per-row kernels below (k_assemble_p1w /
+// k_assemble_el3w, FEM355_ASM_ROWS; bit for bit, tests/test_gpu_parity.py): the accumulator form k_asm_tet4_acc.
+// (An owner form -- one thread per (row, column) output scanning the row's incidences -- measured 3.85 ms for the
+// 10M elastic cube, 3.7 ms with the element blocks formed once per incidence: its owners test every (incidence,
+// node) pair of the row and 3/4 of a wave's lanes idle at each, VALU-bound; the accumulator form 2.55 ms.)
 
 // a + b never fused with the product that formed b (the row kernels store the product to LDS before adding it)
 __device__ __forceinline__ double add_nc(double a, double b) {
@@ -712,147 +704,6 @@ __global__ void k_sell_zero(const int64_t* __restrict__ slice_ptr, int64_t ns, i
         vals[i] = 0.0;
 }
 
-template <int BS, int R, int OPT, bool STORE>
-__global__ void __launch_bounds__(256) k_asm_tet4_tile(const double* __restrict__ X, const int64_t* __restrict__ conn,
-                                                       double E, double nu, const int32_t* __restrict__ inc_ptr,
-                                                       const int32_t* __restrict__ inc, int64_t N,
-                                                       const int32_t* __restrict__ rowptr,
-                                                       const int32_t* __restrict__ colidx,
-                                                       const int64_t* __restrict__ slice_ptr,
-                                                       double* __restrict__ vals, int64_t* __restrict__ bad,
-                                                       int64_t ntiles) {
-    static_assert(64 % R == 0, "a tile lies inside one slice");
-    constexpr int B2 = BS * BS;
-    constexpr int ND = BS == 1 ? 4 : 13;   // per incidence: bs = 1 the 4 values of the element row; bs = 3 g, V
-    __shared__ int ip_s[R + 1];
-    __shared__ int rp_s[R + 1];
-    __shared__ int col_s[AT_SEGCAP];
-    __shared__ uint2 pos_s[AT_TB];         // the 4 nodes' column slots in the row, 16 bits each (0xffff: none)
-    __shared__ double dat_s[ND][AT_TB];   // structure of arrays: conflict-free stores by the incidence threads
-    __shared__ int8_t a_s[AT_TB];
-    const int tid = threadIdx.x;
-    const int64_t per = (ntiles + NXCD - 1) / NXCD;   // XCD-contiguous tile ranges (shared gathers stay in one L2)
-    const int64_t tile = (int64_t)(blockIdx.x % NXCD) * per + blockIdx.x / NXCD;
-    if (tile >= ntiles) return;
-    const int64_t r0 = tile * R;
-    const int64_t s = r0 >> 6;
-    const int l0 = (int)(r0 & 63);
-    const int64_t e0 = slice_ptr[s];
-    const int W = (int)((slice_ptr[s + 1] - e0) >> 6);
-    if (tid <= R) {
-        const int64_t r = r0 + tid < N ? r0 + tid : N;
-        ip_s[tid] = inc_ptr[r];
-        rp_s[tid] = rowptr[r];
-    }
-    __syncthreads();
-    const int seg0 = rp_s[0], segn = rp_s[R] - seg0;
-    const bool staged = segn <= AT_SEGCAP;
-    if (staged)
-        for (int q = tid; q < segn; q += 256) col_s[q] = colidx[seg0 + q];
-    const int T0 = ip_s[0], T1 = ip_s[R];
-    const Lame L = lame(E, nu);
-    const int nout = R * W;
-    for (int o0 = 0; o0 < nout; o0 += 256 * OPT) {
-        double acc[OPT][B2];
-#pragma unroll
-        for (int q = 0; q < OPT; ++q) {
-            const int o = o0 + q * 256 + tid, r = o % R, k = o / R;
-#pragma unroll
-            for (int c = 0; c < B2; ++c) acc[q][c] = 0.0;
-            if (!STORE && o < nout && k < rp_s[r + 1] - rp_s[r]) {
-                const int64_t Ei = e0 + (int64_t)k * 64 + l0 + r;
-#pragma unroll
-                for (int c = 0; c < B2; ++c) acc[q][c] = vals[BS == 1 ? Ei : sell_val(Ei, B2, c)];
-            }
-        }
-        for (int b0 = T0; b0 < T1; b0 += AT_TB) {
-            __syncthreads();   // col_s staged / previous batch consumed
-            const int t = b0 + tid;
-            if (t < T1) {
-                int lo = 0, hi = R;   // row of incidence t: last r with ip_s[r] <= t
-                while (hi - lo > 1) {
-                    const int m = (lo + hi) >> 1;
-                    if (ip_s[m] <= t) lo = m;
-                    else hi = m;
-                }
-                const int r = lo;
-                const int ea = inc[t];
-                const int64_t e = ea >> 2;
-                const int a = ea & 3;
-                const int64_t* c = conn + 4 * e;
-                double g[4][3];
-                const double det = tet4_grads(X, c, g);
-                if (o0 == 0 && fabs(det) < 1e-12) atomicMin((unsigned long long*)bad, (unsigned long long)e);
-                const double V = fabs(det) / 6.0;
-                const int cl = rp_s[r] - seg0, cn = rp_s[r + 1] - rp_s[r];
-                const int32_t* cs = staged ? col_s + cl : colidx + seg0 + cl;
-                uint32_t pk[2] = {0u, 0u};
-#pragma unroll
-                for (int bb = 0; bb < 4; ++bb) {
-                    const int j = (int)c[bb];
-                    int l = 0, h = cn;
-                    while (l < h) {
-                        const int m = (l + h) >> 1;
-                        if (cs[m] < j) l = m + 1;
-                        else h = m;
-                    }
-                    const uint32_t p = (l < cn && cs[l] == j) ? (uint32_t)l : 0xffffu;
-                    pk[bb >> 1] |= p << (16 * (bb & 1));
-                    if constexpr (BS == 1) dat_s[bb][tid] = p1_value(g[a], g[bb], E, V);
-                }
-                pos_s[tid] = make_uint2(pk[0], pk[1]);
-                if constexpr (BS == 3) {
-#pragma unroll
-                    for (int bb = 0; bb < 4; ++bb)
-#pragma unroll
-                        for (int q = 0; q < 3; ++q) dat_s[3 * bb + q][tid] = g[bb][q];
-                    dat_s[12][tid] = V;
-                    a_s[tid] = (int8_t)a;
-                }
-            }
-            __syncthreads();
-#pragma unroll
-            for (int q = 0; q < OPT; ++q) {
-                const int o = o0 + q * 256 + tid, r = o % R, k = o / R;
-                if (o >= nout || k >= rp_s[r + 1] - rp_s[r]) continue;
-                const int j0 = max(ip_s[r], b0) - b0, j1 = min(ip_s[r + 1], b0 + AT_TB) - b0;
-                for (int jj = j0; jj < j1; ++jj) {
-                    const uint2 pp = pos_s[jj];
-#pragma unroll
-                    for (int bb = 0; bb < 4; ++bb) {
-                        const uint32_t p = ((bb < 2 ? pp.x : pp.y) >> (16 * (bb & 1))) & 0xffffu;
-                        if (p != (uint32_t)k) continue;
-                        if constexpr (BS == 1) {
-                            acc[q][0] += dat_s[bb][jj];
-                        } else {
-                            const int aa = a_s[jj];
-                            const double ga[3] = {dat_s[3 * aa][jj], dat_s[3 * aa + 1][jj], dat_s[3 * aa + 2][jj]};
-                            const double gb[3] = {dat_s[3 * bb][jj], dat_s[3 * bb + 1][jj], dat_s[3 * bb + 2][jj]};
-                            const double V = dat_s[12][jj];
-                            const double dot = el_dot(ga, gb);
-#pragma unroll
-                            for (int rr = 0; rr < 3; ++rr)
-#pragma unroll
-                                for (int kk = 0; kk < 3; ++kk)
-                                    acc[q][rr * 3 + kk] =
-                                        add_nc(acc[q][rr * 3 + kk], el_value(L, ga, gb, rr, kk, dot, V));
-                        }
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < OPT; ++q) {
-            const int o = o0 + q * 256 + tid, r = o % R, k = o / R;
-            if (o >= nout) continue;
-            if (!STORE && k >= rp_s[r + 1] - rp_s[r]) continue;   // adding: padding stays as stored
-            const int64_t Ei = e0 + (int64_t)k * 64 + l0 + r;
-#pragma unroll
-            for (int c = 0; c < B2; ++c) vals[BS == 1 ? Ei : sell_val(Ei, B2, c)] = acc[q][c];
-        }
-    }
-}
-
 // Accumulator form (default): one workgroup per R rows of a slice, the rows' block values accumulated in LDS.
 // Items = (row, j-th incident element of the row); per batch the j0..j0+J-1 items of every row are formed by one
 // thread each (gradients, volume, the column slots of the element's nodes in the row) and staged in LDS; then
@@ -863,15 +714,18 @@ __global__ void __launch_bounds__(256) k_asm_tet4_tile(const double* __restrict_
 // k_assemble_el3w bit for bit, without their owner loops (whose lanes stepped through every item to find their
 // few matches). The rows' accumulators are written out whole slice columns at a time (coalesced SELL stores).
 // Columns past ACC_W per row: the accumulators cover the row's columns in windows of ACC_W, one sweep per window.
+// LDS strides padded (R + 1, NI + 1): a row's lanes update accumulators of different columns and read staged
+// values of different element nodes at once, which power-of-two strides put into one bank (bs = 3: 5.8 -> 3.0 ms).
 template <int R_, int J_, int LPR_, int W_, int SEG_>
 struct AccCfg {
     static constexpr int R = R_, J = J_, LPR = LPR_, W = W_, SEG = SEG_;
 };
 // bs = 1: lanes (row, b), 64 rows (a slice), 4 items per row per batch, 32 accumulated columns per row (10M cube:
 // 0.86 ms; 16 columns 0.79 ms but two sweeps for rows past 16 columns, 8 items per row 1.16 ms at 3 waves per SIMD).
-// bs = 3 runs the owner form (k_asm_tet4_tile): the accumulator form with lanes (row, b, rr) measured 5.7-6.2 ms
-// against 3.85 ms there (16-row tiles, 3-4 workgroups per CU: each batch's dependent element loads are exposed).
+// bs = 3: lanes (row, b, rr), 16 rows, 8 items per row per batch, 16 accumulated columns (10M cube: 2.55 ms; 16
+// items per row 2.95, 12 items 2.83, 4 items 2.66 ms).
 using AccP1 = AccCfg<64, 4, 4, 32, 1024>;
+using AccEl = AccCfg<16, 8, 16, 16, 512>;
 
 template <int BS, class Cfg, bool STORE>
 __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__ X, const int64_t* __restrict__ conn,
@@ -891,10 +745,12 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
     __shared__ int ip_s[R + 1];
     __shared__ int rp_s[R + 1];
     __shared__ int col_s[SEG];
-    __shared__ double dat_s[ND][NI];
+    // padded strides: the sweep's lanes of one row read dat_s rows of different element nodes and update
+    // accumulators of different columns -- with power-of-two strides those all fall into one LDS bank
+    __shared__ double dat_s[ND][NI + 1];
     __shared__ uint2 pos_s[NI];
     __shared__ uint8_t a_s[NI];             // local index of the row's node; bit 7: the element repeats a node
-    __shared__ double acc_s[AW * B2][R];
+    __shared__ double acc_s[AW * B2][R + 1];
     __shared__ int maxc_s;
     const int tid = threadIdx.x;
     const int64_t per = (ntiles + NXCD - 1) / NXCD;
@@ -1546,8 +1402,8 @@ int fem_assemble_tet4_ex(const double* coords, const int64_t* conn, double E, do
             set_error("fem_assemble_tet4: the row kernels (FEM355_ASM_ROWS) need csr2sell");
             return FEM_EARG;
         }
-        // wave per row (k_assemble_p1w / k_assemble_el3w, CSR-addressed through csr2sell; the tile kernel's bits):
-        // kept as the reference formulation of the tile kernel's summation order
+        // wave per row (k_assemble_p1w / k_assemble_el3w, CSR-addressed through csr2sell; k_asm_tet4_acc's bits):
+        // kept as the reference formulation of the accumulator kernel's summation order
         if (store) {
             hipLaunchKernelGGL(k_sell_zero, dim3(2048), dim3(256), 0, st, slice_ptr, cdiv(N, 64), bs * bs, vals);
             FEM_LAUNCHED();
@@ -1569,19 +1425,12 @@ int fem_assemble_tet4_ex(const double* coords, const int64_t* conn, double E, do
     } while (0)
         if (store) AA_LAUNCH(1, AccP1, true);
         else AA_LAUNCH(1, AccP1, false);
-#undef AA_LAUNCH
         FEM_LAUNCHED();
         return FEM_OK;
     }
-    constexpr int R = 32;
-    const int64_t ntiles = cdiv(N, 64) * (64 / R);   // every lane of the last slice (padding rows: zeros)
-    const dim3 g((unsigned)(cdiv(ntiles, NXCD) * NXCD));
-#define AT_LAUNCH(BS_, OPT_, ST_)                                                                                   \
-    hipLaunchKernelGGL((k_asm_tet4_tile<BS_, R, OPT_, ST_>), g, dim3(256), 0, st, coords, conn, E, nu, inc_ptr, inc, N, \
-                       rowptr, colidx, slice_ptr, vals, bad_idx, ntiles)
-    if (store) AT_LAUNCH(3, 3, true);
-    else AT_LAUNCH(3, 3, false);
-#undef AT_LAUNCH
+    if (store) AA_LAUNCH(3, AccEl, true);
+    else AA_LAUNCH(3, AccEl, false);
+#undef AA_LAUNCH
     FEM_LAUNCHED();
     return FEM_OK;
 }

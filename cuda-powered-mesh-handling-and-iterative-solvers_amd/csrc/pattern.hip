@@ -313,12 +313,6 @@ __global__ void __launch_bounds__(256) k_graph_small(const int64_t* __restrict__
             const int t = sl + u * LPN;
             cand[u] = t < C ? (int)conn[(int64_t)(cand[u] / npe) * npe + (t - (t / npe) * npe)] : -1;
         }
-        if (far) {   // a neighbour farther than 16-bit deltas reach (the SELL keeps int32 columns then)
-            bool f = false;
-#pragma unroll
-            for (int u = 0; u < CPL; ++u) f |= cand[u] >= 0 && (cand[u] - node > 32767 || node - cand[u] > 32767);
-            if (__ballot(f) && lane == 0 && !*far) atomicOr(far, 1);
-        }
         for (int q = sl; q < HS; q += LPN) tab[q] = -1;
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -349,11 +343,17 @@ __global__ void __launch_bounds__(256) k_graph_small(const int64_t* __restrict__
             if (sl == 0) defer[node] = 1;
             continue;
         }
+        bool f = false;   // a neighbour farther than 16-bit deltas reach (the SELL keeps int32 columns then)
         if (sl < U) {
             const int v = uq[sl];
             int rank = 0;
             for (int u = 0; u < U; ++u) rank += (uq[u] < v);
             trow[rank] = v;
+            f = v - node > 32767 || node - v > 32767;
+        }
+        if (far) {
+            const unsigned long long fb = __ballot(f);
+            if (fb && lane == __ffsll((long long)fb) - 1 && !*far) atomicOr(far, 1);
         }
         if (sl == 0) {
             row_len[node] = U;

@@ -862,18 +862,25 @@ def test_cols16_flag_from_graph_count_matches_bandwidth(gpu, m, gap):
     assert (g.dcols is not None) == (bw <= 32767), (m, gap, bw)
 
 
-@pytest.mark.parametrize("case", ["kuhn", "permuted", "fan"])
+@pytest.mark.parametrize("case", ["kuhn", "permuted", "fan", "repeated", "twice"])
 def test_tile_assembly_bit_identical_to_row_kernels(gpu, case, monkeypatch):
-    """c3d4 / P1 assembly straight into SELL: the row-tile kernel (k_asm_tet4_tile, default; fresh matrices stored
+    """c3d4 / P1 assembly straight into SELL: the accumulator kernel (k_asm_tet4_acc, default; fresh matrices stored
     whole without a memset) gives the SELL values -- padding included -- of the wave-per-row kernels
     (k_assemble_p1w / k_assemble_el3w onto a zeroed matrix, FEM355_ASM_ROWS) bit for bit, and adding a second time
     onto stored values too. Cases: a jittered cube, a randomly renumbered cube (wide slices), and a 1,500-tet fan (a
-    row of 1,503 columns: the CSR segment searched in memory, many output passes)."""
+    row of 1,503 columns: the CSR segment searched in memory, many output passes), a cube whose element 3 lists a
+    node twice (the ordered path for an element hitting one column twice; its rows are NaN -- the element is singular
+    -- so the bits are compared and the operator check skipped) and a cube with every element listed twice (rows of ~48 incidences: several item batches)."""
     _, mesh, _, system = _mods()
     if case == "fan":
         c, t = _helix_fan(1500)
     else:
         c, t = mesh.kuhn_cube(7, jitter=0.12)
+        if case == "repeated":
+            t = t.clone()
+            t[3, 3] = t[3, 0]
+        if case == "twice":
+            t = t.repeat(2, 1)
         if case == "permuted":
             perm = torch.randperm(c.shape[0], generator=torch.Generator().manual_seed(11))
             inv = torch.empty_like(perm)
@@ -895,6 +902,10 @@ def test_tile_assembly_bit_identical_to_row_kernels(gpu, case, monkeypatch):
             A.add_tet4(cg, tg, Ek, NU)
             out.append((first, A.vals.clone()))
         monkeypatch.delenv("FEM355_ASM_ROWS", raising=False)
+        if case == "repeated":   # the singular element's rows are NaN in both: compare the bits
+            assert all(torch.equal(out[0][i].view(torch.int64), out[1][i].view(torch.int64)) for i in (0, 1))
+            assert not bool(torch.isnan(out[0][0][: out[0][0].numel() // 2]).all())
+            continue
         assert not bool(torch.isnan(out[0][0]).any())
         assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1]), (case, kind)
         Ko = R.tet4_K(c, t, E, NU) if bs == 3 else 2.5 * R.tet4_poisson_K(c, t)
