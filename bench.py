@@ -8,8 +8,8 @@ Workload: Kuhn-cube mesh n=119 -> 10,110,954 P1 tets, 1,728,0
     `value` = steps/s of the whole job (for N>1: the same global system element-partitioned over the ranks,
     strong scaling), measured between barrier+synchronize brackets, max over ranks.
   * DOFs/s = n_DOF / (assembly incl. pattern build + PCG solve to rtol 1e-8 on sqrt(r.z)), reported beside:
-    steady state (`dofs_per_s`, the median of --dof-passes identical passes after the first, all listed in
-    `dofs_passes_ms`) and first use (`dofs_per_s_cold`, which also pays the device allocations of this mesh size).
+    steady state (`dofs_per_s`: median assembly + median solve of --dof-passes identical passes after the first,
+    all listed in `dofs_passes_ms`) and first use (`dofs_per_s_cold`, which also pays the device allocations of this mesh size).
   * roofline: the dominant kernel of the active schedule, algorithmic bytes (8 + idx) nnz + 4 (n+1) + 16 n
     (§8(d); idx = 2 for 16-bit deltas, 4 for int32) over its device time measured live with hip events on the
     solver stream inside the timed region. bs=1 default (persistent schedule, k_pcg_persist): per ITERATION —
@@ -218,7 +218,7 @@ def measure(a, kind, coords, tets, dev):
     # ---- assembly (pattern + values + Jacobi) and solve to tolerance: DOFs/s. The first pass pays the first-use
     # device allocations of this mesh size (torch's caching allocator, the solver's buffer cache) and is reported as
     # dofs_per_s_cold; the --dof-passes passes after it, timed the same way, give the steady-state dofs_per_s (their
-    # median; same work every pass: the pattern, the values, the Jacobi weights and the whole solve are recomputed
+    # medians; same work every pass: the pattern, the values, the Jacobi weights and the whole solve are recomputed
     # from the mesh)
     reorder_ms = []
 
@@ -254,8 +254,11 @@ def measure(a, kind, coords, tets, dev):
         A, w, b, res, t_asm, t_solve = assemble_and_solve()
         assert res.iterations == res_cold.iterations and res.status == res_cold.status
         passes.append((t_asm, t_solve))
-    # steady state: the median pass by assembly + solve wall time (every pass repeats the whole work)
-    t_asm, t_solve = sorted(passes, key=lambda p: p[0] + p[1])[len(passes) // 2]
+    # steady state: the median assembly time and the median solve time of the passes (every pass repeats the whole
+    # work; one pass's assembly can pay a first-use allocation of the caching allocator, and the solve times vary
+    # by a few percent from box to box, so a median pass by the sum can carry the assembly outlier)
+    t_asm = sorted(p[0] for p in passes)[len(passes) // 2]
+    t_solve = sorted(p[1] for p in passes)[len(passes) // 2]
 
     # ---- fixed-iteration timing (the metric)
     run = system.PcgRunner(A, b, w, tol=0.0, schedule=a.schedule)
