@@ -270,7 +270,9 @@ __device__ __forceinline__ int ht_bits(int C, int maxbits) {
 
 // LPN lanes per node (64 or 32): with 32 each half-wave builds its own row in half the wave's table, so two rows'
 // dependent incidence / connectivity loads are in flight per wave; rows over LPN / 64 * G_SCAP candidates defer.
-template <int LPN>
+// NPE > 0 (even, connectivity rows 16-byte aligned): a lane takes whole incidences -- the element's node ids in
+// NPE / 2 16-byte loads of one row -- instead of one node id per candidate slot (NPE = 0: any npe)
+template <int LPN, int NPE>
 __global__ void __launch_bounds__(256) k_graph_small(const int64_t* __restrict__ conn, int npe,
                                                      const int32_t* __restrict__ inc_ptr,
                                                      const int32_t* __restrict__ inc, int64_t N,
@@ -301,17 +303,38 @@ __global__ void __launch_bounds__(256) k_graph_small(const int64_t* __restrict__
         const int hb = ht_bits(C, MAXB), HS = 1 << hb;
         // all of the lane's candidates loaded before any insert (the incidence loads, then the connectivity loads,
         // in flight together instead of one dependent pair per insert)
-        constexpr int CPL = (SCAP + LPN - 1) / LPN;
+        constexpr int IPL = NPE > 0 ? (SCAP / (NPE > 0 ? NPE : 1) + LPN - 1) / LPN : 0;   // incidences per lane
+        constexpr int CPL = NPE > 0 ? IPL * NPE : (SCAP + LPN - 1) / LPN;
         int cand[CPL];
+        if constexpr (NPE > 0) {
+            const int ninc = C / NPE;
+            int el[IPL];
 #pragma unroll
-        for (int u = 0; u < CPL; ++u) {
-            const int t = sl + u * LPN;
-            cand[u] = t < C ? inc[start + t / npe] : 0;
-        }
+            for (int u = 0; u < IPL; ++u) {
+                const int t = sl + u * LPN;
+                el[u] = t < ninc ? inc[start + t] / NPE : -1;
+            }
 #pragma unroll
-        for (int u = 0; u < CPL; ++u) {
-            const int t = sl + u * LPN;
-            cand[u] = t < C ? (int)conn[(int64_t)(cand[u] / npe) * npe + (t - (t / npe) * npe)] : -1;
+            for (int u = 0; u < IPL; ++u) {
+                const longlong2* row = reinterpret_cast<const longlong2*>(conn + (int64_t)(el[u] < 0 ? 0 : el[u]) * NPE);
+#pragma unroll
+                for (int h = 0; h < NPE / 2; ++h) {
+                    const longlong2 v = row[h];
+                    cand[u * NPE + 2 * h] = el[u] < 0 ? -1 : (int)v.x;
+                    cand[u * NPE + 2 * h + 1] = el[u] < 0 ? -1 : (int)v.y;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < CPL; ++u) {
+                const int t = sl + u * LPN;
+                cand[u] = t < C ? inc[start + t / npe] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < CPL; ++u) {
+                const int t = sl + u * LPN;
+                cand[u] = t < C ? (int)conn[(int64_t)(cand[u] / npe) * npe + (t - (t / npe) * npe)] : -1;
+            }
         }
         for (int q = sl; q < HS; q += LPN) tab[q] = -1;
         __builtin_amdgcn_wave_barrier();
@@ -854,8 +877,16 @@ int fem_graph_count2(const int64_t* conn, int npe, const int32_t* inc_ptr, const
     if (overflow) FEM_HIP(hipMemsetAsync(overflow, 0, sizeof(int32_t), S(stream)));
     if (N <= 0) return FEM_OK;
     const int64_t grid = std::min<int64_t>(cdiv(N, G_WAVES), 16384);
-    hipLaunchKernelGGL(k_graph_small<FEM_GRAPH_LPN>, dim3((unsigned)grid), dim3(256), 0, S(stream), conn, npe, inc_ptr, inc, N,
-                       row_len, tmp, defer_flags(tmp, N), overflow);
+    const bool al16 = (reinterpret_cast<uintptr_t>(conn) & 15) == 0;
+#define GS_LAUNCH(NPE_)                                                                                           \
+    hipLaunchKernelGGL((k_graph_small<FEM_GRAPH_LPN, NPE_>), dim3((unsigned)grid), dim3(256), 0, S(stream), conn, \
+                       npe, inc_ptr, inc, N, row_len, tmp, defer_flags(tmp, N), overflow)
+    if (al16 && npe == 4 && getenv("FEM355_GRAPH_SLOTS") == nullptr) GS_LAUNCH(4);
+    else if (al16 && npe == 6) GS_LAUNCH(6);
+    else if (al16 && npe == 8) GS_LAUNCH(8);
+    else if (al16 && npe == 10) GS_LAUNCH(10);
+    else GS_LAUNCH(0);
+#undef GS_LAUNCH
     FEM_LAUNCHED();
     return graph_count(conn, npe, inc_ptr, inc, N, row_len, defer_flags(tmp, N), overflow, S(stream));
 }
