@@ -316,12 +316,16 @@ __global__ void __launch_bounds__(256) k_graph_small(const int64_t* __restrict__
             }
 #pragma unroll
             for (int u = 0; u < IPL; ++u) {
-                const longlong2* row = reinterpret_cast<const longlong2*>(conn + (int64_t)(el[u] < 0 ? 0 : el[u]) * NPE);
 #pragma unroll
-                for (int h = 0; h < NPE / 2; ++h) {
-                    const longlong2 v = row[h];
-                    cand[u * NPE + 2 * h] = el[u] < 0 ? -1 : (int)v.x;
-                    cand[u * NPE + 2 * h + 1] = el[u] < 0 ? -1 : (int)v.y;
+                for (int h = 0; h < NPE; ++h) cand[u * NPE + h] = -1;
+                if (el[u] >= 0) {   // no load for an empty slot (an element-free mesh may pass no connectivity)
+                    const longlong2* row = reinterpret_cast<const longlong2*>(conn + (int64_t)el[u] * NPE);
+#pragma unroll
+                    for (int h = 0; h < NPE / 2; ++h) {
+                        const longlong2 v = row[h];
+                        cand[u * NPE + 2 * h] = (int)v.x;
+                        cand[u * NPE + 2 * h + 1] = (int)v.y;
+                    }
                 }
             }
         } else {
