@@ -725,7 +725,10 @@ struct AccCfg {
 // bs = 3: lanes (row, b, rr), 16 rows, 8 items per row per batch, 16 accumulated columns (10M cube: 2.55 ms; 16
 // items per row 2.95, 12 items 2.83, 4 items 2.66 ms).
 using AccP1 = AccCfg<64, 4, 4, 32, 1024>;
-using AccEl = AccCfg<16, 8, 16, 16, 512>;
+#ifndef FEM_EL3_CFG
+#define FEM_EL3_CFG 16, 8, 16, 16, 512
+#endif
+using AccEl = AccCfg<FEM_EL3_CFG>;
 
 template <int BS, class Cfg, bool STORE>
 __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__ X, const int64_t* __restrict__ conn,
@@ -739,9 +742,13 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
     constexpr int R = Cfg::R, J = Cfg::J, LPR = Cfg::LPR, AW = Cfg::W, SEG = Cfg::SEG;
     constexpr int B2 = BS * BS;
     constexpr int NI = R * J;
+    constexpr int NT = R * LPR;                        // threads of the workgroup
+    constexpr int RPL = (BS == 3 && LPR == 4) ? 3 : 1;   // block rows per sweep lane (bs = 3: lanes (row, b) or
+                                                         // (row, b, rr))
     constexpr int ND = BS == 1 ? 4 : 13;
-    static_assert(NI <= 256, "one item per thread per batch");
-    static_assert(64 % R == 0 && R * LPR == 256 && 64 % LPR == 0, "tile geometry");
+    static_assert(NI <= NT, "one item per thread per batch");
+    static_assert(64 % R == 0 && NT <= 256 && NT % 64 == 0 && 64 % LPR == 0, "tile geometry");
+    static_assert(BS == 1 || LPR == 4 || LPR == 16, "bs = 3 lanes: (row, b) or (row, b, rr)");
     __shared__ int ip_s[R + 1];
     __shared__ int rp_s[R + 1];
     __shared__ int col_s[SEG];
@@ -775,16 +782,17 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
     const int seg0 = rp_s[0], segn = rp_s[R] - seg0;
     const bool staged = segn <= SEG;
     if (staged)
-        for (int q = tid; q < segn; q += 256) col_s[q] = colidx[seg0 + q];
+        for (int q = tid; q < segn; q += NT) col_s[q] = colidx[seg0 + q];
     const int maxc = maxc_s;
     const Lame L = lame(E, nu);
-    // phase-2 lane: row lr, element node lb, block row lrr
-    const int lr = tid / LPR, lb = (tid % LPR) / (BS == 1 ? 1 : 4), lrr = BS == 1 ? 0 : tid % 4;
+    // phase-2 lane: row lr, element node lb, block rows lrr .. lrr + RPL - 1
+    const int lr = tid / LPR, lb = (BS == 1 || LPR == 4) ? tid % LPR : (tid % LPR) / 4;
+    const int lrr = (BS == 1 || LPR == 4) ? 0 : tid % 4;
     const bool lactive = BS == 1 || lrr < 3;
     for (int c0 = 0; c0 < W; c0 += AW) {
         const int cw = min(AW, W - c0);
         __syncthreads();
-        for (int q = tid; q < AW * B2 * R; q += 256) {
+        for (int q = tid; q < AW * B2 * R; q += NT) {
             const int r = q % R, kc = q / R, k = kc / B2, c = kc - k * B2;
             double v = 0.0;
             if (!STORE && k < cw && c0 + k < rp_s[r + 1] - rp_s[r])
@@ -879,7 +887,7 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                 const int k = (int)praw - c0;
                 const bool hit = lactive && praw != 0xffffu && k >= 0 && k < cw;
                 const uint8_t af = a_s[it];
-                double v[BS];
+                double v[BS * RPL];
                 if (hit) {
                     if constexpr (BS == 1) {
                         v[0] = dat_s[lb][it];
@@ -890,14 +898,16 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                         const double V = dat_s[12][it];
                         const double dot = el_dot(ga, gb);
 #pragma unroll
-                        for (int cc = 0; cc < 3; ++cc) v[cc] = el_value(L, ga, gb, lrr, cc, dot, V);
+                        for (int q = 0; q < RPL; ++q)
+#pragma unroll
+                            for (int cc = 0; cc < 3; ++cc) v[q * 3 + cc] = el_value(L, ga, gb, lrr + q, cc, dot, V);
                     }
                 }
                 const bool any_rep = __ballot(hit && (af & 0x80)) != 0;
                 if (!any_rep) {
                     if (hit) {
 #pragma unroll
-                        for (int cc = 0; cc < BS; ++cc) {
+                        for (int cc = 0; cc < BS * RPL; ++cc) {
                             double* ap = &acc_s[k * B2 + lrr * BS + cc][lr];
                             *ap = add_nc(*ap, v[cc]);
                         }
@@ -906,7 +916,7 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                     for (int b = 0; b < 4; ++b) {
                         if (hit && lb == b) {
 #pragma unroll
-                            for (int cc = 0; cc < BS; ++cc) {
+                            for (int cc = 0; cc < BS * RPL; ++cc) {
                                 double* ap = &acc_s[k * B2 + lrr * BS + cc][lr];
                                 *ap = add_nc(*ap, v[cc]);
                             }
@@ -918,7 +928,7 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
             }
         }
         __syncthreads();
-        for (int q = tid; q < cw * B2 * R; q += 256) {
+        for (int q = tid; q < cw * B2 * R; q += NT) {
             const int r = q % R, kc = q / R, k = kc / B2, c = kc - k * B2;
             if (!STORE && c0 + k >= rp_s[r + 1] - rp_s[r]) continue;   // adding: padding stays as stored
             const int64_t Ei = e0 + (int64_t)(c0 + k) * 64 + l0 + r;
@@ -1420,7 +1430,8 @@ int fem_assemble_tet4_ex(const double* coords, const int64_t* conn, double E, do
 #define AA_LAUNCH(BS_, CFG_, ST_)                                                                                   \
     do {                                                                                                            \
         const int64_t nt = cdiv(N, 64) * (64 / CFG_::R);                                                            \
-        hipLaunchKernelGGL((k_asm_tet4_acc<BS_, CFG_, ST_>), dim3((unsigned)(cdiv(nt, NXCD) * NXCD)), dim3(256), 0,  \
+        hipLaunchKernelGGL((k_asm_tet4_acc<BS_, CFG_, ST_>), dim3((unsigned)(cdiv(nt, NXCD) * NXCD)),               \
+                           dim3(CFG_::R * CFG_::LPR), 0,                                                             \
                            st, coords, conn, E, nu, inc_ptr, inc, N, rowptr, colidx, slice_ptr, vals, bad_idx, nt); \
     } while (0)
         if (store) AA_LAUNCH(1, AccP1, true);
