@@ -253,7 +253,8 @@ constexpr int G_SCAP = 384;     // candidate capacity of the small-row kernel
 constexpr int G_TCAP = 32;      // rows of at most this many neighbours are produced by k_graph_small
 
 // Small rows in one pass (every P1 / Q1 / wedge row of ordinary meshes): wave per node, candidates deduplicated
-// through a wave-private LDS hash table (512 slots, linear probing, compare-and-swap), the unique set compacted
+// through a wave-private LDS hash table (linear probing, compare-and-swap; the row's own node added after), the
+// unique set compacted
 // and rank-sorted, written to tmp[node * G_TCAP + rank] with row_len[node]. Rows with more than G_SCAP candidates or
 // G_TCAP neighbours get tmp[node * G_TCAP] = -1 and are left to k_graph (count and fill passes skip the rest).
 constexpr int G_HT = 512;
@@ -282,6 +283,7 @@ __global__ void __launch_bounds__(256) k_graph_small(const int64_t* __restrict__
     constexpr int HTS = G_HT / NPW;               // table slots per node
     constexpr int SCAP = G_SCAP * LPN / 64;       // candidates per node (load <= 3/4 of the table)
     constexpr int MAXB = (HTS == 512) ? 9 : (HTS == 256 ? 8 : 7);
+    constexpr int LB = LPN == 64 ? 6 : 5;         // log2(LPN): the compaction reads LPN slots at a time
     __shared__ int ht[G_WAVES][G_HT];
     __shared__ int uniq[G_WAVES][64];
     const int wid = threadIdx.x >> 6;
@@ -300,7 +302,12 @@ __global__ void __launch_bounds__(256) k_graph_small(const int64_t* __restrict__
             if (sl == 0) defer[node] = 1;
             continue;
         }
-        const int hb = ht_bits(C, MAXB), HS = 1 << hb;
+        // the row's own node is in every incidence: it is left out of the hash (a quarter of the P1 inserts) and
+        // added after the compaction; the table holds the other candidates' distinct values (at most Cn) with a free
+        // slot to end every probe, and at least one slot per lane
+        const int Cn = C - C / npe;
+        const int hbw = 32 - __clz(Cn);   // smallest b with 2^b > Cn
+        const int hb = hbw < LB ? LB : (hbw > MAXB ? MAXB : hbw), HS = 1 << hb;
         // all of the lane's candidates loaded before any insert (the incidence loads, then the connectivity loads,
         // in flight together instead of one dependent pair per insert)
         constexpr int IPL = NPE > 0 ? (SCAP / (NPE > 0 ? NPE : 1) + LPN - 1) / LPN : 0;   // incidences per lane
@@ -345,7 +352,7 @@ __global__ void __launch_bounds__(256) k_graph_small(const int64_t* __restrict__
 #pragma unroll
         for (int u = 0; u < CPL; ++u) {
             const int v = cand[u];
-            if (v < 0) continue;
+            if (v < 0 || v == (int)node) continue;
             unsigned h = ((unsigned)v * 2654435761u) >> (32 - hb);
             while (true) {
                 const int old = atomicCAS(&tab[h], -1, v);
@@ -364,6 +371,10 @@ __global__ void __launch_bounds__(256) k_graph_small(const int64_t* __restrict__
                 if (pos < LPN) uq[pos] = v;
             }
             U += __popcll(m);
+        }
+        if (C > 0) {   // the row's own node
+            if (sl == U && U < LPN) uq[U] = (int)node;
+            ++U;
         }
         __builtin_amdgcn_wave_barrier();
         if (U > G_TCAP || U > LPN) {
