@@ -697,6 +697,20 @@ __device__ __forceinline__ double p1_value(const double ga[3], const double gb[3
     return kappa * dot * V;
 }
 
+// position of j in the ascending cs[0, n) (0xffff: absent): branch-free halving whose step count depends on n only
+// (rows of one wave share it), every read inside [0, n)
+__device__ __forceinline__ uint32_t sorted_pos(const int32_t* cs, int n, int j) {
+    if (n <= 0) return 0xffffu;
+    int b = 0;
+    for (int len = n; len > 1;) {
+        const int half = len >> 1;
+        b = cs[b + half] < j ? b + half : b;
+        len -= half;
+    }
+    b += cs[b] < j;
+    return (b < n && cs[b] == j) ? (uint32_t)b : 0xffffu;
+}
+
 // zero the SELL values of slices [0, ns) (slice_ptr on the device)
 __global__ void k_sell_zero(const int64_t* __restrict__ slice_ptr, int64_t ns, int bs2, double* __restrict__ vals) {
     const int64_t n = slice_ptr[ns] * bs2;
@@ -848,13 +862,7 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                     for (int bb = 0; bb < 4; ++bb) {
                         const int j = (int)c[bb];
                         nodes[bb] = j;
-                        int l = 0, h = cn;
-                        while (l < h) {
-                            const int m = (l + h) >> 1;
-                            if (cs[m] < j) l = m + 1;
-                            else h = m;
-                        }
-                        const uint32_t p = (l < cn && cs[l] == j) ? (uint32_t)l : 0xffffu;
+                        const uint32_t p = sorted_pos(cs, cn, j);
                         pk[bb >> 1] |= p << (16 * (bb & 1));
                         if constexpr (BS == 1) dat_s[bb][it0] = p1_value(g[a], g[bb], E, V);
                     }
