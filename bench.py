@@ -231,10 +231,9 @@ def measure(a, kind, coords, tets, dev):
             ff, fx = f[perm], inv[fixed]
             sync()
             reorder_ms.append((time.perf_counter() - t0) * 1e3)
-        # the Dirichlet mask first: its small torch launches then queue up while the pattern kernels run
-        mask = torch.zeros((N, 1 if kind == "poisson" else 3), dtype=torch.uint8, device=dev)
-        mask[fx] = 1
         A = system.assemble_tet4_system(c, t, kind, E, nu)
+        mask = torch.zeros((N, A.bs), dtype=torch.uint8, device=dev)
+        mask[fx] = 1
         w = A.jacobi(mask.view(-1))
         sync()
         t_asm = time.perf_counter() - t0
