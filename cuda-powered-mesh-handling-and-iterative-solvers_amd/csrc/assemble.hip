@@ -855,14 +855,15 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                     if (c0 == 0 && fabs(det) < 1e-12) atomicMin((unsigned long long*)bad, (unsigned long long)e);
                     const double V = fabs(det) / 6.0;
                     const int cl = rp_s[r] - seg0, cn = rp_s[r + 1] - rp_s[r];
-                    const int32_t* cs = staged ? col_s + cl : colidx + seg0 + cl;
                     int nodes[4];
                     pk[0] = pk[1] = 0u;
 #pragma unroll
                     for (int bb = 0; bb < 4; ++bb) {
                         const int j = (int)c[bb];
                         nodes[bb] = j;
-                        const uint32_t p = sorted_pos(cs, cn, j);
+                        // the tile-uniform branch keeps the LDS search on ds_read (one pointer for both would
+                        // make every probe a flat load)
+                        const uint32_t p = staged ? sorted_pos(col_s + cl, cn, j) : sorted_pos(colidx + seg0 + cl, cn, j);
                         pk[bb >> 1] |= p << (16 * (bb & 1));
                         if constexpr (BS == 1) dat_s[bb][it0] = p1_value(g[a], g[bb], E, V);
                     }

@@ -200,19 +200,26 @@ __global__ void __launch_bounds__(256) k_inc_l2(const int32_t* __restrict__ knod
     if (node0 + nn == N && threadIdx.x == 0) inc_ptr[N] = hi;
     for (int j = threadIdx.x; j < B; j += 256) cnt[j] = st[j];
     __syncthreads();
-    for (int e0 = wid * 64; e0 < n; e0 += 256) {   // into node segments (arrival order inside a segment)
-        const int e = e0 + lane;
-        const bool valid = e < n;
-        const int kn = valid ? (fits ? ln[e] : (int)(knode[lo + e] - node0)) : 0;
-        const int p = agg_add<true>(cnt, kn, valid);
-        if (valid) {
-            const int sl = fits ? ls[e] : kslot[lo + e];
-            if (fits) {
-                out[p] = sl;
+    // into node segments (arrival order inside a segment); the two tiers in separate loops, so the LDS tier's reads
+    // stay ds_read (a pointer that may be LDS or global makes flat loads)
+    if (fits) {
+        for (int e0 = wid * 64; e0 < n; e0 += 256) {
+            const int e = e0 + lane;
+            const bool valid = e < n;
+            const int kn = valid ? (int)ln[e] : 0;
+            const int p = agg_add<true>(cnt, kn, valid);
+            if (valid) {
+                out[p] = ls[e];
                 on[p] = (uint8_t)kn;
-            } else {
-                scratch[lo + p] = sl;
             }
+        }
+    } else {
+        for (int e0 = wid * 64; e0 < n; e0 += 256) {
+            const int e = e0 + lane;
+            const bool valid = e < n;
+            const int kn = valid ? (int)(knode[lo + e] - node0) : 0;
+            const int p = agg_add<true>(cnt, kn, valid);
+            if (valid) scratch[lo + p] = kslot[lo + e];
         }
     }
     __syncthreads();
