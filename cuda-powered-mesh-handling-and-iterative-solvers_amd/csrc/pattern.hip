@@ -629,7 +629,10 @@ __global__ void __launch_bounds__(256) k_sell_fill_graph(const int32_t* __restri
                                                          int32_t* __restrict__ cols, int16_t* __restrict__ dcols,
                                                          int64_t* __restrict__ csr2sell, int32_t* __restrict__ overflow) {
     __shared__ int32_t rp_s[4][65];
+    constexpr int TS = G_TCAP + 1;   // padded row stride: lane = row reads hit distinct banks
+    __shared__ int32_t row_s[4][64 * TS];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int32_t* rows = row_s[wid];
     for (int64_t s = (int64_t)blockIdx.x * 4 + wid; s < nslices; s += (int64_t)gridDim.x * 4) {
         const int64_t r = s * 64 + lane;
         const int64_t e0 = slice_ptr[s];
@@ -637,7 +640,27 @@ __global__ void __launch_bounds__(256) k_sell_fill_graph(const int32_t* __restri
         const int64_t rlast = min(s * 64 + 64, nrows);
         rp_s[wid][lane] = rowptr[min(r, rlast)];
         if (lane == 0) rp_s[wid][64] = rowptr[rlast];
+        // the slice's 64 graph rows (contiguous in tmp: 64 x 32 slots) staged in LDS with 16-byte coalesced loads,
+        // instead of lanes reading their rows 128 bytes apart -- twice (SELL columns, then CSR colidx)
+        {
+            const int4* src4 = reinterpret_cast<const int4*>(tmp + s * 64 * G_TCAP);
+            const int nr = (int)(rlast - s * 64);
+#pragma unroll
+            for (int u = 0; u < G_TCAP / 4; ++u) {
+                const int q = u * 64 + lane;          // int4 index: row q / 8, slots 4 (q % 8) ..
+                const int rr = q >> 3, k = (q & 7) * 4;
+                if (rr < nr) {
+                    const int4 v = src4[q];
+                    rows[rr * TS + k] = v.x;
+                    rows[rr * TS + k + 1] = v.y;
+                    rows[rr * TS + k + 2] = v.z;
+                    rows[rr * TS + k + 3] = v.w;
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         int len = 0, rp = 0;
         bool dfr = true;
         if (r < nrows) {
@@ -645,14 +668,18 @@ __global__ void __launch_bounds__(256) k_sell_fill_graph(const int32_t* __restri
             len = rp_s[wid][lane + 1] - rp;
             dfr = defer[r] != 0;
         }
-        const int32_t* src = dfr ? colidx + rp : tmp + r * G_TCAP;
         const int pad = (r < nrows) ? (int)r : (int)(nrows - 1);   // near the row: 16-bit deltas stay small
         bool far = false;
         for (int k0 = 0; k0 < w; k0 += 8) {
-            int cv[8];   // the row's next 8 columns loaded before any store (src may alias nothing written here,
-                         // but the compiler cannot know: without the staging every load waits for the stores)
+            int cv[8];   // the row's next 8 columns read before any store (a deferred row's from colidx: the
+                         // compiler cannot know it aliases nothing written here)
 #pragma unroll
-            for (int u = 0; u < 8; ++u) cv[u] = (k0 + u < len) ? src[k0 + u] : pad;
+            for (int u = 0; u < 8; ++u) {
+                const int k = k0 + u;
+                if (k >= len) cv[u] = pad;
+                else if (dfr) cv[u] = colidx[rp + k];
+                else cv[u] = rows[lane * TS + k];
+            }
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const int k = k0 + u;
@@ -679,9 +706,9 @@ __global__ void __launch_bounds__(256) k_sell_fill_graph(const int32_t* __restri
             const int k = p - rp_s[wid][lo];
             if (csr2sell) csr2sell[p] = e0 + (int64_t)k * 64 + lo;
             const int64_t row = s * 64 + lo;
-            if (!defer[row]) colidx[p] = tmp[row * G_TCAP + k];
+            if (!defer[row]) colidx[p] = rows[lo * TS + k];
         }
-        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_wave_barrier();   // the staged rows consumed before the next slice overwrites them
     }
 }
 
