@@ -64,6 +64,7 @@ SIGNATURES = {
     "fem_assemble_from_ke_ex": (_I, [_P, _P, _I, _I, _P, _P, _L, _P, _P, _P, _P, _L, _L, _I, _P, _P]),
     "fem_assemble_tet4": (_I, [_P, _P, _D, _D, _I, _P, _P, _L, _P, _P, _P, _P, _P, _P, _P]),
     "fem_assemble_tet4_ex": (_I, [_P, _P, _D, _D, _I, _P, _P, _L, _P, _P, _P, _P, _I, _P, _P, _P]),
+    "fem_assemble_tet4_ex2": (_I, [_P, _P, _D, _D, _I, _P, _P, _L, _P, _P, _P, _P, _I, _I, _P, _P, _P]),
     "fem_sell_to_csr_vals": (_I, [_P, _I, _P, _L, _P, _P, _P, _P]),
     "fem_jacobi": (_I, [_P, _I, _P, _P, _P, _P, _L, _P, _P, _P]),
     "fem_ebe_apply": (_I, [_P, _P, _I, _I, _P, _P, _L, _P, _P, _P]),

@@ -738,7 +738,11 @@ struct AccCfg {
 // 0.86 ms; 16 columns 0.79 ms but two sweeps for rows past 16 columns, 8 items per row 1.16 ms at 3 waves per SIMD).
 // bs = 3: lanes (row, b, rr), 16 rows, 8 items per row per batch, 16 accumulated columns (10M cube: 2.55 ms; 16
 // items per row 2.95, 12 items 2.83, 4 items 2.66 ms).
-using AccP1 = AccCfg<64, 4, 4, 32, 1024>;
+#ifndef FEM_P1_CFG
+#define FEM_P1_CFG 64, 4, 4, 32, 1024
+#endif
+using AccP1 = AccCfg<FEM_P1_CFG>;
+using AccP1w16 = AccCfg<64, 4, 4, 16, 1024>;   // patterns of at most 16 columns per row (10M cube: 0.67 vs 0.74 ms)
 #ifndef FEM_EL3_CFG
 #define FEM_EL3_CFG 16, 8, 16, 16, 512
 #endif
@@ -1406,10 +1410,10 @@ int fem_assemble_from_ke_ex(const double* Ke, const int64_t* conn, int npe, int 
     return FEM_OK;
 }
 
-int fem_assemble_tet4_ex(const double* coords, const int64_t* conn, double E, double nu, int bs,
-                         const int32_t* inc_ptr, const int32_t* inc, int64_t N, const int32_t* rowptr,
-                         const int32_t* colidx, const int64_t* csr2sell, const int64_t* slice_ptr, int store,
-                         double* vals, int64_t* bad_idx, fem_stream_t stream) {
+int fem_assemble_tet4_ex2(const double* coords, const int64_t* conn, double E, double nu, int bs,
+                          const int32_t* inc_ptr, const int32_t* inc, int64_t N, const int32_t* rowptr,
+                          const int32_t* colidx, const int64_t* csr2sell, const int64_t* slice_ptr, int store,
+                          int max_width, double* vals, int64_t* bad_idx, fem_stream_t stream) {
     if (bs != 1 && bs != 3) {
         set_error("fem_assemble_tet4: block size %d unsupported", bs);
         return FEM_EARG;
@@ -1443,8 +1447,13 @@ int fem_assemble_tet4_ex(const double* coords, const int64_t* conn, double E, do
                            dim3(CFG_::R * CFG_::LPR), 0,                                                             \
                            st, coords, conn, E, nu, inc_ptr, inc, N, rowptr, colidx, slice_ptr, vals, bad_idx, nt); \
     } while (0)
-        if (store) AA_LAUNCH(1, AccP1, true);
-        else AA_LAUNCH(1, AccP1, false);
+        if (max_width > 0 && max_width <= AccP1w16::W) {
+            if (store) AA_LAUNCH(1, AccP1w16, true);
+            else AA_LAUNCH(1, AccP1w16, false);
+        } else {
+            if (store) AA_LAUNCH(1, AccP1, true);
+            else AA_LAUNCH(1, AccP1, false);
+        }
         FEM_LAUNCHED();
         return FEM_OK;
     }
@@ -1453,6 +1462,14 @@ int fem_assemble_tet4_ex(const double* coords, const int64_t* conn, double E, do
 #undef AA_LAUNCH
     FEM_LAUNCHED();
     return FEM_OK;
+}
+
+int fem_assemble_tet4_ex(const double* coords, const int64_t* conn, double E, double nu, int bs,
+                         const int32_t* inc_ptr, const int32_t* inc, int64_t N, const int32_t* rowptr,
+                         const int32_t* colidx, const int64_t* csr2sell, const int64_t* slice_ptr, int store,
+                         double* vals, int64_t* bad_idx, fem_stream_t stream) {
+    return fem_assemble_tet4_ex2(coords, conn, E, nu, bs, inc_ptr, inc, N, rowptr, colidx, csr2sell, slice_ptr, store,
+                                 0, vals, bad_idx, stream);
 }
 
 int fem_assemble_tet4(const double* coords, const int64_t* conn, double E, double nu, int bs, const int32_t* inc_ptr,

@@ -91,6 +91,7 @@ class Graph:
     cols: torch.Tensor
     c2s: torch.Tensor = None     # CSR -> SELL entry map, formed on first use (csr2sell)
     dcols: torch.Tensor = None   # int16 col - row deltas, or None when the bandwidth exceeds 32767
+    max_width: int = 0           # widest SELL slice in columns (0: unknown)
 
     @property
     def csr2sell(self):
@@ -183,8 +184,9 @@ def _build_graph(elements, n_nodes, compress):
     slice_ptr = torch.empty(ns + 1, dtype=I64, device=dev)
     work64 = torch.empty(int(lib.fem_scan_work_len(ns)) + 1, dtype=I64, device=dev)
     C.check(lib.fem_scan_i64(C.ptr(width), ns, C.ptr(slice_ptr), C.ptr(work64), st), "fem_scan_i64")
-    nnz, ent, nbad, far = (int(v) for v in torch.stack([rowptr[-1].to(I64), slice_ptr[-1], bad[0].to(I64),
-                                                          ovf[0].to(I64)]).cpu())
+    sizes = torch.stack([rowptr[-1].to(I64), slice_ptr[-1], bad[0].to(I64), ovf[0].to(I64),
+                         width.max() if ns > 0 else slice_ptr[-1]])
+    nnz, ent, nbad, far, maxw = (int(v) for v in sizes.cpu())
     if nbad:   # the sync of the build; the message names the offending node like check_connectivity
         check_connectivity(elements, n_nodes)
     # int32 row pointers / column slots: the int32 scan would wrap past 2^31 entries; the int64 slice scan cannot
@@ -202,6 +204,7 @@ def _build_graph(elements, n_nodes, compress):
     del tmp
     g = Graph(n_nodes, npe, inc_ptr, inc, rowptr, colidx, diagpos, slice_ptr, cols)
     g.dcols = dcols
+    g.max_width = maxw // 64 if ns > 0 else 0   # widest slice, in columns (the value kernels' window choice)
     return g
 
 
@@ -305,12 +308,13 @@ class SellMatrix:
         bad = _dev_scalar(self.device, I64, elements.shape[0])
         store = self._fresh   # a fresh matrix is stored whole (padding zeroed): no memset, no read of the values
         self._fresh = False
-        C.check(lib.fem_assemble_tet4_ex(C.ptr(coords), C.ptr(elements), float(E), float(nu), self.bs,
-                                         C.ptr(self.g.inc_ptr), C.ptr(self.g.inc), self.g.n_nodes,
-                                         C.ptr(self.g.rowptr), C.ptr(self.g.colidx),
-                                         C.ptr(self.g.csr2sell) if os.environ.get("FEM355_ASM_ROWS") else None,
-                                         C.ptr(self.g.slice_ptr), 1 if store else 0, C.ptr(self._vals), C.ptr(bad),
-                                         C.stream(self.device)), "fem_assemble_tet4_ex")
+        C.check(lib.fem_assemble_tet4_ex2(C.ptr(coords), C.ptr(elements), float(E), float(nu), self.bs,
+                                          C.ptr(self.g.inc_ptr), C.ptr(self.g.inc), self.g.n_nodes,
+                                          C.ptr(self.g.rowptr), C.ptr(self.g.colidx),
+                                          C.ptr(self.g.csr2sell) if os.environ.get("FEM355_ASM_ROWS") else None,
+                                          C.ptr(self.g.slice_ptr), 1 if store else 0, self.g.max_width,
+                                          C.ptr(self._vals), C.ptr(bad), C.stream(self.device)),
+                "fem_assemble_tet4_ex2")
         self._bad = (bad, elements.shape[0])
         return self
 

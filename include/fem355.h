@@ -203,6 +203,13 @@ int fem_assemble_tet4_ex(const double* coords, const int64_t* conn, double E, do
                          const int32_t* inc_ptr, const int32_t* inc, int64_t N, const int32_t* rowptr,
                          const int32_t* colidx, const int64_t* csr2sell, const int64_t* slice_ptr, int store,
                          double* vals, int64_t* bad_idx, fem_stream_t stream);
+/* fem_assemble_tet4_ex with the pattern's widest slice (max over slices of (slice_ptr[s+1] - slice_ptr[s]) / 64;
+ * 0 = unknown): a P1 pattern of at most 16 columns per row takes the 16-column accumulator window (one sweep per
+ * slice, less LDS per workgroup). Same values bit for bit whatever max_width says. */
+int fem_assemble_tet4_ex2(const double* coords, const int64_t* conn, double E, double nu, int bs,
+                          const int32_t* inc_ptr, const int32_t* inc, int64_t N, const int32_t* rowptr,
+                          const int32_t* colidx, const int64_t* csr2sell, const int64_t* slice_ptr, int store,
+                          int max_width, double* vals, int64_t* bad_idx, fem_stream_t stream);
 
 /* SELL -> CSR values (export / testing): csr_vals [nnz*bs*bs] row-major blocks. */
 int fem_sell_to_csr_vals(const double* vals, int bs, const int32_t* rowptr, int64_t nrows,
