@@ -60,27 +60,38 @@ static int inb_shift(int64_t N) {   // bucket = 128 nodes, 256 when N / 128 woul
     return b;
 }
 
-// one LDS add per distinct key of the wave's first-lane group, ones for the rest; returns the lane's slot for
-// the scatter variant (base of the group + rank among the lanes of the same key)
-template <bool SCATTER>
+// one LDS add per distinct key for the first AGG key groups of the wave (the group of the lowest remaining lane,
+// found by one ballot), ones for the lanes left after them; returns the lane's slot for the scatter variant (base of
+// its group + rank among the lanes of the same key)
+#ifndef FEM_INC_AGG
+#define FEM_INC_AGG 1   // level 1 at 10M: 1 group 146 + 215 us, 4 groups 156 + 225, 8 groups 151 + 224
+#endif
+template <bool SCATTER, int AGG = 1>
 __device__ __forceinline__ int agg_add(int* lds, int key, bool valid) {
     const int lane = threadIdx.x & 63;
-    const unsigned long long mv = __ballot(valid);
-    if (!mv) return -1;
-    const int src = __ffsll((long long)mv) - 1;
-    const int k0 = __shfl(key, src, 64);
-    const bool same = valid && key == k0;
-    const unsigned long long ms = __ballot(same);
-    int base = 0;
-    if (lane == src) base = atomicAdd(&lds[k0], __popcll(ms));
-    base = __shfl(base, src, 64);
-    if (!SCATTER) {
-        if (valid && !same) atomicAdd(&lds[key], 1);
-        return 0;
-    }
     const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-    if (same) return base + __popcll(ms & lt);
-    return valid ? atomicAdd(&lds[key], 1) : -1;
+    unsigned long long rem = __ballot(valid);
+    int pos = -1;
+#pragma unroll
+    for (int g = 0; g < AGG; ++g) {
+        if (!rem) return pos;
+        const int src = __ffsll((long long)rem) - 1;
+        const int k0 = __shfl(key, src, 64);
+        const bool same = ((rem >> lane) & 1) && key == k0;
+        const unsigned long long ms = __ballot(same);
+        int base = 0;
+        if (lane == src) base = atomicAdd(&lds[k0], __popcll(ms));
+        if (SCATTER) {
+            base = __shfl(base, src, 64);
+            if (same) pos = base + __popcll(ms & lt);
+        }
+        rem &= ~ms;
+    }
+    if ((rem >> lane) & 1) {
+        const int p = atomicAdd(&lds[key], 1);
+        if (SCATTER) pos = p;
+    }
+    return pos;
 }
 
 template <bool SCATTER>
@@ -112,7 +123,7 @@ __global__ void __launch_bounds__(INB_T1) k_inc_l1(const int64_t* __restrict__ c
                 valid = false;
             }
             const int key = valid ? (int)(v >> bsh) : 0;
-            const int pos = agg_add<SCATTER>(hist, key, valid);
+            const int pos = agg_add<SCATTER, FEM_INC_AGG>(hist, key, valid);   // a wave's slots: a few buckets
             if (SCATTER && valid) {
                 knode[pos] = (int32_t)v;
                 kslot[pos] = (int32_t)i;
