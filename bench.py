@@ -300,6 +300,26 @@ def measure(a, kind, coords, tets, dev):
     iter_ms = spmv_ms if persist else spmv_ms + ms[1] / max(cnt[1], 1) + ms[2] / max(cnt[2], 1)
     s8d = s8d_models(A.n, A.g.nnz * A.bs * A.bs, spmv_ms, iter_ms, persist)
     ceiling = system.stream_ceiling(dev)
+    # the assembly's value kernel alone, outside every timed region: one launch on a fresh matrix of the same
+    # pattern (the store path of the assembly passes) between hip events on the library's stream (torch's current
+    # stream), against SURVEY §8(d)'s B_asm = 112 M + 8 nnz (conn + gathered coordinates in, every value written
+    # once; nnz counts scalar values, so x bs^2 for the block system). Skipped with --reorder (renumbered mesh).
+    asm_roof = None
+    if a.reorder != "rcm":
+        A2 = system.SellMatrix(A.g, A.bs)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        sync()
+        ev[0].record()
+        A2.add_tet4(coords, tets, E, nu)
+        ev[1].record()
+        sync()
+        vms = ev[0].elapsed_time(ev[1])
+        b_asm = 112 * M + 8 * A.g.nnz * A.bs * A.bs
+        asm_roof = {"kernel": f"k_asm_tet4_acc<{A.bs}>", "values_ms": vms, "B_asm": b_asm,
+                    "achieved_GBps": b_asm / (vms * 1e-3) / 1e9, "peak": HBM_PEAK_GBPS,
+                    "frac": b_asm / (vms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                    "model": "SURVEY 8(d) B_asm = 112 M + 8 nnz (values only; the pattern build excluded)"}
+        del A2
     workload_key = f"kuhn{a.n}_{kind}"
     out = {
         "metric": METRIC,
@@ -339,6 +359,7 @@ def measure(a, kind, coords, tets, dev):
                      "per": "iteration (whole PCG iteration in the persistent kernel)" if persist else "SpMV launch",
                      "stream_ceiling_GBps": ceiling, "frac_of_stream_read": achieved / ceiling["read"],
                      "s8d": s8d},
+        "assembly_roofline": asm_roof,
         "cpu_baseline": None,
     }
     return out
