@@ -198,7 +198,7 @@ int fem_assemble_tet4(const double* coords, const int64_t* conn, double E, doubl
                       int64_t* bad_idx, fem_stream_t stream);
 /* fem_assemble_tet4 with store != 0 for a matrix whose values were never written: every SELL value is written
  * (padding zeroed) and nothing is read, so the caller skips zeroing it. Same values bit for bit as zeroing +
- * fem_assemble_tet4 (csr2sell is not read by the default row-tile kernel; pass it for FEM355_ASM_ROWS). */
+ * fem_assemble_tet4 (csr2sell is not read by the default accumulator kernel; pass it for FEM355_ASM_ROWS). */
 int fem_assemble_tet4_ex(const double* coords, const int64_t* conn, double E, double nu, int bs,
                          const int32_t* inc_ptr, const int32_t* inc, int64_t N, const int32_t* rowptr,
                          const int32_t* colidx, const int64_t* csr2sell, const int64_t* slice_ptr, int store,
