@@ -730,9 +730,12 @@ __global__ void k_sell_zero(const int64_t* __restrict__ slice_ptr, int64_t ns, i
 // Columns past ACC_W per row: the accumulators cover the row's columns in windows of ACC_W, one sweep per window.
 // LDS strides padded (R + 1, NI + 1): a row's lanes update accumulators of different columns and read staged
 // values of different element nodes at once, which power-of-two strides put into one bank (bs = 3: 5.8 -> 3.0 ms).
-template <int R_, int J_, int LPR_, int W_, int SEG_>
+template <int R_, int J_, int LPR_, int W_, int SEG_, bool XP_ = false>
 struct AccCfg {
     static constexpr int R = R_, J = J_, LPR = LPR_, W = W_, SEG = SEG_;
+    // XP: the next batch's vertex coordinates loaded during the current batch's sweep (a third pipeline stage, 24
+    // more VGPRs: for bs = 3, whose occupancy LDS caps anyway)
+    static constexpr bool XP = XP_;
 };
 // bs = 1: lanes (row, b), 64 rows (a slice), 4 items per row per batch, 32 accumulated columns per row (10M cube:
 // 0.86 ms; 16 columns 0.79 ms but two sweeps for rows past 16 columns, 8 items per row 1.16 ms at 3 waves per SIMD).
@@ -744,7 +747,7 @@ struct AccCfg {
 using AccP1 = AccCfg<FEM_P1_CFG>;
 using AccP1w16 = AccCfg<64, 4, 4, 16, 1024>;   // patterns of at most 16 columns per row (10M cube: 0.67 vs 0.74 ms)
 #ifndef FEM_EL3_CFG
-#define FEM_EL3_CFG 16, 8, 16, 16, 512
+#define FEM_EL3_CFG 16, 8, 16, 16, 512, true
 #endif
 using AccEl = AccCfg<FEM_EL3_CFG>;
 
@@ -824,6 +827,7 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
         int ea_n = 0;
         bool v_n = false;
         int64_t cn_n[4] = {0, 0, 0, 0};
+        double xn[Cfg::XP ? 4 : 1][3];
         if (tid < NI) {
             const int t = ip_s[ir] + ij;
             v_n = t < ip_s[ir + 1];
@@ -832,12 +836,25 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
         if (v_n) {
 #pragma unroll
             for (int b = 0; b < 4; ++b) cn_n[b] = conn[4 * (int64_t)(ea_n >> 2) + b];
+            if constexpr (Cfg::XP) {
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) xn[b][q] = X[3 * cn_n[b] + q];
+            }
         }
         for (int j0 = 0; j0 < maxc; j0 += J) {
             __syncthreads();   // accumulators initialised / previous batch swept
             const bool vcur = v_n;
             const int eacur = ea_n;
             const int64_t cncur[4] = {cn_n[0], cn_n[1], cn_n[2], cn_n[3]};
+            double xc[Cfg::XP ? 4 : 1][3];
+            if constexpr (Cfg::XP) {
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) xc[b][q] = xn[b][q];
+            }
             v_n = false;
             if (tid < NI && j0 + J < maxc) {
                 const int t = ip_s[ir] + j0 + J + ij;
@@ -855,7 +872,9 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                     const int a = ea & 3;
                     const int64_t* c = cncur;
                     double g[4][3];
-                    const double det = tet4_grads_n(X, cncur, g);
+                    double det;
+                    if constexpr (Cfg::XP) det = tet4_grads_p(xc, g);
+                    else det = tet4_grads_n(X, cncur, g);
                     if (c0 == 0 && fabs(det) < 1e-12) atomicMin((unsigned long long*)bad, (unsigned long long)e);
                     const double V = fabs(det) / 6.0;
                     const int cl = rp_s[r] - seg0, cn = rp_s[r + 1] - rp_s[r];
@@ -893,7 +912,16 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                 for (int b = 0; b < 4; ++b) cn_n[b] = conn[4 * (int64_t)(ea_n >> 2) + b];
             }
             // sweep: lanes of one row are consecutive lanes of one wave, in lockstep
+#pragma unroll
             for (int jj = 0; jj < J; ++jj) {
+                if constexpr (Cfg::XP) {
+                    if (jj == J / 2 && v_n) {   // the next batch's coordinates, under the second half of the sweep
+#pragma unroll
+                        for (int b = 0; b < 4; ++b)
+#pragma unroll
+                            for (int q = 0; q < 3; ++q) xn[b][q] = X[3 * cn_n[b] + q];
+                    }
+                }
                 const int it = lr * J + jj;
                 const uint2 pp = pos_s[it];
                 const uint32_t praw = ((lb < 2 ? pp.x : pp.y) >> (16 * (lb & 1))) & 0xffffu;

@@ -16,14 +16,8 @@ __host__ __device__ inline Lame lame(double E, double nu) {
 
 // gradients of the P1 shape functions (rows of inv([1 x y z]) 1..3) and signed det of the edge matrix, from the
 // element's node ids (already loaded)
-__device__ __forceinline__ double tet4_grads_n(const double* __restrict__ X, const int64_t c[4], double g[4][3]) {
-    double p[4][3];
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-        const int64_t n = c[a];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) p[a][k] = X[3 * n + k];
-    }
+// gradients and det from the 4 vertices' coordinates
+__device__ __forceinline__ double tet4_grads_p(const double p[4][3], double g[4][3]) {
     double e1[3], e2[3], e3[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -44,6 +38,17 @@ __device__ __forceinline__ double tet4_grads_n(const double* __restrict__ X, con
         g[0][k] = -(g[1][k] + g[2][k] + g[3][k]);
     }
     return det;
+}
+
+__device__ __forceinline__ double tet4_grads_n(const double* __restrict__ X, const int64_t c[4], double g[4][3]) {
+    double p[4][3];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+        const int64_t n = c[a];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) p[a][k] = X[3 * n + k];
+    }
+    return tet4_grads_p(p, g);
 }
 
 __device__ __forceinline__ double tet4_grads(const double* __restrict__ X, const int64_t* __restrict__ c,
