@@ -745,7 +745,12 @@ struct AccCfg {
 #define FEM_P1_CFG 64, 4, 4, 32, 1024
 #endif
 using AccP1 = AccCfg<FEM_P1_CFG>;
-using AccP1w16 = AccCfg<64, 4, 4, 16, 1024>;   // patterns of at most 16 columns per row (10M cube: 0.67 vs 0.74 ms)
+#ifndef FEM_P1W16_CFG
+#define FEM_P1W16_CFG 64, 4, 4, 16, 1024
+#endif
+// patterns of at most 16 columns per row (10M cube: 0.67 vs 0.74 ms); with the coordinate prefetch (XP) 0.83 ms:
+// 107 VGPRs, 4 instead of 6 waves per SIMD
+using AccP1w16 = AccCfg<FEM_P1W16_CFG>;
 #ifndef FEM_EL3_CFG
 #define FEM_EL3_CFG 16, 8, 16, 16, 512, true
 #endif
