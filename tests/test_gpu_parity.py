@@ -902,6 +902,14 @@ def test_tile_assembly_bit_identical_to_row_kernels(gpu, case, monkeypatch):
             A.add_tet4(cg, tg, Ek, NU)
             out.append((first, A.vals.clone()))
         monkeypatch.delenv("FEM355_ASM_ROWS", raising=False)
+        if bs == 1 and case in ("kuhn", "twice"):   # the 16-column window (max_width <= 16) vs the 32-column one
+            assert 0 < g.max_width <= 16
+            mw, g.max_width = g.max_width, 0
+            A32 = system.SellMatrix(g, bs)
+            A32.add_tet4(cg, tg, Ek, NU)
+            g.max_width = mw
+            assert torch.equal(A32.vals, out[0][0]), case
+            del A32
         if case == "repeated":   # the singular element's entries are NaN in both (payloads may differ)
             for i in (0, 1):
                 na, nb = torch.isnan(out[0][i]), torch.isnan(out[1][i])
