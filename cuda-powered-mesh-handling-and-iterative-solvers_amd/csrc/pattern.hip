@@ -97,7 +97,7 @@ __device__ __forceinline__ int agg_add(int* lds, int key, bool valid) {
 template <bool SCATTER>
 __global__ void __launch_bounds__(INB_T1) k_inc_l1(const int64_t* __restrict__ conn, int64_t total, int64_t N, int bsh,
                                                 int nb, int32_t* __restrict__ cnt, const int32_t* __restrict__ off,
-                                                int32_t* __restrict__ knode, int32_t* __restrict__ kslot,
+                                                int2* __restrict__ kpair,
                                                 int32_t* __restrict__ bad) {
     extern __shared__ int hist[];
     const int G = gridDim.x, b = blockIdx.x;
@@ -125,8 +125,7 @@ __global__ void __launch_bounds__(INB_T1) k_inc_l1(const int64_t* __restrict__ c
             const int key = valid ? (int)(v >> bsh) : 0;
             const int pos = agg_add<SCATTER, FEM_INC_AGG>(hist, key, valid);   // a wave's slots: a few buckets
             if (SCATTER && valid) {
-                knode[pos] = (int32_t)v;
-                kslot[pos] = (int32_t)i;
+                kpair[pos] = make_int2((int32_t)v, (int32_t)i);   // (node, slot): one 8-byte store
             }
         }
     }
@@ -137,7 +136,7 @@ __global__ void __launch_bounds__(INB_T1) k_inc_l1(const int64_t* __restrict__ c
 }
 
 // level 2: one workgroup per bucket; boff = the level-1 scan (bucket q's entries [boff[q G], boff[(q + 1) G]))
-__global__ void __launch_bounds__(256) k_inc_l2(const int32_t* __restrict__ knode, const int32_t* __restrict__ kslot,
+__global__ void __launch_bounds__(256) k_inc_l2(const int2* __restrict__ kpair,
                                                 const int32_t* __restrict__ boff, int G, int64_t N, int bsh,
                                                 int32_t* __restrict__ scratch, int32_t* __restrict__ inc_ptr,
                                                 int32_t* __restrict__ inc) {
@@ -163,8 +162,9 @@ __global__ void __launch_bounds__(256) k_inc_l2(const int32_t* __restrict__ knod
 #pragma unroll
         for (int u = 0; u < EPT; ++u) {
             const int e = u * 256 + threadIdx.x;
-            kn_r[u] = e < n ? knode[lo + e] : 0;
-            ks_r[u] = e < n ? kslot[lo + e] : 0;
+            const int2 kp = e < n ? kpair[lo + e] : make_int2(0, 0);
+            kn_r[u] = kp.x;
+            ks_r[u] = kp.y;
         }
 #pragma unroll
         for (int u = 0; u < EPT; ++u) {
@@ -181,7 +181,7 @@ __global__ void __launch_bounds__(256) k_inc_l2(const int32_t* __restrict__ knod
         for (int e0 = wid * 64; e0 < n; e0 += 256) {
             const int e = e0 + lane;
             const bool valid = e < n;
-            const int kn = valid ? (int)(knode[lo + e] - node0) : 0;
+            const int kn = valid ? (int)(kpair[lo + e].x - node0) : 0;
             agg_add<false>(cnt, kn, valid);
         }
     }
@@ -228,9 +228,10 @@ __global__ void __launch_bounds__(256) k_inc_l2(const int32_t* __restrict__ knod
         for (int e0 = wid * 64; e0 < n; e0 += 256) {
             const int e = e0 + lane;
             const bool valid = e < n;
-            const int kn = valid ? (int)(knode[lo + e] - node0) : 0;
+            const int2 kp = valid ? kpair[lo + e] : make_int2(0, 0);
+            const int kn = valid ? (int)(kp.x - node0) : 0;
             const int p = agg_add<true>(cnt, kn, valid);
-            if (valid) scratch[lo + p] = kslot[lo + e];
+            if (valid) scratch[lo + p] = kp.y;
         }
     }
     __syncthreads();
@@ -814,24 +815,23 @@ static int incidence_bucket(const int64_t* conn, int64_t total, int64_t N, int32
     const int nb = (int)((N + ((int64_t)1 << bsh) - 1) >> bsh);
     const int64_t ncnt = (int64_t)nb * INB_G1;
     const size_t a4 = align256(sizeof(int32_t) * total), ac = align256(sizeof(int32_t) * (ncnt + 1));
-    int32_t* knode = reinterpret_cast<int32_t*>(base);
-    int32_t* kslot = reinterpret_cast<int32_t*>(base + a4);
+    int2* kpair = reinterpret_cast<int2*>(base);   // (node, slot) pairs: the first two int32 arrays' space
     int32_t* scratch = reinterpret_cast<int32_t*>(base + 2 * a4);
     int32_t* cnt = reinterpret_cast<int32_t*>(base + 3 * a4);
     int32_t* off = reinterpret_cast<int32_t*>(base + 3 * a4 + ac);
     int32_t* swork = reinterpret_cast<int32_t*>(base + 3 * a4 + 2 * ac);
     const size_t l1 = sizeof(int) * (size_t)nb;
     hipLaunchKernelGGL(k_inc_l1<false>, dim3(INB_G1), dim3(INB_T1), l1, st, conn, total, N, bsh, nb, cnt,
-                       (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, bad);
+                       (const int32_t*)nullptr, (int2*)nullptr, bad);
     FEM_LAUNCHED();
     int rc = fem_scan_i32(cnt, ncnt, off, swork, stream);
     if (rc != FEM_OK) return rc;
     hipLaunchKernelGGL(k_inc_l1<true>, dim3(INB_G1), dim3(INB_T1), l1, st, conn, total, N, bsh, nb, (int32_t*)nullptr,
-                       off, knode, kslot, (int32_t*)nullptr);
+                       off, kpair, (int32_t*)nullptr);
     FEM_LAUNCHED();
     const int B = 1 << bsh;
     const size_t l2 = sizeof(int) * (size_t)(2 * B + 1 + 2 * INB_CAP) + 2 * (size_t)INB_CAP;
-    hipLaunchKernelGGL(k_inc_l2, dim3((unsigned)nb), dim3(256), l2, st, knode, kslot, off, INB_G1, N, bsh, scratch,
+    hipLaunchKernelGGL(k_inc_l2, dim3((unsigned)nb), dim3(256), l2, st, kpair, off, INB_G1, N, bsh, scratch,
                        inc_ptr, inc);
     FEM_LAUNCHED();
     return FEM_OK;
