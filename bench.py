@@ -8,15 +8,16 @@ Workload: Kuhn-cube mesh n=119 -> 10,110,954 P1 tets, 1,728,0
     `value` = steps/s of the whole job (for N>1: the same global system element-partitioned over the ranks,
     strong scaling), measured between barrier+synchronize brackets, max over ranks.
   * DOFs/s = n_DOF / (assembly incl. pattern build + PCG solve to rtol 1e-8 on sqrt(r.z)), reported beside:
-    steady state (`dofs_per_s`: median assembly + median solve of --dof-passes identical passes after the first,
-    all listed in `dofs_passes_ms`) and first use (`dofs_per_s_cold`, which also pays the device allocations of this mesh size).
+    steady state (`dofs_per_s`: the median by total of --dof-passes identical passes after the first, all listed in
+    `dofs_passes_ms`; `dofs_per_s_split_medians`: median assembly + median solve) and first use (`dofs_per_s_cold`, which also pays the device allocations of this mesh size).
   * roofline: the dominant kernel of the active schedule, algorithmic bytes (8 + idx) nnz + 4 (n+1) + 16 n
     (§8(d); idx = 2 for 16-bit deltas, 4 for int32) over its device time measured live with hip events on the
     solver stream inside the timed region. bs=1 default (persistent schedule, k_pcg_persist): per ITERATION —
     the whole PCG iteration moves just those bytes (matrix, u gather, u store); other schedules: per SpMV launch
     (k_pcg_d1 deferred, k_pcg_spmv_dot three-kernel).
   * cpu_baseline: the oracle (torch-CPU restatement of the reference's EBE PCG, oracle/ref_cpu.py) timed on the
-    host cores on a bounded sample (assembly + a few iterations of the same 10M system), rank 0 at N=1 only.
+    host cores on a bounded sample of the same 10M system (element assembly, EBE matvec, 10 PCG iterations), rank 0
+    at N=1 only; the assembly + solve wall it implies for the GPU line's iteration count is projected beside it.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 """
@@ -52,14 +53,14 @@ def parse():
     ap.add_argument("--rtol", type=float, default=1e-8)
     ap.add_argument("--dof-passes", type=int, default=3,
                     help="steady-state assembly + solve passes after the cold one; DOFs/s is the median pass")
-    ap.add_argument("--cpu-iters", type=int, default=3)
+    ap.add_argument("--cpu-iters", type=int, default=10, help="CPU-baseline PCG iterations (Poisson)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--elastic", type=int, default=1,
                     help="poisson runs: also measure the 10M-tet linear-elasticity system (BASELINE configs[2]/[3]) "
                          "with the same steps, reported under \"elasticity\" in the same JSON line")
     ap.add_argument("--elastic-timeout", type=float, default=240.0,
                     help="seconds the elasticity companion may take before the line is printed without it")
-    ap.add_argument("--cpu-iters-elastic", type=int, default=2)
+    ap.add_argument("--cpu-iters-elastic", type=int, default=10, help="CPU-baseline PCG iterations (elasticity)")
     ap.add_argument("--schedule", type=int, default=None, help="PCG kernel schedule (0 three-kernel, 1 fused, 2 deferred, 3 persistent; "
                     "default: persistent for bs=1, three-kernel for bs=3)")
     ap.add_argument("--graph", type=int, default=0, help="capture k iterations per hipGraph (0 = plain launches)")
@@ -123,26 +124,78 @@ def s8d_models(n, nnz, spmv_ms, iter_ms, persist):
             "frac_iter": b_iter / (iter_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
 
 
-def cpu_baseline(n, kind, iters):
-    """Oracle (reference op sequence on torch-CPU) on the same mesh: assembly + `iters` EBE-PCG iterations."""
+def cpu_threads():
+    """Host threads for the CPU baseline and what they are based on (torch.set_num_threads with the
+    core count stated). The affinity mask sizes it; a thread cap in the environment (OMP_NUM_THREADS: the GPU box
+    sets 16, its CPU share, while the mask and os.cpu_count() show the whole machine) bounds it."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = os.environ.get("OMP_NUM_THREADS", "")
+    threads = min(aff, int(cap)) if cap.isdigit() and int(cap) > 0 else aff
+    quota = None
+    try:
+        q = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q and q[0] != "max":
+            quota = int(q[0]) / int(q[1])
+    except (OSError, ValueError, IndexError):
+        pass
+    return threads, {"affinity_cpus": aff, "os_cpu_count": os.cpu_count(), "omp_num_threads": cap or None,
+                     "cgroup_cpu_quota": quota}
+
+
+def cpu_baseline(n, kind, iters, solve_iters=None):
+    """Oracle (the reference's op sequence on torch-CPU, oracle/ref_cpu.py) on the same mesh, BASELINE.md §3's
+    three numbers: element assembly (`compute_c3d4_K_matrix`, `solver/element.py:883-903`), the EBE matvec
+    (`compute_nodal_forces`, `:429-464`) and `iters` Jacobi-PCG iterations (`solver/solver.py:766-812`), timed
+    on the host cores with torch.set_num_threads(threads) (cpu_threads). The assembly + fixed-iteration wall is
+    measured; the wall of the GPU line's whole solve (solve_iters iterations) is projected from the iteration rate."""
     from oracle import ref_cpu as R
-    coords, tets = mesh.kuhn_cube(n)
-    threads = torch.get_num_threads()
-    t0 = time.perf_counter()
-    K = R.tet4_poisson_K(coords, tets) if kind == "poisson" else R.tet4_K(coords, tets, 113.8e9, 0.342)
-    t_asm = time.perf_counter() - t0
-    N = coords.shape[0]
-    dpn = 1 if kind == "poisson" else 3
-    f, fixed = mesh.cube_poisson_case(coords) if kind == "poisson" else mesh.cube_elasticity_case(coords)
-    Minv = R.diag_preconditioner(K, tets, N, dpn=dpn)
-    Minv[fixed] = 0.0
-    t0 = time.perf_counter()
-    R.pcg(K, tets, f.view(N, dpn), Minv, tol=0.0, max_iter=iters)
-    t_it = time.perf_counter() - t0
-    return {"value": iters / t_it, "unit": "CG iterations/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
-            "sample": f"oracle/ref_cpu.py torch-CPU EBE Jacobi-PCG on the same {tets.shape[0]:,}-tet {kind} system: "
-                      f"{iters} iterations after element assembly ({t_asm:.2f} s) + setup; fp64",
-            "assembly_s": t_asm}
+    threads, tinfo = cpu_threads()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        coords, tets = mesh.kuhn_cube(n)
+        t0 = time.perf_counter()
+        K = R.tet4_poisson_K(coords, tets) if kind == "poisson" else R.tet4_K(coords, tets, 113.8e9, 0.342)
+        t_asm = time.perf_counter() - t0
+        N = coords.shape[0]
+        dpn = 1 if kind == "poisson" else 3
+        f, fixed = mesh.cube_poisson_case(coords) if kind == "poisson" else mesh.cube_elasticity_case(coords)
+        t0 = time.perf_counter()
+        Minv = R.diag_preconditioner(K, tets, N, dpn=dpn)
+        Minv[fixed] = 0.0
+        t_setup = time.perf_counter() - t0
+        p = torch.ones(N, dpn, dtype=torch.float64)
+        R.nodal_forces(K, tets, p)                     # first touch of the gather / scatter buffers
+        reps = 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            R.nodal_forces(K, tets, p)
+        t_mv = (time.perf_counter() - t0) / reps
+        t0 = time.perf_counter()
+        R.pcg(K, tets, f.view(N, dpn), Minv, tol=0.0, max_iter=iters)
+        t_it = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(prev)
+    out = {"value": iters / t_it, "unit": "CG iterations/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
+           "threads_basis": tinfo,
+           "sample": f"oracle/ref_cpu.py torch-CPU (the reference's op sequence) on the same {tets.shape[0]:,}-tet "
+                     f"{kind} system: element assembly, {reps} EBE matvecs, {iters} Jacobi-PCG iterations; fp64",
+           "assembly_s": t_asm, "setup_s": t_setup, "ebe_matvec_ms": t_mv * 1e3, "cg_iters": iters,
+           "cg_s": t_it, "assembly_plus_fixed_iters_wall_s": t_asm + t_setup + t_it}
+    if solve_iters:
+        out["solve_iters"] = solve_iters
+        out["projected_assembly_plus_solve_wall_s"] = t_asm + t_setup + solve_iters * t_it / iters
+    return out
+
+
+def attach_cpu_baseline(out, cb):
+    """cpu_baseline into the bench dict, with the assembly + solve wall-clock ratio GPU vs CPU (north_star: >= 10x
+    the reference CPU's assembly + CG wall-clock at 1 GPU) -- same system, same iteration count to rtol."""
+    out["cpu_baseline"] = cb
+    proj = cb.get("projected_assembly_plus_solve_wall_s")
+    gpu_s = (out.get("assembly_ms", 0.0) + out.get("solve_ms", 0.0)) * 1e-3
+    if proj and gpu_s > 0:
+        out["vs_cpu_assembly_plus_solve"] = proj / gpu_s
 
 
 def main():
@@ -176,7 +229,7 @@ def main():
         coords, tets = permute_nodes(coords, tets, a.permute)
     out = measure(a, a.kind, coords, tets, dev)
     if not a.no_cpu_baseline and rank == 0:
-        out["cpu_baseline"] = cpu_baseline(a.n, a.kind, a.cpu_iters)
+        attach_cpu_baseline(out, cpu_baseline(a.n, a.kind, a.cpu_iters, out["solve_iters"]))
     # BASELINE configs[2] beside the metric: the same steps on the 10M-tet linear-elasticity system (north_star:
     # CG it/s on elasticity at 1/2/4/8 GPUs), its own CPU-oracle sample; a failure is reported, never fatal
     if a.kind == "poisson" and a.elastic:
@@ -185,7 +238,7 @@ def main():
         def companion():
             d = measure(a, "elastic", coords, tets, dev)
             if not a.no_cpu_baseline:
-                d["cpu_baseline"] = cpu_baseline(a.n, "elastic", a.cpu_iters_elastic)
+                attach_cpu_baseline(d, cpu_baseline(a.n, "elastic", a.cpu_iters_elastic, d["solve_iters"]))
             return d
         guard = dist.CompanionGuard(out, "elasticity", rank=0, timeout=a.elastic_timeout)
         guard.run(companion)
@@ -254,11 +307,12 @@ def measure(a, kind, coords, tets, dev):
         A, w, b, res, t_asm, t_solve = assemble_and_solve()
         assert res.iterations == res_cold.iterations and res.status == res_cold.status
         passes.append((t_asm, t_solve))
-    # steady state: the median assembly time and the median solve time of the passes (every pass repeats the whole
-    # work; one pass's assembly can pay a first-use allocation of the caching allocator, and the solve times vary
-    # by a few percent from box to box, so a median pass by the sum can carry the assembly outlier)
-    t_asm = sorted(p[0] for p in passes)[len(passes) // 2]
-    t_solve = sorted(p[1] for p in passes)[len(passes) // 2]
+    # steady state: the median pass by its assembly + solve total (a measured pass: dofs_per_s, assembly_ms and
+    # solve_ms all come from it); the medians of the assembly times and of the solve times taken separately (they
+    # may come from different passes) are reported beside it
+    t_asm, t_solve = sorted(passes, key=lambda p: p[0] + p[1])[len(passes) // 2]
+    t_asm_med = sorted(p[0] for p in passes)[len(passes) // 2]
+    t_solve_med = sorted(p[1] for p in passes)[len(passes) // 2]
 
     # ---- fixed-iteration timing (the metric)
     run = system.PcgRunner(A, b, w, tol=0.0, schedule=a.schedule)
@@ -342,6 +396,9 @@ def measure(a, kind, coords, tets, dev):
         "assembly_ms": t_asm * 1e3,
         "solve_ms": t_solve * 1e3,
         "dofs_passes_ms": [[round(x * 1e3, 4), round(y * 1e3, 4)] for x, y in passes],
+        "dofs_per_s_split_medians": A.n / (t_asm_med + t_solve_med),
+        "assembly_ms_median": t_asm_med * 1e3,
+        "solve_ms_median": t_solve_med * 1e3,
         "dofs_per_s_cold": A.n / (t_asm_cold + t_solve_cold),
         "assembly_ms_cold": t_asm_cold * 1e3,
         "solve_ms_cold": t_solve_cold * 1e3,

@@ -24,6 +24,7 @@ PCG_RUNNING, PCG_CONVERGED, PCG_MAXITER, PCG_BREAKDOWN, PCG_ALPHA_NAN, PCG_BETA_
 MODE_CG_STABLE, MODE_PCG, MODE_CG_CONSTRAINED = 0, 1, 2
 # include/fem355.h FEM_TUNE_*: the library's default set for a new context, and the merged-update flag
 TUNE_UPD1 = 1024
+TUNE_U2_HOLD, TUNE_U2_SMALL = 2048, 4096   # test-only knobs of the merged update (include/fem355.h)
 TUNE_DEFAULT = 1 | 2 | 4 | 8 | 128 | TUNE_UPD1
 KIND_ELASTIC, KIND_POISSON, KIND_MASS = 0, 1, 2
 ISO_SUM, ISO_STACK, ISO_VOLUME, ISO_MASS = 0, 1, 2, 3
@@ -114,6 +115,7 @@ SIGNATURES = {
     "fem_pcg_set_entries": (_I, [_P, _L]),
     "fem_pcg_get_schedule": (_I, [_P]),
     "fem_pcg_uniform_slices": (_I, [_P, _L, _L, _P, _P, _P]),
+    "fem_pcg_persist_build": (_I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_I)]),
     "fem_pcg_persist_profile": (_I, [_P, _I, _P, ctypes.POINTER(_I)]),
     "fem_pcg_set_constraints": (_I, [_P, _I, _L, _P, _P, _L, _P, _P, _L, _P, _P, _P, _P, _P]),
     "fem_enforce_constraints": (_I, [_P, _P, _L, _I, _L, _P, _P, _L, _P, _P, _L, _P, _P, _P, _P, _P, _P]),

@@ -442,18 +442,35 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_pupdate(int64_t n, double* __
 // two kernels' 10) and one launch boundary fewer. Every workgroup must be resident at once: the grid is sized from
 // the occupancy query (u2_setup); the wait is bounded in time (FEM_PCG_SYNC_TIMEOUT, never a hang).
 constexpr int U2_NPT = 8;                 // double2 elements per thread whose z stays in registers
-enum { U2_REL = 0, U2_BC = 32, U2_TMO = 64, U2_WORDS = 96 };   // release word, broadcast (beta, halt), give-up
+enum { U2_REL = 0, U2_BC = 32, U2_WORDS = 96 };   // release word, broadcast (beta, halt)
+constexpr unsigned U2_GIVEUP = 0xffffffffu;        // release-word value of a launch a waiter gave up on
 constexpr uint64_t U2_WAIT_TICKS = 200000000ull;   // 2 s of s_memrealtime (100 MHz)
+// sync-site code of a merged-update give-up (fem_pcg_sync_site; the persistent kernel's codes are 1-3)
+constexpr int U2_SITE = 4;
+
+// the give-up verdict (status, halt, site) with atomic stores: every writer of a given launch stores the same values
+__device__ __forceinline__ void u2_give_up(PcgState* st, unsigned e) {
+    __hip_atomic_store(&st->stop_iter, U2_SITE + 16 * (int)(e & 0x7ffffffu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&st->status, (int)FEM_PCG_SYNC_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&st->halt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update2(int64_t n, double* __restrict__ x, double* __restrict__ p,
                                                            double* __restrict__ r, const double* __restrict__ q,
                                                            const double* __restrict__ w, PcgState* __restrict__ st,
                                                            RedBuf red, double* __restrict__ hist, int64_t hist_len,
-                                                           unsigned* __restrict__ sync) {
+                                                           unsigned* __restrict__ sync, int hold) {
     __shared__ double lds4[4];
     __shared__ int flag;
     __shared__ double bc_s[2];
     if (st->halt || st->iter >= st->max_iter) return;
+    if (hold && blockIdx.x == 0) {   // FEM_TUNE_U2_HOLD (tests): workgroup 0 arrives after every waiter gave up
+        if (threadIdx.x == 0) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__builtin_amdgcn_s_memrealtime() - t0 < U2_WAIT_TICKS + U2_WAIT_TICKS / 2) __builtin_amdgcn_s_sleep(127);
+        }
+        __syncthreads();
+    }
     const unsigned e = st->u2_epoch + 1;
     const double alpha = st->alpha;
     const bool cg = st->mode != FEM_MODE_PCG;
@@ -508,36 +525,59 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update2(int64_t n, double* __
     double rz_new;
     const bool last = reduce_grid(acc, red.part(RED_K2), red.cnt(RED_K2), &rz_new, lds4, &flag);
     if (threadIdx.x == 0) {
+        // The release word decides the launch ONCE, by compare-and-swap from the previous epoch (e - 1): the last
+        // workgroup swaps in e (release), a waiter that gave up swaps in U2_GIVEUP. Whichever swap lands first
+        // wins, so either every workgroup applies the x / p update or none does (then r holds r_{k+1} and x x_k,
+        // the status is FEM_PCG_SYNC_TIMEOUT with the give-up site, and fem_pcg_solve re-solves from x0).
         double beta = 0.0, halt = 0.0;
         bool ok = true;
         if (last) {
+            const int it0 = st->iter;
             finish_rz(st, rz_new, hist, hist_len);
             beta = st->beta;
             halt = st->halt ? 1.0 : 0.0;
             __hip_atomic_store(reinterpret_cast<double*>(sync + U2_BC), beta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(reinterpret_cast<double*>(sync + U2_BC) + 1, halt, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+            // the broadcast's write-through stores drained before the release (the guide's sc1 hand-off form; the
+            // asm's memory clobber also keeps the compiler from moving them past the swap)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(sync + U2_REL, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            unsigned expect = e - 1;
+            if (!__hip_atomic_compare_exchange_strong(sync + U2_REL, &expect, e, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT)) {
+                // a waiter gave up first: undo the commit (the iteration did not complete) and keep its verdict
+                st->iter = it0;
+                u2_give_up(st, e);
+                ok = false;
+            }
         } else {
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            unsigned v = 0;
             for (unsigned spins = 0;; ++spins) {
-                if (__hip_atomic_load(sync + U2_REL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= e) break;
+                v = __hip_atomic_load(sync + U2_REL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (v != e - 1) break;   // released (e) or given up (U2_GIVEUP)
                 if ((spins & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > U2_WAIT_TICKS) {
-                    ok = false;
+                    unsigned expect = e - 1;
+                    if (__hip_atomic_compare_exchange_strong(sync + U2_REL, &expect, U2_GIVEUP, __ATOMIC_RELAXED,
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                        v = U2_GIVEUP;   // a workgroup that never became resident: stop instead of hanging
+                    else
+                        v = expect;      // the release landed first
                     break;
                 }
                 __builtin_amdgcn_s_sleep(2);
             }
-            if (ok) {
+            // no load below may be moved above the poll by the compiler (the hardware issues it only after the
+            // branch on the polled value); the broadcast is read with write-through (sc1) loads
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (v == e) {
                 beta = __hip_atomic_load(reinterpret_cast<const double*>(sync + U2_BC), __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT);
                 halt = __hip_atomic_load(reinterpret_cast<const double*>(sync + U2_BC) + 1, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT);
-            } else {   // a workgroup that never became resident: stop the solve instead of hanging
-                __hip_atomic_store(sync + U2_TMO, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                st->status = FEM_PCG_SYNC_TIMEOUT;
-                st->halt = 1;
+            } else {
+                u2_give_up(st, e);
+                ok = false;
             }
         }
         bc_s[0] = beta;
@@ -1968,6 +2008,7 @@ static int u2_setup(fem_pcg* s) {
     if (per_cu < 0) return FEM_OK;   // no resident grid: the two-kernel update stays
     int64_t want = cdiv(s->n / 2 + 1, PCG_BLOCK);
     want = cdiv(want, NXCD) * NXCD;
+    if (s->tune & FEM_TUNE_U2_SMALL) want = NXCD;   // tests: past the register-cached elements at small n
     s->u2_grid = (int)(want < per_cu ? want : per_cu);
     if (!s->u2_sync) {
         hipError_t e = pool_alloc((void**)&s->u2_sync, sizeof(unsigned) * U2_WORDS, s->stream, s->bs == 1);
@@ -1983,7 +2024,7 @@ static int u2_setup(fem_pcg* s) {
 
 static int launch_update2(fem_pcg* s) {
     hipLaunchKernelGGL(k_pcg_update2, dim3(s->u2_grid), dim3(PCG_BLOCK), 0, s->stream, s->n, s->x, s->p0, s->r, s->q,
-                       s->w, s->st, s->red, s->hist, s->hist_len, s->u2_sync);
+                       s->w, s->st, s->red, s->hist, s->hist_len, s->u2_sync, (s->tune & FEM_TUNE_U2_HOLD) ? 1 : 0);
     FEM_LAUNCHED();
     return FEM_OK;
 }
@@ -2865,6 +2906,31 @@ static int launch_persist(fem_pcg* s, int k, unsigned long long* prof) {
         FEM_HIP(hipLaunchKernel(fn, dim3(G), dim3(PK_T), args, persist_lds(s), s->stream));
     FEM_LAUNCHED();
     s->launched += k;
+    return FEM_OK;
+}
+
+int fem_pcg_persist_build(fem_pcg* s, int* slots, int* overflow, int* pack) {
+    *slots = 0;
+    *overflow = 0;
+    *pack = 0;
+    if (!s->persist || s->pk_grid <= 0) return FEM_OK;
+    const int G = s->pk_grid;
+    int64_t ns = s->nslices;
+    if (s->pd) ns = s->pd_split[s->pd_rank + 1] - s->pd_split[s->pd_rank];
+    const int64_t maxL = (ns + G - 1) / G;
+    const int pk = (int)((maxL + PK_WAVES - 1) / PK_WAVES);
+    *overflow = s->pk_ovf;
+    *pack = (s->bs == 3 || s->pd || (s->tune & FEM_TUNE_PK_PACK)) ? pk : 0;
+    // the same selection as launch_persist (persist_fn / persist_fn_dist / persist3_fn, non-instrumented)
+    if (s->bs == 3) {
+        *slots = P3_MAXS;
+    } else if (s->pd) {
+        *slots = pk <= 1 ? 1 : pk == 2 ? 2 : pk <= PK_MAXS_DIST ? PK_MAXS_DIST : PK_MAXS;
+    } else {
+        const int small = (*pack <= 4 && !(s->tune & FEM_TUNE_PK_WIDE)) ? *pack : 0;
+        *slots = (small >= 1 && small <= 4 && !s->pk_ovf && (s->tune & FEM_TUNE_PK_SC1))
+                     ? (small == 1 ? 1 : small == 2 ? 2 : 4) : PK_MAXS;
+    }
     return FEM_OK;
 }
 

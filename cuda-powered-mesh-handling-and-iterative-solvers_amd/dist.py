@@ -290,8 +290,9 @@ class PartitionGroup:
         C.check(self.lib.fem_p2p_deliver(arr, len(runs), C.stream(self.dev)), "fem_p2p_deliver")
 
     def solve(self, bs_local, ws, tol, max_iter, mode=C.MODE_PCG, variant=None, exchange=EXCHANGE_ALLREDUCE,
-              fused=False):
-        """Phase-driven (P)CG over the P partitions; returns (per-rank x, iterations, status)."""
+              fused=False, fixed=False):
+        """Phase-driven (P)CG over the P partitions; returns (per-rank x, iterations, status).
+        fixed: exactly `max_iter` iteration passes (x_k after k iterations; no stop-test pass after the last)."""
         # every context on the current stream: the phases of all ranks and the group sums serialise in order
         variant = VARIANT_SINGLE if variant is None else int(variant)
         runs = [_GroupRunner(r, b, w, tol, mode, variant, exchange, fused)
@@ -315,10 +316,10 @@ class PartitionGroup:
             step(ph)
         it = 0
         # the single-reduction form tests convergence at the start of the next iteration: one extra pass
-        for it in range(max_iter + (1 if variant == VARIANT_SINGLE else 0)):
+        for it in range(max_iter + (1 if variant == VARIANT_SINGLE and not fixed else 0)):
             for ph in iteration:
                 step(ph)
-            if (it + 1) % 16 == 0:
+            if not fixed and (it + 1) % 16 == 0:
                 i_, s_, _ = runs[0].poll()
                 if s_ != C.PCG_RUNNING:
                     break
@@ -523,6 +524,9 @@ def bench_main(a, metric):
         out, _ = run_chain(path, same_gpu, lambda: persist("poisson"), lambda: rccl("poisson"), rank)
     else:
         out = rccl(a.kind)
+    drop = os.environ.get("FEM355_DIST_DROP_RANK", "")
+    if drop and rank == 0 and isinstance(out, dict):   # a fault-injected run is labelled as such in its line
+        out.setdefault("config", {})["fault_injection"] = f"FEM355_DIST_DROP_RANK={drop}"
     guard = None
     if a.kind == "poisson" and getattr(a, "elastic", 0):
         def companion():

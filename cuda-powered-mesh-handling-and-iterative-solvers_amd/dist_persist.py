@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 from dataclasses import dataclass
 
 import torch
@@ -100,6 +101,9 @@ class RankRunner:
             # this rank publishes nothing; FEM355_DIST_DROP_RANK=r selects rank r from the environment
             if drop is None:
                 drop = os.environ.get("FEM355_DIST_DROP_RANK", "") == str(rank)
+                if drop:   # fault injection from the environment is never silent (bench.py labels its line too)
+                    print(f"[rank {rank}] FAULT INJECTION ACTIVE: FEM355_DIST_DROP_RANK={rank} -- this rank publishes "
+                          "nothing; every persistent multi-GPU launch will time out", file=sys.stderr, flush=True)
             if fine or drop:
                 C.check(self.lib.fem_pcg_set_tuning(self.h, self.TUNE_DEFAULT | (self.TUNE_DIST_FINE if fine else 0)
                                                     | (self.TUNE_DIST_DROP if drop else 0)), "fem_pcg_set_tuning")

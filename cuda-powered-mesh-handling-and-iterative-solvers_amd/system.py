@@ -482,6 +482,14 @@ class PcgRunner:
         [s_begin, s_end) of the context's matrix copy (after start())."""
         return uniform_slices(self.lib, self.h, s_begin, s_end)
 
+    def persist_build(self):
+        """(register slots per wave, overflow build, packed slices per wave) of the persistent launches (after
+        start(); zeros when the context does not run schedule 3)."""
+        sl, ov, pk = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        C.check(self.lib.fem_pcg_persist_build(self.h, ctypes.byref(sl), ctypes.byref(ov), ctypes.byref(pk)),
+                "fem_pcg_persist_build")
+        return sl.value, ov.value, pk.value
+
     def profile(self, k, every=1):
         """k iterations with hip events around the kernels of every `every`-th one -> (ms sums, counts)."""
         ms = (ctypes.c_double * 3)()

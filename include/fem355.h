@@ -381,8 +381,9 @@ int fem_pcg_iterate(fem_pcg* s, int k);
 /* [sync] read iteration count, status and last r.z (or r.r). Guard stops (FEM_PCG_BREAKDOWN / _ALPHA_NAN) report
  * the reference's printed iteration; every other status the completed iterations */
 int fem_pcg_poll(fem_pcg* s, int* iters, int* status, double* rz);
-/* [sync] diagnostic of a FEM_PCG_SYNC_TIMEOUT: the persistent kernel's give-up site code (1 grid barrier,
- * 2 u-flag window, 3 rank sums of the DIST build; + 16 * epoch), 0 for any other status */
+/* [sync] diagnostic of a FEM_PCG_SYNC_TIMEOUT: the give-up site code (persistent kernel: 1 grid barrier, 2 u-flag
+ * window, 3 rank sums of the DIST build, + 16 * epoch; merged update k_pcg_update2: 4 + 16 * launch since start),
+ * 0 for any other status */
 int fem_pcg_sync_site(fem_pcg* s, int* site);
 /* [sync] out6 = {rz (rs_old), pq (p.Ap), alpha, beta, rz_new, completed iterations} for the host messages */
 int fem_pcg_scalars(fem_pcg* s, double* out6);
@@ -409,6 +410,10 @@ int fem_pcg_get_schedule(fem_pcg* s);
  * SpMV over those slices reads (padding included) */
 int fem_pcg_uniform_slices(fem_pcg* s, int64_t s_begin, int64_t s_end, int64_t* uniform, int64_t* nslices,
                            int64_t* index_bytes);
+/* [host] the persistent build the context's launches run (valid after fem_pcg_start; all 0 when the schedule is not
+ * 3): register slots per wave (bs = 1: 1, 2, 4 or 7; bs = 3: 2), 1 for the overflow build, and the packed
+ * assignment's slices per wave (0: the even spread) */
+int fem_pcg_persist_build(fem_pcg* s, int* slots, int* overflow, int* pack);
 /* persistent schedule only: k iterations of the instrumented kernel build; host_out[G * 8] = per-workgroup shader-clock
  * sums of the phases (u wait, SpMV, block sum, barrier + partial sums, step, update + drain + flag, launch prologue,
  * launch epilogue), then host_out[G * 8 + G * 16] = every wave's own SpMV clock sum; *grid = G */
@@ -440,7 +445,11 @@ int fem_enforce_constraints(double* x, double* r, int64_t n, int order, int64_t 
  * order of the per-block p.q partials (deterministic for a given flag set). */
 enum { FEM_TUNE_REVERSE = 1, FEM_TUNE_PAIR = 2, FEM_TUNE_PK_SC1 = 4, FEM_TUNE_PK_PACK = 8, FEM_TUNE_C1F = 16,
        FEM_TUNE_PK_COOP = 32, FEM_TUNE_DIST_FINE = 64, FEM_TUNE_PK_UNI = 128, FEM_TUNE_PK_WIDE = 256,
-       FEM_TUNE_DIST_DROP = 512, FEM_TUNE_UPD1 = 1024 };
+       FEM_TUNE_DIST_DROP = 512, FEM_TUNE_UPD1 = 1024, FEM_TUNE_U2_HOLD = 2048, FEM_TUNE_U2_SMALL = 4096 };
+/* FEM_TUNE_U2_HOLD / FEM_TUNE_U2_SMALL (tests only): the merged update's give-up path -- workgroup 0 arrives only after
+ * every other workgroup's bounded wait ran out, so the launch must end with FEM_PCG_SYNC_TIMEOUT, no x / p update
+ * anywhere and the give-up site 4 (+ 16 * launch); and its grid capped at 8 workgroups, so a small system reaches the
+ * loops past the register-cached elements. */
 /* FEM_TUNE_UPD1 (default): single-GPU 3-kernel schedule (bs = 3 past the persistent kernel's capacity) -- the r / z
  * update and the x / p update run as ONE launch with every workgroup resident (k_pcg_update2: the last workgroup
  * finishes r.z and releases the others), z kept in registers in between: 8 vector streams per iteration instead of

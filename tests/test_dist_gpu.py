@@ -74,3 +74,51 @@ def test_local_spmv_partials_sum_to_global(gpu):
     for r in grp.ranks:
         acc.index_add_(0, r.rm.nodes, r.A.matvec(x[r.rm.nodes].contiguous()))
     assert rel(acc, y) < 1e-13
+
+
+def test_config3_elasticity_10m_eight_partitions_vs_oracle(gpu, cube119):
+    """BASELINE configs[3]'s workload on one GPU: the 10,110,954-tet elasticity system over 8 RCB element
+    partitions (the bench's N = 8 element partition, `subdivision.ipynb:248-279` per-part maps), every rank's local
+    operator, halo-summed Jacobi and single-reduction kernels with the neighbour exchange (the RCCL path's
+    k_cg1_update / k_cg1_spmv, the p2p slots delivered in-process), checked against the oracle: (a) the ranks'
+    local SpMV partials summed over their global node ids = the reference's EBE product (`solver/element.py:429-464`)
+    at 1e-12; the distributed Jacobi = the oracle's at 1e-14; (b) 5 fixed iterations = the oracle PCG's 5th iterate
+    (`solver/solver.py:766-812`) at 1e-10; (c) copies of shared nodes bit-identical on every rank."""
+    import fem355  # noqa: F401
+    from fem355 import dist as fd
+    c, t, N = cube119.c, cube119.t, cube119.N
+    f, fixed, dinv = cube119.case("elastic")
+    grp = fd.PartitionGroup(c.to(gpu), t.to(gpu), 8, "elastic", cube119.E, cube119.NU)
+    assert len(grp.ranks) == 8 and sum(r.rm.elem_ids.numel() for r in grp.ranks) == t.shape[0]
+    assert all(r.A.use16 for r in grp.ranks)
+    # (a) summed partials
+    p, y_ref = cube119.matvec_ref("elastic", 11)
+    pg = p.to(gpu)
+    acc = torch.zeros((N, 3), dtype=F64, device=gpu)
+    for r in grp.ranks:
+        y = r.A.matvec(pg[r.rm.nodes].reshape(-1).contiguous())
+        acc.index_add_(0, r.rm.nodes, y.view(-1, 3))
+    assert rel(acc, y_ref) < 1e-12
+    del acc, pg
+    gmask = torch.zeros((N, 3), dtype=torch.uint8, device=gpu)
+    gmask[fixed.to(gpu)] = 1
+    ws = grp.jacobi([gmask[r.rm.nodes].reshape(-1).contiguous() for r in grp.ranks])
+    for r, wl in zip(grp.ranks, ws):
+        assert rel(wl, dinv[r.rm.nodes.cpu()].reshape(-1)) < 1e-14
+    # (b) 5 fixed iterations of the bench's N > 1 RCCL-path iteration (single reduction, neighbour exchange)
+    fg = f.to(gpu)
+    bl = [r.local(fg) for r in grp.ranks]
+    xs, it, st = grp.solve(bl, ws, 0.0, 5, variant=1, exchange="p2p", fixed=True)
+    assert it == 5, (it, st)
+    u = fd.gather_solution(grp.ranks, xs, N, 3)
+    assert rel(u, cube119.pcg_ref("elastic", 5)) < 1e-10
+    # (c) shared copies bit-identical
+    for a in range(8):
+        for b in range(a + 1, 8):
+            ra, rb = grp.ranks[a].rm, grp.ranks[b].rm
+            m = torch.isin(ra.nodes, rb.nodes)
+            if int(m.sum()) == 0:
+                continue
+            common = ra.nodes[m]
+            ia, ib = torch.searchsorted(ra.nodes, common), torch.searchsorted(rb.nodes, common)
+            assert torch.equal(xs[a].view(-1, 3)[ia], xs[b].view(-1, 3)[ib])

@@ -173,6 +173,37 @@ def test_dist_persist_elastic_matches_single_gpu(gpu, n, jitter):
     assert rel(xs[0], x1) < 1e-12 and torch.equal(xs[0], xs[1])
 
 
+def test_dist_persist_elastic_rank_share_vs_oracle(gpu):
+    """The N = 8 per-rank share of configs[3] (n = 59: 1,232,274 tets, the size one rank of the 10M system holds at
+    N = 8) on the DIST k_pcg_persist3 build over 2 emulated ranks, against the ORACLE: 20 fixed iterations equal the
+    reference PCG's 20th iterate (`solver/solver.py:766-812`, over the reference's element matrices,
+    `solver/element.py:883-903`) at 1e-10, every rank running the persistent schedule with its state on chip."""
+    from oracle import ref_cpu as R
+    C, DP, mesh, system = _mods()
+    E, NU = 113.8e9, 0.342
+    c, t = mesh.kuhn_cube(59)
+    N = c.shape[0]
+    f, fixed = mesh.cube_elasticity_case(c)
+    mask = torch.zeros((N, 3), dtype=torch.uint8, device=gpu)
+    mask[fixed.to(gpu)] = 1
+    b = f.reshape(-1).to(F64).to(gpu)
+    grp = DP.EmulatedGroup(c.to(gpu), t.to(gpu), 2, b, fixed_mask=mask.view(-1), kind="elastic", E=E, nu=NU, tol=0.0)
+    try:
+        grp.start()
+        assert all(rr.effective_schedule() == system.SCHED_PERSIST for rr in grp.ranks)
+        grp.iterate(20)
+        it, stt, _ = grp.poll()
+        assert it == 20 and stt == C.PCG_RUNNING
+        x = grp.x().cpu()
+    finally:
+        grp.close()
+    K = R.tet4_K(c, t, E, NU)
+    dinv = R.diag_preconditioner(K, t, N, dpn=3)
+    dinv[fixed] = 0.0
+    u_ref, it_ref, _ = R.pcg(K, t, f.reshape(N, 3).to(F64), dinv, tol=0.0, max_iter=20)
+    assert it_ref == 20 and rel(x, u_ref.reshape(-1)) < 1e-10
+
+
 # ---------------------------------------------------------------------------- the N > 1 failure chain (DESIGN §6.1)
 def test_dist_persist_drop_publish_gives_up(gpu):
     """Fault injection (FEM_TUNE_DIST_DROP on rank 1: it publishes no u row and no flag): every rank's launch ends

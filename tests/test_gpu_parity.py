@@ -802,14 +802,17 @@ def test_element_row_assembly_bit_identical_to_column_form(gpu, etype, n, rep, m
     assert torch.equal(a, b), etype
 
 
-@pytest.mark.parametrize("kind,mode", [("elastic", "cg"), ("elastic", "pcg"), ("poisson", "pcg")])
-def test_merged_update_matches_two_kernel_update(gpu, kind, mode):
+@pytest.mark.parametrize("kind,mode,small", [("elastic", "cg", False), ("elastic", "pcg", False),
+                                             ("poisson", "pcg", False), ("elastic", "pcg", True),
+                                             ("elastic", "cg", True)])
+def test_merged_update_matches_two_kernel_update(gpu, kind, mode, small):
     """3-kernel schedule: the merged r/z + x/p update (k_pcg_update2, FEM_TUNE_UPD1, default) against the two
     vector kernels it replaces, on an odd number of dofs (the scalar tail), stable CG with its history and PCG: same
     stop, iterations +-1, x 1e-12, the first 20 residual norms 1e-12 (p = z + beta p rounds z first, so the bits may
-    differ)."""
+    differ). small: the merged update's grid capped at 8 workgroups (FEM_TUNE_U2_SMALL) on a 50,625-dof system, so
+    its loops past the register-cached z (n/2 > 8 x 256 x 8) run as well."""
     _, mesh, _, system = _mods()
-    c, t = mesh.kuhn_cube(10, jitter=0.1)        # 1,331 nodes: n odd for both kinds
+    c, t = mesh.kuhn_cube(24 if small else 10, jitter=0.1)   # 15,625 / 1,331 nodes: n odd for both kinds
     N = c.shape[0]
     if kind == "elastic":
         f, fixed = mesh.cube_elasticity_case(c)
@@ -825,13 +828,53 @@ def test_merged_update_matches_two_kernel_update(gpu, kind, mode):
     md = C_MODE[mode]
     b = f.reshape(-1).to(gpu, F64)
     tol = 1e-9 * float(torch.linalg.norm(b))
+    tn0 = CAPI().TUNE_DEFAULT | (CAPI().TUNE_U2_SMALL if small else 0)
     runs = [A.pcg(b, w=w, mode=md, tol=tol, max_iter=5000, history=True, schedule=0, tune=tn)
-            for tn in (CAPI().TUNE_DEFAULT, CAPI().TUNE_DEFAULT & ~CAPI().TUNE_UPD1)]
+            for tn in (tn0, CAPI().TUNE_DEFAULT & ~CAPI().TUNE_UPD1)]
     a, o = runs
     assert A.n % 2 == 1 and a.schedule == 0 and o.schedule == 0
+    assert not small or A.n // 2 > 8 * 256 * 8
     assert a.status == o.status == CAPI().PCG_CONVERGED and abs(a.iterations - o.iterations) <= 1
     assert rel(a.x, o.x) < 1e-12
     assert rel(a.history[:20], o.history[:20]) < 1e-12
+
+
+def test_merged_update_give_up_is_all_or_nothing(gpu):
+    """a merged-update launch whose wait gives up must end with FEM_PCG_SYNC_TIMEOUT, the give-up
+    site 4 (+ 16 x launch) and NO workgroup's x update -- also when the late workgroup arrives afterwards and finishes
+    r.z (FEM_TUNE_U2_HOLD holds workgroup 0 back past every other workgroup's 2 s wait). fem_pcg_solve then re-solves
+    from x0 with the two-kernel update: the same result as a solve without the merged update."""
+    import ctypes
+    _, mesh, _, system = _mods()
+    cap = CAPI()
+    c, t = mesh.kuhn_cube(12, jitter=0.1)
+    N = c.shape[0]
+    f, fixed = mesh.cube_elasticity_case(c)
+    A = system.assemble_tet4_system(c.to(gpu), t.to(gpu), "elastic", E, NU)
+    mask = torch.zeros((N, 3), dtype=torch.uint8, device=gpu)
+    mask[fixed.to(gpu)] = 1
+    w = A.jacobi(mask.view(-1))
+    b = f.reshape(-1).to(gpu, F64)
+    x0 = torch.randn(A.n, dtype=F64, generator=torch.Generator().manual_seed(5)).to(gpu)
+    run = system.PcgRunner(A, b, w, x0=x0, tol=0.0, schedule=0)
+    try:
+        run.set_tuning(cap.TUNE_DEFAULT | cap.TUNE_U2_HOLD)
+        run.start()
+        run.iterate(3)
+        it, stt, rz = ctypes.c_int(), ctypes.c_int(), ctypes.c_double()
+        cap.check(run.lib.fem_pcg_poll(run.h, ctypes.byref(it), ctypes.byref(stt), ctypes.byref(rz)), "poll")
+        site = ctypes.c_int()
+        cap.check(run.lib.fem_pcg_sync_site(run.h, ctypes.byref(site)), "site")
+        assert stt.value == cap.PCG_SYNC_TIMEOUT and it.value == 0, (it.value, stt.value)
+        assert site.value == 4 + 16 * 1, site.value
+        assert torch.equal(run.x, x0)            # nobody applied x += alpha p
+    finally:
+        run.close()
+    tol = 1e-9 * float(torch.sqrt(torch.dot(b, w * b)))
+    held = A.pcg(b, w=w, tol=tol, max_iter=5000, schedule=0, tune=cap.TUNE_DEFAULT | cap.TUNE_U2_HOLD)
+    plain = A.pcg(b, w=w, tol=tol, max_iter=5000, schedule=0, tune=cap.TUNE_DEFAULT & ~cap.TUNE_UPD1)
+    assert held.status == plain.status == cap.PCG_CONVERGED and held.iterations == plain.iterations
+    assert torch.equal(held.x, plain.x)
 
 
 def _helix_fan(m):

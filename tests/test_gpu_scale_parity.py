@@ -9,7 +9,10 @@ runs `pytest -x`).
     matrices (`solver/solver.py:766-812`): iterations within +-2, u within 1e-10;
   * configs[2] (10M-tet P1 elasticity, n = 119): the assembled SELL operator applied to a seeded vector against the
     oracle's EBE product `R.nodal_forces(R.tet4_K(...))` (`solver/element.py:429-464`, `:883-903`) to 1e-12, and the
-    first 5 Jacobi-PCG iterates of the default bs = 3 schedule against `R.pcg` to 1e-10.
+    first 5 Jacobi-PCG iterates of the default bs = 3 schedule against `R.pcg` to 1e-10;
+  * the metric (10M-tet P1 Poisson): the bench's operator and the exact persistent build it times (7 slots, 26,992
+    slice-uniform slices) for 5 iterates against the oracle, and the same on the cube renumbered at random and then by
+    device RCM (a mesh in file order).
 The oracle's element matrices at 10M tets take ~12 GB of host memory and ~10 s on the box's 16 cores."""
 import pytest
 import torch
@@ -59,29 +62,93 @@ def test_config1_poisson_1m_solve_vs_oracle(gpu):
     assert rel(u, u_ref) < 1e-10
 
 
-def test_config2_elasticity_10m_operator_and_iterates_vs_oracle(gpu):
+def test_config2_elasticity_10m_operator_and_iterates_vs_oracle(gpu, cube119):
     """BASELINE configs[2]: 10,110,954 tets, 5,184,000 DOFs. The assembled operator (fused on-the-fly assembly into
     SELL-64 with 16-bit deltas, the bench's) equals the reference's EBE operator over its own element matrices, and
     the default bs = 3 schedule's first 5 PCG iterates equal the reference PCG's."""
     _, mesh, _, system = _mods()
-    c, t = mesh.kuhn_cube(119)
-    N = c.shape[0]
+    c, t, N = cube119.c, cube119.t, cube119.N
     assert t.shape[0] == 10_110_954
-    f, fixed = mesh.cube_elasticity_case(c)
+    f, fixed, dinv = cube119.case("elastic")
     A = system.assemble_tet4_system(c.to(gpu), t.to(gpu), "elastic", E, NU)
     assert A.use16
-    p = torch.randn(N, 3, dtype=F64, generator=torch.Generator().manual_seed(11))
+    p, y_ref = cube119.matvec_ref("elastic", 11)
     y = A.matvec(p.reshape(-1).to(gpu)).cpu()
-    K = R.tet4_K(c, t, E, NU)
-    assert rel(y, R.nodal_forces(K, t, p).reshape(-1)) < 1e-12
+    assert rel(y, y_ref.reshape(-1)) < 1e-12
     mask = torch.zeros((N, 3), dtype=torch.uint8, device=gpu)
     mask[fixed.to(gpu)] = 1
     w = A.jacobi(mask.view(-1))
-    b = f.reshape(-1).to(F64)
+    b = f.reshape(-1)
     res = A.pcg(b, w=w, tol=0.0, max_iter=5)
     assert res.iterations == 5
-    dinv = R.diag_preconditioner(K, t, N, dpn=3)
-    dinv[fixed] = 0.0
     assert rel(w.cpu(), dinv.reshape(-1)) < 1e-14
-    u_ref, it_ref, _ = R.pcg(K, t, b.view(N, 3), dinv, tol=0.0, max_iter=5)
-    assert it_ref == 5 and rel(res.x.cpu(), u_ref.reshape(-1)) < 1e-10
+    assert rel(res.x.cpu(), cube119.pcg_ref("elastic", 5).reshape(-1)) < 1e-10
+
+
+def _poisson_persistent_iterates(system, A, b, w, steps):
+    """The bench's fixed-iteration path: a PcgRunner with the default (persistent) schedule, a warm-up launch then a
+    timed launch (`bench.py` measure()); returns (runner facts, x after sum(steps) iterations)."""
+    run = system.PcgRunner(A, b, w, tol=0.0)
+    try:
+        run.start()
+        facts = {"schedule": run.effective_schedule(), "build": run.persist_build(), "uniform": run.uniform_slices()}
+        for k in steps:
+            run.profile(k, every=k)
+        assert run.poll()[0] == sum(steps)
+        return facts, run.x.clone()
+    finally:
+        run.close()
+
+
+def test_metric_poisson_10m_persistent_vs_oracle(gpu, cube119):
+    """The metric's own system (BASELINE.json: 10M-tet P1 Poisson): the operator assembled by bench.py's path
+    against the oracle's EBE product over its element matrices (`solver/element.py:429-464`) at 1e-12, the Jacobi
+    weights at 1e-14, and the exact kernel build the bench times -- the 7-slot k_pcg_persist with the packed
+    assignment and slice-uniform deltas on 26,992 of 27,000 slices -- for 5 iterations (a 2-step warm-up launch and a
+    3-step timed launch, like bench.py) against the oracle PCG's 5th iterate (`solver/solver.py:766-812`) at 1e-10."""
+    _, mesh, _, system = _mods()
+    c, t, N = cube119.c, cube119.t, cube119.N
+    f, fixed, dinv = cube119.case("poisson")
+    A = system.assemble_tet4_system(c.to(gpu), t.to(gpu), "poisson")
+    assert A.use16 and A.n == 1_728_000
+    p, y_ref = cube119.matvec_ref("poisson", 12)
+    assert rel(A.matvec(p.reshape(-1).to(gpu)), y_ref.reshape(-1)) < 1e-12
+    mask = torch.zeros(N, dtype=torch.uint8, device=gpu)
+    mask[fixed.to(gpu)] = 1
+    w = A.jacobi(mask)
+    assert rel(w, dinv.reshape(-1)) < 1e-14
+    facts, x = _poisson_persistent_iterates(system, A, f.reshape(-1), w, (2, 3))
+    assert facts["schedule"] == system.SCHED_PERSIST
+    assert facts["build"] == (7, 0, 7), facts
+    assert facts["uniform"][:2] == (26_992, 27_000), facts
+    assert rel(x, cube119.pcg_ref("poisson", 5).reshape(-1)) < 1e-10
+
+
+def test_metric_poisson_10m_rcm_renumbered_vs_oracle(gpu, cube119):
+    """The metric system as a mesh in file order would hand it over: the cube's nodes randomly renumbered (seed 7,
+    `bench.py --permute 7`), then device RCM (`bench.py --reorder rcm`). The renumbered operator and the persistent
+    schedule's first 5 iterates, mapped back to the cube's numbering, against the same oracle products."""
+    _, mesh, _, system = _mods()
+    c, t, N = cube119.c, cube119.t, cube119.N
+    f, fixed, dinv = cube119.case("poisson")
+    perm1 = torch.randperm(N, generator=torch.Generator().manual_seed(7))
+    inv1 = torch.empty_like(perm1)
+    inv1[perm1] = torch.arange(N)
+    cp, tp = c[perm1].to(gpu), inv1[t].to(gpu)
+    perm2, inv2 = system.rcm_order(tp, N)
+    c2, t2 = system.renumber(cp, tp, perm2, inv2)
+    P = perm1[perm2.cpu()]                    # new node j is the cube's node P[j]
+    Pinv = torch.empty_like(P)
+    Pinv[P] = torch.arange(N)
+    A = system.assemble_tet4_system(c2, t2, "poisson")
+    assert A.use16                            # RCM brings every |col - row| under 32767
+    p, y_ref = cube119.matvec_ref("poisson", 12)
+    y = A.matvec(p.reshape(-1)[P].to(gpu)).cpu()
+    assert rel(y[Pinv], y_ref.reshape(-1)) < 1e-12
+    mask = torch.zeros(N, dtype=torch.uint8, device=gpu)
+    mask[Pinv[fixed].to(gpu)] = 1
+    w = A.jacobi(mask)
+    assert rel(w.cpu()[Pinv], dinv.reshape(-1)) < 1e-14
+    facts, x = _poisson_persistent_iterates(system, A, f.reshape(-1)[P], w, (2, 3))
+    assert facts["schedule"] == system.SCHED_PERSIST and facts["build"][1] == 0, facts
+    assert rel(x.cpu()[Pinv], cube119.pcg_ref("poisson", 5).reshape(-1)) < 1e-10
