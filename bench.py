@@ -138,6 +138,8 @@ def cpu_threads():
             quota = int(q[0]) / int(q[1])
     except (OSError, ValueError, IndexError):
         pass
+    if quota:   # a CPU quota below the mask (a container's share of the host) bounds it as well
+        threads = max(1, min(threads, int(quota + 0.999)))
     return threads, {"affinity_cpus": aff, "os_cpu_count": os.cpu_count(), "omp_num_threads": cap or None,
                      "cgroup_cpu_quota": quota}
 

@@ -525,55 +525,133 @@ __global__ void __launch_bounds__(256) k_graph(const int64_t* __restrict__ conn,
     }
 }
 
-// Rows of more than G_UCAP neighbours (no limit): wave per row, ascending selection straight from the incidence
-// list — each step takes the wave-wide minimum candidate above the previous one. O(U * C / 64) per row; such rows
-// are rare (a node shared by hundreds of elements). Nodes are found 64 at a time by a ballot over the flags.
+// Rows of more than G_UCAP neighbours (no limit; a node shared by thousands of elements): a 1024-thread workgroup
+// per row marks the row's candidates in a bitmap of node ids held in LDS (GB_WORDS words: a window of 2^20 ids;
+// ids past the window in further passes over the candidates), then reads the set bits back in ascending order --
+// sorted and deduplicated at once, O(C) per window with C the row's candidate count (the former ascending selection
+// was O(U C): a 1.1M-tet fan did not finish in 3 minutes). Pass 0 finds the candidates' id range (and the 16-bit
+// delta check). The workgroups find their rows 1024 flags at a time.
+constexpr int GB_T = 1024;
+constexpr int GB_WORDS = 32768;                    // 128 KB of LDS: 2^20 node ids per window
+constexpr size_t GB_LDS = sizeof(uint32_t) * GB_WORDS;
+
 __device__ __forceinline__ int wave_min_i32(int v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
     return v;
 }
 
+__device__ __forceinline__ int big_cand(const int64_t* conn, int npe, const int32_t* inc, int start, int t) {
+    const int k = t / npe, b = t - k * npe;
+    return (int)conn[(int64_t)(inc[start + k] / npe) * npe + b];
+}
+
+// exclusive scan of one int per thread over GB_T threads (wave scans by shuffles, then the 16 wave totals)
+__device__ __forceinline__ int gb_scan(int v, int* wsum, int* total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(incl, o);
+        if (lane >= o) incl += u;
+    }
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    int before = 0, all = 0;
+    for (int w = 0; w < GB_T / 64; ++w) {
+        const int x = wsum[w];
+        before += (w < wid) ? x : 0;
+        all += x;
+    }
+    *total = all;
+    __syncthreads();   // wsum reusable
+    return before + incl - v;
+}
+
 template <bool FILL>
-__global__ void __launch_bounds__(256) k_graph_big(const int64_t* __restrict__ conn, int npe,
-                                                   const int32_t* __restrict__ inc_ptr,
-                                                   const int32_t* __restrict__ inc, int64_t N,
-                                                   int32_t* __restrict__ row_len, const int32_t* __restrict__ rowptr,
-                                                   int32_t* __restrict__ colidx, int32_t* __restrict__ diagpos,
-                                                   int32_t* __restrict__ far) {
-    const int wid = threadIdx.x >> 6;
-    const int lane = threadIdx.x & 63;
-    for (int64_t base = ((int64_t)blockIdx.x * G_WAVES + wid) * 64; base < N;
-         base += (int64_t)gridDim.x * G_WAVES * 64) {
-        const int64_t me = base + lane;
-        const bool big = me < N && (FILL ? rowptr[me + 1] - rowptr[me] > G_UCAP : row_len[me] < 0);
-        unsigned long long m = __ballot(big);
-        while (m) {
-            const int64_t node = base + (__ffsll((long long)m) - 1);
-            m &= m - 1;
+__global__ void __launch_bounds__(GB_T) k_graph_big(const int64_t* __restrict__ conn, int npe,
+                                                    const int32_t* __restrict__ inc_ptr,
+                                                    const int32_t* __restrict__ inc, int64_t N,
+                                                    int32_t* __restrict__ row_len, const int32_t* __restrict__ rowptr,
+                                                    int32_t* __restrict__ colidx, int32_t* __restrict__ diagpos,
+                                                    int32_t* __restrict__ far) {
+    extern __shared__ uint32_t bm[];               // [GB_WORDS]
+    __shared__ int rows_s[GB_T];
+    __shared__ int nrows_s, lo_s, hi_s;
+    __shared__ int wsum[GB_T / 64];
+    const int tid = threadIdx.x;
+    for (int64_t base = (int64_t)blockIdx.x * GB_T; base < N; base += (int64_t)gridDim.x * GB_T) {
+        if (tid == 0) nrows_s = 0;
+        __syncthreads();
+        const int64_t me = base + tid;
+        if (me < N && (FILL ? rowptr[me + 1] - rowptr[me] > G_UCAP : row_len[me] < 0))
+            rows_s[atomicAdd(&nrows_s, 1)] = tid;
+        __syncthreads();
+        const int nr = nrows_s;
+        for (int q = 0; q < nr; ++q) {
+            const int64_t node = base + rows_s[q];
             const int start = inc_ptr[node];
             const int C = (inc_ptr[node + 1] - start) * npe;
-            const int32_t rp = FILL ? rowptr[node] : 0;
-            int prev = -1, U = 0;
-            while (true) {
-                int best = INT_MAX;
-                for (int t = lane; t < C; t += 64) {
-                    const int k = t / npe, b = t - k * npe;
-                    const int v = (int)conn[(int64_t)(inc[start + k] / npe) * npe + b];
-                    if (v > prev && v < best) best = v;
-                }
-                best = wave_min_i32(best);
-                if (best == INT_MAX) break;
-                if (!FILL && far && lane == 0 && (best - node > 32767 || node - best > 32767) && !*far)
-                    atomicOr(far, 1);
-                if (FILL && lane == 0) {
-                    colidx[rp + U] = best;
-                    if (best == (int)node) diagpos[node] = rp + U;
-                }
-                ++U;
-                prev = best;
+            int lo = INT_MAX, hi = -1;
+            for (int t = tid; t < C; t += GB_T) {
+                const int v = big_cand(conn, npe, inc, start, t);
+                lo = min(lo, v);
+                hi = max(hi, v);
             }
-            if (!FILL && lane == 0) row_len[node] = U;
+            lo = wave_min_i32(lo);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) hi = max(hi, __shfl_xor(hi, o));
+            if (tid == 0) {
+                lo_s = INT_MAX;
+                hi_s = -1;
+            }
+            __syncthreads();
+            if ((tid & 63) == 0) {
+                atomicMin(&lo_s, lo);
+                atomicMax(&hi_s, hi);
+            }
+            __syncthreads();
+            lo = lo_s;
+            hi = hi_s;
+            if (!FILL && far && tid == 0 && hi >= lo && (hi - (int)node > 32767 || (int)node - lo > 32767) && !*far)
+                atomicOr(far, 1);
+            const int32_t rp = FILL ? rowptr[node] : 0;
+            int U = 0;
+            for (int64_t w0 = lo; w0 <= hi; w0 += (int64_t)GB_WORDS * 32) {
+                const int64_t span = min<int64_t>((int64_t)hi - w0 + 1, (int64_t)GB_WORDS * 32);
+                const int nw = (int)((span + 31) >> 5);
+                for (int k = tid; k < nw; k += GB_T) bm[k] = 0u;
+                __syncthreads();
+                for (int t = tid; t < C; t += GB_T) {
+                    const int64_t d = (int64_t)big_cand(conn, npe, inc, start, t) - w0;
+                    if (d >= 0 && d < span) atomicOr(&bm[d >> 5], 1u << (d & 31));
+                }
+                __syncthreads();
+                // thread tid owns words [k0, k1): count, scan, then (fill) write its ids in ascending order
+                const int per = (nw + GB_T - 1) / GB_T;
+                const int k0 = min(tid * per, nw), k1 = min(k0 + per, nw);
+                int cnt = 0;
+                for (int k = k0; k < k1; ++k) cnt += __popc(bm[k]);
+                int total;
+                const int off = gb_scan(cnt, wsum, &total);
+                if (FILL) {
+                    int o = rp + U + off;
+                    for (int k = k0; k < k1; ++k) {
+                        uint32_t m = bm[k];
+                        while (m) {
+                            const int bit = __ffs(m) - 1;
+                            m &= m - 1;
+                            const int v = (int)(w0 + 32 * (int64_t)k + bit);
+                            colidx[o] = v;
+                            if (v == (int)node) diagpos[node] = o;
+                            ++o;
+                        }
+                    }
+                }
+                U += total;
+                __syncthreads();   // bitmap reusable
+            }
+            if (!FILL && tid == 0) row_len[node] = U;
         }
     }
 }
@@ -888,9 +966,23 @@ static int graph_grid(int64_t N) {
 }
 
 static int big_grid(int64_t N) {
-    int64_t g = cdiv(N, (int64_t)G_WAVES * 64);
-    if (g > 2048) g = 2048;
+    int64_t g = cdiv(N, (int64_t)GB_T);
+    if (g > 1024) g = 1024;
     return (int)(g < 1 ? 1 : g);
+}
+
+// the big-row kernels take 128 KB of dynamic LDS (set once per process)
+static int big_lds_attr() {
+    static const int rc = [] {
+        if (hipFuncSetAttribute((const void*)k_graph_big<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)GB_LDS) != hipSuccess ||
+            hipFuncSetAttribute((const void*)k_graph_big<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)GB_LDS) != hipSuccess)
+            return (int)FEM_EHIP;
+        return (int)FEM_OK;
+    }();
+    if (rc != FEM_OK) set_error("k_graph_big: cannot allow %zu bytes of dynamic LDS", GB_LDS);
+    return rc;
 }
 
 // count: k_graph for every row (done = null) or for the rows k_graph_small left, then k_graph_big for the rows
@@ -901,7 +993,8 @@ static int graph_count(const int64_t* conn, int npe, const int32_t* inc_ptr, con
     hipLaunchKernelGGL(k_graph<false>, dim3(graph_grid(N)), dim3(256), 0, st, conn, npe, inc_ptr, inc, N, row_len,
                        (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, defer, overflow);
     FEM_LAUNCHED();
-    hipLaunchKernelGGL(k_graph_big<false>, dim3(big_grid(N)), dim3(256), 0, st, conn, npe, inc_ptr, inc, N, row_len,
+    if (const int rc = big_lds_attr()) return rc;
+    hipLaunchKernelGGL(k_graph_big<false>, dim3(big_grid(N)), dim3(GB_T), GB_LDS, st, conn, npe, inc_ptr, inc, N, row_len,
                        (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, overflow);
     FEM_LAUNCHED();
     return FEM_OK;
@@ -912,7 +1005,8 @@ static int graph_fill(const int64_t* conn, int npe, const int32_t* inc_ptr, cons
     hipLaunchKernelGGL(k_graph<true>, dim3(graph_grid(N)), dim3(256), 0, st, conn, npe, inc_ptr, inc, N,
                        (int32_t*)nullptr, rowptr, colidx, diagpos, defer, (int32_t*)nullptr);
     FEM_LAUNCHED();
-    hipLaunchKernelGGL(k_graph_big<true>, dim3(big_grid(N)), dim3(256), 0, st, conn, npe, inc_ptr, inc, N,
+    if (const int rc = big_lds_attr()) return rc;
+    hipLaunchKernelGGL(k_graph_big<true>, dim3(big_grid(N)), dim3(GB_T), GB_LDS, st, conn, npe, inc_ptr, inc, N,
                        (int32_t*)nullptr, rowptr, colidx, diagpos, (int32_t*)nullptr);
     FEM_LAUNCHED();
     return FEM_OK;

@@ -905,6 +905,39 @@ def test_cols16_flag_from_graph_count_matches_bandwidth(gpu, m, gap):
     assert (g.dcols is not None) == (bw <= 32767), (m, gap, bw)
 
 
+@pytest.mark.parametrize("m,spread", [(200_000, 1), (200_000, 7)])
+def test_hub_row_pattern_is_bounded_and_exact(gpu, m, spread):
+    """A node shared by m = 200,000 tets (a row of 200,003 columns): the node-graph pattern's
+    big-row tier (k_graph_big: an LDS bitmap of node ids per 2^20-id window, O(candidates) per window) builds it
+    within a stated bound -- 10 s for the whole pattern, warm -- and the pattern equals the oracle's coalesced COO
+    (`R.node_pattern`, `subdivision.ipynb:118-139`) bit for bit, diagonal positions included. spread: the fan's node
+    ids multiplied by 7 (1.4M ids: two bitmap windows, int32 columns, unused nodes with empty rows)."""
+    import time
+    _, _, _, system = _mods()
+    c, t = _helix_fan(m)
+    N = c.shape[0]
+    if spread > 1:
+        t = t * spread
+        N = (N - 1) * spread + 1
+    tg = t.to(gpu)
+    system.build_graph(tg[:1000], N)                  # module loads / first-use costs outside the bound
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    g = system.build_graph(tg, N)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    assert dt < 10.0, dt
+    rp, ci = R.node_pattern(t, N)
+    assert torch.equal(g.rowptr.long().cpu(), rp) and torch.equal(g.colidx.long().cpu(), ci)
+    assert int(rp[1] - rp[0]) == m + 3
+    rows = torch.repeat_interleave(torch.arange(N), rp[1:] - rp[:-1])
+    dpos = torch.full((N,), -1, dtype=torch.long)
+    on = ci == rows
+    dpos[rows[on]] = torch.nonzero(on, as_tuple=True)[0]
+    assert torch.equal(g.diagpos.long().cpu(), dpos)
+    assert (g.dcols is not None) == (spread == 1 and m + 2 <= 32767)
+
+
 @pytest.mark.parametrize("case", ["kuhn", "permuted", "fan", "repeated", "twice"])
 def test_tile_assembly_bit_identical_to_row_kernels(gpu, case, monkeypatch):
     """c3d4 / P1 assembly straight into SELL: the accumulator kernel (k_asm_tet4_acc, default; fresh matrices stored

@@ -33,11 +33,14 @@ def _helix_fan(m):
     return c, torch.stack([torch.zeros_like(a), a, a + 1, a + 2], 1)
 
 
-@pytest.mark.parametrize("case", ["permuted", "lexicographic", "components", "fan"])
+@pytest.mark.parametrize("case", ["permuted", "lexicographic", "components", "fan", "bigfan"])
 def test_device_rcm_equals_oracle(gpu, case):
+    """bigfan: a 1.1M-tet fan -- a hub row of 1.1M columns (the pattern's bitmap tier) and, from the helix end, a
+    BFS level of ~1.1M nodes, wide enough for many rounds of the level-write kernel's 4,096-node scan (the wide-level
+    path)."""
     mesh, _, system = _mods()
-    if case == "fan":
-        c, t = _helix_fan(300)
+    if case in ("fan", "bigfan"):
+        c, t = _helix_fan(300 if case == "fan" else 1_100_000)
         N = c.shape[0]
     elif case == "components":
         c, t = mesh.kuhn_cube(4)
