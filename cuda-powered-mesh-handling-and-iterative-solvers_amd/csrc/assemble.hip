@@ -518,13 +518,17 @@ __global__ void __launch_bounds__(256) k_assemble_ke_w(const double* __restrict_
 // other. Every slot therefore sums its contributions in ascending (incidence, b) order from +0.0, exactly as
 // k_assemble_ke_w<..., CSRW>: the row sums are bit-identical. Columns are taken KR_LMAX at a time (wider rows: one
 // more pass over the incidences per window); an element listing one node twice adds its b's in ascending order.
+// SELLW: the row sums go straight into the SELL planes of a fresh matrix (stored, the row's padding entries zeroed;
+// 8-byte stores whose 16 rows per 128-byte line are written by the workgroups of one XCD at about the same time),
+// instead of the block-CSR buffer + k_csr_add_sell pass (FEM355_KE_SELLW A/B).
 constexpr int KR_LMAX = 64;
-template <int NPE>
+template <int NPE, bool SELLW = false>
 __global__ void __launch_bounds__(256) k_assemble_ke_rows3(const double* __restrict__ Ke, const int64_t* __restrict__ conn,
                                                            const int32_t* __restrict__ inc_ptr,
                                                            const int32_t* __restrict__ inc, int64_t N,
                                                            const int32_t* __restrict__ rowptr,
-                                                           const int32_t* __restrict__ colidx, double* __restrict__ out) {
+                                                           const int32_t* __restrict__ colidx, double* __restrict__ out,
+                                                           const int64_t* __restrict__ slice_ptr = nullptr) {
     constexpr int BS = 3, B2 = 9, D = NPE * BS, RV = BS * D;
     constexpr int NL = (RV + 63) / 64;    // K_e loads per lane per incidence
     constexpr int KU = 64 / NPE;          // incidences per batch: one lane per (incidence, element node)
@@ -617,10 +621,36 @@ __global__ void __launch_bounds__(256) k_assemble_ke_rows3(const double* __restr
                 }
             }
             __builtin_amdgcn_wave_barrier();
-            double* o = out + (int64_t)(lo + j0) * B2;
-            for (int t = lane; t < nj * B2; t += 64) o[t] = acc[t];
+            if constexpr (SELLW) {
+                const int64_t p0 = slice_ptr[i >> 6];
+                double* o = out + B2 * p0 + (i & 63);
+                for (int t = lane; t < nj * B2; t += 64) {
+                    const int sl = t / B2, rc = t - B2 * (t / B2);
+                    o[(int64_t)64 * (B2 * (j0 + sl) + rc)] = acc[t];
+                }
+            } else {
+                double* o = out + (int64_t)(lo + j0) * B2;
+                for (int t = lane; t < nj * B2; t += 64) o[t] = acc[t];
+            }
+        }
+        if constexpr (SELLW) {   // the row's padding entries of its slice
+            const int64_t p0 = slice_ptr[i >> 6];
+            const int w = (int)((slice_ptr[(i >> 6) + 1] - p0) >> 6);
+            double* o = out + B2 * p0 + (i & 63);
+            for (int t = len * B2 + lane; t < w * B2; t += 64) o[(int64_t)64 * t] = 0.0;
         }
     }
+}
+
+// zero the lanes past the last row (N % 64 .. 63) of the last slice, every entry and plane (store paths that write
+// rows only)
+__global__ void k_sell_tail_zero(const int64_t* __restrict__ slice_ptr, int64_t N, int B2, double* __restrict__ vals) {
+    const int64_t s = (N - 1) >> 6;
+    const int64_t p0 = slice_ptr[s];
+    const int w = (int)((slice_ptr[s + 1] - p0) >> 6);
+    const int l0 = (int)(N & 63);
+    for (int t = threadIdx.x; t < w * B2 * 64; t += blockDim.x)
+        if ((t & 63) >= l0) vals[B2 * p0 + t] = 0.0;
 }
 
 // SELL planes += block-CSR row sums (k_assemble_ke_w<..., CSRW>): wave per slice, lane = row; for every (entry k,
@@ -678,18 +708,21 @@ __device__ __forceinline__ double add_nc(double a, double b) {
     return a + b;
 }
 
-// entry (rr, kk) of the elastic block (a, b) of a c3d4 element, V (lambda g_a g_b^T + mu g_b g_a^T + mu (g_a . g_b)
-// I), evaluated without contractions so the two assembly forms that evaluate it in different code agree bit for bit
-__device__ __forceinline__ double el_dot(const double* ga, const double* gb) {
+// Elastic blocks by sums (both assembly forms, bit for bit): per incident element the row node a contributes the
+// products M_ab[r][c] += (V g_a[r]) g_b[c] and P_ab += (V g_a) . g_b for every element node b (V g_a formed once per
+// element and row); the block is K_ab = lambda M_ab + mu M_ab^T + mu P_ab I, formed once from the sums when the
+// row is written -- the element formula V (lambda g_a g_b^T + mu g_b g_a^T + mu (g_a . g_b) I) summed in another
+// order (rounding-level difference; the oracle checks stay at 1e-12). Per product one multiply and one add instead
+// of the element formula's eight operations per entry.
+__device__ __forceinline__ double el_pdot(const double* vga, const double* gb) {
 #pragma clang fp contract(off)
-    return ga[0] * gb[0] + ga[1] * gb[1] + ga[2] * gb[2];
+    return vga[0] * gb[0] + vga[1] * gb[1] + vga[2] * gb[2];
 }
-__device__ __forceinline__ double el_value(const Lame& L, const double* ga, const double* gb, int rr, int kk,
-                                           double dot, double V) {
+__device__ __forceinline__ double el_combine(const Lame& L, double m_rc, double m_cr, double p, bool diag) {
 #pragma clang fp contract(off)
-    double s = L.lam * ga[rr] * gb[kk] + L.mu * ga[kk] * gb[rr];
-    if (rr == kk) s += L.mu * dot;
-    return s * V;
+    double s = L.lam * m_rc + L.mu * m_cr;
+    if (diag) s += L.mu * p;
+    return s;
 }
 
 __device__ __forceinline__ double p1_value(const double ga[3], const double gb[3], double kappa, double V) {
@@ -730,17 +763,22 @@ __global__ void k_sell_zero(const int64_t* __restrict__ slice_ptr, int64_t ns, i
 // Columns past ACC_W per row: the accumulators cover the row's columns in windows of ACC_W, one sweep per window.
 // LDS strides padded (R + 1, NI + 1): a row's lanes update accumulators of different columns and read staged
 // values of different element nodes at once, which power-of-two strides put into one bank (bs = 3: 5.8 -> 3.0 ms).
-template <int R_, int J_, int LPR_, int W_, int SEG_, bool XP_ = false>
+template <int R_, int J_, int LPR_, int W_, int SEG_, bool XP_ = false, bool XS_ = false>
 struct AccCfg {
     static constexpr int R = R_, J = J_, LPR = LPR_, W = W_, SEG = SEG_;
     // XP: the next batch's vertex coordinates loaded during the current batch's sweep (a third pipeline stage, 24
     // more VGPRs: for bs = 3, whose occupancy LDS caps anyway)
     static constexpr bool XP = XP_;
+    // XS: the coordinates of the tile's CSR column segment staged in LDS once (every node of an element incident to a
+    // row is a column of that row, found by the item's column search anyway): no coordinate gathers per batch
+    static constexpr bool XS = XS_;
 };
 // bs = 1: lanes (row, b), 64 rows (a slice), 4 items per row per batch, 32 accumulated columns per row (10M cube:
 // 0.86 ms; 16 columns 0.79 ms but two sweeps for rows past 16 columns, 8 items per row 1.16 ms at 3 waves per SIMD).
 // bs = 3: lanes (row, b, rr), 16 rows, 8 items per row per batch, 16 accumulated columns (10M cube: 2.55 ms; 16
-// items per row 2.95, 12 items 2.83, 4 items 2.66 ms).
+// items per row 2.95, 12 items 2.83, 4 items 2.66 ms; with the M / P sums since round 4: 2.45 ms. The coordinates of
+// the tile's columns staged in LDS instead of the per-batch prefetch (XS): 3.0 ms at 8 items per row, 2.96 / 3.37 /
+// 3.12 ms at 5 / 6 / 4 -- the staging's gathers at the tile start are exposed, and 3 instead of 4 tiles per CU).
 #ifndef FEM_P1_CFG
 #define FEM_P1_CFG 64, 4, 4, 32, 1024
 #endif
@@ -752,7 +790,7 @@ using AccP1 = AccCfg<FEM_P1_CFG>;
 // 107 VGPRs, 4 instead of 6 waves per SIMD
 using AccP1w16 = AccCfg<FEM_P1W16_CFG>;
 #ifndef FEM_EL3_CFG
-#define FEM_EL3_CFG 16, 8, 16, 16, 512, true
+#define FEM_EL3_CFG 16, 8, 16, 16, 256, true, false
 #endif
 using AccEl = AccCfg<FEM_EL3_CFG>;
 
@@ -771,19 +809,22 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
     constexpr int NT = R * LPR;                        // threads of the workgroup
     constexpr int RPL = (BS == 3 && LPR == 4) ? 3 : 1;   // block rows per sweep lane (bs = 3: lanes (row, b) or
                                                          // (row, b, rr))
-    constexpr int ND = BS == 1 ? 4 : 13;
+    constexpr int ND = BS == 1 ? 4 : 15;                // staged per item: P1 values / (V g_a, g_0 .. g_3)
+    constexpr int AV = BS == 1 ? 1 : 10;                // accumulated per column: the value / M (9) and P
     static_assert(NI <= NT, "one item per thread per batch");
     static_assert(64 % R == 0 && NT <= 256 && NT % 64 == 0 && 64 % LPR == 0, "tile geometry");
     static_assert(BS == 1 || LPR == 4 || LPR == 16, "bs = 3 lanes: (row, b) or (row, b, rr)");
+    static_assert(!(Cfg::XP && Cfg::XS), "coordinates either prefetched per batch or staged per tile");
     __shared__ int ip_s[R + 1];
     __shared__ int rp_s[R + 1];
     __shared__ int col_s[SEG];
+    __shared__ double xs_s[Cfg::XS ? SEG : 1][3];
     // padded strides: the sweep's lanes of one row read dat_s rows of different element nodes and update
     // accumulators of different columns -- with power-of-two strides those all fall into one LDS bank
     __shared__ double dat_s[ND][NI + 1];
     __shared__ uint2 pos_s[NI];
     __shared__ uint8_t a_s[NI];             // local index of the row's node; bit 7: the element repeats a node
-    __shared__ double acc_s[AW * B2][R + 1];
+    __shared__ double acc_s[AW * AV][R + 1];
     __shared__ int maxc_s;
     const int tid = threadIdx.x;
     const int64_t per = (ntiles + NXCD - 1) / NXCD;
@@ -808,22 +849,28 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
     const int seg0 = rp_s[0], segn = rp_s[R] - seg0;
     const bool staged = segn <= SEG;
     if (staged)
-        for (int q = tid; q < segn; q += NT) col_s[q] = colidx[seg0 + q];
+        for (int q = tid; q < segn; q += NT) {
+            const int cq = colidx[seg0 + q];
+            col_s[q] = cq;
+            if constexpr (Cfg::XS) {
+                xs_s[q][0] = X[3 * (int64_t)cq];
+                xs_s[q][1] = X[3 * (int64_t)cq + 1];
+                xs_s[q][2] = X[3 * (int64_t)cq + 2];
+            }
+        }
     const int maxc = maxc_s;
     const Lame L = lame(E, nu);
     // phase-2 lane: row lr, element node lb, block rows lrr .. lrr + RPL - 1
     const int lr = tid / LPR, lb = (BS == 1 || LPR == 4) ? tid % LPR : (tid % LPR) / 4;
-    const int lrr = (BS == 1 || LPR == 4) ? 0 : tid % 4;
-    const bool lactive = BS == 1 || lrr < 3;
+    const int lrr = (BS == 1 || LPR == 4) ? 0 : tid % 4;   // bs = 3, LPR = 16: rr = 3 is the P lane
     for (int c0 = 0; c0 < W; c0 += AW) {
         const int cw = min(AW, W - c0);
         __syncthreads();
-        for (int q = tid; q < AW * B2 * R; q += NT) {
-            const int r = q % R, kc = q / R, k = kc / B2, c = kc - k * B2;
-            double v = 0.0;
-            if (!STORE && k < cw && c0 + k < rp_s[r + 1] - rp_s[r])
-                v = vals[BS == 1 ? e0 + (int64_t)(c0 + k) * 64 + l0 + r
-                                 : sell_val(e0 + (int64_t)(c0 + k) * 64 + l0 + r, B2, c)];
+        for (int q = tid; q < AW * AV * R; q += NT) {
+            const int r = q % R, kc = q / R, k = kc / AV;
+            double v = 0.0;   // bs = 3: the sums start from zero, stored values are added when the row is written
+            if (BS == 1 && !STORE && k < cw && c0 + k < rp_s[r + 1] - rp_s[r])
+                v = vals[e0 + (int64_t)(c0 + k) * 64 + l0 + r];
             acc_s[kc][r] = v;
         }
         // software pipeline over the batches: a thread's next incidence entry is loaded before the current batch
@@ -876,14 +923,9 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                     const int64_t e = ea >> 2;
                     const int a = ea & 3;
                     const int64_t* c = cncur;
-                    double g[4][3];
-                    double det;
-                    if constexpr (Cfg::XP) det = tet4_grads_p(xc, g);
-                    else det = tet4_grads_n(X, cncur, g);
-                    if (c0 == 0 && fabs(det) < 1e-12) atomicMin((unsigned long long*)bad, (unsigned long long)e);
-                    const double V = fabs(det) / 6.0;
                     const int cl = rp_s[r] - seg0, cn = rp_s[r + 1] - rp_s[r];
                     int nodes[4];
+                    uint32_t pp[4];
                     pk[0] = pk[1] = 0u;
 #pragma unroll
                     for (int bb = 0; bb < 4; ++bb) {
@@ -891,19 +933,46 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                         nodes[bb] = j;
                         // the tile-uniform branch keeps the LDS search on ds_read (one pointer for both would
                         // make every probe a flat load)
-                        const uint32_t p = staged ? sorted_pos(col_s + cl, cn, j) : sorted_pos(colidx + seg0 + cl, cn, j);
-                        pk[bb >> 1] |= p << (16 * (bb & 1));
-                        if constexpr (BS == 1) dat_s[bb][it0] = p1_value(g[a], g[bb], E, V);
+                        pp[bb] = staged ? sorted_pos(col_s + cl, cn, j) : sorted_pos(colidx + seg0 + cl, cn, j);
+                        pk[bb >> 1] |= pp[bb] << (16 * (bb & 1));
+                    }
+                    double g[4][3];
+                    double det;
+                    if constexpr (Cfg::XS) {
+                        if (staged) {   // every element node is a column of the row: its coordinates are in LDS
+                            double xq[4][3];
+#pragma unroll
+                            for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+                                for (int q = 0; q < 3; ++q) xq[bb][q] = xs_s[cl + (int)pp[bb]][q];
+                            det = tet4_grads_p(xq, g);
+                        } else {
+                            det = tet4_grads_n(X, cncur, g);
+                        }
+                    } else if constexpr (Cfg::XP) {
+                        det = tet4_grads_p(xc, g);
+                    } else {
+                        det = tet4_grads_n(X, cncur, g);
+                    }
+                    if (c0 == 0 && fabs(det) < 1e-12) atomicMin((unsigned long long*)bad, (unsigned long long)e);
+                    const double V = fabs(det) / 6.0;
+                    if constexpr (BS == 1) {
+#pragma unroll
+                        for (int bb = 0; bb < 4; ++bb) dat_s[bb][it0] = p1_value(g[a], g[bb], E, V);
                     }
                     const bool rep = nodes[0] == nodes[1] || nodes[0] == nodes[2] || nodes[0] == nodes[3] ||
                                      nodes[1] == nodes[2] || nodes[1] == nodes[3] || nodes[2] == nodes[3];
                     aflag = (uint8_t)(a | (rep ? 0x80 : 0));
                     if constexpr (BS == 3) {
 #pragma unroll
+                        for (int q = 0; q < 3; ++q) {
+                            const double gaq = a == 0 ? g[0][q] : a == 1 ? g[1][q] : a == 2 ? g[2][q] : g[3][q];
+                            dat_s[q][it0] = V * gaq;
+                        }
+#pragma unroll
                         for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
-                            for (int q = 0; q < 3; ++q) dat_s[3 * bb + q][it0] = g[bb][q];
-                        dat_s[12][it0] = V;
+                            for (int q = 0; q < 3; ++q) dat_s[3 + 3 * bb + q][it0] = g[bb][q];
                     }
                 }
                 if (tid < NI) {
@@ -931,40 +1000,62 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                 const uint2 pp = pos_s[it];
                 const uint32_t praw = ((lb < 2 ? pp.x : pp.y) >> (16 * (lb & 1))) & 0xffffu;
                 const int k = (int)praw - c0;
-                const bool hit = lactive && praw != 0xffffu && k >= 0 && k < cw;
+                const bool hit = praw != 0xffffu && k >= 0 && k < cw;
                 const uint8_t af = a_s[it];
-                double v[BS * RPL];
+                // bs = 3: NV products M[r][c] = (V g_a[r]) g_b[c] of the lane's block rows, then (P lane / LPR = 4)
+                // P = (V g_a) . g_b; every value lands in its own accumulator slot of column k
+                constexpr int NV = BS == 1 ? 1 : (LPR == 4 ? 10 : 3);
+                double v[NV];
+                int slot0 = 0;        // first accumulator slot of the lane's values (consecutive)
+                int nv = 0;           // values of this lane
                 if (hit) {
                     if constexpr (BS == 1) {
                         v[0] = dat_s[lb][it];
+                        nv = 1;
                     } else {
-                        const int aa = af & 3;
-                        const double ga[3] = {dat_s[3 * aa][it], dat_s[3 * aa + 1][it], dat_s[3 * aa + 2][it]};
-                        const double gb[3] = {dat_s[3 * lb][it], dat_s[3 * lb + 1][it], dat_s[3 * lb + 2][it]};
-                        const double V = dat_s[12][it];
-                        const double dot = el_dot(ga, gb);
+                        const double gb[3] = {dat_s[3 + 3 * lb][it], dat_s[4 + 3 * lb][it], dat_s[5 + 3 * lb][it]};
+                        if (LPR == 4) {
+                            const double vga[3] = {dat_s[0][it], dat_s[1][it], dat_s[2][it]};
 #pragma unroll
-                        for (int q = 0; q < RPL; ++q)
+                            for (int rr = 0; rr < 3; ++rr)
 #pragma unroll
-                            for (int cc = 0; cc < 3; ++cc) v[q * 3 + cc] = el_value(L, ga, gb, lrr + q, cc, dot, V);
+                                for (int cc = 0; cc < 3; ++cc) v[rr * 3 + cc] = vga[rr] * gb[cc];
+                            v[NV - 1] = el_pdot(vga, gb);
+                            nv = 10;
+                        } else if (lrr < 3) {
+                            const double vr = dat_s[lrr][it];
+#pragma unroll
+                            for (int cc = 0; cc < 3; ++cc) v[cc] = vr * gb[cc];
+                            slot0 = lrr * 3;
+                            nv = 3;
+                        } else {
+                            const double vga[3] = {dat_s[0][it], dat_s[1][it], dat_s[2][it]};
+                            v[0] = el_pdot(vga, gb);
+                            slot0 = 9;
+                            nv = 1;
+                        }
                     }
                 }
                 const bool any_rep = __ballot(hit && (af & 0x80)) != 0;
                 if (!any_rep) {
                     if (hit) {
 #pragma unroll
-                        for (int cc = 0; cc < BS * RPL; ++cc) {
-                            double* ap = &acc_s[k * B2 + lrr * BS + cc][lr];
-                            *ap = add_nc(*ap, v[cc]);
+                        for (int cc = 0; cc < NV; ++cc) {
+                            if (cc < nv) {
+                                double* ap = &acc_s[k * AV + slot0 + cc][lr];
+                                *ap = add_nc(*ap, v[cc]);
+                            }
                         }
                     }
                 } else {   // an element repeating a node: its nodes' contributions one after the other (b order)
                     for (int b = 0; b < 4; ++b) {
                         if (hit && lb == b) {
 #pragma unroll
-                            for (int cc = 0; cc < BS * RPL; ++cc) {
-                                double* ap = &acc_s[k * B2 + lrr * BS + cc][lr];
-                                *ap = add_nc(*ap, v[cc]);
+                            for (int cc = 0; cc < NV; ++cc) {
+                                if (cc < nv) {
+                                    double* ap = &acc_s[k * AV + slot0 + cc][lr];
+                                    *ap = add_nc(*ap, v[cc]);
+                                }
                             }
                         }
                         __builtin_amdgcn_wave_barrier();
@@ -978,7 +1069,16 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
             const int r = q % R, kc = q / R, k = kc / B2, c = kc - k * B2;
             if (!STORE && c0 + k >= rp_s[r + 1] - rp_s[r]) continue;   // adding: padding stays as stored
             const int64_t Ei = e0 + (int64_t)(c0 + k) * 64 + l0 + r;
-            vals[BS == 1 ? Ei : sell_val(Ei, B2, c)] = acc_s[kc][r];
+            if constexpr (BS == 1) {
+                vals[Ei] = acc_s[kc][r];
+            } else {
+                const int rr = c / 3, cc = c - 3 * (c / 3);
+                double kv = el_combine(L, acc_s[k * AV + c][r], acc_s[k * AV + cc * 3 + rr][r], acc_s[k * AV + 9][r],
+                                       rr == cc);
+                double* dst = &vals[sell_val(Ei, B2, c)];
+                if constexpr (!STORE) kv = add_nc(*dst, kv);
+                *dst = kv;
+            }
         }
     }
 }
@@ -1074,7 +1174,7 @@ __global__ void __launch_bounds__(256) k_assemble_el3w(const double* __restrict_
                                                        const int32_t* __restrict__ colidx,
                                                        const int64_t* __restrict__ csr2sell, double* __restrict__ vals,
                                                        int64_t* __restrict__ bad) {
-    __shared__ double blk_s[AW_WAVES][AE_K][4][9];
+    __shared__ double blk_s[AW_WAVES][AE_K][4][10];   // per (element, b): M_ab (9) and P_ab
     __shared__ uint32_t pos_s[AW_WAVES][AE_K];
     __shared__ int col_s[AW_WAVES][21];
     constexpr int JG = 21;
@@ -1090,12 +1190,9 @@ __global__ void __launch_bounds__(256) k_assemble_el3w(const double* __restrict_
             const int jl = lane / 3, r = lane - 3 * (lane / 3);
             const bool owner = lane < nj * 3;
             int64_t Ei = 0;
-            double acc[3] = {0.0, 0.0, 0.0};
-            if (owner) {
-                Ei = csr2sell[lo + j0 + jl];
-#pragma unroll
-                for (int c = 0; c < 3; ++c) acc[c] = vals[sell_val(Ei, 9, r * 3 + c)];
-            }
+            // owner (column jl, block row r): M row r and M column r of the block, P; stored values added at the end
+            double mr[3] = {0.0, 0.0, 0.0}, mc[3] = {0.0, 0.0, 0.0}, pp = 0.0;
+            if (owner) Ei = csr2sell[lo + j0 + jl];
             for (int k0 = 0; k0 < C; k0 += AE_K) {
                 const int nk = min(AE_K, C - k0);
                 __builtin_amdgcn_wave_barrier();
@@ -1108,15 +1205,18 @@ __global__ void __launch_bounds__(256) k_assemble_el3w(const double* __restrict_
                     const double det = tet4_grads(X, c, g);
                     if (j0 == 0 && fabs(det) < 1e-12) atomicMin((unsigned long long*)bad, (unsigned long long)e);
                     const double V = fabs(det) / 6.0;
+                    double vga[3];
+#pragma unroll
+                    for (int q = 0; q < 3; ++q)
+                        vga[q] = V * (a == 0 ? g[0][q] : a == 1 ? g[1][q] : a == 2 ? g[2][q] : g[3][q]);
                     uint32_t packed = 0;
 #pragma unroll
                     for (int b = 0; b < 4; ++b) {
-                        const double dot = el_dot(g[a], g[b]);
 #pragma unroll
                         for (int rr = 0; rr < 3; ++rr)
 #pragma unroll
-                            for (int kk = 0; kk < 3; ++kk)
-                                blk_s[wid][lane][b][rr * 3 + kk] = el_value(L, g[a], g[b], rr, kk, dot, V);
+                            for (int kk = 0; kk < 3; ++kk) blk_s[wid][lane][b][rr * 3 + kk] = vga[rr] * g[b][kk];
+                        blk_s[wid][lane][b][9] = el_pdot(vga, g[b]);
                         const int j = (int)c[b];
                         int l = 0, h = nj;
                         while (l < h) {
@@ -1136,10 +1236,13 @@ __global__ void __launch_bounds__(256) k_assemble_el3w(const double* __restrict_
 #pragma unroll
                         for (int b = 0; b < 4; ++b)
                             if (((pk >> (8 * b)) & 0xffu) == (uint32_t)jl) {
-                                const double* br = &blk_s[wid][k][b][r * 3];
-                                acc[0] += br[0];
-                                acc[1] += br[1];
-                                acc[2] += br[2];
+                                const double* br = blk_s[wid][k][b];
+#pragma unroll
+                                for (int c = 0; c < 3; ++c) {
+                                    mr[c] += br[r * 3 + c];
+                                    mc[c] += br[c * 3 + r];
+                                }
+                                pp += br[9];
                             }
                     }
                 }
@@ -1147,7 +1250,10 @@ __global__ void __launch_bounds__(256) k_assemble_el3w(const double* __restrict_
             }
             if (owner) {
 #pragma unroll
-                for (int c = 0; c < 3; ++c) vals[sell_val(Ei, 9, r * 3 + c)] = acc[c];
+                for (int c = 0; c < 3; ++c) {
+                    double* dst = &vals[sell_val(Ei, 9, r * 3 + c)];
+                    *dst = add_nc(*dst, el_combine(L, mr[c], mc[c], pp, r == c));
+                }
             }
             __builtin_amdgcn_wave_barrier();
         }
@@ -1394,11 +1500,25 @@ int fem_assemble_from_ke_ex(const double* Ke, const int64_t* conn, int npe, int 
                 FEM_HIP(hipStreamSynchronize(S(stream)));
                 nnz &= 0xffffffffLL;
             }
-            double* tmp = nullptr;
-            FEM_HIP(hipMallocAsync((void**)&tmp, sizeof(double) * 9 * (size_t)(nnz > 0 ? nnz : 1), S(stream)));
             // FEM355_KE_COLS set: the column-owner form (k_assemble_ke_w) instead of the element-row form (read per
             // call: the parity test compares both in one process)
             const bool colform = getenv("FEM355_KE_COLS") != nullptr;
+            if (store && !colform && getenv("FEM355_KE_SELLW") != nullptr) {   // straight into the SELL planes
+#define FEM_KE_S(P)                                                                                             \
+    if (npe == P)                                                                                               \
+        hipLaunchKernelGGL((k_assemble_ke_rows3<P, true>), g, dim3(256), 0, S(stream), Ke, conn, inc_ptr, inc, N, \
+                           rowptr, colidx, vals, slice_ptr);
+                FEM_KE_S(4) FEM_KE_S(6) FEM_KE_S(8) FEM_KE_S(10)
+#undef FEM_KE_S
+                FEM_LAUNCHED();
+                if (N & 63) {
+                    hipLaunchKernelGGL(k_sell_tail_zero, dim3(1), dim3(256), 0, S(stream), slice_ptr, N, 9, vals);
+                    FEM_LAUNCHED();
+                }
+                return FEM_OK;
+            }
+            double* tmp = nullptr;
+            FEM_HIP(hipMallocAsync((void**)&tmp, sizeof(double) * 9 * (size_t)(nnz > 0 ? nnz : 1), S(stream)));
 #define FEM_KE_C(P)                                                                                             \
     if (npe == P && colform)                                                                                    \
         hipLaunchKernelGGL((k_assemble_ke_w<3, P, FEM_KE_RPL3, true>), g, dim3(256), 0, S(stream), Ke, conn,     \

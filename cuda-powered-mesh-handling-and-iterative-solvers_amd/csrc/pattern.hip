@@ -52,6 +52,7 @@ constexpr int INB_G1 = 512;        // level-1 workgroups (chunks of slots), 1024
 constexpr int INB_T1 = 1024;
 constexpr int INB_MAXB = 16384;    // buckets (LDS histogram of level 1: 64 KB)
 constexpr int INB_CAP = 3584;      // entries of a bucket sorted in LDS (10 bytes each)
+constexpr int INC_BIG = 4096;      // node segments longer than this are sorted by k_inc_big (> INB_CAP: global tier)
 constexpr int INB_MAXSH = 8;       // at most 256 nodes per bucket: N <= 4M nodes (larger meshes: the radix form)
 
 static int inb_shift(int64_t N) {   // bucket = 128 nodes, 256 when N / 128 would exceed INB_MAXB buckets
@@ -258,6 +259,7 @@ __global__ void __launch_bounds__(256) k_inc_l2(const int2* __restrict__ kpair,
             while (l + 1 < B && st[l + 1] <= p) ++l;   // empty segments share a start
             a = st[l];
             z = st[l + 1];
+            if (z - a > INC_BIG) continue;   // a hub's segment: k_inc_big sorts it (the rank sort is O(len^2))
             int r = a;
             for (int u = a; u < z; ++u) r += (scratch[lo + u] < v);
             inc[lo + r] = v;
@@ -568,6 +570,82 @@ __device__ __forceinline__ int gb_scan(int v, int* wsum, int* total) {
     return before + incl - v;
 }
 
+// The ascending distinct values of get(0 .. C-1) (non-negative ints), written through put(rank, value); returns
+// their count. Bitmap windows of GB_WORDS * 32 ids over [min, max] in LDS (bm), one pass over the values per
+// window. Whole-workgroup call (GB_T threads, uniform arguments); *lo / *hi receive the value range.
+template <bool PUT, class Get, class Put>
+__device__ int gb_sorted_unique(Get get, int C, Put put, uint32_t* bm, int* wsum, int* lo_s, int* hi_s, int* lo_out,
+                                int* hi_out) {
+    const int tid = threadIdx.x;
+    int lo = INT_MAX, hi = -1;
+    for (int t = tid; t < C; t += GB_T) {
+        const int v = get(t);
+        lo = min(lo, v);
+        hi = max(hi, v);
+    }
+    lo = wave_min_i32(lo);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) hi = max(hi, __shfl_xor(hi, o));
+    if (tid == 0) {
+        *lo_s = INT_MAX;
+        *hi_s = -1;
+    }
+    __syncthreads();
+    if ((tid & 63) == 0) {
+        atomicMin(lo_s, lo);
+        atomicMax(hi_s, hi);
+    }
+    __syncthreads();
+    lo = *lo_s;
+    hi = *hi_s;
+    *lo_out = lo;
+    *hi_out = hi;
+    int U = 0;
+    for (int64_t w0 = lo; w0 <= hi; w0 += (int64_t)GB_WORDS * 32) {
+        const int64_t span = min<int64_t>((int64_t)hi - w0 + 1, (int64_t)GB_WORDS * 32);
+        const int nw = (int)((span + 31) >> 5);
+        for (int k = tid; k < nw; k += GB_T) bm[k] = 0u;
+        __syncthreads();
+        for (int t = tid; t < C; t += GB_T) {
+            const int64_t d = (int64_t)get(t) - w0;
+            if (d >= 0 && d < span) atomicOr(&bm[d >> 5], 1u << (d & 31));
+        }
+        __syncthreads();
+        // thread tid owns words [k0, k1): count, scan, then write its values in ascending order
+        const int per = (nw + GB_T - 1) / GB_T;
+        const int k0 = min(tid * per, nw), k1 = min(k0 + per, nw);
+        int cnt = 0;
+        for (int k = k0; k < k1; ++k) cnt += __popc(bm[k]);
+        int total;
+        const int off = gb_scan(cnt, wsum, &total);
+        if (PUT) {
+            int o = U + off;
+            for (int k = k0; k < k1; ++k) {
+                uint32_t m = bm[k];
+                while (m) {
+                    const int bit = __ffs(m) - 1;
+                    m &= m - 1;
+                    put(o++, (int)(w0 + 32 * (int64_t)k + bit));
+                }
+            }
+        }
+        U += total;
+        __syncthreads();   // bitmap reusable
+    }
+    return U;
+}
+
+// the rows / nodes of [base, base + GB_T) with `big(i)`, gathered into rows_s (any order; each is independent)
+template <class Big>
+__device__ int gb_collect(int64_t base, int64_t N, Big big, int* rows_s, int* nrows_s) {
+    if (threadIdx.x == 0) *nrows_s = 0;
+    __syncthreads();
+    const int64_t me = base + threadIdx.x;
+    if (me < N && big(me)) rows_s[atomicAdd(nrows_s, 1)] = (int)threadIdx.x;
+    __syncthreads();
+    return *nrows_s;
+}
+
 template <bool FILL>
 __global__ void __launch_bounds__(GB_T) k_graph_big(const int64_t* __restrict__ conn, int npe,
                                                     const int32_t* __restrict__ inc_ptr,
@@ -579,79 +657,48 @@ __global__ void __launch_bounds__(GB_T) k_graph_big(const int64_t* __restrict__ 
     __shared__ int rows_s[GB_T];
     __shared__ int nrows_s, lo_s, hi_s;
     __shared__ int wsum[GB_T / 64];
-    const int tid = threadIdx.x;
     for (int64_t base = (int64_t)blockIdx.x * GB_T; base < N; base += (int64_t)gridDim.x * GB_T) {
-        if (tid == 0) nrows_s = 0;
-        __syncthreads();
-        const int64_t me = base + tid;
-        if (me < N && (FILL ? rowptr[me + 1] - rowptr[me] > G_UCAP : row_len[me] < 0))
-            rows_s[atomicAdd(&nrows_s, 1)] = tid;
-        __syncthreads();
-        const int nr = nrows_s;
+        const int nr = gb_collect(base, N, [&](int64_t i) {
+            return FILL ? rowptr[i + 1] - rowptr[i] > G_UCAP : row_len[i] < 0;
+        }, rows_s, &nrows_s);
         for (int q = 0; q < nr; ++q) {
             const int64_t node = base + rows_s[q];
             const int start = inc_ptr[node];
             const int C = (inc_ptr[node + 1] - start) * npe;
-            int lo = INT_MAX, hi = -1;
-            for (int t = tid; t < C; t += GB_T) {
-                const int v = big_cand(conn, npe, inc, start, t);
-                lo = min(lo, v);
-                hi = max(hi, v);
-            }
-            lo = wave_min_i32(lo);
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) hi = max(hi, __shfl_xor(hi, o));
-            if (tid == 0) {
-                lo_s = INT_MAX;
-                hi_s = -1;
-            }
-            __syncthreads();
-            if ((tid & 63) == 0) {
-                atomicMin(&lo_s, lo);
-                atomicMax(&hi_s, hi);
-            }
-            __syncthreads();
-            lo = lo_s;
-            hi = hi_s;
-            if (!FILL && far && tid == 0 && hi >= lo && (hi - (int)node > 32767 || (int)node - lo > 32767) && !*far)
-                atomicOr(far, 1);
             const int32_t rp = FILL ? rowptr[node] : 0;
-            int U = 0;
-            for (int64_t w0 = lo; w0 <= hi; w0 += (int64_t)GB_WORDS * 32) {
-                const int64_t span = min<int64_t>((int64_t)hi - w0 + 1, (int64_t)GB_WORDS * 32);
-                const int nw = (int)((span + 31) >> 5);
-                for (int k = tid; k < nw; k += GB_T) bm[k] = 0u;
-                __syncthreads();
-                for (int t = tid; t < C; t += GB_T) {
-                    const int64_t d = (int64_t)big_cand(conn, npe, inc, start, t) - w0;
-                    if (d >= 0 && d < span) atomicOr(&bm[d >> 5], 1u << (d & 31));
-                }
-                __syncthreads();
-                // thread tid owns words [k0, k1): count, scan, then (fill) write its ids in ascending order
-                const int per = (nw + GB_T - 1) / GB_T;
-                const int k0 = min(tid * per, nw), k1 = min(k0 + per, nw);
-                int cnt = 0;
-                for (int k = k0; k < k1; ++k) cnt += __popc(bm[k]);
-                int total;
-                const int off = gb_scan(cnt, wsum, &total);
-                if (FILL) {
-                    int o = rp + U + off;
-                    for (int k = k0; k < k1; ++k) {
-                        uint32_t m = bm[k];
-                        while (m) {
-                            const int bit = __ffs(m) - 1;
-                            m &= m - 1;
-                            const int v = (int)(w0 + 32 * (int64_t)k + bit);
-                            colidx[o] = v;
-                            if (v == (int)node) diagpos[node] = o;
-                            ++o;
-                        }
-                    }
-                }
-                U += total;
-                __syncthreads();   // bitmap reusable
+            int lo, hi;
+            const int U = gb_sorted_unique<FILL>(
+                [&](int t) { return big_cand(conn, npe, inc, start, t); }, C,
+                [&](int o, int v) {
+                    colidx[rp + o] = v;
+                    if (v == (int)node) diagpos[node] = rp + o;
+                },
+                bm, wsum, &lo_s, &hi_s, &lo, &hi);
+            if (!FILL && threadIdx.x == 0) {
+                row_len[node] = U;
+                if (far && hi >= lo && (hi - (int)node > 32767 || (int)node - lo > 32767) && !*far) atomicOr(far, 1);
             }
-            if (!FILL && tid == 0) row_len[node] = U;
+        }
+    }
+}
+
+// node segments of the incidence longer than INC_BIG (hub nodes; k_inc_l2 leaves them in arrival order in scratch):
+// ascending into inc by the bitmap sort (slots are distinct)
+__global__ void __launch_bounds__(GB_T) k_inc_big(const int32_t* __restrict__ inc_ptr, int64_t N,
+                                                  const int32_t* __restrict__ scratch, int32_t* __restrict__ inc) {
+    extern __shared__ uint32_t bm[];
+    __shared__ int rows_s[GB_T];
+    __shared__ int nrows_s, lo_s, hi_s;
+    __shared__ int wsum[GB_T / 64];
+    for (int64_t base = (int64_t)blockIdx.x * GB_T; base < N; base += (int64_t)gridDim.x * GB_T) {
+        const int nr = gb_collect(base, N, [&](int64_t i) { return inc_ptr[i + 1] - inc_ptr[i] > INC_BIG; }, rows_s,
+                                  &nrows_s);
+        for (int q = 0; q < nr; ++q) {
+            const int64_t node = base + rows_s[q];
+            const int a = inc_ptr[node], C = inc_ptr[node + 1] - a;
+            int lo, hi;
+            gb_sorted_unique<true>([&](int t) { return scratch[a + t]; }, C,
+                                   [&](int o, int v) { inc[a + o] = v; }, bm, wsum, &lo_s, &hi_s, &lo, &hi);
         }
     }
 }
@@ -886,6 +933,28 @@ int64_t fem_incidence_work_bytes(int64_t total, int64_t N) {
     return radix > bucket ? radix : bucket;
 }
 
+static int big_grid(int64_t N) {
+    int64_t g = cdiv(N, (int64_t)GB_T);
+    if (g > 1024) g = 1024;
+    return (int)(g < 1 ? 1 : g);
+}
+
+// the big-row kernels take 128 KB of dynamic LDS (set once per process)
+static int big_lds_attr() {
+    static const int rc = [] {
+        if (hipFuncSetAttribute((const void*)k_graph_big<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)GB_LDS) != hipSuccess ||
+            hipFuncSetAttribute((const void*)k_graph_big<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)GB_LDS) != hipSuccess ||
+            hipFuncSetAttribute((const void*)k_inc_big, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)GB_LDS) != hipSuccess)
+            return (int)FEM_EHIP;
+        return (int)FEM_OK;
+    }();
+    if (rc != FEM_OK) set_error("k_graph_big: cannot allow %zu bytes of dynamic LDS", GB_LDS);
+    return rc;
+}
+
 static int incidence_bucket(const int64_t* conn, int64_t total, int64_t N, int32_t* inc_ptr, int32_t* inc,
                             char* base, int32_t* bad, fem_stream_t stream) {
     hipStream_t st = S(stream);
@@ -912,6 +981,11 @@ static int incidence_bucket(const int64_t* conn, int64_t total, int64_t N, int32
     hipLaunchKernelGGL(k_inc_l2, dim3((unsigned)nb), dim3(256), l2, st, kpair, off, INB_G1, N, bsh, scratch,
                        inc_ptr, inc);
     FEM_LAUNCHED();
+    if (total > INC_BIG) {   // hub segments (the launch finds them; for ordinary meshes it only reads inc_ptr)
+        if (const int brc = big_lds_attr()) return brc;
+        hipLaunchKernelGGL(k_inc_big, dim3(big_grid(N)), dim3(GB_T), GB_LDS, st, inc_ptr, N, scratch, inc);
+        FEM_LAUNCHED();
+    }
     return FEM_OK;
 }
 
@@ -963,26 +1037,6 @@ static int graph_grid(int64_t N) {
     int64_t g = cdiv(N, G_WAVES);
     if (g > 4096) g = 4096;
     return (int)(g < 1 ? 1 : g);
-}
-
-static int big_grid(int64_t N) {
-    int64_t g = cdiv(N, (int64_t)GB_T);
-    if (g > 1024) g = 1024;
-    return (int)(g < 1 ? 1 : g);
-}
-
-// the big-row kernels take 128 KB of dynamic LDS (set once per process)
-static int big_lds_attr() {
-    static const int rc = [] {
-        if (hipFuncSetAttribute((const void*)k_graph_big<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)GB_LDS) != hipSuccess ||
-            hipFuncSetAttribute((const void*)k_graph_big<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)GB_LDS) != hipSuccess)
-            return (int)FEM_EHIP;
-        return (int)FEM_OK;
-    }();
-    if (rc != FEM_OK) set_error("k_graph_big: cannot allow %zu bytes of dynamic LDS", GB_LDS);
-    return rc;
 }
 
 // count: k_graph for every row (done = null) or for the rows k_graph_small left, then k_graph_big for the rows

@@ -795,11 +795,18 @@ def test_element_row_assembly_bit_identical_to_column_form(gpu, etype, n, rep, m
     if rep > 1:
         rp = g.rowptr.cpu()
         assert int((rp[1:] - rp[:-1]).max()) > 64 or int((g.inc_ptr[1:] - g.inc_ptr[:-1]).max()) > 64
+    def fresh():
+        A = system.SellMatrix(g, 3)
+        A._vals.fill_(float("nan"))   # a fresh matrix is stored whole: no entry may be left unwritten
+        return A.add_element_matrices(K, tg).vals.clone()
     monkeypatch.delenv("FEM355_KE_COLS", raising=False)
-    a = system.SellMatrix(g, 3).add_element_matrices(K, tg).vals.clone()
+    a = fresh()
+    monkeypatch.setenv("FEM355_KE_SELLW", "1")      # the row sums straight into the SELL planes
+    d = fresh()
+    monkeypatch.delenv("FEM355_KE_SELLW", raising=False)
     monkeypatch.setenv("FEM355_KE_COLS", "1")
-    b = system.SellMatrix(g, 3).add_element_matrices(K, tg).vals.clone()
-    assert torch.equal(a, b), etype
+    b = fresh()
+    assert torch.equal(a, b) and torch.equal(a, d), etype
 
 
 @pytest.mark.parametrize("kind,mode,small", [("elastic", "cg", False), ("elastic", "pcg", False),

@@ -81,6 +81,8 @@ def main():
     out["elements_total"] = total_el
     print(json.dumps(out), flush=True)
 
+    if a.cpu_sample <= 0:   # profiling passes: GPU work only
+        return
     from oracle import ref_cpu as R
     cpu = {}
     for et, gen, n in FAMILIES:
