@@ -63,6 +63,7 @@ SIGNATURES = {
     "fem_sell_csr2sell": (_I, [_P, _L, _P, _P, _P]),
     "fem_assemble_from_ke": (_I, [_P, _P, _I, _I, _P, _P, _L, _P, _P, _P, _P, _P, _P]),
     "fem_assemble_from_ke_ex": (_I, [_P, _P, _I, _I, _P, _P, _L, _P, _P, _P, _P, _L, _L, _I, _P, _P]),
+    "fem_assemble_from_ke_ex2": (_I, [_P, _P, _I, _I, _P, _P, _L, _P, _P, _P, _P, _L, _L, _I, _I, _P, _P]),
     "fem_assemble_tet4": (_I, [_P, _P, _D, _D, _I, _P, _P, _L, _P, _P, _P, _P, _P, _P, _P]),
     "fem_assemble_tet4_ex": (_I, [_P, _P, _D, _D, _I, _P, _P, _L, _P, _P, _P, _P, _I, _P, _P, _P]),
     "fem_assemble_tet4_ex2": (_I, [_P, _P, _D, _D, _I, _P, _P, _L, _P, _P, _P, _P, _I, _I, _P, _P, _P]),
@@ -116,6 +117,13 @@ SIGNATURES = {
     "fem_pcg_get_schedule": (_I, [_P]),
     "fem_pcg_uniform_slices": (_I, [_P, _L, _L, _P, _P, _P]),
     "fem_pcg_persist_build": (_I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    "fem_sell_sl_pattern": (_I, [_L, _P, _P, _I, _P, _P, _P, _P, _P]),
+    "fem_assemble_tet4_sl": (_I, [_P, _P, _D, _D, _I, _P, _P, _L, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P]),
+    "fem_assemble_from_ke_sl": (_I, [_P, _P, _I, _P, _P, _L, _P, _P, _P, _I, _I, _P, _P]),
+    "fem_jacobi_sl": (_I, [_P, _I, _P, _P, _P, _P, _P, _L, _P, _P, _P]),
+    "fem_spmv_sl": (_I, [_L, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "fem_sell_sl_unpair": (_I, [_L, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "fem_pcg_set_layout": (_I, [_P, _P, _P, _P, _P, _P, _I]),
     "fem_pcg_persist_profile": (_I, [_P, _I, _P, ctypes.POINTER(_I)]),
     "fem_pcg_set_constraints": (_I, [_P, _I, _L, _P, _P, _L, _P, _P, _L, _P, _P, _P, _P, _P]),
     "fem_enforce_constraints": (_I, [_P, _P, _L, _I, _L, _P, _P, _L, _P, _P, _L, _P, _P, _P, _P, _P, _P]),

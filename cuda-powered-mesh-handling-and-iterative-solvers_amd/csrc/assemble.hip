@@ -522,6 +522,100 @@ __global__ void __launch_bounds__(256) k_assemble_ke_w(const double* __restrict_
 // 8-byte stores whose 16 rows per 128-byte line are written by the workgroups of one XCD at about the same time),
 // instead of the block-CSR buffer + k_csr_add_sell pass (FEM355_KE_SELLW A/B).
 constexpr int KR_LMAX = 64;
+
+// per-lane constants of the element-row form: for the lane's NL loaded values, element node b of the value's column
+// and the offset r*3 + c inside the 3x3 block
+template <int NPE>
+struct KeRowLane {
+    static constexpr int BS = 3, D = NPE * BS, RV = BS * D, NL = (RV + 63) / 64, KU = 64 / NPE;
+    int vb[NL], vo[NL];
+    bool vv[NL];
+    __device__ __forceinline__ explicit KeRowLane(int lane) {
+#pragma unroll
+        for (int m = 0; m < NL; ++m) {
+            const int idx = lane + 64 * m;
+            vv[m] = idx < RV;
+            const int r = idx / D, col = idx - D * (idx / D);
+            vb[m] = col / BS;
+            vo[m] = r * BS + (col - BS * (col / BS));
+        }
+    }
+};
+
+// One wave, one row i, one column window [j0, j0 + nj) of it (cs = those columns, staged by the caller): acc[slot *
+// 9 + r * 3 + c] += the row's K_e block rows over its incidences in ascending (incidence, b) order (acc zeroed by the
+// caller). Scratch: slot_s / koff_s / eid_s [64] of this wave.
+template <int NPE>
+__device__ __forceinline__ void ke_row3(const KeRowLane<NPE>& L, const double* __restrict__ Ke,
+                                        const int64_t* __restrict__ conn, const int32_t* __restrict__ inc, int t0,
+                                        int C, const int* cs, int nj, double* acc, int* slot_s, int64_t* koff_s,
+                                        int* eid_s, int lane) {
+    constexpr int B2 = 9, D = KeRowLane<NPE>::D, RV = KeRowLane<NPE>::RV, NL = KeRowLane<NPE>::NL;
+    constexpr int KU = KeRowLane<NPE>::KU;
+    for (int k0 = 0; k0 < C; k0 += 64) {
+        const int nk = min(64, C - k0);
+        __builtin_amdgcn_wave_barrier();
+        if (lane < nk) {
+            const int ea = inc[t0 + k0 + lane];
+            const int e = ea / NPE;
+            koff_s[lane] = (int64_t)e * D * D + (int64_t)(ea - e * NPE) * RV;
+            eid_s[lane] = e;
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (int kb = 0; kb < nk; kb += KU) {
+            const int nu = min(KU, nk - kb);
+            double v[KU][NL];
+#pragma unroll
+            for (int u = 0; u < KU; ++u) {
+                const int64_t ko = koff_s[kb + (u < nu ? u : 0)];
+#pragma unroll
+                for (int m = 0; m < NL; ++m) v[u][m] = (u < nu && L.vv[m]) ? Ke[ko + lane + 64 * m] : 0.0;
+            }
+            int dup = 0;
+            if (lane < nu * NPE) {   // slot of node b of incidence u in this column window (-1: outside)
+                const int u = lane / NPE, b = lane - NPE * (lane / NPE);
+                const int64_t eb = (int64_t)eid_s[kb + u] * NPE;
+                const int node = (int)conn[eb + b];
+                int l = 0, h = nj;
+                while (l < h) {
+                    const int mid = (l + h) >> 1;
+                    if (cs[mid] < node) l = mid + 1;
+                    else h = mid;
+                }
+                slot_s[lane] = (l < nj && cs[l] == node) ? l : -1;
+                for (int b2 = 0; b2 < b; ++b2) dup |= (int)conn[eb + b2] == node;
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (!__any(dup)) {
+#pragma unroll
+                for (int u = 0; u < KU; ++u) {
+                    if (u >= nu) break;
+#pragma unroll
+                    for (int m = 0; m < NL; ++m) {
+                        if (!L.vv[m]) continue;
+                        const int s = slot_s[u * NPE + L.vb[m]];
+                        if (s >= 0) acc[s * B2 + L.vo[m]] += v[u][m];
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
+            } else {   // an element lists a node twice: its b's one after the other
+                for (int u = 0; u < nu; ++u)
+                    for (int bb = 0; bb < NPE; ++bb) {
+#pragma unroll
+                        for (int m = 0; m < NL; ++m) {
+                            if (!L.vv[m] || L.vb[m] != bb) continue;
+                            const int s = slot_s[u * NPE + bb];
+                            if (s >= 0) acc[s * B2 + L.vo[m]] += v[u][m];
+                        }
+                        __builtin_amdgcn_wave_barrier();
+                    }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
 template <int NPE, bool SELLW = false>
 __global__ void __launch_bounds__(256) k_assemble_ke_rows3(const double* __restrict__ Ke, const int64_t* __restrict__ conn,
                                                            const int32_t* __restrict__ inc_ptr,
@@ -529,25 +623,14 @@ __global__ void __launch_bounds__(256) k_assemble_ke_rows3(const double* __restr
                                                            const int32_t* __restrict__ rowptr,
                                                            const int32_t* __restrict__ colidx, double* __restrict__ out,
                                                            const int64_t* __restrict__ slice_ptr = nullptr) {
-    constexpr int BS = 3, B2 = 9, D = NPE * BS, RV = BS * D;
-    constexpr int NL = (RV + 63) / 64;    // K_e loads per lane per incidence
-    constexpr int KU = 64 / NPE;          // incidences per batch: one lane per (incidence, element node)
+    constexpr int B2 = 9;
     __shared__ int cols_s[AW_WAVES][KR_LMAX];
     __shared__ double acc_s[AW_WAVES][KR_LMAX * B2];
     __shared__ int slot_s[AW_WAVES][64];
     __shared__ int64_t koff_s[AW_WAVES][64];
     __shared__ int eid_s[AW_WAVES][64];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int vb[NL], vo[NL];   // per loaded value: element node b of its column, offset r*3 + c in the 3x3 block
-    bool vv[NL];
-#pragma unroll
-    for (int m = 0; m < NL; ++m) {
-        const int idx = lane + 64 * m;
-        vv[m] = idx < RV;
-        const int r = idx / D, col = idx - D * (idx / D);
-        vb[m] = col / BS;
-        vo[m] = r * BS + (col - BS * (col / BS));
-    }
+    const KeRowLane<NPE> L(lane);
     int* cs = cols_s[wid];
     double* acc = acc_s[wid];
     const RowWalk rw = row_walk(AW_WAVES);
@@ -559,68 +642,7 @@ __global__ void __launch_bounds__(256) k_assemble_ke_rows3(const double* __restr
             __builtin_amdgcn_wave_barrier();
             if (lane < nj) cs[lane] = colidx[lo + j0 + lane];
             for (int t = lane; t < nj * B2; t += 64) acc[t] = 0.0;
-            for (int k0 = 0; k0 < C; k0 += 64) {
-                const int nk = min(64, C - k0);
-                __builtin_amdgcn_wave_barrier();
-                if (lane < nk) {
-                    const int ea = inc[t0 + k0 + lane];
-                    const int e = ea / NPE;
-                    koff_s[wid][lane] = (int64_t)e * D * D + (int64_t)(ea - e * NPE) * RV;
-                    eid_s[wid][lane] = e;
-                }
-                __builtin_amdgcn_wave_barrier();
-                for (int kb = 0; kb < nk; kb += KU) {
-                    const int nu = min(KU, nk - kb);
-                    double v[KU][NL];
-#pragma unroll
-                    for (int u = 0; u < KU; ++u) {
-                        const int64_t ko = koff_s[wid][kb + (u < nu ? u : 0)];
-#pragma unroll
-                        for (int m = 0; m < NL; ++m) v[u][m] = (u < nu && vv[m]) ? Ke[ko + lane + 64 * m] : 0.0;
-                    }
-                    int dup = 0;
-                    if (lane < nu * NPE) {   // slot of node b of incidence u in this column window (-1: outside)
-                        const int u = lane / NPE, b = lane - NPE * (lane / NPE);
-                        const int64_t eb = (int64_t)eid_s[wid][kb + u] * NPE;
-                        const int node = (int)conn[eb + b];
-                        int l = 0, h = nj;
-                        while (l < h) {
-                            const int mid = (l + h) >> 1;
-                            if (cs[mid] < node) l = mid + 1;
-                            else h = mid;
-                        }
-                        slot_s[wid][lane] = (l < nj && cs[l] == node) ? l : -1;
-                        for (int b2 = 0; b2 < b; ++b2) dup |= (int)conn[eb + b2] == node;
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    if (!__any(dup)) {
-#pragma unroll
-                        for (int u = 0; u < KU; ++u) {
-                            if (u >= nu) break;
-#pragma unroll
-                            for (int m = 0; m < NL; ++m) {
-                                if (!vv[m]) continue;
-                                const int s = slot_s[wid][u * NPE + vb[m]];
-                                if (s >= 0) acc[s * B2 + vo[m]] += v[u][m];
-                            }
-                            __builtin_amdgcn_wave_barrier();
-                        }
-                    } else {   // an element lists a node twice: its b's one after the other
-                        for (int u = 0; u < nu; ++u)
-                            for (int bb = 0; bb < NPE; ++bb) {
-#pragma unroll
-                                for (int m = 0; m < NL; ++m) {
-                                    if (!vv[m] || vb[m] != bb) continue;
-                                    const int s = slot_s[wid][u * NPE + bb];
-                                    if (s >= 0) acc[s * B2 + vo[m]] += v[u][m];
-                                }
-                                __builtin_amdgcn_wave_barrier();
-                            }
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
+            ke_row3<NPE>(L, Ke, conn, inc, t0, C, cs, nj, acc, slot_s[wid], koff_s[wid], eid_s[wid], lane);
             if constexpr (SELLW) {
                 const int64_t p0 = slice_ptr[i >> 6];
                 double* o = out + B2 * p0 + (i & 63);
@@ -638,6 +660,73 @@ __global__ void __launch_bounds__(256) k_assemble_ke_rows3(const double* __restr
             const int w = (int)((slice_ptr[(i >> 6) + 1] - p0) >> 6);
             double* o = out + B2 * p0 + (i & 63);
             for (int t = len * B2 + lane; t < w * B2; t += 64) o[(int64_t)64 * t] = 0.0;
+        }
+    }
+}
+
+// Tile form (default for fem_assemble_from_ke_ex2, bs = 3): R consecutive rows of one SELL slice per workgroup, a
+// wave per row running the element-row sums above (the same additions in the same order: bit-identical), the R
+// rows' sums of a column window kept in LDS together ([R][Wc * 9 + 1], Wc = min(widest slice, 64) columns: dynamic
+// LDS sized to the pattern), then written straight into the SELL planes -- per (entry, block value) R contiguous
+// doubles (R = 16: one whole 128-byte line) -- padding entries and lanes past the last row zeroed in store mode.
+// No block-CSR buffer, no k_csr_add_sell pass (c3d10: 1.85 GB written once instead of written, read and written).
+// Tiles of a slice run on one XCD, so its lines are completed in one L2.
+template <int NPE, int R, bool STORE, bool LA = false>
+__global__ void __launch_bounds__(R * 64) k_assemble_ke_tile3(const double* __restrict__ Ke,
+                                                               const int64_t* __restrict__ conn,
+                                                               const int32_t* __restrict__ inc_ptr,
+                                                               const int32_t* __restrict__ inc, int64_t N,
+                                                               const int32_t* __restrict__ rowptr,
+                                                               const int32_t* __restrict__ colidx,
+                                                               const int64_t* __restrict__ slice_ptr,
+                                                               double* __restrict__ vals, int Wc, int64_t ntiles) {
+    constexpr int B2 = 9;
+    extern __shared__ double tacc[];          // [R][Wc * 9 + 1]
+    __shared__ int cols_s[R][KR_LMAX];
+    __shared__ int slot_s[R][64];
+    __shared__ int64_t koff_s[R][64];
+    __shared__ int eid_s[R][64];
+    __shared__ int len_s[R];
+    // slice s on XCD s % 8 (its R-row tiles consecutive there: a slice's plane lines complete in one L2), slices
+    // interleaved over the XCDs (heavy rows numbered together, e.g. c3d10 corner nodes, spread over all of them)
+    constexpr int T = 64 / R;
+    const int64_t kx = blockIdx.x / NXCD;
+    const int64_t tile = ((kx / T) * NXCD + blockIdx.x % NXCD) * T + kx % T;
+    if (tile >= ntiles) return;
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t r0 = tile * R, i = r0 + wid;
+    const int64_t p0 = slice_ptr[r0 >> 6];
+    const int W = (int)((slice_ptr[(r0 >> 6) + 1] - p0) >> 6);
+    const int l0 = (int)(r0 & 63);
+    const int rs = Wc * B2 + 1;              // row stride (odd: the write-out's R rows fall into different banks)
+    const KeRowLane<NPE> L(lane);
+    int lo = 0, len = 0, t0 = 0, C = 0;
+    if (i < N) {
+        lo = rowptr[i];
+        len = rowptr[i + 1] - lo;
+        t0 = inc_ptr[i];
+        C = inc_ptr[i + 1] - t0;
+    }
+    if (lane == 0) len_s[wid] = len;
+    double* acc = tacc + wid * rs;
+    for (int j0 = 0; j0 < W; j0 += Wc) {
+        const int nw = min(Wc, W - j0);              // entries of this window (slice-wide)
+        const int nj = max(0, min(Wc, len - j0));    // of them real columns of this row
+        __syncthreads();                             // the previous window written out
+        if (lane < nj) cols_s[wid][lane] = colidx[lo + j0 + lane];
+        for (int t = lane; t < nw * B2; t += 64) acc[t] = 0.0;
+        if (nj > 0) ke_row3<NPE>(L, Ke, conn, inc, t0, C, cols_s[wid], nj, acc, slot_s[wid], koff_s[wid], eid_s[wid],
+                                 lane);
+        __syncthreads();
+        double* dst = vals + B2 * p0 + (int64_t)64 * B2 * j0 + l0;
+        for (int q = threadIdx.x; q < nw * B2 * R; q += R * 64) {
+            const int r = q % R, pl = q / R, k = pl / B2, rc = pl - B2 * (pl / B2);
+            const double v = tacc[r * rs + k * B2 + rc];
+            // LA: the plane-paired layout A (the solver layout of bs = 3), else the plain planes
+            double* d = LA ? vals + sell_val_a(p0 + (int64_t)64 * (j0 + k) + l0 + r, rc)
+                           : dst + (int64_t)64 * (k * B2 + rc) + r;
+            if constexpr (STORE) *d = v;                          // padding / missing rows: zero sums
+            else if (j0 + k < len_s[r]) *d += v;                  // adding: padding stays as stored
         }
     }
 }
@@ -794,7 +883,11 @@ using AccP1w16 = AccCfg<FEM_P1W16_CFG>;
 #endif
 using AccEl = AccCfg<FEM_EL3_CFG>;
 
-template <int BS, class Cfg, bool STORE>
+// SL: the values go into the solver layout -- bs = 1 (whole-slice tiles): lane-paired entries of the pattern's
+// k_sell_sl_pattern, and in a slice-uniform slice (uoff[s] >= 0) the accumulators are indexed by the slice's delta
+// list (the column search looks up node - row in it), so a row's missing offsets hold zeros there; bs = 3: the
+// plane-paired layout A (sell_val_a). The same additions in the same order as the plain layout: only positions differ.
+template <int BS, class Cfg, bool STORE, bool SL = false>
 __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__ X, const int64_t* __restrict__ conn,
                                                       double E, double nu, const int32_t* __restrict__ inc_ptr,
                                                       const int32_t* __restrict__ inc, int64_t N,
@@ -802,7 +895,9 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                                                       const int32_t* __restrict__ colidx,
                                                       const int64_t* __restrict__ slice_ptr,
                                                       double* __restrict__ vals, int64_t* __restrict__ bad,
-                                                      int64_t ntiles) {
+                                                      int64_t ntiles, const int32_t* __restrict__ uoff = nullptr,
+                                                      const int16_t* __restrict__ ucol = nullptr) {
+    static_assert(!SL || BS == 3 || Cfg::R == 64, "solver layout, bs = 1: one slice per tile");
     constexpr int R = Cfg::R, J = Cfg::J, LPR = Cfg::LPR, AW = Cfg::W, SEG = Cfg::SEG;
     constexpr int B2 = BS * BS;
     constexpr int NI = R * J;
@@ -847,8 +942,12 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
     }
     __syncthreads();
     const int seg0 = rp_s[0], segn = rp_s[R] - seg0;
-    const bool staged = segn <= SEG;
-    if (staged)
+    // SL: a slice-uniform slice searches its delta list (W entries) instead of the rows' CSR columns
+    const int uo = (SL && BS == 1) ? uoff[r0 >> 6] : -1;   // bs = 3: layout A, per-lane columns
+    const bool staged = SL && uo >= 0 ? true : segn <= SEG;
+    if (SL && uo >= 0)
+        for (int q = tid; q < W; q += NT) col_s[q] = ucol[uo + q];
+    else if (staged)
         for (int q = tid; q < segn; q += NT) {
             const int cq = colidx[seg0 + q];
             col_s[q] = cq;
@@ -869,8 +968,8 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
         for (int q = tid; q < AW * AV * R; q += NT) {
             const int r = q % R, kc = q / R, k = kc / AV;
             double v = 0.0;   // bs = 3: the sums start from zero, stored values are added when the row is written
-            if (BS == 1 && !STORE && k < cw && c0 + k < rp_s[r + 1] - rp_s[r])
-                v = vals[e0 + (int64_t)(c0 + k) * 64 + l0 + r];
+            if (BS == 1 && !STORE && k < cw && ((SL && uo >= 0) || c0 + k < rp_s[r + 1] - rp_s[r]))
+                v = vals[SL ? e0 + pair_pos(c0 + k, W, l0 + r) : e0 + (int64_t)(c0 + k) * 64 + l0 + r];
             acc_s[kc][r] = v;
         }
         // software pipeline over the batches: a thread's next incidence entry is loaded before the current batch
@@ -923,14 +1022,16 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                     const int64_t e = ea >> 2;
                     const int a = ea & 3;
                     const int64_t* c = cncur;
-                    const int cl = rp_s[r] - seg0, cn = rp_s[r + 1] - rp_s[r];
+                    const bool ulist = SL && uo >= 0;
+                    const int cl = ulist ? 0 : rp_s[r] - seg0, cn = ulist ? W : rp_s[r + 1] - rp_s[r];
+                    const int kshift = ulist ? (int)(r0 + r) : 0;   // list entries are deltas node - row
                     int nodes[4];
                     uint32_t pp[4];
                     pk[0] = pk[1] = 0u;
 #pragma unroll
                     for (int bb = 0; bb < 4; ++bb) {
-                        const int j = (int)c[bb];
-                        nodes[bb] = j;
+                        nodes[bb] = (int)c[bb];
+                        const int j = nodes[bb] - kshift;
                         // the tile-uniform branch keeps the LDS search on ds_read (one pointer for both would
                         // make every probe a flat load)
                         pp[bb] = staged ? sorted_pos(col_s + cl, cn, j) : sorted_pos(colidx + seg0 + cl, cn, j);
@@ -1067,15 +1168,15 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
         __syncthreads();
         for (int q = tid; q < cw * B2 * R; q += NT) {
             const int r = q % R, kc = q / R, k = kc / B2, c = kc - k * B2;
-            if (!STORE && c0 + k >= rp_s[r + 1] - rp_s[r]) continue;   // adding: padding stays as stored
+            if (!STORE && !(SL && uo >= 0) && c0 + k >= rp_s[r + 1] - rp_s[r]) continue;   // adding: padding stays
             const int64_t Ei = e0 + (int64_t)(c0 + k) * 64 + l0 + r;
             if constexpr (BS == 1) {
-                vals[Ei] = acc_s[kc][r];
+                vals[SL ? e0 + pair_pos(c0 + k, W, l0 + r) : Ei] = acc_s[kc][r];
             } else {
                 const int rr = c / 3, cc = c - 3 * (c / 3);
                 double kv = el_combine(L, acc_s[k * AV + c][r], acc_s[k * AV + cc * 3 + rr][r], acc_s[k * AV + 9][r],
                                        rr == cc);
-                double* dst = &vals[sell_val(Ei, B2, c)];
+                double* dst = &vals[SL ? sell_val_a(Ei, c) : sell_val(Ei, B2, c)];
                 if constexpr (!STORE) kv = add_nc(*dst, kv);
                 *dst = kv;
             }
@@ -1293,6 +1394,45 @@ __global__ void k_jacobi(const double* __restrict__ vals, int bs, const int32_t*
     }
 }
 
+// Jacobi weights of a bs = 1 matrix in the solver layout (k_sell_sl_pattern): the diagonal at the paired position of
+// the row's diagonal entry -- the list position of delta 0 in a slice-uniform slice, its CSR index otherwise
+template <int BS>
+__global__ void k_jacobi_sl(const double* __restrict__ svals, const int32_t* __restrict__ rowptr,
+                            const int32_t* __restrict__ diagpos, const int64_t* __restrict__ slice_ptr,
+                            const int32_t* __restrict__ uoff, const int16_t* __restrict__ ucol, int64_t nrows,
+                            const uint8_t* __restrict__ mask, double* __restrict__ w) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nrows * BS; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = t / BS;
+        const int r = (int)(t - i * BS);
+        const int64_t s = i >> 6;
+        const int l = (int)(i & 63);
+        const int64_t p0 = slice_ptr[s];
+        const int wd = (int)((slice_ptr[s + 1] - p0) >> 6);
+        const int32_t dp = diagpos[i];
+        const int uo = BS == 1 ? uoff[s] : -1;
+        int k = -1;
+        if (dp >= 0) {
+            if (uo >= 0) {
+                for (int u = 0; u < wd; ++u)
+                    if (ucol[uo + u] == 0) {
+                        k = u;
+                        break;
+                    }
+            } else {
+                k = dp - rowptr[i];
+            }
+        }
+        const double dg = k < 0 ? 0.0
+                          : BS == 1 ? svals[p0 + pair_pos(k, wd, l)]
+                                    : svals[sell_val_a(p0 + 64 * (int64_t)k + l, r * 3 + r)];
+        const int64_t i_ = t;   // the dof
+        double v = 1.0 / dg;
+        if (v == INFINITY) v = 0.0;  // `solver/solver.py:831` (only +inf)
+        if (mask && mask[i_]) v = 0.0;
+        w[i_] = v;
+    }
+}
+
 __global__ void k_sell_diag(const double* __restrict__ vals, int bs, const int32_t* __restrict__ diagpos,
                             const int64_t* __restrict__ csr2sell, int64_t nrows, double* __restrict__ out) {
     const int64_t n = nrows * bs;
@@ -1476,10 +1616,59 @@ int fem_assemble_from_ke(const double* Ke, const int64_t* conn, int npe, int bs,
                                    vals, stream);
 }
 
+// tile form of the bs = 3 stored-K_e assembly (k_assemble_ke_tile3): R = 16 rows per tile while the LDS allows
+// (whole 128-byte plane lines), else 8; false when the pattern's width is unknown or the form is switched off
+static int ke_tile_launch(const double* Ke, const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc,
+                          int64_t N, const int32_t* rowptr, const int32_t* colidx, const int64_t* slice_ptr, int store,
+                          int max_width, double* vals, hipStream_t st, bool* done, bool la = false) {
+    *done = false;
+    if (max_width <= 0) return FEM_OK;
+    if (!la && (getenv("FEM355_KE_ROWS") != nullptr || getenv("FEM355_KE_COLS") != nullptr)) return FEM_OK;
+    const int Wc = max_width < KR_LMAX ? max_width : KR_LMAX;
+    const int R = (16 * (Wc * 9 + 1) * 8 + 16 * 1280 <= 65536) ? 16 : 8;
+    const size_t dyn = sizeof(double) * (size_t)R * (Wc * 9 + 1);
+    const int64_t ntiles = cdiv(N, 64) * (64 / R);   // whole slices: lanes past the last row are zeroed too
+    const dim3 g((unsigned)(cdiv(cdiv(N, 64), NXCD) * NXCD * (64 / R)));
+#define FEM_KT(P, RR, ST, LA_)                                                                                     \
+    if (npe == P && R == RR && (store != 0) == ST && la == LA_)                                                    \
+        hipLaunchKernelGGL((k_assemble_ke_tile3<P, RR, ST, LA_>), g, dim3(RR * 64), dyn, st, Ke, conn, inc_ptr, inc,\
+                           N, rowptr, colidx, slice_ptr, vals, Wc, ntiles);
+#define FEM_KT_ALL(P) FEM_KT(P, 16, true, false) FEM_KT(P, 16, false, false) FEM_KT(P, 8, true, false)             \
+    FEM_KT(P, 8, false, false) FEM_KT(P, 16, true, true) FEM_KT(P, 16, false, true) FEM_KT(P, 8, true, true)          \
+    FEM_KT(P, 8, false, true)
+    FEM_KT_ALL(4) FEM_KT_ALL(6) FEM_KT_ALL(8) FEM_KT_ALL(10)
+#undef FEM_KT_ALL
+#undef FEM_KT
+    FEM_LAUNCHED();
+    *done = true;
+    return FEM_OK;
+}
+
+static int assemble_from_ke(const double* Ke, const int64_t* conn, int npe, int bs, const int32_t* inc_ptr,
+                            const int32_t* inc, int64_t N, const int32_t* rowptr, const int32_t* colidx,
+                            const int64_t* csr2sell, const int64_t* slice_ptr, int64_t nnz, int64_t ent, int store,
+                            int max_width, double* vals, fem_stream_t stream);
+
 int fem_assemble_from_ke_ex(const double* Ke, const int64_t* conn, int npe, int bs, const int32_t* inc_ptr,
                             const int32_t* inc, int64_t N, const int32_t* rowptr, const int32_t* colidx,
                             const int64_t* csr2sell, const int64_t* slice_ptr, int64_t nnz, int64_t ent, int store,
                             double* vals, fem_stream_t stream) {
+    return assemble_from_ke(Ke, conn, npe, bs, inc_ptr, inc, N, rowptr, colidx, csr2sell, slice_ptr, nnz, ent, store,
+                            0, vals, stream);
+}
+
+int fem_assemble_from_ke_ex2(const double* Ke, const int64_t* conn, int npe, int bs, const int32_t* inc_ptr,
+                             const int32_t* inc, int64_t N, const int32_t* rowptr, const int32_t* colidx,
+                             const int64_t* csr2sell, const int64_t* slice_ptr, int64_t nnz, int64_t ent, int store,
+                             int max_width, double* vals, fem_stream_t stream) {
+    return assemble_from_ke(Ke, conn, npe, bs, inc_ptr, inc, N, rowptr, colidx, csr2sell, slice_ptr, nnz, ent, store,
+                            max_width, vals, stream);
+}
+
+static int assemble_from_ke(const double* Ke, const int64_t* conn, int npe, int bs, const int32_t* inc_ptr,
+                            const int32_t* inc, int64_t N, const int32_t* rowptr, const int32_t* colidx,
+                            const int64_t* csr2sell, const int64_t* slice_ptr, int64_t nnz, int64_t ent, int store,
+                            int max_width, double* vals, fem_stream_t stream) {
     if (store && ent < 0) {
         set_error("fem_assemble_from_ke_ex: store mode needs the SELL entry count");
         return FEM_EARG;
@@ -1494,6 +1683,10 @@ int fem_assemble_from_ke_ex(const double* Ke, const int64_t* conn, int npe, int 
         // the SELL planes (the in-place variant's scattered 8-byte plane updates measured 4.6x their bytes in
         // WRITE_SIZE on c3d10); FEM355_KE_DIRECT=1 keeps the in-place kernel
         if (csrw) {
+            bool tiled = false;
+            const int trc = ke_tile_launch(Ke, conn, npe, inc_ptr, inc, N, rowptr, colidx, slice_ptr, store, max_width,
+                                           vals, S(stream), &tiled);
+            if (trc != FEM_OK || tiled) return trc;
             if (nnz < 0) {   // not given: one device-to-host read of rowptr[N]
                 nnz = 0;
                 FEM_HIP(hipMemcpyAsync(&nnz, rowptr + N, sizeof(int32_t), hipMemcpyDeviceToHost, S(stream)));
@@ -1617,6 +1810,60 @@ int fem_assemble_tet4_ex2(const double* coords, const int64_t* conn, double E, d
     return FEM_OK;
 }
 
+int fem_assemble_tet4_sl(const double* coords, const int64_t* conn, double E, double nu, int bs,
+                         const int32_t* inc_ptr, const int32_t* inc, int64_t N, const int32_t* rowptr,
+                         const int32_t* colidx, const int64_t* slice_ptr, const int32_t* uoff, const int16_t* ucol,
+                         int store, int max_width, double* svals, int64_t* bad_idx, fem_stream_t stream) {
+    if (N <= 0) return FEM_OK;
+    if (bs == 1 && (!uoff || !ucol)) {
+        set_error("fem_assemble_tet4_sl: the solver-layout pattern (fem_sell_sl_pattern) is required");
+        return FEM_EARG;
+    }
+    if (bs != 1 && bs != 3) {
+        set_error("fem_assemble_tet4_sl: block size %d unsupported", bs);
+        return FEM_EARG;
+    }
+    hipStream_t st = S(stream);
+#define AS_LAUNCH(BS_, CFG_, ST_)                                                                                   \
+    do {                                                                                                            \
+        const int64_t nt = cdiv(N, 64) * (64 / CFG_::R);                                                            \
+        hipLaunchKernelGGL((k_asm_tet4_acc<BS_, CFG_, ST_, true>), dim3((unsigned)(cdiv(nt, NXCD) * NXCD)),         \
+                           dim3(CFG_::R * CFG_::LPR), 0, st, coords, conn, E, nu, inc_ptr, inc, N, rowptr, colidx,   \
+                           slice_ptr, svals, bad_idx, nt, uoff, ucol);                                               \
+    } while (0)
+    if (bs == 3) {
+        if (store) AS_LAUNCH(3, AccEl, true);
+        else AS_LAUNCH(3, AccEl, false);
+    } else if (max_width > 0 && max_width <= AccP1w16::W) {
+        if (store) AS_LAUNCH(1, AccP1w16, true);
+        else AS_LAUNCH(1, AccP1w16, false);
+    } else {
+        if (store) AS_LAUNCH(1, AccP1, true);
+        else AS_LAUNCH(1, AccP1, false);
+    }
+#undef AS_LAUNCH
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_assemble_from_ke_sl(const double* Ke, const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc,
+                            int64_t N, const int32_t* rowptr, const int32_t* colidx, const int64_t* slice_ptr,
+                            int store, int max_width, double* svals, fem_stream_t stream) {
+    if (N <= 0) return FEM_OK;
+    if (!(npe == 4 || npe == 6 || npe == 8 || npe == 10) || max_width <= 0) {
+        set_error("fem_assemble_from_ke_sl: npe 4/6/8/10 and the pattern width required");
+        return FEM_EARG;
+    }
+    bool done = false;
+    const int rc = ke_tile_launch(Ke, conn, npe, inc_ptr, inc, N, rowptr, colidx, slice_ptr, store, max_width, svals,
+                                  S(stream), &done, true);
+    if (rc == FEM_OK && !done) {
+        set_error("fem_assemble_from_ke_sl: tile form not launched");
+        return FEM_EARG;
+    }
+    return rc;
+}
+
 int fem_assemble_tet4_ex(const double* coords, const int64_t* conn, double E, double nu, int bs,
                          const int32_t* inc_ptr, const int32_t* inc, int64_t N, const int32_t* rowptr,
                          const int32_t* colidx, const int64_t* csr2sell, const int64_t* slice_ptr, int store,
@@ -1648,6 +1895,20 @@ int fem_jacobi(const double* vals, int bs, const int32_t* rowptr, const int32_t*
                const int64_t* slice_ptr, int64_t nrows, const uint8_t* mask, double* w, fem_stream_t stream) {
     hipLaunchKernelGGL(k_jacobi, dim3(stream_grid(nrows * bs, 256)), dim3(256), 0, S(stream), vals, bs, rowptr,
                        diagpos, csr2sell, slice_ptr, nrows, mask, w);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_jacobi_sl(const double* svals, int bs, const int32_t* rowptr, const int32_t* diagpos,
+                  const int64_t* slice_ptr, const int32_t* uoff, const int16_t* ucol, int64_t nrows,
+                  const uint8_t* mask, double* w, fem_stream_t stream) {
+    if (nrows <= 0) return FEM_OK;
+    if (bs == 1)
+        hipLaunchKernelGGL(k_jacobi_sl<1>, dim3(stream_grid(nrows, 256)), dim3(256), 0, S(stream), svals, rowptr,
+                           diagpos, slice_ptr, uoff, ucol, nrows, mask, w);
+    else
+        hipLaunchKernelGGL(k_jacobi_sl<3>, dim3(stream_grid(nrows * 3, 256)), dim3(256), 0, S(stream), svals, rowptr,
+                           diagpos, slice_ptr, uoff, ucol, nrows, mask, w);
     FEM_LAUNCHED();
     return FEM_OK;
 }

@@ -153,4 +153,17 @@ __device__ __forceinline__ bool reduce_grid(double partial, double* partials, un
     return true;
 }
 
+// value rc of entry E (= slice base + 64 k + lane) of a bs = 3 matrix in the plane-paired layout A (sell_pair3.hpp):
+// the entry's 576-double chunk holds values (2t, 2t + 1) of lane l at 128 t + 2 l, value 8 at 512 + l
+__device__ __forceinline__ int64_t sell_val_a(int64_t E, int rc) {
+    const int64_t lane = E & 63;
+    return (E - lane) * 9 + (rc < 8 ? 128 * (rc >> 1) + 2 * lane + (rc & 1) : 512 + lane);
+}
+
+// entry k of a SELL-64 slice of width w in the lane-paired layout (sell_pair.hpp), offset from the slice base, lane l
+__device__ __forceinline__ int64_t pair_pos(int k, int w, int l) {
+    const int np = w >> 1;
+    return k < 2 * np ? (int64_t)(k >> 1) * 128 + 2 * l + (k & 1) : (int64_t)np * 128 + l;
+}
+
 }  // namespace fem

@@ -175,6 +175,38 @@ __global__ void __launch_bounds__(256) k_spmv(int64_t nslices, int64_t nrows, co
     }
 }
 
+// y = A x on the lane-paired layout (bs = 1; slice-uniform deltas where uoff says so): the solver layout's SpMV
+template <int U>
+__global__ void __launch_bounds__(256) k_spmv_pair(int64_t nslices, int64_t nrows, const int64_t* __restrict__ slice_ptr,
+                                                   const int16_t* __restrict__ pcols, const double* __restrict__ pvals,
+                                                   const int32_t* __restrict__ uoff, const int16_t* __restrict__ ucol,
+                                                   const double* __restrict__ x, double* __restrict__ y) {
+    const int lane = threadIdx.x & 63;
+    SliceWalk wk = slice_walk(nslices);
+    for (int64_t s = wk.s; s < wk.end; s += wk.step) {
+        const double v = sell_row_pair<U>(s, lane, slice_ptr, pcols, pvals, x, 0, 0, uoff, ucol);
+        const int64_t row = s * 64 + lane;
+        if (row < nrows) y[row] = v;
+    }
+}
+
+// y = A x on the plane-paired layout A (bs = 3, plain 16-bit columns): the bs = 3 solver layout's SpMV
+__global__ void __launch_bounds__(256) k_spmv_a(int64_t nslices, int64_t nrows, const int64_t* __restrict__ slice_ptr,
+                                                const int16_t* __restrict__ cols, const double* __restrict__ pvals,
+                                                const double* __restrict__ x, double* __restrict__ y) {
+    const int lane = threadIdx.x & 63;
+    SliceWalk wk = slice_walk(nslices);
+    for (int64_t s = wk.s; s < wk.end; s += wk.step) {
+        double o[3];
+        sell_row_paired<3>(s, lane, slice_ptr, cols, pvals, x, o);
+        const int64_t row = s * 64 + lane;
+        if (row < nrows) {
+#pragma unroll
+            for (int r = 0; r < 3; ++r) y[row * 3 + r] = o[r];
+        }
+    }
+}
+
 // ---------------------------------------------------------------- PCG device state
 struct PcgState {
     double rz;        // r.z of the current iterate (rs_old)
@@ -1613,6 +1645,9 @@ struct fem_pcg {
     int16_t* pcols16;
     int32_t* puoff;         // FEM_TUNE_PK_UNI (bs = 1): per-slice offset into pucol, -1 = per-lane deltas
     int16_t* pucol;
+    int pext;               // pvals / pcols16 / puoff / pucol belong to the caller (fem_pcg_set_layout): never freed
+    const int32_t* pwin_ext;   // the caller's gather windows for a pwin_G-workgroup grid (nullable)
+    int pwin_G;
     Constraints con;
     // owned device memory
     double* r;
@@ -2622,6 +2657,82 @@ int fem_pcg_get_schedule(fem_pcg* s) {
     return s->deferred ? 2 : 0;
 }
 
+__global__ void k_sell_sl_pattern(int64_t nslices, int64_t nrows, const int64_t* __restrict__ slice_ptr,
+                                  const int16_t* __restrict__ cin, int16_t* __restrict__ pout,
+                                  int16_t* __restrict__ ucol, int32_t* __restrict__ uoff, int G, int* __restrict__ win);
+
+int fem_sell_sl_pattern(int64_t nrows, const int64_t* slice_ptr, const int16_t* dcols, int G, int16_t* pcols,
+                        int16_t* ucol, int32_t* uoff, int32_t* win, fem_stream_t stream) {
+    const int64_t ns = cdiv(nrows, 64);
+    if (ns <= 0) return FEM_OK;
+    if (G > 0) {
+        hipLaunchKernelGGL(k_pk_window_init, dim3(cdiv(G, 256)), dim3(256), 0, S(stream), G, G, win);
+        FEM_LAUNCHED();
+    }
+    hipLaunchKernelGGL(k_sell_sl_pattern, dim3((unsigned)cdiv(ns, 4)), dim3(256), 0, S(stream), ns, nrows, slice_ptr,
+                       dcols, pcols, ucol, uoff, G > 0 ? G : 0, win);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_sell_sl_unpair(int64_t nrows, int bs, const int64_t* slice_ptr, const int16_t* dcols, const int32_t* uoff,
+                       const int16_t* ucol, const int32_t* rowptr, const double* svals, double* vals,
+                       fem_stream_t stream) {
+    const int64_t ns = cdiv(nrows, 64);
+    if (ns <= 0) return FEM_OK;
+    if (bs == 3) {
+        hipLaunchKernelGGL(k_sell3_from_a, dim3(stream_grid(ns * 64, 256)), dim3(256), 0, S(stream), ns, slice_ptr,
+                           svals, vals);
+        FEM_LAUNCHED();
+        return FEM_OK;
+    }
+    hipLaunchKernelGGL(k_sell_sl_unpair, dim3(stream_grid(ns * 64, 256)), dim3(256), 0, S(stream), ns, slice_ptr, dcols,
+                       uoff, ucol, rowptr, nrows, svals, vals);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_spmv_sl(int64_t nrows, int bs, const int64_t* slice_ptr, const int16_t* pcols, const double* svals,
+                const int32_t* uoff, const int16_t* ucol, const double* x, double* y, fem_stream_t stream) {
+    const int64_t ns = cdiv(nrows, 64);
+    if (ns <= 0) return FEM_OK;
+    // slice_walk needs a multiple of 8 workgroups (one XCD range each)
+    if (bs == 3) {   // pcols: the plain 16-bit deltas (layout A pairs values only)
+        hipLaunchKernelGGL(k_spmv_a, dim3(grid_multiple_of_xcd(cdiv(ns, 4), 2048)), dim3(256), 0, S(stream), ns, nrows,
+                           slice_ptr, pcols, svals, x, y);
+        FEM_LAUNCHED();
+        return FEM_OK;
+    }
+    hipLaunchKernelGGL(k_spmv_pair<SPMV_UP>, dim3(grid_multiple_of_xcd(cdiv(ns, 4), 2048)), dim3(256), 0, S(stream), ns, nrows,
+                       slice_ptr, pcols, svals, uoff, ucol, x, y);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_pcg_set_layout(fem_pcg* s, const double* svals, const int16_t* pcols, const int32_t* uoff,
+                       const int16_t* ucol, const int32_t* win, int G) {
+    if ((s->bs != 1 && s->bs != 3) || !s->cols16 || s->dist || s->pd || (s->bs == 1 && !pcols)) {
+        set_error("fem_pcg_set_layout: single-GPU contexts with 16-bit columns only (fem_pcg_set_cols16 first); "
+                  "bs = 1 needs the paired columns");
+        return FEM_EARG;
+    }
+    if (!s->pext) {   // buffers of an earlier refresh go back to the pool
+        pool_free(s->pvals, s->stream);
+        pool_free(s->pcols16, s->stream);
+        pool_free(s->puoff, s->stream);
+        pool_free(s->pucol, s->stream);
+    }
+    s->pext = 1;
+    s->pvals = const_cast<double*>(svals);
+    s->pcols16 = s->bs == 1 ? const_cast<int16_t*>(pcols) : nullptr;   // bs = 3: layout A reads cols16
+    s->puoff = s->bs == 1 ? const_cast<int32_t*>(uoff) : nullptr;
+    s->pucol = s->bs == 1 ? const_cast<int16_t*>(ucol) : nullptr;
+    s->pwin_ext = win;
+    s->pwin_G = win ? G : 0;
+    s->pk_win_ok = 0;
+    return FEM_OK;
+}
+
 int fem_pcg_uniform_slices(fem_pcg* s, int64_t s_begin, int64_t s_end, int64_t* uniform, int64_t* nslices,
                            int64_t* index_bytes) {
     if (s_end < 0 || s_end > s->nslices) s_end = s->nslices;
@@ -2750,6 +2861,10 @@ static int persist_setup(fem_pcg* s) {
         FEM_HIP(pool_alloc((void**)&s->pk_sync, sizeof(unsigned) * pk_sync_words(G), s->stream, s->bs == 1));
         s->pk_grid = G;
         s->pk_win_ok = 0;
+    }
+    if (!s->pk_win_ok && s->pwin_ext && s->pwin_G == G) {   // formed with the solver-layout pattern
+        FEM_HIP(hipMemcpyAsync(s->pk_win, s->pwin_ext, sizeof(int32_t) * 2 * G, hipMemcpyDeviceToDevice, s->stream));
+        s->pk_win_ok = 1;
     }
     if (!s->pk_win_ok) {   // [lo | hi] per logical workgroup, from the matrix columns (no host round trip)
         hipLaunchKernelGGL(k_pk_window_init, dim3(cdiv(G, 256)), dim3(256), 0, s->stream, G, G, s->pk_win);
@@ -2934,6 +3049,93 @@ int fem_pcg_persist_build(fem_pcg* s, int* slots, int* overflow, int* pack) {
     return FEM_OK;
 }
 
+// The solver layout of a bs = 1 pattern (FEM_TUNE_PK_UNI + lane pairing decided from the pattern alone, once per
+// pattern): the qualification of k_sell_uniform on the plain 16-bit deltas (padding entries are delta 0 by
+// construction and get value 0 from the assembly), uoff / ucol of the uniform slices, and the lane-paired per-lane
+// deltas pout (a uniform slice's list deltas at every lane, like k_sell_uniform's copy). The value kernels then write
+// the paired layout directly (fem_assemble_tet4_sl), so a solve needs no conversion pass.
+// With G > 0 the same pass also forms the persistent schedule's gather windows for a G-workgroup grid (k_pk_window's
+// work: the union of the slice's deltas, one atomic pair per slice), so the solve's start needs neither pass.
+__global__ void __launch_bounds__(256) k_sell_sl_pattern(int64_t nslices, int64_t nrows,
+                                                         const int64_t* __restrict__ slice_ptr,
+                                                         const int16_t* __restrict__ cin, int16_t* __restrict__ pout,
+                                                         int16_t* __restrict__ ucol, int32_t* __restrict__ uoff, int G,
+                                                         int* __restrict__ win) {
+    __shared__ int cand_all[4][SU_MAXW];
+    const int64_t s = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;   // one wave per slice
+    const int l = threadIdx.x & 63;
+    int* cand = cand_all[(threadIdx.x >> 6) & 3];
+    if (s >= nslices) return;   // wave-uniform
+    const int64_t p0 = slice_ptr[s];
+    const int w = (int)((slice_ptr[s + 1] - p0) >> 6);
+    const int64_t row = s * 64 + l;
+    if (G > 0) {   // gather window (k_pk_window): the delta union of the slice over its owner workgroup
+        int dmin = 0, dmax = 0;
+        if (row < nrows)
+            for (int k = 0; k < w; ++k) {
+                const int d = cin[p0 + 64 * k + l];
+                dmin = d < dmin ? d : dmin;
+                dmax = d > dmax ? d : dmax;
+            }
+        int64_t cmin, cmax;
+        pk_slice_span(s, nrows, dmin, dmax, &cmin, &cmax);
+        const int64_t WV = (int64_t)G * PK_WAVES;
+        auto owner = [&](int64_t r) { return (int)((((r >> 6) + 1) * WV - 1) / nslices / PK_WAVES); };
+        if (l == 0) {
+            const int me = owner(row);
+            atomicMin(win + me, owner(cmin));
+            atomicMax(win + G + me, owner(cmax));
+        }
+    }
+    bool ok = (s + 1) * 64 <= nrows && w > 0 && w <= SU_MAXW;
+    int len = 0;
+    if (ok) {
+        int prev = -(1 << 30);
+        for (int k = 0; k < w; ++k) {
+            const int d = cin[p0 + 64 * k + l];
+            if (len == k && d > prev) {
+                ++len;
+                prev = d;
+            } else if (d != 0) {
+                ok = false;
+            }
+        }
+    }
+    ok = __all(ok);
+    const unsigned long long full = __ballot(ok && len == w);
+    if (ok && full) {
+        const int c = __builtin_ctzll(full);
+        for (int k = 0; k < w; ++k) {
+            const int d = __shfl((int)cin[p0 + 64 * k + l], c, 64);
+            if (l == 0) cand[k] = d;
+            const int64_t col = row + d;
+            if (col < 0 || col >= nrows) ok = false;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        int i = 0;
+        for (int k = 0; k < len && ok; ++k) {
+            const int d = cin[p0 + 64 * k + l];
+            while (i < w && cand[i] < d) ++i;
+            if (i == w || cand[i] != d) ok = false;
+            ++i;
+        }
+    } else {
+        ok = false;
+    }
+    ok = __all(ok);
+    if (!ok) {
+        if (l == 0) uoff[s] = -1;
+        for (int k = 0; k < w; ++k) pout[p0 + pair_pos(k, w, l)] = cin[p0 + 64 * k + l];
+        return;
+    }
+    const int32_t uo = (int32_t)(2 * (p0 >> 6));   // even: the deltas are read as int32 pairs
+    for (int k = 0; k < w; ++k) pout[p0 + pair_pos(k, w, l)] = (int16_t)cand[k];
+    for (int k = l; k < w; k += 64) ucol[uo + k] = (int16_t)cand[k];
+    if (l == 0) uoff[s] = uo;
+}
+
 // host view of the state: the deferred schedule keeps it in the bank of the current launch parity
 static PcgState state_view(const fem_pcg* s) {
     PcgState h = *s->st_host;
@@ -2957,6 +3159,14 @@ static PcgState state_view(const fem_pcg* s) {
 static int refresh_pairing(fem_pcg* s) {
     const bool want = (s->bs == 1 || s->bs == 3) && s->cols16 && (s->tune & FEM_TUNE_PAIR) && !s->fused;
     s->paired = 0;
+    if (s->pext) {   // the matrix was assembled in the solver layout: nothing to convert
+        if (!want) {
+            set_error("PCG: a solver-layout matrix needs the paired schedules (FEM_TUNE_PAIR, 16-bit columns, not fused)");
+            return FEM_EARG;
+        }
+        s->paired = 1;
+        return FEM_OK;
+    }
     if (!want || s->nslices == 0) return FEM_OK;
     int64_t ent = s->sell_ent;
     if (ent < 0) {   // not given by the caller: one device-to-host read (a host sync)
@@ -3044,8 +3254,17 @@ int fem_pcg_start(fem_pcg* s) {
         s->launched = 0;
         return FEM_OK;   // every rank must finish its start before any rank launches (a host barrier)
     }
-    if ((rc = (s->cols16 ? fem_spmv16(s->nrows, s->bs, s->slice_ptr, s->cols16, s->vals, s->x, s->q, s->stream)
-                          : fem_spmv(s->nrows, s->bs, s->slice_ptr, s->cols, s->vals, s->x, s->q, s->stream)))) return rc;
+    if (s->pext) {   // solver layout: r0 = b - A x0 from the paired values
+        if (s->bs == 1)
+            hipLaunchKernelGGL(k_spmv_pair<SPMV_UP>, dim3(s->grid_spmv), dim3(256), 0, s->stream, s->nslices, s->nrows,
+                               s->slice_ptr, s->pcols16, s->pvals, s->puoff, s->pucol, s->x, s->q);
+        else
+            hipLaunchKernelGGL(k_spmv_a, dim3(s->grid_spmv), dim3(256), 0, s->stream, s->nslices, s->nrows,
+                               s->slice_ptr, s->cols16, s->pvals, s->x, s->q);
+        FEM_LAUNCHED();
+    } else if ((rc = (s->cols16 ? fem_spmv16(s->nrows, s->bs, s->slice_ptr, s->cols16, s->vals, s->x, s->q, s->stream)
+                                 : fem_spmv(s->nrows, s->bs, s->slice_ptr, s->cols, s->vals, s->x, s->q, s->stream))))
+        return rc;
     if (s->persist) {   // single-reduction start: r0 = b - A x0, u0 = w r0 (in q), p = s = 0, g0 -> red[1]
         const int zrc = persist_reset_sync(s);   // after the state upload: zeroes st->pk_epoch too
         if (zrc) return zrc;
@@ -3758,6 +3977,12 @@ void fem_pcg_destroy(fem_pcg* s) {
     if (s->c1f_win) (void)hipFree(s->c1f_win);
     if (s->c1f_flags) (void)hipFree(s->c1f_flags);
     if (s->con.tmp) (void)hipFree(s->con.tmp);
+    if (s->pext) {   // the caller's solver-layout arrays
+        s->pvals = nullptr;
+        s->pcols16 = nullptr;
+        s->puoff = nullptr;
+        s->pucol = nullptr;
+    }
     pool_free(s->pvals, s->stream);
     pool_free(s->pcols16, s->stream);
     pool_free(s->puoff, s->stream);

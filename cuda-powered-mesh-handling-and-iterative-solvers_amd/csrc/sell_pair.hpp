@@ -148,6 +148,42 @@ __attribute__((unused)) static __global__ void __launch_bounds__(256) k_sell_uni
     if (l == 0) uoff[s] = uo;
 }
 
+// plain SELL values of a solver-layout (paired, slice-uniform) bs = 1 matrix: lane l walks its row's plain deltas and
+// the slice's list (uniform) or maps plain entry k to its paired position (other slices); padding entries zero
+__attribute__((unused)) static __global__ void __launch_bounds__(256) k_sell_sl_unpair(int64_t nslices,
+                                                               const int64_t* __restrict__ slice_ptr,
+                                                               const int16_t* __restrict__ cin,
+                                                               const int32_t* __restrict__ uoff,
+                                                               const int16_t* __restrict__ ucol,
+                                                               const int32_t* __restrict__ rowptr, int64_t nrows,
+                                                               const double* __restrict__ vin,
+                                                               double* __restrict__ vout) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nslices * 64;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = t >> 6;
+        const int l = (int)(t & 63);
+        const int64_t p0 = slice_ptr[s];
+        const int w = (int)((slice_ptr[s + 1] - p0) >> 6);
+        const int64_t row = s * 64 + l;
+        const int len = row < nrows ? rowptr[row + 1] - rowptr[row] : 0;
+        const int uo = uoff[s];
+        int u = 0;
+        for (int k = 0; k < w; ++k) {
+            double v = 0.0;
+            if (k < len) {
+                int pos = k;
+                if (uo >= 0) {   // the list position of this entry's delta (rows' deltas are subsequences of it)
+                    const int d = cin[p0 + 64 * k + l];
+                    while (u < w && (int)ucol[uo + u] < d) ++u;
+                    pos = u++;
+                }
+                v = vin[p0 + pair_pos(pos, w, l)];
+            }
+            vout[p0 + 64 * k + l] = v;
+        }
+    }
+}
+
 // y_row (bs = 1) of one slice row in the paired layout; U pairs in flight. UNI: the slice's deltas from the
 // wave-uniform list ucl (k_sell_uniform), else per lane from cols.
 template <int U, int SC1, bool UNI>

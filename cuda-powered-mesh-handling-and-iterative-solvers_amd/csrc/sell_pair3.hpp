@@ -48,6 +48,23 @@ static __global__ void k_sell3_to_a(int64_t nslices, const int64_t* __restrict__
     }
 }
 
+// layout A -> plain (the solver layout's values back into the plain planes)
+[[maybe_unused]] static __global__ void k_sell3_from_a(int64_t nslices, const int64_t* __restrict__ slice_ptr,
+                                                       const double* __restrict__ vin, double* __restrict__ vout) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nslices * 64;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = t >> 6;
+        const int l = (int)(t & 63);
+        const int64_t p0 = slice_ptr[s];
+        const int w = (int)((slice_ptr[s + 1] - p0) >> 6);
+        for (int k = 0; k < w; ++k) {
+            const int64_t c = 9 * p0 + 576 * (int64_t)k;
+            for (int e = 0; e < 8; ++e) vout[c + 64 * e + l] = vin[c + 128 * (e >> 1) + 2 * l + (e & 1)];
+            vout[c + 512 + l] = vin[c + 512 + l];
+        }
+    }
+}
+
 [[maybe_unused]] static __global__ void k_sell3_to_b(int64_t nslices, const int64_t* __restrict__ slice_ptr,
                                     const double* __restrict__ vin, const int16_t* __restrict__ cin,
                                     double* __restrict__ vout, int16_t* __restrict__ cout) {

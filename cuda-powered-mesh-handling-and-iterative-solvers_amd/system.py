@@ -106,6 +106,30 @@ class Graph:
                 self.c2s = c2s
         return self.c2s
 
+    def solver_layout(self):
+        """The bs = 1 solver layout of this pattern (include/fem355.h fem_sell_sl_pattern): lane-paired deltas,
+        slice-uniform delta lists, and the persistent schedule's gather windows for this device's grid -- formed once
+        per pattern, on first use. None without 16-bit deltas."""
+        if self.dcols is None:
+            return None
+        sl = getattr(self, "_sl", None)
+        if sl is None:
+            dev = self.rowptr.device
+            with C.device_scope(dev):
+                ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+                G = (ncu // 8) * 8
+                ent = self.sell_entries
+                ns = (self.n_nodes + 63) // 64
+                sl = SolverLayout(torch.empty(max(ent, 1), dtype=torch.int16, device=dev),
+                                  torch.empty(2 * (ent // 64) + 2, dtype=torch.int16, device=dev),
+                                  torch.empty(max(ns, 1), dtype=I32, device=dev),
+                                  torch.empty(max(2 * G, 1), dtype=I32, device=dev), G)
+                C.check(C.lib().fem_sell_sl_pattern(self.n_nodes, C.ptr(self.slice_ptr), C.ptr(self.dcols), G,
+                                                    C.ptr(sl.pcols), C.ptr(sl.ucol), C.ptr(sl.uoff), C.ptr(sl.win),
+                                                    C.stream(dev)), "fem_sell_sl_pattern")
+            self._sl = sl
+        return sl
+
     @property
     def nnz(self):
         return int(self.colidx.numel())
@@ -113,6 +137,16 @@ class Graph:
     @property
     def sell_entries(self):
         return int(self.cols.numel())
+
+
+@dataclass
+class SolverLayout:
+    """Solver layout of a bs = 1 pattern (Graph.solver_layout): paired deltas, uniform lists, gather windows."""
+    pcols: torch.Tensor
+    ucol: torch.Tensor
+    uoff: torch.Tensor
+    win: torch.Tensor
+    G: int
 
 
 def check_connectivity(elements: torch.Tensor, n_nodes: int):
@@ -261,17 +295,57 @@ class SellMatrix:
         self.device = graph.cols.device
         # values are zeroed lazily: the first add_element_matrices of a fresh matrix STORES every value (padding
         # included) instead of adding onto a zeroed buffer -- one memset and one read of the matrix fewer
-        self._vals = torch.empty(max(graph.sell_entries, 1) * bs * bs, dtype=F64, device=self.device)
+        self._vals = None            # plain SELL values, allocated on first use
+        self._svals = None           # solver layout values (include/fem355.h fem_assemble_tet4_sl)
+        self._plain_ok = False       # which of the two holds the current values
+        self._sl_ok = False
         self._fresh = True
         self.use16 = graph.dcols is not None   # 16-bit column deltas in every SpMV of this matrix
+
+    def _plain_buf(self):
+        if self._vals is None:
+            self._vals = torch.empty(max(self.g.sell_entries, 1) * self.bs * self.bs, dtype=F64, device=self.device)
+        return self._vals
+
+    @property
+    def solver_layout(self):
+        """True while the values live in the solver layout (the default of a fresh matrix's assembly: the PCG reads
+        them as they are, no per-solve conversion, one resident copy); `vals` then forms the plain copy on demand."""
+        return self._sl_ok
 
     @property
     def vals(self):
         """SELL values [entries * bs * bs] (plane layout); zero until something was added."""
         if self._fresh:
-            self._vals.zero_()
+            self._plain_buf().zero_()
             self._fresh = False
+            self._plain_ok = True
+        elif not self._plain_ok and self._sl_ok:   # plain copy of a solver-layout matrix
+            sl = self.g.solver_layout()
+            C.check(C.lib().fem_sell_sl_unpair(self.g.n_nodes, self.bs, C.ptr(self.g.slice_ptr), C.ptr(self.g.dcols),
+                                               C.ptr(sl.uoff), C.ptr(sl.ucol), C.ptr(self.g.rowptr),
+                                               C.ptr(self._svals), C.ptr(self._plain_buf()), C.stream(self.device)),
+                    "fem_sell_sl_unpair")
+            self._plain_ok = True
         return self._vals
+
+    def _sl_target(self):
+        """True when the next assembly writes the solver layout: 16-bit deltas, a fresh matrix or one held only there
+        (FEM355_SL=0 keeps the plain layout)."""
+        return (self.use16 and self.bs in (1, 3) and os.environ.get("FEM355_SL", "1") != "0"
+                and (self._fresh or (self._sl_ok and not self._plain_ok)))
+
+    def _svals_buf(self):
+        if self._svals is None:
+            self._svals = torch.empty(max(self.g.sell_entries, 1) * self.bs * self.bs, dtype=F64, device=self.device)
+        return self._svals
+
+    def _modify_plain(self):
+        """The plain values about to change: current (or fresh), and the solver layout stale afterwards."""
+        if not self._fresh:
+            self.vals   # noqa: B018 -- forms the plain copy when only the solver layout holds the values
+        self._plain_buf()
+        self._sl_ok = False
 
     @property
     def n_rows(self):
@@ -293,21 +367,53 @@ class SellMatrix:
         inc_ptr, inc_ = inc if inc is not None else (
             (self.g.inc_ptr, self.g.inc) if npe == self.g.npe and elements.shape[0] * npe == self.g.inc.numel()
             else incidence(elements, self.g.n_nodes))
+        # bs = 3 with the pattern's widest slice known: the tile form writes the SELL planes directly (csr2sell unused)
+        tiled = self.bs == 3 and self.g.max_width > 0 and not os.environ.get("FEM355_KE_ROWS") \
+            and not os.environ.get("FEM355_KE_COLS") and not os.environ.get("FEM355_KE_DIRECT")
+        if tiled and npe in (4, 6, 8, 10) and self._sl_target():   # straight into the solver layout (layout A)
+            store = self._fresh
+            self._fresh = False
+            C.check(lib.fem_assemble_from_ke_sl(C.ptr(Ke), C.ptr(elements), npe, C.ptr(inc_ptr), C.ptr(inc_),
+                                                self.g.n_nodes, C.ptr(self.g.rowptr), C.ptr(self.g.colidx),
+                                                C.ptr(self.g.slice_ptr), 1 if store else 0, self.g.max_width,
+                                                C.ptr(self._svals_buf()), C.stream(self.device)),
+                    "fem_assemble_from_ke_sl")
+            self._sl_ok, self._plain_ok = True, False
+            return self
+        self._modify_plain()
         store = self._fresh
         self._fresh = False
-        C.check(lib.fem_assemble_from_ke_ex(C.ptr(Ke), C.ptr(elements), npe, self.bs, C.ptr(inc_ptr), C.ptr(inc_),
-                                            self.g.n_nodes, C.ptr(self.g.rowptr), C.ptr(self.g.colidx),
-                                            C.ptr(self.g.csr2sell), C.ptr(self.g.slice_ptr), self.g.nnz,
-                                            self.g.sell_entries, 1 if store else 0, C.ptr(self._vals),
-                                            C.stream(self.device)), "fem_assemble_from_ke_ex")
+        self._plain_ok = True
+        C.check(lib.fem_assemble_from_ke_ex2(C.ptr(Ke), C.ptr(elements), npe, self.bs, C.ptr(inc_ptr), C.ptr(inc_),
+                                             self.g.n_nodes, C.ptr(self.g.rowptr), C.ptr(self.g.colidx),
+                                             None if tiled else C.ptr(self.g.csr2sell), C.ptr(self.g.slice_ptr),
+                                             self.g.nnz, self.g.sell_entries, 1 if store else 0,
+                                             self.g.max_width if tiled else 0, C.ptr(self._vals),
+                                             C.stream(self.device)), "fem_assemble_from_ke_ex2")
         return self
 
     def add_tet4(self, coords: torch.Tensor, elements: torch.Tensor, E: float, nu: float = 0.0):
         """vals += the c3d4 operator computed on the fly (bs=3: elasticity E, nu; bs=1: Poisson, kappa=E)."""
         lib = C.lib()
         bad = _dev_scalar(self.device, I64, elements.shape[0])
+        self._bad = (bad, elements.shape[0])
+        # 16-bit deltas: straight into the solver layout (fresh matrix, or one already held there)
+        if self._sl_target() and not os.environ.get("FEM355_ASM_ROWS"):
+            sl = self.g.solver_layout() if self.bs == 1 else None
+            store = self._fresh
+            self._fresh = False
+            C.check(lib.fem_assemble_tet4_sl(C.ptr(coords), C.ptr(elements), float(E), float(nu), self.bs,
+                                             C.ptr(self.g.inc_ptr), C.ptr(self.g.inc), self.g.n_nodes,
+                                             C.ptr(self.g.rowptr), C.ptr(self.g.colidx), C.ptr(self.g.slice_ptr),
+                                             C.ptr(sl.uoff) if sl else None, C.ptr(sl.ucol) if sl else None,
+                                             1 if store else 0, self.g.max_width, C.ptr(self._svals_buf()), C.ptr(bad),
+                                             C.stream(self.device)), "fem_assemble_tet4_sl")
+            self._sl_ok, self._plain_ok = True, False
+            return self
+        self._modify_plain()
         store = self._fresh   # a fresh matrix is stored whole (padding zeroed): no memset, no read of the values
         self._fresh = False
+        self._plain_ok = True
         C.check(lib.fem_assemble_tet4_ex2(C.ptr(coords), C.ptr(elements), float(E), float(nu), self.bs,
                                           C.ptr(self.g.inc_ptr), C.ptr(self.g.inc), self.g.n_nodes,
                                           C.ptr(self.g.rowptr), C.ptr(self.g.colidx),
@@ -315,7 +421,6 @@ class SellMatrix:
                                           C.ptr(self.g.slice_ptr), 1 if store else 0, self.g.max_width,
                                           C.ptr(self._vals), C.ptr(bad), C.stream(self.device)),
                 "fem_assemble_tet4_ex2")
-        self._bad = (bad, elements.shape[0])
         return self
 
     def check_singular(self):
@@ -328,7 +433,15 @@ class SellMatrix:
         lib = C.lib()
         x = x.to(F64).contiguous()
         y = out if out is not None else torch.empty(self.n, dtype=F64, device=self.device)
-        if self.use16:
+        if self._sl_ok:
+            if self.bs == 1:
+                sl = self.g.solver_layout()
+                pc, uo, uc = C.ptr(sl.pcols), C.ptr(sl.uoff), C.ptr(sl.ucol)
+            else:   # layout A: plain deltas
+                pc, uo, uc = C.ptr(self.g.dcols), None, None
+            C.check(lib.fem_spmv_sl(self.g.n_nodes, self.bs, C.ptr(self.g.slice_ptr), pc, C.ptr(self._svals), uo, uc,
+                                    C.ptr(x), C.ptr(y), C.stream(self.device)), "fem_spmv_sl")
+        elif self.use16:
             C.check(lib.fem_spmv16(self.g.n_nodes, self.bs, C.ptr(self.g.slice_ptr), C.ptr(self.g.dcols),
                                    C.ptr(self.vals), C.ptr(x), C.ptr(y), C.stream(self.device)), "fem_spmv16")
         else:
@@ -341,10 +454,34 @@ class SellMatrix:
         if self.use16:
             C.check(C.lib().fem_pcg_set_cols16(h, C.ptr(self.g.dcols)), "fem_pcg_set_cols16")
 
+    def solver_vals_ptr(self, fused=False):
+        """The values pointer a (P)CG context is created with: the solver layout's when it holds the values (the
+        context then reads them through attach_layout), else the plain values."""
+        if self._sl_ok and not fused:
+            return C.ptr(self._svals)
+        return C.ptr(self.vals)
+
+    def attach_layout(self, h, fused=False):
+        """Hand a context the solver-layout values (+ the bs = 1 pattern, the gather windows) (fem_pcg_set_layout):
+        no conversion at start."""
+        if self._sl_ok and not fused:
+            sl = self.g.solver_layout()
+            one = self.bs == 1
+            C.check(C.lib().fem_pcg_set_layout(h, C.ptr(self._svals), C.ptr(sl.pcols) if one else None,
+                                               C.ptr(sl.uoff) if one else None, C.ptr(sl.ucol) if one else None,
+                                               C.ptr(sl.win), sl.G), "fem_pcg_set_layout")
+
     def jacobi(self, fixed_mask: torch.Tensor = None):
         """w = 1/diag(A) (inf -> 0), zero on fixed DOFs (uint8 mask [n])."""
         lib = C.lib()
         w = torch.empty(self.n, dtype=F64, device=self.device)
+        if self._sl_ok:
+            sl = self.g.solver_layout() if self.bs == 1 else None
+            C.check(lib.fem_jacobi_sl(C.ptr(self._svals), self.bs, C.ptr(self.g.rowptr), C.ptr(self.g.diagpos),
+                                      C.ptr(self.g.slice_ptr), C.ptr(sl.uoff) if sl else None,
+                                      C.ptr(sl.ucol) if sl else None, self.g.n_nodes,
+                                      C.ptr(fixed_mask), C.ptr(w), C.stream(self.device)), "fem_jacobi_sl")
+            return w
         C.check(lib.fem_jacobi(C.ptr(self.vals), self.bs, C.ptr(self.g.rowptr), C.ptr(self.g.diagpos),
                                None, C.ptr(self.g.slice_ptr), self.g.n_nodes,
                                C.ptr(fixed_mask), C.ptr(w), C.stream(self.device)), "fem_jacobi")
@@ -382,7 +519,11 @@ class SellMatrix:
         w = w.to(device=self.device, dtype=F64).contiguous().view(-1)
         hist = torch.full((max(max_iter, 1),), float("nan"), dtype=F64, device=self.device) if history else None
         h = ctypes.c_void_p()
-        args = (self.g.n_nodes, self.bs, C.ptr(self.g.slice_ptr), C.ptr(self.g.cols), C.ptr(self.vals), C.ptr(b),
+        sched = _schedule(fused, schedule, self.bs)
+        # the solver layout is read by the paired schedules (FEM_TUNE_PAIR = 2); fused / constrained contexts: plain
+        plain = sched == SCHED_FUSED or constraints is not None or (tune is not None and not (int(tune) & 2))
+        args = (self.g.n_nodes, self.bs, C.ptr(self.g.slice_ptr), C.ptr(self.g.cols), self.solver_vals_ptr(plain),
+                C.ptr(b),
                 C.ptr(x), C.ptr(w), mode, float(tol), float(eps), C.ptr(hist), hist.numel() if hist is not None else 0,
                 C.stream(self.device), ctypes.byref(h))
         rc = lib.fem_pcg_create(*args)
@@ -392,11 +533,12 @@ class SellMatrix:
             rc = lib.fem_pcg_create(*args)
         C.check(rc, "fem_pcg_create")
         try:
-            C.check(lib.fem_pcg_set_schedule(h, _schedule(fused, schedule, self.bs)), "fem_pcg_set_schedule")
+            C.check(lib.fem_pcg_set_schedule(h, sched), "fem_pcg_set_schedule")
             if tune is not None:
                 C.check(lib.fem_pcg_set_tuning(h, int(tune)), "fem_pcg_set_tuning")
             C.check(lib.fem_pcg_set_entries(h, self.g.sell_entries), "fem_pcg_set_entries")
             self.attach_cols16(h)
+            self.attach_layout(h, plain)
             if constraints is not None:
                 C.check(lib.fem_pcg_set_constraints(h, *constraints.args()), "fem_pcg_set_constraints")
             it, stt, rz = ctypes.c_int(), ctypes.c_int(), ctypes.c_double()
@@ -440,19 +582,32 @@ class PcgRunner:
         self.stream = torch.cuda.Stream(device=A.device)
         self.stream.wait_stream(torch.cuda.current_stream(A.device))
         self.h = ctypes.c_void_p()
-        C.check(self.lib.fem_pcg_create(A.g.n_nodes, A.bs, C.ptr(A.g.slice_ptr), C.ptr(A.g.cols), C.ptr(A.vals),
-                                        C.ptr(self.b), C.ptr(self.x), C.ptr(self.w), mode, float(tol), float(eps),
-                                        None, 0, ctypes.c_void_p(self.stream.cuda_stream), ctypes.byref(self.h)),
-                "fem_pcg_create")
         self.schedule = 0 if isinstance(self, _DistMarker) else _schedule(fused, schedule, A.bs)
+        self.constraints = constraints   # keeps the device arrays alive with the context
+        self._mode, self._tol, self._eps = mode, float(tol), float(eps)
+        # solver-layout values (bs = 1) unless the context must read the plain ones (distributed, fused, constrained)
+        self._create(isinstance(self, _DistMarker) or self.schedule == SCHED_FUSED or constraints is not None)
+
+    def _create(self, plain):
+        A = self.A
+        C.check(self.lib.fem_pcg_create(A.g.n_nodes, A.bs, C.ptr(A.g.slice_ptr), C.ptr(A.g.cols),
+                                        A.solver_vals_ptr(plain), C.ptr(self.b), C.ptr(self.x), C.ptr(self.w),
+                                        self._mode, self._tol, self._eps, None, 0,
+                                        ctypes.c_void_p(self.stream.cuda_stream), ctypes.byref(self.h)),
+                "fem_pcg_create")
         C.check(self.lib.fem_pcg_set_schedule(self.h, self.schedule), "fem_pcg_set_schedule")
         C.check(self.lib.fem_pcg_set_entries(self.h, A.g.sell_entries), "fem_pcg_set_entries")
         A.attach_cols16(self.h)
-        self.constraints = constraints   # keeps the device arrays alive with the context
-        if constraints is not None:
-            C.check(self.lib.fem_pcg_set_constraints(self.h, *constraints.args()), "fem_pcg_set_constraints")
+        A.attach_layout(self.h, plain)
+        self._sl = A.solver_layout and not plain
+        if self.constraints is not None:
+            C.check(self.lib.fem_pcg_set_constraints(self.h, *self.constraints.args()), "fem_pcg_set_constraints")
 
     def set_tuning(self, flags):
+        if self._sl and not (int(flags) & 2):   # no FEM_TUNE_PAIR: a context over the plain values instead
+            self.lib.fem_pcg_destroy(self.h)
+            self.h = ctypes.c_void_p()
+            self._create(True)
         C.check(self.lib.fem_pcg_set_tuning(self.h, int(flags)), "fem_pcg_set_tuning")
 
     def finish(self):

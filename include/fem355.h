@@ -192,6 +192,13 @@ int fem_assemble_from_ke_ex(const double* Ke, const int64_t* conn, int npe, int 
                             const int32_t* inc, int64_t N, const int32_t* rowptr, const int32_t* colidx,
                             const int64_t* csr2sell, const int64_t* slice_ptr, int64_t nnz, int64_t ent, int store,
                             double* vals, fem_stream_t stream);
+/* fem_assemble_from_ke_ex with the widest SELL slice in block columns (max_width > 0, from the pattern build): bs = 3
+ * then runs the tile form -- the rows of a slice summed together in LDS and written straight into the SELL planes
+ * (no block-CSR buffer, csr2sell unused and may be NULL). Same values bit for bit. max_width <= 0: as _ex. */
+int fem_assemble_from_ke_ex2(const double* Ke, const int64_t* conn, int npe, int bs, const int32_t* inc_ptr,
+                             const int32_t* inc, int64_t N, const int32_t* rowptr, const int32_t* colidx,
+                             const int64_t* csr2sell, const int64_t* slice_ptr, int64_t nnz, int64_t ent, int store,
+                             int max_width, double* vals, fem_stream_t stream);
 int fem_assemble_tet4(const double* coords, const int64_t* conn, double E, double nu, int bs,
                       const int32_t* inc_ptr, const int32_t* inc, int64_t N, const int32_t* rowptr,
                       const int32_t* colidx, const int64_t* csr2sell, const int64_t* slice_ptr, double* vals,
@@ -410,6 +417,46 @@ int fem_pcg_get_schedule(fem_pcg* s);
  * SpMV over those slices reads (padding included) */
 int fem_pcg_uniform_slices(fem_pcg* s, int64_t s_begin, int64_t s_end, int64_t* uniform, int64_t* nslices,
                            int64_t* index_bytes);
+/* ------------------------------------------------------------------ solver layout
+ * The matrix stored straight in the layout the PCG schedules read, so a solve converts nothing and the matrix is
+ * resident once. bs = 1: lane-paired SELL entries (entry k of lane l of a slice of width w at 128 (k / 2) + 2 l + k % 2,
+ * the odd tail at 128 (w / 2) + l), and in every slice whose rows take their columns at one sorted list of offsets
+ * (slice-uniform) those offsets stored once, the rows' missing offsets holding value 0. bs = 3: the plane-paired
+ * layout A (entry E = slice base + 64 k + lane: values (2t, 2t + 1) at 9 (E - lane) + 128 t + 2 lane, value 8 at
+ * 9 (E - lane) + 512 + lane), columns the plain 16-bit deltas.
+ *   fem_sell_sl_pattern : from the plain 16-bit deltas (fem_graph_sell_fill): pcols [entries] paired deltas, uoff
+ *                         [nslices] (-1: per-lane deltas), ucol [2 (entries / 64) + 2] lists; with G > 0 also the
+ *                         persistent schedule's gather windows win [2 G] for a G-workgroup grid (G = CUs rounded
+ *                         down to a multiple of 8). bs = 3 reads only the windows
+ *   fem_assemble_tet4_sl: the c3d4 values (bs = 1: Poisson, kappa = E; bs = 3: elasticity E, nu) into svals
+ *                         [entries bs^2] in that layout (store != 0: every value written; else added) --
+ *                         fem_assemble_tet4_ex2's sums, bit for bit, at other positions; uoff / ucol unused for bs = 3
+ *   fem_assemble_from_ke_sl: bs = 3 stored element matrices (npe 4 / 6 / 8 / 10, the pattern's widest slice
+ *                         max_width) into layout A -- fem_assemble_from_ke_ex2's sums, bit for bit
+ *   fem_jacobi_sl       : fem_jacobi of such a matrix;  fem_spmv_sl: y = A x (bs = 3: pcols = the plain deltas);
+ *   fem_sell_sl_unpair  : its plain SELL values
+ *   fem_pcg_set_layout  : a context (16-bit columns set) reads the caller's svals (bs = 1 also pcols / uoff / ucol)
+ *                         and windows (nullable) instead of building its own paired copy: no conversion at
+ *                         fem_pcg_start; the arrays must outlive the context; vals of fem_pcg_create is then not read. */
+int fem_sell_sl_pattern(int64_t nrows, const int64_t* slice_ptr, const int16_t* dcols, int G, int16_t* pcols,
+                        int16_t* ucol, int32_t* uoff, int32_t* win, fem_stream_t stream);
+int fem_assemble_tet4_sl(const double* coords, const int64_t* conn, double E, double nu, int bs,
+                         const int32_t* inc_ptr, const int32_t* inc, int64_t N, const int32_t* rowptr,
+                         const int32_t* colidx, const int64_t* slice_ptr, const int32_t* uoff, const int16_t* ucol,
+                         int store, int max_width, double* svals, int64_t* bad_idx, fem_stream_t stream);
+int fem_assemble_from_ke_sl(const double* Ke, const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc,
+                            int64_t N, const int32_t* rowptr, const int32_t* colidx, const int64_t* slice_ptr,
+                            int store, int max_width, double* svals, fem_stream_t stream);
+int fem_jacobi_sl(const double* svals, int bs, const int32_t* rowptr, const int32_t* diagpos,
+                  const int64_t* slice_ptr, const int32_t* uoff, const int16_t* ucol, int64_t nrows,
+                  const uint8_t* mask, double* w, fem_stream_t stream);
+int fem_spmv_sl(int64_t nrows, int bs, const int64_t* slice_ptr, const int16_t* pcols, const double* svals,
+                const int32_t* uoff, const int16_t* ucol, const double* x, double* y, fem_stream_t stream);
+int fem_sell_sl_unpair(int64_t nrows, int bs, const int64_t* slice_ptr, const int16_t* dcols, const int32_t* uoff,
+                       const int16_t* ucol, const int32_t* rowptr, const double* svals, double* vals,
+                       fem_stream_t stream);
+int fem_pcg_set_layout(fem_pcg* s, const double* svals, const int16_t* pcols, const int32_t* uoff,
+                       const int16_t* ucol, const int32_t* win, int G);
 /* [host] the persistent build the context's launches run (valid after fem_pcg_start; all 0 when the schedule is not
  * 3): register slots per wave (bs = 1: 1, 2, 4 or 7; bs = 3: 2), 1 for the overflow build, and the packed
  * assignment's slices per wave (0: the even spread) */

@@ -521,7 +521,7 @@ def test_fresh_matrix_store_equals_zero_and_add(gpu, etype, n):
         Kb = K if bs == 3 else K[:, 0::3, 0::3].contiguous()
         Mb = Me if bs == 3 else Me[:, 0::3, 0::3].contiguous()
         fresh = system.SellMatrix(g, bs)
-        fresh._vals.fill_(float("nan"))          # garbage: every value must be written by the store pass
+        fresh._plain_buf().fill_(float("nan"))          # garbage: every value must be written by the store pass
         fresh.add_element_matrices(Kb, tg)
         zeroed = system.SellMatrix(g, bs)
         zeroed.vals                               # zero first, then the add path
@@ -679,6 +679,118 @@ def test_slice_uniform_deltas_are_bit_identical(gpu, case):
         assert torch.equal(x1, x0) and rz1 == rz0, (case, sched)
 
 
+@pytest.mark.parametrize("case", ["kuhn", "kuhn_unused_node", "permuted", "wide"])
+def test_solver_layout_is_bit_identical_to_plain(gpu, case, monkeypatch):
+    """P1 assembly straight into the solver layout (lane-paired entries, slice-uniform delta lists
+    from the pattern, the persistent schedule's gather windows formed with the pattern) against the plain SELL matrix
+    whose contexts build their own paired copy at every start (FEM355_SL=0): the plain values formed back from the
+    solver layout, Jacobi weights, the operator, fixed iterations of the persistent / deferred / 3-kernel schedules
+    and a solve to tolerance -- all bit for bit; a second assembly added onto the first as well. Cases: Kuhn cube,
+    an unused node (empty row, partial uniformity), a random numbering (no uniform slice), a fan (a 43-column row:
+    the 32-column accumulator window, two sweeps)."""
+    _, mesh, _, system = _mods()
+    c, t = mesh.kuhn_cube(13, jitter=0.1)
+    N = c.shape[0]
+    if case == "kuhn_unused_node":
+        c = torch.cat([c[:700], torch.tensor([[4.0, 4.0, 4.0]], dtype=c.dtype), c[700:]])
+        t = t + (t >= 700).to(t.dtype)
+        N += 1
+    elif case == "permuted":
+        perm = torch.randperm(N, generator=torch.Generator().manual_seed(11))
+        inv = torch.empty_like(perm)
+        inv[perm] = torch.arange(N)
+        c, t = c[perm], inv[t]
+    elif case == "wide":   # a hub row of 43 columns: the 32-column window, two sweeps
+        c, t = _helix_fan(40)
+        N = c.shape[0]
+    cg, tg = c.to(gpu), t.to(gpu)
+    monkeypatch.setenv("FEM355_SL", "0")
+    P = system.assemble_tet4_system(cg, tg, "poisson", 1.7)
+    monkeypatch.delenv("FEM355_SL", raising=False)
+    S = system.assemble_tet4_system(cg, tg, "poisson", 1.7)
+    assert S.solver_layout and not P.solver_layout
+    mask = torch.zeros(N, dtype=torch.uint8, device=gpu)
+    mask[::7] = 1
+    wS, wP = S.jacobi(mask), P.jacobi(mask)
+    assert torch.equal(wS, wP)
+    x = torch.randn(N, dtype=F64, generator=torch.Generator().manual_seed(3)).to(gpu)
+    assert torch.equal(S.matvec(x), P.matvec(x))
+    b = torch.randn(N, dtype=F64, generator=torch.Generator().manual_seed(2)).to(gpu)
+    for sched in (3, 2, 0):
+        _, rzS, xS = _fixed_iterates(system, S, b, wS, sched, None, 30)
+        _, rzP, xP = _fixed_iterates(system, P, b, wP, sched, None, 30)
+        assert torch.equal(xS, xP) and rzS == rzP, (case, sched)
+    tol = 1e-9 * float(torch.sqrt(torch.dot(b, wP * b)))
+    rS, rP = S.pcg(b, w=wS, tol=tol, max_iter=3000), P.pcg(b, w=wP, tol=tol, max_iter=3000)
+    assert rS.iterations == rP.iterations and torch.equal(rS.x, rP.x)
+    assert S.solver_layout   # nothing above needed the plain copy
+    assert torch.equal(S.vals, P.vals)   # the plain values formed back from the solver layout
+    # adding a second assembly onto the solver layout
+    S2 = system.assemble_tet4_system(cg, tg, "poisson", 1.7)
+    S2.add_tet4(cg, tg, 0.3)
+    monkeypatch.setenv("FEM355_SL", "0")
+    P2 = system.assemble_tet4_system(cg, tg, "poisson", 1.7)
+    P2.add_tet4(cg, tg, 0.3)
+    assert S2.solver_layout and torch.equal(S2.vals, P2.vals)
+
+
+@pytest.mark.parametrize("case", ["tet4", "tet4_permuted", "c3d8", "tet4_plus_ke"])
+def test_solver_layout_elastic_is_bit_identical_to_plain(gpu, case, monkeypatch):
+    """bs = 3 solver layout: the c3d4 accumulator kernel and the stored-K_e tile kernel write the
+    plane-paired layout A the paired schedules read, so no start converts the matrix and one copy is resident.
+    Against the plain matrix (FEM355_SL=0, whose contexts build their layout-A copy at start): Jacobi weights, the
+    operator, fixed iterations of the persistent / deferred / 3-kernel schedules, a solve to tolerance and the plain
+    values formed back -- bit for bit. Cases: a jittered Kuhn cube, the same renumbered at random (wide slices), a
+    hexahedral box from stored K_e (stored then added; the reference's c3d10 rule is not positive definite, Q2), and c3d4 values plus the same operator's K_e added on top."""
+    el, mesh, _, system = _mods()
+    if case == "c3d8":
+        c, t = mesh.hex_box(7, jitter=0.1)
+    else:
+        c, t = mesh.kuhn_cube(9, jitter=0.1)
+    if case == "tet4_permuted":
+        perm = torch.randperm(c.shape[0], generator=torch.Generator().manual_seed(11))
+        inv = torch.empty_like(perm)
+        inv[perm] = torch.arange(perm.numel())
+        c, t = c[perm], inv[t]
+    N = c.shape[0]
+    cg, tg = c.to(gpu), t.to(gpu)
+    g = system.build_graph(tg, N)
+    K = None if case.startswith("tet4") and case != "tet4_plus_ke" else \
+        el.compute_K_matrix(cg, tg, "c3d8" if case == "c3d8" else "c3d4", E, NU, device=gpu, dtype=F64)
+
+    def build():
+        A = system.SellMatrix(g, 3)
+        if case == "c3d8":
+            A.add_element_matrices(K, tg)
+            A.add_element_matrices(K, tg)
+        else:
+            A.add_tet4(cg, tg, E, NU)
+            if K is not None:
+                A.add_element_matrices(K, tg)
+        return A
+    monkeypatch.setenv("FEM355_SL", "0")
+    P = build()
+    monkeypatch.delenv("FEM355_SL", raising=False)
+    S = build()
+    assert S.solver_layout and not P.solver_layout
+    mask = torch.zeros(3 * N, dtype=torch.uint8, device=gpu)
+    mask[::11] = 1
+    wS, wP = S.jacobi(mask), P.jacobi(mask)
+    assert torch.equal(wS, wP)
+    x = torch.randn(3 * N, dtype=F64, generator=torch.Generator().manual_seed(3)).to(gpu)
+    assert torch.equal(S.matvec(x), P.matvec(x))
+    b = torch.randn(3 * N, dtype=F64, generator=torch.Generator().manual_seed(2)).to(gpu)
+    for sched in (3, 2, 0):
+        _, rzS, xS = _fixed_iterates(system, S, b, wS, sched, None, 25)
+        _, rzP, xP = _fixed_iterates(system, P, b, wP, sched, None, 25)
+        assert torch.equal(xS, xP) and rzS == rzP, (case, sched)
+    tol = 1e-8 * float(torch.sqrt(torch.dot(b, wP * b)))
+    rS, rP = S.pcg(b, w=wS, tol=tol, max_iter=4000), P.pcg(b, w=wP, tol=tol, max_iter=4000)
+    assert rS.iterations == rP.iterations and torch.equal(rS.x, rP.x)
+    assert S.solver_layout
+    assert torch.equal(S.vals, P.vals)
+
+
 @pytest.mark.parametrize("n,jitter", [(20, 0.1), (66, 0.0), (80, 0.05)])
 def test_persistent_slot_builds_are_bit_identical(gpu, n, jitter):
     """When every wave owns at most 1 / 2 / 4 slices the persistent schedule runs a one- / two- / four-slot build with
@@ -778,8 +890,9 @@ def test_persistent_falls_back_and_guards(gpu):
 
 @pytest.mark.parametrize("etype,n,rep", [("c3d8", 5, 1), ("c3d6", 4, 1), ("c3d10", 4, 1), ("c3d10", 3, 9)])
 def test_element_row_assembly_bit_identical_to_column_form(gpu, etype, n, rep, monkeypatch):
-    """bs = 3 assembly from stored K_e: the element-row kernel (k_assemble_ke_rows3, default) and the column-owner
-    kernel (k_assemble_ke_w, FEM355_KE_COLS) give the same SELL values bit for bit -- also with every element
+    """bs = 3 assembly from stored K_e: the tile kernel (k_assemble_ke_tile3, default), the element-row kernel
+    (k_assemble_ke_rows3 + block-CSR buffer, FEM355_KE_ROWS; its direct-SELL variant FEM355_KE_SELLW) and the
+    column-owner kernel (k_assemble_ke_w, FEM355_KE_COLS) give the same SELL values bit for bit, stored and added -- also with every element
     repeated (rows past 64 incident elements and past the 64-column window) and with a node listed twice in one
     element (the ordered duplicate path)."""
     el, mesh, _, system = _mods()
@@ -795,18 +908,29 @@ def test_element_row_assembly_bit_identical_to_column_form(gpu, etype, n, rep, m
     if rep > 1:
         rp = g.rowptr.cpu()
         assert int((rp[1:] - rp[:-1]).max()) > 64 or int((g.inc_ptr[1:] - g.inc_ptr[:-1]).max()) > 64
-    def fresh():
+    def fresh(twice=False):
         A = system.SellMatrix(g, 3)
-        A._vals.fill_(float("nan"))   # a fresh matrix is stored whole: no entry may be left unwritten
-        return A.add_element_matrices(K, tg).vals.clone()
-    monkeypatch.delenv("FEM355_KE_COLS", raising=False)
-    a = fresh()
-    monkeypatch.setenv("FEM355_KE_SELLW", "1")      # the row sums straight into the SELL planes
+        A._plain_buf().fill_(float("nan"))   # a fresh matrix is stored whole: no entry may be left unwritten
+        A.add_element_matrices(K, tg)
+        if twice:                     # and adding onto stored values
+            A.add_element_matrices(K, tg)
+        return A.vals.clone()
+    for v in ("FEM355_KE_COLS", "FEM355_KE_ROWS", "FEM355_KE_SELLW"):
+        monkeypatch.delenv(v, raising=False)
+    a, a2 = fresh(), fresh(True)          # tile form (default: rows of a slice together, straight into SELL)
+    monkeypatch.setenv("FEM355_KE_ROWS", "1")       # element-row form + block-CSR buffer + slice pass
+    r, r2 = fresh(), fresh(True)
+    monkeypatch.setenv("FEM355_KE_SELLW", "1")      # element-row form, row sums straight into the SELL planes
     d = fresh()
     monkeypatch.delenv("FEM355_KE_SELLW", raising=False)
-    monkeypatch.setenv("FEM355_KE_COLS", "1")
+    monkeypatch.delenv("FEM355_KE_ROWS", raising=False)
+    monkeypatch.setenv("FEM355_KE_COLS", "1")       # column-owner form
     b = fresh()
-    assert torch.equal(a, b) and torch.equal(a, d), etype
+    monkeypatch.delenv("FEM355_KE_COLS", raising=False)
+    monkeypatch.setenv("FEM355_SL", "0")            # tile form into the plain planes instead of the solver layout
+    p, p2 = fresh(), fresh(True)
+    assert torch.equal(a, b) and torch.equal(a, r) and torch.equal(a, d) and torch.equal(a2, r2), etype
+    assert torch.equal(a, p) and torch.equal(a2, p2), etype
 
 
 @pytest.mark.parametrize("kind,mode,small", [("elastic", "cg", False), ("elastic", "pcg", False),
@@ -979,7 +1103,7 @@ def test_tile_assembly_bit_identical_to_row_kernels(gpu, case, monkeypatch):
             else:
                 monkeypatch.delenv("FEM355_ASM_ROWS", raising=False)
             A = system.SellMatrix(g, bs)
-            A._vals.fill_(float("nan"))    # a fresh matrix's buffer is never read by the store path
+            A._plain_buf().fill_(float("nan"))    # a fresh matrix's buffer is never read by the store path
             A.add_tet4(cg, tg, Ek, NU)
             first = A.vals.clone()
             A.add_tet4(cg, tg, Ek, NU)
