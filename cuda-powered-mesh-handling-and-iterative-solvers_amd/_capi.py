@@ -144,6 +144,13 @@ SIGNATURES = {
     "fem_ipc_close": (_I, [_P]),
     "fem_sell_diag": (_I, [_P, _I, _P, _P, _L, _P, _P]),
     "fem_jacobi_from_diag": (_I, [_P, _L, _P, _P, _P]),
+    "fem_mf_create": (_I, [_P, _P, _L, _L, _I, _D, _D, ctypes.POINTER(_L), _P, ctypes.POINTER(_P)]),
+    "fem_mf_destroy": (_I, [_P]),
+    "fem_mf_apply": (_I, [_P, _P, _P, _P]),
+    "fem_mf_diag": (_I, [_P, _P, _P]),
+    "fem_mf_info": (_I, [_P, ctypes.POINTER(_L)]),
+    "fem_mf_order": (_I, [_P, _P, _P, _P, _P, _P]),
+    "fem_pcg_set_operator_mf": (_I, [_P, _P]),
     "fem_comm_unique_id": (_I, [ctypes.c_char_p]),
     "fem_comm_init": (_I, [_I, _I, ctypes.c_char_p, ctypes.POINTER(_P)]),
     "fem_comm_destroy": (_I, [_P]),

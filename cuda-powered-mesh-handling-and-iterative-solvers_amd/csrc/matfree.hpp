@@ -1,0 +1,329 @@
+// Element-chunk (matrix-free) c3d4 operator: y = K x = sum_e P_e^T K_e P_e x formed from the vertex coordinates in
+// every application, never stored -- the reference's element-by-element product (`compute_nodal_forces`,
+// `solver/element.py:429-464`) with K_e of `compute_c3d4_K_matrix` (`:883-903`) evaluated in closed form:
+//   elasticity  f_a = V sigma(H) g_a,  H = sum_b x_b g_b^T,  sigma = lambda tr(H) I + mu (H + H^T)
+//               (= sum_b K_ab x_b with K_ab = V (lambda g_a g_b^T + mu g_b g_a^T + mu (g_a . g_b) I));
+//   Poisson     f_a = kappa V g_a . (sum_b g_b x_b).
+// Layout (built once per mesh by fem_mf_create, matfree.hip): the elements in Morton order of their centroids, cut
+// into chunks of <= MF_EC elements touching <= MF_NC nodes; per chunk its local nodes (ascending global id) and, per
+// local node, the (element, corner) pairs that touch it in ascending order. One workgroup per chunk gathers the local
+// nodes' coordinates and x into LDS, forms the element vectors f (MF_PASS elements at a time), and every local node
+// sums its pairs in that fixed order into a slot (chunk-major); a node's value is the sum of its slots in ascending
+// chunk order (k_mf_gather). Deterministic: no atomics, every sum in a fixed order.
+#pragma once
+#include "common.hpp"
+#include "element.hpp"
+
+namespace fem {
+
+constexpr int MF_EC = 512;      // elements per chunk (at most)
+constexpr int MF_NC = 256;      // local nodes per chunk (at most; local ids are bytes)
+constexpr int MF_PASS = 256;    // elements formed per pass (= threads of the workgroup)
+constexpr int MF_BLOCK = 256;
+
+enum { MF_APPLY = 0, MF_DOT = 1, MF_DIAG = 2 };
+
+// device view of the operator
+struct MfOp {
+    int64_t nchunks, nslots, nnodes;
+    int bs;
+    const int32_t* cptr;    // [nchunks + 1] element offsets (into the Morton-ordered arrays)
+    const int32_t* sbase;   // [nchunks + 1] slot offsets (= local node counts, prefix summed)
+    const int32_t* cnode;   // [nslots] global node of each slot (ascending within a chunk)
+    const uint32_t* eloc;   // [M] the element's 4 local node ids, one byte each (corner b in byte b)
+    const uint16_t* lptr;   // [nslots + nchunks] per chunk c at sbase[c] + c: first pair of local node l, + end
+    const uint16_t* lent;   // [4 M] per chunk at 4 cptr[c]: pairs (element_in_chunk << 2 | corner), node-major
+    const int32_t* nptr;    // [nnodes + 1] node -> its slots
+    const int32_t* nslot;   // [nslots] slots of each node, ascending (= ascending chunk)
+    const double* X;        // [nnodes, 3] coordinates
+    double lam, mu, kappa;
+};
+
+// the host object (fem_mf of the C-ABI, matfree.hip) as pcg.hip's K1 sees it
+MfOp mf_op(const fem_mf* m);
+double* mf_slots(const fem_mf* m);
+int mf_bs(const fem_mf* m);
+int64_t mf_nodes(const fem_mf* m);
+int mf_apply(fem_mf* m, const double* x, double* y, hipStream_t st);
+
+// element vectors of one element: f[a][c] for the 4 corners (BS = 3: c = 0..2; BS = 1: c = 0). DIAG: the diagonal of
+// the corner's own block (K_aa)_cc instead of (K_e x)_a.
+template <int BS, int MODE>
+__device__ __forceinline__ void mf_element(const double xc[4][3], const double xv[4][BS], double lam, double mu,
+                                           double kappa, double f[4][BS]) {
+    double g[4][3];
+    const double det = tet4_grads_p(xc, g);
+    const double V = fabs(det) / 6.0;
+    if constexpr (MODE == MF_DIAG) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            const double gg = g[a][0] * g[a][0] + g[a][1] * g[a][1] + g[a][2] * g[a][2];
+            if constexpr (BS == 1) {
+                f[a][0] = kappa * gg * V;
+            } else {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) f[a][c] = V * ((lam + mu) * (g[a][c] * g[a][c]) + mu * gg);
+            }
+        }
+        return;
+    }
+    if constexpr (BS == 1) {
+        double gu[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            gu[k] = g[0][k] * xv[0][0] + g[1][k] * xv[1][0] + g[2][k] * xv[2][0] + g[3][k] * xv[3][0];
+        const double s = kappa * V;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) f[a][0] = s * (g[a][0] * gu[0] + g[a][1] * gu[1] + g[a][2] * gu[2]);
+    } else {
+        // H[i][j] = sum_b x_b[i] g_b[j]
+        double H[3][3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                H[i][j] = xv[0][i] * g[0][j] + xv[1][i] * g[1][j] + xv[2][i] * g[2][j] + xv[3][i] * g[3][j];
+        const double tr = H[0][0] + H[1][1] + H[2][2];
+        const double lt = lam * tr;
+        // V sigma (symmetric)
+        const double s00 = V * (lt + 2.0 * mu * H[0][0]);
+        const double s11 = V * (lt + 2.0 * mu * H[1][1]);
+        const double s22 = V * (lt + 2.0 * mu * H[2][2]);
+        const double s01 = V * (mu * (H[0][1] + H[1][0]));
+        const double s02 = V * (mu * (H[0][2] + H[2][0]));
+        const double s12 = V * (mu * (H[1][2] + H[2][1]));
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            f[a][0] = s00 * g[a][0] + s01 * g[a][1] + s02 * g[a][2];
+            f[a][1] = s01 * g[a][0] + s11 * g[a][1] + s12 * g[a][2];
+            f[a][2] = s02 * g[a][0] + s12 * g[a][1] + s22 * g[a][2];
+        }
+    }
+}
+
+// LDS of one chunk application
+template <int BS>
+struct MfLds {
+    double nd[MF_NC][3 + BS];        // per local node: coordinates, then x (rows 16-byte aligned: 48 / 32 bytes)
+    double fs[4 * BS][MF_PASS + 1];  // element vectors of the current pass: [corner * BS + c][element]
+    uint16_t lp[MF_NC + 1];          // pair pointers of the local nodes
+    alignas(16) uint16_t ent[4 * MF_EC];   // the chunk's pairs, node-major
+};
+
+// What a thread loads for one chunk ahead of its use (software pipeline over a workgroup's chunks): the chunk's
+// ranges, this thread's local node (id, coordinates, x), pair pointer, 8 pairs and the local ids of its 2 elements.
+template <int BS>
+struct MfPf {
+    int e0, ne, s0, nn;
+    int node;
+    uint16_t lp;
+    uint4 ent;
+    uint32_t el[MF_EC / MF_PASS];
+    double xv[3], pv[BS];
+};
+
+// stage 1: everything but the node-dependent gathers
+template <int BS>
+__device__ __forceinline__ void mf_pf1(const MfOp& op, int64_t c, MfPf<BS>& f) {
+    const int tid = threadIdx.x;
+    f.e0 = op.cptr[c];
+    f.ne = op.cptr[c + 1] - f.e0;
+    f.s0 = op.sbase[c];
+    f.nn = op.sbase[c + 1] - f.s0;
+    f.node = 0;
+    f.lp = 0;
+    if (tid < f.nn) {
+        f.node = op.cnode[f.s0 + tid];
+        f.lp = op.lptr[f.s0 + c + tid];
+    }
+    f.ent = make_uint4(0, 0, 0, 0);
+    if (8 * tid < 4 * f.ne) f.ent = reinterpret_cast<const uint4*>(op.lent + 4 * (int64_t)f.e0)[tid];
+#pragma unroll
+    for (int j = 0; j < MF_EC / MF_PASS; ++j) f.el[j] = tid + MF_PASS * j < f.ne ? op.eloc[f.e0 + tid + MF_PASS * j] : 0u;
+}
+
+// stage 2: the local node's coordinates and x (after stage 1's node id arrived)
+template <int BS, int MODE>
+__device__ __forceinline__ void mf_pf2(const MfOp& op, const double* __restrict__ x, MfPf<BS>& f) {
+    if ((int)threadIdx.x < f.nn) {
+        const int64_t g = f.node;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) f.xv[k] = op.X[3 * g + k];
+#pragma unroll
+        for (int k = 0; k < BS; ++k) f.pv[k] = MODE == MF_DIAG ? 0.0 : x[BS * g + k];
+    }
+}
+
+// Every chunk of this workgroup (chunk ranges per XCD, consecutive chunks -- neighbours in space -- at once on one XCD,
+// whose L2 then holds their shared nodes): the slot values of its local nodes (slots[(sbase[c] + l) * BS + c]); the
+// next chunk's data is loaded while the current one is formed. MODE_DOT returns this thread's part of
+// sum_l x_l . slot_l over its chunks (0 elsewhere). x unused for MF_DIAG.
+template <int BS, int MODE>
+__device__ __forceinline__ double mf_walk(const MfOp& op, const double* __restrict__ x, double* __restrict__ slots,
+                                          MfLds<BS>& L) {
+    const int tid = threadIdx.x;
+    const int64_t per = (op.nchunks + NXCD - 1) / NXCD;
+    const int64_t base = (int64_t)(blockIdx.x % NXCD) * per;
+    const int64_t nb = gridDim.x / NXCD;
+    int64_t k = blockIdx.x / NXCD;
+    double dot = 0.0;
+    if (k >= per || base + k >= op.nchunks) return dot;
+    MfPf<BS> cur, nxt;
+    mf_pf1<BS>(op, base + k, cur);
+    mf_pf2<BS, MODE>(op, x, cur);
+    for (;;) {
+        const int64_t c = base + k;
+        __syncthreads();   // the previous chunk's LDS reads are done
+        if (tid < cur.nn) {
+#pragma unroll
+            for (int q = 0; q < 3; ++q) L.nd[tid][q] = cur.xv[q];
+#pragma unroll
+            for (int q = 0; q < BS; ++q) L.nd[tid][3 + q] = cur.pv[q];
+            L.lp[tid] = cur.lp;
+        }
+        if (tid == 0) L.lp[cur.nn] = (uint16_t)(4 * cur.ne);
+        if (8 * tid < 4 * cur.ne) reinterpret_cast<uint4*>(L.ent)[tid] = cur.ent;
+        const int64_t kn = k + nb;
+        const bool more = kn < per && base + kn < op.nchunks;
+        if (more) mf_pf1<BS>(op, base + kn, nxt);
+        __syncthreads();
+        double acc[BS];
+#pragma unroll
+        for (int q = 0; q < BS; ++q) acc[q] = 0.0;
+        int pos = tid < cur.nn ? L.lp[tid] : 0;
+        const int end = tid < cur.nn ? L.lp[tid + 1] : 0;
+        // the node's pairs split at the pass boundary (pairs ascend by element): lower bound of 4 MF_PASS
+        int mid = end;
+        if (cur.ne > MF_PASS) {
+            int lo = pos, len = end - pos;
+            while (len > 0) {
+                const int half = len >> 1;
+                if (L.ent[lo + half] < 4 * MF_PASS) {
+                    lo += half + 1;
+                    len -= half + 1;
+                } else {
+                    len = half;
+                }
+            }
+            mid = lo;
+        }
+#pragma unroll
+        for (int j = 0; j < MF_EC / MF_PASS; ++j) {
+            const int h = MF_PASS * j;
+            if (h >= cur.ne) break;
+            if (h + tid < cur.ne) {
+                const uint32_t w = cur.el[j];
+                double xc[4][3], xv[4][BS], f[4][BS];
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const int l = (w >> (8 * b)) & 0xff;
+                    const double2* r = reinterpret_cast<const double2*>(&L.nd[l][0]);
+                    const double2 a0 = r[0], a1 = r[1];
+                    xc[b][0] = a0.x;
+                    xc[b][1] = a0.y;
+                    xc[b][2] = a1.x;
+                    if constexpr (BS == 1) {
+                        xv[b][0] = a1.y;
+                    } else {
+                        const double2 a2 = r[2];
+                        xv[b][0] = a1.y;
+                        xv[b][1] = a2.x;
+                        xv[b][2] = a2.y;
+                    }
+                }
+                mf_element<BS, MODE>(xc, xv, op.lam, op.mu, op.kappa, f);
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+#pragma unroll
+                    for (int q = 0; q < BS; ++q) L.fs[b * BS + q][tid] = f[b][q];
+            }
+            if (j == 0 && more) mf_pf2<BS, MODE>(op, x, nxt);   // the next chunk's gathers, under this chunk's work
+            __syncthreads();
+            // every local node adds its pairs of this pass in ascending (element, corner) order; the pair reads of
+            // four steps are issued before their adds (independent LDS loads, one latency per four pairs)
+            const int stop = j == 0 ? mid : end;
+            for (; pos + 4 <= stop; pos += 4) {
+                int pe[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) pe[u] = L.ent[pos + u];
+                double v[4][BS];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int el = (pe[u] >> 2) - h, b = pe[u] & 3;
+#pragma unroll
+                    for (int q = 0; q < BS; ++q) v[u][q] = L.fs[b * BS + q][el];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+#pragma unroll
+                    for (int q = 0; q < BS; ++q) acc[q] += v[u][q];
+            }
+            for (; pos < stop; ++pos) {
+                const int pe = L.ent[pos];
+                const int el = (pe >> 2) - h, b = pe & 3;
+#pragma unroll
+                for (int q = 0; q < BS; ++q) acc[q] += L.fs[b * BS + q][el];
+            }
+            __syncthreads();
+        }
+        if (tid < cur.nn) {
+#pragma unroll
+            for (int q = 0; q < BS; ++q) {
+                slots[(int64_t)(cur.s0 + tid) * BS + q] = acc[q];
+                if constexpr (MODE == MF_DOT) dot += cur.pv[q] * acc[q];
+            }
+        }
+        if (!more) break;
+        k = kn;
+        cur = nxt;
+    }
+    return dot;
+}
+
+// resident workgroups of a chunk kernel (one pass of the grid over the chunks), cached per kernel
+inline int mf_resident_grid(const void* fn, int block, int64_t nchunks) {
+    static int cache[8] = {0};
+    static const void* keys[8] = {nullptr};
+    int per_cu = 0;
+    for (int i = 0; i < 8; ++i)
+        if (keys[i] == fn) per_cu = cache[i];
+    if (per_cu == 0) {
+        int dev = 0, ncu = 0, nb = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, block, 0) != hipSuccess || nb < 1)
+            nb = 1, ncu = 256;
+        per_cu = ((ncu / NXCD) * NXCD) * nb;
+        for (int i = 0; i < 8; ++i)
+            if (!keys[i] || keys[i] == fn) {
+                keys[i] = fn;
+                cache[i] = per_cu;
+                break;
+            }
+    }
+    int64_t g = per_cu;
+    const int64_t want = ((nchunks + NXCD - 1) / NXCD) * NXCD;
+    if (want < g) g = want;
+    return (int)(g < NXCD ? NXCD : g);
+}
+
+// y[node] = sum of the node's slots in ascending chunk order (0 for a node of no element)
+template <int BS>
+__global__ void __launch_bounds__(256) k_mf_gather(MfOp op, const double* __restrict__ slots, double* __restrict__ y) {
+    for (int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; a < op.nnodes;
+         a += (int64_t)gridDim.x * blockDim.x) {
+        const int k0 = op.nptr[a], k1 = op.nptr[a + 1];
+        double s[BS];
+#pragma unroll
+        for (int k = 0; k < BS; ++k) s[k] = 0.0;
+        for (int k = k0; k < k1; ++k) {
+            const int64_t sl = op.nslot[k];
+#pragma unroll
+            for (int c = 0; c < BS; ++c) s[c] += slots[sl * BS + c];
+        }
+#pragma unroll
+        for (int c = 0; c < BS; ++c) y[a * BS + c] = s[c];
+    }
+}
+
+}  // namespace fem

@@ -25,6 +25,7 @@
 
 #include "sell_pair.hpp"
 #include "sell_pair3.hpp"
+#include "matfree.hpp"
 
 namespace fem {
 
@@ -1723,6 +1724,8 @@ struct fem_pcg {
     int upd1;
     int u2_grid;
     unsigned* u2_sync;                    // [U2_WORDS]: release epoch, broadcast (beta, halt), give-up
+    // element-chunk operator (fem_pcg_set_operator_mf): K1 = k_pcg_mf_dot + k_mf_gather instead of a SELL SpMV
+    fem_mf* mf;
 };
 
 #define FEM_NCCL(call)                                                                         \
@@ -1741,7 +1744,42 @@ static double* st_red(fem_pcg* s, int k) {
     return reinterpret_cast<double*>(reinterpret_cast<char*>(s->st) + offsetof(PcgState, red)) + k;
 }
 
+// K1 on the element-chunk operator (matfree.hpp): the chunks' slot values of q = A p and the p.q partials (sum over
+// every chunk's local nodes of p . slot = p . A p), then alpha as k_pcg_spmv_dot; the slots are summed into q by
+// k_mf_gather. Workgroups walk chunks XCD-contiguously (chunk ranges per XCD, consecutive chunks at once).
+template <int BS>
+__global__ void __launch_bounds__(MF_BLOCK) k_pcg_mf_dot(MfOp op, const double* __restrict__ p,
+                                                         double* __restrict__ slots, PcgState* __restrict__ st,
+                                                         RedBuf red) {
+    __shared__ MfLds<BS> L;
+    __shared__ double lds4[4];
+    __shared__ int flag;
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->xupd = 0;
+    if (st->halt || st->iter >= st->max_iter) return;
+    double dot = mf_walk<BS, MF_DOT>(op, p, slots, L);
+    dot = block_sum256(dot, lds4);
+    double pq;
+    if (reduce_grid(dot, red.part(RED_K1), red.cnt(RED_K1), &pq, lds4, &flag) && threadIdx.x == 0) finish_pq(st, pq);
+}
+
+static int launch_mf_dot(fem_pcg* s) {
+    const MfOp op = mf_op(s->mf);
+    double* sl = mf_slots(s->mf);
+    const int G = mf_resident_grid(s->bs == 3 ? (const void*)k_pcg_mf_dot<3> : (const void*)k_pcg_mf_dot<1>, MF_BLOCK,
+                                   op.nchunks);
+    if (s->bs == 3) hipLaunchKernelGGL(k_pcg_mf_dot<3>, dim3(G), dim3(MF_BLOCK), 0, s->stream, op, s->p0, sl, s->st, s->red);
+    else hipLaunchKernelGGL(k_pcg_mf_dot<1>, dim3(G), dim3(MF_BLOCK), 0, s->stream, op, s->p0, sl, s->st, s->red);
+    FEM_LAUNCHED();
+    if (op.nnodes > 0) {
+        if (s->bs == 3) hipLaunchKernelGGL(k_mf_gather<3>, dim3(stream_grid(op.nnodes, 256)), dim3(256), 0, s->stream, op, sl, s->q);
+        else hipLaunchKernelGGL(k_mf_gather<1>, dim3(stream_grid(op.nnodes, 256)), dim3(256), 0, s->stream, op, sl, s->q);
+        FEM_LAUNCHED();
+    }
+    return FEM_OK;
+}
+
 static int launch_spmv_dot(fem_pcg* s) {
+    if (s->mf) return launch_mf_dot(s);
     if (s->cols16) {
 #define FEM_K1D(B, F, D)                                                                                           \
     hipLaunchKernelGGL((k_pcg_spmv_dot<B, F, D, int16_t>), dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream,     \
@@ -2589,6 +2627,22 @@ int fem_pcg_create(int64_t nrows, int bs, const int64_t* slice_ptr, const int32_
     return FEM_OK;
 }
 
+int fem_pcg_set_operator_mf(fem_pcg* s, fem_mf* m) {
+    if (!s || !m || mf_bs(m) != s->bs || mf_nodes(m) != s->nrows) {
+        set_error("fem_pcg_set_operator_mf: the operator's block size / node count do not match the context");
+        return FEM_EARG;
+    }
+    if (s->dist || s->pd || s->has_con || s->graph) {
+        set_error("fem_pcg_set_operator_mf: single-GPU contexts without constraints or a captured graph only");
+        return FEM_EARG;
+    }
+    s->mf = m;
+    s->fused = s->deferred = s->persist_req = s->persist_fit_only = s->persist = 0;
+    s->cols16 = nullptr;
+    s->pext = 0;
+    return FEM_OK;
+}
+
 int fem_pcg_set_entries(fem_pcg* s, int64_t entries) {
     if (entries < 0) {
         set_error("fem_pcg_set_entries: negative entry count %lld", (long long)entries);
@@ -2610,6 +2664,14 @@ int fem_pcg_set_schedule(fem_pcg* s, int sched) {
     // 4 = auto: the persistent schedule when it applies -- for bs = 3 only while every wave's slices fit on chip (the
     // overflow build streams most of the 10M-tet elastic state and measured 633 vs 436 us per iteration), else the
     // 3-kernel schedule; for bs = 1 schedule 3 (its overflow build beats the deferred fallback)
+    if (s->mf) {   // the element-chunk operator runs the 3-kernel schedule only (4 = auto selects it)
+        if (sched != 0 && sched != 4) {
+            set_error("fem_pcg_set_schedule: the element-chunk operator runs the 3-kernel schedule");
+            return FEM_EARG;
+        }
+        s->fused = s->deferred = s->persist_req = s->persist_fit_only = s->persist = 0;
+        return FEM_OK;
+    }
     const bool auto3 = sched == 4 && s->bs == 3;
     if (sched == 4) sched = (s->dist || s->mode == FEM_MODE_CG_CONSTRAINED) ? 0 : 3;
     if (sched != 0 && s->dist) {
@@ -3254,7 +3316,9 @@ int fem_pcg_start(fem_pcg* s) {
         s->launched = 0;
         return FEM_OK;   // every rank must finish its start before any rank launches (a host barrier)
     }
-    if (s->pext) {   // solver layout: r0 = b - A x0 from the paired values
+    if (s->mf) {   // element-chunk operator: r0 = b - A x0 from the element formula
+        if ((rc = mf_apply(s->mf, s->x, s->q, s->stream))) return rc;
+    } else if (s->pext) {   // solver layout: r0 = b - A x0 from the paired values
         if (s->bs == 1)
             hipLaunchKernelGGL(k_spmv_pair<SPMV_UP>, dim3(s->grid_spmv), dim3(256), 0, s->stream, s->nslices, s->nrows,
                                s->slice_ptr, s->pcols16, s->pvals, s->puoff, s->pucol, s->x, s->q);

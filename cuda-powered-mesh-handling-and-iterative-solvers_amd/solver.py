@@ -264,7 +264,7 @@ def static_structure_solver(coords, force, fixed, c3d4=None, c3d6=None, c3d8=Non
 
 # ============================================================================ fused mesh -> solution pipeline
 def solve_tet4(coords, elements, f, fixed, kind="poisson", E=1.0, nu=0.0, tol=1e-8, max_iter=10000, device="cuda:0",
-               rtol=None, reorder=None):
+               rtol=None, reorder=None, operator="assembled"):
     """Assembly + Jacobi-PCG straight from the mesh (the benchmark pipeline; no element matrices stored):
     c3d4 Poisson (dpn 1, kappa = E) or elasticity (dpn 3), Dirichlet zero on `fixed` nodes via zeros in the
     exact Jacobi M_inv, reference PCG semantics (absolute tol on sqrt(r.z); `rtol` scales it by sqrt(r0.z0)).
@@ -286,7 +286,10 @@ def solve_tet4(coords, elements, f, fixed, kind="poisson", E=1.0, nu=0.0, tol=1e
         perm, inv = _sys.rcm_order(elements, N)
         coords, elements = _sys.renumber(coords, elements, perm, inv)
         fixed_mask, b = fixed_mask[perm], b[perm]
-    A = _sys.assemble_tet4_system(coords, elements, kind, E, nu)
+    if operator == "matfree":
+        A = _sys.MatFreeOperator(coords, elements, kind, E, nu)
+    else:
+        A = _sys.assemble_tet4_system(coords, elements, kind, E, nu)
     A.check_singular()
     mask = torch.zeros((N, A.bs), dtype=torch.uint8, device=dev)
     mask[fixed_mask] = 1

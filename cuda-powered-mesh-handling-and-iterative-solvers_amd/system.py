@@ -555,6 +555,122 @@ class SellMatrix:
         return PcgResult(x, it.value, stt.value, rz.value, sc[1], hist, ran)
 
 
+@_scoped
+class MatFreeOperator:
+    """Element-chunk c3d4 operator (include/fem355.h fem_mf_*, csrc/matfree.hip): y = K x formed from the vertex
+    coordinates in every application -- the reference's element-by-element product (`compute_nodal_forces`,
+    `solver/element.py:429-464`) of the c3d4 stiffness (`compute_c3d4_K_matrix`, `:883-903`; kind "elastic", 3 dofs
+    per node) or the P1 Laplacian (kind "poisson", kappa = E), no matrix in memory. Same interface as SellMatrix for
+    what the solvers use (n, bs, matvec, diag, jacobi, pcg, PcgRunner)."""
+
+    is_matfree = True
+
+    def __init__(self, coords: torch.Tensor, elements: torch.Tensor, kind="elastic", E=1.0, nu=0.0):
+        lib = C.lib()
+        self.device = coords.device
+        self.coords = coords.to(F64).contiguous()
+        self.elements = elements.to(torch.int64).contiguous()
+        self.kind = kind
+        self.bs = 1 if kind == "poisson" else 3
+        self.n_nodes = self.coords.shape[0]
+        self.n = self.n_nodes * self.bs
+        self.M = self.elements.shape[0]
+        self.h = ctypes.c_void_p()
+        bad = ctypes.c_int64(-1)
+        k = C.KIND_POISSON if kind == "poisson" else C.KIND_ELASTIC
+        C.check(lib.fem_mf_create(C.ptr(self.coords), C.ptr(self.elements), self.M, self.n_nodes, k, float(E),
+                                  float(nu), ctypes.byref(bad), C.stream(self.device), ctypes.byref(self.h)),
+                "fem_mf_create")
+
+    def info(self):
+        """{chunks, slots, bs, static bytes one application streams, M, N}"""
+        out = (ctypes.c_int64 * 6)()
+        C.check(C.lib().fem_mf_info(self.h, out), "fem_mf_info")
+        keys = ("chunks", "slots", "bs", "static_bytes", "elements", "nodes")
+        return dict(zip(keys, list(out)))
+
+    def layout(self):
+        """(Morton element order [M], chunk element offsets, chunk slot offsets, slot nodes) as device int32."""
+        i = self.info()
+        z = lambda k: torch.empty(max(k, 1), dtype=torch.int32, device=self.device)
+        eo, cp, sb, cn = z(self.M), z(i["chunks"] + 1), z(i["chunks"] + 1), z(i["slots"])
+        C.check(C.lib().fem_mf_order(self.h, C.ptr(eo), C.ptr(cp), C.ptr(sb), C.ptr(cn), C.stream(self.device)),
+                "fem_mf_order")
+        return eo[: self.M], cp[: i["chunks"] + 1], sb[: i["chunks"] + 1], cn[: i["slots"]]
+
+    def algorithmic_bytes(self):
+        """HBM bytes one application must move at least: the static layout streams + the coordinates, x and y once."""
+        return self.info()["static_bytes"] + 24 * self.n_nodes + 16 * self.n
+
+    def matvec(self, x: torch.Tensor, out: torch.Tensor = None):
+        x = x.to(device=self.device, dtype=F64).contiguous().view(-1)
+        y = out if out is not None else torch.empty(self.n, dtype=F64, device=self.device)
+        C.check(C.lib().fem_mf_apply(self.h, C.ptr(x), C.ptr(y), C.stream(self.device)), "fem_mf_apply")
+        return y
+
+    def diag(self):
+        d = torch.empty(self.n, dtype=F64, device=self.device)
+        C.check(C.lib().fem_mf_diag(self.h, C.ptr(d), C.stream(self.device)), "fem_mf_diag")
+        return d
+
+    def jacobi(self, fixed_mask: torch.Tensor = None):
+        """w = 1/diag(K) (inf -> 0), zero on fixed DOFs (uint8 mask [n])."""
+        d = self.diag()
+        w = torch.empty_like(d)
+        C.check(C.lib().fem_jacobi_from_diag(C.ptr(d), self.n, C.ptr(fixed_mask), C.ptr(w), C.stream(self.device)),
+                "fem_jacobi_from_diag")
+        return w
+
+    def check_singular(self):
+        return None   # fem_mf_create already raised for a singular element
+
+    def create_context(self, b, x, w, mode, tol, eps, hist, hist_len, stream, h):
+        lib = C.lib()
+        C.check(lib.fem_pcg_create(self.n_nodes, self.bs, None, None, None, C.ptr(b), C.ptr(x), C.ptr(w), mode,
+                                   float(tol), float(eps), C.ptr(hist), hist_len, stream, ctypes.byref(h)),
+                "fem_pcg_create")
+        rc = lib.fem_pcg_set_operator_mf(h, self.h)
+        if rc != C.FEM_OK:
+            lib.fem_pcg_destroy(h)
+            C.check(rc, "fem_pcg_set_operator_mf")
+
+    def pcg(self, b, x0=None, w=None, mode=C.MODE_PCG, tol=1e-8, max_iter=1000, eps=1e-30, history=False, chunk=32):
+        """Device (P)CG on this operator (3-kernel schedule with the merged update); returns a PcgResult."""
+        lib = C.lib()
+        b = b.to(device=self.device, dtype=F64).contiguous().view(-1)
+        x = (torch.zeros(self.n, dtype=F64, device=self.device) if x0 is None
+             else x0.to(device=self.device, dtype=F64).clone().contiguous().view(-1))
+        w = w.to(device=self.device, dtype=F64).contiguous().view(-1)
+        hist = torch.full((max(max_iter, 1),), float("nan"), dtype=F64, device=self.device) if history else None
+        h = ctypes.c_void_p()
+        self.create_context(b, x, w, mode, tol, eps, hist, hist.numel() if hist is not None else 0,
+                            C.stream(self.device), h)
+        try:
+            it, stt, rz = ctypes.c_int(), ctypes.c_int(), ctypes.c_double()
+            C.check(lib.fem_pcg_solve(h, int(max_iter), int(chunk), ctypes.byref(it), ctypes.byref(stt),
+                                      ctypes.byref(rz)), "fem_pcg_solve")
+            sc = (ctypes.c_double * 6)()
+            C.check(lib.fem_pcg_scalars(h, sc), "fem_pcg_scalars")
+            ran = int(lib.fem_pcg_get_schedule(h))
+            _check_sync(stt.value)
+        finally:
+            lib.fem_pcg_destroy(h)
+        if hist is not None:
+            hist = hist[: min(it.value, hist.numel())]
+        return PcgResult(x, it.value, stt.value, rz.value, sc[1], hist, ran)
+
+    def close(self):
+        if getattr(self, "h", None):
+            C.lib().fem_mf_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def _check_sync(status):
     if status == C.PCG_SYNC_TIMEOUT:
         raise RuntimeError("persistent PCG: an in-launch wait gave up (grid synchronisation timed out); "
@@ -582,7 +698,8 @@ class PcgRunner:
         self.stream = torch.cuda.Stream(device=A.device)
         self.stream.wait_stream(torch.cuda.current_stream(A.device))
         self.h = ctypes.c_void_p()
-        self.schedule = 0 if isinstance(self, _DistMarker) else _schedule(fused, schedule, A.bs)
+        self.schedule = (0 if isinstance(self, _DistMarker) or getattr(A, "is_matfree", False)
+                         else _schedule(fused, schedule, A.bs))
         self.constraints = constraints   # keeps the device arrays alive with the context
         self._mode, self._tol, self._eps = mode, float(tol), float(eps)
         # solver-layout values (bs = 1) unless the context must read the plain ones (distributed, fused, constrained)
@@ -590,6 +707,11 @@ class PcgRunner:
 
     def _create(self, plain):
         A = self.A
+        if getattr(A, "is_matfree", False):
+            A.create_context(self.b, self.x, self.w, self._mode, self._tol, self._eps, None, 0,
+                             ctypes.c_void_p(self.stream.cuda_stream), self.h)
+            self._sl = False
+            return
         C.check(self.lib.fem_pcg_create(A.g.n_nodes, A.bs, C.ptr(A.g.slice_ptr), C.ptr(A.g.cols),
                                         A.solver_vals_ptr(plain), C.ptr(self.b), C.ptr(self.x), C.ptr(self.w),
                                         self._mode, self._tol, self._eps, None, 0,

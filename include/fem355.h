@@ -640,6 +640,33 @@ int fem_pcg_dist_buffer(fem_pcg* s, int phase, double** ptr, int64_t* n);
 /* dev_ptr_array: DEVICE array of P device pointers; sums the P buffers (rank order) into each of them */
 int fem_group_allreduce(double* const* dev_ptr_array, int P, int64_t n, fem_stream_t stream);
 
+/* ------------------------------------------------------------------ element-chunk operator (matrix-free c3d4)
+ * y = K x of the c3d4 stiffness (kind FEM_KIND_ELASTIC, bs = 3: K_e of compute_c3d4_K_matrix, `solver/element.py:
+ * 883-903`) or the P1 Laplacian (FEM_KIND_POISSON, bs = 1, kappa = E) formed element by element from the vertex
+ * coordinates in every application -- the reference's element-by-element product `compute_nodal_forces`
+ * (`solver/element.py:429-464`) without K_e in memory. Elements in Morton order, cut into chunks of <= 512 elements /
+ * <= 256 nodes; per chunk a fixed-order sum per local node into a slot, per node a fixed-order sum of its slots
+ * (deterministic). coords [N,3] and conn [M,4] (int64) must stay alive and unchanged while the operator is used.
+ * FEM_ESINGULAR (*bad_idx = smallest element with |det| < 1e-12, `solver/element.py:857-858`), FEM_EARG for a node
+ * outside [0, N). */
+typedef struct fem_mf fem_mf;
+int fem_mf_create(const double* coords, const int64_t* conn, int64_t M, int64_t N, int kind, double E, double nu,
+                  int64_t* bad_idx, fem_stream_t stream, fem_mf** out);
+int fem_mf_destroy(fem_mf* m);
+/* y = K x ([N*bs] each; y overwritten) */
+int fem_mf_apply(fem_mf* m, const double* x, double* y, fem_stream_t stream);
+/* d = diag(K) [N*bs] (the exact diagonal) */
+int fem_mf_diag(fem_mf* m, double* d, fem_stream_t stream);
+/* out6 = {chunks, slots, bs, static bytes streamed per application, M, N} */
+int fem_mf_info(fem_mf* m, int64_t* out6);
+/* device copies of the layout (each nullable): Morton element order [M], chunk element offsets and slot offsets
+ * [chunks + 1], slot nodes [slots] */
+int fem_mf_order(fem_mf* m, int32_t* eorder, int32_t* cptr, int32_t* sbase, int32_t* cnode, fem_stream_t stream);
+/* the context's operator becomes m (nrows = N, bs = m's; create the context with NULL slice_ptr / cols / vals):
+ * K1 = the chunk kernel with the p.q reduction + the slot gather, then the merged update; single GPU, modes PCG and
+ * CG_STABLE, schedule 0 */
+int fem_pcg_set_operator_mf(fem_pcg* s, fem_mf* m);
+
 #ifdef __cplusplus
 }
 #endif

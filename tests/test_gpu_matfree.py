@@ -1,0 +1,195 @@
+"""GPU tier of the element-chunk (matrix-free) c3d4 operator (`csrc/matfree.hip`, `system.MatFreeOperator`): the
+reference's element-by-element product `compute_nodal_forces` (`solver/element.py:429-464`) of the c3d4 stiffness
+(`compute_c3d4_K_matrix`, `:883-903`) and of the P1 Laplacian, formed from the coordinates in every application.
+
+Checked against the oracle's EBE product over its element matrices (`oracle/ref_cpu.py` nodal_forces / tet4_K /
+tet4_poisson_K) at 1e-12, against the assembled SELL operator, for the exact diagonal, bit-determinism, chunk
+splitting (a mesh whose 512-element chunks touch more than 256 nodes), a fan around a hub node, random numbering,
+errors, the (P)CG on it against the oracle PCG (`solver/solver.py:766-812`), and at the configs[2] size (10M tets)."""
+import pytest
+import torch
+
+from conftest import rel
+from oracle import ref_cpu as R
+
+pytestmark = pytest.mark.gpu
+E, NU = 113.8e9, 0.342
+F64 = torch.float64
+
+
+def _mods():
+    import fem355  # noqa: F401
+    from fem355 import mesh, solver, system
+    return mesh, solver, system
+
+
+def _disjoint_tets(m, seed=3):
+    """m tets with 4 private nodes each (every 512-element chunk touches 2,048 nodes: the 64-element split)."""
+    g = torch.Generator().manual_seed(seed)
+    base = torch.rand(m, 1, 3, generator=g, dtype=F64) * 10.0
+    ref = torch.tensor([[0, 0, 0], [1, 0, 0], [0, 1, 0], [0, 0, 1]], dtype=F64)
+    c = (base + ref + 0.1 * torch.rand(m, 4, 3, generator=g, dtype=F64)).reshape(-1, 3)
+    t = torch.arange(4 * m, dtype=torch.int64).reshape(m, 4)
+    return c, t
+
+
+def _fan(k):
+    """k tets around the hub node 0 (a node in every element: one row touching k + 2 nodes)."""
+    ang = torch.arange(k + 1, dtype=F64) * (2 * torch.pi / k)
+    ring = torch.stack([torch.cos(ang), torch.sin(ang), torch.zeros_like(ang)], 1)
+    c = torch.cat([torch.tensor([[0.0, 0.0, 1.0], [0.0, 0.0, -1.0]], dtype=F64), ring[:-1]], 0)
+    i = torch.arange(k)
+    t = torch.stack([torch.zeros(k, dtype=torch.int64), torch.ones(k, dtype=torch.int64), 2 + i, 2 + (i + 1) % k], 1)
+    return c, t
+
+
+def _meshes():
+    mesh, _, _ = _mods()
+    out = {}
+    out["kuhn6"] = mesh.kuhn_cube(6, jitter=0.15)
+    out["kuhn14"] = mesh.kuhn_cube(14, jitter=0.1)
+    c, t = mesh.kuhn_cube(10, jitter=0.1)
+    g = torch.Generator().manual_seed(5)
+    perm = torch.randperm(c.shape[0], generator=g)
+    inv = torch.empty_like(perm)
+    inv[perm] = torch.arange(perm.numel())
+    out["permuted"] = (c[perm], inv[t][torch.randperm(t.shape[0], generator=g)])
+    out["disjoint"] = _disjoint_tets(1100)
+    out["fan"] = _fan(700)
+    return out
+
+
+@pytest.mark.parametrize("name", ["kuhn6", "kuhn14", "permuted", "disjoint", "fan"])
+@pytest.mark.parametrize("kind", ["elastic", "poisson"])
+def test_operator_vs_oracle_ebe(gpu, name, kind):
+    _, _, system = _mods()
+    c, t = _meshes()[name]
+    N, dpn = c.shape[0], 3 if kind == "elastic" else 1
+    Ek = E if kind == "elastic" else 2.5
+    A = system.MatFreeOperator(c.to(gpu), t.to(gpu), kind, Ek, NU)
+    K = R.tet4_K(c, t, E, NU) if kind == "elastic" else R.tet4_poisson_K(c, t, kappa=Ek)
+    x = torch.randn(N, dpn, dtype=F64, generator=torch.Generator().manual_seed(1))
+    y = A.matvec(x.reshape(-1).to(gpu))
+    y_ref = R.nodal_forces(K, t, x).reshape(-1)
+    assert rel(y, y_ref) < 1e-12
+    # bit-deterministic: a second application gives the same bits
+    assert torch.equal(A.matvec(x.reshape(-1).to(gpu)), y)
+    # exact diagonal against the oracle's element matrices (the true diagonal, not the Q1 column-0 quirk)
+    d_ref = torch.zeros(N * dpn, dtype=F64)
+    dm = R.dof_map(t, dpn)
+    d_ref.index_add_(0, dm.reshape(-1), torch.diagonal(K, dim1=1, dim2=2).reshape(-1))
+    assert rel(A.diag(), d_ref) < 1e-13
+    info = A.info()
+    assert info["elements"] == t.shape[0] and info["nodes"] == N
+    if name == "disjoint":   # 512-element chunks touch 2,048 nodes: cut into pieces of 64 elements (256 nodes)
+        assert info["chunks"] == (t.shape[0] + 63) // 64
+        assert info["slots"] == 4 * t.shape[0]
+
+
+def test_layout_invariants(gpu):
+    """Morton order is a permutation; every chunk holds <= 512 elements and <= 256 nodes; slot nodes ascend inside a
+    chunk and each (chunk, node) pair appears once; every node of an element is a slot of the element's chunk."""
+    mesh, _, system = _mods()
+    c, t = mesh.kuhn_cube(12, jitter=0.1)
+    A = system.MatFreeOperator(c.to(gpu), t.to(gpu), "elastic", E, NU)
+    eo, cp, sb, cn = (v.cpu().long() for v in A.layout())
+    assert torch.equal(eo.sort().values, torch.arange(t.shape[0]))
+    assert int((cp[1:] - cp[:-1]).max()) <= 512 and int((sb[1:] - sb[:-1]).max()) <= 256
+    for ch in range(cp.numel() - 1):
+        nodes = cn[sb[ch]:sb[ch + 1]]
+        assert torch.all(nodes[1:] > nodes[:-1])
+        want = torch.unique(t[eo[cp[ch]:cp[ch + 1]]].reshape(-1))
+        assert torch.equal(nodes, want)
+
+
+def test_errors_and_empty(gpu):
+    mesh, _, system = _mods()
+    c, t = mesh.kuhn_cube(3)
+    bad = t.clone()
+    bad[5, 2] = bad[5, 1]          # a repeated node: zero volume
+    with pytest.raises(ValueError, match="Singular matrix"):
+        system.MatFreeOperator(c.to(gpu), bad.to(gpu), "elastic", E, NU)
+    oob = t.clone()
+    oob[7, 0] = c.shape[0]
+    with pytest.raises(Exception, match="outside"):
+        system.MatFreeOperator(c.to(gpu), oob.to(gpu), "elastic", E, NU)
+    A = system.MatFreeOperator(c.to(gpu), t[:0].to(gpu), "elastic", E, NU)
+    y = A.matvec(torch.ones(c.shape[0] * 3, dtype=F64, device=gpu))
+    assert float(y.abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("kind", ["elastic", "poisson"])
+def test_pcg_vs_oracle_and_assembled(gpu, kind):
+    """Jacobi-PCG to rtol 1e-8 on the matrix-free operator: u within 1e-10 of the oracle PCG over the reference's
+    element matrices, iterations within +-2; the first 20 iterates match the assembled operator's
+    3-kernel schedule at 1e-10."""
+    mesh, solver, system = _mods()
+    c, t = mesh.kuhn_cube(8, jitter=0.12)
+    N = c.shape[0]
+    dpn = 3 if kind == "elastic" else 1
+    f, fixed = mesh.cube_elasticity_case(c) if kind == "elastic" else mesh.cube_poisson_case(c)
+    u, res, A = solver.solve_tet4(c, t, f, fixed, kind=kind, E=E if kind == "elastic" else 1.0, nu=NU,
+                                  rtol=1e-8, device=gpu, operator="matfree")
+    assert getattr(A, "is_matfree", False)
+    K = R.tet4_K(c, t, E, NU) if kind == "elastic" else R.tet4_poisson_K(c, t)
+    dinv = R.diag_preconditioner(K, t, N, dpn=dpn)
+    dinv[fixed] = 0.0
+    b = f.reshape(N, dpn).to(F64)
+    tol = 1e-8 * float(torch.sqrt((b * dinv * b).sum()))
+    u_ref, it_ref, _ = R.pcg(K, t, b, dinv, tol=tol, max_iter=5000)
+    assert abs(res.iterations - it_ref) <= 2
+    assert rel(u.cpu().reshape(N, dpn), u_ref) < 1e-9
+    # fixed iterations against the assembled operator's schedule
+    As = system.assemble_tet4_system(c.to(gpu), t.to(gpu), kind, E if kind == "elastic" else 1.0, NU)
+    mask = torch.zeros((N, dpn), dtype=torch.uint8, device=gpu)
+    mask[fixed.to(gpu)] = 1
+    w = As.jacobi(mask.view(-1))
+    w_mf = A.jacobi(mask.view(-1))
+    assert rel(w_mf, w) < 1e-14
+    r1 = As.pcg(b.reshape(-1), w=w, tol=0.0, max_iter=20, schedule=0)
+    r2 = A.pcg(b.reshape(-1), w=w, tol=0.0, max_iter=20)
+    assert r1.iterations == r2.iterations == 20
+    assert rel(r2.x, r1.x) < 1e-10
+
+
+def test_runner_chunks_bit_identical(gpu):
+    """The bench's fixed-iteration runner on the matrix-free operator: 3 + 4 iterations in two launches give the same
+    bits as 7 in one (device state carried between launches)."""
+    mesh, _, system = _mods()
+    c, t = mesh.kuhn_cube(9, jitter=0.1)
+    f, fixed = mesh.cube_elasticity_case(c)
+    A = system.MatFreeOperator(c.to(gpu), t.to(gpu), "elastic", E, NU)
+    mask = torch.zeros((c.shape[0], 3), dtype=torch.uint8, device=gpu)
+    mask[fixed.to(gpu)] = 1
+    w = A.jacobi(mask.view(-1))
+    xs = []
+    for steps in ((7,), (3, 4)):
+        run = system.PcgRunner(A, f.reshape(-1), w, tol=0.0)
+        try:
+            run.start()
+            for k in steps:
+                run.iterate(k)
+            assert run.poll()[0] == 7
+            xs.append(run.x.clone())
+        finally:
+            run.close()
+    assert torch.equal(xs[0], xs[1])
+
+
+def test_config2_matfree_10m_operator_and_iterates_vs_oracle(gpu, cube119):
+    """BASELINE configs[2] (10,110,954 tets, 5,184,000 DOFs) on the matrix-free operator: the operator on a seeded
+    vector against the oracle's EBE product over its element matrices at 1e-12, the exact Jacobi weights at 1e-14,
+    and the first 5 Jacobi-PCG iterates against the oracle PCG at 1e-10."""
+    _, _, system = _mods()
+    c, t, N = cube119.c, cube119.t, cube119.N
+    f, fixed, dinv = cube119.case("elastic")
+    A = system.MatFreeOperator(c.to(gpu), t.to(gpu), "elastic", E, NU)
+    p, y_ref = cube119.matvec_ref("elastic", 11)
+    assert rel(A.matvec(p.reshape(-1).to(gpu)), y_ref.reshape(-1)) < 1e-12
+    mask = torch.zeros((N, 3), dtype=torch.uint8, device=gpu)
+    mask[fixed.to(gpu)] = 1
+    w = A.jacobi(mask.view(-1))
+    assert rel(w, dinv.reshape(-1)) < 1e-14
+    res = A.pcg(f.reshape(-1), w=w, tol=0.0, max_iter=5)
+    assert res.iterations == 5
+    assert rel(res.x, cube119.pcg_ref("elastic", 5).reshape(-1)) < 1e-10
