@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--elastic", type=int, default=1,
                     help="poisson runs: also measure the 10M-tet linear-elasticity system (BASELINE configs[2]/[3]) "
                          "with the same steps, reported under \"elasticity\" in the same JSON line")
+    ap.add_argument("--matfree", type=int, default=1,
+                    help="elasticity companion: also the element-chunk (matrix-free) operator, under \"matfree\"")
     ap.add_argument("--elastic-timeout", type=float, default=240.0,
                     help="seconds the elasticity companion may take before the line is printed without it")
     ap.add_argument("--cpu-iters-elastic", type=int, default=10, help="CPU-baseline PCG iterations (elasticity)")
@@ -239,6 +241,11 @@ def main():
 
         def companion():
             d = measure(a, "elastic", coords, tets, dev)
+            if a.matfree:
+                try:
+                    d["matfree"] = measure_matfree(a, coords, tets, dev, d)
+                except Exception as e:   # reported, never fatal to the line
+                    d["matfree"] = {"error": f"{type(e).__name__}: {e}"}
             if not a.no_cpu_baseline:
                 attach_cpu_baseline(d, cpu_baseline(a.n, "elastic", a.cpu_iters_elastic, d["solve_iters"]))
             return d
@@ -256,6 +263,79 @@ def permute_nodes(coords, tets, seed):
     inv = torch.empty_like(perm)
     inv[perm] = torch.arange(perm.numel(), device=coords.device)
     return coords[perm].contiguous(), inv[tets].contiguous()
+
+
+MF_FLOPS_PER_ELEMENT = 197   # csrc/matfree.hpp mf_element (elastic, FMA = 2) + the 12 node-sum adds
+FP64_PEAK_TFLOPS = 78.6       # MI355X_MICROARCH.md: fp64 vector
+
+
+def measure_matfree(a, coords, tets, dev, ref):
+    """The 10M elasticity system on the element-chunk operator (system.MatFreeOperator: K p formed from the
+    coordinates in every iteration, no matrix): DOFs/s (operator build + Jacobi + solve to rtol, median of the passes
+    after a cold one), the fixed-iteration CG it/s with its kernel split, and the solve's agreement with the assembled
+    operator's (`ref`, measure()'s elasticity dict: iterations +-2)."""
+    M, N = tets.shape[0], coords.shape[0]
+    f, fixed = mesh.cube_elasticity_case(coords)
+    E, nu = 113.8e9, 0.342
+
+    def build_and_solve():
+        t0 = time.perf_counter()
+        A = system.MatFreeOperator(coords, tets, "elastic", E, nu)
+        mask = torch.zeros((N, 3), dtype=torch.uint8, device=dev)
+        mask[fixed] = 1
+        w = A.jacobi(mask.view(-1))
+        sync()
+        t_b = time.perf_counter() - t0
+        b = f.reshape(-1).to(torch.float64).contiguous()
+        tol = a.rtol * float(torch.sqrt(torch.dot(b, w * b)))
+        sync()
+        t0 = time.perf_counter()
+        res = A.pcg(b, None, w=w, mode=C.MODE_PCG, tol=tol, max_iter=20000, chunk=64)
+        sync()
+        return A, w, b, res, t_b, time.perf_counter() - t0
+
+    A, w, b, res, tb_cold, ts_cold = build_and_solve()
+    passes = []
+    for _ in range(max(a.dof_passes, 1)):
+        del A, w, b, res
+        A, w, b, res, t_b, t_s = build_and_solve()
+        passes.append((t_b, t_s))
+    t_b, t_s = sorted(passes, key=lambda p: p[0] + p[1])[len(passes) // 2]
+    assert abs(res.iterations - ref["solve_iters"]) <= 2, (res.iterations, ref["solve_iters"])
+    run = system.PcgRunner(A, b, w, tol=0.0)
+    run.start()
+    run.iterate(a.warmup)
+    sync()
+    t0 = time.perf_counter()
+    ms, cnt = run.profile(a.steps, every=a.sample_every)
+    sync()
+    dt = time.perf_counter() - t0
+    it, _, _ = run.poll()
+    assert it == a.warmup + a.steps
+    run.close()
+    info = A.info()
+    k1 = ms[0] / max(cnt[0], 1)
+    upd = ms[1] / max(cnt[1], 1)
+    flops = MF_FLOPS_PER_ELEMENT * M
+    # HBM bytes one K1 must move: the static layout (element local ids, pair lists, chunk tables), the coordinates and
+    # p once, the slot values written; the merged update reads them back with the node -> slot lists
+    alg = info["static_bytes"] - 4 * (N + 1) - 4 * info["slots"] + 24 * N + 24 * N + 24 * info["slots"]
+    return {
+        "value": a.steps / dt, "unit": "CG iterations/s", "ms_per_step": dt / a.steps * 1e3,
+        "vs_assembled": (a.steps / dt) / ref["value"],
+        "kernel_ms": {"k_pcg_mf_dot": k1, "update_with_slot_sums": upd, "sampled_launches": cnt[0]},
+        "dofs_per_s": 3 * N / (t_b + t_s), "build_ms": t_b * 1e3, "solve_ms": t_s * 1e3,
+        "dofs_per_s_cold": 3 * N / (tb_cold + ts_cold), "solve_iters": res.iterations,
+        "solve_iters_assembled": ref["solve_iters"], "layout": info,
+        "roofline": {"bound": "fp64 VALU issue / latency", "kernel": "k_pcg_mf_dot<3>",
+                     "flops_per_launch": flops, "achieved_TFLOPs": flops / (k1 * 1e-3) / 1e12,
+                     "peak_TFLOPs": FP64_PEAK_TFLOPS, "frac_flops": flops / (k1 * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                     "algorithmic_bytes": alg, "achieved_GBps": alg / (k1 * 1e-3) / 1e9,
+                     "frac_hbm": alg / (k1 * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                     "model": f"{MF_FLOPS_PER_ELEMENT} flops per element; bytes: layout + coordinates + p + slots"},
+        "operator": "element-chunk (matrix-free): Morton-ordered chunks of <= 512 elements / 256 nodes, "
+                    "fixed-order slot sums (csrc/matfree.hip)",
+    }
 
 
 def measure(a, kind, coords, tets, dev):

@@ -25,6 +25,7 @@ MODE_CG_STABLE, MODE_PCG, MODE_CG_CONSTRAINED = 0, 1, 2
 # include/fem355.h FEM_TUNE_*: the library's default set for a new context, and the merged-update flag
 TUNE_UPD1 = 1024
 TUNE_U2_HOLD, TUNE_U2_SMALL = 2048, 4096   # test-only knobs of the merged update (include/fem355.h)
+TUNE_MF_GATHER = 8192   # element-chunk operator: q summed by a gather launch instead of inside the merged update
 TUNE_DEFAULT = 1 | 2 | 4 | 8 | 128 | TUNE_UPD1
 KIND_ELASTIC, KIND_POISSON, KIND_MASS = 0, 1, 2
 ISO_SUM, ISO_STACK, ISO_VOLUME, ISO_MASS = 0, 1, 2, 3

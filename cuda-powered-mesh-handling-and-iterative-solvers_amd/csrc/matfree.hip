@@ -266,7 +266,7 @@ __global__ void k_mf_nptr(const int32_t* __restrict__ skey, int64_t nslots, int6
 template <int BS, int MODE>
 __global__ void __launch_bounds__(MF_BLOCK) k_mf_apply(MfOp op, const double* __restrict__ x,
                                                        double* __restrict__ slots) {
-    __shared__ MfLds<BS> L;
+    __shared__ MfLds<BS, mf_fc<MODE>()> L;
     (void)mf_walk<BS, MODE>(op, x, slots, L);
 }
 

@@ -14,14 +14,30 @@
 #include "common.hpp"
 #include "element.hpp"
 
+#include <stdlib.h>
+
 namespace fem {
 
 constexpr int MF_EC = 512;      // elements per chunk (at most)
 constexpr int MF_NC = 256;      // local nodes per chunk (at most; local ids are bytes)
 constexpr int MF_PASS = 256;    // elements formed per pass (= threads of the workgroup)
 constexpr int MF_BLOCK = 256;
+#ifndef FEM_MF_UNROLL
+#define FEM_MF_UNROLL 4
+#endif
+constexpr int MF_U = FEM_MF_UNROLL;   // pairs whose LDS reads are issued together in the node sums
+// FEM_MF_F0 = 1: corner 0's element vector not staged, f_0 = -(f_1 + f_2 + f_3) (mf_element's own formula) re-formed by
+// the node sums that need it -- 3 of 4 vectors in LDS, 4 instead of 3 workgroups per CU for bs = 3; measured slower
+// (10M elastic chunk kernel 326 vs 231 us: the corner-0 branch diverges inside every wave's node sums), off
+#ifndef FEM_MF_F0
+#define FEM_MF_F0 0
+#endif
 
 enum { MF_APPLY = 0, MF_DOT = 1, MF_DIAG = 2 };
+
+// staged corners of a mode (the diagonal's corner-0 values are not -(f_1 + f_2 + f_3))
+template <int MODE>
+constexpr int mf_fc() { return (FEM_MF_F0 && MODE != MF_DIAG) ? 3 : 4; }
 
 // device view of the operator
 struct MfOp {
@@ -46,69 +62,120 @@ int mf_bs(const fem_mf* m);
 int64_t mf_nodes(const fem_mf* m);
 int mf_apply(fem_mf* m, const double* x, double* y, hipStream_t st);
 
-// element vectors of one element: f[a][c] for the 4 corners (BS = 3: c = 0..2; BS = 1: c = 0). DIAG: the diagonal of
-// the corner's own block (K_aa)_cc instead of (K_e x)_a.
+// 1 / x to full precision without the IEEE division sequence: v_rcp_f64 and two Newton steps (within an ulp)
+__device__ __forceinline__ double mf_rcp(double x) {
+    double y = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, y, 1.0);
+    y = fma(y, e, y);
+    e = fma(-x, y, 1.0);
+    return fma(y, e, y);
+}
+
+// Element vectors of one element: f[a][c] for the 4 corners (BS = 3: c = 0..2; BS = 1: c = 0). DIAG: the diagonal of
+// the corner's own block (K_aa)_cc instead of (K_e x)_a. In cofactor form: with the edge vectors e_b = x_b - x_0 and
+// their cofactors c_1 = e_2 x e_3, c_2 = e_3 x e_1, c_3 = e_1 x e_2, c_0 = -(c_1 + c_2 + c_3), the gradients are
+// g_b = c_b / det and V = |det| / 6, so V g_a g_b^T = c_a c_b^T / (6 |det|): every product is formed from the
+// unscaled cofactors and scaled once by s = 1 / (6 |det|).
 template <int BS, int MODE>
 __device__ __forceinline__ void mf_element(const double xc[4][3], const double xv[4][BS], double lam, double mu,
                                            double kappa, double f[4][BS]) {
-    double g[4][3];
-    const double det = tet4_grads_p(xc, g);
-    const double V = fabs(det) / 6.0;
+    double e[3][3], c[4][3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        e[0][k] = xc[1][k] - xc[0][k];
+        e[1][k] = xc[2][k] - xc[0][k];
+        e[2][k] = xc[3][k] - xc[0][k];
+    }
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {   // c_{b+1} = e_{b+1} x e_{b+2} (indices mod 3)
+        const double* u = e[(b + 1) % 3];
+        const double* v = e[(b + 2) % 3];
+        c[b + 1][0] = u[1] * v[2] - u[2] * v[1];
+        c[b + 1][1] = u[2] * v[0] - u[0] * v[2];
+        c[b + 1][2] = u[0] * v[1] - u[1] * v[0];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) c[0][k] = -(c[1][k] + c[2][k] + c[3][k]);
+    const double det = e[0][0] * c[1][0] + e[0][1] * c[1][1] + e[0][2] * c[1][2];
+    const double sc = mf_rcp(6.0 * fabs(det));
     if constexpr (MODE == MF_DIAG) {
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
-            const double gg = g[a][0] * g[a][0] + g[a][1] * g[a][1] + g[a][2] * g[a][2];
+            const double cc = c[a][0] * c[a][0] + c[a][1] * c[a][1] + c[a][2] * c[a][2];
             if constexpr (BS == 1) {
-                f[a][0] = kappa * gg * V;
+                f[a][0] = kappa * cc * sc;
             } else {
 #pragma unroll
-                for (int c = 0; c < 3; ++c) f[a][c] = V * ((lam + mu) * (g[a][c] * g[a][c]) + mu * gg);
+                for (int q = 0; q < 3; ++q) f[a][q] = sc * ((lam + mu) * (c[a][q] * c[a][q]) + mu * cc);
             }
         }
         return;
     }
     if constexpr (BS == 1) {
-        double gu[3];
+        double gu[3];   // det x the gradient of x
 #pragma unroll
-        for (int k = 0; k < 3; ++k)
-            gu[k] = g[0][k] * xv[0][0] + g[1][k] * xv[1][0] + g[2][k] * xv[2][0] + g[3][k] * xv[3][0];
-        const double s = kappa * V;
+        for (int k = 0; k < 3; ++k) {
+            const double d1 = xv[1][0] - xv[0][0], d2 = xv[2][0] - xv[0][0], d3 = xv[3][0] - xv[0][0];
+            gu[k] = c[1][k] * d1 + c[2][k] * d2 + c[3][k] * d3;
+        }
+        const double s = kappa * sc;
 #pragma unroll
-        for (int a = 0; a < 4; ++a) f[a][0] = s * (g[a][0] * gu[0] + g[a][1] * gu[1] + g[a][2] * gu[2]);
+        for (int a = 1; a < 4; ++a) f[a][0] = s * (c[a][0] * gu[0] + c[a][1] * gu[1] + c[a][2] * gu[2]);
+        f[0][0] = -(f[1][0] + f[2][0] + f[3][0]);
     } else {
-        // H[i][j] = sum_b x_b[i] g_b[j]
+        // H[i][j] = sum_b (x_b - x_0)[i] c_b[j]   (det x the displacement gradient)
+        double d[3][3];
+#pragma unroll
+        for (int b = 0; b < 3; ++b)
+#pragma unroll
+            for (int i = 0; i < 3; ++i) d[b][i] = xv[b + 1][i] - xv[0][i];
         double H[3][3];
 #pragma unroll
         for (int i = 0; i < 3; ++i)
 #pragma unroll
-            for (int j = 0; j < 3; ++j)
-                H[i][j] = xv[0][i] * g[0][j] + xv[1][i] * g[1][j] + xv[2][i] * g[2][j] + xv[3][i] * g[3][j];
-        const double tr = H[0][0] + H[1][1] + H[2][2];
-        const double lt = lam * tr;
-        // V sigma (symmetric)
-        const double s00 = V * (lt + 2.0 * mu * H[0][0]);
-        const double s11 = V * (lt + 2.0 * mu * H[1][1]);
-        const double s22 = V * (lt + 2.0 * mu * H[2][2]);
-        const double s01 = V * (mu * (H[0][1] + H[1][0]));
-        const double s02 = V * (mu * (H[0][2] + H[2][0]));
-        const double s12 = V * (mu * (H[1][2] + H[2][1]));
+            for (int j = 0; j < 3; ++j) H[i][j] = d[0][i] * c[1][j] + d[1][i] * c[2][j] + d[2][i] * c[3][j];
+        const double lt = lam * (H[0][0] + H[1][1] + H[2][2]);
+        const double m2 = 2.0 * mu;
+        // s sigma(H), symmetric
+        const double s00 = sc * (lt + m2 * H[0][0]);
+        const double s11 = sc * (lt + m2 * H[1][1]);
+        const double s22 = sc * (lt + m2 * H[2][2]);
+        const double s01 = sc * (mu * (H[0][1] + H[1][0]));
+        const double s02 = sc * (mu * (H[0][2] + H[2][0]));
+        const double s12 = sc * (mu * (H[1][2] + H[2][1]));
 #pragma unroll
-        for (int a = 0; a < 4; ++a) {
-            f[a][0] = s00 * g[a][0] + s01 * g[a][1] + s02 * g[a][2];
-            f[a][1] = s01 * g[a][0] + s11 * g[a][1] + s12 * g[a][2];
-            f[a][2] = s02 * g[a][0] + s12 * g[a][1] + s22 * g[a][2];
+        for (int a = 1; a < 4; ++a) {
+            f[a][0] = s00 * c[a][0] + s01 * c[a][1] + s02 * c[a][2];
+            f[a][1] = s01 * c[a][0] + s11 * c[a][1] + s12 * c[a][2];
+            f[a][2] = s02 * c[a][0] + s12 * c[a][1] + s22 * c[a][2];
         }
+#pragma unroll
+        for (int q = 0; q < 3; ++q) f[0][q] = -(f[1][q] + f[2][q] + f[3][q]);
     }
 }
 
 // LDS of one chunk application
-template <int BS>
+template <int BS, int FC>
 struct MfLds {
     double nd[MF_NC][3 + BS];        // per local node: coordinates, then x (rows 16-byte aligned: 48 / 32 bytes)
-    double fs[4 * BS][MF_PASS + 1];  // element vectors of the current pass: [corner * BS + c][element]
+    double fs[FC * BS][MF_PASS + 1];   // element vectors of the current pass: [staged corner * BS + c][element]
     uint16_t lp[MF_NC + 1];          // pair pointers of the local nodes
     alignas(16) uint16_t ent[4 * MF_EC];   // the chunk's pairs, node-major
 };
+
+// the element vector of pair pe (element << 2 | corner) of the pass starting at element h
+template <int BS, int FC>
+__device__ __forceinline__ void mf_pair_value(const MfLds<BS, FC>& L, int pe, int h, double v[BS]) {
+    const int el = (pe >> 2) - h, b = pe & 3;
+    if (FC == 3 && b == 0) {
+#pragma unroll
+        for (int q = 0; q < BS; ++q) v[q] = -(L.fs[q][el] + L.fs[BS + q][el] + L.fs[2 * BS + q][el]);
+    } else {
+        const int row = (b - (4 - FC)) * BS;
+#pragma unroll
+        for (int q = 0; q < BS; ++q) v[q] = L.fs[row + q][el];
+    }
+}
 
 // What a thread loads for one chunk ahead of its use (software pipeline over a workgroup's chunks): the chunk's
 // ranges, this thread's local node (id, coordinates, x), pair pointer, 8 pairs and the local ids of its 2 elements.
@@ -160,7 +227,8 @@ __device__ __forceinline__ void mf_pf2(const MfOp& op, const double* __restrict_
 // sum_l x_l . slot_l over its chunks (0 elsewhere). x unused for MF_DIAG.
 template <int BS, int MODE>
 __device__ __forceinline__ double mf_walk(const MfOp& op, const double* __restrict__ x, double* __restrict__ slots,
-                                          MfLds<BS>& L) {
+                                          MfLds<BS, mf_fc<MODE>()>& L) {
+    constexpr int FC = mf_fc<MODE>();
     const int tid = threadIdx.x;
     const int64_t per = (op.nchunks + NXCD - 1) / NXCD;
     const int64_t base = (int64_t)(blockIdx.x % NXCD) * per;
@@ -168,11 +236,15 @@ __device__ __forceinline__ double mf_walk(const MfOp& op, const double* __restri
     int64_t k = blockIdx.x / NXCD;
     double dot = 0.0;
     if (k >= per || base + k >= op.nchunks) return dot;
-    MfPf<BS> cur, nxt;
+    // three chunks in flight: cur (installed in LDS now), n1 (its node gathers issued at the top of this chunk,
+    // needed at the next install), n2 (its ids / pairs / local ids issued now, its gathers at the next chunk's top):
+    // every load has a whole chunk of work to arrive (~1-2 us of HBM latency under load)
+    MfPf<BS> cur, n1, n2;
     mf_pf1<BS>(op, base + k, cur);
+    bool has1 = k + nb < per && base + k + nb < op.nchunks;
+    if (has1) mf_pf1<BS>(op, base + k + nb, n1);
     mf_pf2<BS, MODE>(op, x, cur);
     for (;;) {
-        const int64_t c = base + k;
         __syncthreads();   // the previous chunk's LDS reads are done
         if (tid < cur.nn) {
 #pragma unroll
@@ -183,9 +255,10 @@ __device__ __forceinline__ double mf_walk(const MfOp& op, const double* __restri
         }
         if (tid == 0) L.lp[cur.nn] = (uint16_t)(4 * cur.ne);
         if (8 * tid < 4 * cur.ne) reinterpret_cast<uint4*>(L.ent)[tid] = cur.ent;
-        const int64_t kn = k + nb;
-        const bool more = kn < per && base + kn < op.nchunks;
-        if (more) mf_pf1<BS>(op, base + kn, nxt);
+        const int64_t k2 = k + 2 * nb;
+        const bool has2 = has1 && k2 < per && base + k2 < op.nchunks;
+        if (has1) mf_pf2<BS, MODE>(op, x, n1);
+        if (has2) mf_pf1<BS>(op, base + k2, n2);
         __syncthreads();
         double acc[BS];
 #pragma unroll
@@ -233,36 +306,31 @@ __device__ __forceinline__ double mf_walk(const MfOp& op, const double* __restri
                 }
                 mf_element<BS, MODE>(xc, xv, op.lam, op.mu, op.kappa, f);
 #pragma unroll
-                for (int b = 0; b < 4; ++b)
+                for (int b = 4 - FC; b < 4; ++b)
 #pragma unroll
-                    for (int q = 0; q < BS; ++q) L.fs[b * BS + q][tid] = f[b][q];
+                    for (int q = 0; q < BS; ++q) L.fs[(b - (4 - FC)) * BS + q][tid] = f[b][q];
             }
-            if (j == 0 && more) mf_pf2<BS, MODE>(op, x, nxt);   // the next chunk's gathers, under this chunk's work
             __syncthreads();
             // every local node adds its pairs of this pass in ascending (element, corner) order; the pair reads of
             // four steps are issued before their adds (independent LDS loads, one latency per four pairs)
             const int stop = j == 0 ? mid : end;
-            for (; pos + 4 <= stop; pos += 4) {
-                int pe[4];
+            for (; pos + MF_U <= stop; pos += MF_U) {
+                int pe[MF_U];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) pe[u] = L.ent[pos + u];
-                double v[4][BS];
+                for (int u = 0; u < MF_U; ++u) pe[u] = L.ent[pos + u];
+                double v[MF_U][BS];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int el = (pe[u] >> 2) - h, b = pe[u] & 3;
+                for (int u = 0; u < MF_U; ++u) mf_pair_value<BS, FC>(L, pe[u], h, v[u]);
 #pragma unroll
-                    for (int q = 0; q < BS; ++q) v[u][q] = L.fs[b * BS + q][el];
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
+                for (int u = 0; u < MF_U; ++u)
 #pragma unroll
                     for (int q = 0; q < BS; ++q) acc[q] += v[u][q];
             }
             for (; pos < stop; ++pos) {
-                const int pe = L.ent[pos];
-                const int el = (pe >> 2) - h, b = pe & 3;
+                double v[BS];
+                mf_pair_value<BS, FC>(L, L.ent[pos], h, v);
 #pragma unroll
-                for (int q = 0; q < BS; ++q) acc[q] += L.fs[b * BS + q][el];
+                for (int q = 0; q < BS; ++q) acc[q] += v[q];
             }
             __syncthreads();
         }
@@ -273,9 +341,11 @@ __device__ __forceinline__ double mf_walk(const MfOp& op, const double* __restri
                 if constexpr (MODE == MF_DOT) dot += cur.pv[q] * acc[q];
             }
         }
-        if (!more) break;
-        k = kn;
-        cur = nxt;
+        if (!has1) break;
+        k += nb;
+        cur = n1;
+        n1 = n2;
+        has1 = has2;
     }
     return dot;
 }
@@ -301,7 +371,12 @@ inline int mf_resident_grid(const void* fn, int block, int64_t nchunks) {
                 break;
             }
     }
-    int64_t g = per_cu;
+    static const int mult = [] {
+        const char* e = getenv("FEM355_MF_GRID_MULT");   // A/B: workgroups per resident slot
+        const int m = e ? atoi(e) : 1;
+        return m < 1 ? 1 : m;
+    }();
+    int64_t g = (int64_t)per_cu * mult;
     const int64_t want = ((nchunks + NXCD - 1) / NXCD) * NXCD;
     if (want < g) g = want;
     return (int)(g < NXCD ? NXCD : g);

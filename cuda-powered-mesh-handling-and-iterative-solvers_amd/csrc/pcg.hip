@@ -488,6 +488,82 @@ __device__ __forceinline__ void u2_give_up(PcgState* st, unsigned e) {
     __hip_atomic_store(&st->halt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The merged update's hand-off (every form of it): the block sums of r.z, the grid reduction, the last workgroup's
+// finish_rz and release, the others' bounded wait and read of the broadcast (beta, halt). false: the launch gave up
+// (no x / p update anywhere).
+__device__ __forceinline__ bool u2_release(double acc, PcgState* __restrict__ st, RedBuf red, double* __restrict__ hist,
+                                           int64_t hist_len, unsigned* __restrict__ sync, unsigned e, double* lds4,
+                                           int* flag_p, double* bc_s, double& beta, bool& upd_p, bool& last) {
+    int& flag = *flag_p;
+    acc = block_sum256(acc, lds4);
+    double rz_new;
+    last = reduce_grid(acc, red.part(RED_K2), red.cnt(RED_K2), &rz_new, lds4, &flag);
+    if (threadIdx.x == 0) {
+        // The release word decides the launch ONCE, by compare-and-swap from the previous epoch (e - 1): the last
+        // workgroup swaps in e (release), a waiter that gave up swaps in U2_GIVEUP. Whichever swap lands first
+        // wins, so either every workgroup applies the x / p update or none does (then r holds r_{k+1} and x x_k,
+        // the status is FEM_PCG_SYNC_TIMEOUT with the give-up site, and fem_pcg_solve re-solves from x0).
+        double beta_ = 0.0, halt = 0.0;
+        bool ok = true;
+        if (last) {
+            const int it0 = st->iter;
+            finish_rz(st, rz_new, hist, hist_len);
+            beta_ = st->beta;
+            halt = st->halt ? 1.0 : 0.0;
+            __hip_atomic_store(reinterpret_cast<double*>(sync + U2_BC), beta_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(reinterpret_cast<double*>(sync + U2_BC) + 1, halt, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            // the broadcast's write-through stores drained before the release (the guide's sc1 hand-off form; the
+            // asm's memory clobber also keeps the compiler from moving them past the swap)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            unsigned expect = e - 1;
+            if (!__hip_atomic_compare_exchange_strong(sync + U2_REL, &expect, e, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT)) {
+                // a waiter gave up first: undo the commit (the iteration did not complete) and keep its verdict
+                st->iter = it0;
+                u2_give_up(st, e);
+                ok = false;
+            }
+        } else {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            unsigned v = 0;
+            for (unsigned spins = 0;; ++spins) {
+                v = __hip_atomic_load(sync + U2_REL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (v != e - 1) break;   // released (e) or given up (U2_GIVEUP)
+                if ((spins & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > U2_WAIT_TICKS) {
+                    unsigned expect = e - 1;
+                    if (__hip_atomic_compare_exchange_strong(sync + U2_REL, &expect, U2_GIVEUP, __ATOMIC_RELAXED,
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                        v = U2_GIVEUP;   // a workgroup that never became resident: stop instead of hanging
+                    else
+                        v = expect;      // the release landed first
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            // no load below may be moved above the poll by the compiler (the hardware issues it only after the
+            // branch on the polled value); the broadcast is read with write-through (sc1) loads
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            if (v == e) {
+                beta_ = __hip_atomic_load(reinterpret_cast<const double*>(sync + U2_BC), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+                halt = __hip_atomic_load(reinterpret_cast<const double*>(sync + U2_BC) + 1, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                u2_give_up(st, e);
+                ok = false;
+            }
+        }
+        bc_s[0] = beta_;
+        bc_s[1] = ok ? halt : -1.0;
+    }
+    __syncthreads();
+    beta = bc_s[0];
+    if (bc_s[1] < 0.0) return false;
+    upd_p = bc_s[1] == 0.0;
+    return true;
+}
+
 __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update2(int64_t n, double* __restrict__ x, double* __restrict__ p,
                                                            double* __restrict__ r, const double* __restrict__ q,
                                                            const double* __restrict__ w, PcgState* __restrict__ st,
@@ -554,72 +630,9 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update2(int64_t n, double* __
         ztail = w[i] * rv;
         acc += rv * ztail;
     }
-    acc = block_sum256(acc, lds4);
-    double rz_new;
-    const bool last = reduce_grid(acc, red.part(RED_K2), red.cnt(RED_K2), &rz_new, lds4, &flag);
-    if (threadIdx.x == 0) {
-        // The release word decides the launch ONCE, by compare-and-swap from the previous epoch (e - 1): the last
-        // workgroup swaps in e (release), a waiter that gave up swaps in U2_GIVEUP. Whichever swap lands first
-        // wins, so either every workgroup applies the x / p update or none does (then r holds r_{k+1} and x x_k,
-        // the status is FEM_PCG_SYNC_TIMEOUT with the give-up site, and fem_pcg_solve re-solves from x0).
-        double beta = 0.0, halt = 0.0;
-        bool ok = true;
-        if (last) {
-            const int it0 = st->iter;
-            finish_rz(st, rz_new, hist, hist_len);
-            beta = st->beta;
-            halt = st->halt ? 1.0 : 0.0;
-            __hip_atomic_store(reinterpret_cast<double*>(sync + U2_BC), beta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(reinterpret_cast<double*>(sync + U2_BC) + 1, halt, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            // the broadcast's write-through stores drained before the release (the guide's sc1 hand-off form; the
-            // asm's memory clobber also keeps the compiler from moving them past the swap)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            unsigned expect = e - 1;
-            if (!__hip_atomic_compare_exchange_strong(sync + U2_REL, &expect, e, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT)) {
-                // a waiter gave up first: undo the commit (the iteration did not complete) and keep its verdict
-                st->iter = it0;
-                u2_give_up(st, e);
-                ok = false;
-            }
-        } else {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            unsigned v = 0;
-            for (unsigned spins = 0;; ++spins) {
-                v = __hip_atomic_load(sync + U2_REL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (v != e - 1) break;   // released (e) or given up (U2_GIVEUP)
-                if ((spins & 63) == 63 && __builtin_amdgcn_s_memrealtime() - t0 > U2_WAIT_TICKS) {
-                    unsigned expect = e - 1;
-                    if (__hip_atomic_compare_exchange_strong(sync + U2_REL, &expect, U2_GIVEUP, __ATOMIC_RELAXED,
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                        v = U2_GIVEUP;   // a workgroup that never became resident: stop instead of hanging
-                    else
-                        v = expect;      // the release landed first
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-            // no load below may be moved above the poll by the compiler (the hardware issues it only after the
-            // branch on the polled value); the broadcast is read with write-through (sc1) loads
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            if (v == e) {
-                beta = __hip_atomic_load(reinterpret_cast<const double*>(sync + U2_BC), __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-                halt = __hip_atomic_load(reinterpret_cast<const double*>(sync + U2_BC) + 1, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                u2_give_up(st, e);
-                ok = false;
-            }
-        }
-        bc_s[0] = beta;
-        bc_s[1] = ok ? halt : -1.0;
-    }
-    __syncthreads();
-    const double beta = bc_s[0];
-    if (bc_s[1] < 0.0) return;
-    const bool upd_p = bc_s[1] == 0.0;
+    double beta;
+    bool upd_p, last;
+    if (!u2_release(acc, st, red, hist, hist_len, sync, e, lds4, &flag, bc_s, beta, upd_p, last)) return;
     double2* x2 = reinterpret_cast<double2*>(x);
     double2* p2 = reinterpret_cast<double2*>(p);
 #pragma unroll
@@ -655,6 +668,102 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update2(int64_t n, double* __
         if (upd_p) p[i] = ztail + beta * p[i];
     }
     if (last && threadIdx.x == 0) st->u2_epoch = e;   // every workgroup read the epoch before the release
+}
+
+// The merged update on the element-chunk operator, one node (BS dofs) per thread-step: q of the node is the sum of
+// its slots in ascending chunk order (k_mf_gather's sum; FROM_Q: read from q written by k_mf_gather instead, the A/B
+// form -- same order of every sum, the same bits), so q is never stored. The release protocol is k_pcg_update2's.
+constexpr int U2_NPN = 6;   // nodes per thread whose z stays in registers
+template <int BS, bool FROM_Q>
+__global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update2_mf(int64_t nn, double* __restrict__ x, double* __restrict__ p,
+                                                              double* __restrict__ r, const double* __restrict__ q,
+                                                              const double* __restrict__ w, PcgState* __restrict__ st,
+                                                              RedBuf red, double* __restrict__ hist, int64_t hist_len,
+                                                              unsigned* __restrict__ sync, int hold, MfOp op,
+                                                              const double* __restrict__ slots) {
+    __shared__ double lds4[4];
+    __shared__ int flag;
+    __shared__ double bc_s[2];
+    if (st->halt || st->iter >= st->max_iter) return;
+    if (hold && blockIdx.x == 0) {   // FEM_TUNE_U2_HOLD (tests)
+        if (threadIdx.x == 0) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__builtin_amdgcn_s_memrealtime() - t0 < U2_WAIT_TICKS + U2_WAIT_TICKS / 2) __builtin_amdgcn_s_sleep(127);
+        }
+        __syncthreads();
+    }
+    const unsigned e = st->u2_epoch + 1;
+    const double alpha = st->alpha;
+    const bool cg = st->mode != FEM_MODE_PCG;
+    const int64_t stride = (int64_t)gridDim.x * PCG_BLOCK;
+    const int64_t a0 = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x;
+    auto node_r = [&](int64_t a, double zc[BS]) -> double {   // r update of node a, z = w r; returns its r.z
+        double qv[BS];
+        if constexpr (FROM_Q) {
+#pragma unroll
+            for (int c = 0; c < BS; ++c) qv[c] = q[a * BS + c];
+        } else {
+#pragma unroll
+            for (int c = 0; c < BS; ++c) qv[c] = 0.0;
+            const int k0 = op.nptr[a], k1 = op.nptr[a + 1];
+            for (int k = k0; k < k1; ++k) {
+                const int64_t sl = op.nslot[k];
+#pragma unroll
+                for (int c = 0; c < BS; ++c) qv[c] += slots[sl * BS + c];
+            }
+        }
+        double s = 0.0;
+#pragma unroll
+        for (int c = 0; c < BS; ++c) {
+            const int64_t d = a * BS + c;
+            double rv = r[d] - alpha * qv[c];
+            const double wv = w[d];
+            if (cg && wv == 0.0) rv = 0.0;
+            r[d] = rv;
+            zc[c] = wv * rv;
+            s += rv * zc[c];
+        }
+        return s;
+    };
+    double z[U2_NPN][BS];
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < U2_NPN; ++k) {
+        const int64_t a = a0 + k * stride;
+#pragma unroll
+        for (int c = 0; c < BS; ++c) z[k][c] = 0.0;
+        if (a < nn) acc += node_r(a, z[k]);
+    }
+    for (int64_t a = a0 + U2_NPN * stride; a < nn; a += stride) {   // past the register capacity
+        double zc[BS];
+        acc += node_r(a, zc);
+    }
+    double beta;
+    bool upd_p, last;
+    if (!u2_release(acc, st, red, hist, hist_len, sync, e, lds4, &flag, bc_s, beta, upd_p, last)) return;
+#pragma unroll
+    for (int k = 0; k < U2_NPN; ++k) {
+        const int64_t a = a0 + k * stride;
+        if (a < nn) {
+#pragma unroll
+            for (int c = 0; c < BS; ++c) {
+                const int64_t d = a * BS + c;
+                const double pv = p[d];
+                x[d] += alpha * pv;
+                if (upd_p) p[d] = z[k][c] + beta * pv;
+            }
+        }
+    }
+    for (int64_t a = a0 + U2_NPN * stride; a < nn; a += stride) {
+#pragma unroll
+        for (int c = 0; c < BS; ++c) {
+            const int64_t d = a * BS + c;
+            const double pv = p[d];
+            x[d] += alpha * pv;
+            if (upd_p) p[d] = w[d] * r[d] + beta * pv;
+        }
+    }
+    if (last && threadIdx.x == 0) st->u2_epoch = e;
 }
 
 // ---------------------------------------------------------------- deferred schedule (3 kernels, no grid atomics)
@@ -1726,6 +1835,7 @@ struct fem_pcg {
     unsigned* u2_sync;                    // [U2_WORDS]: release epoch, broadcast (beta, halt), give-up
     // element-chunk operator (fem_pcg_set_operator_mf): K1 = k_pcg_mf_dot + k_mf_gather instead of a SELL SpMV
     fem_mf* mf;
+    int mf_qfuse;   // the merged update reads q from the slots (no gather launch); set per launch of K1 + update2
 };
 
 #define FEM_NCCL(call)                                                                         \
@@ -1751,7 +1861,7 @@ template <int BS>
 __global__ void __launch_bounds__(MF_BLOCK) k_pcg_mf_dot(MfOp op, const double* __restrict__ p,
                                                          double* __restrict__ slots, PcgState* __restrict__ st,
                                                          RedBuf red) {
-    __shared__ MfLds<BS> L;
+    __shared__ MfLds<BS, mf_fc<MF_DOT>()> L;
     __shared__ double lds4[4];
     __shared__ int flag;
     if (blockIdx.x == 0 && threadIdx.x == 0) st->xupd = 0;
@@ -1770,7 +1880,8 @@ static int launch_mf_dot(fem_pcg* s) {
     if (s->bs == 3) hipLaunchKernelGGL(k_pcg_mf_dot<3>, dim3(G), dim3(MF_BLOCK), 0, s->stream, op, s->p0, sl, s->st, s->red);
     else hipLaunchKernelGGL(k_pcg_mf_dot<1>, dim3(G), dim3(MF_BLOCK), 0, s->stream, op, s->p0, sl, s->st, s->red);
     FEM_LAUNCHED();
-    if (op.nnodes > 0) {
+    s->mf_qfuse = s->upd1 && !(s->tune & FEM_TUNE_MF_GATHER);
+    if (op.nnodes > 0 && !s->mf_qfuse) {
         if (s->bs == 3) hipLaunchKernelGGL(k_mf_gather<3>, dim3(stream_grid(op.nnodes, 256)), dim3(256), 0, s->stream, op, sl, s->q);
         else hipLaunchKernelGGL(k_mf_gather<1>, dim3(stream_grid(op.nnodes, 256)), dim3(256), 0, s->stream, op, sl, s->q);
         FEM_LAUNCHED();
@@ -2067,16 +2178,27 @@ static int u2_setup(fem_pcg* s) {
     s->upd1 = 0;
     if (!(s->tune & FEM_TUNE_UPD1) || s->dist || s->fused || s->deferred || s->persist || s->has_con || s->n < 2)
         return FEM_OK;
-    static std::atomic<int> occ[64];
+    // per instantiation launched (the element-chunk operator's forms sum the slots in the update and hold more
+    // registers): every workgroup of the launch must be resident at once
+    static std::atomic<int> occ[3][64];
+    const int var = s->mf ? (s->bs == 3 ? 2 : 1) : 0;
     int dev = 0;
     FEM_HIP(hipGetDevice(&dev));
-    int per_cu = occ[dev & 63].load();
+    int per_cu = occ[var][dev & 63].load();
     if (per_cu == 0) {
         int ncu = 0, nb = 0;
         FEM_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-        FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pcg_update2, PCG_BLOCK, 0));
+        // the element-chunk forms: the smaller residency of the two (slot sums / q read) per block size
+        int nb2 = 0;
+        const void* fn = var == 0 ? (const void*)k_pcg_update2 : var == 1 ? (const void*)k_pcg_update2_mf<1, false>
+                                                                       : (const void*)k_pcg_update2_mf<3, false>;
+        const void* fn2 = var == 0 ? fn : var == 1 ? (const void*)k_pcg_update2_mf<1, true>
+                                                   : (const void*)k_pcg_update2_mf<3, true>;
+        FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb2, fn2, PCG_BLOCK, 0));
+        FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, PCG_BLOCK, 0));
+        nb = nb2 < nb ? nb2 : nb;
         per_cu = (nb < 1 || ncu < NXCD) ? -1 : ((ncu / NXCD) * NXCD) * (nb < 8 ? nb : 8);
-        occ[dev & 63].store(per_cu);
+        occ[var][dev & 63].store(per_cu);
     }
     if (per_cu < 0) return FEM_OK;   // no resident grid: the two-kernel update stays
     int64_t want = cdiv(s->n / 2 + 1, PCG_BLOCK);
@@ -2096,8 +2218,27 @@ static int u2_setup(fem_pcg* s) {
 }
 
 static int launch_update2(fem_pcg* s) {
+    const int hold = (s->tune & FEM_TUNE_U2_HOLD) ? 1 : 0;
+    if (s->mf) {   // node form; q from the operator's slots inside the update unless a gather launch wrote it
+        const MfOp op = mf_op(s->mf);
+        const double* sl = mf_slots(s->mf);
+        const int64_t nn = s->nrows;
+#define FEM_U2MF(B, FQ)                                                                                               \
+    hipLaunchKernelGGL((k_pcg_update2_mf<B, FQ>), dim3(s->u2_grid), dim3(PCG_BLOCK), 0, s->stream, nn, s->x, s->p0,    \
+                       s->r, s->q, s->w, s->st, s->red, s->hist, s->hist_len, s->u2_sync, hold, op, sl)
+        if (s->bs == 3) {
+            if (s->mf_qfuse) FEM_U2MF(3, false);
+            else FEM_U2MF(3, true);
+        } else {
+            if (s->mf_qfuse) FEM_U2MF(1, false);
+            else FEM_U2MF(1, true);
+        }
+#undef FEM_U2MF
+        FEM_LAUNCHED();
+        return FEM_OK;
+    }
     hipLaunchKernelGGL(k_pcg_update2, dim3(s->u2_grid), dim3(PCG_BLOCK), 0, s->stream, s->n, s->x, s->p0, s->r, s->q,
-                       s->w, s->st, s->red, s->hist, s->hist_len, s->u2_sync, (s->tune & FEM_TUNE_U2_HOLD) ? 1 : 0);
+                       s->w, s->st, s->red, s->hist, s->hist_len, s->u2_sync, hold);
     FEM_LAUNCHED();
     return FEM_OK;
 }

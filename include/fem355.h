@@ -492,7 +492,10 @@ int fem_enforce_constraints(double* x, double* r, int64_t n, int order, int64_t 
  * order of the per-block p.q partials (deterministic for a given flag set). */
 enum { FEM_TUNE_REVERSE = 1, FEM_TUNE_PAIR = 2, FEM_TUNE_PK_SC1 = 4, FEM_TUNE_PK_PACK = 8, FEM_TUNE_C1F = 16,
        FEM_TUNE_PK_COOP = 32, FEM_TUNE_DIST_FINE = 64, FEM_TUNE_PK_UNI = 128, FEM_TUNE_PK_WIDE = 256,
-       FEM_TUNE_DIST_DROP = 512, FEM_TUNE_UPD1 = 1024, FEM_TUNE_U2_HOLD = 2048, FEM_TUNE_U2_SMALL = 4096 };
+       FEM_TUNE_DIST_DROP = 512, FEM_TUNE_UPD1 = 1024, FEM_TUNE_U2_HOLD = 2048, FEM_TUNE_U2_SMALL = 4096,
+       FEM_TUNE_MF_GATHER = 8192 };
+/* FEM_TUNE_MF_GATHER (A/B): on the element-chunk operator, q = A p is summed from the slots by a gather launch and
+ * read by the merged update, instead of the update summing each dof's slots itself (the default; same bits). */
 /* FEM_TUNE_U2_HOLD / FEM_TUNE_U2_SMALL (tests only): the merged update's give-up path -- workgroup 0 arrives only after
  * every other workgroup's bounded wait ran out, so the launch must end with FEM_PCG_SYNC_TIMEOUT, no x / p update
  * anywhere and the give-up site 4 (+ 16 * launch); and its grid capped at 8 workgroups, so a small system reaches the

@@ -176,6 +176,35 @@ def test_runner_chunks_bit_identical(gpu):
     assert torch.equal(xs[0], xs[1])
 
 
+@pytest.mark.parametrize("kind", ["elastic", "poisson"])
+def test_update_fused_q_bit_identical(gpu, kind):
+    """The merged update summing each dof's slots itself (default) against the gather launch + stored q
+    (FEM_TUNE_MF_GATHER), and with the update's grid capped at 8 workgroups (FEM_TUNE_U2_SMALL: the loop past the
+    register-cached elements, and an odd dof count): the same bits after 9 iterations."""
+    mesh, _, system = _mods()
+    from fem355 import _capi as C
+    c, t = mesh.kuhn_cube(7, jitter=0.1)
+    if kind == "poisson":   # an odd dof count: the update's scalar tail
+        c = torch.cat([c, torch.tensor([[0.5, 0.5, 2.0]], dtype=F64)], 0)
+    f, fixed = mesh.cube_elasticity_case(c) if kind == "elastic" else mesh.cube_poisson_case(c)
+    A = system.MatFreeOperator(c.to(gpu), t.to(gpu), kind, E if kind == "elastic" else 1.0, NU)
+    mask = torch.zeros((c.shape[0], A.bs), dtype=torch.uint8, device=gpu)
+    mask[fixed.to(gpu)] = 1
+    w = A.jacobi(mask.view(-1))
+    xs = []
+    for extra in (0, C.TUNE_MF_GATHER, C.TUNE_U2_SMALL, C.TUNE_U2_SMALL | C.TUNE_MF_GATHER):
+        run = system.PcgRunner(A, f.reshape(-1), w, tol=0.0)
+        try:
+            run.set_tuning(C.TUNE_DEFAULT | extra)
+            run.start()
+            run.iterate(9)
+            assert run.poll()[0] == 9
+            xs.append(run.x.clone())
+        finally:
+            run.close()
+    assert all(torch.equal(xs[0], v) for v in xs[1:])
+
+
 def test_config2_matfree_10m_operator_and_iterates_vs_oracle(gpu, cube119):
     """BASELINE configs[2] (10,110,954 tets, 5,184,000 DOFs) on the matrix-free operator: the operator on a seeded
     vector against the oracle's EBE product over its element matrices at 1e-12, the exact Jacobi weights at 1e-14,

@@ -7,7 +7,7 @@ NAME=$1; FLAGS=$2
 OUT=../build/var_$NAME
 mkdir -p $OUT
 OBJS=""
-for f in runtime pattern assemble pcg stress topology csr_abi reorder; do
+for f in runtime pattern assemble pcg stress topology csr_abi reorder matfree; do
   EX=""; [ $f = pcg ] && EX="-mllvm -disable-promote-alloca-to-vector"
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -munsafe-fp-atomics $EX $FLAGS -c $f.hip -o $OUT/$f.o &
   OBJS="$OBJS $OUT/$f.o"

@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--kind", default="elastic")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--no-assembled", action="store_true")
+    ap.add_argument("--tune-extra", type=int, default=int(os.environ.get("FEM355_PROBE_TUNE", "0")),
+                    help="FEM_TUNE_* flags added to the library default (e.g. 8192: q by a gather launch)")
     a = ap.parse_args()
     C.lib()
     dev = torch.device("cuda", 0)
@@ -65,6 +67,8 @@ def main():
     mask[fixed] = 1
     w = A.jacobi(mask.view(-1))
     run = system.PcgRunner(A, f.reshape(-1), w, tol=0.0)
+    if a.tune_extra:
+        run.set_tuning(C.TUNE_DEFAULT | a.tune_extra)
     run.start()
     run.profile(5, every=1)
     ms, n = run.profile(a.iters, every=1)
