@@ -2,11 +2,12 @@
 // fem_mf_diag). The chunk kernels themselves are in matfree.hpp (shared with the PCG's K1 in pcg.hip).
 //
 // Build, all on the device except two small host reads of the per-chunk node counts:
-//   1. node bounding box; per element its Morton key (10 bits per axis of the centroid), the connectivity range check
+//   1. node bounding box; per element the Morton key of its centroid's cell (cubic cells ~one element cluster wide, at
+//      most 10 bits per axis), the connectivity range check
 //      and the singular check (|det| < 1e-12, `solver/element.py:857-858`, the smallest such element reported);
 //   2. elements sorted by key (stable radix sort: equal keys keep their file order);
-//   3. chunks of MF_EC consecutive sorted elements; a chunk touching more than MF_NC nodes is cut into pieces of 64
-//      elements (<= 256 nodes each, always);
+//   3. chunks of MF_EC consecutive sorted elements; a chunk touching more than MF_NC nodes is cut into pieces of
+//      MF_PIECE elements (<= MF_NC nodes each, always);
 //   4. per chunk (one workgroup): the (node << 11 | element << 2 | corner) keys of its 4 ne corners sorted in LDS, the
 //      local node list, the node-major pair list and every element's 4 local ids;
 //   5. node -> slots: the (node, slot) pairs sorted by node (stable: slots ascend within a node).
@@ -30,6 +31,7 @@ struct fem_mf {
     uint16_t* lent = nullptr;
     int32_t* nptr = nullptr;
     int32_t* nslot = nullptr;
+    int32_t* spos = nullptr;     // node-major slot positions (null: chunk-major slots)
     double* slots = nullptr;     // [nslots * bs] scratch of every application
     fem::MfOp op() const {
         fem::MfOp o{};
@@ -45,6 +47,7 @@ struct fem_mf {
         o.lent = lent;
         o.nptr = nptr;
         o.nslot = nslot;
+        o.spos = spos;
         o.X = X;
         o.lam = lam;
         o.mu = mu;
@@ -97,7 +100,7 @@ __device__ __forceinline__ uint32_t mf_spread10(uint32_t v) {   // 10 bits -> ev
 // bad[1]: smallest singular element
 __global__ void __launch_bounds__(256) k_mf_keys(const double* __restrict__ X, const int64_t* __restrict__ conn,
                                                  int64_t M, int64_t N, const double* __restrict__ part, int nparts,
-                                                 uint32_t* __restrict__ keys, int32_t* __restrict__ ids,
+                                                 double cells, uint32_t* __restrict__ keys, int32_t* __restrict__ ids,
                                                  unsigned long long* __restrict__ bad) {
     __shared__ double box[6];
     if (threadIdx.x < 6) {
@@ -130,12 +133,13 @@ __global__ void __launch_bounds__(256) k_mf_keys(const double* __restrict__ X, c
             for (int k = 0; k < 3; ++k) p[b][k] = X[3 * c[b] + k];
         const double det = tet4_grads_p(p, g);
         if (!(fabs(det) >= 1e-12)) atomicMin(&bad[1], (unsigned long long)e);
+        // cubic cells, `cells` of them along the longest extent (capped at 1024 per axis)
+        const double ext = fmax(box[3] - box[0], fmax(box[4] - box[1], box[5] - box[2]));
         uint32_t q[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            const double ext = box[3 + k] - box[k];
             const double cen = 0.25 * (p[0][k] + p[1][k] + p[2][k] + p[3][k]);
-            double t = ext > 0.0 ? (cen - box[k]) / ext * 1024.0 : 0.0;
+            double t = ext > 0.0 ? (cen - box[k]) / ext * cells : 0.0;
             t = fmin(fmax(t, 0.0), 1023.0);
             q[k] = (uint32_t)t;
         }
@@ -143,12 +147,14 @@ __global__ void __launch_bounds__(256) k_mf_keys(const double* __restrict__ X, c
     }
 }
 
-// bitonic sort of 2048 keys in LDS (256 threads)
+// bitonic sort of MF_SORT keys in LDS (256 threads)
+constexpr int MF_SORT = 4 * MF_EC < 256 ? 256 : 4 * MF_EC;   // a chunk's (element, corner) pairs, padded
+constexpr int MF_SPT = MF_SORT / 256;                        // pairs per thread in the scans
 template <typename T>
-__device__ __forceinline__ void mf_bitonic2048(T* s) {
-    for (int k = 2; k <= 2048; k <<= 1)
+__device__ __forceinline__ void mf_bitonic(T* s) {
+    for (int k = 2; k <= MF_SORT; k <<= 1)
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < 2048; i += 256) {
+            for (int i = threadIdx.x; i < MF_SORT; i += 256) {
                 const int ixj = i ^ j;
                 if (ixj > i) {
                     const T a = s[i], b = s[ixj];
@@ -193,18 +199,18 @@ __device__ __forceinline__ void mf_chunk_range(const int32_t* cptr, int64_t c, i
 __global__ void __launch_bounds__(256) k_mf_count(const int64_t* __restrict__ conn, const int32_t* __restrict__ order,
                                                   int64_t M, const int32_t* __restrict__ cptr, int64_t nchunks,
                                                   int32_t* __restrict__ count) {
-    __shared__ uint32_t s[2048];
+    __shared__ uint32_t s[MF_SORT];
     __shared__ int sc[256];
     const int64_t c = blockIdx.x;
     if (c >= nchunks) return;
     int e0, ne;
     mf_chunk_range(cptr, c, M, &e0, &ne);
-    for (int k = threadIdx.x; k < 2048; k += 256)
+    for (int k = threadIdx.x; k < MF_SORT; k += 256)
         s[k] = k < 4 * ne ? (uint32_t)conn[4 * (int64_t)order[e0 + (k >> 2)] + (k & 3)] : 0xffffffffu;
     __syncthreads();
-    mf_bitonic2048(s);
+    mf_bitonic(s);
     int h = 0;
-    for (int k = 8 * threadIdx.x; k < 8 * threadIdx.x + 8; ++k)
+    for (int k = MF_SPT * threadIdx.x; k < MF_SPT * threadIdx.x + MF_SPT; ++k)
         h += (k < 4 * ne && (k == 0 || s[k] != s[k - 1])) ? 1 : 0;
     int total;
     (void)mf_block_scan(h, sc, &total);
@@ -217,24 +223,24 @@ __global__ void __launch_bounds__(256) k_mf_fill(const int64_t* __restrict__ con
                                                  int64_t nchunks, int32_t* __restrict__ cnode,
                                                  uint16_t* __restrict__ lptr, uint16_t* __restrict__ lent,
                                                  uint8_t* __restrict__ eloc) {
-    __shared__ uint64_t s[2048];
+    __shared__ uint64_t s[MF_SORT];
     __shared__ int sc[256];
     const int64_t c = blockIdx.x;
     if (c >= nchunks) return;
     const int e0 = cptr[c], ne = cptr[c + 1] - e0;
     const int s0 = sbase[c];
-    for (int k = threadIdx.x; k < 2048; k += 256)
+    for (int k = threadIdx.x; k < MF_SORT; k += 256)
         s[k] = k < 4 * ne ? ((uint64_t)conn[4 * (int64_t)order[e0 + (k >> 2)] + (k & 3)] << 11) | (uint64_t)k
                           : ~(uint64_t)0;
     __syncthreads();
-    mf_bitonic2048(s);
-    const int k0 = 8 * threadIdx.x;
+    mf_bitonic(s);
+    const int k0 = MF_SPT * threadIdx.x;
     int h = 0;
-    for (int k = k0; k < k0 + 8; ++k) h += (k < 4 * ne && (k == 0 || (s[k] >> 11) != (s[k - 1] >> 11))) ? 1 : 0;
+    for (int k = k0; k < k0 + MF_SPT; ++k) h += (k < 4 * ne && (k == 0 || (s[k] >> 11) != (s[k - 1] >> 11))) ? 1 : 0;
     int total;
     int lid = mf_block_scan(h, sc, &total) - 1;
     uint16_t* lp = lptr + s0 + c;
-    for (int k = k0; k < k0 + 8 && k < 4 * ne; ++k) {
+    for (int k = k0; k < k0 + MF_SPT && k < 4 * ne; ++k) {
         const uint64_t key = s[k];
         if (k == 0 || (key >> 11) != (s[k - 1] >> 11)) {
             ++lid;
@@ -262,12 +268,18 @@ __global__ void k_mf_nptr(const int32_t* __restrict__ skey, int64_t nslots, int6
     }
 }
 
+// spos[nslot[k]] = k: where each slot is stored in the node-major order
+__global__ void k_mf_spos(const int32_t* __restrict__ nslot, int64_t nslots, int32_t* __restrict__ spos) {
+    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < nslots; k += (int64_t)gridDim.x * 256)
+        spos[nslot[k]] = (int32_t)k;
+}
+
 // ---------------------------------------------------------------- application
 template <int BS, int MODE>
 __global__ void __launch_bounds__(MF_BLOCK) k_mf_apply(MfOp op, const double* __restrict__ x,
                                                        double* __restrict__ slots) {
-    __shared__ MfLds<BS, mf_fc<MODE>()> L;
-    (void)mf_walk<BS, MODE>(op, x, slots, L);
+    __shared__ MfKernelLds<BS, MODE> L;
+    (void)mf_walk_any<BS, MODE>(op, x, slots, L);
 }
 
 static int mf_run(fem_mf* m, int mode, const double* x, double* y, hipStream_t st) {
@@ -304,7 +316,8 @@ int mf_apply(fem_mf* m, const double* x, double* y, hipStream_t st) { return mf_
 
 static void mf_free(fem_mf* m) {
     if (!m) return;
-    void* ps[] = {m->eorder, m->cptr, m->sbase, m->cnode, m->eloc, m->lptr, m->lent, m->nptr, m->nslot, m->slots};
+    void* ps[] = {m->eorder, m->cptr, m->sbase, m->cnode, m->eloc, m->lptr, m->lent, m->nptr, m->nslot, m->spos,
+                  m->slots};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     delete m;
@@ -374,8 +387,14 @@ int fem_mf_create(const double* coords, const int64_t* conn, int64_t M, int64_t 
         MF_TRY(hipMalloc(&m->eorder, sizeof(int32_t) * (size_t)M));
         if (N > 0) hipLaunchKernelGGL(k_mf_bbox, dim3(nparts), dim3(256), 0, st, coords, N, part);
         else MF_TRY(hipMemsetAsync(part, 0, sizeof(double) * 6, st));
-        hipLaunchKernelGGL(k_mf_keys, dim3(stream_grid(M, 256)), dim3(256), 0, st, coords, conn, M, N, part, nparts, keys,
-                           ids, bad);
+        // Morton cells about one element cluster wide: (M / 6)^(1/3) along the longest extent -- one hex of a Kuhn
+        // cube per cell (its 6 tets share a key and keep their file order), so chunks are compact blocks of whole
+        // clusters and their boundary nodes (the slots shared with other chunks) few. FEM355_MF_CELLS overrides.
+        double cells = cbrt((double)M / 6.0);
+        if (const char* ev = getenv("FEM355_MF_CELLS")) cells = atof(ev);
+        cells = cells < 1.0 ? 1.0 : (cells > 1024.0 ? 1024.0 : cells);
+        hipLaunchKernelGGL(k_mf_keys, dim3(stream_grid(M, 256)), dim3(256), 0, st, coords, conn, M, N, part, nparts,
+                           cells, keys, ids, bad);
         MF_TRY(hipGetLastError());
         unsigned long long hb[2];
         MF_TRY(hipMemcpyAsync(hb, bad, sizeof(hb), hipMemcpyDeviceToHost, st));
@@ -397,7 +416,7 @@ int fem_mf_create(const double* coords, const int64_t* conn, int64_t M, int64_t 
         MF_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys2, ids, m->eorder, (int)M, 0, 30, st));
         (void)hipFree(tmp);
         tmp = nullptr;
-        // chunk sizes: uniform MF_EC, then pieces of 64 for chunks touching more than MF_NC nodes
+        // chunk sizes: uniform MF_EC, then pieces of MF_PIECE (4 MF_PIECE <= MF_NC nodes) for chunks touching more
         const int64_t nc0 = cdiv(M, MF_EC);
         int32_t* cnt = ids;   // reused (nc0 <= M)
         hipLaunchKernelGGL(k_mf_count, dim3((unsigned)nc0), dim3(256), 0, st, conn, m->eorder, M, (const int32_t*)nullptr,
@@ -415,7 +434,7 @@ int fem_mf_create(const double* coords, const int64_t* conn, int64_t M, int64_t 
                 hcp.push_back((int32_t)a);
             } else {
                 split = true;
-                for (int64_t b = 0; b < ne; b += 64) hcp.push_back((int32_t)(a + b));
+                for (int64_t b = 0; b < ne; b += MF_PIECE) hcp.push_back((int32_t)(a + b));
             }
         }
         hcp.push_back((int32_t)M);
@@ -464,6 +483,15 @@ int fem_mf_create(const double* coords, const int64_t* conn, int64_t M, int64_t 
         MF_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb, m->cnode, skey, sid, m->nslot, (int)tot, 0, bits, st));
         hipLaunchKernelGGL(k_mf_nptr, dim3(stream_grid(tot + 1, 256)), dim3(256), 0, st, skey, tot, N, m->nptr);
         MF_TRY(hipGetLastError());
+        // node-major slot storage (default): the chunk kernel writes each slot where its node's slots are contiguous,
+        // so the readers (merged update, gather) stream them instead of following nslot. FEM355_MF_NODEMAJOR=0: the
+        // chunk-major slots (A/B)
+        const char* nm = getenv("FEM355_MF_NODEMAJOR");
+        if (!nm || atoi(nm) != 0) {
+            MF_TRY(hipMalloc(&m->spos, sizeof(int32_t) * (size_t)tot));
+            hipLaunchKernelGGL(k_mf_spos, dim3(stream_grid(tot, 256)), dim3(256), 0, st, m->nslot, tot, m->spos);
+            MF_TRY(hipGetLastError());
+        }
         MF_TRY(hipStreamSynchronize(st));
     }
 done:

@@ -18,9 +18,23 @@
 
 namespace fem {
 
-constexpr int MF_EC = 512;      // elements per chunk (at most)
-constexpr int MF_NC = 256;      // local nodes per chunk (at most; local ids are bytes)
-constexpr int MF_PASS = 256;    // elements formed per pass (= threads of the workgroup)
+// Chunk geometry. FEM_MF_WAVE (default): a chunk per WAVE -- <= 64 elements / <= 64 nodes (pieces of 16 elements when
+// more), every wave of a workgroup walking its own chunks with no workgroup barrier, ~10 KB of LDS per wave. Else a
+// chunk per workgroup: <= 512 elements / <= 256 nodes (pieces of 64), two passes of 256 elements, 41.6 KB per
+// workgroup and its barriers.
+#ifndef FEM_MF_WAVE
+#define FEM_MF_WAVE 0
+#endif
+#if FEM_MF_WAVE
+constexpr int MF_EC = 64;       // elements per chunk (at most)
+constexpr int MF_NC = 64;       // local nodes per chunk (at most)
+constexpr int MF_PIECE = 16;    // elements per piece of a chunk that touched more than MF_NC nodes
+#else
+constexpr int MF_EC = 512;
+constexpr int MF_NC = 256;      // local ids are bytes
+constexpr int MF_PIECE = 64;
+#endif
+constexpr int MF_PASS = 256;    // elements formed per pass (= threads of the workgroup; workgroup chunks)
 constexpr int MF_BLOCK = 256;
 #ifndef FEM_MF_UNROLL
 #define FEM_MF_UNROLL 4
@@ -51,6 +65,8 @@ struct MfOp {
     const uint16_t* lent;   // [4 M] per chunk at 4 cptr[c]: pairs (element_in_chunk << 2 | corner), node-major
     const int32_t* nptr;    // [nnodes + 1] node -> its slots
     const int32_t* nslot;   // [nslots] slots of each node, ascending (= ascending chunk)
+    const int32_t* spos;    // [nslots] or null: node-major slot storage -- slot s stored at spos[s], a node's slots at
+                            // [nptr[a], nptr[a + 1]) (readers stream them; nslot unused)
     const double* X;        // [nnodes, 3] coordinates
     double lam, mu, kappa;
 };
@@ -182,7 +198,7 @@ __device__ __forceinline__ void mf_pair_value(const MfLds<BS, FC>& L, int pe, in
 template <int BS>
 struct MfPf {
     int e0, ne, s0, nn;
-    int node;
+    int node, sp;
     uint16_t lp;
     uint4 ent;
     uint32_t el[MF_EC / MF_PASS];
@@ -201,6 +217,7 @@ __device__ __forceinline__ void mf_pf1(const MfOp& op, int64_t c, MfPf<BS>& f) {
     f.lp = 0;
     if (tid < f.nn) {
         f.node = op.cnode[f.s0 + tid];
+        f.sp = op.spos ? op.spos[f.s0 + tid] : f.s0 + tid;
         f.lp = op.lptr[f.s0 + c + tid];
     }
     f.ent = make_uint4(0, 0, 0, 0);
@@ -337,7 +354,7 @@ __device__ __forceinline__ double mf_walk(const MfOp& op, const double* __restri
         if (tid < cur.nn) {
 #pragma unroll
             for (int q = 0; q < BS; ++q) {
-                slots[(int64_t)(cur.s0 + tid) * BS + q] = acc[q];
+                slots[(int64_t)cur.sp * BS + q] = acc[q];
                 if constexpr (MODE == MF_DOT) dot += cur.pv[q] * acc[q];
             }
         }
@@ -348,6 +365,198 @@ __device__ __forceinline__ double mf_walk(const MfOp& op, const double* __restri
         has1 = has2;
     }
     return dot;
+}
+
+// LDS of one wave's chunk (FEM_MF_WAVE)
+template <int BS, int FC>
+struct MfLdsW {
+    double nd[MF_NC][3 + BS];
+    double fs[FC * BS][MF_EC + 1];
+    uint16_t lp[MF_NC + 1];
+    alignas(16) uint16_t ent[4 * MF_EC];
+};
+
+// LDS hand-off between the lanes of one wave: program order for the compiler (the hardware runs a wave's LDS
+// operations in order)
+__device__ __forceinline__ void mf_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+template <int BS>
+struct MfPfW {
+    int e0, ne, s0, nn;
+    int node, sp;
+    uint16_t lp;
+    uint2 ent;
+    uint32_t el;
+    double xv[3], pv[BS];
+};
+
+template <int BS>
+__device__ __forceinline__ void mf_pfw1(const MfOp& op, int64_t c, MfPfW<BS>& f) {
+    const int lane = threadIdx.x & 63;
+    f.e0 = __builtin_amdgcn_readfirstlane(op.cptr[c]);
+    f.ne = __builtin_amdgcn_readfirstlane(op.cptr[c + 1]) - f.e0;
+    f.s0 = __builtin_amdgcn_readfirstlane(op.sbase[c]);
+    f.nn = __builtin_amdgcn_readfirstlane(op.sbase[c + 1]) - f.s0;
+    f.node = 0;
+    f.lp = 0;
+    if (lane < f.nn) {
+        f.node = op.cnode[f.s0 + lane];
+        f.sp = op.spos ? op.spos[f.s0 + lane] : f.s0 + lane;
+        f.lp = op.lptr[f.s0 + c + lane];
+    }
+    f.ent = make_uint2(0, 0);
+    if (4 * lane < 4 * f.ne) f.ent = reinterpret_cast<const uint2*>(op.lent + 4 * (int64_t)f.e0)[lane];
+    f.el = lane < f.ne ? op.eloc[f.e0 + lane] : 0u;
+}
+
+template <int BS, int MODE>
+__device__ __forceinline__ void mf_pfw2(const MfOp& op, const double* __restrict__ x, MfPfW<BS>& f) {
+    if ((int)(threadIdx.x & 63) < f.nn) {
+        const int64_t g = f.node;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) f.xv[k] = op.X[3 * g + k];
+#pragma unroll
+        for (int k = 0; k < BS; ++k) f.pv[k] = MODE == MF_DIAG ? 0.0 : x[BS * g + k];
+    }
+}
+
+// Every chunk of this WAVE (chunk ranges per XCD; consecutive chunks on one XCD at once), three chunks in flight as in
+// mf_walk; lane l < nn owns local node l, lane e < ne element e. No workgroup barrier: the waves of a workgroup only
+// share the CU.
+template <int BS, int MODE>
+__device__ __forceinline__ double mf_walk_w(const MfOp& op, const double* __restrict__ x, double* __restrict__ slots,
+                                            MfLdsW<BS, mf_fc<MODE>()>& L) {
+    constexpr int FC = mf_fc<MODE>();
+    const int lane = threadIdx.x & 63;
+    constexpr int WPB = MF_BLOCK / 64;
+    const int64_t per = (op.nchunks + NXCD - 1) / NXCD;
+    const int64_t base = (int64_t)(blockIdx.x % NXCD) * per;
+    const int64_t nb = (int64_t)(gridDim.x / NXCD) * WPB;
+    int64_t k = (int64_t)(blockIdx.x / NXCD) * WPB + (threadIdx.x >> 6);
+    double dot = 0.0;
+    if (k >= per || base + k >= op.nchunks) return dot;
+    MfPfW<BS> cur, n1, n2;
+    mf_pfw1<BS>(op, base + k, cur);
+    bool has1 = k + nb < per && base + k + nb < op.nchunks;
+    if (has1) mf_pfw1<BS>(op, base + k + nb, n1);
+    mf_pfw2<BS, MODE>(op, x, cur);
+    for (;;) {
+        mf_wave_sync();   // the previous chunk's LDS reads are done
+        if (lane < cur.nn) {
+#pragma unroll
+            for (int q = 0; q < 3; ++q) L.nd[lane][q] = cur.xv[q];
+#pragma unroll
+            for (int q = 0; q < BS; ++q) L.nd[lane][3 + q] = cur.pv[q];
+            L.lp[lane] = cur.lp;
+        }
+        if (lane == 0) L.lp[cur.nn] = (uint16_t)(4 * cur.ne);
+        if (lane < cur.ne) reinterpret_cast<uint2*>(L.ent)[lane] = cur.ent;
+        const int64_t k2 = k + 2 * nb;
+        const bool has2 = has1 && k2 < per && base + k2 < op.nchunks;
+        if (has1) mf_pfw2<BS, MODE>(op, x, n1);
+        if (has2) mf_pfw1<BS>(op, base + k2, n2);
+        mf_wave_sync();
+        if (lane < cur.ne) {
+            const uint32_t w = cur.el;
+            double xc[4][3], xv[4][BS], f[4][BS];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int l = (w >> (8 * b)) & 0xff;
+                const double2* r = reinterpret_cast<const double2*>(&L.nd[l][0]);
+                const double2 a0 = r[0], a1 = r[1];
+                xc[b][0] = a0.x;
+                xc[b][1] = a0.y;
+                xc[b][2] = a1.x;
+                if constexpr (BS == 1) {
+                    xv[b][0] = a1.y;
+                } else {
+                    const double2 a2 = r[2];
+                    xv[b][0] = a1.y;
+                    xv[b][1] = a2.x;
+                    xv[b][2] = a2.y;
+                }
+            }
+            mf_element<BS, MODE>(xc, xv, op.lam, op.mu, op.kappa, f);
+#pragma unroll
+            for (int b = 4 - FC; b < 4; ++b)
+#pragma unroll
+                for (int q = 0; q < BS; ++q) L.fs[(b - (4 - FC)) * BS + q][lane] = f[b][q];
+        }
+        mf_wave_sync();
+        if (lane < cur.nn) {
+            double acc[BS];
+#pragma unroll
+            for (int q = 0; q < BS; ++q) acc[q] = 0.0;
+            int pos = L.lp[lane];
+            const int end = L.lp[lane + 1];
+            for (; pos + MF_U <= end; pos += MF_U) {
+                int pe[MF_U];
+#pragma unroll
+                for (int u = 0; u < MF_U; ++u) pe[u] = L.ent[pos + u];
+                double v[MF_U][BS];
+#pragma unroll
+                for (int u = 0; u < MF_U; ++u) {
+                    const int el = pe[u] >> 2, b = pe[u] & 3;
+                    if (FC == 3 && b == 0) {
+#pragma unroll
+                        for (int q = 0; q < BS; ++q) v[u][q] = -(L.fs[q][el] + L.fs[BS + q][el] + L.fs[2 * BS + q][el]);
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < BS; ++q) v[u][q] = L.fs[(b - (4 - FC)) * BS + q][el];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < MF_U; ++u)
+#pragma unroll
+                    for (int q = 0; q < BS; ++q) acc[q] += v[u][q];
+            }
+            for (; pos < end; ++pos) {
+                const int pe = L.ent[pos];
+                const int el = pe >> 2, b = pe & 3;
+#pragma unroll
+                for (int q = 0; q < BS; ++q) {
+                    const double v = (FC == 3 && b == 0)
+                                         ? -(L.fs[q][el] + L.fs[BS + q][el] + L.fs[2 * BS + q][el])
+                                         : L.fs[(b - (4 - FC)) * BS + q][el];
+                    acc[q] += v;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < BS; ++q) {
+                slots[(int64_t)cur.sp * BS + q] = acc[q];
+                if constexpr (MODE == MF_DOT) dot += cur.pv[q] * acc[q];
+            }
+        }
+        if (!has1) break;
+        k += nb;
+        cur = n1;
+        n1 = n2;
+        has1 = has2;
+    }
+    return dot;
+}
+
+// the walker of the build's geometry, with its LDS
+template <int BS, int MODE>
+struct MfKernelLds {
+#if FEM_MF_WAVE
+    MfLdsW<BS, mf_fc<MODE>()> w[MF_BLOCK / 64];
+#else
+    MfLds<BS, mf_fc<MODE>()> b;
+#endif
+};
+template <int BS, int MODE>
+__device__ __forceinline__ double mf_walk_any(const MfOp& op, const double* __restrict__ x, double* __restrict__ slots,
+                                              MfKernelLds<BS, MODE>& L) {
+#if FEM_MF_WAVE
+    return mf_walk_w<BS, MODE>(op, x, slots, L.w[threadIdx.x >> 6]);
+#else
+    return mf_walk<BS, MODE>(op, x, slots, L.b);
+#endif
 }
 
 // resident workgroups of a chunk kernel (one pass of the grid over the chunks), cached per kernel
@@ -392,7 +601,7 @@ __global__ void __launch_bounds__(256) k_mf_gather(MfOp op, const double* __rest
 #pragma unroll
         for (int k = 0; k < BS; ++k) s[k] = 0.0;
         for (int k = k0; k < k1; ++k) {
-            const int64_t sl = op.nslot[k];
+            const int64_t sl = op.spos ? k : op.nslot[k];
 #pragma unroll
             for (int c = 0; c < BS; ++c) s[c] += slots[sl * BS + c];
         }

@@ -707,7 +707,7 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update2_mf(int64_t nn, double
             for (int c = 0; c < BS; ++c) qv[c] = 0.0;
             const int k0 = op.nptr[a], k1 = op.nptr[a + 1];
             for (int k = k0; k < k1; ++k) {
-                const int64_t sl = op.nslot[k];
+                const int64_t sl = op.spos ? k : op.nslot[k];
 #pragma unroll
                 for (int c = 0; c < BS; ++c) qv[c] += slots[sl * BS + c];
             }
@@ -1861,12 +1861,12 @@ template <int BS>
 __global__ void __launch_bounds__(MF_BLOCK) k_pcg_mf_dot(MfOp op, const double* __restrict__ p,
                                                          double* __restrict__ slots, PcgState* __restrict__ st,
                                                          RedBuf red) {
-    __shared__ MfLds<BS, mf_fc<MF_DOT>()> L;
+    __shared__ MfKernelLds<BS, MF_DOT> L;
     __shared__ double lds4[4];
     __shared__ int flag;
     if (blockIdx.x == 0 && threadIdx.x == 0) st->xupd = 0;
     if (st->halt || st->iter >= st->max_iter) return;
-    double dot = mf_walk<BS, MF_DOT>(op, p, slots, L);
+    double dot = mf_walk_any<BS, MF_DOT>(op, p, slots, L);
     dot = block_sum256(dot, lds4);
     double pq;
     if (reduce_grid(dot, red.part(RED_K1), red.cnt(RED_K1), &pq, lds4, &flag) && threadIdx.x == 0) finish_pq(st, pq);
