@@ -154,6 +154,13 @@ __global__ void __launch_bounds__(256) k_iso_geom(const double* __restrict__ X, 
 constexpr int ISO_MAX_IP = 32;
 constexpr int ISO_IPC = 16;   // points whose geometry is staged in LDS at once
 
+// LDS hand-off between the lanes of one wave (program order for the compiler; a wave's LDS operations run in order)
+__device__ __forceinline__ void iso_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 template <int NPE, bool MASS>
 __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, const int64_t* __restrict__ conn,
                                                 int64_t M, double E, double nu, const double* __restrict__ dN,
@@ -166,6 +173,9 @@ __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, co
     // sum B^T D B is symmetric; mirrored entries equal the directly formed ones up to the order of two products),
     // 55 blocks, one per lane. c3d8 / c3d6 (<= 64 blocks): every block formed directly.
     // mode FEM_ISO_MASS (E = rho, Nv = shape values [n_ip][NPE]): block (a,b) = rho sum_q w_q |detJ_q| N_a N_b I3.
+    // Every wave walks its elements (grid-stride; the grid is the resident one) with wave-level LDS hand-offs only:
+    // no workgroup barrier after the rule tables are staged, the next element's coordinates and the one after's node
+    // ids are loaded while the current element is formed.
     constexpr int D = 3 * NPE;
     constexpr bool SYM = NPE * NPE > 64;
     constexpr int NS = SYM ? NPE * (NPE + 1) / 2 : NPE * NPE;
@@ -185,13 +195,15 @@ __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, co
     if (mass)
         for (int t = threadIdx.x; t < n_ip * NPE; t += 256) nv_s[t] = Nv[t];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t e = (int64_t)blockIdx.x * 4 + wid;
-    const bool active = e < M;
-    if (active && lane < NPE * 3) {
-        int a = lane / 3, k = lane - 3 * (lane / 3);
-        x_s[wid][a][k] = X[3 * conn[e * NPE + a] + k];
-    }
-    __syncthreads();
+    __syncthreads();   // rule tables staged (the only workgroup barrier)
+    const int64_t step = (int64_t)gridDim.x * 4;
+    const bool xl = lane < NPE * 3;   // lane (node a, coordinate k) of the coordinate loads
+    const int xa = lane / 3, xk = lane - 3 * (lane / 3);
+    int64_t e = (int64_t)blockIdx.x * 4 + wid;
+    int64_t cn = (xl && e < M) ? conn[e * NPE + xa] : 0;
+    double xr = (xl && e < M) ? X[3 * cn + xk] : 0.0;
+    int64_t e1 = e + step;
+    int64_t cn1 = (xl && e1 < M) ? conn[e1 * NPE + xa] : 0;
     const Lame L = lame(E, nu);
     int ba = 0, bb = 0;   // this lane's block (SYM: ba <= bb), lane < NS
     if (SYM) {
@@ -207,6 +219,14 @@ __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, co
     }
     const bool mirror = SYM && ba != bb;
     const bool blk_lane = lane < NS;
+  for (; e < M; e += step) {
+    iso_wave_sync();   // the previous element's LDS reads are done
+    if (xl) x_s[wid][xa][xk] = xr;
+    const int64_t e2 = e1 + step;
+    const double xr1 = (xl && e1 < M) ? X[3 * cn1 + xk] : 0.0;
+    const int64_t cn2 = (xl && e2 < M) ? conn[e2 * NPE + xa] : 0;
+    iso_wave_sync();
+    const bool active = true;
     double acc[9];
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[t] = 0.0;
@@ -257,7 +277,7 @@ __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, co
             c_s[wid][lane] = mass ? fabs(det) * w[q] * E
                                   : (mode == FEM_ISO_SUM) ? det * w[q] : (mode == FEM_ISO_STACK ? det : vol);
         }
-        __syncthreads();
+        iso_wave_sync();
         for (int ql = 0; ql < nq; ++ql) {
             const double coef = c_s[wid][ql];
             if (mass) {
@@ -292,9 +312,9 @@ __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, co
                     }
             }
         }
-        __syncthreads();
+        iso_wave_sync();
     }
-    if (mode != FEM_ISO_STACK && active) {   // (the loop above ended on a barrier: gk_s is free)
+    if (mode != FEM_ISO_STACK && active) {   // (the loop above ended on a wave sync: gk_s is free)
         double* ks = gk_s[wid];
         if (blk_lane) {
 #pragma unroll
@@ -311,6 +331,10 @@ __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, co
         const double2* ks2 = reinterpret_cast<const double2*>(ks);
         for (int t = lane; t < D * D / 2; t += 64) out2[t] = ks2[t];
     }
+    xr = xr1;
+    cn1 = cn2;
+    e1 = e2;
+  }
 }
 
 // ---------------------------------------------------------------- SELL value addressing
@@ -1566,6 +1590,24 @@ int fem_iso_geom(const double* coords, const int64_t* conn, int64_t M, int npe, 
     return FEM_OK;
 }
 
+// grid of the element-walking k_iso_ke: the resident workgroups (occupancy with the rule tables' dynamic LDS), at most
+// one element per wave
+static unsigned iso_grid(const void* fn, size_t lds, int64_t M) {
+    int dev = 0, ncu = 0, nb = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, 256, lds) != hipSuccess || nb < 1)
+        nb = 1, ncu = 256;
+    int64_t g = (int64_t)ncu * nb;
+    const int64_t want = cdiv(M, 4);
+    if (want < g) g = want;
+    return (unsigned)(g < 1 ? 1 : g);
+}
+// the walking grid pays for c3d10 (K_e 2.0 -> 1.9 ms, M_e 1.5 -> 1.3 ms on the configs[4] set); the cheaper c3d8 /
+// c3d6 elements ran 5-7 % slower walking than with a wave per element (1.45 -> 1.55, 1.01 -> 1.08 ms for c3d8)
+static unsigned iso_grid_npe(const void* fn, size_t lds, int64_t M, int npe) {
+    return npe == 10 ? iso_grid(fn, lds, M) : (unsigned)cdiv(M, 4);
+}
+
 int fem_iso_ke(const double* coords, const int64_t* conn, int64_t M, int npe, double E, double nu, const double* dN,
                const double* w, int n_ip, int mode, double* Ke, fem_stream_t stream) {
     if (mode != FEM_ISO_SUM && mode != FEM_ISO_STACK && mode != FEM_ISO_VOLUME) {
@@ -1577,8 +1619,10 @@ int fem_iso_ke(const double* coords, const int64_t* conn, int64_t M, int npe, do
         set_error("fem_iso_ke: n_ip = %d out of range [1, %d]", n_ip, ISO_MAX_IP);
         return FEM_EARG;
     }
-    dim3 g((unsigned)cdiv(M, 4));
     const size_t lds = sizeof(double) * (size_t)n_ip * npe * 3;
+    const void* fn = npe == 6 ? (const void*)k_iso_ke<6, false> : npe == 8 ? (const void*)k_iso_ke<8, false>
+                                                                            : (const void*)k_iso_ke<10, false>;
+    const dim3 g(iso_grid_npe(fn, lds, M, npe));
     switch (npe) {
         case 6: hipLaunchKernelGGL((k_iso_ke<6, false>), g, dim3(256), lds, S(stream), coords, conn, M, E, nu, dN, w, n_ip, mode, Ke); break;
         case 8: hipLaunchKernelGGL((k_iso_ke<8, false>), g, dim3(256), lds, S(stream), coords, conn, M, E, nu, dN, w, n_ip, mode, Ke); break;
@@ -1596,9 +1640,11 @@ int fem_iso_mass(const double* coords, const int64_t* conn, int64_t M, int npe, 
         set_error("fem_iso_mass: n_ip = %d out of range [1, %d]", n_ip, ISO_MAX_IP);
         return FEM_EARG;
     }
-    dim3 g((unsigned)cdiv(M, 4));
     const int mode = FEM_ISO_MASS;
     const size_t lds = sizeof(double) * (size_t)n_ip * npe * 4;
+    const void* fn = npe == 6 ? (const void*)k_iso_ke<6, true> : npe == 8 ? (const void*)k_iso_ke<8, true>
+                                                                           : (const void*)k_iso_ke<10, true>;
+    const dim3 g(iso_grid_npe(fn, lds, M, npe));
     switch (npe) {
         case 6: hipLaunchKernelGGL((k_iso_ke<6, true>), g, dim3(256), lds, S(stream), coords, conn, M, rho, 0.0, dN, w, n_ip, mode, Me, Nv); break;
         case 8: hipLaunchKernelGGL((k_iso_ke<8, true>), g, dim3(256), lds, S(stream), coords, conn, M, rho, 0.0, dN, w, n_ip, mode, Me, Nv); break;

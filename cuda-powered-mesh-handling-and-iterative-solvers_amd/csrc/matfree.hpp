@@ -214,6 +214,7 @@ __device__ __forceinline__ void mf_pf1(const MfOp& op, int64_t c, MfPf<BS>& f) {
     f.s0 = op.sbase[c];
     f.nn = op.sbase[c + 1] - f.s0;
     f.node = 0;
+    f.sp = 0;   // every field defined in every lane: the copies of the software pipeline read them all
     f.lp = 0;
     if (tid < f.nn) {
         f.node = op.cnode[f.s0 + tid];
@@ -402,6 +403,7 @@ __device__ __forceinline__ void mf_pfw1(const MfOp& op, int64_t c, MfPfW<BS>& f)
     f.s0 = __builtin_amdgcn_readfirstlane(op.sbase[c]);
     f.nn = __builtin_amdgcn_readfirstlane(op.sbase[c + 1]) - f.s0;
     f.node = 0;
+    f.sp = 0;   // every field defined in every lane: the copies of the software pipeline read them all
     f.lp = 0;
     if (lane < f.nn) {
         f.node = op.cnode[f.s0 + lane];
@@ -586,6 +588,10 @@ inline int mf_resident_grid(const void* fn, int block, int64_t nchunks) {
         return m < 1 ? 1 : m;
     }();
     int64_t g = (int64_t)per_cu * mult;
+    if (const char* cap = getenv("FEM355_MF_GRID_CAP")) {   // tests: a small grid walks many chunks per workgroup
+        const int64_t c = atoll(cap);
+        if (c >= NXCD && c < g) g = (c / NXCD) * NXCD;
+    }
     const int64_t want = ((nchunks + NXCD - 1) / NXCD) * NXCD;
     if (want < g) g = want;
     return (int)(g < NXCD ? NXCD : g);
