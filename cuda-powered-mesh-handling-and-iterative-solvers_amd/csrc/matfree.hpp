@@ -198,7 +198,7 @@ __device__ __forceinline__ void mf_pair_value(const MfLds<BS, FC>& L, int pe, in
 template <int BS>
 struct MfPf {
     int e0, ne, s0, nn;
-    int node, sp;
+    int node;
     uint16_t lp;
     uint4 ent;
     uint32_t el[MF_EC / MF_PASS];
@@ -214,11 +214,9 @@ __device__ __forceinline__ void mf_pf1(const MfOp& op, int64_t c, MfPf<BS>& f) {
     f.s0 = op.sbase[c];
     f.nn = op.sbase[c + 1] - f.s0;
     f.node = 0;
-    f.sp = 0;   // every field defined in every lane: the copies of the software pipeline read them all
     f.lp = 0;
     if (tid < f.nn) {
         f.node = op.cnode[f.s0 + tid];
-        f.sp = op.spos ? op.spos[f.s0 + tid] : f.s0 + tid;
         f.lp = op.lptr[f.s0 + c + tid];
     }
     f.ent = make_uint4(0, 0, 0, 0);
@@ -277,6 +275,11 @@ __device__ __forceinline__ double mf_walk(const MfOp& op, const double* __restri
         const bool has2 = has1 && k2 < per && base + k2 < op.nchunks;
         if (has1) mf_pf2<BS, MODE>(op, x, n1);
         if (has2) mf_pf1<BS>(op, base + k2, n2);
+        // where this thread's slot is stored (node-major or chunk-major), read under the chunk's work -- not carried in
+        // the prefetch record (a slot position carried there through the record copies was measured wrong in some
+        // lanes when workgroups walked more than one chunk; the chunk's own base is)
+        int spc = 0;
+        if (tid < cur.nn) spc = op.spos ? op.spos[cur.s0 + tid] : cur.s0 + tid;
         __syncthreads();
         double acc[BS];
 #pragma unroll
@@ -355,7 +358,7 @@ __device__ __forceinline__ double mf_walk(const MfOp& op, const double* __restri
         if (tid < cur.nn) {
 #pragma unroll
             for (int q = 0; q < BS; ++q) {
-                slots[(int64_t)cur.sp * BS + q] = acc[q];
+                slots[(int64_t)spc * BS + q] = acc[q];
                 if constexpr (MODE == MF_DOT) dot += cur.pv[q] * acc[q];
             }
         }
@@ -388,7 +391,7 @@ __device__ __forceinline__ void mf_wave_sync() {
 template <int BS>
 struct MfPfW {
     int e0, ne, s0, nn;
-    int node, sp;
+    int node;
     uint16_t lp;
     uint2 ent;
     uint32_t el;
@@ -403,11 +406,9 @@ __device__ __forceinline__ void mf_pfw1(const MfOp& op, int64_t c, MfPfW<BS>& f)
     f.s0 = __builtin_amdgcn_readfirstlane(op.sbase[c]);
     f.nn = __builtin_amdgcn_readfirstlane(op.sbase[c + 1]) - f.s0;
     f.node = 0;
-    f.sp = 0;   // every field defined in every lane: the copies of the software pipeline read them all
     f.lp = 0;
     if (lane < f.nn) {
         f.node = op.cnode[f.s0 + lane];
-        f.sp = op.spos ? op.spos[f.s0 + lane] : f.s0 + lane;
         f.lp = op.lptr[f.s0 + c + lane];
     }
     f.ent = make_uint2(0, 0);
@@ -461,6 +462,8 @@ __device__ __forceinline__ double mf_walk_w(const MfOp& op, const double* __rest
         const bool has2 = has1 && k2 < per && base + k2 < op.nchunks;
         if (has1) mf_pfw2<BS, MODE>(op, x, n1);
         if (has2) mf_pfw1<BS>(op, base + k2, n2);
+        int spc = 0;   // this lane's slot position (see mf_walk)
+        if (lane < cur.nn) spc = op.spos ? op.spos[cur.s0 + lane] : cur.s0 + lane;
         mf_wave_sync();
         if (lane < cur.ne) {
             const uint32_t w = cur.el;
@@ -529,7 +532,7 @@ __device__ __forceinline__ double mf_walk_w(const MfOp& op, const double* __rest
             }
 #pragma unroll
             for (int q = 0; q < BS; ++q) {
-                slots[(int64_t)cur.sp * BS + q] = acc[q];
+                slots[(int64_t)spc * BS + q] = acc[q];
                 if constexpr (MODE == MF_DOT) dot += cur.pv[q] * acc[q];
             }
         }
