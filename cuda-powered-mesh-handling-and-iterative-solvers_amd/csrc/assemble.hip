@@ -337,6 +337,166 @@ __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, co
   }
 }
 
+template <int NPE, bool MASS>
+__global__ void __launch_bounds__(256) k_iso_ke1(const double* __restrict__ X, const int64_t* __restrict__ conn,
+                                                int64_t M, double E, double nu, const double* __restrict__ dN,
+                                                const double* __restrict__ w, int n_ip, int mode,
+                                                double* __restrict__ Ke, const double* __restrict__ Nv = nullptr) {
+    // (the one-element-per-wave form: c3d8 / c3d6, whose cheaper elements ran 5-7 % slower in the walking k_iso_ke)
+    // Wave per element, 4 per block. Per chunk of up to ISO_IPC points, lane q of a wave forms the Jacobian,
+    // detJ and the global gradients of point q (`einsum("ji,mjk->mik")`, `einsum("mij,nj->mni")`) into LDS —
+    // all points of the chunk at once, one barrier — then lane (a,b), a <= b, adds the 3x3 block of every point
+    // in point order. c3d10 (100 blocks > 64 lanes): only a <= b, block (b,a) written as its transpose (K_e =
+    // sum B^T D B is symmetric; mirrored entries equal the directly formed ones up to the order of two products),
+    // 55 blocks, one per lane. c3d8 / c3d6 (<= 64 blocks): every block formed directly.
+    // mode FEM_ISO_MASS (E = rho, Nv = shape values [n_ip][NPE]): block (a,b) = rho sum_q w_q |detJ_q| N_a N_b I3.
+    constexpr int D = 3 * NPE;
+    constexpr bool SYM = NPE * NPE > 64;
+    constexpr int NS = SYM ? NPE * (NPE + 1) / 2 : NPE * NPE;
+    static_assert(NS <= 64, "one block per lane");
+    // rule tables in dynamic LDS sized to the rule (n_ip NPE 3 natural derivatives, then n_ip NPE shape values)
+    extern __shared__ double iso_dyn[];
+    double* dn_s = iso_dyn;
+    double* nv_s = iso_dyn + n_ip * NPE * 3;
+    __shared__ double x_s[4][NPE][3];
+    // point gradients of the current chunk; after the last chunk the same space stages the element matrix so
+    // that the wave writes it out as contiguous 16-byte stores
+    constexpr int GK = (ISO_IPC * NPE * 3 > D * D) ? ISO_IPC * NPE * 3 : D * D;
+    __shared__ double gk_s[4][GK];
+    __shared__ double c_s[4][ISO_IPC];
+    constexpr bool mass = MASS;   // mode == FEM_ISO_MASS
+    for (int t = threadIdx.x; t < n_ip * NPE * 3; t += 256) dn_s[t] = dN[t];
+    if (mass)
+        for (int t = threadIdx.x; t < n_ip * NPE; t += 256) nv_s[t] = Nv[t];
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t e = (int64_t)blockIdx.x * 4 + wid;
+    const bool active = e < M;
+    if (active && lane < NPE * 3) {
+        int a = lane / 3, k = lane - 3 * (lane / 3);
+        x_s[wid][a][k] = X[3 * conn[e * NPE + a] + k];
+    }
+    __syncthreads();
+    const Lame L = lame(E, nu);
+    int ba = 0, bb = 0;   // this lane's block (SYM: ba <= bb), lane < NS
+    if (SYM) {
+        int t = lane;
+        while (ba < NPE && t >= NPE - ba) {
+            t -= NPE - ba;
+            ++ba;
+        }
+        bb = ba + t;
+    } else {
+        ba = lane / NPE;
+        bb = lane - NPE * (lane / NPE);
+    }
+    const bool mirror = SYM && ba != bb;
+    const bool blk_lane = lane < NS;
+    double acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[t] = 0.0;
+
+    double vol = 0.0;
+    if (mode == FEM_ISO_VOLUME) {  // wedge volume: 3 sub-tets (`solver/element.py:2198-2232`)
+        const int T[3][4] = {{0, 1, 2, 3}, {1, 2, 4, 3}, {2, 4, 5, 3}};
+        for (int s = 0; s < 3; ++s) {
+            double u[3], v[3], d[3];
+            for (int k = 0; k < 3; ++k) {
+                u[k] = x_s[wid][T[s][1]][k] - x_s[wid][T[s][0]][k];
+                v[k] = x_s[wid][T[s][2]][k] - x_s[wid][T[s][0]][k];
+                d[k] = x_s[wid][T[s][3]][k] - x_s[wid][T[s][0]][k];
+            }
+            double cx = u[1] * v[2] - u[2] * v[1], cy = u[2] * v[0] - u[0] * v[2], cz = u[0] * v[1] - u[1] * v[0];
+            vol += fabs(cx * d[0] + cy * d[1] + cz * d[2]) / 6.0;
+        }
+    }
+
+    for (int q0 = 0; q0 < n_ip; q0 += ISO_IPC) {
+        const int nq = min(ISO_IPC, n_ip - q0);
+        if (lane < nq) {
+            const int q = q0 + lane;
+            const double* dq = dn_s + q * NPE * 3;
+            double J[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll 1
+            for (int j = 0; j < NPE; ++j) {   // node order j ascending for every entry, as the einsum loop
+                const double d[3] = {dq[j * 3], dq[j * 3 + 1], dq[j * 3 + 2]};
+                const double xx[3] = {x_s[wid][j][0], x_s[wid][j][1], x_s[wid][j][2]};
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) J[3 * i + k] += d[i] * xx[k];
+            }
+            const double c00 = J[4] * J[8] - J[5] * J[7], c01 = J[5] * J[6] - J[3] * J[8],
+                         c02 = J[3] * J[7] - J[4] * J[6];
+            const double det = J[0] * c00 + J[1] * c01 + J[2] * c02;
+            const double id = 1.0 / det;
+            const double Ji[9] = {c00 * id, (J[2] * J[7] - J[1] * J[8]) * id, (J[1] * J[5] - J[2] * J[4]) * id,
+                                  c01 * id, (J[0] * J[8] - J[2] * J[6]) * id, (J[2] * J[3] - J[0] * J[5]) * id,
+                                  c02 * id, (J[1] * J[6] - J[0] * J[7]) * id, (J[0] * J[4] - J[1] * J[3]) * id};
+#pragma unroll 1
+            for (int n = 0; n < NPE; ++n)
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+                    gk_s[wid][(lane * NPE + n) * 3 + i] =
+                        Ji[3 * i] * dq[n * 3] + Ji[3 * i + 1] * dq[n * 3 + 1] + Ji[3 * i + 2] * dq[n * 3 + 2];
+            c_s[wid][lane] = mass ? fabs(det) * w[q] * E
+                                  : (mode == FEM_ISO_SUM) ? det * w[q] : (mode == FEM_ISO_STACK ? det : vol);
+        }
+        __syncthreads();
+        for (int ql = 0; ql < nq; ++ql) {
+            const double coef = c_s[wid][ql];
+            if (mass) {
+                if (blk_lane) {
+                    const double s = nv_s[(q0 + ql) * NPE + ba] * nv_s[(q0 + ql) * NPE + bb] * coef;
+                    acc[0] += s;
+                    acc[4] += s;
+                    acc[8] += s;
+                }
+            } else if (blk_lane) {
+                const double* ga = &gk_s[wid][(ql * NPE + ba) * 3];
+                const double* gb = &gk_s[wid][(ql * NPE + bb) * 3];
+                const double dot = ga[0] * gb[0] + ga[1] * gb[1] + ga[2] * gb[2];
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        double s = L.lam * ga[i] * gb[k] + L.mu * ga[k] * gb[i];
+                        if (i == k) s += L.mu * dot;
+                        if (mode == FEM_ISO_STACK) acc[3 * i + k] = s * coef;
+                        else acc[3 * i + k] += s * coef;
+                    }
+            }
+            if (mode == FEM_ISO_STACK && active && blk_lane) {
+                double* out = Ke + ((int64_t)(q0 + ql) * M + e) * D * D;
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        out[(3 * ba + i) * D + 3 * bb + k] = acc[3 * i + k];
+                        if (mirror) out[(3 * bb + k) * D + 3 * ba + i] = acc[3 * i + k];
+                    }
+            }
+        }
+        __syncthreads();
+    }
+    if (mode != FEM_ISO_STACK && active) {   // (the loop above ended on a barrier: gk_s is free)
+        double* ks = gk_s[wid];
+        if (blk_lane) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    ks[(3 * ba + i) * D + 3 * bb + k] = acc[3 * i + k];
+                    if (mirror) ks[(3 * bb + k) * D + 3 * ba + i] = acc[3 * i + k];
+                }
+        }
+        __builtin_amdgcn_wave_barrier();
+        // D*D is even for every NPE here, and e * D * D * 8 bytes is 16-byte aligned
+        double2* out2 = reinterpret_cast<double2*>(Ke + e * D * D);
+        const double2* ks2 = reinterpret_cast<const double2*>(ks);
+        for (int t = lane; t < D * D / 2; t += 64) out2[t] = ks2[t];
+    }
+}
+
 // ---------------------------------------------------------------- SELL value addressing
 // entry index E = slice_ptr[s] + 64 k + lane  ->  value index of block entry rc (row-major in the block)
 __device__ __forceinline__ int64_t sell_val(int64_t E, int bs2, int rc) {
@@ -1620,12 +1780,11 @@ int fem_iso_ke(const double* coords, const int64_t* conn, int64_t M, int npe, do
         return FEM_EARG;
     }
     const size_t lds = sizeof(double) * (size_t)n_ip * npe * 3;
-    const void* fn = npe == 6 ? (const void*)k_iso_ke<6, false> : npe == 8 ? (const void*)k_iso_ke<8, false>
-                                                                            : (const void*)k_iso_ke<10, false>;
+    const void* fn = (const void*)k_iso_ke<10, false>;   // the walking grid (c3d10 only, iso_grid_npe)
     const dim3 g(iso_grid_npe(fn, lds, M, npe));
     switch (npe) {
-        case 6: hipLaunchKernelGGL((k_iso_ke<6, false>), g, dim3(256), lds, S(stream), coords, conn, M, E, nu, dN, w, n_ip, mode, Ke); break;
-        case 8: hipLaunchKernelGGL((k_iso_ke<8, false>), g, dim3(256), lds, S(stream), coords, conn, M, E, nu, dN, w, n_ip, mode, Ke); break;
+        case 6: hipLaunchKernelGGL((k_iso_ke1<6, false>), g, dim3(256), lds, S(stream), coords, conn, M, E, nu, dN, w, n_ip, mode, Ke); break;
+        case 8: hipLaunchKernelGGL((k_iso_ke1<8, false>), g, dim3(256), lds, S(stream), coords, conn, M, E, nu, dN, w, n_ip, mode, Ke); break;
         case 10: hipLaunchKernelGGL((k_iso_ke<10, false>), g, dim3(256), lds, S(stream), coords, conn, M, E, nu, dN, w, n_ip, mode, Ke); break;
         default: set_error("fem_iso_ke: unsupported nodes per element %d", npe); return FEM_EBADTYPE;
     }
@@ -1642,12 +1801,11 @@ int fem_iso_mass(const double* coords, const int64_t* conn, int64_t M, int npe, 
     }
     const int mode = FEM_ISO_MASS;
     const size_t lds = sizeof(double) * (size_t)n_ip * npe * 4;
-    const void* fn = npe == 6 ? (const void*)k_iso_ke<6, true> : npe == 8 ? (const void*)k_iso_ke<8, true>
-                                                                           : (const void*)k_iso_ke<10, true>;
+    const void* fn = (const void*)k_iso_ke<10, true>;   // the walking grid (c3d10 only, iso_grid_npe)
     const dim3 g(iso_grid_npe(fn, lds, M, npe));
     switch (npe) {
-        case 6: hipLaunchKernelGGL((k_iso_ke<6, true>), g, dim3(256), lds, S(stream), coords, conn, M, rho, 0.0, dN, w, n_ip, mode, Me, Nv); break;
-        case 8: hipLaunchKernelGGL((k_iso_ke<8, true>), g, dim3(256), lds, S(stream), coords, conn, M, rho, 0.0, dN, w, n_ip, mode, Me, Nv); break;
+        case 6: hipLaunchKernelGGL((k_iso_ke1<6, true>), g, dim3(256), lds, S(stream), coords, conn, M, rho, 0.0, dN, w, n_ip, mode, Me, Nv); break;
+        case 8: hipLaunchKernelGGL((k_iso_ke1<8, true>), g, dim3(256), lds, S(stream), coords, conn, M, rho, 0.0, dN, w, n_ip, mode, Me, Nv); break;
         case 10: hipLaunchKernelGGL((k_iso_ke<10, true>), g, dim3(256), lds, S(stream), coords, conn, M, rho, 0.0, dN, w, n_ip, mode, Me, Nv); break;
         default: set_error("fem_iso_mass: unsupported nodes per element %d", npe); return FEM_EBADTYPE;
     }

@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--kind", default="elastic")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--no-assembled", action="store_true")
+    ap.add_argument("--graph", type=int, default=0, help="also time the iterations replayed from a hipGraph of k")
     ap.add_argument("--tune-extra", type=int, default=int(os.environ.get("FEM355_PROBE_TUNE", "0")),
                     help="FEM_TUNE_* flags added to the library default (e.g. 8192: q by a gather launch)")
     a = ap.parse_args()
@@ -81,6 +82,16 @@ def main():
     dt = (time.perf_counter() - t0) / a.iters
     out["iter_ms"] = dt * 1e3
     out["it_per_s"] = 1.0 / dt
+    if a.graph:
+        run.use_graph(a.graph)
+        run.iterate(a.graph)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run.iterate(a.iters)
+        run.poll()
+        dt = (time.perf_counter() - t0) / a.iters
+        out["graph_iter_ms"] = dt * 1e3
+        out["graph_it_per_s"] = 1.0 / dt
     run.close()
     print(json.dumps(out))
 
