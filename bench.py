@@ -59,8 +59,9 @@ def parse():
     ap.add_argument("--elastic", type=int, default=1,
                     help="poisson runs: also measure the 10M-tet linear-elasticity system (BASELINE configs[2]/[3]) "
                          "with the same steps, reported under \"elasticity\" in the same JSON line")
-    ap.add_argument("--mf-graph", type=int, default=1,
-                    help="matrix-free companion: time hipGraph replays (1) or plain launches (0)")
+    ap.add_argument("--mf-graph", type=int, default=0,
+                    help="matrix-free companion: time hipGraph replays (1; measured equal to plain launches: the "
+                         "~11 us between the two kernels of an iteration is device-side) or plain launches (0)")
     ap.add_argument("--matfree", type=int, default=1,
                     help="elasticity companion: also the element-chunk (matrix-free) operator, under \"matfree\"")
     ap.add_argument("--elastic-timeout", type=float, default=240.0,
