@@ -19,7 +19,6 @@ try:
     from .element import *  # noqa: F401,F403  (the reference's `from element import *`)
     from .element import _dev, _key, cached_incidence, compute_c3d4_K_matrix, compute_c3d6_K_matrix, \
         compute_c3d8_K_matrix
-    from .shell import *  # noqa: F401,F403
     from .constraints import *  # noqa: F401,F403
     from .constraints import ConstraintSet
 except ImportError:  # pragma: no cover - flat import from the package directory
@@ -28,7 +27,6 @@ except ImportError:  # pragma: no cover - flat import from the package directory
     from element import *  # type: ignore # noqa
     from element import _dev, _key, cached_incidence, compute_c3d4_K_matrix, compute_c3d6_K_matrix, \
         compute_c3d8_K_matrix  # type: ignore
-    from shell import *  # type: ignore # noqa
     from constraints import *  # type: ignore # noqa
     from constraints import ConstraintSet  # type: ignore
 
