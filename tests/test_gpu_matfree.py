@@ -228,6 +228,36 @@ def test_update_fused_q_bit_identical(gpu, kind):
     assert all(torch.equal(xs[0], v) for v in xs[1:])
 
 
+def test_update_give_up_is_all_or_nothing(gpu):
+    """The merged update on the element-chunk operator shares k_pcg_update2's release protocol (u2_release): with
+    workgroup 0 held back past every other workgroup's wait (FEM_TUNE_U2_HOLD) the launch ends with
+    FEM_PCG_SYNC_TIMEOUT at give-up site 4 (+ 16 x launch) and no workgroup's x update."""
+    import ctypes
+    mesh, _, system = _mods()
+    from fem355 import _capi as C
+    c, t = mesh.kuhn_cube(12, jitter=0.1)
+    f, fixed = mesh.cube_elasticity_case(c)
+    A = system.MatFreeOperator(c.to(gpu), t.to(gpu), "elastic", E, NU)
+    mask = torch.zeros((c.shape[0], 3), dtype=torch.uint8, device=gpu)
+    mask[fixed.to(gpu)] = 1
+    w = A.jacobi(mask.view(-1))
+    x0 = torch.randn(A.n, dtype=F64, generator=torch.Generator().manual_seed(5)).to(gpu)
+    run = system.PcgRunner(A, f.reshape(-1), w, x0=x0, tol=0.0)
+    try:
+        run.set_tuning(C.TUNE_DEFAULT | C.TUNE_U2_HOLD)
+        run.start()
+        run.iterate(3)
+        it, stt, rz = ctypes.c_int(), ctypes.c_int(), ctypes.c_double()
+        C.check(run.lib.fem_pcg_poll(run.h, ctypes.byref(it), ctypes.byref(stt), ctypes.byref(rz)), "poll")
+        site = ctypes.c_int()
+        C.check(run.lib.fem_pcg_sync_site(run.h, ctypes.byref(site)), "site")
+        assert stt.value == C.PCG_SYNC_TIMEOUT and it.value == 0, (it.value, stt.value)
+        assert site.value == 4 + 16 * 1, site.value
+        assert torch.equal(run.x, x0)
+    finally:
+        run.close()
+
+
 def test_config2_matfree_10m_operator_and_iterates_vs_oracle(gpu, cube119):
     """BASELINE configs[2] (10,110,954 tets, 5,184,000 DOFs) on the matrix-free operator: the operator on a seeded
     vector against the oracle's EBE product over its element matrices at 1e-12, the exact Jacobi weights at 1e-14,
