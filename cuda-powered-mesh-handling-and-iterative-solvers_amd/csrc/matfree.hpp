@@ -18,6 +18,19 @@
 
 namespace fem {
 
+// slot stores (FEM_MF_NT = 1: non-temporal, the merged update reads them once after the kernel boundary)
+#ifndef FEM_MF_NT
+#define FEM_MF_NT 0
+#endif
+__device__ __forceinline__ void mf_store_slot(double* p, double v) {
+#if FEM_MF_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
+
 // Chunk geometry. FEM_MF_WAVE (default): a chunk per WAVE -- <= 64 elements / <= 64 nodes (pieces of 16 elements when
 // more), every wave of a workgroup walking its own chunks with no workgroup barrier, ~10 KB of LDS per wave. Else a
 // chunk per workgroup: <= 512 elements / <= 256 nodes (pieces of 64), two passes of 256 elements, 41.6 KB per
@@ -358,7 +371,7 @@ __device__ __forceinline__ double mf_walk(const MfOp& op, const double* __restri
         if (tid < cur.nn) {
 #pragma unroll
             for (int q = 0; q < BS; ++q) {
-                slots[(int64_t)spc * BS + q] = acc[q];
+                mf_store_slot(&slots[(int64_t)spc * BS + q], acc[q]);
                 if constexpr (MODE == MF_DOT) dot += cur.pv[q] * acc[q];
             }
         }
@@ -532,7 +545,7 @@ __device__ __forceinline__ double mf_walk_w(const MfOp& op, const double* __rest
             }
 #pragma unroll
             for (int q = 0; q < BS; ++q) {
-                slots[(int64_t)spc * BS + q] = acc[q];
+                mf_store_slot(&slots[(int64_t)spc * BS + q], acc[q]);
                 if constexpr (MODE == MF_DOT) dot += cur.pv[q] * acc[q];
             }
         }

@@ -673,6 +673,9 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update2(int64_t n, double* __
 // The merged update on the element-chunk operator, one node (BS dofs) per thread-step: q of the node is the sum of
 // its slots in ascending chunk order (k_mf_gather's sum; FROM_Q: read from q written by k_mf_gather instead, the A/B
 // form -- same order of every sum, the same bits), so q is never stored. The release protocol is k_pcg_update2's.
+#ifndef FEM_MF_NTL
+#define FEM_MF_NTL 0   // 1: the merged update reads the slots with non-temporal loads (read once)
+#endif
 constexpr int U2_NPN = 6;   // nodes per thread whose z stays in registers
 template <int BS, bool FROM_Q>
 __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update2_mf(int64_t nn, double* __restrict__ x, double* __restrict__ p,
@@ -709,7 +712,13 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update2_mf(int64_t nn, double
             for (int k = k0; k < k1; ++k) {
                 const int64_t sl = op.spos ? k : op.nslot[k];
 #pragma unroll
-                for (int c = 0; c < BS; ++c) qv[c] += slots[sl * BS + c];
+                for (int c = 0; c < BS; ++c) {
+#if FEM_MF_NTL
+                    qv[c] += __builtin_nontemporal_load(&slots[sl * BS + c]);
+#else
+                    qv[c] += slots[sl * BS + c];
+#endif
+                }
             }
         }
         double s = 0.0;
