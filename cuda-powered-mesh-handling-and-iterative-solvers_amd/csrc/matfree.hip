@@ -6,8 +6,8 @@
 //      most 10 bits per axis), the connectivity range check
 //      and the singular check (|det| < 1e-12, `solver/element.py:857-858`, the smallest such element reported);
 //   2. elements sorted by key (stable radix sort: equal keys keep their file order);
-//   3. chunks of MF_EC consecutive sorted elements; a chunk touching more than MF_NC nodes is cut into pieces of
-//      MF_PIECE elements (<= MF_NC nodes each, always);
+//   3. chunks of MF_EC consecutive sorted elements; a chunk touching more than MF_NC nodes is halved, and each half
+//      that still does halved again, down to MF_PIECE elements (<= MF_NC nodes each, always);
 //   4. per chunk (one workgroup): the (node << 11 | element << 2 | corner) keys of its 4 ne corners sorted in LDS, the
 //      local node list, the node-major pair list and every element's 4 local ids;
 //   5. node -> slots: the (node, slot) pairs sorted by node (stable: slots ascend within a node).
@@ -184,27 +184,27 @@ __device__ __forceinline__ int mf_block_scan(int v, int* sc, int* total) {
     return incl - v;
 }
 
-__device__ __forceinline__ void mf_chunk_range(const int32_t* cptr, int64_t c, int64_t M, int* e0, int* ne) {
+__device__ __forceinline__ void mf_chunk_range(const int32_t* cptr, int64_t c, int64_t M, int ec, int* e0, int* ne) {
     if (cptr) {
         *e0 = cptr[c];
         *ne = cptr[c + 1] - cptr[c];
     } else {
-        const int64_t a = c * MF_EC;
+        const int64_t a = c * ec;
         *e0 = (int)a;
-        *ne = (int)((M - a) < MF_EC ? (M - a) : MF_EC);
+        *ne = (int)((M - a) < ec ? (M - a) : ec);
     }
 }
 
-// local node count of every chunk (cptr null: uniform chunks of MF_EC)
+// local node count of every chunk (cptr null: uniform chunks of ec <= MF_EC elements)
 __global__ void __launch_bounds__(256) k_mf_count(const int64_t* __restrict__ conn, const int32_t* __restrict__ order,
                                                   int64_t M, const int32_t* __restrict__ cptr, int64_t nchunks,
-                                                  int32_t* __restrict__ count) {
+                                                  int32_t* __restrict__ count, int ec) {
     __shared__ uint32_t s[MF_SORT];
     __shared__ int sc[256];
     const int64_t c = blockIdx.x;
     if (c >= nchunks) return;
     int e0, ne;
-    mf_chunk_range(cptr, c, M, &e0, &ne);
+    mf_chunk_range(cptr, c, M, ec, &e0, &ne);
     for (int k = threadIdx.x; k < MF_SORT; k += 256)
         s[k] = k < 4 * ne ? (uint32_t)conn[4 * (int64_t)order[e0 + (k >> 2)] + (k & 3)] : 0xffffffffu;
     __syncthreads();
@@ -416,25 +416,45 @@ int fem_mf_create(const double* coords, const int64_t* conn, int64_t M, int64_t 
         MF_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys2, ids, m->eorder, (int)M, 0, 30, st));
         (void)hipFree(tmp);
         tmp = nullptr;
-        // chunk sizes: uniform MF_EC, then pieces of MF_PIECE (4 MF_PIECE <= MF_NC nodes) for chunks touching more
-        const int64_t nc0 = cdiv(M, MF_EC);
-        int32_t* cnt = ids;   // reused (nc0 <= M)
-        hipLaunchKernelGGL(k_mf_count, dim3((unsigned)nc0), dim3(256), 0, st, conn, m->eorder, M, (const int32_t*)nullptr,
-                           nc0, cnt);
-        MF_TRY(hipGetLastError());
-        std::vector<int32_t> hc((size_t)nc0);
-        MF_TRY(hipMemcpyAsync(hc.data(), cnt, sizeof(int32_t) * (size_t)nc0, hipMemcpyDeviceToHost, st));
-        MF_TRY(hipStreamSynchronize(st));
-        std::vector<int32_t> hcp;
-        hcp.reserve((size_t)nc0 + 1);
+        // chunk sizes: uniform MF_EC; a chunk touching more than MF_NC nodes is halved, a half that still does
+        // halved again, down to MF_PIECE (4 MF_PIECE <= MF_NC nodes). The node counts of the uniform chunkings of
+        // MF_EC >> l elements, level by level while some chunk of the level above is over (hcl[l]).
+        int32_t* cnt = ids;   // reused (chunks <= M)
+        constexpr int LMAX = [] { int l = 0; while ((MF_EC >> l) > MF_PIECE) ++l; return l; }();
+        std::vector<std::vector<int32_t>> hcl;
+        for (int l = 0; l <= LMAX; ++l) {
+            const int ec = MF_EC >> l;
+            const int64_t ncl = cdiv(M, ec);
+            hipLaunchKernelGGL(k_mf_count, dim3((unsigned)ncl), dim3(256), 0, st, conn, m->eorder, M,
+                               (const int32_t*)nullptr, ncl, cnt, ec);
+            MF_TRY(hipGetLastError());
+            hcl.emplace_back((size_t)ncl);
+            MF_TRY(hipMemcpyAsync(hcl.back().data(), cnt, sizeof(int32_t) * (size_t)ncl, hipMemcpyDeviceToHost, st));
+            MF_TRY(hipStreamSynchronize(st));
+            bool over = false;
+            for (int32_t v : hcl.back()) over |= v > MF_NC;
+            if (!over) break;
+        }
+        std::vector<int32_t> hcp, hn;
+        hcp.reserve((size_t)hcl[0].size() + 1);
+        hn.reserve((size_t)hcl[0].size());
         bool split = false;
-        for (int64_t c = 0; c < nc0; ++c) {
-            const int64_t a = c * MF_EC, ne = (M - a) < MF_EC ? (M - a) : MF_EC;
-            if (hc[(size_t)c] <= MF_NC) {
+        // emit level-l chunk idx: whole if it fits (or is a piece), else its two halves of level l + 1
+        std::vector<std::pair<int, int64_t>> todo;
+        for (int64_t c = (int64_t)hcl[0].size() - 1; c >= 0; --c) todo.emplace_back(0, c);
+        while (!todo.empty()) {
+            const auto [l, idx] = todo.back();
+            todo.pop_back();
+            const int64_t a = idx * (int64_t)(MF_EC >> l);
+            if (a >= M) continue;
+            const int32_t nodes = hcl[(size_t)l][(size_t)idx];
+            if (nodes <= MF_NC || l == LMAX || l + 1 >= (int)hcl.size()) {
                 hcp.push_back((int32_t)a);
+                hn.push_back(nodes);
+                split |= l > 0;
             } else {
-                split = true;
-                for (int64_t b = 0; b < ne; b += MF_PIECE) hcp.push_back((int32_t)(a + b));
+                todo.emplace_back(l + 1, 2 * idx + 1);
+                todo.emplace_back(l + 1, 2 * idx);
             }
         }
         hcp.push_back((int32_t)M);
@@ -443,16 +463,7 @@ int fem_mf_create(const double* coords, const int64_t* conn, int64_t M, int64_t 
         MF_TRY(hipMalloc(&m->cptr, sizeof(int32_t) * (size_t)(nch + 1)));
         MF_TRY(hipMalloc(&m->sbase, sizeof(int32_t) * (size_t)(nch + 1)));
         MF_TRY(hipMemcpyAsync(m->cptr, hcp.data(), sizeof(int32_t) * (size_t)(nch + 1), hipMemcpyHostToDevice, st));
-        std::vector<int32_t> hn;
-        if (split) {
-            hipLaunchKernelGGL(k_mf_count, dim3((unsigned)nch), dim3(256), 0, st, conn, m->eorder, M, m->cptr, nch, cnt);
-            MF_TRY(hipGetLastError());
-            hn.resize((size_t)nch);
-            MF_TRY(hipMemcpyAsync(hn.data(), cnt, sizeof(int32_t) * (size_t)nch, hipMemcpyDeviceToHost, st));
-            MF_TRY(hipStreamSynchronize(st));
-        } else {
-            hn = hc;
-        }
+        (void)split;
         std::vector<int32_t> hs((size_t)nch + 1);
         int64_t tot = 0;
         for (int64_t c = 0; c < nch; ++c) {
