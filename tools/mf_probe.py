@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--kind", default="elastic")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--no-assembled", action="store_true")
+    ap.add_argument("--rotate", type=float, default=0.0,
+                    help="rotate the cube by this many degrees about (1,1,2) (Morton cells no longer on its hexes)")
     ap.add_argument("--graph", type=int, default=0, help="also time the iterations replayed from a hipGraph of k")
     ap.add_argument("--tune-extra", type=int, default=int(os.environ.get("FEM355_PROBE_TUNE", "0")),
                     help="FEM_TUNE_* flags added to the library default (e.g. 8192: q by a gather launch)")
@@ -43,9 +45,18 @@ def main():
     C.lib()
     dev = torch.device("cuda", 0)
     c, t = mesh.kuhn_cube(a.n, device=dev)
+    c0 = c   # the load case on the cube's own faces
+    if a.rotate:
+        import math
+        k = torch.tensor([1.0, 1.0, 2.0], dtype=torch.float64, device=dev)
+        k = k / k.norm()
+        th = math.radians(a.rotate)
+        K = torch.tensor([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]], dtype=torch.float64, device=dev)
+        Rm = torch.eye(3, dtype=torch.float64, device=dev) + math.sin(th) * K + (1 - math.cos(th)) * (K @ K)
+        c = (c @ Rm.T).contiguous()
     N = c.shape[0]
     Ek = E if a.kind == "elastic" else 1.0
-    out = {"n": a.n, "kind": a.kind, "tets": t.shape[0], "nodes": N}
+    out = {"n": a.n, "kind": a.kind, "tets": t.shape[0], "nodes": N, "rotate_deg": a.rotate}
     for _ in range(2):
         ms, A = ev(lambda: system.MatFreeOperator(c, t, a.kind, Ek, NU))
     out["mf_build_ms"] = ms
@@ -59,10 +70,12 @@ def main():
         out["asm_ms"] = ms
         ys = As.matvec(x)
         out["rel_vs_assembled"] = float((y - ys).abs().max() / ys.abs().max())
+        out["max_abs"] = [float(y.abs().max()), float(ys.abs().max()), float((y - ys).abs().max())]
+        out["bitwise_equal_frac"] = float((y == ys).double().mean())
         ms, _ = ev(lambda: As.matvec(x, ys), reps=20)
         out["sell_spmv_ms"] = ms
         del As
-    f, fixed = mesh.cube_elasticity_case(c) if a.kind == "elastic" else mesh.cube_poisson_case(c)
+    f, fixed = mesh.cube_elasticity_case(c0) if a.kind == "elastic" else mesh.cube_poisson_case(c0)
     dpn = A.bs
     mask = torch.zeros((N, dpn), dtype=torch.uint8, device=dev)
     mask[fixed] = 1
