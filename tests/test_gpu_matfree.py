@@ -86,6 +86,42 @@ def test_operator_vs_oracle_ebe(gpu, name, kind):
         assert info["slots"] == 4 * t.shape[0]
 
 
+def test_halving_split(gpu):
+    """Chunks past the 256-node cap are halved, and halves still past it halved again, down to 64 elements
+    (fem_mf_create). A Kuhn cube rotated off the Morton grid with small disjoint tets scattered through it (4 nodes
+    of their own each): every chunk is an aligned power-of-two range of 64..512 elements (the last one may be short)
+    within the node cap, more than one chunk size occurs, and the operator matches the oracle's EBE product."""
+    import math
+    mesh, _, system = _mods()
+    c, t = mesh.kuhn_cube(16, jitter=0.1)
+    k = torch.tensor([1.0, 1.0, 2.0], dtype=F64)
+    k = k / k.norm()
+    th = math.radians(17.0)
+    K3 = torch.tensor([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]], dtype=F64)
+    Rm = torch.eye(3, dtype=F64) + math.sin(th) * K3 + (1 - math.cos(th)) * (K3 @ K3)
+    c = c @ Rm.T
+    g = torch.Generator().manual_seed(11)
+    m = 1500
+    base = c.min(0).values + torch.rand(m, 1, 3, generator=g, dtype=F64) * (c.max(0).values - c.min(0).values)
+    ref = torch.tensor([[0, 0, 0], [1, 0, 0], [0, 1, 0], [0, 0, 1]], dtype=F64)
+    small = (base + 0.01 * ref).reshape(-1, 3)
+    t = torch.cat([t, c.shape[0] + torch.arange(4 * m).view(m, 4)], 0)
+    c = torch.cat([c, small], 0).contiguous()
+    A = system.MatFreeOperator(c.to(gpu), t.to(gpu), "elastic", E, NU)
+    _, cp, sb, _ = A.layout()
+    cp, sb = cp.cpu().long(), sb.cpu().long()
+    M = t.shape[0]
+    sizes, nodes = (cp[1:] - cp[:-1]).tolist(), (sb[1:] - sb[:-1]).tolist()
+    assert int(cp[0]) == 0 and int(cp[-1]) == M
+    assert all(1 <= v <= 256 for v in nodes)
+    for a, s in zip(cp[:-1].tolist()[:-1], sizes[:-1]):
+        assert s in (64, 128, 256, 512) and a % s == 0, (a, s)
+    assert len(set(sizes[:-1])) >= 2, sorted(set(sizes))
+    x = torch.randn(c.shape[0], 3, dtype=F64, generator=torch.Generator().manual_seed(2))
+    Ke = R.tet4_K(c, t, E, NU)
+    assert rel(A.matvec(x.reshape(-1).to(gpu)), R.nodal_forces(Ke, t, x).reshape(-1)) < 1e-12
+
+
 @pytest.mark.parametrize("nodemajor", ["1", "0"])
 def test_chunk_walk_bit_identical(gpu, monkeypatch, nodemajor):
     """Workgroups walking many chunks (the software pipeline's rotation: three chunks in flight) give the same bits as
