@@ -32,7 +32,8 @@ struct fem_mf {
     int32_t* nptr = nullptr;
     int32_t* nslot = nullptr;
     int32_t* spos = nullptr;     // node-major slot positions (null: chunk-major slots)
-    double* slots = nullptr;     // [nslots * bs] scratch of every application
+    double* slots = nullptr;     // [nslots * bs] scratch of the stand-alone applications (fem_mf_apply / fem_mf_diag:
+                                 // one stream at a time); every (P)CG context has its own (fem_pcg_set_operator_mf)
     fem::MfOp op() const {
         fem::MfOp o{};
         o.nchunks = nchunks;
@@ -282,13 +283,15 @@ __global__ void __launch_bounds__(MF_BLOCK) k_mf_apply(MfOp op, const double* __
     (void)mf_walk_any<BS, MODE>(op, x, slots, L);
 }
 
-static int mf_run(fem_mf* m, int mode, const double* x, double* y, hipStream_t st) {
+// one application into y through the slot buffer `slots` ([nslots * bs]: the operator's own for the stand-alone
+// calls, a (P)CG context's own inside a solve, so applications on different streams never share scratch)
+static int mf_run(fem_mf* m, int mode, const double* x, double* y, double* slots, hipStream_t st) {
     const MfOp op = m->op();
     if (m->nchunks > 0) {
 #define FEM_MFA(B, MD)                                                                                              \
     hipLaunchKernelGGL((k_mf_apply<B, MD>),                                                                          \
                        dim3(mf_resident_grid((const void*)k_mf_apply<B, MD>, MF_BLOCK, m->nchunks)), dim3(MF_BLOCK), \
-                       0, st, op, x, m->slots)
+                       0, st, op, x, slots)
         if (m->bs == 3) {
             if (mode == MF_DIAG) FEM_MFA(3, MF_DIAG);
             else FEM_MFA(3, MF_APPLY);
@@ -300,8 +303,8 @@ static int mf_run(fem_mf* m, int mode, const double* x, double* y, hipStream_t s
         FEM_LAUNCHED();
     }
     if (m->N > 0) {
-        if (m->bs == 3) hipLaunchKernelGGL(k_mf_gather<3>, dim3(stream_grid(m->N, 256)), dim3(256), 0, st, op, m->slots, y);
-        else hipLaunchKernelGGL(k_mf_gather<1>, dim3(stream_grid(m->N, 256)), dim3(256), 0, st, op, m->slots, y);
+        if (m->bs == 3) hipLaunchKernelGGL(k_mf_gather<3>, dim3(stream_grid(m->N, 256)), dim3(256), 0, st, op, slots, y);
+        else hipLaunchKernelGGL(k_mf_gather<1>, dim3(stream_grid(m->N, 256)), dim3(256), 0, st, op, slots, y);
         FEM_LAUNCHED();
     }
     return FEM_OK;
@@ -312,7 +315,11 @@ MfOp mf_op(const fem_mf* m) { return m->op(); }
 double* mf_slots(const fem_mf* m) { return m->slots; }
 int mf_bs(const fem_mf* m) { return m->bs; }
 int64_t mf_nodes(const fem_mf* m) { return m->N; }
-int mf_apply(fem_mf* m, const double* x, double* y, hipStream_t st) { return mf_run(m, MF_APPLY, x, y, st); }
+int64_t mf_nslots(const fem_mf* m) { return m->nslots; }
+int mf_apply(fem_mf* m, const double* x, double* y, double* slots, hipStream_t st) {
+    return mf_run(m, MF_APPLY, x, y, slots, st);
+}
+int mf_diag(fem_mf* m, double* d, double* slots, hipStream_t st) { return mf_run(m, MF_DIAG, nullptr, d, slots, st); }
 
 static void mf_free(fem_mf* m) {
     if (!m) return;
@@ -529,7 +536,7 @@ int fem_mf_apply(fem_mf* m, const double* x, double* y, fem_stream_t stream) {
         set_error("fem_mf_apply: bad arguments");
         return FEM_EARG;
     }
-    return mf_run(m, MF_APPLY, x, y, S(stream));
+    return mf_run(m, MF_APPLY, x, y, m->slots, S(stream));
 }
 
 int fem_mf_diag(fem_mf* m, double* d, fem_stream_t stream) {
@@ -537,7 +544,7 @@ int fem_mf_diag(fem_mf* m, double* d, fem_stream_t stream) {
         set_error("fem_mf_diag: bad arguments");
         return FEM_EARG;
     }
-    return mf_run(m, MF_DIAG, nullptr, d, S(stream));
+    return mf_run(m, MF_DIAG, nullptr, d, m->slots, S(stream));
 }
 
 int fem_mf_info(fem_mf* m, int64_t* out6) {

@@ -89,7 +89,10 @@ MfOp mf_op(const fem_mf* m);
 double* mf_slots(const fem_mf* m);
 int mf_bs(const fem_mf* m);
 int64_t mf_nodes(const fem_mf* m);
-int mf_apply(fem_mf* m, const double* x, double* y, hipStream_t st);
+int64_t mf_nslots(const fem_mf* m);
+// y = K x / d = diag K through the caller's slot buffer ([mf_nslots * bs] doubles)
+int mf_apply(fem_mf* m, const double* x, double* y, double* slots, hipStream_t st);
+int mf_diag(fem_mf* m, double* d, double* slots, hipStream_t st);
 
 // 1 / x to full precision without the IEEE division sequence: v_rcp_f64 and two Newton steps (within an ulp)
 __device__ __forceinline__ double mf_rcp(double x) {
@@ -228,6 +231,11 @@ __device__ __forceinline__ void mf_pf1(const MfOp& op, int64_t c, MfPf<BS>& f) {
     f.nn = op.sbase[c + 1] - f.s0;
     f.node = 0;
     f.lp = 0;
+    // every field defined in every lane (the pipeline copies whole records; stage 2 fills xv / pv for tid < nn)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) f.xv[k] = 0.0;
+#pragma unroll
+    for (int k = 0; k < BS; ++k) f.pv[k] = 0.0;
     if (tid < f.nn) {
         f.node = op.cnode[f.s0 + tid];
         f.lp = op.lptr[f.s0 + c + tid];
@@ -420,6 +428,10 @@ __device__ __forceinline__ void mf_pfw1(const MfOp& op, int64_t c, MfPfW<BS>& f)
     f.nn = __builtin_amdgcn_readfirstlane(op.sbase[c + 1]) - f.s0;
     f.node = 0;
     f.lp = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) f.xv[k] = 0.0;
+#pragma unroll
+    for (int k = 0; k < BS; ++k) f.pv[k] = 0.0;
     if (lane < f.nn) {
         f.node = op.cnode[f.s0 + lane];
         f.lp = op.lptr[f.s0 + c + lane];

@@ -1844,6 +1844,7 @@ struct fem_pcg {
     unsigned* u2_sync;                    // [U2_WORDS]: release epoch, broadcast (beta, halt), give-up
     // element-chunk operator (fem_pcg_set_operator_mf): K1 = k_pcg_mf_dot + k_mf_gather instead of a SELL SpMV
     fem_mf* mf;
+    double* mf_sl;  // this context's slot buffer [nslots * bs] (no other context or stream writes it)
     int mf_qfuse;   // the merged update reads q from the slots (no gather launch); set per launch of K1 + update2
 };
 
@@ -1881,9 +1882,91 @@ __global__ void __launch_bounds__(MF_BLOCK) k_pcg_mf_dot(MfOp op, const double* 
     if (reduce_grid(dot, red.part(RED_K1), red.cnt(RED_K1), &pq, lds4, &flag) && threadIdx.x == 0) finish_pq(st, pq);
 }
 
+// Distributed single-reduction iteration on the element-chunk operator (BASELINE configs[3] as north_star puts it:
+// element partitions, the rank's own elements formed in every application, the halo-DOF partials exchanged inside the
+// iteration). Replaces k_cg1_spmv's SpMV by two launches: the rank's chunks into its slots (v = A_r u, never a matrix),
+// then the slot gather -- v per local node in ascending chunk order, d = u.v over all local rows (the rank partials of
+// an operator sum, as k_cg1_spmv's), the interface rows packed for the exchange, the step committed by the last block.
+// k_cg1_update then reads v like the assembled path's q.
+template <int BS>
+__global__ void __launch_bounds__(MF_BLOCK) k_cg1_mf_slots(MfOp op, const double* __restrict__ u,
+                                                           double* __restrict__ slots, const PcgState* __restrict__ st,
+                                                           int always, P2PArgs xp, const double* __restrict__ recv,
+                                                           const double* __restrict__ send, int64_t off) {
+    __shared__ MfKernelLds<BS, MF_APPLY> L;
+    if (!always) {   // the step of this pass, from the unchanged state (committed by k_cg1_mf_gather)
+        const Cg1Step k = cg1_eval(st, cg1_scalar(recv, send, off, 0, xp), cg1_scalar(recv, send, off, 1, xp));
+        if (!k.go) return;
+    }
+    (void)mf_walk_any<BS, MF_APPLY>(op, u, slots, L);
+}
+
+template <int BS>
+__global__ void __launch_bounds__(PCG_BLOCK) k_cg1_mf_gather(MfOp op, const double* __restrict__ slots,
+                                                             const double* __restrict__ u, double* __restrict__ v,
+                                                             const int32_t* __restrict__ ipos, double* __restrict__ send,
+                                                             int64_t off, PcgState* __restrict__ st, RedBuf red,
+                                                             int always, P2PArgs xp, const double* __restrict__ recv,
+                                                             double* hist, int64_t hist_len) {
+    __shared__ double lds4[4];
+    __shared__ int flag;
+    Cg1Step k{};
+    if (!always) {
+        k = cg1_eval(st, cg1_scalar(recv, send, off, 0, xp), cg1_scalar(recv, send, off, 1, xp));
+        if (!k.go) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) cg1_commit(st, k, hist, hist_len);
+            return;
+        }
+    }
+    double dot = 0.0;
+    for (int64_t a = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; a < op.nnodes;
+         a += (int64_t)gridDim.x * PCG_BLOCK) {
+        double o[BS];
+#pragma unroll
+        for (int c = 0; c < BS; ++c) o[c] = 0.0;
+        const int k0 = op.nptr[a], k1 = op.nptr[a + 1];
+        for (int kk = k0; kk < k1; ++kk) {
+            const int64_t sl = op.spos ? kk : op.nslot[kk];
+#pragma unroll
+            for (int c = 0; c < BS; ++c) o[c] += slots[sl * BS + c];
+        }
+        const int32_t j = ipos ? ipos[a] : -1;
+#pragma unroll
+        for (int c = 0; c < BS; ++c) {
+            v[a * BS + c] = o[c];
+            dot += u[a * BS + c] * o[c];
+            if (j >= 0) {
+                if (xp.P) {   // straight into every peer's message slot for this node
+                    for (int r = 0; r < xp.P; ++r) {
+                        const int dst = xp.csrc[(int64_t)j * xp.P + r];
+                        if (dst >= 0) xp.psend[dst + c] = o[c];
+                    }
+                } else {
+                    send[(int64_t)j * BS + c] = o[c];
+                }
+            }
+        }
+    }
+    dot = block_sum256(dot, lds4);
+    double d;
+    if (reduce_grid(dot, red.part(RED_K1), red.cnt(RED_K1), &d, lds4, &flag) && threadIdx.x == 0) {
+        if (!always) cg1_commit(st, k, hist, hist_len);   // every block of the three kernels has read the state
+        st->red[0] = d;
+        send[off] = st->red[1];
+        send[off + 1] = d;
+        for (int r = 0; r < xp.P; ++r) {
+            const int dst = xp.ssrc[r];
+            if (dst >= 0) {
+                xp.psend[dst] = st->red[1];
+                xp.psend[dst + 1] = d;
+            }
+        }
+    }
+}
+
 static int launch_mf_dot(fem_pcg* s) {
     const MfOp op = mf_op(s->mf);
-    double* sl = mf_slots(s->mf);
+    double* sl = s->mf_sl;
     const int G = mf_resident_grid(s->bs == 3 ? (const void*)k_pcg_mf_dot<3> : (const void*)k_pcg_mf_dot<1>, MF_BLOCK,
                                    op.nchunks);
     if (s->bs == 3) hipLaunchKernelGGL(k_pcg_mf_dot<3>, dim3(G), dim3(MF_BLOCK), 0, s->stream, op, s->p0, sl, s->st, s->red);
@@ -1987,6 +2070,36 @@ static P2PArgs p2p_args(const fem_pcg* s) {
 static int cg1_spmv(fem_pcg* s, int always) {
     const int64_t off = s->nI * s->bs;
     const int32_t* ipos = s->nI > 0 ? s->ipos : nullptr;
+    if (s->mf) {   // element-chunk operator: the rank's chunks into the context's slots, then the slot gather
+        const MfOp op = mf_op(s->mf);
+        const P2PArgs xp = p2p_args(s);
+        if (op.nchunks > 0) {
+            const void* fn = s->bs == 3 ? (const void*)k_cg1_mf_slots<3> : (const void*)k_cg1_mf_slots<1>;
+            const int G = mf_resident_grid(fn, MF_BLOCK, op.nchunks);
+            if (s->bs == 3)
+                hipLaunchKernelGGL(k_cg1_mf_slots<3>, dim3(G), dim3(MF_BLOCK), 0, s->stream, op, s->cg1_u, s->mf_sl,
+                                   s->st, always, xp, s->cg1_recv, s->cg1_send, off);
+            else
+                hipLaunchKernelGGL(k_cg1_mf_slots<1>, dim3(G), dim3(MF_BLOCK), 0, s->stream, op, s->cg1_u, s->mf_sl,
+                                   s->st, always, xp, s->cg1_recv, s->cg1_send, off);
+            FEM_LAUNCHED();
+        }
+        const int Gg = grid_multiple_of_xcd(cdiv(s->nrows, PCG_BLOCK), 1024);
+        if (s->bs == 3)
+            hipLaunchKernelGGL(k_cg1_mf_gather<3>, dim3(Gg), dim3(PCG_BLOCK), 0, s->stream, op, s->mf_sl, s->cg1_u,
+                               s->q, ipos, s->cg1_send, off, s->st, s->red, always, xp, s->cg1_recv, s->hist,
+                               s->hist_len);
+        else
+            hipLaunchKernelGGL(k_cg1_mf_gather<1>, dim3(Gg), dim3(PCG_BLOCK), 0, s->stream, op, s->mf_sl, s->cg1_u,
+                               s->q, ipos, s->cg1_send, off, s->st, s->red, always, xp, s->cg1_recv, s->hist,
+                               s->hist_len);
+        FEM_LAUNCHED();
+        if (!s->comm && s->p2p) return FEM_OK;
+        if (!s->comm)
+            FEM_HIP(hipMemcpyAsync(s->cg1_recv, s->cg1_send, sizeof(double) * (size_t)cg1_len(s),
+                                   hipMemcpyDeviceToDevice, s->stream));
+        return FEM_OK;
+    }
 #define FEM_CG1(B, CI, PR, C, V)                                                                                   \
     hipLaunchKernelGGL((k_cg1_spmv<B, CI, PR>), dim3(s->grid_spmv), dim3(PCG_BLOCK), 0, s->stream, s->nslices,     \
                        s->nrows, s->slice_ptr, C, V, s->cg1_u, s->q, ipos, s->cg1_send, off, s->st, s->red, always, \
@@ -2140,7 +2253,7 @@ static void host_state_free(void* p, hipStream_t st) {
 
 static int c1f_setup(fem_pcg* s) {
     s->c1f = 0;
-    if (!(s->tune & FEM_TUNE_C1F) || !s->dist || !s->cg1 || s->nslices == 0) return FEM_OK;
+    if (!(s->tune & FEM_TUNE_C1F) || !s->dist || !s->cg1 || s->nslices == 0 || s->mf) return FEM_OK;
     int dev = 0, ncu = 0, nb = 0;
     FEM_HIP(hipGetDevice(&dev));
     FEM_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
@@ -2230,7 +2343,7 @@ static int launch_update2(fem_pcg* s) {
     const int hold = (s->tune & FEM_TUNE_U2_HOLD) ? 1 : 0;
     if (s->mf) {   // node form; q from the operator's slots inside the update unless a gather launch wrote it
         const MfOp op = mf_op(s->mf);
-        const double* sl = mf_slots(s->mf);
+        const double* sl = s->mf_sl;
         const int64_t nn = s->nrows;
 #define FEM_U2MF(B, FQ)                                                                                               \
     hipLaunchKernelGGL((k_pcg_update2_mf<B, FQ>), dim3(s->u2_grid), dim3(PCG_BLOCK), 0, s->stream, nn, s->x, s->p0,    \
@@ -2298,6 +2411,10 @@ static int c1f_launch(fem_pcg* s) {
 
 static int dist_phase(fem_pcg* s, int phase) {
     int rc = FEM_OK;
+    if (s->mf && !s->cg1 && phase < 10) {
+        set_error("dist_phase: the element-chunk operator runs the single-reduction distributed iteration (variant 1)");
+        return FEM_EARG;
+    }
     switch (phase) {
         case 0:
             if ((rc = launch_spmv_dot(s))) return rc;
@@ -2319,8 +2436,14 @@ static int dist_phase(fem_pcg* s, int phase) {
                                    s->w);
                 FEM_LAUNCHED();
             }
-            if ((rc = (s->cols16 ? fem_spmv16(s->nrows, s->bs, s->slice_ptr, s->cols16, s->vals, s->x, s->q, s->stream)
-                          : fem_spmv(s->nrows, s->bs, s->slice_ptr, s->cols, s->vals, s->x, s->q, s->stream)))) return rc;
+            if (s->mf) {
+                if ((rc = mf_apply(s->mf, s->x, s->q, s->mf_sl, s->stream))) return rc;
+            } else if ((rc = (s->cols16 ? fem_spmv16(s->nrows, s->bs, s->slice_ptr, s->cols16, s->vals, s->x, s->q,
+                                                     s->stream)
+                                        : fem_spmv(s->nrows, s->bs, s->slice_ptr, s->cols, s->vals, s->x, s->q,
+                                                   s->stream)))) {
+                return rc;
+            }
             return halo_pack(s, s->q, false, false);
         case 11:
             hipLaunchKernelGGL(k_halo_unpack<false>, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->nrows, s->bs,
@@ -2646,8 +2769,9 @@ int fem_pcg_set_constraints(fem_pcg* s, int order, int64_t R, const int64_t* rbe
                             int64_t S, const int64_t* spc_dof, const double* spc_val, int64_t G, const int64_t* r3_ptr,
                             const int64_t* r3_master, const double* r3_wsum, const int64_t* r3_slave,
                             const double* r3_w) {
-    if (s->mode != FEM_MODE_CG_CONSTRAINED || s->dist || s->fused || s->deferred || s->graph) {
-        set_error("fem_pcg_set_constraints: needs a CG_CONSTRAINED, single-GPU, 3-kernel context without a graph");
+    if (s->mode != FEM_MODE_CG_CONSTRAINED || s->dist || s->fused || s->deferred || s->graph || s->mf) {
+        set_error("fem_pcg_set_constraints: needs a CG_CONSTRAINED, single-GPU, 3-kernel context without a graph "
+                  "over an assembled matrix");
         return FEM_EARG;
     }
     Constraints c;
@@ -2782,10 +2906,13 @@ int fem_pcg_set_operator_mf(fem_pcg* s, fem_mf* m) {
         set_error("fem_pcg_set_operator_mf: the operator's block size / node count do not match the context");
         return FEM_EARG;
     }
-    if (s->dist || s->pd || s->has_con || s->graph) {
-        set_error("fem_pcg_set_operator_mf: single-GPU contexts without constraints or a captured graph only");
+    if (s->pd || s->has_con || s->graph || s->mode == FEM_MODE_CG_CONSTRAINED) {
+        set_error("fem_pcg_set_operator_mf: contexts without constraints (CG_STABLE / PCG mode), the row-partitioned "
+                  "schedule or a captured graph only");
         return FEM_EARG;
     }
+    if (!s->mf_sl && mf_nslots(m) > 0)   // the context's own slots: concurrent solves / applications never share them
+        FEM_HIP(hipMalloc(&s->mf_sl, sizeof(double) * (size_t)mf_bs(m) * (size_t)mf_nslots(m)));
     s->mf = m;
     s->fused = s->deferred = s->persist_req = s->persist_fit_only = s->persist = 0;
     s->cols16 = nullptr;
@@ -3467,7 +3594,7 @@ int fem_pcg_start(fem_pcg* s) {
         return FEM_OK;   // every rank must finish its start before any rank launches (a host barrier)
     }
     if (s->mf) {   // element-chunk operator: r0 = b - A x0 from the element formula
-        if ((rc = mf_apply(s->mf, s->x, s->q, s->stream))) return rc;
+        if ((rc = mf_apply(s->mf, s->x, s->q, s->mf_sl, s->stream))) return rc;
     } else if (s->pext) {   // solver layout: r0 = b - A x0 from the paired values
         if (s->bs == 1)
             hipLaunchKernelGGL(k_spmv_pair<SPMV_UP>, dim3(s->grid_spmv), dim3(256), 0, s->stream, s->nslices, s->nrows,
@@ -4191,6 +4318,7 @@ void fem_pcg_destroy(fem_pcg* s) {
     if (s->c1f_win) (void)hipFree(s->c1f_win);
     if (s->c1f_flags) (void)hipFree(s->c1f_flags);
     if (s->con.tmp) (void)hipFree(s->con.tmp);
+    if (s->mf_sl) (void)hipFree(s->mf_sl);
     if (s->pext) {   // the caller's solver-layout arrays
         s->pvals = nullptr;
         s->pcols16 = nullptr;

@@ -157,11 +157,20 @@ def rank_mesh(elements, part, rank, nparts, n_nodes, sharing=None) -> RankMesh:
 
 
 # ============================================================================ device side
+OPERATORS = ("assembled", "matfree")
+
+
 class DistSystem:
-    """One rank's share: local SELL operator + halo maps. `comm` = RCCL communicator (None: phase-driven)."""
+    """One rank's share: local operator + halo maps. `comm` = RCCL communicator (None: phase-driven).
+    operator "assembled": the rank's elements assembled into a local SELL matrix (unassembled at shared nodes);
+    "matfree": the element-chunk operator over the rank's own elements (system.MatFreeOperator, csrc/matfree.hpp) --
+    the reference's element-by-element product (`solver/element.py:429-464`) restricted to the partition, formed from
+    the coordinates in every application; single-reduction iteration only."""
 
     def __init__(self, coords, elements, part, rank, nparts, kind="poisson", E=1.0, nu=0.0, comm=None,
-                 sharing=None, touch=None):
+                 sharing=None, touch=None, operator="assembled"):
+        if operator not in OPERATORS:
+            raise ValueError(f"unknown operator {operator!r} (one of {OPERATORS})")
         self.lib = C.lib()
         self.dev = coords.device
         self.rm = rank_mesh(elements, part, rank, nparts, coords.shape[0], sharing)
@@ -169,8 +178,14 @@ class DistSystem:
         self._elements, self._part, self._n_nodes = elements, part, coords.shape[0]
         self._p2p = None
         self.comm = comm
-        lc = coords[self.rm.nodes].contiguous()
-        self.A = _sys.assemble_tet4_system(lc, self.rm.conn, kind, E, nu)
+        self.operator = operator
+        lc = coords[self.rm.nodes].to(F64).contiguous()
+        self.n_nodes = lc.shape[0]
+        if operator == "matfree":
+            self._lc = lc   # the operator reads the local coordinates and connectivity in every application
+            self.A = _sys.MatFreeOperator(lc, self.rm.conn, "poisson" if kind == "poisson" else "elastic", E, nu)
+        else:
+            self.A = _sys.assemble_tet4_system(lc, self.rm.conn, kind, E, nu)
         self.bs = self.A.bs
         self.hbuf = torch.empty(max(self.rm.n_iface, 1) * self.bs, dtype=F64, device=self.dev)
 
@@ -183,10 +198,12 @@ class DistSystem:
         return v_global.reshape(-1, self.bs)[self.rm.nodes].reshape(-1).to(F64).contiguous()
 
     def diag_local(self):
+        if self.operator == "matfree":
+            return self.A.diag()
         d = torch.empty(self.n, dtype=F64, device=self.dev)
         g = self.A.g
-        C.check(self.lib.fem_sell_diag(C.ptr(self.A.vals), self.bs, C.ptr(g.diagpos), C.ptr(g.csr2sell), g.n_nodes,
-                                       C.ptr(d), C.stream(self.dev)), "fem_sell_diag")
+        C.check(self.lib.fem_sell_diag(C.ptr(self.A.plain_values()), self.bs, C.ptr(g.diagpos), C.ptr(g.csr2sell),
+                                       g.n_nodes, C.ptr(d), C.stream(self.dev)), "fem_sell_diag")
         return d
 
     def halo_pack(self, v):
@@ -194,7 +211,7 @@ class DistSystem:
                                        C.stream(self.dev)), "fem_halo_pack")
 
     def halo_unpack(self, v):
-        C.check(self.lib.fem_halo_unpack(C.ptr(v), self.bs, C.ptr(self.rm.ipos), self.A.g.n_nodes, C.ptr(self.hbuf),
+        C.check(self.lib.fem_halo_unpack(C.ptr(v), self.bs, C.ptr(self.rm.ipos), self.n_nodes, C.ptr(self.hbuf),
                                          C.stream(self.dev)), "fem_halo_unpack")
 
     def jacobi_from(self, dsum, fixed_mask_local):
@@ -207,7 +224,7 @@ class DistSystem:
         """M_inv of the ASSEMBLED global matrix: the local diagonals are halo-summed first (RCCL)."""
         d = self.diag_local()
         C.check(self.lib.fem_halo_sum(self.comm, C.ptr(d), self.bs, C.ptr(self.rm.imap), self.rm.n_iface,
-                                      C.ptr(self.rm.ipos), self.A.g.n_nodes, C.ptr(self.hbuf), C.stream(self.dev)),
+                                      C.ptr(self.rm.ipos), self.n_nodes, C.ptr(self.hbuf), C.stream(self.dev)),
                 "fem_halo_sum")
         return self.jacobi_from(d, fixed_mask_local)
 
@@ -223,12 +240,18 @@ class DistSystem:
                fused=False):
         return DistRunner(self, b, w, tol, mode, hist_len, variant, exchange, fused)
 
+    def check_variant(self, variant, fused=False):
+        if self.operator == "matfree" and (int(variant) != VARIANT_SINGLE or fused):
+            raise ValueError("the element-chunk operator runs the single-reduction distributed iteration (variant 1, "
+                             "two kernels)")
+
 
 class DistRunner(_sys._DistMarker, _sys.PcgRunner):
     """(P)CG context of one rank in distributed mode."""
 
     def __init__(self, ds: DistSystem, b, w, tol, mode, hist_len=0, variant=None, exchange=EXCHANGE_ALLREDUCE,
                  fused=False):
+        ds.check_variant(VARIANT_SINGLE if variant is None else variant, fused)
         super().__init__(ds.A, b, w, mode=mode, tol=tol)
         self.ds = ds
         self.hist = torch.full((max(hist_len, 1),), float("nan"), dtype=F64, device=ds.dev) if hist_len else None
@@ -258,13 +281,13 @@ class PartitionGroup:
     """All P partitions in ONE process on ONE GPU, exchanges summed by a group kernel in rank order: exercises the
     distributed kernels, halo maps and ownership without RCCL (which refuses two ranks per device)."""
 
-    def __init__(self, coords, elements, nparts, kind="poisson", E=1.0, nu=0.0):
+    def __init__(self, coords, elements, nparts, kind="poisson", E=1.0, nu=0.0, operator="assembled"):
         self.lib = C.lib()
         part = rcb_partition(element_centroids(coords, elements), nparts)
         touch = touch_masks(elements, part, nparts, coords.shape[0])
         sharing = node_sharing(elements, part, nparts, coords.shape[0], touch)
         self.part = part
-        self.ranks = [DistSystem(coords, elements, part, r, nparts, kind, E, nu, None, sharing, touch)
+        self.ranks = [DistSystem(coords, elements, part, r, nparts, kind, E, nu, None, sharing, touch, operator)
                       for r in range(nparts)]
         self.dev = coords.device
 
@@ -338,17 +361,21 @@ class _GroupRunner:
 
     def __init__(self, ds: DistSystem, b, w, tol, mode, variant=0, exchange=EXCHANGE_ALLREDUCE, fused=False):
         self.lib = C.lib()
+        ds.check_variant(variant, fused)
         A = ds.A
         self.b = b.to(F64).contiguous()
         self.w = w.to(F64).contiguous()
         self.x = torch.zeros(A.n, dtype=F64, device=A.device)
         self.h = ctypes.c_void_p()
-        C.check(self.lib.fem_pcg_create(A.g.n_nodes, A.bs, C.ptr(A.g.slice_ptr), C.ptr(A.g.cols), C.ptr(A.vals),
-                                        C.ptr(self.b), C.ptr(self.x), C.ptr(self.w), mode, float(tol), 1e-30, None,
-                                        0, C.stream(A.device), ctypes.byref(self.h)), "fem_pcg_create")
-        C.check(self.lib.fem_pcg_set_schedule(self.h, 0), "fem_pcg_set_schedule")
-        C.check(self.lib.fem_pcg_set_entries(self.h, A.g.sell_entries), "fem_pcg_set_entries")
-        A.attach_cols16(self.h)
+        if ds.operator == "matfree":
+            A.create_context(self.b, self.x, self.w, mode, float(tol), 1e-30, None, 0, C.stream(A.device), self.h)
+        else:
+            C.check(self.lib.fem_pcg_create(A.g.n_nodes, A.bs, C.ptr(A.g.slice_ptr), C.ptr(A.g.cols),
+                                            C.ptr(A.plain_values()), C.ptr(self.b), C.ptr(self.x), C.ptr(self.w), mode, float(tol), 1e-30, None,
+                                            0, C.stream(A.device), ctypes.byref(self.h)), "fem_pcg_create")
+            C.check(self.lib.fem_pcg_set_schedule(self.h, 0), "fem_pcg_set_schedule")
+            C.check(self.lib.fem_pcg_set_entries(self.h, A.g.sell_entries), "fem_pcg_set_entries")
+            A.attach_cols16(self.h)
         C.check(self.lib.fem_pcg_set_dist(self.h, 1, None, ds.rm.n_iface, C.ptr(ds.rm.imap), C.ptr(ds.rm.ipos),
                                           C.ptr(ds.rm.own)), "fem_pcg_set_dist")
         C.check(self.lib.fem_pcg_set_dist_variant(self.h, int(variant)), "fem_pcg_set_dist_variant")
@@ -507,11 +534,11 @@ def bench_main(a, metric):
     path = getattr(a, "dist_path", "auto")
     comm = None
 
-    def rccl(kind):
+    def rccl(kind, operator="assembled"):
         nonlocal comm
         if comm is None:
             comm = init_comm(rank, world)
-        return rccl_measure(a, kind, comm, rank, world, dev, tdist, metric)
+        return rccl_measure(a, kind, comm, rank, world, dev, tdist, metric, operator)
 
     def persist(kind):
         from . import dist_persist
@@ -530,7 +557,20 @@ def bench_main(a, metric):
     guard = None
     if a.kind == "poisson" and getattr(a, "elastic", 0):
         def companion():
-            return run_chain(path, same_gpu, lambda: persist("elastic"), lambda: rccl("elastic"), rank)[0]
+            out_e, how = run_chain(path, same_gpu, lambda: persist("elastic"), lambda: rccl("elastic"), rank)
+            # BASELINE configs[3] as north_star states it -- element partitions, RCCL exchange of the halo-DOF
+            # partials inside every iteration -- measured on every N > 1 run next to the schedule above, with the
+            # assembled local operator and with the element-chunk (matrix-free) one. RCCL refuses two ranks on one
+            # GPU, so the same-GPU rehearsal skips it.
+            if same_gpu:
+                er = {"skipped": "all ranks on one GPU (RCCL refuses two ranks per device)"}
+            else:
+                er = {"assembled": out_e if how == "rccl" else element_rccl(lambda: rccl("elastic", "assembled"))}
+                er["matfree"] = element_rccl(lambda: rccl("elastic", "matfree"))
+            if rank == 0 and isinstance(out_e, dict):
+                out_e = dict(out_e)
+                out_e["element_rccl"] = er
+            return out_e
         guard = CompanionGuard(out, "elasticity", rank=rank, timeout=float(getattr(a, "elastic_timeout", 240.0)))
         out = guard.run(companion)
         guard.emit()
@@ -545,9 +585,21 @@ def bench_main(a, metric):
         guard.close()
 
 
-def rccl_measure(a, kind, comm, rank, world, dev, tdist, metric):
+def element_rccl(fn):
+    """One element-partition measurement for the "element_rccl" block: its bench dict minus the line-level keys, or
+    {"error": ...} (raised on every rank alike: the setup and the checks are collective)."""
+    try:
+        d = fn()
+        return None if d is None else {k: v for k, v in d.items() if k not in COMPANION_DROP + ("cpu_baseline",)}
+    except Exception as e:   # noqa: BLE001 -- reported in the line
+        sys.stderr.write(f"element_rccl measurement failed: {type(e).__name__}: {e}\n")
+        return {"error": f"{type(e).__name__}: {e}"}
+
+
+def rccl_measure(a, kind, comm, rank, world, dev, tdist, metric, operator="assembled"):
     """The RCCL element-partition measurement of `kind` on the n-cube (every rank calls it); returns the bench
-    dict on rank 0, None elsewhere."""
+    dict on rank 0, None elsewhere. operator "matfree": every rank applies the element-chunk operator of its own
+    elements (no matrix), single-reduction iteration with the configured exchange."""
     def barrier_sync():
         torch.cuda.synchronize()
         tdist.barrier()
@@ -569,7 +621,7 @@ def rccl_measure(a, kind, comm, rank, world, dev, tdist, metric):
     # connections (set up on the first collective) with the whole setup on a small cube
     c0, t0_ = _mesh.kuhn_cube(8, device=dev)
     p0 = rcb_partition(element_centroids(c0, t0_), world)
-    d0 = DistSystem(c0, t0_, p0, rank, world, kind, E, nu, comm)
+    d0 = DistSystem(c0, t0_, p0, rank, world, kind, E, nu, comm, operator=operator)
     d0.jacobi(torch.zeros(d0.n, dtype=torch.uint8, device=dev))
     wbuf = torch.ones(1 << 16, dtype=F64, device=dev)
     C.check(C.lib().fem_allreduce_sum(comm, C.ptr(wbuf), wbuf.numel(), C.stream(dev)), "fem_allreduce_sum")
@@ -583,7 +635,7 @@ def rccl_measure(a, kind, comm, rank, world, dev, tdist, metric):
     sharing = node_sharing(tets, part, world, N, touch)
     torch.cuda.synchronize()
     stages["partition_ms"] = (time.perf_counter() - t0) * 1e3
-    ds = DistSystem(coords, tets, part, rank, world, kind, E, nu, comm, sharing, touch)
+    ds = DistSystem(coords, tets, part, rank, world, kind, E, nu, comm, sharing, touch, operator)
     torch.cuda.synchronize()
     stages["rank_mesh_assembly_ms"] = (time.perf_counter() - t0) * 1e3 - stages["partition_ms"]
     bs = ds.bs
@@ -614,9 +666,10 @@ def rccl_measure(a, kind, comm, rank, world, dev, tdist, metric):
             print(f"[rank {rank}] graph capture failed, plain launches: {e}", file=sys.stderr, flush=True)
             return 0
 
-    variant = int(getattr(a, "dist_variant", VARIANT_SINGLE))
+    mf = operator == "matfree"
+    variant = VARIANT_SINGLE if mf else int(getattr(a, "dist_variant", VARIANT_SINGLE))
     exchange = getattr(a, "dist_exchange", EXCHANGE_ALLREDUCE) if variant == VARIANT_SINGLE else EXCHANGE_ALLREDUCE
-    fused = bool(getattr(a, "dist_fused", 0)) and variant == VARIANT_SINGLE
+    fused = bool(getattr(a, "dist_fused", 0)) and variant == VARIANT_SINGLE and not mf
 
     def solve_to_tol():
         run = ds.runner(b, w, tol=tol, variant=variant, exchange=exchange, fused=fused)
@@ -665,7 +718,7 @@ def rccl_measure(a, kind, comm, rank, world, dev, tdist, metric):
         ms, cnt = run.profile(max(a.sample_every, 20), every=1)
     run.close()
     spmv_ms = tmax(ms[0] / max(cnt[0], 1))
-    alg = ds.A.algorithmic_bytes_spmv()
+    alg = ds.A.algorithmic_bytes() if mf else ds.A.algorithmic_bytes_spmv()
     alg_total = torch.tensor([float(alg)], dtype=torch.float64)
     tdist.all_reduce(alg_total)
     nI = ds.rm.n_iface
@@ -678,6 +731,8 @@ def rccl_measure(a, kind, comm, rank, world, dev, tdist, metric):
             "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": f"{tets.shape[0]:,}-tet P1 {kind} Kuhn cube n={a.n}, Jacobi-PCG fixed "
                                    f"iterations, element-partitioned (RCB) over {world} GPUs, "
+                                   + ("element-chunk (matrix-free) operator of each rank's own elements, " if mf
+                                      else "assembled local SELL operator, ")
                                    + ("RCCL neighbour send/recv of [r.z, u.Au | shared rows] with every other rank"
                                       " (single reduction: one grouped exchange per iteration)"
                                       if variant and exchange == EXCHANGE_P2P else
@@ -685,6 +740,7 @@ def rccl_measure(a, kind, comm, rank, world, dev, tdist, metric):
                                       if variant else "RCCL halo all-reduce + r.z all-reduce"),
                        "tets": int(tets.shape[0]), "dofs": N * bs, "interface_nodes": nI,
                        "parallelism": f"element partition x{world}", "graph_iterations": graph_k,
+                       "operator": operator,
                        "dist_variant": "single-reduction" if variant else "two-reduction",
                        "dist_exchange": exchange, "dist_fused_iteration": fused,
                        "dist_exchange_fallback": fallback},
@@ -697,7 +753,8 @@ def rccl_measure(a, kind, comm, rank, world, dev, tdist, metric):
                            "pupdate": ms[2] / max(cnt[2], 1)}),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                          "frac": achieved / 8000.0, "traffic": None,
-                         "kernel": ("k_cg1_spmv" if variant else "k_pcg_spmv_dot") + " (rank 0 local)",
+                         "kernel": ("k_cg1_mf_slots + k_cg1_mf_gather" if mf else
+                                    "k_cg1_spmv" if variant else "k_pcg_spmv_dot") + " (rank 0 local)",
                          "algorithmic_bytes": alg, "stream_ceiling_GBps": ceiling,
                          "frac_of_stream_read": achieved / ceiling["read"]},
             "cpu_baseline": None,

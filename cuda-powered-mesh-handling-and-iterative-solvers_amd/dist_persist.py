@@ -90,8 +90,8 @@ class RankRunner:
         self.stream.wait_stream(torch.cuda.current_stream(A.device))
         self.h = ctypes.c_void_p()
         with C.device_scope(A.device):
-            C.check(self.lib.fem_pcg_create(A.g.n_nodes, A.bs, C.ptr(A.g.slice_ptr), C.ptr(A.g.cols), C.ptr(A.vals),
-                                            C.ptr(self.b), C.ptr(self.x), C.ptr(self.w), mode, float(tol), float(eps),
+            C.check(self.lib.fem_pcg_create(A.g.n_nodes, A.bs, C.ptr(A.g.slice_ptr), C.ptr(A.g.cols),
+                                            C.ptr(A.plain_values()), C.ptr(self.b), C.ptr(self.x), C.ptr(self.w), mode, float(tol), float(eps),
                                             None, 0, ctypes.c_void_p(self.stream.cuda_stream), ctypes.byref(self.h)),
                     "fem_pcg_create")
             C.check(self.lib.fem_pcg_set_entries(self.h, A.g.sell_entries), "fem_pcg_set_entries")

@@ -315,7 +315,16 @@ class SellMatrix:
 
     @property
     def vals(self):
-        """SELL values [entries * bs * bs] (plane layout); zero until something was added."""
+        """SELL values [entries * bs * bs] (plane layout); zero until something was added. The caller may edit them in
+        place: once handed out, the plain values are the matrix (a solver-layout copy is dropped, so later matvec /
+        jacobi / pcg read the edited values; the next solve converts them at its start)."""
+        v = self.plain_values()
+        self._sl_ok = False
+        return v
+
+    def plain_values(self):
+        """The plain SELL values for READING (kernels, exports): formed from the solver layout when only it holds the
+        values, which stays the matrix -- edits through this tensor are not seen by solves (use `vals` to edit)."""
         if self._fresh:
             self._plain_buf().zero_()
             self._fresh = False
@@ -343,7 +352,7 @@ class SellMatrix:
     def _modify_plain(self):
         """The plain values about to change: current (or fresh), and the solver layout stale afterwards."""
         if not self._fresh:
-            self.vals   # noqa: B018 -- forms the plain copy when only the solver layout holds the values
+            self.plain_values()   # forms the plain copy when only the solver layout holds the values
         self._plain_buf()
         self._sl_ok = False
 
@@ -443,10 +452,10 @@ class SellMatrix:
                                     C.ptr(x), C.ptr(y), C.stream(self.device)), "fem_spmv_sl")
         elif self.use16:
             C.check(lib.fem_spmv16(self.g.n_nodes, self.bs, C.ptr(self.g.slice_ptr), C.ptr(self.g.dcols),
-                                   C.ptr(self.vals), C.ptr(x), C.ptr(y), C.stream(self.device)), "fem_spmv16")
+                                   C.ptr(self.plain_values()), C.ptr(x), C.ptr(y), C.stream(self.device)), "fem_spmv16")
         else:
             C.check(lib.fem_spmv(self.g.n_nodes, self.bs, C.ptr(self.g.slice_ptr), C.ptr(self.g.cols),
-                                 C.ptr(self.vals), C.ptr(x), C.ptr(y), C.stream(self.device)), "fem_spmv")
+                                 C.ptr(self.plain_values()), C.ptr(x), C.ptr(y), C.stream(self.device)), "fem_spmv")
         return y
 
     def attach_cols16(self, h):
@@ -459,7 +468,7 @@ class SellMatrix:
         context then reads them through attach_layout), else the plain values."""
         if self._sl_ok and not fused:
             return C.ptr(self._svals)
-        return C.ptr(self.vals)
+        return C.ptr(self.plain_values())
 
     def attach_layout(self, h, fused=False):
         """Hand a context the solver-layout values (+ the bs = 1 pattern, the gather windows) (fem_pcg_set_layout):
@@ -482,7 +491,7 @@ class SellMatrix:
                                       C.ptr(sl.ucol) if sl else None, self.g.n_nodes,
                                       C.ptr(fixed_mask), C.ptr(w), C.stream(self.device)), "fem_jacobi_sl")
             return w
-        C.check(lib.fem_jacobi(C.ptr(self.vals), self.bs, C.ptr(self.g.rowptr), C.ptr(self.g.diagpos),
+        C.check(lib.fem_jacobi(C.ptr(self.plain_values()), self.bs, C.ptr(self.g.rowptr), C.ptr(self.g.diagpos),
                                None, C.ptr(self.g.slice_ptr), self.g.n_nodes,
                                C.ptr(fixed_mask), C.ptr(w), C.stream(self.device)), "fem_jacobi")
         return w
@@ -491,7 +500,7 @@ class SellMatrix:
         """(rowptr, colidx, vals[nnz, bs, bs]) in block-CSR (export / testing)."""
         lib = C.lib()
         out = torch.empty(max(self.g.nnz, 1) * self.bs * self.bs, dtype=F64, device=self.device)
-        C.check(lib.fem_sell_to_csr_vals(C.ptr(self.vals), self.bs, C.ptr(self.g.rowptr), self.g.n_nodes,
+        C.check(lib.fem_sell_to_csr_vals(C.ptr(self.plain_values()), self.bs, C.ptr(self.g.rowptr), self.g.n_nodes,
                                          C.ptr(self.g.csr2sell), C.ptr(self.g.slice_ptr), C.ptr(out),
                                          C.stream(self.device)), "fem_sell_to_csr_vals")
         return self.g.rowptr, self.g.colidx, out[: self.g.nnz * self.bs * self.bs].view(-1, self.bs, self.bs)
@@ -626,6 +635,9 @@ class MatFreeOperator:
 
     def create_context(self, b, x, w, mode, tol, eps, hist, hist_len, stream, h):
         lib = C.lib()
+        if mode == C.MODE_CG_CONSTRAINED:
+            raise ValueError("the element-chunk operator has no constrained CG (SPC / RBE2 / RBE3 projections need "
+                             "the assembled matrix: SellMatrix.pcg(..., constraints=...))")
         C.check(lib.fem_pcg_create(self.n_nodes, self.bs, None, None, None, C.ptr(b), C.ptr(x), C.ptr(w), mode,
                                    float(tol), float(eps), C.ptr(hist), hist_len, stream, ctypes.byref(h)),
                 "fem_pcg_create")
@@ -698,6 +710,12 @@ class PcgRunner:
         self.stream = torch.cuda.Stream(device=A.device)
         self.stream.wait_stream(torch.cuda.current_stream(A.device))
         self.h = ctypes.c_void_p()
+        if getattr(A, "is_matfree", False):   # one form only: refuse what it would otherwise ignore
+            if constraints is not None:
+                raise ValueError("the element-chunk operator has no constrained CG (constraints= needs a SellMatrix)")
+            if fused or (schedule is not None and int(schedule) not in (SCHED_THREE, SCHED_AUTO)):
+                raise ValueError("the element-chunk operator runs the three-kernel schedule (no fused / deferred / "
+                                 "persistent form)")
         self.schedule = (0 if isinstance(self, _DistMarker) or getattr(A, "is_matfree", False)
                          else _schedule(fused, schedule, A.bs))
         self.constraints = constraints   # keeps the device arrays alive with the context

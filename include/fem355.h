@@ -666,8 +666,14 @@ int fem_mf_info(fem_mf* m, int64_t* out6);
  * [chunks + 1], slot nodes [slots] */
 int fem_mf_order(fem_mf* m, int32_t* eorder, int32_t* cptr, int32_t* sbase, int32_t* cnode, fem_stream_t stream);
 /* the context's operator becomes m (nrows = N, bs = m's; create the context with NULL slice_ptr / cols / vals):
- * K1 = the chunk kernel with the p.q reduction + the slot gather, then the merged update; single GPU, modes PCG and
- * CG_STABLE, schedule 0 */
+ * K1 = the chunk kernel with the p.q reduction + the slot gather, then the merged update; modes PCG and CG_STABLE
+ * (FEM_EARG for CG_CONSTRAINED, and fem_pcg_set_constraints refuses an operator context), schedule 0. The context
+ * allocates its own slot buffer, so contexts (and fem_mf_apply / fem_mf_diag, which use the operator's) may run on
+ * different streams at once. Distributed contexts (fem_pcg_set_dist, element partitions: m = the rank's own
+ * elements over its local nodes) run the single-reduction iteration (variant 1, all-reduce or neighbour exchange,
+ * not fused): per iteration k_cg1_update, the rank's chunks into the slots, and the slot gather that packs the
+ * interface rows and the [g, d] pair -- BASELINE configs[3] with no assembled matrix (`solver/element.py:429-464`
+ * per partition, `subdivision.ipynb:248-279`). */
 int fem_pcg_set_operator_mf(fem_pcg* s, fem_mf* m);
 
 #ifdef __cplusplus

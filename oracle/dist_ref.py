@@ -38,24 +38,28 @@ def gdot(a, b, own_rows):
     return t[0]
 
 
-def _setup(coords, rm, f, fixed, kind, E, nu):
-    """Local operator (halo-summed), Jacobi inverse of the assembled diagonal, local rhs and owned-dof mask."""
+def _setup(coords, rm, f, fixed, kind, E, nu, operator="ebe"):
+    """Local operator (halo-summed), Jacobi inverse of the assembled diagonal, local rhs and owned-dof mask.
+    operator "ebe": the rank's element matrices and the reference's EBE product; "matfree": the closed-form element
+    vectors of the rank's elements formed in every application (the element-chunk operator's algebra, no K_e)."""
     lc = coords[rm.nodes]
-    if kind == "poisson":
-        K = E * R.tet4_poisson_K(lc, rm.conn)
-        bs = 1
-    else:
-        K = R.tet4_K(lc, rm.conn, E, nu)
-        bs = 3
+    bs = 1 if kind == "poisson" else 3
     n_loc = rm.nodes.numel()
+    if operator == "matfree":
+        def A(v):
+            return halo_sum(R.tet4_forces_matfree(lc, rm.conn, v, kind, E, nu), rm, bs)
 
-    def A(v):
-        y = R.nodal_forces(K, rm.conn, v.view(n_loc, bs)).reshape(-1)
-        return halo_sum(y, rm, bs)
+        diag = halo_sum(R.tet4_diag_matfree(lc, rm.conn, kind, E, nu), rm, bs)
+    else:
+        K = E * R.tet4_poisson_K(lc, rm.conn) if kind == "poisson" else R.tet4_K(lc, rm.conn, E, nu)
 
-    dofs = (rm.conn.unsqueeze(-1) * bs + torch.arange(bs)).reshape(-1)
-    diag = torch.zeros(n_loc * bs, dtype=F64).index_add_(0, dofs, torch.diagonal(K, dim1=1, dim2=2).reshape(-1))
-    diag = halo_sum(diag, rm, bs)
+        def A(v):
+            y = R.nodal_forces(K, rm.conn, v.view(n_loc, bs)).reshape(-1)
+            return halo_sum(y, rm, bs)
+
+        dofs = (rm.conn.unsqueeze(-1) * bs + torch.arange(bs)).reshape(-1)
+        diag = torch.zeros(n_loc * bs, dtype=F64).index_add_(0, dofs, torch.diagonal(K, dim1=1, dim2=2).reshape(-1))
+        diag = halo_sum(diag, rm, bs)
     Minv = 1.0 / diag
     Minv[Minv == float("inf")] = 0.0
     gfix = torch.zeros(coords.shape[0], dtype=torch.bool)
@@ -88,12 +92,14 @@ def dist_pcg(coords, elements, f, fixed, rm, kind="poisson", E=1.0, nu=0.0, tol=
     return x, max_iter, "max_iter"
 
 
-def dist_pcg_single(coords, elements, f, fixed, rm, kind="poisson", E=1.0, nu=0.0, tol=1e-8, max_iter=1000):
+def dist_pcg_single(coords, elements, f, fixed, rm, kind="poisson", E=1.0, nu=0.0, tol=1e-8, max_iter=1000,
+                    operator="ebe"):
     """The single-reduction (Chronopoulos-Gear) form of the same PCG, as csrc/pcg.hip k_cg1_* runs it on N>1 GPUs:
     u = M r and v = A u carried alongside r, beta = g/g_prev, p.Ap = d - beta g/alpha_prev, alpha = g/p.Ap with
     g = r.u and d = u.v; p = u + beta p, s = v + beta s, x += alpha p, r -= alpha s. Stop test sqrt(r.z) < tol as
-    `solver/solver.py:805`, evaluated at the top of the next pass. Returns (x_local, iterations, status)."""
-    A, Minv, b, own = _setup(coords, rm, f, fixed, kind, E, nu)
+    `solver/solver.py:805`, evaluated at the top of the next pass. operator "matfree": the form the N > 1 element-chunk
+    path runs (k_cg1_mf_*). Returns (x_local, iterations, status)."""
+    A, Minv, b, own = _setup(coords, rm, f, fixed, kind, E, nu, operator)
     x = torch.zeros_like(b)
     r = b - A(x)
     u = Minv * r

@@ -320,6 +320,69 @@ def nodal_forces(K, elements, u):
     return y.view(u.shape)
 
 
+# ----------------------------------------------------------------------------- element product without K_e
+def _lame(E, nu):
+    c = E / ((1.0 + nu) * (1.0 - 2.0 * nu))
+    return c * nu, c * ((1.0 - 2.0 * nu) / 2.0)
+
+
+def tet4_cofactors(coords, elements):
+    """Cofactor vectors c [M,4,3] (c_1 = e_2 x e_3, c_2 = e_3 x e_1, c_3 = e_1 x e_2, c_0 = -(c_1 + c_2 + c_3), with
+    e_b = x_b - x_0) and det [M]: the P1 gradients are c_b / det and V = |det| / 6 (`solver/element.py:835-881`,
+    `:514-541` restated without the 4x4 inverse)."""
+    x = coords[elements]
+    e = x[:, 1:, :] - x[:, :1, :]
+    c1 = torch.cross(e[:, 1], e[:, 2], dim=1)
+    c2 = torch.cross(e[:, 2], e[:, 0], dim=1)
+    c3 = torch.cross(e[:, 0], e[:, 1], dim=1)
+    return torch.stack([-(c1 + c2 + c3), c1, c2, c3], 1), (e[:, 0] * c1).sum(1)
+
+
+def tet4_element_forces(coords, elements, u, kind="elastic", E=1.0, nu=0.0):
+    """Element vectors f_e = K_e u_e [M,4,dpn] of the c3d4 stiffness (`compute_c3d4_K_matrix`, `solver/element.py:
+    883-903`) or the P1 Laplacian (kappa = E), formed in closed form from the cofactors -- what the element-chunk
+    operator (csrc/matfree.hpp mf_element) evaluates: f_a = s sigma(H) c_a with H = sum_b (u_b - u_0) c_b^T,
+    sigma(H) = lambda tr(H) I + mu (H + H^T), s = 1 / (6 |det|); Poisson f_a = kappa s c_a . sum_b c_b (u_b - u_0).
+    Equal to the K_e product up to rounding (tests/test_matfree_cpu.py pins it to tet4_K / tet4_poisson_K)."""
+    c, det = tet4_cofactors(coords, elements)
+    s = 1.0 / (6.0 * det.abs())
+    if kind == "poisson":
+        ue = u.reshape(-1)[elements]
+        gu = torch.einsum("mbk,mb->mk", c[:, 1:, :], ue[:, 1:] - ue[:, :1])
+        return (E * s)[:, None, None] * torch.einsum("mak,mk->ma", c, gu).unsqueeze(-1)
+    lam, mu = _lame(E, nu)
+    ue = u.reshape(-1, 3)[elements]
+    d = ue[:, 1:, :] - ue[:, :1, :]
+    H = torch.einsum("mbi,mbj->mij", d, c[:, 1:, :])
+    tr = H.diagonal(dim1=1, dim2=2).sum(1)
+    sig = lam * tr[:, None, None] * torch.eye(3, dtype=F64) + mu * (H + H.transpose(1, 2))
+    return torch.einsum("mij,maj->mai", sig * s[:, None, None], c)
+
+
+def tet4_forces_matfree(coords, elements, u, kind="elastic", E=1.0, nu=0.0):
+    """y = sum_e P_e^T f_e: the reference's element-by-element product (`solver/element.py:429-464`: gather, local
+    product, index_add) with the closed-form element vectors instead of a stored K_e. u [N*dpn] -> y [N*dpn]."""
+    dpn = 1 if kind == "poisson" else 3
+    f = tet4_element_forces(coords, elements, u, kind, E, nu)
+    y = torch.zeros(coords.shape[0] * dpn, dtype=F64)
+    return y.index_add_(0, dof_map(elements, dpn).reshape(-1), f.reshape(-1))
+
+
+def tet4_diag_matfree(coords, elements, kind="elastic", E=1.0, nu=0.0):
+    """The exact diagonal of the same operator from the cofactors: (K_aa)_qq = s ((lambda + mu) c_aq^2 + mu |c_a|^2),
+    Poisson kappa s |c_a|^2 (csrc/matfree.hpp MF_DIAG). [N*dpn]."""
+    c, det = tet4_cofactors(coords, elements)
+    s = 1.0 / (6.0 * det.abs())
+    cc = (c * c).sum(2)
+    if kind == "poisson":
+        dv, dpn = (E * s)[:, None] * cc, 1
+    else:
+        lam, mu = _lame(E, nu)
+        dv, dpn = s[:, None, None] * ((lam + mu) * c * c + mu * cc[:, :, None]), 3
+    y = torch.zeros(coords.shape[0] * dpn, dtype=F64)
+    return y.index_add_(0, dof_map(elements, dpn).reshape(-1), dv.reshape(-1))
+
+
 def diag_preconditioner(K, elements, N, dpn=3, compat_colzero=False):
     """`compute_diagonal_preconditioner`, `solver/solver.py:814-833`.
     compat_colzero=True reproduces the reference slice bug (Q1: column 0 of every element row, `:828`);

@@ -37,17 +37,22 @@ def _worker(rank, world, port, kind, out_path, variant):
         E, nu = 113.8e9, 0.342
     part = fd.rcb_partition(fd.element_centroids(coords, tets), world)
     rm = fd.rank_mesh(tets, part, rank, world, coords.shape[0])
-    solve = dist_ref.dist_pcg_single if variant == "single" else dist_ref.dist_pcg
-    x, it, st = solve(coords, tets, f, fixed, rm, kind, E, nu, tol=1e-9, max_iter=2000)
+    if variant == "matfree":   # the N > 1 element-chunk form: single reduction, element vectors formed every application
+        x, it, st = dist_ref.dist_pcg_single(coords, tets, f, fixed, rm, kind, E, nu, tol=1e-9, max_iter=2000,
+                                             operator="matfree")
+    else:
+        solve = dist_ref.dist_pcg_single if variant == "single" else dist_ref.dist_pcg
+        x, it, st = solve(coords, tets, f, fixed, rm, kind, E, nu, tol=1e-9, max_iter=2000)
     torch.save({"nodes": rm.nodes, "own": rm.own, "x": x, "it": it, "st": st, "nI": rm.n_iface},
                f"{out_path}.{rank}")
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("variant", ["two", "single"])
+@pytest.mark.parametrize("variant", ["two", "single", "matfree"])
 @pytest.mark.parametrize("kind", ["poisson", "elastic"])
 def test_partitioned_pcg_matches_serial(tmp_path, kind, variant):
-    """Both distributed forms: two reductions per iteration, and the single-reduction (Chronopoulos-Gear) form."""
+    """Both distributed forms: two reductions per iteration, and the single-reduction (Chronopoulos-Gear) form --
+    the latter also on the element-vector operator without stored K_e (the N > 1 element-chunk path's algebra)."""
     from fem355 import mesh
     from oracle import ref_cpu as R
     world = 2

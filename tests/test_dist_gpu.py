@@ -61,6 +61,59 @@ def test_partition_group_matches_single_gpu(gpu, kind, P, variant, exchange, fus
             assert torch.equal(xs[a].view(-1, bs)[ia], xs[c].view(-1, bs)[ic])
 
 
+@pytest.mark.parametrize("exchange", ["allreduce", "p2p"])
+@pytest.mark.parametrize("kind,P", [("poisson", 2), ("poisson", 8), ("elastic", 3), ("elastic", 8)])
+def test_partition_group_matfree_matches_single_gpu(gpu, kind, P, exchange):
+    """The element-chunk operator under the element partition (north_star's configs[3] design): every rank forms its
+    own elements' products from the coordinates (k_cg1_mf_slots + k_cg1_mf_gather, no matrix), the interface rows
+    travel in the single-reduction exchange. Against the single-GPU assembled solve: Jacobi on every local row,
+    solution 1e-10, iterations +-2, shared copies bit-identical; the other variants are refused."""
+    import fem355  # noqa: F401
+    from fem355 import dist as fd, mesh, system
+    coords, tets = mesh.kuhn_cube(10, jitter=0.1)
+    coords, tets = coords.to(gpu), tets.to(gpu)
+    N = coords.shape[0]
+    if kind == "poisson":
+        f, fixed = mesh.cube_poisson_case(coords)
+        E, nu = 1.0, 0.0
+    else:
+        f, fixed = mesh.cube_elasticity_case(coords)
+        E, nu = 113.8e9, 0.342
+    A = system.assemble_tet4_system(coords, tets, kind, E, nu)
+    bs = A.bs
+    gmask = torch.zeros((N, bs), dtype=torch.uint8, device=gpu)
+    gmask[fixed] = 1
+    w = A.jacobi(gmask.view(-1))
+    b = f.reshape(-1).to(F64)
+    tol = 1e-9 * float(torch.sqrt(torch.dot(b, w * b)))
+    ref = A.pcg(b, w=w, tol=tol, max_iter=3000)
+    assert ref.status == 1
+    grp = fd.PartitionGroup(coords, tets, P, kind, E, nu, operator="matfree")
+    assert all(r.operator == "matfree" and getattr(r.A, "is_matfree", False) for r in grp.ranks)
+    masks = [gmask[r.rm.nodes].reshape(-1).contiguous() for r in grp.ranks]
+    ws = grp.jacobi(masks)
+    for r, wl in zip(grp.ranks, ws):
+        assert rel(wl, w.view(-1, bs)[r.rm.nodes].reshape(-1)) < 1e-13
+    bl = [r.local(f) for r in grp.ranks]
+    xs, it, st = grp.solve(bl, ws, tol, 3000, variant=1, exchange=exchange)
+    assert st == 1 and abs(it - ref.iterations) <= 2, (it, ref.iterations)
+    u = fd.gather_solution(grp.ranks, xs, N, bs)
+    assert rel(u.reshape(-1), ref.x) < 1e-10
+    for a in range(P):
+        for c in range(a + 1, P):
+            ra, rc = grp.ranks[a].rm, grp.ranks[c].rm
+            m = torch.isin(ra.nodes, rc.nodes)
+            if int(m.sum()) == 0:
+                continue
+            common = ra.nodes[m]
+            ia, ic = torch.searchsorted(ra.nodes, common), torch.searchsorted(rc.nodes, common)
+            assert torch.equal(xs[a].view(-1, bs)[ia], xs[c].view(-1, bs)[ic])
+    with pytest.raises(ValueError):
+        grp.solve(bl, ws, tol, 10, variant=0)
+    with pytest.raises(ValueError):
+        grp.solve(bl, ws, tol, 10, variant=1, fused=True)
+
+
 def test_local_spmv_partials_sum_to_global(gpu):
     import fem355  # noqa: F401
     from fem355 import dist as fd, mesh, system
@@ -113,6 +166,50 @@ def test_config3_elasticity_10m_eight_partitions_vs_oracle(gpu, cube119):
     u = fd.gather_solution(grp.ranks, xs, N, 3)
     assert rel(u, cube119.pcg_ref("elastic", 5)) < 1e-10
     # (c) shared copies bit-identical
+    for a in range(8):
+        for b in range(a + 1, 8):
+            ra, rb = grp.ranks[a].rm, grp.ranks[b].rm
+            m = torch.isin(ra.nodes, rb.nodes)
+            if int(m.sum()) == 0:
+                continue
+            common = ra.nodes[m]
+            ia, ib = torch.searchsorted(ra.nodes, common), torch.searchsorted(rb.nodes, common)
+            assert torch.equal(xs[a].view(-1, 3)[ia], xs[b].view(-1, 3)[ib])
+
+
+def test_config3_elasticity_10m_eight_partitions_matfree_vs_oracle(gpu, cube119):
+    """configs[3] as north_star states it, on one GPU: the 10,110,954-tet elasticity system over 8 RCB element
+    partitions, every rank's operator the element-chunk product of ITS OWN elements (no assembled matrix anywhere),
+    the halo-summed exact Jacobi, and the single-reduction iteration with the neighbour exchange (k_cg1_mf_slots /
+    k_cg1_mf_gather / k_cg1_update, p2p slots delivered in-process). Against the oracle: (a) the ranks' local products
+    summed over their global node ids = the reference's EBE product (`solver/element.py:429-464`) at 1e-12; Jacobi =
+    the oracle's at 1e-13; (b) 5 fixed iterations = the oracle PCG's 5th iterate (`solver/solver.py:766-812`) at
+    1e-10; (c) copies of shared nodes bit-identical on every rank."""
+    import fem355  # noqa: F401
+    from fem355 import dist as fd
+    c, t, N = cube119.c, cube119.t, cube119.N
+    f, fixed, dinv = cube119.case("elastic")
+    grp = fd.PartitionGroup(c.to(gpu), t.to(gpu), 8, "elastic", cube119.E, cube119.NU, operator="matfree")
+    assert len(grp.ranks) == 8 and sum(r.rm.elem_ids.numel() for r in grp.ranks) == t.shape[0]
+    p, y_ref = cube119.matvec_ref("elastic", 11)
+    pg = p.to(gpu)
+    acc = torch.zeros((N, 3), dtype=F64, device=gpu)
+    for r in grp.ranks:
+        y = r.A.matvec(pg[r.rm.nodes].reshape(-1).contiguous())
+        acc.index_add_(0, r.rm.nodes, y.view(-1, 3))
+    assert rel(acc, y_ref) < 1e-12
+    del acc, pg
+    gmask = torch.zeros((N, 3), dtype=torch.uint8, device=gpu)
+    gmask[fixed.to(gpu)] = 1
+    ws = grp.jacobi([gmask[r.rm.nodes].reshape(-1).contiguous() for r in grp.ranks])
+    for r, wl in zip(grp.ranks, ws):
+        assert rel(wl, dinv[r.rm.nodes.cpu()].reshape(-1)) < 1e-13
+    fg = f.to(gpu)
+    bl = [r.local(fg) for r in grp.ranks]
+    xs, it, st = grp.solve(bl, ws, 0.0, 5, variant=1, exchange="p2p", fixed=True)
+    assert it == 5, (it, st)
+    u = fd.gather_solution(grp.ranks, xs, N, 3)
+    assert rel(u, cube119.pcg_ref("elastic", 5)) < 1e-10
     for a in range(8):
         for b in range(a + 1, 8):
             ra, rb = grp.ranks[a].rm, grp.ranks[b].rm

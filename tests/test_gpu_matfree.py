@@ -311,3 +311,80 @@ def test_config2_matfree_10m_operator_and_iterates_vs_oracle(gpu, cube119):
     res = A.pcg(f.reshape(-1), w=w, tol=0.0, max_iter=5)
     assert res.iterations == 5
     assert rel(res.x, cube119.pcg_ref("elastic", 5).reshape(-1)) < 1e-10
+
+
+def test_refuses_what_it_cannot_run(gpu):
+    """a constrained solve on the element-chunk operator used to run as plain CG (constraints dropped).
+    Python refuses constraints= / CG_CONSTRAINED / non-default schedules; the C-ABI refuses a CG_CONSTRAINED context
+    for the operator and constraints on an operator context."""
+    import ctypes
+    mesh, _, system = _mods()
+    from fem355 import _capi as C
+    from fem355 import constraints as CS
+    c, t = mesh.kuhn_cube(4)
+    A = system.MatFreeOperator(c.to(gpu), t.to(gpu), "elastic", E, NU)
+    b = torch.ones(A.n, dtype=F64, device=gpu)
+    w = torch.ones(A.n, dtype=F64, device=gpu)
+    cons = CS.ConstraintSet(A.n_nodes, 3, gpu, CS.parse_spc_list([{"node": 0, "dofs": [0, 1, 2], "value": 0.0}], "cpu"),
+                            CS.parse_rbe2_list([], "cpu"))
+    with pytest.raises(ValueError):
+        system.PcgRunner(A, b, w, mode=C.MODE_CG_CONSTRAINED, constraints=cons)
+    with pytest.raises(ValueError):
+        system.PcgRunner(A, b, w, fused=True)
+    with pytest.raises(ValueError):
+        system.PcgRunner(A, b, w, schedule=3)
+    with pytest.raises(ValueError):
+        A.pcg(b, w=w, mode=C.MODE_CG_CONSTRAINED)
+    lib = C.lib()
+    x = torch.zeros_like(b)
+    h = ctypes.c_void_p()
+    C.check(lib.fem_pcg_create(A.n_nodes, 3, None, None, None, C.ptr(b), C.ptr(x), C.ptr(w), C.MODE_CG_CONSTRAINED,
+                               0.0, 1e-30, None, 0, C.stream(torch.device(gpu)), ctypes.byref(h)), "fem_pcg_create")
+    try:
+        assert lib.fem_pcg_set_operator_mf(h, A.h) == C.FEM_EARG
+    finally:
+        lib.fem_pcg_destroy(h)
+    h = ctypes.c_void_p()
+    C.check(lib.fem_pcg_create(A.n_nodes, 3, None, None, None, C.ptr(b), C.ptr(x), C.ptr(w), C.MODE_CG_STABLE,
+                               0.0, 1e-30, None, 0, C.stream(torch.device(gpu)), ctypes.byref(h)), "fem_pcg_create")
+    try:
+        C.check(lib.fem_pcg_set_operator_mf(h, A.h), "fem_pcg_set_operator_mf")
+        assert lib.fem_pcg_set_constraints(h, *cons.args()) == C.FEM_EARG
+    finally:
+        lib.fem_pcg_destroy(h)
+
+
+def test_concurrent_runners_on_one_operator(gpu):
+    """every application used to write the operator's one slot buffer, so two runners on their own
+    streams raced. Each (P)CG context now owns its slots: two runners iterating interleaved on their own streams (and
+    stand-alone applications on the current stream between them) give the same iterates bit for bit as one runner
+    alone."""
+    mesh, _, system = _mods()
+    c, t = mesh.kuhn_cube(14, jitter=0.1)
+    cg, tg = c.to(gpu), t.to(gpu)
+    A = system.MatFreeOperator(cg, tg, "elastic", E, NU)
+    f, fixed = mesh.cube_elasticity_case(cg)
+    mask = torch.zeros((c.shape[0], 3), dtype=torch.uint8, device=gpu)
+    mask[fixed] = 1
+    w = A.jacobi(mask.view(-1))
+    b = f.reshape(-1).to(F64)
+    solo = system.PcgRunner(A, b, w)
+    solo.start()
+    solo.iterate(40)
+    solo.poll()
+    ref = solo.x.clone()
+    solo.close()
+    r1, r2 = system.PcgRunner(A, b, w), system.PcgRunner(A, b * 2.0, w)
+    r1.start()
+    r2.start()
+    p = torch.randn(A.n, dtype=F64, device=gpu)
+    y0 = A.matvec(p)
+    for _ in range(8):
+        r1.iterate(5)
+        r2.iterate(5)
+        y = A.matvec(p)
+    r1.poll()
+    r2.poll()
+    assert torch.equal(r1.x, ref)
+    assert torch.equal(r2.x, 2.0 * ref)   # a linear solve from x0 = 0: twice the load, twice every iterate (exact)
+    assert torch.equal(y, y0)

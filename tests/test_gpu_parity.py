@@ -1216,3 +1216,28 @@ def test_empty_mesh(gpu, capsys):
     assert capsys.readouterr().out.startswith("Terminating early at iteration 1: p^T K p = 0.000e+00")
     A = system.assemble_tet4_system(coords.to(gpu), el.to(gpu), "poisson")
     assert float(A.matvec(torch.ones(10, dtype=F64, device=gpu)).abs().max()) == 0.0
+
+
+def test_vals_edits_are_seen_by_solves(gpu):
+    """a solver-layout matrix used to keep solving with its layout copy after the caller edited `vals`
+    in place. Once handed out, the plain values are the matrix: matvec, Jacobi and the solve see the edit (x2 values:
+    twice the product, half the weights, half the solution -- exact in binary floating point)."""
+    _, mesh, _, system = _mods()
+    c, t = mesh.kuhn_cube(8, jitter=0.1)
+    cg, tg = c.to(gpu), t.to(gpu)
+    A = system.assemble_tet4_system(cg, tg, "poisson")
+    assert A.solver_layout
+    N = c.shape[0]
+    mask = torch.zeros(N, dtype=torch.uint8, device=gpu)
+    mask[:50] = 1
+    p = torch.randn(N, dtype=F64, generator=torch.Generator().manual_seed(4)).to(gpu)
+    y, w = A.matvec(p), A.jacobi(mask)
+    b = torch.ones(N, dtype=F64, device=gpu)
+    r1 = A.pcg(b, w=w, tol=0.0, max_iter=30)
+    A.vals.mul_(2.0)
+    assert not A.solver_layout
+    assert torch.equal(A.matvec(p), 2.0 * y)
+    w2 = A.jacobi(mask)
+    assert torch.equal(w2, 0.5 * w)
+    r2 = A.pcg(b, w=w2, tol=0.0, max_iter=30)
+    assert torch.equal(r2.x, 0.5 * r1.x)

@@ -12,38 +12,17 @@ F64 = torch.float64
 E, NU = 113.8e9, 0.342
 
 
-def _lame(E, nu):
-    c = E / ((1.0 + nu) * (1.0 - 2.0 * nu))
-    return c * nu, c * ((1.0 - 2.0 * nu) / 2.0)
-
-
-def _cofactors(x):
-    """x [M,4,3] -> (c [M,4,3] cofactor vectors with c_0 = -(c_1 + c_2 + c_3), det [M])."""
-    e = x[:, 1:, :] - x[:, :1, :]
-    c1 = torch.cross(e[:, 1], e[:, 2], dim=1)
-    c2 = torch.cross(e[:, 2], e[:, 0], dim=1)
-    c3 = torch.cross(e[:, 0], e[:, 1], dim=1)
-    c = torch.stack([-(c1 + c2 + c3), c1, c2, c3], 1)
-    det = (e[:, 0] * c1).sum(1)
-    return c, det
-
-
 def _mf_elastic(x, u, E, nu):
-    lam, mu = _lame(E, nu)
-    c, det = _cofactors(x)
-    s = 1.0 / (6.0 * det.abs())
-    d = u[:, 1:, :] - u[:, :1, :]                          # [M,3,3]: (u_b - u_0)[i]
-    H = torch.einsum("mbi,mbj->mij", d, c[:, 1:, :])       # sum_b (u_b - u_0) c_b^T
-    tr = H.diagonal(dim1=1, dim2=2).sum(1)
-    sig = lam * tr[:, None, None] * torch.eye(3, dtype=F64) + mu * (H + H.transpose(1, 2))
-    return torch.einsum("mij,maj->mai", sig * s[:, None, None], c)   # f_a = s sigma c_a
+    """x [M,4,3] element coordinates, u [M,4,3] element displacements -> the oracle's closed-form element vectors."""
+    M = x.shape[0]
+    t = torch.arange(4 * M).view(M, 4)
+    return R.tet4_element_forces(x.reshape(-1, 3), t, u.reshape(-1), "elastic", E, nu)
 
 
 def _mf_poisson(x, u, kappa):
-    c, det = _cofactors(x)
-    s = kappa / (6.0 * det.abs())
-    gu = torch.einsum("mbk,mb->mk", c[:, 1:, :], u[:, 1:] - u[:, :1])
-    return s[:, None] * torch.einsum("mak,mk->ma", c, gu)
+    M = x.shape[0]
+    t = torch.arange(4 * M).view(M, 4)
+    return R.tet4_element_forces(x.reshape(-1, 3), t, u.reshape(-1), "poisson", kappa)[..., 0]
 
 
 @pytest.mark.parametrize("jitter", [0.0, 0.15])
@@ -66,3 +45,21 @@ def test_cofactor_form_equals_element_matrices(jitter):
     fp_ref = torch.einsum("mij,mj->mi", Kp, up[tets])
     assert rel(_mf_poisson(x, up[tets], 2.5), fp_ref) < 1e-13
 
+
+
+@pytest.mark.parametrize("kind", ["elastic", "poisson"])
+def test_matfree_product_and_diagonal_vs_element_matrices(kind):
+    """The oracle's EBE product without K_e (`tet4_forces_matfree`, the element-chunk operator's algebra) and its exact
+    diagonal against the reference op sequence over stored element matrices (`nodal_forces`, `solver/element.py:
+    429-464`)."""
+    from fem355 import mesh
+    coords, tets = mesh.kuhn_cube(5, jitter=0.15)
+    N = coords.shape[0]
+    dpn, Ek = (3, E) if kind == "elastic" else (1, 2.5)
+    K = R.tet4_K(coords, tets, E, NU) if kind == "elastic" else R.tet4_poisson_K(coords, tets, kappa=Ek)
+    u = torch.randn(N * dpn, dtype=F64, generator=torch.Generator().manual_seed(3))
+    y = R.tet4_forces_matfree(coords, tets, u, kind, Ek, NU)
+    assert rel(y, R.nodal_forces(K, tets, u.view(N, dpn)).reshape(-1)) < 1e-13
+    d = torch.zeros(N * dpn, dtype=F64).index_add_(0, R.dof_map(tets, dpn).reshape(-1),
+                                                    torch.diagonal(K, dim1=1, dim2=2).reshape(-1))
+    assert rel(R.tet4_diag_matfree(coords, tets, kind, Ek, NU), d) < 1e-13
