@@ -16,8 +16,9 @@ Workload: Kuhn-cube mesh n=119 -> 10,110,954 P1 tets, 1,728,0
     the whole PCG iteration moves just those bytes (matrix, u gather, u store); other schedules: per SpMV launch
     (k_pcg_d1 deferred, k_pcg_spmv_dot three-kernel).
   * cpu_baseline: the oracle (torch-CPU restatement of the reference's EBE PCG, oracle/ref_cpu.py) timed on the
-    host cores on a bounded sample of the same 10M system (element assembly, EBE matvec, 10 PCG iterations), rank 0
-    at N=1 only; the assembly + solve wall it implies for the GPU line's iteration count is projected beside it.
+    host cores on a bounded sample of the same 10M system (element assembly, EBE matvec, 50 fixed PCG iterations:
+    BASELINE.md §3), rank 0 at N=1 only. Measured ratio: the CPU's assembly + 50 iterations against the GPU's
+    assembly + 50 timed iterations; the whole-solve wall is projected from the CPU iteration rate (labelled so).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 """
@@ -54,7 +55,8 @@ def parse():
     ap.add_argument("--rtol", type=float, default=1e-8)
     ap.add_argument("--dof-passes", type=int, default=3,
                     help="steady-state assembly + solve passes after the cold one; DOFs/s is the median pass")
-    ap.add_argument("--cpu-iters", type=int, default=10, help="CPU-baseline PCG iterations (Poisson)")
+    ap.add_argument("--cpu-iters", type=int, default=50,
+                    help="CPU-baseline PCG iterations (Poisson; BASELINE.md §3: a fixed 50)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--elastic", type=int, default=1,
                     help="poisson runs: also measure the 10M-tet linear-elasticity system (BASELINE configs[2]/[3]) "
@@ -66,7 +68,14 @@ def parse():
                     help="elasticity companion: also the element-chunk (matrix-free) operator, under \"matfree\"")
     ap.add_argument("--elastic-timeout", type=float, default=240.0,
                     help="seconds the elasticity companion may take before the line is printed without it")
-    ap.add_argument("--cpu-iters-elastic", type=int, default=10, help="CPU-baseline PCG iterations (elasticity)")
+    ap.add_argument("--cpu-iters-elastic", type=int, default=50, help="CPU-baseline PCG iterations (elasticity)")
+    ap.add_argument("--reference-api", type=int, default=1,
+                    help="elasticity companion: also the time to solution through the reference's own hand-off "
+                         "(compute_c3d4_K_matrix -> compute_diagonal_preconditioner -> "
+                         "preconditioned_conjugate_gradient_solver), under \"reference_api\"")
+    ap.add_argument("--mixed", type=int, default=1,
+                    help="poisson runs: also BASELINE configs[4] (2M-element c3d8 / c3d6 / c3d10 stiffness + mass "
+                         "assembly) under \"mixed\"")
     ap.add_argument("--schedule", type=int, default=None, help="PCG kernel schedule (0 three-kernel, 1 fused, 2 deferred, 3 persistent; "
                     "default: persistent for bs=1, three-kernel for bs=3)")
     ap.add_argument("--graph", type=int, default=0, help="capture k iterations per hipGraph (0 = plain launches)")
@@ -197,13 +206,22 @@ def cpu_baseline(n, kind, iters, solve_iters=None):
 
 
 def attach_cpu_baseline(out, cb):
-    """cpu_baseline into the bench dict, with the assembly + solve wall-clock ratio GPU vs CPU (north_star: >= 10x
-    the reference CPU's assembly + CG wall-clock at 1 GPU) -- same system, same iteration count to rtol."""
+    """cpu_baseline into the bench dict, with the assembly + CG wall-clock ratios GPU vs CPU (north_star: >= 10x the
+    reference CPU's assembly + CG wall-clock at 1 GPU): measured on the same fixed iteration count (the CPU's
+    assembly + its `cg_iters` iterations against the GPU's assembly + as many timed iterations), and projected to the
+    whole solve to rtol (the CPU iteration rate times the GPU line's iteration count; a projection, so named)."""
     out["cpu_baseline"] = cb
+    k = cb.get("cg_iters")
+    if k and out.get("ms_per_step"):
+        gpu_fixed_s = (out.get("assembly_ms", 0.0) + k * out["ms_per_step"]) * 1e-3
+        out["vs_cpu_assembly_plus_fixed_iters"] = {
+            "ratio": cb["assembly_plus_fixed_iters_wall_s"] / gpu_fixed_s, "iterations": k,
+            "cpu_wall_s": cb["assembly_plus_fixed_iters_wall_s"], "gpu_wall_s": gpu_fixed_s,
+            "gpu_basis": "assembly_ms (steady pass) + iterations x ms_per_step (timed region)"}
     proj = cb.get("projected_assembly_plus_solve_wall_s")
     gpu_s = (out.get("assembly_ms", 0.0) + out.get("solve_ms", 0.0)) * 1e-3
     if proj and gpu_s > 0:
-        out["vs_cpu_assembly_plus_solve"] = proj / gpu_s
+        out["projected_vs_cpu_assembly_plus_solve"] = proj / gpu_s
 
 
 def main():
@@ -250,11 +268,23 @@ def main():
                     d["matfree"] = measure_matfree(a, coords, tets, dev, d)
                 except Exception as e:   # reported, never fatal to the line
                     d["matfree"] = {"error": f"{type(e).__name__}: {e}"}
+            if a.reference_api:
+                try:
+                    d["reference_api"] = measure_reference_api(a, coords, tets, dev, d)
+                except Exception as e:   # reported, never fatal to the line
+                    d["reference_api"] = {"error": f"{type(e).__name__}: {e}"}
             if not a.no_cpu_baseline:
                 attach_cpu_baseline(d, cpu_baseline(a.n, "elastic", a.cpu_iters_elastic, d["solve_iters"]))
             return d
         guard = dist.CompanionGuard(out, "elasticity", rank=0, timeout=a.elastic_timeout)
         guard.run(companion)
+        if a.mixed:
+            del coords, tets
+            torch.cuda.empty_cache()
+            try:
+                out["mixed"] = measure_mixed(a, dev)
+            except Exception as e:   # reported, never fatal to the line
+                out["mixed"] = {"error": f"{type(e).__name__}: {e}"}
         guard.emit()
         guard.close()
     else:
@@ -352,6 +382,154 @@ def measure_matfree(a, coords, tets, dev, ref):
         "operator": "element-chunk (matrix-free): Morton-ordered chunks of <= 512 elements / 256 nodes, "
                     "fixed-order slot sums (csrc/matfree.hip)",
     }
+
+
+MIXED_FAMILIES = (("c3d8", "hex_box", 88), ("c3d6", "wedge_box", 70), ("c3d10", "tet10_cube", 48))
+RHO = 4.47e-3   # solver_example.ipynb:38-40
+
+
+def measure_mixed(a, dev):
+    """BASELINE configs[4]: "2M-element P2 tet + hex/wedge mixed mesh, mass+stiffness assembly, 1 x MI355X" -- three
+    separate boxes (P2 / linear faces are nonconforming): c3d8 88^3 = 681,472 hexes, c3d6 2 x 70^3 =
+    686,000 wedges, c3d10 6 x 48^3 = 663,552 quadratic tets, jittered. Per family one job: element stiffness through
+    the reference API (`compute_K_matrix`, `solver/element.py:419-427`, default rule / single=True) and the consistent
+    mass (`compute_M_matrix(..., scalar=True)`: its factor M_s of M = M_s (x) I3, [M, npe, npe] -- the 3x3 blocks of a
+    vector-field mass are multiples of I3, so the stored and assembled mass is the bs = 1 M_s on the same node pattern;
+    no reference function: parity unpinned) on the current stream, the pattern (node graph
+    + SELL layout) on a second stream from a second host thread meanwhile, then both global assemblies; host clock
+    around the whole job, device idle at both ends, best of --dof-passes after a cold pass. Per stage the kernel time
+    (hip events, separate passes) and bytes: K_e / M_e written, K_e read + SELL values written by the assembly."""
+    import threading
+    from fem355 import element
+    E, nu = 113.8e9, 0.342
+    F64 = torch.float64
+
+    def ev(fn):
+        s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s0.record()
+        r = fn()
+        s1.record()
+        sync()
+        return s0.elapsed_time(s1), r
+
+    out = {"config": "c3d8 88^3 + c3d6 2 x 70^3 + c3d10 6 x 48^3 hexes / wedges / P2 tets (2,031,024 elements), "
+                     "jitter 0.1, stiffness (bs = 3) + consistent mass (its scalar factor M_s, bs = 1: M = M_s (x) I3), "
+                     "fp64"}
+    total_ms, total_el, total_bytes = 0.0, 0, 0
+    for et, gen, n in MIXED_FAMILIES:
+        c, el = getattr(mesh, gen)(n, jitter=0.1, device=dev)
+        N = c.shape[0]
+        side = torch.cuda.Stream(device=dev)
+
+        def job():
+            box = []
+
+            def pattern():
+                torch.cuda.set_device(dev)
+                with torch.cuda.stream(side):
+                    box.append(system.build_graph(el, N))
+            th = threading.Thread(target=pattern)
+            th.start()
+            K = element.compute_K_matrix(c, el, et, E, nu, device=dev, dtype=F64)
+            Me = element.compute_M_matrix(c, el, et, RHO, device=dev, dtype=F64, scalar=True)
+            th.join()
+            g = box[0]
+            torch.cuda.current_stream(dev).wait_stream(side)
+            A = system.SellMatrix(g, 3).add_element_matrices(K, el)
+            Am = system.SellMatrix(g, 1).add_element_matrices(Me, el)
+            return K, Me, g, A, Am
+
+        walls = []
+        for _ in range(1 + max(a.dof_passes, 1)):
+            sync()
+            t0 = time.perf_counter()
+            K, Me, g, A, Am = job()
+            sync()
+            walls.append((time.perf_counter() - t0) * 1e3)
+            del K, Me, A, Am, g
+        # kernel times by stage (events; not overlapped), outside the timed jobs
+        ms_k, K = ev(lambda: element.compute_K_matrix(c, el, et, E, nu, device=dev, dtype=F64))
+        ms_g, g = ev(lambda: system.build_graph(el, N))
+        ms_a, A = ev(lambda: system.SellMatrix(g, 3).add_element_matrices(K, el))
+        ms_m, Me = ev(lambda: element.compute_M_matrix(c, el, et, RHO, device=dev, dtype=F64, scalar=True))
+        ms_ma, Am = ev(lambda: system.SellMatrix(g, 1).add_element_matrices(Me, el))
+        ke_bytes = K.numel() * 8
+        me_bytes = Me.numel() * 8
+        sell_bytes = g.sell_entries * 9 * 8
+        mass = float(Am.plain_values().sum())
+        nnzb = g.nnz
+        del K, Me, A, Am, g
+        torch.cuda.empty_cache()
+        best = min(walls[1:])
+        total_ms += best
+        total_el += int(el.shape[0])
+        total_bytes += 2 * ke_bytes + sell_bytes + 2 * me_bytes + sell_bytes // 9
+        out[et] = {"elements": int(el.shape[0]), "nodes": N, "nnz_blocks": nnzb, "job_ms": best,
+                   "job_passes_ms": [round(w, 3) for w in walls],
+                   "stage_ms": {"Ke": ms_k, "pattern": ms_g, "assemble_K": ms_a, "Me": ms_m, "assemble_M": ms_ma},
+                   "Ke_write_GBps": ke_bytes / (ms_k * 1e-3) / 1e9, "Me_write_GBps": me_bytes / (ms_m * 1e-3) / 1e9,
+                   "assemble_K_GBps": (ke_bytes + sell_bytes) / (ms_a * 1e-3) / 1e9,
+                   "total_mass_over_rho": mass / RHO}
+    out["elements_total"] = total_el
+    out["set_ms"] = total_ms
+    out["value"] = total_el / (total_ms * 1e-3)
+    out["unit"] = "elements/s (stiffness + mass, patterns and both global assemblies)"
+    out["roofline"] = {"bound": "hbm", "algorithmic_bytes": total_bytes,
+                       "achieved_GBps": total_bytes / (total_ms * 1e-3) / 1e9,
+                       "frac": total_bytes / (total_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                       "model": "K_e and M_s,e written and each read once by its assembly, the bs = 3 stiffness and "
+                                "bs = 1 mass SELL values written once (the set's job time; the pattern excluded)"}
+    return out
+
+
+def measure_reference_api(a, coords, tets, dev, ref):
+    """configs[2] through the reference's own hand-off, as the notebooks call it: `compute_c3d4_K_matrix` (K [M,12,12]
+    on the device, 11.6 GB at 10M tets; `solver/element.py:883-903`) -> `compute_diagonal_preconditioner` (the exact
+    diagonal, fixed DOFs zeroed: the reference's PCG has no other Dirichlet handling, `solver/solver.py:814-833`) ->
+    `preconditioned_conjugate_gradient_solver` (`solver/solver.py:766-812`: the stored K_e assembled into SELL, then
+    the device PCG) to the bench's tolerance. Time to solution per stage; pass 1 builds the pattern inside the solver
+    call, pass 2 finds it cached (a second solve on the same mesh). Iterations must agree with the fused pipeline's
+    (`ref`, +-2). The solver's prints go to stderr (the bench's stdout is its JSON line)."""
+    import contextlib
+    from fem355 import solver as S
+    N = coords.shape[0]
+    f, fixed = mesh.cube_elasticity_case(coords)
+    E, nu = 113.8e9, 0.342
+    f = f.to(torch.float64)
+    passes = []
+    for cold in (True, False):
+        if cold:
+            S._GRAPH_CACHE.clear()
+        sync()
+        t0 = time.perf_counter()
+        K = S.compute_c3d4_K_matrix(coords, tets, E, nu, device=dev, dtype=torch.float64)
+        sync()
+        t1 = time.perf_counter()
+        Minv = S.compute_diagonal_preconditioner(K, tets, N, device=dev, dtype=torch.float64, exact_diagonal=True)
+        Minv[fixed] = 0.0
+        sync()
+        t2 = time.perf_counter()
+        b = f.reshape(-1)
+        tol = a.rtol * float(torch.sqrt(torch.dot(b, Minv.reshape(-1) * b)))
+        sync()
+        t3 = time.perf_counter()
+        with contextlib.redirect_stdout(sys.stderr):
+            u, res = S.preconditioned_conjugate_gradient_solver(K, tets, f, Minv, tol=tol, max_iter=20000, device=dev,
+                                                                dtype=torch.float64, return_info=True)
+        sync()
+        t4 = time.perf_counter()
+        passes.append({"element_K_ms": (t1 - t0) * 1e3, "preconditioner_ms": (t2 - t1) * 1e3,
+                       "pcg_call_ms": (t4 - t3) * 1e3, "total_ms": (t1 - t0 + t2 - t1 + t4 - t3) * 1e3,
+                       "iterations": res.iterations, "status": res.status})
+        del K, Minv, u, res
+    torch.cuda.empty_cache()
+    assert all(abs(p["iterations"] - ref["solve_iters"]) <= 2 for p in passes), (passes, ref["solve_iters"])
+    warm = passes[1]
+    return {"route": "compute_c3d4_K_matrix -> compute_diagonal_preconditioner(exact_diagonal=True) -> "
+                     "preconditioned_conjugate_gradient_solver (K [M,12,12] fp64 on the device)",
+            "cold_pattern": passes[0], "cached_pattern": warm, "time_to_solution_ms": warm["total_ms"],
+            "dofs_per_s": 3 * N / (warm["total_ms"] * 1e-3), "solve_iters": warm["iterations"],
+            "solve_iters_fused_pipeline": ref["solve_iters"]}
 
 
 def measure(a, kind, coords, tets, dev):

@@ -44,6 +44,7 @@ SIGNATURES = {
     "fem_iso_ke": (_I, [_P, _P, _L, _I, _D, _D, _P, _P, _I, _I, _P, _P]),
     "fem_iso_geom": (_I, [_P, _P, _L, _I, _P, _P, _P, _P, _P]),
     "fem_iso_mass": (_I, [_P, _P, _L, _I, _D, _P, _P, _P, _I, _P, _P]),
+    "fem_iso_mass_scalar": (_I, [_P, _P, _L, _I, _D, _P, _P, _P, _I, _P, _P]),
     "fem_pcg_scalars": (_I, [_P, ctypes.POINTER(_D)]),
     "fem_scan_work_len": (_L, [_L]),
     "fem_incidence_work_bytes": (_L, [_L, _L]),
@@ -150,6 +151,7 @@ SIGNATURES = {
     "fem_mf_apply": (_I, [_P, _P, _P, _P]),
     "fem_mf_diag": (_I, [_P, _P, _P]),
     "fem_mf_info": (_I, [_P, ctypes.POINTER(_L)]),
+    "fem_mf_spcheck": (_I, [_P]),
     "fem_mf_order": (_I, [_P, _P, _P, _P, _P, _P]),
     "fem_pcg_set_operator_mf": (_I, [_P, _P]),
     "fem_comm_unique_id": (_I, [ctypes.c_char_p]),

@@ -161,7 +161,7 @@ __device__ __forceinline__ void iso_wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-template <int NPE, bool MASS>
+template <int NPE, bool MASS, bool SC = false>
 __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, const int64_t* __restrict__ conn,
                                                 int64_t M, double E, double nu, const double* __restrict__ dN,
                                                 const double* __restrict__ w, int n_ip, int mode,
@@ -314,7 +314,17 @@ __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, co
         }
         iso_wave_sync();
     }
-    if (mode != FEM_ISO_STACK && active) {   // (the loop above ended on a wave sync: gk_s is free)
+    if (SC && active) {   // scalar mass (MASS only): the NPE x NPE factor of M_e = M_s (x) I3, acc[0] of each block
+        double* ks = gk_s[wid];
+        if (blk_lane) {
+            ks[ba * NPE + bb] = acc[0];
+            if (mirror) ks[bb * NPE + ba] = acc[0];
+        }
+        __builtin_amdgcn_wave_barrier();
+        double2* out2 = reinterpret_cast<double2*>(Ke + e * NPE * NPE);   // NPE^2 even: 16-byte aligned rows
+        const double2* ks2 = reinterpret_cast<const double2*>(ks);
+        for (int t = lane; t < NPE * NPE / 2; t += 64) out2[t] = ks2[t];
+    } else if (mode != FEM_ISO_STACK && active) {   // (the loop above ended on a wave sync: gk_s is free)
         double* ks = gk_s[wid];
         if (blk_lane) {
 #pragma unroll
@@ -337,7 +347,7 @@ __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, co
   }
 }
 
-template <int NPE, bool MASS>
+template <int NPE, bool MASS, bool SC = false>
 __global__ void __launch_bounds__(256) k_iso_ke1(const double* __restrict__ X, const int64_t* __restrict__ conn,
                                                 int64_t M, double E, double nu, const double* __restrict__ dN,
                                                 const double* __restrict__ w, int n_ip, int mode,
@@ -478,7 +488,17 @@ __global__ void __launch_bounds__(256) k_iso_ke1(const double* __restrict__ X, c
         }
         __syncthreads();
     }
-    if (mode != FEM_ISO_STACK && active) {   // (the loop above ended on a barrier: gk_s is free)
+    if (SC && active) {   // scalar mass: as k_iso_ke
+        double* ks = gk_s[wid];
+        if (blk_lane) {
+            ks[ba * NPE + bb] = acc[0];
+            if (mirror) ks[bb * NPE + ba] = acc[0];
+        }
+        __builtin_amdgcn_wave_barrier();
+        double2* out2 = reinterpret_cast<double2*>(Ke + e * NPE * NPE);
+        const double2* ks2 = reinterpret_cast<const double2*>(ks);
+        for (int t = lane; t < NPE * NPE / 2; t += 64) out2[t] = ks2[t];
+    } else if (mode != FEM_ISO_STACK && active) {   // (the loop above ended on a barrier: gk_s is free)
         double* ks = gk_s[wid];
         if (blk_lane) {
 #pragma unroll
@@ -911,6 +931,108 @@ __global__ void __launch_bounds__(R * 64) k_assemble_ke_tile3(const double* __re
                            : dst + (int64_t)64 * (k * B2 + rc) + r;
             if constexpr (STORE) *d = v;                          // padding / missing rows: zero sums
             else if (j0 + k < len_s[r]) *d += v;                  // adding: padding stays as stored
+        }
+    }
+}
+
+// bs = 1 stored-K_e rows (scalar systems from stored element matrices, e.g. the consistent-mass factor M_s of
+// M = M_s (x) I3): per incidence of the row the element's row a of K_e (NPE contiguous doubles), lanes (incidence u,
+// element node b) for 64 / NPE incidences at once; every slot sums in ascending (incidence, b) order from +0.0, the
+// order of k_assemble_ke_w<1, NPE> (bit-identical). acc: the window's nj sums in LDS (zeroed by the caller).
+template <int NPE>
+__device__ __forceinline__ void ke_row1(const double* __restrict__ Ke, const int64_t* __restrict__ conn,
+                                        const int32_t* __restrict__ inc, int t0, int C, const int* cs, int nj,
+                                        double* acc, int lane) {
+    constexpr int KU = 64 / NPE;
+    const int u = lane / NPE, b = lane - NPE * (lane / NPE);
+    for (int k0 = 0; k0 < C; k0 += KU) {
+        const int nu = min(KU, C - k0);
+        double v = 0.0;
+        int s = -1, dup = 0;
+        if (u < nu) {
+            const int ea = inc[t0 + k0 + u];
+            const int e = ea / NPE;
+            v = Ke[(int64_t)e * NPE * NPE + (ea - e * NPE) * NPE + b];
+            const int64_t eb = (int64_t)e * NPE;
+            const int node = (int)conn[eb + b];
+            int l = 0, h = nj;
+            while (l < h) {
+                const int mid = (l + h) >> 1;
+                if (cs[mid] < node) l = mid + 1;
+                else h = mid;
+            }
+            s = (l < nj && cs[l] == node) ? l : -1;
+            for (int b2 = 0; b2 < b; ++b2) dup |= (int)conn[eb + b2] == node;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (!__any(dup)) {
+            for (int uu = 0; uu < nu; ++uu) {   // one incidence at a time: its NPE slots are distinct
+                if (u == uu && s >= 0) acc[s] += v;
+                __builtin_amdgcn_wave_barrier();
+            }
+        } else {   // an element lists a node twice: its b's one after the other
+            for (int uu = 0; uu < nu; ++uu)
+                for (int bb = 0; bb < NPE; ++bb) {
+                    if (u == uu && b == bb && s >= 0) acc[s] += v;
+                    __builtin_amdgcn_wave_barrier();
+                }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Tile form of the bs = 1 stored-K_e assembly: k_assemble_ke_tile3's geometry with one value per entry -- R rows of a
+// slice per workgroup, a wave per row (ke_row1), the window's sums in LDS, then written straight into the SELL values
+// (R contiguous doubles per entry), padding entries and lanes past the last row zeroed in store mode. No csr2sell, no
+// memset, no read of the old values when storing; adding reads each value once and sums onto it in k_assemble_ke_w's
+// order.
+template <int NPE, int R, bool STORE>
+__global__ void __launch_bounds__(R * 64) k_assemble_ke_tile1(const double* __restrict__ Ke,
+                                                               const int64_t* __restrict__ conn,
+                                                               const int32_t* __restrict__ inc_ptr,
+                                                               const int32_t* __restrict__ inc, int64_t N,
+                                                               const int32_t* __restrict__ rowptr,
+                                                               const int32_t* __restrict__ colidx,
+                                                               const int64_t* __restrict__ slice_ptr,
+                                                               double* __restrict__ vals, int Wc, int64_t ntiles) {
+    extern __shared__ double tacc1[];         // [R][Wc + 1]
+    __shared__ int cols_s[R][KR_LMAX];
+    __shared__ int len_s[R];
+    constexpr int T = 64 / R;
+    const int64_t kx = blockIdx.x / NXCD;
+    const int64_t tile = ((kx / T) * NXCD + blockIdx.x % NXCD) * T + kx % T;
+    if (tile >= ntiles) return;
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t r0 = tile * R, i = r0 + wid;
+    const int64_t p0 = slice_ptr[r0 >> 6];
+    const int W = (int)((slice_ptr[(r0 >> 6) + 1] - p0) >> 6);
+    const int l0 = (int)(r0 & 63);
+    const int rs = Wc + 1;
+    int lo = 0, len = 0, t0 = 0, C = 0;
+    if (i < N) {
+        lo = rowptr[i];
+        len = rowptr[i + 1] - lo;
+        t0 = inc_ptr[i];
+        C = inc_ptr[i + 1] - t0;
+    }
+    if (lane == 0) len_s[wid] = len;
+    double* acc = tacc1 + wid * rs;
+    for (int j0 = 0; j0 < W; j0 += Wc) {
+        const int nw = min(Wc, W - j0);
+        const int nj = max(0, min(Wc, len - j0));
+        __syncthreads();   // the previous window written out
+        if (lane < nj) cols_s[wid][lane] = colidx[lo + j0 + lane];
+        // adding: the sums start from the stored values (k_assemble_ke_w<1>'s ((v + c_1) + c_2) ...: the same bits)
+        for (int t = lane; t < nw; t += 64)
+            acc[t] = (!STORE && t < nj) ? vals[p0 + (int64_t)64 * (j0 + t) + l0 + wid] : 0.0;
+        __builtin_amdgcn_wave_barrier();
+        if (nj > 0) ke_row1<NPE>(Ke, conn, inc, t0, C, cols_s[wid], nj, acc, lane);
+        __syncthreads();
+        for (int q = threadIdx.x; q < nw * R; q += R * 64) {
+            const int r = q % R, k = q / R;
+            const double v = tacc1[r * rs + k];
+            double* d = vals + p0 + (int64_t)64 * (j0 + k) + l0 + r;
+            if (STORE || j0 + k < len_s[r]) *d = v;   // adding: padding stays as stored
         }
     }
 }
@@ -1792,8 +1914,21 @@ int fem_iso_ke(const double* coords, const int64_t* conn, int64_t M, int npe, do
     return FEM_OK;
 }
 
+static int iso_mass(const double* coords, const int64_t* conn, int64_t M, int npe, double rho, const double* Nv,
+                    const double* dN, const double* w, int n_ip, double* Me, bool scalar, hipStream_t st);
+
 int fem_iso_mass(const double* coords, const int64_t* conn, int64_t M, int npe, double rho, const double* Nv,
                  const double* dN, const double* w, int n_ip, double* Me, fem_stream_t stream) {
+    return iso_mass(coords, conn, M, npe, rho, Nv, dN, w, n_ip, Me, false, S(stream));
+}
+
+int fem_iso_mass_scalar(const double* coords, const int64_t* conn, int64_t M, int npe, double rho, const double* Nv,
+                        const double* dN, const double* w, int n_ip, double* Ms, fem_stream_t stream) {
+    return iso_mass(coords, conn, M, npe, rho, Nv, dN, w, n_ip, Ms, true, S(stream));
+}
+
+static int iso_mass(const double* coords, const int64_t* conn, int64_t M, int npe, double rho, const double* Nv,
+                    const double* dN, const double* w, int n_ip, double* Me, bool scalar, hipStream_t st) {
     if (M <= 0) return FEM_OK;
     if (n_ip < 1 || n_ip > ISO_MAX_IP) {
         set_error("fem_iso_mass: n_ip = %d out of range [1, %d]", n_ip, ISO_MAX_IP);
@@ -1803,12 +1938,15 @@ int fem_iso_mass(const double* coords, const int64_t* conn, int64_t M, int npe, 
     const size_t lds = sizeof(double) * (size_t)n_ip * npe * 4;
     const void* fn = (const void*)k_iso_ke<10, true>;   // the walking grid (c3d10 only, iso_grid_npe)
     const dim3 g(iso_grid_npe(fn, lds, M, npe));
+#define FEM_IM(K, P, SC_) hipLaunchKernelGGL((K<P, true, SC_>), g, dim3(256), lds, st, coords, conn, M, rho, 0.0, dN, w, \
+                                             n_ip, mode, Me, Nv)
     switch (npe) {
-        case 6: hipLaunchKernelGGL((k_iso_ke1<6, true>), g, dim3(256), lds, S(stream), coords, conn, M, rho, 0.0, dN, w, n_ip, mode, Me, Nv); break;
-        case 8: hipLaunchKernelGGL((k_iso_ke1<8, true>), g, dim3(256), lds, S(stream), coords, conn, M, rho, 0.0, dN, w, n_ip, mode, Me, Nv); break;
-        case 10: hipLaunchKernelGGL((k_iso_ke<10, true>), g, dim3(256), lds, S(stream), coords, conn, M, rho, 0.0, dN, w, n_ip, mode, Me, Nv); break;
+        case 6: if (scalar) FEM_IM(k_iso_ke1, 6, true); else FEM_IM(k_iso_ke1, 6, false); break;
+        case 8: if (scalar) FEM_IM(k_iso_ke1, 8, true); else FEM_IM(k_iso_ke1, 8, false); break;
+        case 10: if (scalar) FEM_IM(k_iso_ke, 10, true); else FEM_IM(k_iso_ke, 10, false); break;
         default: set_error("fem_iso_mass: unsupported nodes per element %d", npe); return FEM_EBADTYPE;
     }
+#undef FEM_IM
     FEM_LAUNCHED();
     return FEM_OK;
 }
@@ -1879,6 +2017,27 @@ static int assemble_from_ke(const double* Ke, const int64_t* conn, int npe, int 
     }
     const bool csrw = bs == 3 && getenv("FEM355_KE_DIRECT") == nullptr && N > 0 &&
                       (npe == 4 || npe == 6 || npe == 8 || npe == 10);
+    // bs = 1 with the pattern's widest slice known: the tile form (k_assemble_ke_tile1; FEM355_KE_ROWS: wave per row)
+    const bool tile1 = bs == 1 && max_width > 0 && N > 0 && (npe == 4 || npe == 6 || npe == 8 || npe == 10) &&
+                       getenv("FEM355_KE_ROWS") == nullptr;
+    if (tile1) {
+        const int Wc = max_width < KR_LMAX ? max_width : KR_LMAX;
+        constexpr int R1 = 16;
+        const size_t dyn = sizeof(double) * (size_t)R1 * (Wc + 1);
+        const int64_t ntiles = cdiv(N, 64) * (64 / R1);
+        const dim3 g((unsigned)(cdiv(cdiv(N, 64), NXCD) * NXCD * (64 / R1)));
+#define FEM_KT1(P)                                                                                                 \
+    if (npe == P) {                                                                                                \
+        if (store) hipLaunchKernelGGL((k_assemble_ke_tile1<P, R1, true>), g, dim3(R1 * 64), dyn, S(stream), Ke, conn, \
+                                      inc_ptr, inc, N, rowptr, colidx, slice_ptr, vals, Wc, ntiles);             \
+        else hipLaunchKernelGGL((k_assemble_ke_tile1<P, R1, false>), g, dim3(R1 * 64), dyn, S(stream), Ke, conn,    \
+                                inc_ptr, inc, N, rowptr, colidx, slice_ptr, vals, Wc, ntiles);                   \
+    }
+        FEM_KT1(4) FEM_KT1(6) FEM_KT1(8) FEM_KT1(10)
+#undef FEM_KT1
+        FEM_LAUNCHED();
+        return FEM_OK;
+    }
     // store mode on the paths that add in place: zero the matrix first (the block-CSR path stores every entry)
     if (store && !csrw && ent > 0) FEM_HIP(hipMemsetAsync(vals, 0, sizeof(double) * bs * bs * (size_t)ent, S(stream)));
     if ((bs == 1 || bs == 3) && (npe == 4 || npe == 6 || npe == 8 || npe == 10)) {   // wave per row

@@ -547,6 +547,22 @@ int fem_mf_diag(fem_mf* m, double* d, fem_stream_t stream) {
     return mf_run(m, MF_DIAG, nullptr, d, m->slots, S(stream));
 }
 
+// debug build only (FEM_MF_SPCHECK = 1): read and reset the carried-vs-reread slot position counters (out8); FEM_EARG
+// in a normal build
+int fem_mf_spcheck(uint64_t* out8) {
+#if FEM_MF_SPCHECK
+    FEM_HIP(hipDeviceSynchronize());
+    FEM_HIP(hipMemcpyFromSymbol(out8, HIP_SYMBOL(mf_spcheck), sizeof(unsigned long long) * 8));
+    unsigned long long z[8] = {0};
+    FEM_HIP(hipMemcpyToSymbol(HIP_SYMBOL(mf_spcheck), z, sizeof(z)));
+    return FEM_OK;
+#else
+    (void)out8;
+    set_error("fem_mf_spcheck: not a FEM_MF_SPCHECK build");
+    return FEM_EARG;
+#endif
+}
+
 int fem_mf_info(fem_mf* m, int64_t* out6) {
     if (!m || !out6) {
         set_error("fem_mf_info: bad arguments");

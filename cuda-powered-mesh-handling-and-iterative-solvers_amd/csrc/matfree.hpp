@@ -62,6 +62,17 @@ constexpr int MF_U = FEM_MF_UNROLL;   // pairs whose LDS reads are issued togeth
 
 enum { MF_APPLY = 0, MF_DOT = 1, MF_DIAG = 2 };
 
+// FEM_MF_SPCHECK = 1 (debug build, tools/mf_spcheck.py; never the default): the slot position ALSO carried through
+// the prefetch records, as the walk did before commit c83e619, and compared at every slot store with the position
+// read under the chunk's work. mf_spcheck: [0] stores checked, [1] mismatches, [2] first mismatch (chunk << 16 | tid),
+// [3] its carried value, [4] the expected one, [5] its walk step (0 = first chunk of the workgroup)
+#ifndef FEM_MF_SPCHECK
+#define FEM_MF_SPCHECK 0
+#endif
+#if FEM_MF_SPCHECK
+__device__ unsigned long long mf_spcheck[8];
+#endif
+
 // staged corners of a mode (the diagonal's corner-0 values are not -(f_1 + f_2 + f_3))
 template <int MODE>
 constexpr int mf_fc() { return (FEM_MF_F0 && MODE != MF_DIAG) ? 3 : 4; }
@@ -215,6 +226,9 @@ template <int BS>
 struct MfPf {
     int e0, ne, s0, nn;
     int node;
+#if FEM_MF_SPCHECK
+    int sp;
+#endif
     uint16_t lp;
     uint4 ent;
     uint32_t el[MF_EC / MF_PASS];
@@ -236,6 +250,10 @@ __device__ __forceinline__ void mf_pf1(const MfOp& op, int64_t c, MfPf<BS>& f) {
     for (int k = 0; k < 3; ++k) f.xv[k] = 0.0;
 #pragma unroll
     for (int k = 0; k < BS; ++k) f.pv[k] = 0.0;
+#if FEM_MF_SPCHECK
+    f.sp = 0;
+    if (tid < f.nn) f.sp = op.spos ? op.spos[f.s0 + tid] : f.s0 + tid;
+#endif
     if (tid < f.nn) {
         f.node = op.cnode[f.s0 + tid];
         f.lp = op.lptr[f.s0 + c + tid];
@@ -273,6 +291,9 @@ __device__ __forceinline__ double mf_walk(const MfOp& op, const double* __restri
     int64_t k = blockIdx.x / NXCD;
     double dot = 0.0;
     if (k >= per || base + k >= op.nchunks) return dot;
+#if FEM_MF_SPCHECK
+    int step = 0;
+#endif
     // three chunks in flight: cur (installed in LDS now), n1 (its node gathers issued at the top of this chunk,
     // needed at the next install), n2 (its ids / pairs / local ids issued now, its gathers at the next chunk's top):
     // every load has a whole chunk of work to arrive (~1-2 us of HBM latency under load)
@@ -382,7 +403,19 @@ __device__ __forceinline__ double mf_walk(const MfOp& op, const double* __restri
                 mf_store_slot(&slots[(int64_t)spc * BS + q], acc[q]);
                 if constexpr (MODE == MF_DOT) dot += cur.pv[q] * acc[q];
             }
+#if FEM_MF_SPCHECK
+            atomicAdd(&mf_spcheck[0], 1ull);
+            if (cur.sp != spc && atomicAdd(&mf_spcheck[1], 1ull) == 0) {
+                mf_spcheck[2] = ((unsigned long long)(base + k) << 16) | (unsigned)tid;
+                mf_spcheck[3] = (unsigned)cur.sp;
+                mf_spcheck[4] = (unsigned)spc;
+                mf_spcheck[5] = (unsigned)step;
+            }
+#endif
         }
+#if FEM_MF_SPCHECK
+        ++step;
+#endif
         if (!has1) break;
         k += nb;
         cur = n1;

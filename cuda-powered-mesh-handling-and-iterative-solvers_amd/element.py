@@ -378,7 +378,7 @@ def _iso_ke(coords, elements, etype, E, nu, points, weights, mode, device, dtype
     return _out(K, device, dtype)
 
 
-def _iso_mass(coords, elements, etype, rho, device, dtype):
+def _iso_mass(coords, elements, etype, rho, device, dtype, scalar=False):
     lib = C.lib()
     dev, coords, elements = _prep(coords, elements, device)
     npe = _ISO[etype][0]
@@ -391,10 +391,11 @@ def _iso_mass(coords, elements, etype, rho, device, dtype):
                     lambda: torch.tensor([_N[etype](*[float(v) for v in p[q]]) for q in range(p.shape[0])], dtype=F64),
                     dev)
     w = _dev_const(("w", w.to("cpu", F64).contiguous().numpy().tobytes()), lambda: w.to("cpu", F64), dev)
-    d = 3 * npe
+    d = npe if scalar else 3 * npe
     Me = torch.empty((M, d, d), dtype=F64, device=dev)
-    C.check(lib.fem_iso_mass(C.ptr(coords), C.ptr(elements), M, npe, float(rho), C.ptr(Nv.contiguous()), C.ptr(dN),
-                             C.ptr(w), p.shape[0], C.ptr(Me), C.stream(dev)), "fem_iso_mass")
+    fn = lib.fem_iso_mass_scalar if scalar else lib.fem_iso_mass
+    C.check(fn(C.ptr(coords), C.ptr(elements), M, npe, float(rho), C.ptr(Nv.contiguous()), C.ptr(dN), C.ptr(w),
+               p.shape[0], C.ptr(Me), C.stream(dev)), "fem_iso_mass")
     return _out(Me, device, dtype)
 
 
@@ -416,13 +417,18 @@ def compute_c3d10_M_matrix(coords, elements, rho, device="cuda:0", dtype=torch.f
     return _iso_mass(coords, elements, "c3d10", rho, device, dtype)
 
 
-def compute_M_matrix(coords, elements, element_type, rho, device="cuda:0", dtype=torch.float32):
-    """Consistent mass dispatch over c3d4 / c3d6 / c3d8 / c3d10 (ValueError otherwise, like compute_K_matrix)."""
+def compute_M_matrix(coords, elements, element_type, rho, device="cuda:0", dtype=torch.float32, scalar=False):
+    """Consistent mass dispatch over c3d4 / c3d6 / c3d8 / c3d10 (ValueError otherwise, like compute_K_matrix).
+    scalar=True (c3d6 / c3d8 / c3d10): the scalar factor Ms [M, npe, npe] of M_e = Ms (x) I3 instead of the
+    [M, 3 npe, 3 npe] matrix -- the same values, 1/9 of the bytes; assembled as a bs = 1 matrix on the node pattern
+    it is the global factor of M = M_s (x) I3. Parity unpinned (no reference function)."""
     et = element_type.lower()
     if et == "c3d4":
+        if scalar:
+            raise ValueError("scalar=True: c3d6 / c3d8 / c3d10 (the c3d4 mass is compute_c3d4_M_matrix)")
         return compute_c3d4_M_matrix(coords, elements, rho, device=device, dtype=dtype)
     if et in _N:
-        return _iso_mass(coords, elements, et, rho, device, dtype)
+        return _iso_mass(coords, elements, et, rho, device, dtype, scalar)
     _unsupported(element_type)
 
 

@@ -389,6 +389,9 @@ class SellMatrix:
                     "fem_assemble_from_ke_sl")
             self._sl_ok, self._plain_ok = True, False
             return self
+        # bs = 1: the tile form as well (k_assemble_ke_tile1: no csr2sell map, no memset)
+        tiled = tiled or (self.bs == 1 and self.g.max_width > 0 and npe in (4, 6, 8, 10)
+                          and not os.environ.get("FEM355_KE_ROWS"))
         self._modify_plain()
         store = self._fresh
         self._fresh = False

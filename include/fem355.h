@@ -99,6 +99,11 @@ int fem_iso_ke(const double* coords, const int64_t* conn, int64_t M, int npe, do
  * (element.py picks rules exact for N_a N_b on affine elements). */
 int fem_iso_mass(const double* coords, const int64_t* conn, int64_t M, int npe, double rho, const double* Nv,
                  const double* dN, const double* w, int n_ip, double* Me, fem_stream_t stream);
+/* the same consistent mass as its scalar factor: Ms [M, npe, npe] with M_e = Ms (x) I3 (block (a, b) = Ms[a][b] I3,
+ * the values of fem_iso_mass's diagonal entries bit for bit) -- 1/9 of the bytes; assembled as a bs = 1 matrix on the
+ * same node pattern it is the global M_s of M = M_s (x) I3 */
+int fem_iso_mass_scalar(const double* coords, const int64_t* conn, int64_t M, int npe, double rho, const double* Nv,
+                        const double* dN, const double* w, int n_ip, double* Ms, fem_stream_t stream);
 /* J [M,3,3] (J[i][k] = sum_j dN[j][i] x_j[k]), global gradients [M,npe,3] and B [M,6,3npe] of an isoparametric
  * element at one point with natural derivatives dN [npe,3]; outputs may be NULL. Replaces compute_c3d8_Jacobian /
  * _shape_gradients / _B_matrix (`solver/element.py:1601-1694`) and the c3d6 (`:2482-2568`) / c3d10
@@ -660,6 +665,11 @@ int fem_mf_destroy(fem_mf* m);
 int fem_mf_apply(fem_mf* m, const double* x, double* y, fem_stream_t stream);
 /* d = diag(K) [N*bs] (the exact diagonal) */
 int fem_mf_diag(fem_mf* m, double* d, fem_stream_t stream);
+/* debug builds only (-DFEM_MF_SPCHECK=1, tools/mf_spcheck.py): the stand-alone applications also carry each slot
+ * position through the chunk walk's prefetch records and compare it at every store with the one read under the chunk;
+ * out8 = {stores checked, mismatches, first mismatch (chunk << 16 | thread), carried, expected, walk step}, counters
+ * reset. FEM_EARG in a normal build. */
+int fem_mf_spcheck(uint64_t* out8);
 /* out6 = {chunks, slots, bs, static bytes streamed per application, M, N} */
 int fem_mf_info(fem_mf* m, int64_t* out6);
 /* device copies of the layout (each nullable): Morton element order [M], chunk element offsets and slot offsets

@@ -1241,3 +1241,44 @@ def test_vals_edits_are_seen_by_solves(gpu):
     assert torch.equal(w2, 0.5 * w)
     r2 = A.pcg(b, w=w2, tol=0.0, max_iter=30)
     assert torch.equal(r2.x, 0.5 * r1.x)
+
+
+@pytest.mark.parametrize("etype,gen,n", [("c3d8", "hex_box", 5), ("c3d6", "wedge_box", 5), ("c3d10", "tet10_cube", 4)])
+def test_scalar_mass_and_bs1_tile_assembly(gpu, etype, gen, n, monkeypatch):
+    """BASELINE configs[4]'s mass as its scalar factor (compute_M_matrix(..., scalar=True), fem_iso_mass_scalar):
+    M_e = Ms (x) I3 bit for bit, and the bs = 1 global Ms (k_assemble_ke_tile1) = the diagonal entries of every 3x3
+    block of the bs = 3 global mass, off-diagonal entries zero; the tile form equals the wave-per-row kernel
+    (FEM355_KE_ROWS) bit for bit when storing and when adding onto stored values. Parity unpinned (no reference mass)."""
+    el_mod, mesh, _, system = _mods()
+    c, t = getattr(mesh, gen)(n, jitter=0.1)
+    cg, tg = c.to(gpu), t.to(gpu)
+    N = c.shape[0]
+    rho = 4.47e-3
+    Ms = el_mod.compute_M_matrix(cg, tg, etype, rho, device=gpu, dtype=F64, scalar=True)
+    Me = el_mod.compute_M_matrix(cg, tg, etype, rho, device=gpu, dtype=F64)
+    npe = t.shape[1]
+    assert Ms.shape == (t.shape[0], npe, npe)
+    kron = torch.einsum("mab,ij->maibj", Ms, torch.eye(3, dtype=F64, device=gpu)).reshape(Me.shape)
+    assert torch.equal(kron, Me)
+    g = system.build_graph(tg, N)
+    A1 = system.SellMatrix(g, 1).add_element_matrices(Ms, tg)
+    A3 = system.SellMatrix(g, 3).add_element_matrices(Me, tg)
+    _, _, v1 = A1.csr()
+    _, _, v3 = A3.csr()
+    for i in range(3):
+        assert torch.equal(v3[:, i, i], v1[:, 0, 0])
+    off = v3.clone()
+    for i in range(3):
+        off[:, i, i] = 0.0
+    assert float(off.abs().max()) == 0.0
+    assert abs(float(v1.sum()) / rho - 1.0) < 1e-12   # total mass = rho x unit volume
+    # tile form vs the wave-per-row kernel: stored, then a second family added on top
+    A1.add_element_matrices(Ms, tg)
+    monkeypatch.setenv("FEM355_KE_ROWS", "1")
+    B1 = system.SellMatrix(g, 1).add_element_matrices(Ms, tg)
+    fresh = B1.plain_values().clone()
+    B1.add_element_matrices(Ms, tg)
+    monkeypatch.delenv("FEM355_KE_ROWS")
+    A1b = system.SellMatrix(g, 1).add_element_matrices(Ms, tg)
+    assert torch.equal(A1b.plain_values(), fresh)
+    assert torch.equal(A1.plain_values(), B1.plain_values())
