@@ -58,6 +58,7 @@ SIGNATURES = {
     "fem_graph_count2": (_I, [_P, _I, _P, _P, _L, _P, _P, _P, _P]),
     "fem_graph_fill2": (_I, [_P, _I, _P, _P, _L, _P, _P, _P, _P, _P]),
     "fem_graph_sell_fill": (_I, [_P, _I, _P, _P, _L, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "fem_graph_sell_fill_sl": (_I, [_P, _I, _P, _P, _L, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P]),
     "fem_scan_i32": (_I, [_P, _L, _P, _P, _P]),
     "fem_scan_i64": (_I, [_P, _L, _P, _P, _P]),
     "fem_sell_widths": (_I, [_P, _L, _P, _P]),

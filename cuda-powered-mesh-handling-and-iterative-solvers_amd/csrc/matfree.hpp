@@ -43,10 +43,13 @@ constexpr int MF_EC = 64;       // elements per chunk (at most)
 constexpr int MF_NC = 64;       // local nodes per chunk (at most)
 constexpr int MF_PIECE = 16;    // elements per piece of a chunk that touched more than MF_NC nodes
 #else
+// 240 nodes (not 256): with the pair pointers in registers and the element vectors unpadded the chunk's LDS is
+// 40,192 bytes, so 4 workgroups (16 waves) share a CU instead of 3 (41.6 KB each)
 constexpr int MF_EC = 512;
-constexpr int MF_NC = 256;      // local ids are bytes
-constexpr int MF_PIECE = 64;
+constexpr int MF_NC = 240;      // local ids are bytes
+constexpr int MF_PIECE = 32;
 #endif
+static_assert(4 * MF_PIECE <= MF_NC, "a piece of MF_PIECE elements always fits the node cap");
 constexpr int MF_PASS = 256;    // elements formed per pass (= threads of the workgroup; workgroup chunks)
 constexpr int MF_BLOCK = 256;
 #ifndef FEM_MF_UNROLL
@@ -68,6 +71,9 @@ enum { MF_APPLY = 0, MF_DOT = 1, MF_DIAG = 2 };
 // [3] its carried value, [4] the expected one, [5] its walk step (0 = first chunk of the workgroup)
 #ifndef FEM_MF_SPCHECK
 #define FEM_MF_SPCHECK 0
+#endif
+#ifndef FEM_MF_PF_UNDEF
+#define FEM_MF_PF_UNDEF 0
 #endif
 #if FEM_MF_SPCHECK
 __device__ unsigned long long mf_spcheck[8];
@@ -197,12 +203,11 @@ __device__ __forceinline__ void mf_element(const double xc[4][3], const double x
     }
 }
 
-// LDS of one chunk application
+// LDS of one chunk application (a local node's pair range [lp, lp1) travels in its thread's registers)
 template <int BS, int FC>
 struct MfLds {
     double nd[MF_NC][3 + BS];        // per local node: coordinates, then x (rows 16-byte aligned: 48 / 32 bytes)
-    double fs[FC * BS][MF_PASS + 1];   // element vectors of the current pass: [staged corner * BS + c][element]
-    uint16_t lp[MF_NC + 1];          // pair pointers of the local nodes
+    double fs[FC * BS][MF_PASS];     // element vectors of the current pass: [staged corner * BS + c][element]
     alignas(16) uint16_t ent[4 * MF_EC];   // the chunk's pairs, node-major
 };
 
@@ -221,11 +226,12 @@ __device__ __forceinline__ void mf_pair_value(const MfLds<BS, FC>& L, int pe, in
 }
 
 // What a thread loads for one chunk ahead of its use (software pipeline over a workgroup's chunks): the chunk's
-// ranges, this thread's local node (id, coordinates, x), pair pointer, 8 pairs and the local ids of its 2 elements.
+// ranges, this thread's local node (id, coordinates, x), its pair range, 8 pairs and the local ids of its 2 elements.
 template <int BS>
 struct MfPf {
     int e0, ne, s0, nn;
     int node;
+    uint16_t lp1;   // end of the node's pairs (lp: their start)
 #if FEM_MF_SPCHECK
     int sp;
 #endif
@@ -245,18 +251,23 @@ __device__ __forceinline__ void mf_pf1(const MfOp& op, int64_t c, MfPf<BS>& f) {
     f.nn = op.sbase[c + 1] - f.s0;
     f.node = 0;
     f.lp = 0;
-    // every field defined in every lane (the pipeline copies whole records; stage 2 fills xv / pv for tid < nn)
+    // every field defined in every lane (the pipeline copies whole records; stage 2 fills xv / pv for tid < nn).
+    // FEM_MF_PF_UNDEF = 1 (debug builds only, tools/mf_spcheck.py): leave them indeterminate as before round 5
+#if !FEM_MF_PF_UNDEF
 #pragma unroll
     for (int k = 0; k < 3; ++k) f.xv[k] = 0.0;
 #pragma unroll
     for (int k = 0; k < BS; ++k) f.pv[k] = 0.0;
+#endif
 #if FEM_MF_SPCHECK
     f.sp = 0;
     if (tid < f.nn) f.sp = op.spos ? op.spos[f.s0 + tid] : f.s0 + tid;
 #endif
+    f.lp1 = 0;
     if (tid < f.nn) {
         f.node = op.cnode[f.s0 + tid];
         f.lp = op.lptr[f.s0 + c + tid];
+        f.lp1 = op.lptr[f.s0 + c + tid + 1];   // the chunk's end marker for its last node
     }
     f.ent = make_uint4(0, 0, 0, 0);
     if (8 * tid < 4 * f.ne) f.ent = reinterpret_cast<const uint4*>(op.lent + 4 * (int64_t)f.e0)[tid];
@@ -309,9 +320,7 @@ __device__ __forceinline__ double mf_walk(const MfOp& op, const double* __restri
             for (int q = 0; q < 3; ++q) L.nd[tid][q] = cur.xv[q];
 #pragma unroll
             for (int q = 0; q < BS; ++q) L.nd[tid][3 + q] = cur.pv[q];
-            L.lp[tid] = cur.lp;
         }
-        if (tid == 0) L.lp[cur.nn] = (uint16_t)(4 * cur.ne);
         if (8 * tid < 4 * cur.ne) reinterpret_cast<uint4*>(L.ent)[tid] = cur.ent;
         const int64_t k2 = k + 2 * nb;
         const bool has2 = has1 && k2 < per && base + k2 < op.nchunks;
@@ -326,8 +335,8 @@ __device__ __forceinline__ double mf_walk(const MfOp& op, const double* __restri
         double acc[BS];
 #pragma unroll
         for (int q = 0; q < BS; ++q) acc[q] = 0.0;
-        int pos = tid < cur.nn ? L.lp[tid] : 0;
-        const int end = tid < cur.nn ? L.lp[tid + 1] : 0;
+        int pos = tid < cur.nn ? (int)cur.lp : 0;
+        const int end = tid < cur.nn ? (int)cur.lp1 : 0;
         // the node's pairs split at the pass boundary (pairs ascend by element): lower bound of 4 MF_PASS
         int mid = end;
         if (cur.ne > MF_PASS) {

@@ -9,6 +9,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "common.hpp"
+#include "sell_pair.hpp"   // sl_pattern_slice (the bs = 1 solver layout, formed in the fill pass)
 
 namespace fem {
 
@@ -758,14 +759,22 @@ __global__ void __launch_bounds__(256) k_sell_fill(const int32_t* __restrict__ r
 // 16-bit deltas; a row comes from k_graph_small's tmp (32 slots per node) or, for the rows it deferred, from colidx
 // (already filled by k_graph / k_graph_big). Lane = CSR position of the slice's contiguous segment: csr2sell, and
 // colidx of the tmp rows, written contiguously (the row of a position by binary search over the slice's row starts).
+// pout != null (fem_graph_sell_fill_sl): the bs = 1 solver layout of the slice too (sl_pattern_slice: lane-paired
+// deltas, slice-uniform lists, the persistent schedule's gather windows) from the deltas this wave just wrote -- the
+// separate k_sell_sl_pattern pass and its re-read of every delta from memory folded in.
 __global__ void __launch_bounds__(256) k_sell_fill_graph(const int32_t* __restrict__ rowptr,
                                                          const int32_t* __restrict__ tmp,
                                                          const uint8_t* __restrict__ defer, int64_t nrows,
                                                          int64_t nslices, const int64_t* __restrict__ slice_ptr,
                                                          int32_t* __restrict__ colidx, int32_t* __restrict__ diagpos,
                                                          int32_t* __restrict__ cols, int16_t* __restrict__ dcols,
-                                                         int64_t* __restrict__ csr2sell, int32_t* __restrict__ overflow) {
+                                                         int64_t* __restrict__ csr2sell, int32_t* __restrict__ overflow,
+                                                         int16_t* __restrict__ pout = nullptr,
+                                                         int16_t* __restrict__ ucol = nullptr,
+                                                         int32_t* __restrict__ uoff = nullptr, int G = 0,
+                                                         int* __restrict__ win = nullptr) {
     __shared__ int32_t rp_s[4][65];
+    __shared__ int cand_all[4][SU_MAXW];
     constexpr int TS = G_TCAP + 1;   // padded row stride: lane = row reads hit distinct banks
     __shared__ int32_t row_s[4][64 * TS];
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -832,6 +841,8 @@ __global__ void __launch_bounds__(256) k_sell_fill_graph(const int32_t* __restri
             }
         }
         if (overflow && __ballot(far) && lane == 0 && !*overflow) atomicOr(overflow, 1);
+        if (pout && dcols) sl_pattern_slice(s, lane, nslices, nrows, slice_ptr, dcols, pout, ucol, uoff, G, win,
+                                            cand_all[wid]);
         const int p0 = rp_s[wid][0], p1 = rp_s[wid][64];
         for (int p = p0 + lane; p < p1; p += 64) {
             int lo = 0, hi = 64;   // last row l with rp_s[l] <= p
@@ -846,6 +857,15 @@ __global__ void __launch_bounds__(256) k_sell_fill_graph(const int32_t* __restri
             if (!defer[row]) colidx[p] = rows[lo * TS + k];
         }
         __builtin_amdgcn_wave_barrier();   // the staged rows consumed before the next slice overwrites them
+    }
+}
+
+// empty gather windows (pcg_persist.hpp k_pk_window_init with lo_empty = G)
+__global__ void k_win_init(int G, int* __restrict__ win) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < G) {
+        win[i] = G;
+        win[G + i] = -1;
     }
 }
 
@@ -1127,6 +1147,31 @@ int fem_graph_sell_fill(const int64_t* conn, int npe, const int32_t* inc_ptr, co
     hipLaunchKernelGGL(k_sell_fill_graph, dim3((unsigned)std::min<int64_t>(cdiv(ns, 4), 16384)), dim3(256), 0, st,
                        rowptr, tmp, defer_flags(tmp, N), N, ns, slice_ptr, colidx, diagpos, cols, dcols, csr2sell,
                        overflow);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
+int fem_graph_sell_fill_sl(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
+                           const int32_t* rowptr, const int32_t* tmp, const int64_t* slice_ptr, int32_t* colidx,
+                           int32_t* diagpos, int32_t* cols, int16_t* dcols, int G, int16_t* pcols, int16_t* ucol,
+                           int32_t* uoff, int32_t* win, fem_stream_t stream) {
+    if (N <= 0) return FEM_OK;
+    if (!dcols || !pcols || !ucol || !uoff || (G > 0 && !win)) {
+        set_error("fem_graph_sell_fill_sl: the 16-bit deltas and the solver-layout arrays are required");
+        return FEM_EARG;
+    }
+    hipStream_t st = S(stream);
+    FEM_HIP(hipMemsetAsync(diagpos, 0xff, sizeof(int32_t) * (size_t)N, st));   // -1: no diagonal
+    if (G > 0) {   // empty windows (k_pk_window_init's values: lo = G, hi = -1)
+        hipLaunchKernelGGL(k_win_init, dim3((unsigned)cdiv(G, 256)), dim3(256), 0, st, G, win);
+        FEM_LAUNCHED();
+    }
+    const int rc = graph_fill(conn, npe, inc_ptr, inc, N, rowptr, colidx, diagpos, defer_flags(tmp, N), st);
+    if (rc != FEM_OK) return rc;
+    const int64_t ns = cdiv(N, 64);
+    hipLaunchKernelGGL(k_sell_fill_graph, dim3((unsigned)std::min<int64_t>(cdiv(ns, 4), 16384)), dim3(256), 0, st,
+                       rowptr, tmp, defer_flags(tmp, N), N, ns, slice_ptr, colidx, diagpos, cols, dcols,
+                       (int64_t*)nullptr, (int32_t*)nullptr, pcols, ucol, uoff, G, win);
     FEM_LAUNCHED();
     return FEM_OK;
 }

@@ -3402,77 +3402,9 @@ __global__ void __launch_bounds__(256) k_sell_sl_pattern(int64_t nslices, int64_
                                                          int* __restrict__ win) {
     __shared__ int cand_all[4][SU_MAXW];
     const int64_t s = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;   // one wave per slice
-    const int l = threadIdx.x & 63;
-    int* cand = cand_all[(threadIdx.x >> 6) & 3];
     if (s >= nslices) return;   // wave-uniform
-    const int64_t p0 = slice_ptr[s];
-    const int w = (int)((slice_ptr[s + 1] - p0) >> 6);
-    const int64_t row = s * 64 + l;
-    if (G > 0) {   // gather window (k_pk_window): the delta union of the slice over its owner workgroup
-        int dmin = 0, dmax = 0;
-        if (row < nrows)
-            for (int k = 0; k < w; ++k) {
-                const int d = cin[p0 + 64 * k + l];
-                dmin = d < dmin ? d : dmin;
-                dmax = d > dmax ? d : dmax;
-            }
-        int64_t cmin, cmax;
-        pk_slice_span(s, nrows, dmin, dmax, &cmin, &cmax);
-        const int64_t WV = (int64_t)G * PK_WAVES;
-        auto owner = [&](int64_t r) { return (int)((((r >> 6) + 1) * WV - 1) / nslices / PK_WAVES); };
-        if (l == 0) {
-            const int me = owner(row);
-            atomicMin(win + me, owner(cmin));
-            atomicMax(win + G + me, owner(cmax));
-        }
-    }
-    bool ok = (s + 1) * 64 <= nrows && w > 0 && w <= SU_MAXW;
-    int len = 0;
-    if (ok) {
-        int prev = -(1 << 30);
-        for (int k = 0; k < w; ++k) {
-            const int d = cin[p0 + 64 * k + l];
-            if (len == k && d > prev) {
-                ++len;
-                prev = d;
-            } else if (d != 0) {
-                ok = false;
-            }
-        }
-    }
-    ok = __all(ok);
-    const unsigned long long full = __ballot(ok && len == w);
-    if (ok && full) {
-        const int c = __builtin_ctzll(full);
-        for (int k = 0; k < w; ++k) {
-            const int d = __shfl((int)cin[p0 + 64 * k + l], c, 64);
-            if (l == 0) cand[k] = d;
-            const int64_t col = row + d;
-            if (col < 0 || col >= nrows) ok = false;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        int i = 0;
-        for (int k = 0; k < len && ok; ++k) {
-            const int d = cin[p0 + 64 * k + l];
-            while (i < w && cand[i] < d) ++i;
-            if (i == w || cand[i] != d) ok = false;
-            ++i;
-        }
-    } else {
-        ok = false;
-    }
-    ok = __all(ok);
-    if (!ok) {
-        if (l == 0) uoff[s] = -1;
-        for (int k = 0; k < w; ++k) pout[p0 + pair_pos(k, w, l)] = cin[p0 + 64 * k + l];
-        return;
-    }
-    const int32_t uo = (int32_t)(2 * (p0 >> 6));   // even: the deltas are read as int32 pairs
-    for (int k = 0; k < w; ++k) pout[p0 + pair_pos(k, w, l)] = (int16_t)cand[k];
-    for (int k = l; k < w; k += 64) ucol[uo + k] = (int16_t)cand[k];
-    if (l == 0) uoff[s] = uo;
+    sl_pattern_slice(s, threadIdx.x & 63, nslices, nrows, slice_ptr, cin, pout, ucol, uoff, G, win,
+                     cand_all[(threadIdx.x >> 6) & 3]);
 }
 
 // host view of the state: the deferred schedule keeps it in the bank of the current launch parity

@@ -29,8 +29,8 @@
 
 namespace fem {
 
-constexpr int PK_T = 1024;               // threads per workgroup (16 waves, 4 per SIMD)
-constexpr int PK_WAVES = PK_T / 64;
+// PK_T / PK_WAVES (threads / waves per workgroup) and pk_slice_span live in sell_pair.hpp: the pattern pass that
+// forms the gather windows (sl_pattern_slice) needs them outside this header
 constexpr int PK_MAXS = 7;               // slices per wave (10M Poisson: 27,000 slices over 4,096 waves -> 7)
 constexpr int PK_U = 2;                  // pairs in flight per lane (4 spills the slot state; persist_probe: 4 = 8)
 // pairs in flight of a build: one slot per wave (small systems: every wave owns at most one slice, e.g. 1M tets or
@@ -824,25 +824,6 @@ __global__ void k_pk_window_init(int G, int lo_empty, int* __restrict__ win) {
         win[i] = lo_empty;
         win[G + i] = -1;
     }
-}
-
-// gather window per logical workgroup: the first and last workgroup owning a column of its rows. A slice-uniform
-// slice (sell_pair.hpp) makes every lane gather at the whole slice's delta list, i.e. also at offsets its own row
-// lacks (value 0 there). So the window of a slice is taken over the UNION of its rows' deltas applied to every row
-// of the slice: [s*64 + min delta, s*64 + 63 + max delta]. Every column any lane reads is then inside a window the
-// workgroup waits on -- no read of an unsynchronised u, whose value (0 * Inf = NaN) would otherwise matter.
-__device__ __forceinline__ void pk_slice_span(int64_t s, int64_t nrows, int dmin, int dmax, int64_t* cmin, int64_t* cmax) {
-    for (int off = 32; off > 0; off >>= 1) {
-        const int a2 = __shfl_xor(dmin, off), b2 = __shfl_xor(dmax, off);
-        dmin = a2 < dmin ? a2 : dmin;
-        dmax = b2 > dmax ? b2 : dmax;
-    }
-    int64_t lo = s * 64 + dmin, hi = s * 64 + 63 + dmax;
-    if (hi >= nrows) hi = nrows - 1;
-    if (lo < 0) lo = 0;
-    if (lo > hi) lo = hi;
-    *cmin = lo;
-    *cmax = hi;
 }
 
 __global__ void k_pk_window(int64_t nslices, int64_t nrows, const int64_t* __restrict__ slice_ptr,

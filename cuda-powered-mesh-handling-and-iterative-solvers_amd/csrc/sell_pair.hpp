@@ -64,6 +64,105 @@ __device__ __forceinline__ double ldx_col(const double* x, int col, int own_lo, 
 // row's real deltas are a subsequence of that row's, every padded column row + delta lies in [0, nrows), and the
 // trailing SELL padding entries of every row are (delta 0, value 0).
 constexpr int SU_MAXW = 64;
+
+constexpr int PK_T = 1024;               // threads per workgroup of the persistent schedule (16 waves, 4 per SIMD)
+constexpr int PK_WAVES = PK_T / 64;
+
+// gather window per logical workgroup: the first and last workgroup owning a column of its rows. A slice-uniform
+// slice (sell_pair.hpp) makes every lane gather at the whole slice's delta list, i.e. also at offsets its own row
+// lacks (value 0 there). So the window of a slice is taken over the UNION of its rows' deltas applied to every row
+// of the slice: [s*64 + min delta, s*64 + 63 + max delta]. Every column any lane reads is then inside a window the
+// workgroup waits on -- no read of an unsynchronised u, whose value (0 * Inf = NaN) would otherwise matter.
+__device__ __forceinline__ void pk_slice_span(int64_t s, int64_t nrows, int dmin, int dmax, int64_t* cmin, int64_t* cmax) {
+    for (int off = 32; off > 0; off >>= 1) {
+        const int a2 = __shfl_xor(dmin, off), b2 = __shfl_xor(dmax, off);
+        dmin = a2 < dmin ? a2 : dmin;
+        dmax = b2 > dmax ? b2 : dmax;
+    }
+    int64_t lo = s * 64 + dmin, hi = s * 64 + 63 + dmax;
+    if (hi >= nrows) hi = nrows - 1;
+    if (lo < 0) lo = 0;
+    if (lo > hi) lo = hi;
+    *cmin = lo;
+    *cmax = hi;
+}
+
+// The solver layout of one slice s of a bs = 1 pattern, by the wave whose lane l is row s * 64 + l (k_sell_sl_pattern,
+// and k_sell_fill_graph right after it wrote the slice's deltas): see k_sell_sl_pattern (pcg.hip). cand: SU_MAXW ints of
+// the wave's LDS. cin: the slice's plain 16-bit deltas (each lane reads only its own row's entries before the shuffles).
+__device__ __forceinline__ void sl_pattern_slice(int64_t s, int l, int64_t nslices, int64_t nrows,
+                                                 const int64_t* __restrict__ slice_ptr, const int16_t* cin,
+                                                 int16_t* __restrict__ pout, int16_t* __restrict__ ucol,
+                                                 int32_t* __restrict__ uoff, int G, int* __restrict__ win, int* cand) {
+    const int64_t p0 = slice_ptr[s];
+    const int w = (int)((slice_ptr[s + 1] - p0) >> 6);
+    const int64_t row = s * 64 + l;
+    if (G > 0) {   // gather window (k_pk_window): the delta union of the slice over its owner workgroup
+        int dmin = 0, dmax = 0;
+        if (row < nrows)
+            for (int k = 0; k < w; ++k) {
+                const int d = cin[p0 + 64 * k + l];
+                dmin = d < dmin ? d : dmin;
+                dmax = d > dmax ? d : dmax;
+            }
+        int64_t cmin, cmax;
+        pk_slice_span(s, nrows, dmin, dmax, &cmin, &cmax);
+        const int64_t WV = (int64_t)G * PK_WAVES;
+        auto owner = [&](int64_t r) { return (int)((((r >> 6) + 1) * WV - 1) / nslices / PK_WAVES); };
+        if (l == 0) {
+            const int me = owner(row);
+            atomicMin(win + me, owner(cmin));
+            atomicMax(win + G + me, owner(cmax));
+        }
+    }
+    bool ok = (s + 1) * 64 <= nrows && w > 0 && w <= SU_MAXW;
+    int len = 0;
+    if (ok) {
+        int prev = -(1 << 30);
+        for (int k = 0; k < w; ++k) {
+            const int d = cin[p0 + 64 * k + l];
+            if (len == k && d > prev) {
+                ++len;
+                prev = d;
+            } else if (d != 0) {
+                ok = false;
+            }
+        }
+    }
+    ok = __all(ok);
+    const unsigned long long full = __ballot(ok && len == w);
+    if (ok && full) {
+        const int c = __builtin_ctzll(full);
+        for (int k = 0; k < w; ++k) {
+            const int d = __shfl((int)cin[p0 + 64 * k + l], c, 64);
+            if (l == 0) cand[k] = d;
+            const int64_t col = row + d;
+            if (col < 0 || col >= nrows) ok = false;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        int i = 0;
+        for (int k = 0; k < len && ok; ++k) {
+            const int d = cin[p0 + 64 * k + l];
+            while (i < w && cand[i] < d) ++i;
+            if (i == w || cand[i] != d) ok = false;
+            ++i;
+        }
+    } else {
+        ok = false;
+    }
+    ok = __all(ok);
+    if (!ok) {
+        if (l == 0) uoff[s] = -1;
+        for (int k = 0; k < w; ++k) pout[p0 + pair_pos(k, w, l)] = cin[p0 + 64 * k + l];
+        return;
+    }
+    const int32_t uo = (int32_t)(2 * (p0 >> 6));   // even: the deltas are read as int32 pairs
+    for (int k = 0; k < w; ++k) pout[p0 + pair_pos(k, w, l)] = (int16_t)cand[k];
+    for (int k = l; k < w; k += 64) ucol[uo + k] = (int16_t)cand[k];
+    if (l == 0) uoff[s] = uo;
+}
 __attribute__((unused)) static __global__ void __launch_bounds__(256) k_sell_uniform(int64_t nslices, int64_t nrows,
                                                              const int64_t* __restrict__ slice_ptr,
                                                              const double* __restrict__ vin,

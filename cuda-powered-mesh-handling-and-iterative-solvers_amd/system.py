@@ -109,22 +109,16 @@ class Graph:
     def solver_layout(self):
         """The bs = 1 solver layout of this pattern (include/fem355.h fem_sell_sl_pattern): lane-paired deltas,
         slice-uniform delta lists, and the persistent schedule's gather windows for this device's grid -- formed once
-        per pattern, on first use. None without 16-bit deltas."""
+        per pattern, on first use (or by build_graph(..., solver_layout=True) in its fill pass). None without 16-bit
+        deltas."""
         if self.dcols is None:
             return None
         sl = getattr(self, "_sl", None)
         if sl is None:
             dev = self.rowptr.device
             with C.device_scope(dev):
-                ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-                G = (ncu // 8) * 8
-                ent = self.sell_entries
-                ns = (self.n_nodes + 63) // 64
-                sl = SolverLayout(torch.empty(max(ent, 1), dtype=torch.int16, device=dev),
-                                  torch.empty(2 * (ent // 64) + 2, dtype=torch.int16, device=dev),
-                                  torch.empty(max(ns, 1), dtype=I32, device=dev),
-                                  torch.empty(max(2 * G, 1), dtype=I32, device=dev), G)
-                C.check(C.lib().fem_sell_sl_pattern(self.n_nodes, C.ptr(self.slice_ptr), C.ptr(self.dcols), G,
+                sl = _solver_layout_arrays(dev, self.sell_entries, self.n_nodes)
+                C.check(C.lib().fem_sell_sl_pattern(self.n_nodes, C.ptr(self.slice_ptr), C.ptr(self.dcols), sl.G,
                                                     C.ptr(sl.pcols), C.ptr(sl.ucol), C.ptr(sl.uoff), C.ptr(sl.win),
                                                     C.stream(dev)), "fem_sell_sl_pattern")
             self._sl = sl
@@ -147,6 +141,17 @@ class SolverLayout:
     uoff: torch.Tensor
     win: torch.Tensor
     G: int
+
+
+def _solver_layout_arrays(dev, ent, n_nodes):
+    """Uninitialised SolverLayout arrays of a pattern with `ent` SELL entries (G: the persistent grid of `dev`)."""
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    G = (ncu // 8) * 8
+    ns = (n_nodes + 63) // 64
+    return SolverLayout(torch.empty(max(ent, 1), dtype=torch.int16, device=dev),
+                        torch.empty(2 * (ent // 64) + 2, dtype=torch.int16, device=dev),
+                        torch.empty(max(ns, 1), dtype=I32, device=dev),
+                        torch.empty(max(2 * G, 1), dtype=I32, device=dev), G)
 
 
 def check_connectivity(elements: torch.Tensor, n_nodes: int):
@@ -180,15 +185,16 @@ def _incidence(elements, n_nodes, checked):
     return inc_ptr, inc
 
 
-def build_graph(elements: torch.Tensor, n_nodes: int, compress: bool = True) -> Graph:
+def build_graph(elements: torch.Tensor, n_nodes: int, compress: bool = True, solver_layout: bool = False) -> Graph:
     """Node-graph CSR + SELL-64 pattern of `elements` (one element family, int64 [M, npe] on the device).
     The rows are the coalesced pattern of the reference's COO assembly (`subdivision.ipynb:118-139`).
-    compress: also derive 16-bit column deltas (used by the SpMV when every |col - row| <= 32767)."""
+    compress: also derive 16-bit column deltas (used by the SpMV when every |col - row| <= 32767).
+    solver_layout: with the deltas, also form the bs = 1 solver layout (Graph.solver_layout) in the same fill pass."""
     with C.device_scope(elements.device):
-        return _build_graph(elements, n_nodes, compress)
+        return _build_graph(elements, n_nodes, compress, solver_layout)
 
 
-def _build_graph(elements, n_nodes, compress):
+def _build_graph(elements, n_nodes, compress, solver_layout=False):
     lib = C.lib()
     dev = elements.device
     elements = elements.contiguous()
@@ -232,11 +238,21 @@ def _build_graph(elements, n_nodes, compress):
     diagpos = torch.empty(n_nodes, dtype=I32, device=dev)
     cols = torch.empty(ent, dtype=I32, device=dev)
     dcols = torch.empty(max(ent, 1), dtype=torch.int16, device=dev) if compress and not far else None
-    C.check(lib.fem_graph_sell_fill(C.ptr(elements), npe, C.ptr(inc_ptr), C.ptr(inc), n_nodes, C.ptr(rowptr),
-                                    C.ptr(tmp), C.ptr(slice_ptr), C.ptr(colidx), C.ptr(diagpos), C.ptr(cols),
-                                    C.ptr(dcols), None, None, st), "fem_graph_sell_fill")
+    sl = None
+    if dcols is not None and solver_layout and os.environ.get("FEM355_SL_SEPARATE") is None:
+        sl = _solver_layout_arrays(dev, ent, n_nodes)
+        C.check(lib.fem_graph_sell_fill_sl(C.ptr(elements), npe, C.ptr(inc_ptr), C.ptr(inc), n_nodes, C.ptr(rowptr),
+                                           C.ptr(tmp), C.ptr(slice_ptr), C.ptr(colidx), C.ptr(diagpos), C.ptr(cols),
+                                           C.ptr(dcols), sl.G, C.ptr(sl.pcols), C.ptr(sl.ucol), C.ptr(sl.uoff),
+                                           C.ptr(sl.win), st), "fem_graph_sell_fill_sl")
+    else:
+        C.check(lib.fem_graph_sell_fill(C.ptr(elements), npe, C.ptr(inc_ptr), C.ptr(inc), n_nodes, C.ptr(rowptr),
+                                        C.ptr(tmp), C.ptr(slice_ptr), C.ptr(colidx), C.ptr(diagpos), C.ptr(cols),
+                                        C.ptr(dcols), None, None, st), "fem_graph_sell_fill")
     del tmp
     g = Graph(n_nodes, npe, inc_ptr, inc, rowptr, colidx, diagpos, slice_ptr, cols)
+    if sl is not None:
+        g._sl = sl
     g.dcols = dcols
     g.max_width = maxw // 64 if ns > 0 else 0   # widest slice, in columns (the value kernels' window choice)
     return g
@@ -811,8 +827,9 @@ def assemble_tet4_system(coords, elements, kind="poisson", E=1.0, nu=0.0, graph=
     """Mesh -> assembled device operator in one pass (pattern + values; element matrices never stored).
     kind: "poisson" (bs=1, kappa=E) or "elastic" (bs=3)."""
     n_nodes = coords.shape[0]
-    g = graph if graph is not None else build_graph(elements, n_nodes)
     bs = 1 if kind == "poisson" else 3
+    # bs = 1: the solver layout formed in the pattern's fill pass (the value kernel writes it straight away)
+    g = graph if graph is not None else build_graph(elements, n_nodes, solver_layout=bs == 1)
     A = SellMatrix(g, bs).add_tet4(coords.to(F64).contiguous(), elements.contiguous(), E, nu)
     return A
 

@@ -154,6 +154,14 @@ int fem_graph_sell_fill(const int64_t* conn, int npe, const int32_t* inc_ptr, co
                         const int32_t* rowptr, const int32_t* tmp, const int64_t* slice_ptr, int32_t* colidx,
                         int32_t* diagpos, int32_t* cols, int16_t* dcols, int64_t* csr2sell, int32_t* overflow,
                         fem_stream_t stream);
+/* fem_graph_sell_fill without csr2sell / overflow, plus the bs = 1 solver layout of fem_sell_sl_pattern (pcols, ucol,
+ * uoff, and for G > 0 the persistent schedule's gather windows win[2 G]) formed in the same slice pass from the deltas
+ * it writes -- the same arrays as fem_sell_sl_pattern, without its separate pass over the deltas. Needs the 16-bit
+ * deltas (no neighbour more than 32767 rows away). */
+int fem_graph_sell_fill_sl(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
+                           const int32_t* rowptr, const int32_t* tmp, const int64_t* slice_ptr, int32_t* colidx,
+                           int32_t* diagpos, int32_t* cols, int16_t* dcols, int G, int16_t* pcols, int16_t* ucol,
+                           int32_t* uoff, int32_t* win, fem_stream_t stream);
 /* exclusive scan of int32 counts -> out[n+1] (out[n] = total); work: int32 [fem_scan_work_len(n)] */
 int fem_scan_i32(const int32_t* in, int64_t n, int32_t* out, int32_t* work, fem_stream_t stream);
 

@@ -1282,3 +1282,36 @@ def test_scalar_mass_and_bs1_tile_assembly(gpu, etype, gen, n, monkeypatch):
     A1b = system.SellMatrix(g, 1).add_element_matrices(Ms, tg)
     assert torch.equal(A1b.plain_values(), fresh)
     assert torch.equal(A1.plain_values(), B1.plain_values())
+
+
+@pytest.mark.parametrize("case", ["kuhn", "permuted"])
+def test_solver_layout_from_the_fill_pass(gpu, case, monkeypatch):
+    """build_graph(..., solver_layout=True) forms the bs = 1 solver layout (paired deltas, slice-uniform lists, gather
+    windows) inside the SELL fill pass (fem_graph_sell_fill_sl): the same arrays as the separate k_sell_sl_pattern
+    pass (FEM355_SL_SEPARATE), bit for bit, and the same solve."""
+    _, mesh, _, system = _mods()
+    c, t = mesh.kuhn_cube(13, jitter=0.1)
+    if case == "permuted":
+        perm = torch.randperm(c.shape[0], generator=torch.Generator().manual_seed(5))
+        inv = torch.empty_like(perm)
+        inv[perm] = torch.arange(perm.numel())
+        c, t = c[perm], inv[t]
+    cg, tg = c.to(gpu), t.to(gpu)
+    N = c.shape[0]
+    gf = system.build_graph(tg, N, solver_layout=True)
+    monkeypatch.setenv("FEM355_SL_SEPARATE", "1")
+    gs = system.build_graph(tg, N, solver_layout=True)
+    monkeypatch.delenv("FEM355_SL_SEPARATE")
+    assert getattr(gs, "_sl", None) is None and gf._sl is not None
+    a, b = gf.solver_layout(), gs.solver_layout()
+    ns = (N + 63) // 64
+    assert torch.equal(a.pcols, b.pcols) and torch.equal(a.uoff[:ns], b.uoff[:ns]) and torch.equal(a.win, b.win)
+    sp = gf.slice_ptr.cpu()
+    uo = b.uoff[:ns].cpu()
+    for q in torch.nonzero(uo >= 0).view(-1).tolist():   # the written part of the lists: w deltas per uniform slice
+        w = int((sp[q + 1] - sp[q]) // 64)
+        o = int(uo[q])
+        assert torch.equal(a.ucol[o:o + w], b.ucol[o:o + w])
+    A1 = system.SellMatrix(gf, 1).add_tet4(cg, tg, 1.0)
+    A2 = system.SellMatrix(gs, 1).add_tet4(cg, tg, 1.0)
+    assert torch.equal(A1._svals, A2._svals)
