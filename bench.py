@@ -258,7 +258,7 @@ def main():
         attach_cpu_baseline(out, cpu_baseline(a.n, a.kind, a.cpu_iters, out["solve_iters"]))
     # BASELINE configs[2] beside the metric: the same steps on the 10M-tet linear-elasticity system (north_star:
     # CG it/s on elasticity at 1/2/4/8 GPUs), its own CPU-oracle sample; a failure is reported, never fatal
-    if a.kind == "poisson" and a.elastic:
+    if a.kind == "poisson" and (a.elastic or a.mixed):
         from fem355 import dist
 
         def companion():
@@ -277,7 +277,8 @@ def main():
                 attach_cpu_baseline(d, cpu_baseline(a.n, "elastic", a.cpu_iters_elastic, d["solve_iters"]))
             return d
         guard = dist.CompanionGuard(out, "elasticity", rank=0, timeout=a.elastic_timeout)
-        guard.run(companion)
+        if a.elastic:
+            guard.run(companion)
         if a.mixed:
             del coords, tets
             torch.cuda.empty_cache()

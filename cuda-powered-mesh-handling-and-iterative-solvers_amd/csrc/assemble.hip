@@ -517,6 +517,76 @@ __global__ void __launch_bounds__(256) k_iso_ke1(const double* __restrict__ X, c
     }
 }
 
+// Scalar consistent mass (fem_iso_mass_scalar): Ms_e[a][b] = rho sum_q w_q |detJ_q| N_a(q) N_b(q) -- the factor of
+// M_e = Ms_e (x) I3. The element's only per-point quantity is c_q = rho w_q |detJ_q|, so one THREAD forms an element:
+// its NPE nodes in registers, per point J (the einsum order of k_iso_ke: node j ascending), detJ and c_q, then the
+// NPE (NPE + 1) / 2 upper-triangle sums in point order (s = (N_a N_b) c_q, the additions and order of k_iso_ke's mass
+// lanes: the same values), written out as the full symmetric NPE x NPE block with 16-byte stores. The wave-per-element
+// form spent its time in per-point lane hand-offs (c3d8 0.9 ms for 681k elements; this form is arithmetic + one
+// contiguous 8 NPE^2-byte store per element).
+template <int NPE>
+__global__ void __launch_bounds__(256) k_iso_mass_s(const double* __restrict__ X, const int64_t* __restrict__ conn,
+                                                    int64_t M, double rho, const double* __restrict__ dN,
+                                                    const double* __restrict__ Nv, const double* __restrict__ w,
+                                                    int n_ip, double* __restrict__ Ms) {
+    extern __shared__ double mtab[];   // dN [n_ip][NPE][3], Nv [n_ip][NPE], w [n_ip]
+    double* dn_s = mtab;
+    double* nv_s = mtab + n_ip * NPE * 3;
+    double* w_s = nv_s + n_ip * NPE;
+    for (int t = threadIdx.x; t < n_ip * NPE * 3; t += 256) dn_s[t] = dN[t];
+    for (int t = threadIdx.x; t < n_ip * NPE; t += 256) nv_s[t] = Nv[t];
+    for (int t = threadIdx.x; t < n_ip; t += 256) w_s[t] = w[t];
+    __syncthreads();
+    constexpr int NS = NPE * (NPE + 1) / 2;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < M; e += (int64_t)gridDim.x * 256) {
+        double x[NPE][3];
+#pragma unroll
+        for (int j = 0; j < NPE; ++j) {
+            const int64_t c = conn[e * NPE + j];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) x[j][k] = X[3 * c + k];
+        }
+        double m[NS];
+#pragma unroll
+        for (int t = 0; t < NS; ++t) m[t] = 0.0;
+#pragma unroll 1
+        for (int q = 0; q < n_ip; ++q) {
+            const double* dq = dn_s + q * NPE * 3;
+            double J[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+            for (int j = 0; j < NPE; ++j) {
+                const double d[3] = {dq[j * 3], dq[j * 3 + 1], dq[j * 3 + 2]};
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) J[3 * i + k] += d[i] * x[j][k];
+            }
+            const double c00 = J[4] * J[8] - J[5] * J[7], c01 = J[5] * J[6] - J[3] * J[8],
+                         c02 = J[3] * J[7] - J[4] * J[6];
+            const double det = J[0] * c00 + J[1] * c01 + J[2] * c02;
+            const double coef = fabs(det) * w_s[q] * rho;
+            const double* nq = nv_s + q * NPE;
+            int t = 0;
+#pragma unroll
+            for (int a = 0; a < NPE; ++a)
+#pragma unroll
+                for (int b = a; b < NPE; ++b) m[t++] += nq[a] * nq[b] * coef;
+        }
+        double2* out = reinterpret_cast<double2*>(Ms + e * NPE * NPE);   // NPE^2 even: 16-byte aligned blocks
+#pragma unroll
+        for (int p = 0; p < NPE * NPE / 2; ++p) {
+            double v2[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int i = 2 * p + h, a = i / NPE, b = i - NPE * (i / NPE);
+                const int lo = a < b ? a : b, hi = a < b ? b : a;
+                v2[h] = m[lo * NPE - lo * (lo - 1) / 2 + (hi - lo)];
+            }
+            out[p] = make_double2(v2[0], v2[1]);
+        }
+    }
+}
+
 // ---------------------------------------------------------------- SELL value addressing
 // entry index E = slice_ptr[s] + 64 k + lane  ->  value index of block entry rc (row-major in the block)
 __device__ __forceinline__ int64_t sell_val(int64_t E, int bs2, int rc) {
@@ -1472,6 +1542,22 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
             }
         }
         __syncthreads();
+        if constexpr (BS == 1 && SL && STORE) {
+            // solver layout, storing: lane-paired entries (2k, 2k + 1) of a row are adjacent, so a thread stores both
+            // as one 16-byte value and a wave one contiguous 1 KB segment (per-entry 8-byte stores left every other
+            // 8 bytes of each segment to the next instruction); the unpaired last entry of an odd-width slice after
+            static_assert(AW % 2 == 0, "windows start at even entries");
+            const int np = W >> 1;
+            const int kp0 = c0 >> 1, kp1 = min((c0 + cw) >> 1, np);
+            for (int q = tid; q < (kp1 - kp0) * R; q += NT) {
+                const int r = q % R, kp = kp0 + q / R, k = 2 * kp - c0;
+                *reinterpret_cast<double2*>(vals + e0 + (int64_t)kp * 128 + 2 * (l0 + r)) =
+                    make_double2(acc_s[k][r], acc_s[k + 1][r]);
+            }
+            if ((W & 1) && c0 + cw == W)
+                for (int r = tid; r < R; r += NT) vals[e0 + (int64_t)np * 128 + l0 + r] = acc_s[W - 1 - c0][r];
+            continue;
+        }
         for (int q = tid; q < cw * B2 * R; q += NT) {
             const int r = q % R, kc = q / R, k = kc / B2, c = kc - k * B2;
             if (!STORE && !(SL && uo >= 0) && c0 + k >= rp_s[r + 1] - rp_s[r]) continue;   // adding: padding stays
@@ -1938,6 +2024,18 @@ static int iso_mass(const double* coords, const int64_t* conn, int64_t M, int np
     const size_t lds = sizeof(double) * (size_t)n_ip * npe * 4;
     const void* fn = (const void*)k_iso_ke<10, true>;   // the walking grid (c3d10 only, iso_grid_npe)
     const dim3 g(iso_grid_npe(fn, lds, M, npe));
+    if (scalar && getenv("FEM355_MASS_WAVE") == nullptr) {   // thread per element (k_iso_mass_s)
+        const size_t tl = sizeof(double) * (size_t)n_ip * (npe * 4 + 1);
+        const dim3 gs((unsigned)std::min<int64_t>(cdiv(M, 256), 65536));
+        switch (npe) {
+            case 6: hipLaunchKernelGGL(k_iso_mass_s<6>, gs, dim3(256), tl, st, coords, conn, M, rho, dN, Nv, w, n_ip, Me); break;
+            case 8: hipLaunchKernelGGL(k_iso_mass_s<8>, gs, dim3(256), tl, st, coords, conn, M, rho, dN, Nv, w, n_ip, Me); break;
+            case 10: hipLaunchKernelGGL(k_iso_mass_s<10>, gs, dim3(256), tl, st, coords, conn, M, rho, dN, Nv, w, n_ip, Me); break;
+            default: set_error("fem_iso_mass: unsupported nodes per element %d", npe); return FEM_EBADTYPE;
+        }
+        FEM_LAUNCHED();
+        return FEM_OK;
+    }
 #define FEM_IM(K, P, SC_) hipLaunchKernelGGL((K<P, true, SC_>), g, dim3(256), lds, st, coords, conn, M, rho, 0.0, dN, w, \
                                              n_ip, mode, Me, Nv)
     switch (npe) {

@@ -77,6 +77,20 @@ __device__ __forceinline__ int wave_max_i(int v) {
     return v;
 }
 
+// FEM_MM_ACQREL = 1 (A/B build): the grid hand-offs in C++ memory-model form -- the arrival counter
+// updated with an agent-scope acq_rel atomic (the compiler's release writes back the XCD L2, its acquire invalidates
+// the CU's L1) instead of the write-through form (sc1 partials drained by s_waitcnt vmcnt(0) before a relaxed atomic,
+// sc1 loads after it: MI355X_MICROARCH.md "Valid forms", the default, measured cheaper)
+#ifndef FEM_MM_ACQREL
+#define FEM_MM_ACQREL 0
+#endif
+__device__ __forceinline__ void fem_drain_stores() {
+#if !FEM_MM_ACQREL
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+}
+constexpr int FEM_ARRIVE_ORDER = FEM_MM_ACQREL ? __ATOMIC_ACQ_REL : __ATOMIC_RELAXED;
+
 // Last-block-done ticket. Every block hands ONE 8-byte partial to the last-arriving block, in the write-through
 // form of MI355X_MICROARCH.md §visibility ("Valid forms", first table row): the partial is stored `sc1`
 // (relaxed agent-scope atomic store), the storing wave drains it with `s_waitcnt vmcnt(0)`, then one
@@ -87,8 +101,8 @@ __device__ __forceinline__ bool publish_partial(double partial, double* partials
                                                 int* lds_flag) {
     if (threadIdx.x == 0) {
         __hip_atomic_store(&partials[blockIdx.x], partial, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fem_drain_stores();
+        unsigned t = __hip_atomic_fetch_add(counter, 1u, FEM_ARRIVE_ORDER, __HIP_MEMORY_SCOPE_AGENT);
         int last = (t == gridDim.x - 1);
         if (last) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *lds_flag = last;
@@ -112,6 +126,8 @@ __device__ __forceinline__ double sum_partials(const double* partials, int n, do
 // atomic / `sc1` load hand-off as publish_partial. Deterministic: the summation order never depends on arrival.
 // Layout of `counters`: (RED_SHARDS + 1) * 32 unsigned; `partials`: gridDim.x + RED_SHARDS doubles.
 constexpr int RED_SHARDS = 32;
+
+
 constexpr int RED_COUNTER_WORDS = (RED_SHARDS + 1) * 32;
 
 __device__ __forceinline__ bool reduce_grid(double partial, double* partials, unsigned* counters, double* total,
@@ -123,8 +139,8 @@ __device__ __forceinline__ bool reduce_grid(double partial, double* partials, un
     double* shard_sums = partials + G;
     if (threadIdx.x == 0) {
         __hip_atomic_store(&partials[blockIdx.x], partial, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        unsigned t = __hip_atomic_fetch_add(&counters[sh * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fem_drain_stores();
+        unsigned t = __hip_atomic_fetch_add(&counters[sh * 32], 1u, FEM_ARRIVE_ORDER, __HIP_MEMORY_SCOPE_AGENT);
         int last = (t == in_shard - 1);
         if (last) __hip_atomic_store(&counters[sh * 32], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *lds_flag = last;
@@ -137,9 +153,9 @@ __device__ __forceinline__ bool reduce_grid(double partial, double* partials, un
     v = block_sum256(v, lds4);
     if (threadIdx.x == 0) {
         __hip_atomic_store(&shard_sums[sh], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        fem_drain_stores();
         unsigned* top = &counters[RED_SHARDS * 32];
-        unsigned t = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned t = __hip_atomic_fetch_add(top, 1u, FEM_ARRIVE_ORDER, __HIP_MEMORY_SCOPE_AGENT);
         int last = (t == nsh - 1);
         if (last) __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *lds_flag = last;

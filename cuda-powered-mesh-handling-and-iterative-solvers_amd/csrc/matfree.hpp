@@ -251,8 +251,10 @@ __device__ __forceinline__ void mf_pf1(const MfOp& op, int64_t c, MfPf<BS>& f) {
     f.nn = op.sbase[c + 1] - f.s0;
     f.node = 0;
     f.lp = 0;
-    // every field defined in every lane (the pipeline copies whole records; stage 2 fills xv / pv for tid < nn).
-    // FEM_MF_PF_UNDEF = 1 (debug builds only, tools/mf_spcheck.py): leave them indeterminate as before round 5
+    // every field defined in every lane: the pipeline copies whole records (cur = n1; n1 = n2), and copying an
+    // indeterminate double is undefined behaviour -- with xv / pv left unset for tid >= nn the compiled walk produced
+    // NaN on multi-chunk walks (the round-4 "slot position" bug). FEM_MF_PF_UNDEF = 1 (debug builds only,
+    // tools/mf_spcheck.py) restores the indeterminate fields to reproduce it
 #if !FEM_MF_PF_UNDEF
 #pragma unroll
     for (int k = 0; k < 3; ++k) f.xv[k] = 0.0;
@@ -326,9 +328,12 @@ __device__ __forceinline__ double mf_walk(const MfOp& op, const double* __restri
         const bool has2 = has1 && k2 < per && base + k2 < op.nchunks;
         if (has1) mf_pf2<BS, MODE>(op, x, n1);
         if (has2) mf_pf1<BS>(op, base + k2, n2);
-        // where this thread's slot is stored (node-major or chunk-major), read under the chunk's work -- not carried in
-        // the prefetch record (a slot position carried there through the record copies was measured wrong in some
-        // lanes when workgroups walked more than one chunk; the chunk's own base is)
+        // where this thread's slot is stored (node-major or chunk-major), read under the chunk's work. (Round 4 moved it
+        // here from the prefetch record after NaNs on multi-chunk walks; round 5 found the cause elsewhere: the records
+        // left xv / pv indeterminate in lanes tid >= nn, and copying indeterminate doubles through cur = n1; n1 = n2 is
+        // undefined behaviour the compiler exploited. The FEM_MF_SPCHECK build carries the position too and compares:
+        // 0 mismatches in every case, NaNs whenever FEM_MF_PF_UNDEF restores the indeterminate fields, none without --
+        // DESIGN §8h. Every field of a record is now defined in every lane; either position source is then correct.)
         int spc = 0;
         if (tid < cur.nn) spc = op.spos ? op.spos[cur.s0 + tid] : cur.s0 + tid;
         __syncthreads();

@@ -514,11 +514,13 @@ __device__ __forceinline__ bool u2_release(double acc, PcgState* __restrict__ st
             __hip_atomic_store(reinterpret_cast<double*>(sync + U2_BC) + 1, halt, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
             // the broadcast's write-through stores drained before the release (the guide's sc1 hand-off form; the
-            // asm's memory clobber also keeps the compiler from moving them past the swap)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // asm's memory clobber also keeps the compiler from moving them past the swap); FEM_MM_ACQREL: a release
+            // swap instead
+            fem_drain_stores();
             unsigned expect = e - 1;
-            if (!__hip_atomic_compare_exchange_strong(sync + U2_REL, &expect, e, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT)) {
+            if (!__hip_atomic_compare_exchange_strong(sync + U2_REL, &expect, e,
+                                                      FEM_MM_ACQREL ? __ATOMIC_RELEASE : __ATOMIC_RELAXED,
+                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
                 // a waiter gave up first: undo the commit (the iteration did not complete) and keep its verdict
                 st->iter = it0;
                 u2_give_up(st, e);
@@ -542,8 +544,13 @@ __device__ __forceinline__ bool u2_release(double acc, PcgState* __restrict__ st
                 __builtin_amdgcn_s_sleep(2);
             }
             // no load below may be moved above the poll by the compiler (the hardware issues it only after the
-            // branch on the polled value); the broadcast is read with write-through (sc1) loads
+            // branch on the polled value); the broadcast is read with write-through (sc1) loads. FEM_MM_ACQREL: one
+            // agent-scope acquire after the poll matched
+#if FEM_MM_ACQREL
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#else
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#endif
             if (v == e) {
                 beta_ = __hip_atomic_load(reinterpret_cast<const double*>(sync + U2_BC), __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT);

@@ -15,5 +15,6 @@ for v in spcheck spundef; do
 done
 timeout -k 10 300 python tools/mf_probe.py --n 119 --iters 50 > gpurun_out/mf_probe_b.log 2>&1; rc=$?
 tail -3 gpurun_out/mf_probe_b.log; [ $rc -ge 124 ] && exit $rc
-timeout -k 10 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --elastic 0 --mixed 0 \
-    > gpurun_out/bench_b.log 2>&1; rc=$?; tail -c 1500 gpurun_out/bench_b.log; exit $rc
+timeout -k 10 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --elastic 0 \
+    > gpurun_out/bench_b.log 2>&1; rc=$?; tail -c 1500 gpurun_out/bench_b.log; [ $rc -ne 0 ] && exit $rc
+bash tools/mm_ab.sh
