@@ -379,8 +379,11 @@ def measure_matfree(a, coords, tets, dev, ref):
                      "peak_TFLOPs": FP64_PEAK_TFLOPS, "frac_flops": flops / (k1 * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
                      "algorithmic_bytes": alg, "achieved_GBps": alg / (k1 * 1e-3) / 1e9,
                      "frac_hbm": alg / (k1 * 1e-3) / 1e9 / HBM_PEAK_GBPS,
+                     # PMC HBM bytes of one K1 launch (FETCH_SIZE x 2 + WRITE_SIZE, tools/pmc_mf.sh), None unless taken
+                     # on this layout (same algorithmic bytes)
+                     "traffic": traffic_from_profiles(f"kuhn{a.n}_elastic_matfree", "k_pcg_mf_dot<3>", alg),
                      "model": f"{MF_FLOPS_PER_ELEMENT} flops per element; bytes: layout + coordinates + p + slots"},
-        "operator": "element-chunk (matrix-free): Morton-ordered chunks of <= 512 elements / 256 nodes, "
+        "operator": "element-chunk (matrix-free): Morton-ordered chunks of <= 512 elements / 240 nodes, "
                     "fixed-order slot sums (csrc/matfree.hip)",
     }
 

@@ -72,11 +72,13 @@ enum { MF_APPLY = 0, MF_DOT = 1, MF_DIAG = 2 };
 #ifndef FEM_MF_SPCHECK
 #define FEM_MF_SPCHECK 0
 #endif
-#ifndef FEM_MF_PF_UNDEF
-#define FEM_MF_PF_UNDEF 0
-#endif
 #if FEM_MF_SPCHECK
 __device__ unsigned long long mf_spcheck[8];
+#endif
+// FEM_MF_PROF (timing builds only, wrong results): bit 0 skips the element formation (the staged vectors are the
+// nodes' x), bit 1 the node sums (each slot gets one pair value) -- what the chunk kernel costs without each phase
+#ifndef FEM_MF_PROF
+#define FEM_MF_PROF 0
 #endif
 
 // staged corners of a mode (the diagonal's corner-0 values are not -(f_1 + f_2 + f_3))
@@ -226,215 +228,235 @@ __device__ __forceinline__ void mf_pair_value(const MfLds<BS, FC>& L, int pe, in
 }
 
 // What a thread loads for one chunk ahead of its use (software pipeline over a workgroup's chunks): the chunk's
-// ranges, this thread's local node (id, coordinates, x), its pair range, 8 pairs and the local ids of its 2 elements.
+// ranges, this thread's local node (id, slot position, pair range, coordinates, x), 8 pairs and the local ids of its
+// 2 elements; and the ranges of the chunk this record carries next (three chunks on).
+//
+// Every load is issued unconditionally (lanes past the chunk's nodes / pairs / elements read a clamped in-range
+// index, their values unused), nothing is computed from a loaded value before its use, and the three records rotate
+// by name (mf_walk unrolls its loop by three), never by copy. A copy of a record, or a select / zero-fill of a field,
+// makes the compiler wait for the loads in flight into it, and a load under a branch makes its wait counts
+// conservative past the branch (s_waitcnt vmcnt(0)): the round-4/5 walk, whose records were copied (cur = n1; n1 =
+// n2) and loaded under `tid < nn`, waited for each prefetch right after issuing it -- ~4 exposed memory latencies per
+// chunk (a FEM_MF_PROF = 3 build, no element formation and no node sums, still took 125 of the kernel's 217 us).
+// Every field is defined in every lane (copying indeterminate values was the round-4 NaN).
+typedef unsigned int mf_u32x4 __attribute__((ext_vector_type(4)));   // a native vector (HIP's uint4 is a union
+                                                                        // wrapper that kept the records in scratch)
 template <int BS>
 struct MfPf {
-    int e0, ne, s0, nn;
-    int node;
-    uint16_t lp1;   // end of the node's pairs (lp: their start)
-#if FEM_MF_SPCHECK
-    int sp;
-#endif
-    uint16_t lp;
-    uint4 ent;
+    int e0, ne, s0, nn;             // this record's chunk: elements [e0, e0 + ne), slots [s0, s0 + nn)
+    int b_e, b_s;                   // ranges of the chunk this record carries next: lane 0 its first element /
+                                    // slot, lane 1 its end (lane-varying addresses keep the loads off the scalar
+                                    // path, whose v_readfirstlane the compiler places right after the load)
+    int node, sp, lp, lp1;          // local node tid: global id, slot position (spos; or unused), its pairs [lp, lp1)
+    mf_u32x4 ent;
     uint32_t el[MF_EC / MF_PASS];
     double xv[3], pv[BS];
 };
 
-// stage 1: everything but the node-dependent gathers
+// stage 0: the ranges of chunk c (cptr / sbase), into the record's b_* (consumed by mf_pf1 a step later)
+template <int BS>
+__device__ __forceinline__ void mf_pf0(const MfOp& op, int64_t c, MfPf<BS>& f) {
+    const int h = threadIdx.x & 1;
+    f.b_e = op.cptr[c + h];
+    f.b_s = op.sbase[c + h];
+}
+
+// stage 1: the chunk's ids / pairs / local ids, after its ranges arrived
 template <int BS>
 __device__ __forceinline__ void mf_pf1(const MfOp& op, int64_t c, MfPf<BS>& f) {
     const int tid = threadIdx.x;
-    f.e0 = op.cptr[c];
-    f.ne = op.cptr[c + 1] - f.e0;
-    f.s0 = op.sbase[c];
-    f.nn = op.sbase[c + 1] - f.s0;
-    f.node = 0;
-    f.lp = 0;
-    // every field defined in every lane: the pipeline copies whole records (cur = n1; n1 = n2), and copying an
-    // indeterminate double is undefined behaviour -- with xv / pv left unset for tid >= nn the compiled walk produced
-    // NaN on multi-chunk walks (the round-4 "slot position" bug). FEM_MF_PF_UNDEF = 1 (debug builds only,
-    // tools/mf_spcheck.py) restores the indeterminate fields to reproduce it
-#if !FEM_MF_PF_UNDEF
+    f.e0 = __builtin_amdgcn_readlane(f.b_e, 0);
+    f.ne = __builtin_amdgcn_readlane(f.b_e, 1) - f.e0;
+    f.s0 = __builtin_amdgcn_readlane(f.b_s, 0);
+    f.nn = __builtin_amdgcn_readlane(f.b_s, 1) - f.s0;
+    const int t = tid < f.nn ? tid : f.nn - 1;   // a chunk has >= 1 node and >= 1 element
+    f.node = op.cnode[f.s0 + t];
+    f.lp = op.lptr[f.s0 + c + t];
+    f.lp1 = op.lptr[f.s0 + c + t + 1];           // the chunk's end marker for its last node
+    f.sp = (op.spos ? op.spos : op.cnode)[f.s0 + t];   // unconditional (chunk-major slots: unused, s0 + tid)
+    const int q = 8 * tid < 4 * f.ne ? tid : (4 * f.ne - 1) >> 3;
+    f.ent = reinterpret_cast<const mf_u32x4*>(op.lent + 4 * (int64_t)f.e0)[q];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) f.xv[k] = 0.0;
-#pragma unroll
-    for (int k = 0; k < BS; ++k) f.pv[k] = 0.0;
-#endif
-#if FEM_MF_SPCHECK
-    f.sp = 0;
-    if (tid < f.nn) f.sp = op.spos ? op.spos[f.s0 + tid] : f.s0 + tid;
-#endif
-    f.lp1 = 0;
-    if (tid < f.nn) {
-        f.node = op.cnode[f.s0 + tid];
-        f.lp = op.lptr[f.s0 + c + tid];
-        f.lp1 = op.lptr[f.s0 + c + tid + 1];   // the chunk's end marker for its last node
+    for (int j = 0; j < MF_EC / MF_PASS; ++j) {
+        const int e = tid + MF_PASS * j < f.ne ? tid + MF_PASS * j : f.ne - 1;
+        f.el[j] = op.eloc[f.e0 + e];
     }
-    f.ent = make_uint4(0, 0, 0, 0);
-    if (8 * tid < 4 * f.ne) f.ent = reinterpret_cast<const uint4*>(op.lent + 4 * (int64_t)f.e0)[tid];
-#pragma unroll
-    for (int j = 0; j < MF_EC / MF_PASS; ++j) f.el[j] = tid + MF_PASS * j < f.ne ? op.eloc[f.e0 + tid + MF_PASS * j] : 0u;
 }
 
 // stage 2: the local node's coordinates and x (after stage 1's node id arrived)
 template <int BS, int MODE>
 __device__ __forceinline__ void mf_pf2(const MfOp& op, const double* __restrict__ x, MfPf<BS>& f) {
-    if ((int)threadIdx.x < f.nn) {
-        const int64_t g = f.node;
+    const int64_t g = f.node;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) f.xv[k] = op.X[3 * g + k];
+    for (int k = 0; k < 3; ++k) f.xv[k] = op.X[3 * g + k];
 #pragma unroll
-        for (int k = 0; k < BS; ++k) f.pv[k] = MODE == MF_DIAG ? 0.0 : x[BS * g + k];
+    for (int k = 0; k < BS; ++k) f.pv[k] = MODE == MF_DIAG ? 0.0 : x[BS * g + k];
+}
+
+// One chunk of the walk: cur is formed and stored, n1 (next chunk) gets its node gathers, n2 (the one after) its ids /
+// pairs / local ids, cur its ranges for three chunks on. Returns whether this workgroup has a next chunk.
+template <int BS, int MODE>
+__device__ __forceinline__ bool mf_step(const MfOp& op, const double* __restrict__ x, double* __restrict__ slots,
+                                        MfLds<BS, mf_fc<MODE>()>& L, int64_t base, int64_t per, int64_t nb,
+                                        int64_t& k, MfPf<BS>& cur, MfPf<BS>& n1, MfPf<BS>& n2, double& dot) {
+    constexpr int FC = mf_fc<MODE>();
+    const int tid = threadIdx.x;
+    // chunks past this workgroup's range load its first chunk's data again (in range, never used)
+    const int64_t first = base + blockIdx.x / NXCD;
+    const auto chunk = [&](int64_t kk) { return kk < per && base + kk < op.nchunks ? base + kk : first; };
+    __syncthreads();   // the previous chunk's LDS reads are done
+    if (tid < cur.nn) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) L.nd[tid][q] = cur.xv[q];
+#pragma unroll
+        for (int q = 0; q < BS; ++q) L.nd[tid][3 + q] = cur.pv[q];
     }
+    if (8 * tid < 4 * cur.ne) reinterpret_cast<mf_u32x4*>(L.ent)[tid] = cur.ent;
+    // issue order: every load a later wait needs has the same younger loads behind it on every path (the prologue's
+    // order matches), so the waits stay partial: s_waitcnt vmcnt(N > 0)
+    mf_pf2<BS, MODE>(op, x, n1);
+    mf_pf0<BS>(op, chunk(k + 3 * nb), cur);
+    mf_pf1<BS>(op, chunk(k + 2 * nb), n2);
+    __syncthreads();
+    double acc[BS];
+#pragma unroll
+    for (int q = 0; q < BS; ++q) acc[q] = 0.0;
+    int pos = tid < cur.nn ? cur.lp : 0;
+    const int end = tid < cur.nn ? cur.lp1 : 0;
+    // the node's pairs split at the pass boundary (pairs ascend by element): lower bound of 4 MF_PASS
+    int mid = end;
+    if (cur.ne > MF_PASS) {
+        int lo = pos, len = end - pos;
+        while (len > 0) {
+            const int half = len >> 1;
+            if (L.ent[lo + half] < 4 * MF_PASS) {
+                lo += half + 1;
+                len -= half + 1;
+            } else {
+                len = half;
+            }
+        }
+        mid = lo;
+    }
+#pragma unroll
+    for (int j = 0; j < MF_EC / MF_PASS; ++j) {
+        const int h = MF_PASS * j;
+        if (h >= cur.ne) break;
+        if (h + tid < cur.ne) {
+            const uint32_t w = cur.el[j];
+            double xc[4][3], xv[4][BS], f[4][BS];
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int l = (w >> (8 * b)) & 0xff;
+                const double2* r = reinterpret_cast<const double2*>(&L.nd[l][0]);
+                const double2 a0 = r[0], a1 = r[1];
+                xc[b][0] = a0.x;
+                xc[b][1] = a0.y;
+                xc[b][2] = a1.x;
+                if constexpr (BS == 1) {
+                    xv[b][0] = a1.y;
+                } else {
+                    const double2 a2 = r[2];
+                    xv[b][0] = a1.y;
+                    xv[b][1] = a2.x;
+                    xv[b][2] = a2.y;
+                }
+            }
+#if FEM_MF_PROF & 1
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+#pragma unroll
+                for (int q = 0; q < BS; ++q) f[b][q] = xv[b][q] + xc[b][q];
+#else
+            mf_element<BS, MODE>(xc, xv, op.lam, op.mu, op.kappa, f);
+#endif
+#pragma unroll
+            for (int b = 4 - FC; b < 4; ++b)
+#pragma unroll
+                for (int q = 0; q < BS; ++q) L.fs[(b - (4 - FC)) * BS + q][tid] = f[b][q];
+        }
+        __syncthreads();
+        // every local node adds its pairs of this pass in ascending (element, corner) order; the pair reads of
+        // four steps are issued before their adds (independent LDS loads, one latency per four pairs)
+        const int stop = j == 0 ? mid : end;
+#if FEM_MF_PROF & 2
+        if (pos < stop) {
+            double v[BS];
+            mf_pair_value<BS, FC>(L, L.ent[pos], h, v);
+#pragma unroll
+            for (int q = 0; q < BS; ++q) acc[q] += v[q];
+            pos = stop;
+        }
+#endif
+        for (; pos + MF_U <= stop; pos += MF_U) {
+            int pe[MF_U];
+#pragma unroll
+            for (int u = 0; u < MF_U; ++u) pe[u] = L.ent[pos + u];
+            double v[MF_U][BS];
+#pragma unroll
+            for (int u = 0; u < MF_U; ++u) mf_pair_value<BS, FC>(L, pe[u], h, v[u]);
+#pragma unroll
+            for (int u = 0; u < MF_U; ++u)
+#pragma unroll
+                for (int q = 0; q < BS; ++q) acc[q] += v[u][q];
+        }
+        for (; pos < stop; ++pos) {
+            double v[BS];
+            mf_pair_value<BS, FC>(L, L.ent[pos], h, v);
+#pragma unroll
+            for (int q = 0; q < BS; ++q) acc[q] += v[q];
+        }
+        __syncthreads();
+    }
+    if (tid < cur.nn) {
+#pragma unroll
+        for (int q = 0; q < BS; ++q) {
+            mf_store_slot(&slots[(int64_t)(op.spos ? cur.sp : cur.s0 + tid) * BS + q], acc[q]);
+            if constexpr (MODE == MF_DOT) dot += cur.pv[q] * acc[q];
+        }
+#if FEM_MF_SPCHECK
+        // the carried position against one read now (the round-4 question)
+        const int spc = op.spos ? op.spos[cur.s0 + tid] : cur.s0 + tid;
+        atomicAdd(&mf_spcheck[0], 1ull);
+        if (op.spos && cur.sp != spc && atomicAdd(&mf_spcheck[1], 1ull) == 0) {
+            mf_spcheck[2] = ((unsigned long long)(base + k) << 16) | (unsigned)tid;
+            mf_spcheck[3] = (unsigned)cur.sp;
+            mf_spcheck[4] = (unsigned)spc;
+            mf_spcheck[5] = 0;
+        }
+#endif
+    }
+    k += nb;
+    return k < per && base + k < op.nchunks;
 }
 
 // Every chunk of this workgroup (chunk ranges per XCD, consecutive chunks -- neighbours in space -- at once on one XCD,
-// whose L2 then holds their shared nodes): the slot values of its local nodes (slots[(sbase[c] + l) * BS + c]); the
-// next chunk's data is loaded while the current one is formed. MODE_DOT returns this thread's part of
-// sum_l x_l . slot_l over its chunks (0 elsewhere). x unused for MF_DIAG.
+// whose L2 then holds their shared nodes): the slot values of its local nodes (slots[spos[sbase[c] + l] * BS + c]);
+// three chunks in flight: cur (installed in LDS and formed now), n1 (its node gathers issued at the top of this
+// chunk), n2 (its ids / pairs / local ids issued now, its ranges a chunk earlier): every load has a whole chunk of
+// work to arrive (~1-2 us of HBM latency under load). MODE_DOT returns this thread's part of sum_l x_l . slot_l over
+// its chunks (0 elsewhere). x unused for MF_DIAG.
 template <int BS, int MODE>
 __device__ __forceinline__ double mf_walk(const MfOp& op, const double* __restrict__ x, double* __restrict__ slots,
                                           MfLds<BS, mf_fc<MODE>()>& L) {
-    constexpr int FC = mf_fc<MODE>();
-    const int tid = threadIdx.x;
     const int64_t per = (op.nchunks + NXCD - 1) / NXCD;
     const int64_t base = (int64_t)(blockIdx.x % NXCD) * per;
     const int64_t nb = gridDim.x / NXCD;
     int64_t k = blockIdx.x / NXCD;
     double dot = 0.0;
     if (k >= per || base + k >= op.nchunks) return dot;
-#if FEM_MF_SPCHECK
-    int step = 0;
-#endif
-    // three chunks in flight: cur (installed in LDS now), n1 (its node gathers issued at the top of this chunk,
-    // needed at the next install), n2 (its ids / pairs / local ids issued now, its gathers at the next chunk's top):
-    // every load has a whole chunk of work to arrive (~1-2 us of HBM latency under load)
-    MfPf<BS> cur, n1, n2;
-    mf_pf1<BS>(op, base + k, cur);
-    bool has1 = k + nb < per && base + k + nb < op.nchunks;
-    if (has1) mf_pf1<BS>(op, base + k + nb, n1);
-    mf_pf2<BS, MODE>(op, x, cur);
+    const auto chunk = [&](int64_t kk) { return kk < per && base + kk < op.nchunks ? base + kk : base + k; };
+    MfPf<BS> A, B, C;   // records rotate by name: the loop body is three steps
+    mf_pf0<BS>(op, chunk(k), A);
+    mf_pf0<BS>(op, chunk(k + nb), B);
+    mf_pf1<BS>(op, chunk(k), A);
+    mf_pf2<BS, MODE>(op, x, A);
+    mf_pf0<BS>(op, chunk(k + 2 * nb), C);
+    mf_pf1<BS>(op, chunk(k + nb), B);
     for (;;) {
-        __syncthreads();   // the previous chunk's LDS reads are done
-        if (tid < cur.nn) {
-#pragma unroll
-            for (int q = 0; q < 3; ++q) L.nd[tid][q] = cur.xv[q];
-#pragma unroll
-            for (int q = 0; q < BS; ++q) L.nd[tid][3 + q] = cur.pv[q];
-        }
-        if (8 * tid < 4 * cur.ne) reinterpret_cast<uint4*>(L.ent)[tid] = cur.ent;
-        const int64_t k2 = k + 2 * nb;
-        const bool has2 = has1 && k2 < per && base + k2 < op.nchunks;
-        if (has1) mf_pf2<BS, MODE>(op, x, n1);
-        if (has2) mf_pf1<BS>(op, base + k2, n2);
-        // where this thread's slot is stored (node-major or chunk-major), read under the chunk's work. (Round 4 moved it
-        // here from the prefetch record after NaNs on multi-chunk walks; round 5 found the cause elsewhere: the records
-        // left xv / pv indeterminate in lanes tid >= nn, and copying indeterminate doubles through cur = n1; n1 = n2 is
-        // undefined behaviour the compiler exploited. The FEM_MF_SPCHECK build carries the position too and compares:
-        // 0 mismatches in every case, NaNs whenever FEM_MF_PF_UNDEF restores the indeterminate fields, none without --
-        // DESIGN §8h. Every field of a record is now defined in every lane; either position source is then correct.)
-        int spc = 0;
-        if (tid < cur.nn) spc = op.spos ? op.spos[cur.s0 + tid] : cur.s0 + tid;
-        __syncthreads();
-        double acc[BS];
-#pragma unroll
-        for (int q = 0; q < BS; ++q) acc[q] = 0.0;
-        int pos = tid < cur.nn ? (int)cur.lp : 0;
-        const int end = tid < cur.nn ? (int)cur.lp1 : 0;
-        // the node's pairs split at the pass boundary (pairs ascend by element): lower bound of 4 MF_PASS
-        int mid = end;
-        if (cur.ne > MF_PASS) {
-            int lo = pos, len = end - pos;
-            while (len > 0) {
-                const int half = len >> 1;
-                if (L.ent[lo + half] < 4 * MF_PASS) {
-                    lo += half + 1;
-                    len -= half + 1;
-                } else {
-                    len = half;
-                }
-            }
-            mid = lo;
-        }
-#pragma unroll
-        for (int j = 0; j < MF_EC / MF_PASS; ++j) {
-            const int h = MF_PASS * j;
-            if (h >= cur.ne) break;
-            if (h + tid < cur.ne) {
-                const uint32_t w = cur.el[j];
-                double xc[4][3], xv[4][BS], f[4][BS];
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const int l = (w >> (8 * b)) & 0xff;
-                    const double2* r = reinterpret_cast<const double2*>(&L.nd[l][0]);
-                    const double2 a0 = r[0], a1 = r[1];
-                    xc[b][0] = a0.x;
-                    xc[b][1] = a0.y;
-                    xc[b][2] = a1.x;
-                    if constexpr (BS == 1) {
-                        xv[b][0] = a1.y;
-                    } else {
-                        const double2 a2 = r[2];
-                        xv[b][0] = a1.y;
-                        xv[b][1] = a2.x;
-                        xv[b][2] = a2.y;
-                    }
-                }
-                mf_element<BS, MODE>(xc, xv, op.lam, op.mu, op.kappa, f);
-#pragma unroll
-                for (int b = 4 - FC; b < 4; ++b)
-#pragma unroll
-                    for (int q = 0; q < BS; ++q) L.fs[(b - (4 - FC)) * BS + q][tid] = f[b][q];
-            }
-            __syncthreads();
-            // every local node adds its pairs of this pass in ascending (element, corner) order; the pair reads of
-            // four steps are issued before their adds (independent LDS loads, one latency per four pairs)
-            const int stop = j == 0 ? mid : end;
-            for (; pos + MF_U <= stop; pos += MF_U) {
-                int pe[MF_U];
-#pragma unroll
-                for (int u = 0; u < MF_U; ++u) pe[u] = L.ent[pos + u];
-                double v[MF_U][BS];
-#pragma unroll
-                for (int u = 0; u < MF_U; ++u) mf_pair_value<BS, FC>(L, pe[u], h, v[u]);
-#pragma unroll
-                for (int u = 0; u < MF_U; ++u)
-#pragma unroll
-                    for (int q = 0; q < BS; ++q) acc[q] += v[u][q];
-            }
-            for (; pos < stop; ++pos) {
-                double v[BS];
-                mf_pair_value<BS, FC>(L, L.ent[pos], h, v);
-#pragma unroll
-                for (int q = 0; q < BS; ++q) acc[q] += v[q];
-            }
-            __syncthreads();
-        }
-        if (tid < cur.nn) {
-#pragma unroll
-            for (int q = 0; q < BS; ++q) {
-                mf_store_slot(&slots[(int64_t)spc * BS + q], acc[q]);
-                if constexpr (MODE == MF_DOT) dot += cur.pv[q] * acc[q];
-            }
-#if FEM_MF_SPCHECK
-            atomicAdd(&mf_spcheck[0], 1ull);
-            if (cur.sp != spc && atomicAdd(&mf_spcheck[1], 1ull) == 0) {
-                mf_spcheck[2] = ((unsigned long long)(base + k) << 16) | (unsigned)tid;
-                mf_spcheck[3] = (unsigned)cur.sp;
-                mf_spcheck[4] = (unsigned)spc;
-                mf_spcheck[5] = (unsigned)step;
-            }
-#endif
-        }
-#if FEM_MF_SPCHECK
-        ++step;
-#endif
-        if (!has1) break;
-        k += nb;
-        cur = n1;
-        n1 = n2;
-        has1 = has2;
+        if (!mf_step<BS, MODE>(op, x, slots, L, base, per, nb, k, A, B, C, dot)) break;
+        if (!mf_step<BS, MODE>(op, x, slots, L, base, per, nb, k, B, C, A, dot)) break;
+        if (!mf_step<BS, MODE>(op, x, slots, L, base, per, nb, k, C, A, B, dot)) break;
     }
     return dot;
 }

@@ -841,8 +841,14 @@ __global__ void __launch_bounds__(256) k_sell_fill_graph(const int32_t* __restri
             }
         }
         if (overflow && __ballot(far) && lane == 0 && !*overflow) atomicOr(overflow, 1);
-        if (pout && dcols) sl_pattern_slice(s, lane, nslices, nrows, slice_ptr, dcols, pout, ucol, uoff, G, win,
-                                            cand_all[wid]);
+        if (pout && dcols) {   // the deltas this lane just stored, re-formed from the staged row (no memory re-read)
+            const auto delta = [&](int k) -> int {
+                const int c = k >= len ? pad : (dfr ? colidx[rp + k] : rows[lane * TS + k]);
+                const int64_t d = (int64_t)c - r;
+                return (d > 32767 || d < -32767) ? 0 : (int)d;
+            };
+            sl_pattern_slice(s, lane, nslices, nrows, slice_ptr, delta, pout, ucol, uoff, G, win, cand_all[wid]);
+        }
         const int p0 = rp_s[wid][0], p1 = rp_s[wid][64];
         for (int p = p0 + lane; p < p1; p += 64) {
             int lo = 0, hi = 64;   // last row l with rp_s[l] <= p

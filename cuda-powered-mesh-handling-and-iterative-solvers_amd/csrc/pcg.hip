@@ -3410,8 +3410,10 @@ __global__ void __launch_bounds__(256) k_sell_sl_pattern(int64_t nslices, int64_
     __shared__ int cand_all[4][SU_MAXW];
     const int64_t s = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;   // one wave per slice
     if (s >= nslices) return;   // wave-uniform
-    sl_pattern_slice(s, threadIdx.x & 63, nslices, nrows, slice_ptr, cin, pout, ucol, uoff, G, win,
-                     cand_all[(threadIdx.x >> 6) & 3]);
+    const int l = threadIdx.x & 63;
+    const int64_t p0 = slice_ptr[s];
+    sl_pattern_slice(s, l, nslices, nrows, slice_ptr, [&](int k) { return (int)cin[p0 + 64 * k + l]; }, pout, ucol,
+                     uoff, G, win, cand_all[(threadIdx.x >> 6) & 3]);
 }
 
 // host view of the state: the deferred schedule keeps it in the bank of the current launch parity

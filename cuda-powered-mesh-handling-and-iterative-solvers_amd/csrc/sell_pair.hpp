@@ -87,21 +87,46 @@ __device__ __forceinline__ void pk_slice_span(int64_t s, int64_t nrows, int dmin
     *cmax = hi;
 }
 
+// a slice's lane-paired 16-bit deltas (pair_pos) written as one 32-bit store per pair (entries 2 k2, 2 k2 + 1 of lane
+// l are adjacent halves), then the unpaired last entry of an odd width: full 256-byte rows per store instruction
+#ifndef FEM_SL_SKIP
+#define FEM_SL_SKIP 0
+#endif
+template <class Delta>
+__device__ __forceinline__ void sl_store_pairs(int16_t* __restrict__ out, int w, int l, const Delta& delta) {
+#if FEM_SL_SKIP & 2
+    return;
+#endif
+    const int np = w >> 1;
+    int32_t* o32 = reinterpret_cast<int32_t*>(out);   // out = pout + slice start: 128-byte aligned
+    for (int k2 = 0; k2 < np; ++k2)
+        o32[k2 * 64 + l] = (int32_t)((uint32_t)(uint16_t)delta(2 * k2) | ((uint32_t)(uint16_t)delta(2 * k2 + 1) << 16));
+    if (w & 1) out[(int64_t)np * 128 + l] = (int16_t)delta(w - 1);
+}
+
 // The solver layout of one slice s of a bs = 1 pattern, by the wave whose lane l is row s * 64 + l (k_sell_sl_pattern,
 // and k_sell_fill_graph right after it wrote the slice's deltas): see k_sell_sl_pattern (pcg.hip). cand: SU_MAXW ints of
-// the wave's LDS. cin: the slice's plain 16-bit deltas (each lane reads only its own row's entries before the shuffles).
+// the wave's LDS. delta(k): this lane's plain 16-bit delta of entry k of the slice (each lane reads only its own row's
+// entries before the shuffles) -- from memory (k_sell_sl_pattern) or from the rows the fill pass holds in LDS.
+template <class Delta>
 __device__ __forceinline__ void sl_pattern_slice(int64_t s, int l, int64_t nslices, int64_t nrows,
-                                                 const int64_t* __restrict__ slice_ptr, const int16_t* cin,
+                                                 const int64_t* __restrict__ slice_ptr, const Delta& delta,
                                                  int16_t* __restrict__ pout, int16_t* __restrict__ ucol,
                                                  int32_t* __restrict__ uoff, int G, int* __restrict__ win, int* cand) {
+#if FEM_SL_SKIP & 4   // timing builds only (wrong layout): the fill pass without the solver layout
+    return;
+#endif
     const int64_t p0 = slice_ptr[s];
     const int w = (int)((slice_ptr[s + 1] - p0) >> 6);
     const int64_t row = s * 64 + l;
+#if FEM_SL_SKIP & 1
+    G = 0;
+#endif
     if (G > 0) {   // gather window (k_pk_window): the delta union of the slice over its owner workgroup
         int dmin = 0, dmax = 0;
         if (row < nrows)
             for (int k = 0; k < w; ++k) {
-                const int d = cin[p0 + 64 * k + l];
+                const int d = delta(k);
                 dmin = d < dmin ? d : dmin;
                 dmax = d > dmax ? d : dmax;
             }
@@ -120,7 +145,7 @@ __device__ __forceinline__ void sl_pattern_slice(int64_t s, int l, int64_t nslic
     if (ok) {
         int prev = -(1 << 30);
         for (int k = 0; k < w; ++k) {
-            const int d = cin[p0 + 64 * k + l];
+            const int d = delta(k);
             if (len == k && d > prev) {
                 ++len;
                 prev = d;
@@ -134,7 +159,7 @@ __device__ __forceinline__ void sl_pattern_slice(int64_t s, int l, int64_t nslic
     if (ok && full) {
         const int c = __builtin_ctzll(full);
         for (int k = 0; k < w; ++k) {
-            const int d = __shfl((int)cin[p0 + 64 * k + l], c, 64);
+            const int d = __shfl(delta(k), c, 64);
             if (l == 0) cand[k] = d;
             const int64_t col = row + d;
             if (col < 0 || col >= nrows) ok = false;
@@ -144,7 +169,7 @@ __device__ __forceinline__ void sl_pattern_slice(int64_t s, int l, int64_t nslic
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         int i = 0;
         for (int k = 0; k < len && ok; ++k) {
-            const int d = cin[p0 + 64 * k + l];
+            const int d = delta(k);
             while (i < w && cand[i] < d) ++i;
             if (i == w || cand[i] != d) ok = false;
             ++i;
@@ -155,11 +180,11 @@ __device__ __forceinline__ void sl_pattern_slice(int64_t s, int l, int64_t nslic
     ok = __all(ok);
     if (!ok) {
         if (l == 0) uoff[s] = -1;
-        for (int k = 0; k < w; ++k) pout[p0 + pair_pos(k, w, l)] = cin[p0 + 64 * k + l];
+        sl_store_pairs(pout + p0, w, l, delta);
         return;
     }
     const int32_t uo = (int32_t)(2 * (p0 >> 6));   // even: the deltas are read as int32 pairs
-    for (int k = 0; k < w; ++k) pout[p0 + pair_pos(k, w, l)] = (int16_t)cand[k];
+    sl_store_pairs(pout + p0, w, l, [&](int k) { return cand[k]; });
     for (int k = l; k < w; k += 64) ucol[uo + k] = (int16_t)cand[k];
     if (l == 0) uoff[s] = uo;
 }

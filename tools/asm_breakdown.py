@@ -62,7 +62,7 @@ def main():
         st = {}
         sync()
         t0 = time.perf_counter()
-        g = system.build_graph(tets, N)
+        g = system.build_graph(tets, N, solver_layout=(bs == 1))
         sync()
         st["graph"] = (time.perf_counter() - t0) * 1e3
         t0 = time.perf_counter()
