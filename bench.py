@@ -317,7 +317,7 @@ def measure_matfree(a, coords, tets, dev, ref):
         t0 = time.perf_counter()
         A = system.MatFreeOperator(coords, tets, "elastic", E, nu)
         mask = torch.zeros((N, 3), dtype=torch.uint8, device=dev)
-        mask[fixed] = 1
+        mask.index_fill_(0, fixed, 1)   # a fill kernel: no host-to-device copy (and host wait) of the 1
         w = A.jacobi(mask.view(-1))
         sync()
         t_b = time.perf_counter() - t0
@@ -566,7 +566,7 @@ def measure(a, kind, coords, tets, dev):
             reorder_ms.append((time.perf_counter() - t0) * 1e3)
         A = system.assemble_tet4_system(c, t, kind, E, nu)
         mask = torch.zeros((N, A.bs), dtype=torch.uint8, device=dev)
-        mask[fx] = 1
+        mask.index_fill_(0, fx, 1)   # a fill kernel: no host-to-device copy (and host wait) of the 1
         w = A.jacobi(mask.view(-1))
         sync()
         t_asm = time.perf_counter() - t0

@@ -70,6 +70,21 @@ __device__ __forceinline__ double block_sum256(double v, double* lds4) {
     double t = (lds4[0] + lds4[1]) + (lds4[2] + lds4[3]);
     return t;
 }
+// the same over NT = 256 or 512 threads (lds: NT / 64 doubles; 512: the two 256-thread trees added)
+template <int NT>
+__device__ __forceinline__ double block_sum(double v, double* lds) {
+    static_assert(NT == 256 || NT == 512, "block_sum: 256 or 512 threads");
+    if constexpr (NT == 256) {
+        return block_sum256(v, lds);
+    } else {
+        v = wave_sum(v);
+        const int w = threadIdx.x >> 6;
+        __syncthreads();
+        if ((threadIdx.x & 63) == 0) lds[w] = v;
+        __syncthreads();
+        return ((lds[0] + lds[1]) + (lds[2] + lds[3])) + ((lds[4] + lds[5]) + (lds[6] + lds[7]));
+    }
+}
 
 __device__ __forceinline__ int wave_max_i(int v) {
 #pragma unroll
@@ -130,6 +145,7 @@ constexpr int RED_SHARDS = 32;
 
 constexpr int RED_COUNTER_WORDS = (RED_SHARDS + 1) * 32;
 
+template <int NT = 256>   // threads of the calling block (lds4: NT / 64 doubles)
 __device__ __forceinline__ bool reduce_grid(double partial, double* partials, unsigned* counters, double* total,
                                             double* lds4, int* lds_flag) {
     const unsigned G = gridDim.x;
@@ -148,9 +164,9 @@ __device__ __forceinline__ bool reduce_grid(double partial, double* partials, un
     __syncthreads();
     if (!*lds_flag) return false;
     double v = 0.0;
-    for (unsigned i = threadIdx.x; i < in_shard; i += 256)
+    for (unsigned i = threadIdx.x; i < in_shard; i += NT)
         v += __hip_atomic_load(&partials[sh + i * RED_SHARDS], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    v = block_sum256(v, lds4);
+    v = block_sum<NT>(v, lds4);
     if (threadIdx.x == 0) {
         __hip_atomic_store(&shard_sums[sh], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         fem_drain_stores();
@@ -165,7 +181,7 @@ __device__ __forceinline__ bool reduce_grid(double partial, double* partials, un
     double s = (threadIdx.x < nsh)
                    ? __hip_atomic_load(&shard_sums[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                    : 0.0;
-    *total = block_sum256(s, lds4);
+    *total = block_sum<NT>(s, lds4);
     return true;
 }
 

@@ -50,8 +50,21 @@ constexpr int MF_NC = 240;      // local ids are bytes
 constexpr int MF_PIECE = 32;
 #endif
 static_assert(4 * MF_PIECE <= MF_NC, "a piece of MF_PIECE elements always fits the node cap");
+// FEM_MF_W512 = 1 (A/B): 512-thread workgroups -- the chunk's 512 element vectors formed in one pass (64 KB of LDS,
+// 2 workgroups per CU: the same 16 waves) and two lanes per local node in the node sums (each sums half of the
+// node's pairs in order, the halves added once: a node's sum no longer waits for its longest-walking neighbour lane)
+#ifndef FEM_MF_W512
+#define FEM_MF_W512 0
+#endif
+#if FEM_MF_W512 && !FEM_MF_WAVE
+constexpr int MF_PASS = 512;
+constexpr int MF_BLOCK = 512;
+constexpr int MF_LPN = 2;       // lanes per local node
+#else
 constexpr int MF_PASS = 256;    // elements formed per pass (= threads of the workgroup; workgroup chunks)
 constexpr int MF_BLOCK = 256;
+constexpr int MF_LPN = 1;
+#endif
 #ifndef FEM_MF_UNROLL
 #define FEM_MF_UNROLL 4
 #endif
@@ -269,7 +282,8 @@ __device__ __forceinline__ void mf_pf1(const MfOp& op, int64_t c, MfPf<BS>& f) {
     f.ne = __builtin_amdgcn_readlane(f.b_e, 1) - f.e0;
     f.s0 = __builtin_amdgcn_readlane(f.b_s, 0);
     f.nn = __builtin_amdgcn_readlane(f.b_s, 1) - f.s0;
-    const int t = tid < f.nn ? tid : f.nn - 1;   // a chunk has >= 1 node and >= 1 element
+    const int tn = tid / MF_LPN;                  // this lane's local node (MF_LPN lanes per node)
+    const int t = tn < f.nn ? tn : f.nn - 1;      // a chunk has >= 1 node and >= 1 element
     f.node = op.cnode[f.s0 + t];
     f.lp = op.lptr[f.s0 + c + t];
     f.lp1 = op.lptr[f.s0 + c + t + 1];           // the chunk's end marker for its last node
@@ -298,18 +312,20 @@ __device__ __forceinline__ void mf_pf2(const MfOp& op, const double* __restrict_
 template <int BS, int MODE>
 __device__ __forceinline__ bool mf_step(const MfOp& op, const double* __restrict__ x, double* __restrict__ slots,
                                         MfLds<BS, mf_fc<MODE>()>& L, int64_t base, int64_t per, int64_t nb,
-                                        int64_t& k, MfPf<BS>& cur, MfPf<BS>& n1, MfPf<BS>& n2, double& dot) {
+                                        int64_t last, int64_t& k, MfPf<BS>& cur, MfPf<BS>& n1, MfPf<BS>& n2,
+                                        double& dot) {
     constexpr int FC = mf_fc<MODE>();
     const int tid = threadIdx.x;
-    // chunks past this workgroup's range load its first chunk's data again (in range, never used)
-    const int64_t first = base + blockIdx.x / NXCD;
-    const auto chunk = [&](int64_t kk) { return kk < per && base + kk < op.nchunks ? base + kk : first; };
+    // chunks past this workgroup's range load its last chunk's data again (in range and in L2, never used)
+    const auto chunk = [&](int64_t kk) { return kk < per && base + kk < op.nchunks ? base + kk : last; };
     __syncthreads();   // the previous chunk's LDS reads are done
-    if (tid < cur.nn) {
+    const int tn = tid / MF_LPN;                   // this lane's local node
+    const bool own = tn < cur.nn && tid % MF_LPN == 0;   // the lane that installs and stores the node
+    if (own) {
 #pragma unroll
-        for (int q = 0; q < 3; ++q) L.nd[tid][q] = cur.xv[q];
+        for (int q = 0; q < 3; ++q) L.nd[tn][q] = cur.xv[q];
 #pragma unroll
-        for (int q = 0; q < BS; ++q) L.nd[tid][3 + q] = cur.pv[q];
+        for (int q = 0; q < BS; ++q) L.nd[tn][3 + q] = cur.pv[q];
     }
     if (8 * tid < 4 * cur.ne) reinterpret_cast<mf_u32x4*>(L.ent)[tid] = cur.ent;
     // issue order: every load a later wait needs has the same younger loads behind it on every path (the prologue's
@@ -321,8 +337,13 @@ __device__ __forceinline__ bool mf_step(const MfOp& op, const double* __restrict
     double acc[BS];
 #pragma unroll
     for (int q = 0; q < BS; ++q) acc[q] = 0.0;
-    int pos = tid < cur.nn ? cur.lp : 0;
-    const int end = tid < cur.nn ? cur.lp1 : 0;
+    int pos = tn < cur.nn ? cur.lp : 0;
+    int end = tn < cur.nn ? cur.lp1 : 0;
+    if constexpr (MF_LPN == 2) {   // lane 0 of the node: the first half of its pairs, lane 1 the rest
+        const int half = (end - pos + 1) >> 1;
+        if (tid & 1) pos += half;
+        else end = pos + half;
+    }
     // the node's pairs split at the pass boundary (pairs ascend by element): lower bound of 4 MF_PASS
     int mid = end;
     if (cur.ne > MF_PASS) {
@@ -408,15 +429,19 @@ __device__ __forceinline__ bool mf_step(const MfOp& op, const double* __restrict
         }
         __syncthreads();
     }
-    if (tid < cur.nn) {
+    if constexpr (MF_LPN == 2) {   // the halves added once (a + b == b + a: both lanes hold the same sum)
+#pragma unroll
+        for (int q = 0; q < BS; ++q) acc[q] += __shfl_xor(acc[q], 1, 64);
+    }
+    if (own) {
 #pragma unroll
         for (int q = 0; q < BS; ++q) {
-            mf_store_slot(&slots[(int64_t)(op.spos ? cur.sp : cur.s0 + tid) * BS + q], acc[q]);
+            mf_store_slot(&slots[(int64_t)(op.spos ? cur.sp : cur.s0 + tn) * BS + q], acc[q]);
             if constexpr (MODE == MF_DOT) dot += cur.pv[q] * acc[q];
         }
 #if FEM_MF_SPCHECK
         // the carried position against one read now (the round-4 question)
-        const int spc = op.spos ? op.spos[cur.s0 + tid] : cur.s0 + tid;
+        const int spc = op.spos ? op.spos[cur.s0 + tn] : cur.s0 + tn;
         atomicAdd(&mf_spcheck[0], 1ull);
         if (op.spos && cur.sp != spc && atomicAdd(&mf_spcheck[1], 1ull) == 0) {
             mf_spcheck[2] = ((unsigned long long)(base + k) << 16) | (unsigned)tid;
@@ -445,7 +470,10 @@ __device__ __forceinline__ double mf_walk(const MfOp& op, const double* __restri
     int64_t k = blockIdx.x / NXCD;
     double dot = 0.0;
     if (k >= per || base + k >= op.nchunks) return dot;
-    const auto chunk = [&](int64_t kk) { return kk < per && base + kk < op.nchunks ? base + kk : base + k; };
+    // this workgroup's last chunk: the stand-in for the chunks past its range (mf_step)
+    const int64_t cnt = (per < op.nchunks - base ? per : op.nchunks - base);
+    const int64_t last = base + k + ((cnt - 1 - k) / nb) * nb;
+    const auto chunk = [&](int64_t kk) { return kk < per && base + kk < op.nchunks ? base + kk : last; };
     MfPf<BS> A, B, C;   // records rotate by name: the loop body is three steps
     mf_pf0<BS>(op, chunk(k), A);
     mf_pf0<BS>(op, chunk(k + nb), B);
@@ -454,9 +482,9 @@ __device__ __forceinline__ double mf_walk(const MfOp& op, const double* __restri
     mf_pf0<BS>(op, chunk(k + 2 * nb), C);
     mf_pf1<BS>(op, chunk(k + nb), B);
     for (;;) {
-        if (!mf_step<BS, MODE>(op, x, slots, L, base, per, nb, k, A, B, C, dot)) break;
-        if (!mf_step<BS, MODE>(op, x, slots, L, base, per, nb, k, B, C, A, dot)) break;
-        if (!mf_step<BS, MODE>(op, x, slots, L, base, per, nb, k, C, A, B, dot)) break;
+        if (!mf_step<BS, MODE>(op, x, slots, L, base, per, nb, last, k, A, B, C, dot)) break;
+        if (!mf_step<BS, MODE>(op, x, slots, L, base, per, nb, last, k, B, C, A, dot)) break;
+        if (!mf_step<BS, MODE>(op, x, slots, L, base, per, nb, last, k, C, A, B, dot)) break;
     }
     return dot;
 }

@@ -772,7 +772,8 @@ __global__ void __launch_bounds__(256) k_sell_fill_graph(const int32_t* __restri
                                                          int16_t* __restrict__ pout = nullptr,
                                                          int16_t* __restrict__ ucol = nullptr,
                                                          int32_t* __restrict__ uoff = nullptr, int G = 0,
-                                                         int* __restrict__ win = nullptr) {
+                                                         int* __restrict__ win = nullptr,
+                                                         int2* __restrict__ span = nullptr) {
     __shared__ int32_t rp_s[4][65];
     __shared__ int cand_all[4][SU_MAXW];
     constexpr int TS = G_TCAP + 1;   // padded row stride: lane = row reads hit distinct banks
@@ -847,7 +848,8 @@ __global__ void __launch_bounds__(256) k_sell_fill_graph(const int32_t* __restri
                 const int64_t d = (int64_t)c - r;
                 return (d > 32767 || d < -32767) ? 0 : (int)d;
             };
-            sl_pattern_slice(s, lane, nslices, nrows, slice_ptr, delta, pout, ucol, uoff, G, win, cand_all[wid]);
+            sl_pattern_slice(s, lane, nslices, nrows, slice_ptr, delta, pout, ucol, uoff, G, win, cand_all[wid],
+                             span);
         }
         const int p0 = rp_s[wid][0], p1 = rp_s[wid][64];
         for (int p = p0 + lane; p < p1; p += 64) {
@@ -863,15 +865,6 @@ __global__ void __launch_bounds__(256) k_sell_fill_graph(const int32_t* __restri
             if (!defer[row]) colidx[p] = rows[lo * TS + k];
         }
         __builtin_amdgcn_wave_barrier();   // the staged rows consumed before the next slice overwrites them
-    }
-}
-
-// empty gather windows (pcg_persist.hpp k_pk_window_init with lo_empty = G)
-__global__ void k_win_init(int G, int* __restrict__ win) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < G) {
-        win[i] = G;
-        win[G + i] = -1;
     }
 }
 
@@ -1168,17 +1161,22 @@ int fem_graph_sell_fill_sl(const int64_t* conn, int npe, const int32_t* inc_ptr,
     }
     hipStream_t st = S(stream);
     FEM_HIP(hipMemsetAsync(diagpos, 0xff, sizeof(int32_t) * (size_t)N, st));   // -1: no diagonal
-    if (G > 0) {   // empty windows (k_pk_window_init's values: lo = G, hi = -1)
-        hipLaunchKernelGGL(k_win_init, dim3((unsigned)cdiv(G, 256)), dim3(256), 0, st, G, win);
-        FEM_LAUNCHED();
-    }
     const int rc = graph_fill(conn, npe, inc_ptr, inc, N, rowptr, colidx, diagpos, defer_flags(tmp, N), st);
     if (rc != FEM_OK) return rc;
     const int64_t ns = cdiv(N, 64);
+    // per-slice owner spans (stream-ordered scratch), reduced into the G windows after the fill pass
+    int2* span = nullptr;
+    if (G > 0) FEM_HIP(hipMallocAsync((void**)&span, sizeof(int2) * (size_t)ns, st));
     hipLaunchKernelGGL(k_sell_fill_graph, dim3((unsigned)std::min<int64_t>(cdiv(ns, 4), 16384)), dim3(256), 0, st,
                        rowptr, tmp, defer_flags(tmp, N), N, ns, slice_ptr, colidx, diagpos, cols, dcols,
-                       (int64_t*)nullptr, (int32_t*)nullptr, pcols, ucol, uoff, G, win);
+                       (int64_t*)nullptr, (int32_t*)nullptr, pcols, ucol, uoff, G, win, span);
     FEM_LAUNCHED();
+    if (G > 0) {
+        hipLaunchKernelGGL(k_win_from_spans, dim3((unsigned)cdiv((int64_t)G * 64, 256)), dim3(256), 0, st, G, ns,
+                           (const int2*)span, win);
+        FEM_LAUNCHED();
+        FEM_HIP(hipFreeAsync(span, st));
+    }
     return FEM_OK;
 }
 

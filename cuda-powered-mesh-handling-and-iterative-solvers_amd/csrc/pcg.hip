@@ -1501,7 +1501,7 @@ __global__ void __launch_bounds__(C1F_BLOCK) k_cg1_fused(Cg1FArgs a) {
     if (threadIdx.x == 0) __hip_atomic_store(a.flags + (size_t)L * 32, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // ---- wait for the u of the gather window
     if (wv == 0) {
-        const int wlo = a.win[L], whi = a.win[G + L];
+        const int wlo = max(a.win[L], 0), whi = min(a.win[G + L], G - 1);   // never outside the flag array
         bool ok = true;
         for (int b0 = wlo; b0 <= whi && ok; b0 += 64) {
             const int jw = b0 + lane;
@@ -1879,14 +1879,15 @@ __global__ void __launch_bounds__(MF_BLOCK) k_pcg_mf_dot(MfOp op, const double* 
                                                          double* __restrict__ slots, PcgState* __restrict__ st,
                                                          RedBuf red) {
     __shared__ MfKernelLds<BS, MF_DOT> L;
-    __shared__ double lds4[4];
+    __shared__ double lds4[MF_BLOCK / 64];
     __shared__ int flag;
     if (blockIdx.x == 0 && threadIdx.x == 0) st->xupd = 0;
     if (st->halt || st->iter >= st->max_iter) return;
     double dot = mf_walk_any<BS, MF_DOT>(op, p, slots, L);
-    dot = block_sum256(dot, lds4);
+    dot = block_sum<MF_BLOCK>(dot, lds4);
     double pq;
-    if (reduce_grid(dot, red.part(RED_K1), red.cnt(RED_K1), &pq, lds4, &flag) && threadIdx.x == 0) finish_pq(st, pq);
+    if (reduce_grid<MF_BLOCK>(dot, red.part(RED_K1), red.cnt(RED_K1), &pq, lds4, &flag) && threadIdx.x == 0)
+        finish_pq(st, pq);
 }
 
 // Distributed single-reduction iteration on the element-chunk operator (BASELINE configs[3] as north_star puts it:
@@ -3005,19 +3006,25 @@ int fem_pcg_get_schedule(fem_pcg* s) {
 
 __global__ void k_sell_sl_pattern(int64_t nslices, int64_t nrows, const int64_t* __restrict__ slice_ptr,
                                   const int16_t* __restrict__ cin, int16_t* __restrict__ pout,
-                                  int16_t* __restrict__ ucol, int32_t* __restrict__ uoff, int G, int* __restrict__ win);
+                                  int16_t* __restrict__ ucol, int32_t* __restrict__ uoff, int G, int* __restrict__ win,
+                                  int2* __restrict__ span);
 
 int fem_sell_sl_pattern(int64_t nrows, const int64_t* slice_ptr, const int16_t* dcols, int G, int16_t* pcols,
                         int16_t* ucol, int32_t* uoff, int32_t* win, fem_stream_t stream) {
     const int64_t ns = cdiv(nrows, 64);
     if (ns <= 0) return FEM_OK;
-    if (G > 0) {
-        hipLaunchKernelGGL(k_pk_window_init, dim3(cdiv(G, 256)), dim3(256), 0, S(stream), G, G, win);
-        FEM_LAUNCHED();
-    }
-    hipLaunchKernelGGL(k_sell_sl_pattern, dim3((unsigned)cdiv(ns, 4)), dim3(256), 0, S(stream), ns, nrows, slice_ptr,
-                       dcols, pcols, ucol, uoff, G > 0 ? G : 0, win);
+    hipStream_t st = S(stream);
+    int2* span = nullptr;   // per-slice owner spans, reduced into the windows (sl_pattern_slice, k_win_from_spans)
+    if (G > 0) FEM_HIP(hipMallocAsync((void**)&span, sizeof(int2) * (size_t)ns, st));
+    hipLaunchKernelGGL(k_sell_sl_pattern, dim3((unsigned)cdiv(ns, 4)), dim3(256), 0, st, ns, nrows, slice_ptr,
+                       dcols, pcols, ucol, uoff, G > 0 ? G : 0, win, span);
     FEM_LAUNCHED();
+    if (G > 0) {
+        hipLaunchKernelGGL(k_win_from_spans, dim3((unsigned)cdiv((int64_t)G * 64, 256)), dim3(256), 0, st, G, ns,
+                           (const int2*)span, win);
+        FEM_LAUNCHED();
+        FEM_HIP(hipFreeAsync(span, st));
+    }
     return FEM_OK;
 }
 
@@ -3406,14 +3413,14 @@ __global__ void __launch_bounds__(256) k_sell_sl_pattern(int64_t nslices, int64_
                                                          const int64_t* __restrict__ slice_ptr,
                                                          const int16_t* __restrict__ cin, int16_t* __restrict__ pout,
                                                          int16_t* __restrict__ ucol, int32_t* __restrict__ uoff, int G,
-                                                         int* __restrict__ win) {
+                                                         int* __restrict__ win, int2* __restrict__ span) {
     __shared__ int cand_all[4][SU_MAXW];
     const int64_t s = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;   // one wave per slice
     if (s >= nslices) return;   // wave-uniform
     const int l = threadIdx.x & 63;
     const int64_t p0 = slice_ptr[s];
     sl_pattern_slice(s, l, nslices, nrows, slice_ptr, [&](int k) { return (int)cin[p0 + 64 * k + l]; }, pout, ucol,
-                     uoff, G, win, cand_all[(threadIdx.x >> 6) & 3]);
+                     uoff, G, win, cand_all[(threadIdx.x >> 6) & 3], span);
 }
 
 // host view of the state: the deferred schedule keeps it in the bank of the current launch parity

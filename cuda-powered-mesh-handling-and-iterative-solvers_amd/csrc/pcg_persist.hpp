@@ -421,7 +421,9 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
         wl[j * 64] = wj;
         uo[j] = wj * rr[j];   // u = w r is how every u was formed (k_cg1_init, the update): bit-identical, no load
     }
-    const int wlo = a.win[L], whi = a.win[G + L];
+    // clamped to the flag array (nranks * G workgroups): a window is never an index outside it, whatever the
+    // array holds
+    const int wlo = max(a.win[L], 0), whi = min(a.win[G + L], (DIST ? a.nranks : 1) * G - 1);
     bool fail = false;
     bool st_loaded = !halt;   // the state is on chip and may have changed (nothing to store after a halt)
     int k = 0;

@@ -152,7 +152,9 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist3(PkArgs a) {
             vl[(j * 3 + c) * 64] = 0.0;
         }
     }
-    const int wlo = a.win[L], whi = a.win[G + L];
+    // clamped to the flag array (nranks * G workgroups): a window is never an index outside it, whatever the
+    // array holds
+    const int wlo = max(a.win[L], 0), whi = min(a.win[G + L], (DIST ? a.nranks : 1) * G - 1);
     bool fail = false;
     bool st_loaded = !halt;
     int k = 0;

@@ -108,11 +108,15 @@ __device__ __forceinline__ void sl_store_pairs(int16_t* __restrict__ out, int w,
 // and k_sell_fill_graph right after it wrote the slice's deltas): see k_sell_sl_pattern (pcg.hip). cand: SU_MAXW ints of
 // the wave's LDS. delta(k): this lane's plain 16-bit delta of entry k of the slice (each lane reads only its own row's
 // entries before the shuffles) -- from memory (k_sell_sl_pattern) or from the rows the fill pass holds in LDS.
+// span != null: the slice's owner-workgroup span (owner(cmin), owner(cmax)) is stored in span[s] and the windows are
+// formed from all spans by k_win_from_spans, instead of two atomics per slice on `win` (the G windows share a few
+// cache lines: 54,000 atomics on 16 lines serialise in the L2 -- 72 us of the 10M fill pass).
 template <class Delta>
 __device__ __forceinline__ void sl_pattern_slice(int64_t s, int l, int64_t nslices, int64_t nrows,
                                                  const int64_t* __restrict__ slice_ptr, const Delta& delta,
                                                  int16_t* __restrict__ pout, int16_t* __restrict__ ucol,
-                                                 int32_t* __restrict__ uoff, int G, int* __restrict__ win, int* cand) {
+                                                 int32_t* __restrict__ uoff, int G, int* __restrict__ win, int* cand,
+                                                 int2* __restrict__ span = nullptr) {
 #if FEM_SL_SKIP & 4   // timing builds only (wrong layout): the fill pass without the solver layout
     return;
 #endif
@@ -135,9 +139,13 @@ __device__ __forceinline__ void sl_pattern_slice(int64_t s, int l, int64_t nslic
         const int64_t WV = (int64_t)G * PK_WAVES;
         auto owner = [&](int64_t r) { return (int)((((r >> 6) + 1) * WV - 1) / nslices / PK_WAVES); };
         if (l == 0) {
-            const int me = owner(row);
-            atomicMin(win + me, owner(cmin));
-            atomicMax(win + G + me, owner(cmax));
+            if (span) {
+                span[s] = make_int2(owner(cmin), owner(cmax));
+            } else {
+                const int me = owner(row);
+                atomicMin(win + me, owner(cmin));
+                atomicMax(win + G + me, owner(cmax));
+            }
         }
     }
     bool ok = (s + 1) * 64 <= nrows && w > 0 && w <= SU_MAXW;
@@ -188,6 +196,44 @@ __device__ __forceinline__ void sl_pattern_slice(int64_t s, int l, int64_t nslic
     for (int k = l; k < w; k += 64) ucol[uo + k] = (int16_t)cand[k];
     if (l == 0) uoff[s] = uo;
 }
+// the gather windows from the per-slice owner spans (sl_pattern_slice with span): a wave per owner workgroup me, its
+// slices {s : owner(s) = me} (owner is monotone in s) found by binary search, min / max over their spans; an owner
+// without slices gets the empty window (G, -1) of k_pk_window_init
+__attribute__((unused)) static __global__ void __launch_bounds__(256) k_win_from_spans(int G, int64_t nslices,
+                                                                                       const int2* __restrict__ span,
+                                                                                       int* __restrict__ win) {
+    const int me = (int)(((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    const int l = threadIdx.x & 63;
+    if (me >= G) return;   // wave-uniform
+    const int64_t WV = (int64_t)G * PK_WAVES;
+    auto owner_s = [&](int64_t s) { return (int)(((s + 1) * WV - 1) / nslices / PK_WAVES); };
+    auto first = [&](int o) {   // first slice whose owner is >= o
+        int64_t lo = 0, hi = nslices;
+        while (lo < hi) {
+            const int64_t m = (lo + hi) >> 1;
+            if (owner_s(m) < o) lo = m + 1;
+            else hi = m;
+        }
+        return lo;
+    };
+    const int64_t s0 = first(me), s1 = first(me + 1);
+    int lo = G, hi = -1;
+    for (int64_t s = s0 + l; s < s1; s += 64) {
+        const int2 v = span[s];
+        lo = v.x < lo ? v.x : lo;
+        hi = v.y > hi ? v.y : hi;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const int a = __shfl_xor(lo, off), b = __shfl_xor(hi, off);
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+    }
+    if (l == 0) {
+        win[me] = lo;
+        win[G + me] = hi;
+    }
+}
+
 __attribute__((unused)) static __global__ void __launch_bounds__(256) k_sell_uniform(int64_t nslices, int64_t nrows,
                                                              const int64_t* __restrict__ slice_ptr,
                                                              const double* __restrict__ vin,

@@ -96,6 +96,8 @@ class RankRunner:
                     "fem_pcg_create")
             C.check(self.lib.fem_pcg_set_entries(self.h, A.g.sell_entries), "fem_pcg_set_entries")
             A.attach_cols16(self.h)
+            # plain_values() above may have formed the plain copy on the current stream: ordered before this stream
+            self.stream.wait_stream(torch.cuda.current_stream(A.device))
             # fine: comm block in fine-grained memory (coherent for the other GPUs' accesses; the default until a
             # real multi-GPU run has shown hipMalloc memory coherent there too). drop: fault injection (tests) --
             # this rank publishes nothing; FEM355_DIST_DROP_RANK=r selects rank r from the environment

@@ -143,9 +143,20 @@ class SolverLayout:
     G: int
 
 
+_NCU = {}
+
+
+def _cu_count(dev):
+    """Compute units of `dev` (cached: this sits between the pattern build's one sync and its next launch)."""
+    k = dev.index if dev.index is not None else torch.cuda.current_device()
+    if k not in _NCU:
+        _NCU[k] = torch.cuda.get_device_properties(dev).multi_processor_count
+    return _NCU[k]
+
+
 def _solver_layout_arrays(dev, ent, n_nodes):
     """Uninitialised SolverLayout arrays of a pattern with `ent` SELL entries (G: the persistent grid of `dev`)."""
-    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    ncu = _cu_count(dev)
     G = (ncu // 8) * 8
     ns = (n_nodes + 63) // 64
     return SolverLayout(torch.empty(max(ent, 1), dtype=torch.int16, device=dev),
@@ -748,6 +759,7 @@ class PcgRunner:
             A.create_context(self.b, self.x, self.w, self._mode, self._tol, self._eps, None, 0,
                              ctypes.c_void_p(self.stream.cuda_stream), self.h)
             self._sl = False
+            self.stream.wait_stream(torch.cuda.current_stream(A.device))
             return
         C.check(self.lib.fem_pcg_create(A.g.n_nodes, A.bs, C.ptr(A.g.slice_ptr), C.ptr(A.g.cols),
                                         A.solver_vals_ptr(plain), C.ptr(self.b), C.ptr(self.x), C.ptr(self.w),
@@ -761,6 +773,9 @@ class PcgRunner:
         self._sl = A.solver_layout and not plain
         if self.constraints is not None:
             C.check(self.lib.fem_pcg_set_constraints(self.h, *self.constraints.args()), "fem_pcg_set_constraints")
+        # the setup above may enqueue work on the current stream that this context's stream reads: the solver
+        # layout formed on first use (paired deltas, uniform lists, gather windows), the plain values formed back
+        self.stream.wait_stream(torch.cuda.current_stream(A.device))
 
     def set_tuning(self, flags):
         if self._sl and not (int(flags) & 2):   # no FEM_TUNE_PAIR: a context over the plain values instead

@@ -38,7 +38,7 @@ def main():
     def whole():
         A = system.assemble_tet4_system(coords, tets, a.kind, E, nu)
         mask = torch.zeros((N, A.bs), dtype=torch.uint8, device=dev)
-        mask[fixed] = 1
+        mask.index_fill_(0, fixed, 1)   # a fill kernel: no host-to-device copy (and host wait) of the 1
         w = A.jacobi(mask.view(-1))
         return A, w
 
@@ -71,7 +71,7 @@ def main():
         st["values"] = (time.perf_counter() - t0) * 1e3
         t0 = time.perf_counter()
         mask = torch.zeros((N, A.bs), dtype=torch.uint8, device=dev)
-        mask[fixed] = 1
+        mask.index_fill_(0, fixed, 1)   # a fill kernel: no host-to-device copy (and host wait) of the 1
         sync()
         st["mask"] = (time.perf_counter() - t0) * 1e3
         t0 = time.perf_counter()
