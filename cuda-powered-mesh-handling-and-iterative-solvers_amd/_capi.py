@@ -62,6 +62,7 @@ SIGNATURES = {
     "fem_scan_i32": (_I, [_P, _L, _P, _P, _P]),
     "fem_scan_i64": (_I, [_P, _L, _P, _P, _P]),
     "fem_sell_widths": (_I, [_P, _L, _P, _P]),
+    "fem_graph_sizes": (_I, [_P, _P, _P, _L, _P, _P, _P, _P]),
     "fem_sell_fill": (_I, [_P, _P, _L, _P, _P, _P, _P]),
     "fem_sell_csr2sell": (_I, [_P, _L, _P, _P, _P]),
     "fem_assemble_from_ke": (_I, [_P, _P, _I, _I, _P, _P, _L, _P, _P, _P, _P, _P, _P]),

@@ -1206,6 +1206,44 @@ int fem_sell_csr2sell(const int32_t* rowptr, int64_t nrows, const int64_t* slice
     return FEM_OK;
 }
 
+// the pattern's sizes in one launch (one block): {nnz = rowptr[N], entries = slice_ptr[ns], *bad, *ovf, widest slice}
+__global__ void __launch_bounds__(256) k_graph_sizes(const int32_t* __restrict__ rowptr,
+                                                     const int64_t* __restrict__ slice_ptr,
+                                                     const int64_t* __restrict__ width, int64_t N, int64_t ns,
+                                                     const int32_t* __restrict__ bad, const int32_t* __restrict__ ovf,
+                                                     int64_t* __restrict__ out) {
+    __shared__ int64_t m_s[4];
+    int64_t m = 0;
+    for (int64_t s = threadIdx.x; s < ns; s += 256) m = width[s] > m ? width[s] : m;
+    for (int o = 32; o > 0; o >>= 1) {
+        const int64_t v = __shfl_xor(m, o, 64);
+        m = v > m ? v : m;
+    }
+    if ((threadIdx.x & 63) == 0) m_s[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t w = m_s[0];
+        for (int i = 1; i < 4; ++i) w = m_s[i] > w ? m_s[i] : w;
+        out[0] = rowptr[N];
+        out[1] = slice_ptr[ns];
+        out[2] = bad ? *bad : 0;
+        out[3] = ovf ? *ovf : 0;
+        out[4] = w;
+    }
+}
+
+int fem_graph_sizes(const int32_t* rowptr, const int64_t* slice_ptr, const int64_t* width, int64_t N,
+                    const int32_t* bad, const int32_t* ovf, int64_t* out5, fem_stream_t stream) {
+    if (N < 0 || !rowptr || !slice_ptr || !out5 || (N > 0 && !width)) {
+        set_error("fem_graph_sizes: rowptr, slice_ptr, out5 (and width for N > 0) are required");
+        return FEM_EARG;
+    }
+    hipLaunchKernelGGL(k_graph_sizes, dim3(1), dim3(256), 0, S(stream), rowptr, slice_ptr, width, N, cdiv(N, 64), bad,
+                       ovf, out5);
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
 int fem_sell_widths(const int32_t* rowptr, int64_t nrows, int64_t* width, fem_stream_t stream) {
     int64_t ns = cdiv(nrows, 64);
     hipLaunchKernelGGL(k_sell_widths, dim3(stream_grid(ns, 256)), dim3(256), 0, S(stream), rowptr, nrows, ns, width);

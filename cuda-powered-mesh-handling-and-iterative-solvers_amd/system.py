@@ -235,8 +235,9 @@ def _build_graph(elements, n_nodes, compress, solver_layout=False):
     slice_ptr = torch.empty(ns + 1, dtype=I64, device=dev)
     work64 = torch.empty(int(lib.fem_scan_work_len(ns)) + 1, dtype=I64, device=dev)
     C.check(lib.fem_scan_i64(C.ptr(width), ns, C.ptr(slice_ptr), C.ptr(work64), st), "fem_scan_i64")
-    sizes = torch.stack([rowptr[-1].to(I64), slice_ptr[-1], bad[0].to(I64), ovf[0].to(I64),
-                         width.max() if ns > 0 else slice_ptr[-1]])
+    sizes = torch.empty(5, dtype=I64, device=dev)   # {nnz, entries, bad, far, widest slice}: one launch
+    C.check(lib.fem_graph_sizes(C.ptr(rowptr), C.ptr(slice_ptr), C.ptr(width), n_nodes, C.ptr(bad), C.ptr(ovf),
+                                C.ptr(sizes), st), "fem_graph_sizes")
     nnz, ent, nbad, far, maxw = (int(v) for v in sizes.cpu())
     if nbad:   # the sync of the build; the message names the offending node like check_connectivity
         check_connectivity(elements, n_nodes)

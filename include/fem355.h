@@ -169,6 +169,11 @@ int fem_scan_i32(const int32_t* in, int64_t n, int32_t* out, int32_t* work, fem_
  *   fem_sell_widths: width [S] int64 = 64 * max row length in the slice (scan it with fem_scan_i64)
  *   fem_sell_fill  : cols (padding = own row) and the CSR->SELL entry map csr2sell [nnz] int64 */
 int fem_sell_widths(const int32_t* rowptr, int64_t nrows, int64_t* width, fem_stream_t stream);
+/* the pattern's sizes for the build's one device-to-host read, in one launch: out5 = {nnz = rowptr[N], SELL entries
+ * = slice_ptr[S], *bad (fem_incidence_checked; 0 if NULL), *ovf (fem_graph_count2; 0 if NULL), widest slice =
+ * max width[s]} (int64, device) */
+int fem_graph_sizes(const int32_t* rowptr, const int64_t* slice_ptr, const int64_t* width, int64_t N,
+                    const int32_t* bad, const int32_t* ovf, int64_t* out5, fem_stream_t stream);
 /* the CSR -> SELL entry map (as fem_sell_fill writes it) from rowptr and slice_ptr alone */
 int fem_sell_csr2sell(const int32_t* rowptr, int64_t nrows, const int64_t* slice_ptr, int64_t* csr2sell,
                       fem_stream_t stream);
