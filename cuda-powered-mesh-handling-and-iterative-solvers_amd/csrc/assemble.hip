@@ -1295,7 +1295,19 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
     __shared__ double dat_s[ND][NI + 1];
     __shared__ uint2 pos_s[NI];
     __shared__ uint8_t a_s[NI];             // local index of the row's node; bit 7: the element repeats a node
-    __shared__ double acc_s[AW * AV][R + 1];
+    // accumulators of (column slot i = k AV + value, row r): [i][r] with a padded row stride (default), or
+    // FEM_ACC_T = 1 (bs = 3, A/B): [r][i] with row stride AW AV + FEM_ACC_PAD -- the sweep's 16 lanes of one row then
+    // hit consecutive slots of their columns, the 4 rows of a wave offset by the padded stride
+#ifndef FEM_ACC_T
+#define FEM_ACC_T 0
+#endif
+#ifndef FEM_ACC_PAD
+#define FEM_ACC_PAD 1
+#endif
+    constexpr bool ACT = FEM_ACC_T && BS == 3;
+    constexpr int ARS = ACT ? AW * AV + FEM_ACC_PAD : R + 1;   // stride of the outer index
+    __shared__ double acc_flat[ACT ? R * ARS : AW * AV * ARS];
+    auto ACC = [&](int i, int r) -> double& { return ACT ? acc_flat[r * ARS + i] : acc_flat[i * ARS + r]; };
     __shared__ int maxc_s;
     const int tid = threadIdx.x;
     const int64_t per = (ntiles + NXCD - 1) / NXCD;
@@ -1346,7 +1358,7 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
             double v = 0.0;   // bs = 3: the sums start from zero, stored values are added when the row is written
             if (BS == 1 && !STORE && k < cw && ((SL && uo >= 0) || c0 + k < rp_s[r + 1] - rp_s[r]))
                 v = vals[SL ? e0 + pair_pos(c0 + k, W, l0 + r) : e0 + (int64_t)(c0 + k) * 64 + l0 + r];
-            acc_s[kc][r] = v;
+            ACC(kc, r) = v;
         }
         // software pipeline over the batches: a thread's next incidence entry is loaded before the current batch
         // is swept and its element's node ids right after, so a batch waits only for its coordinates
@@ -1519,7 +1531,7 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
 #pragma unroll
                         for (int cc = 0; cc < NV; ++cc) {
                             if (cc < nv) {
-                                double* ap = &acc_s[k * AV + slot0 + cc][lr];
+                                double* ap = &ACC(k * AV + slot0 + cc, lr);
                                 *ap = add_nc(*ap, v[cc]);
                             }
                         }
@@ -1530,7 +1542,7 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
 #pragma unroll
                             for (int cc = 0; cc < NV; ++cc) {
                                 if (cc < nv) {
-                                    double* ap = &acc_s[k * AV + slot0 + cc][lr];
+                                    double* ap = &ACC(k * AV + slot0 + cc, lr);
                                     *ap = add_nc(*ap, v[cc]);
                                 }
                             }
@@ -1552,10 +1564,10 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
             for (int q = tid; q < (kp1 - kp0) * R; q += NT) {
                 const int r = q % R, kp = kp0 + q / R, k = 2 * kp - c0;
                 *reinterpret_cast<double2*>(vals + e0 + (int64_t)kp * 128 + 2 * (l0 + r)) =
-                    make_double2(acc_s[k][r], acc_s[k + 1][r]);
+                    make_double2(ACC(k, r), ACC(k + 1, r));
             }
             if ((W & 1) && c0 + cw == W)
-                for (int r = tid; r < R; r += NT) vals[e0 + (int64_t)np * 128 + l0 + r] = acc_s[W - 1 - c0][r];
+                for (int r = tid; r < R; r += NT) vals[e0 + (int64_t)np * 128 + l0 + r] = ACC(W - 1 - c0, r);
             continue;
         }
         for (int q = tid; q < cw * B2 * R; q += NT) {
@@ -1563,10 +1575,10 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
             if (!STORE && !(SL && uo >= 0) && c0 + k >= rp_s[r + 1] - rp_s[r]) continue;   // adding: padding stays
             const int64_t Ei = e0 + (int64_t)(c0 + k) * 64 + l0 + r;
             if constexpr (BS == 1) {
-                vals[SL ? e0 + pair_pos(c0 + k, W, l0 + r) : Ei] = acc_s[kc][r];
+                vals[SL ? e0 + pair_pos(c0 + k, W, l0 + r) : Ei] = ACC(kc, r);
             } else {
                 const int rr = c / 3, cc = c - 3 * (c / 3);
-                double kv = el_combine(L, acc_s[k * AV + c][r], acc_s[k * AV + cc * 3 + rr][r], acc_s[k * AV + 9][r],
+                double kv = el_combine(L, ACC(k * AV + c, r), ACC(k * AV + cc * 3 + rr, r), ACC(k * AV + 9, r),
                                        rr == cc);
                 double* dst = &vals[SL ? sell_val_a(Ei, c) : sell_val(Ei, B2, c)];
                 if constexpr (!STORE) kv = add_nc(*dst, kv);
