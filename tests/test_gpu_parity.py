@@ -1315,3 +1315,58 @@ def test_solver_layout_from_the_fill_pass(gpu, case, monkeypatch):
     A1 = system.SellMatrix(gf, 1).add_tet4(cg, tg, 1.0)
     A2 = system.SellMatrix(gs, 1).add_tet4(cg, tg, 1.0)
     assert torch.equal(A1._svals, A2._svals)
+
+
+def _windows_restated(g, G, pk_waves=16):
+    """The persistent schedule's gather windows restated on the host from the pattern's 16-bit deltas (k_pk_window /
+    pk_slice_span, csrc/pcg_persist.hpp, sell_pair.hpp): per slice the union of its rows' deltas applied to the whole
+    slice, mapped to owner workgroups; per owner the min / max over its slices, (G, -1) for an owner without any."""
+    N = g.n_nodes
+    ns = (N + 63) // 64
+    sp = g.slice_ptr.cpu().tolist()
+    d = g.dcols.cpu().to(torch.int64)
+    W = G * pk_waves
+    owner = lambda r: (((r >> 6) + 1) * W - 1) // ns // pk_waves
+    lo = [G] * G
+    hi = [-1] * G
+    for s in range(ns):
+        w = (sp[s + 1] - sp[s]) // 64
+        blk = d[sp[s]:sp[s + 1]].view(w, 64)
+        rows = min(64, N - s * 64)
+        dmin = min(0, int(blk[:, :rows].min())) if w else 0
+        dmax = max(0, int(blk[:, :rows].max())) if w else 0
+        cl, ch = s * 64 + dmin, min(s * 64 + 63 + dmax, N - 1)
+        cl = max(cl, 0)
+        cl = min(cl, ch)
+        me = owner(s * 64)
+        lo[me] = min(lo[me], owner(cl))
+        hi[me] = max(hi[me], owner(ch))
+    return torch.tensor(lo + hi, dtype=torch.int32)
+
+
+@pytest.mark.parametrize("case", ["kuhn", "permuted", "ragged"])
+def test_gather_windows_from_slice_spans(gpu, case, monkeypatch):
+    """Round 5: the gather windows are reduced from per-slice owner spans (k_win_from_spans) instead of two atomics
+    per slice. Both producers -- the fill pass (fem_graph_sell_fill_sl) and the separate pass (fem_sell_sl_pattern)
+    -- against the host restatement of k_pk_window, exactly: a Kuhn cube, a random numbering (every window spans the
+    grid), and a mesh whose last slice is partial."""
+    _, mesh, _, system = _mods()
+    n = 12 if case == "ragged" else 13
+    c, t = mesh.kuhn_cube(n, jitter=0.1)
+    if case == "permuted":
+        perm = torch.randperm(c.shape[0], generator=torch.Generator().manual_seed(9))
+        inv = torch.empty_like(perm)
+        inv[perm] = torch.arange(perm.numel())
+        c, t = c[perm], inv[t]
+    N = c.shape[0]
+    assert case != "ragged" or N % 64 != 0
+    tg = t.to(gpu)
+    gf = system.build_graph(tg, N, solver_layout=True)
+    monkeypatch.setenv("FEM355_SL_SEPARATE", "1")
+    gs = system.build_graph(tg, N, solver_layout=True)
+    monkeypatch.delenv("FEM355_SL_SEPARATE")
+    a, b = gf.solver_layout(), gs.solver_layout()
+    torch.cuda.synchronize()
+    want = _windows_restated(gf, a.G)
+    assert torch.equal(a.win.cpu()[: 2 * a.G], want)
+    assert torch.equal(b.win.cpu()[: 2 * b.G], want)
