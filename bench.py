@@ -363,9 +363,10 @@ def measure_matfree(a, coords, tets, dev, ref):
     k1 = ms[0] / max(cnt[0], 1)
     upd = ms[1] / max(cnt[1], 1)
     flops = MF_FLOPS_PER_ELEMENT * M
-    # HBM bytes one K1 must move: the static layout (element local ids, pair lists, chunk tables), the coordinates and
-    # p once, the slot values written; the merged update reads them back with the node -> slot lists
-    alg = info["static_bytes"] - 4 * (N + 1) - 4 * info["slots"] + 24 * N + 24 * N + 24 * info["slots"]
+    # HBM bytes one K1 must move: the static layout (element local ids, pair lists, chunk tables, the node-major slot
+    # positions spos -- carried in the walk's prefetch records since round 5), the coordinates and p once, the slot
+    # values written; the merged update reads the slots back with the node -> slot pointers (nptr, not K1's)
+    alg = info["static_bytes"] - 4 * (N + 1) + 24 * N + 24 * N + 24 * info["slots"]
     return {
         "value": a.steps / dt, "unit": "CG iterations/s", "ms_per_step": dt / a.steps * 1e3,
         "vs_assembled": (a.steps / dt) / ref["value"],
@@ -382,7 +383,8 @@ def measure_matfree(a, coords, tets, dev, ref):
                      # PMC HBM bytes of one K1 launch (FETCH_SIZE x 2 + WRITE_SIZE, tools/pmc_mf.sh), None unless taken
                      # on this layout (same algorithmic bytes)
                      "traffic": traffic_from_profiles(f"kuhn{a.n}_elastic_matfree", "k_pcg_mf_dot<3>", alg),
-                     "model": f"{MF_FLOPS_PER_ELEMENT} flops per element; bytes: layout + coordinates + p + slots"},
+                     "model": f"{MF_FLOPS_PER_ELEMENT} flops per element; bytes: layout (incl. spos) + coordinates + p "
+                              "+ slots"},
         "operator": "element-chunk (matrix-free): Morton-ordered chunks of <= 512 elements / 240 nodes, "
                     "fixed-order slot sums (csrc/matfree.hip)",
     }
