@@ -137,6 +137,9 @@ __global__ void __launch_bounds__(INB_T1) k_inc_l1(const int64_t* __restrict__ c
     }
 }
 
+#ifndef FEM_INC_NOSORT
+#define FEM_INC_NOSORT 0
+#endif
 // level 2: one workgroup per bucket; boff = the level-1 scan (bucket q's entries [boff[q G], boff[(q + 1) G]))
 __global__ void __launch_bounds__(256) k_inc_l2(const int2* __restrict__ kpair,
                                                 const int32_t* __restrict__ boff, int G, int64_t N, int bsh,
@@ -246,9 +249,14 @@ __global__ void __launch_bounds__(256) k_inc_l2(const int2* __restrict__ kpair,
             const int j = on[p];
             a = st[j];
             z = st[j + 1];
+#if FEM_INC_NOSORT   // timing builds only (wrong order): the segments left in arrival order
+            (void)j; (void)z;
+            inc[lo + p] = v;
+#else
             int r = a;
             for (int u = a; u < z; ++u) r += (out[u] < v);
             inc[lo + r] = v;
+#endif
         } else {
             v = scratch[lo + p];
             int l = 0, h = B;   // segment of position p: last j with st[j] <= p
