@@ -253,8 +253,14 @@ __global__ void __launch_bounds__(256) k_inc_l2(const int2* __restrict__ kpair,
             (void)j; (void)z;
             inc[lo + p] = v;
 #else
-            int r = a;
-            for (int u = a; u < z; ++u) r += (out[u] < v);
+            // rank = segment start + the number of smaller slots in the segment; four LDS reads in flight per step
+            // (one dependent read per step made the ~24-long segments a chain of LDS latencies)
+            int r = a, u = a;
+            for (; u + 4 <= z; u += 4) {
+                const int o0 = out[u], o1 = out[u + 1], o2 = out[u + 2], o3 = out[u + 3];
+                r += (int)(o0 < v) + (int)(o1 < v) + (int)(o2 < v) + (int)(o3 < v);
+            }
+            for (; u < z; ++u) r += (out[u] < v);
             inc[lo + r] = v;
 #endif
         } else {
