@@ -1209,6 +1209,31 @@ __device__ __forceinline__ uint32_t sorted_pos(const int32_t* cs, int n, int j) 
     return (b < n && cs[b] == j) ? (uint32_t)b : 0xffffu;
 }
 
+// sorted_pos of four keys in one lockstep search (the same halving steps and result per key): the four probes of a
+// step are independent LDS reads in flight together instead of four searches one after another
+__device__ __forceinline__ void sorted_pos4(const int32_t* cs, int n, const int j[4], uint32_t p[4]) {
+    if (n <= 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) p[q] = 0xffffu;
+        return;
+    }
+    int b[4] = {0, 0, 0, 0};
+    for (int len = n; len > 1;) {
+        const int half = len >> 1;
+        int v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = cs[b[q] + half];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) b[q] = v[q] < j[q] ? b[q] + half : b[q];
+        len -= half;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        b[q] += cs[b[q]] < j[q];
+        p[q] = (b[q] < n && cs[b[q]] == j[q]) ? (uint32_t)b[q] : 0xffffu;
+    }
+}
+
 // zero the SELL values of slices [0, ns) (slice_ptr on the device)
 __global__ void k_sell_zero(const int64_t* __restrict__ slice_ptr, int64_t ns, int bs2, double* __restrict__ vals) {
     const int64_t n = slice_ptr[ns] * bs2;
@@ -1289,6 +1314,22 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
     __shared__ int ip_s[R + 1];
     __shared__ int rp_s[R + 1];
     __shared__ int col_s[SEG];
+    // FEM_ASM_HASH (bs = 1, slice-uniform tiles): the slice's delta list also in a 64-slot open-addressing table
+    // (delta -> list position), so an element node's column is one LDS read (rarely two) instead of a binary search
+    // whose reads depend on each other. A timing build without any column search (FEM_ASM_NOSEARCH, wrong values)
+    // ran the 10M P1 value kernel in 544 instead of 724 us.
+#ifndef FEM_ASM_HASH
+#define FEM_ASM_HASH 1
+#endif
+#ifndef FEM_ASM_NOSEARCH
+#define FEM_ASM_NOSEARCH 0
+#endif
+#ifndef FEM_ASM_SEARCH4
+#define FEM_ASM_SEARCH4 1   // the other tiles: the four binary searches of an item in lockstep (sorted_pos4)
+#endif
+    constexpr bool HT = FEM_ASM_HASH && SL && BS == 1;
+    constexpr int HTN = 64;
+    __shared__ int2 ht_s[HT ? HTN : 1];
     __shared__ double xs_s[Cfg::XS ? SEG : 1][3];
     // padded strides: the sweep's lanes of one row read dat_s rows of different element nodes and update
     // accumulators of different columns -- with power-of-two strides those all fall into one LDS bank
@@ -1333,9 +1374,20 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
     // SL: a slice-uniform slice searches its delta list (W entries) instead of the rows' CSR columns
     const int uo = (SL && BS == 1) ? uoff[r0 >> 6] : -1;   // bs = 3: layout A, per-lane columns
     const bool staged = SL && uo >= 0 ? true : segn <= SEG;
-    if (SL && uo >= 0)
+    const bool use_ht = HT && uo >= 0 && W <= HTN / 2;
+    if (SL && uo >= 0) {
         for (int q = tid; q < W; q += NT) col_s[q] = ucol[uo + q];
-    else if (staged)
+        if (use_ht) {   // empty the table, then every list entry claims a slot (linear probing, compare-and-swap)
+            for (int q = tid; q < HTN; q += NT) ht_s[q] = make_int2(INT_MIN, 0);
+            __syncthreads();
+            if (tid < W) {
+                const int d = ucol[uo + tid];
+                unsigned h = ((unsigned)d * 2654435761u) >> 26;
+                while (atomicCAS(&ht_s[h].x, INT_MIN, d) != INT_MIN) h = (h + 1) & (HTN - 1);
+                ht_s[h].y = tid;
+            }
+        }
+    } else if (staged)
         for (int q = tid; q < segn; q += NT) {
             const int cq = colidx[seg0 + q];
             col_s[q] = cq;
@@ -1416,13 +1468,42 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                     int nodes[4];
                     uint32_t pp[4];
                     pk[0] = pk[1] = 0u;
+#if !FEM_ASM_NOSEARCH
+                    if (!use_ht && FEM_ASM_SEARCH4) {   // the four nodes' binary searches in lockstep
+                        int jj4[4];
+#pragma unroll
+                        for (int bb = 0; bb < 4; ++bb) jj4[bb] = (int)c[bb] - kshift;
+                        if (staged) sorted_pos4(col_s + cl, cn, jj4, pp);
+                        else sorted_pos4(colidx + seg0 + cl, cn, jj4, pp);
+                    }
+#endif
 #pragma unroll
                     for (int bb = 0; bb < 4; ++bb) {
                         nodes[bb] = (int)c[bb];
                         const int j = nodes[bb] - kshift;
                         // the tile-uniform branch keeps the LDS search on ds_read (one pointer for both would
                         // make every probe a flat load)
-                        pp[bb] = staged ? sorted_pos(col_s + cl, cn, j) : sorted_pos(colidx + seg0 + cl, cn, j);
+#if FEM_ASM_NOSEARCH   // timing builds only (wrong values): no column search, a fixed in-range slot
+                        pp[bb] = (uint32_t)(bb < cn ? bb : 0);
+                        (void)j;
+#else
+                        if (use_ht) {   // deltas are unique: the first matching key, or an empty slot = absent
+                            unsigned h = ((unsigned)j * 2654435761u) >> 26;
+                            uint32_t q = 0xffffu;
+                            for (int probe = 0; probe < HTN; ++probe) {
+                                const int2 e = ht_s[h];
+                                if (e.x == j) {
+                                    q = (uint32_t)e.y;
+                                    break;
+                                }
+                                if (e.x == INT_MIN) break;
+                                h = (h + 1) & (HTN - 1);
+                            }
+                            pp[bb] = q;
+                        } else if (!FEM_ASM_SEARCH4) {
+                            pp[bb] = staged ? sorted_pos(col_s + cl, cn, j) : sorted_pos(colidx + seg0 + cl, cn, j);
+                        }
+#endif
                         pk[bb >> 1] |= pp[bb] << (16 * (bb & 1));
                     }
                     double g[4][3];
