@@ -2265,7 +2265,7 @@ static int assemble_from_ke(const double* Ke, const int64_t* conn, int npe, int 
                 return FEM_OK;
             }
             double* tmp = nullptr;
-            FEM_HIP(hipMallocAsync((void**)&tmp, sizeof(double) * 9 * (size_t)(nnz > 0 ? nnz : 1), S(stream)));
+            FEM_HIP(::fem::malloc_async((void**)&tmp, sizeof(double) * 9 * (size_t)(nnz > 0 ? nnz : 1), S(stream)));
 #define FEM_KE_C(P)                                                                                             \
     if (npe == P && colform)                                                                                    \
         hipLaunchKernelGGL((k_assemble_ke_w<3, P, FEM_KE_RPL3, true>), g, dim3(256), 0, S(stream), Ke, conn,     \

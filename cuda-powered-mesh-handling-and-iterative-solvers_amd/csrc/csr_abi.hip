@@ -159,15 +159,15 @@ struct NodeGraph {
 
 static int node_graph(const int64_t* conn, int64_t M, int npe, int64_t N, hipStream_t st, bool cols, NodeGraph* g) {
     const fem_stream_t fs = reinterpret_cast<fem_stream_t>(st);
-    FEM_HIP(hipMallocAsync((void**)&g->inc_ptr, sizeof(int32_t) * (N + 1), st));
-    FEM_HIP(hipMallocAsync((void**)&g->inc, sizeof(int32_t) * (M * npe > 0 ? M * npe : 1), st));
+    FEM_HIP(::fem::malloc_async((void**)&g->inc_ptr, sizeof(int32_t) * (N + 1), st));
+    FEM_HIP(::fem::malloc_async((void**)&g->inc, sizeof(int32_t) * (M * npe > 0 ? M * npe : 1), st));
     int rc = fem_incidence(conn, M, npe, N, g->inc_ptr, g->inc, nullptr, fs);
     if (rc) return rc;
     int32_t *row_len = nullptr, *tmp = nullptr, *work = nullptr;
-    FEM_HIP(hipMallocAsync((void**)&row_len, sizeof(int32_t) * N, st));
-    FEM_HIP(hipMallocAsync((void**)&tmp, sizeof(int32_t) * fem_graph_tmp_len(N), st));
-    FEM_HIP(hipMallocAsync((void**)&g->rowptr, sizeof(int32_t) * (N + 1), st));
-    FEM_HIP(hipMallocAsync((void**)&work, sizeof(int32_t) * (fem_scan_work_len(N) + 1), st));
+    FEM_HIP(::fem::malloc_async((void**)&row_len, sizeof(int32_t) * N, st));
+    FEM_HIP(::fem::malloc_async((void**)&tmp, sizeof(int32_t) * fem_graph_tmp_len(N), st));
+    FEM_HIP(::fem::malloc_async((void**)&g->rowptr, sizeof(int32_t) * (N + 1), st));
+    FEM_HIP(::fem::malloc_async((void**)&work, sizeof(int32_t) * (fem_scan_work_len(N) + 1), st));
     if ((rc = fem_graph_count2(conn, npe, g->inc_ptr, g->inc, N, row_len, tmp, nullptr, fs))) return rc;
     if ((rc = fem_scan_i32(row_len, N, g->rowptr, work, fs))) return rc;
     int32_t nnz = 0;
@@ -176,8 +176,8 @@ static int node_graph(const int64_t* conn, int64_t M, int npe, int64_t N, hipStr
     g->nnz = nnz;
     if (cols) {
         int32_t* diag = nullptr;
-        FEM_HIP(hipMallocAsync((void**)&g->colidx, sizeof(int32_t) * (g->nnz > 0 ? g->nnz : 1), st));
-        FEM_HIP(hipMallocAsync((void**)&diag, sizeof(int32_t) * N, st));
+        FEM_HIP(::fem::malloc_async((void**)&g->colidx, sizeof(int32_t) * (g->nnz > 0 ? g->nnz : 1), st));
+        FEM_HIP(::fem::malloc_async((void**)&diag, sizeof(int32_t) * N, st));
         if ((rc = fem_graph_fill2(conn, npe, g->inc_ptr, g->inc, N, g->rowptr, tmp, g->colidx, diag, fs))) return rc;
         FEM_HIP(hipFreeAsync(diag, st));
     }
@@ -208,8 +208,8 @@ int fem_solid_ke(int type, const double* coords, const int64_t* conn, int64_t M,
         const double pt[3] = {1.0 / 3.0, 1.0 / 3.0, 0.0};
         double* dip = nullptr;
         double* dN = nullptr;
-        FEM_HIP(hipMallocAsync((void**)&dip, sizeof(pt), st));
-        FEM_HIP(hipMallocAsync((void**)&dN, sizeof(double) * 18, st));
+        FEM_HIP(::fem::malloc_async((void**)&dip, sizeof(pt), st));
+        FEM_HIP(::fem::malloc_async((void**)&dN, sizeof(double) * 18, st));
         FEM_HIP(hipMemcpyAsync(dip, pt, sizeof(pt), hipMemcpyHostToDevice, st));
         hipLaunchKernelGGL(k_dn_table, dim3(1), dim3(64), 0, st, 6, dip, 1, dN);
         FEM_LAUNCHED();
@@ -224,7 +224,7 @@ int fem_solid_ke(int type, const double* coords, const int64_t* conn, int64_t M,
         return FEM_EARG;
     }
     double* dN = nullptr;
-    FEM_HIP(hipMallocAsync((void**)&dN, sizeof(double) * n_ip * npe * 3, st));
+    FEM_HIP(::fem::malloc_async((void**)&dN, sizeof(double) * n_ip * npe * 3, st));
     hipLaunchKernelGGL(k_dn_table, dim3(cdiv(n_ip, 64)), dim3(64), 0, st, npe, ip, n_ip, dN);
     FEM_LAUNCHED();
     // single=False: per-point stack for c3d8 / c3d10 (Q6); c3d6's flag only selects the one-point rule
@@ -273,8 +273,8 @@ int fem_csr_fill(const double* Ke, const int64_t* conn, int64_t M, int npe, int 
     const hipStream_t st = S(stream);
     NodeGraph g;
     g.inc_ptr = nullptr;
-    FEM_HIP(hipMallocAsync((void**)&g.inc_ptr, sizeof(int32_t) * (n_nodes + 1), st));
-    FEM_HIP(hipMallocAsync((void**)&g.inc, sizeof(int32_t) * (M * npe > 0 ? M * npe : 1), st));
+    FEM_HIP(::fem::malloc_async((void**)&g.inc_ptr, sizeof(int32_t) * (n_nodes + 1), st));
+    FEM_HIP(::fem::malloc_async((void**)&g.inc, sizeof(int32_t) * (M * npe > 0 ? M * npe : 1), st));
     int rc = fem_incidence(conn, M, npe, n_nodes, g.inc_ptr, g.inc, nullptr, stream);
     if (!rc) {
         hipLaunchKernelGGL(k_csr_fill, dim3(stream_grid(n_nodes * dpn, 256)), dim3(256), 0, st, Ke, conn, npe, dpn,
@@ -312,20 +312,20 @@ int fem_pcg_csr(const int32_t* rowptr, const int32_t* colidx, const double* vals
     int rc = FEM_OK;
     int32_t nnz = 0;
     FEM_HIP(hipMemcpyAsync(&nnz, rowptr + n, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    FEM_HIP(hipMallocAsync((void**)&width, sizeof(int64_t) * ns, st));
-    FEM_HIP(hipMallocAsync((void**)&slice_ptr, sizeof(int64_t) * (ns + 1), st));
-    FEM_HIP(hipMallocAsync((void**)&work, sizeof(int64_t) * (fem_scan_work_len(ns) + 1), st));
+    FEM_HIP(::fem::malloc_async((void**)&width, sizeof(int64_t) * ns, st));
+    FEM_HIP(::fem::malloc_async((void**)&slice_ptr, sizeof(int64_t) * (ns + 1), st));
+    FEM_HIP(::fem::malloc_async((void**)&work, sizeof(int64_t) * (fem_scan_work_len(ns) + 1), st));
     if ((rc = fem_sell_widths(rowptr, n, width, stream))) return rc;
     if ((rc = fem_scan_i64(width, ns, slice_ptr, work, stream))) return rc;
     int64_t ent = 0;
     FEM_HIP(hipMemcpyAsync(&ent, slice_ptr + ns, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     FEM_HIP(hipStreamSynchronize(st));
-    FEM_HIP(hipMallocAsync((void**)&cols, sizeof(int32_t) * (ent > 0 ? ent : 1), st));
-    FEM_HIP(hipMallocAsync((void**)&csr2sell, sizeof(int64_t) * (nnz > 0 ? nnz : 1), st));
-    FEM_HIP(hipMallocAsync((void**)&sv, sizeof(double) * (ent > 0 ? ent : 1), st));
-    FEM_HIP(hipMallocAsync((void**)&d16, sizeof(int16_t) * (ent > 0 ? ent : 1), st));
-    FEM_HIP(hipMallocAsync((void**)&ovf, sizeof(int32_t), st));
-    FEM_HIP(hipMallocAsync((void**)&w, sizeof(double) * n, st));
+    FEM_HIP(::fem::malloc_async((void**)&cols, sizeof(int32_t) * (ent > 0 ? ent : 1), st));
+    FEM_HIP(::fem::malloc_async((void**)&csr2sell, sizeof(int64_t) * (nnz > 0 ? nnz : 1), st));
+    FEM_HIP(::fem::malloc_async((void**)&sv, sizeof(double) * (ent > 0 ? ent : 1), st));
+    FEM_HIP(::fem::malloc_async((void**)&d16, sizeof(int16_t) * (ent > 0 ? ent : 1), st));
+    FEM_HIP(::fem::malloc_async((void**)&ovf, sizeof(int32_t), st));
+    FEM_HIP(::fem::malloc_async((void**)&w, sizeof(double) * n, st));
     FEM_HIP(hipMemsetAsync(sv, 0, sizeof(double) * (ent > 0 ? ent : 1), st));
     FEM_HIP(hipMemsetAsync(ovf, 0, sizeof(int32_t), st));
     if ((rc = fem_sell_fill(rowptr, colidx, n, slice_ptr, cols, csr2sell, stream))) return rc;

@@ -1041,7 +1041,7 @@ int fem_incidence_checked(const int64_t* conn, int64_t M, int npe, int64_t N, in
     const size_t tb = inc_sort_temp_bytes(total, bits);
     char* base = reinterpret_cast<char*>(work);
     const bool own = base == nullptr;   // no caller workspace: stream-ordered allocation
-    if (own) FEM_HIP(hipMallocAsync((void**)&base, (size_t)fem_incidence_work_bytes(total, N), st));
+    if (own) FEM_HIP(::fem::malloc_async((void**)&base, (size_t)fem_incidence_work_bytes(total, N), st));
     if (getenv("FEM355_INC_RADIX") == nullptr && inb_shift(N) <= INB_MAXSH) {
         const int rc = incidence_bucket(conn, total, N, inc_ptr, inc, base, bad, stream);
         if (own) FEM_HIP(hipFreeAsync(base, st));
@@ -1180,7 +1180,7 @@ int fem_graph_sell_fill_sl(const int64_t* conn, int npe, const int32_t* inc_ptr,
     const int64_t ns = cdiv(N, 64);
     // per-slice owner spans (stream-ordered scratch), reduced into the G windows after the fill pass
     int2* span = nullptr;
-    if (G > 0) FEM_HIP(hipMallocAsync((void**)&span, sizeof(int2) * (size_t)ns, st));
+    if (G > 0) FEM_HIP(::fem::stream_scratch((void**)&span, sizeof(int2) * (size_t)ns, st));
     hipLaunchKernelGGL(k_sell_fill_graph, dim3((unsigned)std::min<int64_t>(cdiv(ns, 4), 16384)), dim3(256), 0, st,
                        rowptr, tmp, defer_flags(tmp, N), N, ns, slice_ptr, colidx, diagpos, cols, dcols,
                        (int64_t*)nullptr, (int32_t*)nullptr, pcols, ucol, uoff, G, win, span);
@@ -1189,7 +1189,6 @@ int fem_graph_sell_fill_sl(const int64_t* conn, int npe, const int32_t* inc_ptr,
         hipLaunchKernelGGL(k_win_from_spans, dim3((unsigned)cdiv((int64_t)G * 64, 256)), dim3(256), 0, st, G, ns,
                            (const int2*)span, win);
         FEM_LAUNCHED();
-        FEM_HIP(hipFreeAsync(span, st));
     }
     return FEM_OK;
 }

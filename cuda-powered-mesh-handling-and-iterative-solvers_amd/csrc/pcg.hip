@@ -2725,7 +2725,7 @@ static int make_constraints(const char* fn, int64_t n, hipStream_t stream, int o
         return FEM_EARG;
     }
     int* bad = nullptr;
-    FEM_HIP(hipMallocAsync((void**)&bad, sizeof(int) * 2, stream));
+    FEM_HIP(::fem::malloc_async((void**)&bad, sizeof(int) * 2, stream));
     FEM_HIP(hipMemsetAsync(bad, 0, sizeof(int) * 2, stream));
     auto chk = [&](const int64_t* v, int64_t m) {
         if (m > 0)
@@ -2807,7 +2807,7 @@ int fem_enforce_constraints(double* x, double* r, int64_t n, int order, int64_t 
     const int rc = make_constraints("fem_enforce_constraints", n, st, order, R, rbe2_slave, rbe2_master, S, spc_dof,
                                     spc_val, G, r3_ptr, r3_master, r3_wsum, r3_slave, r3_w, &c);
     if (rc != FEM_OK) return rc;
-    if (R > 0) FEM_HIP(hipMallocAsync((void**)&c.tmp, sizeof(double) * (size_t)R, st));
+    if (R > 0) FEM_HIP(::fem::malloc_async((void**)&c.tmp, sizeof(double) * (size_t)R, st));
     const int lrc = launch_constraints(st, x, r, c, nullptr, 1);
     if (lrc != FEM_OK) return lrc;
     if (c.tmp) FEM_HIP(hipFreeAsync(c.tmp, st));
@@ -3015,7 +3015,7 @@ int fem_sell_sl_pattern(int64_t nrows, const int64_t* slice_ptr, const int16_t* 
     if (ns <= 0) return FEM_OK;
     hipStream_t st = S(stream);
     int2* span = nullptr;   // per-slice owner spans, reduced into the windows (sl_pattern_slice, k_win_from_spans)
-    if (G > 0) FEM_HIP(hipMallocAsync((void**)&span, sizeof(int2) * (size_t)ns, st));
+    if (G > 0) FEM_HIP(::fem::stream_scratch((void**)&span, sizeof(int2) * (size_t)ns, st));
     hipLaunchKernelGGL(k_sell_sl_pattern, dim3((unsigned)cdiv(ns, 4)), dim3(256), 0, st, ns, nrows, slice_ptr,
                        dcols, pcols, ucol, uoff, G > 0 ? G : 0, win, span);
     FEM_LAUNCHED();
@@ -3023,7 +3023,6 @@ int fem_sell_sl_pattern(int64_t nrows, const int64_t* slice_ptr, const int16_t* 
         hipLaunchKernelGGL(k_win_from_spans, dim3((unsigned)cdiv((int64_t)G * 64, 256)), dim3(256), 0, st, G, ns,
                            (const int2*)span, win);
         FEM_LAUNCHED();
-        FEM_HIP(hipFreeAsync(span, st));
     }
     return FEM_OK;
 }

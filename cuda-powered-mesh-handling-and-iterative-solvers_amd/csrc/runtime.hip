@@ -1,6 +1,10 @@
 // Error plumbing, version, and device-wide exclusive scans (pattern build / SELL slice offsets).
 #include <stdarg.h>
 
+#include <atomic>
+#include <mutex>
+#include <vector>
+
 #include "common.hpp"
 
 namespace fem {
@@ -11,6 +15,55 @@ void set_error(const char* fmt, ...) {
     va_start(ap, fmt);
     vsnprintf(g_err, sizeof(g_err), fmt, ap);
     va_end(ap);
+}
+
+hipError_t malloc_async(void** p, size_t bytes, hipStream_t st) {
+    static std::atomic<uint64_t> kept{0};   // devices whose default pool keeps its memory
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64 && !((kept.load() >> dev) & 1)) {
+        hipMemPool_t pool;
+        if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+            uint64_t keep_all = UINT64_MAX;
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep_all);
+        }
+        kept.fetch_or(1ull << dev);
+    }
+    return hipMallocAsync(p, bytes, st);
+}
+
+hipError_t stream_scratch(void** p, size_t bytes, hipStream_t st) {
+    struct Entry {
+        hipStream_t st;
+        int dev;
+        void* ptr;
+        size_t bytes;
+    };
+    static std::mutex mu;
+    static std::vector<Entry> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    std::lock_guard<std::mutex> lk(mu);
+    for (Entry& e : cache) {
+        if (e.st != st || e.dev != dev) continue;
+        if (e.bytes >= bytes) {
+            *p = e.ptr;
+            return hipSuccess;
+        }
+        (void)hipFreeAsync(e.ptr, st);   // stream-ordered: earlier work on st that used it runs first
+        e.ptr = nullptr;
+        e.bytes = 0;
+        const hipError_t rc = malloc_async(&e.ptr, bytes, st);
+        if (rc != hipSuccess) return rc;
+        e.bytes = bytes;
+        *p = e.ptr;
+        return hipSuccess;
+    }
+    Entry e{st, dev, nullptr, bytes};
+    const hipError_t rc = malloc_async(&e.ptr, bytes, st);
+    if (rc != hipSuccess) return rc;
+    cache.push_back(e);
+    *p = e.ptr;
+    return hipSuccess;
 }
 
 // ---------------------------------------------------------------- 3-phase exclusive scan

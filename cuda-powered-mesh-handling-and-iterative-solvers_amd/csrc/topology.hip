@@ -92,7 +92,7 @@ static int scan_flags(const int32_t* flags, int64_t* out, int64_t n, hipStream_t
     size_t tb = 0;
     FEM_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, flags, out, (int)n, st));
     void* tmp = nullptr;
-    FEM_HIP(hipMallocAsync(&tmp, tb, st));
+    FEM_HIP(::fem::malloc_async(&tmp, tb, st));
     FEM_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, flags, out, (int)n, st));
     FEM_HIP(hipFreeAsync(tmp, st));
     return FEM_OK;
@@ -356,7 +356,7 @@ int fem_topo_create(const int64_t* conn, int64_t M, int npe, const int32_t* ftab
         if (hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kout, vin, vout, (int)nf, 0, end_bit, st))
             return FEM_EHIP;
         void* tmp = nullptr;
-        if (hipMallocAsync(&tmp, tb, st)) return FEM_EHIP;
+        if (::fem::malloc_async(&tmp, tb, st)) return FEM_EHIP;
         if (hipcub::DeviceRadixSort::SortPairs(tmp, tb, kin, kout, vin, vout, (int)nf, 0, end_bit, st))
             return FEM_EHIP;
         (void)hipFreeAsync(tmp, st);
@@ -458,8 +458,8 @@ int fem_topo_boundary(fem_topo* t, const int64_t* conn, int Fs, const int32_t* s
     if (n == 0) return FEM_OK;
     int32_t* flag = nullptr;
     int64_t* pos = nullptr;
-    FEM_HIP(hipMallocAsync((void**)&flag, 4 * n, t->stream));
-    FEM_HIP(hipMallocAsync((void**)&pos, 8 * n, t->stream));
+    FEM_HIP(::fem::malloc_async((void**)&flag, 4 * n, t->stream));
+    FEM_HIP(::fem::malloc_async((void**)&pos, 8 * n, t->stream));
     const dim3 g(stream_grid(n, 256)), b(256);
     hipLaunchKernelGGL(k_boundary_flags, g, b, 0, t->stream, t->mult, t->M, t->F, Fs, sm, flag);
     int rc = FEM_OK;
