@@ -58,6 +58,12 @@ hipError_t stream_scratch(void** p, size_t bytes, hipStream_t st) {
         *p = e.ptr;
         return hipSuccess;
     }
+    // a process that keeps creating streams: at most 8 kept buffers, the oldest released (hipFree waits for the
+    // device, which only a ninth stream's first call pays)
+    if (cache.size() >= 8) {
+        if (cache.front().ptr) (void)hipFree(cache.front().ptr);
+        cache.erase(cache.begin());
+    }
     Entry e{st, dev, nullptr, bytes};
     const hipError_t rc = malloc_async(&e.ptr, bytes, st);
     if (rc != hipSuccess) return rc;

@@ -1370,3 +1370,28 @@ def test_gather_windows_from_slice_spans(gpu, case, monkeypatch):
     want = _windows_restated(gf, a.G)
     assert torch.equal(a.win.cpu()[: 2 * a.G], want)
     assert torch.equal(b.win.cpu()[: 2 * b.G], want)
+
+
+def test_span_scratch_across_streams(gpu):
+    """The slice spans live in a per-stream scratch kept between calls (runtime.hip stream_scratch, at most 8 kept):
+    the solver layout built on twelve streams in turn -- the first streams' buffers evicted, a larger mesh growing a
+    stream's buffer -- gives the windows and paired deltas of the first build, exactly."""
+    _, mesh, _, system = _mods()
+    ref = {}
+    for n in (9, 13):
+        c, t = mesh.kuhn_cube(n, jitter=0.1)
+        tg, N = t.to(gpu), c.shape[0]
+        g = system.build_graph(tg, N, solver_layout=True)
+        sl = g.solver_layout()
+        torch.cuda.synchronize()
+        ref[n] = (tg, N, sl.win.cpu(), sl.pcols.cpu(), sl.uoff.cpu())
+    streams = [torch.cuda.Stream(device=gpu) for _ in range(12)]
+    for k, s in enumerate(streams):
+        n = 9 if k % 3 else 13
+        tg, N, win, pcols, uoff = ref[n]
+        with torch.cuda.stream(s):
+            g = system.build_graph(tg, N, solver_layout=True)
+            sl = g.solver_layout()
+        s.synchronize()
+        assert torch.equal(sl.win.cpu(), win) and torch.equal(sl.pcols.cpu(), pcols), (k, n)
+        assert torch.equal(sl.uoff.cpu(), uoff), (k, n)
