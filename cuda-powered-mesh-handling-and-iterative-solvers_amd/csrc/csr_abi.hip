@@ -223,15 +223,15 @@ int fem_solid_ke(int type, const double* coords, const int64_t* conn, int64_t M,
         set_error("fem_solid_ke: integration points / weights required");
         return FEM_EARG;
     }
+    // the shape-function table in the stream's kept scratch: a hipFreeAsync here would hold the host until the
+    // K_e kernel finished (runtime.hip stream_scratch)
     double* dN = nullptr;
-    FEM_HIP(::fem::malloc_async((void**)&dN, sizeof(double) * n_ip * npe * 3, st));
+    FEM_HIP(::fem::stream_scratch((void**)&dN, sizeof(double) * n_ip * npe * 3, st));
     hipLaunchKernelGGL(k_dn_table, dim3(cdiv(n_ip, 64)), dim3(64), 0, st, npe, ip, n_ip, dN);
     FEM_LAUNCHED();
     // single=False: per-point stack for c3d8 / c3d10 (Q6); c3d6's flag only selects the one-point rule
     const int mode = (single || npe == 6) ? FEM_ISO_SUM : FEM_ISO_STACK;
-    const int rc = fem_iso_ke(coords, conn, M, npe, E, nu, dN, w, n_ip, mode, Ke, stream);
-    (void)hipFreeAsync(dN, st);
-    return rc;
+    return fem_iso_ke(coords, conn, M, npe, E, nu, dN, w, n_ip, mode, Ke, stream);
 }
 
 int fem_csr_pattern(const int64_t* conn, int64_t M, int npe, int dofs_per_node, int64_t n_nodes, int32_t* rowptr,
