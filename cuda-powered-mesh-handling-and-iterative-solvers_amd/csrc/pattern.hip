@@ -754,16 +754,8 @@ __global__ void __launch_bounds__(256) k_sell_fill(const int32_t* __restrict__ r
         }
         const int pad = (r < nrows) ? (int)r : (int)(nrows - 1);   // near the row: 16-bit deltas stay small
         for (int k = 0; k < w; ++k) cols[e0 + (int64_t)k * 64 + lane] = (k < len) ? colidx[rp + k] : pad;
-        const int p0 = rp_s[wid][0], p1 = rp_s[wid][64];
-        for (int p = p0 + lane; p < p1; p += 64) {
-            int lo = 0, hi = 64;   // last row l with rp_s[l] <= p
-            while (hi - lo > 1) {
-                const int mid = (lo + hi) >> 1;
-                if (rp_s[wid][mid] <= p) lo = mid;
-                else hi = mid;
-            }
-            csr2sell[p] = e0 + (int64_t)(p - rp_s[wid][lo]) * 64 + lo;
-        }
+        // csr2sell row-wise: the row's lane stores its run (the wave's runs tile the slice's CSR segment)
+        for (int k = 0; k < len; ++k) csr2sell[rp + k] = e0 + (int64_t)k * 64 + lane;
         __builtin_amdgcn_wave_barrier();
     }
 }
@@ -868,11 +860,15 @@ __global__ void __launch_bounds__(256) k_sell_fill_graph(const int32_t* __restri
 #ifndef FEM_FILL_ROWWISE
 #define FEM_FILL_ROWWISE 1   // 10M Poisson fill pass 242 -> 188 us (0: the binary search per entry, A/B)
 #endif
-        if (FEM_FILL_ROWWISE && !csr2sell) {
-            // CSR colidx row-wise: the lane of a row stores its own contiguous run (the wave's runs tile one
-            // contiguous block) -- no binary search of the row per entry
-            if (r < nrows && !dfr)
-                for (int k = 0; k < len; ++k) colidx[rp + k] = rows[lane * TS + k];
+        if (FEM_FILL_ROWWISE) {
+            // CSR colidx (and csr2sell) row-wise: the lane of a row stores its own contiguous run (the wave's runs
+            // tile one contiguous block) -- no binary search of the row per entry
+            if (r < nrows) {
+                if (!dfr)
+                    for (int k = 0; k < len; ++k) colidx[rp + k] = rows[lane * TS + k];
+                if (csr2sell)
+                    for (int k = 0; k < len; ++k) csr2sell[rp + k] = e0 + (int64_t)k * 64 + lane;
+            }
             __builtin_amdgcn_wave_barrier();
             continue;
         }
@@ -906,15 +902,9 @@ __global__ void __launch_bounds__(256) k_sell_csr2sell(const int32_t* __restrict
         rp_s[wid][lane] = rowptr[min(r, rlast)];
         if (lane == 0) rp_s[wid][64] = rowptr[rlast];
         __builtin_amdgcn_wave_barrier();
-        const int p0 = rp_s[wid][0], p1 = rp_s[wid][64];
-        for (int p = p0 + lane; p < p1; p += 64) {
-            int lo = 0, hi = 64;
-            while (hi - lo > 1) {
-                const int mid = (lo + hi) >> 1;
-                if (rp_s[wid][mid] <= p) lo = mid;
-                else hi = mid;
-            }
-            csr2sell[p] = e0 + (int64_t)(p - rp_s[wid][lo]) * 64 + lo;
+        if (r < nrows) {   // row-wise: the row's lane stores its run (the wave's runs tile the slice's segment)
+            const int rp = rp_s[wid][lane], len = rp_s[wid][lane + 1] - rp;
+            for (int k = 0; k < len; ++k) csr2sell[rp + k] = e0 + (int64_t)k * 64 + lane;
         }
         __builtin_amdgcn_wave_barrier();
     }
