@@ -719,13 +719,18 @@ __global__ void __launch_bounds__(GB_T) k_inc_big(const int32_t* __restrict__ in
 }
 
 // ---------------------------------------------------------------- SELL-64
-__global__ void k_sell_widths(const int32_t* __restrict__ rowptr, int64_t nrows, int64_t nslices,
-                              int64_t* __restrict__ width) {
-    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nslices; s += (int64_t)gridDim.x * blockDim.x) {
-        int w = 0;
-        int64_t r0 = s * 64, r1 = min(r0 + 64, nrows);
-        for (int64_t r = r0; r < r1; ++r) w = max(w, rowptr[r + 1] - rowptr[r]);
-        width[s] = (int64_t)w * 64;
+// wave per slice, lane = row (coalesced row pointers, one shuffle reduction) -- a thread per slice walked its 64 rows
+// one dependent load at a time on 1 / 64 of the threads
+__global__ void __launch_bounds__(256) k_sell_widths(const int32_t* __restrict__ rowptr, int64_t nrows,
+                                                     int64_t nslices, int64_t* __restrict__ width) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t s = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; s < nslices;
+         s += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+        const int64_t r = s * 64 + lane;
+        int w = r < nrows ? rowptr[r + 1] - rowptr[r] : 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) w = max(w, __shfl_xor(w, o, 64));
+        if (lane == 0) width[s] = (int64_t)w * 64;
     }
 }
 
@@ -1221,14 +1226,26 @@ int fem_sell_csr2sell(const int32_t* rowptr, int64_t nrows, const int64_t* slice
 }
 
 // the pattern's sizes in one launch (one block): {nnz = rowptr[N], entries = slice_ptr[ns], *bad, *ovf, widest slice}
-__global__ void __launch_bounds__(256) k_graph_sizes(const int32_t* __restrict__ rowptr,
-                                                     const int64_t* __restrict__ slice_ptr,
-                                                     const int64_t* __restrict__ width, int64_t N, int64_t ns,
-                                                     const int32_t* __restrict__ bad, const int32_t* __restrict__ ovf,
-                                                     int64_t* __restrict__ out) {
-    __shared__ int64_t m_s[4];
+// (1024 threads, eight width loads in flight per thread: the 256-thread loop of one dependent load per step took
+// 28 us at 10M -- on the critical path, right before the build's one read-back)
+constexpr int GS_T = 1024;
+__global__ void __launch_bounds__(GS_T) k_graph_sizes(const int32_t* __restrict__ rowptr,
+                                                      const int64_t* __restrict__ slice_ptr,
+                                                      const int64_t* __restrict__ width, int64_t N, int64_t ns,
+                                                      const int32_t* __restrict__ bad, const int32_t* __restrict__ ovf,
+                                                      int64_t* __restrict__ out) {
+    __shared__ int64_t m_s[GS_T / 64];
     int64_t m = 0;
-    for (int64_t s = threadIdx.x; s < ns; s += 256) m = width[s] > m ? width[s] : m;
+    constexpr int U = 8;
+    int64_t s = threadIdx.x;
+    for (; s + (U - 1) * GS_T < ns; s += U * GS_T) {
+        int64_t v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = width[s + u * GS_T];
+#pragma unroll
+        for (int u = 0; u < U; ++u) m = v[u] > m ? v[u] : m;
+    }
+    for (; s < ns; s += GS_T) m = width[s] > m ? width[s] : m;
     for (int o = 32; o > 0; o >>= 1) {
         const int64_t v = __shfl_xor(m, o, 64);
         m = v > m ? v : m;
@@ -1237,7 +1254,7 @@ __global__ void __launch_bounds__(256) k_graph_sizes(const int32_t* __restrict__
     __syncthreads();
     if (threadIdx.x == 0) {
         int64_t w = m_s[0];
-        for (int i = 1; i < 4; ++i) w = m_s[i] > w ? m_s[i] : w;
+        for (int i = 1; i < GS_T / 64; ++i) w = m_s[i] > w ? m_s[i] : w;
         out[0] = rowptr[N];
         out[1] = slice_ptr[ns];
         out[2] = bad ? *bad : 0;
@@ -1252,15 +1269,16 @@ int fem_graph_sizes(const int32_t* rowptr, const int64_t* slice_ptr, const int64
         set_error("fem_graph_sizes: rowptr, slice_ptr, out5 (and width for N > 0) are required");
         return FEM_EARG;
     }
-    hipLaunchKernelGGL(k_graph_sizes, dim3(1), dim3(256), 0, S(stream), rowptr, slice_ptr, width, N, cdiv(N, 64), bad,
-                       ovf, out5);
+    hipLaunchKernelGGL(k_graph_sizes, dim3(1), dim3(GS_T), 0, S(stream), rowptr, slice_ptr, width, N, cdiv(N, 64),
+                       bad, ovf, out5);
     FEM_LAUNCHED();
     return FEM_OK;
 }
 
 int fem_sell_widths(const int32_t* rowptr, int64_t nrows, int64_t* width, fem_stream_t stream) {
     int64_t ns = cdiv(nrows, 64);
-    hipLaunchKernelGGL(k_sell_widths, dim3(stream_grid(ns, 256)), dim3(256), 0, S(stream), rowptr, nrows, ns, width);
+    hipLaunchKernelGGL(k_sell_widths, dim3(stream_grid(ns * 64, 256)), dim3(256), 0, S(stream), rowptr, nrows, ns,
+                       width);
     FEM_LAUNCHED();
     return FEM_OK;
 }

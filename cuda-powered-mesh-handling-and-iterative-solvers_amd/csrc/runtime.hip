@@ -80,20 +80,27 @@ constexpr int SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
 
 template <typename T>
 __device__ __forceinline__ T block_exclusive_scan(T v, T* lds, T* total) {
-    // Hillis-Steele over 256 threads in LDS (setup-path kernel; simplicity over speed)
-    const int t = threadIdx.x;
-    lds[t] = v;
-    __syncthreads();
-    for (int o = 1; o < SCAN_BLOCK; o <<= 1) {
-        T add = (t >= o) ? lds[t - o] : T(0);
-        __syncthreads();
-        lds[t] += add;
-        __syncthreads();
+    // wave scans by shuffles, then the four wave totals through LDS: two barriers (the Hillis-Steele form over 256
+    // threads in LDS took sixteen, and the three scan kernels of the 10M pattern build ~90 us)
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    T x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const T y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
     }
-    T incl = lds[t];
-    *total = lds[SCAN_BLOCK - 1];
+    if (lane == 63) lds[wid] = x;
     __syncthreads();
-    return incl - v;
+    T off = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < SCAN_BLOCK / 64; ++w) {
+        const T t = lds[w];
+        off += w < wid ? t : T(0);
+        tot += t;
+    }
+    *total = tot;
+    __syncthreads();   // lds is reused by the caller's next scan
+    return off + x - v;
 }
 
 template <typename T>
@@ -133,19 +140,50 @@ __global__ void __launch_bounds__(SCAN_BLOCK) k_tile_scan(const T* __restrict__ 
     int64_t base = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_ITEMS;
     T v[SCAN_ITEMS];
     T s = 0;
+    // a thread's eight consecutive items as 16-byte vector accesses where aligned and whole (int32: two per thread
+    // instead of eight 4-byte accesses 32 bytes apart across the wave)
+    constexpr bool VEC = sizeof(T) == 4;
+    const bool vec = VEC && base + SCAN_ITEMS <= n && ((reinterpret_cast<uintptr_t>(in + base) |
+                                                        reinterpret_cast<uintptr_t>(out + base)) & 15) == 0;
+    if (vec) {
+        const int4* p4 = reinterpret_cast<const int4*>(in + base);
 #pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
-        int64_t i = base + k;
-        v[k] = (i < n) ? in[i] : T(0);
-        s += v[k];
+        for (int h = 0; h < SCAN_ITEMS / 4; ++h) {
+            const int4 q = p4[h];
+            v[4 * h] = (T)q.x;
+            v[4 * h + 1] = (T)q.y;
+            v[4 * h + 2] = (T)q.z;
+            v[4 * h + 3] = (T)q.w;
+        }
+#pragma unroll
+        for (int k = 0; k < SCAN_ITEMS; ++k) s += v[k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < SCAN_ITEMS; ++k) {
+            int64_t i = base + k;
+            v[k] = (i < n) ? in[i] : T(0);
+            s += v[k];
+        }
     }
     T tot;
     T ex = block_exclusive_scan<T>(s, lds, &tot) + sums[blockIdx.x];
+    if (vec) {
+        int o[SCAN_ITEMS];
 #pragma unroll
-    for (int k = 0; k < SCAN_ITEMS; ++k) {
-        int64_t i = base + k;
-        if (i < n) out[i] = ex;
-        ex += v[k];
+        for (int k = 0; k < SCAN_ITEMS; ++k) {
+            o[k] = (int)ex;
+            ex += v[k];
+        }
+        int4* q4 = reinterpret_cast<int4*>(out + base);
+#pragma unroll
+        for (int h = 0; h < SCAN_ITEMS / 4; ++h) q4[h] = make_int4(o[4 * h], o[4 * h + 1], o[4 * h + 2], o[4 * h + 3]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < SCAN_ITEMS; ++k) {
+            int64_t i = base + k;
+            if (i < n) out[i] = ex;
+            ex += v[k];
+        }
     }
     if (blockIdx.x == ntiles - 1 && threadIdx.x == 0) out[n] = sums[ntiles];
 }
