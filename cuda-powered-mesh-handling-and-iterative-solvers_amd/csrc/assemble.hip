@@ -1886,7 +1886,13 @@ __global__ void k_jacobi_sl(const double* __restrict__ svals, const int32_t* __r
                             const int32_t* __restrict__ diagpos, const int64_t* __restrict__ slice_ptr,
                             const int32_t* __restrict__ uoff, const int16_t* __restrict__ ucol, int64_t nrows,
                             const uint8_t* __restrict__ mask, double* __restrict__ w) {
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nrows * BS; t += (int64_t)gridDim.x * blockDim.x) {
+    // wave-uniform trip count (the ballot below needs every lane): lanes past the end work on the last dof, unstored
+    const int64_t nd = nrows * BS;
+    for (int64_t t0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); t0 < nd;
+         t0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t tl = t0 + (threadIdx.x & 63);
+        const bool act = tl < nd;
+        const int64_t t = act ? tl : nd - 1;
         const int64_t i = t / BS;
         const int r = (int)(t - i * BS);
         const int64_t s = i >> 6;
@@ -1896,16 +1902,21 @@ __global__ void k_jacobi_sl(const double* __restrict__ svals, const int32_t* __r
         const int32_t dp = diagpos[i];
         const int uo = BS == 1 ? uoff[s] : -1;
         int k = -1;
-        if (dp >= 0) {
-            if (uo >= 0) {
-                for (int u = 0; u < wd; ++u)
-                    if (ucol[uo + u] == 0) {
-                        k = u;
-                        break;
-                    }
-            } else {
-                k = dp - rowptr[i];
+        if (BS == 1 && uo >= 0) {
+            // slice-uniform: the wave's 64 rows are this slice (the grid stride is a multiple of 64), so the list
+            // position of delta 0 is found by one compare per lane and a ballot -- not a walk of dependent loads
+            const int lane = threadIdx.x & 63;
+            for (int u0 = 0; u0 < wd; u0 += 64) {
+                const bool z = u0 + lane < wd && ucol[uo + u0 + lane] == 0;
+                const unsigned long long m = __ballot(z);
+                if (m) {
+                    k = u0 + __ffsll((long long)m) - 1;
+                    break;
+                }
             }
+            if (dp < 0) k = -1;
+        } else if (dp >= 0) {
+            k = dp - rowptr[i];
         }
         const double dg = k < 0 ? 0.0
                           : BS == 1 ? svals[p0 + pair_pos(k, wd, l)]
@@ -1914,7 +1925,7 @@ __global__ void k_jacobi_sl(const double* __restrict__ svals, const int32_t* __r
         double v = 1.0 / dg;
         if (v == INFINITY) v = 0.0;  // `solver/solver.py:831` (only +inf)
         if (mask && mask[i_]) v = 0.0;
-        w[i_] = v;
+        if (act) w[i_] = v;
     }
 }
 
