@@ -294,6 +294,11 @@ constexpr int G_TCAP = 32;      // rows of at most this many neighbours are prod
 // and rank-sorted, written to tmp[node * G_TCAP + rank] with row_len[node]. Rows with more than G_SCAP candidates or
 // G_TCAP neighbours get tmp[node * G_TCAP] = -1 and are left to k_graph (count and fill passes skip the rest).
 constexpr int G_HT = 512;
+// tmp's deferral flags are followed by one int: the number of rows k_graph_small deferred (0: the deferred-row
+// kernels return at once; zeroed by fem_graph_count2)
+__device__ __forceinline__ int32_t* ndefer_out(uint8_t* defer, int64_t N) {
+    return reinterpret_cast<int32_t*>(defer) + (N + 3) / 4;
+}
 #ifndef FEM_GRAPH_LPN
 #define FEM_GRAPH_LPN 32   // k_graph_small lanes per node (two rows per wave)
 #endif
@@ -335,7 +340,10 @@ __global__ void __launch_bounds__(256) k_graph_small(const int64_t* __restrict__
         const int C = (inc_ptr[node + 1] - start) * npe;
         int32_t* trow = tmp + node * G_TCAP;
         if (C > SCAP) {
-            if (sl == 0) defer[node] = 1;
+            if (sl == 0) {
+                defer[node] = 1;
+                atomicAdd(ndefer_out(defer, N), 1);
+            }
             continue;
         }
         // the row's own node is in every incidence: it is left out of the hash (a quarter of the P1 inserts) and
@@ -414,7 +422,10 @@ __global__ void __launch_bounds__(256) k_graph_small(const int64_t* __restrict__
         }
         __builtin_amdgcn_wave_barrier();
         if (U > G_TCAP || U > LPN) {
-            if (sl == 0) defer[node] = 1;
+            if (sl == 0) {
+                defer[node] = 1;
+                atomicAdd(ndefer_out(defer, N), 1);
+            }
             continue;
         }
         bool f = false;   // a neighbour farther than 16-bit deltas reach (the SELL keeps int32 columns then)
@@ -466,7 +477,8 @@ __global__ void __launch_bounds__(256) k_graph(const int64_t* __restrict__ conn,
                                                int64_t N, int32_t* __restrict__ row_len,
                                                const int32_t* __restrict__ rowptr, int32_t* __restrict__ colidx,
                                                int32_t* __restrict__ diagpos, const uint8_t* __restrict__ defer,
-                                               int32_t* __restrict__ far) {
+                                               int32_t* __restrict__ far, const int32_t* __restrict__ ndefer = nullptr) {
+    if (ndefer && *ndefer == 0) return;   // k_graph_small deferred no row: nothing to do here
     __shared__ int ht[G_WAVES][G_HT2];
     __shared__ int uniq[G_WAVES][G_UCAP];
     __shared__ int cnt_s[G_WAVES];
@@ -667,7 +679,9 @@ __global__ void __launch_bounds__(GB_T) k_graph_big(const int64_t* __restrict__ 
                                                     const int32_t* __restrict__ inc, int64_t N,
                                                     int32_t* __restrict__ row_len, const int32_t* __restrict__ rowptr,
                                                     int32_t* __restrict__ colidx, int32_t* __restrict__ diagpos,
-                                                    int32_t* __restrict__ far) {
+                                                    int32_t* __restrict__ far,
+                                                    const int32_t* __restrict__ ndefer = nullptr) {
+    if (ndefer && *ndefer == 0) return;   // only k_graph_small's deferred rows can be this long
     extern __shared__ uint32_t bm[];               // [GB_WORDS]
     __shared__ int rows_s[GB_T];
     __shared__ int nrows_s, lo_s, hi_s;
@@ -1083,24 +1097,26 @@ static int graph_grid(int64_t N) {
 // row has a neighbour farther than 32767 rows (the SELL pattern then keeps int32 columns).
 static int graph_count(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
                        int32_t* row_len, const uint8_t* defer, int32_t* overflow, hipStream_t st) {
+    const int32_t* nd = defer ? reinterpret_cast<const int32_t*>(defer) + (N + 3) / 4 : nullptr;
     hipLaunchKernelGGL(k_graph<false>, dim3(graph_grid(N)), dim3(256), 0, st, conn, npe, inc_ptr, inc, N, row_len,
-                       (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, defer, overflow);
+                       (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, defer, overflow, nd);
     FEM_LAUNCHED();
     if (const int rc = big_lds_attr()) return rc;
     hipLaunchKernelGGL(k_graph_big<false>, dim3(big_grid(N)), dim3(GB_T), GB_LDS, st, conn, npe, inc_ptr, inc, N, row_len,
-                       (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, overflow);
+                       (const int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, overflow, nd);
     FEM_LAUNCHED();
     return FEM_OK;
 }
 
 static int graph_fill(const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc, int64_t N,
                       const int32_t* rowptr, int32_t* colidx, int32_t* diagpos, const uint8_t* defer, hipStream_t st) {
+    const int32_t* nd = defer ? reinterpret_cast<const int32_t*>(defer) + (N + 3) / 4 : nullptr;
     hipLaunchKernelGGL(k_graph<true>, dim3(graph_grid(N)), dim3(256), 0, st, conn, npe, inc_ptr, inc, N,
-                       (int32_t*)nullptr, rowptr, colidx, diagpos, defer, (int32_t*)nullptr);
+                       (int32_t*)nullptr, rowptr, colidx, diagpos, defer, (int32_t*)nullptr, nd);
     FEM_LAUNCHED();
     if (const int rc = big_lds_attr()) return rc;
     hipLaunchKernelGGL(k_graph_big<true>, dim3(big_grid(N)), dim3(GB_T), GB_LDS, st, conn, npe, inc_ptr, inc, N,
-                       (int32_t*)nullptr, rowptr, colidx, diagpos, (int32_t*)nullptr);
+                       (int32_t*)nullptr, rowptr, colidx, diagpos, (int32_t*)nullptr, nd);
     FEM_LAUNCHED();
     return FEM_OK;
 }
@@ -1112,8 +1128,9 @@ int fem_graph_count(const int64_t* conn, int npe, const int32_t* inc_ptr, const 
     return graph_count(conn, npe, inc_ptr, inc, N, row_len, nullptr, overflow, S(stream));
 }
 
-// tmp: [N * G_TCAP] rows of k_graph_small, then N bytes of deferral flags (rows left to k_graph / k_graph_big)
-int64_t fem_graph_tmp_len(int64_t N) { return N * G_TCAP + (N + 3) / 4; }
+// tmp: [N * G_TCAP] rows of k_graph_small, then N bytes of deferral flags (rows left to k_graph / k_graph_big), then
+// the number of deferred rows
+int64_t fem_graph_tmp_len(int64_t N) { return N * G_TCAP + (N + 3) / 4 + 1; }
 static uint8_t* defer_flags(int32_t* tmp, int64_t N) { return reinterpret_cast<uint8_t*>(tmp + N * G_TCAP); }
 static const uint8_t* defer_flags(const int32_t* tmp, int64_t N) {
     return reinterpret_cast<const uint8_t*>(tmp + N * G_TCAP);
@@ -1124,6 +1141,7 @@ int fem_graph_count2(const int64_t* conn, int npe, const int32_t* inc_ptr, const
     if (overflow) FEM_HIP(hipMemsetAsync(overflow, 0, sizeof(int32_t), S(stream)));
     if (N <= 0) return FEM_OK;
     const int64_t grid = std::min<int64_t>(cdiv(N, G_WAVES), 16384);
+    FEM_HIP(hipMemsetAsync(tmp + N * G_TCAP + (N + 3) / 4, 0, sizeof(int32_t), S(stream)));   // deferred rows
     const bool al16 = (reinterpret_cast<uintptr_t>(conn) & 15) == 0;
 #define GS_LAUNCH(NPE_)                                                                                           \
     hipLaunchKernelGGL((k_graph_small<FEM_GRAPH_LPN, NPE_>), dim3((unsigned)grid), dim3(256), 0, S(stream), conn, \
