@@ -134,6 +134,7 @@ __global__ void __launch_bounds__(INB_T1) k_inc_l1(const int64_t* __restrict__ c
     if (!SCATTER) {
         __syncthreads();
         for (int q = threadIdx.x; q < nb; q += INB_T1) cnt[(int64_t)q * G + b] = hist[q];
+        if (b == 0 && threadIdx.x == 0) cnt[(int64_t)nb * G] = 0;   // the hub flag k_inc_l2 sets (k_inc_big's gate)
     }
 }
 
@@ -144,7 +145,7 @@ __global__ void __launch_bounds__(INB_T1) k_inc_l1(const int64_t* __restrict__ c
 __global__ void __launch_bounds__(256) k_inc_l2(const int2* __restrict__ kpair,
                                                 const int32_t* __restrict__ boff, int G, int64_t N, int bsh,
                                                 int32_t* __restrict__ scratch, int32_t* __restrict__ inc_ptr,
-                                                int32_t* __restrict__ inc) {
+                                                int32_t* __restrict__ inc, int32_t* __restrict__ hub) {
     extern __shared__ int lds[];
     const int B = 1 << bsh;
     int* cnt = lds;                 // [B] counts, then cursors
@@ -274,7 +275,10 @@ __global__ void __launch_bounds__(256) k_inc_l2(const int2* __restrict__ kpair,
             while (l + 1 < B && st[l + 1] <= p) ++l;   // empty segments share a start
             a = st[l];
             z = st[l + 1];
-            if (z - a > INC_BIG) continue;   // a hub's segment: k_inc_big sorts it (the rank sort is O(len^2))
+            if (z - a > INC_BIG) {   // a hub's segment: k_inc_big sorts it (the rank sort is O(len^2))
+                *hub = 1;
+                continue;
+            }
             int r = a;
             for (int u = a; u < z; ++u) r += (scratch[lo + u] < v);
             inc[lo + r] = v;
@@ -714,7 +718,9 @@ __global__ void __launch_bounds__(GB_T) k_graph_big(const int64_t* __restrict__ 
 // node segments of the incidence longer than INC_BIG (hub nodes; k_inc_l2 leaves them in arrival order in scratch):
 // ascending into inc by the bitmap sort (slots are distinct)
 __global__ void __launch_bounds__(GB_T) k_inc_big(const int32_t* __restrict__ inc_ptr, int64_t N,
-                                                  const int32_t* __restrict__ scratch, int32_t* __restrict__ inc) {
+                                                  const int32_t* __restrict__ scratch, int32_t* __restrict__ inc,
+                                                  const int32_t* __restrict__ hub) {
+    if (*hub == 0) return;   // k_inc_l2 met no hub segment
     extern __shared__ uint32_t bm[];
     __shared__ int rows_s[GB_T];
     __shared__ int nrows_s, lo_s, hi_s;
@@ -1032,11 +1038,12 @@ static int incidence_bucket(const int64_t* conn, int64_t total, int64_t N, int32
     const int B = 1 << bsh;
     const size_t l2 = sizeof(int) * (size_t)(2 * B + 1 + 2 * INB_CAP) + 2 * (size_t)INB_CAP;
     hipLaunchKernelGGL(k_inc_l2, dim3((unsigned)nb), dim3(256), l2, st, kpair, off, INB_G1, N, bsh, scratch,
-                       inc_ptr, inc);
+                       inc_ptr, inc, cnt + ncnt);
     FEM_LAUNCHED();
     if (total > INC_BIG) {   // hub segments (the launch finds them; for ordinary meshes it only reads inc_ptr)
         if (const int brc = big_lds_attr()) return brc;
-        hipLaunchKernelGGL(k_inc_big, dim3(big_grid(N)), dim3(GB_T), GB_LDS, st, inc_ptr, N, scratch, inc);
+        hipLaunchKernelGGL(k_inc_big, dim3(big_grid(N)), dim3(GB_T), GB_LDS, st, inc_ptr, N, scratch, inc,
+                           (const int32_t*)(cnt + ncnt));
         FEM_LAUNCHED();
     }
     return FEM_OK;
