@@ -19,8 +19,9 @@ import torch
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FEM355_LIB", os.path.join(PKG_DIR, "lib", "libfem355.so"))
 
-FEM_OK, FEM_EBADTYPE, FEM_ESINGULAR, FEM_EHIP, FEM_ERCCL, FEM_EARG = range(6)
-PCG_RUNNING, PCG_CONVERGED, PCG_MAXITER, PCG_BREAKDOWN, PCG_ALPHA_NAN, PCG_BETA_NAN, PCG_SYNC_TIMEOUT = range(7)
+FEM_OK, FEM_EBADTYPE, FEM_ESINGULAR, FEM_EHIP, FEM_ERCCL, FEM_EARG, FEM_ESTATE = range(7)
+(PCG_RUNNING, PCG_CONVERGED, PCG_MAXITER, PCG_BREAKDOWN, PCG_ALPHA_NAN, PCG_BETA_NAN, PCG_SYNC_TIMEOUT,
+ PCG_BAD_WINDOW) = range(8)
 MODE_CG_STABLE, MODE_PCG, MODE_CG_CONSTRAINED = 0, 1, 2
 # include/fem355.h FEM_TUNE_*: the library's default set for a new context, and the merged-update flag
 TUNE_UPD1 = 1024
@@ -114,6 +115,7 @@ SIGNATURES = {
     "fem_pcg_iterate": (_I, [_P, _I]),
     "fem_pcg_poll": (_I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_D)]),
     "fem_pcg_sync_site": (_I, [_P, ctypes.POINTER(_I)]),
+    "fem_pcg_debug_window": (_I, [_P, _I, _I, _I]),
     "fem_pcg_solve": (_I, [_P, _I, _I, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_D)]),
     "fem_pcg_use_graph": (_I, [_P, _I]),
     "fem_pcg_set_schedule": (_I, [_P, _I]),
@@ -135,6 +137,7 @@ SIGNATURES = {
     "fem_pcg_profile": (_I, [_P, _I, _I, ctypes.POINTER(_D), ctypes.POINTER(_I)]),
     "fem_pcg_destroy": (None, [_P]),
     "fem_pcg_release_cache": (_I, []),
+    "fem_release_scratch": (_I, []),
     "fem_pcg_set_rows": (_I, [_P, _I, _I, _P, _I]),
     "fem_pcg_comm_block": (_I, [_P, ctypes.POINTER(_P), ctypes.POINTER(_L)]),
     "fem_pcg_col_window": (_I, [_P, ctypes.POINTER(_L), ctypes.POINTER(_L)]),
@@ -297,8 +300,13 @@ def scope_module(namespace: dict):
 
 
 def release_cache() -> int:
-    """Free the solver buffers the library keeps for reuse (MB released)."""
-    return int(_lib.fem_pcg_release_cache()) if _lib is not None else 0
+    """Free the solver buffers the library keeps for reuse (MB released), and its per-stream scratch."""
+    if _lib is None:
+        return 0
+    mb = int(_lib.fem_pcg_release_cache())
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        _lib.fem_release_scratch()
+    return mb
 
 
 atexit.register(release_cache)

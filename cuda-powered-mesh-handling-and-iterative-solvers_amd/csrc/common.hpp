@@ -9,6 +9,19 @@
 
 namespace fem {
 
+constexpr unsigned PK_SITE_WINDOW = 4u;
+
+// a gather window [lo, hi] (lo > hi: empty) must lie inside the nflags u-flags. One that does not is an invariant
+// broken upstream (windows formed from the wrong pattern, or read before they were formed): the kernels then never
+// index past the flag array AND end the launch with FEM_PCG_BAD_WINDOW, which fem_pcg_poll turns into an error
+__device__ __forceinline__ bool pk_window_bad(int lo, int hi, int nflags) {
+    return lo <= hi && (lo < 0 || hi >= nflags);
+}
+// the launch's final status after a give-up: a bad window, or a synchronisation timeout (the site word tells)
+__device__ __forceinline__ int pk_fail_status(unsigned site) {
+    return (site & 15u) == PK_SITE_WINDOW ? FEM_PCG_BAD_WINDOW : FEM_PCG_SYNC_TIMEOUT;
+}
+
 constexpr int WAVE = 64;
 constexpr int NXCD = 8;
 
@@ -35,11 +48,13 @@ void set_error(const char* fmt, ...);
 
 inline hipStream_t S(fem_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
-// hipMallocAsync from the current device's default pool, whose release threshold is raised to "keep everything"
-// on first use (runtime.hip): with the default threshold of 0 every stream synchronisation hands the pool's memory
-// back, and the next stream-ordered allocation maps it again -- ~0.2 ms of host time per scratch allocation (the
-// 10M pattern fill's slice spans), on the critical path after the pattern's size read-back
+// stream-ordered allocation from the library's private pool of the current device (runtime.hip): it keeps up to
+// 256 MB of freed memory across synchronisations (with a threshold of 0 every synchronisation hands the memory back
+// and the next allocation maps it again -- ~0.2 ms of host time per scratch allocation on the 10M pattern fill's
+// critical path), and returns anything above that to the driver; the device's default pool is left untouched
 hipError_t malloc_async(void** p, size_t bytes, hipStream_t st);
+// free every kept per-stream scratch buffer and trim the private pools (fem_release_scratch)
+int release_scratch();
 // Stream-private scratch kept between calls (runtime.hip): `bytes` of device memory owned by stream st until a later
 // call on the same stream asks for more (then reallocated, stream-ordered). For per-call scratch on the critical path:
 // hipFreeAsync costs ~0.2 ms of host time here (measured on the 10M pattern fill, whose whole host call took 224 us

@@ -1501,8 +1501,14 @@ __global__ void __launch_bounds__(C1F_BLOCK) k_cg1_fused(Cg1FArgs a) {
     if (threadIdx.x == 0) __hip_atomic_store(a.flags + (size_t)L * 32, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // ---- wait for the u of the gather window
     if (wv == 0) {
-        const int wlo = max(a.win[L], 0), whi = min(a.win[G + L], G - 1);   // never outside the flag array
+        // never outside the flag array; a window outside it ends the solve with FEM_PCG_BAD_WINDOW (reported, not run)
+        const int wraw0 = a.win[L], wraw1 = a.win[G + L];
+        const int wlo = max(wraw0, 0), whi = min(wraw1, G - 1);
         bool ok = true;
+        if (pk_window_bad(wraw0, wraw1, G)) {
+            if (lane == 0) __hip_atomic_store(tmo, PK_SITE_WINDOW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = false;
+        }
         for (int b0 = wlo; b0 <= whi && ok; b0 += 64) {
             const int jw = b0 + lane;
             bool done = jw > whi;
@@ -1527,9 +1533,9 @@ __global__ void __launch_bounds__(C1F_BLOCK) k_cg1_fused(Cg1FArgs a) {
         }
     }
     __syncthreads();
-    if (!ok_lds) {   // a neighbour never arrived: end the solve (the reduction below is abandoned)
+    if (!ok_lds) {   // a neighbour never arrived (or a bad window): end the solve (the reduction is abandoned)
         if (threadIdx.x == 0) {
-            st->status = FEM_PCG_SYNC_TIMEOUT;
+            st->status = pk_fail_status(__hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
             st->halt = 1;
         }
         return;
@@ -1852,6 +1858,7 @@ struct fem_pcg {
     // element-chunk operator (fem_pcg_set_operator_mf): K1 = k_pcg_mf_dot + k_mf_gather instead of a SELL SpMV
     fem_mf* mf;
     double* mf_sl;  // this context's slot buffer [nslots * bs] (no other context or stream writes it)
+    int64_t mf_sl_cap;   // doubles mf_sl holds (a later operator with more slots reallocates it)
     int mf_qfuse;   // the merged update reads q from the slots (no gather launch); set per launch of K1 + update2
 };
 
@@ -2919,8 +2926,21 @@ int fem_pcg_set_operator_mf(fem_pcg* s, fem_mf* m) {
                   "schedule or a captured graph only");
         return FEM_EARG;
     }
-    if (!s->mf_sl && mf_nslots(m) > 0)   // the context's own slots: concurrent solves / applications never share them
-        FEM_HIP(hipMalloc(&s->mf_sl, sizeof(double) * (size_t)mf_bs(m) * (size_t)mf_nslots(m)));
+    if (s->dist && !s->cg1) {
+        set_error("fem_pcg_set_operator_mf: a distributed context runs the element-chunk operator in the "
+                  "single-reduction variant only (fem_pcg_set_dist_variant(s, 1))");
+        return FEM_EARG;
+    }
+    // the context's own slots (concurrent solves / applications never share them), sized for THIS operator: a second
+    // operator over the same nodes with more elements (more slots) gets a larger buffer, never the old one
+    const int64_t need = (int64_t)mf_bs(m) * (int64_t)mf_nslots(m);
+    if (need > s->mf_sl_cap) {
+        if (s->mf_sl) FEM_HIP(hipFree(s->mf_sl));
+        s->mf_sl = nullptr;
+        s->mf_sl_cap = 0;
+        FEM_HIP(hipMalloc(&s->mf_sl, sizeof(double) * (size_t)need));
+        s->mf_sl_cap = need;
+    }
     s->mf = m;
     s->fused = s->deferred = s->persist_req = s->persist_fit_only = s->persist = 0;
     s->cols16 = nullptr;
@@ -3492,6 +3512,11 @@ static int refresh_pairing(fem_pcg* s) {
 }
 
 int fem_pcg_start(fem_pcg* s) {
+    if (s->mf && s->dist && !s->cg1) {   // fem_pcg_set_dist resets the variant to 0: refuse at setup, not at phase 0
+        set_error("fem_pcg_start: a distributed element-chunk context needs the single-reduction variant "
+                  "(fem_pcg_set_dist_variant(s, 1))");
+        return FEM_EARG;
+    }
     {
         int prc = refresh_pairing(s);
         if (!prc) prc = persist_setup(s);
@@ -3669,6 +3694,10 @@ int fem_pcg_set_dist_variant(fem_pcg* s, int variant) {
         set_error("fem_pcg_set_dist_variant: needs a distributed context without a captured graph, variant 0 or 1");
         return FEM_EARG;
     }
+    if (s->mf && variant == 0) {
+        set_error("fem_pcg_set_dist_variant: the element-chunk operator runs the single-reduction variant (1) only");
+        return FEM_EARG;
+    }
     for (double** b : {&s->cg1_s, &s->cg1_u, &s->cg1_send, &s->cg1_recv}) {
         if (*b) (void)hipFree(*b);
         *b = nullptr;
@@ -3834,6 +3863,24 @@ static int fem_pcg_poll_raw(fem_pcg* s, int* iters, int* status, double* rz) {
     if (iters) *iters = (stt == FEM_PCG_BREAKDOWN || stt == FEM_PCG_ALPHA_NAN) ? h.stop_iter : h.iter;
     if (status) *status = stt;
     if (rz) *rz = (h.iter > 0) ? h.rz_new : h.rz;
+    if (stt == FEM_PCG_BAD_WINDOW) {
+        set_error("PCG: a workgroup's gather window lay outside the u-flag array (internal invariant broken; the "
+                  "launch ended without running, iterate not meaningful)");
+        return FEM_ESTATE;
+    }
+    return FEM_OK;
+}
+
+int fem_pcg_debug_window(fem_pcg* s, int L, int lo, int hi) {
+    int32_t* win = s->persist ? s->pk_win : s->c1f_win;
+    const int G = s->persist ? s->pk_grid : s->c1f_grid;
+    if (!win || G <= 0 || L < 0 || L >= G) {
+        set_error("fem_pcg_debug_window: no gather windows in this context (or L outside [0, %d))", G);
+        return FEM_EARG;
+    }
+    FEM_HIP(hipMemcpyAsync(win + L, &lo, sizeof(int32_t), hipMemcpyHostToDevice, s->stream));
+    FEM_HIP(hipMemcpyAsync(win + G + L, &hi, sizeof(int32_t), hipMemcpyHostToDevice, s->stream));
+    FEM_HIP(hipStreamSynchronize(s->stream));
     return FEM_OK;
 }
 

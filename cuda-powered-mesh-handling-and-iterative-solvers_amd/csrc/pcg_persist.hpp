@@ -82,7 +82,8 @@ __device__ __forceinline__ void pk_st(unsigned* p, unsigned v) {
 // one lane spins until *p >= target; false on give-up (own or another spinner's)
 // the give-up word holds the site of the first give-up (diagnostics, reported by fem_pcg_sync_site for a
 // FEM_PCG_SYNC_TIMEOUT): 1 + 16 * epoch local grid barrier, 2 + 16 * epoch u-flag window, 3 + 16 * epoch
-// rank sums (DIST)
+// rank sums (DIST), PK_SITE_WINDOW: a gather window outside the flag array (status FEM_PCG_BAD_WINDOW)
+// (PK_SITE_WINDOW, pk_window_bad, pk_fail_status: common.hpp)
 __device__ __forceinline__ bool pk_wait_ge(const unsigned* p, unsigned target, unsigned* tmo) {
     const uint64_t t0 = pk_now();
     for (unsigned spins = 0;; ++spins) {
@@ -422,9 +423,15 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
         uo[j] = wj * rr[j];   // u = w r is how every u was formed (k_cg1_init, the update): bit-identical, no load
     }
     // clamped to the flag array (nranks * G workgroups): a window is never an index outside it, whatever the
-    // array holds
-    const int wlo = max(a.win[L], 0), whi = min(a.win[G + L], (DIST ? a.nranks : 1) * G - 1);
+    // array holds; a window outside it is reported (FEM_PCG_BAD_WINDOW, every spinner released), not run
+    const int nflags = (DIST ? a.nranks : 1) * G;
+    const int wraw0 = a.win[L], wraw1 = a.win[G + L];
+    const int wlo = max(wraw0, 0), whi = min(wraw1, nflags - 1);
     bool fail = false;
+    if (pk_window_bad(wraw0, wraw1, nflags)) {
+        if (threadIdx.x == 0) pk_st(sy + PK_TMO, PK_SITE_WINDOW);
+        fail = true;
+    }
     bool st_loaded = !halt;   // the state is on chip and may have changed (nothing to store after a halt)
     int k = 0;
     if constexpr (DIST) {
@@ -799,8 +806,8 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
     }
     if (L == 0 && threadIdx.x == 0) {
         if (fail) {
-            status = FEM_PCG_SYNC_TIMEOUT;
             stop_iter = (int)pk_ld(sy + PK_TMO);   // where the first give-up happened (see pk_wait_ge)
+            status = pk_fail_status((unsigned)stop_iter);
             halt = 1;
         }
         st->iter = it;

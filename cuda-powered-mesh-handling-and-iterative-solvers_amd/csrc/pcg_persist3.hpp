@@ -153,9 +153,15 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist3(PkArgs a) {
         }
     }
     // clamped to the flag array (nranks * G workgroups): a window is never an index outside it, whatever the
-    // array holds
-    const int wlo = max(a.win[L], 0), whi = min(a.win[G + L], (DIST ? a.nranks : 1) * G - 1);
+    // array holds; a window outside it is reported (FEM_PCG_BAD_WINDOW, every spinner released), not run
+    const int nflags = (DIST ? a.nranks : 1) * G;
+    const int wraw0 = a.win[L], wraw1 = a.win[G + L];
+    const int wlo = max(wraw0, 0), whi = min(wraw1, nflags - 1);
     bool fail = false;
+    if (pk_window_bad(wraw0, wraw1, nflags)) {
+        if (threadIdx.x == 0) pk_st(sy + PK_TMO, PK_SITE_WINDOW);
+        fail = true;
+    }
     bool st_loaded = !halt;
     int k = 0;
     if constexpr (DIST) {
@@ -496,8 +502,8 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist3(PkArgs a) {
     if (wv == 0) store_state();
     if (L == 0 && threadIdx.x == 0) {
         if (fail) {
-            status = FEM_PCG_SYNC_TIMEOUT;
             stop_iter = (int)pk_ld(sy + PK_TMO);
+            status = pk_fail_status((unsigned)stop_iter);
             halt = 1;
         }
         st->iter = it;

@@ -17,33 +17,63 @@ void set_error(const char* fmt, ...) {
     va_end(ap);
 }
 
+// Stream-ordered scratch comes from a private memory pool per device (never the device's default pool, whose
+// attributes other libraries in the process share). The pool keeps at most FEM_POOL_KEEP bytes (256 MB) of freed
+// memory across synchronisations -- enough for the small per-call scratch whose reuse the pattern-build latency
+// work relies on; larger stream-ordered frees (graph build temporaries, CSR export buffers: GBs at 10M DOFs) go back
+// to the driver at the next synchronisation instead of staying reserved (torch's caching allocator can then reuse
+// them). fem_release_scratch() trims the pool to zero.
+constexpr uint64_t FEM_POOL_KEEP = 256ull << 20;
+static std::mutex g_pool_mu;
+static hipMemPool_t g_pool[64] = {};
+
+static hipMemPool_t scratch_pool(int dev) {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    if (!g_pool[dev]) {
+        hipMemPoolProps props;
+        memset(&props, 0, sizeof(props));
+        props.allocType = hipMemAllocationTypePinned;
+        props.handleTypes = hipMemHandleTypeNone;
+        props.location.type = hipMemLocationTypeDevice;
+        props.location.id = dev;
+        hipMemPool_t pool = nullptr;
+        if (hipMemPoolCreate(&pool, &props) != hipSuccess) return nullptr;
+        uint64_t keep = FEM_POOL_KEEP;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+        g_pool[dev] = pool;
+    }
+    return g_pool[dev];
+}
+
 hipError_t malloc_async(void** p, size_t bytes, hipStream_t st) {
-    static std::atomic<uint64_t> kept{0};   // devices whose default pool keeps its memory
     int dev = 0;
-    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64 && !((kept.load() >> dev) & 1)) {
-        hipMemPool_t pool;
-        if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-            uint64_t keep_all = UINT64_MAX;
-            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep_all);
-        }
-        kept.fetch_or(1ull << dev);
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+        hipMemPool_t pool = scratch_pool(dev);
+        if (pool) return hipMallocFromPoolAsync(p, bytes, pool, st);
     }
     return hipMallocAsync(p, bytes, st);
 }
 
+struct ScratchEntry {
+    hipStream_t st;
+    int dev;
+    void* ptr;
+    size_t bytes;
+};
+static std::mutex g_scratch_mu;
+static std::vector<ScratchEntry> g_scratch;
+
+// per-stream scratch kept between calls (host cost of a hipFreeAsync per call: it waits for the kernel, ~200 us).
+// Stream-ordered users only, and never under stream capture: a captured graph would record the pointer, which a
+// later larger request reallocates (the call refuses a capturing stream with hipErrorStreamCaptureUnsupported).
 hipError_t stream_scratch(void** p, size_t bytes, hipStream_t st) {
-    struct Entry {
-        hipStream_t st;
-        int dev;
-        void* ptr;
-        size_t bytes;
-    };
-    static std::mutex mu;
-    static std::vector<Entry> cache;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone)
+        return hipErrorStreamCaptureUnsupported;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) dev = -1;
-    std::lock_guard<std::mutex> lk(mu);
-    for (Entry& e : cache) {
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    for (ScratchEntry& e : g_scratch) {
         if (e.st != st || e.dev != dev) continue;
         if (e.bytes >= bytes) {
             *p = e.ptr;
@@ -58,18 +88,34 @@ hipError_t stream_scratch(void** p, size_t bytes, hipStream_t st) {
         *p = e.ptr;
         return hipSuccess;
     }
-    // a process that keeps creating streams: at most 8 kept buffers, the oldest released (hipFree waits for the
-    // device, which only a ninth stream's first call pays)
-    if (cache.size() >= 8) {
-        if (cache.front().ptr) (void)hipFree(cache.front().ptr);
-        cache.erase(cache.begin());
+    // a process that keeps creating streams: at most 8 kept buffers, the oldest released. hipFree (device-wide
+    // synchronisation), not hipFreeAsync: the evicted entry's stream may no longer exist, and a free ordered on this
+    // stream would not wait for that stream's work. Only a ninth stream's first call pays it.
+    if (g_scratch.size() >= 8) {
+        if (g_scratch.front().ptr) (void)hipFree(g_scratch.front().ptr);
+        g_scratch.erase(g_scratch.begin());
     }
-    Entry e{st, dev, nullptr, bytes};
+    ScratchEntry e{st, dev, nullptr, bytes};
     const hipError_t rc = malloc_async(&e.ptr, bytes, st);
     if (rc != hipSuccess) return rc;
-    cache.push_back(e);
+    g_scratch.push_back(e);
     *p = e.ptr;
     return hipSuccess;
+}
+
+// every kept per-stream buffer freed (after a device synchronisation) and the scratch pools trimmed to zero
+int release_scratch() {
+    {
+        std::lock_guard<std::mutex> lk(g_scratch_mu);
+        if (!g_scratch.empty()) FEM_HIP(hipDeviceSynchronize());
+        for (ScratchEntry& e : g_scratch)
+            if (e.ptr) (void)hipFree(e.ptr);
+        g_scratch.clear();
+    }
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (int d = 0; d < 64; ++d)
+        if (g_pool[d]) (void)hipMemPoolTrimTo(g_pool[d], 0);
+    return FEM_OK;
 }
 
 // ---------------------------------------------------------------- 3-phase exclusive scan
@@ -212,6 +258,8 @@ extern "C" {
 
 const char* fem_last_error(void) { return g_err; }
 int fem_version(void) { return 100; }
+
+int fem_release_scratch(void) { return release_scratch(); }
 
 int64_t fem_scan_work_len(int64_t n) { return cdiv(n > 0 ? n : 1, SCAN_TILE) + 1; }
 

@@ -494,6 +494,17 @@ def compute_wedge_volumes(coords, elements, device="cuda:0", dtype=torch.float32
     return _out(v[:, 0] + v[:, 1] + v[:, 2], device, dtype)
 
 
+def compute_hexahedral_volumes(coords, elements, device="cuda:0", dtype=torch.float32):
+    """Sum of the 6 sub-tet |volumes| (p0,p1,p3,p4), (p1,p2,p3,p6), (p1,p3,p4,p5), (p3,p4,p5,p7), (p3,p5,p6,p7),
+    (p3,p5,p6,p1), added in that order -> [M]. `solver/element.py:1248-1291` (the sub-tet volumes come from the c3d4
+    geometry kernel, |det| / 6 as the reference's inner `v`)."""
+    el = torch.as_tensor(elements).to(LONG)
+    subs = torch.stack([el[:, [0, 1, 3, 4]], el[:, [1, 2, 3, 6]], el[:, [1, 3, 4, 5]], el[:, [3, 4, 5, 7]],
+                        el[:, [3, 5, 6, 7]], el[:, [3, 5, 6, 1]]], 1).reshape(-1, 4)
+    v = compute_tetrahedral_volumes(coords, subs, device=device, dtype=F64).view(-1, 6)
+    return _out(v[:, 0] + v[:, 1] + v[:, 2] + v[:, 3] + v[:, 4] + v[:, 5], device, dtype)
+
+
 def compute_c3d6_K_matrix(coords, elements, E, nu, integral_point=None, single=True, device="cuda:0",
                           dtype=torch.float32):
     """single=True: B at (1/3,1/3,0) times the wedge volume; single=False: sum_ip w detJ B^T D B with the

@@ -803,6 +803,10 @@ class PcgRunner:
         _check_sync(stt.value)
         return it.value, stt.value, rz.value
 
+    def debug_window(self, L, lo, hi):
+        """Test-only fault injection: overwrite logical workgroup L's gather window (after start())."""
+        C.check(self.lib.fem_pcg_debug_window(self.h, int(L), int(lo), int(hi)), "fem_pcg_debug_window")
+
     def effective_schedule(self):
         """The schedule the context runs (after start(): SCHED_PERSIST may have fallen back to SCHED_DEFERRED)."""
         return int(self.lib.fem_pcg_get_schedule(self.h))

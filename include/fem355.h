@@ -39,6 +39,7 @@ enum {
     FEM_EHIP = 3,       /* HIP runtime error -> RuntimeError */
     FEM_ERCCL = 4,      /* RCCL error -> RuntimeError */
     FEM_EARG = 5,       /* bad argument / capacity exceeded */
+    FEM_ESTATE = 6,     /* a device-side invariant was found broken (e.g. FEM_PCG_BAD_WINDOW) -> RuntimeError */
 };
 
 /* status words of the (P)CG state, mirrored on the host as the reference's print strings
@@ -52,6 +53,9 @@ enum {
     FEM_PCG_BETA_NAN = 5,   /* (`solver/solver.py:214-218`) */
     FEM_PCG_SYNC_TIMEOUT = 6, /* persistent schedule: an in-launch wait gave up (seconds without progress); the
                                * iterate is not meaningful -> RuntimeError */
+    FEM_PCG_BAD_WINDOW = 7,   /* persistent / fused schedules: a workgroup's gather window lay outside the u-flag
+                               * array (an internal invariant broken upstream). The kernel never indexes past the
+                               * array; it ends the launch, and fem_pcg_poll / fem_pcg_solve return FEM_ESTATE */
 };
 
 /* CG_CONSTRAINED: constrained_conjugate_gradient_solver / new_constrained_conjugate_gradient_solver
@@ -404,8 +408,13 @@ int fem_pcg_start(fem_pcg* s);
 /* enqueue k iterations (no host sync); iterations after a stop are no-ops on the device */
 int fem_pcg_iterate(fem_pcg* s, int k);
 /* [sync] read iteration count, status and last r.z (or r.r). Guard stops (FEM_PCG_BREAKDOWN / _ALPHA_NAN) report
- * the reference's printed iteration; every other status the completed iterations */
+ * the reference's printed iteration; every other status the completed iterations. Returns FEM_ESTATE (status
+ * FEM_PCG_BAD_WINDOW, message in fem_last_error) when a launch found a gather window outside its flag array */
 int fem_pcg_poll(fem_pcg* s, int* iters, int* status, double* rz);
+/* [debug, test-only] overwrite logical workgroup L's gather window with [lo, hi] in the active schedule's window
+ * array (persistent or fused; call after fem_pcg_start): the fault-injection knob behind the FEM_PCG_BAD_WINDOW
+ * test. FEM_EARG when the context has no window array */
+int fem_pcg_debug_window(fem_pcg* s, int L, int lo, int hi);
 /* [sync] diagnostic of a FEM_PCG_SYNC_TIMEOUT: the give-up site code (persistent kernel: 1 grid barrier, 2 u-flag
  * window, 3 rank sums of the DIST build, + 16 * epoch; merged update k_pcg_update2: 4 + 16 * launch since start),
  * 0 for any other status */
@@ -604,6 +613,9 @@ int fem_ipc_close(void* ptr);
 /* [host] free the buffers that destroyed bs = 1 contexts left in the library's recycling cache (capped at
  * FEM355_PCG_CACHE_MB, default 1024 MB; invisible to torch's allocator); returns the MB released */
 int fem_pcg_release_cache(void);
+/* [host, sync] free the per-stream scratch buffers the library keeps between calls and trim its private stream-
+ * ordered pools (capped at 256 MB of retained memory each) to zero; called by the Python layer at exit */
+int fem_release_scratch(void);
 
 /* ------------------------------------------------------------------ multi-GPU (element partition, RCCL)
  * One process per GPU. Every rank holds the SELL matrix of ITS elements over its local nodes (unassembled at

@@ -177,6 +177,17 @@ def wedge_volumes(coords, elements):
         vol(p[:, 2], p[:, 4], p[:, 5], p[:, 3])
 
 
+def hex_volumes(coords, elements):
+    """Sum of 6 sub-tet |det| / 6, in the reference's order. `solver/element.py:1248-1291`."""
+    p = coords[elements]
+
+    def vol(a, b, c, d):
+        return torch.abs(torch.det(torch.stack([b - a, c - a, d - a], dim=1))) / 6.0
+    return (vol(p[:, 0], p[:, 1], p[:, 3], p[:, 4]) + vol(p[:, 1], p[:, 2], p[:, 3], p[:, 6]) +
+            vol(p[:, 1], p[:, 3], p[:, 4], p[:, 5]) + vol(p[:, 3], p[:, 4], p[:, 5], p[:, 7]) +
+            vol(p[:, 3], p[:, 5], p[:, 6], p[:, 7]) + vol(p[:, 3], p[:, 5], p[:, 6], p[:, 1]))
+
+
 def iso_K(coords, elements, etype, E, nu, points=None, weights=None, single=True):
     """`compute_c3d8_K_matrix` (`solver/element.py:1754-1803`), `compute_c3d10_K_matrix` (`:1191-1239`) and
     `compute_c3d6_K_matrix` (`:2631-2676`) in one restatement: sum_ip w * signed detJ * B^T D B.

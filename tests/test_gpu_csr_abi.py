@@ -121,3 +121,33 @@ def test_solid_ke_vs_reference(gpu, etype, npe):
     with pytest.raises(ValueError):
         C.check(lib.fem_solid_ke(20, C.ptr(X), C.ptr(el), M, E, NU, C.ptr(ip), C.ptr(w), ip.shape[0], 1, C.ptr(K1),
                                  C.stream(gpu)), "fem_solid_ke")
+
+
+def test_scratch_memory_returns_to_baseline(gpu):
+    """the library's stream-ordered scratch (graph build temporaries of fem_csr_pattern, the 9 nnz
+    staging of fem_csr_fill) comes from a private pool that keeps at most 256 MB across synchronisations, so the
+    device's free memory returns to within that of its baseline after a large pattern + fill (a 1.2M-tet elastic
+    cube: ~1 GB of temporaries), and fem_release_scratch trims the rest."""
+    C, lib = _lib()
+    from fem355 import mesh
+    c, t = mesh.kuhn_cube(59)
+    N = c.shape[0]
+    K = torch.randn(t.shape[0], 12, 12, dtype=F64, generator=torch.Generator().manual_seed(1)).to(gpu)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    free0 = torch.cuda.mem_get_info()[0]
+    el, rowptr, colidx, diag = _csr(C, lib, t, N, 3, gpu)
+    vals = torch.zeros(colidx.numel(), dtype=F64, device=gpu)
+    C.check(lib.fem_csr_fill(C.ptr(K), C.ptr(el), el.shape[0], 4, 3, N, C.ptr(rowptr), C.ptr(colidx), C.ptr(vals),
+                             C.stream(gpu)), "fem_csr_fill")
+    torch.cuda.synchronize()
+    held = sum(x.numel() * x.element_size() for x in (el, rowptr, colidx, diag, vals))
+    del el, rowptr, colidx, diag, vals
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    free1 = torch.cuda.mem_get_info()[0]
+    assert free0 - free1 <= (256 << 20) + (16 << 20), (free0 - free1, held)
+    C.check(lib.fem_release_scratch(), "fem_release_scratch")
+    torch.cuda.empty_cache()
+    free2 = torch.cuda.mem_get_info()[0]
+    assert free0 - free2 <= (16 << 20), free0 - free2

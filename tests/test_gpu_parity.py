@@ -106,6 +106,10 @@ def test_isoparametric_vs_golden(gpu, etype):
         assert rel(fn[2](c, e, ip, device=gpu, dtype=F64), g["B"][q]) < 1e-12
     if etype == "c3d6":
         assert rel(el.compute_wedge_volumes(c, e, device=gpu, dtype=F64), g["vol"]) < 1e-13
+    if etype == "c3d8":   # compute_hexahedral_volumes (`solver/element.py:1248-1291`), both orientations
+        v = el.compute_hexahedral_volumes(c, e, device=gpu, dtype=F64)
+        assert v.shape == (e.shape[0],) and rel(v, g["vol"]) < 1e-13
+        assert el.compute_hexahedral_volumes(c, e, device=gpu).dtype == torch.float32   # the reference's default
 
 
 # ------------------------------------------------------------------ L2 operators
@@ -625,6 +629,38 @@ def test_persistent_chunks_are_bit_identical(gpu):
         run.close()
     assert outs[0][0] == outs[1][0] == outs[2][0] and outs[0][0][0] == 36
     assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][1], outs[2][1])
+
+
+@pytest.mark.parametrize("kind", ["poisson", "elastic"])
+def test_persistent_bad_window_is_an_error(gpu, kind):
+    """A gather window outside the u-flag array (injected through the debug knob after start) is reported, not
+    clamped into silently wrong iterates: the launch ends, fem_pcg_poll returns FEM_ESTATE -> FemError, and the next
+    context on the same device runs normally (no fault, no hang)."""
+    _, mesh, _, system = _mods()
+    from fem355 import _capi as C
+    c, t = mesh.kuhn_cube(12, jitter=0.1)
+    f, fixed = mesh.cube_poisson_case(c)
+    A = system.assemble_tet4_system(c.to(gpu), t.to(gpu), kind, E=1.0, nu=0.3)
+    mask = torch.zeros(A.n // A.bs, dtype=torch.uint8, device=gpu)
+    mask[fixed.to(gpu)] = 1
+    if A.bs == 3:
+        mask = mask.repeat_interleave(3)
+    w = A.jacobi(mask)
+    b = torch.ones(A.n, dtype=F64, device=gpu) * (1 - mask.to(F64))
+    for lo, hi in ((0, 1 << 20), (-7, 2)):
+        run = system.PcgRunner(A, b, w, tol=0.0, schedule=3)
+        run.start()
+        assert run.effective_schedule() == 3
+        run.debug_window(1, lo, hi)
+        run.iterate(5)
+        with pytest.raises(C.FemError, match="gather window"):
+            run.poll()
+        run.close()
+    run = system.PcgRunner(A, b, w, tol=0.0, schedule=3)
+    run.start()
+    run.iterate(5)
+    assert run.poll()[:2] == (5, 0)
+    run.close()
 
 
 def _fixed_iterates(system, A, b, w, sched, flags, k):

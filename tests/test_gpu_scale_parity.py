@@ -11,8 +11,9 @@ runs `pytest -x`).
     oracle's EBE product `R.nodal_forces(R.tet4_K(...))` (`solver/element.py:429-464`, `:883-903`) to 1e-12, and the
     first 5 Jacobi-PCG iterates of the default bs = 3 schedule against `R.pcg` to 1e-10;
   * the metric (10M-tet P1 Poisson): the bench's operator and the exact persistent build it times (7 slots, 26,992
-    slice-uniform slices) for 5 iterates against the oracle, and the same on the cube renumbered at random and then by
-    device RCM (a mesh in file order).
+    slice-uniform slices) for 5 iterates against the oracle, the bench's whole DOFs/s solve to rtol 1e-8 (682
+    iterations) against the oracle PCG end to end, and the same 5 iterates on the cube renumbered at random and then
+    by device RCM (a mesh in file order).
 The oracle's element matrices at 10M tets take ~12 GB of host memory and ~10 s on the box's 16 cores."""
 import pytest
 import torch
@@ -160,6 +161,40 @@ def test_metric_poisson_10m_persistent_vs_oracle(gpu, cube119):
     assert facts["build"] == (7, 0, 7), facts
     assert facts["uniform"][:2] == (26_992, 27_000), facts
     assert rel(x, cube119.pcg_ref("poisson", 5).reshape(-1)) < 1e-10
+
+
+def test_metric_poisson_10m_full_solve_vs_oracle(gpu, cube119):
+    """The metric's DOFs/s solve end to end: bench.py's assembly, Jacobi weights and Jacobi-PCG
+    to rtol 1e-8 on sqrt(r.z) (the persistent kernel, one launch, stopping itself) against `R.pcg`
+    (`solver/solver.py:766-812`) over the oracle's element matrices, its operator applied as the COO-coalesced CSR the
+    reference assembles (`subdivision.ipynb:118-139`; equal to the EBE product to ~1e-16, and ~25x faster on the host,
+    so the 682 oracle iterations take ~30 s). Contract: iterations within +-2, u within 1e-10."""
+    _, _, _, system = _mods()
+    from fem355 import _capi as C
+    c, t, N = cube119.c, cube119.t, cube119.N
+    f, fixed, dinv = cube119.case("poisson")
+    A = system.assemble_tet4_system(c.to(gpu), t.to(gpu), "poisson")
+    mask = torch.zeros(N, dtype=torch.uint8, device=gpu)
+    mask.index_fill_(0, fixed.to(gpu), 1)
+    w = A.jacobi(mask)
+    b = f.reshape(-1).to(gpu)
+    tol = 1e-8 * float(torch.sqrt(torch.dot(b, w * b)))
+    res = A.pcg(b, None, w=w, mode=C.MODE_PCG, tol=tol, max_iter=20000, chunk=64)
+    assert res.status == C.PCG_CONVERGED
+    u, iters = res.x.cpu(), res.iterations
+    del A, w, res
+    K = cube119.K("poisson")
+    rows = t.unsqueeze(2).expand(-1, 4, 4).reshape(-1)
+    cols = t.unsqueeze(1).expand(-1, 4, 4).reshape(-1)
+    Acsr = torch.sparse_coo_tensor(torch.stack([rows, cols]), K.reshape(-1), (N, N)).coalesce().to_sparse_csr()
+    del rows, cols
+    p, y_ref = cube119.matvec_ref("poisson", 12)
+    assert rel(Acsr @ p, y_ref) < 1e-14          # the CSR form is the oracle's EBE operator
+    tol_ref = 1e-8 * float(torch.sqrt(torch.sum(f * dinv * f)))
+    u_ref, it_ref, st = R.pcg(K, t, f, dinv, tol=tol_ref, max_iter=5000,
+                              matvec=lambda v: (Acsr @ v.reshape(-1, 1)).reshape(v.shape))
+    assert st == "converged" and abs(iters - it_ref) <= 2, (iters, it_ref)
+    assert rel(u, u_ref.reshape(-1)) < 1e-10
 
 
 def test_metric_poisson_10m_rcm_renumbered_vs_oracle(gpu, cube119):

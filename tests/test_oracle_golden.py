@@ -63,6 +63,10 @@ def test_isoparametric_solids():
             dN = R.DN[et](*[float(v) for v in p[q]])
             assert rel(R.iso_jacobian(c, e, dN), g["J"][q]) < 1e-15
             assert rel(R.iso_gradients(c, e, dN), g["grads"][q]) < 1e-14
+        if et == "c3d8":   # compute_hexahedral_volumes (`solver/element.py:1248-1291`)
+            assert rel(R.hex_volumes(c, e), g["vol"]) == 0.0
+        if et == "c3d6":
+            assert rel(R.wedge_volumes(c, e), g["vol"]) < 1e-15
 
 
 def test_poisson_derivation_and_solve():
