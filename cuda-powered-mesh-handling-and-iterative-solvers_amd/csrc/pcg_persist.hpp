@@ -614,11 +614,27 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
             PK_MARK(2);
             if (threadIdx.x == 0) __hip_atomic_store(pd + L, dsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // (pk_block_sum ended on a workgroup barrier: the grid barrier needs no entry barrier of its own)
+#if FEM_PK_PROBE_NOBAR
+            // timing probe only (wrong scalars): no grid barrier, every workgroup steps on its own partial -- the
+            // neighbour-only coupling (u-flags) a pipelined iteration would leave, i.e. its speed bound
+            // (the arrivals still count, without the wait, so the chunk-end barrier's epochs stay consistent)
+            if (threadIdx.x == 0) {
+                lds_dg[0] = dsum;
+                lds_dg[1] = g;
+                const unsigned old = __hip_atomic_fetch_add(sy + PK_GRP + grp * PK_LINE, 1u, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
+                if ((old + 1) % nper == 0)   // workgroups desynchronise: every nper-th arrival of the group
+                    for (int r = 0; r < NXCD; ++r)
+                        __hip_atomic_fetch_add(sy + PK_GEN + r * PK_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __syncthreads();
+#else
             if (!(DIST ? pk_barrier_dist(a, sy, grp, nper, e, &lds_ok, pd, k > 0 ? pd + G : nullptr, G, lds_dg, false)
                        : pk_barrier(sy, grp, nper, e, &lds_ok, pd, k > 0 ? pd + G : nullptr, G, lds_dg, false))) {
                 fail = true;
                 break;
             }
+#endif
             elast = e;
             const double d = lds_dg[0];
             if (k > 0) g = lds_dg[1];

@@ -80,8 +80,8 @@ def phase_profile(A, b, w, warm, iters, ghz=2.4, per_wg=False, tune=None, sched=
     out = {p: {"mean_us": float(t[:, i].mean()), "max_us": float(t[:, i].max()), "min_us": float(t[:, i].min())}
            for i, p in enumerate(names)} | {"total_mean_us": float(t[:, :6].sum(1).mean())}
     busy = tw > 0
-    out["wave_spmv_us"] = {"mean_busy": float(tw[busy].mean()), "max": float(tw.max()),
-                           "min_busy": float(tw[busy].min()),
+    out["wave_spmv_us"] = {"mean_busy": float(tw[busy].mean()) if busy.any() else 0.0, "max": float(tw.max()),
+                           "min_busy": float(tw[busy].min()) if busy.any() else 0.0,
                            "wg_max_mean": float(tw.max(1).values.mean()), "wg_max_max": float(tw.max(1).values.max())}
     if per_wg:   # packed assignment: WG L owns [L S / G, (L+1) S / G), its waves ceil(maxL / 16) slices each in order
         G = g.value
