@@ -677,13 +677,34 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update2(int64_t n, double* __
     if (last && threadIdx.x == 0) st->u2_epoch = e;   // every workgroup read the epoch before the release
 }
 
-// The merged update on the element-chunk operator, one node (BS dofs) per thread-step: q of the node is the sum of
-// its slots in ascending chunk order (k_mf_gather's sum; FROM_Q: read from q written by k_mf_gather instead, the A/B
-// form -- same order of every sum, the same bits), so q is never stored. The release protocol is k_pcg_update2's.
+// The merged update on the element-chunk operator: k_pcg_update2's thread layout (a double2 of dofs per thread-step,
+// the z of the first U2_NPT in registers across the release, every vector stream read / written as 16-byte lanes),
+// with q of each dof formed in place from the node-major slots -- q_d = the sum of node d / BS's slots, component
+// d % BS, in ascending chunk order (k_mf_gather's sum, the same bits) -- so q is never stored. FROM_Q: q read from
+// the array k_mf_gather wrote (the A/B form; the same bits again). The release protocol is k_pcg_update2's, and so is
+// the order of every other operation: given equal q the update is bit-identical to k_pcg_update2's.
+// (Round 5 ran one node per thread-step: three 8-byte accesses per vector 24 bytes apart across the lanes, 93 us for
+// the 10M elastic cube's 380 MB.)
 #ifndef FEM_MF_NTL
 #define FEM_MF_NTL 0   // 1: the merged update reads the slots with non-temporal loads (read once)
 #endif
-constexpr int U2_NPN = 6;   // nodes per thread whose z stays in registers
+template <int BS>
+__device__ __forceinline__ double mf_q_dof(const MfOp& op, const double* __restrict__ slots, int64_t d) {
+    const int64_t a = d / BS;
+    const int c = (int)(d - a * BS);
+    const int k0 = op.nptr[a], k1 = op.nptr[a + 1];
+    double s = 0.0;
+    for (int k = k0; k < k1; ++k) {
+        const int64_t sl = op.spos ? k : op.nslot[k];
+#if FEM_MF_NTL
+        s += __builtin_nontemporal_load(&slots[sl * BS + c]);
+#else
+        s += slots[sl * BS + c];
+#endif
+    }
+    return s;
+}
+
 template <int BS, bool FROM_Q>
 __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update2_mf(int64_t nn, double* __restrict__ x, double* __restrict__ p,
                                                               double* __restrict__ r, const double* __restrict__ q,
@@ -705,79 +726,96 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update2_mf(int64_t nn, double
     const unsigned e = st->u2_epoch + 1;
     const double alpha = st->alpha;
     const bool cg = st->mode != FEM_MODE_PCG;
-    const int64_t stride = (int64_t)gridDim.x * PCG_BLOCK;
-    const int64_t a0 = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x;
-    auto node_r = [&](int64_t a, double zc[BS]) -> double {   // r update of node a, z = w r; returns its r.z
-        double qv[BS];
-        if constexpr (FROM_Q) {
-#pragma unroll
-            for (int c = 0; c < BS; ++c) qv[c] = q[a * BS + c];
-        } else {
-#pragma unroll
-            for (int c = 0; c < BS; ++c) qv[c] = 0.0;
-            const int k0 = op.nptr[a], k1 = op.nptr[a + 1];
-            for (int k = k0; k < k1; ++k) {
-                const int64_t sl = op.spos ? k : op.nslot[k];
-#pragma unroll
-                for (int c = 0; c < BS; ++c) {
-#if FEM_MF_NTL
-                    qv[c] += __builtin_nontemporal_load(&slots[sl * BS + c]);
-#else
-                    qv[c] += slots[sl * BS + c];
-#endif
-                }
-            }
-        }
-        double s = 0.0;
-#pragma unroll
-        for (int c = 0; c < BS; ++c) {
-            const int64_t d = a * BS + c;
-            double rv = r[d] - alpha * qv[c];
-            const double wv = w[d];
-            if (cg && wv == 0.0) rv = 0.0;
-            r[d] = rv;
-            zc[c] = wv * rv;
-            s += rv * zc[c];
-        }
-        return s;
+    const int64_t n = nn * BS;
+    const int64_t n2 = n >> 1, stride = (int64_t)gridDim.x * PCG_BLOCK;
+    const int64_t i0 = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x;
+    const double2* q2 = reinterpret_cast<const double2*>(q);
+    const double2* w2 = reinterpret_cast<const double2*>(w);
+    double2* r2 = reinterpret_cast<double2*>(r);
+    auto qpair = [&](int64_t i) -> double2 {
+        if constexpr (FROM_Q) return q2[i];
+        return make_double2(mf_q_dof<BS>(op, slots, 2 * i), mf_q_dof<BS>(op, slots, 2 * i + 1));
     };
-    double z[U2_NPN][BS];
+    double2 z[U2_NPT];
     double acc = 0.0;
 #pragma unroll
-    for (int k = 0; k < U2_NPN; ++k) {
-        const int64_t a = a0 + k * stride;
-#pragma unroll
-        for (int c = 0; c < BS; ++c) z[k][c] = 0.0;
-        if (a < nn) acc += node_r(a, z[k]);
+    for (int k = 0; k < U2_NPT; ++k) {
+        const int64_t i = i0 + k * stride;
+        z[k] = make_double2(0.0, 0.0);
+        if (i < n2) {
+            double2 rv = r2[i], wv = w2[i];
+            const double2 qv = qpair(i);
+            rv.x = rv.x - alpha * qv.x;
+            rv.y = rv.y - alpha * qv.y;
+            if (cg) {
+                if (wv.x == 0.0) rv.x = 0.0;
+                if (wv.y == 0.0) rv.y = 0.0;
+            }
+            r2[i] = rv;
+            z[k] = make_double2(wv.x * rv.x, wv.y * rv.y);
+            acc += rv.x * z[k].x;
+            acc += rv.y * z[k].y;
+        }
     }
-    for (int64_t a = a0 + U2_NPN * stride; a < nn; a += stride) {   // past the register capacity
-        double zc[BS];
-        acc += node_r(a, zc);
+    for (int64_t i = i0 + U2_NPT * stride; i < n2; i += stride) {   // past the register capacity
+        double2 rv = r2[i], wv = w2[i];
+        const double2 qv = qpair(i);
+        rv.x = rv.x - alpha * qv.x;
+        rv.y = rv.y - alpha * qv.y;
+        if (cg) {
+            if (wv.x == 0.0) rv.x = 0.0;
+            if (wv.y == 0.0) rv.y = 0.0;
+        }
+        r2[i] = rv;
+        acc += rv.x * (wv.x * rv.x);
+        acc += rv.y * (wv.y * rv.y);
+    }
+    double ztail = 0.0;
+    const bool tail = (n & 1) && blockIdx.x == 0 && threadIdx.x == 0;
+    if (tail) {
+        const int64_t i = n - 1;
+        double rv = r[i] - alpha * (FROM_Q ? q[i] : mf_q_dof<BS>(op, slots, i));
+        if (cg && w[i] == 0.0) rv = 0.0;
+        r[i] = rv;
+        ztail = w[i] * rv;
+        acc += rv * ztail;
     }
     double beta;
     bool upd_p, last;
     if (!u2_release(acc, st, red, hist, hist_len, sync, e, lds4, &flag, bc_s, beta, upd_p, last)) return;
+    double2* x2 = reinterpret_cast<double2*>(x);
+    double2* p2 = reinterpret_cast<double2*>(p);
 #pragma unroll
-    for (int k = 0; k < U2_NPN; ++k) {
-        const int64_t a = a0 + k * stride;
-        if (a < nn) {
-#pragma unroll
-            for (int c = 0; c < BS; ++c) {
-                const int64_t d = a * BS + c;
-                const double pv = p[d];
-                x[d] += alpha * pv;
-                if (upd_p) p[d] = z[k][c] + beta * pv;
+    for (int k = 0; k < U2_NPT; ++k) {
+        const int64_t i = i0 + k * stride;
+        if (i < n2) {
+            double2 pv = p2[i], xv = x2[i];
+            xv.x += alpha * pv.x;
+            xv.y += alpha * pv.y;
+            x2[i] = xv;
+            if (upd_p) {
+                pv.x = z[k].x + beta * pv.x;
+                pv.y = z[k].y + beta * pv.y;
+                p2[i] = pv;
             }
         }
     }
-    for (int64_t a = a0 + U2_NPN * stride; a < nn; a += stride) {
-#pragma unroll
-        for (int c = 0; c < BS; ++c) {
-            const int64_t d = a * BS + c;
-            const double pv = p[d];
-            x[d] += alpha * pv;
-            if (upd_p) p[d] = w[d] * r[d] + beta * pv;
+    for (int64_t i = i0 + U2_NPT * stride; i < n2; i += stride) {
+        double2 pv = p2[i], xv = x2[i];
+        xv.x += alpha * pv.x;
+        xv.y += alpha * pv.y;
+        x2[i] = xv;
+        if (upd_p) {
+            const double2 rv = r2[i], wv = w2[i];
+            pv.x = wv.x * rv.x + beta * pv.x;
+            pv.y = wv.y * rv.y + beta * pv.y;
+            p2[i] = pv;
         }
+    }
+    if (tail) {
+        const int64_t i = n - 1;
+        x[i] += alpha * p[i];
+        if (upd_p) p[i] = ztail + beta * p[i];
     }
     if (last && threadIdx.x == 0) st->u2_epoch = e;
 }

@@ -124,7 +124,13 @@ __device__ __forceinline__ bool pk_barrier(unsigned* sy, int grp, unsigned nper,
                                                         __HIP_MEMORY_SCOPE_AGENT);
             // last of its group: arrive on all 8 replicas of the top counter (one line each); every workgroup polls
             // its group's replica (32 pollers per line, no leader -> generation hop)
+#if FEM_PK_PROBE_NOBAR
+            // (probe: workgroups reach the chunk-end barrier while others of their group still iterate, so the add
+            // that completes any epoch's count bumps the replicas, whoever makes it)
+            if ((old + 1) % nper == 0)
+#else
             if (old == e * nper - 1)
+#endif
                 for (int r = 0; r < NXCD; ++r)
                     __hip_atomic_fetch_add(sy + PK_GEN + r * PK_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             ok = pk_wait_ge(sy + PK_GEN + grp * PK_LINE, e * NXCD, tmo);

@@ -135,9 +135,14 @@ def main():
         for sched in sol:
             if sched != s0:
                 out[f"solve_dx_rel_{sched}"] = float((sol[s0] - sol[sched]).norm() / sol[s0].norm())
+        if a.prof:
+            print(json.dumps({"n": n, "prof_only": out.get("prof")}), flush=True)
         xs = {}
         for sched in a.scheds:
-            out[f"rate{sched}"], xs[sched] = rate(A, b, w, sched, a.warm, a.iters, a.chunk)
+            try:
+                out[f"rate{sched}"], xs[sched] = rate(A, b, w, sched, a.warm, a.iters, a.chunk)
+            except RuntimeError as e:   # timing probes with wrong scalars may end in a give-up
+                out[f"rate{sched}"] = {"error": str(e)}
         for sched in xs:
             if sched != s0:
                 out[f"rate_dx_rel_{sched}"] = float((xs[s0] - xs[sched]).norm() / xs[s0].norm())
