@@ -76,6 +76,9 @@ def parse():
     ap.add_argument("--mixed", type=int, default=1,
                     help="poisson runs: also BASELINE configs[4] (2M-element c3d8 / c3d6 / c3d10 stiffness + mass "
                          "assembly) under \"mixed\"")
+    ap.add_argument("--mixed-ke", default="full", choices=["full", "packed"],
+                    help="configs[4] stiffness: the full [M, d, d] K_e of compute_K_matrix, or its packed symmetric "
+                         "form (upper blocks; fem_iso_ke_sym + fem_assemble_from_ke_sym)")
     ap.add_argument("--schedule", type=int, default=None, help="PCG kernel schedule (0 three-kernel, 1 fused, 2 deferred, 3 persistent; "
                     "default: persistent for bs=1, three-kernel for bs=3)")
     ap.add_argument("--graph", type=int, default=0, help="capture k iterations per hipGraph (0 = plain launches)")
@@ -398,7 +401,9 @@ def measure_mixed(a, dev):
     """BASELINE configs[4]: "2M-element P2 tet + hex/wedge mixed mesh, mass+stiffness assembly, 1 x MI355X" -- three
     separate boxes (P2 / linear faces are nonconforming): c3d8 88^3 = 681,472 hexes, c3d6 2 x 70^3 =
     686,000 wedges, c3d10 6 x 48^3 = 663,552 quadratic tets, jittered. Per family one job: element stiffness through
-    the reference API (`compute_K_matrix`, `solver/element.py:419-427`, default rule / single=True) and the consistent
+    the reference API (`compute_K_matrix`, `solver/element.py:419-427`, default rule / single=True; --mixed-ke packed:
+    its packed symmetric form, upper 3x3 blocks only, `element._solid_ke_sym` + `SellMatrix.add_element_matrices_sym`,
+    the same sums, measured slower overall) and the consistent
     mass (`compute_M_matrix(..., scalar=True)`: its factor M_s of M = M_s (x) I3, [M, npe, npe] -- the 3x3 blocks of a
     vector-field mass are multiples of I3, so the stored and assembled mass is the bs = 1 M_s on the same node pattern;
     no reference function: parity unpinned) on the current stream, the pattern (node graph
@@ -426,6 +431,18 @@ def measure_mixed(a, dev):
         c, el = getattr(mesh, gen)(n, jitter=0.1, device=dev)
         N = c.shape[0]
         side = torch.cuda.Stream(device=dev)
+        if a.mixed_ke == "packed":   # upper 3x3 blocks only (measured slower overall: DESIGN §10)
+            def ke_fn():
+                return element._solid_ke_sym(c, el, et, E, nu, device=dev)
+
+            def asm_fn(S, K):
+                return S.add_element_matrices_sym(K, el)
+        else:
+            def ke_fn():
+                return element.compute_K_matrix(c, el, et, E, nu, device=dev, dtype=F64)
+
+            def asm_fn(S, K):
+                return S.add_element_matrices(K, el)
 
         def job():
             box = []
@@ -436,12 +453,12 @@ def measure_mixed(a, dev):
                     box.append(system.build_graph(el, N))
             th = threading.Thread(target=pattern)
             th.start()
-            K = element.compute_K_matrix(c, el, et, E, nu, device=dev, dtype=F64)
+            K = ke_fn()
             Me = element.compute_M_matrix(c, el, et, RHO, device=dev, dtype=F64, scalar=True)
             th.join()
             g = box[0]
             torch.cuda.current_stream(dev).wait_stream(side)
-            A = system.SellMatrix(g, 3).add_element_matrices(K, el)
+            A = asm_fn(system.SellMatrix(g, 3), K)
             Am = system.SellMatrix(g, 1).add_element_matrices(Me, el)
             return K, Me, g, A, Am
 
@@ -454,9 +471,9 @@ def measure_mixed(a, dev):
             walls.append((time.perf_counter() - t0) * 1e3)
             del K, Me, A, Am, g
         # kernel times by stage (events; not overlapped), outside the timed jobs
-        ms_k, K = ev(lambda: element.compute_K_matrix(c, el, et, E, nu, device=dev, dtype=F64))
+        ms_k, K = ev(ke_fn)
         ms_g, g = ev(lambda: system.build_graph(el, N))
-        ms_a, A = ev(lambda: system.SellMatrix(g, 3).add_element_matrices(K, el))
+        ms_a, A = ev(lambda: asm_fn(system.SellMatrix(g, 3), K))
         ms_m, Me = ev(lambda: element.compute_M_matrix(c, el, et, RHO, device=dev, dtype=F64, scalar=True))
         ms_ma, Am = ev(lambda: system.SellMatrix(g, 1).add_element_matrices(Me, el))
         ke_bytes = K.numel() * 8
@@ -484,7 +501,8 @@ def measure_mixed(a, dev):
                        "achieved_GBps": total_bytes / (total_ms * 1e-3) / 1e9,
                        "frac": total_bytes / (total_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS,
                        "model": "K_e and M_s,e written and each read once by its assembly, the bs = 3 stiffness and "
-                                "bs = 1 mass SELL values written once (the set's job time; the pattern excluded)"}
+                                "bs = 1 mass SELL values written once (the set's job time; the pattern excluded)"
+                                + ("; K_e in its packed symmetric form (upper blocks)" if a.mixed_ke == "packed" else "")}
     return out
 
 

@@ -150,6 +150,14 @@ __global__ void __launch_bounds__(256) k_iso_geom(const double* __restrict__ X, 
     }
 }
 
+// ---------------------------------------------------------------- packed symmetric element matrices (bs = 3)
+// K_e = sum_q B_q^T D B_q is symmetric: the internal assembly path stores only its upper 3x3 blocks (a <= b), row-major
+// over the upper triangle (block index ke_sym_blk(a, b)), 9 doubles each, padded to an even count per element
+// (16-byte aligned elements): c3d10 496 doubles instead of 900, c3d8 324 of 576, c3d6 190 of 324, c3d4 78 of 144.
+__host__ __device__ constexpr int ke_sym_nb(int npe) { return npe * (npe + 1) / 2; }
+__host__ __device__ constexpr int ke_sym_stride(int npe) { return (9 * ke_sym_nb(npe) + 1) & ~1; }
+__host__ __device__ constexpr int ke_sym_blk(int npe, int a, int b) { return a * npe - a * (a - 1) / 2 + (b - a); }
+
 // ---------------------------------------------------------------- isoparametric solids (wave per element)
 constexpr int ISO_MAX_IP = 32;
 constexpr int ISO_IPC = 16;   // points whose geometry is staged in LDS at once
@@ -161,7 +169,7 @@ __device__ __forceinline__ void iso_wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-template <int NPE, bool MASS, bool SC = false>
+template <int NPE, bool MASS, bool SC = false, bool PK = false>
 __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, const int64_t* __restrict__ conn,
                                                 int64_t M, double E, double nu, const double* __restrict__ dN,
                                                 const double* __restrict__ w, int n_ip, int mode,
@@ -177,7 +185,10 @@ __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, co
     // no workgroup barrier after the rule tables are staged, the next element's coordinates and the one after's node
     // ids are loaded while the current element is formed.
     constexpr int D = 3 * NPE;
-    constexpr bool SYM = NPE * NPE > 64;
+    // PK (stiffness only): the packed symmetric form -- lanes form the upper blocks a <= b only, written as
+    // ke_sym_stride(NPE) doubles per element (ke_row3's packed read mirrors the lower ones)
+    static_assert(!PK || !MASS, "packed K_e: stiffness only");
+    constexpr bool SYM = NPE * NPE > 64 || PK;
     constexpr int NS = SYM ? NPE * (NPE + 1) / 2 : NPE * NPE;
     static_assert(NS <= 64, "one block per lane");
     // rule tables in dynamic LDS sized to the rule (n_ip NPE 3 natural derivatives, then n_ip NPE shape values)
@@ -324,6 +335,18 @@ __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, co
         double2* out2 = reinterpret_cast<double2*>(Ke + e * NPE * NPE);   // NPE^2 even: 16-byte aligned rows
         const double2* ks2 = reinterpret_cast<const double2*>(ks);
         for (int t = lane; t < NPE * NPE / 2; t += 64) out2[t] = ks2[t];
+    } else if (PK && mode != FEM_ISO_STACK && active) {   // packed upper blocks, lane = packed block index
+        double* ks = gk_s[wid];
+        constexpr int PKS = ke_sym_stride(NPE);
+        if (blk_lane) {
+#pragma unroll
+            for (int t = 0; t < 9; ++t) ks[lane * 9 + t] = acc[t];
+        }
+        if (lane == 0 && PKS > 9 * NS) ks[9 * NS] = 0.0;   // the padding double of an odd 9 NS
+        __builtin_amdgcn_wave_barrier();
+        double2* out2 = reinterpret_cast<double2*>(Ke + e * PKS);   // PKS even: 16-byte aligned elements
+        const double2* ks2 = reinterpret_cast<const double2*>(ks);
+        for (int t = lane; t < PKS / 2; t += 64) out2[t] = ks2[t];
     } else if (mode != FEM_ISO_STACK && active) {   // (the loop above ended on a wave sync: gk_s is free)
         double* ks = gk_s[wid];
         if (blk_lane) {
@@ -347,7 +370,7 @@ __global__ void __launch_bounds__(256) k_iso_ke(const double* __restrict__ X, co
   }
 }
 
-template <int NPE, bool MASS, bool SC = false>
+template <int NPE, bool MASS, bool SC = false, bool PK = false>
 __global__ void __launch_bounds__(256) k_iso_ke1(const double* __restrict__ X, const int64_t* __restrict__ conn,
                                                 int64_t M, double E, double nu, const double* __restrict__ dN,
                                                 const double* __restrict__ w, int n_ip, int mode,
@@ -361,7 +384,10 @@ __global__ void __launch_bounds__(256) k_iso_ke1(const double* __restrict__ X, c
     // 55 blocks, one per lane. c3d8 / c3d6 (<= 64 blocks): every block formed directly.
     // mode FEM_ISO_MASS (E = rho, Nv = shape values [n_ip][NPE]): block (a,b) = rho sum_q w_q |detJ_q| N_a N_b I3.
     constexpr int D = 3 * NPE;
-    constexpr bool SYM = NPE * NPE > 64;
+    // PK (stiffness only): the packed symmetric form -- lanes form the upper blocks a <= b only, written as
+    // ke_sym_stride(NPE) doubles per element (ke_row3's packed read mirrors the lower ones)
+    static_assert(!PK || !MASS, "packed K_e: stiffness only");
+    constexpr bool SYM = NPE * NPE > 64 || PK;
     constexpr int NS = SYM ? NPE * (NPE + 1) / 2 : NPE * NPE;
     static_assert(NS <= 64, "one block per lane");
     // rule tables in dynamic LDS sized to the rule (n_ip NPE 3 natural derivatives, then n_ip NPE shape values)
@@ -498,6 +524,18 @@ __global__ void __launch_bounds__(256) k_iso_ke1(const double* __restrict__ X, c
         double2* out2 = reinterpret_cast<double2*>(Ke + e * NPE * NPE);
         const double2* ks2 = reinterpret_cast<const double2*>(ks);
         for (int t = lane; t < NPE * NPE / 2; t += 64) out2[t] = ks2[t];
+    } else if (PK && mode != FEM_ISO_STACK && active) {   // packed upper blocks (as k_iso_ke)
+        double* ks = gk_s[wid];
+        constexpr int PKS = ke_sym_stride(NPE);
+        if (blk_lane) {
+#pragma unroll
+            for (int t = 0; t < 9; ++t) ks[lane * 9 + t] = acc[t];
+        }
+        if (lane == 0 && PKS > 9 * NS) ks[9 * NS] = 0.0;
+        __builtin_amdgcn_wave_barrier();
+        double2* out2 = reinterpret_cast<double2*>(Ke + e * PKS);
+        const double2* ks2 = reinterpret_cast<const double2*>(ks);
+        for (int t = lane; t < PKS / 2; t += 64) out2[t] = ks2[t];
     } else if (mode != FEM_ISO_STACK && active) {   // (the loop above ended on a barrier: gk_s is free)
         double* ks = gk_s[wid];
         if (blk_lane) {
@@ -819,20 +857,30 @@ struct KeRowLane {
 // One wave, one row i, one column window [j0, j0 + nj) of it (cs = those columns, staged by the caller): acc[slot *
 // 9 + r * 3 + c] += the row's K_e block rows over its incidences in ascending (incidence, b) order (acc zeroed by the
 // caller). Scratch: slot_s / koff_s / eid_s [64] of this wave.
-template <int NPE>
+// PK: Ke holds the packed upper blocks (ke_sym_stride(NPE) doubles per element): block (a, b) of the row's element
+// node a is read from block ke_sym_blk(a, b) for a <= b and as the transpose of block ke_sym_blk(b, a) otherwise --
+// the same values in the same (incidence, b) order, so the sums equal the full-K_e sums whenever the full K_e's lower
+// blocks are the transposes of its upper ones (c3d10: mirrored by k_iso_ke, bit-identical)
+template <int NPE, bool PK = false>
 __device__ __forceinline__ void ke_row3(const KeRowLane<NPE>& L, const double* __restrict__ Ke,
                                         const int64_t* __restrict__ conn, const int32_t* __restrict__ inc, int t0,
                                         int C, const int* cs, int nj, double* acc, int* slot_s, int64_t* koff_s,
                                         int* eid_s, int lane) {
     constexpr int B2 = 9, D = KeRowLane<NPE>::D, RV = KeRowLane<NPE>::RV, NL = KeRowLane<NPE>::NL;
     constexpr int KU = KeRowLane<NPE>::KU;
+    constexpr int PKS = ke_sym_stride(NPE);
+    int vt[NL];   // PK: offset of the value inside the transposed block (c * 3 + r for vo = r * 3 + c)
+#pragma unroll
+    for (int m = 0; m < NL; ++m) vt[m] = (L.vo[m] % 3) * 3 + L.vo[m] / 3;
     for (int k0 = 0; k0 < C; k0 += 64) {
         const int nk = min(64, C - k0);
         __builtin_amdgcn_wave_barrier();
         if (lane < nk) {
             const int ea = inc[t0 + k0 + lane];
             const int e = ea / NPE;
-            koff_s[lane] = (int64_t)e * D * D + (int64_t)(ea - e * NPE) * RV;
+            // PK: the element's packed base, times 16, plus its node a (< 16)
+            koff_s[lane] = PK ? (int64_t)e * PKS * 16 + (ea - e * NPE)
+                              : (int64_t)e * D * D + (int64_t)(ea - e * NPE) * RV;
             eid_s[lane] = e;
         }
         __builtin_amdgcn_wave_barrier();
@@ -842,8 +890,19 @@ __device__ __forceinline__ void ke_row3(const KeRowLane<NPE>& L, const double* _
 #pragma unroll
             for (int u = 0; u < KU; ++u) {
                 const int64_t ko = koff_s[kb + (u < nu ? u : 0)];
+                if constexpr (PK) {
+                    const int a = (int)(ko & 15);
+                    const int64_t base = ko >> 4;
 #pragma unroll
-                for (int m = 0; m < NL; ++m) v[u][m] = (u < nu && L.vv[m]) ? Ke[ko + lane + 64 * m] : 0.0;
+                    for (int m = 0; m < NL; ++m) {
+                        const int b = L.vb[m];
+                        const int off = a <= b ? ke_sym_blk(NPE, a, b) * 9 + L.vo[m] : ke_sym_blk(NPE, b, a) * 9 + vt[m];
+                        v[u][m] = (u < nu && L.vv[m]) ? Ke[base + off] : 0.0;
+                    }
+                } else {
+#pragma unroll
+                    for (int m = 0; m < NL; ++m) v[u][m] = (u < nu && L.vv[m]) ? Ke[ko + lane + 64 * m] : 0.0;
+                }
             }
             int dup = 0;
             if (lane < nu * NPE) {   // slot of node b of incidence u in this column window (-1: outside)
@@ -945,7 +1004,7 @@ __global__ void __launch_bounds__(256) k_assemble_ke_rows3(const double* __restr
 // doubles (R = 16: one whole 128-byte line) -- padding entries and lanes past the last row zeroed in store mode.
 // No block-CSR buffer, no k_csr_add_sell pass (c3d10: 1.85 GB written once instead of written, read and written).
 // Tiles of a slice run on one XCD, so its lines are completed in one L2.
-template <int NPE, int R, bool STORE, bool LA = false>
+template <int NPE, int R, bool STORE, bool LA = false, bool PK = false>
 __global__ void __launch_bounds__(R * 64) k_assemble_ke_tile3(const double* __restrict__ Ke,
                                                                const int64_t* __restrict__ conn,
                                                                const int32_t* __restrict__ inc_ptr,
@@ -989,8 +1048,8 @@ __global__ void __launch_bounds__(R * 64) k_assemble_ke_tile3(const double* __re
         __syncthreads();                             // the previous window written out
         if (lane < nj) cols_s[wid][lane] = colidx[lo + j0 + lane];
         for (int t = lane; t < nw * B2; t += 64) acc[t] = 0.0;
-        if (nj > 0) ke_row3<NPE>(L, Ke, conn, inc, t0, C, cols_s[wid], nj, acc, slot_s[wid], koff_s[wid], eid_s[wid],
-                                 lane);
+        if (nj > 0) ke_row3<NPE, PK>(L, Ke, conn, inc, t0, C, cols_s[wid], nj, acc, slot_s[wid], koff_s[wid],
+                                     eid_s[wid], lane);
         __syncthreads();
         double* dst = vals + B2 * p0 + (int64_t)64 * B2 * j0 + l0;
         for (int q = threadIdx.x; q < nw * B2 * R; q += R * 64) {
@@ -2104,6 +2163,32 @@ int fem_iso_ke(const double* coords, const int64_t* conn, int64_t M, int npe, do
     return FEM_OK;
 }
 
+int fem_ke_sym_stride(int npe) { return (npe >= 1 && npe <= 15) ? ke_sym_stride(npe) : -1; }
+
+int fem_iso_ke_sym(const double* coords, const int64_t* conn, int64_t M, int npe, double E, double nu,
+                   const double* dN, const double* w, int n_ip, int mode, double* Kp, fem_stream_t stream) {
+    if (mode != FEM_ISO_SUM && mode != FEM_ISO_VOLUME) {
+        set_error("fem_iso_ke_sym: mode %d (the packed form takes FEM_ISO_SUM / FEM_ISO_VOLUME)", mode);
+        return FEM_EARG;
+    }
+    if (M <= 0) return FEM_OK;
+    if (n_ip < 1 || n_ip > ISO_MAX_IP) {
+        set_error("fem_iso_ke_sym: n_ip = %d out of range [1, %d]", n_ip, ISO_MAX_IP);
+        return FEM_EARG;
+    }
+    const size_t lds = sizeof(double) * (size_t)n_ip * npe * 3;
+    const void* fn = (const void*)k_iso_ke<10, false, false, true>;
+    const dim3 g(iso_grid_npe(fn, lds, M, npe));
+    switch (npe) {
+        case 6: hipLaunchKernelGGL((k_iso_ke1<6, false, false, true>), g, dim3(256), lds, S(stream), coords, conn, M, E, nu, dN, w, n_ip, mode, Kp); break;
+        case 8: hipLaunchKernelGGL((k_iso_ke1<8, false, false, true>), g, dim3(256), lds, S(stream), coords, conn, M, E, nu, dN, w, n_ip, mode, Kp); break;
+        case 10: hipLaunchKernelGGL((k_iso_ke<10, false, false, true>), g, dim3(256), lds, S(stream), coords, conn, M, E, nu, dN, w, n_ip, mode, Kp); break;
+        default: set_error("fem_iso_ke_sym: unsupported nodes per element %d", npe); return FEM_EBADTYPE;
+    }
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
 static int iso_mass(const double* coords, const int64_t* conn, int64_t M, int npe, double rho, const double* Nv,
                     const double* dN, const double* w, int n_ip, double* Me, bool scalar, hipStream_t st);
 
@@ -2164,24 +2249,26 @@ int fem_assemble_from_ke(const double* Ke, const int64_t* conn, int npe, int bs,
 // (whole 128-byte plane lines), else 8; false when the pattern's width is unknown or the form is switched off
 static int ke_tile_launch(const double* Ke, const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc,
                           int64_t N, const int32_t* rowptr, const int32_t* colidx, const int64_t* slice_ptr, int store,
-                          int max_width, double* vals, hipStream_t st, bool* done, bool la = false) {
+                          int max_width, double* vals, hipStream_t st, bool* done, bool la = false, bool pk = false) {
     *done = false;
     if (max_width <= 0) return FEM_OK;
-    if (!la && (getenv("FEM355_KE_ROWS") != nullptr || getenv("FEM355_KE_COLS") != nullptr)) return FEM_OK;
+    if (!la && !pk && (getenv("FEM355_KE_ROWS") != nullptr || getenv("FEM355_KE_COLS") != nullptr)) return FEM_OK;
     const int Wc = max_width < KR_LMAX ? max_width : KR_LMAX;
     const int R = (16 * (Wc * 9 + 1) * 8 + 16 * 1280 <= 65536) ? 16 : 8;
     const size_t dyn = sizeof(double) * (size_t)R * (Wc * 9 + 1);
     const int64_t ntiles = cdiv(N, 64) * (64 / R);   // whole slices: lanes past the last row are zeroed too
     const dim3 g((unsigned)(cdiv(cdiv(N, 64), NXCD) * NXCD * (64 / R)));
-#define FEM_KT(P, RR, ST, LA_)                                                                                     \
-    if (npe == P && R == RR && (store != 0) == ST && la == LA_)                                                    \
-        hipLaunchKernelGGL((k_assemble_ke_tile3<P, RR, ST, LA_>), g, dim3(RR * 64), dyn, st, Ke, conn, inc_ptr, inc,\
-                           N, rowptr, colidx, slice_ptr, vals, Wc, ntiles);
-#define FEM_KT_ALL(P) FEM_KT(P, 16, true, false) FEM_KT(P, 16, false, false) FEM_KT(P, 8, true, false)             \
-    FEM_KT(P, 8, false, false) FEM_KT(P, 16, true, true) FEM_KT(P, 16, false, true) FEM_KT(P, 8, true, true)          \
-    FEM_KT(P, 8, false, true)
+#define FEM_KT(P, RR, ST, LA_, PK_)                                                                                \
+    if (npe == P && R == RR && (store != 0) == ST && la == LA_ && pk == PK_)                                       \
+        hipLaunchKernelGGL((k_assemble_ke_tile3<P, RR, ST, LA_, PK_>), g, dim3(RR * 64), dyn, st, Ke, conn, inc_ptr,\
+                           inc, N, rowptr, colidx, slice_ptr, vals, Wc, ntiles);
+#define FEM_KT_LA(P, PK_) FEM_KT(P, 16, true, false, PK_) FEM_KT(P, 16, false, false, PK_)                          \
+    FEM_KT(P, 8, true, false, PK_) FEM_KT(P, 8, false, false, PK_) FEM_KT(P, 16, true, true, PK_)                    \
+    FEM_KT(P, 16, false, true, PK_) FEM_KT(P, 8, true, true, PK_) FEM_KT(P, 8, false, true, PK_)
+#define FEM_KT_ALL(P) FEM_KT_LA(P, false) FEM_KT_LA(P, true)
     FEM_KT_ALL(4) FEM_KT_ALL(6) FEM_KT_ALL(8) FEM_KT_ALL(10)
 #undef FEM_KT_ALL
+#undef FEM_KT_LA
 #undef FEM_KT
     FEM_LAUNCHED();
     *done = true;
@@ -2424,6 +2511,25 @@ int fem_assemble_from_ke_sl(const double* Ke, const int64_t* conn, int npe, cons
                                   S(stream), &done, true);
     if (rc == FEM_OK && !done) {
         set_error("fem_assemble_from_ke_sl: tile form not launched");
+        return FEM_EARG;
+    }
+    return rc;
+}
+
+int fem_assemble_from_ke_sym(const double* Kp, const int64_t* conn, int npe, const int32_t* inc_ptr,
+                             const int32_t* inc, int64_t N, const int32_t* rowptr, const int32_t* colidx,
+                             const int64_t* slice_ptr, int store, int max_width, int layout_a, double* vals,
+                             fem_stream_t stream) {
+    if (N <= 0) return FEM_OK;
+    if (!(npe == 4 || npe == 6 || npe == 8 || npe == 10) || max_width <= 0) {
+        set_error("fem_assemble_from_ke_sym: npe 4/6/8/10 and the pattern width required");
+        return FEM_EARG;
+    }
+    bool done = false;
+    const int rc = ke_tile_launch(Kp, conn, npe, inc_ptr, inc, N, rowptr, colidx, slice_ptr, store, max_width, vals,
+                                  S(stream), &done, layout_a != 0, true);
+    if (rc == FEM_OK && !done) {
+        set_error("fem_assemble_from_ke_sym: tile form not launched");
         return FEM_EARG;
     }
     return rc;

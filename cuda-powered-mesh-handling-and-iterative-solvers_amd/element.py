@@ -378,6 +378,33 @@ def _iso_ke(coords, elements, etype, E, nu, points, weights, mode, device, dtype
     return _out(K, device, dtype)
 
 
+def _solid_ke_sym(coords, elements, element_type, E, nu, device="cuda:0"):
+    """Internal assembly path of configs[4]: `compute_K_matrix(..., single=True)` of c3d6 / c3d8 / c3d10 (default
+    rules; `solver/element.py:1754-1803`, `:2631-2676`, `:1191-1239`) in the packed symmetric form -- only the upper
+    3x3 blocks, [M, fem_ke_sym_stride(npe)] fp64 on the device (include/fem355.h fem_iso_ke_sym), for
+    `system.SellMatrix.add_element_matrices_sym`. The upper blocks are compute_K_matrix's bit for bit."""
+    et = element_type.lower()
+    if et not in ("c3d6", "c3d8", "c3d10"):
+        _unsupported(element_type)
+    lib = C.lib()
+    dev, coords, elements = _prep(coords, elements, device)
+    npe = _ISO[et][0]
+    if elements.shape[1] != npe:
+        raise ValueError(f"{et} expects {npe} nodes per element, got {elements.shape[1]}")
+    if et == "c3d6":   # single=True: B at (1/3, 1/3, 0) times the wedge volume (`solver/element.py:2656-2659`)
+        p, w, mode = torch.tensor([[1 / 3, 1 / 3, 0.0]], dtype=F64), torch.ones(1, dtype=F64), C.ISO_VOLUME
+    else:
+        (p, w), mode = _points_weights(et, None), C.ISO_SUM
+    dN = _dn_table(et, p, dev)
+    wh = w.detach().to("cpu", F64).contiguous()
+    wd = _dev_const(("w", wh.numpy().tobytes()), lambda: wh, dev)
+    M = elements.shape[0]
+    Kp = torch.empty((M, int(lib.fem_ke_sym_stride(npe))), dtype=F64, device=dev)
+    C.check(lib.fem_iso_ke_sym(C.ptr(coords), C.ptr(elements), M, npe, float(E), float(nu), C.ptr(dN), C.ptr(wd),
+                               dN.shape[0], mode, C.ptr(Kp), C.stream(dev)), "fem_iso_ke_sym")
+    return Kp
+
+
 def _iso_mass(coords, elements, etype, rho, device, dtype, scalar=False):
     lib = C.lib()
     dev, coords, elements = _prep(coords, elements, device)

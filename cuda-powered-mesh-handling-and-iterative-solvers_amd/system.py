@@ -432,6 +432,39 @@ class SellMatrix:
                                              C.stream(self.device)), "fem_assemble_from_ke_ex2")
         return self
 
+    def add_element_matrices_sym(self, Kp: torch.Tensor, elements: torch.Tensor, inc=None):
+        """vals += coalesce(P_e^T K_e P_e) from the packed symmetric K_e of `element._solid_ke_sym` (bs = 3: upper
+        blocks only, the lower ones read as their transposes; include/fem355.h fem_assemble_from_ke_sym) -- the
+        configs[4] internal path: about half the element-matrix bytes written and read. Same sums in the same order
+        as `add_element_matrices` of the full K_e whose lower blocks mirror its upper ones."""
+        lib = C.lib()
+        if self.bs != 3 or self.g.max_width <= 0:
+            raise ValueError("packed K_e assembly: bs = 3 with the pattern's slice width (tile form)")
+        elements = elements.contiguous()
+        npe = elements.shape[1]
+        if Kp.dtype != F64 or Kp.dim() != 2 or Kp.shape[1] != int(lib.fem_ke_sym_stride(npe)):
+            raise ValueError(f"packed K_e must be fp64 [M, {int(lib.fem_ke_sym_stride(npe))}]")
+        Kp = Kp.contiguous()
+        inc_ptr, inc_ = inc if inc is not None else (
+            (self.g.inc_ptr, self.g.inc) if npe == self.g.npe and elements.shape[0] * npe == self.g.inc.numel()
+            else incidence(elements, self.g.n_nodes))
+        if self._sl_target():
+            store = self._fresh
+            self._fresh = False
+            out, la = self._svals_buf(), 1
+            self._sl_ok, self._plain_ok = True, False
+        else:
+            self._modify_plain()
+            store = self._fresh
+            self._fresh = False
+            self._plain_ok = True
+            out, la = self._vals, 0
+        C.check(lib.fem_assemble_from_ke_sym(C.ptr(Kp), C.ptr(elements), npe, C.ptr(inc_ptr), C.ptr(inc_),
+                                             self.g.n_nodes, C.ptr(self.g.rowptr), C.ptr(self.g.colidx),
+                                             C.ptr(self.g.slice_ptr), 1 if store else 0, self.g.max_width, la,
+                                             C.ptr(out), C.stream(self.device)), "fem_assemble_from_ke_sym")
+        return self
+
     def add_tet4(self, coords: torch.Tensor, elements: torch.Tensor, E: float, nu: float = 0.0):
         """vals += the c3d4 operator computed on the fly (bs=3: elasticity E, nu; bs=1: Poisson, kappa=E)."""
         lib = C.lib()

@@ -96,6 +96,14 @@ int fem_tet4_geom(const double* coords, const int64_t* conn, int64_t M, double* 
  * compute_c3d10_K_matrix (`:1191-1239`). */
 int fem_iso_ke(const double* coords, const int64_t* conn, int64_t M, int npe, double E, double nu,
                const double* dN, const double* w, int n_ip, int mode, double* Ke, fem_stream_t stream);
+/* fem_iso_ke_sym: the same K_e (modes FEM_ISO_SUM / FEM_ISO_VOLUME) in the packed symmetric form of the internal
+ * assembly path: per element only the upper 3x3 blocks (a <= b), row-major over the upper triangle (block (a, b) at
+ * (a npe - a (a - 1) / 2 + b - a) * 9, entries r * 3 + c), fem_ke_sym_stride(npe) doubles per element (9 npe (npe + 1)
+ * / 2 rounded up to even: c3d10 496 of 900, c3d8 324 of 576, c3d6 190 of 324). The upper blocks equal fem_iso_ke's
+ * bit for bit. Consumed by fem_assemble_from_ke_sym; the reference-named functions keep the full [M, d, d]. */
+int fem_ke_sym_stride(int npe);
+int fem_iso_ke_sym(const double* coords, const int64_t* conn, int64_t M, int npe, double E, double nu,
+                   const double* dN, const double* w, int n_ip, int mode, double* Kp, fem_stream_t stream);
 /* fem_iso_mass: consistent mass of c3d8 / c3d6 / c3d10 (npe = 8 / 6 / 10) — no reference function exists (the
  * reference notebook calls a compute_c3d4_M_matrix defined nowhere, `solver_example.ipynb:221`): parity unpinned.
  *   Me[M, 3 npe, 3 npe], block (a,b) = rho sum_q w_q |detJ_q| N_a(q) N_b(q) I3
@@ -474,6 +482,15 @@ int fem_assemble_tet4_sl(const double* coords, const int64_t* conn, double E, do
 int fem_assemble_from_ke_sl(const double* Ke, const int64_t* conn, int npe, const int32_t* inc_ptr, const int32_t* inc,
                             int64_t N, const int32_t* rowptr, const int32_t* colidx, const int64_t* slice_ptr,
                             int store, int max_width, double* svals, fem_stream_t stream);
+/* bs = 3 assembly from packed symmetric K_e (fem_iso_ke_sym; the tile form of fem_assemble_from_ke_ex2 / _sl): block
+ * (a, b) read from the upper block, (b, a) from its transpose, in the same (incidence, b) order -- the same sums as
+ * from the full K_e whose lower blocks mirror the upper ones. layout_a = 1: vals is the bs = 3 solver layout (as
+ * fem_assemble_from_ke_sl), 0: the plain planes. Internal path of configs[4] (`solver/element.py:1191-1239,1754-1803`
+ * K_e, `subdivision.ipynb:118-139` COO assembly semantics). */
+int fem_assemble_from_ke_sym(const double* Kp, const int64_t* conn, int npe, const int32_t* inc_ptr,
+                             const int32_t* inc, int64_t N, const int32_t* rowptr, const int32_t* colidx,
+                             const int64_t* slice_ptr, int store, int max_width, int layout_a, double* vals,
+                             fem_stream_t stream);
 int fem_jacobi_sl(const double* svals, int bs, const int32_t* rowptr, const int32_t* diagpos,
                   const int64_t* slice_ptr, const int32_t* uoff, const int16_t* ucol, int64_t nrows,
                   const uint8_t* mask, double* w, fem_stream_t stream);

@@ -112,6 +112,44 @@ def test_isoparametric_vs_golden(gpu, etype):
         assert el.compute_hexahedral_volumes(c, e, device=gpu).dtype == torch.float32   # the reference's default
 
 
+@pytest.mark.parametrize("etype,n", [("c3d8", 7), ("c3d6", 6), ("c3d10", 4)])
+def test_packed_symmetric_ke_assembly(gpu, etype, n, monkeypatch):
+    """configs[4]'s internal path: K_e stored as its upper 3x3 blocks only
+    (`element._solid_ke_sym`, include/fem355.h fem_iso_ke_sym) equals compute_K_matrix's upper blocks bit for bit, and
+    the global matrix assembled from it (lower blocks read as transposes) equals the one assembled from the full K_e:
+    bit for bit for c3d10 (whose full K_e mirrors its upper blocks), to 1e-14 for c3d8 / c3d6 (their lower blocks are
+    formed directly, rounding in another order) -- stored first, then added on top, in the solver layout and in the
+    plain planes."""
+    el, mesh, _, system = _mods()
+    from fem355 import _capi as C
+    gen = {"c3d8": mesh.hex_box, "c3d6": mesh.wedge_box, "c3d10": mesh.tet10_cube}[etype]
+    c, e = gen(n, jitter=0.1)
+    c, e = c.to(gpu), e.to(gpu)
+    npe = e.shape[1]
+    K = el.compute_K_matrix(c, e, etype, E, NU, device=gpu, dtype=F64)
+    Kp = el._solid_ke_sym(c, e, etype, E, NU, device=gpu)
+    stride = int(C.lib().fem_ke_sym_stride(npe))
+    assert Kp.shape == (e.shape[0], stride) and stride == (9 * npe * (npe + 1) // 2 + 1) // 2 * 2
+    blocks = [(a, b) for a in range(npe) for b in range(a, npe)]
+    up = torch.stack([K[:, 3 * a:3 * a + 3, 3 * b:3 * b + 3].reshape(-1, 9) for a, b in blocks], 1).reshape(-1, 9 * len(blocks))
+    assert torch.equal(Kp[:, :up.shape[1]], up)
+    assert not Kp[:, up.shape[1]:].any()
+    g = system.build_graph(e, c.shape[0])
+    for sl in ("1", "0"):
+        monkeypatch.setenv("FEM355_SL", sl)
+        Af = system.SellMatrix(g, 3).add_element_matrices(K, e)
+        As = system.SellMatrix(g, 3).add_element_matrices_sym(Kp, e)
+        assert Af.solver_layout == As.solver_layout == (sl == "1")
+        for step in range(2):
+            vf, vs = Af.plain_values(), As.plain_values()
+            if etype == "c3d10":
+                assert torch.equal(vf, vs), (sl, step)
+            else:
+                assert rel(vs, vf) < 1e-14, (sl, step)
+            Af.add_element_matrices(K, e)
+            As.add_element_matrices_sym(Kp, e)
+
+
 # ------------------------------------------------------------------ L2 operators
 def test_ebe_operator_vs_golden(gpu):
     el, *_ = _mods()
