@@ -218,11 +218,22 @@ __device__ __forceinline__ void mf_element(const double xc[4][3], const double x
     }
 }
 
+// FEM_MF_ELC = 1 (default): the element vectors of a pass staged [element][corner][component] (one element's 4 BS
+// values contiguous: its thread stores them as 16-byte writes, a node's pair read is one 16-byte and one 8-byte LDS
+// read for BS = 3 instead of three 8-byte reads 2 KB apart); 0: [corner * BS + component][element] (rounds 4-5).
+// Corner 0 staged either way (FC = 4 only).
+#ifndef FEM_MF_ELC
+#define FEM_MF_ELC 1
+#endif
+template <int FC>
+constexpr bool mf_elc() { return FEM_MF_ELC && FC == 4; }
+
 // LDS of one chunk application (a local node's pair range [lp, lp1) travels in its thread's registers)
 template <int BS, int FC>
 struct MfLds {
     double nd[MF_NC][3 + BS];        // per local node: coordinates, then x (rows 16-byte aligned: 48 / 32 bytes)
-    double fs[FC * BS][MF_PASS];     // element vectors of the current pass: [staged corner * BS + c][element]
+    // element vectors of the current pass: [staged corner * BS + c][element], or (mf_elc) fe[element][corner][c]
+    alignas(16) double fs[FC * BS][MF_PASS];
     alignas(16) uint16_t ent[4 * MF_EC];   // the chunk's pairs, node-major
 };
 
@@ -230,6 +241,22 @@ struct MfLds {
 template <int BS, int FC>
 __device__ __forceinline__ void mf_pair_value(const MfLds<BS, FC>& L, int pe, int h, double v[BS]) {
     const int el = (pe >> 2) - h, b = pe & 3;
+    if constexpr (mf_elc<FC>()) {
+        const double* fe = &L.fs[0][0];
+        const int base = (el * 4 + b) * BS;
+        if constexpr (BS == 3) {   // 24 bytes at 8 (mod 16) when b is odd: the 16-byte read one double later
+            const int odd = b & 1;
+            const double2 d = *reinterpret_cast<const double2*>(fe + base + odd);
+            const double sgl = fe[base + (odd ? 0 : 2)];
+            v[0] = odd ? sgl : d.x;
+            v[1] = odd ? d.x : d.y;
+            v[2] = odd ? d.y : sgl;
+        } else {
+#pragma unroll
+            for (int q = 0; q < BS; ++q) v[q] = fe[base + q];
+        }
+        return;
+    }
     if (FC == 3 && b == 0) {
 #pragma unroll
         for (int q = 0; q < BS; ++q) v[q] = -(L.fs[q][el] + L.fs[BS + q][el] + L.fs[2 * BS + q][el]);
@@ -391,10 +418,21 @@ __device__ __forceinline__ bool mf_step(const MfOp& op, const double* __restrict
 #else
             mf_element<BS, MODE>(xc, xv, op.lam, op.mu, op.kappa, f);
 #endif
+            if constexpr (mf_elc<FC>()) {   // the element's 4 BS values contiguous (16-byte stores)
+                double2* fe2 = reinterpret_cast<double2*>(&L.fs[0][0] + tid * 4 * BS);
+                double fl[4 * BS];
 #pragma unroll
-            for (int b = 4 - FC; b < 4; ++b)
+                for (int b = 0; b < 4; ++b)
 #pragma unroll
-                for (int q = 0; q < BS; ++q) L.fs[(b - (4 - FC)) * BS + q][tid] = f[b][q];
+                    for (int q = 0; q < BS; ++q) fl[b * BS + q] = f[b][q];
+#pragma unroll
+                for (int t = 0; t < 2 * BS; ++t) fe2[t] = make_double2(fl[2 * t], fl[2 * t + 1]);
+            } else {
+#pragma unroll
+                for (int b = 4 - FC; b < 4; ++b)
+#pragma unroll
+                    for (int q = 0; q < BS; ++q) L.fs[(b - (4 - FC)) * BS + q][tid] = f[b][q];
+            }
         }
         __syncthreads();
         // every local node adds its pairs of this pass in ascending (element, corner) order; the pair reads of

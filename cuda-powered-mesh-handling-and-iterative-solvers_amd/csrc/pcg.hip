@@ -1248,17 +1248,6 @@ __device__ __forceinline__ void cg1_commit(PcgState* st, const Cg1Step& k, doubl
     st->iter = k.it + 1;
 }
 
-// the slot sum of component c of local node a (ascending chunk order: k_mf_gather's sum, the same bits)
-template <int BS>
-__device__ __forceinline__ double mf_node_sum(const MfOp& op, const double* __restrict__ slots, int64_t a, int c) {
-    const int k0 = op.nptr[a], k1 = op.nptr[a + 1];
-    double s = 0.0;
-    for (int kk = k0; kk < k1; ++kk) s += slots[(op.spos ? kk : op.nslot[kk]) * BS + c];
-    return s;
-}
-
-// MF: the element-chunk operator -- v of the dof formed here from the operator's slots (mf_node_sum), never stored
-template <bool MF = false>
 __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_update(int64_t n, int bs, double* __restrict__ x,
                                                           double* __restrict__ r, double* __restrict__ p,
                                                           double* __restrict__ sv, double* __restrict__ u,
@@ -1267,7 +1256,7 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_update(int64_t n, int bs, dou
                                                           const int32_t* __restrict__ ipos,
                                                           const uint8_t* __restrict__ own, PcgState* __restrict__ st,
                                                           RedBuf red, P2PArgs xp, const double* __restrict__ send,
-                                                          int64_t off, MfOp op = MfOp{}, const double* slots = nullptr) {
+                                                          int64_t off) {
     __shared__ double lds4[4];
     __shared__ int flag;
     const Cg1Step k = cg1_eval(st, cg1_scalar(recv, send, off, 0, xp), cg1_scalar(recv, send, off, 1, xp));
@@ -1278,10 +1267,7 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_update(int64_t n, int bs, dou
     for (int64_t i = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * PCG_BLOCK) {
         const int64_t node = i / bs;
         const int32_t j = ipos ? ipos[node] : -1;
-        double vi;
-        if constexpr (MF) vi = bs == 3 ? mf_node_sum<3>(op, slots, node, (int)(i - node * 3))
-                                       : mf_node_sum<1>(op, slots, node, 0);
-        else vi = v[i];
+        double vi = v[i];
         if (j >= 0) {
             const int c = (int)(i - node * bs);
             if (xp.P) {   // rank-ordered sum of the partials (own partial = the local row itself)
@@ -1951,41 +1937,30 @@ __global__ void __launch_bounds__(MF_BLOCK) k_pcg_mf_dot(MfOp op, const double* 
 
 // Distributed single-reduction iteration on the element-chunk operator (BASELINE configs[3] as north_star puts it:
 // element partitions, the rank's own elements formed in every application, the halo-DOF partials exchanged inside the
-// iteration). Replaces k_cg1_spmv's SpMV by two launches:
-//   k_cg1_mf_slots : the rank's chunks into its slots (v = A_r u, never a matrix) AND d = u.v over all local rows
-//                    (sum over the slots of u_node . slot: the rank partial of the operator sum, as k_cg1_spmv's)
-//                    by one grid reduction -> st->red[0];
-//   k_cg1_mf_iface : the interface rows only -- their slot sums packed for the exchange -- and [g, d]; its last
-//                    block commits the step.
-// k_cg1_update then forms v of every node from the slots itself (k_cg1_update<true>): no v vector is written or read,
-// and at world size 1 (no interface rows) the pack kernel is a single tail. Round 5 ran a gather over every node
-// (v stored, d reduced there) between the two: at the N = 8 rank share 11.7 us of its 56.8 us iteration.
+// iteration). Replaces k_cg1_spmv's SpMV by two launches: the rank's chunks into its slots (v = A_r u, never a matrix),
+// then the slot gather -- v per local node in ascending chunk order, d = u.v over all local rows (the rank partials of
+// an operator sum, as k_cg1_spmv's), the interface rows packed for the exchange, the step committed by the last block.
+// k_cg1_update then reads v like the assembled path's q.
 template <int BS>
 __global__ void __launch_bounds__(MF_BLOCK) k_cg1_mf_slots(MfOp op, const double* __restrict__ u,
-                                                           double* __restrict__ slots, PcgState* __restrict__ st,
+                                                           double* __restrict__ slots, const PcgState* __restrict__ st,
                                                            int always, P2PArgs xp, const double* __restrict__ recv,
-                                                           const double* __restrict__ send, int64_t off, RedBuf red) {
-    __shared__ MfKernelLds<BS, MF_DOT> L;
-    __shared__ double lds4[MF_BLOCK / 64];
-    __shared__ int flag;
-    if (!always) {   // the step of this pass, from the unchanged state (committed by k_cg1_mf_iface)
+                                                           const double* __restrict__ send, int64_t off) {
+    __shared__ MfKernelLds<BS, MF_APPLY> L;
+    if (!always) {   // the step of this pass, from the unchanged state (committed by k_cg1_mf_gather)
         const Cg1Step k = cg1_eval(st, cg1_scalar(recv, send, off, 0, xp), cg1_scalar(recv, send, off, 1, xp));
         if (!k.go) return;
     }
-    double dot = mf_walk_any<BS, MF_DOT>(op, u, slots, L);
-    dot = block_sum<MF_BLOCK>(dot, lds4);
-    double d;
-    if (reduce_grid<MF_BLOCK>(dot, red.part(RED_K1), red.cnt(RED_K1), &d, lds4, &flag) && threadIdx.x == 0)
-        st->red[0] = d;
+    (void)mf_walk_any<BS, MF_APPLY>(op, u, slots, L);
 }
 
 template <int BS>
-__global__ void __launch_bounds__(PCG_BLOCK) k_cg1_mf_iface(MfOp op, const double* __restrict__ slots,
-                                                            const int32_t* __restrict__ imap, int64_t nI,
-                                                            double* __restrict__ send, int64_t off,
-                                                            PcgState* __restrict__ st, RedBuf red, int always,
-                                                            P2PArgs xp, const double* __restrict__ recv, double* hist,
-                                                            int64_t hist_len) {
+__global__ void __launch_bounds__(PCG_BLOCK) k_cg1_mf_gather(MfOp op, const double* __restrict__ slots,
+                                                             const double* __restrict__ u, double* __restrict__ v,
+                                                             const int32_t* __restrict__ ipos, double* __restrict__ send,
+                                                             int64_t off, PcgState* __restrict__ st, RedBuf red,
+                                                             int always, P2PArgs xp, const double* __restrict__ recv,
+                                                             double* hist, int64_t hist_len) {
     __shared__ double lds4[4];
     __shared__ int flag;
     Cg1Step k{};
@@ -1996,26 +1971,40 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_mf_iface(MfOp op, const doubl
             return;
         }
     }
-    for (int64_t j = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; j < nI; j += (int64_t)gridDim.x * PCG_BLOCK) {
-        const int32_t a = imap[j];
-        if (a < 0) continue;   // an interface node of other ranks only (send keeps its zeros)
+    double dot = 0.0;
+    for (int64_t a = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; a < op.nnodes;
+         a += (int64_t)gridDim.x * PCG_BLOCK) {
+        double o[BS];
+#pragma unroll
+        for (int c = 0; c < BS; ++c) o[c] = 0.0;
+        const int k0 = op.nptr[a], k1 = op.nptr[a + 1];
+        for (int kk = k0; kk < k1; ++kk) {
+            const int64_t sl = op.spos ? kk : op.nslot[kk];
+#pragma unroll
+            for (int c = 0; c < BS; ++c) o[c] += slots[sl * BS + c];
+        }
+        const int32_t j = ipos ? ipos[a] : -1;
 #pragma unroll
         for (int c = 0; c < BS; ++c) {
-            const double o = mf_node_sum<BS>(op, slots, a, c);
-            if (xp.P) {   // straight into every peer's message slot for this node
-                for (int r = 0; r < xp.P; ++r) {
-                    const int dst = xp.csrc[j * xp.P + r];
-                    if (dst >= 0) xp.psend[dst + c] = o;
+            v[a * BS + c] = o[c];
+            dot += u[a * BS + c] * o[c];
+            if (j >= 0) {
+                if (xp.P) {   // straight into every peer's message slot for this node
+                    for (int r = 0; r < xp.P; ++r) {
+                        const int dst = xp.csrc[(int64_t)j * xp.P + r];
+                        if (dst >= 0) xp.psend[dst + c] = o[c];
+                    }
+                } else {
+                    send[(int64_t)j * BS + c] = o[c];
                 }
-            } else {
-                send[j * BS + c] = o;
             }
         }
     }
-    double unused;   // the grid reduction as a completion count: its last block packs [g, d] and commits
-    if (reduce_grid(0.0, red.part(RED_INIT), red.cnt(RED_INIT), &unused, lds4, &flag) && threadIdx.x == 0) {
+    dot = block_sum256(dot, lds4);
+    double d;
+    if (reduce_grid(dot, red.part(RED_K1), red.cnt(RED_K1), &d, lds4, &flag) && threadIdx.x == 0) {
         if (!always) cg1_commit(st, k, hist, hist_len);   // every block of the three kernels has read the state
-        const double d = st->red[0];
+        st->red[0] = d;
         send[off] = st->red[1];
         send[off + 1] = d;
         for (int r = 0; r < xp.P; ++r) {
@@ -2134,7 +2123,7 @@ static P2PArgs p2p_args(const fem_pcg* s) {
 static int cg1_spmv(fem_pcg* s, int always) {
     const int64_t off = s->nI * s->bs;
     const int32_t* ipos = s->nI > 0 ? s->ipos : nullptr;
-    if (s->mf) {   // element-chunk operator: the rank's chunks into the context's slots (+ d), the interface pack
+    if (s->mf) {   // element-chunk operator: the rank's chunks into the context's slots, then the slot gather
         const MfOp op = mf_op(s->mf);
         const P2PArgs xp = p2p_args(s);
         if (op.nchunks > 0) {
@@ -2142,22 +2131,21 @@ static int cg1_spmv(fem_pcg* s, int always) {
             const int G = mf_resident_grid(fn, MF_BLOCK, op.nchunks);
             if (s->bs == 3)
                 hipLaunchKernelGGL(k_cg1_mf_slots<3>, dim3(G), dim3(MF_BLOCK), 0, s->stream, op, s->cg1_u, s->mf_sl,
-                                   s->st, always, xp, s->cg1_recv, s->cg1_send, off, s->red);
+                                   s->st, always, xp, s->cg1_recv, s->cg1_send, off);
             else
                 hipLaunchKernelGGL(k_cg1_mf_slots<1>, dim3(G), dim3(MF_BLOCK), 0, s->stream, op, s->cg1_u, s->mf_sl,
-                                   s->st, always, xp, s->cg1_recv, s->cg1_send, off, s->red);
+                                   s->st, always, xp, s->cg1_recv, s->cg1_send, off);
             FEM_LAUNCHED();
-        } else {   // no element on this rank: d = 0
-            FEM_HIP(hipMemsetAsync(st_red(s, 0), 0, sizeof(double), s->stream));
         }
-        const int Gi = grid_multiple_of_xcd(cdiv(s->nI > 0 ? s->nI : 1, PCG_BLOCK), 1024);
-        const int32_t* imap = s->nI > 0 ? s->imap : nullptr;
+        const int Gg = grid_multiple_of_xcd(cdiv(s->nrows, PCG_BLOCK), 1024);
         if (s->bs == 3)
-            hipLaunchKernelGGL(k_cg1_mf_iface<3>, dim3(Gi), dim3(PCG_BLOCK), 0, s->stream, op, s->mf_sl, imap, s->nI,
-                               s->cg1_send, off, s->st, s->red, always, xp, s->cg1_recv, s->hist, s->hist_len);
+            hipLaunchKernelGGL(k_cg1_mf_gather<3>, dim3(Gg), dim3(PCG_BLOCK), 0, s->stream, op, s->mf_sl, s->cg1_u,
+                               s->q, ipos, s->cg1_send, off, s->st, s->red, always, xp, s->cg1_recv, s->hist,
+                               s->hist_len);
         else
-            hipLaunchKernelGGL(k_cg1_mf_iface<1>, dim3(Gi), dim3(PCG_BLOCK), 0, s->stream, op, s->mf_sl, imap, s->nI,
-                               s->cg1_send, off, s->st, s->red, always, xp, s->cg1_recv, s->hist, s->hist_len);
+            hipLaunchKernelGGL(k_cg1_mf_gather<1>, dim3(Gg), dim3(PCG_BLOCK), 0, s->stream, op, s->mf_sl, s->cg1_u,
+                               s->q, ipos, s->cg1_send, off, s->st, s->red, always, xp, s->cg1_recv, s->hist,
+                               s->hist_len);
         FEM_LAUNCHED();
         if (!s->comm && s->p2p) return FEM_OK;
         if (!s->comm)
@@ -2185,14 +2173,9 @@ static int cg1_spmv(fem_pcg* s, int always) {
 }
 
 static int cg1_step_update(fem_pcg* s) {
-    if (s->mf)   // v of every dof from the operator's slots (k_cg1_mf_slots wrote them; no v vector)
-        hipLaunchKernelGGL(k_cg1_update<true>, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->bs, s->x,
-                           s->r, s->p0, s->cg1_s, s->cg1_u, s->q, s->w, s->cg1_recv, s->nI > 0 ? s->ipos : nullptr,
-                           s->own, s->st, s->red, p2p_args(s), s->cg1_send, s->nI * s->bs, mf_op(s->mf), s->mf_sl);
-    else
-        hipLaunchKernelGGL(k_cg1_update<false>, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->bs, s->x,
-                           s->r, s->p0, s->cg1_s, s->cg1_u, s->q, s->w, s->cg1_recv, s->nI > 0 ? s->ipos : nullptr,
-                           s->own, s->st, s->red, p2p_args(s), s->cg1_send, s->nI * s->bs);
+    hipLaunchKernelGGL(k_cg1_update, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->bs, s->x, s->r, s->p0,
+                       s->cg1_s, s->cg1_u, s->q, s->w, s->cg1_recv, s->nI > 0 ? s->ipos : nullptr, s->own, s->st,
+                       s->red, p2p_args(s), s->cg1_send, s->nI * s->bs);
     FEM_LAUNCHED();
     return FEM_OK;
 }

@@ -753,7 +753,7 @@ def rccl_measure(a, kind, comm, rank, world, dev, tdist, metric, operator="assem
                            "pupdate": ms[2] / max(cnt[2], 1)}),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                          "frac": achieved / 8000.0, "traffic": None,
-                         "kernel": ("k_cg1_mf_slots + k_cg1_mf_iface" if mf else
+                         "kernel": ("k_cg1_mf_slots + k_cg1_mf_gather" if mf else
                                     "k_cg1_spmv" if variant else "k_pcg_spmv_dot") + " (rank 0 local)",
                          "algorithmic_bytes": alg, "stream_ceiling_GBps": ceiling,
                          "frac_of_stream_read": achieved / ceiling["read"]},

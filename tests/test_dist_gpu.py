@@ -65,7 +65,7 @@ def test_partition_group_matches_single_gpu(gpu, kind, P, variant, exchange, fus
 @pytest.mark.parametrize("kind,P", [("poisson", 2), ("poisson", 8), ("elastic", 3), ("elastic", 8)])
 def test_partition_group_matfree_matches_single_gpu(gpu, kind, P, exchange):
     """The element-chunk operator under the element partition (north_star's configs[3] design): every rank forms its
-    own elements' products from the coordinates (k_cg1_mf_slots + k_cg1_mf_iface, no matrix), the interface rows
+    own elements' products from the coordinates (k_cg1_mf_slots + k_cg1_mf_gather, no matrix), the interface rows
     travel in the single-reduction exchange. Against the single-GPU assembled solve: Jacobi on every local row,
     solution 1e-10, iterations +-2, shared copies bit-identical; the other variants are refused."""
     import fem355  # noqa: F401
@@ -181,7 +181,7 @@ def test_config3_elasticity_10m_eight_partitions_matfree_vs_oracle(gpu, cube119)
     """configs[3] as north_star states it, on one GPU: the 10,110,954-tet elasticity system over 8 RCB element
     partitions, every rank's operator the element-chunk product of ITS OWN elements (no assembled matrix anywhere),
     the halo-summed exact Jacobi, and the single-reduction iteration with the neighbour exchange (k_cg1_mf_slots /
-    k_cg1_mf_iface / k_cg1_update, p2p slots delivered in-process). Against the oracle: (a) the ranks' local products
+    k_cg1_mf_gather / k_cg1_update, p2p slots delivered in-process). Against the oracle: (a) the ranks' local products
     summed over their global node ids = the reference's EBE product (`solver/element.py:429-464`) at 1e-12; Jacobi =
     the oracle's at 1e-13; (b) 5 fixed iterations = the oracle PCG's 5th iterate (`solver/solver.py:766-812`) at
     1e-10; (c) copies of shared nodes bit-identical on every rank."""
