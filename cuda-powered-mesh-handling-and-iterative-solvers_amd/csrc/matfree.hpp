@@ -218,12 +218,13 @@ __device__ __forceinline__ void mf_element(const double xc[4][3], const double x
     }
 }
 
-// FEM_MF_ELC = 1 (default): the element vectors of a pass staged [element][corner][component] (one element's 4 BS
-// values contiguous: its thread stores them as 16-byte writes, a node's pair read is one 16-byte and one 8-byte LDS
-// read for BS = 3 instead of three 8-byte reads 2 KB apart); 0: [corner * BS + component][element] (rounds 4-5).
-// Corner 0 staged either way (FC = 4 only).
+// FEM_MF_ELC = 1 (A/B): the element vectors of a pass staged [element][corner][component] (one
+// element's 4 BS values contiguous: its thread stores them as 16-byte writes, a node's pair read is one 16-byte and
+// one 8-byte LDS read for BS = 3 instead of three 8-byte reads 2 KB apart). Measured slower on the 10M elastic cube:
+// chunk kernel 220.4 / 221.3 vs 195.9 / 196.9 us (profiles/r06f_mf_elc_ab.txt): the select between the two read
+// shapes costs VALU and the 16-byte reads at 24-byte strides conflict more; 0 (default): [corner * BS + c][element].
 #ifndef FEM_MF_ELC
-#define FEM_MF_ELC 1
+#define FEM_MF_ELC 0
 #endif
 template <int FC>
 constexpr bool mf_elc() { return FEM_MF_ELC && FC == 4; }
