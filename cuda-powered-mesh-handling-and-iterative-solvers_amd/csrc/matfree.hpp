@@ -230,11 +230,29 @@ template <int FC>
 constexpr bool mf_elc() { return FEM_MF_ELC && FC == 4; }
 
 // LDS of one chunk application (a local node's pair range [lp, lp1) travels in its thread's registers)
+// FEM_MF_NDSKEW = 1 (default): the local-node rows of nd skewed by one 16-byte unit every 16 rows. A row is 3 (BS = 3)
+// or 2 (BS = 1) 16-byte units, so rows l and l + 16 (or l + 8) start in the same 16-byte bank group, and the element
+// lanes' corner reads (16-byte reads of structured local ids: cube neighbours 1, k, k^2 apart) collide there
+#ifndef FEM_MF_NDSKEW
+#define FEM_MF_NDSKEW 1
+#endif
 template <int BS, int FC>
 struct MfLds {
-    double nd[MF_NC][3 + BS];        // per local node: coordinates, then x (rows 16-byte aligned: 48 / 32 bytes)
-    // element vectors of the current pass: [staged corner * BS + c][element], or (mf_elc) fe[element][corner][c]
-    alignas(16) double fs[FC * BS][MF_PASS];
+    static constexpr int NDU = (3 + BS) / 2;   // 16-byte units per node row
+    // per local node: coordinates, then x (rows of NDU 16-byte units; row l at unit l NDU (+ l / 16 skewed))
+    double2 ndu[MF_NC * NDU + (FEM_MF_NDSKEW ? MF_NC / 16 + 1 : 0)];
+    __device__ __forceinline__ double2* nd_row(int l) { return ndu + l * NDU + (FEM_MF_NDSKEW ? (l >> 4) : 0); }
+    __device__ __forceinline__ const double2* nd_row(int l) const {
+        return ndu + l * NDU + (FEM_MF_NDSKEW ? (l >> 4) : 0);
+    }
+    // element vectors of the current pass: [staged corner * BS + c][element], or (mf_elc) fe[element][corner][c].
+    // Row stride MF_PASS + FEM_MF_FSPAD (default 1): the node sums' lanes read the corners of SHARED elements in the
+    // same step -- same element, rows 3 apart -- which a stride of 256 doubles (= 0 mod the 32 eight-byte bank pairs)
+    // put into one bank; an odd stride spreads them
+#ifndef FEM_MF_FSPAD
+#define FEM_MF_FSPAD 1
+#endif
+    alignas(16) double fs[FC * BS][MF_PASS + FEM_MF_FSPAD];
     alignas(16) uint16_t ent[4 * MF_EC];   // the chunk's pairs, node-major
 };
 
@@ -351,9 +369,9 @@ __device__ __forceinline__ bool mf_step(const MfOp& op, const double* __restrict
     const bool own = tn < cur.nn && tid % MF_LPN == 0;   // the lane that installs and stores the node
     if (own) {
 #pragma unroll
-        for (int q = 0; q < 3; ++q) L.nd[tn][q] = cur.xv[q];
+        for (int q = 0; q < 3; ++q) reinterpret_cast<double*>(L.nd_row(tn))[q] = cur.xv[q];
 #pragma unroll
-        for (int q = 0; q < BS; ++q) L.nd[tn][3 + q] = cur.pv[q];
+        for (int q = 0; q < BS; ++q) reinterpret_cast<double*>(L.nd_row(tn))[3 + q] = cur.pv[q];
     }
     if (8 * tid < 4 * cur.ne) reinterpret_cast<mf_u32x4*>(L.ent)[tid] = cur.ent;
     // issue order: every load a later wait needs has the same younger loads behind it on every path (the prologue's
@@ -397,7 +415,7 @@ __device__ __forceinline__ bool mf_step(const MfOp& op, const double* __restrict
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
                 const int l = (w >> (8 * b)) & 0xff;
-                const double2* r = reinterpret_cast<const double2*>(&L.nd[l][0]);
+                const double2* r = L.nd_row(l);
                 const double2 a0 = r[0], a1 = r[1];
                 xc[b][0] = a0.x;
                 xc[b][1] = a0.y;
