@@ -230,11 +230,11 @@ template <int FC>
 constexpr bool mf_elc() { return FEM_MF_ELC && FC == 4; }
 
 // LDS of one chunk application (a local node's pair range [lp, lp1) travels in its thread's registers)
-// FEM_MF_NDSKEW = 1 (default): the local-node rows of nd skewed by one 16-byte unit every 16 rows. A row is 3 (BS = 3)
-// or 2 (BS = 1) 16-byte units, so rows l and l + 16 (or l + 8) start in the same 16-byte bank group, and the element
-// lanes' corner reads (16-byte reads of structured local ids: cube neighbours 1, k, k^2 apart) collide there
+// FEM_MF_NDSKEW = 1 (A/B): the local-node rows of nd skewed by one 16-byte unit every 16 rows (a row is 3 (BS = 3) or
+// 2 (BS = 1) 16-byte units, so rows l and l + 16 start in the same 16-byte bank group). Measured slower on the 10M
+// elastic cube: chunk kernel 185-186 vs 179-180 us (profiles/r06h_mf_ndskew_ab.txt); off
 #ifndef FEM_MF_NDSKEW
-#define FEM_MF_NDSKEW 1
+#define FEM_MF_NDSKEW 0
 #endif
 template <int BS, int FC>
 struct MfLds {

@@ -688,12 +688,36 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update2(int64_t n, double* __
 #ifndef FEM_MF_NTL
 #define FEM_MF_NTL 0   // 1: the merged update reads the slots with non-temporal loads (read once)
 #endif
+// The first MF_QK slots of the node are loaded unconditionally (indices clamped to the node's last slot) and the ones
+// past its count added as +0.0 -- the same bits (a sum started from +0.0 is never -0.0, and x + 0.0 == x otherwise),
+// but the loads of all the thread's register-cached steps go out together instead of one dependent loop per dof
+// (nodes have 2.06 slots on average on the 10M cube; more than MF_QK continue in a loop)
+constexpr int MF_QK = 4;
+#ifndef FEM_MF_QK_ON
+#define FEM_MF_QK_ON 1   // 0: the plain loop (A/B)
+#endif
 template <int BS>
 __device__ __forceinline__ double mf_q_dof(const MfOp& op, const double* __restrict__ slots, int64_t d) {
     const int64_t a = d / BS;
     const int c = (int)(d - a * BS);
     const int k0 = op.nptr[a], k1 = op.nptr[a + 1];
     double s = 0.0;
+    if (FEM_MF_QK_ON && op.spos && k1 > k0) {   // node-major slots: the node's slots are k0 .. k1 - 1
+        double v[MF_QK];
+#pragma unroll
+        for (int q = 0; q < MF_QK; ++q) {
+            const int k = k0 + q < k1 ? k0 + q : k1 - 1;
+#if FEM_MF_NTL
+            v[q] = __builtin_nontemporal_load(&slots[(int64_t)k * BS + c]);
+#else
+            v[q] = slots[(int64_t)k * BS + c];
+#endif
+        }
+#pragma unroll
+        for (int q = 0; q < MF_QK; ++q) s += k0 + q < k1 ? v[q] : 0.0;
+        for (int k = k0 + MF_QK; k < k1; ++k) s += slots[(int64_t)k * BS + c];
+        return s;
+    }
     for (int k = k0; k < k1; ++k) {
         const int64_t sl = op.spos ? k : op.nslot[k];
 #if FEM_MF_NTL
