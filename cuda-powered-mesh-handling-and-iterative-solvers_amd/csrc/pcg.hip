@@ -2002,10 +2002,27 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_mf_gather(MfOp op, const doub
 #pragma unroll
         for (int c = 0; c < BS; ++c) o[c] = 0.0;
         const int k0 = op.nptr[a], k1 = op.nptr[a + 1];
-        for (int kk = k0; kk < k1; ++kk) {
-            const int64_t sl = op.spos ? kk : op.nslot[kk];
+        if (FEM_MF_QK_ON && op.spos && k1 > k0) {   // the update's fixed-count loads (mf_q_dof): the same bits
+            double v[MF_QK][BS];
 #pragma unroll
-            for (int c = 0; c < BS; ++c) o[c] += slots[sl * BS + c];
+            for (int q = 0; q < MF_QK; ++q) {
+                const int k = k0 + q < k1 ? k0 + q : k1 - 1;
+#pragma unroll
+                for (int c = 0; c < BS; ++c) v[q][c] = slots[(int64_t)k * BS + c];
+            }
+#pragma unroll
+            for (int q = 0; q < MF_QK; ++q)
+#pragma unroll
+                for (int c = 0; c < BS; ++c) o[c] += k0 + q < k1 ? v[q][c] : 0.0;
+            for (int kk = k0 + MF_QK; kk < k1; ++kk)
+#pragma unroll
+                for (int c = 0; c < BS; ++c) o[c] += slots[(int64_t)kk * BS + c];
+        } else {
+            for (int kk = k0; kk < k1; ++kk) {
+                const int64_t sl = op.spos ? kk : op.nslot[kk];
+#pragma unroll
+                for (int c = 0; c < BS; ++c) o[c] += slots[sl * BS + c];
+            }
         }
         const int32_t j = ipos ? ipos[a] : -1;
 #pragma unroll
