@@ -1272,6 +1272,8 @@ __device__ __forceinline__ void cg1_commit(PcgState* st, const Cg1Step& k, doubl
     st->iter = k.it + 1;
 }
 
+// Every vector read and written as 16-byte lanes (a double2 of dofs per thread-step; round 5: one 8-byte dof per
+// thread), the per-dof arithmetic unchanged
 __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_update(int64_t n, int bs, double* __restrict__ x,
                                                           double* __restrict__ r, double* __restrict__ p,
                                                           double* __restrict__ sv, double* __restrict__ u,
@@ -1288,35 +1290,58 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_update(int64_t n, int bs, dou
     const double alpha = k.alpha, beta = k.beta;
     const bool cg = st->mode != FEM_MODE_PCG;
     double acc = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; i < n; i += (int64_t)gridDim.x * PCG_BLOCK) {
+    // one dof: v (exchanged where the node is shared), then p, s, x, r, u; returns r.u when the node is owned
+    auto dof = [&](int64_t i, double vi, double ui, double pi0, double si0, double xi, double ri0, double wi, double& po,
+                   double& so, double& xo, double& ro, double& uo) -> double {
         const int64_t node = i / bs;
         const int32_t j = ipos ? ipos[node] : -1;
-        double vi = v[i];
         if (j >= 0) {
             const int c = (int)(i - node * bs);
             if (xp.P) {   // rank-ordered sum of the partials (own partial = the local row itself)
-                double acc = 0.0;
-                for (int r = 0; r < xp.P; ++r) {
-                    const int src = xp.csrc[(int64_t)j * xp.P + r];
-                    if (src == -1) acc += vi;
-                    else if (src >= 0) acc += xp.precv[src + c];
+                double a = 0.0;
+                for (int q = 0; q < xp.P; ++q) {
+                    const int src = xp.csrc[(int64_t)j * xp.P + q];
+                    if (src == -1) a += vi;
+                    else if (src >= 0) a += xp.precv[src + c];
                 }
-                vi = acc;
+                vi = a;
             } else {
                 vi = recv[(int64_t)j * bs + c];
             }
         }
-        const double pi = u[i] + beta * p[i];
-        const double si = vi + beta * sv[i];
-        p[i] = pi;
-        sv[i] = si;
-        x[i] += alpha * pi;
-        double ri = r[i] - alpha * si;
-        if (cg && w[i] == 0.0) ri = 0.0;
-        r[i] = ri;
-        const double ui = w[i] * ri;
-        u[i] = ui;
-        if (!own || own[node]) acc += ri * ui;
+        po = ui + beta * pi0;
+        so = vi + beta * si0;
+        xo = xi + alpha * po;
+        double rv = ri0 - alpha * so;
+        if (cg && wi == 0.0) rv = 0.0;
+        ro = rv;
+        uo = wi * rv;
+        return (!own || own[node]) ? rv * uo : 0.0;
+    };
+    const int64_t n2 = n >> 1;
+    for (int64_t i2 = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; i2 < n2; i2 += (int64_t)gridDim.x * PCG_BLOCK) {
+        const double2 v2 = reinterpret_cast<const double2*>(v)[i2], u2 = reinterpret_cast<const double2*>(u)[i2];
+        const double2 p2 = reinterpret_cast<const double2*>(p)[i2], s2 = reinterpret_cast<const double2*>(sv)[i2];
+        const double2 x2 = reinterpret_cast<const double2*>(x)[i2], r2 = reinterpret_cast<const double2*>(r)[i2];
+        const double2 w2 = reinterpret_cast<const double2*>(w)[i2];
+        double2 po, so, xo, ro, uo;
+        acc += dof(2 * i2, v2.x, u2.x, p2.x, s2.x, x2.x, r2.x, w2.x, po.x, so.x, xo.x, ro.x, uo.x);
+        acc += dof(2 * i2 + 1, v2.y, u2.y, p2.y, s2.y, x2.y, r2.y, w2.y, po.y, so.y, xo.y, ro.y, uo.y);
+        reinterpret_cast<double2*>(p)[i2] = po;
+        reinterpret_cast<double2*>(sv)[i2] = so;
+        reinterpret_cast<double2*>(x)[i2] = xo;
+        reinterpret_cast<double2*>(r)[i2] = ro;
+        reinterpret_cast<double2*>(u)[i2] = uo;
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {   // the odd dof
+        const int64_t i = n - 1;
+        double po, so, xo, ro, uo;
+        acc += dof(i, v[i], u[i], p[i], sv[i], x[i], r[i], w[i], po, so, xo, ro, uo);
+        p[i] = po;
+        sv[i] = so;
+        x[i] = xo;
+        r[i] = ro;
+        u[i] = uo;
     }
     acc = block_sum256(acc, lds4);
     double g;
