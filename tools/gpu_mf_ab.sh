@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 VS=$(echo "$1" | tr ',' ' '); P=${2:-mfab}
-timeout -k 10 300 python -u -m pytest tests/test_gpu_matfree.py -x -q --timeout 120 --timeout-method thread \
+[ -n "$SKIP_TESTS" ] || timeout -k 10 300 python -u -m pytest tests/test_gpu_matfree.py -x -q --timeout 120 --timeout-method thread \
   -p no:cacheprovider > gpurun_out/${P}_tests.log 2>&1 || { tail -30 gpurun_out/${P}_tests.log; exit 1; }
 tail -2 gpurun_out/${P}_tests.log
 D=cuda-powered-mesh-handling-and-iterative-solvers_amd
