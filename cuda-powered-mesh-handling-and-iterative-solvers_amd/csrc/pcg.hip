@@ -729,6 +729,57 @@ __device__ __forceinline__ double mf_q_dof(const MfOp& op, const double* __restr
     return s;
 }
 
+// FEM_MF_QLDS = 1 (A/B): the slot values a wave's 128 dofs of one thread-step need -- one contiguous node-major range --
+// staged into LDS by 16-byte lanes first (2-3 coalesced wave loads instead of 8 scattered 8-byte ones per dof pair),
+// then summed from LDS in the same order (the same bits); ranges over MF_QCAP doubles take the direct loads.
+// Measured slightly slower than the fixed-count direct loads (update 75.8-78.1 vs 73.4-75.9 us on the 10M elastic
+// cube, profiles/r06l_mf_qlds_prof_ab.txt: the staging serialises a wave's thread-steps); off
+#ifndef FEM_MF_QLDS
+#define FEM_MF_QLDS 0
+#endif
+constexpr int MF_QCAP = 512;
+template <int BS>
+__device__ __forceinline__ bool mf_q_stage(const MfOp& op, const double* __restrict__ slots, double* qs, int64_t iw,
+                                           int64_t i, int64_t n, int lane, double2& qv) {
+    const int64_t d_lo = 2 * iw, d_hi = (2 * iw + 128 < n ? 2 * iw + 128 : n) - 1;
+    const int64_t a_lo = d_lo / BS, a_hi = d_hi / BS;
+    const int s_lo = op.nptr[a_lo], s_hi = op.nptr[a_hi + 1];
+    const int64_t st0 = ((int64_t)BS * s_lo) & ~(int64_t)1;
+    const int len = (int)((int64_t)BS * s_hi - st0);
+    if (len > MF_QCAP) return false;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // the previous step's LDS reads of this wave are done
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const double2* s2 = reinterpret_cast<const double2*>(slots + st0);
+    for (int t = lane; 2 * t < len; t += 64) {
+        if (2 * t + 1 < len) {
+            const double2 v = s2[t];
+            qs[2 * t] = v.x;
+            qs[2 * t + 1] = v.y;
+        } else {
+            qs[2 * t] = slots[st0 + 2 * t];
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    double q[2] = {0.0, 0.0};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int64_t d = 2 * i + h;
+        if (d < n) {
+            const int64_t a = d / BS;
+            const int c = (int)(d - a * BS);
+            const int k0 = op.nptr[a], k1 = op.nptr[a + 1];
+            double sum = 0.0;
+            for (int k = k0; k < k1; ++k) sum += qs[(int64_t)BS * k + c - st0];
+            q[h] = sum;
+        }
+    }
+    qv = make_double2(q[0], q[1]);
+    return true;
+}
+
 template <int BS, bool FROM_Q>
 __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update2_mf(int64_t nn, double* __restrict__ x, double* __restrict__ p,
                                                               double* __restrict__ r, const double* __restrict__ q,
@@ -756,8 +807,20 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update2_mf(int64_t nn, double
     const double2* q2 = reinterpret_cast<const double2*>(q);
     const double2* w2 = reinterpret_cast<const double2*>(w);
     double2* r2 = reinterpret_cast<double2*>(r);
+    constexpr bool QL = FEM_MF_QLDS && !FROM_Q;
+    __shared__ double qst[QL ? PCG_BLOCK / 64 : 1][QL ? MF_QCAP : 1];
+    const int lane = threadIdx.x & 63;
+    double* qs = qst[QL ? (threadIdx.x >> 6) : 0];
+    // q of the pair (2 i, 2 i + 1): staged when the node-major slots allow (every lane of the wave calls it: the wave's
+    // first pair iw is uniform), else the direct fixed-count loads
     auto qpair = [&](int64_t i) -> double2 {
         if constexpr (FROM_Q) return q2[i];
+        if constexpr (QL) {
+            double2 qv;
+            const int64_t iw = i - lane;
+            if (op.spos && iw < n2 && mf_q_stage<BS>(op, slots, qs, iw, i, n, lane, qv)) return qv;
+        }
+        if (i >= n2) return make_double2(0.0, 0.0);
         return make_double2(mf_q_dof<BS>(op, slots, 2 * i), mf_q_dof<BS>(op, slots, 2 * i + 1));
     };
     double2 z[U2_NPT];
@@ -766,9 +829,9 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update2_mf(int64_t nn, double
     for (int k = 0; k < U2_NPT; ++k) {
         const int64_t i = i0 + k * stride;
         z[k] = make_double2(0.0, 0.0);
+        const double2 qv = qpair(i);   // the whole wave (staging)
         if (i < n2) {
             double2 rv = r2[i], wv = w2[i];
-            const double2 qv = qpair(i);
             rv.x = rv.x - alpha * qv.x;
             rv.y = rv.y - alpha * qv.y;
             if (cg) {
@@ -781,9 +844,11 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_pcg_update2_mf(int64_t nn, double
             acc += rv.y * z[k].y;
         }
     }
-    for (int64_t i = i0 + U2_NPT * stride; i < n2; i += stride) {   // past the register capacity
-        double2 rv = r2[i], wv = w2[i];
+    for (int64_t ib = i0 - lane + U2_NPT * stride; ib < n2; ib += stride) {   // past the register capacity (the
+        const int64_t i = ib + lane;                                           // wave together: staging)
         const double2 qv = qpair(i);
+        if (i >= n2) continue;
+        double2 rv = r2[i], wv = w2[i];
         rv.x = rv.x - alpha * qv.x;
         rv.y = rv.y - alpha * qv.y;
         if (cg) {

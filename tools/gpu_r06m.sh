@@ -1,11 +1,12 @@
 #!/bin/bash
-# Round 6 probes: (1) K1 phase-skip timing builds (FEM_MF_PROF 1/2/3, wrong results) against the default on the 10M
+# Round 6 probes: (1) the LDS-staged update slot sums (FEM_MF_QLDS) A/B and the K1 phase-skip timing builds
+# (FEM_MF_PROF 1/2/3, wrong results) against the default on the 10M
 # elastic cube; (2) the resident grid of the chunk kernels capped (FEM355_MF_GRID_CAP) at the N = 8 rank share, where
 # 2,450 chunks leave ~2.4 per workgroup of the default grid (world-1 RCCL line, element-chunk operator).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-SKIP_TESTS=1 bash tools/gpu_mf_ab.sh prof1,prof2,prof3 r06l || exit $?
+bash tools/gpu_mf_ab.sh qlds0,prof1,prof2,prof3 r06l || exit $?
 for cap in 0 512 256; do
   if [ $cap = 0 ]; then unset FEM355_MF_GRID_CAP; else export FEM355_MF_GRID_CAP=$cap; fi
   timeout -k 10 300 python bench.py --force-dist --n 59 --steps 200 --warmup 20 --no-cpu-baseline --mixed 0 \
