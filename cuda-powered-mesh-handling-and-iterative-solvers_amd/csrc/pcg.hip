@@ -1337,8 +1337,15 @@ __device__ __forceinline__ void cg1_commit(PcgState* st, const Cg1Step& k, doubl
     st->iter = k.it + 1;
 }
 
+// FEM_MF_DIST_NOGATHER = 1 (A/B): the distributed element-chunk iteration without the gather pass -- d = u.v reduced
+// in the chunk walk (MF_DOT), an interface-only pack kernel (k_cg1_mf_iface), and v of every dof formed from the
+// slots inside k_cg1_update<true> (the fixed-count loads of mf_q_dof): no v vector written or read
+#ifndef FEM_MF_DIST_NOGATHER
+#define FEM_MF_DIST_NOGATHER 0
+#endif
 // Every vector read and written as 16-byte lanes (a double2 of dofs per thread-step; round 5: one 8-byte dof per
-// thread), the per-dof arithmetic unchanged
+// thread), the per-dof arithmetic unchanged. MF: v from the element-chunk operator's slots (never stored)
+template <bool MF = false>
 __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_update(int64_t n, int bs, double* __restrict__ x,
                                                           double* __restrict__ r, double* __restrict__ p,
                                                           double* __restrict__ sv, double* __restrict__ u,
@@ -1347,7 +1354,8 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_update(int64_t n, int bs, dou
                                                           const int32_t* __restrict__ ipos,
                                                           const uint8_t* __restrict__ own, PcgState* __restrict__ st,
                                                           RedBuf red, P2PArgs xp, const double* __restrict__ send,
-                                                          int64_t off) {
+                                                          int64_t off, MfOp op = MfOp{},
+                                                          const double* __restrict__ slots = nullptr) {
     __shared__ double lds4[4];
     __shared__ int flag;
     const Cg1Step k = cg1_eval(st, cg1_scalar(recv, send, off, 0, xp), cg1_scalar(recv, send, off, 1, xp));
@@ -1384,8 +1392,14 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_update(int64_t n, int bs, dou
         return (!own || own[node]) ? rv * uo : 0.0;
     };
     const int64_t n2 = n >> 1;
+    auto vpair = [&](int64_t i2) -> double2 {
+        if constexpr (MF)
+            return bs == 3 ? make_double2(mf_q_dof<3>(op, slots, 2 * i2), mf_q_dof<3>(op, slots, 2 * i2 + 1))
+                           : make_double2(mf_q_dof<1>(op, slots, 2 * i2), mf_q_dof<1>(op, slots, 2 * i2 + 1));
+        return reinterpret_cast<const double2*>(v)[i2];
+    };
     for (int64_t i2 = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; i2 < n2; i2 += (int64_t)gridDim.x * PCG_BLOCK) {
-        const double2 v2 = reinterpret_cast<const double2*>(v)[i2], u2 = reinterpret_cast<const double2*>(u)[i2];
+        const double2 v2 = vpair(i2), u2 = reinterpret_cast<const double2*>(u)[i2];
         const double2 p2 = reinterpret_cast<const double2*>(p)[i2], s2 = reinterpret_cast<const double2*>(sv)[i2];
         const double2 x2 = reinterpret_cast<const double2*>(x)[i2], r2 = reinterpret_cast<const double2*>(r)[i2];
         const double2 w2 = reinterpret_cast<const double2*>(w)[i2];
@@ -1401,7 +1415,10 @@ __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_update(int64_t n, int bs, dou
     if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {   // the odd dof
         const int64_t i = n - 1;
         double po, so, xo, ro, uo;
-        acc += dof(i, v[i], u[i], p[i], sv[i], x[i], r[i], w[i], po, so, xo, ro, uo);
+        double vt;
+        if constexpr (MF) vt = bs == 3 ? mf_q_dof<3>(op, slots, i) : mf_q_dof<1>(op, slots, i);
+        else vt = v[i];
+        acc += dof(i, vt, u[i], p[i], sv[i], x[i], r[i], w[i], po, so, xo, ro, uo);
         p[i] = po;
         sv[i] = so;
         x[i] = xo;
@@ -2068,6 +2085,78 @@ __global__ void __launch_bounds__(MF_BLOCK) k_cg1_mf_slots(MfOp op, const double
     (void)mf_walk_any<BS, MF_APPLY>(op, u, slots, L);
 }
 
+// FEM_MF_DIST_NOGATHER: the walk also reduces d = u.v (sum over the slots of u_node . slot) -> st->red[0]
+template <int BS>
+__global__ void __launch_bounds__(MF_BLOCK) k_cg1_mf_slots_dot(MfOp op, const double* __restrict__ u,
+                                                               double* __restrict__ slots, PcgState* __restrict__ st,
+                                                               int always, P2PArgs xp, const double* __restrict__ recv,
+                                                               const double* __restrict__ send, int64_t off,
+                                                               RedBuf red) {
+    __shared__ MfKernelLds<BS, MF_DOT> L;
+    __shared__ double lds4[MF_BLOCK / 64];
+    __shared__ int flag;
+    if (!always) {   // the step of this pass, from the unchanged state (committed by k_cg1_mf_iface)
+        const Cg1Step k = cg1_eval(st, cg1_scalar(recv, send, off, 0, xp), cg1_scalar(recv, send, off, 1, xp));
+        if (!k.go) return;
+    }
+    double dot = mf_walk_any<BS, MF_DOT>(op, u, slots, L);
+    dot = block_sum<MF_BLOCK>(dot, lds4);
+    double d;
+    if (reduce_grid<MF_BLOCK>(dot, red.part(RED_K1), red.cnt(RED_K1), &d, lds4, &flag) && threadIdx.x == 0)
+        st->red[0] = d;
+}
+
+// FEM_MF_DIST_NOGATHER: the interface rows only -- their slot sums packed for the exchange -- and [g, d]; the last
+// block commits the step
+template <int BS>
+__global__ void __launch_bounds__(PCG_BLOCK) k_cg1_mf_iface(MfOp op, const double* __restrict__ slots,
+                                                            const int32_t* __restrict__ imap, int64_t nI,
+                                                            double* __restrict__ send, int64_t off,
+                                                            PcgState* __restrict__ st, RedBuf red, int always,
+                                                            P2PArgs xp, const double* __restrict__ recv, double* hist,
+                                                            int64_t hist_len) {
+    __shared__ double lds4[4];
+    __shared__ int flag;
+    Cg1Step k{};
+    if (!always) {
+        k = cg1_eval(st, cg1_scalar(recv, send, off, 0, xp), cg1_scalar(recv, send, off, 1, xp));
+        if (!k.go) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) cg1_commit(st, k, hist, hist_len);
+            return;
+        }
+    }
+    for (int64_t j = (int64_t)blockIdx.x * PCG_BLOCK + threadIdx.x; j < nI; j += (int64_t)gridDim.x * PCG_BLOCK) {
+        const int32_t a = imap[j];
+        if (a < 0) continue;   // an interface node of other ranks only (send keeps its zeros)
+#pragma unroll
+        for (int c = 0; c < BS; ++c) {
+            const double o = mf_q_dof<BS>(op, slots, (int64_t)a * BS + c);
+            if (xp.P) {   // straight into every peer's message slot for this node
+                for (int q = 0; q < xp.P; ++q) {
+                    const int dst = xp.csrc[j * xp.P + q];
+                    if (dst >= 0) xp.psend[dst + c] = o;
+                }
+            } else {
+                send[j * BS + c] = o;
+            }
+        }
+    }
+    double unused;   // the grid reduction as a completion count: its last block packs [g, d] and commits
+    if (reduce_grid(0.0, red.part(RED_INIT), red.cnt(RED_INIT), &unused, lds4, &flag) && threadIdx.x == 0) {
+        if (!always) cg1_commit(st, k, hist, hist_len);   // every block of the three kernels has read the state
+        const double d = st->red[0];
+        send[off] = st->red[1];
+        send[off + 1] = d;
+        for (int q = 0; q < xp.P; ++q) {
+            const int dst = xp.ssrc[q];
+            if (dst >= 0) {
+                xp.psend[dst] = st->red[1];
+                xp.psend[dst + 1] = d;
+            }
+        }
+    }
+}
+
 template <int BS>
 __global__ void __launch_bounds__(PCG_BLOCK) k_cg1_mf_gather(MfOp op, const double* __restrict__ slots,
                                                              const double* __restrict__ u, double* __restrict__ v,
@@ -2254,6 +2343,37 @@ static P2PArgs p2p_args(const fem_pcg* s) {
 static int cg1_spmv(fem_pcg* s, int always) {
     const int64_t off = s->nI * s->bs;
     const int32_t* ipos = s->nI > 0 ? s->ipos : nullptr;
+    if (s->mf && FEM_MF_DIST_NOGATHER) {   // chunks into the slots + d, then the interface pack only
+        const MfOp op = mf_op(s->mf);
+        const P2PArgs xp = p2p_args(s);
+        if (op.nchunks > 0) {
+            const void* fn = s->bs == 3 ? (const void*)k_cg1_mf_slots_dot<3> : (const void*)k_cg1_mf_slots_dot<1>;
+            const int G = mf_resident_grid(fn, MF_BLOCK, op.nchunks);
+            if (s->bs == 3)
+                hipLaunchKernelGGL(k_cg1_mf_slots_dot<3>, dim3(G), dim3(MF_BLOCK), 0, s->stream, op, s->cg1_u,
+                                   s->mf_sl, s->st, always, xp, s->cg1_recv, s->cg1_send, off, s->red);
+            else
+                hipLaunchKernelGGL(k_cg1_mf_slots_dot<1>, dim3(G), dim3(MF_BLOCK), 0, s->stream, op, s->cg1_u,
+                                   s->mf_sl, s->st, always, xp, s->cg1_recv, s->cg1_send, off, s->red);
+            FEM_LAUNCHED();
+        } else {   // no element on this rank: d = 0
+            FEM_HIP(hipMemsetAsync(st_red(s, 0), 0, sizeof(double), s->stream));
+        }
+        const int Gi = grid_multiple_of_xcd(cdiv(s->nI > 0 ? s->nI : 1, PCG_BLOCK), 1024);
+        const int32_t* imap = s->nI > 0 ? s->imap : nullptr;
+        if (s->bs == 3)
+            hipLaunchKernelGGL(k_cg1_mf_iface<3>, dim3(Gi), dim3(PCG_BLOCK), 0, s->stream, op, s->mf_sl, imap, s->nI,
+                               s->cg1_send, off, s->st, s->red, always, xp, s->cg1_recv, s->hist, s->hist_len);
+        else
+            hipLaunchKernelGGL(k_cg1_mf_iface<1>, dim3(Gi), dim3(PCG_BLOCK), 0, s->stream, op, s->mf_sl, imap, s->nI,
+                               s->cg1_send, off, s->st, s->red, always, xp, s->cg1_recv, s->hist, s->hist_len);
+        FEM_LAUNCHED();
+        if (!s->comm && s->p2p) return FEM_OK;
+        if (!s->comm)
+            FEM_HIP(hipMemcpyAsync(s->cg1_recv, s->cg1_send, sizeof(double) * (size_t)cg1_len(s),
+                                   hipMemcpyDeviceToDevice, s->stream));
+        return FEM_OK;
+    }
     if (s->mf) {   // element-chunk operator: the rank's chunks into the context's slots, then the slot gather
         const MfOp op = mf_op(s->mf);
         const P2PArgs xp = p2p_args(s);
@@ -2304,9 +2424,14 @@ static int cg1_spmv(fem_pcg* s, int always) {
 }
 
 static int cg1_step_update(fem_pcg* s) {
-    hipLaunchKernelGGL(k_cg1_update, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->bs, s->x, s->r, s->p0,
-                       s->cg1_s, s->cg1_u, s->q, s->w, s->cg1_recv, s->nI > 0 ? s->ipos : nullptr, s->own, s->st,
-                       s->red, p2p_args(s), s->cg1_send, s->nI * s->bs);
+    if (s->mf && FEM_MF_DIST_NOGATHER)
+        hipLaunchKernelGGL(k_cg1_update<true>, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->bs, s->x,
+                           s->r, s->p0, s->cg1_s, s->cg1_u, s->q, s->w, s->cg1_recv, s->nI > 0 ? s->ipos : nullptr,
+                           s->own, s->st, s->red, p2p_args(s), s->cg1_send, s->nI * s->bs, mf_op(s->mf), s->mf_sl);
+    else
+        hipLaunchKernelGGL(k_cg1_update<false>, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->bs, s->x,
+                           s->r, s->p0, s->cg1_s, s->cg1_u, s->q, s->w, s->cg1_recv, s->nI > 0 ? s->ipos : nullptr,
+                           s->own, s->st, s->red, p2p_args(s), s->cg1_send, s->nI * s->bs);
     FEM_LAUNCHED();
     return FEM_OK;
 }
