@@ -1249,6 +1249,22 @@ __device__ __forceinline__ double el_combine(const Lame& L, double m_rc, double 
     return s;
 }
 
+#ifndef FEM_ACC_POSREP
+#define FEM_ACC_POSREP 1   // bs = 3: the repeated-node flag in the position fields (one LDS read less per step)
+#endif
+// the accumulator kernel's column positions are 16-bit fields (bs = 3: 15-bit beside the flag), all-ones = absent
+constexpr int acc_max_cols(int bs) { return FEM_ACC_POSREP && bs == 3 ? 0x7fff : 0xffff; }
+
+// lane L of every quad (four consecutive lanes) to all four lanes of it (DPP quad_perm, no LDS)
+template <int L>
+__device__ __forceinline__ double quad_bcast(double x) {
+    constexpr int ctrl = L | (L << 2) | (L << 4) | (L << 6);
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)b, ctrl, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), ctrl, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
 __device__ __forceinline__ double p1_value(const double ga[3], const double gb[3], double kappa, double V) {
     const double dot = ga[0] * gb[0] + ga[1] * gb[1] + ga[2] * gb[2];
     return kappa * dot * V;
@@ -1328,6 +1344,10 @@ struct AccCfg {
 // items per row 2.95, 12 items 2.83, 4 items 2.66 ms; with the M / P sums since round 4: 2.45 ms. The coordinates of
 // the tile's columns staged in LDS instead of the per-batch prefetch (XS): 3.0 ms at 8 items per row, 2.96 / 3.37 /
 // 3.12 ms at 5 / 6 / 4 -- the staging's gathers at the tile start are exposed, and 3 instead of 4 tiles per CU).
+// Round 6, the sweep's LDS operations per (row, item) step cut from 13 to 8 (profiles/r06o_acc_sweep_ab.txt, 10M
+// cube, bit-identical): the adds as LDS atomics (FEM_ACC_ATOM: 2277 -> 2248 us; P1 649 -> 641 us), the P sum from
+// the quad's products over DPP and the repeated-node flag in the position fields (FEM_ACC_PDPP + FEM_ACC_POSREP:
+// 2117 us; all three 2067 us).
 #ifndef FEM_P1_CFG
 #define FEM_P1_CFG 64, 4, 4, 32, 1024
 #endif
@@ -1403,6 +1423,14 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
 #endif
 #ifndef FEM_ACC_PAD
 #define FEM_ACC_PAD 1
+#endif
+    // bs = 3: positions of 15 bits, the repeated-node flag in bit 15 of every field (no a_s read in the sweep)
+    constexpr bool POSREP = FEM_ACC_POSREP && BS == 3;
+#ifndef FEM_ACC_ATOM
+#define FEM_ACC_ATOM 1   // sweep adds as LDS atomics
+#endif
+#ifndef FEM_ACC_PDPP
+#define FEM_ACC_PDPP 1   // bs = 3: the P sum from the quad's products (DPP) instead of three more LDS reads
 #endif
     constexpr bool ACT = FEM_ACC_T && BS == 3;
     constexpr int ARS = ACT ? AW * AV + FEM_ACC_PAD : R + 1;   // stride of the outer index
@@ -1563,7 +1591,7 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                             pp[bb] = staged ? sorted_pos(col_s + cl, cn, j) : sorted_pos(colidx + seg0 + cl, cn, j);
                         }
 #endif
-                        pk[bb >> 1] |= pp[bb] << (16 * (bb & 1));
+                        pk[bb >> 1] |= (POSREP ? pp[bb] & 0x7fffu : pp[bb]) << (16 * (bb & 1));
                     }
                     double g[4][3];
                     double det;
@@ -1605,6 +1633,10 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                     }
                 }
                 if (tid < NI) {
+                    if (POSREP && (aflag & 0x80)) {   // bit 15 of every field: the element repeats a node
+                        pk[0] |= 0x80008000u;
+                        pk[1] |= 0x80008000u;
+                    }
                     pos_s[it0] = make_uint2(pk[0], pk[1]);
                     a_s[it0] = aflag;
                 }
@@ -1627,17 +1659,38 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                 }
                 const int it = lr * J + jj;
                 const uint2 pp = pos_s[it];
-                const uint32_t praw = ((lb < 2 ? pp.x : pp.y) >> (16 * (lb & 1))) & 0xffffu;
+                const uint32_t fld = ((lb < 2 ? pp.x : pp.y) >> (16 * (lb & 1))) & 0xffffu;
+                constexpr uint32_t NOPOS = POSREP ? 0x7fffu : 0xffffu;
+                const uint32_t praw = fld & NOPOS;
                 const int k = (int)praw - c0;
-                const bool hit = praw != 0xffffu && k >= 0 && k < cw;
-                const uint8_t af = a_s[it];
+                const bool hit = praw != NOPOS && k >= 0 && k < cw;
+                const uint8_t af = POSREP ? (uint8_t)((fld >> 15) << 7) : a_s[it];
                 // bs = 3: NV products M[r][c] = (V g_a[r]) g_b[c] of the lane's block rows, then (P lane / LPR = 4)
                 // P = (V g_a) . g_b; every value lands in its own accumulator slot of column k
                 constexpr int NV = BS == 1 ? 1 : (LPR == 4 ? 10 : 3);
                 double v[NV];
                 int slot0 = 0;        // first accumulator slot of the lane's values (consecutive)
                 int nv = 0;           // values of this lane
-                if (hit) {
+                constexpr bool PDPP = FEM_ACC_PDPP && BS == 3 && LPR == 16;
+                if constexpr (PDPP) {
+                    // lanes (row, b, rr) of one quad share the item and node b: lane rr < 3 forms block row rr, and
+                    // the P lane takes the three products (V g_a[q]) g_b[q] it needs from lanes q = 0, 1, 2 of its
+                    // quad (DPP broadcasts) -- el_pdot's rounded products summed in its order, without its three
+                    // LDS reads. Unconditional (every lane active for the DPP); the values of a miss are not used.
+                    const double gb[3] = {dat_s[3 + 3 * lb][it], dat_s[4 + 3 * lb][it], dat_s[5 + 3 * lb][it]};
+                    const double vr = dat_s[lrr < 3 ? lrr : 2][it];
+#pragma unroll
+                    for (int cc = 0; cc < 3; ++cc) v[cc] = vr * gb[cc];
+                    const double p0 = quad_bcast<0>(v[0]), p1 = quad_bcast<1>(v[1]), p2 = quad_bcast<2>(v[2]);
+                    if (lrr == 3) {
+                        v[0] = add_nc(add_nc(p0, p1), p2);
+                        slot0 = 9;
+                        nv = hit ? 1 : 0;
+                    } else {
+                        slot0 = lrr * 3;
+                        nv = hit ? 3 : 0;
+                    }
+                } else if (hit) {
                     if constexpr (BS == 1) {
                         v[0] = dat_s[lb][it];
                         nv = 1;
@@ -1672,7 +1725,14 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                         for (int cc = 0; cc < NV; ++cc) {
                             if (cc < nv) {
                                 double* ap = &ACC(k * AV + slot0 + cc, lr);
+#if FEM_ACC_ATOM
+                                // one LDS add (ds_add_f64, no return) instead of a read, a wait and a write: the
+                                // row's lanes of one step hit distinct slots and a wave's LDS operations complete
+                                // in issue order, so every slot still sums in ascending incidence order
+                                __hip_atomic_fetch_add(ap, v[cc], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
                                 *ap = add_nc(*ap, v[cc]);
+#endif
                             }
                         }
                     }
@@ -2417,6 +2477,11 @@ int fem_assemble_tet4_ex2(const double* coords, const int64_t* conn, double E, d
         return FEM_EARG;
     }
     if (N <= 0) return FEM_OK;
+    if (max_width >= acc_max_cols(bs)) {
+        set_error("fem_assemble_tet4: a row of %d columns exceeds the value kernel's %d", max_width,
+                  acc_max_cols(bs) - 1);
+        return FEM_EARG;
+    }
     hipStream_t st = S(stream);
     if (getenv("FEM355_ASM_ROWS") != nullptr) {
         if (!csr2sell) {
@@ -2473,6 +2538,11 @@ int fem_assemble_tet4_sl(const double* coords, const int64_t* conn, double E, do
     }
     if (bs != 1 && bs != 3) {
         set_error("fem_assemble_tet4_sl: block size %d unsupported", bs);
+        return FEM_EARG;
+    }
+    if (max_width >= acc_max_cols(bs)) {
+        set_error("fem_assemble_tet4_sl: a row of %d columns exceeds the value kernel's %d", max_width,
+                  acc_max_cols(bs) - 1);
         return FEM_EARG;
     }
     hipStream_t st = S(stream);

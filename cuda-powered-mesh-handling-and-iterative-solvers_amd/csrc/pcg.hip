@@ -1337,12 +1337,18 @@ __device__ __forceinline__ void cg1_commit(PcgState* st, const Cg1Step& k, doubl
     st->iter = k.it + 1;
 }
 
-// FEM_MF_DIST_NOGATHER = 1 (A/B): the distributed element-chunk iteration without the gather pass -- d = u.v reduced
-// in the chunk walk (MF_DOT), an interface-only pack kernel (k_cg1_mf_iface), and v of every dof formed from the
-// slots inside k_cg1_update<true> (the fixed-count loads of mf_q_dof): no v vector written or read
+// The gather-free distributed element-chunk iteration: d = u.v reduced in the chunk walk (MF_DOT), an interface-only
+// pack kernel (k_cg1_mf_iface), and v of every dof formed from the slots inside k_cg1_update<true> (the fixed-count
+// loads of mf_q_dof): no v vector written or read. It saves the gather pass's v stream and pays a second grid
+// reduction and one more launch, so it wins on large partitions only (world-1 RCCL lines, round 6: 1.73M nodes 285.5
+// vs 302.7 us per iteration, 216k nodes -- the N = 8 rank share of the 10M cube -- 55.2 vs 53.8 us): chosen per
+// context at fem_pcg_set_operator_mf when the partition has at least MF_NOGATHER_MIN_NODES nodes (the linear fit of
+// the two points crosses at ~330k). FEM_MF_DIST_NOGATHER = 0 / 1 (build) or FEM355_MF_NOGATHER=0 / 1 (run) force
+// either form. Both pack the same exchange message, so ranks may differ in the form they run.
 #ifndef FEM_MF_DIST_NOGATHER
-#define FEM_MF_DIST_NOGATHER 0
+#define FEM_MF_DIST_NOGATHER -1
 #endif
+constexpr int64_t MF_NOGATHER_MIN_NODES = 400000;
 // Every vector read and written as 16-byte lanes (a double2 of dofs per thread-step; round 5: one 8-byte dof per
 // thread), the per-dof arithmetic unchanged. MF: v from the element-chunk operator's slots (never stored)
 template <bool MF = false>
@@ -2028,6 +2034,7 @@ struct fem_pcg {
     fem_mf* mf;
     double* mf_sl;  // this context's slot buffer [nslots * bs] (no other context or stream writes it)
     int64_t mf_sl_cap;   // doubles mf_sl holds (a later operator with more slots reallocates it)
+    int mf_nogather;     // distributed element-chunk iteration: the gather-free form (FEM_MF_DIST_NOGATHER)
     int mf_qfuse;   // the merged update reads q from the slots (no gather launch); set per launch of K1 + update2
 };
 
@@ -2343,7 +2350,7 @@ static P2PArgs p2p_args(const fem_pcg* s) {
 static int cg1_spmv(fem_pcg* s, int always) {
     const int64_t off = s->nI * s->bs;
     const int32_t* ipos = s->nI > 0 ? s->ipos : nullptr;
-    if (s->mf && FEM_MF_DIST_NOGATHER) {   // chunks into the slots + d, then the interface pack only
+    if (s->mf && s->mf_nogather) {   // chunks into the slots + d, then the interface pack only
         const MfOp op = mf_op(s->mf);
         const P2PArgs xp = p2p_args(s);
         if (op.nchunks > 0) {
@@ -2424,7 +2431,7 @@ static int cg1_spmv(fem_pcg* s, int always) {
 }
 
 static int cg1_step_update(fem_pcg* s) {
-    if (s->mf && FEM_MF_DIST_NOGATHER)
+    if (s->mf && s->mf_nogather)
         hipLaunchKernelGGL(k_cg1_update<true>, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->bs, s->x,
                            s->r, s->p0, s->cg1_s, s->cg1_u, s->q, s->w, s->cg1_recv, s->nI > 0 ? s->ipos : nullptr,
                            s->own, s->st, s->red, p2p_args(s), s->cg1_send, s->nI * s->bs, mf_op(s->mf), s->mf_sl);
@@ -3236,6 +3243,12 @@ int fem_pcg_set_operator_mf(fem_pcg* s, fem_mf* m) {
         s->mf_sl_cap = need;
     }
     s->mf = m;
+    {
+        const char* e = getenv("FEM355_MF_NOGATHER");
+        s->mf_nogather = e ? (atoi(e) != 0)
+                           : FEM_MF_DIST_NOGATHER >= 0 ? FEM_MF_DIST_NOGATHER
+                                                       : (int)(mf_nodes(m) >= MF_NOGATHER_MIN_NODES);
+    }
     s->fused = s->deferred = s->persist_req = s->persist_fit_only = s->persist = 0;
     s->cols16 = nullptr;
     s->pext = 0;

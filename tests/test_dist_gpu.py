@@ -61,15 +61,27 @@ def test_partition_group_matches_single_gpu(gpu, kind, P, variant, exchange, fus
             assert torch.equal(xs[a].view(-1, bs)[ia], xs[c].view(-1, bs)[ic])
 
 
+@pytest.mark.parametrize("form", ["auto", "nogather", "mixed"])
 @pytest.mark.parametrize("exchange", ["allreduce", "p2p"])
 @pytest.mark.parametrize("kind,P", [("poisson", 2), ("poisson", 8), ("elastic", 3), ("elastic", 8)])
-def test_partition_group_matfree_matches_single_gpu(gpu, kind, P, exchange):
+def test_partition_group_matfree_matches_single_gpu(gpu, kind, P, exchange, form, monkeypatch):
     """The element-chunk operator under the element partition (north_star's configs[3] design): every rank forms its
     own elements' products from the coordinates (k_cg1_mf_slots + k_cg1_mf_gather, no matrix), the interface rows
     travel in the single-reduction exchange. Against the single-GPU assembled solve: Jacobi on every local row,
-    solution 1e-10, iterations +-2, shared copies bit-identical; the other variants are refused."""
+    solution 1e-10, iterations +-2, shared copies bit-identical; the other variants are refused.
+    form: auto (partitions this small run the gather form), nogather (FEM355_MF_NOGATHER=1: k_cg1_mf_slots_dot +
+    k_cg1_mf_iface + k_cg1_update<true>, the form large partitions choose), mixed (odd ranks gather-free: both forms
+    pack the same exchange message)."""
     import fem355  # noqa: F401
     from fem355 import dist as fd, mesh, system
+    if form != "auto":
+        orig, calls = system.MatFreeOperator.create_context, [0]
+
+        def create_context(self, *a, **k):   # the form is read from the environment when a context is created
+            monkeypatch.setenv("FEM355_MF_NOGATHER", "1" if form == "nogather" or calls[0] % 2 else "0")
+            calls[0] += 1
+            return orig(self, *a, **k)
+        monkeypatch.setattr(system.MatFreeOperator, "create_context", create_context)
     coords, tets = mesh.kuhn_cube(10, jitter=0.1)
     coords, tets = coords.to(gpu), tets.to(gpu)
     N = coords.shape[0]
