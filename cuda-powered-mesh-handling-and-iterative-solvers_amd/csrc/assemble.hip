@@ -1250,7 +1250,8 @@ __device__ __forceinline__ double el_combine(const Lame& L, double m_rc, double 
 }
 
 #ifndef FEM_ACC_POSREP
-#define FEM_ACC_POSREP 1   // bs = 3: the repeated-node flag in the position fields (one LDS read less per step)
+#define FEM_ACC_POSREP 0   // bs = 3: the repeated-node flag in the position fields (no a_s read; without the
+                           // atomics' per-step check, FEM_ACC_ATOM, nothing reads the flag)
 #endif
 // the accumulator kernel's column positions are 16-bit fields (bs = 3: 15-bit beside the flag), all-ones = absent
 constexpr int acc_max_cols(int bs) { return FEM_ACC_POSREP && bs == 3 ? 0x7fff : 0xffff; }
@@ -1344,10 +1345,10 @@ struct AccCfg {
 // items per row 2.95, 12 items 2.83, 4 items 2.66 ms; with the M / P sums since round 4: 2.45 ms. The coordinates of
 // the tile's columns staged in LDS instead of the per-batch prefetch (XS): 3.0 ms at 8 items per row, 2.96 / 3.37 /
 // 3.12 ms at 5 / 6 / 4 -- the staging's gathers at the tile start are exposed, and 3 instead of 4 tiles per CU).
-// Round 6, the sweep's LDS operations per (row, item) step cut from 13 to 8 (profiles/r06o_acc_sweep_ab.txt, 10M
-// cube, bit-identical): the adds as LDS atomics (FEM_ACC_ATOM: 2277 -> 2248 us; P1 649 -> 641 us), the P sum from
-// the quad's products over DPP and the repeated-node flag in the position fields (FEM_ACC_PDPP + FEM_ACC_POSREP:
-// 2117 us; all three 2067 us).
+// Round 6, the sweep's LDS operations per (row, item) step cut from 13 to 6 (profiles/r06o_acc_sweep_ab.txt,
+// r06r_acc_sweep_step2_ab.txt; 10M cube, bit-identical): the adds as LDS atomics (FEM_ACC_ATOM: 2277 -> 2248 us;
+// P1 649 -> 641 us), the P sum from the quad's products over DPP (FEM_ACC_PDPP), g_b read once per quad
+// (FEM_ACC_GDPP), and no per-step repeated-node check under the atomics: 1952 us; P1 618 us.
 #ifndef FEM_P1_CFG
 #define FEM_P1_CFG 64, 4, 4, 32, 1024
 #endif
@@ -1429,6 +1430,9 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
 #ifndef FEM_ACC_ATOM
 #define FEM_ACC_ATOM 1   // sweep adds as LDS atomics
 #endif
+#ifndef FEM_ACC_GDPP
+#define FEM_ACC_GDPP 1   // bs = 3 (with PDPP): g_b read once per quad and shared over DPP
+#endif
 #ifndef FEM_ACC_PDPP
 #define FEM_ACC_PDPP 1   // bs = 3: the P sum from the quad's products (DPP) instead of three more LDS reads
 #endif
@@ -1489,6 +1493,11 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
     // phase-2 lane: row lr, element node lb, block rows lrr .. lrr + RPL - 1
     const int lr = tid / LPR, lb = (BS == 1 || LPR == 4) ? tid % LPR : (tid % LPR) / 4;
     const int lrr = (BS == 1 || LPR == 4) ? 0 : tid % 4;   // bs = 3, LPR = 16: rr = 3 is the P lane
+    constexpr bool PDPP = FEM_ACC_PDPP && BS == 3 && LPR == 16;
+    constexpr bool REPCHK = !FEM_ACC_ATOM;
+    constexpr int ISTR = ACT ? 1 : ARS;   // accumulator stride between a column's consecutive slots
+    // PDPP: the lane's first slot (block row lrr: 3 lrr, P lane: 9) and its accumulator address at column 0
+    double* const abase = PDPP ? &ACC(lrr < 3 ? 3 * lrr : 9, lr) : nullptr;
     for (int c0 = 0; c0 < W; c0 += AW) {
         const int cw = min(AW, W - c0);
         __syncthreads();
@@ -1671,25 +1680,24 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                 double v[NV];
                 int slot0 = 0;        // first accumulator slot of the lane's values (consecutive)
                 int nv = 0;           // values of this lane
-                constexpr bool PDPP = FEM_ACC_PDPP && BS == 3 && LPR == 16;
                 if constexpr (PDPP) {
                     // lanes (row, b, rr) of one quad share the item and node b: lane rr < 3 forms block row rr, and
                     // the P lane takes the three products (V g_a[q]) g_b[q] it needs from lanes q = 0, 1, 2 of its
                     // quad (DPP broadcasts) -- el_pdot's rounded products summed in its order, without its three
                     // LDS reads. Unconditional (every lane active for the DPP); the values of a miss are not used.
+#if FEM_ACC_GDPP   // lane rr < 3 of the quad reads g_b[rr] alone, the quad shares the three over DPP
+                    const double gmine = dat_s[3 + 3 * lb + (lrr < 3 ? lrr : 2)][it];
+                    const double gb[3] = {quad_bcast<0>(gmine), quad_bcast<1>(gmine), quad_bcast<2>(gmine)};
+#else
                     const double gb[3] = {dat_s[3 + 3 * lb][it], dat_s[4 + 3 * lb][it], dat_s[5 + 3 * lb][it]};
+#endif
                     const double vr = dat_s[lrr < 3 ? lrr : 2][it];
 #pragma unroll
                     for (int cc = 0; cc < 3; ++cc) v[cc] = vr * gb[cc];
                     const double p0 = quad_bcast<0>(v[0]), p1 = quad_bcast<1>(v[1]), p2 = quad_bcast<2>(v[2]);
-                    if (lrr == 3) {
-                        v[0] = add_nc(add_nc(p0, p1), p2);
-                        slot0 = 9;
-                        nv = hit ? 1 : 0;
-                    } else {
-                        slot0 = lrr * 3;
-                        nv = hit ? 3 : 0;
-                    }
+                    if (lrr == 3) v[0] = add_nc(add_nc(p0, p1), p2);
+                    slot0 = lrr < 3 ? 3 * lrr : 9;
+                    nv = hit ? (lrr == 3 ? 1 : 3) : 0;
                 } else if (hit) {
                     if constexpr (BS == 1) {
                         v[0] = dat_s[lb][it];
@@ -1718,13 +1726,18 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                         }
                     }
                 }
-                const bool any_rep = __ballot(hit && (af & 0x80)) != 0;
+                // REPCHK (plain read-modify-writes): an element repeating a node would give two lanes of one step
+                // the same accumulator, so such a step goes node by node. With LDS atomics both adds land, and such an
+                // element has a determinant of exactly 0 (two equal columns, or a zero one): it is reported by `bad`
+                // (check_singular raises) and its NaN / inf values are never a result -- no per-step check.
+                const bool any_rep = REPCHK && __ballot(hit && (af & 0x80)) != 0;
                 if (!any_rep) {
                     if (hit) {
 #pragma unroll
                         for (int cc = 0; cc < NV; ++cc) {
                             if (cc < nv) {
-                                double* ap = &ACC(k * AV + slot0 + cc, lr);
+                                // PDPP: the lane's slot base is loop-invariant (abase), one multiply per address
+                                double* ap = PDPP ? abase + (k * AV + cc) * ISTR : &ACC(k * AV + slot0 + cc, lr);
 #if FEM_ACC_ATOM
                                 // one LDS add (ds_add_f64, no return) instead of a read, a wait and a write: the
                                 // row's lanes of one step hit distinct slots and a wave's LDS operations complete
