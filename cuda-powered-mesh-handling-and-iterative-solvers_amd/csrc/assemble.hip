@@ -1408,8 +1408,17 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
 #define FEM_ASM_SEARCH4 1   // the other tiles: the four binary searches of an item in lockstep (sorted_pos4)
 #endif
     constexpr bool HT = FEM_ASM_HASH && SL && BS == 1;
+    // FEM_ASM_HASH3 (bs = 3): the tile's longest row (the first of them) is the reference; its deltas (column - row)
+    // go into the same 64-slot table, and every row whose deltas equal them (all of a Kuhn cube's interior tiles)
+    // looks its element nodes' positions up there -- the same positions as the binary search, one LDS read each
+    // instead of ~5 dependent ones. Other rows keep the lockstep search.
+#ifndef FEM_ASM_HASH3
+#define FEM_ASM_HASH3 0   // measured slower (profiles/r06u_acc_negative_ab.txt): off
+#endif
+    constexpr bool HT3 = FEM_ASM_HASH3 && BS == 3;
     constexpr int HTN = 64;
-    __shared__ int2 ht_s[HT ? HTN : 1];
+    __shared__ int2 ht_s[(HT || HT3) ? HTN : 1];
+    __shared__ int hrow_s[HT3 ? R : 1];   // HT3: row r's deltas are the reference row's
     __shared__ double xs_s[Cfg::XS ? SEG : 1][3];
     // padded strides: the sweep's lanes of one row read dat_s rows of different element nodes and update
     // accumulators of different columns -- with power-of-two strides those all fall into one LDS bank
@@ -1427,6 +1436,12 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
 #endif
     // bs = 3: positions of 15 bits, the repeated-node flag in bit 15 of every field (no a_s read in the sweep)
     constexpr bool POSREP = FEM_ACC_POSREP && BS == 3;
+#ifndef FEM_ACC_PROBE
+#define FEM_ACC_PROBE 0   // timing builds (wrong values): 1 no gradients, 2 no sweep, with FEM_ASM_NOSEARCH no search
+#endif
+#ifndef FEM_ACC_PF2
+#define FEM_ACC_PF2 0   // loads a whole phase ahead (measured slower, profiles/r06u_acc_negative_ab.txt)
+#endif
 #ifndef FEM_ACC_ATOM
 #define FEM_ACC_ATOM 1   // sweep adds as LDS atomics
 #endif
@@ -1488,6 +1503,35 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                 xs_s[q][2] = X[3 * (int64_t)cq + 2];
             }
         }
+    bool use_ht3 = false;
+    if constexpr (HT3) {
+        int rref = 0, lref = rp_s[1] - rp_s[0];   // (every thread: the same reference row)
+        for (int r = 1; r < R; ++r) {
+            const int len = rp_s[r + 1] - rp_s[r];
+            if (len > lref) {
+                lref = len;
+                rref = r;
+            }
+        }
+        use_ht3 = staged && lref > 0 && lref <= HTN / 2;
+        if (use_ht3) {
+            for (int q = tid; q < HTN; q += NT) ht_s[q] = make_int2(INT_MIN, 0);
+            if (tid < R) hrow_s[tid] = (rp_s[tid + 1] - rp_s[tid]) == lref;
+            __syncthreads();   // col_s staged, table empty
+            const int cref = rp_s[rref] - seg0;
+            const int64_t gref = r0 + rref;
+            if (tid < lref) {
+                const int d = (int)(col_s[cref + tid] - gref);
+                unsigned h = ((unsigned)d * 2654435761u) >> 26;
+                while (atomicCAS(&ht_s[h].x, INT_MIN, d) != INT_MIN) h = (h + 1) & (HTN - 1);
+                ht_s[h].y = tid;
+            }
+            for (int q = tid; q < R * lref; q += NT) {   // a row of another delta list: back to the search
+                const int r = q / lref, k = q - r * lref;
+                if (hrow_s[r] && col_s[rp_s[r] - seg0 + k] - (r0 + r) != col_s[cref + k] - gref) hrow_s[r] = 0;
+            }
+        }
+    }
     const int maxc = maxc_s;
     const Lame L = lame(E, nu);
     // phase-2 lane: row lr, element node lb, block rows lrr .. lrr + RPL - 1
@@ -1530,6 +1574,16 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                     for (int q = 0; q < 3; ++q) xn[b][q] = X[3 * cn_n[b] + q];
             }
         }
+        // PF2 (XP): incidence entries two batches ahead, node ids one batch ahead loaded as a batch starts (under
+        // its phase 1), coordinates one batch ahead as its sweep starts -- each load a whole phase before its use
+        constexpr bool PF2 = FEM_ACC_PF2 && Cfg::XP;
+        int ea_nn = 0;
+        bool v_nn = false;
+        if (PF2 && tid < NI && J < maxc) {
+            const int t = ip_s[ir] + J + ij;
+            v_nn = t < ip_s[ir + 1];
+            if (v_nn) ea_nn = inc[t];
+        }
         for (int j0 = 0; j0 < maxc; j0 += J) {
             __syncthreads();   // accumulators initialised / previous batch swept
             const bool vcur = v_n;
@@ -1542,11 +1596,26 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
 #pragma unroll
                     for (int q = 0; q < 3; ++q) xc[b][q] = xn[b][q];
             }
-            v_n = false;
-            if (tid < NI && j0 + J < maxc) {
-                const int t = ip_s[ir] + j0 + J + ij;
-                v_n = t < ip_s[ir + 1];
-                if (v_n) ea_n = inc[t];
+            if constexpr (PF2) {
+                v_n = v_nn;
+                ea_n = ea_nn;
+                if (v_n) {
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) cn_n[b] = conn[4 * (int64_t)(ea_n >> 2) + b];
+                }
+                v_nn = false;
+                if (tid < NI && j0 + 2 * J < maxc) {
+                    const int t = ip_s[ir] + j0 + 2 * J + ij;
+                    v_nn = t < ip_s[ir + 1];
+                    if (v_nn) ea_nn = inc[t];
+                }
+            } else {
+                v_n = false;
+                if (tid < NI && j0 + J < maxc) {
+                    const int t = ip_s[ir] + j0 + J + ij;
+                    v_n = t < ip_s[ir + 1];
+                    if (v_n) ea_n = inc[t];
+                }
             }
             {
                 const int it0 = tid;
@@ -1564,8 +1633,19 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                     int nodes[4];
                     uint32_t pp[4];
                     pk[0] = pk[1] = 0u;
+                    // a table row: positions from the hash of the deltas node - row (hshift)
+                    const bool hrow = use_ht || (HT3 && use_ht3 && hrow_s[r]);
+                    const int hshift = use_ht ? kshift : (int)(r0 + r);
 #if !FEM_ASM_NOSEARCH
-                    if (!use_ht && FEM_ASM_SEARCH4) {   // the four nodes' binary searches in lockstep
+                    int2 hfirst[4];   // HT3 table rows: the four keys' first probes, read together
+                    if (HT3 && hrow && !use_ht) {
+#pragma unroll
+                        for (int bb = 0; bb < 4; ++bb) {
+                            const int jd = (int)c[bb] - hshift;
+                            hfirst[bb] = ht_s[((unsigned)jd * 2654435761u) >> 26];
+                        }
+                    }
+                    if (!hrow && FEM_ASM_SEARCH4) {   // the four nodes' binary searches in lockstep
                         int jj4[4];
 #pragma unroll
                         for (int bb = 0; bb < 4; ++bb) jj4[bb] = (int)c[bb] - kshift;
@@ -1583,12 +1663,15 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                         pp[bb] = (uint32_t)(bb < cn ? bb : 0);
                         (void)j;
 #else
-                        if (use_ht) {   // deltas are unique: the first matching key, or an empty slot = absent
-                            unsigned h = ((unsigned)j * 2654435761u) >> 26;
+                        if (HT3 && hrow && !use_ht && hfirst[bb].x == nodes[bb] - hshift) {
+                            pp[bb] = (uint32_t)hfirst[bb].y;   // (the usual case: no collision on the first probe)
+                        } else if (hrow) {   // deltas are unique: the first matching key, or an empty slot = absent
+                            const int jd = nodes[bb] - hshift;
+                            unsigned h = ((unsigned)jd * 2654435761u) >> 26;
                             uint32_t q = 0xffffu;
                             for (int probe = 0; probe < HTN; ++probe) {
                                 const int2 e = ht_s[h];
-                                if (e.x == j) {
+                                if (e.x == jd) {
                                     q = (uint32_t)e.y;
                                     break;
                                 }
@@ -1616,7 +1699,15 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                             det = tet4_grads_n(X, cncur, g);
                         }
                     } else if constexpr (Cfg::XP) {
+#if FEM_ACC_PROBE & 1   // timing builds only (wrong values): no gradients (the coordinates stand in), det = 1
+                        det = 1.0;
+#pragma unroll
+                        for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+                            for (int q = 0; q < 3; ++q) g[bb][q] = xc[bb][q];
+#else
                         det = tet4_grads_p(xc, g);
+#endif
                     } else {
                         det = tet4_grads_n(X, cncur, g);
                     }
@@ -1626,9 +1717,11 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
 #pragma unroll
                         for (int bb = 0; bb < 4; ++bb) dat_s[bb][it0] = p1_value(g[a], g[bb], E, V);
                     }
-                    const bool rep = nodes[0] == nodes[1] || nodes[0] == nodes[2] || nodes[0] == nodes[3] ||
-                                     nodes[1] == nodes[2] || nodes[1] == nodes[3] || nodes[2] == nodes[3];
-                    aflag = (uint8_t)(a | (rep ? 0x80 : 0));
+                    if constexpr (REPCHK || POSREP) {   // (nothing reads the flag otherwise)
+                        const bool rep = nodes[0] == nodes[1] || nodes[0] == nodes[2] || nodes[0] == nodes[3] ||
+                                         nodes[1] == nodes[2] || nodes[1] == nodes[3] || nodes[2] == nodes[3];
+                        aflag = (uint8_t)(a | (rep ? 0x80 : 0));
+                    }
                     if constexpr (BS == 3) {
 #pragma unroll
                         for (int q = 0; q < 3; ++q) {
@@ -1647,19 +1740,19 @@ __global__ void __launch_bounds__(256) k_asm_tet4_acc(const double* __restrict__
                         pk[1] |= 0x80008000u;
                     }
                     pos_s[it0] = make_uint2(pk[0], pk[1]);
-                    a_s[it0] = aflag;
+                    if constexpr (REPCHK) a_s[it0] = aflag;
                 }
             }
             __syncthreads();
-            if (v_n) {   // the next batch's element node ids (its incidence entry was loaded above)
+            if (!PF2 && v_n) {   // the next batch's element node ids (its incidence entry was loaded above)
 #pragma unroll
                 for (int b = 0; b < 4; ++b) cn_n[b] = conn[4 * (int64_t)(ea_n >> 2) + b];
             }
             // sweep: lanes of one row are consecutive lanes of one wave, in lockstep
 #pragma unroll
-            for (int jj = 0; jj < J; ++jj) {
+            for (int jj = 0; jj < ((FEM_ACC_PROBE & 2) ? 0 : J); ++jj) {   // (probe 2: no sweep, timing only)
                 if constexpr (Cfg::XP) {
-                    if (jj == J / 2 && v_n) {   // the next batch's coordinates, under the second half of the sweep
+                    if (jj == (PF2 ? 0 : J / 2) && v_n) {   // the next batch's coordinates, under the sweep
 #pragma unroll
                         for (int b = 0; b < 4; ++b)
 #pragma unroll
