@@ -31,6 +31,9 @@ namespace fem {
 
 // PK_T / PK_WAVES (threads / waves per workgroup) and pk_slice_span live in sell_pair.hpp: the pattern pass that
 // forms the gather windows (sl_pattern_slice) needs them outside this header
+#ifndef FEM_PK_PF
+#define FEM_PK_PF 0   // L2 prefetch of the next SpMV's first slice under the grid barrier (A/B)
+#endif
 constexpr int PK_MAXS = 7;               // slices per wave (10M Poisson: 27,000 slices over 4,096 waves -> 7)
 constexpr int PK_U = 2;                  // pairs in flight per lane (4 spills the slot state; persist_probe: 4 = 8)
 // pairs in flight of a build: one slot per wave (small systems: every wave owns at most one slice, e.g. 1M tets or
@@ -618,6 +621,16 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
             PK_MARK(1);
             const double dsum = pk_block_sum(dp, lds16);
             PK_MARK(2);
+            // FEM_PK_PF: waves 1..15 load one 8-byte word of every 128-byte line of the first 8 KB of the slice the
+            // next SpMV starts with (the matrix never changes), so those lines sit in L2 when the barrier releases
+            // and the memory-side cache streams part of the next SpMV while every workgroup waits; nothing computed
+            // from them (the results are unchanged), and wave 0 -- the one that polls -- issues none
+            double pfv = 0.0;
+            if (FEM_PK_PF && wv != 0 && nreg > 0) {
+                const int jf = (a.rev && (((it + 1) & 1) != 0)) ? nreg - 1 : 0;
+                const int64_t q0 = slp[s0 + jf], q1 = slp[s0 + jf + 1];
+                if ((int64_t)lane * 16 < q1 - q0) pfv = vap[q0 + (int64_t)lane * 16];
+            }
             if (threadIdx.x == 0) __hip_atomic_store(pd + L, dsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // (pk_block_sum ended on a workgroup barrier: the grid barrier needs no entry barrier of its own)
 #if FEM_PK_PROBE_NOBAR
@@ -641,6 +654,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist(PkArgs a) {
                 break;
             }
 #endif
+            if (FEM_PK_PF) asm volatile("" ::"v"(pfv));   // (keeps the loads; they completed under the barrier)
             elast = e;
             const double d = lds_dg[0];
             if (k > 0) g = lds_dg[1];
