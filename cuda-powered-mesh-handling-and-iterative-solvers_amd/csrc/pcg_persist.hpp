@@ -32,7 +32,7 @@ namespace fem {
 // PK_T / PK_WAVES (threads / waves per workgroup) and pk_slice_span live in sell_pair.hpp: the pattern pass that
 // forms the gather windows (sl_pattern_slice) needs them outside this header
 #ifndef FEM_PK_PF
-#define FEM_PK_PF 0   // L2 prefetch of the next SpMV's first slice under the grid barrier (A/B)
+#define FEM_PK_PF 0   // L2 prefetch of the next SpMV's first slice under the grid barrier: measured slower (r06v), off
 #endif
 constexpr int PK_MAXS = 7;               // slices per wave (10M Poisson: 27,000 slices over 4,096 waves -> 7)
 constexpr int PK_U = 2;                  // pairs in flight per lane (4 spills the slot state; persist_probe: 4 = 8)
