@@ -87,6 +87,9 @@ def parse():
     ap.add_argument("--reorder", default="none", choices=["none", "rcm"],
                     help="rcm: renumber the nodes by device reverse Cuthill-McKee inside every assembly pass "
                          "(timed with it; reported as reorder_ms)")
+    ap.add_argument("--pipelined", type=int, default=0,
+                    help="1: the pipelined (Ghysels-Vanroose) persistent iteration for bs = 1 systems of <= 2 slices "
+                         "per wave (FEM_TUNE_PK_GV; the 1M cube, a rank share of the 10M one); ignored elsewhere")
     ap.add_argument("--force-dist", action="store_true", help="run the RCCL element-partitioned path even at N=1")
     ap.add_argument("--dist-variant", type=int, default=1,
                     help="N>1: 1 = single-reduction PCG (one all-reduce per iteration), 0 = two reductions")
@@ -575,6 +578,9 @@ def measure(a, kind, coords, tets, dev):
     # from the mesh)
     reorder_ms = []
 
+    # --pipelined 1: the pipelined persistent iteration where it applies (include/fem355.h FEM_TUNE_PK_GV)
+    tune = (C.TUNE_DEFAULT | C.TUNE_PK_GV) if a.pipelined else None
+
     def assemble_and_solve():
         t0 = time.perf_counter()
         c, t, ff, fx = coords, tets, f, fixed
@@ -595,7 +601,8 @@ def measure(a, kind, coords, tets, dev):
         tol = a.rtol * float(torch.sqrt(torch.dot(b, w * b)))
         sync()
         t0 = time.perf_counter()
-        res = A.pcg(b, None, w=w, mode=C.MODE_PCG, tol=tol, max_iter=20000, chunk=64, schedule=a.schedule)
+        res = A.pcg(b, None, w=w, mode=C.MODE_PCG, tol=tol, max_iter=20000, chunk=64, schedule=a.schedule,
+                    tune=tune)
         sync()
         return A, w, b, res, t_asm, time.perf_counter() - t0
 
@@ -615,11 +622,12 @@ def measure(a, kind, coords, tets, dev):
     t_solve_med = sorted(p[1] for p in passes)[len(passes) // 2]
 
     # ---- fixed-iteration timing (the metric)
-    run = system.PcgRunner(A, b, w, tol=0.0, schedule=a.schedule)
+    run = system.PcgRunner(A, b, w, tol=0.0, schedule=a.schedule, tune=tune)
     run.start()
     if a.graph:
         run.use_graph(a.graph)
     persist = run.effective_schedule() == system.SCHED_PERSIST
+    pipelined = persist and run.pipelined()
     n_uni, n_sl, idx_total = run.uniform_slices()
     # the W warm-up steps go through the same launch path as the timed steps (persistent: one launch, events of the
     # context created here rather than next to the timed launch)
@@ -639,6 +647,8 @@ def measure(a, kind, coords, tets, dev):
     kernel = {system.SCHED_THREE: "k_pcg_spmv_dot", system.SCHED_FUSED: "k_pcg_spmv_dot<FUSED>",
               system.SCHED_DEFERRED: "k_pcg_d1",
               system.SCHED_PERSIST: "k_pcg_persist3" if A.bs == 3 else "k_pcg_persist"}[run.effective_schedule()]
+    if pipelined:
+        kernel = "k_pcg_persist_gv"
     run.close()
 
     # per launch of the measured kernel: one SpMV (3-kernel / deferred) or one whole iteration (persistent: the
@@ -707,6 +717,7 @@ def measure(a, kind, coords, tets, dev):
         + (", device RCM renumbering in every assembly pass" if a.reorder == "rcm" else ""),
         "reorder_ms": (sorted(reorder_ms)[len(reorder_ms) // 2] if reorder_ms else None),
         "solve_status": res.status,
+        "pipelined": pipelined,
         "kernel_ms": ({"persist_iteration": spmv_ms, "iterations_per_launch": a.steps} if persist else
                       {"spmv_dot": spmv_ms, "update": ms[1] / max(cnt[1], 1), "pupdate": ms[2] / max(cnt[2], 1),
                        "sampled_launches": cnt[0]}),

@@ -27,6 +27,7 @@ MODE_CG_STABLE, MODE_PCG, MODE_CG_CONSTRAINED = 0, 1, 2
 TUNE_UPD1 = 1024
 TUNE_U2_HOLD, TUNE_U2_SMALL = 2048, 4096   # test-only knobs of the merged update (include/fem355.h)
 TUNE_MF_GATHER = 8192   # element-chunk operator: q summed by a gather launch instead of inside the merged update
+TUNE_PK_GV = 16384      # persistent schedule, small bs = 1 systems: the pipelined (Ghysels-Vanroose) iteration
 TUNE_DEFAULT = 1 | 2 | 4 | 8 | 128 | TUNE_UPD1
 KIND_ELASTIC, KIND_POISSON, KIND_MASS = 0, 1, 2
 ISO_SUM, ISO_STACK, ISO_VOLUME, ISO_MASS = 0, 1, 2, 3
@@ -126,6 +127,7 @@ SIGNATURES = {
     "fem_pcg_get_schedule": (_I, [_P]),
     "fem_pcg_uniform_slices": (_I, [_P, _L, _L, _P, _P, _P]),
     "fem_pcg_persist_build": (_I, [_P, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    "fem_pcg_pipelined": (_I, [_P, ctypes.POINTER(_I)]),
     "fem_sell_sl_pattern": (_I, [_L, _P, _P, _I, _P, _P, _P, _P, _P]),
     "fem_assemble_tet4_sl": (_I, [_P, _P, _D, _D, _I, _P, _P, _L, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P]),
     "fem_assemble_from_ke_sl": (_I, [_P, _P, _I, _P, _P, _L, _P, _P, _P, _I, _I, _P, _P]),

@@ -1803,6 +1803,7 @@ __global__ void k_c1f_window(int64_t nslices, int64_t nrows, const int64_t* __re
 }  // namespace fem
 #include "pcg_persist.hpp"
 #include "pcg_persist3.hpp"
+#include "pcg_persist_gv.hpp"
 namespace fem {
 
 // ---------------------------------------------------------------- constraint projections (CG_CONSTRAINED)
@@ -2012,6 +2013,10 @@ struct fem_pcg {
     int pk_ovf;           // overflow build (more than PK_MAXS slices per wave)
     double* pk_v;         // [n] v of the overflow rows
     int pk_coop;          // launch through hipLaunchCooperativeKernel (fem_pcg_solve; FEM_TUNE_PK_COOP elsewhere)
+    int pk_gv;            // pipelined persistent iteration (FEM_TUNE_PK_GV, pcg_persist_gv.hpp)
+    double* gv_buf;       // its vectors: u, w, q, z, m[0], m[1] ([6 n])
+    int64_t gv_cap;       // doubles gv_buf holds
+    int gv_init_pending;  // the next launch forms w0 = A u0, m0 and gamma0 / delta0
     int64_t pk_epochs;    // upper bound of the barrier epochs enqueued since the sync words were last zeroed
     hipEvent_t pev[2];    // fem_pcg_profile's events of the persistent launch (created once per context)
     // distributed persistent schedule (fem_pcg_set_rows): rows partitioned over ranks, one persistent launch per
@@ -3556,6 +3561,29 @@ static int persist_setup(fem_pcg* s) {
     if (ovf && !s->pk_v) FEM_HIP(pool_alloc((void**)&s->pk_v, sizeof(double) * (size_t)s->n, s->stream, s->bs == 1));
     s->pk_ovf = ovf ? 1 : 0;
     s->persist = 1;
+    s->pk_gv = 0;
+    if ((s->tune & FEM_TUNE_PK_GV) && (s->tune & FEM_TUNE_PK_SC1) && s->bs == 1 && !ovf && s->mode == FEM_MODE_PCG) {
+        const int64_t maxL = (s->nslices + G - 1) / G;
+        const int pack = (int)((maxL + PK_WAVES - 1) / PK_WAVES);
+        if (pack <= GV_MAXS) {
+            static std::mutex gv_mu;
+            static int gv_ok[64] = {};   // per device: 0 unknown, 1 resident, 2 not
+            std::lock_guard<std::mutex> lk(gv_mu);
+            int& slot = gv_ok[dev & 63];
+            if (slot == 0) {
+                int res = 1;
+                for (int v = 0; v < 2 && res == 1; ++v) {
+                    const void* f = v ? (const void*)k_pcg_persist_gv<2> : (const void*)k_pcg_persist_gv<1>;
+                    FEM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GV_LDS));
+                    int nb = 0;
+                    FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, PK_T, GV_LDS));
+                    if (nb < 1) res = 2;
+                }
+                slot = res;
+            }
+            s->pk_gv = slot == 1;
+        }
+    }
     return FEM_OK;
 }
 
@@ -3591,6 +3619,7 @@ static int persist_setup_dist(fem_pcg* s) {
     }
     s->pk_ovf = 0;
     s->persist = 1;
+    s->pk_gv = 0;
     return FEM_OK;
 }
 
@@ -3669,6 +3698,34 @@ static int launch_persist(fem_pcg* s, int k, unsigned long long* prof) {
         const int64_t maxL = (a.nslices + G - 1) / G;
         a.pack = (int)((maxL + PK_WAVES - 1) / PK_WAVES);
     }
+    if (s->pk_gv && !s->pd && s->bs == 1) {   // pipelined (pcg_persist_gv.hpp): packed slices, <= GV_MAXS per wave
+        if (prof) {
+            set_error("persistent PCG: no instrumented (PROF) build of the pipelined iteration");
+            return FEM_EARG;
+        }
+        const int64_t maxL = (s->nslices + G - 1) / G;
+        a.pack = (int)((maxL + PK_WAVES - 1) / PK_WAVES);
+        const int64_t n = s->n;
+        GvArgs g;
+        g.u = s->gv_buf;
+        g.w = s->gv_buf + n;
+        g.q = s->gv_buf + 2 * n;
+        g.z = s->gv_buf + 3 * n;
+        g.m[0] = s->gv_buf + 4 * n;
+        g.m[1] = s->gv_buf + 5 * n;
+        g.init = s->gv_init_pending;
+        s->gv_init_pending = 0;
+        s->pk_epochs += 1;   // the init barrier
+        void* gargs[] = {&a, &g};
+        const void* gfn = a.pack <= 1 ? (const void*)k_pcg_persist_gv<1> : (const void*)k_pcg_persist_gv<2>;
+        if (s->pk_coop || (s->tune & FEM_TUNE_PK_COOP))
+            FEM_HIP(hipLaunchCooperativeKernel(gfn, dim3(G), dim3(PK_T), gargs, GV_LDS, s->stream));
+        else
+            FEM_HIP(hipLaunchKernel(gfn, dim3(G), dim3(PK_T), gargs, GV_LDS, s->stream));
+        FEM_LAUNCHED();
+        s->launched += k;
+        return FEM_OK;
+    }
     void* args[] = {&a};
     if (s->pd && !prof && s->pd_prof) a.prof = prof = s->pd_prof;
     if (s->bs == 3) {   // plane-paired values, per-lane 16-bit node deltas; no instrumented build
@@ -3700,6 +3757,11 @@ static int launch_persist(fem_pcg* s, int k, unsigned long long* prof) {
         FEM_HIP(hipLaunchKernel(fn, dim3(G), dim3(PK_T), args, persist_lds(s), s->stream));
     FEM_LAUNCHED();
     s->launched += k;
+    return FEM_OK;
+}
+
+int fem_pcg_pipelined(fem_pcg* s, int* on) {
+    *on = (s && s->persist && s->pk_gv) ? 1 : 0;
     return FEM_OK;
 }
 
@@ -3888,6 +3950,18 @@ int fem_pcg_start(fem_pcg* s) {
     if (s->persist) {   // single-reduction start: r0 = b - A x0, u0 = w r0 (in q), p = s = 0, g0 -> red[1]
         const int zrc = persist_reset_sync(s);   // after the state upload: zeroes st->pk_epoch too
         if (zrc) return zrc;
+        if (s->pk_gv) {   // pipelined: its vectors (q = z = 0; u, w, m formed by the first launch)
+            const int64_t need = 6 * s->n;
+            if (need > s->gv_cap) {
+                pool_free(s->gv_buf, s->stream);
+                s->gv_buf = nullptr;
+                s->gv_cap = 0;
+                FEM_HIP(pool_alloc((void**)&s->gv_buf, sizeof(double) * (size_t)need, s->stream, true));
+                s->gv_cap = need;
+            }
+            FEM_HIP(hipMemsetAsync(s->gv_buf, 0, sizeof(double) * (size_t)need, s->stream));
+            s->gv_init_pending = 1;
+        }
         hipLaunchKernelGGL(k_cg1_init, dim3(s->grid_vec), dim3(PCG_BLOCK), 0, s->stream, s->n, s->bs, s->b, s->r,
                            s->q, s->w, s->p0, s->p1, s->q, (const uint8_t*)nullptr, s->st, s->red);
         FEM_LAUNCHED();
@@ -4634,6 +4708,7 @@ void fem_pcg_destroy(fem_pcg* s) {
     pool_free(s->pk_part, s->stream);
     pool_free(s->pk_sync, s->stream);
     pool_free(s->pk_v, s->stream);
+    pool_free(s->gv_buf, s->stream);
     pool_free(s->u2_sync, s->stream);
     pool_free(s->st, s->stream);
     host_state_free(s->st_host, s->stream);

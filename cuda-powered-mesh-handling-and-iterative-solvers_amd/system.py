@@ -762,7 +762,8 @@ class PcgRunner:
     """Persistent (P)CG context for fixed-iteration timing (bench.py): start once, iterate k, poll."""
 
     def __init__(self, A: SellMatrix, b, w, x0=None, mode=C.MODE_PCG, tol=0.0, eps=1e-30, fused=False,
-                 schedule=None, constraints=None):
+                 schedule=None, constraints=None, tune=None):
+        """tune: the context's FEM_TUNE_* flags instead of the library default (e.g. TUNE_DEFAULT | TUNE_PK_GV)."""
         self.lib = C.lib()
         self.A = A
         self.device = A.device
@@ -786,6 +787,8 @@ class PcgRunner:
         self._mode, self._tol, self._eps = mode, float(tol), float(eps)
         # solver-layout values (bs = 1) unless the context must read the plain ones (distributed, fused, constrained)
         self._create(isinstance(self, _DistMarker) or self.schedule == SCHED_FUSED or constraints is not None)
+        if tune is not None:
+            self.set_tuning(tune)
 
     def _create(self, plain):
         A = self.A
@@ -848,6 +851,13 @@ class PcgRunner:
         """(slices stored with slice-uniform deltas, slices, column-index bytes per SpMV) over the slices
         [s_begin, s_end) of the context's matrix copy (after start())."""
         return uniform_slices(self.lib, self.h, s_begin, s_end)
+
+    def pipelined(self):
+        """True when the started context runs the pipelined persistent iteration (tune |= TUNE_PK_GV; bs = 1, single
+        GPU, PCG mode, at most 2 slices per wave -- include/fem355.h FEM_TUNE_PK_GV)."""
+        on = ctypes.c_int()
+        C.check(self.lib.fem_pcg_pipelined(self.h, ctypes.byref(on)), "fem_pcg_pipelined")
+        return bool(on.value)
 
     def persist_build(self):
         """(register slots per wave, overflow build, packed slices per wave) of the persistent launches (after

@@ -505,6 +505,8 @@ int fem_pcg_set_layout(fem_pcg* s, const double* svals, const int16_t* pcols, co
  * 3): register slots per wave (bs = 1: 1, 2, 4 or 7; bs = 3: 2), 1 for the overflow build, and the packed
  * assignment's slices per wave (0: the even spread) */
 int fem_pcg_persist_build(fem_pcg* s, int* slots, int* overflow, int* pack);
+/* 1 in *on when the started context runs the pipelined persistent iteration (FEM_TUNE_PK_GV), else 0 */
+int fem_pcg_pipelined(fem_pcg* s, int* on);
 /* persistent schedule only: k iterations of the instrumented kernel build; host_out[G * 8] = per-workgroup shader-clock
  * sums of the phases (u wait, SpMV, block sum, barrier + partial sums, step, update + drain + flag, launch prologue,
  * launch epilogue), then host_out[G * 8 + G * 16] = every wave's own SpMV clock sum; *grid = G */
@@ -537,7 +539,12 @@ int fem_enforce_constraints(double* x, double* r, int64_t n, int order, int64_t 
 enum { FEM_TUNE_REVERSE = 1, FEM_TUNE_PAIR = 2, FEM_TUNE_PK_SC1 = 4, FEM_TUNE_PK_PACK = 8, FEM_TUNE_C1F = 16,
        FEM_TUNE_PK_COOP = 32, FEM_TUNE_DIST_FINE = 64, FEM_TUNE_PK_UNI = 128, FEM_TUNE_PK_WIDE = 256,
        FEM_TUNE_DIST_DROP = 512, FEM_TUNE_UPD1 = 1024, FEM_TUNE_U2_HOLD = 2048, FEM_TUNE_U2_SMALL = 4096,
-       FEM_TUNE_MF_GATHER = 8192 };
+       FEM_TUNE_MF_GATHER = 8192, FEM_TUNE_PK_GV = 16384 };
+/* FEM_TUNE_PK_GV (opt-in, set before fem_pcg_start): persistent schedule, bs = 1, single GPU, PCG mode, systems of at
+ * most 2 slices per wave (~2M rows on 256 CUs: the 1M-tet cube, a rank share of the 10M one) -- the pipelined
+ * (Ghysels-Vanroose) Jacobi-PCG, whose grid reduction runs under the next SpMV (csrc/pcg_persist_gv.hpp). Its
+ * iterates leave the single-reduction ones at rounding level (recurrences for M^-1 r and A M^-1 r); other contexts
+ * ignore the flag. fem_pcg_pipelined reports whether the started context runs it. */
 /* FEM_TUNE_MF_GATHER (A/B): on the element-chunk operator, q = A p is summed from the slots by a gather launch and
  * read by the merged update, instead of the update summing each dof's slots itself (the default; same bits). */
 /* FEM_TUNE_U2_HOLD / FEM_TUNE_U2_SMALL (tests only): the merged update's give-up path -- workgroup 0 arrives only after

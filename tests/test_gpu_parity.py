@@ -1469,3 +1469,22 @@ def test_span_scratch_across_streams(gpu):
         s.synchronize()
         assert torch.equal(sl.win.cpu(), win) and torch.equal(sl.pcols.cpu(), pcols), (k, n)
         assert torch.equal(sl.uoff.cpu(), uoff), (k, n)
+
+
+@pytest.mark.gpu
+def test_value_kernel_refuses_rows_past_16bit_positions(gpu):
+    """The accumulator value kernel keeps column positions in 16-bit fields: a pattern whose widest row has 65,535
+    columns or more (here a hub node shared by 21,846 tets, 65,539 columns) is refused with FEM_EARG -> FemError by
+    fem_assemble_tet4*, never assembled with aliased positions. A normal pattern on the same device assembles after."""
+    _, mesh, _, system = _mods()
+    from fem355 import _capi as C
+    ne = 21846
+    g = torch.Generator().manual_seed(5)
+    c = torch.cat([torch.zeros(1, 3, dtype=F64), torch.rand(3 * ne, 3, generator=g, dtype=F64) + 0.5]).to(gpu)
+    t = torch.cat([torch.zeros(ne, 1, dtype=torch.int64),
+                   torch.arange(1, 3 * ne + 1, dtype=torch.int64).view(ne, 3)], dim=1).to(gpu)
+    with pytest.raises(C.FemError, match="columns exceeds"):
+        system.assemble_tet4_system(c, t, "poisson", E=1.0, nu=0.3)
+    c2, t2 = mesh.kuhn_cube(4, jitter=0.1)
+    A = system.assemble_tet4_system(c2.to(gpu), t2.to(gpu), "poisson", E=1.0, nu=0.3)
+    assert A.n == c2.shape[0]

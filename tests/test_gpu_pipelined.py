@@ -1,0 +1,108 @@
+"""GPU tier: the pipelined persistent Jacobi-PCG (FEM_TUNE_PK_GV, csrc/pcg_persist_gv.hpp) -- the Ghysels-Vanroose
+recurrences with the grid reduction posted before the SpMV and waited for after it. Against the single-reduction
+persistent schedule, which tests/test_gpu_scale_parity.py pins to the oracle's R.pcg:
+  * the first iterates within 1e-10 (the recurrences for M^-1 r and A M^-1 r differ at rounding level);
+  * launch boundaries change nothing: 40 iterations in one launch or in chunks are bit-identical;
+  * solves to rtol 1e-8 converge in the same iterations +-2, with x within 1e-8 of the single-reduction solution
+    and the true residual within 2x of the tolerance (the method's attainable accuracy, not a parity bound);
+  * contexts outside its scope (bs = 3, CG mode) keep the single-reduction kernel."""
+import pytest
+import torch
+
+from conftest import rel
+
+pytestmark = pytest.mark.gpu
+F64 = torch.float64
+
+
+def _mods():
+    import fem355  # noqa: F401
+    from fem355 import _capi as C, mesh, system
+    return C, mesh, system
+
+
+def _case(mesh, system, n, gpu, jitter=0.0, kind="poisson"):
+    c, t = mesh.kuhn_cube(n, jitter=jitter)
+    c, t = c.to(gpu), t.to(gpu)
+    if kind == "poisson":
+        f, fixed = mesh.cube_poisson_case(c)
+        mask = torch.zeros(c.shape[0], dtype=torch.uint8, device=gpu)
+        mask[fixed] = 1
+        A = system.assemble_tet4_system(c, t, "poisson")
+    else:
+        f, fixed = mesh.cube_elasticity_case(c)
+        mask = torch.zeros((c.shape[0], 3), dtype=torch.uint8, device=gpu)
+        mask[fixed] = 1
+        mask = mask.view(-1)
+        A = system.assemble_tet4_system(c, t, "elastic", 113.8e9, 0.342)
+    w = A.jacobi(mask)
+    return A, f.reshape(-1).to(F64), w
+
+
+def _iterate(system, A, b, w, chunks, tune, mode=None):
+    kw = {} if mode is None else {"mode": mode}
+    run = system.PcgRunner(A, b, w, tol=0.0, schedule=3, tune=tune, **kw)
+    run.start()
+    on = run.pipelined()
+    for k in chunks:
+        run.iterate(k)
+    it, status = run.poll()[:2]
+    x = run.x.clone()
+    run.close()
+    return x, it, status, on
+
+
+@pytest.mark.parametrize("n,jitter", [(24, 0.1), (40, 0.0)])
+def test_pipelined_first_iterates(gpu, n, jitter):
+    C, mesh, system = _mods()
+    A, b, w = _case(mesh, system, n, gpu, jitter)
+    gv = C.TUNE_DEFAULT | C.TUNE_PK_GV
+    for k in (1, 2, 5):
+        x_gv, it, status, on = _iterate(system, A, b, w, (k,), gv)
+        x_sr, it_sr, _, on_sr = _iterate(system, A, b, w, (k,), C.TUNE_DEFAULT)
+        assert on and not on_sr
+        assert it == it_sr == k and status == C.PCG_RUNNING
+        assert rel(x_gv, x_sr) < 1e-10, (k, rel(x_gv, x_sr))
+
+
+def test_pipelined_launch_boundaries_bit_identical(gpu):
+    C, mesh, system = _mods()
+    A, b, w = _case(mesh, system, 32, gpu, 0.05)
+    gv = C.TUNE_DEFAULT | C.TUNE_PK_GV
+    xs = []
+    for chunks in ((40,), (10, 10, 20), (1, 39), (1, 1, 1, 37)):
+        x, it, status, on = _iterate(system, A, b, w, chunks, gv)
+        assert on and it == 40 and status == C.PCG_RUNNING
+        xs.append(x)
+    for x in xs[1:]:
+        assert torch.equal(xs[0], x)
+
+
+@pytest.mark.parametrize("n,jitter", [(30, 0.1), (55, 0.0)])
+def test_pipelined_solve(gpu, n, jitter):
+    """n = 55: the 1M-tet configs[1] cube (998,250 tets)."""
+    C, mesh, system = _mods()
+    A, b, w = _case(mesh, system, n, gpu, jitter)
+    tol = 1e-8 * float(torch.sqrt(torch.dot(b, w * b)))
+    ref = A.pcg(b, w=w, tol=tol, max_iter=5000, schedule=3)
+    gv = A.pcg(b, w=w, tol=tol, max_iter=5000, schedule=3, tune=C.TUNE_DEFAULT | C.TUNE_PK_GV)
+    assert ref.status == C.PCG_CONVERGED and gv.status == C.PCG_CONVERGED
+    assert abs(gv.iterations - ref.iterations) <= 2, (gv.iterations, ref.iterations)
+    assert rel(gv.x, ref.x) < 1e-8, rel(gv.x, ref.x)
+    # the true preconditioned residual of the pipelined solution against the tolerance it stopped on
+    r = b - A.matvec(gv.x)
+    fixed = w == 0
+    r[fixed] = 0.0
+    assert float(torch.sqrt(torch.dot(r, w * r))) < 2 * tol
+
+
+def test_pipelined_scope(gpu):
+    C, mesh, system = _mods()
+    gv = C.TUNE_DEFAULT | C.TUNE_PK_GV
+    A, b, w = _case(mesh, system, 12, gpu, 0.1, kind="elastic")
+    _, it, _, on = _iterate(system, A, b, w, (5,), gv)
+    assert not on and it == 5
+    A, b, w = _case(mesh, system, 12, gpu, 0.1)
+    wcg = (w != 0).to(F64)
+    _, it, _, on = _iterate(system, A, b, wcg, (5,), gv, mode=C.MODE_CG_STABLE)
+    assert not on and it == 5
