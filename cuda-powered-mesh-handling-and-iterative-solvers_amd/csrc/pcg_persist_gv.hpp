@@ -29,6 +29,10 @@
 
 namespace fem {
 
+#ifndef FEM_GV_PROBE
+#define FEM_GV_PROBE 0   // timing builds only (wrong results): 1 no barrier wait in the loop, 2 no m-flag wait
+#endif
+
 struct GvArgs {
     double* u;     // M^-1 r by recurrence
     double* w;     // A u by recurrence
@@ -38,6 +42,10 @@ struct GvArgs {
     int init;      // first launch after fem_pcg_start: form w0 = A u0 and m0, reduce gamma0 / delta0
 };
 
+#ifndef FEM_GV_EARLY
+#define FEM_GV_EARLY 1   // post gamma / delta and arrive before the x update and the m hand-off
+#endif
+constexpr bool GV_EARLY = FEM_GV_EARLY;
 constexpr int GV_MAXS = 2;   // slices per wave (packed assignment)
 // LDS: head (wave sums of gamma [0, 16), the ok word, the barrier sums [18, 20), wave sums of delta [20, 36)), then x
 // and the Jacobi weights of the workgroup's rows
@@ -50,7 +58,11 @@ __device__ __forceinline__ void gv_arrive(unsigned* sy, int grp, unsigned nper, 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned old = __hip_atomic_fetch_add(sy + PK_GRP + grp * PK_LINE, 1u, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
+#if FEM_GV_PROBE   // (timing builds: workgroups run epochs apart, so whichever add completes a group's count bumps)
+    if ((old + 1) % nper == 0)
+#else
     if (old == e * nper - 1)
+#endif
         for (int r = 0; r < NXCD; ++r)
             __hip_atomic_fetch_add(sy + PK_GEN + r * PK_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -85,7 +97,7 @@ __device__ __forceinline__ bool gv_wait(unsigned* sy, int grp, unsigned e, int* 
 
 // the two partial sums of this workgroup (waves in order), valid in thread 0; ends on a workgroup barrier after
 // every wave drained its stores (the m rows of the update)
-__device__ __forceinline__ void gv_block_sums(double a, double b, double* lds16, double* sa, double* sb) {
+__device__ __forceinline__ void gv_block_sums(double a, double b, double* lds16, double* sa, double* sb, bool drain) {
     a = wave_sum(a);
     b = wave_sum(b);
     const int w = threadIdx.x >> 6;
@@ -93,7 +105,7 @@ __device__ __forceinline__ void gv_block_sums(double a, double b, double* lds16,
         lds16[w] = a;
         lds16[PK_WAVES + 4 + w] = b;   // (after the ok word and the barrier sums of the head)
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
         double ta = 0.0, tb = 0.0;
@@ -171,6 +183,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist_gv(PkArgs a, GvArgs gv) {
         fail = true;
     }
     const bool st_loaded = !halt;
+    if (threadIdx.x == 0) lds_ok = 1;   // (read only after a workgroup barrier)
     const int64_t* slp = pk_launder(a.slice_ptr);
     const int16_t* cop = pk_launder(a.cols);
     const double* vap = pk_launder(a.vals);
@@ -199,7 +212,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist_gv(PkArgs a, GvArgs gv) {
             asm volatile("" ::: "memory");
         }
         double gs = 0.0, ds = 0.0;
-        gv_block_sums(gp, dp, lds16, &gs, &ds);
+        gv_block_sums(gp, dp, lds16, &gs, &ds, true);
         const unsigned e = ep + 1;
         double* pb = a.part + (size_t)(e & 1u) * 2 * G;
         if (threadIdx.x == 0) {
@@ -222,8 +235,8 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist_gv(PkArgs a, GvArgs gv) {
     if (!halt && !fail) {
         for (k = 0; k < a.kmax; ++k) {
             // ---- the arrival of this iteration (its partials were posted by the last update), then the m window
-            if (k > 0 && threadIdx.x == 0) gv_arrive(sy, grp, nper, ep);
-            if (wv == 0) {
+            if (!GV_EARLY && k > 0 && threadIdx.x == 0) gv_arrive(sy, grp, nper, ep);
+            if (wv == 0 && !(FEM_GV_PROBE & 2)) {   // (probe 2, timing only: no m-flag wait)
                 bool ok = true;
                 for (int b0 = wlo; b0 <= whi && ok; b0 += 64) {
                     const int jw = b0 + lane;
@@ -264,7 +277,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist_gv(PkArgs a, GvArgs gv) {
                 }
             }
             // ---- gamma, delta of this iterate
-            if (k > 0) {
+            if (k > 0 && !(FEM_GV_PROBE & 1)) {   // (probe 1, timing only: no wait, stale scalars)
                 double* pb = a.part + (size_t)(ep & 1u) * 2 * G;
                 if (!gv_wait(sy, grp, ep, &lds_ok, pb, pb + G, G, lds_dg)) {
                     fail = true;
@@ -306,40 +319,79 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist_gv(PkArgs a, GvArgs gv) {
             double* mst = pk_launder((it & 1) ? gv.m[0] : gv.m[1]);   // m of iteration it + 1
             unsigned rbi = rb;
             asm volatile("" : "+v"(rbi));
+            const unsigned e = ep + 1;
+            if constexpr (GV_EARLY) {
+                // the vectors gamma / delta need first, their partials posted and the arrival on barrier e made at
+                // once; x and the hand-off of m follow (the arrival no longer waits for the m stores to drain)
 #pragma unroll
-            for (int j = 0; j < MAXS; ++j) {
-                if (j < nreg) {
-                    zz[j] = nn[j] + bnew * zz[j];
-                    qq[j] = mm[j] + bnew * qq[j];
-                    ss[j] = ww[j] + bnew * ss[j];
-                    pp[j] = uu[j] + bnew * pp[j];
-                    xl[j * 64] += al * pp[j];
-                    rr[j] = rr[j] - al * ss[j];
-                    uu[j] = uu[j] - al * qq[j];
-                    ww[j] = ww[j] - al * zz[j];
-                    mm[j] = wl[j * 64] * ww[j];
-                    if (GV_ON(j))
-                        __hip_atomic_store(mst + (rbi + 64u * j), mm[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    gp += rr[j] * uu[j];
-                    dp += ww[j] * uu[j];
+                for (int j = 0; j < MAXS; ++j) {
+                    if (j < nreg) {
+                        zz[j] = nn[j] + bnew * zz[j];
+                        qq[j] = mm[j] + bnew * qq[j];
+                        ss[j] = ww[j] + bnew * ss[j];
+                        pp[j] = uu[j] + bnew * pp[j];
+                        rr[j] = rr[j] - al * ss[j];
+                        uu[j] = uu[j] - al * qq[j];
+                        ww[j] = ww[j] - al * zz[j];
+                        gp += rr[j] * uu[j];
+                        dp += ww[j] * uu[j];
+                    }
+                }
+                double gs = 0.0, ds = 0.0;
+                gv_block_sums(gp, dp, lds16, &gs, &ds, false);
+                if (threadIdx.x == 0) {
+                    double* pb = a.part + (size_t)(e & 1u) * 2 * G;
+                    __hip_atomic_store(pb + L, gs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(pb + G + L, ds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    gv_arrive(sy, grp, nper, e);
+                }
+#pragma unroll
+                for (int j = 0; j < MAXS; ++j) {
+                    if (j < nreg) {
+                        xl[j * 64] += al * pp[j];
+                        mm[j] = wl[j * 64] * ww[j];
+                        if (GV_ON(j))
+                            __hip_atomic_store(mst + (rbi + 64u * j), mm[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave drains its m stores
+                __syncthreads();
+                if (threadIdx.x == 0) pk_st(uf + L * PK_LINE, e);
+            } else {
+#pragma unroll
+                for (int j = 0; j < MAXS; ++j) {
+                    if (j < nreg) {
+                        zz[j] = nn[j] + bnew * zz[j];
+                        qq[j] = mm[j] + bnew * qq[j];
+                        ss[j] = ww[j] + bnew * ss[j];
+                        pp[j] = uu[j] + bnew * pp[j];
+                        xl[j * 64] += al * pp[j];
+                        rr[j] = rr[j] - al * ss[j];
+                        uu[j] = uu[j] - al * qq[j];
+                        ww[j] = ww[j] - al * zz[j];
+                        mm[j] = wl[j * 64] * ww[j];
+                        if (GV_ON(j))
+                            __hip_atomic_store(mst + (rbi + 64u * j), mm[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        gp += rr[j] * uu[j];
+                        dp += ww[j] * uu[j];
+                    }
+                }
+                double gs = 0.0, ds = 0.0;
+                gv_block_sums(gp, dp, lds16, &gs, &ds, true);   // (every wave drained its m stores)
+                if (threadIdx.x == 0) {
+                    double* pb = a.part + (size_t)(e & 1u) * 2 * G;
+                    __hip_atomic_store(pb + L, gs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(pb + G + L, ds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    pk_st(uf + L * PK_LINE, e);
                 }
             }
             it += 1;
-            double gs = 0.0, ds = 0.0;
-            gv_block_sums(gp, dp, lds16, &gs, &ds);   // (every wave drained its m stores)
-            const unsigned e = ep + 1;
-            if (threadIdx.x == 0) {
-                double* pb = a.part + (size_t)(e & 1u) * 2 * G;
-                __hip_atomic_store(pb + L, gs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(pb + G + L, ds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                pk_st(uf + L * PK_LINE, e);
-            }
             ep = e;
         }
     }
     // ---- chunk end without a stop: reduce the posted gamma / delta (the next launch starts from them); stop test
     if (!fail && !halt && k == a.kmax && a.kmax > 0) {
-        if (threadIdx.x == 0) gv_arrive(sy, grp, nper, ep);
+        if (!GV_EARLY && threadIdx.x == 0) gv_arrive(sy, grp, nper, ep);   // (GV_EARLY: arrived in the update)
         double* pb = a.part + (size_t)(ep & 1u) * 2 * G;
         if (!gv_wait(sy, grp, ep, &lds_ok, pb, pb + G, G, lds_dg)) {
             fail = true;
