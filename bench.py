@@ -87,6 +87,9 @@ def parse():
     ap.add_argument("--reorder", default="none", choices=["none", "rcm"],
                     help="rcm: renumber the nodes by device reverse Cuthill-McKee inside every assembly pass "
                          "(timed with it; reported as reorder_ms)")
+    ap.add_argument("--config1", type=int, default=1,
+                    help="1: also measure BASELINE configs[1] (1M-tet Poisson) on the single-reduction and the "
+                         "pipelined persistent kernels, reported under \"config1\"")
     ap.add_argument("--pipelined", type=int, default=0,
                     help="1: the pipelined (Ghysels-Vanroose) persistent iteration for bs = 1 systems of <= 2 slices "
                          "per wave (FEM_TUNE_PK_GV; the 1M cube, a rank share of the 10M one); ignored elsewhere")
@@ -292,6 +295,11 @@ def main():
                 out["mixed"] = measure_mixed(a, dev)
             except Exception as e:   # reported, never fatal to the line
                 out["mixed"] = {"error": f"{type(e).__name__}: {e}"}
+        if a.config1:
+            try:
+                out["config1"] = measure_config1(a, dev)
+            except Exception as e:   # reported, never fatal to the line
+                out["config1"] = {"error": f"{type(e).__name__}: {e}"}
         guard.emit()
         guard.close()
     else:
@@ -506,6 +514,24 @@ def measure_mixed(a, dev):
                        "model": "K_e and M_s,e written and each read once by its assembly, the bs = 3 stiffness and "
                                 "bs = 1 mass SELL values written once (the set's job time; the pattern excluded)"
                                 + ("; K_e in its packed symmetric form (upper blocks)" if a.mixed_ke == "packed" else "")}
+    return out
+
+
+def measure_config1(a, dev):
+    """BASELINE configs[1] beside the metric: the 1M-tet P1 Poisson cube (n = 55, 998,250 tets), assembly + Jacobi-PCG,
+    on the single-reduction persistent kernel and on the pipelined one (FEM_TUNE_PK_GV, which applies at this size;
+    DESIGN §8i) -- 500 timed fixed iterations each, whatever --steps the metric line uses."""
+    import copy
+    c1, t1 = mesh.kuhn_cube(55, device=dev)
+    out = {"config": {"workload": f"{t1.shape[0]:,}-tet P1 poisson Kuhn cube n=55, Jacobi-PCG fixed iterations",
+                      "tets": int(t1.shape[0]), "nodes": int(c1.shape[0])}}
+    keep = ("value", "unit", "steps", "ms_per_step", "dofs_per_s", "assembly_ms", "solve_ms", "solve_iters",
+            "pipelined", "kernel_ms")
+    for pl in (0, 1):
+        b = copy.copy(a)
+        b.n, b.steps, b.warmup, b.pipelined = 55, 500, 50, pl
+        d = measure(b, "poisson", c1, t1, dev)
+        out["pipelined" if pl else "single_reduction"] = {k: d[k] for k in keep if k in d}
     return out
 
 
