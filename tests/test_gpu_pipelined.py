@@ -88,6 +88,7 @@ def test_pipelined_solve(gpu, n, jitter):
     gv = A.pcg(b, w=w, tol=tol, max_iter=5000, schedule=3, tune=C.TUNE_DEFAULT | C.TUNE_PK_GV)
     assert ref.status == C.PCG_CONVERGED and gv.status == C.PCG_CONVERGED
     assert abs(gv.iterations - ref.iterations) <= 2, (gv.iterations, ref.iterations)
+    print(f"n={n}: iterations {gv.iterations} vs {ref.iterations}, rel x {rel(gv.x, ref.x):.2e}")
     assert rel(gv.x, ref.x) < 1e-8, rel(gv.x, ref.x)
     # the true preconditioned residual of the pipelined solution against the tolerance it stopped on
     r = b - A.matvec(gv.x)
@@ -106,3 +107,37 @@ def test_pipelined_scope(gpu):
     wcg = (w != 0).to(F64)
     _, it, _, on = _iterate(system, A, b, wcg, (5,), gv, mode=C.MODE_CG_STABLE)
     assert not on and it == 5
+
+
+def test_pipelined_config1_vs_oracle(gpu):
+    """BASELINE configs[1] (998,250 tets) on the pipelined kernel against the oracle's R.pcg over its own element
+    matrices: the first 5 iterates within 1e-10; the solve to rtol 1e-8 within +-2 iterations and u within 1e-10, the
+    contract of the single-reduction kernel (test_gpu_scale_parity.py). Measured on MI355X: 3.5e-14 after 5 iterates,
+    330 = 330 iterations, u 9.9e-11 (deterministic: the same bits every run)."""
+    from oracle import ref_cpu as R
+    C, mesh, system = _mods()
+    c, t = mesh.kuhn_cube(55)
+    f, fixed = mesh.cube_poisson_case(c)
+    N = c.shape[0]
+    KP = R.tet4_poisson_K(c, t)
+    dinv = R.diag_preconditioner(KP, t, N, dpn=1)
+    dinv[fixed] = 0.0
+    bo = f.reshape(N, 1).to(F64)
+    A = system.assemble_tet4_system(c.to(gpu), t.to(gpu), "poisson")
+    mask = torch.zeros(N, dtype=torch.uint8, device=gpu)
+    mask[fixed.to(gpu)] = 1
+    w = A.jacobi(mask)
+    b = f.reshape(-1).to(F64).to(gpu)
+    gv = C.TUNE_DEFAULT | C.TUNE_PK_GV
+    x5, it, _, on = _iterate(system, A, b, w, (5,), gv)
+    u5, _, _ = R.pcg(KP, t, bo, dinv, tol=0.0, max_iter=5)
+    assert on and it == 5
+    assert rel(x5.cpu(), u5.reshape(-1)) < 1e-10
+    tol = 1e-8 * float(torch.sqrt(torch.sum(bo * dinv * bo)))
+    res = A.pcg(b, w=w, tol=tol, max_iter=5000, schedule=3, tune=gv)
+    u_ref, it_ref, st = R.pcg(KP, t, bo, dinv, tol=tol, max_iter=5000)
+    assert st == "converged" and res.status == C.PCG_CONVERGED
+    assert abs(res.iterations - it_ref) <= 2, (res.iterations, it_ref)
+    print(f"configs[1] pipelined vs oracle: 5 iterates {rel(x5.cpu(), u5.reshape(-1)):.2e}, solve "
+          f"{res.iterations} vs {it_ref} iterations, rel u {rel(res.x.cpu(), u_ref.reshape(-1)):.2e}")
+    assert rel(res.x.cpu(), u_ref.reshape(-1)) < 1e-10
