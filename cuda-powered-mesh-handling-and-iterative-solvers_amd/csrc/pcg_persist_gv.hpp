@@ -42,6 +42,9 @@ struct GvArgs {
     int init;      // first launch after fem_pcg_start: form w0 = A u0 and m0, reduce gamma0 / delta0
 };
 
+#ifndef FEM_GV_U1
+#define FEM_GV_U1 8   // one-slot build: lane pairs in flight per slice
+#endif
 #ifndef FEM_GV_EARLY
 #define FEM_GV_EARLY 1   // post gamma / delta and arrive before the x update and the m hand-off
 #endif
@@ -122,6 +125,8 @@ __device__ __forceinline__ void gv_block_sums(double a, double b, double* lds16,
 template <int MAXS>
 __global__ void __launch_bounds__(PK_T) k_pcg_persist_gv(PkArgs a, GvArgs gv) {
     static_assert(MAXS >= 1 && MAXS <= GV_MAXS, "slots per wave");
+    // lane pairs in flight per slice (pk_u: 8 for one slot, 4 for two)
+    constexpr int GU = MAXS == 1 ? FEM_GV_U1 : pk_u<MAXS, false>();
     static_assert(GV_LDS_HEAD >= sizeof(double) * (2 * PK_WAVES + 4), "LDS head: two sets of wave sums");
     extern __shared__ __attribute__((aligned(16))) double pk_lds_raw[];
     double* lds16 = pk_lds_raw;
@@ -197,7 +202,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist_gv(PkArgs a, GvArgs gv) {
 #pragma unroll
         for (int j = 0; j < MAXS; ++j) {
             if (j < nreg) {
-                const double v = sell_row_pair<pk_u<MAXS, false>(), 1>(s0 + j, lane, slp, cop, vap, u0, 0, 0, uop, ucp);
+                const double v = sell_row_pair<GU, 1>(s0 + j, lane, slp, cop, vap, u0, 0, 0, uop, ucp);
                 const unsigned row = rb + 64u * j;
                 const bool on = GV_ON(j);
                 const double wj = wl[j * 64];
@@ -272,7 +277,7 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist_gv(PkArgs a, GvArgs gv) {
 #pragma unroll
                 for (int j = 0; j < MAXS; ++j) {
                     if (j < nreg)
-                        nn[j] = sell_row_pair<pk_u<MAXS, false>(), 1>(s0 + j, lane, slp, cop, vap, mvp, 0, 0, uop, ucp);
+                        nn[j] = sell_row_pair<GU, 1>(s0 + j, lane, slp, cop, vap, mvp, 0, 0, uop, ucp);
                     asm volatile("" ::: "memory");
                 }
             }
