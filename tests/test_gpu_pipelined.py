@@ -141,3 +141,28 @@ def test_pipelined_config1_vs_oracle(gpu):
     print(f"configs[1] pipelined vs oracle: 5 iterates {rel(x5.cpu(), u5.reshape(-1)):.2e}, solve "
           f"{res.iterations} vs {it_ref} iterations, rel u {rel(res.x.cpu(), u_ref.reshape(-1)):.2e}")
     assert rel(res.x.cpu(), u_ref.reshape(-1)) < 1e-10
+
+
+def test_pipelined_initial_guess_max_iter_and_history(gpu):
+    """A non-zero x0 (r0 = b - A x0 formed by the start kernel, w0 = A u0 by the first launch), a solve stopped by
+    max_iter (status PCG_MAXITER at exactly max_iter iterations, as the single-reduction kernel), and the residual
+    history (sqrt(r.u) per iteration, the reference's printed norms) against the single-reduction kernel's."""
+    C, mesh, system = _mods()
+    A, b, w = _case(mesh, system, 28, gpu, 0.1)
+    gv = C.TUNE_DEFAULT | C.TUNE_PK_GV
+    g = torch.Generator(device="cpu").manual_seed(3)
+    x0 = (torch.rand(A.n, generator=g, dtype=F64) - 0.5).to(gpu)
+    x0[w == 0] = 0.0
+    tol = 1e-8 * float(torch.sqrt(torch.dot(b, w * b)))
+    ref = A.pcg(b, x0=x0, w=w, tol=tol, max_iter=5000, schedule=3, history=True)
+    res = A.pcg(b, x0=x0, w=w, tol=tol, max_iter=5000, schedule=3, history=True, tune=gv)
+    assert ref.status == res.status == C.PCG_CONVERGED
+    assert abs(res.iterations - ref.iterations) <= 2
+    assert rel(res.x, ref.x) < 1e-8
+    h, hr = res.history, ref.history
+    m = min(len(h), len(hr))
+    assert m > 10 and rel(torch.as_tensor(h[:m]), torch.as_tensor(hr[:m])) < 1e-6
+    ref = A.pcg(b, x0=x0, w=w, tol=tol, max_iter=17, schedule=3)
+    res = A.pcg(b, x0=x0, w=w, tol=tol, max_iter=17, schedule=3, tune=gv)
+    assert ref.status == res.status == C.PCG_MAXITER and ref.iterations == res.iterations == 17
+    assert rel(res.x, ref.x) < 1e-10
