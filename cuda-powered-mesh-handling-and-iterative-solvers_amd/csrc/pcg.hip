@@ -2026,6 +2026,7 @@ struct fem_pcg {
     int64_t pd_split[PK_MAX_RANKS + 1];   // global slice bounds of the ranks
     char* pd_block;                       // this rank's comm block (hipMalloc: exportable through IPC)
     int64_t pd_block_bytes, pd_off_flag, pd_off_red, pd_off_rflag;
+    int64_t pd_off_m1;    // FEM_TUNE_PK_GV: the second m region of the comm block (m[0] is the u region at 0)
     char* pd_peer[PK_MAX_RANKS];          // comm blocks of all ranks (own included), set by fem_pcg_set_peers
     int pd_peers_ok;
     int32_t* pd_pub;                      // [G][nranks][2] rows of each local workgroup gathered by each rank
@@ -3620,6 +3621,17 @@ static int persist_setup_dist(fem_pcg* s) {
     s->pk_ovf = 0;
     s->persist = 1;
     s->pk_gv = 0;
+    if (s->pd_off_m1 > 0 && s->mode == FEM_MODE_PCG && dist_maxs(s) <= GV_MAXS) {   // pipelined DIST build
+        int res = 1;
+        for (int v = 0; v < 2 && res == 1; ++v) {
+            const void* f = v ? (const void*)k_pcg_persist_gv<2, true> : (const void*)k_pcg_persist_gv<1, true>;
+            FEM_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)GV_LDS));
+            int nb = 0;
+            FEM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, PK_T, GV_LDS));
+            if (nb < 1) res = 2;
+        }
+        s->pk_gv = res == 1;
+    }
     return FEM_OK;
 }
 
@@ -3698,26 +3710,38 @@ static int launch_persist(fem_pcg* s, int k, unsigned long long* prof) {
         const int64_t maxL = (a.nslices + G - 1) / G;
         a.pack = (int)((maxL + PK_WAVES - 1) / PK_WAVES);
     }
-    if (s->pk_gv && !s->pd && s->bs == 1) {   // pipelined (pcg_persist_gv.hpp): packed slices, <= GV_MAXS per wave
+    if (s->pk_gv && s->bs == 1) {   // pipelined (pcg_persist_gv.hpp): packed slices, <= GV_MAXS per wave
         if (prof) {
             set_error("persistent PCG: no instrumented (PROF) build of the pipelined iteration");
             return FEM_EARG;
         }
-        const int64_t maxL = (s->nslices + G - 1) / G;
-        a.pack = (int)((maxL + PK_WAVES - 1) / PK_WAVES);
+        if (!s->pd) {
+            const int64_t maxL = (s->nslices + G - 1) / G;
+            a.pack = (int)((maxL + PK_WAVES - 1) / PK_WAVES);
+        }   // (distributed: this rank's packing, set above)
         const int64_t n = s->n;
         GvArgs g;
         g.u = s->gv_buf;
         g.w = s->gv_buf + n;
         g.q = s->gv_buf + 2 * n;
         g.z = s->gv_buf + 3 * n;
-        g.m[0] = s->gv_buf + 4 * n;
-        g.m[1] = s->gv_buf + 5 * n;
-        g.init = s->gv_init_pending;
-        s->gv_init_pending = 0;
-        s->pk_epochs += 1;   // the init barrier
+        if (s->pd) {   // the gathered m in the comm blocks: m[0] the u region, m[1] after it
+            g.m[0] = reinterpret_cast<double*>(s->pd_block);
+            g.m[1] = reinterpret_cast<double*>(s->pd_block + s->pd_off_m1);
+            g.moff[0] = 0;
+            g.moff[1] = s->pd_off_m1;
+            g.init = 0;   // (a.init)
+        } else {
+            g.m[0] = s->gv_buf + 4 * n;
+            g.m[1] = s->gv_buf + 5 * n;
+            g.moff[0] = g.moff[1] = 0;
+            g.init = s->gv_init_pending;
+            s->gv_init_pending = 0;
+        }
+        s->pk_epochs += 2;   // the init barriers
         void* gargs[] = {&a, &g};
-        const void* gfn = a.pack <= 1 ? (const void*)k_pcg_persist_gv<1> : (const void*)k_pcg_persist_gv<2>;
+        const void* gfn = s->pd ? (a.pack <= 1 ? (const void*)k_pcg_persist_gv<1, true> : (const void*)k_pcg_persist_gv<2, true>)
+                                : (a.pack <= 1 ? (const void*)k_pcg_persist_gv<1> : (const void*)k_pcg_persist_gv<2>);
         if (s->pk_coop || (s->tune & FEM_TUNE_PK_COOP))
             FEM_HIP(hipLaunchCooperativeKernel(gfn, dim3(G), dim3(PK_T), gargs, GV_LDS, s->stream));
         else
@@ -3932,6 +3956,17 @@ int fem_pcg_start(fem_pcg* s) {
         s->pk_epochs = 0;
         s->pd_init_pending = 1;
         s->launched = 0;
+        if (s->pk_gv) {   // pipelined: its vectors u, w, q, z (global length); m lives in the comm block
+            const int64_t need = 6 * s->n;
+            if (need > s->gv_cap) {
+                pool_free(s->gv_buf, s->stream);
+                s->gv_buf = nullptr;
+                s->gv_cap = 0;
+                FEM_HIP(pool_alloc((void**)&s->gv_buf, sizeof(double) * (size_t)need, s->stream, true));
+                s->gv_cap = need;
+            }
+            FEM_HIP(hipMemsetAsync(s->gv_buf, 0, sizeof(double) * (size_t)need, s->stream));
+        }
         return FEM_OK;   // every rank must finish its start before any rank launches (a host barrier)
     }
     if (s->mf) {   // element-chunk operator: r0 = b - A x0 from the element formula
@@ -4473,9 +4508,12 @@ int fem_pcg_set_rows(fem_pcg* s, int nranks, int rank, const int64_t* slice_spli
     s->pd_rank = rank;
     s->pd_nranks = nranks;
     for (int q = 0; q <= nranks; ++q) s->pd_split[q] = slice_split[q];
-    // comm block: u (global length) | u-flags of all nranks * G workgroups | rank sums | rank epoch lines
+    // comm block: u (global length) [| m[1] (FEM_TUNE_PK_GV, bs = 1)] | u-flags of all nranks * G workgroups | rank
+    // sums | rank epoch lines
     const int64_t line = sizeof(unsigned) * PK_LINE;
-    s->pd_off_flag = (int64_t)cdiv(sizeof(double) * (s->n + 2), 256) * 256;
+    const int64_t vreg = (int64_t)cdiv(sizeof(double) * (s->n + 2), 256) * 256;
+    s->pd_off_m1 = ((s->tune & FEM_TUNE_PK_GV) && s->bs == 1) ? vreg : 0;
+    s->pd_off_flag = vreg + s->pd_off_m1;
     s->pd_off_red = s->pd_off_flag + (int64_t)nranks * G * line;
     s->pd_off_rflag = s->pd_off_red + 256;
     s->pd_block_bytes = s->pd_off_rflag + PK_MAX_RANKS * NXCD * line;   // [rank][XCD group] epoch lines

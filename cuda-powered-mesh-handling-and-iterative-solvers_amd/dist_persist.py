@@ -77,7 +77,9 @@ class RankRunner:
     TUNE_DEFAULT, TUNE_DIST_FINE, TUNE_DIST_DROP = 1 | 2 | 4 | 8 | 128, 64, 512
 
     def __init__(self, rs: RankSetup, b, split, rank, nranks, tol=0.0, mode=C.MODE_PCG, eps=1e-30, grid=0,
-                 stream=None, x0=None, fine=False, drop=None):
+                 stream=None, x0=None, fine=False, drop=None, gv=False):
+        """gv: the pipelined (Ghysels-Vanroose) DIST build (FEM_TUNE_PK_GV; bs = 1, PCG mode, <= 2 slices per wave
+        on this rank -- else the single-reduction build runs, see pipelined())."""
         self.lib = C.lib()
         A = rs.A
         self.A, self.rs, self.rank, self.nranks = A, rs, rank, nranks
@@ -106,9 +108,10 @@ class RankRunner:
                 if drop:   # fault injection from the environment is never silent (bench.py labels its line too)
                     print(f"[rank {rank}] FAULT INJECTION ACTIVE: FEM355_DIST_DROP_RANK={rank} -- this rank publishes "
                           "nothing; every persistent multi-GPU launch will time out", file=sys.stderr, flush=True)
-            if fine or drop:
+            if fine or drop or gv:   # (before fem_pcg_set_rows: the pipelined build's comm block has a second m region)
                 C.check(self.lib.fem_pcg_set_tuning(self.h, self.TUNE_DEFAULT | (self.TUNE_DIST_FINE if fine else 0)
-                                                    | (self.TUNE_DIST_DROP if drop else 0)), "fem_pcg_set_tuning")
+                                                    | (self.TUNE_DIST_DROP if drop else 0)
+                                                    | (C.TUNE_PK_GV if gv else 0)), "fem_pcg_set_tuning")
             sp = (ctypes.c_int64 * (nranks + 1))(*split)
             C.check(self.lib.fem_pcg_set_rows(self.h, nranks, rank, sp, int(grid)), "fem_pcg_set_rows")
             base, nbytes = ctypes.c_void_p(), ctypes.c_int64()
@@ -164,6 +167,12 @@ class RankRunner:
     def effective_schedule(self):
         return int(self.lib.fem_pcg_get_schedule(self.h))
 
+    def pipelined(self):
+        """True when the started rank runs the pipelined DIST build."""
+        on = ctypes.c_int()
+        C.check(self.lib.fem_pcg_pipelined(self.h, ctypes.byref(on)), "fem_pcg_pipelined")
+        return bool(on.value)
+
     def debug(self, which, n):
         buf = (ctypes.c_int32 * n)()
         with C.device_scope(self.device):
@@ -196,7 +205,7 @@ class EmulatedGroup:
     launches run concurrently; the comm blocks are plain device pointers (no IPC)."""
 
     def __init__(self, coords, elements, nranks, b, fixed_mask=None, kind="poisson", E=1.0, nu=0.0, tol=0.0,
-                 mode=C.MODE_PCG, x0=None, fine=False, drop_rank=-1):
+                 mode=C.MODE_PCG, x0=None, fine=False, drop_rank=-1, gv=False):
         dev = coords.device
         ncu = torch.cuda.get_device_properties(dev).multi_processor_count
         # a multiple of 8 workgroups per rank within its CU-mask share (at 3+ ranks leave headroom: the masks are
@@ -217,7 +226,7 @@ class EmulatedGroup:
             st = torch.cuda.ExternalStream(raw.value, device=dev)
             rs = assemble_rank(coords, elements, self.split, r, kind, E, nu, fixed_mask)
             self.ranks.append(RankRunner(rs, b, self.split, r, nranks, tol=tol, mode=mode, grid=grid, x0=x0,
-                                         stream=st, fine=fine, drop=(r == drop_rank)))
+                                         stream=st, fine=fine, drop=(r == drop_rank), gv=gv))
         torch.cuda.synchronize(dev)
         bases = [rr.block for rr in self.ranks]
         windows = [rr.col_window for rr in self.ranks]

@@ -166,3 +166,46 @@ def test_pipelined_initial_guess_max_iter_and_history(gpu):
     res = A.pcg(b, x0=x0, w=w, tol=tol, max_iter=17, schedule=3, tune=gv)
     assert ref.status == res.status == C.PCG_MAXITER and ref.iterations == res.iterations == 17
     assert rel(res.x, ref.x) < 1e-10
+
+
+@pytest.mark.parametrize("n,jitter", [(24, 0.1), (40, 0.0)])
+def test_pipelined_dist_emulated_ranks(gpu, n, jitter):
+    """The pipelined DIST build (rows over ranks, in-kernel hand-offs through the comm blocks; the rank exchange of
+    gamma / delta announced in the arrival and waited for after the SpMV) on 2 ranks emulated on one GPU
+    (dist_persist.EmulatedGroup, tests/test_gpu_dist_persist.py): against the single-GPU pipelined solve, iterations
+    +-1 and x within 1e-10 (the partial sums group by rank first); fixed iterations in chunks bit-identical."""
+    C, mesh, system = _mods()
+    from fem355 import dist_persist as DP
+    c, t = mesh.kuhn_cube(n, jitter=jitter)
+    c, t = c.to(gpu), t.to(gpu)
+    f, fixed = mesh.cube_poisson_case(c)
+    mask = torch.zeros(c.shape[0], dtype=torch.uint8, device=gpu)
+    mask[fixed] = 1
+    A = system.assemble_tet4_system(c, t, "poisson")
+    w = A.jacobi(mask)
+    b = f.reshape(-1).to(F64)
+    tol = 1e-9 * float(torch.sqrt(torch.dot(b, w * b)))
+    ref = A.pcg(b, w=w, tol=tol, max_iter=5000, schedule=3, tune=C.TUNE_DEFAULT | C.TUNE_PK_GV)
+    grp = DP.EmulatedGroup(c, t, 2, b, fixed_mask=mask, tol=tol, gv=True)
+    try:
+        it, stt = grp.solve(max_iter=5000, chunk=97)
+        assert all(r.pipelined() for r in grp.ranks)
+        assert stt == C.PCG_CONVERGED and ref.status == C.PCG_CONVERGED
+        assert abs(it - ref.iterations) <= 1, (it, ref.iterations)
+        print(f"n={n}: dist pipelined {it} vs {ref.iterations} iterations, rel x {rel(grp.x(), ref.x):.2e}")
+        assert rel(grp.x(), ref.x) < 1e-10
+    finally:
+        grp.close()
+    xs = []
+    for chunks in ((40,), (10, 10, 20), (1, 39)):
+        grp = DP.EmulatedGroup(c, t, 2, b, fixed_mask=mask, tol=0.0, gv=True)
+        try:
+            grp.start()
+            for k in chunks:
+                grp.iterate(k)
+            it, stt, _ = grp.poll()
+            assert it == 40 and stt == C.PCG_RUNNING
+            xs.append(grp.x())
+        finally:
+            grp.close()
+    assert torch.equal(xs[0], xs[1]) and torch.equal(xs[0], xs[2])
