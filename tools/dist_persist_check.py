@@ -2,7 +2,9 @@
 """Distributed persistent PCG on ONE GPU (emulated ranks, dist_persist.EmulatedGroup): solve / fixed-iteration
 parity against the single-GPU persistent schedule and per-iteration time, for a list of rank counts.
 
-    python tools/dist_persist_check.py [--n 24] [--ranks 1 2 4] [--iters 1 5 50] [--rtol 1e-9]
+    python tools/dist_persist_check.py [--n 24] [--ranks 1 2 4] [--iters 1 5 50] [--rtol 1e-9] [--gv]
+
+--gv: the pipelined build (FEM_TUNE_PK_GV) for the ranks and the single-GPU reference alike.
 """
 import argparse
 import json
@@ -26,7 +28,9 @@ def main():
     ap.add_argument("--rtol", type=float, default=1e-9)
     ap.add_argument("--time-iters", type=int, default=0)
     ap.add_argument("--prof", action="store_true")
+    ap.add_argument("--gv", action="store_true")
     a = ap.parse_args()
+    tune = (C.TUNE_DEFAULT | C.TUNE_PK_GV) if a.gv else None
     dev = torch.device("cuda", 0)
     c, t = mesh.kuhn_cube(a.n, device=dev)
     f, fixed = mesh.cube_poisson_case(c)
@@ -37,18 +41,18 @@ def main():
     w = A.jacobi(mask)
     ref = {}
     for k in a.iters:
-        run = system.PcgRunner(A, b, w, tol=0.0, schedule=3)
+        run = system.PcgRunner(A, b, w, tol=0.0, schedule=3, tune=tune)
         run.start()
         run.iterate(k)
         ref[k] = (run.poll(), run.x.clone())
         run.close()
     tol = a.rtol * float(torch.sqrt(torch.dot(b, w * b)))
-    r3 = A.pcg(b, w=w, tol=tol, max_iter=20000, schedule=3)
-    out = {"n": a.n, "rows": A.n, "single": {"solve_iters": r3.iterations, "status": r3.status}}
+    r3 = A.pcg(b, w=w, tol=tol, max_iter=20000, schedule=3, tune=tune)
+    out = {"n": a.n, "rows": A.n, "gv": a.gv, "single": {"solve_iters": r3.iterations, "status": r3.status}}
     for P in a.ranks:
         res = {}
         for k in a.iters:
-            grp = DP.EmulatedGroup(c, t, P, b, fixed_mask=mask, tol=0.0)
+            grp = DP.EmulatedGroup(c, t, P, b, fixed_mask=mask, tol=0.0, gv=a.gv)
             grp.start()
             t0 = time.perf_counter()
             grp.iterate(k)
@@ -72,14 +76,14 @@ def main():
                             "x_rel": float((x - ref[k][1]).abs().max() / ref[k][1].abs().max().clamp_min(1e-300)),
                             "wall_ms": dt * 1e3}
             grp.close()
-        grp = DP.EmulatedGroup(c, t, P, b, fixed_mask=mask, tol=tol)
+        grp = DP.EmulatedGroup(c, t, P, b, fixed_mask=mask, tol=tol, gv=a.gv)
         it, stt = grp.solve(max_iter=20000, chunk=512)
         x = grp.x()
         res["solve"] = {"iters": it, "status": stt,
                         "x_rel": float((x - r3.x).abs().max() / r3.x.abs().max())}
         grp.close()
         if a.time_iters:
-            grp = DP.EmulatedGroup(c, t, P, b, fixed_mask=mask, tol=0.0)
+            grp = DP.EmulatedGroup(c, t, P, b, fixed_mask=mask, tol=0.0, gv=a.gv)
             grp.start()
             grp.iterate(5)
             t0 = time.perf_counter()
