@@ -375,6 +375,10 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False, kind="pois
             lib.fem_stream_destroy(ctypes.c_void_p(raw_stream))
 
     fine = True   # comm-block variant of the current attempt (see ATTEMPTS)
+    # bench.py --pipelined 1 (opt-in): the pipelined DIST build (Poisson); its iterates leave the single-reduction
+    # ones at rounding level, so the self-check compares against the single-GPU pipelined solve at 1e-8
+    gv = bool(getattr(a, "pipelined", 0)) and kind == "poisson"
+    check_tol = 1e-8 if gv else 1e-10
 
     bs = 1 if kind == "poisson" else 3
     E, nu = (1.0, 0.0) if kind == "poisson" else (113.8e9, 0.342)
@@ -398,7 +402,7 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False, kind="pois
         lo, hi = rs.lo * bs, rs.hi * bs
         bz = tsum(float(torch.dot(b[lo:hi], (rs.w * b)[lo:hi])))
         tol = rtol * bz ** 0.5
-        run = RankRunner(rs, b, split, rank, world, tol=tol, grid=grid, stream=stream(), fine=fine)
+        run = RankRunner(rs, b, split, rank, world, tol=tol, grid=grid, stream=stream(), fine=fine, gv=gv)
         opened = connect(run, tdist, rank, world)
         barrier_sync()
         t0 = time.perf_counter()
@@ -445,7 +449,8 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False, kind="pois
         A = _system.assemble_tet4_system(coords, tets, kind, E, nu)
         w = A.jacobi(gmask)
         tol = a.rtol * float(torch.sqrt(torch.dot(b, w * b)))
-        ref = A.pcg(b, w=w, tol=tol, max_iter=20000, schedule=3)
+        ref = A.pcg(b, w=w, tol=tol, max_iter=20000, schedule=3,
+                    tune=(C.TUNE_DEFAULT | C.TUNE_PK_GV) if gv else None)
         ref_x, ref_it, ref_st = ref.x.cpu(), ref.iterations, ref.status
         del A, w, ref
     verdict = [0, "not run"]
@@ -467,7 +472,7 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False, kind="pois
                 for lo, hi, xp in parts:
                     x[lo * bs:hi * bs] = xp
                 err = float((x - ref_x).abs().max() / ref_x.abs().max())
-                ok = int(stt == C.PCG_CONVERGED and ref_st == C.PCG_CONVERGED and abs(it - ref_it) <= 1 and err < 1e-10)
+                ok = int(stt == C.PCG_CONVERGED and ref_st == C.PCG_CONVERGED and abs(it - ref_it) <= 1 and err < check_tol)
                 why = f"{attempt} comm blocks: status {stt} / {ref_st}, iterations {it} / {ref_it}, x rel diff {err:.3e}"
             verdict = [ok, why]
             tdist.broadcast_object_list(verdict, src=0)
@@ -484,10 +489,11 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False, kind="pois
         return False, None
 
     # fixed-iteration timing: W warm-up steps, then exactly K steps as one launch per rank, max over ranks
-    run = RankRunner(rs, b, split, rank, world, tol=0.0, grid=grid, stream=stream(), fine=fine)
+    run = RankRunner(rs, b, split, rank, world, tol=0.0, grid=grid, stream=stream(), fine=fine, gv=gv)
     opened = connect(run, tdist, rank, world)
     barrier_sync()
     run.start()
+    pipelined = tmin(1.0 if run.pipelined() else 0.0) > 0
     barrier_sync()
     if a.warmup > 0:
         run.profile(a.warmup)
@@ -536,11 +542,12 @@ def bench_persist(a, metric, rank, world, dev, tdist, same_gpu=False, kind="pois
                        "comm_block": "fine-grained" if fine else "coarse-grained (hipMalloc)",
                        "self_check": verdict[1], "attempts": attempts_log},
             "dofs_per_s": N * bs / (t_asm + t_solve), "assembly_ms": t_asm * 1e3, "solve_ms": t_solve * 1e3,
-            "solve_iters": it, "solve_status": stt,
+            "solve_iters": it, "solve_status": stt, "pipelined": pipelined,
             "kernel_ms": {"persist_iteration_max_over_ranks": per_it * 1e3, "iterations_per_launch": a.steps},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                          "frac": achieved / 8000.0, "traffic": None,
-                         "kernel": ("k_pcg_persist" if bs == 1 else "k_pcg_persist3") + "<DIST> (rank 0's rows; per GPU)",
+                         "kernel": ("k_pcg_persist_gv" if pipelined else "k_pcg_persist" if bs == 1 else "k_pcg_persist3")
+                                   + "<DIST> (rank 0's rows; per GPU)",
                          "algorithmic_bytes": alg_own,
                          "algorithmic_bytes_all_ranks": alg_total,
                          "aggregate_GBps": alg_total / per_it / 1e9,

@@ -228,7 +228,7 @@ def test_dist_persist_drop_publish_gives_up(gpu):
         grp.close()
 
 
-def _bench_two_ranks(extra_env, n=40, timeout=300):
+def _bench_two_ranks(extra_env, n=40, timeout=300, extra_args=()):
     import json
     import os
     import socket
@@ -242,7 +242,7 @@ def _bench_two_ranks(extra_env, n=40, timeout=300):
     env = dict(os.environ, FEM355_DIST_SAME_GPU="1", MASTER_ADDR="127.0.0.1", **extra_env)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", "--cube-n", str(n),
-           "--steps", "20", "--warmup", "5", "--elastic", "0", "--no-cpu-baseline"]
+           "--steps", "20", "--warmup", "5", "--elastic", "0", "--no-cpu-baseline", *extra_args]
     t0 = time.perf_counter()
     p = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=timeout)
     dt = time.perf_counter() - t0
@@ -260,6 +260,18 @@ def test_bench_two_ranks_same_gpu_prints_one_line(gpu):
     cfg = lines[0]["config"]
     assert lines[0]["value"] > 0 and lines[0]["n_gpus"] == 2
     assert cfg["comm_block"] == "fine-grained" and cfg["attempts"][0]["ok"], cfg
+    assert dt < 120.0, dt
+
+
+def test_bench_two_ranks_same_gpu_pipelined(gpu):
+    """`bench.py --gpus 2 --pipelined 1` on this GPU: the pipelined DIST build (a second m region in the IPC-mapped
+    comm blocks) passes the self-check against the single-GPU pipelined solve and times its steps."""
+    p, lines, dt = _bench_two_ranks({}, extra_args=("--pipelined", "1"))
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert len(lines) == 1, p.stdout[-2000:]
+    line = lines[0]
+    assert line["pipelined"] is True and line["value"] > 0 and line["n_gpus"] == 2
+    assert line["config"]["attempts"][0]["ok"], line["config"]
     assert dt < 120.0, dt
 
 
