@@ -47,6 +47,9 @@ struct GvArgs {
 #ifndef FEM_GV_U1
 #define FEM_GV_U1 8   // one-slot build: lane pairs in flight per slice
 #endif
+#ifndef FEM_GV_SYNCWAVE
+#define FEM_GV_SYNCWAVE 0   // measured neutral (profiles/r06za_gv_syncwave_ab.txt): off
+#endif
 #ifndef FEM_GV_EARLY
 #define FEM_GV_EARLY 1   // post gamma / delta and arrive before the x update and the m hand-off
 #endif
@@ -244,7 +247,10 @@ __global__ void __launch_bounds__(PK_T) k_pcg_persist_gv(PkArgs a, GvArgs gv) {
     // packed assignment: a.pack (<= MAXS, host) slices per wave in order
     const int sL0 = (int)((int64_t)L * a.nslices / G);
     const int nL = (int)((int64_t)(L + 1) * a.nslices / G) - sL0;
-    const int lo = wv * a.pack < nL ? wv * a.pack : nL;
+    // FEM_GV_SYNCWAVE: when the workgroup's slices leave a wave free, wave 0 takes none -- it is the wave that polls
+    // the grid barrier, which it then does while the other waves run the SpMV (the sums are read under it too)
+    const int wsl = (FEM_GV_SYNCWAVE && nL <= (PK_WAVES - 1) * a.pack) ? wv - 1 : wv;
+    const int lo = wsl < 0 ? nL : (wsl * a.pack < nL ? wsl * a.pack : nL);
     const int s0 = sL0 + lo + (DIST ? (int)a.sbase : 0);   // DIST: this rank's slices start at global slice sbase
     const int nreg = nL - lo < a.pack ? nL - lo : a.pack;
     const int nrows = (int)a.nrows;
