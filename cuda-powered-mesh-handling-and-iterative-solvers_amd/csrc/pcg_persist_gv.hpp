@@ -58,7 +58,10 @@ constexpr int GV_MAXS = 2;   // slices per wave (packed assignment)
 // LDS: head (wave sums of gamma [0, 16), the ok word, the barrier sums [18, 20), wave sums of delta [20, 36)), then x
 // and the Jacobi weights of the workgroup's rows
 constexpr size_t GV_LDS_HEAD = 512;
-constexpr size_t GV_LDS = GV_LDS_HEAD + sizeof(double) * 2 * GV_MAXS * PK_WAVES * 64;
+#ifndef FEM_GV_BIGLDS
+#define FEM_GV_BIGLDS 0   // A/B: the single-reduction LDS size; measured no different (profiles/r06zb_gv_biglds_ab.txt)
+#endif
+constexpr size_t GV_LDS = FEM_GV_BIGLDS ? PK_LDS : GV_LDS_HEAD + sizeof(double) * 2 * GV_MAXS * PK_WAVES * 64;
 
 // arrival of this workgroup on the grid barrier of epoch e (thread 0; the caller drained the partial stores):
 // pk_barrier's counters -- the arrival that completes a group adds to the 8 replicas of the top counter
