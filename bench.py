@@ -79,6 +79,9 @@ def parse():
     ap.add_argument("--mixed-ke", default="full", choices=["full", "packed"],
                     help="configs[4] stiffness: the full [M, d, d] K_e of compute_K_matrix, or its packed symmetric "
                          "form (upper blocks; fem_iso_ke_sym + fem_assemble_from_ke_sym)")
+    ap.add_argument("--mixed-km", default="split", choices=["fused", "split"],
+                    help="configs[4] global assemblies: two separate calls, or stiffness and mass in one pass "
+                         "(fem_assemble_from_ke_mass_sl, bit-identical; measured no faster: DESIGN §8i)")
     ap.add_argument("--schedule", type=int, default=None, help="PCG kernel schedule (0 three-kernel, 1 fused, 2 deferred, 3 persistent; "
                     "default: persistent for bs=1, three-kernel for bs=3)")
     ap.add_argument("--graph", type=int, default=0, help="capture k iterations per hipGraph (0 = plain launches)")
@@ -438,6 +441,9 @@ def measure_mixed(a, dev):
                      "jitter 0.1, stiffness (bs = 3) + consistent mass (its scalar factor M_s, bs = 1: M = M_s (x) I3), "
                      "fp64"}
     total_ms, total_el, total_bytes = 0.0, 0, 0
+    fused_km = a.mixed_km == "fused" and a.mixed_ke == "full"
+    out["global_assembly"] = ("stiffness + mass in one pass (fem_assemble_from_ke_mass_sl)" if fused_km
+                              else "stiffness and mass in separate passes")
     for et, gen, n in MIXED_FAMILIES:
         c, el = getattr(mesh, gen)(n, jitter=0.1, device=dev)
         N = c.shape[0]
@@ -469,8 +475,12 @@ def measure_mixed(a, dev):
             th.join()
             g = box[0]
             torch.cuda.current_stream(dev).wait_stream(side)
-            A = asm_fn(system.SellMatrix(g, 3), K)
-            Am = system.SellMatrix(g, 1).add_element_matrices(Me, el)
+            Am = system.SellMatrix(g, 1)
+            if fused_km:   # one pass: one column search and one incidence walk for both matrices
+                A = system.SellMatrix(g, 3).add_stiffness_and_mass(K, Me, el, Am)
+            else:
+                A = asm_fn(system.SellMatrix(g, 3), K)
+                Am.add_element_matrices(Me, el)
             return K, Me, g, A, Am
 
         walls = []
@@ -487,6 +497,14 @@ def measure_mixed(a, dev):
         ms_a, A = ev(lambda: asm_fn(system.SellMatrix(g, 3), K))
         ms_m, Me = ev(lambda: element.compute_M_matrix(c, el, et, RHO, device=dev, dtype=F64, scalar=True))
         ms_ma, Am = ev(lambda: system.SellMatrix(g, 1).add_element_matrices(Me, el))
+        ms_km = None
+        if fused_km:
+            def km():
+                mm = system.SellMatrix(g, 1)
+                return system.SellMatrix(g, 3).add_stiffness_and_mass(K, Me, el, mm), mm
+            ms_km, (A2, Am2) = ev(km)
+            assert torch.equal(Am2.plain_values(), Am.plain_values())   # the fused mass is the separate one's bits
+            del A2, Am2
         ke_bytes = K.numel() * 8
         me_bytes = Me.numel() * 8
         sell_bytes = g.sell_entries * 9 * 8
@@ -500,7 +518,8 @@ def measure_mixed(a, dev):
         total_bytes += 2 * ke_bytes + sell_bytes + 2 * me_bytes + sell_bytes // 9
         out[et] = {"elements": int(el.shape[0]), "nodes": N, "nnz_blocks": nnzb, "job_ms": best,
                    "job_passes_ms": [round(w, 3) for w in walls],
-                   "stage_ms": {"Ke": ms_k, "pattern": ms_g, "assemble_K": ms_a, "Me": ms_m, "assemble_M": ms_ma},
+                   "stage_ms": {"Ke": ms_k, "pattern": ms_g, "assemble_K": ms_a, "Me": ms_m, "assemble_M": ms_ma,
+                                "assemble_K_and_M_one_pass": ms_km},
                    "Ke_write_GBps": ke_bytes / (ms_k * 1e-3) / 1e9, "Me_write_GBps": me_bytes / (ms_m * 1e-3) / 1e9,
                    "assemble_K_GBps": (ke_bytes + sell_bytes) / (ms_a * 1e-3) / 1e9,
                    "total_mass_over_rho": mass / RHO}

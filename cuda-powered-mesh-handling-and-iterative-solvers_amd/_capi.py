@@ -48,6 +48,7 @@ SIGNATURES = {
     "fem_ke_sym_stride": (_I, [_I]),
     "fem_iso_ke_sym": (_I, [_P, _P, _L, _I, _D, _D, _P, _P, _I, _I, _P, _P]),
     "fem_assemble_from_ke_sym": (_I, [_P, _P, _I, _P, _P, _L, _P, _P, _P, _I, _I, _I, _P, _P]),
+    "fem_assemble_from_ke_mass_sl": (_I, [_P, _P, _P, _I, _P, _P, _L, _P, _P, _P, _I, _I, _P, _P, _P]),
     "fem_iso_mass": (_I, [_P, _P, _L, _I, _D, _P, _P, _P, _I, _P, _P]),
     "fem_iso_mass_scalar": (_I, [_P, _P, _L, _I, _D, _P, _P, _P, _I, _P, _P]),
     "fem_pcg_scalars": (_I, [_P, ctypes.POINTER(_D)]),

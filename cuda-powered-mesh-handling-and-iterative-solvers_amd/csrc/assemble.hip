@@ -861,17 +861,39 @@ struct KeRowLane {
 // node a is read from block ke_sym_blk(a, b) for a <= b and as the transpose of block ke_sym_blk(b, a) otherwise --
 // the same values in the same (incidence, b) order, so the sums equal the full-K_e sums whenever the full K_e's lower
 // blocks are the transposes of its upper ones (c3d10: mirrored by k_iso_ke, bit-identical)
-template <int NPE, bool PK = false>
+// FEM_KE_ATOM = 1 (A/B; measured no faster, profiles/r06ze_ke_atom_fused_ab.txt): each add is one LDS add (ds_add_f64, no return) instead of a read, a wait and a write --
+// the lanes of one step hit distinct accumulators (distinct (b, r, c); distinct slots per b, or one b per step in the
+// repeated-node branch) and a wave's LDS operations complete in issue order, so every accumulator still sums in
+// ascending (incidence, b) order, bit for bit; 0 (default): the read-modify-write form
+#ifndef FEM_KE_ATOM
+#define FEM_KE_ATOM 0
+#endif
+__device__ __forceinline__ void ke_lds_add(double* p, double v) {
+#if FEM_KE_ATOM
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
+    *p += v;
+#endif
+}
+
+// MS: also the scalar element matrices Me [M, NPE, NPE] (e.g. the consistent-mass factor M_s of M = M_s (x) I3) of the
+// same elements, into accm[slot]: the lane holding value (r, c) = (0, 0) of column b (lane 3 b of the first value
+// group) adds Me's (a, b) in the same step as its K value -- per slot ascending (incidence, b) from the caller's start
+// value, the order of ke_row1 (bit-identical to k_assemble_ke_tile1), with no column search of its own
+template <int NPE, bool PK = false, bool MS = false>
 __device__ __forceinline__ void ke_row3(const KeRowLane<NPE>& L, const double* __restrict__ Ke,
                                         const int64_t* __restrict__ conn, const int32_t* __restrict__ inc, int t0,
                                         int C, const int* cs, int nj, double* acc, int* slot_s, int64_t* koff_s,
-                                        int* eid_s, int lane) {
+                                        int* eid_s, int lane, const double* __restrict__ Me = nullptr,
+                                        double* accm = nullptr) {
     constexpr int B2 = 9, D = KeRowLane<NPE>::D, RV = KeRowLane<NPE>::RV, NL = KeRowLane<NPE>::NL;
     constexpr int KU = KeRowLane<NPE>::KU;
     constexpr int PKS = ke_sym_stride(NPE);
     int vt[NL];   // PK: offset of the value inside the transposed block (c * 3 + r for vo = r * 3 + c)
 #pragma unroll
     for (int m = 0; m < NL; ++m) vt[m] = (L.vo[m] % 3) * 3 + L.vo[m] / 3;
+    static_assert(!MS || !PK, "ke_row3: the fused scalar matrix takes the full K_e");
+    const bool mlane = MS && L.vv[0] && L.vo[0] == 0;   // value (0, 0) of column L.vb[0] in group 0 (lane 3 b)
     for (int k0 = 0; k0 < C; k0 += 64) {
         const int nk = min(64, C - k0);
         __builtin_amdgcn_wave_barrier();
@@ -887,6 +909,7 @@ __device__ __forceinline__ void ke_row3(const KeRowLane<NPE>& L, const double* _
         for (int kb = 0; kb < nk; kb += KU) {
             const int nu = min(KU, nk - kb);
             double v[KU][NL];
+            double mv[MS ? KU : 1];
 #pragma unroll
             for (int u = 0; u < KU; ++u) {
                 const int64_t ko = koff_s[kb + (u < nu ? u : 0)];
@@ -902,6 +925,11 @@ __device__ __forceinline__ void ke_row3(const KeRowLane<NPE>& L, const double* _
                 } else {
 #pragma unroll
                     for (int m = 0; m < NL; ++m) v[u][m] = (u < nu && L.vv[m]) ? Ke[ko + lane + 64 * m] : 0.0;
+                }
+                if constexpr (MS) {   // Me row a of the incidence's element, value b = lane / 3 (lanes 3 b)
+                    const int e = eid_s[kb + (u < nu ? u : 0)];
+                    const int a = (int)((ko - (int64_t)e * D * D) / RV);
+                    mv[u] = (u < nu && mlane) ? Me[((int64_t)e * NPE + a) * NPE + lane / 3] : 0.0;
                 }
             }
             int dup = 0;
@@ -927,7 +955,9 @@ __device__ __forceinline__ void ke_row3(const KeRowLane<NPE>& L, const double* _
                     for (int m = 0; m < NL; ++m) {
                         if (!L.vv[m]) continue;
                         const int s = slot_s[u * NPE + L.vb[m]];
-                        if (s >= 0) acc[s * B2 + L.vo[m]] += v[u][m];
+                        if (s >= 0) ke_lds_add(&acc[s * B2 + L.vo[m]], v[u][m]);
+                        if constexpr (MS)
+                            if (m == 0 && mlane && s >= 0) ke_lds_add(&accm[s], mv[u]);
                     }
                     __builtin_amdgcn_wave_barrier();
                 }
@@ -938,7 +968,9 @@ __device__ __forceinline__ void ke_row3(const KeRowLane<NPE>& L, const double* _
                         for (int m = 0; m < NL; ++m) {
                             if (!L.vv[m] || L.vb[m] != bb) continue;
                             const int s = slot_s[u * NPE + bb];
-                            if (s >= 0) acc[s * B2 + L.vo[m]] += v[u][m];
+                            if (s >= 0) ke_lds_add(&acc[s * B2 + L.vo[m]], v[u][m]);
+                            if constexpr (MS)
+                                if (m == 0 && mlane && s >= 0) ke_lds_add(&accm[s], mv[u]);
                         }
                         __builtin_amdgcn_wave_barrier();
                     }
@@ -1004,7 +1036,11 @@ __global__ void __launch_bounds__(256) k_assemble_ke_rows3(const double* __restr
 // doubles (R = 16: one whole 128-byte line) -- padding entries and lanes past the last row zeroed in store mode.
 // No block-CSR buffer, no k_csr_add_sell pass (c3d10: 1.85 GB written once instead of written, read and written).
 // Tiles of a slice run on one XCD, so its lines are completed in one L2.
-template <int NPE, int R, bool STORE, bool LA = false, bool PK = false>
+// MS: the same pass also assembles the scalar element matrices Me of the same elements into the plain bs = 1 SELL
+// values mvals of the same pattern (the mass factor beside the stiffness: one column search, one incidence walk, one
+// launch), their window sums in LDS after the K sums ([R][Wc + 1]) and written out like k_assemble_ke_tile1's
+// (bit-identical to it, store or add)
+template <int NPE, int R, bool STORE, bool LA = false, bool PK = false, bool MS = false>
 __global__ void __launch_bounds__(R * 64) k_assemble_ke_tile3(const double* __restrict__ Ke,
                                                                const int64_t* __restrict__ conn,
                                                                const int32_t* __restrict__ inc_ptr,
@@ -1012,9 +1048,11 @@ __global__ void __launch_bounds__(R * 64) k_assemble_ke_tile3(const double* __re
                                                                const int32_t* __restrict__ rowptr,
                                                                const int32_t* __restrict__ colidx,
                                                                const int64_t* __restrict__ slice_ptr,
-                                                               double* __restrict__ vals, int Wc, int64_t ntiles) {
+                                                               double* __restrict__ vals, int Wc, int64_t ntiles,
+                                                               const double* __restrict__ Me = nullptr,
+                                                               double* __restrict__ mvals = nullptr) {
     constexpr int B2 = 9;
-    extern __shared__ double tacc[];          // [R][Wc * 9 + 1]
+    extern __shared__ double tacc[];          // [R][Wc * 9 + 1] (MS: then [R][Wc + 1])
     __shared__ int cols_s[R][KR_LMAX];
     __shared__ int slot_s[R][64];
     __shared__ int64_t koff_s[R][64];
@@ -1042,15 +1080,30 @@ __global__ void __launch_bounds__(R * 64) k_assemble_ke_tile3(const double* __re
     }
     if (lane == 0) len_s[wid] = len;
     double* acc = tacc + wid * rs;
+    const int rsm = Wc + 1;
+    double* taccm = tacc + R * rs;             // MS
+    double* accm = taccm + wid * rsm;
     for (int j0 = 0; j0 < W; j0 += Wc) {
         const int nw = min(Wc, W - j0);              // entries of this window (slice-wide)
         const int nj = max(0, min(Wc, len - j0));    // of them real columns of this row
         __syncthreads();                             // the previous window written out
         if (lane < nj) cols_s[wid][lane] = colidx[lo + j0 + lane];
         for (int t = lane; t < nw * B2; t += 64) acc[t] = 0.0;
-        if (nj > 0) ke_row3<NPE, PK>(L, Ke, conn, inc, t0, C, cols_s[wid], nj, acc, slot_s[wid], koff_s[wid],
-                                     eid_s[wid], lane);
+        if constexpr (MS)   // adding: the mass sums start from the stored values (k_assemble_ke_tile1's order)
+            for (int t = lane; t < nw; t += 64)
+                accm[t] = (!STORE && t < nj) ? mvals[p0 + (int64_t)64 * (j0 + t) + l0 + wid] : 0.0;
+        __builtin_amdgcn_wave_barrier();
+        if (nj > 0) ke_row3<NPE, PK, MS>(L, Ke, conn, inc, t0, C, cols_s[wid], nj, acc, slot_s[wid], koff_s[wid],
+                                         eid_s[wid], lane, Me, accm);
         __syncthreads();
+        if constexpr (MS) {
+            for (int q = threadIdx.x; q < nw * R; q += R * 64) {
+                const int r = q % R, k = q / R;
+                const double v = taccm[r * rsm + k];
+                double* d = mvals + p0 + (int64_t)64 * (j0 + k) + l0 + r;
+                if (STORE || j0 + k < len_s[r]) *d = v;   // adding: padding stays as stored
+            }
+        }
         double* dst = vals + B2 * p0 + (int64_t)64 * B2 * j0 + l0;
         for (int q = threadIdx.x; q < nw * B2 * R; q += R * 64) {
             const int r = q % R, pl = q / R, k = pl / B2, rc = pl - B2 * (pl / B2);
@@ -2446,6 +2499,29 @@ static int assemble_from_ke(const double* Ke, const int64_t* conn, int npe, int 
                             const int64_t* csr2sell, const int64_t* slice_ptr, int64_t nnz, int64_t ent, int store,
                             int max_width, double* vals, fem_stream_t stream);
 
+// the fused stiffness + scalar (mass) form of the tile assembly (k_assemble_ke_tile3<..., LA, MS>): K into the solver
+// layout A of the bs = 3 values, Me into the plain bs = 1 values of the same pattern
+static int ke_tile_launch_ms(const double* Ke, const double* Me, const int64_t* conn, int npe, const int32_t* inc_ptr,
+                             const int32_t* inc, int64_t N, const int32_t* rowptr, const int32_t* colidx,
+                             const int64_t* slice_ptr, int store, int max_width, double* svals, double* mvals,
+                             hipStream_t st) {
+    const int Wc = max_width < KR_LMAX ? max_width : KR_LMAX;
+    const int R = (16 * (Wc * 10 + 2) * 8 + 16 * 1280 <= 65536) ? 16 : 8;
+    const size_t dyn = sizeof(double) * (size_t)R * (Wc * 10 + 2);
+    const int64_t ntiles = cdiv(N, 64) * (64 / R);
+    const dim3 g((unsigned)(cdiv(cdiv(N, 64), NXCD) * NXCD * (64 / R)));
+#define FEM_KTM(P, RR, ST)                                                                                          \
+    if (npe == P && R == RR && (store != 0) == ST)                                                                  \
+        hipLaunchKernelGGL((k_assemble_ke_tile3<P, RR, ST, true, false, true>), g, dim3(RR * 64), dyn, st, Ke, conn,\
+                           inc_ptr, inc, N, rowptr, colidx, slice_ptr, svals, Wc, ntiles, Me, mvals);
+#define FEM_KTM_ALL(P) FEM_KTM(P, 16, true) FEM_KTM(P, 16, false) FEM_KTM(P, 8, true) FEM_KTM(P, 8, false)
+    FEM_KTM_ALL(4) FEM_KTM_ALL(6) FEM_KTM_ALL(8) FEM_KTM_ALL(10)
+#undef FEM_KTM_ALL
+#undef FEM_KTM
+    FEM_LAUNCHED();
+    return FEM_OK;
+}
+
 int fem_assemble_from_ke_ex(const double* Ke, const int64_t* conn, int npe, int bs, const int32_t* inc_ptr,
                             const int32_t* inc, int64_t N, const int32_t* rowptr, const int32_t* colidx,
                             const int64_t* csr2sell, const int64_t* slice_ptr, int64_t nnz, int64_t ent, int store,
@@ -2690,6 +2766,19 @@ int fem_assemble_from_ke_sl(const double* Ke, const int64_t* conn, int npe, cons
         return FEM_EARG;
     }
     return rc;
+}
+
+int fem_assemble_from_ke_mass_sl(const double* Ke, const double* Me, const int64_t* conn, int npe,
+                                 const int32_t* inc_ptr, const int32_t* inc, int64_t N, const int32_t* rowptr,
+                                 const int32_t* colidx, const int64_t* slice_ptr, int store, int max_width,
+                                 double* svals, double* mvals, fem_stream_t stream) {
+    if (N <= 0) return FEM_OK;
+    if (!(npe == 4 || npe == 6 || npe == 8 || npe == 10) || max_width <= 0 || !Ke || !Me || !svals || !mvals) {
+        set_error("fem_assemble_from_ke_mass_sl: npe 4/6/8/10, the pattern width and all four arrays required");
+        return FEM_EARG;
+    }
+    return ke_tile_launch_ms(Ke, Me, conn, npe, inc_ptr, inc, N, rowptr, colidx, slice_ptr, store, max_width, svals,
+                             mvals, S(stream));
 }
 
 int fem_assemble_from_ke_sym(const double* Kp, const int64_t* conn, int npe, const int32_t* inc_ptr,

@@ -432,6 +432,41 @@ class SellMatrix:
                                              C.stream(self.device)), "fem_assemble_from_ke_ex2")
         return self
 
+    def add_stiffness_and_mass(self, Ke: torch.Tensor, Me: torch.Tensor, elements: torch.Tensor, mass: "SellMatrix"):
+        """This bs = 3 matrix += coalesce(P_e^T K_e P_e) and the bs = 1 `mass` (same pattern object) += coalesce(P_e^T
+        Me_e P_e) in ONE pass (include/fem355.h fem_assemble_from_ke_mass_sl: one column search and one incidence walk
+        for both). Me is the scalar [M, npe, npe] of `compute_M_matrix(..., scalar=True)`. Both results are bit-identical
+        to `add_element_matrices(Ke, ...)` and `mass.add_element_matrices(Me, ...)`; where the fused form does not apply
+        (plain layout wanted, a non-fresh pair in different states, another pattern) the two separate calls run."""
+        lib = C.lib()
+        elements = elements.contiguous()
+        npe = elements.shape[1]
+        Ke = Ke.to(F64).contiguous()
+        Me = Me.to(F64).contiguous()
+        if Me.shape[-1] != npe or Ke.shape[-1] != 3 * npe:
+            raise ValueError(f"element matrix sizes {Ke.shape[-1]} / {Me.shape[-1]} != 3*{npe} / {npe}")
+        fused = (self.bs == 3 and mass.bs == 1 and mass.g is self.g and self.g.max_width > 0
+                 and npe in (4, 6, 8, 10) and npe == self.g.npe and elements.shape[0] * npe == self.g.inc.numel()
+                 and self._sl_target() and self._fresh == mass._fresh
+                 and not any(os.environ.get(k) for k in ("FEM355_KE_ROWS", "FEM355_KE_COLS", "FEM355_KE_DIRECT",
+                                                         "FEM355_KM_SPLIT")))
+        if not fused:
+            self.add_element_matrices(Ke, elements)
+            mass.add_element_matrices(Me, elements)
+            return self
+        store = self._fresh
+        self._fresh = False
+        mass._modify_plain()
+        mass._fresh = False
+        C.check(lib.fem_assemble_from_ke_mass_sl(C.ptr(Ke), C.ptr(Me), C.ptr(elements), npe, C.ptr(self.g.inc_ptr),
+                                                 C.ptr(self.g.inc), self.g.n_nodes, C.ptr(self.g.rowptr),
+                                                 C.ptr(self.g.colidx), C.ptr(self.g.slice_ptr), 1 if store else 0,
+                                                 self.g.max_width, C.ptr(self._svals_buf()), C.ptr(mass._vals),
+                                                 C.stream(self.device)), "fem_assemble_from_ke_mass_sl")
+        self._sl_ok, self._plain_ok = True, False
+        mass._plain_ok = True
+        return self
+
     def add_element_matrices_sym(self, Kp: torch.Tensor, elements: torch.Tensor, inc=None):
         """vals += coalesce(P_e^T K_e P_e) from the packed symmetric K_e of `element._solid_ke_sym` (bs = 3: upper
         blocks only, the lower ones read as their transposes; include/fem355.h fem_assemble_from_ke_sym) -- the

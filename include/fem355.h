@@ -491,6 +491,17 @@ int fem_assemble_from_ke_sym(const double* Kp, const int64_t* conn, int npe, con
                              const int32_t* inc, int64_t N, const int32_t* rowptr, const int32_t* colidx,
                              const int64_t* slice_ptr, int store, int max_width, int layout_a, double* vals,
                              fem_stream_t stream);
+/* Stiffness and mass of one element family in one pass (configs[4]'s internal path): the bs = 3 K_e [M, 3 npe, 3 npe]
+ * into layout A svals (fem_assemble_from_ke_sl's sums, bit for bit) and the scalar Me [M, npe, npe] (the consistent
+ * mass factor M_s of M = M_s (x) I3) into the plain bs = 1 SELL values mvals of the same pattern
+ * (fem_assemble_from_ke_ex2's bs = 1 sums, bit for bit); store != 0: both fresh (every value written), else both added.
+ * One column search and one incidence walk for both matrices. Replaces the two assembly calls a caller of the
+ * reference would make over `compute_K_matrix` (`solver/element.py:419-427`) and a mass matrix of the same mesh
+ * (`solver_example.ipynb:216,221`), with the COO semantics of `subdivision.ipynb:118-139`. */
+int fem_assemble_from_ke_mass_sl(const double* Ke, const double* Me, const int64_t* conn, int npe,
+                                 const int32_t* inc_ptr, const int32_t* inc, int64_t N, const int32_t* rowptr,
+                                 const int32_t* colidx, const int64_t* slice_ptr, int store, int max_width,
+                                 double* svals, double* mvals, fem_stream_t stream);
 int fem_jacobi_sl(const double* svals, int bs, const int32_t* rowptr, const int32_t* diagpos,
                   const int64_t* slice_ptr, const int32_t* uoff, const int16_t* ucol, int64_t nrows,
                   const uint8_t* mask, double* w, fem_stream_t stream);

@@ -150,6 +150,46 @@ def test_packed_symmetric_ke_assembly(gpu, etype, n, monkeypatch):
             As.add_element_matrices_sym(Kp, e)
 
 
+@pytest.mark.parametrize("etype,n", [("c3d8", 7), ("c3d6", 6), ("c3d10", 4), ("c3d10", 9)])
+def test_fused_stiffness_mass_assembly(gpu, etype, n, monkeypatch):
+    """configs[4]'s one-pass stiffness + mass assembly (include/fem355.h fem_assemble_from_ke_mass_sl,
+    `SellMatrix.add_stiffness_and_mass`): the bs = 3 stiffness (solver layout) and the bs = 1 mass factor (plain
+    planes) of one pass equal the two separate tile assemblies bit for bit -- stored fresh, then added on top; an
+    element listing a node twice takes the ordered branch in both; FEM355_KM_SPLIT=1 runs the two calls and gives
+    the same bits."""
+    el, mesh, _, system = _mods()
+    gen = {"c3d8": mesh.hex_box, "c3d6": mesh.wedge_box, "c3d10": mesh.tet10_cube}[etype]
+    c, e = gen(n, jitter=0.1)
+    if n == 4:   # one element repeats a node (a degenerate element: its values are summed in (b) order)
+        e = e.clone()
+        e[3, 1] = e[3, 0]
+    c, e = c.to(gpu), e.to(gpu)
+    K = el.compute_K_matrix(c, e, etype, E, NU, device=gpu, dtype=F64)
+    Me = el.compute_M_matrix(c, e, etype, 7850.0, device=gpu, dtype=F64, scalar=True)
+    g = system.build_graph(e, c.shape[0])
+
+    def bits(A):   # NaN-safe bit comparison (a degenerate element's K_e is not finite)
+        return A.plain_values().view(torch.int64)
+
+    for steps in (1, 2):   # stored fresh; stored, then added (no read in between: both calls fused)
+        Ks, Ms = system.SellMatrix(g, 3), system.SellMatrix(g, 1)
+        Kf, Mf = system.SellMatrix(g, 3), system.SellMatrix(g, 1)
+        Kx, Mx = system.SellMatrix(g, 3), system.SellMatrix(g, 1)
+        for _ in range(steps):
+            Ks.add_element_matrices(K, e)
+            Ms.add_element_matrices(Me, e)
+            Kf.add_stiffness_and_mass(K, Me, e, Mf)
+            assert Kf.solver_layout and Mf._plain_ok and not Mf.solver_layout   # the fused call ran
+            with monkeypatch.context() as mp:
+                mp.setenv("FEM355_KM_SPLIT", "1")
+                Kx.add_stiffness_and_mass(K, Me, e, Mx)
+        assert Kf.solver_layout == Ks.solver_layout
+        assert torch.equal(bits(Kf), bits(Ks)), steps
+        assert torch.equal(bits(Mf), bits(Ms)), steps
+        assert torch.equal(bits(Kx), bits(Ks)) and torch.equal(bits(Mx), bits(Ms))
+        assert float(Mf.plain_values().sum()) > 0.0
+
+
 # ------------------------------------------------------------------ L2 operators
 def test_ebe_operator_vs_golden(gpu):
     el, *_ = _mods()
