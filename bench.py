@@ -129,6 +129,17 @@ def traffic_from_profiles(workload_key, kernel, alg):
     return d.get("bytes_per_launch")
 
 
+def traffic_source(workload_key):
+    """Where `traffic` comes from: a PMC run of this bench command (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate
+    passes, tools/pmc_traffic.py), committed under profiles/ -- not counted live in this run (no in-process PMC)."""
+    try:
+        src = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json"))).get(workload_key, {}).get("source")
+    except Exception:
+        src = None
+    return f"profiles/pmc_traffic.json[{workload_key}] <- {src} (committed rocprofv3 PMC passes, not this run)" \
+        if src else None
+
+
 def cpu_model():
     """The host CPU's model name (report it beside the core count)."""
     try:
@@ -768,6 +779,8 @@ def measure(a, kind, coords, tets, dev):
                        "sampled_launches": cnt[0]}),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic_from_profiles(workload_key, kernel, alg),
+                     "traffic_source": traffic_source(workload_key)
+                     if traffic_from_profiles(workload_key, kernel, alg) is not None else None,
                      "kernel": kernel, "algorithmic_bytes": alg,
                      "per": "iteration (whole PCG iteration in the persistent kernel)" if persist else "SpMV launch",
                      "stream_ceiling_GBps": ceiling, "frac_of_stream_read": achieved / ceiling["read"],
