@@ -2553,7 +2553,10 @@ static int assemble_from_ke(const double* Ke, const int64_t* conn, int npe, int 
                        getenv("FEM355_KE_ROWS") == nullptr;
     if (tile1) {
         const int Wc = max_width < KR_LMAX ? max_width : KR_LMAX;
-        constexpr int R1 = 16;
+#ifndef FEM_KE_R1
+#define FEM_KE_R1 16
+#endif
+        constexpr int R1 = FEM_KE_R1;   // rows per tile (FEM_KE_R1: A/B of the tile height)
         const size_t dyn = sizeof(double) * (size_t)R1 * (Wc + 1);
         const int64_t ntiles = cdiv(N, 64) * (64 / R1);
         const dim3 g((unsigned)(cdiv(cdiv(N, 64), NXCD) * NXCD * (64 / R1)));
