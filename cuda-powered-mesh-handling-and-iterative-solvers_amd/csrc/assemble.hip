@@ -861,6 +861,35 @@ struct KeRowLane {
 // node a is read from block ke_sym_blk(a, b) for a <= b and as the transpose of block ke_sym_blk(b, a) otherwise --
 // the same values in the same (incidence, b) order, so the sums equal the full-K_e sums whenever the full K_e's lower
 // blocks are the transposes of its upper ones (c3d10: mirrored by k_iso_ke, bit-identical)
+// An element listing one node twice, seen by the lanes (u, b) = u NPE + b holding node b of incidence u: 1 in the lane
+// when one of the lanes (u, b2 < b) holds the same node. Cross-lane reads of the nodes the lanes already hold (NPE - 1
+// independent ds_bpermute, the whole wave active) instead of reloading the element's first b nodes from memory one
+// after the other (a loop of up to NPE - 1 dependent global loads per incidence pass). Lanes without an incidence
+// pass a distinct negative node (-1 - lane): never a match. FEM_KE_DUPLOAD = 1: the reload loop (A/B).
+#ifndef FEM_KE_DUPLOAD
+#define FEM_KE_DUPLOAD 0
+#endif
+// ke_row3 (bs = 3) takes the cross-lane check from 8 nodes per element on: c3d6's stiffness measured slower with it
+// (0.83 vs 0.66 ms; c3d10 1.87 vs 2.19, c3d8 1.67 vs 1.69; profiles/r06zg_dup_check_ab.txt); ke_row1 for every NPE
+// FEM_KE_ATOM1 = 1 (default): ke_row1's adds as LDS atomics (ds_add_f64, no return) -- one incidence per step, so the
+// lanes of a step hit distinct slots, and a wave's LDS operations complete in issue order: the same sums, bit for bit.
+// bs = 1 stored-matrix assembly 2-4 % faster (profiles/r06zg_dup_check_ab.txt); 0: read-modify-write
+#ifndef FEM_KE_ATOM1
+#define FEM_KE_ATOM1 1
+#endif
+template <int NPE>
+constexpr bool ke_dup_shfl3() { return !FEM_KE_DUPLOAD && NPE >= 8; }
+template <int NPE>
+__device__ __forceinline__ int ke_dup_in_incidence(int node, int b, int lane) {
+    int dup = 0;
+#pragma unroll
+    for (int d = 1; d < NPE; ++d) {
+        const int o = __shfl(node, lane >= d ? lane - d : lane, 64);
+        dup |= (b >= d && o == node) ? 1 : 0;
+    }
+    return dup;
+}
+
 // FEM_KE_ATOM = 1 (A/B; measured no faster, profiles/r06ze_ke_atom_fused_ab.txt): each add is one LDS add (ds_add_f64, no return) instead of a read, a wait and a write --
 // the lanes of one step hit distinct accumulators (distinct (b, r, c); distinct slots per b, or one b per step in the
 // repeated-node branch) and a wave's LDS operations complete in issue order, so every accumulator still sums in
@@ -933,10 +962,11 @@ __device__ __forceinline__ void ke_row3(const KeRowLane<NPE>& L, const double* _
                 }
             }
             int dup = 0;
+            int node = -1 - lane;
             if (lane < nu * NPE) {   // slot of node b of incidence u in this column window (-1: outside)
                 const int u = lane / NPE, b = lane - NPE * (lane / NPE);
                 const int64_t eb = (int64_t)eid_s[kb + u] * NPE;
-                const int node = (int)conn[eb + b];
+                node = (int)conn[eb + b];
                 int l = 0, h = nj;
                 while (l < h) {
                     const int mid = (l + h) >> 1;
@@ -944,8 +974,10 @@ __device__ __forceinline__ void ke_row3(const KeRowLane<NPE>& L, const double* _
                     else h = mid;
                 }
                 slot_s[lane] = (l < nj && cs[l] == node) ? l : -1;
-                for (int b2 = 0; b2 < b; ++b2) dup |= (int)conn[eb + b2] == node;
+                if constexpr (!ke_dup_shfl3<NPE>())
+                    for (int b2 = 0; b2 < b; ++b2) dup |= (int)conn[eb + b2] == node;
             }
+            if constexpr (ke_dup_shfl3<NPE>()) dup = ke_dup_in_incidence<NPE>(node, lane - NPE * (lane / NPE), lane);
             __builtin_amdgcn_wave_barrier();
             if (!__any(dup)) {
 #pragma unroll
@@ -1130,13 +1162,13 @@ __device__ __forceinline__ void ke_row1(const double* __restrict__ Ke, const int
     for (int k0 = 0; k0 < C; k0 += KU) {
         const int nu = min(KU, C - k0);
         double v = 0.0;
-        int s = -1, dup = 0;
+        int s = -1, dup = 0, node = -1 - lane;
         if (u < nu) {
             const int ea = inc[t0 + k0 + u];
             const int e = ea / NPE;
-            v = Ke[(int64_t)e * NPE * NPE + (ea - e * NPE) * NPE + b];
             const int64_t eb = (int64_t)e * NPE;
-            const int node = (int)conn[eb + b];
+            node = (int)conn[eb + b];   // (issued before the value: the search waits for it alone)
+            v = Ke[(int64_t)e * NPE * NPE + (ea - e * NPE) * NPE + b];
             int l = 0, h = nj;
             while (l < h) {
                 const int mid = (l + h) >> 1;
@@ -1144,12 +1176,21 @@ __device__ __forceinline__ void ke_row1(const double* __restrict__ Ke, const int
                 else h = mid;
             }
             s = (l < nj && cs[l] == node) ? l : -1;
+#if FEM_KE_DUPLOAD
             for (int b2 = 0; b2 < b; ++b2) dup |= (int)conn[eb + b2] == node;
+#endif
         }
+#if !FEM_KE_DUPLOAD
+        dup = ke_dup_in_incidence<NPE>(node, b, lane);
+#endif
         __builtin_amdgcn_wave_barrier();
         if (!__any(dup)) {
             for (int uu = 0; uu < nu; ++uu) {   // one incidence at a time: its NPE slots are distinct
+#if FEM_KE_ATOM1
+                if (u == uu && s >= 0) __hip_atomic_fetch_add(&acc[s], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
                 if (u == uu && s >= 0) acc[s] += v;
+#endif
                 __builtin_amdgcn_wave_barrier();
             }
         } else {   // an element lists a node twice: its b's one after the other

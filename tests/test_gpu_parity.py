@@ -188,6 +188,13 @@ def test_fused_stiffness_mass_assembly(gpu, etype, n, monkeypatch):
         assert torch.equal(bits(Mf), bits(Ms)), steps
         assert torch.equal(bits(Kx), bits(Ks)) and torch.equal(bits(Mx), bits(Ms))
         assert float(Mf.plain_values().sum()) > 0.0
+        if steps == 1:   # against the independent forms: column-owner K (FEM355_KE_COLS), wave-per-row mass
+            with monkeypatch.context() as mp:
+                mp.setenv("FEM355_KE_COLS", "1")
+                assert torch.equal(bits(system.SellMatrix(g, 3).add_element_matrices(K, e)), bits(Ks))
+            with monkeypatch.context() as mp:
+                mp.setenv("FEM355_KE_ROWS", "1")
+                assert torch.equal(bits(system.SellMatrix(g, 1).add_element_matrices(Me, e)), bits(Ms))
 
 
 # ------------------------------------------------------------------ L2 operators
