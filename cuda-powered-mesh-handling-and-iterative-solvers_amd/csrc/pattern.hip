@@ -474,6 +474,10 @@ __global__ void k_graph_copy(const int32_t* __restrict__ tmp, const uint8_t* __r
 // G_UCAP + 64 keys, so probing always ends) and is marked row_len = -1 for k_graph_big; the fill pass recognises
 // those rows by their length. Rows finished by k_graph_small (defer[node] == 0) are skipped.
 constexpr int G_HT2 = 2048;
+#ifndef FEM_GRAPH_KB
+#define FEM_GRAPH_KB 4   // candidate passes whose loads k_graph issues together (1: one dependent pair per pass, A/B)
+#endif
+constexpr int G_KB = FEM_GRAPH_KB;
 
 template <bool FILL>
 __global__ void __launch_bounds__(256) k_graph(const int64_t* __restrict__ conn, int npe,
@@ -506,26 +510,46 @@ __global__ void __launch_bounds__(256) k_graph(const int64_t* __restrict__ conn,
         for (int q = lane; q < HS; q += 64) ht[wid][q] = -1;
         if (lane == 0) cnt_s[wid] = 0;
         __builtin_amdgcn_wave_barrier();
-        for (int t0 = 0; t0 < C; t0 += 64) {
-            if (cnt_s[wid] > G_UCAP) break;                      // wave-uniform: read after the barrier below
-            const int t = t0 + lane;
-            if (t < C) {
-                const int k = t / npe, b = t - k * npe;
-                const int e = inc[start + k] / npe;
-                const int v = (int)conn[(int64_t)e * npe + b];
-                if (!FILL && far && (v - node > 32767 || node - v > 32767) && !*far) atomicOr(far, 1);
-                unsigned h = ((unsigned)v * 2654435761u) >> (32 - hb);
-                while (true) {
-                    const int old = atomicCAS(&ht[wid][h], -1, v);
-                    if (old == -1) {
-                        atomicAdd(&cnt_s[wid], 1);
-                        break;
-                    }
-                    if (old == v) break;
-                    h = (h + 1) & (HS - 1);
-                }
+        // G_KB passes of 64 candidates at a time: their incidence loads, then their connectivity loads, in flight
+        // together (one dependent pair per G_KB passes instead of per pass; indices clamped into the row); the
+        // inserts then run pass by pass with the G_UCAP stop checked before each, as before
+        bool over = false;
+        for (int t0 = 0; t0 < C && !over; t0 += 64 * G_KB) {
+            int cv[G_KB];
+#pragma unroll
+            for (int j = 0; j < G_KB; ++j) {
+                const int t = min(t0 + 64 * j + lane, C - 1);
+                cv[j] = inc[start + t / npe];
             }
-            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int j = 0; j < G_KB; ++j) {
+                const int t = min(t0 + 64 * j + lane, C - 1);
+                cv[j] = (int)conn[(int64_t)(cv[j] / npe) * npe + (t - (t / npe) * npe)];
+            }
+#pragma unroll
+            for (int j = 0; j < G_KB; ++j) {
+                if (t0 + 64 * j >= C) break;                     // wave-uniform
+                if (cnt_s[wid] > G_UCAP) {                       // wave-uniform: read after the barrier below
+                    over = true;
+                    break;
+                }
+                const int t = t0 + 64 * j + lane;
+                if (t < C) {
+                    const int v = cv[j];
+                    if (!FILL && far && (v - node > 32767 || node - v > 32767) && !*far) atomicOr(far, 1);
+                    unsigned h = ((unsigned)v * 2654435761u) >> (32 - hb);
+                    while (true) {
+                        const int old = atomicCAS(&ht[wid][h], -1, v);
+                        if (old == -1) {
+                            atomicAdd(&cnt_s[wid], 1);
+                            break;
+                        }
+                        if (old == v) break;
+                        h = (h + 1) & (HS - 1);
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
         }
         if (cnt_s[wid] > G_UCAP) {
             if (!FILL && lane == 0) row_len[node] = -1;
