@@ -877,6 +877,10 @@ struct KeRowLane {
 #ifndef FEM_KE_ATOM1
 #define FEM_KE_ATOM1 1
 #endif
+// FEM_KE_PIPE1 = 1 (A/B): ke_row1's passes software-pipelined (loads one / two passes ahead); 0 (default): one pass at a time
+#ifndef FEM_KE_PIPE1
+#define FEM_KE_PIPE1 0
+#endif
 template <int NPE>
 constexpr bool ke_dup_shfl3() { return !FEM_KE_DUPLOAD && NPE >= 8; }
 template <int NPE>
@@ -1159,6 +1163,67 @@ __device__ __forceinline__ void ke_row1(const double* __restrict__ Ke, const int
                                         double* acc, int lane) {
     constexpr int KU = 64 / NPE;
     const int u = lane / NPE, b = lane - NPE * (lane / NPE);
+#if FEM_KE_PIPE1
+    // software pipeline over the row's passes of KU incidences: the incidence entries two passes ahead and the node
+    // ids / values one pass ahead are in flight while a pass searches and adds. Every load is unconditional (indices
+    // clamped into the row; validity kept apart), so the waits stay partial; the same adds in the same order
+    if (C <= 0) return;
+    const auto ld_inc = [&](int kk) { return inc[t0 + min(kk + u, C - 1)]; };
+    int eaB = ld_inc(0);
+    int eaC = ld_inc(KU);
+    int nodeB, nodeC = 0;
+    double vB, vC = 0.0;
+    {
+        const int e = eaB / NPE;
+        nodeB = (int)conn[(int64_t)e * NPE + b];
+        vB = Ke[(int64_t)e * NPE * NPE + (eaB - e * NPE) * NPE + b];
+    }
+    for (int k0 = 0; k0 < C; k0 += KU) {
+        const int nu = min(KU, C - k0);
+        const int eaD = ld_inc(k0 + 2 * KU);
+        {
+            const int e = eaC / NPE;
+            nodeC = (int)conn[(int64_t)e * NPE + b];
+            vC = Ke[(int64_t)e * NPE * NPE + (eaC - e * NPE) * NPE + b];
+        }
+        const bool on = u < nu;
+        const int node = on ? nodeB : -1 - lane;
+        const double v = vB;
+        int s = -1;
+        if (on) {
+            int l = 0, h = nj;
+            while (l < h) {
+                const int mid = (l + h) >> 1;
+                if (cs[mid] < node) l = mid + 1;
+                else h = mid;
+            }
+            s = (l < nj && cs[l] == node) ? l : -1;
+        }
+        const int dup = ke_dup_in_incidence<NPE>(node, b, lane);
+        __builtin_amdgcn_wave_barrier();
+        if (!__any(dup)) {
+            for (int uu = 0; uu < nu; ++uu) {   // one incidence at a time: its NPE slots are distinct
+#if FEM_KE_ATOM1
+                if (u == uu && s >= 0) __hip_atomic_fetch_add(&acc[s], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
+                if (u == uu && s >= 0) acc[s] += v;
+#endif
+                __builtin_amdgcn_wave_barrier();
+            }
+        } else {   // an element lists a node twice: its b's one after the other
+            for (int uu = 0; uu < nu; ++uu)
+                for (int bb = 0; bb < NPE; ++bb) {
+                    if (u == uu && b == bb && s >= 0) acc[s] += v;
+                    __builtin_amdgcn_wave_barrier();
+                }
+        }
+        eaC = eaD;
+        nodeB = nodeC;
+        vB = vC;
+    }
+    __builtin_amdgcn_wave_barrier();
+    return;
+#endif
     for (int k0 = 0; k0 < C; k0 += KU) {
         const int nu = min(KU, C - k0);
         double v = 0.0;
